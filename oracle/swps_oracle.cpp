@@ -1,0 +1,887 @@
+// =============================================================================
+// ORACLE — TEST INFRASTRUCTURE ONLY.
+//
+// A plain-C++ (g++) CPU restatement of SwiftMPI's data-parallel hot path,
+// written from the reference's behaviour (reference @ /root/reference/src,
+// read as text; no reference source is compiled into this file).  It is the
+// checker for the MI355X product in swiftmpi_amd/: only tests/,
+// __graft_entry__.smoke() and bench.py's `cpu_baseline` leg may load it.
+// The product never links, loads or calls anything under oracle/.
+//
+// Parity pinning:
+//   * LCG / float-LCG streams: pinned bit-exactly against the reference's own
+//     utils/random.h compiled unmodified (oracle/ref_harness -> oracle/_ref),
+//     fixture tests/golden/lcg_seed2008.json.
+//   * LR end-to-end: pinned against the reference binary's recorded outputs on
+//     its bundled data.txt (log-loss/accuracy after 20 and 100
+//     epochs), fixture tests/golden/lr_reference_quality.json.
+//   * BKDR, fmix64, hash-frag map, exp table, unigram table, CBOW-NS step and
+//     AdaGrad: restated from the cited lines; known answers derived from the
+//     code (no reference test asserts values — unittest/utils/common_test.h
+//     only logs).  Those rows are "pinned by construction", not by execution.
+//
+// Precision modes: storage_f32 = 0 keeps every parameter in fp64 exactly like
+// the reference (Vec::value_type = double, utils/vec1.h:8).  storage_f32 = 1
+// rounds the stored server/cache values to fp32 after every write while all
+// arithmetic stays fp64 — the exact semantics of the product's fp32 tables.
+// =============================================================================
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+extern "C" {
+
+// ---- hashing ---------------------------------------------------------------
+// utils/string.h:130-137  BKDRHash<size_t>(str, seed=13131); `char` is signed
+// on x86-64, so bytes >= 0x80 contribute sign-extended negative values.
+uint64_t orc_bkdr(const char *s) {
+  uint64_t h = 0;
+  while (*s) {
+    h = h * 13131ULL + (uint64_t)(int64_t)(signed char)(*s++);
+  }
+  return h;
+}
+
+// utils/HashFunction.h:16-24  MurmurHash3 fmix64.
+uint64_t orc_fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+// cluster/hashfrag.h:33-49  BasicHashFrag::init; node ids are 1..num_nodes.
+// Returns -1 when frag_num < num_nodes (the reference divides by zero).
+int orc_hashfrag_table(int frag_num, int num_nodes, uint32_t *out) {
+  if (num_nodes <= 0 || frag_num <= 0) return -1;
+  int each = int(frag_num / num_nodes);
+  if (each == 0) return -1;
+  for (int i = 0; i < frag_num; i++) {
+    int id = int(uint32_t(i / each)) + 1;
+    if (id < 1) id = 1;
+    if (id > num_nodes) id = num_nodes;
+    out[i] = (uint32_t)id;
+  }
+  return 0;
+}
+
+// cluster/hashfrag.h:51-56  to_node_id = map_table[fmix64(key) % frag_num].
+int orc_to_node_id(uint64_t key, int frag_num, const uint32_t *table) {
+  int frag = (int)(orc_fmix64(key) % (uint64_t)frag_num);
+  return (int)table[frag];
+}
+
+// parameter/sparsetable.h:143  in-server shard id.
+int orc_shard_id(uint64_t key, int shard_num) {
+  return (int)(orc_fmix64(key) % (uint64_t)shard_num);
+}
+
+// ---- RNG: utils/random.h:25-47 --------------------------------------------
+static inline uint64_t lcg_next(uint64_t &x) {
+  x = x * 25214903917ULL + 11ULL;
+  return x;
+}
+static inline float flcg_next(uint64_t &y) {
+  y = y * 4903917ULL + 11ULL;
+  return (float)y / (float)std::numeric_limits<unsigned long>::max();
+}
+
+void orc_lcg_sequence(uint64_t seed, uint64_t n, uint64_t *out) {
+  uint64_t x = seed;
+  for (uint64_t i = 0; i < n; i++) out[i] = lcg_next(x);
+}
+
+void orc_float_lcg_sequence(uint64_t n, uint64_t *states, float *out) {
+  uint64_t y = std::numeric_limits<unsigned long>::max() / 2;
+  for (uint64_t i = 0; i < n; i++) {
+    out[i] = flcg_next(y);
+    states[i] = y;
+  }
+}
+
+// ---- ExpTable: apps/word2vec/word2vec_global.h:240-272 ----------------------
+// t[i] = e/(e+1) with e = (float)exp((double)((i/1000.f*2-1)*6)).
+void orc_exptable(float *out) {
+  for (int i = 0; i < 1000; i++) {
+    float x = (i / (float)1000 * 2 - 1) * 6;
+    float e = (float)::exp((double)x);
+    out[i] = e / (e + 1);
+  }
+}
+
+// glibc rand() — the oracle calls libc itself (the function the reference's
+// Vec::randInit uses, utils/vec1.h:229-232).
+void orc_libc_rand_sequence(unsigned seed, uint64_t skip, uint64_t n, int32_t *out) {
+  srand(seed);
+  for (uint64_t i = 0; i < skip; i++) (void)rand();
+  for (uint64_t i = 0; i < n; i++) out[i] = rand();
+}
+
+}  // extern "C"
+
+// =============================================================================
+// word2vec CBOW-NS, reference semantics of apps/word2vec/word2vec_global.h
+// with nthreads = 1 (the deterministic configuration).
+// =============================================================================
+namespace {
+
+thread_local std::string g_err;
+
+struct Line {
+  std::vector<uint64_t> words;
+  bool valid = false;
+};
+
+// split(line, " ") — utils/string.h:34-48: only ' ' delimits.
+static std::vector<std::string> split_space(const std::string &s) {
+  std::vector<std::string> cols;
+  size_t start = s.find_first_not_of(' ', 0);
+  while (start != std::string::npos) {
+    size_t last = s.find_first_of(' ', start);
+    if (last == std::string::npos) {
+      cols.push_back(s.substr(start));
+    } else {
+      cols.push_back(s.substr(start, last - start));
+    }
+    if (last == std::string::npos) break;
+    start = s.find_first_not_of(' ', last);
+  }
+  return cols;
+}
+
+// LineFileReader::getline semantics (utils/string.h:91-120): split on '\n',
+// strip the delimiter, a final fragment without '\n' is still a line.
+static bool read_lines(const char *path, std::vector<std::string> &lines) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  char *buf = nullptr;
+  size_t cap = 0;
+  ssize_t n;
+  while ((n = getdelim(&buf, &cap, '\n', f)) >= 0) {
+    if (n >= 1 && buf[n - 1] == '\n') buf[--n] = 0;
+    lines.emplace_back(buf);  // NUL-terminated like std::string(cline)
+  }
+  free(buf);
+  fclose(f);
+  return true;
+}
+
+struct W2VCfg {
+  int32_t dim, window, negative, min_sentence_length, minibatch, storage_f32;
+  float sample, alpha, lr;
+  uint64_t table_size;
+  int32_t key_mode;  // 0 = BKDR (word2vec_global.h:205), 1 = atoi (word2vec.h:206)
+};
+
+struct Row {
+  std::vector<double> h, v;
+};
+struct SParam {
+  std::vector<double> h, v, h2, v2;
+};
+struct Grad {
+  std::vector<double> hg, vg;
+  int hc = 0, vc = 0;
+};
+
+static inline double store_round(double x, bool f32) { return f32 ? (double)(float)x : x; }
+
+struct W2V {
+  W2VCfg cfg;
+  std::vector<Line> lines;
+  std::map<uint64_t, int> word_freq;
+  std::unordered_set<uint64_t> local_keys;  // global minibatch key set
+  std::vector<uint64_t> wordids;
+  size_t train_words = 0;
+  std::vector<uint32_t> table;  // unigram table as indices into wordids
+  std::unordered_map<uint64_t, SParam> server;
+  std::unordered_map<uint64_t, Row> cache;
+  std::unordered_map<uint64_t, Grad> grads;
+  std::unordered_map<uint64_t, uint32_t> vid;
+  uint64_t rng = 2008;                                              // random.h:44-47
+  uint64_t frng = std::numeric_limits<unsigned long>::max() / 2;    // random.h:40-41
+  float exptab[1000];
+  // stats
+  uint64_t kept = 0, pushes = 0, pulls = 0, actual_train_words = 0;
+  double error_sum = 0;
+  uint64_t error_cnt = 0;
+  // optional trace of negative draws (vids) for the first `trace_cap` draws
+  std::vector<int64_t> neg_trace;
+  size_t trace_cap = 0;
+
+  int D() const { return cfg.dim; }
+  bool f32() const { return cfg.storage_f32 != 0; }
+
+  uint64_t key_of(const std::string &w) const {
+    if (cfg.key_mode == 1) return (uint64_t)(int64_t)std::atoi(w.c_str());
+    return orc_bkdr(w.c_str());
+  }
+
+  // word2vec_global.h:215-227 parse_instance
+  void parse(const std::string &s, Line &ln) const {
+    ln.words.clear();
+    for (auto &w : split_space(s)) ln.words.push_back(key_of(w));
+    ln.valid = (int)ln.words.size() >= cfg.min_sentence_length;
+  }
+
+  // word2vec_global.h:385-444 gather_keys(file, nlines) with nthreads = 1
+  void gather_all() {
+    for (auto &ln : lines) {
+      if (!ln.valid) continue;
+      train_words += ln.words.size();
+      for (auto k : ln.words) {
+        auto it = word_freq.find(k);
+        if (it != word_freq.end())
+          it->second++;
+        else {
+          word_freq[k] = 1;
+          local_keys.insert(k);
+        }
+      }
+    }
+  }
+
+  // word2vec_global.h:467-497 gen_unigram_table (literal 1e8-entry loop)
+  void gen_unigram_table() {
+    for (auto k : local_keys) wordids.push_back(k);
+    for (size_t i = 0; i < wordids.size(); i++) vid[wordids[i]] = (uint32_t)i;
+    const uint64_t T = cfg.table_size;
+    table.assign(T, 0);
+    double pw = 0, power = 0.75;
+    for (auto &it : word_freq) pw += std::pow(it.second, power);
+    size_t i = 0;
+    double d1 = std::pow(word_freq[wordids[i]], power) / (double)pw;
+    for (uint64_t a = 0; a < T; a++) {
+      table[a] = (uint32_t)i;
+      if ((int64_t)a / (double)T > d1) {
+        i++;
+        if (i >= wordids.size()) throw std::runtime_error("unigram table walked past the vocab (reference UB)");
+        d1 += std::pow(word_freq[wordids[i]], power) / (double)pw;
+      }
+      if (i >= word_freq.size()) i = word_freq.size() - 1;
+    }
+  }
+
+  // WParam() random init, utils/vec1.h:229-232: (rand()/(float)RAND_MAX-0.5)/D
+  void init_row_rand(std::vector<double> &x) {
+    for (int i = 0; i < D(); i++) {
+      float r = rand() / (float)RAND_MAX;
+      x[i] = store_round(((double)r - 0.5) / (double)(size_t)D(), f32());
+    }
+  }
+
+  // The first full pull (word2vec_global.h:557-562): every vocab key misses on
+  // the server in `_local_keys` iteration order; each WParam() draws D rand()
+  // for h then D for v.  rand_offset = rand() calls made before (port binds).
+  void init_params_rand(unsigned seed, uint64_t rand_offset) {
+    srand(seed);
+    for (uint64_t i = 0; i < rand_offset; i++) (void)rand();
+    for (auto k : local_keys) {
+      SParam p;
+      p.h.assign(D(), 0);
+      p.v.assign(D(), 0);
+      p.h2.assign(D(), 0);
+      p.v2.assign(D(), 0);
+      init_row_rand(p.h);
+      init_row_rand(p.v);
+      server[k] = p;
+    }
+    full_pull_to_cache();
+  }
+
+  void full_pull_to_cache() {
+    for (auto k : local_keys) {
+      auto &p = server[k];
+      cache[k] = Row{p.h, p.v};
+      Grad g;
+      g.hg.assign(D(), 0);
+      g.vg.assign(D(), 0);
+      grads[k] = g;
+    }
+  }
+
+  // float-LCG keep test, word2vec_global.h:725-731
+  bool to_sample(uint64_t word) {
+    if (cfg.sample < 0) return true;
+    auto it = word_freq.find(word);
+    if (it == word_freq.end()) throw std::runtime_error("word outside the vocab reached to_sample (reference UB)");
+    float freq = float(it->second) / (float)train_words;
+    float ran = (float)(1 - std::sqrt((double)(cfg.sample / freq)));
+    return flcg_next(frng) > ran;
+  }
+
+  Row &cache_row(uint64_t k) {
+    auto it = cache.find(k);
+    if (it == cache.end()) {  // dense_hash_map::operator[] inserts zeros
+      Row r;
+      r.h.assign(D(), 0);
+      r.v.assign(D(), 0);
+      it = cache.emplace(k, r).first;
+    }
+    return it->second;
+  }
+  Grad &grad_row(uint64_t k) {
+    auto it = grads.find(k);
+    if (it == grads.end()) {
+      Grad g;
+      g.hg.assign(D(), 0);
+      g.vg.assign(D(), 0);
+      it = grads.emplace(k, g).first;
+    }
+    return it->second;
+  }
+
+  float exp_lookup(float f) const { return exptab[(int)((f + 6) * (1000 / 6 / 2))]; }
+
+  // word2vec_global.h:654-719 learn_instance (CBOW, negative sampling)
+  void learn_instance(const std::vector<uint64_t> &w) {
+    const int W = cfg.window, N = cfg.negative, Dd = D();
+    int b = (int)(lcg_next(rng) % (uint64_t)W);
+    (void)b;
+    int n = (int)w.size();
+    std::vector<double> neu1(Dd), neu1e(Dd), tmp(Dd);
+    for (int pos = 0; pos < n; pos++) {
+      uint64_t word = w[pos];
+      if (!to_sample(word)) continue;
+      kept++;
+      std::fill(neu1.begin(), neu1.end(), 0.0);
+      std::fill(neu1e.begin(), neu1e.end(), 0.0);
+      b = (int)(lcg_next(rng) % (uint64_t)W);
+      for (int a = b; a < W * 2 + 1 - b; a++) {
+        if (a == W) continue;
+        int c = pos - W + a;
+        if (c < 0 || c >= n) continue;
+        Row &r = cache_row(w[c]);
+        for (int i = 0; i < Dd; i++) neu1[i] += r.v[i];
+      }
+      for (int d = 0; d < N + 1; d++) {
+        uint64_t target;
+        int label;
+        if (d == 0) {
+          target = word;
+          label = 1;
+        } else {
+          uint64_t ti = (lcg_next(rng) >> 16) % cfg.table_size;
+          target = wordids[table[ti]];
+          if (target == 0) {
+            ti = (lcg_next(rng) >> 16) % cfg.table_size;
+            target = wordids[table[ti]];
+          }
+          if (neg_trace.size() < trace_cap) neg_trace.push_back((int64_t)table[ti]);
+          if (target == word) continue;
+          label = 0;
+        }
+        Row &t = cache_row(target);
+        double dot = 0;
+        for (int i = 0; i < Dd; i++) dot += neu1[i] * t.h[i];
+        float f = 0;
+        f += dot;
+        float g;
+        if (f > 6)
+          g = (label - 1) * cfg.alpha;
+        else if (f < -6)
+          g = (label - 0) * cfg.alpha;
+        else
+          g = (label - exp_lookup(f)) * cfg.alpha;
+        error_sum += 10000 * g * g;
+        error_cnt++;
+        for (int i = 0; i < Dd; i++) {
+          tmp[i] = (double)g * t.h[i];
+          neu1e[i] += tmp[i];
+        }
+        Grad &gr = grad_row(target);
+        gr.hc++;
+        for (int i = 0; i < Dd; i++) {
+          double p = (double)g * neu1[i];
+          gr.hg[i] += p;
+        }
+      }
+      for (int a = b; a < W * 2 + 1 - b; a++) {
+        if (a == W) continue;
+        int c = pos - W + a;
+        if (c < 0 || c >= n) continue;
+        Grad &gr = grad_row(w[c]);
+        gr.vc++;
+        for (int i = 0; i < Dd; i++) gr.vg[i] += neu1e[i];
+      }
+    }
+  }
+
+  // gather_keys(file, line_id, B, 3) — next B+3 valid lines after `start`
+  std::unordered_set<uint64_t> gather_window(size_t start) {
+    std::unordered_set<uint64_t> K;
+    int count = 0;
+    size_t li = start;
+    for (int task = 0; task < 3; task++) {
+      while (li < lines.size()) {
+        const Line &ln = lines[li++];
+        if (!ln.valid) continue;
+        for (auto k : ln.words) K.insert(k);
+        count++;
+        if (count > cfg.minibatch) break;
+      }
+    }
+    return K;
+  }
+
+  // global_pull_access.h:80-101 callback + server.h:131-151 handler
+  void pull(const std::unordered_set<uint64_t> &K) {
+    pulls++;
+    for (auto k : K) {
+      auto it = server.find(k);
+      if (it == server.end()) throw std::runtime_error("pull of a key the full pull never inserted");
+      cache[k] = Row{it->second.h, it->second.v};
+      Grad g;
+      g.hg.assign(D(), 0);
+      g.vg.assign(D(), 0);
+      grads[k] = g;
+    }
+  }
+
+  // global_push_access.h:48-67 + word2vec_global.h:122-134 (mean) +
+  // word2vec_global.h:176-185 (AdaGrad, fp64)
+  void push(const std::unordered_set<uint64_t> &K) {
+    pushes++;
+    const double lr = (double)cfg.lr;
+    const double fudge = (double)1e-6f;
+    const bool rf = f32();
+    for (auto k : K) {
+      auto git = grads.find(k);
+      if (git == grads.end()) continue;
+      Grad &g = git->second;
+      std::vector<double> hg = g.hg, vg = g.vg;
+      if (g.hc > 0)
+        for (auto &x : hg) x /= g.hc;
+      if (g.vc > 0)
+        for (auto &x : vg) x /= g.vc;
+      std::fill(g.hg.begin(), g.hg.end(), 0.0);
+      std::fill(g.vg.begin(), g.vg.end(), 0.0);
+      g.hc = g.vc = 0;
+      auto sit = server.find(k);
+      if (sit == server.end()) throw std::runtime_error("push of an unknown key");
+      SParam &p = sit->second;
+      for (int i = 0; i < D(); i++) {
+        double h2 = p.h2[i] + hg[i] * hg[i];
+        double v2 = p.v2[i] + vg[i] * vg[i];
+        double hn = p.h[i] + (hg[i] * lr) / std::sqrt(h2 + fudge);
+        double vn = p.v[i] + (vg[i] * lr) / std::sqrt(v2 + fudge);
+        p.h2[i] = store_round(h2, rf);
+        p.v2[i] = store_round(v2, rf);
+        p.h[i] = store_round(hn, rf);
+        p.v[i] = store_round(vn, rf);
+      }
+    }
+  }
+
+  // word2vec_global.h:591-651 TrainModelThread(0) with nthreads = 1
+  void train_iter() {
+    actual_train_words = 0;
+    int line_counter = 0;
+    size_t cur_train_words = 0;
+    std::unordered_set<uint64_t> K;
+    size_t li = 0;
+    while (li < lines.size()) {
+      const Line &ln = lines[li++];
+      learn_instance(ln.words);
+      cur_train_words += ln.words.size();
+      actual_train_words += ln.words.size();
+      line_counter++;
+      if (line_counter == 1) {
+        K = gather_window(li);
+        pull(K);
+      }
+      if (line_counter > 0 && line_counter % cfg.minibatch == 0) {
+        push(K);
+        K = gather_window(li);
+        pull(K);
+      }
+      if (cur_train_words > train_words / 1) break;
+    }
+    push(K);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+typedef struct {
+  int32_t dim, window, negative, min_sentence_length, minibatch, storage_f32;
+  float sample, alpha, lr;
+  uint64_t table_size;
+  int32_t key_mode;
+} orc_w2v_cfg;
+
+const char *orc_last_error(void) { return g_err.c_str(); }
+
+void *orc_w2v_create(const char *corpus_path, const orc_w2v_cfg *c) {
+  try {
+    W2V *m = new W2V();
+    m->cfg = W2VCfg{c->dim,    c->window, c->negative, c->min_sentence_length, c->minibatch, c->storage_f32,
+                    c->sample, c->alpha,  c->lr,       c->table_size,          c->key_mode};
+    std::vector<std::string> raw;
+    if (!read_lines(corpus_path, raw)) {
+      g_err = "cannot open corpus";
+      delete m;
+      return nullptr;
+    }
+    m->lines.resize(raw.size());
+    for (size_t i = 0; i < raw.size(); i++) m->parse(raw[i], m->lines[i]);
+    m->gather_all();
+    if (m->local_keys.size() < 5) {  // word2vec_global.h:556: train() returns
+      g_err = "fewer than 5 keys";
+      delete m;
+      return nullptr;
+    }
+    m->gen_unigram_table();
+    orc_exptable(m->exptab);
+    return m;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
+void orc_w2v_destroy(void *h) { delete (W2V *)h; }
+
+uint64_t orc_w2v_vocab_size(void *h) { return ((W2V *)h)->wordids.size(); }
+uint64_t orc_w2v_train_words(void *h) { return ((W2V *)h)->train_words; }
+
+// vocab in `_wordids` order (unordered_set iteration order) with counts
+void orc_w2v_vocab(void *h, uint64_t *keys, int32_t *counts) {
+  W2V *m = (W2V *)h;
+  for (size_t i = 0; i < m->wordids.size(); i++) {
+    keys[i] = m->wordids[i];
+    counts[i] = m->word_freq[m->wordids[i]];
+  }
+}
+
+// unigram table entries (as vids = index into the vocab order) at given slots
+void orc_w2v_table_at(void *h, const uint64_t *idx, uint64_t n, uint32_t *out) {
+  W2V *m = (W2V *)h;
+  for (uint64_t i = 0; i < n; i++) out[i] = m->table[idx[i]];
+}
+
+// run-length form of the unigram table: start slot of every vid (V+1 entries)
+int orc_w2v_table_starts(void *h, uint64_t *starts) {
+  W2V *m = (W2V *)h;
+  size_t V = m->wordids.size();
+  size_t cur = 0;
+  starts[0] = 0;
+  for (uint64_t a = 1; a < m->table.size(); a++) {
+    if (m->table[a] != m->table[a - 1]) {
+      if (m->table[a] != m->table[a - 1] + 1) return -1;
+      cur = m->table[a];
+      starts[cur] = a;
+    }
+  }
+  for (size_t i = cur + 1; i <= V; i++) starts[i] = m->table.size();
+  return 0;
+}
+
+int orc_w2v_init_rand(void *h, unsigned seed, uint64_t rand_offset) {
+  try {
+    ((W2V *)h)->init_params_rand(seed, rand_offset);
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// set server params (and the full-pull cache) for vocab vids 0..V-1; each row
+// is [h(D) | v(D)] in the given precision (double).
+void orc_w2v_set_params(void *hh, const double *hv) {
+  W2V *m = (W2V *)hh;
+  int D = m->D();
+  for (size_t i = 0; i < m->wordids.size(); i++) {
+    SParam p;
+    p.h.assign(hv + i * 2 * D, hv + i * 2 * D + D);
+    p.v.assign(hv + i * 2 * D + D, hv + i * 2 * D + 2 * D);
+    for (auto &x : p.h) x = store_round(x, m->f32());
+    for (auto &x : p.v) x = store_round(x, m->f32());
+    p.h2.assign(D, 0);
+    p.v2.assign(D, 0);
+    m->server[m->wordids[i]] = p;
+  }
+  m->full_pull_to_cache();
+}
+
+// get server params per vid: [h | v | h2 | v2] (4·D doubles per row)
+void orc_w2v_get_params(void *hh, double *out) {
+  W2V *m = (W2V *)hh;
+  int D = m->D();
+  for (size_t i = 0; i < m->wordids.size(); i++) {
+    SParam &p = m->server[m->wordids[i]];
+    double *o = out + i * 4 * D;
+    std::copy(p.h.begin(), p.h.end(), o);
+    std::copy(p.v.begin(), p.v.end(), o + D);
+    std::copy(p.h2.begin(), p.h2.end(), o + 2 * D);
+    std::copy(p.v2.begin(), p.v2.end(), o + 3 * D);
+  }
+}
+
+void orc_w2v_trace_negatives(void *h, uint64_t cap) { ((W2V *)h)->trace_cap = cap; }
+uint64_t orc_w2v_negatives(void *h, int64_t *out, uint64_t cap) {
+  W2V *m = (W2V *)h;
+  uint64_t n = std::min<uint64_t>(cap, m->neg_trace.size());
+  std::copy(m->neg_trace.begin(), m->neg_trace.begin() + n, out);
+  return n;
+}
+
+int orc_w2v_train(void *h, int niters) {
+  try {
+    for (int i = 0; i < niters; i++) ((W2V *)h)->train_iter();
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// stats: [kept, pushes, pulls, actual_train_words, rng, frng]
+void orc_w2v_stats(void *h, uint64_t *out) {
+  W2V *m = (W2V *)h;
+  out[0] = m->kept;
+  out[1] = m->pushes;
+  out[2] = m->pulls;
+  out[3] = m->actual_train_words;
+  out[4] = m->rng;
+  out[5] = m->frng;
+}
+
+}  // extern "C"
+
+// =============================================================================
+// Sparse logistic regression — apps/logistic/lr.cpp with nthreads = 1.
+// =============================================================================
+namespace {
+
+struct LRIns {
+  float target;
+  std::vector<std::pair<uint32_t, float>> feas;
+};
+
+// lr.cpp:103-131 parse_instance2 (blank / '#' lines are skipped; the
+// reference's read past the NUL of an empty line is not reproduced).
+static bool lr_parse(const std::string &line, LRIns &ins) {
+  const char *p = line.c_str();
+  ins.feas.clear();
+  while (*p == ' ') p++;
+  if (*p == 0 || *p == '#') return false;
+  float value;
+  int nchar, feature;
+  if (std::sscanf(p, "%f%n", &value, &nchar) >= 1) {
+    p += nchar;
+    ins.target = value;
+    while (std::sscanf(p, "%d:%f%n", &feature, &value, &nchar) >= 2) {
+      p += nchar;
+      ins.feas.emplace_back((uint32_t)feature, value);
+    }
+    return true;
+  }
+  throw std::runtime_error("cannot parse line");
+}
+
+struct LRParam {
+  float val = 0, g2 = 0;
+};
+struct LRGrad {
+  float val = 0;
+  int count = 0;
+};
+
+struct LR {
+  int minibatch = 200;
+  float lr = 0.05f;
+  std::vector<std::string> raw;
+  std::vector<LRIns> ins;  // valid lines only
+  std::unordered_set<uint32_t> all_keys;
+  std::unordered_map<uint32_t, LRParam> server;
+  std::unordered_map<uint32_t, float> cache;
+  std::unordered_map<uint32_t, LRGrad> grads;
+  uint64_t frng = std::numeric_limits<unsigned long>::max() / 2;
+  std::vector<double> epoch_err;
+  uint64_t batches = 0;
+
+  // lr.cpp:45-56: init w = global_random().gen_float() on a miss
+  void pull(const std::unordered_set<uint32_t> &K) {
+    for (auto k : K) {
+      auto it = server.find(k);
+      if (it == server.end()) {
+        LRParam p;
+        p.val = flcg_next(frng);
+        it = server.emplace(k, p).first;
+      }
+      cache[k] = it->second.val;
+      grads[k] = LRGrad();
+    }
+  }
+  // lr.cpp:32-38 (mean) + lr.cpp:68-75 (AdaGrad fp32)
+  void push(const std::unordered_set<uint32_t> &K) {
+    for (auto k : K) {
+      auto it = grads.find(k);
+      if (it == grads.end()) continue;
+      LRGrad g = it->second;
+      it->second = LRGrad();
+      if (g.count == 0) throw std::runtime_error("zero-count push (reference stream desync, lr.cpp:34-35)");
+      float m = float(g.val / g.count);
+      LRParam &p = server[k];
+      p.g2 += m * m;
+      p.val += lr * m / float(std::sqrt(p.g2 + 1e-6f));
+    }
+  }
+  // lr.cpp:358-375
+  float learn(const LRIns &x) {
+    float sum = 0;
+    for (auto &f : x.feas) {
+      float w = cache[f.first];
+      float prod = w * f.second;
+      sum += prod;
+    }
+    float predict = 1. / (1. + std::exp(-sum));
+    float error = x.target - predict;
+    for (auto &f : x.feas) {
+      float grad = error * f.second;
+      LRGrad &g = grads[f.first];
+      g.val += grad;
+      g.count++;
+    }
+    return error * error;
+  }
+  void train(int niters) {
+    // lr.cpp:161-166 first full gather + pull
+    std::unordered_set<uint32_t> K0;
+    for (auto &x : ins)
+      for (auto &f : x.feas) K0.insert(f.first);
+    for (auto k : K0) {
+      cache[k] = 0;
+      grads[k] = LRGrad();
+    }
+    pull(K0);
+    for (int it = 0; it < niters; it++) {
+      double total = 0;
+      int nrec = 0;
+      size_t li = 0;
+      while (true) {
+        // gather_keys(file, B): next B+1 valid lines
+        std::unordered_set<uint32_t> K;
+        size_t end = std::min(ins.size(), li + (size_t)minibatch + 1);
+        for (size_t j = li; j < end; j++)
+          for (auto &f : ins[j].feas) K.insert(f.first);
+        if (K.empty()) throw std::runtime_error("empty minibatch: the reference hangs here (global_pull_access.h:33-42)");
+        cache.clear();
+        grads.clear();
+        for (auto k : K) {
+          cache[k] = 0;
+          grads[k] = LRGrad();
+        }
+        pull(K);
+        for (size_t j = li; j < end; j++) {
+          total += learn(ins[j]);
+          nrec++;
+        }
+        push(K);
+        batches++;
+        li = end;
+        if (li >= ins.size()) break;
+      }
+      epoch_err.push_back(total / nrec);
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+void *orc_lr_create(const char *path, int minibatch, float lr) {
+  try {
+    LR *m = new LR();
+    m->minibatch = minibatch;
+    m->lr = lr;
+    if (!read_lines(path, m->raw)) {
+      g_err = "cannot open dataset";
+      delete m;
+      return nullptr;
+    }
+    for (auto &s : m->raw) {
+      LRIns x;
+      if (lr_parse(s, x)) m->ins.push_back(x);
+    }
+    return m;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+void orc_lr_destroy(void *h) { delete (LR *)h; }
+uint64_t orc_lr_num_instances(void *h) { return ((LR *)h)->ins.size(); }
+
+int orc_lr_train(void *h, int niters, double *epoch_err) {
+  try {
+    LR *m = (LR *)h;
+    m->train(niters);
+    for (int i = 0; i < niters; i++) epoch_err[i] = m->epoch_err[m->epoch_err.size() - niters + i];
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+uint64_t orc_lr_num_keys(void *h) { return ((LR *)h)->server.size(); }
+// keys (ascending) with their weight and AdaGrad accumulator
+void orc_lr_params(void *h, uint32_t *keys, float *w, float *g2) {
+  LR *m = (LR *)h;
+  std::vector<uint32_t> ks;
+  for (auto &kv : m->server) ks.push_back(kv.first);
+  std::sort(ks.begin(), ks.end());
+  for (size_t i = 0; i < ks.size(); i++) {
+    keys[i] = ks[i];
+    w[i] = m->server[ks[i]].val;
+    g2[i] = m->server[ks[i]].g2;
+  }
+}
+
+// lr.cpp:376-385 predict_instance with the current server weights; targets out
+void orc_lr_predict(void *h, float *pred, float *target) {
+  LR *m = (LR *)h;
+  for (size_t i = 0; i < m->ins.size(); i++) {
+    float sum = 0;
+    for (auto &f : m->ins[i].feas) {
+      auto it = m->server.find(f.first);
+      float w = it == m->server.end() ? 0.f : it->second.val;
+      float prod = w * f.second;
+      sum += prod;
+    }
+    pred[i] = 1. / (1. + std::exp(-sum));
+    target[i] = m->ins[i].target;
+  }
+}
+
+// order in which the first full pull visits keys (unordered_set iteration)
+uint64_t orc_lr_pull_order(void *h, uint32_t *out, uint64_t cap) {
+  LR *m = (LR *)h;
+  std::unordered_set<uint32_t> K0;
+  for (auto &x : m->ins)
+    for (auto &f : x.feas) K0.insert(f.first);
+  uint64_t n = 0;
+  for (auto k : K0)
+    if (n < cap) out[n++] = k;
+  return n;
+}
+
+}  // extern "C"
