@@ -1,0 +1,190 @@
+"""Headline benchmark: CBOW negative-sampling word2vec trained words/sec on a
+synthetic text8-shaped corpus, D=300, table in one HBM shard per GPU
+(BASELINE.json configs[1]).
+
+A "step" is one reference minibatch: pull of the gathered key set, training of
+`--minibatch` lines (learn_instance for every kept position), push of the mean
+gradients with AdaGrad — all on the GPU through libswps.so.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+N > 1: every rank trains its own corpus shard of the same size (the
+reference's per-rank local data) against its own full-vocab shard: weak
+scaling, replicas (no cross-GPU key sharding yet — see DESIGN.md §Multi-GPU).
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def make_corpus(tokens, vocab, line_len, seed):
+    """Zipf(s=1) over `vocab` word ids, `tokens` tokens in lines of `line_len`
+    (the synthetic text8 stand-in)."""
+    rng = np.random.default_rng(seed)
+    cdf = np.cumsum(1.0 / np.arange(1, vocab + 1))
+    cdf /= cdf[-1]
+    ids = np.searchsorted(cdf, rng.random(tokens), side="right").astype(np.uint32)
+    np.minimum(ids, vocab - 1, out=ids)
+    off = np.arange(0, tokens, line_len, dtype=np.uint64)
+    off = np.append(off, np.uint64(tokens))
+    return ids, off
+
+
+def word_keys(lib, vocab):
+    return np.array([lib.bkdr("w%d" % i) for i in range(vocab)], dtype=np.uint64)
+
+
+def cpu_baseline(ids, off, keys, args, lines):
+    """The oracle (single-threaded C++ port of the reference algorithm, fp64
+    like the reference) on the first `lines` lines of the same corpus."""
+    import oracle
+    oracle.build()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "sample.txt")
+        with open(path, "w") as f:
+            for l in range(lines):
+                a, b = int(off[l]), int(off[l + 1])
+                f.write(" ".join("w%d" % x for x in ids[a:b]) + "\n")
+        m = oracle.W2V(path, args.dim, window=args.window, negative=args.negative, minibatch=args.minibatch,
+                       sample=args.sample, alpha=args.alpha, lr=args.lr, table_size=int(1e8))
+        m.init_rand(1, 2)
+        t0 = time.perf_counter()
+        m.train(1)
+        dt = time.perf_counter() - t0
+        words = m.stats()["actual_train_words"]
+    return {"value": words / dt, "unit": "words/s", "cores": 1, "kind": "port",
+            "sample": "oracle/swps_oracle.cpp (fp64, nthreads=1 semantics) on the first %d lines (%d words) of "
+                      "the same corpus, 1 epoch, D=%d; %.1f s" % (lines, words, args.dim, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dim", type=int, default=300)
+    ap.add_argument("--window", type=int, default=5)
+    ap.add_argument("--negative", type=int, default=5)
+    ap.add_argument("--sample", type=float, default=1e-5)
+    ap.add_argument("--alpha", type=float, default=0.05)
+    ap.add_argument("--lr", type=float, default=0.7)
+    ap.add_argument("--minibatch", type=int, default=1000)
+    ap.add_argument("--tokens", type=int, default=17005207)
+    ap.add_argument("--vocab", type=int, default=253854)
+    ap.add_argument("--line-len", type=int, default=1000)
+    ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--cpu-lines", type=int, default=300)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import swiftmpi_amd as sw
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    ids, off = make_corpus(args.tokens, args.vocab, args.line_len, seed=8 + rank)
+    keys = word_keys(sw, args.vocab)
+    t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
+                 device=local)
+    w = sw.Word2Vec(t, window=args.window, negative=args.negative, minibatch=args.minibatch, sample=args.sample,
+                    alpha=args.alpha, init="ref", profile=True)
+    w.load_tokens(ids, off, keys)
+    w.init()
+    info = w.info()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    w.train_batches(args.warmup)
+    w.sync()
+    s0 = w.stats()
+    w.kernel_times(reset=True)
+    barrier()
+    t0 = time.perf_counter()
+    w.train_batches(args.steps)
+    w.sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    s1 = w.stats()
+    kt = w.kernel_times()
+    words = s1["words"] - s0["words"]
+    if dist is not None:
+        tt = torch.tensor([dt, float(words)], dtype=torch.float64, device="cuda")
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        dt, total_words = float(mx[0]), float(tt[1])
+    else:
+        total_words = float(words)
+
+    D, es = args.dim, (8 if args.dtype == "f64" else 4)
+    kept = s1["kept"] - s0["kept"]
+    ctx_rows, tgt_rows = s1["ctx_rows"] - s0["ctx_rows"], s1["tgt_rows"] - s0["tgt_rows"]
+    pulled, pushed = s1["pulled"] - s0["pulled"], s1["pushed"] - s0["pushed"]
+    # SURVEY.md §8(d) algorithmic bytes: each touched row read once (forward)
+    fwd_ms, fwd_n = kt["forward"]
+    fwd_bytes = es * D * (ctx_rows + tgt_rows)
+    fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+    # whole step: rows read + gradients written (2x) + pull (16D/key) + push (40D+8 per key)
+    step_bytes = 2 * es * D * (ctx_rows + tgt_rows) + pulled * 4 * es * D + pushed * (10 * es * D + 8)
+    step_gbs = step_bytes / dt / 1e9
+
+    out = {
+        "metric": "SGNS trained words/sec at 1/8 GPUs; sparse push/pull HBM GB/s vs peak",
+        "value": total_words / dt,
+        "unit": "words/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 storage, f64 accumulate" if args.dtype == "f32" else "f64",
+        "data": "synthetic Zipf(s=1) text8 stand-in, random-init (reference glibc-rand) params",
+        "config": {"workload": "word2vec CBOW-NS (the reference's 'SGNS' app) text8-shaped corpus %d tokens, "
+                               "vocab %d, dim %d, window %d, negative %d, sample %g, minibatch %d lines of %d "
+                               "tokens, table in one HBM shard" % (args.tokens, info["vocab"], D, args.window,
+                                                                  args.negative, args.sample, args.minibatch,
+                                                                  args.line_len),
+                   "global_batch": args.minibatch * world, "parallelism": "replicas" if world > 1 else "1 GPU",
+                   "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"]},
+        "roofline": {"bound": "hbm", "kernel": "k_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1),
+                     "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS},
+        "kernel_ms": {k: v[0] for k, v in kt.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(ids, off, keys, args, args.cpu_lines)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,213 @@
+/*
+ * swps.h — C ABI of the MI355X-native SwiftMPI hot path (libswps.so).
+ *
+ * One process per GPU.  The library owns all device memory; callers pass
+ * plain pointers and sizes (device pointers where noted "d_", host pointers
+ * otherwise).  Every function returns 0 (SWPS_OK) or a negative SWPS_E_*
+ * code and never aborts; the message of the last failure on the calling
+ * thread is returned by swps_last_error().
+ *
+ * Reference interfaces replaced (paths relative to logicxin/SwiftMPI src/):
+ *   swps_table_*      SparseTable / SparseTableShard   parameter/sparsetable.h:17-149
+ *                     + the server's pull/push handlers cluster/server.h:106-176
+ *   swps_pull         GlobalPullAccess::pull_with_barrier
+ *                         parameter/global_pull_access.h:28-43  (+ accessmethod.h:63-70)
+ *   swps_push         GlobalPushAccess::push_with_barrier
+ *                         parameter/global_push_access.h:26-43  (+ accessmethod.h:102-121)
+ *   swps_assign/load  SparseTable::assign, ClusterServer::load  sparsetable.h:117, server.h:49-62
+ *   swps_dump         SparseTable::output                        sparsetable.h:127-132
+ *   swps_to_node_id   BasicHashFrag::to_node_id                  cluster/hashfrag.h:51-56
+ *   swps_w2v_*        Word2Vec<MiniBatch>::train / MiniBatch     apps/word2vec/word2vec_global.h:284-731
+ *   swps_lr_*         LR::train / learn_instance / predict       apps/logistic/lr.cpp:157-398
+ */
+#ifndef SWPS_H_
+#define SWPS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes --------------------------------------------------------- */
+#define SWPS_OK 0
+#define SWPS_E_OOM (-1)         /* device or host allocation failed / table full */
+#define SWPS_E_BADKEY (-2)      /* push of a key the table never saw (server.h CHECK) */
+#define SWPS_E_HIP (-3)         /* HIP runtime error */
+#define SWPS_E_RCCL (-4)        /* RCCL error */
+#define SWPS_E_CFG (-5)         /* invalid configuration */
+#define SWPS_E_STATE (-6)       /* call out of order */
+#define SWPS_E_UNSUPPORTED (-7) /* input whose reference behaviour is undefined */
+#define SWPS_E_IO (-8)          /* file I/O */
+
+const char *swps_last_error(void);
+int swps_version(void);
+
+/* ---- parameter table (server shard in HBM) ------------------------------ */
+/* Layouts: one row per key.
+ *   SWPS_LAYOUT_W2V : [h(D) | v(D) | h2sum(D) | v2sum(D)]   (WParam, word2vec_global.h:34-48)
+ *     pull value  = [h(D) | v(D)]                           (WLocalParam)
+ *     push value  = [mean h_grad(D) | mean v_grad(D)] fp64  (WLocalGrad wire, :122-134)
+ *     push rule   = AdaGrad ascent                          (:176-185)
+ *   SWPS_LAYOUT_LR  : [w | grad2sum]                         (LRParam, lr.cpp:7-10)
+ *     pull value  = [w]; push value = [mean grad] fp32;  AdaGrad (lr.cpp:68-75)
+ */
+#define SWPS_LAYOUT_W2V 0
+#define SWPS_LAYOUT_LR 1
+
+#define SWPS_F32 0 /* fp32 storage, fp64 arithmetic */
+#define SWPS_F64 1 /* fp64 storage (the reference's Vec precision) */
+
+/* key initialisation on a pull miss (PullAccessMethod::init_param) */
+#define SWPS_INIT_ZERO 0
+#define SWPS_INIT_HASH 1 /* W2V: (u-0.5)/D, LR: u in [0,1); u from (seed,key,i) */
+
+typedef struct swps_table swps_table;
+
+typedef struct {
+  int32_t device;     /* HIP device ordinal */
+  int32_t layout;     /* SWPS_LAYOUT_* */
+  int32_t dtype;      /* SWPS_F32 / SWPS_F64 */
+  int32_t dim;        /* D (W2V) — ignored for LR */
+  uint64_t capacity;  /* max keys held by this shard */
+  float learning_rate; /* server.initial_learning_rate */
+  float fudge;        /* AdaGrad fudge factor (reference: 1e-6f) */
+  int32_t init_mode;  /* SWPS_INIT_* */
+  uint64_t seed;
+} swps_table_cfg;
+
+int swps_table_create(const swps_table_cfg *cfg, swps_table **out);
+int swps_table_destroy(swps_table *t);
+int swps_table_size(swps_table *t, uint64_t *nkeys);
+int swps_table_sync(swps_table *t);
+/* per-key element counts of a full row / a pull value / a push value */
+int swps_table_row_elems(swps_table *t, int32_t *row, int32_t *pull, int32_t *push);
+
+/* Batched pull: find-or-insert each key (keys in one call must be distinct,
+ * as the reference's std::unordered_set key sets are) and write its pull
+ * value to d_vals[n][pull elems] in the table dtype. */
+int swps_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals);
+/* Batched push: apply the push rule with the mean gradients d_grads[n][push
+ * elems] (fp64 for W2V, fp32 for LR).  Unknown key -> SWPS_E_BADKEY. */
+int swps_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads);
+/* Overwrite / read full rows (table dtype, d_rows[n][row elems]). */
+int swps_assign(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_rows);
+int swps_export(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_rows);
+/* all keys currently held (host array of capacity cap) */
+int swps_table_keys(swps_table *t, uint64_t *keys, uint64_t cap, uint64_t *n);
+/* Text dump/load in the reference format (sparsetable.h:63-70):
+ *   W2V: "key\tv0 v1 ... v(D-1)\th0 ... h(D-1)\n"   (word2vec_global.h:102-112)
+ *   LR : "key\tw\n"                                  (lr.cpp:24-27)
+ * at ostream default precision (6 significant digits). load keeps only keys
+ * owned by `node_id` under the hash-frag map (server.h:49-62); node_id 0 or
+ * world 1 keeps all. */
+int swps_dump(swps_table *t, const char *path);
+int swps_load(swps_table *t, const char *path, int32_t frag_num, int32_t world, int32_t node_id);
+
+/* ---- key -> node map (BasicHashFrag) ------------------------------------ */
+uint64_t swps_fmix64(uint64_t x);                       /* utils/HashFunction.h:16-24 */
+uint64_t swps_bkdr(const char *s);                      /* utils/string.h:130-137 */
+int swps_hashfrag_table(int32_t frag_num, int32_t num_nodes, uint32_t *out); /* hashfrag.h:33-49 */
+int swps_to_node_id(const uint64_t *keys, uint64_t n, int32_t frag_num, const uint32_t *table,
+                    int32_t *out);                      /* hashfrag.h:51-56 (host) */
+
+/* ---- word2vec CBOW negative sampling (apps/word2vec) --------------------- */
+typedef struct swps_w2v swps_w2v;
+
+#define SWPS_KEY_BKDR 0 /* word2vec_global.h:205-207 hash_fn */
+#define SWPS_KEY_ATOI 1 /* word2vec.h:221 hash_fn2 */
+
+#define SWPS_W2V_INIT_REF 0   /* reference: glibc rand() stream, _local_keys order */
+#define SWPS_W2V_INIT_TABLE 1 /* keep whatever the table holds (HASH/ZERO/loaded) */
+
+typedef struct {
+  int32_t window;              /* word2vec.window */
+  int32_t negative;            /* word2vec.negative */
+  int32_t min_sentence_length; /* word2vec.min_sentence_length */
+  int32_t minibatch;           /* worker.minibatch (lines) */
+  float sample;                /* word2vec.sample (<0: no subsampling) */
+  float alpha;                 /* word2vec.learning_rate */
+  uint64_t unigram_size;       /* table_size (reference: 1e8) */
+  int32_t key_mode;            /* SWPS_KEY_* */
+  int32_t init_mode;           /* SWPS_W2V_INIT_* */
+  uint32_t rand_seed;          /* glibc srand seed (reference: 1) */
+  uint64_t rand_offset;        /* rand() calls before the first pull (reference: 2 port binds) */
+  int32_t deterministic;       /* 1: fixed reduction order (always true today) */
+  int32_t profile;             /* 1: time kernels with HIP events */
+} swps_w2v_cfg;
+
+/* The table must use SWPS_LAYOUT_W2V; ctx is bound to the table's device. */
+int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out);
+int swps_w2v_destroy(swps_w2v *w);
+/* Corpus ingest.  text: one instance per line, words split on ' ' only.
+ * tokens: word ids into word_keys (the key each word string hashes to);
+ * line_off has nlines+1 entries. */
+int swps_w2v_load_text(swps_w2v *w, const char *path);
+int swps_w2v_load_tokens(swps_w2v *w, const uint32_t *word_ids, uint64_t ntok, const uint64_t *line_off,
+                         uint64_t nlines, const uint64_t *word_keys, uint64_t nwords);
+/* vocab in _wordids order (vid order): keys[V], counts[V]; V via *n */
+int swps_w2v_vocab(swps_w2v *w, uint64_t *keys, int32_t *counts, uint64_t cap, uint64_t *n);
+int swps_w2v_info(swps_w2v *w, uint64_t *out8); /* V, train_words, nlines, ntok, nbatches, max_batch_tok, lstate, fstate */
+/* first full pull: insert every vocab key (init per cfg.init_mode) and fill the cache */
+int swps_w2v_init(swps_w2v *w);
+/* Train the next `count` minibatches of the per-epoch schedule
+ * (word2vec_global.h:591-651); the batch cursor wraps into the next epoch. */
+int swps_w2v_train_batches(swps_w2v *w, uint64_t count);
+int swps_w2v_train_epochs(swps_w2v *w, int32_t niters);
+int swps_w2v_sync(swps_w2v *w);
+/* cumulative stats: [batches, kept positions, train words, gradient records, lstate, fstate,
+ *  pulled keys, pushed keys, context rows read, target rows read] */
+int swps_w2v_stats(swps_w2v *w, uint64_t *out10);
+/* rows of all vocab keys in vid order, host buffer [V][4D] fp64 */
+int swps_w2v_get_params(swps_w2v *w, double *out);
+/* set h,v of all vocab keys (vid order, host [V][2D] fp64), zero h2/v2, refresh the cache */
+int swps_w2v_set_params(swps_w2v *w, const double *hv);
+/* unigram table entries (vids) at host-given slots */
+int swps_w2v_unigram_at(swps_w2v *w, const uint64_t *idx, uint64_t n, uint32_t *out);
+/* negative-draw trace of the next traced batch (vids), -1 = cleared */
+int swps_w2v_trace_negatives(swps_w2v *w, uint64_t cap);
+int swps_w2v_negatives(swps_w2v *w, int64_t *out, uint64_t cap, uint64_t *n);
+/* per-kernel device time (ms) and launch counts since the last reset:
+ * out[2*k] = ms, out[2*k+1] = launches for k in {keep, forward, sort, gather, push, pull} */
+int swps_w2v_kernel_times(swps_w2v *w, double *out12, int32_t reset);
+/* the HIP stream all of this context's work is issued on */
+void *swps_w2v_stream(swps_w2v *w);
+
+/* ---- host-only helpers (no device needed; used by the CPU test-suite) ---- */
+/* run-length form of gen_unigram_table (word2vec_global.h:467-497): start slot
+ * of each word in vocab order (V+1 entries, starts[V] = table_size) */
+int swps_unigram_starts(const uint64_t *keys, const int32_t *counts, uint64_t V, uint64_t table_size,
+                        uint64_t *starts);
+/* glibc rand() after srand(seed), `skip` outputs discarded (Vec::randInit's stream) */
+int swps_glibc_rand(uint32_t seed, uint64_t skip, uint64_t n, int32_t *out);
+
+/* ---- sparse logistic regression (apps/logistic/lr.cpp) ------------------- */
+typedef struct swps_lr swps_lr;
+
+typedef struct {
+  int32_t minibatch;  /* worker.minibatch: a batch is B+1 valid lines (lr.cpp:308-354) */
+  int32_t init_ref;   /* 1: first-pull init from the float LCG in _local_keys order (lr.cpp:48-50) */
+  int32_t profile;
+} swps_lr_cfg;
+
+int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out);
+int swps_lr_destroy(swps_lr *l);
+/* libsvm/libfm text (lr.cpp:103-131) or CSR arrays (row_off has nrows+1) */
+int swps_lr_load_text(swps_lr *l, const char *path);
+int swps_lr_load_csr(swps_lr *l, const float *labels, uint64_t nrows, const uint64_t *row_off, const uint32_t *feat,
+                     const float *vals);
+int swps_lr_init(swps_lr *l);
+/* one epoch per iter; err_out[niters] = mean squared error (lr.cpp:231) */
+int swps_lr_train(swps_lr *l, int32_t niters, double *err_out);
+int swps_lr_train_batches(swps_lr *l, uint64_t count);
+int swps_lr_predict(swps_lr *l, float *pred_out, float *target_out, uint64_t cap);
+int swps_lr_params(swps_lr *l, uint32_t *keys, float *w, float *g2, uint64_t cap, uint64_t *n);
+int swps_lr_info(swps_lr *l, uint64_t *out4); /* nrows, nkeys, nbatches, nnz */
+int swps_lr_sync(swps_lr *l);
+int swps_lr_kernel_times(swps_lr *l, double *out8, int32_t reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWPS_H_ */

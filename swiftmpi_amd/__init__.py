@@ -1,0 +1,372 @@
+"""swiftmpi_amd — MI355X-native rebuild of SwiftMPI's data-parallel hot path.
+
+The pull -> gradient -> push loop of SwiftMPI's sparse parameter server
+(word2vec CBOW negative sampling, sparse logistic regression) runs as HIP
+kernels over HBM-resident key-hash-sharded tables (libswps.so, C ABI in
+include/swps.h).  This package is the Python mirror of the reference's app
+interfaces over that ABI:
+
+    Table     <- parameter/sparsetable.h + cluster/server.h pull/push handlers
+    Word2Vec  <- apps/word2vec/word2vec_global.h  (Word2Vec<MiniBatch>)
+    LR        <- apps/logistic/lr.cpp             (LR)
+    Config    <- utils/ConfigParser.h
+
+Every compute call goes through libswps.so; if it is missing the import of the
+classes below raises (no CPU fallback).
+"""
+import ctypes
+
+import numpy as np
+
+from . import capi
+from .capi import SwpsError, check, ptr
+
+__all__ = ["Table", "Word2Vec", "LR", "Config", "SwpsError", "bkdr", "fmix64", "hashfrag_table", "to_node_id",
+           "load_library"]
+
+
+def load_library():
+    return capi.lib()
+
+
+def bkdr(word):
+    """BKDRHash<size_t>(word, 13131) (utils/string.h:130-137)."""
+    if isinstance(word, str):
+        word = word.encode("utf-8")
+    return int(capi.lib().swps_bkdr(word))
+
+
+def fmix64(x):
+    return int(capi.lib().swps_fmix64(x))
+
+
+def hashfrag_table(frag_num, num_nodes):
+    out = np.zeros(frag_num, dtype=np.uint32)
+    check(capi.lib().swps_hashfrag_table(frag_num, num_nodes, ptr(out)))
+    return out
+
+
+def to_node_id(keys, frag_num, table):
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    out = np.zeros(len(keys), dtype=np.int32)
+    check(capi.lib().swps_to_node_id(ptr(keys), len(keys), frag_num, ptr(table), ptr(out)))
+    return out
+
+
+def unigram_starts(keys, counts, table_size=int(1e8)):
+    """Run-length form of gen_unigram_table (host helper of libswps)."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    counts = np.ascontiguousarray(counts, dtype=np.int32)
+    out = np.zeros(len(keys) + 1, dtype=np.uint64)
+    check(capi.lib().swps_unigram_starts(ptr(keys), ptr(counts), len(keys), table_size, ptr(out)))
+    return out
+
+
+def glibc_rand(n, seed=1, skip=0):
+    out = np.zeros(n, dtype=np.int32)
+    check(capi.lib().swps_glibc_rand(seed, skip, n, ptr(out)))
+    return out
+
+
+class Config:
+    """The reference's INI-like config (utils/ConfigParser.h:84-115):
+    ``[section]`` headers, ``key: value`` lines, ``#`` comments, ``import path``.
+    ``get(section, key)`` raises KeyError like the reference's CHECK."""
+
+    def __init__(self, path=None):
+        self.sections = {}
+        if path:
+            self.parse(path)
+
+    def parse(self, path):
+        cur = ""
+        with open(path) as f:
+            for line in f:
+                line = line.strip(" \t\n\r")
+                if not line or line.startswith("#"):
+                    continue
+                if line.startswith("import"):
+                    sub = line.split(" ", 1)[1].strip()
+                    if sub == path:
+                        raise ValueError("recursive import")
+                    self.parse(sub)
+                    continue
+                if line[0] == "[" and line[-1] == "]":
+                    cur = line[1:-1].strip()
+                    if not cur:
+                        raise ValueError("empty section")
+                    continue
+                if ":" not in line:
+                    raise ValueError(f"bad config line: {line}")
+                k, v = line.split(":", 1)
+                self.sections.setdefault(cur, {}).setdefault(k.strip(), v.strip())
+        return self
+
+    def get(self, section, key):
+        try:
+            return self.sections[section][key]
+        except KeyError:
+            raise KeyError(f"no such key:\t[{section}]\t{key}")
+
+    def get_int(self, section, key):
+        return int(self.get(section, key))
+
+    def get_float(self, section, key):
+        return float(self.get(section, key))
+
+
+class Table:
+    """One HBM parameter shard (SparseTable + server access methods)."""
+
+    def __init__(self, layout="w2v", dim=100, capacity=1 << 20, dtype="f32", learning_rate=0.7, fudge=1e-6,
+                 init="hash", seed=0, device=0):
+        cfg = capi.TableCfg(device, capi.LAYOUT_W2V if layout == "w2v" else capi.LAYOUT_LR,
+                            capi.F64 if dtype == "f64" else capi.F32, dim, capacity, learning_rate, fudge,
+                            capi.INIT_HASH if init == "hash" else capi.INIT_ZERO, seed)
+        h = ctypes.c_void_p()
+        check(capi.lib().swps_table_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.layout, self.dim, self.dtype, self.device = layout, dim, dtype, device
+        r, p, q = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        capi.lib().swps_table_row_elems(self.h, ctypes.byref(r), ctypes.byref(p), ctypes.byref(q))
+        self.row_elems, self.pull_elems, self.push_elems = r.value, p.value, q.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            capi.lib().swps_table_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def torch_dtype(self):
+        import torch
+        return torch.float64 if self.dtype == "f64" else torch.float32
+
+    def size(self):
+        n = ctypes.c_uint64()
+        check(capi.lib().swps_table_size(self.h, ctypes.byref(n)))
+        return n.value
+
+    def pull(self, keys):
+        """keys: int64/uint64 CUDA tensor of distinct keys -> [n, pull_elems] tensor."""
+        import torch
+        out = torch.empty((keys.numel(), self.pull_elems), dtype=self.torch_dtype, device=keys.device)
+        check(capi.lib().swps_pull(self.h, ptr(keys), keys.numel(), ptr(out)))
+        return out
+
+    def push(self, keys, grads):
+        """grads: [n, push_elems] CUDA tensor, fp64 (w2v) or fp32 (lr) — the reference wire types."""
+        check(capi.lib().swps_push(self.h, ptr(keys), keys.numel(), ptr(grads)))
+        capi.lib().swps_table_sync(self.h)
+
+    def assign(self, keys, rows):
+        check(capi.lib().swps_assign(self.h, ptr(keys), keys.numel(), ptr(rows)))
+
+    def export(self, keys):
+        import torch
+        out = torch.empty((keys.numel(), self.row_elems), dtype=self.torch_dtype, device=keys.device)
+        check(capi.lib().swps_export(self.h, ptr(keys), keys.numel(), ptr(out)))
+        return out
+
+    def keys(self):
+        n = self.size()
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        m = ctypes.c_uint64()
+        check(capi.lib().swps_table_keys(self.h, ptr(out), len(out), ctypes.byref(m)))
+        return out[:m.value]
+
+    def dump(self, path):
+        check(capi.lib().swps_dump(self.h, path.encode()))
+
+    def load(self, path, frag_num=1000, world=1, node_id=0):
+        check(capi.lib().swps_load(self.h, path.encode(), frag_num, world, node_id))
+
+
+KT_NAMES = ["keep", "forward", "sort", "gather", "push", "pull"]
+
+
+class Word2Vec:
+    """CBOW negative-sampling word2vec (Word2Vec<MiniBatch>, word2vec_global.h:541-748)."""
+
+    def __init__(self, table, window=5, negative=5, min_sentence_length=1, minibatch=100, sample=1e-5, alpha=0.05,
+                 unigram_size=int(1e8), key_mode="bkdr", init="ref", rand_seed=1, rand_offset=2, profile=False):
+        assert table.layout == "w2v"
+        cfg = capi.W2VCfg(window, negative, min_sentence_length, minibatch, sample, alpha, unigram_size,
+                          capi.KEY_ATOI if key_mode == "atoi" else capi.KEY_BKDR,
+                          capi.W2V_INIT_REF if init == "ref" else capi.W2V_INIT_TABLE, rand_seed, rand_offset, 1,
+                          int(profile))
+        h = ctypes.c_void_p()
+        check(capi.lib().swps_w2v_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.table = table
+        self.dim = table.dim
+
+    @classmethod
+    def from_config(cls, config, table_kwargs=None, **kw):
+        """Build a Table + Word2Vec from the reference's demo.conf keys."""
+        c = config if isinstance(config, Config) else Config(config)
+        dim = c.get_int("word2vec", "len_vec")
+        tk = dict(layout="w2v", dim=dim, learning_rate=c.get_float("server", "initial_learning_rate"))
+        tk.update(table_kwargs or {})
+        t = Table(**tk)
+        args = dict(window=c.get_int("word2vec", "window"), negative=c.get_int("word2vec", "negative"),
+                    min_sentence_length=c.get_int("word2vec", "min_sentence_length"),
+                    minibatch=c.get_int("worker", "minibatch"), sample=c.get_float("word2vec", "sample"),
+                    alpha=c.get_float("word2vec", "learning_rate"))
+        args.update(kw)
+        return cls(t, **args)
+
+    def close(self):
+        if getattr(self, "h", None):
+            capi.lib().swps_w2v_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def load_text(self, path):
+        check(capi.lib().swps_w2v_load_text(self.h, path.encode()))
+
+    def load_tokens(self, word_ids, line_off, word_keys):
+        word_ids = np.ascontiguousarray(word_ids, dtype=np.uint32)
+        line_off = np.ascontiguousarray(line_off, dtype=np.uint64)
+        word_keys = np.ascontiguousarray(word_keys, dtype=np.uint64)
+        check(capi.lib().swps_w2v_load_tokens(self.h, ptr(word_ids), len(word_ids), ptr(line_off),
+                                               len(line_off) - 1, ptr(word_keys), len(word_keys)))
+
+    def info(self):
+        o = np.zeros(8, dtype=np.uint64)
+        check(capi.lib().swps_w2v_info(self.h, ptr(o)))
+        return dict(zip(["vocab", "train_words", "lines", "tokens", "batches", "max_batch_tokens", "lstate",
+                         "fstate"], [int(x) for x in o]))
+
+    def vocab(self):
+        V = self.info()["vocab"]
+        keys = np.zeros(V, dtype=np.uint64)
+        counts = np.zeros(V, dtype=np.int32)
+        n = ctypes.c_uint64()
+        check(capi.lib().swps_w2v_vocab(self.h, ptr(keys), ptr(counts), V, ctypes.byref(n)))
+        return keys, counts
+
+    def init(self):
+        check(capi.lib().swps_w2v_init(self.h))
+
+    def train_batches(self, count):
+        check(capi.lib().swps_w2v_train_batches(self.h, count))
+
+    def train(self, niters=1):
+        check(capi.lib().swps_w2v_train_epochs(self.h, niters))
+
+    def sync(self):
+        check(capi.lib().swps_w2v_sync(self.h))
+
+    def stats(self):
+        o = np.zeros(10, dtype=np.uint64)
+        check(capi.lib().swps_w2v_stats(self.h, ptr(o)))
+        return dict(zip(["batches", "kept", "words", "pairs", "lstate", "fstate", "pulled", "pushed", "ctx_rows",
+                         "tgt_rows"], [int(x) for x in o]))
+
+    def get_params(self):
+        V = self.info()["vocab"]
+        out = np.zeros((V, 4 * self.dim), dtype=np.float64)
+        check(capi.lib().swps_w2v_get_params(self.h, ptr(out)))
+        return out
+
+    def set_params(self, hv):
+        hv = np.ascontiguousarray(hv, dtype=np.float64)
+        check(capi.lib().swps_w2v_set_params(self.h, ptr(hv)))
+
+    def unigram_at(self, idx):
+        idx = np.ascontiguousarray(idx, dtype=np.uint64)
+        out = np.zeros(len(idx), dtype=np.uint32)
+        check(capi.lib().swps_w2v_unigram_at(self.h, ptr(idx), len(idx), ptr(out)))
+        return out
+
+    def trace_negatives(self, cap):
+        check(capi.lib().swps_w2v_trace_negatives(self.h, cap))
+
+    def negatives(self, cap):
+        out = np.zeros(max(cap, 1), dtype=np.int64)
+        n = ctypes.c_uint64()
+        check(capi.lib().swps_w2v_negatives(self.h, ptr(out), cap, ctypes.byref(n)))
+        return out[:n.value]
+
+    def kernel_times(self, reset=False):
+        o = np.zeros(12, dtype=np.float64)
+        check(capi.lib().swps_w2v_kernel_times(self.h, ptr(o), int(reset)))
+        return {k: (o[2 * i], int(o[2 * i + 1])) for i, k in enumerate(KT_NAMES)}
+
+    def stream(self):
+        return capi.lib().swps_w2v_stream(self.h)
+
+
+class LR:
+    """Sparse logistic regression with server-side AdaGrad (lr.cpp:133-411)."""
+
+    def __init__(self, table, minibatch=200, init_ref=True, profile=False):
+        assert table.layout == "lr"
+        cfg = capi.LRCfg(minibatch, int(init_ref), int(profile))
+        h = ctypes.c_void_p()
+        check(capi.lib().swps_lr_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.table = table
+
+    def close(self):
+        if getattr(self, "h", None):
+            capi.lib().swps_lr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def load_text(self, path):
+        check(capi.lib().swps_lr_load_text(self.h, path.encode()))
+
+    def load_csr(self, labels, row_off, feat, vals):
+        labels = np.ascontiguousarray(labels, dtype=np.float32)
+        row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+        feat = np.ascontiguousarray(feat, dtype=np.uint32)
+        vals = np.ascontiguousarray(vals, dtype=np.float32)
+        check(capi.lib().swps_lr_load_csr(self.h, ptr(labels), len(labels), ptr(row_off), ptr(feat), ptr(vals)))
+
+    def init(self):
+        check(capi.lib().swps_lr_init(self.h))
+
+    def train(self, niters):
+        err = np.zeros(niters, dtype=np.float64)
+        check(capi.lib().swps_lr_train(self.h, niters, ptr(err)))
+        return err
+
+    def train_batches(self, count):
+        check(capi.lib().swps_lr_train_batches(self.h, count))
+
+    def sync(self):
+        check(capi.lib().swps_lr_sync(self.h))
+
+    def info(self):
+        o = np.zeros(4, dtype=np.uint64)
+        check(capi.lib().swps_lr_info(self.h, ptr(o)))
+        return dict(zip(["rows", "keys", "batches", "nnz"], [int(x) for x in o]))
+
+    def predict(self):
+        n = self.info()["rows"]
+        p = np.zeros(n, dtype=np.float32)
+        t = np.zeros(n, dtype=np.float32)
+        check(capi.lib().swps_lr_predict(self.h, ptr(p), ptr(t), n))
+        return p, t
+
+    def params(self):
+        n = self.info()["keys"]
+        keys = np.zeros(max(n, 1), dtype=np.uint32)
+        w = np.zeros(max(n, 1), dtype=np.float32)
+        g2 = np.zeros(max(n, 1), dtype=np.float32)
+        m = ctypes.c_uint64()
+        check(capi.lib().swps_lr_params(self.h, ptr(keys), ptr(w), ptr(g2), len(keys), ctypes.byref(m)))
+        return keys[:m.value], w[:m.value], g2[:m.value]
+
+    def kernel_times(self, reset=False):
+        o = np.zeros(8, dtype=np.float64)
+        check(capi.lib().swps_lr_kernel_times(self.h, ptr(o), int(reset)))
+        return {k: (o[2 * i], int(o[2 * i + 1])) for i, k in enumerate(["forward", "sort", "gather", "push"])}

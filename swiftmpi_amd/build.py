@@ -1,0 +1,84 @@
+"""Build libswps.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+    python -m swiftmpi_amd.build [--force]
+
+The shared library lands in swiftmpi_amd/lib/ (git-ignored, travels to the GPU
+box with the repo snapshot).  Object files are cached in build/.
+"""
+import concurrent.futures
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+OBJDIR = os.path.join(ROOT, "build", "swps")
+LIBDIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIBDIR, "libswps.so")
+ARCH = os.environ.get("SWPS_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+# -ffp-contract=off: the reference's fp64 arithmetic rounds every product
+# before the add (x86-64 without FMA); contracting into fma would change bits.
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}", "-I" + INCLUDE, "-I" + CSRC,
+          "-Wall", "-Wno-unused-result"]
+LDFLAGS = ["-shared", f"--offload-arch={ARCH}"]
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+
+
+def headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    return hs
+
+
+def _obj(src):
+    return os.path.join(OBJDIR, os.path.basename(src) + ".o")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src):
+    obj = _obj(src)
+    cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = sources()
+    hdrs = headers()
+    todo = [s for s in srcs if force or _stale(_obj(s), [s] + hdrs)]
+    if todo:
+        workers = min(len(todo), int(os.environ.get("MAX_JOBS", "8")), 16)
+        with concurrent.futures.ThreadPoolExecutor(workers) as ex:
+            for obj in ex.map(_compile, todo):
+                if verbose:
+                    print("compiled", obj)
+    objs = [_obj(s) for s in srcs]
+    if force or todo or _stale(LIB, objs):
+        cmd = [HIPCC] + LDFLAGS + objs + ["-o", LIB]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print("linked", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,138 @@
+// Host-side utilities of libswps: error state, BKDR key hashing, glibc rand()
+// emulation, the hash-frag node map and the reference config file format.
+#include <cstdio>
+#include <fstream>
+
+#include "swps_internal.h"
+
+namespace swps {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+// utils/string.h:130-137 BKDRHash<size_t>(s, 13131); `char` is signed on
+// x86-64 so non-ASCII bytes add sign-extended values.
+uint64_t bkdr(const char *s) {
+  uint64_t h = 0;
+  while (*s) h = h * 13131ULL + (uint64_t)(int64_t)(signed char)(*s++);
+  return h;
+}
+
+// glibc srandom_r/random_r for TYPE_3 (degree 31, separation 3): the state
+// is seeded by the Park–Miller LCG, 310 outputs are discarded, and each output
+// is (r[i-31] + r[i-3]) >> 1.  Reproduces rand() after srand(seed), which the
+// reference's Vec::randInit draws from (utils/vec1.h:229-232).
+GlibcRand::GlibcRand(uint32_t seed) {
+  if (seed == 0) seed = 1;
+  int32_t s[34];
+  s[0] = (int32_t)seed;
+  for (int i = 1; i < 31; i++) {
+    int64_t hi = s[i - 1] / 127773, lo = s[i - 1] % 127773;
+    int64_t w = 16807 * lo - 2836 * hi;
+    if (w < 0) w += 2147483647;
+    s[i] = (int32_t)w;
+  }
+  for (int i = 31; i < 34; i++) s[i] = s[i - 31];
+  for (int i = 0; i < 34; i++) r[i] = s[i];
+  idx = 0;  // r holds o[i..i+33] as a ring starting at idx
+  for (int i = 34; i < 344; i++) (void)next();
+  produced = 0;
+}
+
+int32_t GlibcRand::next() {
+  // ring of the last 34 words, r[idx] the oldest (i-34): new = r[i-31] + r[i-3]
+  int32_t v = (int32_t)((uint32_t)r[(idx + 3) % 34] + (uint32_t)r[(idx + 31) % 34]);
+  r[idx] = v;
+  idx = (idx + 1) % 34;
+  produced++;
+  return (int32_t)((uint32_t)v >> 1);
+}
+
+int Config::parse(const std::string &path) {
+  std::ifstream f(path);
+  if (!f) return fail(SWPS_E_IO, "conf can not open: " + path);
+  auto trim = [](std::string s) {
+    size_t a = s.find_first_not_of(" \t\n\r");
+    if (a == std::string::npos) return std::string();
+    size_t b = s.find_last_not_of(" \t\n\r");
+    return s.substr(a, b - a + 1);
+  };
+  std::string line, cur;
+  while (std::getline(f, line)) {
+    line = trim(line);
+    if (line.empty() || line[0] == '#') continue;
+    if (line.compare(0, 6, "import") == 0) {
+      std::string p = trim(line.substr(line.find(' ') + 1));
+      if (p == path) return fail(SWPS_E_CFG, "recursive import");
+      SWPS_TRY(parse(p));
+      continue;
+    }
+    if (line.front() == '[' && line.back() == ']') {
+      cur = trim(line.substr(1, line.size() - 2));
+      if (cur.empty()) return fail(SWPS_E_CFG, "empty section");
+      continue;
+    }
+    size_t c = line.find(':');
+    if (c == std::string::npos) return fail(SWPS_E_CFG, "bad config line: " + line);
+    std::string k = trim(line.substr(0, c)), v = trim(line.substr(c + 1));
+    bool placed = false;
+    for (auto &s : sections)
+      if (s.first == cur) {
+        bool dup = false;
+        for (auto &kv : s.second) dup |= kv.first == k;
+        if (!dup) s.second.emplace_back(k, v);  // std::map::insert keeps the first
+        placed = true;
+      }
+    if (!placed) sections.push_back({cur, {{k, v}}});
+  }
+  return SWPS_OK;
+}
+
+bool Config::get(const std::string &sec, const std::string &key, std::string &out) const {
+  for (auto &s : sections)
+    if (s.first == sec)
+      for (auto &kv : s.second)
+        if (kv.first == key) {
+          out = kv.second;
+          return true;
+        }
+  return false;
+}
+
+}  // namespace swps
+
+extern "C" {
+
+const char *swps_last_error(void) { return swps::g_last_error.c_str(); }
+int swps_version(void) { return 1; }
+
+uint64_t swps_fmix64(uint64_t x) { return swps::fmix64(x); }
+uint64_t swps_bkdr(const char *s) { return swps::bkdr(s); }
+
+// cluster/hashfrag.h:33-49: frag i -> node clamp(i / int(frag_num/num_nodes) + 1, 1, num_nodes)
+int swps_hashfrag_table(int32_t frag_num, int32_t num_nodes, uint32_t *out) {
+  if (num_nodes <= 0 || frag_num <= 0) return swps::fail(SWPS_E_CFG, "frag_num and num_nodes must be positive");
+  int each = frag_num / num_nodes;
+  if (each == 0) return swps::fail(SWPS_E_CFG, "frag_num < num_nodes (reference divides by zero)");
+  for (int i = 0; i < frag_num; i++) {
+    int id = (int)(uint32_t)(i / each) + 1;
+    if (id < 1) id = 1;
+    if (id > num_nodes) id = num_nodes;
+    out[i] = (uint32_t)id;
+  }
+  return SWPS_OK;
+}
+
+// cluster/hashfrag.h:51-56
+int swps_to_node_id(const uint64_t *keys, uint64_t n, int32_t frag_num, const uint32_t *table, int32_t *out) {
+  if (frag_num <= 0) return swps::fail(SWPS_E_CFG, "frag_num must be positive");
+  for (uint64_t i = 0; i < n; i++) out[i] = (int32_t)table[swps::fmix64(keys[i]) % (uint64_t)frag_num];
+  return SWPS_OK;
+}
+
+}  // extern "C"

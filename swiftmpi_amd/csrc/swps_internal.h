@@ -1,0 +1,151 @@
+// Internal definitions shared by the libswps translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "swps.h"
+
+namespace swps {
+
+// ---- errors (thread-local message, negative codes; never abort) -----------
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define SWPS_HIP(call)                                                                            \
+  do {                                                                                            \
+    hipError_t e_ = (call);                                                                       \
+    if (e_ != hipSuccess) return ::swps::fail(SWPS_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define SWPS_TRY(call)          \
+  do {                          \
+    int rc_ = (call);           \
+    if (rc_ != SWPS_OK) return rc_; \
+  } while (0)
+
+// ---- device buffer ----------------------------------------------------------
+struct DevMem {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DevMem() = default;
+  DevMem(const DevMem &) = delete;
+  DevMem &operator=(const DevMem &) = delete;
+  ~DevMem() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  // grow-only; contents are not preserved
+  int ensure(size_t b) {
+    if (b <= bytes && p) return SWPS_OK;
+    release();
+    size_t nb = b ? b : 16;
+    if (hipMalloc(&p, nb) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(SWPS_E_OOM, "hipMalloc of " + std::to_string(nb) + " bytes failed");
+    }
+    bytes = nb;
+    return SWPS_OK;
+  }
+  template <typename T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+template <typename T> int upload(DevMem &m, const std::vector<T> &v, hipStream_t s) {
+  SWPS_TRY(m.ensure(v.size() * sizeof(T)));
+  if (!v.empty()) SWPS_HIP(hipMemcpyAsync(m.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  return SWPS_OK;
+}
+
+// ---- hashing / RNG (host + device) ----------------------------------------
+__host__ __device__ inline uint64_t fmix64(uint64_t x) {  // utils/HashFunction.h:16-24
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ULL;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+
+// Affine LCG x -> a*x + c (mod 2^64) advanced k steps by doubling.
+// Main stream: a = 25214903917, c = 11; float stream: a = 4903917, c = 11
+// (utils/random.h:29-36).
+constexpr uint64_t kLcgA = 25214903917ULL;
+constexpr uint64_t kFlcgA = 4903917ULL;
+constexpr uint64_t kLcgC = 11ULL;
+
+__host__ __device__ inline uint64_t lcg_jump(uint64_t x, uint64_t k, uint64_t a, uint64_t c) {
+  uint64_t acc_a = 1, acc_c = 0, cur_a = a, cur_c = c;
+  while (k) {
+    if (k & 1) {
+      acc_a = acc_a * cur_a;
+      acc_c = acc_c * cur_a + cur_c;
+    }
+    cur_c = (cur_a + 1) * cur_c;
+    cur_a = cur_a * cur_a;
+    k >>= 1;
+  }
+  return acc_a * x + acc_c;
+}
+
+// gen_float of the float LCG state AFTER the step (random.h:33-36)
+__host__ __device__ inline float flcg_value(uint64_t y) {
+  return (float)y / 18446744073709551616.0f;
+}
+
+// ---- host utilities (swps_host.cpp) -----------------------------------------
+uint64_t bkdr(const char *s);
+// glibc random_r TYPE_3 (the generator behind rand()): r[i] = r[i-3] + r[i-31]
+struct GlibcRand {
+  int32_t r[34];
+  int idx = 0;
+  uint64_t produced = 0;
+  explicit GlibcRand(uint32_t seed);
+  int32_t next();
+};
+// reference config file format (utils/ConfigParser.h:84-115)
+struct Config {
+  std::vector<std::pair<std::string, std::vector<std::pair<std::string, std::string>>>> sections;
+  int parse(const std::string &path);
+  bool get(const std::string &sec, const std::string &key, std::string &out) const;
+};
+
+}  // namespace swps
+
+// ---- the HBM parameter shard -------------------------------------------------
+struct swps_table {
+  swps_table_cfg cfg{};
+  int row_elems = 0, pull_elems = 0, push_elems = 0;
+  size_t esize = 4;
+  uint64_t nslots = 0, mask = 0;
+  hipStream_t stream = nullptr;
+  swps::DevMem keys;      // [nslots] u64, EMPTY = ~0 (sparsetable.h:25 empty key)
+  swps::DevMem slot_row;  // [nslots] u32 dense row index
+  swps::DevMem row_key;   // [capacity] u64
+  swps::DevMem rows;      // [capacity][row_elems] T
+  swps::DevMem counters;  // [0] = nrows (u32), [1] = error flag
+  swps::DevMem scratch;   // per-call row indices
+  uint32_t host_nrows = 0;
+};
+
+namespace swps {
+constexpr uint64_t kEmptyKey = ~0ULL;
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+// table internals used by the app contexts (same library)
+int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s);
+int table_lookup(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s);
+int table_check_error(swps_table *t, hipStream_t s);
+int table_set_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_vals, hipStream_t s);
+int table_get_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s);
+}  // namespace swps

@@ -1,0 +1,491 @@
+// HBM-resident parameter shard: an open-addressed (linear probing) u64-key
+// hash index over a dense row store, with the reference's pull / push access
+// methods as kernels.
+//
+// Replaces parameter/sparsetable.h:17-149 (google::dense_hash_map shards
+// behind pthread RWLocks, 4 heap Vecs per key) and the server handlers of
+// cluster/server.h:129-176 with their access methods
+// (apps/word2vec/word2vec_global.h:158-191, apps/logistic/lr.cpp:45-81).
+//
+// HBM layout (row-major, one dense row per key, 16-B aligned for D % 4 == 0):
+//   keys[nslots]      u64   slot -> key (EMPTY = ~0, the reference's empty key)
+//   slot_row[nslots]  u32   slot -> dense row index
+//   row_key[cap]      u64   row -> key (dump / key listing)
+//   rows[cap][R]      T     W2V: [h | v | h2sum | v2sum] (R = 4D); LR: [w | g2] (R = 2)
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+
+#include "swps_internal.h"
+
+using namespace swps;
+
+namespace {
+
+__device__ __forceinline__ uint64_t slot_hash(uint64_t key) { return splitmix64(key ^ 0x5851f42d4c957f2dULL); }
+
+__global__ void k_find_or_insert(const uint64_t *__restrict__ keys, uint64_t n, uint64_t *tkeys, uint32_t *slot_row,
+                                 uint64_t *row_key, uint32_t *counters, uint64_t mask, uint64_t cap,
+                                 uint32_t *out_rows, uint8_t *out_new) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t key = keys[i];
+  uint32_t row = kNoRow;
+  uint8_t isnew = 0;
+  if (key == kEmptyKey) {
+    atomicOr(&counters[1], 4u);  // the reference's empty key cannot be stored
+  } else {
+    uint64_t s = slot_hash(key) & mask;
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+      uint64_t k = __hip_atomic_load(&tkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == kEmptyKey) {
+        unsigned long long old =
+            atomicCAS((unsigned long long *)&tkeys[s], (unsigned long long)kEmptyKey, (unsigned long long)key);
+        if (old == kEmptyKey) {
+          uint32_t r = atomicAdd(&counters[0], 1u);
+          if (r >= cap) {
+            atomicOr(&counters[1], 1u);
+          } else {
+            slot_row[s] = r;
+            row_key[r] = key;
+            row = r;
+            isnew = 1;
+          }
+          break;
+        }
+        k = old;
+      }
+      if (k == key) {
+        row = slot_row[s];
+        break;
+      }
+      s = (s + 1) & mask;
+    }
+    if (row == kNoRow && !isnew) atomicOr(&counters[1], 1u);
+  }
+  out_rows[i] = row;
+  if (out_new) out_new[i] = isnew;
+}
+
+__global__ void k_lookup(const uint64_t *__restrict__ keys, uint64_t n, const uint64_t *__restrict__ tkeys,
+                         const uint32_t *__restrict__ slot_row, uint64_t mask, uint32_t *out_rows,
+                         uint32_t *counters) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t key = keys[i];
+  uint32_t row = kNoRow;
+  uint64_t s = slot_hash(key) & mask;
+  for (uint64_t probe = 0; probe <= mask; probe++) {
+    uint64_t k = tkeys[s];
+    if (k == key) {
+      row = slot_row[s];
+      break;
+    }
+    if (k == kEmptyKey) break;
+    s = (s + 1) & mask;
+  }
+  if (row == kNoRow && counters) atomicOr(&counters[1], 2u);
+  out_rows[i] = row;
+}
+
+__device__ __forceinline__ float unit_hash(uint64_t seed, uint64_t key, uint64_t i) {
+  uint64_t z = splitmix64(seed ^ splitmix64(key + 0x632be59bd9b4e019ULL * (i + 1)));
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// PullAccessMethod::init_param on a miss (accessmethod.h:64-67), one wave per key.
+template <typename T>
+__global__ void k_init_rows(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rows_idx,
+                            const uint8_t *__restrict__ isnew, uint64_t n, T *rows, int R, int layout, int D,
+                            int mode, uint64_t seed) {
+  uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int lane = threadIdx.x & 63;
+  if (w >= n || !isnew[w]) return;
+  T *row = rows + (uint64_t)rows_idx[w] * R;
+  uint64_t key = keys[w];
+  for (int e = lane; e < R; e += 64) {
+    T val = 0;
+    if (mode == SWPS_INIT_HASH) {
+      if (layout == SWPS_LAYOUT_W2V) {
+        if (e < 2 * D) val = (T)(((double)unit_hash(seed, key, e) - 0.5) / (double)D);
+      } else if (e == 0) {
+        val = (T)unit_hash(seed, key, 0);
+      }
+    }
+    row[e] = val;
+  }
+}
+
+template <typename T>
+__global__ void k_copy_rows_out(const uint32_t *__restrict__ rows_idx, uint64_t n, const T *__restrict__ rows, int R,
+                                int ncopy, T *__restrict__ out) {
+  uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int lane = threadIdx.x & 63;
+  if (w >= n) return;
+  uint32_t r = rows_idx[w];
+  for (int e = lane; e < ncopy; e += 64) out[w * ncopy + e] = r == kNoRow ? (T)0 : rows[(uint64_t)r * R + e];
+}
+
+template <typename T>
+__global__ void k_copy_rows_in(const uint32_t *__restrict__ rows_idx, uint64_t n, T *__restrict__ rows, int R,
+                               const T *__restrict__ in) {
+  uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int lane = threadIdx.x & 63;
+  if (w >= n) return;
+  uint32_t r = rows_idx[w];
+  if (r == kNoRow) return;
+  for (int e = lane; e < R; e += 64) rows[(uint64_t)r * R + e] = in[w * R + e];
+}
+
+// WPushAccessMethod::apply_push_value (word2vec_global.h:176-185), fp64 math:
+//   h2 += g_h*g_h; v2 += g_v*g_v; h += lr*g_h/sqrt(h2+fudge); v likewise.
+template <typename T>
+__global__ void k_push_w2v(const uint32_t *__restrict__ rows_idx, uint64_t n, const double *__restrict__ grads,
+                           T *__restrict__ rows, int D, double lr, double fudge) {
+  uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int lane = threadIdx.x & 63;
+  if (w >= n) return;
+  uint32_t r = rows_idx[w];
+  if (r == kNoRow) return;
+  T *row = rows + (uint64_t)r * 4 * D;
+  const double *g = grads + w * 2 * D;
+  for (int i = lane; i < D; i += 64) {
+    double gh = g[i], gv = g[D + i];
+    double h2 = (double)row[2 * D + i] + gh * gh;
+    double v2 = (double)row[3 * D + i] + gv * gv;
+    double hn = (double)row[i] + (gh * lr) / sqrt(h2 + fudge);
+    double vn = (double)row[D + i] + (gv * lr) / sqrt(v2 + fudge);
+    row[2 * D + i] = (T)h2;
+    row[3 * D + i] = (T)v2;
+    row[i] = (T)hn;
+    row[D + i] = (T)vn;
+  }
+}
+
+// LRPushAccessMethod::apply_push_value (lr.cpp:68-75), in the storage type
+// (fp32 for SWPS_F32, exactly the reference's float arithmetic).
+template <typename T>
+__global__ void k_push_lr(const uint32_t *__restrict__ rows_idx, uint64_t n, const float *__restrict__ grads,
+                          T *__restrict__ rows, T lr, T fudge) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t r = rows_idx[i];
+  if (r == kNoRow) return;
+  T m = (T)grads[i];
+  T *row = rows + (uint64_t)r * 2;
+  T g2 = row[1] + m * m;
+  row[1] = g2;
+  T step = lr * m;
+  row[0] = row[0] + step / (T)sqrt(g2 + fudge);
+}
+
+inline unsigned blocks_for(uint64_t threads, unsigned bs = 256) { return (unsigned)((threads + bs - 1) / bs); }
+
+}  // namespace
+
+namespace swps {
+
+int table_check_error(swps_table *t, hipStream_t s) {
+  uint32_t h[2];
+  SWPS_HIP(hipMemcpyAsync(h, t->counters.p, sizeof(h), hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  t->host_nrows = h[0] > t->cfg.capacity ? (uint32_t)t->cfg.capacity : h[0];
+  if (h[1]) {
+    uint32_t z = 0;
+    SWPS_HIP(hipMemcpy((uint32_t *)t->counters.p + 1, &z, 4, hipMemcpyHostToDevice));
+    if (h[1] & 1) return fail(SWPS_E_OOM, "table capacity exhausted");
+    if (h[1] & 4) return fail(SWPS_E_BADKEY, "key ~0 is the table's empty key");
+    return fail(SWPS_E_BADKEY, "new key should be inited before (push of an unknown key)");
+  }
+  return SWPS_OK;
+}
+
+int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  DevMem isnew;
+  SWPS_TRY(isnew.ensure(n));
+  k_find_or_insert<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(),
+                                                  t->row_key.as<uint64_t>(), t->counters.as<uint32_t>(), t->mask,
+                                                  t->cfg.capacity, d_rows_out, isnew.as<uint8_t>());
+  SWPS_HIP(hipGetLastError());
+  if (t->cfg.dtype == SWPS_F64)
+    k_init_rows<double><<<blocks_for(n * 64), 256, 0, s>>>(d_keys, d_rows_out, isnew.as<uint8_t>(), n,
+                                                           t->rows.as<double>(), t->row_elems, t->cfg.layout,
+                                                           t->cfg.dim, t->cfg.init_mode, t->cfg.seed);
+  else
+    k_init_rows<float><<<blocks_for(n * 64), 256, 0, s>>>(d_keys, d_rows_out, isnew.as<uint8_t>(), n,
+                                                          t->rows.as<float>(), t->row_elems, t->cfg.layout,
+                                                          t->cfg.dim, t->cfg.init_mode, t->cfg.seed);
+  SWPS_HIP(hipGetLastError());
+  return table_check_error(t, s);  // also keeps `isnew` alive until the kernels retire
+}
+
+int table_lookup(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  k_lookup<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(), t->mask,
+                                          d_rows_out, t->counters.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+int table_set_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_vals, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  if (t->cfg.dtype == SWPS_F64)
+    k_copy_rows_in<double><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<double>(), t->row_elems,
+                                                              (const double *)d_vals);
+  else
+    k_copy_rows_in<float><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<float>(), t->row_elems,
+                                                             (const float *)d_vals);
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+int table_get_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  if (t->cfg.dtype == SWPS_F64)
+    k_copy_rows_out<double><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<double>(), t->row_elems,
+                                                               t->row_elems, (double *)d_vals);
+  else
+    k_copy_rows_out<float><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<float>(), t->row_elems,
+                                                              t->row_elems, (float *)d_vals);
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+}  // namespace swps
+
+extern "C" {
+
+int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
+  if (!cfg || !out) return fail(SWPS_E_CFG, "null argument");
+  *out = nullptr;
+  if (cfg->layout != SWPS_LAYOUT_W2V && cfg->layout != SWPS_LAYOUT_LR) return fail(SWPS_E_CFG, "unknown layout");
+  if (cfg->dtype != SWPS_F32 && cfg->dtype != SWPS_F64) return fail(SWPS_E_CFG, "unknown dtype");
+  if (cfg->layout == SWPS_LAYOUT_W2V && cfg->dim <= 0) return fail(SWPS_E_CFG, "dim must be positive");
+  if (cfg->capacity == 0 || cfg->capacity >= 0xFFFFFFF0ULL) return fail(SWPS_E_CFG, "capacity out of range");
+  SWPS_HIP(hipSetDevice(cfg->device));
+  swps_table *t = new swps_table();
+  t->cfg = *cfg;
+  if (t->cfg.fudge == 0.0f) t->cfg.fudge = 1e-6f;
+  t->esize = cfg->dtype == SWPS_F64 ? 8 : 4;
+  if (cfg->layout == SWPS_LAYOUT_W2V) {
+    t->row_elems = 4 * cfg->dim;
+    t->pull_elems = 2 * cfg->dim;
+    t->push_elems = 2 * cfg->dim;
+  } else {
+    t->row_elems = 2;
+    t->pull_elems = 1;
+    t->push_elems = 1;
+    t->cfg.dim = 1;
+  }
+  uint64_t ns = 1;
+  while (ns < 2 * cfg->capacity) ns <<= 1;
+  t->nslots = ns;
+  t->mask = ns - 1;
+  int rc = SWPS_OK;
+  if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) rc = fail(SWPS_E_HIP, "stream");
+  if (!rc) rc = t->keys.ensure(ns * 8);
+  if (!rc) rc = t->slot_row.ensure(ns * 4);
+  if (!rc) rc = t->row_key.ensure(cfg->capacity * 8);
+  if (!rc) rc = t->rows.ensure(cfg->capacity * (uint64_t)t->row_elems * t->esize);
+  if (!rc) rc = t->counters.ensure(16);
+  if (!rc && hipMemsetAsync(t->keys.p, 0xFF, ns * 8, t->stream) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
+  if (!rc && hipMemsetAsync(t->slot_row.p, 0xFF, ns * 4, t->stream) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
+  if (!rc && hipMemsetAsync(t->counters.p, 0, 16, t->stream) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
+  if (!rc && hipStreamSynchronize(t->stream) != hipSuccess) rc = fail(SWPS_E_HIP, "sync");
+  if (rc) {
+    if (t->stream) (void)hipStreamDestroy(t->stream);
+    delete t;
+    return rc;
+  }
+  *out = t;
+  return SWPS_OK;
+}
+
+int swps_table_destroy(swps_table *t) {
+  if (!t) return SWPS_OK;
+  (void)hipSetDevice(t->cfg.device);
+  if (t->stream) {
+    (void)hipStreamSynchronize(t->stream);
+    (void)hipStreamDestroy(t->stream);
+  }
+  delete t;
+  return SWPS_OK;
+}
+
+int swps_table_sync(swps_table *t) {
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_HIP(hipStreamSynchronize(t->stream));
+  return SWPS_OK;
+}
+
+int swps_table_size(swps_table *t, uint64_t *n) {
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(table_check_error(t, t->stream));
+  *n = t->host_nrows;
+  return SWPS_OK;
+}
+
+int swps_table_row_elems(swps_table *t, int32_t *row, int32_t *pull, int32_t *push) {
+  if (row) *row = t->row_elems;
+  if (pull) *pull = t->pull_elems;
+  if (push) *push = t->push_elems;
+  return SWPS_OK;
+}
+
+int swps_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals) {
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(t->scratch.ensure(n * 4));
+  uint32_t *rows = t->scratch.as<uint32_t>();
+  SWPS_TRY(table_find_or_insert(t, d_keys, n, rows, t->stream));
+  if (t->cfg.dtype == SWPS_F64)
+    k_copy_rows_out<double><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, t->rows.as<double>(), t->row_elems,
+                                                                       t->pull_elems, (double *)d_vals);
+  else
+    k_copy_rows_out<float><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, t->rows.as<float>(), t->row_elems,
+                                                                      t->pull_elems, (float *)d_vals);
+  SWPS_HIP(hipGetLastError());
+  SWPS_HIP(hipStreamSynchronize(t->stream));
+  return SWPS_OK;
+}
+
+int swps_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads) {
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(t->scratch.ensure(n * 4));
+  uint32_t *rows = t->scratch.as<uint32_t>();
+  SWPS_TRY(table_lookup(t, d_keys, n, rows, t->stream));
+  if (t->cfg.layout == SWPS_LAYOUT_W2V) {
+    double lr = (double)t->cfg.learning_rate, fudge = (double)t->cfg.fudge;
+    if (t->cfg.dtype == SWPS_F64)
+      k_push_w2v<double><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, (const double *)d_grads,
+                                                                    t->rows.as<double>(), t->cfg.dim, lr, fudge);
+    else
+      k_push_w2v<float><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, (const double *)d_grads,
+                                                                   t->rows.as<float>(), t->cfg.dim, lr, fudge);
+  } else {
+    if (t->cfg.dtype == SWPS_F64)
+      k_push_lr<double><<<blocks_for(n), 256, 0, t->stream>>>(rows, n, (const float *)d_grads, t->rows.as<double>(),
+                                                              (double)t->cfg.learning_rate, (double)t->cfg.fudge);
+    else
+      k_push_lr<float><<<blocks_for(n), 256, 0, t->stream>>>(rows, n, (const float *)d_grads, t->rows.as<float>(),
+                                                             t->cfg.learning_rate, t->cfg.fudge);
+  }
+  SWPS_HIP(hipGetLastError());
+  return table_check_error(t, t->stream);
+}
+
+int swps_assign(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_rows) {
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(t->scratch.ensure(n * 4));
+  uint32_t *rows = t->scratch.as<uint32_t>();
+  SWPS_TRY(table_find_or_insert(t, d_keys, n, rows, t->stream));
+  SWPS_TRY(table_set_rows(t, rows, n, d_rows, t->stream));
+  SWPS_HIP(hipStreamSynchronize(t->stream));
+  return SWPS_OK;
+}
+
+int swps_export(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_rows) {
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(t->scratch.ensure(n * 4));
+  uint32_t *rows = t->scratch.as<uint32_t>();
+  SWPS_TRY(table_lookup(t, d_keys, n, rows, t->stream));
+  SWPS_TRY(table_get_rows(t, rows, n, d_rows, t->stream));
+  return table_check_error(t, t->stream);
+}
+
+int swps_table_keys(swps_table *t, uint64_t *keys, uint64_t cap, uint64_t *n) {
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(table_check_error(t, t->stream));
+  uint64_t m = t->host_nrows;
+  *n = m;
+  if (cap < m) return fail(SWPS_E_CFG, "key buffer too small");
+  if (m) SWPS_HIP(hipMemcpy(keys, t->row_key.p, m * 8, hipMemcpyDeviceToHost));
+  return SWPS_OK;
+}
+
+// SparseTable::output (sparsetable.h:127-132) with WParam / LRParam's
+// operator<< (word2vec_global.h:102-112, lr.cpp:24-27): ostream precision 6.
+int swps_dump(swps_table *t, const char *path) {
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(table_check_error(t, t->stream));
+  uint64_t m = t->host_nrows;
+  std::vector<uint64_t> keys(m);
+  std::vector<char> rows(m * t->row_elems * t->esize);
+  if (m) {
+    SWPS_HIP(hipMemcpy(keys.data(), t->row_key.p, m * 8, hipMemcpyDeviceToHost));
+    SWPS_HIP(hipMemcpy(rows.data(), t->rows.p, rows.size(), hipMemcpyDeviceToHost));
+  }
+  FILE *f = fopen(path, "w");
+  if (!f) return fail(SWPS_E_IO, std::string("cannot write ") + path);
+  auto val = [&](uint64_t r, int e) -> double {
+    size_t off = r * t->row_elems + e;
+    return t->esize == 8 ? ((double *)rows.data())[off] : (double)((float *)rows.data())[off];
+  };
+  const int D = t->cfg.dim;
+  for (uint64_t r = 0; r < m; r++) {
+    fprintf(f, "%llu\t", (unsigned long long)keys[r]);
+    if (t->cfg.layout == SWPS_LAYOUT_W2V) {
+      for (int i = 0; i < D; i++) fprintf(f, i < D - 1 ? "%g " : "%g\t", val(r, D + i));
+      for (int i = 0; i < D; i++) fprintf(f, i < D - 1 ? "%g " : "%g\n", val(r, i));
+    } else {
+      fprintf(f, "%g\n", val(r, 0));
+    }
+  }
+  fclose(f);
+  return SWPS_OK;
+}
+
+// ClusterServer::load (server.h:49-62): keep keys whose hash-frag node is
+// `node_id`; h2/v2 (grad2sum) start at 0.
+int swps_load(swps_table *t, const char *path, int32_t frag_num, int32_t world, int32_t node_id) {
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  std::ifstream f(path);
+  if (!f) return fail(SWPS_E_IO, std::string("cannot open ") + path);
+  std::vector<uint32_t> map;
+  bool filter = world > 1 && node_id > 0;
+  if (filter) {
+    map.resize(frag_num);
+    SWPS_TRY(swps_hashfrag_table(frag_num, world, map.data()));
+  }
+  const int D = t->cfg.dim, R = t->row_elems;
+  std::vector<uint64_t> keys;
+  std::vector<double> vals;
+  std::string line;
+  while (std::getline(f, line)) {
+    if (line.empty()) continue;
+    std::istringstream is(line);
+    uint64_t key;
+    if (!(is >> key)) return fail(SWPS_E_IO, "bad parameter line");
+    std::vector<double> row(R, 0.0);
+    if (t->cfg.layout == SWPS_LAYOUT_W2V) {
+      for (int i = 0; i < D; i++) is >> row[D + i];  // v first (word2vec_global.h:113-121)
+      for (int i = 0; i < D; i++) is >> row[i];
+    } else {
+      is >> row[0];
+    }
+    if (!is) return fail(SWPS_E_IO, "truncated parameter line");
+    if (filter && (int)map[fmix64(key) % (uint64_t)frag_num] != node_id) continue;
+    keys.push_back(key);
+    vals.insert(vals.end(), row.begin(), row.end());
+  }
+  uint64_t n = keys.size();
+  if (!n) return SWPS_OK;
+  DevMem dk, dv;
+  SWPS_TRY(upload(dk, keys, t->stream));
+  if (t->esize == 8) {
+    SWPS_TRY(upload(dv, vals, t->stream));
+  } else {
+    std::vector<float> fv(vals.begin(), vals.end());
+    SWPS_TRY(upload(dv, fv, t->stream));
+    SWPS_HIP(hipStreamSynchronize(t->stream));
+  }
+  SWPS_TRY(swps_assign(t, dk.as<uint64_t>(), n, dv.p));
+  return SWPS_OK;
+}
+
+}  // extern "C"

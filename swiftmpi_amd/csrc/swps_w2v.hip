@@ -1,0 +1,1277 @@
+// word2vec CBOW negative sampling on one MI355X: the reference's
+// pull -> learn_instance -> push minibatch loop (apps/word2vec/
+// word2vec_global.h:552-731, nthreads = 1 semantics) as a chain of HIP
+// kernels over HBM-resident data.
+//
+// Per minibatch n (trained lines T_n, gathered key set K_n, U = |K_n|):
+//   k_pull      cache[vid] <- table row (h, v) for vid in K_n; local[vid] = u
+//               (global_pull_access.h:80-101: params[key]=val, grads reset)
+//   k_keep      float-LCG subsample test per token, LCG jumped to the
+//               token's stream offset (word2vec_global.h:725-731)
+//   scans       kept positions per line -> main-LCG draw offset per kept
+//               position (1 draw per line + (1+negative) per kept position)
+//   k_forward   one wave per kept position: neu1 = sum of context v rows,
+//               dots with the positive and the negative h rows (fp64),
+//               exp-table sigmoid, neu1e; writes neu1/neu1e rows and one
+//               (key, pair index) record per target and per context
+//               (word2vec_global.h:663-718)
+//   radix sort  records by local key index (stable: position order kept)
+//   k_gather    chunked segmented sums  h_grad[k] = sum g*neu1[p],
+//               v_grad[k] = sum neu1e[p]  into per-chunk partials (no atomics)
+//   k_push      partials summed in chunk order, mean over the counts
+//               (word2vec_global.h:122-134), AdaGrad on the table row
+//               (word2vec_global.h:176-185)
+// Params are read only from the frozen cache during a batch, exactly like the
+// reference worker.  Negatives outside K_n read the stale cache and their
+// gradients are dropped (the reference resets them at the next pull).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <limits>
+#include <map>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "swps_internal.h"
+
+using namespace swps;
+
+namespace {
+
+constexpr int kMaxJump = 64;
+__constant__ uint64_t c_jumpA[kMaxJump + 1];
+__constant__ uint64_t c_jumpC[kMaxJump + 1];
+
+template <typename T> struct V16;
+template <> struct V16<float> {
+  using V = float4;
+  static constexpr int E = 4;
+};
+template <> struct V16<double> {
+  using V = double2;
+  static constexpr int E = 2;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__global__ void k_build_unigram(const uint64_t *__restrict__ starts, uint32_t V, uint64_t T, int32_t *__restrict__ table) {
+  uint64_t a = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (; a < T; a += stride) {
+    uint32_t lo = 0, hi = V;  // largest i with starts[i] <= a
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (starts[mid] <= a)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    table[a] = (int32_t)lo;
+  }
+}
+
+// cache <- table rows (h, v) for the listed vids; local[vid] = u when set_local
+template <typename T>
+__global__ __launch_bounds__(256) void k_pull(const int32_t *__restrict__ K, uint32_t U,
+                                              const uint32_t *__restrict__ vid_row, const T *__restrict__ rows,
+                                              int D, T *__restrict__ cache_h, T *__restrict__ cache_v,
+                                              int32_t *__restrict__ local, int set_local) {
+  using V = typename V16<T>::V;
+  constexpr int E = V16<T>::E;
+  const int lane = threadIdx.x & 63;
+  const int NC = D / E;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += (uint64_t)gridDim.x * 4) {
+    const int32_t vid = K ? K[u] : (int32_t)u;
+    const V *src = (const V *)(rows + (uint64_t)vid_row[vid] * 4 * D);
+    V *dh = (V *)(cache_h + (uint64_t)vid * D);
+    V *dv = (V *)(cache_v + (uint64_t)vid * D);
+    for (int c = lane; c < NC; c += 64) {
+      dh[c] = src[c];
+      dv[c] = src[NC + c];
+    }
+    if (set_local && lane == 0) local[vid] = (int32_t)u;
+  }
+}
+
+// float-LCG keep flag per token (to_sample, word2vec_global.h:725-731)
+__global__ void k_keep(const int32_t *__restrict__ tok, uint64_t t0, uint64_t nt, const float *__restrict__ ran,
+                       uint64_t fstate, int sample_on, int32_t *__restrict__ kflag) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nt) return;
+  if (i == nt) {
+    kflag[i] = 0;
+    return;
+  }
+  int32_t keep = 1;
+  if (sample_on) {
+    uint64_t y = lcg_jump(fstate, i + 1, kFlcgA, kLcgC);
+    keep = flcg_value(y) > ran[tok[t0 + i]];
+  }
+  kflag[i] = keep;
+}
+
+// main-LCG draws per line: 1 (learn_instance's initial b) + kept*(1+negative)
+__global__ void k_line_draws(const int64_t *__restrict__ line_off, uint64_t l0, uint64_t nl, uint64_t t0,
+                             const int32_t *__restrict__ kscan, int N, uint64_t *__restrict__ ldraw) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > nl) return;
+  if (j == nl) {
+    ldraw[j] = 0;
+    return;
+  }
+  uint64_t a = (uint64_t)line_off[l0 + j] - t0, b = (uint64_t)line_off[l0 + j + 1] - t0;
+  uint64_t kept = (uint64_t)(kscan[b] - kscan[a]);
+  ldraw[j] = 1 + kept * (uint64_t)(N + 1);
+}
+
+// kept positions in order + the LCG state just before each position's draws
+__global__ void k_compact(const int32_t *__restrict__ tok_line, const int64_t *__restrict__ line_off, uint64_t t0,
+                          uint64_t nt, uint64_t l0, const int32_t *__restrict__ kscan,
+                          const uint64_t *__restrict__ ldoff, uint64_t lstate, int N, int32_t *__restrict__ pos_tok,
+                          uint64_t *__restrict__ pos_state) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nt) return;
+  int32_t p = kscan[i];
+  if (kscan[i + 1] == p) return;
+  int32_t l = tok_line[t0 + i];
+  uint64_t ls = (uint64_t)line_off[l] - t0;
+  uint64_t rank = (uint64_t)(p - kscan[ls]);
+  pos_tok[p] = (int32_t)(t0 + i);
+  pos_state[p] = lcg_jump(lstate, ldoff[l - l0] + 1 + rank * (uint64_t)(N + 1), kLcgA, kLcgC);
+}
+
+template <typename T> struct FwdArgs {
+  const int32_t *tok, *tok_line;
+  const int64_t *line_off;
+  const int32_t *pos_tok;
+  const uint64_t *pos_state;
+  int P;
+  const T *cache_h, *cache_v;
+  const int32_t *local;
+  uint32_t U;
+  const int32_t *unigram;
+  uint64_t uni_size;
+  const float *exptab;
+  int D, W, N;
+  float alpha;
+  T *neu1, *neu1e;
+  uint32_t *pkeys, *pvals;
+  float *pg;
+  uint64_t HOFF;
+  int32_t *trace;
+  unsigned long long *rows_touched;  // [0] context rows, [1] target rows
+};
+
+// One wave per kept position (learn_instance's per-position body).
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void k_forward(FwdArgs<T> a) {
+  using V = typename V16<T>::V;
+  constexpr int E = V16<T>::E;
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= a.P) return;
+  const int D = a.D, W = a.W, N = a.N, NC = D / E;
+  const int t = a.pos_tok[p];
+  const int l = a.tok_line[t];
+  const int64_t ls = a.line_off[l];
+  const int n = (int)(a.line_off[l + 1] - ls), pos = (int)(t - ls);
+  const int word = a.tok[t];
+  const uint64_t s = a.pos_state[p];
+  // lane k draws x_{k+1}: k = 0 -> b, k = 1..N -> negatives
+  const uint64_t x = c_jumpA[(lane < kMaxJump ? lane : 0) + 1] * s + c_jumpC[(lane < kMaxJump ? lane : 0) + 1];
+  const uint64_t x0 = __shfl(x, 0, 64);
+  const int b = (int)(x0 % (uint64_t)W);
+  int tgt = word;
+  int skip = 0;
+  if (lane >= 1 && lane <= N) {
+    tgt = a.unigram[(x >> 16) % a.uni_size];
+    skip = tgt == word;
+    if (a.trace) a.trace[(int64_t)p * N + lane - 1] = tgt;
+  }
+  const int nslot = 2 * (W - b);
+  int cvid = -1;
+  if (lane < nslot) {
+    int aa = b + lane;
+    if (aa >= W) aa++;
+    const int c = pos - W + aa;
+    if (c >= 0 && c < n) cvid = a.tok[ls + c];
+  }
+  double acc[NCH][E];
+#pragma unroll
+  for (int c = 0; c < NCH; c++)
+#pragma unroll
+    for (int k = 0; k < E; k++) acc[c][k] = 0.0;
+  for (int j = 0; j < nslot; j++) {
+    const int cv = __shfl(cvid, j, 64);
+    if (cv < 0) continue;
+    const V *row = (const V *)(a.cache_v + (uint64_t)cv * D);
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int ci = lane + c * 64;
+      if (ci < NC) {
+        V v = row[ci];
+        const T *e = (const T *)&v;
+#pragma unroll
+        for (int k = 0; k < E; k++) acc[c][k] += (double)e[k];
+      }
+    }
+  }
+  double ne[NCH][E];
+#pragma unroll
+  for (int c = 0; c < NCH; c++)
+#pragma unroll
+    for (int k = 0; k < E; k++) ne[c][k] = 0.0;
+  float gk = 0.f;
+  for (int d = 0; d <= N; d++) {
+    const int tv = __shfl(tgt, d, 64);
+    const int sk = __shfl(skip, d, 64);
+    if (sk) continue;
+    const V *row = (const V *)(a.cache_h + (uint64_t)tv * D);
+    V hv[NCH];
+    double part = 0.0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int ci = lane + c * 64;
+      if (ci < NC) {
+        hv[c] = row[ci];
+        const T *e = (const T *)&hv[c];
+#pragma unroll
+        for (int k = 0; k < E; k++) part += acc[c][k] * (double)e[k];
+      }
+    }
+    part = wave_sum(part);
+    float f = 0;
+    f += part;
+    const int label = d == 0 ? 1 : 0;
+    float g;
+    if (f > 6)
+      g = (label - 1) * a.alpha;
+    else if (f < -6)
+      g = (label - 0) * a.alpha;
+    else
+      g = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int ci = lane + c * 64;
+      if (ci < NC) {
+        const T *e = (const T *)&hv[c];
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+          const double prod = (double)g * (double)e[k];
+          ne[c][k] += prod;
+        }
+      }
+    }
+    if (lane == d) gk = g;
+  }
+  if (lane == 0) {
+    int nctx = 0;
+    for (int j = 0; j < nslot; j++) nctx += __shfl(cvid, j, 64) >= 0;
+    atomicAdd(&a.rows_touched[0], (unsigned long long)nctx);
+  }
+  {
+    const unsigned long long tb = __ballot(lane <= N && !skip);
+    if (lane == 0) atomicAdd(&a.rows_touched[1], (unsigned long long)__popcll(tb));
+  }
+  V *o1 = (V *)(a.neu1 + (uint64_t)p * D);
+  V *o2 = (V *)(a.neu1e + (uint64_t)p * D);
+#pragma unroll
+  for (int c = 0; c < NCH; c++) {
+    const int ci = lane + c * 64;
+    if (ci < NC) {
+      V v1, v2;
+      T *e1 = (T *)&v1, *e2 = (T *)&v2;
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        e1[k] = (T)acc[c][k];
+        e2[k] = (T)ne[c][k];
+      }
+      o1[ci] = v1;
+      o2[ci] = v2;
+    }
+  }
+  if (lane <= N) {
+    const uint64_t i = (uint64_t)p * (N + 1) + lane;
+    uint32_t key = a.U;
+    if (!skip) {
+      const int32_t u = a.local[tgt];
+      if (u >= 0) key = (uint32_t)u;
+    }
+    a.pkeys[i] = key;
+    a.pvals[i] = (uint32_t)i;
+    a.pg[i] = gk;
+  }
+  if (lane < 2 * W) {
+    const uint64_t i = a.HOFF + (uint64_t)p * 2 * W + lane;
+    uint32_t key = a.U;
+    if (cvid >= 0) {
+      const int32_t u = a.local[cvid];
+      if (u >= 0) key = (uint32_t)u;
+    }
+    a.pkeys[i] = key;
+    a.pvals[i] = (uint32_t)i;
+  }
+}
+
+// Segment bounds of each (local key, kind) run in the sorted records:
+// seg[0][u], seg[1][u] = h-pair range; seg[2][u], seg[3][u] = v-pair range.
+__global__ void k_segments(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, uint64_t M,
+                           uint64_t HOFF, uint32_t U, uint32_t *__restrict__ seg) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const uint32_t k = keys[i];
+  if (k >= U) return;
+  const int kind = vals[i] >= HOFF;
+  const bool first = i == 0 || keys[i - 1] != k || (int)(vals[i - 1] >= HOFF) != kind;
+  const bool last = i + 1 == M || keys[i + 1] != k || (int)(vals[i + 1] >= HOFF) != kind;
+  if (first) seg[(2 * kind) * U + k] = (uint32_t)i;
+  if (last) seg[(2 * kind + 1) * U + k] = (uint32_t)(i + 1);
+}
+
+__global__ void k_item_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t *__restrict__ cnt) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > 2ull * U) return;
+  if (j == 2ull * U) {
+    cnt[j] = 0;
+    return;
+  }
+  const uint32_t u = (uint32_t)(j >> 1), kind = (uint32_t)(j & 1);
+  const uint32_t c = seg[(2 * kind + 1) * U + u] - seg[(2 * kind) * U + u];
+  cnt[j] = (c + CH - 1) / CH;
+}
+
+template <typename T> struct GatherArgs {
+  const uint32_t *item_off, *seg, *vals;
+  uint32_t U, CH;
+  const T *neu1, *neu1e;
+  const float *pg;
+  uint64_t HOFF;
+  int N1, W2, D;
+  T *partial;
+};
+
+// One wave per chunk of <= CH records of one (key, kind): the fp64 sum of
+// g*neu1[p] (h) or neu1e[p] (v) over the chunk, in record (= position) order.
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void k_gather(GatherArgs<T> a) {
+  using V = typename V16<T>::V;
+  constexpr int E = V16<T>::E;
+  constexpr int UNR = 4;
+  const int lane = threadIdx.x & 63;
+  const int NC = a.D / E;
+  const uint32_t U2 = 2 * a.U;
+  const uint32_t NI = a.item_off[U2];
+  for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
+    uint32_t lo = 0, hi = U2;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.item_off[mid] <= item)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const uint32_t u = lo >> 1, kind = lo & 1, j = item - a.item_off[lo];
+    const uint32_t s = a.seg[(2 * kind) * a.U + u] + j * a.CH;
+    const uint32_t e = min(s + a.CH, a.seg[(2 * kind + 1) * a.U + u]);
+    double acc[NCH][E];
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+#pragma unroll
+      for (int k = 0; k < E; k++) acc[c][k] = 0.0;
+    for (uint32_t i0 = s; i0 < e; i0 += UNR) {
+      const V *rp[UNR];
+      double gg[UNR];
+#pragma unroll
+      for (int q = 0; q < UNR; q++) {
+        const uint32_t i = min(i0 + q, e - 1);
+        const uint32_t pi = a.vals[i];
+        if (kind == 0) {
+          const uint64_t p = pi / (uint32_t)a.N1;
+          gg[q] = (double)a.pg[pi];
+          rp[q] = (const V *)(a.neu1 + p * a.D);
+        } else {
+          const uint64_t p = (pi - a.HOFF) / (uint32_t)a.W2;
+          gg[q] = 1.0;
+          rp[q] = (const V *)(a.neu1e + p * a.D);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; c++) {
+        const int ci = lane + c * 64;
+        if (ci < NC) {
+          V rv[UNR];
+#pragma unroll
+          for (int q = 0; q < UNR; q++) rv[q] = rp[q][ci];
+#pragma unroll
+          for (int q = 0; q < UNR; q++) {
+            if (i0 + q < e) {
+              const T *ev = (const T *)&rv[q];
+#pragma unroll
+              for (int k = 0; k < E; k++) {
+                if (kind == 0) {
+                  const double prod = gg[q] * (double)ev[k];
+                  acc[c][k] += prod;
+                } else {
+                  acc[c][k] += (double)ev[k];
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+    V *out = (V *)(a.partial + (uint64_t)item * a.D);
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int ci = lane + c * 64;
+      if (ci < NC) {
+        V v;
+        T *ev = (T *)&v;
+#pragma unroll
+        for (int k = 0; k < E; k++) ev[k] = (T)acc[c][k];
+        out[ci] = v;
+      }
+    }
+  }
+}
+
+template <typename T> struct PushArgs {
+  const int32_t *K;
+  uint32_t U;
+  const uint32_t *vid_row, *seg, *item_off;
+  const T *partial;
+  T *rows;
+  int32_t *local;
+  int D;
+  double lr, fudge;
+};
+
+// Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
+// (word2vec_global.h:176-185) per key, fp64 math; one wave per key.
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void k_push(PushArgs<T> a) {
+  using V = typename V16<T>::V;
+  constexpr int E = V16<T>::E;
+  const int lane = threadIdx.x & 63;
+  const int D = a.D, NC = D / E;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < a.U; u += (uint64_t)gridDim.x * 4) {
+    const int32_t vid = a.K[u];
+    if (lane == 0) a.local[vid] = -1;
+    const uint32_t hc = a.seg[1 * a.U + u] - a.seg[0 * a.U + u];
+    const uint32_t vc = a.seg[3 * a.U + u] - a.seg[2 * a.U + u];
+    if (hc == 0 && vc == 0) continue;
+    const uint32_t ih0 = a.item_off[2 * u], ih1 = a.item_off[2 * u + 1], iv1 = a.item_off[2 * u + 2];
+    V *row = (V *)(a.rows + (uint64_t)a.vid_row[vid] * 4 * D);
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int ci = lane + c * 64;
+      if (ci >= NC) continue;
+      for (int half = 0; half < 2; half++) {
+        const uint32_t cnt = half ? vc : hc;
+        if (cnt == 0) continue;
+        const uint32_t i0 = half ? ih1 : ih0, i1 = half ? iv1 : ih1;
+        double sum[E];
+#pragma unroll
+        for (int k = 0; k < E; k++) sum[k] = 0.0;
+        for (uint32_t it = i0; it < i1; it++) {
+          V pv = ((const V *)(a.partial + (uint64_t)it * D))[ci];
+          const T *pe = (const T *)&pv;
+#pragma unroll
+          for (int k = 0; k < E; k++) sum[k] += (double)pe[k];
+        }
+        V w = row[half * NC + ci], w2 = row[(2 + half) * NC + ci];
+        T *we = (T *)&w, *w2e = (T *)&w2;
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+          const double g = sum[k] / (double)cnt;
+          const double gsq = g * g;
+          const double acc2 = (double)w2e[k] + gsq;
+          const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
+          w2e[k] = (T)acc2;
+          we[k] = (T)((double)we[k] + step);
+        }
+        row[half * NC + ci] = w;
+        row[(2 + half) * NC + ci] = w2;
+      }
+    }
+  }
+}
+
+__global__ void k_trace_copy(const int32_t *__restrict__ src, uint64_t n, int32_t *__restrict__ dst) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+inline unsigned nblk(uint64_t threads, unsigned bs = 256) { return (unsigned)std::max<uint64_t>(1, (threads + bs - 1) / bs); }
+
+// ---- per-kernel HIP-event timing ----------------------------------------
+enum { KT_KEEP = 0, KT_FWD, KT_SORT, KT_GATHER, KT_PUSH, KT_PULL, KT_N };
+
+struct Timer {
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  double ms[KT_N] = {0};
+  uint64_t cnt[KT_N] = {0};
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  hipEvent_t begin(hipStream_t s) {
+    if (!on) return nullptr;
+    hipEvent_t e = get();
+    (void)hipEventRecord(e, s);
+    return e;
+  }
+  void end(int k, hipEvent_t b, hipStream_t s) {
+    if (!on || !b) return;
+    hipEvent_t e = get();
+    (void)hipEventRecord(e, s);
+    pending.push_back({k, {b, e}});
+  }
+  void resolve() {  // caller has synchronized the stream
+    for (auto &q : pending) {
+      float t = 0;
+      (void)hipEventElapsedTime(&t, q.second.first, q.second.second);
+      ms[q.first] += t;
+      cnt[q.first]++;
+      pool.push_back(q.second.first);
+      pool.push_back(q.second.second);
+    }
+    pending.clear();
+  }
+  ~Timer() {
+    for (auto &q : pending) {
+      (void)hipEventDestroy(q.second.first);
+      (void)hipEventDestroy(q.second.second);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+}  // namespace
+
+struct swps_w2v {
+  swps_table *t = nullptr;
+  swps_w2v_cfg cfg{};
+  int D = 0, W = 0, N = 0, NCH = 1;
+  bool f64 = false;
+  hipStream_t s = nullptr;
+  // host corpus / vocab
+  std::vector<int32_t> tok;
+  std::vector<int32_t> tok_line;
+  std::vector<int64_t> line_off;
+  std::vector<uint8_t> line_valid;
+  std::vector<uint64_t> vocab_keys;
+  std::vector<int32_t> counts;
+  uint64_t train_words = 0;
+  bool loaded = false, inited = false;
+  // schedule (identical every epoch)
+  struct Batch {
+    uint64_t l0, l1, kofs;
+    uint32_t U;
+  };
+  std::vector<Batch> batches;
+  std::vector<int32_t> allK;
+  uint64_t max_tok = 0, max_U = 0, max_lines = 0;
+  uint64_t cursor = 0;  // next global batch index
+  // device
+  DevMem d_tok, d_tok_line, d_line_off, d_ran, d_exptab, d_unigram, d_starts, d_vid_row, d_cache_h, d_cache_v,
+      d_local, d_K;
+  DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_pos_tok, d_pos_state, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
+      d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_tmp, d_trace, d_rows_touched;
+  uint64_t *h_small = nullptr;  // pinned readback
+  // RNG (utils/random.h:44-47, seed 2008)
+  uint64_t lstate = 2008ULL;
+  uint64_t fstate = std::numeric_limits<unsigned long>::max() / 2;
+  // stats
+  uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
+  // negative trace
+  uint64_t trace_cap = 0;
+  std::vector<int64_t> trace;
+  Timer timer;
+};
+
+namespace {
+
+int check_cfg(swps_w2v *w) {
+  const auto &c = w->cfg;
+  if (c.window <= 0 || 2 * c.window > 64) return fail(SWPS_E_CFG, "window must be in [1, 32]");
+  if (c.negative < 0 || c.negative + 1 > 64) return fail(SWPS_E_CFG, "negative must be in [0, 63]");
+  if (c.minibatch <= 0) return fail(SWPS_E_CFG, "minibatch must be positive");
+  if (c.unigram_size == 0 || c.unigram_size > (1ULL << 31)) return fail(SWPS_E_CFG, "unigram_size out of range");
+  const int E = w->f64 ? 2 : 4;
+  if (w->D % E != 0) return fail(SWPS_E_UNSUPPORTED, "dim must be a multiple of 16 bytes (4 fp32 / 2 fp64)");
+  int nc = w->D / E;
+  w->NCH = (nc + 63) / 64;
+  if (w->NCH > 4) return fail(SWPS_E_UNSUPPORTED, "dim too large (max 1024 fp32 / 512 fp64)");
+  return SWPS_OK;
+}
+
+// Vocab (word2vec_global.h:385-444, nthreads = 1): word counts over valid
+// lines, `_local_keys` filled in first-occurrence order; vid = position in the
+// std::unordered_set iteration order (= `_wordids`, the unigram-table order).
+int ingest(swps_w2v *w, const std::vector<uint64_t> &tok_keys, std::vector<int64_t> &&line_off) {
+  const uint64_t nl = line_off.size() - 1;
+  w->line_off = std::move(line_off);
+  w->line_valid.assign(nl, 0);
+  std::unordered_map<uint64_t, int32_t> cnt;
+  std::unordered_set<uint64_t> local_keys;
+  uint64_t tw = 0;
+  for (uint64_t l = 0; l < nl; l++) {
+    const int64_t a = w->line_off[l], b = w->line_off[l + 1];
+    const bool valid = (b - a) >= w->cfg.min_sentence_length;
+    w->line_valid[l] = valid;
+    if (!valid) continue;
+    tw += (uint64_t)(b - a);
+    for (int64_t i = a; i < b; i++) {
+      auto it = cnt.find(tok_keys[i]);
+      if (it != cnt.end())
+        it->second++;
+      else {
+        cnt.emplace(tok_keys[i], 1);
+        local_keys.insert(tok_keys[i]);
+      }
+    }
+  }
+  if (local_keys.size() < 5) return fail(SWPS_E_UNSUPPORTED, "fewer than 5 keys (word2vec_global.h:556 returns)");
+  w->train_words = tw;
+  w->vocab_keys.assign(local_keys.begin(), local_keys.end());
+  std::unordered_map<uint64_t, int32_t> vid;
+  vid.reserve(w->vocab_keys.size() * 2);
+  w->counts.resize(w->vocab_keys.size());
+  for (size_t i = 0; i < w->vocab_keys.size(); i++) {
+    if (w->vocab_keys[i] == 0)
+      return fail(SWPS_E_UNSUPPORTED, "a vocab key hashes to 0 (the reference redraws such negatives)");
+    vid[w->vocab_keys[i]] = (int32_t)i;
+    w->counts[i] = cnt[w->vocab_keys[i]];
+  }
+  const uint64_t nt = tok_keys.size();
+  w->tok.resize(nt);
+  w->tok_line.resize(nt);
+  for (uint64_t l = 0; l < nl; l++)
+    for (int64_t i = w->line_off[l]; i < w->line_off[l + 1]; i++) {
+      auto it = vid.find(tok_keys[i]);
+      if (it == vid.end())
+        return fail(SWPS_E_UNSUPPORTED, "a word occurs only in lines shorter than min_sentence_length "
+                                        "(to_sample reads past word_freq in the reference)");
+      w->tok[i] = it->second;
+      w->tok_line[i] = (int32_t)l;
+    }
+  w->loaded = true;
+  return SWPS_OK;
+}
+
+// gen_unigram_table (word2vec_global.h:467-497) in run-length form: the
+// 1e8-entry walk assigns word i the slots [start_i, start_{i+1}); the switch
+// to word i+1 happens at the first slot a >= start_i with a/T > d1_i.
+void unigram_starts(const uint64_t *keys, const int32_t *counts, size_t V, uint64_t T, std::vector<uint64_t> &starts) {
+  std::vector<std::pair<uint64_t, int32_t>> by_key(V);
+  for (size_t i = 0; i < V; i++) by_key[i] = {keys[i], counts[i]};
+  std::sort(by_key.begin(), by_key.end());
+  double pw = 0;
+  for (auto &kc : by_key) pw += std::pow(kc.second, 0.75);  // std::map order
+  starts.assign(V + 1, T);
+  starts[0] = 0;
+  double d1 = std::pow(counts[0], 0.75) / (double)pw;
+  for (size_t i = 0; i + 1 < V; i++) {
+    const uint64_t lo = starts[i];
+    auto pred = [&](uint64_t a) { return (int64_t)a / (double)T > d1; };
+    uint64_t a = (uint64_t)std::max<double>((double)lo, std::floor(d1 * (double)T));
+    if (a > T) a = T;
+    while (a > lo && pred(a - 1)) a--;
+    while (a < T && !pred(a)) a++;
+    if (a >= T) break;  // word i runs to the end; later words get no slots
+    starts[i + 1] = a + 1;
+    d1 += std::pow(counts[i + 1], 0.75) / (double)pw;
+  }
+}
+
+// The per-epoch batch schedule of TrainModelThread(0) (word2vec_global.h:
+// 591-651): line 1 trains before the first gather (its gradients are dropped
+// by the pull), then a push/gather/pull every `minibatch` lines; the gather
+// window is the next minibatch+3 valid lines (3 tasks, `line_count >
+// minibatch`); the epoch stops after the line where cur_train_words exceeds
+// train_words.
+void build_schedule(swps_w2v *w) {
+  const uint64_t nl = w->line_off.size() - 1;
+  const int B = w->cfg.minibatch;
+  w->batches.clear();
+  w->allK.clear();
+  auto window = [&](uint64_t li) {
+    std::vector<int32_t> K;
+    int count = 0;
+    for (int task = 0; task < 3; task++)
+      while (li < nl) {
+        const uint64_t l = li++;
+        if (!w->line_valid[l]) continue;
+        for (int64_t i = w->line_off[l]; i < w->line_off[l + 1]; i++) K.push_back(w->tok[i]);
+        if (++count > B) break;
+      }
+    std::sort(K.begin(), K.end());
+    K.erase(std::unique(K.begin(), K.end()), K.end());
+    return K;
+  };
+  auto emit = [&](uint64_t l0, uint64_t l1, const std::vector<int32_t> *K) {
+    swps_w2v::Batch b{l0, l1, w->allK.size(), 0};
+    if (K) {
+      b.U = (uint32_t)K->size();
+      w->allK.insert(w->allK.end(), K->begin(), K->end());
+    }
+    w->batches.push_back(b);
+  };
+  std::vector<int32_t> K;
+  bool haveK = false;
+  uint64_t start = 0, cur = 0, line_counter = 0, last = 0;
+  for (uint64_t li = 0; li < nl; li++) {
+    cur += (uint64_t)(w->line_off[li + 1] - w->line_off[li]);
+    line_counter++;
+    last = li + 1;
+    if (line_counter == 1) {
+      emit(start, li + 1, haveK ? &K : nullptr);
+      K = window(li + 1);
+      haveK = true;
+      start = li + 1;
+    }
+    if (line_counter % (uint64_t)B == 0) {
+      emit(start, li + 1, haveK ? &K : nullptr);
+      K = window(li + 1);
+      start = li + 1;
+    }
+    if (cur > w->train_words) break;
+  }
+  emit(start, last, haveK ? &K : nullptr);
+  w->max_tok = w->max_U = w->max_lines = 0;
+  for (auto &b : w->batches) {
+    w->max_tok = std::max<uint64_t>(w->max_tok, (uint64_t)(w->line_off[b.l1] - w->line_off[b.l0]));
+    w->max_U = std::max<uint64_t>(w->max_U, b.U);
+    w->max_lines = std::max<uint64_t>(w->max_lines, b.l1 - b.l0);
+  }
+}
+
+int upload_corpus(swps_w2v *w) {
+  hipStream_t s = w->s;
+  const uint64_t V = w->vocab_keys.size();
+  SWPS_TRY(upload(w->d_tok, w->tok, s));
+  SWPS_TRY(upload(w->d_tok_line, w->tok_line, s));
+  SWPS_TRY(upload(w->d_line_off, w->line_off, s));
+  SWPS_TRY(upload(w->d_K, w->allK, s));
+  // subsampling thresholds (word2vec_global.h:728-729), computed on the host
+  std::vector<float> ran(V);
+  for (uint64_t i = 0; i < V; i++) {
+    float freq = float(w->counts[i]) / (float)w->train_words;
+    ran[i] = (float)(1 - std::sqrt((double)(w->cfg.sample / freq)));
+  }
+  SWPS_TRY(upload(w->d_ran, ran, s));
+  // ExpTable (word2vec_global.h:252-258)
+  std::vector<float> ex(1000);
+  for (int i = 0; i < 1000; i++) {
+    float x = (i / (float)1000 * 2 - 1) * 6;
+    float e = (float)std::exp((double)x);
+    ex[i] = e / (e + 1);
+  }
+  SWPS_TRY(upload(w->d_exptab, ex, s));
+  std::vector<uint64_t> starts;
+  unigram_starts(w->vocab_keys.data(), w->counts.data(), V, w->cfg.unigram_size, starts);
+  SWPS_TRY(upload(w->d_starts, starts, s));
+  SWPS_TRY(w->d_unigram.ensure(w->cfg.unigram_size * 4));
+  k_build_unigram<<<4096, 256, 0, s>>>(w->d_starts.as<uint64_t>(), (uint32_t)V, w->cfg.unigram_size,
+                                       w->d_unigram.as<int32_t>());
+  SWPS_HIP(hipGetLastError());
+  const size_t es = w->f64 ? 8 : 4;
+  SWPS_TRY(w->d_cache_h.ensure(V * w->D * es));
+  SWPS_TRY(w->d_cache_v.ensure(V * w->D * es));
+  SWPS_TRY(w->d_local.ensure(V * 4));
+  SWPS_HIP(hipMemsetAsync(w->d_local.p, 0xFF, V * 4, s));
+  SWPS_TRY(w->d_vid_row.ensure(V * 4));
+  SWPS_HIP(hipStreamSynchronize(s));  // host vectors above go out of scope
+  return SWPS_OK;
+}
+
+template <typename T> int pull_all(swps_w2v *w) {
+  const uint64_t V = w->vocab_keys.size();
+  k_pull<T><<<nblk(V * 64), 256, 0, w->s>>>(nullptr, (uint32_t)V, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(),
+                                            w->D, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(), w->d_local.as<int32_t>(),
+                                            0);
+  SWPS_HIP(hipGetLastError());
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  return SWPS_OK;
+}
+
+template <typename T> int set_hv(swps_w2v *w, const double *hv) {
+  const uint64_t V = w->vocab_keys.size();
+  const int D = w->D;
+  std::vector<T> rows(V * 4 * D, (T)0);
+  for (uint64_t i = 0; i < V; i++)
+    for (int e = 0; e < 2 * D; e++) rows[i * 4 * D + e] = (T)hv[i * 2 * D + e];
+  DevMem d;
+  SWPS_TRY(upload(d, rows, w->s));
+  SWPS_TRY(table_set_rows(w->t, w->d_vid_row.as<uint32_t>(), V, d.p, w->s));
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  return pull_all<T>(w);
+}
+
+template <int NCH, typename T> void launch_forward(const FwdArgs<T> &a, hipStream_t s) {
+  k_forward<T, NCH><<<nblk((uint64_t)a.P * 64), 256, 0, s>>>(a);
+}
+template <int NCH, typename T> void launch_gather(const GatherArgs<T> &a, unsigned grid, hipStream_t s) {
+  k_gather<T, NCH><<<grid, 256, 0, s>>>(a);
+}
+template <int NCH, typename T> void launch_push(const PushArgs<T> &a, hipStream_t s) {
+  k_push<T, NCH><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
+}
+
+constexpr uint32_t kChunk = 128;
+
+template <typename T> int run_batch(swps_w2v *w) {
+  const uint64_t nb = w->batches.size();
+  const swps_w2v::Batch &B = w->batches[w->cursor % nb];
+  hipStream_t s = w->s;
+  Timer &tm = w->timer;
+  const int D = w->D, W = w->W, N = w->N;
+  const uint64_t t0 = (uint64_t)w->line_off[B.l0], t1 = (uint64_t)w->line_off[B.l1];
+  const uint64_t nt = t1 - t0, nl = B.l1 - B.l0;
+  const uint32_t U = B.U;
+  const int32_t *K = w->d_K.as<int32_t>() + B.kofs;
+  const bool sample_on = w->cfg.sample >= 0;
+  // ---- pull (global_pull_access.h:28-107 + server.h:129-154) ----
+  if (U) {
+    hipEvent_t e = tm.begin(s);
+    k_pull<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(), D,
+                                                     w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
+                                                     w->d_local.as<int32_t>(), 1);
+    SWPS_HIP(hipGetLastError());
+    tm.end(KT_PULL, e, s);
+  }
+  // ---- subsample mask + LCG offsets ----
+  SWPS_TRY(w->d_kflag.ensure((nt + 1) * 4));
+  SWPS_TRY(w->d_kscan.ensure((nt + 1) * 4));
+  SWPS_TRY(w->d_ldraw.ensure((nl + 1) * 8));
+  SWPS_TRY(w->d_ldoff.ensure((nl + 1) * 8));
+  hipEvent_t ek = tm.begin(s);
+  k_keep<<<nblk(nt + 1), 256, 0, s>>>(w->d_tok.as<int32_t>(), t0, nt, w->d_ran.as<float>(), w->fstate, sample_on,
+                                      w->d_kflag.as<int32_t>());
+  SWPS_HIP(hipGetLastError());
+  size_t tb1 = 0, tb2 = 0;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, w->d_kflag.as<int32_t>(), w->d_kscan.as<int32_t>(),
+                                            (int)(nt + 1), s));
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, w->d_ldraw.as<uint64_t>(), w->d_ldoff.as<uint64_t>(),
+                                            (int)(nl + 1), s));
+  SWPS_TRY(w->d_tmp.ensure(std::max(tb1, tb2)));
+  size_t tb = w->d_tmp.bytes;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, tb, w->d_kflag.as<int32_t>(), w->d_kscan.as<int32_t>(),
+                                            (int)(nt + 1), s));
+  k_line_draws<<<nblk(nl + 1), 256, 0, s>>>(w->d_line_off.as<int64_t>(), B.l0, nl, t0, w->d_kscan.as<int32_t>(), N,
+                                            w->d_ldraw.as<uint64_t>());
+  SWPS_HIP(hipGetLastError());
+  tb = w->d_tmp.bytes;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, tb, w->d_ldraw.as<uint64_t>(), w->d_ldoff.as<uint64_t>(),
+                                            (int)(nl + 1), s));
+  SWPS_TRY(w->d_pos_tok.ensure((nt + 1) * 4));
+  SWPS_TRY(w->d_pos_state.ensure((nt + 1) * 8));
+  k_compact<<<nblk(nt), 256, 0, s>>>(w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(), t0, nt, B.l0,
+                                     w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(), w->lstate, N,
+                                     w->d_pos_tok.as<int32_t>(), w->d_pos_state.as<uint64_t>());
+  SWPS_HIP(hipGetLastError());
+  tm.end(KT_KEEP, ek, s);
+  SWPS_HIP(hipMemcpyAsync(&w->h_small[0], w->d_kscan.as<int32_t>() + nt, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipMemcpyAsync(&w->h_small[1], w->d_ldoff.as<uint64_t>() + nl, 8, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  const uint64_t P = w->h_small[0] & 0xFFFFFFFFull;
+  const uint64_t draws = w->h_small[1];
+  const uint64_t lstate_in = w->lstate;
+  (void)lstate_in;
+  w->lstate = lcg_jump(w->lstate, draws, kLcgA, kLcgC);
+  if (sample_on) w->fstate = lcg_jump(w->fstate, nt, kFlcgA, kLcgC);
+  w->st_batches++;
+  w->st_kept += P;
+  w->st_words += nt;
+  w->st_pulled += U;
+  const bool tracing = w->trace.size() < w->trace_cap;
+  if (P > 0 && (U > 0 || tracing)) {
+    // ---- forward (learn_instance) ----
+    const uint64_t HOFF = P * (uint64_t)(N + 1);
+    const uint64_t M = HOFF + P * (uint64_t)(2 * W);
+    if (M >= (1ULL << 31)) return fail(SWPS_E_UNSUPPORTED, "minibatch too large (2^31 gradient records)");
+    SWPS_TRY(w->d_neu1.ensure(P * D * sizeof(T)));
+    SWPS_TRY(w->d_neu1e.ensure(P * D * sizeof(T)));
+    SWPS_TRY(w->d_pkeys.ensure(M * 4));
+    SWPS_TRY(w->d_pvals.ensure(M * 4));
+    SWPS_TRY(w->d_pkeys_s.ensure(M * 4));
+    SWPS_TRY(w->d_pvals_s.ensure(M * 4));
+    SWPS_TRY(w->d_pg.ensure(HOFF * 4));
+    if (tracing) SWPS_TRY(w->d_trace.ensure(std::max<uint64_t>(1, P * N) * 4));
+    FwdArgs<T> fa{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(),
+                  w->d_pos_tok.as<int32_t>(), w->d_pos_state.as<uint64_t>(), (int)P, w->d_cache_h.as<T>(),
+                  w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), U, w->d_unigram.as<int32_t>(),
+                  w->cfg.unigram_size, w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<T>(),
+                  w->d_neu1e.as<T>(), w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), w->d_pg.as<float>(),
+                  HOFF, tracing ? w->d_trace.as<int32_t>() : nullptr,
+                  w->d_rows_touched.as<unsigned long long>()};
+    hipEvent_t ef = tm.begin(s);
+    switch (w->NCH) {
+      case 1: launch_forward<1>(fa, s); break;
+      case 2: launch_forward<2>(fa, s); break;
+      case 3: launch_forward<3>(fa, s); break;
+      default: launch_forward<4>(fa, s); break;
+    }
+    SWPS_HIP(hipGetLastError());
+    tm.end(KT_FWD, ef, s);
+    if (tracing) {
+      std::vector<int32_t> tr(P * N);
+      if (!tr.empty()) {
+        SWPS_HIP(hipMemcpyAsync(tr.data(), w->d_trace.p, tr.size() * 4, hipMemcpyDeviceToHost, s));
+        SWPS_HIP(hipStreamSynchronize(s));
+      }
+      for (auto v : tr)
+        if (w->trace.size() < w->trace_cap) w->trace.push_back(v);
+    }
+    if (U > 0) {
+      // ---- inverted index: stable radix sort of records by local key ----
+      int bits = 1;
+      while ((1ULL << bits) <= U) bits++;
+      hipEvent_t es = tm.begin(s);
+      size_t sb = 0;
+      SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                                                  w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (int)M, 0,
+                                                  bits, s));
+      SWPS_TRY(w->d_tmp.ensure(sb));
+      sb = w->d_tmp.bytes;
+      SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(w->d_tmp.p, sb, w->d_pkeys.as<uint32_t>(),
+                                                  w->d_pkeys_s.as<uint32_t>(), w->d_pvals.as<uint32_t>(),
+                                                  w->d_pvals_s.as<uint32_t>(), (int)M, 0, bits, s));
+      SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
+      SWPS_HIP(hipMemsetAsync(w->d_seg.p, 0, (uint64_t)U * 16, s));
+      k_segments<<<nblk(M), 256, 0, s>>>(w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, HOFF, U,
+                                         w->d_seg.as<uint32_t>());
+      SWPS_HIP(hipGetLastError());
+      SWPS_TRY(w->d_icnt.ensure((2ULL * U + 1) * 4));
+      SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
+      k_item_counts<<<nblk(2ULL * U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, w->d_icnt.as<uint32_t>());
+      SWPS_HIP(hipGetLastError());
+      size_t ib = 0;
+      SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, ib, w->d_icnt.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
+                                                (int)(2 * U + 1), s));
+      SWPS_TRY(w->d_tmp.ensure(ib));
+      ib = w->d_tmp.bytes;
+      SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, ib, w->d_icnt.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
+                                                (int)(2 * U + 1), s));
+      tm.end(KT_SORT, es, s);
+      // ---- chunked segmented gradient sums ----
+      const uint64_t max_items = 2ULL * U + M / kChunk + 1;
+      SWPS_TRY(w->d_partial.ensure(max_items * D * sizeof(T)));
+      GatherArgs<T> ga{w->d_ioff.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U, kChunk,
+                       w->d_neu1.as<T>(), w->d_neu1e.as<T>(), w->d_pg.as<float>(), HOFF, N + 1, 2 * W, D,
+                       w->d_partial.as<T>()};
+      const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(max_items * 64), 8192);
+      hipEvent_t eg = tm.begin(s);
+      switch (w->NCH) {
+        case 1: launch_gather<1>(ga, ggrid, s); break;
+        case 2: launch_gather<2>(ga, ggrid, s); break;
+        case 3: launch_gather<3>(ga, ggrid, s); break;
+        default: launch_gather<4>(ga, ggrid, s); break;
+      }
+      SWPS_HIP(hipGetLastError());
+      tm.end(KT_GATHER, eg, s);
+      w->st_pairs += M;
+    }
+  }
+  if (U > 0) {
+    // ---- push: mean + AdaGrad (also clears the local index map) ----
+    if (P == 0) {
+      SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
+      SWPS_HIP(hipMemsetAsync(w->d_seg.p, 0, (uint64_t)U * 16, s));
+      SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
+      SWPS_HIP(hipMemsetAsync(w->d_ioff.p, 0, (2ULL * U + 1) * 4, s));
+    }
+    PushArgs<T> pa{K, U, w->d_vid_row.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
+                   w->d_partial.as<T>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
+                   (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge};
+    hipEvent_t ep = tm.begin(s);
+    switch (w->NCH) {
+      case 1: launch_push<1>(pa, s); break;
+      case 2: launch_push<2>(pa, s); break;
+      case 3: launch_push<3>(pa, s); break;
+      default: launch_push<4>(pa, s); break;
+    }
+    SWPS_HIP(hipGetLastError());
+    tm.end(KT_PUSH, ep, s);
+    w->st_pushed += U;
+  }
+  w->cursor++;
+  return SWPS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
+  if (!t || !cfg || !out) return fail(SWPS_E_CFG, "null argument");
+  *out = nullptr;
+  if (t->cfg.layout != SWPS_LAYOUT_W2V) return fail(SWPS_E_CFG, "table layout must be SWPS_LAYOUT_W2V");
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  swps_w2v *w = new swps_w2v();
+  w->t = t;
+  w->cfg = *cfg;
+  w->D = t->cfg.dim;
+  w->W = cfg->window;
+  w->N = cfg->negative;
+  w->f64 = t->cfg.dtype == SWPS_F64;
+  w->s = t->stream;
+  w->timer.on = cfg->profile != 0;
+  int rc = check_cfg(w);
+  if (!rc && hipHostMalloc((void **)&w->h_small, 64) != hipSuccess) rc = fail(SWPS_E_OOM, "pinned alloc");
+  if (!rc) rc = w->d_rows_touched.ensure(16);
+  if (!rc && hipMemset(w->d_rows_touched.p, 0, 16) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
+  if (!rc) {
+    uint64_t A[kMaxJump + 1], C[kMaxJump + 1];
+    for (int k = 0; k <= kMaxJump; k++) {
+      A[k] = lcg_jump(1, k, kLcgA, kLcgC) - lcg_jump(0, k, kLcgA, kLcgC);
+      C[k] = lcg_jump(0, k, kLcgA, kLcgC);
+    }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_jumpA), A, sizeof(A)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_jumpC), C, sizeof(C)) != hipSuccess)
+      rc = fail(SWPS_E_HIP, "constant upload");
+  }
+  if (rc) {
+    if (w->h_small) (void)hipHostFree(w->h_small);
+    delete w;
+    return rc;
+  }
+  *out = w;
+  return SWPS_OK;
+}
+
+int swps_w2v_destroy(swps_w2v *w) {
+  if (!w) return SWPS_OK;
+  (void)hipSetDevice(w->t->cfg.device);
+  (void)hipStreamSynchronize(w->s);
+  if (w->h_small) (void)hipHostFree(w->h_small);
+  delete w;
+  return SWPS_OK;
+}
+
+// LineFileReader + split(" ") + BKDRHash / atoi (word2vec_global.h:215-227)
+int swps_w2v_load_text(swps_w2v *w, const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return fail(SWPS_E_IO, std::string("no such file or directory: ") + path);
+  std::vector<uint64_t> keys;
+  std::vector<int64_t> off{0};
+  char *buf = nullptr;
+  size_t cap = 0;
+  ssize_t n;
+  std::string word;
+  while ((n = getdelim(&buf, &cap, '\n', f)) >= 0) {
+    if (n >= 1 && buf[n - 1] == '\n') buf[--n] = 0;
+    const size_t len = strlen(buf);  // std::string(cline) stops at a NUL
+    size_t i = 0;
+    while (i < len) {
+      while (i < len && buf[i] == ' ') i++;
+      if (i >= len) break;
+      size_t j = i;
+      while (j < len && buf[j] != ' ') j++;
+      word.assign(buf + i, j - i);
+      keys.push_back(w->cfg.key_mode == SWPS_KEY_ATOI ? (uint64_t)(int64_t)atoi(word.c_str()) : bkdr(word.c_str()));
+      i = j;
+    }
+    off.push_back((int64_t)keys.size());
+  }
+  free(buf);
+  fclose(f);
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  SWPS_TRY(ingest(w, keys, std::move(off)));
+  build_schedule(w);
+  return upload_corpus(w);
+}
+
+int swps_w2v_load_tokens(swps_w2v *w, const uint32_t *word_ids, uint64_t ntok, const uint64_t *line_off,
+                         uint64_t nlines, const uint64_t *word_keys, uint64_t nwords) {
+  if (line_off[0] != 0 || line_off[nlines] != ntok) return fail(SWPS_E_CFG, "line_off must span [0, ntok]");
+  std::vector<uint64_t> keys(ntok);
+  for (uint64_t i = 0; i < ntok; i++) {
+    if (word_ids[i] >= nwords) return fail(SWPS_E_CFG, "word id out of range");
+    keys[i] = word_keys[word_ids[i]];
+  }
+  std::vector<int64_t> off(line_off, line_off + nlines + 1);
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  SWPS_TRY(ingest(w, keys, std::move(off)));
+  build_schedule(w);
+  return upload_corpus(w);
+}
+
+int swps_w2v_vocab(swps_w2v *w, uint64_t *keys, int32_t *counts, uint64_t cap, uint64_t *n) {
+  *n = w->vocab_keys.size();
+  if (cap < *n) return fail(SWPS_E_CFG, "buffer too small");
+  for (size_t i = 0; i < w->vocab_keys.size(); i++) {
+    if (keys) keys[i] = w->vocab_keys[i];
+    if (counts) counts[i] = w->counts[i];
+  }
+  return SWPS_OK;
+}
+
+int swps_w2v_info(swps_w2v *w, uint64_t *o) {
+  o[0] = w->vocab_keys.size();
+  o[1] = w->train_words;
+  o[2] = w->line_off.empty() ? 0 : w->line_off.size() - 1;
+  o[3] = w->tok.size();
+  o[4] = w->batches.size();
+  o[5] = w->max_tok;
+  o[6] = w->lstate;
+  o[7] = w->fstate;
+  return SWPS_OK;
+}
+
+// The first full pull (word2vec_global.h:557-562 -> accessmethod.h:63-70):
+// every vocab key misses and gets a fresh WParam.
+int swps_w2v_init(swps_w2v *w) {
+  if (!w->loaded) return fail(SWPS_E_STATE, "load a corpus first");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  const uint64_t V = w->vocab_keys.size();
+  DevMem dk;
+  SWPS_TRY(upload(dk, w->vocab_keys, w->s));
+  SWPS_TRY(table_find_or_insert(w->t, dk.as<uint64_t>(), V, w->d_vid_row.as<uint32_t>(), w->s));
+  if (w->cfg.init_mode == SWPS_W2V_INIT_REF) {
+    // Vec::randInit (vec1.h:229-232): (rand()/(float)RAND_MAX - 0.5)/D, h then
+    // v per key, keys in _local_keys order, after rand_offset earlier calls.
+    GlibcRand r(w->cfg.rand_seed);
+    for (uint64_t i = 0; i < w->cfg.rand_offset; i++) (void)r.next();
+    const int D = w->D;
+    std::vector<double> hv(V * 2 * D);
+    for (uint64_t i = 0; i < V * 2 * D; i++) {
+      float x = r.next() / (float)2147483647;
+      hv[i] = ((double)x - 0.5) / (double)(size_t)D;
+    }
+    SWPS_TRY(w->f64 ? set_hv<double>(w, hv.data()) : set_hv<float>(w, hv.data()));
+  } else {
+    SWPS_TRY(w->f64 ? pull_all<double>(w) : pull_all<float>(w));
+  }
+  w->inited = true;
+  return SWPS_OK;
+}
+
+int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
+  if (!w->inited) return fail(SWPS_E_STATE, "call swps_w2v_init first");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  for (uint64_t i = 0; i < count; i++) SWPS_TRY(w->f64 ? run_batch<double>(w) : run_batch<float>(w));
+  return SWPS_OK;
+}
+
+int swps_w2v_train_epochs(swps_w2v *w, int32_t niters) {
+  if (w->cursor % std::max<size_t>(1, w->batches.size()) != 0) return fail(SWPS_E_STATE, "not at an epoch boundary");
+  SWPS_TRY(swps_w2v_train_batches(w, (uint64_t)niters * w->batches.size()));
+  return swps_w2v_sync(w);
+}
+
+int swps_w2v_sync(swps_w2v *w) {
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  w->timer.resolve();
+  return SWPS_OK;
+}
+
+int swps_w2v_stats(swps_w2v *w, uint64_t *o) {
+  o[0] = w->st_batches;
+  o[1] = w->st_kept;
+  o[2] = w->st_words;
+  o[3] = w->st_pairs;
+  o[4] = w->lstate;
+  o[5] = w->fstate;
+  o[6] = w->st_pulled;
+  o[7] = w->st_pushed;
+  uint64_t rt[2] = {0, 0};
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  SWPS_HIP(hipMemcpy(rt, w->d_rows_touched.p, 16, hipMemcpyDeviceToHost));
+  o[8] = rt[0];
+  o[9] = rt[1];
+  return SWPS_OK;
+}
+
+int swps_w2v_get_params(swps_w2v *w, double *out) {
+  SWPS_TRY(swps_w2v_sync(w));
+  const uint64_t V = w->vocab_keys.size();
+  const int R = 4 * w->D;
+  DevMem d;
+  const size_t es = w->f64 ? 8 : 4;
+  SWPS_TRY(d.ensure(V * R * es));
+  SWPS_TRY(table_get_rows(w->t, w->d_vid_row.as<uint32_t>(), V, d.p, w->s));
+  std::vector<char> h(V * R * es);
+  SWPS_HIP(hipMemcpyAsync(h.data(), d.p, h.size(), hipMemcpyDeviceToHost, w->s));
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  for (uint64_t i = 0; i < V * R; i++) out[i] = w->f64 ? ((double *)h.data())[i] : (double)((float *)h.data())[i];
+  return SWPS_OK;
+}
+
+int swps_w2v_set_params(swps_w2v *w, const double *hv) {
+  if (!w->inited) SWPS_TRY(swps_w2v_init(w));
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  return w->f64 ? set_hv<double>(w, hv) : set_hv<float>(w, hv);
+}
+
+int swps_w2v_unigram_at(swps_w2v *w, const uint64_t *idx, uint64_t n, uint32_t *out) {
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  for (uint64_t i = 0; i < n; i++) {
+    if (idx[i] >= w->cfg.unigram_size) return fail(SWPS_E_CFG, "slot out of range");
+    SWPS_HIP(hipMemcpy(out + i, w->d_unigram.as<int32_t>() + idx[i], 4, hipMemcpyDeviceToHost));
+  }
+  return SWPS_OK;
+}
+
+int swps_w2v_trace_negatives(swps_w2v *w, uint64_t cap) {
+  w->trace_cap = cap;
+  w->trace.clear();
+  return SWPS_OK;
+}
+
+int swps_w2v_negatives(swps_w2v *w, int64_t *out, uint64_t cap, uint64_t *n) {
+  *n = std::min<uint64_t>(cap, w->trace.size());
+  std::copy(w->trace.begin(), w->trace.begin() + *n, out);
+  return SWPS_OK;
+}
+
+int swps_w2v_kernel_times(swps_w2v *w, double *out, int32_t reset) {
+  SWPS_TRY(swps_w2v_sync(w));
+  for (int k = 0; k < KT_N; k++) {
+    out[2 * k] = w->timer.ms[k];
+    out[2 * k + 1] = (double)w->timer.cnt[k];
+    if (reset) {
+      w->timer.ms[k] = 0;
+      w->timer.cnt[k] = 0;
+    }
+  }
+  return SWPS_OK;
+}
+
+void *swps_w2v_stream(swps_w2v *w) { return (void *)w->s; }
+
+int swps_unigram_starts(const uint64_t *keys, const int32_t *counts, uint64_t V, uint64_t table_size,
+                        uint64_t *starts) {
+  if (V == 0 || table_size == 0) return fail(SWPS_E_CFG, "empty vocab or table");
+  std::vector<uint64_t> st;
+  unigram_starts(keys, counts, V, table_size, st);
+  std::copy(st.begin(), st.end(), starts);
+  return SWPS_OK;
+}
+
+int swps_glibc_rand(uint32_t seed, uint64_t skip, uint64_t n, int32_t *out) {
+  GlibcRand r(seed);
+  for (uint64_t i = 0; i < skip; i++) (void)r.next();
+  for (uint64_t i = 0; i < n; i++) out[i] = r.next();
+  return SWPS_OK;
+}
+
+}  // extern "C"

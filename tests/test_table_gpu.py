@@ -1,0 +1,64 @@
+"""The HBM parameter shard: pull / push / assign / export / dump / load."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pull_inserts_and_push_adagrad(lib, gpu):
+    D = 8
+    t = lib.Table("w2v", dim=D, capacity=1000, dtype="f64", learning_rate=0.7, init="hash", seed=3)
+    keys = torch.tensor(np.random.default_rng(0).choice(2 ** 62, 300, replace=False), dtype=torch.int64,
+                        device=gpu)
+    v1 = t.pull(keys)
+    assert t.size() == 300 and v1.shape == (300, 2 * D)
+    assert (v1.abs() <= 0.5 / D).all() and v1.abs().sum() > 0
+    v2 = t.pull(keys)  # hits return the same rows
+    assert torch.equal(v1, v2)
+    g = torch.randn(300, 2 * D, dtype=torch.float64, device=gpu) * 1e-2
+    rows0 = t.export(keys)
+    t.push(keys, g)
+    rows1 = t.export(keys)
+    h, v = rows0[:, :D], rows0[:, D:2 * D]
+    gh, gv = g[:, :D], g[:, D:]
+    h2 = gh * gh
+    exp_h = h + (gh * 0.7) / torch.sqrt(h2 + float(np.float32(1e-6)))
+    assert torch.allclose(rows1[:, :D], exp_h, rtol=1e-12, atol=0)
+    assert torch.allclose(rows1[:, 2 * D:3 * D], h2, rtol=1e-12, atol=0)
+
+
+def test_push_unknown_key_is_error(lib, gpu):
+    t = lib.Table("lr", capacity=10, dtype="f32")
+    k = torch.tensor([5, 6], dtype=torch.int64, device=gpu)
+    t.pull(k[:1])
+    with pytest.raises(lib.SwpsError) as e:
+        t.push(k, torch.zeros(2, 1, dtype=torch.float32, device=gpu))
+    assert "BADKEY" in str(e.value)
+
+
+def test_capacity_exhausted_is_error(lib, gpu):
+    t = lib.Table("lr", capacity=4, dtype="f32")
+    with pytest.raises(lib.SwpsError) as e:
+        t.pull(torch.arange(10, dtype=torch.int64, device=gpu))
+    assert "OOM" in str(e.value)
+
+
+def test_w2v_dump_format_and_sharded_load(lib, gpu, tmp_path):
+    D = 4
+    t = lib.Table("w2v", dim=D, capacity=100, dtype="f32", init="hash", seed=1)
+    keys = torch.arange(1, 51, dtype=torch.int64, device=gpu)
+    t.pull(keys)
+    path = str(tmp_path / "out.txt")
+    t.dump(path)
+    lines = open(path).read().strip().split("\n")
+    assert len(lines) == 50
+    key, v, h = lines[0].split("\t")
+    assert len(v.split(" ")) == D and len(h.split(" ")) == D
+    # server.h:49-62: each server keeps only the keys its hash-frag node owns
+    fm = lib.hashfrag_table(1000, 2)
+    owners = lib.to_node_id(np.arange(1, 51, dtype=np.uint64), 1000, fm)
+    for node in (1, 2):
+        t2 = lib.Table("w2v", dim=D, capacity=100, dtype="f32")
+        t2.load(path, frag_num=1000, world=2, node_id=node)
+        assert sorted(int(k) for k in t2.keys()) == [i + 1 for i in range(50) if owners[i] == node]
