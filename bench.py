@@ -85,8 +85,10 @@ def main():
     ap.add_argument("--vocab", type=int, default=253854)
     ap.add_argument("--line-len", type=int, default=1000)
     ap.add_argument("--dtype", default="f32")
-    ap.add_argument("--cpu-lines", type=int, default=300)
+    ap.add_argument("--cpu-lines", type=int, default=2500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fast", action="store_true",
+                    help="fp32 neu1/neu1e intermediates (default: fp64, the reference-parity mode)")
     args = ap.parse_args()
 
     import torch
@@ -108,7 +110,7 @@ def main():
     t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
                  device=local)
     w = sw.Word2Vec(t, window=args.window, negative=args.negative, minibatch=args.minibatch, sample=args.sample,
-                    alpha=args.alpha, init="ref", profile=True)
+                    alpha=args.alpha, init="ref", profile=True, fp64_intermediates=not args.fast)
     w.load_tokens(ids, off, keys)
     w.init()
     info = w.info()
@@ -163,7 +165,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 storage, f64 accumulate" if args.dtype == "f32" else "f64",
+        "dtype": ("f32 table, f32 intermediates, f64 accumulate" if args.fast else
+                  "f32 table, f64 intermediates + accumulate") if args.dtype == "f32" else "f64",
         "data": "synthetic Zipf(s=1) text8 stand-in, random-init (reference glibc-rand) params",
         "config": {"workload": "word2vec CBOW-NS (the reference's 'SGNS' app) text8-shaped corpus %d tokens, "
                                "vocab %d, dim %d, window %d, negative %d, sample %g, minibatch %d lines of %d "

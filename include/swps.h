@@ -133,7 +133,8 @@ typedef struct {
   int32_t init_mode;           /* SWPS_W2V_INIT_* */
   uint32_t rand_seed;          /* glibc srand seed (reference: 1) */
   uint64_t rand_offset;        /* rand() calls before the first pull (reference: 2 port binds) */
-  int32_t deterministic;       /* 1: fixed reduction order (always true today) */
+  int32_t fp64_intermediates;  /* 1: neu1/neu1e and gradient sums kept in fp64 like the reference's Vec
+                                * (parity mode for fp32 tables); 0: fp32 (fast mode). fp64 tables: always */
   int32_t profile;             /* 1: time kernels with HIP events */
 } swps_w2v_cfg;
 

@@ -131,197 +131,259 @@ __global__ void k_line_draws(const int64_t *__restrict__ line_off, uint64_t l0, 
   ldraw[j] = 1 + kept * (uint64_t)(N + 1);
 }
 
-// kept positions in order + the LCG state just before each position's draws
-__global__ void k_compact(const int32_t *__restrict__ tok_line, const int64_t *__restrict__ line_off, uint64_t t0,
-                          uint64_t nt, uint64_t l0, const int32_t *__restrict__ kscan,
-                          const uint64_t *__restrict__ ldoff, uint64_t lstate, int N, int32_t *__restrict__ pos_tok,
-                          uint64_t *__restrict__ pos_state) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nt) return;
-  int32_t p = kscan[i];
-  if (kscan[i + 1] == p) return;
-  int32_t l = tok_line[t0 + i];
-  uint64_t ls = (uint64_t)line_off[l] - t0;
-  uint64_t rank = (uint64_t)(p - kscan[ls]);
-  pos_tok[p] = (int32_t)(t0 + i);
-  pos_state[p] = lcg_jump(lstate, ldoff[l - l0] + 1 + rank * (uint64_t)(N + 1), kLcgA, kLcgC);
+// x mod d for a fixed divisor d < 2^63 with the precomputed m = floor((2^64-1)/d):
+// q = mulhi(x, m) underestimates x/d by at most 2, so two corrections are exact.
+__device__ __forceinline__ uint64_t fast_mod(uint64_t x, uint64_t d, uint64_t m) {
+  const uint64_t q = __umul64hi(x, m);
+  uint64_t r = x - q * d;
+  if (r >= d) r -= d;
+  if (r >= d) r -= d;
+  return r;
 }
 
-template <typename T> struct FwdArgs {
+struct RecArgs {
   const int32_t *tok, *tok_line;
   const int64_t *line_off;
-  const int32_t *pos_tok;
-  const uint64_t *pos_state;
-  int P;
-  const T *cache_h, *cache_v;
+  uint64_t t0, nt, l0;
+  const int32_t *kscan;
+  const uint64_t *ldoff;
+  uint64_t lstate;
+  int W, N;
+  uint64_t mW;  // floor((2^64-1)/W)
+  const int32_t *unigram;
+  uint64_t uni_size, mT;
   const int32_t *local;
   uint32_t U;
-  const int32_t *unigram;
-  uint64_t uni_size;
+  int32_t *rec;     // [P][RS]: word, ctx vid x 2W (-1 = none), target vid x (N+1) (-1 = skipped)
+  uint32_t *pkeys, *pvals;
+  int32_t *trace;
+  unsigned long long *rows_touched;
+};
+
+// One thread per token of the batch; for every kept position (to_sample true)
+// replays learn_instance's LCG draws (word2vec_global.h:669,686-691) from the
+// jumped state: b, the negatives from the unigram table, the context slots
+// a = b..2W-b (a != W) inside the line; writes the position record and the
+// (local key, record index) gradient records (key U = not in the batch's
+// pulled key set: dropped, as the reference's pull reset drops them).
+__global__ __launch_bounds__(256) void k_records(RecArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int nctx = 0, ntgt = 0;
+  if (i < a.nt) {
+    const int32_t p = a.kscan[i];
+    if (a.kscan[i + 1] != p) {
+      const uint64_t P = (uint64_t)a.kscan[a.nt];
+      const int W = a.W, N = a.N, RS = 2 * W + N + 2;
+      const uint64_t HOFF = P * (uint64_t)(N + 1);
+      const uint64_t t = a.t0 + i;
+      const int32_t l = a.tok_line[t];
+      const int64_t ls = a.line_off[l];
+      const int n = (int)(a.line_off[l + 1] - ls), pos = (int)((int64_t)t - ls);
+      const int32_t word = a.tok[t];
+      const uint64_t rank = (uint64_t)(p - a.kscan[(uint64_t)ls - a.t0]);
+      uint64_t x = lcg_jump(a.lstate, a.ldoff[l - a.l0] + 1 + rank * (uint64_t)(N + 1), kLcgA, kLcgC);
+      x = x * kLcgA + kLcgC;
+      const int b = (int)fast_mod(x, (uint64_t)W, a.mW);
+      int32_t *r = a.rec + (uint64_t)p * RS;
+      r[0] = word;
+      for (int j = 0; j < 2 * W; j++) {
+        int32_t cv = -1;
+        if (j < 2 * (W - b)) {
+          int aa = b + j;
+          if (aa >= W) aa++;
+          const int c = pos - W + aa;
+          if (c >= 0 && c < n) cv = a.tok[ls + c];
+        }
+        r[1 + j] = cv;
+        uint32_t key = a.U;
+        if (cv >= 0) {
+          nctx++;
+          const int32_t u = a.local[cv];
+          if (u >= 0) key = (uint32_t)u;
+        }
+        const uint64_t k = HOFF + (uint64_t)p * 2 * W + j;
+        a.pkeys[k] = key;
+        a.pvals[k] = (uint32_t)k;
+      }
+      for (int d = 0; d <= N; d++) {
+        int32_t tv = word;
+        if (d > 0) {
+          x = x * kLcgA + kLcgC;
+          tv = a.unigram[fast_mod(x >> 16, a.uni_size, a.mT)];
+          if (a.trace) a.trace[(uint64_t)p * N + d - 1] = tv;
+          if (tv == word) tv = -1;
+        }
+        r[1 + 2 * W + d] = tv;
+        uint32_t key = a.U;
+        if (tv >= 0) {
+          ntgt++;
+          const int32_t u = a.local[tv];
+          if (u >= 0) key = (uint32_t)u;
+        }
+        const uint64_t k = (uint64_t)p * (N + 1) + d;
+        a.pkeys[k] = key;
+        a.pvals[k] = (uint32_t)k;
+      }
+    }
+  }
+  // rows the forward will read (roofline accounting), one atomic per wave
+  unsigned long long c = (unsigned long long)nctx, g = (unsigned long long)ntgt;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    c += __shfl_xor(c, off, 64);
+    g += __shfl_xor(g, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (c | g)) {
+    atomicAdd(&a.rows_touched[0], c);
+    atomicAdd(&a.rows_touched[1], g);
+  }
+}
+
+// E consecutive elements of type X as one register chunk, converted to / from
+// fp64 (16 B of the table type per lane; 32 B when fp32 rows carry fp64
+// intermediates).
+template <typename X, int E> struct Chk;
+template <> struct Chk<float, 4> {
+  using R = float4;
+  static __device__ __forceinline__ R ld(const float *p) { return *(const float4 *)p; }
+  static __device__ __forceinline__ double at(const R &r, int k) { return (double)((const float *)&r)[k]; }
+  static __device__ __forceinline__ void st(float *p, const double (&v)[4]) {
+    *(float4 *)p = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+  }
+};
+template <> struct Chk<double, 4> {
+  struct R {
+    double2 a, b;
+  };
+  static __device__ __forceinline__ R ld(const double *p) {
+    R r;
+    r.a = ((const double2 *)p)[0];
+    r.b = ((const double2 *)p)[1];
+    return r;
+  }
+  static __device__ __forceinline__ double at(const R &r, int k) { return ((const double *)&r)[k]; }
+  static __device__ __forceinline__ void st(double *p, const double (&v)[4]) {
+    ((double2 *)p)[0] = make_double2(v[0], v[1]);
+    ((double2 *)p)[1] = make_double2(v[2], v[3]);
+  }
+};
+template <> struct Chk<double, 2> {
+  using R = double2;
+  static __device__ __forceinline__ R ld(const double *p) { return *(const double2 *)p; }
+  static __device__ __forceinline__ double at(const R &r, int k) { return ((const double *)&r)[k]; }
+  static __device__ __forceinline__ void st(double *p, const double (&v)[2]) { *(double2 *)p = make_double2(v[0], v[1]); }
+};
+
+template <typename T, typename A> struct FwdArgs {
+  const int32_t *rec;
+  int P;
+  const T *cache_h, *cache_v;
   const float *exptab;
   int D, W, N;
   float alpha;
-  T *neu1, *neu1e;
-  uint32_t *pkeys, *pvals;
+  A *neu1, *neu1e;
   float *pg;
-  uint64_t HOFF;
-  int32_t *trace;
-  unsigned long long *rows_touched;  // [0] context rows, [1] target rows
 };
 
-// One wave per kept position (learn_instance's per-position body).
-template <typename T, int NCH>
-__global__ __launch_bounds__(256) void k_forward(FwdArgs<T> a) {
-  using V = typename V16<T>::V;
+// One wave per kept position (the body of learn_instance's position loop,
+// word2vec_global.h:663-718).  All context v rows and target h rows of the
+// position are loaded in groups of G slots whose loads are issued together;
+// neu1 sums the context rows in slot order, then each target's dot with
+// neu1 is a wave reduction in fp64, g comes from the exp table, and
+// neu1e accumulates g*h.  Writes neu1, neu1e (gradient sources) and g.
+template <typename T, typename A, int NCH, int G>
+__global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
   constexpr int E = V16<T>::E;
+  using CT = Chk<T, E>;
+  using CA = Chk<A, E>;
   const int lane = threadIdx.x & 63;
-  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int p = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (p >= a.P) return;
   const int D = a.D, W = a.W, N = a.N, NC = D / E;
-  const int t = a.pos_tok[p];
-  const int l = a.tok_line[t];
-  const int64_t ls = a.line_off[l];
-  const int n = (int)(a.line_off[l + 1] - ls), pos = (int)(t - ls);
-  const int word = a.tok[t];
-  const uint64_t s = a.pos_state[p];
-  // lane k draws x_{k+1}: k = 0 -> b, k = 1..N -> negatives
-  const uint64_t x = c_jumpA[(lane < kMaxJump ? lane : 0) + 1] * s + c_jumpC[(lane < kMaxJump ? lane : 0) + 1];
-  const uint64_t x0 = __shfl(x, 0, 64);
-  const int b = (int)(x0 % (uint64_t)W);
-  int tgt = word;
-  int skip = 0;
-  if (lane >= 1 && lane <= N) {
-    tgt = a.unigram[(x >> 16) % a.uni_size];
-    skip = tgt == word;
-    if (a.trace) a.trace[(int64_t)p * N + lane - 1] = tgt;
-  }
-  const int nslot = 2 * (W - b);
-  int cvid = -1;
-  if (lane < nslot) {
-    int aa = b + lane;
-    if (aa >= W) aa++;
-    const int c = pos - W + aa;
-    if (c >= 0 && c < n) cvid = a.tok[ls + c];
-  }
-  double acc[NCH][E];
+  const int S = 2 * W + N + 1;  // slots: contexts then targets
+  const int32_t *r = a.rec + (uint64_t)p * (S + 1);
+  double acc[NCH][E], ne[NCH][E];
 #pragma unroll
   for (int c = 0; c < NCH; c++)
 #pragma unroll
-    for (int k = 0; k < E; k++) acc[c][k] = 0.0;
-  for (int j = 0; j < nslot; j++) {
-    const int cv = __shfl(cvid, j, 64);
-    if (cv < 0) continue;
-    const V *row = (const V *)(a.cache_v + (uint64_t)cv * D);
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      const int ci = lane + c * 64;
-      if (ci < NC) {
-        V v = row[ci];
-        const T *e = (const T *)&v;
-#pragma unroll
-        for (int k = 0; k < E; k++) acc[c][k] += (double)e[k];
-      }
+    for (int k = 0; k < E; k++) {
+      acc[c][k] = 0.0;
+      ne[c][k] = 0.0;
     }
-  }
-  double ne[NCH][E];
-#pragma unroll
-  for (int c = 0; c < NCH; c++)
-#pragma unroll
-    for (int k = 0; k < E; k++) ne[c][k] = 0.0;
   float gk = 0.f;
-  for (int d = 0; d <= N; d++) {
-    const int tv = __shfl(tgt, d, 64);
-    const int sk = __shfl(skip, d, 64);
-    if (sk) continue;
-    const V *row = (const V *)(a.cache_h + (uint64_t)tv * D);
-    V hv[NCH];
-    double part = 0.0;
+  for (int s0 = 0; s0 < S; s0 += G) {
+    typename CT::R rows[G][NCH];
+    int32_t vid[G];
 #pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      const int ci = lane + c * 64;
-      if (ci < NC) {
-        hv[c] = row[ci];
-        const T *e = (const T *)&hv[c];
+    for (int q = 0; q < G; q++) {
+      const int slot = s0 + q;
+      vid[q] = slot < S ? r[1 + slot] : -1;
+      if (vid[q] >= 0) {
+        const T *src = (slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * D;
 #pragma unroll
-        for (int k = 0; k < E; k++) part += acc[c][k] * (double)e[k];
-      }
-    }
-    part = wave_sum(part);
-    float f = 0;
-    f += part;
-    const int label = d == 0 ? 1 : 0;
-    float g;
-    if (f > 6)
-      g = (label - 1) * a.alpha;
-    else if (f < -6)
-      g = (label - 0) * a.alpha;
-    else
-      g = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      const int ci = lane + c * 64;
-      if (ci < NC) {
-        const T *e = (const T *)&hv[c];
-#pragma unroll
-        for (int k = 0; k < E; k++) {
-          const double prod = (double)g * (double)e[k];
-          ne[c][k] += prod;
+        for (int c = 0; c < NCH; c++) {
+          const int ci = lane + c * 64;
+          if (ci < NC) rows[q][c] = CT::ld(src + ci * E);
         }
       }
     }
-    if (lane == d) gk = g;
+#pragma unroll
+    for (int q = 0; q < G; q++) {
+      const int slot = s0 + q;
+      if (vid[q] < 0) continue;
+      if (slot < 2 * W) {
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          if (lane + c * 64 < NC)
+#pragma unroll
+            for (int k = 0; k < E; k++) acc[c][k] += CT::at(rows[q][c], k);
+      } else {
+        const int d = slot - 2 * W;
+        double part = 0.0;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          if (lane + c * 64 < NC)
+#pragma unroll
+            for (int k = 0; k < E; k++) {
+              const double prod = acc[c][k] * CT::at(rows[q][c], k);
+              part += prod;
+            }
+        part = wave_sum(part);
+        float f = 0;
+        f += part;
+        const int label = d == 0 ? 1 : 0;
+        float g;
+        if (f > 6)
+          g = (label - 1) * a.alpha;
+        else if (f < -6)
+          g = (label - 0) * a.alpha;
+        else
+          g = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          if (lane + c * 64 < NC)
+#pragma unroll
+            for (int k = 0; k < E; k++) {
+              const double prod = (double)g * CT::at(rows[q][c], k);
+              ne[c][k] += prod;
+            }
+        if (lane == d) gk = g;
+      }
+    }
   }
-  if (lane == 0) {
-    int nctx = 0;
-    for (int j = 0; j < nslot; j++) nctx += __shfl(cvid, j, 64) >= 0;
-    atomicAdd(&a.rows_touched[0], (unsigned long long)nctx);
-  }
-  {
-    const unsigned long long tb = __ballot(lane <= N && !skip);
-    if (lane == 0) atomicAdd(&a.rows_touched[1], (unsigned long long)__popcll(tb));
-  }
-  V *o1 = (V *)(a.neu1 + (uint64_t)p * D);
-  V *o2 = (V *)(a.neu1e + (uint64_t)p * D);
 #pragma unroll
   for (int c = 0; c < NCH; c++) {
     const int ci = lane + c * 64;
     if (ci < NC) {
-      V v1, v2;
-      T *e1 = (T *)&v1, *e2 = (T *)&v2;
-#pragma unroll
-      for (int k = 0; k < E; k++) {
-        e1[k] = (T)acc[c][k];
-        e2[k] = (T)ne[c][k];
-      }
-      o1[ci] = v1;
-      o2[ci] = v2;
+      CA::st(a.neu1 + (uint64_t)p * D + ci * E, acc[c]);
+      CA::st(a.neu1e + (uint64_t)p * D + ci * E, ne[c]);
     }
   }
-  if (lane <= N) {
-    const uint64_t i = (uint64_t)p * (N + 1) + lane;
-    uint32_t key = a.U;
-    if (!skip) {
-      const int32_t u = a.local[tgt];
-      if (u >= 0) key = (uint32_t)u;
-    }
-    a.pkeys[i] = key;
-    a.pvals[i] = (uint32_t)i;
-    a.pg[i] = gk;
-  }
-  if (lane < 2 * W) {
-    const uint64_t i = a.HOFF + (uint64_t)p * 2 * W + lane;
-    uint32_t key = a.U;
-    if (cvid >= 0) {
-      const int32_t u = a.local[cvid];
-      if (u >= 0) key = (uint32_t)u;
-    }
-    a.pkeys[i] = key;
-    a.pvals[i] = (uint32_t)i;
-  }
+  if (lane <= N) a.pg[(uint64_t)p * (N + 1) + lane] = gk;
 }
 
 // Segment bounds of each (local key, kind) run in the sorted records:
-// seg[0][u], seg[1][u] = h-pair range; seg[2][u], seg[3][u] = v-pair range.
+// seg[0][u], seg[1][u] = h-record range; seg[2][u], seg[3][u] = v-record range.
 __global__ void k_segments(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, uint64_t M,
                            uint64_t HOFF, uint32_t U, uint32_t *__restrict__ seg) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -347,106 +409,155 @@ __global__ void k_item_counts(const uint32_t *__restrict__ seg, uint32_t U, uint
   cnt[j] = (c + CH - 1) / CH;
 }
 
-template <typename T> struct GatherArgs {
-  const uint32_t *item_off, *seg, *vals;
-  uint32_t U, CH;
-  const T *neu1, *neu1e;
+// item descriptors {first record, end record | kind << 31, (key, kind) index j, chunk}
+__global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__restrict__ ioff, uint32_t U,
+                            uint32_t CH, uint4 *__restrict__ desc) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2ull * U) return;
+  const uint32_t u = (uint32_t)(j >> 1), kind = (uint32_t)(j & 1);
+  const uint32_t s = seg[(2 * kind) * U + u], e = seg[(2 * kind + 1) * U + u];
+  const uint32_t o = ioff[j], n = ioff[j + 1] - o;
+  for (uint32_t k = 0; k < n; k++) {
+    const uint32_t cs = s + k * CH;
+    desc[o + k] = make_uint4(cs, min(cs + CH, e) | (kind << 31), (uint32_t)j, k);
+  }
+}
+
+template <typename A> struct GatherArgs {
+  const uint4 *desc;
+  const uint32_t *ioff, *vals;
+  uint32_t U;
+  const A *neu1, *neu1e;
   const float *pg;
   uint64_t HOFF;
   int N1, W2, D;
-  T *partial;
+  A *partial;
 };
 
-// One wave per chunk of <= CH records of one (key, kind): the fp64 sum of
-// g*neu1[p] (h) or neu1e[p] (v) over the chunk, in record (= position) order.
-template <typename T, int NCH>
-__global__ __launch_bounds__(256) void k_gather(GatherArgs<T> a) {
-  using V = typename V16<T>::V;
+// One wave per chunk of <= 128 records of one (key, kind): the fp64 sum, in
+// record (= position) order, of g*neu1[p] (h records: accu_h(g*neu1),
+// word2vec_global.h:705) or neu1e[p] (v records: accu_v(neu1e), :716).
+// Record indices and g are loaded for the whole chunk up front; rows are
+// fetched UNR at a time.
+template <typename T, typename A, int NCH, int UNR>
+__global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
   constexpr int E = V16<T>::E;
-  constexpr int UNR = 4;
+  using CA = Chk<A, E>;
   const int lane = threadIdx.x & 63;
   const int NC = a.D / E;
-  const uint32_t U2 = 2 * a.U;
-  const uint32_t NI = a.item_off[U2];
+  const uint32_t NI = a.ioff[2 * a.U];
   for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
-    uint32_t lo = 0, hi = U2;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a.item_off[mid] <= item)
-        lo = mid;
-      else
-        hi = mid;
+    const uint4 d = a.desc[__builtin_amdgcn_readfirstlane(item)];
+    const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
+    uint32_t p0 = 0, p1 = 0;
+    float g0 = 1.f, g1 = 1.f;
+    if (lane < (int)n) {
+      const uint32_t pi = a.vals[s + lane];
+      if (kind == 0) {
+        p0 = pi / (uint32_t)a.N1;
+        g0 = a.pg[pi];
+      } else {
+        p0 = (uint32_t)((pi - a.HOFF) / (uint32_t)a.W2);
+      }
     }
-    const uint32_t u = lo >> 1, kind = lo & 1, j = item - a.item_off[lo];
-    const uint32_t s = a.seg[(2 * kind) * a.U + u] + j * a.CH;
-    const uint32_t e = min(s + a.CH, a.seg[(2 * kind + 1) * a.U + u]);
+    if (lane + 64 < (int)n) {
+      const uint32_t pi = a.vals[s + 64 + lane];
+      if (kind == 0) {
+        p1 = pi / (uint32_t)a.N1;
+        g1 = a.pg[pi];
+      } else {
+        p1 = (uint32_t)((pi - a.HOFF) / (uint32_t)a.W2);
+      }
+    }
+    const A *base = kind == 0 ? a.neu1 : a.neu1e;
     double acc[NCH][E];
 #pragma unroll
     for (int c = 0; c < NCH; c++)
 #pragma unroll
       for (int k = 0; k < E; k++) acc[c][k] = 0.0;
-    for (uint32_t i0 = s; i0 < e; i0 += UNR) {
-      const V *rp[UNR];
+    for (uint32_t r0 = 0; r0 < n; r0 += UNR) {
+      typename CA::R rv[UNR][NCH];
       double gg[UNR];
 #pragma unroll
       for (int q = 0; q < UNR; q++) {
-        const uint32_t i = min(i0 + q, e - 1);
-        const uint32_t pi = a.vals[i];
-        if (kind == 0) {
-          const uint64_t p = pi / (uint32_t)a.N1;
-          gg[q] = (double)a.pg[pi];
-          rp[q] = (const V *)(a.neu1 + p * a.D);
-        } else {
-          const uint64_t p = (pi - a.HOFF) / (uint32_t)a.W2;
-          gg[q] = 1.0;
-          rp[q] = (const V *)(a.neu1e + p * a.D);
+        const uint32_t idx = min(r0 + q, n - 1);
+        const uint32_t pr = idx < 64 ? __shfl(p0, (int)idx, 64) : __shfl(p1, (int)(idx - 64), 64);
+        gg[q] = (double)(idx < 64 ? __shfl(g0, (int)idx, 64) : __shfl(g1, (int)(idx - 64), 64));
+        const A *src = base + (uint64_t)pr * a.D;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+          const int ci = lane + c * 64;
+          if (ci < NC) rv[q][c] = CA::ld(src + ci * E);
         }
       }
 #pragma unroll
-      for (int c = 0; c < NCH; c++) {
-        const int ci = lane + c * 64;
-        if (ci < NC) {
-          V rv[UNR];
+      for (int q = 0; q < UNR; q++) {
+        if (r0 + q < n) {
 #pragma unroll
-          for (int q = 0; q < UNR; q++) rv[q] = rp[q][ci];
-#pragma unroll
-          for (int q = 0; q < UNR; q++) {
-            if (i0 + q < e) {
-              const T *ev = (const T *)&rv[q];
+          for (int c = 0; c < NCH; c++)
+            if (lane + c * 64 < NC)
 #pragma unroll
               for (int k = 0; k < E; k++) {
                 if (kind == 0) {
-                  const double prod = gg[q] * (double)ev[k];
+                  const double prod = gg[q] * CA::at(rv[q][c], k);
                   acc[c][k] += prod;
                 } else {
-                  acc[c][k] += (double)ev[k];
+                  acc[c][k] += CA::at(rv[q][c], k);
                 }
               }
-            }
-          }
         }
       }
     }
-    V *out = (V *)(a.partial + (uint64_t)item * a.D);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
       const int ci = lane + c * 64;
-      if (ci < NC) {
-        V v;
-        T *ev = (T *)&v;
-#pragma unroll
-        for (int k = 0; k < E; k++) ev[k] = (T)acc[c][k];
-        out[ci] = v;
-      }
+      if (ci < NC) CA::st(a.partial + (uint64_t)item * a.D + ci * E, acc[c]);
     }
   }
 }
 
-template <typename T> struct PushArgs {
+constexpr uint32_t kGroup = 16;  // hot keys: partials are pre-summed in groups of 16
+
+// Hot (key, kind) runs with more than kGroup chunks: each group leader sums
+// its group's partials in chunk order into its own slot (second level).
+template <typename T, typename A, int NCH>
+__global__ __launch_bounds__(256) void k_combine(GatherArgs<A> a) {
+  constexpr int E = V16<T>::E;
+  using CA = Chk<A, E>;
+  const int lane = threadIdx.x & 63;
+  const int NC = a.D / E;
+  const uint32_t NI = a.ioff[2 * a.U];
+  for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
+    const uint4 d = a.desc[__builtin_amdgcn_readfirstlane(item)];
+    const uint32_t j = d.z, k = d.w;
+    const uint32_t i1 = a.ioff[j + 1], nchunk = i1 - a.ioff[j];
+    if (nchunk <= kGroup || (k % kGroup) != 0) continue;
+    const uint32_t end = min(item + kGroup, i1);
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int ci = lane + c * 64;
+      if (ci >= NC) continue;
+      typename CA::R rv[kGroup];
+#pragma unroll
+      for (uint32_t q = 0; q < kGroup; q++) rv[q] = CA::ld(a.partial + (uint64_t)min(item + q, end - 1) * a.D + ci * E);
+      double sum[E];
+#pragma unroll
+      for (int kk = 0; kk < E; kk++) sum[kk] = 0.0;
+#pragma unroll
+      for (uint32_t q = 0; q < kGroup; q++)
+        if (item + q < end)
+#pragma unroll
+          for (int kk = 0; kk < E; kk++) sum[kk] += CA::at(rv[q], kk);
+      CA::st(a.partial + (uint64_t)item * a.D + ci * E, sum);
+    }
+  }
+}
+
+template <typename T, typename A> struct PushArgs {
   const int32_t *K;
   uint32_t U;
-  const uint32_t *vid_row, *seg, *item_off;
-  const T *partial;
+  const uint32_t *vid_row, *seg, *ioff;
+  const A *partial;
   T *rows;
   int32_t *local;
   int D;
@@ -455,10 +566,12 @@ template <typename T> struct PushArgs {
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
 // (word2vec_global.h:176-185) per key, fp64 math; one wave per key.
-template <typename T, int NCH>
-__global__ __launch_bounds__(256) void k_push(PushArgs<T> a) {
-  using V = typename V16<T>::V;
+template <typename T, typename A, int NCH>
+__global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
   constexpr int E = V16<T>::E;
+  using CT = Chk<T, E>;
+  using CA = Chk<A, E>;
+  constexpr int PU = 8;
   const int lane = threadIdx.x & 63;
   const int D = a.D, NC = D / E;
   for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < a.U; u += (uint64_t)gridDim.x * 4) {
@@ -467,8 +580,7 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T> a) {
     const uint32_t hc = a.seg[1 * a.U + u] - a.seg[0 * a.U + u];
     const uint32_t vc = a.seg[3 * a.U + u] - a.seg[2 * a.U + u];
     if (hc == 0 && vc == 0) continue;
-    const uint32_t ih0 = a.item_off[2 * u], ih1 = a.item_off[2 * u + 1], iv1 = a.item_off[2 * u + 2];
-    V *row = (V *)(a.rows + (uint64_t)a.vid_row[vid] * 4 * D);
+    T *row = a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
       const int ci = lane + c * 64;
@@ -476,29 +588,38 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T> a) {
       for (int half = 0; half < 2; half++) {
         const uint32_t cnt = half ? vc : hc;
         if (cnt == 0) continue;
-        const uint32_t i0 = half ? ih1 : ih0, i1 = half ? iv1 : ih1;
+        const uint32_t i0 = a.ioff[2 * u + half], i1 = a.ioff[2 * u + half + 1];
+        const uint32_t stride = (i1 - i0) > kGroup ? kGroup : 1;
         double sum[E];
 #pragma unroll
         for (int k = 0; k < E; k++) sum[k] = 0.0;
-        for (uint32_t it = i0; it < i1; it++) {
-          V pv = ((const V *)(a.partial + (uint64_t)it * D))[ci];
-          const T *pe = (const T *)&pv;
+        for (uint32_t it0 = i0; it0 < i1; it0 += PU * stride) {
+          typename CA::R pv[PU];
 #pragma unroll
-          for (int k = 0; k < E; k++) sum[k] += (double)pe[k];
+          for (int q = 0; q < PU; q++) {
+            const uint32_t it = min(it0 + q * stride, i1 - 1);
+            pv[q] = CA::ld(a.partial + (uint64_t)it * D + ci * E);
+          }
+#pragma unroll
+          for (int q = 0; q < PU; q++)
+            if (it0 + q * stride < i1)
+#pragma unroll
+              for (int k = 0; k < E; k++) sum[k] += CA::at(pv[q], k);
         }
-        V w = row[half * NC + ci], w2 = row[(2 + half) * NC + ci];
-        T *we = (T *)&w, *w2e = (T *)&w2;
+        T *w = row + half * D + ci * E, *w2 = row + (2 + half) * D + ci * E;
+        const typename CT::R wr = CT::ld(w), w2r = CT::ld(w2);
+        double wn[E], w2n[E];
 #pragma unroll
         for (int k = 0; k < E; k++) {
           const double g = sum[k] / (double)cnt;
           const double gsq = g * g;
-          const double acc2 = (double)w2e[k] + gsq;
+          const double acc2 = CT::at(w2r, k) + gsq;
           const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
-          w2e[k] = (T)acc2;
-          we[k] = (T)((double)we[k] + step);
+          w2n[k] = acc2;
+          wn[k] = CT::at(wr, k) + step;
         }
-        row[half * NC + ci] = w;
-        row[(2 + half) * NC + ci] = w2;
+        CT::st(w2, w2n);
+        CT::st(w, wn);
       }
     }
   }
@@ -591,8 +712,8 @@ struct swps_w2v {
   // device
   DevMem d_tok, d_tok_line, d_line_off, d_ran, d_exptab, d_unigram, d_starts, d_vid_row, d_cache_h, d_cache_v,
       d_local, d_K;
-  DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_pos_tok, d_pos_state, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
-      d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_tmp, d_trace, d_rows_touched;
+  DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_rec, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
+      d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_desc, d_tmp, d_trace, d_rows_touched;
   uint64_t *h_small = nullptr;  // pinned readback
   // RNG (utils/random.h:44-47, seed 2008)
   uint64_t lstate = 2008ULL;
@@ -824,19 +945,20 @@ template <typename T> int set_hv(swps_w2v *w, const double *hv) {
   return pull_all<T>(w);
 }
 
-template <int NCH, typename T> void launch_forward(const FwdArgs<T> &a, hipStream_t s) {
-  k_forward<T, NCH><<<nblk((uint64_t)a.P * 64), 256, 0, s>>>(a);
+template <int NCH, typename T, typename A> void launch_forward(const FwdArgs<T, A> &a, hipStream_t s) {
+  k_forward<T, A, NCH, 8><<<nblk((uint64_t)a.P * 64), 256, 0, s>>>(a);
 }
-template <int NCH, typename T> void launch_gather(const GatherArgs<T> &a, unsigned grid, hipStream_t s) {
-  k_gather<T, NCH><<<grid, 256, 0, s>>>(a);
+template <int NCH, typename T, typename A> void launch_gather(const GatherArgs<A> &a, unsigned grid, hipStream_t s) {
+  constexpr int UNR = sizeof(A) * V16<T>::E > 16 ? 4 : 8;
+  k_gather<T, A, NCH, UNR><<<grid, 256, 0, s>>>(a);
+  k_combine<T, A, NCH><<<grid, 256, 0, s>>>(a);
 }
-template <int NCH, typename T> void launch_push(const PushArgs<T> &a, hipStream_t s) {
-  k_push<T, NCH><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
+template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A> &a, hipStream_t s) {
+  k_push<T, A, NCH><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
 }
-
 constexpr uint32_t kChunk = 128;
 
-template <typename T> int run_batch(swps_w2v *w) {
+template <typename T, typename A> int run_batch(swps_w2v *w) {
   const uint64_t nb = w->batches.size();
   const swps_w2v::Batch &B = w->batches[w->cursor % nb];
   hipStream_t s = w->s;
@@ -880,12 +1002,6 @@ template <typename T> int run_batch(swps_w2v *w) {
   tb = w->d_tmp.bytes;
   SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, tb, w->d_ldraw.as<uint64_t>(), w->d_ldoff.as<uint64_t>(),
                                             (int)(nl + 1), s));
-  SWPS_TRY(w->d_pos_tok.ensure((nt + 1) * 4));
-  SWPS_TRY(w->d_pos_state.ensure((nt + 1) * 8));
-  k_compact<<<nblk(nt), 256, 0, s>>>(w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(), t0, nt, B.l0,
-                                     w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(), w->lstate, N,
-                                     w->d_pos_tok.as<int32_t>(), w->d_pos_state.as<uint64_t>());
-  SWPS_HIP(hipGetLastError());
   tm.end(KT_KEEP, ek, s);
   SWPS_HIP(hipMemcpyAsync(&w->h_small[0], w->d_kscan.as<int32_t>() + nt, 4, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipMemcpyAsync(&w->h_small[1], w->d_ldoff.as<uint64_t>() + nl, 8, hipMemcpyDeviceToHost, s));
@@ -893,7 +1009,6 @@ template <typename T> int run_batch(swps_w2v *w) {
   const uint64_t P = w->h_small[0] & 0xFFFFFFFFull;
   const uint64_t draws = w->h_small[1];
   const uint64_t lstate_in = w->lstate;
-  (void)lstate_in;
   w->lstate = lcg_jump(w->lstate, draws, kLcgA, kLcgC);
   if (sample_on) w->fstate = lcg_jump(w->fstate, nt, kFlcgA, kLcgC);
   w->st_batches++;
@@ -902,25 +1017,34 @@ template <typename T> int run_batch(swps_w2v *w) {
   w->st_pulled += U;
   const bool tracing = w->trace.size() < w->trace_cap;
   if (P > 0 && (U > 0 || tracing)) {
-    // ---- forward (learn_instance) ----
+    // ---- position records + gradient records (learn_instance's draws) ----
     const uint64_t HOFF = P * (uint64_t)(N + 1);
     const uint64_t M = HOFF + P * (uint64_t)(2 * W);
+    const int RS = 2 * W + N + 2;
     if (M >= (1ULL << 31)) return fail(SWPS_E_UNSUPPORTED, "minibatch too large (2^31 gradient records)");
-    SWPS_TRY(w->d_neu1.ensure(P * D * sizeof(T)));
-    SWPS_TRY(w->d_neu1e.ensure(P * D * sizeof(T)));
+    SWPS_TRY(w->d_rec.ensure(P * RS * 4));
+    SWPS_TRY(w->d_neu1.ensure(P * D * sizeof(A)));
+    SWPS_TRY(w->d_neu1e.ensure(P * D * sizeof(A)));
     SWPS_TRY(w->d_pkeys.ensure(M * 4));
     SWPS_TRY(w->d_pvals.ensure(M * 4));
     SWPS_TRY(w->d_pkeys_s.ensure(M * 4));
     SWPS_TRY(w->d_pvals_s.ensure(M * 4));
     SWPS_TRY(w->d_pg.ensure(HOFF * 4));
     if (tracing) SWPS_TRY(w->d_trace.ensure(std::max<uint64_t>(1, P * N) * 4));
-    FwdArgs<T> fa{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(),
-                  w->d_pos_tok.as<int32_t>(), w->d_pos_state.as<uint64_t>(), (int)P, w->d_cache_h.as<T>(),
-                  w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), U, w->d_unigram.as<int32_t>(),
-                  w->cfg.unigram_size, w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<T>(),
-                  w->d_neu1e.as<T>(), w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), w->d_pg.as<float>(),
-                  HOFF, tracing ? w->d_trace.as<int32_t>() : nullptr,
-                  w->d_rows_touched.as<unsigned long long>()};
+    RecArgs ra{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(), t0, nt, B.l0,
+               w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(), lstate_in, W, N, ~0ULL / (uint64_t)W,
+               w->d_unigram.as<int32_t>(), w->cfg.unigram_size, ~0ULL / w->cfg.unigram_size,
+               w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(), w->d_pkeys.as<uint32_t>(),
+               w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
+               w->d_rows_touched.as<unsigned long long>()};
+    hipEvent_t er = tm.begin(s);
+    k_records<<<nblk(nt), 256, 0, s>>>(ra);
+    SWPS_HIP(hipGetLastError());
+    tm.end(KT_KEEP, er, s);
+    // ---- forward (learn_instance) ----
+    FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
+                     w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
+                     w->d_pg.as<float>()};
     hipEvent_t ef = tm.begin(s);
     switch (w->NCH) {
       case 1: launch_forward<1>(fa, s); break;
@@ -972,17 +1096,21 @@ template <typename T> int run_batch(swps_w2v *w) {
       tm.end(KT_SORT, es, s);
       // ---- chunked segmented gradient sums ----
       const uint64_t max_items = 2ULL * U + M / kChunk + 1;
-      SWPS_TRY(w->d_partial.ensure(max_items * D * sizeof(T)));
-      GatherArgs<T> ga{w->d_ioff.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U, kChunk,
-                       w->d_neu1.as<T>(), w->d_neu1e.as<T>(), w->d_pg.as<float>(), HOFF, N + 1, 2 * W, D,
-                       w->d_partial.as<T>()};
-      const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(max_items * 64), 8192);
+      SWPS_TRY(w->d_partial.ensure(max_items * D * sizeof(A)));
+      SWPS_TRY(w->d_desc.ensure(max_items * 16));
+      k_item_desc<<<nblk(2ULL * U), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk,
+                                                 w->d_desc.as<uint4>());
+      SWPS_HIP(hipGetLastError());
+      GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
+                       w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), HOFF, N + 1, 2 * W, D,
+                       w->d_partial.as<A>()};
+      const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(max_items * 64), 16384);
       hipEvent_t eg = tm.begin(s);
       switch (w->NCH) {
-        case 1: launch_gather<1>(ga, ggrid, s); break;
-        case 2: launch_gather<2>(ga, ggrid, s); break;
-        case 3: launch_gather<3>(ga, ggrid, s); break;
-        default: launch_gather<4>(ga, ggrid, s); break;
+        case 1: launch_gather<1, T, A>(ga, ggrid, s); break;
+        case 2: launch_gather<2, T, A>(ga, ggrid, s); break;
+        case 3: launch_gather<3, T, A>(ga, ggrid, s); break;
+        default: launch_gather<4, T, A>(ga, ggrid, s); break;
       }
       SWPS_HIP(hipGetLastError());
       tm.end(KT_GATHER, eg, s);
@@ -997,9 +1125,9 @@ template <typename T> int run_batch(swps_w2v *w) {
       SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
       SWPS_HIP(hipMemsetAsync(w->d_ioff.p, 0, (2ULL * U + 1) * 4, s));
     }
-    PushArgs<T> pa{K, U, w->d_vid_row.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
-                   w->d_partial.as<T>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
-                   (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge};
+    PushArgs<T, A> pa{K, U, w->d_vid_row.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
+                      w->d_partial.as<A>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
+                      (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge};
     hipEvent_t ep = tm.begin(s);
     switch (w->NCH) {
       case 1: launch_push<1>(pa, s); break;
@@ -1166,7 +1294,14 @@ int swps_w2v_init(swps_w2v *w) {
 int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
   if (!w->inited) return fail(SWPS_E_STATE, "call swps_w2v_init first");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
-  for (uint64_t i = 0; i < count; i++) SWPS_TRY(w->f64 ? run_batch<double>(w) : run_batch<float>(w));
+  for (uint64_t i = 0; i < count; i++) {
+    if (w->f64)
+      SWPS_TRY((run_batch<double, double>(w)));
+    else if (w->cfg.fp64_intermediates)
+      SWPS_TRY((run_batch<float, double>(w)));
+    else
+      SWPS_TRY((run_batch<float, float>(w)));
+  }
   return SWPS_OK;
 }
 

@@ -23,7 +23,8 @@ def test_pull_inserts_and_push_adagrad(lib, gpu):
     h, v = rows0[:, :D], rows0[:, D:2 * D]
     gh, gv = g[:, :D], g[:, D:]
     h2 = gh * gh
-    exp_h = h + (gh * 0.7) / torch.sqrt(h2 + float(np.float32(1e-6)))
+    lr = float(np.float32(0.7))  # float initial_learning_rate promoted to double
+    exp_h = h + (gh * lr) / torch.sqrt(h2 + float(np.float32(1e-6)))
     assert torch.allclose(rows1[:, :D], exp_h, rtol=1e-12, atol=0)
     assert torch.allclose(rows1[:, 2 * D:3 * D], h2, rtol=1e-12, atol=0)
 
