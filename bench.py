@@ -87,8 +87,10 @@ def main():
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--cpu-lines", type=int, default=2500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fast", action="store_true",
-                    help="fp32 neu1/neu1e intermediates (default: fp64, the reference-parity mode)")
+    ap.add_argument("--parity", action="store_true",
+                    help="time the fp64-intermediate parity mode instead of the default fast mode")
+    ap.add_argument("--no-parity-leg", action="store_true",
+                    help="skip the extra parity-mode timing reported beside the fast-mode value")
     args = ap.parse_args()
 
     import torch
@@ -107,32 +109,46 @@ def main():
 
     ids, off = make_corpus(args.tokens, args.vocab, args.line_len, seed=8 + rank)
     keys = word_keys(sw, args.vocab)
-    t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
-                 device=local)
-    w = sw.Word2Vec(t, window=args.window, negative=args.negative, minibatch=args.minibatch, sample=args.sample,
-                    alpha=args.alpha, init="ref", profile=True, fp64_intermediates=not args.fast)
-    w.load_tokens(ids, off, keys)
-    w.init()
-    info = w.info()
 
     def barrier():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
 
+    def build(fp64_intermediates):
+        t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
+                     device=local)
+        w = sw.Word2Vec(t, window=args.window, negative=args.negative, minibatch=args.minibatch,
+                        sample=args.sample, alpha=args.alpha, init="ref", profile=False,
+                        fp64_intermediates=fp64_intermediates)
+        w.load_tokens(ids, off, keys)
+        w.init()
+        return t, w
+
+    def timed(w, steps):
+        s0 = w.stats()
+        barrier()
+        t0 = time.perf_counter()
+        w.train_batches(steps)
+        w.sync()
+        barrier()
+        dt = time.perf_counter() - t0
+        s1 = w.stats()
+        return dt, {k: s1[k] - s0[k] for k in s1 if k not in ("lstate", "fstate")}
+
+    parity_main = args.parity
+    t, w = build(fp64_intermediates=parity_main)
+    info = w.info()
     w.train_batches(args.warmup)
     w.sync()
-    s0 = w.stats()
+    dt, d = timed(w, args.steps)           # the measured region: no event timing inside
+    words = d["words"]
+    w.set_profile(True)                     # a second, profiled pass for the per-kernel roofline
     w.kernel_times(reset=True)
-    barrier()
-    t0 = time.perf_counter()
-    w.train_batches(args.steps)
-    w.sync()
-    barrier()
-    dt = time.perf_counter() - t0
-    s1 = w.stats()
+    _, dp = timed(w, args.steps)
     kt = w.kernel_times()
-    words = s1["words"] - s0["words"]
+    w.set_profile(False)
+    del w, t
     if dist is not None:
         tt = torch.tensor([dt, float(words)], dtype=torch.float64, device="cuda")
         mx = tt.clone()
@@ -143,16 +159,33 @@ def main():
         total_words = float(words)
 
     D, es = args.dim, (8 if args.dtype == "f64" else 4)
-    kept = s1["kept"] - s0["kept"]
-    ctx_rows, tgt_rows = s1["ctx_rows"] - s0["ctx_rows"], s1["tgt_rows"] - s0["tgt_rows"]
-    pulled, pushed = s1["pulled"] - s0["pulled"], s1["pushed"] - s0["pushed"]
-    # SURVEY.md §8(d) algorithmic bytes: each touched row read once (forward)
+    kept = d["kept"]
+    # SURVEY.md §8(d) algorithmic bytes of k_forward: each touched row read once
+    ctx_rows, tgt_rows = dp["ctx_rows"], dp["tgt_rows"]
     fwd_ms, fwd_n = kt["forward"]
     fwd_bytes = es * D * (ctx_rows + tgt_rows)
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
-    # whole step: rows read + gradients written (2x) + pull (16D/key) + push (40D+8 per key)
-    step_bytes = 2 * es * D * (ctx_rows + tgt_rows) + pulled * 4 * es * D + pushed * (10 * es * D + 8)
+    # whole step (§8(d) full formula): rows read + gradients written + pull 16D/key + push (40D+8)/key
+    step_bytes = (2 * es * D * (d["ctx_rows"] + d["tgt_rows"]) + d["pulled"] * 4 * es * D +
+                  d["pushed"] * (10 * es * D + 8))
     step_gbs = step_bytes / dt / 1e9
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_fast.json")
+    if os.path.exists(pmc) and not parity_main and args.dim == 300 and args.minibatch == 1000:
+        prof = json.load(open(pmc))
+        for k, v in prof["kernels"].items():
+            if k.startswith("k_forward") and "hbm_bytes_corrected" in v:
+                traffic, traffic_src = v["hbm_bytes_corrected"], "profiles/r01_pmc_fast.json (FETCH_SIZE*2 + WRITE_SIZE)"
+
+    parity_leg = None
+    if rank == 0 and world == 1 and not parity_main and not args.no_parity_leg:
+        t2, w2 = build(fp64_intermediates=True)
+        w2.train_batches(args.warmup)
+        w2.sync()
+        pdt, pd = timed(w2, args.steps)
+        parity_leg = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
+                      "mode": "fp64 neu1/neu1e + gradient partials (reference-parity mode)"}
+        del w2, t2
 
     out = {
         "metric": "SGNS trained words/sec at 1/8 GPUs; sparse push/pull HBM GB/s vs peak",
@@ -165,10 +198,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("f32 table, f32 intermediates, f64 accumulate" if args.fast else
-                  "f32 table, f64 intermediates + accumulate") if args.dtype == "f32" else "f64",
+        "dtype": ("f32 table, f64 intermediates + accumulate" if parity_main else
+                  "f32 table, f32 intermediates, f64 accumulate") if args.dtype == "f32" else "f64",
         "data": "synthetic Zipf(s=1) text8 stand-in, random-init (reference glibc-rand) params",
-        "config": {"workload": "word2vec CBOW-NS (the reference's 'SGNS' app) text8-shaped corpus %d tokens, "
+        "config": {"mode": "parity (fp64 intermediates)" if parity_main else "fast (fp32 intermediates)",
+                   "workload": "word2vec CBOW-NS (the reference's 'SGNS' app) text8-shaped corpus %d tokens, "
                                "vocab %d, dim %d, window %d, negative %d, sample %g, minibatch %d lines of %d "
                                "tokens, table in one HBM shard" % (args.tokens, info["vocab"], D, args.window,
                                                                   args.negative, args.sample, args.minibatch,
@@ -176,10 +210,12 @@ def main():
                    "global_batch": args.minibatch * world, "parallelism": "replicas" if world > 1 else "1 GPU",
                    "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"]},
         "roofline": {"bound": "hbm", "kernel": "k_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1),
                      "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS},
         "kernel_ms": {k: v[0] for k, v in kt.items()},
+        "parity_mode": parity_leg,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ids, off, keys, args, args.cpu_lines)

@@ -170,8 +170,10 @@ int swps_w2v_unigram_at(swps_w2v *w, const uint64_t *idx, uint64_t n, uint32_t *
 int swps_w2v_trace_negatives(swps_w2v *w, uint64_t cap);
 int swps_w2v_negatives(swps_w2v *w, int64_t *out, uint64_t cap, uint64_t *n);
 /* per-kernel device time (ms) and launch counts since the last reset:
- * out[2*k] = ms, out[2*k+1] = launches for k in {keep, forward, sort, gather, push, pull} */
-int swps_w2v_kernel_times(swps_w2v *w, double *out12, int32_t reset);
+ * out[2*k] = ms, out[2*k+1] = launches for k in {plan, forward, sort, gather, push, pull, records} */
+int swps_w2v_kernel_times(swps_w2v *w, double *out14, int32_t reset);
+/* switch HIP-event kernel timing on/off (syncs the stream) */
+int swps_w2v_set_profile(swps_w2v *w, int32_t on);
 /* the HIP stream all of this context's work is issued on */
 void *swps_w2v_stream(swps_w2v *w);
 

@@ -18,4 +18,6 @@ rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step bench 600 python bench.py --steps 20 --warmup 3 || exit $?
-step bench_fast 600 python bench.py --steps 20 --warmup 3 --fast --no-cpu-baseline || exit $?
+step bench_fast 600 python bench.py --steps 20 --warmup 3 --parity --no-cpu-baseline || exit $?
+step bench_b100 600 python bench.py --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline || exit $?
+step bench_b100_fast 600 python bench.py --steps 200 --warmup 10 --minibatch 100 --parity --no-cpu-baseline || exit $?

@@ -184,7 +184,7 @@ class Table:
         check(capi.lib().swps_load(self.h, path.encode(), frag_num, world, node_id))
 
 
-KT_NAMES = ["keep", "forward", "sort", "gather", "push", "pull"]
+KT_NAMES = ["plan", "forward", "sort", "gather", "push", "pull", "records"]
 
 
 class Word2Vec:
@@ -295,9 +295,12 @@ class Word2Vec:
         return out[:n.value]
 
     def kernel_times(self, reset=False):
-        o = np.zeros(12, dtype=np.float64)
+        o = np.zeros(2 * len(KT_NAMES), dtype=np.float64)
         check(capi.lib().swps_w2v_kernel_times(self.h, ptr(o), int(reset)))
         return {k: (o[2 * i], int(o[2 * i + 1])) for i, k in enumerate(KT_NAMES)}
+
+    def set_profile(self, on):
+        check(capi.lib().swps_w2v_set_profile(self.h, int(on)))
 
     def stream(self):
         return capi.lib().swps_w2v_stream(self.h)

@@ -84,6 +84,7 @@ PROTOS = {
     "swps_w2v_trace_negatives": (ctypes.c_int, [_p, _u64]),
     "swps_w2v_negatives": (ctypes.c_int, [_p, _p, _u64, ctypes.POINTER(_u64)]),
     "swps_w2v_kernel_times": (ctypes.c_int, [_p, _p, _i32]),
+    "swps_w2v_set_profile": (ctypes.c_int, [_p, _i32]),
     "swps_w2v_stream": (_p, [_p]),
     "swps_unigram_starts": (ctypes.c_int, [_p, _p, _u64, _u64, _p]),
     "swps_glibc_rand": (ctypes.c_int, [ctypes.c_uint32, _u64, _u64, _p]),

@@ -100,35 +100,56 @@ __global__ __launch_bounds__(256) void k_pull(const int32_t *__restrict__ K, uin
   }
 }
 
-// float-LCG keep flag per token (to_sample, word2vec_global.h:725-731)
-__global__ void k_keep(const int32_t *__restrict__ tok, uint64_t t0, uint64_t nt, const float *__restrict__ ran,
-                       uint64_t fstate, int sample_on, int32_t *__restrict__ kflag) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > nt) return;
-  if (i == nt) {
-    kflag[i] = 0;
-    return;
+// float-LCG keep flags for the epoch (to_sample, word2vec_global.h:725-731):
+// token t consumes the (t+1)-th draw after the epoch's start state.  Each
+// thread jumps once to the start of its run of kKeepRun tokens, then steps.
+constexpr int kKeepRun = 16;
+__global__ void k_keep(const int32_t *__restrict__ tok, uint64_t nt, const float *__restrict__ ran, uint64_t fstate,
+                       int sample_on, int32_t *__restrict__ kflag) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = r * kKeepRun;
+  if (i0 > nt) return;
+  uint64_t y = sample_on ? lcg_jump(fstate, i0, kFlcgA, kLcgC) : 0;
+  for (uint64_t i = i0; i < i0 + kKeepRun && i <= nt; i++) {
+    if (i == nt) {
+      kflag[i] = 0;
+      break;
+    }
+    int32_t keep = 1;
+    if (sample_on) {
+      y = y * kFlcgA + kLcgC;
+      keep = flcg_value(y) > ran[tok[i]];
+    }
+    kflag[i] = keep;
   }
-  int32_t keep = 1;
-  if (sample_on) {
-    uint64_t y = lcg_jump(fstate, i + 1, kFlcgA, kLcgC);
-    keep = flcg_value(y) > ran[tok[t0 + i]];
-  }
-  kflag[i] = keep;
 }
 
 // main-LCG draws per line: 1 (learn_instance's initial b) + kept*(1+negative)
-__global__ void k_line_draws(const int64_t *__restrict__ line_off, uint64_t l0, uint64_t nl, uint64_t t0,
-                             const int32_t *__restrict__ kscan, int N, uint64_t *__restrict__ ldraw) {
+__global__ void k_line_draws(const int64_t *__restrict__ line_off, uint64_t nl, const int32_t *__restrict__ kscan,
+                             int N, uint64_t *__restrict__ ldraw) {
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j > nl) return;
   if (j == nl) {
     ldraw[j] = 0;
     return;
   }
-  uint64_t a = (uint64_t)line_off[l0 + j] - t0, b = (uint64_t)line_off[l0 + j + 1] - t0;
-  uint64_t kept = (uint64_t)(kscan[b] - kscan[a]);
+  uint64_t kept = (uint64_t)(kscan[line_off[j + 1]] - kscan[line_off[j]]);
   ldraw[j] = 1 + kept * (uint64_t)(N + 1);
+}
+
+// kept-count prefix at each batch boundary (token offsets given)
+__global__ void k_bounds(const int32_t *__restrict__ kscan, const int64_t *__restrict__ btok, uint64_t n,
+                         int32_t *__restrict__ out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = kscan[btok[i]];
+}
+
+// kept token indices of a batch in order
+__global__ void k_positions(const int32_t *__restrict__ kscan, uint64_t t0, uint64_t nt, int32_t *__restrict__ pos_tok) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nt) return;
+  const int32_t a = kscan[t0 + i];
+  if (kscan[t0 + i + 1] != a) pos_tok[a - kscan[t0]] = (int32_t)(t0 + i);
 }
 
 // x mod d for a fixed divisor d < 2^63 with the precomputed m = floor((2^64-1)/d):
@@ -144,10 +165,11 @@ __device__ __forceinline__ uint64_t fast_mod(uint64_t x, uint64_t d, uint64_t m)
 struct RecArgs {
   const int32_t *tok, *tok_line;
   const int64_t *line_off;
-  uint64_t t0, nt, l0;
-  const int32_t *kscan;
-  const uint64_t *ldoff;
-  uint64_t lstate;
+  const int32_t *pos_tok;
+  uint32_t P;
+  const int32_t *kscan;   // epoch-wide
+  const uint64_t *ldoff;  // epoch-wide
+  uint64_t lstate;        // main LCG state at the epoch start
   int W, N;
   uint64_t mW;  // floor((2^64-1)/W)
   const int32_t *unigram;
@@ -155,75 +177,72 @@ struct RecArgs {
   const int32_t *local;
   uint32_t U;
   int32_t *rec;     // [P][RS]: word, ctx vid x 2W (-1 = none), target vid x (N+1) (-1 = skipped)
-  uint32_t *pkeys, *pvals;
+  uint32_t *pkeys, *pvals;  // slot-major: h record (p,d) at d*P+p; v record (p,j) at (N+1)*P + j*P+p
   int32_t *trace;
   unsigned long long *rows_touched;
 };
 
-// One thread per token of the batch; for every kept position (to_sample true)
-// replays learn_instance's LCG draws (word2vec_global.h:669,686-691) from the
-// jumped state: b, the negatives from the unigram table, the context slots
-// a = b..2W-b (a != W) inside the line; writes the position record and the
-// (local key, record index) gradient records (key U = not in the batch's
-// pulled key set: dropped, as the reference's pull reset drops them).
+// One thread per kept position: replays learn_instance's LCG draws
+// (word2vec_global.h:669,686-691) from the jumped state — b, the negatives
+// from the unigram table, the context slots a = b..2W-b (a != W) inside the
+// line — and writes the position record plus the (local key, record index)
+// gradient records (key U = not in the batch's pulled key set: dropped, as the
+// reference's pull reset drops them).
 __global__ __launch_bounds__(256) void k_records(RecArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int nctx = 0, ntgt = 0;
-  if (i < a.nt) {
-    const int32_t p = a.kscan[i];
-    if (a.kscan[i + 1] != p) {
-      const uint64_t P = (uint64_t)a.kscan[a.nt];
-      const int W = a.W, N = a.N, RS = 2 * W + N + 2;
-      const uint64_t HOFF = P * (uint64_t)(N + 1);
-      const uint64_t t = a.t0 + i;
-      const int32_t l = a.tok_line[t];
-      const int64_t ls = a.line_off[l];
-      const int n = (int)(a.line_off[l + 1] - ls), pos = (int)((int64_t)t - ls);
-      const int32_t word = a.tok[t];
-      const uint64_t rank = (uint64_t)(p - a.kscan[(uint64_t)ls - a.t0]);
-      uint64_t x = lcg_jump(a.lstate, a.ldoff[l - a.l0] + 1 + rank * (uint64_t)(N + 1), kLcgA, kLcgC);
-      x = x * kLcgA + kLcgC;
-      const int b = (int)fast_mod(x, (uint64_t)W, a.mW);
-      int32_t *r = a.rec + (uint64_t)p * RS;
-      r[0] = word;
-      for (int j = 0; j < 2 * W; j++) {
-        int32_t cv = -1;
-        if (j < 2 * (W - b)) {
-          int aa = b + j;
-          if (aa >= W) aa++;
-          const int c = pos - W + aa;
-          if (c >= 0 && c < n) cv = a.tok[ls + c];
-        }
-        r[1 + j] = cv;
-        uint32_t key = a.U;
-        if (cv >= 0) {
-          nctx++;
-          const int32_t u = a.local[cv];
-          if (u >= 0) key = (uint32_t)u;
-        }
-        const uint64_t k = HOFF + (uint64_t)p * 2 * W + j;
-        a.pkeys[k] = key;
-        a.pvals[k] = (uint32_t)k;
+  if (p < a.P) {
+    const uint64_t P = a.P;
+    const int W = a.W, N = a.N, RS = 2 * W + N + 2;
+    const uint64_t HOFF = P * (uint64_t)(N + 1);
+    const uint64_t t = (uint64_t)a.pos_tok[p];
+    const int32_t l = a.tok_line[t];
+    const int64_t ls = a.line_off[l];
+    const int n = (int)(a.line_off[l + 1] - ls), pos = (int)((int64_t)t - ls);
+    const int32_t word = a.tok[t];
+    const uint64_t rank = (uint64_t)(a.kscan[t] - a.kscan[ls]);
+    uint64_t x = lcg_jump(a.lstate, a.ldoff[l] + 1 + rank * (uint64_t)(N + 1), kLcgA, kLcgC);
+    x = x * kLcgA + kLcgC;
+    const int b = (int)fast_mod(x, (uint64_t)W, a.mW);
+    int32_t *r = a.rec + p * RS;
+    r[0] = word;
+    for (int j = 0; j < 2 * W; j++) {
+      int32_t cv = -1;
+      if (j < 2 * (W - b)) {
+        int aa = b + j;
+        if (aa >= W) aa++;
+        const int c = pos - W + aa;
+        if (c >= 0 && c < n) cv = a.tok[ls + c];
       }
-      for (int d = 0; d <= N; d++) {
-        int32_t tv = word;
-        if (d > 0) {
-          x = x * kLcgA + kLcgC;
-          tv = a.unigram[fast_mod(x >> 16, a.uni_size, a.mT)];
-          if (a.trace) a.trace[(uint64_t)p * N + d - 1] = tv;
-          if (tv == word) tv = -1;
-        }
-        r[1 + 2 * W + d] = tv;
-        uint32_t key = a.U;
-        if (tv >= 0) {
-          ntgt++;
-          const int32_t u = a.local[tv];
-          if (u >= 0) key = (uint32_t)u;
-        }
-        const uint64_t k = (uint64_t)p * (N + 1) + d;
-        a.pkeys[k] = key;
-        a.pvals[k] = (uint32_t)k;
+      r[1 + j] = cv;
+      uint32_t key = a.U;
+      if (cv >= 0) {
+        nctx++;
+        const int32_t u = a.local[cv];
+        if (u >= 0) key = (uint32_t)u;
       }
+      const uint64_t k = HOFF + (uint64_t)j * P + p;
+      a.pkeys[k] = key;
+      a.pvals[k] = (uint32_t)k;
+    }
+    for (int d = 0; d <= N; d++) {
+      int32_t tv = word;
+      if (d > 0) {
+        x = x * kLcgA + kLcgC;
+        tv = a.unigram[fast_mod(x >> 16, a.uni_size, a.mT)];
+        if (a.trace) a.trace[p * N + d - 1] = tv;
+        if (tv == word) tv = -1;
+      }
+      r[1 + 2 * W + d] = tv;
+      uint32_t key = a.U;
+      if (tv >= 0) {
+        ntgt++;
+        const int32_t u = a.local[tv];
+        if (u >= 0) key = (uint32_t)u;
+      }
+      const uint64_t k = (uint64_t)d * P + p;
+      a.pkeys[k] = key;
+      a.pvals[k] = (uint32_t)k;
     }
   }
   // rows the forward will read (roofline accounting), one atomic per wave
@@ -239,39 +258,43 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
   }
 }
 
-// E consecutive elements of type X as one register chunk, converted to / from
-// fp64 (16 B of the table type per lane; 32 B when fp32 rows carry fp64
-// intermediates).
+// Chunk ci = elements [E*ci, E*ci+E) of a D-element row, held by one lane as
+// one register chunk and converted to / from fp64.  16 B of the table type per
+// lane; when fp32 rows carry fp64 intermediates (E = 4 doubles) the row is
+// stored as two planes [D/2 | D/2] of double2 so every load/store instruction
+// of a wave is contiguous.
 template <typename X, int E> struct Chk;
 template <> struct Chk<float, 4> {
   using R = float4;
-  static __device__ __forceinline__ R ld(const float *p) { return *(const float4 *)p; }
+  static __device__ __forceinline__ R ld(const float *row, int ci, int) { return ((const float4 *)row)[ci]; }
   static __device__ __forceinline__ double at(const R &r, int k) { return (double)((const float *)&r)[k]; }
-  static __device__ __forceinline__ void st(float *p, const double (&v)[4]) {
-    *(float4 *)p = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+  static __device__ __forceinline__ void st(float *row, int ci, int, const double (&v)[4]) {
+    ((float4 *)row)[ci] = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
   }
 };
 template <> struct Chk<double, 4> {
   struct R {
     double2 a, b;
   };
-  static __device__ __forceinline__ R ld(const double *p) {
+  static __device__ __forceinline__ R ld(const double *row, int ci, int D) {
     R r;
-    r.a = ((const double2 *)p)[0];
-    r.b = ((const double2 *)p)[1];
+    r.a = ((const double2 *)row)[ci];
+    r.b = ((const double2 *)(row + D / 2))[ci];
     return r;
   }
   static __device__ __forceinline__ double at(const R &r, int k) { return ((const double *)&r)[k]; }
-  static __device__ __forceinline__ void st(double *p, const double (&v)[4]) {
-    ((double2 *)p)[0] = make_double2(v[0], v[1]);
-    ((double2 *)p)[1] = make_double2(v[2], v[3]);
+  static __device__ __forceinline__ void st(double *row, int ci, int D, const double (&v)[4]) {
+    ((double2 *)row)[ci] = make_double2(v[0], v[1]);
+    ((double2 *)(row + D / 2))[ci] = make_double2(v[2], v[3]);
   }
 };
 template <> struct Chk<double, 2> {
   using R = double2;
-  static __device__ __forceinline__ R ld(const double *p) { return *(const double2 *)p; }
+  static __device__ __forceinline__ R ld(const double *row, int ci, int) { return ((const double2 *)row)[ci]; }
   static __device__ __forceinline__ double at(const R &r, int k) { return ((const double *)&r)[k]; }
-  static __device__ __forceinline__ void st(double *p, const double (&v)[2]) { *(double2 *)p = make_double2(v[0], v[1]); }
+  static __device__ __forceinline__ void st(double *row, int ci, int, const double (&v)[2]) {
+    ((double2 *)row)[ci] = make_double2(v[0], v[1]);
+  }
 };
 
 template <typename T, typename A> struct FwdArgs {
@@ -323,7 +346,7 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
           const int ci = lane + c * 64;
-          if (ci < NC) rows[q][c] = CT::ld(src + ci * E);
+          if (ci < NC) rows[q][c] = CT::ld(src, ci, D);
         }
       }
     }
@@ -375,11 +398,11 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
   for (int c = 0; c < NCH; c++) {
     const int ci = lane + c * 64;
     if (ci < NC) {
-      CA::st(a.neu1 + (uint64_t)p * D + ci * E, acc[c]);
-      CA::st(a.neu1e + (uint64_t)p * D + ci * E, ne[c]);
+      CA::st(a.neu1 + (uint64_t)p * D, ci, D, acc[c]);
+      CA::st(a.neu1e + (uint64_t)p * D, ci, D, ne[c]);
     }
   }
-  if (lane <= N) a.pg[(uint64_t)p * (N + 1) + lane] = gk;
+  if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
 }
 
 // Segment bounds of each (local key, kind) run in the sorted records:
@@ -430,7 +453,8 @@ template <typename A> struct GatherArgs {
   const A *neu1, *neu1e;
   const float *pg;
   uint64_t HOFF;
-  int N1, W2, D;
+  uint32_t P;
+  int D;
   A *partial;
 };
 
@@ -451,22 +475,23 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
     const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
     uint32_t p0 = 0, p1 = 0;
     float g0 = 1.f, g1 = 1.f;
+    // records are slot-major: index = slot*P + p (v records after HOFF)
     if (lane < (int)n) {
       const uint32_t pi = a.vals[s + lane];
       if (kind == 0) {
-        p0 = pi / (uint32_t)a.N1;
+        p0 = pi % a.P;
         g0 = a.pg[pi];
       } else {
-        p0 = (uint32_t)((pi - a.HOFF) / (uint32_t)a.W2);
+        p0 = (uint32_t)((pi - a.HOFF) % a.P);
       }
     }
     if (lane + 64 < (int)n) {
       const uint32_t pi = a.vals[s + 64 + lane];
       if (kind == 0) {
-        p1 = pi / (uint32_t)a.N1;
+        p1 = pi % a.P;
         g1 = a.pg[pi];
       } else {
-        p1 = (uint32_t)((pi - a.HOFF) / (uint32_t)a.W2);
+        p1 = (uint32_t)((pi - a.HOFF) % a.P);
       }
     }
     const A *base = kind == 0 ? a.neu1 : a.neu1e;
@@ -487,7 +512,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
           const int ci = lane + c * 64;
-          if (ci < NC) rv[q][c] = CA::ld(src + ci * E);
+          if (ci < NC) rv[q][c] = CA::ld(src, ci, a.D);
         }
       }
 #pragma unroll
@@ -511,7 +536,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
       const int ci = lane + c * 64;
-      if (ci < NC) CA::st(a.partial + (uint64_t)item * a.D + ci * E, acc[c]);
+      if (ci < NC) CA::st(a.partial + (uint64_t)item * a.D, ci, a.D, acc[c]);
     }
   }
 }
@@ -539,7 +564,7 @@ __global__ __launch_bounds__(256) void k_combine(GatherArgs<A> a) {
       if (ci >= NC) continue;
       typename CA::R rv[kGroup];
 #pragma unroll
-      for (uint32_t q = 0; q < kGroup; q++) rv[q] = CA::ld(a.partial + (uint64_t)min(item + q, end - 1) * a.D + ci * E);
+      for (uint32_t q = 0; q < kGroup; q++) rv[q] = CA::ld(a.partial + (uint64_t)min(item + q, end - 1) * a.D, ci, a.D);
       double sum[E];
 #pragma unroll
       for (int kk = 0; kk < E; kk++) sum[kk] = 0.0;
@@ -548,7 +573,7 @@ __global__ __launch_bounds__(256) void k_combine(GatherArgs<A> a) {
         if (item + q < end)
 #pragma unroll
           for (int kk = 0; kk < E; kk++) sum[kk] += CA::at(rv[q], kk);
-      CA::st(a.partial + (uint64_t)item * a.D + ci * E, sum);
+      CA::st(a.partial + (uint64_t)item * a.D, ci, a.D, sum);
     }
   }
 }
@@ -598,7 +623,7 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
 #pragma unroll
           for (int q = 0; q < PU; q++) {
             const uint32_t it = min(it0 + q * stride, i1 - 1);
-            pv[q] = CA::ld(a.partial + (uint64_t)it * D + ci * E);
+            pv[q] = CA::ld(a.partial + (uint64_t)it * D, ci, D);
           }
 #pragma unroll
           for (int q = 0; q < PU; q++)
@@ -606,8 +631,8 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
 #pragma unroll
               for (int k = 0; k < E; k++) sum[k] += CA::at(pv[q], k);
         }
-        T *w = row + half * D + ci * E, *w2 = row + (2 + half) * D + ci * E;
-        const typename CT::R wr = CT::ld(w), w2r = CT::ld(w2);
+        T *w = row + half * D, *w2 = row + (2 + half) * D;
+        const typename CT::R wr = CT::ld(w, ci, D), w2r = CT::ld(w2, ci, D);
         double wn[E], w2n[E];
 #pragma unroll
         for (int k = 0; k < E; k++) {
@@ -618,8 +643,8 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
           w2n[k] = acc2;
           wn[k] = CT::at(wr, k) + step;
         }
-        CT::st(w2, w2n);
-        CT::st(w, wn);
+        CT::st(w2, ci, D, w2n);
+        CT::st(w, ci, D, wn);
       }
     }
   }
@@ -633,7 +658,7 @@ __global__ void k_trace_copy(const int32_t *__restrict__ src, uint64_t n, int32_
 inline unsigned nblk(uint64_t threads, unsigned bs = 256) { return (unsigned)std::max<uint64_t>(1, (threads + bs - 1) / bs); }
 
 // ---- per-kernel HIP-event timing ----------------------------------------
-enum { KT_KEEP = 0, KT_FWD, KT_SORT, KT_GATHER, KT_PUSH, KT_PULL, KT_N };
+enum { KT_KEEP = 0, KT_FWD, KT_SORT, KT_GATHER, KT_PUSH, KT_PULL, KT_REC, KT_N };
 
 struct Timer {
   bool on = false;
@@ -712,12 +737,15 @@ struct swps_w2v {
   // device
   DevMem d_tok, d_tok_line, d_line_off, d_ran, d_exptab, d_unigram, d_starts, d_vid_row, d_cache_h, d_cache_v,
       d_local, d_K;
-  DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_rec, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
+  DevMem d_btok, d_bounds;
+  DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_pos_tok, d_rec, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
       d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_desc, d_tmp, d_trace, d_rows_touched;
   uint64_t *h_small = nullptr;  // pinned readback
   // RNG (utils/random.h:44-47, seed 2008)
   uint64_t lstate = 2008ULL;
   uint64_t fstate = std::numeric_limits<unsigned long>::max() / 2;
+  uint64_t lstate_epoch = 0;        // main LCG state at the current epoch's start
+  std::vector<uint32_t> plan_P;     // kept positions per batch of the current epoch
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
   // negative trace
@@ -890,6 +918,10 @@ int upload_corpus(swps_w2v *w) {
   SWPS_TRY(upload(w->d_tok_line, w->tok_line, s));
   SWPS_TRY(upload(w->d_line_off, w->line_off, s));
   SWPS_TRY(upload(w->d_K, w->allK, s));
+  std::vector<int64_t> btok;  // token offset of every batch start + the epoch end
+  for (auto &b : w->batches) btok.push_back(w->line_off[b.l0]);
+  btok.push_back(w->line_off[w->batches.back().l1]);
+  SWPS_TRY(upload(w->d_btok, btok, s));
   // subsampling thresholds (word2vec_global.h:728-729), computed on the host
   std::vector<float> ran(V);
   for (uint64_t i = 0; i < V; i++) {
@@ -958,17 +990,70 @@ template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A>
 }
 constexpr uint32_t kChunk = 128;
 
+// Subsample masks and main-LCG offsets for a whole epoch.  They depend only on
+// the two RNG streams (the float LCG advances one draw per processed token,
+// the main LCG 1 + kept*(1+negative) draws per line), never on the
+// parameters, so one pass per epoch replaces per-batch host syncs.
+int plan_epoch(swps_w2v *w) {
+  hipStream_t s = w->s;
+  const uint64_t nb = w->batches.size();
+  const uint64_t L = w->batches[nb - 1].l1;             // lines processed per epoch
+  const uint64_t T = (uint64_t)w->line_off[L];          // tokens processed per epoch
+  const bool sample_on = w->cfg.sample >= 0;
+  SWPS_TRY(w->d_kflag.ensure((T + 1) * 4));
+  SWPS_TRY(w->d_kscan.ensure((T + 1) * 4));
+  SWPS_TRY(w->d_ldraw.ensure((L + 1) * 8));
+  SWPS_TRY(w->d_ldoff.ensure((L + 1) * 8));
+  hipEvent_t ek = w->timer.begin(s);
+  k_keep<<<nblk((T + kKeepRun) / kKeepRun), 256, 0, s>>>(w->d_tok.as<int32_t>(), T, w->d_ran.as<float>(), w->fstate, sample_on,
+                                     w->d_kflag.as<int32_t>());
+  SWPS_HIP(hipGetLastError());
+  size_t tb1 = 0, tb2 = 0;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, w->d_kflag.as<int32_t>(), w->d_kscan.as<int32_t>(),
+                                            (int)(T + 1), s));
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, w->d_ldraw.as<uint64_t>(), w->d_ldoff.as<uint64_t>(),
+                                            (int)(L + 1), s));
+  SWPS_TRY(w->d_tmp.ensure(std::max(tb1, tb2)));
+  size_t tb = w->d_tmp.bytes;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, tb, w->d_kflag.as<int32_t>(), w->d_kscan.as<int32_t>(),
+                                            (int)(T + 1), s));
+  k_line_draws<<<nblk(L + 1), 256, 0, s>>>(w->d_line_off.as<int64_t>(), L, w->d_kscan.as<int32_t>(), w->N,
+                                           w->d_ldraw.as<uint64_t>());
+  SWPS_HIP(hipGetLastError());
+  tb = w->d_tmp.bytes;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, tb, w->d_ldraw.as<uint64_t>(), w->d_ldoff.as<uint64_t>(),
+                                            (int)(L + 1), s));
+  w->timer.end(KT_KEEP, ek, s);
+  // per-batch kept counts: kscan at every batch's token boundary
+  SWPS_TRY(w->d_bounds.ensure((nb + 1) * 4));
+  k_bounds<<<nblk(nb + 1), 256, 0, s>>>(w->d_kscan.as<int32_t>(), w->d_btok.as<int64_t>(), nb + 1,
+                                        w->d_bounds.as<int32_t>());
+  SWPS_HIP(hipGetLastError());
+  std::vector<int32_t> ks(nb + 1);
+  SWPS_HIP(hipMemcpyAsync(ks.data(), w->d_bounds.p, (nb + 1) * 4, hipMemcpyDeviceToHost, s));
+  uint64_t draws = 0;
+  SWPS_HIP(hipMemcpyAsync(&draws, w->d_ldoff.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  w->plan_P.resize(nb);
+  for (uint64_t i = 0; i < nb; i++) w->plan_P[i] = (uint32_t)(ks[i + 1] - ks[i]);
+  w->lstate_epoch = w->lstate;
+  w->lstate = lcg_jump(w->lstate, draws, kLcgA, kLcgC);
+  if (sample_on) w->fstate = lcg_jump(w->fstate, T, kFlcgA, kLcgC);
+  return SWPS_OK;
+}
+
 template <typename T, typename A> int run_batch(swps_w2v *w) {
   const uint64_t nb = w->batches.size();
-  const swps_w2v::Batch &B = w->batches[w->cursor % nb];
+  if (w->cursor % nb == 0) SWPS_TRY(plan_epoch(w));
+  const uint64_t bi = w->cursor % nb;
+  const swps_w2v::Batch &B = w->batches[bi];
   hipStream_t s = w->s;
   Timer &tm = w->timer;
   const int D = w->D, W = w->W, N = w->N;
   const uint64_t t0 = (uint64_t)w->line_off[B.l0], t1 = (uint64_t)w->line_off[B.l1];
-  const uint64_t nt = t1 - t0, nl = B.l1 - B.l0;
+  const uint64_t nt = t1 - t0;
   const uint32_t U = B.U;
   const int32_t *K = w->d_K.as<int32_t>() + B.kofs;
-  const bool sample_on = w->cfg.sample >= 0;
   // ---- pull (global_pull_access.h:28-107 + server.h:129-154) ----
   if (U) {
     hipEvent_t e = tm.begin(s);
@@ -978,39 +1063,7 @@ template <typename T, typename A> int run_batch(swps_w2v *w) {
     SWPS_HIP(hipGetLastError());
     tm.end(KT_PULL, e, s);
   }
-  // ---- subsample mask + LCG offsets ----
-  SWPS_TRY(w->d_kflag.ensure((nt + 1) * 4));
-  SWPS_TRY(w->d_kscan.ensure((nt + 1) * 4));
-  SWPS_TRY(w->d_ldraw.ensure((nl + 1) * 8));
-  SWPS_TRY(w->d_ldoff.ensure((nl + 1) * 8));
-  hipEvent_t ek = tm.begin(s);
-  k_keep<<<nblk(nt + 1), 256, 0, s>>>(w->d_tok.as<int32_t>(), t0, nt, w->d_ran.as<float>(), w->fstate, sample_on,
-                                      w->d_kflag.as<int32_t>());
-  SWPS_HIP(hipGetLastError());
-  size_t tb1 = 0, tb2 = 0;
-  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, w->d_kflag.as<int32_t>(), w->d_kscan.as<int32_t>(),
-                                            (int)(nt + 1), s));
-  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, w->d_ldraw.as<uint64_t>(), w->d_ldoff.as<uint64_t>(),
-                                            (int)(nl + 1), s));
-  SWPS_TRY(w->d_tmp.ensure(std::max(tb1, tb2)));
-  size_t tb = w->d_tmp.bytes;
-  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, tb, w->d_kflag.as<int32_t>(), w->d_kscan.as<int32_t>(),
-                                            (int)(nt + 1), s));
-  k_line_draws<<<nblk(nl + 1), 256, 0, s>>>(w->d_line_off.as<int64_t>(), B.l0, nl, t0, w->d_kscan.as<int32_t>(), N,
-                                            w->d_ldraw.as<uint64_t>());
-  SWPS_HIP(hipGetLastError());
-  tb = w->d_tmp.bytes;
-  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, tb, w->d_ldraw.as<uint64_t>(), w->d_ldoff.as<uint64_t>(),
-                                            (int)(nl + 1), s));
-  tm.end(KT_KEEP, ek, s);
-  SWPS_HIP(hipMemcpyAsync(&w->h_small[0], w->d_kscan.as<int32_t>() + nt, 4, hipMemcpyDeviceToHost, s));
-  SWPS_HIP(hipMemcpyAsync(&w->h_small[1], w->d_ldoff.as<uint64_t>() + nl, 8, hipMemcpyDeviceToHost, s));
-  SWPS_HIP(hipStreamSynchronize(s));
-  const uint64_t P = w->h_small[0] & 0xFFFFFFFFull;
-  const uint64_t draws = w->h_small[1];
-  const uint64_t lstate_in = w->lstate;
-  w->lstate = lcg_jump(w->lstate, draws, kLcgA, kLcgC);
-  if (sample_on) w->fstate = lcg_jump(w->fstate, nt, kFlcgA, kLcgC);
+  const uint64_t P = w->plan_P[bi];
   w->st_batches++;
   w->st_kept += P;
   w->st_words += nt;
@@ -1022,6 +1075,7 @@ template <typename T, typename A> int run_batch(swps_w2v *w) {
     const uint64_t M = HOFF + P * (uint64_t)(2 * W);
     const int RS = 2 * W + N + 2;
     if (M >= (1ULL << 31)) return fail(SWPS_E_UNSUPPORTED, "minibatch too large (2^31 gradient records)");
+    SWPS_TRY(w->d_pos_tok.ensure(P * 4));
     SWPS_TRY(w->d_rec.ensure(P * RS * 4));
     SWPS_TRY(w->d_neu1.ensure(P * D * sizeof(A)));
     SWPS_TRY(w->d_neu1e.ensure(P * D * sizeof(A)));
@@ -1031,16 +1085,17 @@ template <typename T, typename A> int run_batch(swps_w2v *w) {
     SWPS_TRY(w->d_pvals_s.ensure(M * 4));
     SWPS_TRY(w->d_pg.ensure(HOFF * 4));
     if (tracing) SWPS_TRY(w->d_trace.ensure(std::max<uint64_t>(1, P * N) * 4));
-    RecArgs ra{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(), t0, nt, B.l0,
-               w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(), lstate_in, W, N, ~0ULL / (uint64_t)W,
-               w->d_unigram.as<int32_t>(), w->cfg.unigram_size, ~0ULL / w->cfg.unigram_size,
-               w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(), w->d_pkeys.as<uint32_t>(),
-               w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
+    RecArgs ra{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(),
+               w->d_pos_tok.as<int32_t>(), (uint32_t)P, w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(),
+               w->lstate_epoch, W, N, ~0ULL / (uint64_t)W, w->d_unigram.as<int32_t>(), w->cfg.unigram_size,
+               ~0ULL / w->cfg.unigram_size, w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(),
+               w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
                w->d_rows_touched.as<unsigned long long>()};
     hipEvent_t er = tm.begin(s);
-    k_records<<<nblk(nt), 256, 0, s>>>(ra);
+    k_positions<<<nblk(nt), 256, 0, s>>>(w->d_kscan.as<int32_t>(), t0, nt, w->d_pos_tok.as<int32_t>());
+    k_records<<<nblk(P), 256, 0, s>>>(ra);
     SWPS_HIP(hipGetLastError());
-    tm.end(KT_KEEP, er, s);
+    tm.end(KT_REC, er, s);
     // ---- forward (learn_instance) ----
     FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
                      w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
@@ -1102,7 +1157,7 @@ template <typename T, typename A> int run_batch(swps_w2v *w) {
                                                  w->d_desc.as<uint4>());
       SWPS_HIP(hipGetLastError());
       GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
-                       w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), HOFF, N + 1, 2 * W, D,
+                       w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), HOFF, (uint32_t)P, D,
                        w->d_partial.as<A>()};
       const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(max_items * 64), 16384);
       hipEvent_t eg = tm.begin(s);
@@ -1375,6 +1430,12 @@ int swps_w2v_trace_negatives(swps_w2v *w, uint64_t cap) {
 int swps_w2v_negatives(swps_w2v *w, int64_t *out, uint64_t cap, uint64_t *n) {
   *n = std::min<uint64_t>(cap, w->trace.size());
   std::copy(w->trace.begin(), w->trace.begin() + *n, out);
+  return SWPS_OK;
+}
+
+int swps_w2v_set_profile(swps_w2v *w, int32_t on) {
+  SWPS_TRY(swps_w2v_sync(w));
+  w->timer.on = on != 0;
   return SWPS_OK;
 }
 
