@@ -9,10 +9,11 @@ gradients with AdaGrad — all on the GPU through libswps.so.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-N > 1: every rank trains its own corpus shard of the same size (the
-reference's per-rank local data) against its own full-vocab shard: weak
-scaling, replicas (no cross-GPU key sharding yet — see DESIGN.md §Multi-GPU).
-Rank 0 prints one JSON line.
+N > 1: every rank trains its own corpus of the same size (the reference's
+per-rank local data) and serves the keys BasicHashFrag assigns to it; each
+minibatch pulls rows from and pushes mean gradients to the owning GPUs with
+RCCL all-to-all-v (swiftmpi_amd/dist.py).  Weak scaling.  Rank 0 prints one
+JSON line.
 """
 import argparse
 import json
@@ -85,6 +86,8 @@ def main():
     ap.add_argument("--vocab", type=int, default=253854)
     ap.add_argument("--line-len", type=int, default=1000)
     ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--frag-num", type=int, default=1000)
+    ap.add_argument("--sharded", action="store_true", help="use the key-sharded multi-GPU path even at N=1")
     ap.add_argument("--cpu-lines", type=int, default=2500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity", action="store_true",
@@ -100,10 +103,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    ngpu = torch.cuda.device_count()
+    sharded = world > 1 or args.sharded
+    backend = None
+    if sharded:
         import torch.distributed as dist
+        local = local % max(ngpu, 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if "MASTER_ADDR" not in os.environ:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
+        if ngpu >= world:  # one GPU per rank: RCCL over xGMI
+            backend = "nccl"
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:               # functional check with ranks sharing a GPU
+            backend = "gloo"
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(local)
 
@@ -116,11 +130,15 @@ def main():
             dist.barrier()
 
     def build(fp64_intermediates):
+        kw = dict(window=args.window, negative=args.negative, minibatch=args.minibatch, sample=args.sample,
+                  alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates)
         t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
-                     device=local)
-        w = sw.Word2Vec(t, window=args.window, negative=args.negative, minibatch=args.minibatch,
-                        sample=args.sample, alpha=args.alpha, init="ref", profile=False,
-                        fp64_intermediates=fp64_intermediates)
+                     device=local, init="hash", seed=1)
+        if sharded:  # key-sharded over the ranks (BasicHashFrag), RCCL all-to-all per minibatch
+            from swiftmpi_amd.dist import ShardedWord2Vec
+            w = ShardedWord2Vec(t, frag_num=args.frag_num, **kw)
+        else:
+            w = sw.Word2Vec(t, init="ref", **kw)
         w.load_tokens(ids, off, keys)
         w.init()
         return t, w
@@ -207,7 +225,10 @@ def main():
                                "tokens, table in one HBM shard" % (args.tokens, info["vocab"], D, args.window,
                                                                   args.negative, args.sample, args.minibatch,
                                                                   args.line_len),
-                   "global_batch": args.minibatch * world, "parallelism": "replicas" if world > 1 else "1 GPU",
+                   "global_batch": args.minibatch * world,
+                   "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num %d), %s all-to-all-v"
+                                   % (world, args.frag_num, "RCCL" if backend == "nccl" else "gloo"))
+                   if sharded else "1 GPU, one HBM shard",
                    "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"]},
         "roofline": {"bound": "hbm", "kernel": "k_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": traffic,

@@ -177,6 +177,30 @@ int swps_w2v_set_profile(swps_w2v *w, int32_t on);
 /* the HIP stream all of this context's work is issued on */
 void *swps_w2v_stream(swps_w2v *w);
 
+/* ---- sharded mode (several GPUs; the caller moves the payloads) ---------
+ * Every rank = a worker with its own corpus + a server for the keys whose
+ * BasicHashFrag node is rank+1 (hashfrag.h:33-56).  Per batch:
+ *   swps_w2v_request     keys of the next batch grouped by owner rank (u64)
+ *   -> all-to-all ->     swps_w2v_serve_pull (owner: [n][h|v] pull values)
+ *   -> all-to-all ->     swps_w2v_step       (install values, learn, emit
+ *                                             mean gradients [U][h|v] fp64)
+ *   -> all-to-all ->     swps_w2v_serve_push (owner: AdaGrad per source rank,
+ *                                             sources in rank order)
+ * Initial full pull: swps_w2v_request(init=1) -> serve_pull(insert=1) ->
+ * swps_w2v_install_init.  Tables must use SWPS_INIT_HASH (the reference's
+ * rand() order would depend on message arrival). */
+int swps_w2v_shard(swps_w2v *w, int32_t rank, int32_t world, int32_t frag_num);
+/* per-batch key counts per owner: out[nb][world] */
+int swps_w2v_batch_counts(swps_w2v *w, uint64_t *out, uint64_t cap, uint64_t *nb);
+/* counts[world] (host); keys into d_keys (device, may be NULL to query n) */
+int swps_w2v_request(swps_w2v *w, int32_t init, uint64_t *counts, uint64_t *d_keys, uint64_t *n);
+/* keys from all sources concatenated in rank order, src_counts[world] (host) */
+int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src_counts, int32_t insert,
+                        void *d_vals);
+int swps_w2v_install_init(swps_w2v *w, const void *d_vals);
+int swps_w2v_step(swps_w2v *w, const void *d_vals, double *d_grads);
+int swps_w2v_serve_push(swps_w2v *w, const double *d_grads, const uint64_t *src_counts);
+
 /* ---- host-only helpers (no device needed; used by the CPU test-suite) ---- */
 /* run-length form of gen_unigram_table (word2vec_global.h:467-497): start slot
  * of each word in vocab order (V+1 entries, starts[V] = table_size) */

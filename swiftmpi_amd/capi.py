@@ -86,6 +86,13 @@ PROTOS = {
     "swps_w2v_kernel_times": (ctypes.c_int, [_p, _p, _i32]),
     "swps_w2v_set_profile": (ctypes.c_int, [_p, _i32]),
     "swps_w2v_stream": (_p, [_p]),
+    "swps_w2v_shard": (ctypes.c_int, [_p, _i32, _i32, _i32]),
+    "swps_w2v_batch_counts": (ctypes.c_int, [_p, _p, _u64, ctypes.POINTER(_u64)]),
+    "swps_w2v_request": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.POINTER(_u64)]),
+    "swps_w2v_serve_pull": (ctypes.c_int, [_p, _p, _p, _i32, _p]),
+    "swps_w2v_install_init": (ctypes.c_int, [_p, _p]),
+    "swps_w2v_step": (ctypes.c_int, [_p, _p, _p]),
+    "swps_w2v_serve_push": (ctypes.c_int, [_p, _p, _p]),
     "swps_unigram_starts": (ctypes.c_int, [_p, _p, _u64, _u64, _p]),
     "swps_glibc_rand": (ctypes.c_int, [ctypes.c_uint32, _u64, _u64, _p]),
     "swps_lr_create": (ctypes.c_int, [_p, ctypes.POINTER(LRCfg), ctypes.POINTER(_p)]),

@@ -253,6 +253,42 @@ int table_get_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_va
   return SWPS_OK;
 }
 
+// pull values (first `ncopy` elements of each row) of known rows
+int table_copy_pull(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  if (t->cfg.dtype == SWPS_F64)
+    k_copy_rows_out<double><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<double>(), t->row_elems,
+                                                               t->pull_elems, (double *)d_vals);
+  else
+    k_copy_rows_out<float><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<float>(), t->row_elems,
+                                                              t->pull_elems, (float *)d_vals);
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+// the push rule on known rows (W2V: fp64 mean gradients [n][2D]; LR: fp32 [n])
+int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  if (t->cfg.layout == SWPS_LAYOUT_W2V) {
+    const double lr = (double)t->cfg.learning_rate, fudge = (double)t->cfg.fudge;
+    if (t->cfg.dtype == SWPS_F64)
+      k_push_w2v<double><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, (const double *)d_grads, t->rows.as<double>(),
+                                                            t->cfg.dim, lr, fudge);
+    else
+      k_push_w2v<float><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, (const double *)d_grads, t->rows.as<float>(),
+                                                           t->cfg.dim, lr, fudge);
+  } else {
+    if (t->cfg.dtype == SWPS_F64)
+      k_push_lr<double><<<blocks_for(n), 256, 0, s>>>(d_rows, n, (const float *)d_grads, t->rows.as<double>(),
+                                                      (double)t->cfg.learning_rate, (double)t->cfg.fudge);
+    else
+      k_push_lr<float><<<blocks_for(n), 256, 0, s>>>(d_rows, n, (const float *)d_grads, t->rows.as<float>(),
+                                                     t->cfg.learning_rate, t->cfg.fudge);
+  }
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
 }  // namespace swps
 
 extern "C" {

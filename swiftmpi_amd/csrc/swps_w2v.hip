@@ -587,11 +587,14 @@ template <typename T, typename A> struct PushArgs {
   int32_t *local;
   int D;
   double lr, fudge;
+  double *grads;  // TO_GRADS: mean gradients [U][2D] (the push request payload)
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
 // (word2vec_global.h:176-185) per key, fp64 math; one wave per key.
-template <typename T, typename A, int NCH>
+// TO_GRADS: stop at the mean and write the push payload (sharded mode: the
+// owner GPU applies AdaGrad, see swps_w2v_serve_push).
+template <typename T, typename A, int NCH, bool TO_GRADS>
 __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
   constexpr int E = V16<T>::E;
   using CT = Chk<T, E>;
@@ -604,15 +607,20 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
     if (lane == 0) a.local[vid] = -1;
     const uint32_t hc = a.seg[1 * a.U + u] - a.seg[0 * a.U + u];
     const uint32_t vc = a.seg[3 * a.U + u] - a.seg[2 * a.U + u];
-    if (hc == 0 && vc == 0) continue;
-    T *row = a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
+    if (hc == 0 && vc == 0 && !TO_GRADS) continue;
+    T *row = TO_GRADS ? nullptr : a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
       const int ci = lane + c * 64;
       if (ci >= NC) continue;
       for (int half = 0; half < 2; half++) {
         const uint32_t cnt = half ? vc : hc;
-        if (cnt == 0) continue;
+        if (cnt == 0) {
+          if (TO_GRADS)
+#pragma unroll
+            for (int k = 0; k < E; k++) a.grads[u * 2 * D + half * D + ci * E + k] = 0.0;
+          continue;
+        }
         const uint32_t i0 = a.ioff[2 * u + half], i1 = a.ioff[2 * u + half + 1];
         const uint32_t stride = (i1 - i0) > kGroup ? kGroup : 1;
         double sum[E];
@@ -631,6 +639,11 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
 #pragma unroll
               for (int k = 0; k < E; k++) sum[k] += CA::at(pv[q], k);
         }
+        if (TO_GRADS) {
+#pragma unroll
+          for (int k = 0; k < E; k++) a.grads[u * 2 * D + half * D + ci * E + k] = sum[k] / (double)cnt;
+          continue;
+        }
         T *w = row + half * D, *w2 = row + (2 + half) * D;
         const typename CT::R wr = CT::ld(w, ci, D), w2r = CT::ld(w2, ci, D);
         double wn[E], w2n[E];
@@ -648,6 +661,35 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
       }
     }
   }
+}
+
+// requester side of a sharded pull: the owners' pull values [U][h|v] (K order)
+// into the worker cache (global_pull_access.h:88-97: params[key] = val)
+template <typename T>
+__global__ __launch_bounds__(256) void k_install(const int32_t *__restrict__ K, uint32_t U, const T *__restrict__ vals,
+                                                 int D, T *__restrict__ cache_h, T *__restrict__ cache_v,
+                                                 int32_t *__restrict__ local, int set_local) {
+  using V = typename V16<T>::V;
+  constexpr int E = V16<T>::E;
+  const int lane = threadIdx.x & 63;
+  const int NC = D / E;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += (uint64_t)gridDim.x * 4) {
+    const int32_t vid = K[u];
+    const V *src = (const V *)(vals + u * 2 * D);
+    V *dh = (V *)(cache_h + (uint64_t)vid * D);
+    V *dv = (V *)(cache_v + (uint64_t)vid * D);
+    for (int c = lane; c < NC; c += 64) {
+      dh[c] = src[c];
+      dv[c] = src[NC + c];
+    }
+    if (set_local && lane == 0) local[vid] = (int32_t)u;
+  }
+}
+
+__global__ void k_vid_keys(const int32_t *__restrict__ K, uint64_t n, const uint64_t *__restrict__ vkeys,
+                           uint64_t *__restrict__ out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = vkeys[K[i]];
 }
 
 __global__ void k_trace_copy(const int32_t *__restrict__ src, uint64_t n, int32_t *__restrict__ dst) {
@@ -745,6 +787,14 @@ struct swps_w2v {
   uint64_t lstate = 2008ULL;
   uint64_t fstate = std::numeric_limits<unsigned long>::max() / 2;
   uint64_t lstate_epoch = 0;        // main LCG state at the current epoch's start
+  // sharded mode: keys owned by BasicHashFrag node rank+1
+  int rank = 0, world = 1, frag_num = 0;
+  bool sharded = false;
+  std::vector<uint64_t> bcounts;   // [nb][world] keys requested per owner per batch
+  std::vector<uint64_t> icounts;   // [world] init request per owner
+  std::vector<int32_t> init_order; // vids grouped by owner
+  DevMem d_vkeys, d_init_order, d_serve_rows;
+  uint64_t serve_n = 0;
   std::vector<uint32_t> plan_P;     // kept positions per batch of the current epoch
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
@@ -986,7 +1036,10 @@ template <int NCH, typename T, typename A> void launch_gather(const GatherArgs<A
   k_combine<T, A, NCH><<<grid, 256, 0, s>>>(a);
 }
 template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A> &a, hipStream_t s) {
-  k_push<T, A, NCH><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
+  if (a.grads)
+    k_push<T, A, NCH, true><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
+  else
+    k_push<T, A, NCH, false><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
 }
 constexpr uint32_t kChunk = 128;
 
@@ -1042,7 +1095,7 @@ int plan_epoch(swps_w2v *w) {
   return SWPS_OK;
 }
 
-template <typename T, typename A> int run_batch(swps_w2v *w) {
+template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals = nullptr, double *d_grads = nullptr) {
   const uint64_t nb = w->batches.size();
   if (w->cursor % nb == 0) SWPS_TRY(plan_epoch(w));
   const uint64_t bi = w->cursor % nb;
@@ -1057,9 +1110,13 @@ template <typename T, typename A> int run_batch(swps_w2v *w) {
   // ---- pull (global_pull_access.h:28-107 + server.h:129-154) ----
   if (U) {
     hipEvent_t e = tm.begin(s);
-    k_pull<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(), D,
-                                                     w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
-                                                     w->d_local.as<int32_t>(), 1);
+    if (d_vals)  // sharded: values pulled from the owners
+      k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
+                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 1);
+    else
+      k_pull<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(), D,
+                                                       w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
+                                                       w->d_local.as<int32_t>(), 1);
     SWPS_HIP(hipGetLastError());
     tm.end(KT_PULL, e, s);
   }
@@ -1182,7 +1239,7 @@ template <typename T, typename A> int run_batch(swps_w2v *w) {
     }
     PushArgs<T, A> pa{K, U, w->d_vid_row.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
                       w->d_partial.as<A>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
-                      (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge};
+                      (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads};
     hipEvent_t ep = tm.begin(s);
     switch (w->NCH) {
       case 1: launch_push<1>(pa, s); break;
@@ -1467,6 +1524,146 @@ int swps_glibc_rand(uint32_t seed, uint64_t skip, uint64_t n, int32_t *out) {
   GlibcRand r(seed);
   for (uint64_t i = 0; i < skip; i++) (void)r.next();
   for (uint64_t i = 0; i < n; i++) out[i] = r.next();
+  return SWPS_OK;
+}
+
+}  // extern "C"
+
+// ============================================================================
+// Sharded mode: every rank is a worker (its own corpus,
+// vocab, RNG streams and full-vocab cache, like a reference MPI rank) and a
+// server for the keys BasicHashFrag assigns to node rank+1.  The caller moves
+// bytes between ranks (RCCL all-to-all-v through torch.distributed; see
+// swiftmpi_amd/dist.py); this library produces and consumes the payloads:
+//   request    keys of the next batch grouped by owner      (pull request)
+//   serve_pull owner: rows of the received keys  [n][h|v]    (pull response)
+//   step       install the pulled rows, learn the batch, emit the mean
+//              gradients [U][h|v] fp64 in request order        (push request)
+//   serve_push owner: AdaGrad per source rank, in rank order (server.h:156-176)
+// ============================================================================
+extern "C" {
+
+int swps_w2v_shard(swps_w2v *w, int32_t rank, int32_t world, int32_t frag_num) {
+  if (!w->loaded) return fail(SWPS_E_STATE, "load a corpus first");
+  if (w->inited) return fail(SWPS_E_STATE, "shard before swps_w2v_init / the first pull");
+  if (world < 1 || rank < 0 || rank >= world) return fail(SWPS_E_CFG, "bad rank/world");
+  if (w->cfg.init_mode == SWPS_W2V_INIT_REF)
+    return fail(SWPS_E_UNSUPPORTED, "sharded mode initialises on the owners (SWPS_W2V_INIT_TABLE + SWPS_INIT_HASH): "
+                                    "the reference's rand() order depends on message arrival");
+  std::vector<uint32_t> map(frag_num);
+  SWPS_TRY(swps_hashfrag_table(frag_num, world, map.data()));
+  const uint64_t V = w->vocab_keys.size(), nb = w->batches.size();
+  std::vector<int32_t> owner(V);
+  for (uint64_t i = 0; i < V; i++) owner[i] = (int32_t)map[fmix64(w->vocab_keys[i]) % (uint64_t)frag_num] - 1;
+  auto by_owner = [&](int32_t a, int32_t b) { return owner[a] != owner[b] ? owner[a] < owner[b] : a < b; };
+  w->bcounts.assign(nb * world, 0);
+  for (uint64_t bi = 0; bi < nb; bi++) {
+    auto &b = w->batches[bi];
+    std::sort(w->allK.begin() + b.kofs, w->allK.begin() + b.kofs + b.U, by_owner);
+    for (uint32_t u = 0; u < b.U; u++) w->bcounts[bi * world + owner[w->allK[b.kofs + u]]]++;
+  }
+  w->init_order.resize(V);
+  for (uint64_t i = 0; i < V; i++) w->init_order[i] = (int32_t)i;
+  std::sort(w->init_order.begin(), w->init_order.end(), by_owner);
+  w->icounts.assign(world, 0);
+  for (uint64_t i = 0; i < V; i++) w->icounts[owner[i]]++;
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  SWPS_TRY(upload(w->d_K, w->allK, w->s));
+  SWPS_TRY(upload(w->d_vkeys, w->vocab_keys, w->s));
+  SWPS_TRY(upload(w->d_init_order, w->init_order, w->s));
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  w->rank = rank;
+  w->world = world;
+  w->frag_num = frag_num;
+  w->sharded = true;
+  return SWPS_OK;
+}
+
+int swps_w2v_batch_counts(swps_w2v *w, uint64_t *out, uint64_t cap, uint64_t *nb) {
+  if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
+  *nb = w->batches.size();
+  if (cap < w->bcounts.size()) return fail(SWPS_E_CFG, "buffer too small");
+  std::copy(w->bcounts.begin(), w->bcounts.end(), out);
+  return SWPS_OK;
+}
+
+int swps_w2v_request(swps_w2v *w, int32_t init, uint64_t *counts, uint64_t *d_keys, uint64_t *n) {
+  if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  if (init) {
+    std::copy(w->icounts.begin(), w->icounts.end(), counts);
+    *n = w->vocab_keys.size();
+    if (d_keys) k_vid_keys<<<nblk(*n), 256, 0, w->s>>>(w->d_init_order.as<int32_t>(), *n, w->d_vkeys.as<uint64_t>(), d_keys);
+  } else {
+    const uint64_t bi = w->cursor % w->batches.size();
+    const auto &b = w->batches[bi];
+    std::copy(w->bcounts.begin() + bi * w->world, w->bcounts.begin() + (bi + 1) * w->world, counts);
+    *n = b.U;
+    if (d_keys && b.U)
+      k_vid_keys<<<nblk(b.U), 256, 0, w->s>>>(w->d_K.as<int32_t>() + b.kofs, b.U, w->d_vkeys.as<uint64_t>(), d_keys);
+  }
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src_counts, int32_t insert,
+                        void *d_vals) {
+  if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  uint64_t n = 0;
+  for (int r = 0; r < w->world; r++) n += src_counts[r];
+  SWPS_TRY(w->d_serve_rows.ensure(std::max<uint64_t>(n, 1) * 4));
+  uint32_t *rows = w->d_serve_rows.as<uint32_t>();
+  if (insert) {  // keys are distinct within a source, not across sources
+    uint64_t off = 0;
+    for (int r = 0; r < w->world; r++) {
+      SWPS_TRY(table_find_or_insert(w->t, d_keys + off, src_counts[r], rows + off, w->s));
+      off += src_counts[r];
+    }
+  } else {
+    SWPS_TRY(table_lookup(w->t, d_keys, n, rows, w->s));
+  }
+  SWPS_TRY(table_copy_pull(w->t, rows, n, d_vals, w->s));
+  w->serve_n = n;
+  return SWPS_OK;
+}
+
+int swps_w2v_install_init(swps_w2v *w, const void *d_vals) {
+  if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  const uint64_t V = w->vocab_keys.size();
+  if (w->f64)
+    k_install<double><<<nblk(V * 64), 256, 0, w->s>>>(w->d_init_order.as<int32_t>(), (uint32_t)V,
+                                                      (const double *)d_vals, w->D, w->d_cache_h.as<double>(),
+                                                      w->d_cache_v.as<double>(), w->d_local.as<int32_t>(), 0);
+  else
+    k_install<float><<<nblk(V * 64), 256, 0, w->s>>>(w->d_init_order.as<int32_t>(), (uint32_t)V,
+                                                     (const float *)d_vals, w->D, w->d_cache_h.as<float>(),
+                                                     w->d_cache_v.as<float>(), w->d_local.as<int32_t>(), 0);
+  SWPS_HIP(hipGetLastError());
+  w->inited = true;
+  return SWPS_OK;
+}
+
+int swps_w2v_step(swps_w2v *w, const void *d_vals, double *d_grads) {
+  if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
+  if (!w->inited) return fail(SWPS_E_STATE, "init first");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  if (w->f64) return run_batch<double, double>(w, d_vals, d_grads);
+  if (w->cfg.fp64_intermediates) return run_batch<float, double>(w, d_vals, d_grads);
+  return run_batch<float, float>(w, d_vals, d_grads);
+}
+
+int swps_w2v_serve_push(swps_w2v *w, const double *d_grads, const uint64_t *src_counts) {
+  if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  uint64_t off = 0;
+  for (int r = 0; r < w->world; r++) {  // one AdaGrad step per source, in rank order
+    SWPS_TRY(table_push_rows(w->t, w->d_serve_rows.as<uint32_t>() + off, src_counts[r],
+                             d_grads + off * 2 * w->D, w->s));
+    off += src_counts[r];
+  }
+  if (off != w->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
   return SWPS_OK;
 }
 

@@ -1,0 +1,209 @@
+"""Key-sharded multi-GPU word2vec: one process per GPU, the reference's
+worker+server-per-rank layout with the ZeroMQ request /
+response path (transfer/transfer.h:86-241) replaced by three all-to-all-v
+exchanges per minibatch over torch.distributed — RCCL over xGMI with the
+"nccl" backend (device buffers, ordered on the library's HIP stream, no host
+sync), gloo with host staging for CPU tests and several ranks sharing one GPU.
+
+Per minibatch, every rank in lockstep:
+  1. request    keys of its next batch, grouped by owner       (pull request)
+  2. serve_pull owners look up rows of the keys they received  (pull response)
+  3. step       install the pulled rows, learn, mean gradients (push request)
+  4. serve_push owners apply AdaGrad once per source rank, in rank order
+Key -> owner rank is BasicHashFrag (cluster/hashfrag.h:33-56) with S = world.
+Per-(step, source, destination) key counts come from the static batch
+schedules and are exchanged once, so no step needs a size handshake.
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import Word2Vec, capi
+from .capi import check, ptr
+
+
+class Exchanger:
+    """all-to-all-v of flat tensors among the ranks of a process group."""
+
+    def __init__(self, group=None, device=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.backend = dist.get_backend(group)
+        self.device = device
+
+    def a2a(self, send, send_counts, recv_counts, width=1):
+        """send holds sum(send_counts)*width elements ordered by destination rank."""
+        ss = [int(c) * width for c in send_counts]
+        rs = [int(c) * width for c in recv_counts]
+        if self.backend == "nccl":
+            out = torch.empty(sum(rs), dtype=send.dtype, device=send.device)
+            dist.all_to_all_single(out, send, rs, ss, group=self.group)
+            return out
+        out = torch.empty(sum(rs), dtype=send.dtype)
+        dist.all_to_all_single(out, send.cpu(), rs, ss, group=self.group)
+        if not send.is_cuda:
+            return out
+        out = out.to(send.device)
+        torch.cuda.synchronize(send.device)  # the library reads it on its own stream
+        return out
+
+    def all_gather_matrix(self, mat):
+        """[rows, world] int64 per rank -> [world(src), rows, world] on every rank."""
+        t = torch.as_tensor(mat, dtype=torch.int64)
+        if self.backend == "nccl":
+            t = t.to(self.device)
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(outs, t, group=self.group)
+        return torch.stack([o.cpu() for o in outs]).numpy()
+
+    def max(self, x):
+        t = torch.tensor([x], dtype=torch.int64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+
+class ShardedWord2Vec:
+    """Word2Vec over key-sharded HBM tables on several GPUs (one per rank).
+
+    The table passed in is this rank's shard (create it with init="hash":
+    owners initialise keys on their first pull)."""
+
+    def __init__(self, table, group=None, frag_num=1000, **kw):
+        kw.setdefault("init", "table")
+        self.w = Word2Vec(table, **kw)
+        self.table = table
+        self.D = table.dim
+        self.dev = torch.device("cuda", table.device)
+        self.ex = Exchanger(group, self.dev)
+        self.rank, self.world = self.ex.rank, self.ex.world
+        self.frag_num = frag_num
+        self.cursor = 0
+        self._ext = None
+
+    # -- setup -----------------------------------------------------------------
+    def load_text(self, path):
+        self.w.load_text(path)
+        self._shard()
+
+    def load_tokens(self, word_ids, line_off, word_keys):
+        self.w.load_tokens(word_ids, line_off, word_keys)
+        self._shard()
+
+    def _shard(self):
+        check(capi.lib().swps_w2v_shard(self.w.h, self.rank, self.world, self.frag_num))
+        nb = self.w.info()["batches"]
+        cnt = np.zeros(nb * self.world, dtype=np.uint64)
+        n = ctypes.c_uint64()
+        check(capi.lib().swps_w2v_batch_counts(self.w.h, ptr(cnt), len(cnt), ctypes.byref(n)))
+        self.nb = nb
+        self.steps_per_epoch = self.ex.max(nb)
+        mat = np.zeros((self.steps_per_epoch, self.world), dtype=np.int64)
+        mat[:nb] = cnt.reshape(nb, self.world).astype(np.int64)
+        g = self.ex.all_gather_matrix(mat)  # [src][step][dst]
+        self.send_counts = g[self.rank]                 # [step][dst]
+        self.recv_counts = g[:, :, self.rank].T.copy()  # [step][src]
+
+    def _stream(self):
+        if self.ex.backend != "nccl":
+            return None
+        if self._ext is None:
+            self._ext = torch.cuda.ExternalStream(self.w.stream(), device=self.dev)
+        return self._ext
+
+    def _sync_for_host(self):
+        if self.ex.backend != "nccl":
+            self.w.sync()
+
+    def _exchange(self, send, sc, rc, width):
+        s = self._stream()
+        if s is None:
+            self._sync_for_host()
+            return self.ex.a2a(send, sc, rc, width)
+        with torch.cuda.stream(s):  # RCCL ordered after / before the library's kernels
+            return self.ex.a2a(send, sc, rc, width)
+
+    def _empty(self, n, dtype):
+        s = self._stream()
+        if s is None:
+            return torch.empty(n, dtype=dtype, device=self.dev)
+        with torch.cuda.stream(s):
+            return torch.empty(n, dtype=dtype, device=self.dev)
+
+    # -- the first full pull (word2vec_global.h:557-562) ------------------------
+    def init(self):
+        L = capi.lib()
+        counts = np.zeros(self.world, dtype=np.uint64)
+        n = ctypes.c_uint64()
+        check(L.swps_w2v_request(self.w.h, 1, ptr(counts), None, ctypes.byref(n)))
+        keys = self._empty(n.value, torch.int64)
+        check(L.swps_w2v_request(self.w.h, 1, ptr(counts), ptr(keys), ctypes.byref(n)))
+        sc = counts.astype(np.int64)
+        rc = self.ex.all_gather_matrix(sc[None, :])[:, 0, self.rank].copy()  # [src]
+        rkeys = self._exchange(keys, sc, rc, 1)
+        vals = self._empty(int(rc.sum()) * 2 * self.D, self.table.torch_dtype)
+        rcu = rc.astype(np.uint64)
+        check(L.swps_w2v_serve_pull(self.w.h, ptr(rkeys), ptr(rcu), 1, ptr(vals)))
+        mine = self._exchange(vals, rc, sc, 2 * self.D)
+        check(L.swps_w2v_install_init(self.w.h, ptr(mine)))
+        self.w.sync()
+
+    # -- one lockstep minibatch ------------------------------------------------
+    def step(self):
+        L = capi.lib()
+        s = self.cursor % self.steps_per_epoch
+        sc, rc = self.send_counts[s], self.recv_counts[s]
+        nsend = int(sc.sum())
+        keys = self._empty(nsend, torch.int64)
+        mine = s < self.nb
+        if mine and nsend:
+            counts = np.zeros(self.world, dtype=np.uint64)
+            n = ctypes.c_uint64()
+            check(L.swps_w2v_request(self.w.h, 0, ptr(counts), ptr(keys), ctypes.byref(n)))
+        rkeys = self._exchange(keys, sc, rc, 1)
+        vals = self._empty(int(rc.sum()) * 2 * self.D, self.table.torch_dtype)
+        rcu = rc.astype(np.uint64)
+        check(L.swps_w2v_serve_pull(self.w.h, ptr(rkeys), ptr(rcu), 0, ptr(vals)))
+        my_vals = self._exchange(vals, rc, sc, 2 * self.D)
+        grads = self._empty(nsend * 2 * self.D, torch.float64)
+        if mine:
+            check(L.swps_w2v_step(self.w.h, ptr(my_vals) if nsend else None, ptr(grads) if nsend else None))
+        rgrads = self._exchange(grads, sc, rc, 2 * self.D)
+        check(L.swps_w2v_serve_push(self.w.h, ptr(rgrads), ptr(rcu)))
+        self.cursor += 1
+
+    def train_steps(self, n):
+        for _ in range(n):
+            self.step()
+
+    train_batches = train_steps
+
+    def train(self, niters=1):
+        self.train_steps(niters * self.steps_per_epoch)
+        self.sync()
+
+    def sync(self):
+        self.w.sync()
+        torch.cuda.synchronize(self.dev)
+
+    def stats(self):
+        return self.w.stats()
+
+    def kernel_times(self, reset=False):
+        return self.w.kernel_times(reset)
+
+    def info(self):
+        return self.w.info()
+
+    def set_profile(self, on):
+        self.w.set_profile(on)
+
+    def shard_rows(self):
+        """(keys, rows [n][4D] fp64) of the keys this rank owns."""
+        keys = self.table.keys()
+        if len(keys) == 0:
+            return keys, np.zeros((0, 4 * self.D))
+        kt = torch.as_tensor(keys.astype(np.int64), device=self.dev)
+        return keys, self.table.export(kt).double().cpu().numpy()

@@ -174,3 +174,40 @@ def test_fast_mode_close_to_parity_mode(lib, oracle_mod, gpu, tmp_path):
     rel = np.abs(outs[1] - outs[0]) / np.maximum(np.abs(outs[0]), 1e-3)
     print("fast-vs-parity rel: median %.3g p99 %.3g max %.3g" % (np.median(rel), np.quantile(rel, 0.99), rel.max()))
     assert np.median(rel) < 1e-5 and np.quantile(rel, 0.99) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype):
+    """The sharded request / serve / step / push path with one rank (gloo,
+    world 1) reproduces the single-GPU path bit for bit."""
+    import torch.distributed as dist
+    from swiftmpi_amd.dist import ShardedWord2Vec
+    path = zipf_corpus(str(tmp_path / "c.txt"), 120, 300, seed=31)
+    kw = dict(window=3, negative=4, minibatch=13, sample=1e-3, unigram_size=10 ** 6)
+    own = not dist.is_initialized()
+    if own:
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        t = lib.Table("w2v", dim=16, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
+        sh = ShardedWord2Vec(t, **kw)
+        sh.load_text(path)
+        sh.init()
+        sh.train(2)
+        t1 = lib.Table("w2v", dim=16, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
+        w1 = lib.Word2Vec(t1, init="table", **kw)
+        w1.load_text(path)
+        w1.init()
+        w1.train(2)
+        vk, _ = w1.vocab()
+        keys, rows = sh.shard_rows()
+        pos = {int(k): i for i, k in enumerate(keys)}
+        got = np.stack([rows[pos[int(k)]] for k in vk])
+        assert np.array_equal(got, w1.get_params())
+    finally:
+        if own:
+            dist.destroy_process_group()
