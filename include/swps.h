@@ -19,6 +19,7 @@
  *   swps_to_node_id   BasicHashFrag::to_node_id                  cluster/hashfrag.h:51-56
  *   swps_w2v_*        Word2Vec<MiniBatch>::train / MiniBatch     apps/word2vec/word2vec_global.h:284-731
  *   swps_lr_*         LR::train / learn_instance / predict       apps/logistic/lr.cpp:157-398
+ *   swps_s2v_*        Sent2Vec::train / learn_instance           apps/sent2vec/sent2vec.cpp:37-181
  */
 #ifndef SWPS_H_
 #define SWPS_H_
@@ -208,6 +209,57 @@ int swps_unigram_starts(const uint64_t *keys, const int32_t *counts, uint64_t V,
                         uint64_t *starts);
 /* glibc rand() after srand(seed), `skip` outputs discarded (Vec::randInit's stream) */
 int swps_glibc_rand(uint32_t seed, uint64_t skip, uint64_t n, int32_t *out);
+
+/* ---- sent2vec (apps/sent2vec/sent2vec.cpp on apps/word2vec/word2vec.h) ---
+ * Sentence vectors against frozen word vectors: Sent2Vec::train
+ * (sent2vec.cpp:37-181).  `words` is an SWPS_LAYOUT_W2V table holding the
+ * word vectors (swps_load of a word2vec dump = ClusterServer::load,
+ * server.h:49-62); it is never updated, only keys a minibatch pull misses
+ * are inserted (accessmethod.h:63-70).  Corpus lines are atoi-keyed words
+ * (word2vec.h:206); the sentence id is BKDR of the line (sent2vec.cpp:75). */
+typedef struct swps_s2v swps_s2v;
+
+typedef struct {
+  int32_t window;              /* word2vec.window */
+  int32_t negative;            /* word2vec.negative */
+  int32_t min_sentence_length; /* word2vec.min_sentence_length */
+  int32_t minibatch;           /* worker.minibatch (lines) */
+  int32_t niters;              /* -niters: learn_instance passes per sentence */
+  float alpha;                 /* word2vec.learning_rate */
+  uint64_t unigram_size;       /* table_size (reference: 1e8) */
+  uint32_t rand_seed;          /* glibc srand seed (reference: 1) */
+  uint64_t rand_offset;        /* rand() calls before the first minibatch pull
+                                * (port binds, table construction, the load) */
+  uint64_t rand_insert_extra;  /* extra rand() calls per key the server inserts:
+                                * 2*D for sparsehash's dense_hash_map::operator[],
+                                * which default-constructs a WParam; 0 otherwise */
+  int32_t profile;             /* 1: time kernels with HIP events */
+} swps_s2v_cfg;
+
+int swps_s2v_create(swps_table *words, const swps_s2v_cfg *cfg, swps_s2v **out);
+int swps_s2v_destroy(swps_s2v *s);
+/* corpus text (one sentence per line) or pre-split tokens: tok_keys[ntok],
+ * line_off[nlines+1], sent_ids[nlines]; fixes the minibatch schedule */
+int swps_s2v_load_text(swps_s2v *s, const char *path);
+int swps_s2v_load_tokens(swps_s2v *s, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,
+                         uint64_t nlines, const uint64_t *sent_ids);
+/* nlines, sentences, minibatches, tokens, inserted keys, max sentences per
+ * minibatch, max records per minibatch, rand() calls, LCG state at the end */
+int swps_s2v_info(swps_s2v *s, uint64_t *out9);
+/* the next `count` minibatches (wrapping to the corpus start) / one full pass */
+int swps_s2v_train_batches(swps_s2v *s, uint64_t count);
+int swps_s2v_train(swps_s2v *s);
+int swps_s2v_sync(swps_s2v *s);
+/* every sentence: ids[n], vectors [n][D] fp64, learn_instance's last g*g */
+int swps_s2v_docs(swps_s2v *s, uint64_t *ids, double *vecs, float *errs, uint64_t cap, uint64_t *n);
+/* the reference's output file: "sent_id\tVec:\tv0 v1 ... \n" (sent2vec.cpp:84) */
+int swps_s2v_dump(swps_s2v *s, const char *path);
+/* [minibatches, sentences, positions, context rows read, target rows read] */
+int swps_s2v_stats(swps_s2v *s, uint64_t *out5);
+int swps_s2v_set_profile(swps_s2v *s, int32_t on);
+/* out[2k] = ms, out[2k+1] = launches for k in {records, docs} */
+int swps_s2v_kernel_times(swps_s2v *s, double *out4, int32_t reset);
+void *swps_s2v_stream(swps_s2v *s);
 
 /* ---- sparse logistic regression (apps/logistic/lr.cpp) ------------------- */
 typedef struct swps_lr swps_lr;

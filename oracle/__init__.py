@@ -31,6 +31,14 @@ class W2VCfg(ctypes.Structure):
                 ("lr", ctypes.c_float), ("table_size", ctypes.c_uint64), ("key_mode", ctypes.c_int32)]
 
 
+class S2VCfg(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("window", ctypes.c_int32), ("negative", ctypes.c_int32),
+                ("min_sentence_length", ctypes.c_int32), ("minibatch", ctypes.c_int32), ("niters", ctypes.c_int32),
+                ("storage_f32", ctypes.c_int32), ("alpha", ctypes.c_float), ("table_size", ctypes.c_uint64),
+                ("rand_seed", ctypes.c_uint32), ("rand_offset", ctypes.c_uint64),
+                ("rand_insert_extra", ctypes.c_uint64)]
+
+
 _lib = None
 
 
@@ -82,6 +90,16 @@ def lib():
         L.orc_lr_predict.argtypes = [_p, _p, _p]
         L.orc_lr_pull_order.restype = _u64
         L.orc_lr_pull_order.argtypes = [_p, _p, _u64]
+        L.orc_s2v_create.restype = _p
+        L.orc_s2v_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(S2VCfg)]
+        L.orc_s2v_destroy.argtypes = [_p]
+        L.orc_s2v_load_words.argtypes = [_p, ctypes.c_char_p]
+        L.orc_s2v_train.argtypes = [_p]
+        L.orc_s2v_num_docs.restype = _u64
+        L.orc_s2v_num_docs.argtypes = [_p]
+        L.orc_s2v_docs.argtypes = [_p, _p, _p, _p]
+        L.orc_s2v_stats.argtypes = [_p, _p]
+        L.orc_s2v_word_rows.argtypes = [_p, _p, _u64, _p]
         _lib = L
     return _lib
 
@@ -252,6 +270,56 @@ class LR:
         out = np.zeros(max(n, 1 << 16), dtype=np.uint32)
         m = lib().orc_lr_pull_order(self.h, _ptr(out), len(out))
         return out[:m]
+
+
+class S2V:
+    """Reference-semantics sent2vec (sent2vec.cpp on word2vec.h's MiniBatch,
+    nthreads = 1).  rand_offset = rand() calls before load_words."""
+
+    def __init__(self, corpus_path, dim, window=5, negative=5, min_sentence_length=1, minibatch=100, niters=1,
+                 alpha=0.05, table_size=int(1e8), storage_f32=False, rand_seed=1, rand_offset=2,
+                 rand_insert_extra=0):
+        c = S2VCfg(dim, window, negative, min_sentence_length, minibatch, niters, int(storage_f32), alpha,
+                   table_size, rand_seed, rand_offset, rand_insert_extra)
+        self.dim = dim
+        self.h = lib().orc_s2v_create(corpus_path.encode(), ctypes.byref(c))
+        if not self.h:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_s2v_destroy(self.h)
+            self.h = None
+
+    def load_words(self, path):
+        if lib().orc_s2v_load_words(self.h, path.encode()) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def train(self):
+        if lib().orc_s2v_train(self.h) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def docs(self):
+        n = int(lib().orc_s2v_num_docs(self.h))
+        ids = np.zeros(max(n, 1), dtype=np.uint64)
+        vecs = np.zeros((max(n, 1), self.dim), dtype=np.float64)
+        errs = np.zeros(max(n, 1), dtype=np.float32)
+        lib().orc_s2v_docs(self.h, _ptr(ids), _ptr(vecs), _ptr(errs))
+        return ids[:n], vecs[:n], errs[:n]
+
+    def stats(self):
+        out = np.zeros(8, dtype=np.uint64)
+        lib().orc_s2v_stats(self.h, _ptr(out))
+        d = dict(zip(["batches", "pulled", "inserted", "rand_calls", "draws", "rng", "server_keys", "err_bits"],
+                     [int(x) for x in out]))
+        d["error_sum"] = float(np.array([d.pop("err_bits")], dtype=np.uint32).view(np.float32)[0])
+        return d
+
+    def word_rows(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros((len(keys), 2 * self.dim), dtype=np.float64)
+        rc = lib().orc_s2v_word_rows(self.h, _ptr(keys), len(keys), _ptr(out))
+        return out, rc == 0
 
 
 def logloss_accuracy(p, y, eps=1e-15):

@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <limits>
 #include <map>
 #include <stdexcept>
@@ -882,6 +883,364 @@ uint64_t orc_lr_pull_order(void *h, uint32_t *out, uint64_t cap) {
   for (auto k : K0)
     if (n < cap) out[n++] = k;
   return n;
+}
+
+}  // extern "C"
+
+// =============================================================================
+// sent2vec — apps/sent2vec/sent2vec.cpp (Sent2Vec) on apps/word2vec/word2vec.h's
+// MiniBatch, nthreads = 1.
+//   * word vectors: ClusterServer::load (cluster/server.h:49-62) of a text
+//     dump "key\tv...\th..." — one WParam (2·D rand()) is constructed before
+//     the loop; never updated afterwards (WordMiniBatch has no push);
+//   * per minibatch: gather the next B+1 valid lines (word2vec.h:323-377:
+//     atoi keys, std::map counts, `_local_keys` a persistent unordered_set
+//     that is cleared, not rebuilt), pull (server.h:129-154: a WParam — 2·D
+//     rand() — per pulled key, misses inserted), a table_size-slot unigram
+//     table in std::map key order (word2vec.h:398-425);
+//   * then B+1 lines (valid or not) are read; each valid line gets
+//     sent_id = BKDR(line), a fresh sentence vector (Vec::random: D rand(),
+//     utils/vec1.h:229-232) and `niters` learn_instance passes
+//     (sent2vec.cpp:109-181): neu1 = sent + sum of context v, positive +
+//     negatives from the minibatch table, neu1e += g*h, sent += alpha*neu1e.
+// `rand_insert_extra` = rand() calls consumed per new server key beyond the
+// WParam that is stored (google::dense_hash_map::operator[] default-constructs
+// the mapped WParam, 2·D, when the key is new: sparsetable.h:45-48); 0 models
+// a map that does not.
+// =============================================================================
+namespace {
+
+struct S2VCfg {
+  int32_t dim, window, negative, min_sentence_length, minibatch, niters, storage_f32;
+  float alpha;
+  uint64_t table_size;
+  uint32_t rand_seed;
+  uint64_t rand_offset;
+  uint64_t rand_insert_extra;
+};
+
+struct S2V {
+  S2VCfg cfg;
+  std::vector<std::string> raw;
+  std::vector<Line> lines;
+  std::unordered_map<uint64_t, Row> server;
+  std::unordered_set<uint64_t> local_keys;  // MiniBatch::_local_keys (one object for the run)
+  std::map<uint64_t, int> word_freq;
+  std::vector<uint64_t> wordids;
+  std::vector<uint64_t> table;  // keys
+  std::unordered_map<uint64_t, Row> cache;
+  uint64_t rng = 2008;
+  float exptab[1000];
+  uint64_t rand_calls = 0, batches = 0, pulled = 0, misses = 0, draws = 0;
+  float err_data = 0;
+  std::vector<uint64_t> ids;
+  std::vector<double> vecs;
+  std::vector<float> errs;
+
+  int D() const { return cfg.dim; }
+  bool f32() const { return cfg.storage_f32 != 0; }
+
+  int32_t R() {
+    rand_calls++;
+    return rand();
+  }
+  // Vec::randInit (utils/vec1.h:229-232)
+  void rand_vec(std::vector<double> &x) {
+    x.assign(D(), 0.0);
+    for (int i = 0; i < D(); i++) {
+      float r = R() / (float)RAND_MAX;
+      x[i] = ((double)r - 0.5) / (double)(size_t)D();
+    }
+  }
+  // SparseTableShard::assign (sparsetable.h:45-48) of a key new to the server
+  void insert(uint64_t k, const Row &p) {
+    for (uint64_t i = 0; i < cfg.rand_insert_extra; i++) (void)R();
+    Row r = p;
+    for (auto &x : r.h) x = store_round(x, f32());
+    for (auto &x : r.v) x = store_round(x, f32());
+    server[k] = r;
+  }
+
+  // ClusterServer::load (server.h:49-62), one server: every key is owned.
+  void load(const char *path) {
+    std::ifstream file(path);
+    if (!file.is_open()) throw std::runtime_error("cannot open word vectors");
+    Row param;  // `param_t param;` — WParam(): h then v
+    rand_vec(param.h);
+    rand_vec(param.v);
+    unsigned long key = 0;
+    bool have = false;
+    while (!file.eof()) {
+      file >> key;  // on failure at EOF `key` keeps the last value
+      have = have || !file.fail();
+      for (int i = 0; i < D(); i++) file >> param.v[i];  // WParam operator>>: v then h
+      for (int i = 0; i < D(); i++) file >> param.h[i];
+      if (!have) break;  // empty file: the reference would assign an uninitialised key
+      if (server.find(key) == server.end()) {
+        insert(key, param);
+      } else {
+        Row r = param;
+        for (auto &x : r.h) x = store_round(x, f32());
+        for (auto &x : r.v) x = store_round(x, f32());
+        server[key] = r;
+      }
+    }
+  }
+
+  // word2vec.h:398-425 (std::map order, literal table_size walk)
+  void gen_unigram_table() {
+    wordids.clear();
+    for (auto &it : word_freq) wordids.push_back(it.first);
+    const uint64_t T = cfg.table_size;
+    table.assign(T, 0);
+    double pw = 0, power = 0.75;
+    for (auto &it : word_freq) pw += std::pow(it.second, power);
+    size_t i = 0;
+    double d1 = std::pow(word_freq[wordids[i]], power) / (double)pw;
+    for (uint64_t a = 0; a < T; a++) {
+      table[a] = wordids[i];
+      if ((int64_t)a / (double)T > d1) {
+        i++;
+        if (i >= wordids.size()) throw std::runtime_error("unigram table walked past the vocab (reference UB)");
+        d1 += std::pow(word_freq[wordids[i]], power) / (double)pw;
+      }
+      if (i >= word_freq.size()) i = word_freq.size() - 1;
+    }
+  }
+
+  float exp_lookup(float f) const { return exptab[(int)((f + 6) * (1000 / 6 / 2))]; }
+
+  // sent2vec.cpp:109-181
+  float learn_instance(const std::vector<uint64_t> &w, std::vector<double> &sent) {
+    const int W = cfg.window, N = cfg.negative, Dd = D();
+    int b = (int)(lcg_next(rng) % (uint64_t)W);
+    draws++;
+    const int n = (int)w.size();
+    float g = 0, f;
+    std::vector<double> neu1(Dd), neu1e(Dd);
+    for (int pos = 0; pos < n; pos++) {
+      const uint64_t word = w[pos];
+      std::fill(neu1e.begin(), neu1e.end(), 0.0);
+      b = (int)(lcg_next(rng) % (uint64_t)W);
+      draws++;
+      neu1 = sent;
+      for (int a = b; a < W * 2 + 1 - b; a++) {
+        if (a == W) continue;
+        int c = pos - W + a;
+        if (c < 0 || c >= n) continue;
+        const Row &r = cache.at(w[c]);
+        for (int i = 0; i < Dd; i++) neu1[i] += r.v[i];
+      }
+      for (int d = 0; d < N + 1; d++) {
+        uint64_t target;
+        int label;
+        if (d == 0) {
+          target = word;
+          label = 1;
+        } else {
+          target = table[(lcg_next(rng) >> 16) % cfg.table_size];
+          draws++;
+          if (target == 0) {
+            target = table[(lcg_next(rng) >> 16) % cfg.table_size];
+            draws++;
+          }
+          if (target == word) continue;
+          label = 0;
+        }
+        const Row &t = cache.at(target);
+        double dot = 0;
+        for (int i = 0; i < Dd; i++) dot += neu1[i] * t.h[i];
+        f = 0;
+        f += dot;
+        if (f > 6)
+          g = (label - 1) * cfg.alpha;
+        else if (f < -6)
+          g = (label - 0) * cfg.alpha;
+        else
+          g = (label - exp_lookup(f)) * cfg.alpha;
+        for (int i = 0; i < Dd; i++) {
+          double p = t.h[i] * (double)g;
+          neu1e[i] += p;
+        }
+      }
+      for (int i = 0; i < Dd; i++) {
+        double p = neu1e[i] * (double)cfg.alpha;
+        sent[i] += p;
+      }
+    }
+    return g * g;
+  }
+
+  // Sent2Vec::train (sent2vec.cpp:37-106)
+  void train() {
+    const int B = cfg.minibatch;
+    const size_t nl = lines.size();
+    size_t li = 0;
+    while (true) {
+      // MiniBatch::gather_keys(file, line_id, B) (word2vec.h:323-377) after clear()
+      local_keys.clear();
+      word_freq.clear();
+      cache.clear();
+      int cnt = 0;
+      for (size_t j = li; j < nl;) {
+        const Line &ln = lines[j++];
+        if (!ln.valid) continue;
+        for (auto k : ln.words) {
+          auto it = word_freq.find(k);
+          if (it != word_freq.end())
+            it->second++;
+          else {
+            word_freq[k] = 1;
+            local_keys.insert(k);
+          }
+        }
+        if (++cnt > B) break;
+      }
+      if (local_keys.size() < 5) break;
+      // MiniBatch::pull (word2vec.h:303-310) -> server.h:143-150 per key
+      for (auto k : local_keys) {
+        Row p;
+        rand_vec(p.h);
+        rand_vec(p.v);
+        auto it = server.find(k);
+        if (it == server.end()) {
+          insert(k, p);
+          it = server.find(k);
+          misses++;
+        }
+        cache[k] = it->second;
+        pulled++;
+      }
+      gen_unigram_table();
+      // the training handler (sent2vec.cpp:48-93)
+      int lc = 0;
+      while (true) {
+        if (lc > B) break;
+        if (li >= nl) break;
+        const size_t l = li++;
+        lc++;
+        if (!lines[l].valid) continue;
+        const uint64_t sent_id = orc_bkdr(raw[l].c_str());
+        std::vector<double> sent;
+        rand_vec(sent);
+        float error = 0;
+        for (int it = 0; it < cfg.niters; it++) error = learn_instance(lines[l].words, sent);
+        err_data += error;
+        ids.push_back(sent_id);
+        vecs.insert(vecs.end(), sent.begin(), sent.end());
+        errs.push_back(error);
+        if (lc > B) break;
+      }
+      batches++;
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+typedef struct {
+  int32_t dim, window, negative, min_sentence_length, minibatch, niters, storage_f32;
+  float alpha;
+  uint64_t table_size;
+  uint32_t rand_seed;
+  uint64_t rand_offset;
+  uint64_t rand_insert_extra;
+} orc_s2v_cfg;
+
+void *orc_s2v_create(const char *corpus_path, const orc_s2v_cfg *c) {
+  try {
+    S2V *m = new S2V();
+    m->cfg = S2VCfg{c->dim,        c->window,     c->negative,  c->min_sentence_length,
+                    c->minibatch,  c->niters,     c->storage_f32, c->alpha,
+                    c->table_size, c->rand_seed,  c->rand_offset, c->rand_insert_extra};
+    if (!read_lines(corpus_path, m->raw)) {
+      g_err = "cannot open corpus";
+      delete m;
+      return nullptr;
+    }
+    m->lines.resize(m->raw.size());
+    for (size_t i = 0; i < m->raw.size(); i++) {  // word2vec.h:212-224 (atoi keys)
+      Line &ln = m->lines[i];
+      for (auto &w : split_space(m->raw[i])) ln.words.push_back((uint64_t)(int64_t)std::atoi(w.c_str()));
+      ln.valid = (int)ln.words.size() >= c->min_sentence_length;
+    }
+    orc_exptable(m->exptab);
+    srand(c->rand_seed);
+    for (uint64_t i = 0; i < c->rand_offset; i++) (void)m->R();
+    return m;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
+void orc_s2v_destroy(void *h) { delete (S2V *)h; }
+
+int orc_s2v_load_words(void *h, const char *path) {
+  try {
+    ((S2V *)h)->load(path);
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+int orc_s2v_train(void *h) {
+  try {
+    ((S2V *)h)->train();
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+uint64_t orc_s2v_num_docs(void *h) { return ((S2V *)h)->ids.size(); }
+
+// sentence ids, vectors [n][D] and per-sentence learn_instance return values
+void orc_s2v_docs(void *h, uint64_t *ids, double *vecs, float *errs) {
+  S2V *m = (S2V *)h;
+  std::copy(m->ids.begin(), m->ids.end(), ids);
+  std::copy(m->vecs.begin(), m->vecs.end(), vecs);
+  std::copy(m->errs.begin(), m->errs.end(), errs);
+}
+
+// [minibatches, pulled keys, inserted keys, rand() calls, LCG draws, LCG state,
+//  server keys, Error::data as float bits]
+void orc_s2v_stats(void *h, uint64_t *out) {
+  S2V *m = (S2V *)h;
+  out[0] = m->batches;
+  out[1] = m->pulled;
+  out[2] = m->misses;
+  out[3] = m->rand_calls;
+  out[4] = m->draws;
+  out[5] = m->rng;
+  out[6] = m->server.size();
+  uint32_t bits;
+  std::memcpy(&bits, &m->err_data, 4);
+  out[7] = bits;
+}
+
+// server rows [h | v] of the given keys (0 and return -1 for unknown keys)
+int orc_s2v_word_rows(void *h, const uint64_t *keys, uint64_t n, double *out) {
+  S2V *m = (S2V *)h;
+  int rc = 0;
+  const int D = m->D();
+  for (uint64_t i = 0; i < n; i++) {
+    auto it = m->server.find(keys[i]);
+    double *o = out + i * 2 * D;
+    if (it == m->server.end()) {
+      std::fill(o, o + 2 * D, 0.0);
+      rc = -1;
+      continue;
+    }
+    std::copy(it->second.h.begin(), it->second.h.end(), o);
+    std::copy(it->second.v.begin(), it->second.v.end(), o + D);
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -8,6 +8,7 @@ interfaces over that ABI:
 
     Table     <- parameter/sparsetable.h + cluster/server.h pull/push handlers
     Word2Vec  <- apps/word2vec/word2vec_global.h  (Word2Vec<MiniBatch>)
+    Sent2Vec  <- apps/sent2vec/sent2vec.cpp       (Sent2Vec)
     LR        <- apps/logistic/lr.cpp             (LR)
     Config    <- utils/ConfigParser.h
 
@@ -15,14 +16,15 @@ Every compute call goes through libswps.so; if it is missing the import of the
 classes below raises (no CPU fallback).
 """
 import ctypes
+import weakref
 
 import numpy as np
 
 from . import capi
 from .capi import SwpsError, check, ptr
 
-__all__ = ["Table", "Word2Vec", "LR", "Config", "SwpsError", "bkdr", "fmix64", "hashfrag_table", "to_node_id",
-           "load_library"]
+__all__ = ["Table", "Word2Vec", "Sent2Vec", "LR", "Config", "SwpsError", "bkdr", "fmix64", "hashfrag_table",
+           "to_node_id", "load_library"]
 
 
 def load_library():
@@ -130,9 +132,12 @@ class Table:
         r, p, q = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         capi.lib().swps_table_row_elems(self.h, ctypes.byref(r), ctypes.byref(p), ctypes.byref(q))
         self.row_elems, self.pull_elems, self.push_elems = r.value, p.value, q.value
+        self._deps = weakref.WeakSet()  # app contexts bound to this shard: closed first
 
     def close(self):
         if getattr(self, "h", None):
+            for d in list(getattr(self, "_deps", ())):
+                d.close()
             capi.lib().swps_table_destroy(self.h)
             self.h = None
 
@@ -201,6 +206,7 @@ class Word2Vec:
         h = ctypes.c_void_p()
         check(capi.lib().swps_w2v_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
+        table._deps.add(self)
         self.table = table
         self.dim = table.dim
 
@@ -306,6 +312,130 @@ class Word2Vec:
         return capi.lib().swps_w2v_stream(self.h)
 
 
+class Sent2Vec:
+    """Sentence vectors against frozen word vectors (Sent2Vec, sent2vec.cpp:14-195,
+    on word2vec.h's MiniBatch: per-minibatch vocab and unigram table).
+
+    glibc rand() bookkeeping (the sentence vectors and the rows of keys a pull
+    misses come from it): ``rand_offset`` = calls before load_word_vector (the
+    two port binds by default); ``rand_insert_extra`` = extra calls per key the
+    server inserts — 0 for a map that does not construct a value on insert,
+    2*dim for sparsehash's dense_hash_map::operator[] (then also add 2*dim per
+    SparseTable shard to ``rand_offset`` for set_empty_key)."""
+
+    def __init__(self, table, window=5, negative=5, min_sentence_length=1, minibatch=100, niters=1, alpha=0.05,
+                 unigram_size=int(1e8), rand_seed=1, rand_offset=2, rand_insert_extra=0, profile=False):
+        assert table.layout == "w2v"
+        self.table = table
+        self.dim = table.dim
+        self.kw = dict(window=window, negative=negative, min_sentence_length=min_sentence_length,
+                       minibatch=minibatch, niters=niters, alpha=alpha, unigram_size=unigram_size,
+                       rand_seed=rand_seed, rand_insert_extra=rand_insert_extra, profile=int(profile))
+        self.rand_offset = rand_offset
+        self.h = None
+
+    @classmethod
+    def from_config(cls, config, table, niters, **kw):
+        c = config if isinstance(config, Config) else Config(config)
+        args = dict(window=c.get_int("word2vec", "window"), negative=c.get_int("word2vec", "negative"),
+                    min_sentence_length=c.get_int("word2vec", "min_sentence_length"),
+                    minibatch=c.get_int("worker", "minibatch"), alpha=c.get_float("word2vec", "learning_rate"),
+                    niters=niters)
+        args.update(kw)
+        return cls(table, **args)
+
+    def load_word_vector(self, path, frag_num=1000, world=1, node_id=0):
+        """ClusterServer::load (server.h:49-62): one WParam (2*dim rand()) is
+        constructed first, then every owned key of the dump is assigned."""
+        before = self.table.size()
+        self.table.load(path, frag_num, world, node_id)
+        inserted = self.table.size() - before
+        self.rand_offset += 2 * self.dim + self.kw["rand_insert_extra"] * inserted
+
+    def _create(self):
+        if self.h is None:
+            k = self.kw
+            cfg = capi.S2VCfg(k["window"], k["negative"], k["min_sentence_length"], k["minibatch"], k["niters"],
+                              k["alpha"], k["unigram_size"], k["rand_seed"], self.rand_offset,
+                              k["rand_insert_extra"], k["profile"])
+            h = ctypes.c_void_p()
+            check(capi.lib().swps_s2v_create(self.table.h, ctypes.byref(cfg), ctypes.byref(h)))
+            self.h = h
+            self.table._deps.add(self)
+
+    def close(self):
+        if getattr(self, "h", None):
+            capi.lib().swps_s2v_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def load_text(self, path):
+        self._create()
+        check(capi.lib().swps_s2v_load_text(self.h, path.encode()))
+
+    def load_tokens(self, tok_keys, line_off, sent_ids):
+        self._create()
+        tok_keys = np.ascontiguousarray(tok_keys, dtype=np.uint64)
+        line_off = np.ascontiguousarray(line_off, dtype=np.uint64)
+        sent_ids = np.ascontiguousarray(sent_ids, dtype=np.uint64)
+        check(capi.lib().swps_s2v_load_tokens(self.h, ptr(tok_keys), len(tok_keys), ptr(line_off),
+                                               len(line_off) - 1, ptr(sent_ids)))
+
+    def info(self):
+        o = np.zeros(9, dtype=np.uint64)
+        check(capi.lib().swps_s2v_info(self.h, ptr(o)))
+        return dict(zip(["lines", "docs", "batches", "tokens", "inserted", "max_batch_docs", "max_batch_records",
+                         "rand_calls", "lstate"], [int(x) for x in o]))
+
+    def train(self):
+        check(capi.lib().swps_s2v_train(self.h))
+
+    def train_batches(self, count):
+        check(capi.lib().swps_s2v_train_batches(self.h, count))
+
+    def sync(self):
+        check(capi.lib().swps_s2v_sync(self.h))
+
+    def docs(self):
+        """(sentence ids, vectors [n, dim] fp64, per-sentence g*g of the last pass)."""
+        n = self.info()["docs"]
+        ids = np.zeros(max(n, 1), dtype=np.uint64)
+        vecs = np.zeros((max(n, 1), self.dim), dtype=np.float64)
+        errs = np.zeros(max(n, 1), dtype=np.float32)
+        m = ctypes.c_uint64()
+        check(capi.lib().swps_s2v_docs(self.h, ptr(ids), ptr(vecs), ptr(errs), len(ids), ctypes.byref(m)))
+        return ids[:n], vecs[:n], errs[:n]
+
+    def error(self):
+        """Error::norm() of the run (sent2vec.cpp:80,105): float mean of g*g."""
+        _, _, errs = self.docs()
+        acc = np.float32(0)
+        for e in errs:
+            acc = np.float32(acc + e)
+        return float(acc / np.float32(len(errs))) if len(errs) else float("nan")
+
+    def dump(self, path):
+        check(capi.lib().swps_s2v_dump(self.h, path.encode()))
+
+    def stats(self):
+        o = np.zeros(5, dtype=np.uint64)
+        check(capi.lib().swps_s2v_stats(self.h, ptr(o)))
+        return dict(zip(["batches", "docs", "positions", "ctx_rows", "tgt_rows"], [int(x) for x in o]))
+
+    def set_profile(self, on):
+        check(capi.lib().swps_s2v_set_profile(self.h, int(on)))
+
+    def kernel_times(self, reset=False):
+        o = np.zeros(4, dtype=np.float64)
+        check(capi.lib().swps_s2v_kernel_times(self.h, ptr(o), int(reset)))
+        return {k: (o[2 * i], int(o[2 * i + 1])) for i, k in enumerate(["records", "docs"])}
+
+    def stream(self):
+        return capi.lib().swps_s2v_stream(self.h)
+
+
 class LR:
     """Sparse logistic regression with server-side AdaGrad (lr.cpp:133-411)."""
 
@@ -315,6 +445,7 @@ class LR:
         h = ctypes.c_void_p()
         check(capi.lib().swps_lr_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
+        table._deps.add(self)
         self.table = table
 
     def close(self):

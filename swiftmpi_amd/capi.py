@@ -47,6 +47,12 @@ class LRCfg(ctypes.Structure):
     _fields_ = [("minibatch", _i32), ("init_ref", _i32), ("profile", _i32)]
 
 
+class S2VCfg(ctypes.Structure):
+    _fields_ = [("window", _i32), ("negative", _i32), ("min_sentence_length", _i32), ("minibatch", _i32),
+                ("niters", _i32), ("alpha", ctypes.c_float), ("unigram_size", _u64), ("rand_seed", ctypes.c_uint32),
+                ("rand_offset", _u64), ("rand_insert_extra", _u64), ("profile", _i32)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/swps.h
 PROTOS = {
     "swps_last_error": (ctypes.c_char_p, []),
@@ -95,6 +101,20 @@ PROTOS = {
     "swps_w2v_serve_push": (ctypes.c_int, [_p, _p, _p]),
     "swps_unigram_starts": (ctypes.c_int, [_p, _p, _u64, _u64, _p]),
     "swps_glibc_rand": (ctypes.c_int, [ctypes.c_uint32, _u64, _u64, _p]),
+    "swps_s2v_create": (ctypes.c_int, [_p, ctypes.POINTER(S2VCfg), ctypes.POINTER(_p)]),
+    "swps_s2v_destroy": (ctypes.c_int, [_p]),
+    "swps_s2v_load_text": (ctypes.c_int, [_p, ctypes.c_char_p]),
+    "swps_s2v_load_tokens": (ctypes.c_int, [_p, _p, _u64, _p, _u64, _p]),
+    "swps_s2v_info": (ctypes.c_int, [_p, _p]),
+    "swps_s2v_train_batches": (ctypes.c_int, [_p, _u64]),
+    "swps_s2v_train": (ctypes.c_int, [_p]),
+    "swps_s2v_sync": (ctypes.c_int, [_p]),
+    "swps_s2v_docs": (ctypes.c_int, [_p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
+    "swps_s2v_dump": (ctypes.c_int, [_p, ctypes.c_char_p]),
+    "swps_s2v_stats": (ctypes.c_int, [_p, _p]),
+    "swps_s2v_set_profile": (ctypes.c_int, [_p, _i32]),
+    "swps_s2v_kernel_times": (ctypes.c_int, [_p, _p, _i32]),
+    "swps_s2v_stream": (_p, [_p]),
     "swps_lr_create": (ctypes.c_int, [_p, ctypes.POINTER(LRCfg), ctypes.POINTER(_p)]),
     "swps_lr_destroy": (ctypes.c_int, [_p]),
     "swps_lr_load_text": (ctypes.c_int, [_p, ctypes.c_char_p]),

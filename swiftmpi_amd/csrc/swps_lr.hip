@@ -256,6 +256,7 @@ int swps_lr_destroy(swps_lr *l) {
   l->timer.resolve();
   if (l->h_small) (void)hipHostFree(l->h_small);
   delete l;
+  (void)hipGetLastError();  // leave no sticky error from the calls above
   return SWPS_OK;
 }
 

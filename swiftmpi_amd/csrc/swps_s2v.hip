@@ -1,0 +1,786 @@
+// sent2vec on one MI355X: the reference's Sent2Vec::train
+// (apps/sent2vec/sent2vec.cpp:37-181, on apps/word2vec/word2vec.h's MiniBatch,
+// nthreads = 1 semantics) as HIP kernels over the HBM word table.
+//
+// The word table is an swps_table (W2V layout) filled by swps_load — the
+// reference's ClusterServer::load (cluster/server.h:49-62) — or by a word2vec
+// run on the same GPU.  WordMiniBatch never pushes, so the table is read-only
+// here apart from the keys a minibatch pull misses, which the server inserts
+// with a fresh WParam (accessmethod.h:63-70).  Everything that depends only
+// on the corpus and the two RNG streams is fixed on the host at load time:
+//   * minibatch windows (word2vec.h:323-377: next B+1 valid lines), their key
+//     sets in `_local_keys` iteration order (pull order), their std::map-
+//     ordered vocab and unigram^0.75 table in run-length form (word2vec.h:
+//     398-425);
+//   * the glibc rand() stream: 2·D per pulled key (the WParam the pull handler
+//     constructs, server.h:143-150), `rand_insert_extra` more per inserted key,
+//     D per sentence (Vec::random, utils/vec1.h:229-232);
+//   * the main-LCG state of every sentence: niters·(1 + L·(1+negative)) draws
+//     each (sent2vec.cpp:112,123,142-146; sent2vec has no subsampling).
+// Per minibatch on the device:
+//   k_s2v_records  one wave per sentence, lanes over its (iter, position)
+//                  pairs: jump the LCG, draw b and the negatives (binary
+//                  search in the minibatch's unigram run starts), write the
+//                  word-table rows the position reads (context v, target h)
+//   k_s2v_docs     one wave per sentence, positions in order: the sentence
+//                  vector lives in registers (fp64), neu1 = sent + sum of the
+//                  context v rows, fp64 dots with the target h rows, exp-table
+//                  sigmoid, neu1e += g*h, sent += alpha*neu1e; written once to
+//                  the HBM doc table with the sentence's error g*g.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <limits>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "swps_internal.h"
+
+using namespace swps;
+
+namespace {
+
+template <typename T> struct RowVec;
+template <> struct RowVec<float> {
+  using V = float4;
+  static constexpr int E = 4;
+};
+template <> struct RowVec<double> {
+  using V = double2;
+  static constexpr int E = 2;
+};
+
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t mod_magic(uint64_t x, uint64_t d, uint64_t m) {
+  const uint64_t q = __umul64hi(x, m);  // underestimates x/d by at most 2
+  uint64_t r = x - q * d;
+  if (r >= d) r -= d;
+  if (r >= d) r -= d;
+  return r;
+}
+
+struct S2VRecArgs {
+  const uint32_t *tok_row;    // word-table row of every token of the sentences
+  const uint64_t *doc_tok;    // [ndocs+1] token offsets
+  const uint64_t *doc_rec;    // [ndocs+1] record offsets (niters * tokens)
+  const uint64_t *doc_lcg;    // [ndocs] main-LCG state before the sentence
+  uint64_t d0, nd;            // sentences of this minibatch
+  const uint32_t *vocab_row;  // minibatch vocab (std::map order) -> word-table row
+  const uint64_t *starts;     // unigram run starts of the minibatch vocab [U+1]
+  uint32_t U;
+  uint64_t T, mT;  // unigram table size, floor((2^64-1)/T)
+  int W, N, niters;
+  uint64_t mW;
+  int32_t *rec;  // [records][2W + N + 1] rows, -1 = none
+};
+
+// learn_instance's draws for every (iter, pos) of one sentence
+// (sent2vec.cpp:112 initial b, :123 b per position, :142-146 negatives; a
+// target equal to the word is skipped, :147-148).
+__global__ __launch_bounds__(256) void k_s2v_records(S2VRecArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= a.nd) return;
+  const uint64_t doc = a.d0 + j;
+  const uint64_t t0 = a.doc_tok[doc];
+  const int L = (int)(a.doc_tok[doc + 1] - t0);
+  const int W = a.W, N = a.N, S = 2 * W + N + 1;
+  const uint64_t per_iter = 1 + (uint64_t)L * (N + 1);
+  const uint64_t r0 = a.doc_rec[doc] - a.doc_rec[a.d0];
+  for (int q = lane; q < L * a.niters; q += 64) {
+    const int it = q / L, p = q - it * L;
+    uint64_t x = lcg_jump(a.doc_lcg[doc], (uint64_t)it * per_iter + 1 + (uint64_t)p * (N + 1), kLcgA, kLcgC);
+    x = x * kLcgA + kLcgC;
+    const int b = (int)mod_magic(x, (uint64_t)W, a.mW);
+    const uint32_t word = a.tok_row[t0 + p];
+    int32_t *r = a.rec + (r0 + q) * (uint64_t)S;
+    for (int s = 0; s < 2 * W; s++) {
+      int32_t cv = -1;
+      if (s < 2 * (W - b)) {
+        int aa = b + s;
+        if (aa >= W) aa++;
+        const int c = p - W + aa;
+        if (c >= 0 && c < L) cv = (int32_t)a.tok_row[t0 + c];
+      }
+      r[s] = cv;
+    }
+    r[2 * W] = (int32_t)word;
+    for (int d = 1; d <= N; d++) {
+      x = x * kLcgA + kLcgC;
+      const uint64_t slot = mod_magic(x >> 16, a.T, a.mT);
+      uint32_t lo = 0, hi = a.U;  // largest i with starts[i] <= slot
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.starts[mid] <= slot)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      const uint32_t row = a.vocab_row[lo];
+      r[2 * W + d] = row == word ? -1 : (int32_t)row;
+    }
+  }
+}
+
+template <typename T> struct S2VDocArgs {
+  const int32_t *rec;
+  const uint64_t *doc_tok, *doc_rec;
+  uint64_t d0, nd;
+  const int32_t *init;  // [ndocs][D] glibc rand() outputs (Vec::random)
+  const T *rows;        // word table rows [h | v | h2 | v2]
+  const float *exptab;
+  int D, W, N, niters;
+  float alpha;
+  T *out;      // doc table [ndocs][D]
+  float *err;  // [ndocs] learn_instance's return value of the last pass
+  unsigned long long *rows_read;
+};
+
+// One wave per sentence: learn_instance (sent2vec.cpp:109-181) for every
+// position of every pass, in order.  Lane l owns elements [E*ci, E*ci+E) for
+// ci = l + 64*c; all arithmetic is fp64 like the reference's Vec, products
+// rounded before their adds (-ffp-contract=off).
+template <typename T, int NCH, int G>
+__global__ __launch_bounds__(256) void k_s2v_docs(S2VDocArgs<T> a) {
+  using V = typename RowVec<T>::V;
+  constexpr int E = RowVec<T>::E;
+  const int lane = threadIdx.x & 63;
+  const uint64_t j = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (j >= a.nd) return;
+  const uint64_t doc = a.d0 + j;
+  const int L = (int)(a.doc_tok[doc + 1] - a.doc_tok[doc]);
+  const int D = a.D, W = a.W, N = a.N, NC = D / E, S = 2 * W + N + 1;
+  const int32_t *rec = a.rec + (a.doc_rec[doc] - a.doc_rec[a.d0]) * (uint64_t)S;
+  double sent[NCH][E];
+  // Vec::random: (rand()/(float)RAND_MAX - 0.5)/D
+#pragma unroll
+  for (int c = 0; c < NCH; c++) {
+    const int ci = lane + c * 64;
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      sent[c][k] = 0.0;
+      if (ci < NC) {
+        const float u = (float)a.init[doc * D + ci * E + k] / (float)2147483647;
+        sent[c][k] = ((double)u - 0.5) / (double)D;
+      }
+    }
+  }
+  float g = 0.f;
+  unsigned long long nctx = 0, ntgt = 0;
+  for (int q = 0; q < L * a.niters; q++) {
+    const int32_t *r = rec + (uint64_t)q * S;
+    double neu1[NCH][E], ne[NCH][E];
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        neu1[c][k] = sent[c][k];
+        ne[c][k] = 0.0;
+      }
+    // neu1 = sent_vec + context v rows in window order (sent2vec.cpp:125-135)
+    for (int s0 = 0; s0 < 2 * W; s0 += G) {
+      V rv[G][NCH];
+      int32_t id[G];
+#pragma unroll
+      for (int u = 0; u < G; u++) {
+        id[u] = s0 + u < 2 * W ? r[s0 + u] : -1;
+        if (id[u] >= 0) {
+          const V *src = (const V *)(a.rows + (uint64_t)id[u] * 4 * D + D);
+#pragma unroll
+          for (int c = 0; c < NCH; c++)
+            if (lane + c * 64 < NC) rv[u][c] = src[lane + c * 64];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < G; u++) {
+        if (id[u] < 0) continue;
+        nctx++;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          if (lane + c * 64 < NC)
+#pragma unroll
+            for (int k = 0; k < E; k++) neu1[c][k] += (double)((const T *)&rv[u][c])[k];
+      }
+    }
+    // positive + negatives (sent2vec.cpp:136-163)
+    for (int s0 = 0; s0 <= N; s0 += G) {
+      V hv[G][NCH];
+      int32_t id[G];
+#pragma unroll
+      for (int u = 0; u < G; u++) {
+        id[u] = s0 + u <= N ? r[2 * W + s0 + u] : -1;
+        if (id[u] >= 0) {
+          const V *src = (const V *)(a.rows + (uint64_t)id[u] * 4 * D);
+#pragma unroll
+          for (int c = 0; c < NCH; c++)
+            if (lane + c * 64 < NC) hv[u][c] = src[lane + c * 64];
+        }
+      }
+      double part[G];
+#pragma unroll
+      for (int u = 0; u < G; u++) {
+        part[u] = 0.0;
+        if (id[u] < 0) continue;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          if (lane + c * 64 < NC)
+#pragma unroll
+            for (int k = 0; k < E; k++) {
+              const double prod = neu1[c][k] * (double)((const T *)&hv[u][c])[k];
+              part[u] += prod;
+            }
+      }
+#pragma unroll
+      for (int u = 0; u < G; u++)
+        if (id[u] >= 0) part[u] = wsum(part[u]);
+#pragma unroll
+      for (int u = 0; u < G; u++) {
+        if (id[u] < 0) continue;
+        ntgt++;
+        const int label = s0 + u == 0 ? 1 : 0;
+        float f = 0;
+        f += part[u];
+        if (f > 6)
+          g = (label - 1) * a.alpha;
+        else if (f < -6)
+          g = (label - 0) * a.alpha;
+        else
+          g = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
+        // neu1e += g * h  (Vec operator*(double, Vec): h[i] * (double)g)
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          if (lane + c * 64 < NC)
+#pragma unroll
+            for (int k = 0; k < E; k++) {
+              const double prod = (double)((const T *)&hv[u][c])[k] * (double)g;
+              ne[c][k] += prod;
+            }
+      }
+    }
+    // sent_vec += alpha * neu1e (sent2vec.cpp:164)
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const double prod = ne[c][k] * (double)a.alpha;
+        sent[c][k] += prod;
+      }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; c++) {
+    const int ci = lane + c * 64;
+    if (ci < NC)
+#pragma unroll
+      for (int k = 0; k < E; k++) a.out[doc * D + ci * E + k] = (T)sent[c][k];
+  }
+  if (lane == 0) {
+    a.err[doc] = g * g;
+    atomicAdd(&a.rows_read[0], nctx);
+    atomicAdd(&a.rows_read[1], ntgt);
+  }
+}
+
+inline unsigned nblk(uint64_t threads, unsigned bs = 256) {
+  return (unsigned)std::max<uint64_t>(1, (threads + bs - 1) / bs);
+}
+
+enum { ST_REC = 0, ST_DOC, ST_N };
+
+}  // namespace
+
+struct swps_s2v {
+  swps_table *t = nullptr;
+  swps_s2v_cfg cfg{};
+  int D = 0, W = 0, N = 0, NCH = 1;
+  bool f64 = false;
+  hipStream_t s = nullptr;
+  // host schedule (fixed at load)
+  struct Batch {
+    uint64_t d0, d1;  // sentences
+    uint64_t v0, s0;  // offsets into the concatenated minibatch vocabs / run starts
+    uint32_t U;
+    uint64_t recs;  // (iter, position) records of the minibatch
+  };
+  std::vector<Batch> batches;
+  std::vector<uint64_t> doc_id, doc_tok, doc_rec, doc_lcg;
+  uint64_t nlines = 0, ntok = 0, misses = 0, rand_calls = 0, max_recs = 0, max_docs = 0;
+  uint64_t lstate_end = 2008;
+  bool loaded = false;
+  uint64_t cursor = 0;
+  // device
+  DevMem d_tok_row, d_doc_tok, d_doc_rec, d_doc_lcg, d_vocab_row, d_starts, d_init, d_exptab, d_rec, d_out, d_err,
+      d_rows_read;
+  // stats and HIP-event kernel timing
+  uint64_t st_batches = 0, st_docs = 0, st_pos = 0;
+  bool timing = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  double ms[ST_N] = {0};
+  uint64_t cnt[ST_N] = {0};
+};
+
+namespace {
+
+hipEvent_t ev_begin(swps_s2v *m) {
+  if (!m->timing) return nullptr;
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  (void)hipEventRecord(e, m->s);
+  return e;
+}
+void ev_end(swps_s2v *m, int k, hipEvent_t b) {
+  if (!b) return;
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  (void)hipEventRecord(e, m->s);
+  m->pending.push_back({k, {b, e}});
+}
+void ev_resolve(swps_s2v *m) {
+  for (auto &p : m->pending) {
+    float t = 0;
+    (void)hipEventElapsedTime(&t, p.second.first, p.second.second);
+    m->ms[p.first] += t;
+    m->cnt[p.first]++;
+    (void)hipEventDestroy(p.second.first);
+    (void)hipEventDestroy(p.second.second);
+  }
+  m->pending.clear();
+}
+
+// run-length unigram^0.75 table of word2vec.h:398-425 over a vocab in std::map
+// (ascending key) order: word i owns slots [st[i], st[i+1]).  The literal walk
+// moves to word i+1 after the first slot a with a/T > d1_i.
+void s2v_unigram_starts(const std::vector<std::pair<uint64_t, int32_t>> &vc, uint64_t T, std::vector<uint64_t> &st) {
+  const size_t V = vc.size();
+  double pw = 0;
+  for (auto &kc : vc) pw += std::pow(kc.second, 0.75);
+  st.assign(V + 1, T);
+  st[0] = 0;
+  double d1 = std::pow(vc[0].second, 0.75) / (double)pw;
+  for (size_t i = 0; i + 1 < V; i++) {
+    const uint64_t lo = st[i];
+    auto pred = [&](uint64_t a) { return (int64_t)a / (double)T > d1; };
+    uint64_t a = (uint64_t)std::max<double>((double)lo, std::floor(d1 * (double)T));
+    if (a > T) a = T;
+    while (a > lo && pred(a - 1)) a--;
+    while (a < T && !pred(a)) a++;
+    if (a >= T) break;  // word i runs to the end; later words get no slots
+    st[i + 1] = a + 1;
+    d1 += std::pow(vc[i + 1].second, 0.75) / (double)pw;
+  }
+}
+
+// The host schedule: Sent2Vec::train's loop (sent2vec.cpp:95-103) replayed
+// over the parsed corpus.  tok_keys/line_off describe every line, sent_ids
+// the BKDR hash of each line (sent2vec.cpp:75).
+int s2v_ingest(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std::vector<uint64_t> &line_off,
+               const std::vector<uint64_t> &sent_ids) {
+  const uint64_t nl = line_off.size() - 1;
+  const int D = m->D, B = m->cfg.minibatch, N = m->N, S = 2 * m->W + m->N + 1;
+  const uint64_t T = m->cfg.unigram_size;
+  hipStream_t s = m->s;
+  SWPS_HIP(hipSetDevice(m->t->cfg.device));
+  std::vector<uint8_t> valid(nl);
+  for (uint64_t l = 0; l < nl; l++)
+    valid[l] = (int64_t)(line_off[l + 1] - line_off[l]) >= (int64_t)m->cfg.min_sentence_length;
+  // keys the server already holds (the loaded word vectors)
+  uint64_t have = 0, got = 0;
+  SWPS_TRY(swps_table_size(m->t, &have));
+  std::vector<uint64_t> tk(std::max<uint64_t>(have, 1));
+  SWPS_TRY(swps_table_keys(m->t, tk.data(), tk.size(), &got));
+  std::unordered_set<uint64_t> present(tk.begin(), tk.begin() + got);
+  GlibcRand rnd(m->cfg.rand_seed);
+  for (uint64_t i = 0; i < m->cfg.rand_offset; i++) (void)rnd.next();
+  auto rand_val = [&](int32_t r) { return ((double)(r / (float)2147483647) - 0.5) / (double)(size_t)D; };
+  std::vector<uint64_t> miss_keys;
+  std::vector<double> miss_rows;     // [h | v | h2 = 0 | v2 = 0] per miss
+  std::unordered_set<uint64_t> lk;   // MiniBatch::_local_keys: one object, cleared per minibatch
+  std::vector<uint64_t> vocab_keys;  // concatenated minibatch vocabs (std::map order)
+  std::vector<uint64_t> starts_all;
+  std::vector<int32_t> init;  // [docs][D] rand() outputs
+  std::vector<uint64_t> doc_tok_keys;
+  m->batches.clear();
+  m->doc_id.clear();
+  m->doc_tok.assign(1, 0);
+  m->doc_rec.assign(1, 0);
+  m->doc_lcg.clear();
+  m->misses = m->max_recs = m->max_docs = 0;
+  uint64_t lstate = 2008ULL;  // utils/random.h:44-47
+  uint64_t li = 0;
+  std::unordered_map<uint64_t, int32_t> freq;
+  while (true) {
+    // gather_keys(file, line_id, B) (word2vec.h:323-377)
+    lk.clear();
+    freq.clear();
+    int cnt = 0;
+    for (uint64_t j = li; j < nl;) {
+      const uint64_t l = j++;
+      if (!valid[l]) continue;
+      for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) {
+        auto it = freq.find(tok_keys[i]);
+        if (it != freq.end())
+          it->second++;
+        else {
+          freq.emplace(tok_keys[i], 1);
+          lk.insert(tok_keys[i]);
+        }
+      }
+      if (++cnt > B) break;
+    }
+    if (lk.size() < 5) break;  // sent2vec.cpp:97
+    if (freq.count(0))
+      return fail(SWPS_E_UNSUPPORTED, "a minibatch vocab holds key 0 (atoi of a non-numeric word): the reference "
+                                      "redraws negatives that hit it, a data-dependent draw count");
+    // MiniBatch::pull: one WParam (2·D rand()) per pulled key in `_local_keys`
+    // order; a miss is inserted with it (server.h:143-150, accessmethod.h:63-70)
+    for (uint64_t k : lk) {
+      if (present.count(k)) {
+        for (int i = 0; i < 2 * D; i++) (void)rnd.next();
+        continue;
+      }
+      const size_t o = miss_rows.size();
+      miss_rows.resize(o + 4 * (size_t)D, 0.0);
+      for (int i = 0; i < 2 * D; i++) miss_rows[o + i] = rand_val(rnd.next());
+      for (uint64_t i = 0; i < m->cfg.rand_insert_extra; i++) (void)rnd.next();
+      miss_keys.push_back(k);
+      present.insert(k);
+      m->misses++;
+    }
+    std::vector<std::pair<uint64_t, int32_t>> vc(freq.begin(), freq.end());
+    std::sort(vc.begin(), vc.end());
+    std::vector<uint64_t> st;
+    s2v_unigram_starts(vc, T, st);
+    swps_s2v::Batch b{m->doc_id.size(), 0, vocab_keys.size(), starts_all.size(), (uint32_t)vc.size(), 0};
+    for (auto &kc : vc) vocab_keys.push_back(kc.first);
+    starts_all.insert(starts_all.end(), st.begin(), st.end());
+    // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not
+    int lc = 0;
+    while (lc <= B && li < nl) {
+      const uint64_t l = li++;
+      lc++;
+      if (!valid[l]) continue;
+      const uint64_t L = line_off[l + 1] - line_off[l];
+      m->doc_id.push_back(sent_ids[l]);
+      for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) doc_tok_keys.push_back(tok_keys[i]);
+      m->doc_tok.push_back(doc_tok_keys.size());
+      m->doc_rec.push_back(m->doc_rec.back() + L * (uint64_t)m->cfg.niters);
+      for (int i = 0; i < D; i++) init.push_back(rnd.next());
+      m->doc_lcg.push_back(lstate);
+      lstate = lcg_jump(lstate, (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1)), kLcgA, kLcgC);
+    }
+    b.d1 = m->doc_id.size();
+    b.recs = m->doc_rec[b.d1] - m->doc_rec[b.d0];
+    m->max_recs = std::max(m->max_recs, b.recs);
+    m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
+    m->batches.push_back(b);
+  }
+  m->lstate_end = lstate;
+  m->rand_calls = rnd.produced;  // includes the rand_offset skipped above
+  m->nlines = nl;
+  m->ntok = doc_tok_keys.size();
+  // misses into the table (they persist for later minibatches, like the
+  // server's inserts); rows = [h | v | h2 = 0 | v2 = 0]
+  if (!miss_keys.empty()) {
+    DevMem dk, dv;
+    SWPS_TRY(upload(dk, miss_keys, s));
+    if (m->f64) {
+      SWPS_TRY(upload(dv, miss_rows, s));
+      SWPS_HIP(hipStreamSynchronize(s));
+    } else {
+      std::vector<float> fr(miss_rows.begin(), miss_rows.end());
+      SWPS_TRY(upload(dv, fr, s));
+      SWPS_HIP(hipStreamSynchronize(s));
+    }
+    SWPS_TRY(swps_assign(m->t, dk.as<uint64_t>(), miss_keys.size(), dv.p));
+  }
+  // key -> word-table row for the minibatch vocabs and every sentence token
+  {
+    DevMem dk, dt;
+    SWPS_TRY(upload(dk, vocab_keys, s));
+    SWPS_TRY(m->d_vocab_row.ensure(std::max<size_t>(vocab_keys.size(), 1) * 4));
+    SWPS_TRY(table_lookup(m->t, dk.as<uint64_t>(), vocab_keys.size(), m->d_vocab_row.as<uint32_t>(), s));
+    SWPS_TRY(upload(dt, doc_tok_keys, s));
+    SWPS_TRY(m->d_tok_row.ensure(std::max<size_t>(doc_tok_keys.size(), 1) * 4));
+    SWPS_TRY(table_lookup(m->t, dt.as<uint64_t>(), doc_tok_keys.size(), m->d_tok_row.as<uint32_t>(), s));
+    SWPS_TRY(table_check_error(m->t, s));  // syncs; every key is present by now
+  }
+  SWPS_TRY(upload(m->d_starts, starts_all, s));
+  SWPS_TRY(upload(m->d_doc_tok, m->doc_tok, s));
+  SWPS_TRY(upload(m->d_doc_rec, m->doc_rec, s));
+  SWPS_TRY(upload(m->d_doc_lcg, m->doc_lcg, s));
+  SWPS_TRY(upload(m->d_init, init, s));
+  std::vector<float> ex(1000);
+  for (int i = 0; i < 1000; i++) {  // ExpTable (word2vec.h:241-253)
+    float x = (i / (float)1000 * 2 - 1) * 6;
+    float e = (float)std::exp((double)x);
+    ex[i] = e / (e + 1);
+  }
+  SWPS_TRY(upload(m->d_exptab, ex, s));
+  const uint64_t nd = m->doc_id.size();
+  SWPS_TRY(m->d_out.ensure(std::max<uint64_t>(nd, 1) * D * (m->f64 ? 8 : 4)));
+  SWPS_TRY(m->d_err.ensure(std::max<uint64_t>(nd, 1) * 4));
+  SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(m->max_recs, 1) * (uint64_t)S * 4));
+  SWPS_HIP(hipStreamSynchronize(s));  // host vectors above go out of scope
+  m->loaded = true;
+  m->cursor = 0;
+  return SWPS_OK;
+}
+
+template <typename T, int NCH> void launch_docs(const S2VDocArgs<T> &a, hipStream_t s) {
+  k_s2v_docs<T, NCH, 8><<<nblk(a.nd * 64), 256, 0, s>>>(a);
+}
+
+template <typename T> int s2v_batch(swps_s2v *m) {
+  const swps_s2v::Batch &b = m->batches[m->cursor];
+  hipStream_t s = m->s;
+  const uint64_t nd = b.d1 - b.d0;
+  m->cursor++;
+  m->st_batches++;
+  if (nd == 0) return SWPS_OK;
+  S2VRecArgs ra{m->d_tok_row.as<uint32_t>(),
+                m->d_doc_tok.as<uint64_t>(),
+                m->d_doc_rec.as<uint64_t>(),
+                m->d_doc_lcg.as<uint64_t>(),
+                b.d0,
+                nd,
+                m->d_vocab_row.as<uint32_t>() + b.v0,
+                m->d_starts.as<uint64_t>() + b.s0,
+                b.U,
+                m->cfg.unigram_size,
+                ~0ULL / m->cfg.unigram_size,
+                m->W,
+                m->N,
+                m->cfg.niters,
+                ~0ULL / (uint64_t)m->W,
+                m->d_rec.as<int32_t>()};
+  hipEvent_t e0 = ev_begin(m);
+  k_s2v_records<<<nblk(nd * 64), 256, 0, s>>>(ra);
+  SWPS_HIP(hipGetLastError());
+  ev_end(m, ST_REC, e0);
+  S2VDocArgs<T> da{m->d_rec.as<int32_t>(), m->d_doc_tok.as<uint64_t>(), m->d_doc_rec.as<uint64_t>(), b.d0, nd,
+                   m->d_init.as<int32_t>(), m->t->rows.as<T>(), m->d_exptab.as<float>(), m->D, m->W, m->N,
+                   m->cfg.niters, m->cfg.alpha, m->d_out.as<T>(), m->d_err.as<float>(),
+                   m->d_rows_read.as<unsigned long long>()};
+  hipEvent_t e1 = ev_begin(m);
+  switch (m->NCH) {
+    case 1: launch_docs<T, 1>(da, s); break;
+    case 2: launch_docs<T, 2>(da, s); break;
+    case 3: launch_docs<T, 3>(da, s); break;
+    default: launch_docs<T, 4>(da, s); break;
+  }
+  SWPS_HIP(hipGetLastError());
+  ev_end(m, ST_DOC, e1);
+  m->st_docs += nd;
+  m->st_pos += b.recs;
+  return SWPS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int swps_s2v_create(swps_table *t, const swps_s2v_cfg *cfg, swps_s2v **out) {
+  if (!t || !cfg || !out) return fail(SWPS_E_CFG, "null argument");
+  *out = nullptr;
+  if (t->cfg.layout != SWPS_LAYOUT_W2V) return fail(SWPS_E_CFG, "word table layout must be SWPS_LAYOUT_W2V");
+  if (cfg->window <= 0 || 2 * cfg->window > 64) return fail(SWPS_E_CFG, "window must be in [1, 32]");
+  if (cfg->negative < 0 || cfg->negative > 62) return fail(SWPS_E_CFG, "negative must be in [0, 62]");
+  if (cfg->minibatch <= 0) return fail(SWPS_E_CFG, "minibatch must be positive");
+  if (cfg->niters <= 0) return fail(SWPS_E_CFG, "niters must be positive (sent2vec.cpp:28)");
+  if (cfg->unigram_size == 0 || cfg->unigram_size > (1ULL << 40)) return fail(SWPS_E_CFG, "unigram_size out of range");
+  const int D = t->cfg.dim;
+  const int E = t->cfg.dtype == SWPS_F64 ? 2 : 4;
+  if (D % E) return fail(SWPS_E_UNSUPPORTED, "dim must be a multiple of 16 bytes (4 fp32 / 2 fp64)");
+  const int nch = (D / E + 63) / 64;
+  if (nch > 4) return fail(SWPS_E_UNSUPPORTED, "dim too large (max 1024 fp32 / 512 fp64)");
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  swps_s2v *m = new swps_s2v();
+  m->t = t;
+  m->cfg = *cfg;
+  m->D = D;
+  m->W = cfg->window;
+  m->N = cfg->negative;
+  m->NCH = nch;
+  m->f64 = t->cfg.dtype == SWPS_F64;
+  m->s = t->stream;
+  m->timing = cfg->profile != 0;
+  int rc = m->d_rows_read.ensure(16);
+  if (!rc && hipMemset(m->d_rows_read.p, 0, 16) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return SWPS_OK;
+}
+
+int swps_s2v_destroy(swps_s2v *m) {
+  if (!m) return SWPS_OK;
+  (void)hipSetDevice(m->t->cfg.device);
+  (void)hipStreamSynchronize(m->s);
+  ev_resolve(m);
+  delete m;
+  (void)hipGetLastError();  // leave no sticky error from the calls above
+  return SWPS_OK;
+}
+
+// LineFileReader + split(" ") + atoi keys (word2vec.h:206,212-224); the
+// sentence id is BKDR of the whole line (sent2vec.cpp:75).
+int swps_s2v_load_text(swps_s2v *m, const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return fail(SWPS_E_IO, std::string("no such file or directory: ") + path);
+  std::vector<uint64_t> keys, off{0}, ids;
+  char *buf = nullptr;
+  size_t cap = 0;
+  ssize_t n;
+  std::string word;
+  while ((n = getdelim(&buf, &cap, '\n', f)) >= 0) {
+    if (n >= 1 && buf[n - 1] == '\n') buf[--n] = 0;
+    const size_t len = strlen(buf);  // std::string(cline) stops at a NUL
+    ids.push_back(bkdr(buf));
+    size_t i = 0;
+    while (i < len) {
+      while (i < len && buf[i] == ' ') i++;
+      if (i >= len) break;
+      size_t j = i;
+      while (j < len && buf[j] != ' ') j++;
+      word.assign(buf + i, j - i);
+      keys.push_back((uint64_t)(int64_t)atoi(word.c_str()));
+      i = j;
+    }
+    off.push_back(keys.size());
+  }
+  free(buf);
+  fclose(f);
+  return s2v_ingest(m, keys, off, ids);
+}
+
+int swps_s2v_load_tokens(swps_s2v *m, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,
+                         uint64_t nlines, const uint64_t *sent_ids) {
+  if (line_off[0] != 0 || line_off[nlines] != ntok) return fail(SWPS_E_CFG, "line_off must span [0, ntok]");
+  return s2v_ingest(m, std::vector<uint64_t>(tok_keys, tok_keys + ntok),
+                    std::vector<uint64_t>(line_off, line_off + nlines + 1),
+                    std::vector<uint64_t>(sent_ids, sent_ids + nlines));
+}
+
+int swps_s2v_info(swps_s2v *m, uint64_t *o) {
+  o[0] = m->nlines;
+  o[1] = m->doc_id.size();
+  o[2] = m->batches.size();
+  o[3] = m->ntok;
+  o[4] = m->misses;
+  o[5] = m->max_docs;
+  o[6] = m->max_recs;
+  o[7] = m->rand_calls;
+  o[8] = m->lstate_end;
+  return SWPS_OK;
+}
+
+int swps_s2v_train_batches(swps_s2v *m, uint64_t count) {
+  if (!m->loaded) return fail(SWPS_E_STATE, "load a corpus first");
+  if (m->batches.empty()) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(m->t->cfg.device));
+  for (uint64_t i = 0; i < count; i++) {
+    if (m->cursor == m->batches.size()) m->cursor = 0;  // another pass over the corpus
+    SWPS_TRY(m->f64 ? s2v_batch<double>(m) : s2v_batch<float>(m));
+  }
+  return SWPS_OK;
+}
+
+int swps_s2v_train(swps_s2v *m) {
+  if (!m->loaded) return fail(SWPS_E_STATE, "load a corpus first");
+  if (m->cursor != 0 && m->cursor != m->batches.size()) return fail(SWPS_E_STATE, "not at the corpus start");
+  m->cursor = 0;
+  SWPS_TRY(swps_s2v_train_batches(m, m->batches.size()));
+  return swps_s2v_sync(m);
+}
+
+int swps_s2v_sync(swps_s2v *m) {
+  SWPS_HIP(hipSetDevice(m->t->cfg.device));
+  SWPS_HIP(hipStreamSynchronize(m->s));
+  ev_resolve(m);
+  return SWPS_OK;
+}
+
+int swps_s2v_docs(swps_s2v *m, uint64_t *ids, double *vecs, float *errs, uint64_t cap, uint64_t *n) {
+  SWPS_TRY(swps_s2v_sync(m));
+  const uint64_t nd = m->doc_id.size();
+  *n = nd;
+  if (cap < nd) return fail(SWPS_E_CFG, "buffer too small");
+  if (ids) std::copy(m->doc_id.begin(), m->doc_id.end(), ids);
+  if (nd && vecs) {
+    const size_t cnt = nd * (size_t)m->D;
+    if (m->f64) {
+      SWPS_HIP(hipMemcpy(vecs, m->d_out.p, cnt * 8, hipMemcpyDeviceToHost));
+    } else {
+      std::vector<float> h(cnt);
+      SWPS_HIP(hipMemcpy(h.data(), m->d_out.p, cnt * 4, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < cnt; i++) vecs[i] = h[i];
+    }
+  }
+  if (nd && errs) SWPS_HIP(hipMemcpy(errs, m->d_err.p, nd * 4, hipMemcpyDeviceToHost));
+  return SWPS_OK;
+}
+
+// the reference's output file (sent2vec.cpp:84): "sent_id\tVec:\tv0 v1 ... \n"
+// (Vec::operator<<, utils/vec1.h:112-118) at ostream precision 6, for the
+// sentences of the minibatches trained so far in this pass.
+int swps_s2v_dump(swps_s2v *m, const char *path) {
+  SWPS_TRY(swps_s2v_sync(m));
+  const uint64_t nd = m->doc_id.size();
+  const uint64_t done = m->cursor ? m->batches[m->cursor - 1].d1 : 0;
+  const int D = m->D;
+  std::vector<double> all(std::max<uint64_t>(nd, 1) * D);
+  uint64_t n = 0;
+  SWPS_TRY(swps_s2v_docs(m, nullptr, all.data(), nullptr, nd, &n));
+  FILE *f = fopen(path, "w");
+  if (!f) return fail(SWPS_E_IO, std::string("cannot write ") + path);
+  for (uint64_t d = 0; d < done; d++) {
+    fprintf(f, "%llu\tVec:\t", (unsigned long long)m->doc_id[d]);
+    for (int i = 0; i < D; i++) fprintf(f, "%g ", all[d * D + i]);
+    fputc('\n', f);
+  }
+  fclose(f);
+  return SWPS_OK;
+}
+
+// [batches, sentences, positions, context rows read, target rows read]
+int swps_s2v_stats(swps_s2v *m, uint64_t *o) {
+  SWPS_TRY(swps_s2v_sync(m));
+  uint64_t rr[2] = {0, 0};
+  SWPS_HIP(hipMemcpy(rr, m->d_rows_read.p, 16, hipMemcpyDeviceToHost));
+  o[0] = m->st_batches;
+  o[1] = m->st_docs;
+  o[2] = m->st_pos;
+  o[3] = rr[0];
+  o[4] = rr[1];
+  return SWPS_OK;
+}
+
+int swps_s2v_set_profile(swps_s2v *m, int32_t on) {
+  SWPS_TRY(swps_s2v_sync(m));
+  m->timing = on != 0;
+  return SWPS_OK;
+}
+
+// out[2k] = ms, out[2k+1] = launches for k in {records, docs}
+int swps_s2v_kernel_times(swps_s2v *m, double *out, int32_t reset) {
+  SWPS_TRY(swps_s2v_sync(m));
+  for (int k = 0; k < ST_N; k++) {
+    out[2 * k] = m->ms[k];
+    out[2 * k + 1] = (double)m->cnt[k];
+    if (reset) {
+      m->ms[k] = 0;
+      m->cnt[k] = 0;
+    }
+  }
+  return SWPS_OK;
+}
+
+void *swps_s2v_stream(swps_s2v *m) { return (void *)m->s; }
+
+}  // extern "C"

@@ -347,6 +347,7 @@ int swps_table_destroy(swps_table *t) {
     (void)hipStreamDestroy(t->stream);
   }
   delete t;
+  (void)hipGetLastError();  // leave no sticky error from the calls above
   return SWPS_OK;
 }
 

@@ -1302,6 +1302,7 @@ int swps_w2v_destroy(swps_w2v *w) {
   (void)hipStreamSynchronize(w->s);
   if (w->h_small) (void)hipHostFree(w->h_small);
   delete w;
+  (void)hipGetLastError();  // leave no sticky error from the calls above
   return SWPS_OK;
 }
 

@@ -28,6 +28,32 @@ def zipf_corpus(path, nlines, vocab, seed, lo=10, hi=30, s=1.0, extra_lines=()):
     return path
 
 
+def int_corpus(path, nlines, vocab, seed, lo=5, hi=25, s=1.0):
+    """Zipf(s) corpus of integer tokens 1..vocab (word2vec.h's atoi keys;
+    sent2vec / word2vec_local input)."""
+    rng = np.random.default_rng(seed)
+    p = 1.0 / np.arange(1, vocab + 1) ** s
+    p /= p.sum()
+    with open(path, "w") as f:
+        for _ in range(nlines):
+            n = int(rng.integers(lo, hi + 1))
+            f.write(" ".join(str(x + 1) for x in rng.choice(vocab, n, p=p)) + "\n")
+    return path
+
+
+def word_dump(path, nwords, dim, seed, first=1):
+    """A word2vec parameter dump in the reference's text format
+    (sparsetable.h:63-70 + WParam operator<<: "key\\tv...\\th...") for keys
+    first..first+nwords-1, values printed at ostream precision 6."""
+    rng = np.random.default_rng(seed)
+    with open(path, "w") as f:
+        for k in rng.permutation(np.arange(first, first + nwords)):
+            v = (rng.random(dim) - 0.5) / dim * 40
+            h = (rng.random(dim) - 0.5) / dim * 40
+            f.write("%d\t%s\t%s\n" % (k, " ".join("%g" % x for x in v), " ".join("%g" % x for x in h)))
+    return path
+
+
 @pytest.fixture(scope="session")
 def oracle_mod():
     import oracle

@@ -1,0 +1,126 @@
+"""sent2vec on the GPU (libswps.so) against the oracle, same inputs
+(apps/sent2vec/sent2vec.cpp on word2vec.h's MiniBatch, nthreads = 1).
+
+Bit-exact: sentence ids, the LCG end state, the number of rand() calls, the
+rows of keys the minibatch pulls insert.  fp64 word table: sentence vectors
+within 1e-9 relative of the oracle (summation order of the dot products
+only).  fp32 word table: within 1e-5 relative of the oracle's fp32-storage
+mode."""
+import numpy as np
+import pytest
+
+from conftest import int_corpus, word_dump
+
+pytestmark = pytest.mark.gpu
+
+
+def run_pair(lib, oracle_mod, tmp_path, dtype="f64", D=16, W=3, N=4, B=20, niters=2, min_len=1, extra=0,
+             vocab=150, dump_vocab=120, nlines=130, table=10 ** 6, seed=5, lo=5, hi=25):
+    corpus = int_corpus(str(tmp_path / "c.txt"), nlines, vocab, seed=seed, lo=lo, hi=hi)
+    dump = word_dump(str(tmp_path / "w.txt"), dump_vocab, D, seed=seed + 1)
+    orc = oracle_mod.S2V(corpus, D, window=W, negative=N, minibatch=B, niters=niters, min_sentence_length=min_len,
+                         table_size=table, storage_f32=(dtype == "f32"), rand_offset=2, rand_insert_extra=extra)
+    orc.load_words(dump)
+    orc.train()
+    t = lib.Table("w2v", dim=D, capacity=vocab + 64, dtype=dtype)
+    s = lib.Sent2Vec(t, window=W, negative=N, minibatch=B, niters=niters, min_sentence_length=min_len,
+                     unigram_size=table, rand_offset=2, rand_insert_extra=extra)
+    s.load_word_vector(dump)
+    s.load_text(corpus)
+    s.train()
+    return orc, t, s
+
+
+@pytest.mark.parametrize("W,N,B,niters,extra", [(3, 4, 20, 2, 0), (5, 5, 7, 1, 32), (2, 3, 45, 3, 0),
+                                                (4, 2, 1, 1, 0)])
+def test_s2v_f64_matches_oracle(lib, oracle_mod, gpu, tmp_path, W, N, B, niters, extra):
+    orc, t, s = run_pair(lib, oracle_mod, tmp_path, W=W, N=N, B=B, niters=niters, extra=extra)
+    io, vo, eo = orc.docs()
+    ig, vg, eg = s.docs()
+    so, info = orc.stats(), s.info()
+    assert len(io) == len(ig) > 0 and np.array_equal(io, ig)
+    assert info["batches"] == so["batches"] and info["inserted"] == so["inserted"]
+    assert info["lstate"] == so["rng"] and info["rand_calls"] == so["rand_calls"]
+    assert np.allclose(vg, vo, rtol=1e-9, atol=1e-12), np.abs(vg - vo).max()
+    assert np.allclose(eg, eo, rtol=1e-5, atol=1e-9)
+    assert abs(s.error() - so["error_sum"] / len(io)) <= 1e-6 * max(1.0, abs(s.error()))
+    # keys the pulls inserted carry the oracle's rand() rows
+    keys = t.keys()
+    import torch
+    rows = t.export(torch.as_tensor(keys.astype(np.int64), device="cuda")).double().cpu().numpy()
+    ref, ok = orc.word_rows(keys)
+    assert ok
+    assert np.array_equal(rows[:, :2 * t.dim], ref)
+
+
+def test_s2v_f32_matches_oracle_f32(lib, oracle_mod, gpu, tmp_path):
+    orc, t, s = run_pair(lib, oracle_mod, tmp_path, dtype="f32", D=32, W=5, N=5, B=15, niters=2)
+    _, vo, _ = orc.docs()
+    _, vg, _ = s.docs()
+    rel = np.abs(vg - vo) / np.maximum(np.abs(vo), 1e-3)
+    assert rel.max() < 1e-5, rel.max()
+
+
+def test_s2v_short_lines_and_tail(lib, oracle_mod, gpu, tmp_path):
+    """min_sentence_length > 1: short lines are read (they count toward the
+    B+1 lines of a minibatch) but neither gathered nor trained; the run stops
+    at the first minibatch with fewer than 5 keys (sent2vec.cpp:97)."""
+    orc, t, s = run_pair(lib, oracle_mod, tmp_path, B=9, min_len=8, lo=1, hi=20, nlines=90, extra=32)
+    io, vo, _ = orc.docs()
+    ig, vg, _ = s.docs()
+    assert np.array_equal(io, ig)
+    assert np.allclose(vg, vo, rtol=1e-9, atol=1e-12)
+    assert s.info()["lstate"] == orc.stats()["rng"]
+
+
+def test_s2v_dump_format(lib, oracle_mod, gpu, tmp_path):
+    orc, t, s = run_pair(lib, oracle_mod, tmp_path, B=30, niters=1)
+    out = str(tmp_path / "sent.txt")
+    s.dump(out)
+    ids, vecs, _ = s.docs()
+    lines = open(out).read().split("\n")
+    assert lines[-1] == "" and len(lines) == len(ids) + 1
+    for i in (0, len(ids) // 2, len(ids) - 1):  # Vec::operator<< (vec1.h:112-118)
+        exp = "%d\tVec:\t" % ids[i] + "".join("%g " % x for x in vecs[i])
+        assert lines[i] == exp
+
+
+def test_s2v_rejects_key_zero(lib, gpu, tmp_path):
+    """atoi of a non-numeric word is key 0; the reference redraws negatives
+    that hit it (a data-dependent draw count): refused, not silently wrong."""
+    p = tmp_path / "c.txt"
+    p.write_text("1 2 3 4 5 6 x\n" * 10)
+    dump = word_dump(str(tmp_path / "w.txt"), 10, 8, seed=1)
+    t = lib.Table("w2v", dim=8, capacity=64, dtype="f64")
+    s = lib.Sent2Vec(t, window=2, negative=2, minibatch=3, unigram_size=10 ** 5)
+    s.load_word_vector(dump)
+    with pytest.raises(lib.SwpsError, match="key 0"):
+        s.load_text(str(p))
+
+
+def test_s2v_bench_shape_properties(lib, gpu):
+    """D=300, 10k sentences of 50-200 tokens (BASELINE config 5's shape at
+    1/1000 scale): run-to-run bit-identical, finite, every position counted."""
+    rng = np.random.default_rng(5)
+    V, nd = 20000, 10000
+    p = 1.0 / np.arange(1, V + 1)
+    cdf = np.cumsum(p / p.sum())
+    lens = rng.integers(50, 201, nd)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    toks = (np.minimum(np.searchsorted(cdf, rng.random(int(off[-1]))), V - 1) + 1).astype(np.uint64)
+    ids = np.arange(1, nd + 1, dtype=np.uint64) * 2654435761
+    outs = []
+    for _ in range(2):
+        t = lib.Table("w2v", dim=300, capacity=V + 16, dtype="f32", init="hash", seed=3)
+        import torch
+        keys = torch.arange(1, V + 1, dtype=torch.int64, device="cuda")
+        t.pull(keys)  # the word table: hash-initialised rows for every word
+        s = lib.Sent2Vec(t, window=5, negative=5, minibatch=4096, niters=1)
+        s.load_tokens(toks, off, ids)
+        s.train()
+        outs.append((s.docs()[1], s.stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.isfinite(outs[0][0]).all()
+    st = outs[0][1]
+    assert st["docs"] == nd and st["positions"] == int(off[-1])
+    assert st["tgt_rows"] >= st["positions"]  # the positive target is never skipped
