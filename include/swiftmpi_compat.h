@@ -1,0 +1,417 @@
+/*
+ * swiftmpi_compat.h — C++11 host-side drop-in for SwiftMPI's parameter-server
+ * key-value API (src/parameter) and its app entry points (src/apps), over the
+ * C ABI of libswps.so (swps.h).  Header-only; needs no MPI, ZeroMQ, glog or
+ * sparsehash.  Link with -lswps.
+ *
+ * Reference interfaces mirrored (paths relative to logicxin/SwiftMPI src/):
+ *   ConfigParser / global_config()     utils/ConfigParser.h:25-133
+ *   LocalParamCache<Key,Param,Grad>    parameter/param.h:13-68
+ *   GlobalPullAccess<Key,Val,Grad>     parameter/global_pull_access.h:15-118
+ *   GlobalPushAccess<Key,Val,Grad>     parameter/global_push_access.h:15-106
+ *   Cluster<Worker,Server,Key>         cluster/cluster.h:9-140 (initialize/finalize)
+ *   Word2VecApp                        apps/word2vec/word2vec_global.h:541-748 + w2v.cpp
+ *   Sent2VecApp                        apps/sent2vec/sent2vec.cpp:14-257
+ *   LRApp                              apps/logistic/lr.cpp:133-509
+ *
+ * Two levels, as in swps.h:
+ *   * PS level: an app keeps its own learn_instance on the host and calls
+ *     pull_with_barrier / push_with_barrier exactly as before; keys and
+ *     values cross into the HBM shard through swps_pull_h / swps_push_h.
+ *     A PullCodec / PushCodec specialisation states how the app's value
+ *     types map onto the reference's wire layouts (word2vec_global.h:122-156,
+ *     lr.cpp:32-43) — the role BinaryBuffer operator<< / >> play there.
+ *   * App level: the whole minibatch loop runs on the GPU (swps_w2v_*,
+ *     swps_s2v_*, swps_lr_*); the classes below read the same config keys
+ *     as the reference's app constructors.
+ * Errors: the reference CHECK-aborts; here every failure throws SwpsError
+ * carrying swps_last_error().
+ */
+#ifndef SWIFTMPI_COMPAT_H_
+#define SWIFTMPI_COMPAT_H_
+
+#include <cstdint>
+#include <cstdlib>
+#include <fstream>
+#include <limits>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <utility>
+#include <vector>
+
+#include "swps.h"
+
+namespace swift_snails {
+
+struct SwpsError : std::runtime_error {
+  int code;
+  SwpsError(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+inline void swps_check(int rc) {
+  if (rc != SWPS_OK) throw SwpsError(rc, swps_last_error());
+}
+
+/* ---- utils/ConfigParser.h ------------------------------------------------ */
+class ConfigValue {
+ public:
+  ConfigValue() {}
+  explicit ConfigValue(const std::string &s) : _s(s) {}
+  int to_int32() const { return std::atoi(_s.c_str()); }
+  float to_float() const { return (float)std::atof(_s.c_str()); }
+  std::string to_string() const { return _s; }
+  bool empty() const { return _s.empty(); }
+
+ private:
+  std::string _s;
+};
+
+/* "[section]" headers, "key: value" lines, '#' comments, "import path";
+ * the first definition of a key wins (std::map::insert); get() of a missing
+ * key throws (the reference CHECK-fails, ConfigParser.h:64-69). */
+class ConfigParser {
+ public:
+  void load_conf(const std::string &path) { _path = path; }
+  void parse() { parse_file(_path); }
+  ConfigValue get(const std::string &section, const std::string &key) const {
+    auto s = _data.find(section);
+    if (s != _data.end()) {
+      auto k = s->second.find(key);
+      if (k != s->second.end()) return ConfigValue(k->second);
+    }
+    throw SwpsError(SWPS_E_CFG, "no such key:\t[" + section + "]\t" + key);
+  }
+  bool has(const std::string &section, const std::string &key) const {
+    auto s = _data.find(section);
+    return s != _data.end() && s->second.count(key);
+  }
+
+ private:
+  static std::string trim(const std::string &s) {
+    const size_t a = s.find_first_not_of(" \t\n\r");
+    if (a == std::string::npos) return std::string();
+    const size_t b = s.find_last_not_of(" \t\n\r");
+    return s.substr(a, b - a + 1);
+  }
+  void parse_file(const std::string &path) {
+    std::ifstream f(path.c_str());
+    if (!f) throw SwpsError(SWPS_E_IO, "conf can not open: " + path);
+    std::string line, cur;
+    while (std::getline(f, line)) {
+      line = trim(line);
+      if (line.empty() || line[0] == '#') continue;
+      if (line.compare(0, 6, "import") == 0) {
+        const std::string p = trim(line.substr(line.find(' ') + 1));
+        if (p == path) throw SwpsError(SWPS_E_CFG, "recursive import");
+        parse_file(p);
+        continue;
+      }
+      if (line[0] == '[' && line[line.size() - 1] == ']') {
+        cur = trim(line.substr(1, line.size() - 2));
+        continue;
+      }
+      const size_t c = line.find(':');
+      if (c == std::string::npos) throw SwpsError(SWPS_E_CFG, "bad config line: " + line);
+      _data[cur].insert(std::make_pair(trim(line.substr(0, c)), trim(line.substr(c + 1))));
+    }
+  }
+  std::string _path;
+  std::map<std::string, std::map<std::string, std::string> > _data;
+};
+
+inline ConfigParser &global_config() {
+  static ConfigParser c;
+  return c;
+}
+
+/* ---- wire codecs ----------------------------------------------------------
+ * PullCodec<Val>:  typedef wire_t (double for word2vec, float for LR);
+ *                  static int elems();  static void decode(const wire_t*, Val&)
+ * PushCodec<Grad>: static void encode(Grad&, wire_t*)  — writes the MEAN
+ *                  gradient the reference's serializer sends and resets it
+ *                  (word2vec_global.h:122-134, lr.cpp:32-38). */
+template <class Val> struct PullCodec;
+template <class Grad> struct PushCodec;
+
+/* The shard this process serves and pulls from (one GPU = one shard). */
+inline swps_table *&global_swps_table() {
+  static swps_table *t = nullptr;
+  return t;
+}
+
+/* ---- parameter/param.h ---------------------------------------------------- */
+template <typename Key, typename Param, typename Grad> class LocalParamCache {
+ public:
+  typedef Key key_t;
+  typedef Param param_t;
+  typedef Grad grad_t;
+
+  void init_keys(const std::unordered_set<key_t> &keys) {
+    for (const auto &key : keys) {
+      _params[key] = param_t();
+      _grads[key] = grad_t();
+    }
+  }
+  void clear() {
+    _params.clear();
+    _grads.clear();
+  }
+  size_t size() const { return _params.size(); }
+  std::unordered_map<key_t, param_t> &params() { return _params; }
+  std::unordered_map<key_t, grad_t> &grads() { return _grads; }
+
+ private:
+  std::unordered_map<key_t, param_t> _params;
+  std::unordered_map<key_t, grad_t> _grads;
+};
+
+/* ---- parameter/global_pull_access.h --------------------------------------
+ * pull_with_barrier: params[key] = pulled value, grads[key] reset
+ * (global_pull_access.h:88-97).  Keys new to the shard are initialised by it
+ * (accessmethod.h:63-70).  An empty key set returns at once (the reference
+ * blocks forever, global_pull_access.h:33-42). */
+template <typename Key, typename Val, typename Grad> class GlobalPullAccess {
+ public:
+  typedef LocalParamCache<Key, Val, Grad> param_cache_t;
+  typedef typename PullCodec<Val>::wire_t wire_t;
+
+  explicit GlobalPullAccess(swps_table *t = nullptr) : _t(t) {}
+
+  void pull_with_barrier(const std::unordered_set<Key> &keys, param_cache_t &cache) {
+    if (keys.empty()) return;
+    swps_table *t = _t ? _t : global_swps_table();
+    if (!t) throw SwpsError(SWPS_E_STATE, "no shard: create a Cluster first");
+    std::vector<uint64_t> k;
+    k.reserve(keys.size());
+    for (const auto &key : keys) k.push_back((uint64_t)key);
+    const int P = PullCodec<Val>::elems();
+    std::vector<wire_t> vals(k.size() * (size_t)P);
+    swps_check(swps_pull_h(t, k.data(), k.size(), vals.data()));
+    for (size_t i = 0; i < k.size(); i++) {
+      const Key key = (Key)k[i];
+      PullCodec<Val>::decode(&vals[i * P], cache.params()[key]);
+      cache.grads()[key] = Grad();
+    }
+  }
+
+ private:
+  swps_table *_t;
+};
+
+/* ---- parameter/global_push_access.h --------------------------------------
+ * push_with_barrier: the mean gradient of every key present in the cache's
+ * grads is applied by the shard's push rule (AdaGrad, word2vec_global.h:
+ * 176-185 / lr.cpp:68-75) and the local gradient is reset
+ * (global_push_access.h:48-67). */
+template <typename Key, typename Val, typename Grad> class GlobalPushAccess {
+ public:
+  typedef LocalParamCache<Key, Val, Grad> param_cache_t;
+  typedef typename PullCodec<Val>::wire_t wire_t;
+
+  explicit GlobalPushAccess(swps_table *t = nullptr) : _t(t) {}
+
+  void push_with_barrier(const std::unordered_set<Key> &keys, param_cache_t &cache) {
+    swps_table *t = _t ? _t : global_swps_table();
+    if (!t) throw SwpsError(SWPS_E_STATE, "no shard: create a Cluster first");
+    int32_t row = 0, pull = 0, push = 0;
+    swps_check(swps_table_row_elems(t, &row, &pull, &push));
+    std::vector<uint64_t> k;
+    std::vector<wire_t> g;
+    for (const auto &key : keys) {
+      auto it = cache.grads().find(key);
+      if (it == cache.grads().end()) continue;
+      k.push_back((uint64_t)key);
+      g.resize(k.size() * (size_t)push);
+      PushCodec<Grad>::encode(it->second, &g[(k.size() - 1) * push]);
+    }
+    if (!k.empty()) swps_check(swps_push_h(t, k.data(), k.size(), g.data()));
+  }
+
+ private:
+  swps_table *_t;
+};
+
+template <class Key, class Val, class Grad> GlobalPullAccess<Key, Val, Grad> &global_pull_access() {
+  static GlobalPullAccess<Key, Val, Grad> a;
+  return a;
+}
+template <class Key, class Val, class Grad> GlobalPushAccess<Key, Val, Grad> &global_push_access() {
+  static GlobalPushAccess<Key, Val, Grad> a;
+  return a;
+}
+
+/* ---- cluster/cluster.h ----------------------------------------------------
+ * One process per GPU.  The shard's shape comes from the config keys the
+ * reference's server reads: [word2vec] len_vec (W2V layout) and
+ * [server] initial_learning_rate.  Rank / device from the launcher's
+ * RANK / LOCAL_RANK (torchrun, mpirun -x) instead of MPI_Comm_rank. */
+struct W2VServer {
+  static int32_t layout() { return SWPS_LAYOUT_W2V; }
+};
+struct LRServer {
+  static int32_t layout() { return SWPS_LAYOUT_LR; }
+};
+struct ClusterWorker {};
+
+template <class WorkerT, class ServerT, class KeyT> class Cluster {
+ public:
+  explicit Cluster(uint64_t capacity = 1u << 22, int32_t dtype = SWPS_F32) {
+    const char *lr = std::getenv("LOCAL_RANK");
+    swps_table_cfg c;
+    c.device = lr ? std::atoi(lr) : 0;
+    c.layout = ServerT::layout();
+    c.dtype = dtype;
+    c.dim = c.layout == SWPS_LAYOUT_W2V ? global_config().get("word2vec", "len_vec").to_int32() : 1;
+    c.capacity = capacity;
+    c.learning_rate = global_config().get("server", "initial_learning_rate").to_float();
+    c.fudge = 1e-6f;
+    c.init_mode = SWPS_INIT_HASH;
+    c.seed = 0;
+    swps_check(swps_table_create(&c, &_t));
+    global_swps_table() = _t;
+  }
+  ~Cluster() {
+    if (global_swps_table() == _t) global_swps_table() = nullptr;
+    swps_table_destroy(_t);
+  }
+  void initialize() {}
+  /* SparseTable::output (sparsetable.h:127-132) to `path` */
+  void finalize(const std::string &path = "") {
+    if (!path.empty()) swps_check(swps_dump(_t, path.c_str()));
+  }
+  swps_table *table() { return _t; }
+
+ private:
+  Cluster(const Cluster &);
+  Cluster &operator=(const Cluster &);
+  swps_table *_t = nullptr;
+};
+
+/* ---- app level ------------------------------------------------------------ */
+
+/* Word2Vec<MiniBatch> (word2vec_global.h:541-748): train() = the first full
+ * pull + niters epochs of the minibatch loop, all on the GPU. */
+class Word2VecApp {
+ public:
+  Word2VecApp(const std::string &path, int niters, swps_table *t = nullptr, int fp64_intermediates = 1)
+      : _path(path), _niters(niters) {
+    swps_w2v_cfg c;
+    c.window = global_config().get("word2vec", "window").to_int32();
+    c.negative = global_config().get("word2vec", "negative").to_int32();
+    c.min_sentence_length = global_config().get("word2vec", "min_sentence_length").to_int32();
+    c.minibatch = global_config().get("worker", "minibatch").to_int32();
+    c.sample = global_config().get("word2vec", "sample").to_float();
+    c.alpha = global_config().get("word2vec", "learning_rate").to_float();
+    c.unigram_size = 100000000ULL;
+    c.key_mode = SWPS_KEY_BKDR;
+    c.init_mode = SWPS_W2V_INIT_REF;
+    c.rand_seed = 1;
+    c.rand_offset = 2;
+    c.fp64_intermediates = fp64_intermediates;
+    c.profile = 0;
+    swps_check(swps_w2v_create(t ? t : global_swps_table(), &c, &_w));
+  }
+  ~Word2VecApp() { swps_w2v_destroy(_w); }
+  void train() {
+    swps_check(swps_w2v_load_text(_w, _path.c_str()));
+    swps_check(swps_w2v_init(_w));
+    swps_check(swps_w2v_train_epochs(_w, _niters));
+  }
+  swps_w2v *handle() { return _w; }
+
+ private:
+  Word2VecApp(const Word2VecApp &);
+  Word2VecApp &operator=(const Word2VecApp &);
+  std::string _path;
+  int _niters;
+  swps_w2v *_w = nullptr;
+};
+
+/* Sent2Vec (sent2vec.cpp:14-195): load_word_vector then train(); the
+ * sentence vectors go to `out_path` in the reference's format. */
+class Sent2VecApp {
+ public:
+  Sent2VecApp(const std::string &path, const std::string &out_path, int niters, swps_table *t = nullptr)
+      : _path(path), _out(out_path), _t(t ? t : global_swps_table()) {
+    _c.window = global_config().get("word2vec", "window").to_int32();
+    _c.negative = global_config().get("word2vec", "negative").to_int32();
+    _c.min_sentence_length = global_config().get("word2vec", "min_sentence_length").to_int32();
+    _c.minibatch = global_config().get("worker", "minibatch").to_int32();
+    _c.niters = niters;
+    _c.alpha = global_config().get("word2vec", "learning_rate").to_float();
+    _c.unigram_size = 100000000ULL;
+    _c.rand_seed = 1;
+    _c.rand_offset = 2;
+    _c.rand_insert_extra = 0;
+    _c.profile = 0;
+  }
+  ~Sent2VecApp() {
+    if (_s) swps_s2v_destroy(_s);
+  }
+  /* ClusterServer::load (server.h:49-62) + the WParam it constructs first */
+  void load_word_vector(const std::string &path) {
+    uint64_t before = 0, after = 0;
+    swps_check(swps_table_size(_t, &before));
+    swps_check(swps_load(_t, path.c_str(), 1000, 1, 0));
+    swps_check(swps_table_size(_t, &after));
+    int32_t row = 0;
+    swps_check(swps_table_row_elems(_t, &row, nullptr, nullptr));
+    _c.rand_offset += (uint64_t)row / 2 + _c.rand_insert_extra * (after - before);
+  }
+  void train() {
+    swps_check(swps_s2v_create(_t, &_c, &_s));
+    swps_check(swps_s2v_load_text(_s, _path.c_str()));
+    swps_check(swps_s2v_train(_s));
+    if (!_out.empty()) swps_check(swps_s2v_dump(_s, _out.c_str()));
+  }
+  swps_s2v *handle() { return _s; }
+
+ private:
+  Sent2VecApp(const Sent2VecApp &);
+  Sent2VecApp &operator=(const Sent2VecApp &);
+  std::string _path, _out;
+  swps_table *_t;
+  swps_s2v_cfg _c;
+  swps_s2v *_s = nullptr;
+};
+
+/* LR (lr.cpp:133-411): train(niters) returns the per-epoch mean squared
+ * error the reference logs (lr.cpp:231); predict() the probabilities. */
+class LRApp {
+ public:
+  LRApp(const std::string &path, swps_table *t = nullptr) {
+    swps_lr_cfg c;
+    c.minibatch = global_config().get("worker", "minibatch").to_int32();
+    c.init_ref = 1;
+    c.profile = 0;
+    swps_check(swps_lr_create(t ? t : global_swps_table(), &c, &_l));
+    swps_check(swps_lr_load_text(_l, path.c_str()));
+    swps_check(swps_lr_init(_l));
+  }
+  ~LRApp() { swps_lr_destroy(_l); }
+  std::vector<double> train(int niters) {
+    std::vector<double> err((size_t)niters);
+    swps_check(swps_lr_train(_l, niters, err.data()));
+    return err;
+  }
+  std::vector<float> predict() {
+    uint64_t info[4];
+    swps_check(swps_lr_info(_l, info));
+    std::vector<float> p(info[0] ? info[0] : 1);
+    swps_check(swps_lr_predict(_l, p.data(), nullptr, p.size()));
+    p.resize(info[0]);
+    return p;
+  }
+
+ private:
+  LRApp(const LRApp &);
+  LRApp &operator=(const LRApp &);
+  swps_lr *_l = nullptr;
+};
+
+}  // namespace swift_snails
+
+#endif /* SWIFTMPI_COMPAT_H_ */

@@ -92,6 +92,12 @@ int swps_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals);
 /* Batched push: apply the push rule with the mean gradients d_grads[n][push
  * elems] (fp64 for W2V, fp32 for LR).  Unknown key -> SWPS_E_BADKEY. */
 int swps_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads);
+/* The same with HOST arrays in the reference's wire types (W2V: fp64
+ * [h|v] pull values and [mean h_grad|mean v_grad] push values; LR: fp32),
+ * staged through HBM by the library — the form a C++ PS client binds
+ * (include/swiftmpi_compat.h: GlobalPullAccess / GlobalPushAccess). */
+int swps_pull_h(swps_table *t, const uint64_t *keys, uint64_t n, void *vals);
+int swps_push_h(swps_table *t, const uint64_t *keys, uint64_t n, const void *grads);
 /* Overwrite / read full rows (table dtype, d_rows[n][row elems]). */
 int swps_assign(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_rows);
 int swps_export(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_rows);

@@ -64,6 +64,8 @@ PROTOS = {
     "swps_table_row_elems": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "swps_pull": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_push": (ctypes.c_int, [_p, _p, _u64, _p]),
+    "swps_pull_h": (ctypes.c_int, [_p, _p, _u64, _p]),
+    "swps_push_h": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_assign": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_export": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_table_keys": (ctypes.c_int, [_p, _p, _u64, ctypes.POINTER(_u64)]),

@@ -435,6 +435,47 @@ int swps_export(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_rows)
   return table_check_error(t, t->stream);
 }
 
+// Host-pointer forms for FFI callers without device memory: the reference's
+// wire types (W2V fp64 [h|v] / [h_grad|v_grad], LR fp32), staged through HBM.
+int swps_pull_h(swps_table *t, const uint64_t *keys, uint64_t n, void *vals) {
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  const int P = t->pull_elems;
+  DevMem dk, dv;
+  SWPS_TRY(dk.ensure(n * 8));
+  SWPS_TRY(dv.ensure(n * P * t->esize));
+  SWPS_HIP(hipMemcpyAsync(dk.p, keys, n * 8, hipMemcpyHostToDevice, t->stream));
+  SWPS_TRY(swps_pull(t, dk.as<uint64_t>(), n, dv.p));  // syncs
+  const bool w2v = t->cfg.layout == SWPS_LAYOUT_W2V;
+  const size_t out_es = w2v ? 8 : 4;
+  if (t->esize == out_es) {
+    SWPS_HIP(hipMemcpy(vals, dv.p, n * P * out_es, hipMemcpyDeviceToHost));
+    return SWPS_OK;
+  }
+  std::vector<char> tmp(n * P * t->esize);
+  SWPS_HIP(hipMemcpy(tmp.data(), dv.p, tmp.size(), hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n * P; i++) {
+    const double x = t->esize == 8 ? ((double *)tmp.data())[i] : (double)((float *)tmp.data())[i];
+    if (w2v)
+      ((double *)vals)[i] = x;
+    else
+      ((float *)vals)[i] = (float)x;
+  }
+  return SWPS_OK;
+}
+
+int swps_push_h(swps_table *t, const uint64_t *keys, uint64_t n, const void *grads) {
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  const size_t gb = n * t->push_elems * (t->cfg.layout == SWPS_LAYOUT_W2V ? 8 : 4);
+  DevMem dk, dg;
+  SWPS_TRY(dk.ensure(n * 8));
+  SWPS_TRY(dg.ensure(gb));
+  SWPS_HIP(hipMemcpyAsync(dk.p, keys, n * 8, hipMemcpyHostToDevice, t->stream));
+  SWPS_HIP(hipMemcpyAsync(dg.p, grads, gb, hipMemcpyHostToDevice, t->stream));
+  return swps_push(t, dk.as<uint64_t>(), n, dg.p);  // syncs via the error check
+}
+
 int swps_table_keys(swps_table *t, uint64_t *keys, uint64_t cap, uint64_t *n) {
   SWPS_HIP(hipSetDevice(t->cfg.device));
   SWPS_TRY(table_check_error(t, t->stream));

@@ -1,0 +1,162 @@
+// C++11 drivers over include/swiftmpi_compat.h — what the reference's app
+// mains (apps/word2vec/w2v.cpp, apps/sent2vec/sent2vec.cpp,
+// apps/logistic/lr.cpp) become when they link libswps instead of the
+// MPI/ZeroMQ parameter server.  Used by tests/test_compat_gpu.py.
+//
+//   compat_apps w2v    -config C -data D -niters N -output O
+//   compat_apps s2v    -config C -data D -niters N -wordvec W -output O
+//   compat_apps lr     -config C -data D -niters N -output O   (per-epoch MSE)
+//   compat_apps ps     -config C                               (PS-level client)
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+
+#include "swiftmpi_compat.h"
+
+using namespace swift_snails;
+
+// ---- the PS-level value types of word2vec_global.h:50-100, restated ------
+static int g_dim = 0;
+struct WLocalParam {
+  std::vector<double> h, v;
+  WLocalParam() : h(g_dim, 0.0), v(g_dim, 0.0) {}
+};
+struct WLocalGrad {
+  std::vector<double> h_grad, v_grad;
+  int h_count = 0, v_count = 0;
+  WLocalGrad() : h_grad(g_dim, 0.0), v_grad(g_dim, 0.0) {}
+  void accu_h(const std::vector<double> &g) {
+    h_count++;
+    for (int i = 0; i < g_dim; i++) h_grad[i] += g[i];
+  }
+  void accu_v(const std::vector<double> &g) {
+    v_count++;
+    for (int i = 0; i < g_dim; i++) v_grad[i] += g[i];
+  }
+};
+namespace swift_snails {
+template <> struct PullCodec<WLocalParam> {
+  typedef double wire_t;
+  static int elems() { return 2 * g_dim; }
+  static void decode(const double *w, WLocalParam &p) {
+    p.h.assign(w, w + g_dim);
+    p.v.assign(w + g_dim, w + 2 * g_dim);
+  }
+};
+template <> struct PushCodec<WLocalGrad> {  // the mean, word2vec_global.h:122-134
+  static void encode(WLocalGrad &g, double *w) {
+    for (int i = 0; i < g_dim; i++) {
+      w[i] = g.h_count > 0 ? g.h_grad[i] / g.h_count : g.h_grad[i];
+      w[g_dim + i] = g.v_count > 0 ? g.v_grad[i] / g.v_count : g.v_grad[i];
+    }
+    g = WLocalGrad();
+  }
+};
+}  // namespace swift_snails
+
+typedef LocalParamCache<uint64_t, WLocalParam, WLocalGrad> cache_t;
+
+static int ps_client() {
+  g_dim = global_config().get("word2vec", "len_vec").to_int32();
+  const double lr = global_config().get("server", "initial_learning_rate").to_float();
+  Cluster<ClusterWorker, W2VServer, uint64_t> cluster(4096, SWPS_F64);
+  cluster.initialize();
+  std::unordered_set<uint64_t> keys;
+  for (uint64_t k = 1; k <= 300; k++) keys.insert(k * 2654435761ULL);
+  cache_t cache, again;
+  cache.init_keys(keys);
+  global_pull_access<uint64_t, WLocalParam, WLocalGrad>().pull_with_barrier(keys, cache);
+  again.init_keys(keys);
+  global_pull_access<uint64_t, WLocalParam, WLocalGrad>().pull_with_barrier(keys, again);
+  for (auto k : keys) {
+    const WLocalParam &a = cache.params()[k], &b = again.params()[k];
+    for (int i = 0; i < g_dim; i++)
+      if (a.h[i] != b.h[i] || a.v[i] != b.v[i] || std::fabs(a.h[i]) > 0.5 / g_dim) {
+        std::printf("FAIL pull k=%llu\n", (unsigned long long)k);
+        return 1;
+      }
+  }
+  // accumulate two gradients per key, push the mean, check AdaGrad
+  std::map<uint64_t, std::vector<double> > mh, mv;
+  for (auto k : keys) {
+    std::vector<double> g1(g_dim), g2(g_dim), g3(g_dim);
+    for (int i = 0; i < g_dim; i++) {
+      g1[i] = std::sin((double)(k % 97) + i);
+      g2[i] = std::cos((double)(k % 89) * i);
+      g3[i] = 0.25 * i - 1.0;
+    }
+    cache.grads()[k].accu_h(g1);
+    cache.grads()[k].accu_h(g2);
+    cache.grads()[k].accu_v(g3);
+    std::vector<double> h(g_dim), v(g_dim);
+    for (int i = 0; i < g_dim; i++) {
+      h[i] = (g1[i] + g2[i]) / 2;
+      v[i] = g3[i];
+    }
+    mh[k] = h;
+    mv[k] = v;
+  }
+  global_push_access<uint64_t, WLocalParam, WLocalGrad>().push_with_barrier(keys, cache);
+  cache_t after;
+  after.init_keys(keys);
+  global_pull_access<uint64_t, WLocalParam, WLocalGrad>().pull_with_barrier(keys, after);
+  const double fudge = (double)1e-6f;
+  double worst = 0;
+  for (auto k : keys) {
+    for (int i = 0; i < g_dim; i++) {  // word2vec_global.h:176-185 from h2 = v2 = 0
+      const double eh = again.params()[k].h[i] + lr * mh[k][i] / std::sqrt(mh[k][i] * mh[k][i] + fudge);
+      const double ev = again.params()[k].v[i] + lr * mv[k][i] / std::sqrt(mv[k][i] * mv[k][i] + fudge);
+      worst = std::fmax(worst, std::fabs(after.params()[k].h[i] - eh));
+      worst = std::fmax(worst, std::fabs(after.params()[k].v[i] - ev));
+    }
+    if (cache.grads()[k].h_count != 0) {
+      std::printf("FAIL grads not reset\n");
+      return 1;
+    }
+  }
+  std::printf("ps ok keys=%zu max|diff|=%.3g\n", keys.size(), worst);
+  return worst < 1e-12 ? 0 : 1;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) return 2;
+  const std::string mode = argv[1];
+  std::map<std::string, std::string> a;
+  for (int i = 2; i + 1 < argc; i += 2) a[argv[i]] = argv[i + 1];
+  try {
+    global_config().load_conf(a["-config"]);
+    global_config().parse();
+    if (mode == "ps") return ps_client();
+    const int niters = std::atoi(a["-niters"].c_str());
+    if (mode == "w2v") {  // apps/word2vec/w2v.cpp:5-61
+      Cluster<ClusterWorker, W2VServer, uint64_t> cluster;
+      cluster.initialize();
+      Word2VecApp w2v(a["-data"], niters);
+      w2v.train();
+      cluster.finalize(a["-output"]);
+    } else if (mode == "s2v") {  // apps/sent2vec/sent2vec.cpp:198-257
+      Cluster<ClusterWorker, W2VServer, uint64_t> cluster;
+      cluster.initialize();
+      Sent2VecApp s2v(a["-data"], a["-output"], niters);
+      s2v.load_word_vector(a["-wordvec"]);
+      s2v.train();
+    } else if (mode == "lr") {  // apps/logistic/lr.cpp:413-509 (train mode)
+      Cluster<ClusterWorker, LRServer, uint32_t> cluster;
+      cluster.initialize();
+      LRApp lr(a["-data"]);
+      std::vector<double> err = lr.train(niters);
+      FILE *f = std::fopen(a["-output"].c_str(), "w");
+      for (double e : err) std::fprintf(f, "%.17g\n", e);
+      std::fclose(f);
+    } else {
+      return 2;
+    }
+  } catch (SwpsError &e) {
+    std::fprintf(stderr, "error %d: %s\n", e.code, e.what());
+    return 3;
+  }
+  std::printf("%s ok\n", mode.c_str());
+  return 0;
+}
