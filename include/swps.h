@@ -190,7 +190,7 @@ void *swps_w2v_stream(swps_w2v *w);
  *   swps_w2v_request     keys of the next batch grouped by owner rank (u64)
  *   -> all-to-all ->     swps_w2v_serve_pull (owner: [n][h|v] pull values)
  *   -> all-to-all ->     swps_w2v_step       (install values, learn, emit
- *                                             mean gradients [U][h|v] fp64)
+ *                                             mean gradients [U][h|v])
  *   -> all-to-all ->     swps_w2v_serve_push (owner: AdaGrad per source rank,
  *                                             sources in rank order)
  * Initial full pull: swps_w2v_request(init=1) -> serve_pull(insert=1) ->
@@ -205,8 +205,11 @@ int swps_w2v_request(swps_w2v *w, int32_t init, uint64_t *counts, uint64_t *d_ke
 int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src_counts, int32_t insert,
                         void *d_vals);
 int swps_w2v_install_init(swps_w2v *w, const void *d_vals);
-int swps_w2v_step(swps_w2v *w, const void *d_vals, double *d_grads);
-int swps_w2v_serve_push(swps_w2v *w, const double *d_grads, const uint64_t *src_counts);
+/* d_grads: mean gradients [U][h|v] in the context's intermediate type — fp64
+ * (the reference's wire format) unless the table is SWPS_F32 with
+ * fp64_intermediates = 0 (fast mode), then fp32 (half the exchange bytes). */
+int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads);
+int swps_w2v_serve_push(swps_w2v *w, const void *d_grads, const uint64_t *src_counts);
 
 /* ---- host-only helpers (no device needed; used by the CPU test-suite) ---- */
 /* run-length form of gen_unigram_table (word2vec_global.h:467-497): start slot

@@ -149,5 +149,6 @@ int table_check_error(swps_table *t, hipStream_t s);
 int table_set_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_vals, hipStream_t s);
 int table_get_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s);
 int table_copy_pull(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s);
-int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s);
+int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
+                    bool grads_f32 = false);
 }  // namespace swps

@@ -127,6 +127,17 @@ __global__ void k_copy_rows_out(const uint32_t *__restrict__ rows_idx, uint64_t 
   for (int e = lane; e < ncopy; e += 64) out[w * ncopy + e] = r == kNoRow ? (T)0 : rows[(uint64_t)r * R + e];
 }
 
+// the same with 16-B lanes (row stride and copy width multiples of 16 B)
+__global__ void k_copy_rows_out16(const uint32_t *__restrict__ rows_idx, uint64_t n, const uint4 *__restrict__ rows,
+                                  int R16, int ncopy16, uint4 *__restrict__ out) {
+  uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int lane = threadIdx.x & 63;
+  if (w >= n) return;
+  uint32_t r = rows_idx[w];
+  for (int e = lane; e < ncopy16; e += 64)
+    out[w * ncopy16 + e] = r == kNoRow ? make_uint4(0, 0, 0, 0) : rows[(uint64_t)r * R16 + e];
+}
+
 template <typename T>
 __global__ void k_copy_rows_in(const uint32_t *__restrict__ rows_idx, uint64_t n, T *__restrict__ rows, int R,
                                const T *__restrict__ in) {
@@ -140,26 +151,42 @@ __global__ void k_copy_rows_in(const uint32_t *__restrict__ rows_idx, uint64_t n
 
 // WPushAccessMethod::apply_push_value (word2vec_global.h:176-185), fp64 math:
 //   h2 += g_h*g_h; v2 += g_v*g_v; h += lr*g_h/sqrt(h2+fudge); v likewise.
-template <typename T>
-__global__ void k_push_w2v(const uint32_t *__restrict__ rows_idx, uint64_t n, const double *__restrict__ grads,
+// G = wire type of the mean gradients (fp64 = the reference's wire format;
+// fp32 for fast-mode contexts).  E elements per lane per chunk (16-B row
+// accesses when D % E == 0, else E = 1).
+template <typename T, int E> struct alignas(sizeof(T) * E) Pack {
+  T v[E];
+};
+
+template <typename T, typename G, int E>
+__global__ void k_push_w2v(const uint32_t *__restrict__ rows_idx, uint64_t n, const G *__restrict__ grads,
                            T *__restrict__ rows, int D, double lr, double fudge) {
   uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   int lane = threadIdx.x & 63;
   if (w >= n) return;
   uint32_t r = rows_idx[w];
   if (r == kNoRow) return;
+  using PT = Pack<T, E>;
+  using PG = Pack<G, E>;
   T *row = rows + (uint64_t)r * 4 * D;
-  const double *g = grads + w * 2 * D;
-  for (int i = lane; i < D; i += 64) {
-    double gh = g[i], gv = g[D + i];
-    double h2 = (double)row[2 * D + i] + gh * gh;
-    double v2 = (double)row[3 * D + i] + gv * gv;
-    double hn = (double)row[i] + (gh * lr) / sqrt(h2 + fudge);
-    double vn = (double)row[D + i] + (gv * lr) / sqrt(v2 + fudge);
-    row[2 * D + i] = (T)h2;
-    row[3 * D + i] = (T)v2;
-    row[i] = (T)hn;
-    row[D + i] = (T)vn;
+  const G *g = grads + w * 2 * D;
+  for (int c = lane; c < D / E; c += 64) {
+    const PG gh = ((const PG *)g)[c], gv = ((const PG *)(g + D))[c];
+    PT h = ((PT *)row)[c], v = ((PT *)(row + D))[c], h2 = ((PT *)(row + 2 * D))[c], v2 = ((PT *)(row + 3 * D))[c];
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      const double a = (double)gh.v[k], b = (double)gv.v[k];
+      const double h2n = (double)h2.v[k] + a * a;
+      const double v2n = (double)v2.v[k] + b * b;
+      h.v[k] = (T)((double)h.v[k] + (a * lr) / sqrt(h2n + fudge));
+      v.v[k] = (T)((double)v.v[k] + (b * lr) / sqrt(v2n + fudge));
+      h2.v[k] = (T)h2n;
+      v2.v[k] = (T)v2n;
+    }
+    ((PT *)(row + 2 * D))[c] = h2;
+    ((PT *)(row + 3 * D))[c] = v2;
+    ((PT *)row)[c] = h;
+    ((PT *)(row + D))[c] = v;
   }
 }
 
@@ -256,7 +283,11 @@ int table_get_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_va
 // pull values (first `ncopy` elements of each row) of known rows
 int table_copy_pull(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s) {
   if (n == 0) return SWPS_OK;
-  if (t->cfg.dtype == SWPS_F64)
+  const size_t rb = (size_t)t->row_elems * t->esize, cb = (size_t)t->pull_elems * t->esize;
+  if (rb % 16 == 0 && cb % 16 == 0)
+    k_copy_rows_out16<<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<uint4>(), (int)(rb / 16),
+                                                        (int)(cb / 16), (uint4 *)d_vals);
+  else if (t->cfg.dtype == SWPS_F64)
     k_copy_rows_out<double><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<double>(), t->row_elems,
                                                                t->pull_elems, (double *)d_vals);
   else
@@ -266,17 +297,35 @@ int table_copy_pull(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_v
   return SWPS_OK;
 }
 
-// the push rule on known rows (W2V: fp64 mean gradients [n][2D]; LR: fp32 [n])
-int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s) {
+template <typename T, typename G>
+void launch_push_w2v(const uint32_t *d_rows, uint64_t n, const G *g, T *rows, int D, double lr, double fudge,
+                     hipStream_t s) {
+  constexpr int E = 16 / sizeof(T);
+  if (D % E == 0)
+    k_push_w2v<T, G, E><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, g, rows, D, lr, fudge);
+  else
+    k_push_w2v<T, G, 1><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, g, rows, D, lr, fudge);
+}
+
+// the push rule on known rows (W2V: mean gradients [n][2D], fp64 or, with
+// grads_f32, fp32; LR: fp32 [n])
+int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
+                    bool grads_f32) {
   if (n == 0) return SWPS_OK;
   if (t->cfg.layout == SWPS_LAYOUT_W2V) {
     const double lr = (double)t->cfg.learning_rate, fudge = (double)t->cfg.fudge;
-    if (t->cfg.dtype == SWPS_F64)
-      k_push_w2v<double><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, (const double *)d_grads, t->rows.as<double>(),
-                                                            t->cfg.dim, lr, fudge);
-    else
-      k_push_w2v<float><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, (const double *)d_grads, t->rows.as<float>(),
-                                                           t->cfg.dim, lr, fudge);
+    const int D = t->cfg.dim;
+    if (t->cfg.dtype == SWPS_F64) {
+      if (grads_f32)
+        launch_push_w2v(d_rows, n, (const float *)d_grads, t->rows.as<double>(), D, lr, fudge, s);
+      else
+        launch_push_w2v(d_rows, n, (const double *)d_grads, t->rows.as<double>(), D, lr, fudge, s);
+    } else {
+      if (grads_f32)
+        launch_push_w2v(d_rows, n, (const float *)d_grads, t->rows.as<float>(), D, lr, fudge, s);
+      else
+        launch_push_w2v(d_rows, n, (const double *)d_grads, t->rows.as<float>(), D, lr, fudge, s);
+    }
   } else {
     if (t->cfg.dtype == SWPS_F64)
       k_push_lr<double><<<blocks_for(n), 256, 0, s>>>(d_rows, n, (const float *)d_grads, t->rows.as<double>(),
@@ -394,22 +443,7 @@ int swps_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_g
   SWPS_TRY(t->scratch.ensure(n * 4));
   uint32_t *rows = t->scratch.as<uint32_t>();
   SWPS_TRY(table_lookup(t, d_keys, n, rows, t->stream));
-  if (t->cfg.layout == SWPS_LAYOUT_W2V) {
-    double lr = (double)t->cfg.learning_rate, fudge = (double)t->cfg.fudge;
-    if (t->cfg.dtype == SWPS_F64)
-      k_push_w2v<double><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, (const double *)d_grads,
-                                                                    t->rows.as<double>(), t->cfg.dim, lr, fudge);
-    else
-      k_push_w2v<float><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, (const double *)d_grads,
-                                                                   t->rows.as<float>(), t->cfg.dim, lr, fudge);
-  } else {
-    if (t->cfg.dtype == SWPS_F64)
-      k_push_lr<double><<<blocks_for(n), 256, 0, t->stream>>>(rows, n, (const float *)d_grads, t->rows.as<double>(),
-                                                              (double)t->cfg.learning_rate, (double)t->cfg.fudge);
-    else
-      k_push_lr<float><<<blocks_for(n), 256, 0, t->stream>>>(rows, n, (const float *)d_grads, t->rows.as<float>(),
-                                                             t->cfg.learning_rate, t->cfg.fudge);
-  }
+  SWPS_TRY(table_push_rows(t, rows, n, d_grads, t->stream));
   SWPS_HIP(hipGetLastError());
   return table_check_error(t, t->stream);
 }

@@ -587,7 +587,7 @@ template <typename T, typename A> struct PushArgs {
   int32_t *local;
   int D;
   double lr, fudge;
-  double *grads;  // TO_GRADS: mean gradients [U][2D] (the push request payload)
+  A *grads;  // TO_GRADS: mean gradients [U][2D] in the intermediate type (the push request payload)
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
@@ -618,7 +618,7 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
         if (cnt == 0) {
           if (TO_GRADS)
 #pragma unroll
-            for (int k = 0; k < E; k++) a.grads[u * 2 * D + half * D + ci * E + k] = 0.0;
+            for (int k = 0; k < E; k++) a.grads[u * 2 * D + half * D + ci * E + k] = (A)0;
           continue;
         }
         const uint32_t i0 = a.ioff[2 * u + half], i1 = a.ioff[2 * u + half + 1];
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
         }
         if (TO_GRADS) {
 #pragma unroll
-          for (int k = 0; k < E; k++) a.grads[u * 2 * D + half * D + ci * E + k] = sum[k] / (double)cnt;
+          for (int k = 0; k < E; k++) a.grads[u * 2 * D + half * D + ci * E + k] = (A)(sum[k] / (double)cnt);
           continue;
         }
         T *w = row + half * D, *w2 = row + (2 + half) * D;
@@ -649,7 +649,7 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
         double wn[E], w2n[E];
 #pragma unroll
         for (int k = 0; k < E; k++) {
-          const double g = sum[k] / (double)cnt;
+          const double g = (double)(A)(sum[k] / (double)cnt);  // the mean in the push payload's type
           const double gsq = g * g;
           const double acc2 = CT::at(w2r, k) + gsq;
           const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
@@ -1095,7 +1095,7 @@ int plan_epoch(swps_w2v *w) {
   return SWPS_OK;
 }
 
-template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals = nullptr, double *d_grads = nullptr) {
+template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals = nullptr, A *d_grads = nullptr) {
   const uint64_t nb = w->batches.size();
   if (w->cursor % nb == 0) SWPS_TRY(plan_epoch(w));
   const uint64_t bi = w->cursor % nb;
@@ -1646,22 +1646,24 @@ int swps_w2v_install_init(swps_w2v *w, const void *d_vals) {
   return SWPS_OK;
 }
 
-int swps_w2v_step(swps_w2v *w, const void *d_vals, double *d_grads) {
+int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads) {
   if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
   if (!w->inited) return fail(SWPS_E_STATE, "init first");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
-  if (w->f64) return run_batch<double, double>(w, d_vals, d_grads);
-  if (w->cfg.fp64_intermediates) return run_batch<float, double>(w, d_vals, d_grads);
-  return run_batch<float, float>(w, d_vals, d_grads);
+  if (w->f64) return run_batch<double, double>(w, d_vals, (double *)d_grads);
+  if (w->cfg.fp64_intermediates) return run_batch<float, double>(w, d_vals, (double *)d_grads);
+  return run_batch<float, float>(w, d_vals, (float *)d_grads);
 }
 
-int swps_w2v_serve_push(swps_w2v *w, const double *d_grads, const uint64_t *src_counts) {
+int swps_w2v_serve_push(swps_w2v *w, const void *d_grads, const uint64_t *src_counts) {
   if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  const bool g32 = !w->f64 && !w->cfg.fp64_intermediates;  // fast mode: fp32 push payload
+  const size_t gsz = g32 ? 4 : 8;
   uint64_t off = 0;
   for (int r = 0; r < w->world; r++) {  // one AdaGrad step per source, in rank order
     SWPS_TRY(table_push_rows(w->t, w->d_serve_rows.as<uint32_t>() + off, src_counts[r],
-                             d_grads + off * 2 * w->D, w->s));
+                             (const char *)d_grads + off * 2 * w->D * gsz, w->s, g32));
     off += src_counts[r];
   }
   if (off != w->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");

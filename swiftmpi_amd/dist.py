@@ -74,6 +74,9 @@ class ShardedWord2Vec:
     def __init__(self, table, group=None, frag_num=1000, **kw):
         kw.setdefault("init", "table")
         self.w = Word2Vec(table, **kw)
+        # push payload: fp64 (the reference's wire format) unless fast mode (fp32 table, fp32 intermediates)
+        fast = table.dtype == "f32" and not kw.get("fp64_intermediates", True)
+        self.grad_dtype = torch.float32 if fast else torch.float64
         self.table = table
         self.D = table.dim
         self.dev = torch.device("cuda", table.device)
@@ -167,7 +170,7 @@ class ShardedWord2Vec:
         rcu = rc.astype(np.uint64)
         check(L.swps_w2v_serve_pull(self.w.h, ptr(rkeys), ptr(rcu), 0, ptr(vals)))
         my_vals = self._exchange(vals, rc, sc, 2 * self.D)
-        grads = self._empty(nsend * 2 * self.D, torch.float64)
+        grads = self._empty(nsend * 2 * self.D, self.grad_dtype)
         if mine:
             check(L.swps_w2v_step(self.w.h, ptr(my_vals) if nsend else None, ptr(grads) if nsend else None))
         rgrads = self._exchange(grads, sc, rc, 2 * self.D)

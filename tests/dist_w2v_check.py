@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--fast", action="store_true", help="fp32 intermediates (fp32 push payload)")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     ngpu = torch.cuda.device_count()
@@ -44,7 +45,7 @@ def main():
     with open(path, "w") as f:
         for _ in range(150 + 40 * rank):
             f.write(" ".join("w%d_%d" % (rank, x) for x in rng.choice(V, int(rng.integers(5, 40)), p=p)) + "\n")
-    kw = dict(window=4, negative=4, minibatch=17, sample=1e-3, unigram_size=10 ** 6)
+    kw = dict(window=4, negative=4, minibatch=17, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=not args.fast)
     D = 16
     # sharded
     t = sw.Table("w2v", dim=D, capacity=4096, dtype=args.dtype, learning_rate=0.7, init="hash", seed=7, device=dev)

@@ -176,14 +176,15 @@ def test_fast_mode_close_to_parity_mode(lib, oracle_mod, gpu, tmp_path):
     assert np.median(rel) < 1e-5 and np.quantile(rel, 0.99) < 1e-2
 
 
-@pytest.mark.parametrize("dtype", ["f64", "f32"])
-def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype):
+@pytest.mark.parametrize("dtype,fp64i", [("f64", True), ("f32", True), ("f32", False)])
+def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i):
     """The sharded request / serve / step / push path with one rank (gloo,
-    world 1) reproduces the single-GPU path bit for bit."""
+    world 1) reproduces the single-GPU path bit for bit — in fast mode too,
+    where the push payload is fp32."""
     import torch.distributed as dist
     from swiftmpi_amd.dist import ShardedWord2Vec
     path = zipf_corpus(str(tmp_path / "c.txt"), 120, 300, seed=31)
-    kw = dict(window=3, negative=4, minibatch=13, sample=1e-3, unigram_size=10 ** 6)
+    kw = dict(window=3, negative=4, minibatch=13, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=fp64i)
     own = not dist.is_initialized()
     if own:
         import socket
