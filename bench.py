@@ -33,14 +33,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 def make_corpus(tokens, vocab, line_len, seed):
     """Zipf(s=1) over `vocab` word ids, `tokens` tokens in lines of `line_len`
     (the synthetic text8 stand-in)."""
-    rng = np.random.default_rng(seed)
-    cdf = np.cumsum(1.0 / np.arange(1, vocab + 1))
-    cdf /= cdf[-1]
-    ids = np.searchsorted(cdf, rng.random(tokens), side="right").astype(np.uint32)
-    np.minimum(ids, vocab - 1, out=ids)
-    off = np.arange(0, tokens, line_len, dtype=np.uint64)
-    off = np.append(off, np.uint64(tokens))
-    return ids, off
+    from swiftmpi_amd.synth import zipf_tokens
+    return zipf_tokens(tokens, vocab, line_len, seed)
 
 
 def word_keys(lib, vocab):
@@ -94,7 +88,13 @@ def main():
                     help="time the fp64-intermediate parity mode instead of the default fast mode")
     ap.add_argument("--no-parity-leg", action="store_true",
                     help="skip the extra parity-mode timing reported beside the fast-mode value")
+    ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
+                    help="w2v: the headline (config 2); lr: config 3 shape; s2v: config 5 shape")
+    ap.add_argument("--lr-batch", type=int, default=65536, help="LR rows per GPU per minibatch (config 3)")
+    ap.add_argument("--s2v-docs", type=int, default=8192, help="sent2vec documents per minibatch")
     args = ap.parse_args()
+    if args.app != "w2v":
+        return bench_other(args)
 
     import torch
     import swiftmpi_amd as sw
@@ -240,6 +240,129 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ids, off, keys, args, args.cpu_lines)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _dist_init(args):
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
+    dist, backend = None, None
+    if world > 1 or args.sharded:
+        import torch.distributed as dist
+        if "MASTER_ADDR" not in os.environ:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
+        if torch.cuda.device_count() >= world:
+            backend = "nccl"
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            backend = "gloo"
+            dist.init_process_group("gloo")
+    return rank, world, local, dist, backend
+
+
+def bench_other(args):
+    """Config 3 (sparse LR, Criteo shape, key-sharded over the GPUs) and
+    config 5 (sent2vec, doc-sharded, word table replicated) — one JSON line
+    each, same timing contract as the headline."""
+    import torch
+    import swiftmpi_amd as sw
+    rank, world, local, dist, backend = _dist_init(args)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    def finish(dt, units):
+        if dist is not None:
+            tt = torch.tensor([dt, float(units)], dtype=torch.float64, device="cuda")
+            mx = tt.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+            return float(mx[0]), float(tt[1])
+        return dt, float(units)
+
+    steps, warm = args.steps, args.warmup
+    if args.app == "lr":
+        from swiftmpi_amd.synth import criteo
+        B1 = args.lr_batch + 1
+        rows = B1 * (steps + warm)
+        y, off, f, v = criteo(rows, seed=3 + rank)
+        t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=args.lr if args.lr != 0.7 else 0.05,
+                     init="hash", seed=1, device=local)
+        if dist is not None:
+            from swiftmpi_amd.dist import ShardedLR
+            m = ShardedLR(t, frag_num=2000, minibatch=args.lr_batch, profile=False)
+            m.load_csr(y, off, f, v)
+            m.init()
+            run = m.train_steps
+            sync = m.sync
+        else:
+            m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False)
+            m.load_csr(y, off, f, v)
+            m.init()
+            run = m.train_batches
+            sync = m.sync
+        run(warm)
+        sync()
+        barrier()
+        t0 = time.perf_counter()
+        run(steps)
+        sync()
+        barrier()
+        dt = time.perf_counter() - t0
+        dt, total = finish(dt, steps * B1)
+        nnz_per_row = 39
+        out = {"metric": "sparse LR trained examples/sec (AdaGrad, key-sharded PS)", "value": total / dt,
+               "unit": "examples/s", "n_gpus": world, "steps": steps, "warmup": warm,
+               "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "f32", "data": "synthetic Criteo-shape hashed features (swiftmpi_amd/synth.py criteo)",
+               "config": {"workload": "sparse logistic regression, 39 features/row, 2^24 hashed feature space, "
+                                      "%d rows per GPU per minibatch" % B1,
+                          "parallelism": ("key-sharded PS over %d GPU(s), %s all-to-all-v" % (world, backend))
+                          if dist is not None else "1 GPU, one HBM shard",
+                          "features_per_s": total * nnz_per_row / dt}}
+    else:
+        from swiftmpi_amd.synth import zipf_tokens
+        V, D = 1000000, args.dim
+        nd = args.s2v_docs * (steps + warm)
+        rng = np.random.default_rng(5 + rank)
+        lens = rng.integers(50, 201, nd)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        ids, _ = zipf_tokens(int(off[-1]), V, 100, seed=5 + rank)
+        toks = ids.astype(np.uint64) + 1
+        sent = (np.arange(nd, dtype=np.uint64) + np.uint64(nd * rank + 1)) * np.uint64(2654435761)
+        t = sw.Table("w2v", dim=D, capacity=V + 1024, dtype="f32", init="hash", seed=3, device=local)
+        keys = torch.arange(1, V + 1, dtype=torch.int64, device="cuda")
+        t.pull(keys)  # the frozen word table (replicated on every GPU)
+        del keys
+        s2 = sw.Sent2Vec(t, window=args.window, negative=args.negative, minibatch=args.s2v_docs, niters=1,
+                         alpha=args.alpha)
+        s2.load_tokens(toks, off, sent)  # each rank generated its own docs: doc-sharded by construction
+        s2.train_batches(warm)
+        s2.sync()
+        barrier()
+        st0 = s2.stats()
+        t0 = time.perf_counter()
+        s2.train_batches(steps)
+        s2.sync()
+        barrier()
+        dt = time.perf_counter() - t0
+        st1 = s2.stats()
+        dt, total = finish(dt, st1["positions"] - st0["positions"])
+        out = {"metric": "sent2vec trained words/sec (frozen word table, doc-sharded)", "value": total / dt,
+               "unit": "words/s", "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": dt * 1e3 / steps,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 table, f64 math",
+               "data": "synthetic Zipf(s=1) docs of 50-200 tokens over V=1M, hash-initialised word table",
+               "config": {"workload": "sent2vec, D=%d, window %d, negative %d, %d docs per minibatch, word table "
+                                      "1M x %d" % (D, args.window, args.negative, args.s2v_docs, D),
+                          "parallelism": "doc-sharded over %d GPU(s), no exchange" % world}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -250,6 +250,11 @@ int swps_s2v_destroy(swps_s2v *s);
 /* corpus text (one sentence per line) or pre-split tokens: tok_keys[ntok],
  * line_off[nlines+1], sent_ids[nlines]; fixes the minibatch schedule */
 int swps_s2v_load_text(swps_s2v *s, const char *path);
+/* Doc-sharded multi-GPU sent2vec (BASELINE config 5): call
+ * before loading; the loaders then keep only the lines whose sentence id
+ * BasicHashFrag maps to node rank+1 (no exchange: documents are independent,
+ * the word table is read-only and replicated on every GPU). */
+int swps_s2v_shard(swps_s2v *s, int32_t rank, int32_t world, int32_t frag_num);
 int swps_s2v_load_tokens(swps_s2v *s, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,
                          uint64_t nlines, const uint64_t *sent_ids);
 /* nlines, sentences, minibatches, tokens, inserted keys, max sentences per
@@ -294,6 +299,27 @@ int swps_lr_params(swps_lr *l, uint32_t *keys, float *w, float *g2, uint64_t cap
 int swps_lr_info(swps_lr *l, uint64_t *out4); /* nrows, nkeys, nbatches, nnz */
 int swps_lr_sync(swps_lr *l);
 int swps_lr_kernel_times(swps_lr *l, double *out8, int32_t reset);
+/* mean of (y-p)^2 over all rows as of each row's last training (lr.cpp:231) */
+int swps_lr_epoch_error(swps_lr *l, double *err);
+void *swps_lr_stream(swps_lr *l);
+
+/* ---- sharded LR (several GPUs; the caller moves the payloads) ------------
+ * Same protocol as sharded word2vec, 1 fp32 value per key (lr.cpp:32-81):
+ *   swps_lr_request -> all-to-all -> swps_lr_serve_pull (owner: weights [n])
+ *   -> all-to-all -> swps_lr_step (install, forward, mean gradients [U] fp32
+ *   in request order) -> all-to-all -> swps_lr_serve_push (owner: AdaGrad
+ *   per source rank, in rank order).
+ * First full pull (lr.cpp:161-166): swps_lr_request(init=1) ->
+ * serve_pull(insert=1) -> swps_lr_install, which also refreshes the worker
+ * cache swps_lr_predict reads.  Tables use SWPS_INIT_HASH and init_ref = 0. */
+int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num);
+int swps_lr_batch_counts(swps_lr *l, uint64_t *out, uint64_t cap, uint64_t *nb);
+int swps_lr_request(swps_lr *l, int32_t init, uint64_t *counts, uint64_t *d_keys, uint64_t *n);
+int swps_lr_serve_pull(swps_lr *l, const uint64_t *d_keys, const uint64_t *src_counts, int32_t insert,
+                       float *d_vals);
+int swps_lr_install(swps_lr *l, const float *d_vals);
+int swps_lr_step(swps_lr *l, const float *d_vals, float *d_grads);
+int swps_lr_serve_push(swps_lr *l, const float *d_grads, const uint64_t *src_counts);
 
 #ifdef __cplusplus
 }

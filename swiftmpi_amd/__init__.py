@@ -362,6 +362,8 @@ class Sent2Vec:
             check(capi.lib().swps_s2v_create(self.table.h, ctypes.byref(cfg), ctypes.byref(h)))
             self.h = h
             self.table._deps.add(self)
+            if getattr(self, "_shard", None):
+                check(capi.lib().swps_s2v_shard(self.h, *self._shard))
 
     def close(self):
         if getattr(self, "h", None):
@@ -380,8 +382,14 @@ class Sent2Vec:
         tok_keys = np.ascontiguousarray(tok_keys, dtype=np.uint64)
         line_off = np.ascontiguousarray(line_off, dtype=np.uint64)
         sent_ids = np.ascontiguousarray(sent_ids, dtype=np.uint64)
+        assert len(sent_ids) == len(line_off) - 1
         check(capi.lib().swps_s2v_load_tokens(self.h, ptr(tok_keys), len(tok_keys), ptr(line_off),
                                                len(line_off) - 1, ptr(sent_ids)))
+
+    def shard(self, rank, world, frag_num=1000):
+        """Keep only the documents BasicHashFrag assigns to `rank` (call before
+        loading; config 5's doc-sharded layout, no exchange)."""
+        self._shard = (rank, world, frag_num)
 
     def info(self):
         o = np.zeros(9, dtype=np.uint64)

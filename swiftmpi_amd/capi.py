@@ -106,6 +106,7 @@ PROTOS = {
     "swps_s2v_create": (ctypes.c_int, [_p, ctypes.POINTER(S2VCfg), ctypes.POINTER(_p)]),
     "swps_s2v_destroy": (ctypes.c_int, [_p]),
     "swps_s2v_load_text": (ctypes.c_int, [_p, ctypes.c_char_p]),
+    "swps_s2v_shard": (ctypes.c_int, [_p, _i32, _i32, _i32]),
     "swps_s2v_load_tokens": (ctypes.c_int, [_p, _p, _u64, _p, _u64, _p]),
     "swps_s2v_info": (ctypes.c_int, [_p, _p]),
     "swps_s2v_train_batches": (ctypes.c_int, [_p, _u64]),
@@ -129,6 +130,15 @@ PROTOS = {
     "swps_lr_info": (ctypes.c_int, [_p, _p]),
     "swps_lr_sync": (ctypes.c_int, [_p]),
     "swps_lr_kernel_times": (ctypes.c_int, [_p, _p, _i32]),
+    "swps_lr_epoch_error": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_double)]),
+    "swps_lr_stream": (_p, [_p]),
+    "swps_lr_shard": (ctypes.c_int, [_p, _i32, _i32, _i32]),
+    "swps_lr_batch_counts": (ctypes.c_int, [_p, _p, _u64, ctypes.POINTER(_u64)]),
+    "swps_lr_request": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.POINTER(_u64)]),
+    "swps_lr_serve_pull": (ctypes.c_int, [_p, _p, _p, _i32, _p]),
+    "swps_lr_install": (ctypes.c_int, [_p, _p]),
+    "swps_lr_step": (ctypes.c_int, [_p, _p, _p]),
+    "swps_lr_serve_push": (ctypes.c_int, [_p, _p, _p]),
 }
 
 _lib = None

@@ -28,60 +28,180 @@ using namespace swps;
 
 namespace {
 
-__global__ void k_lr_forward(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
+// weight of vid: from the shard rows [w | g2] (single GPU) or, vid_row ==
+// nullptr, from the worker's pulled cache (sharded mode, param.h:13-68)
+__device__ __forceinline__ float weight(const uint32_t *__restrict__ vid_row, const float *__restrict__ w, int32_t v) {
+  return vid_row ? w[(uint64_t)vid_row[v] * 2] : w[v];
+}
+
+// Ordered fp32 sum of one value per lane (lanes [0, m)) added to acc in lane
+// order — the reference's sequential `sum += ...` (bit-exact), with the loads
+// of all lanes issued in parallel.
+__device__ __forceinline__ float ordered_add(float acc, float x, int m) {
+  for (int k = 0; k < m; k++) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k));
+  return acc;
+}
+
+// One wave per example (LR::learn_instance, lr.cpp:358-375): lane k holds
+// feature k of the row (64 at a time), s = sum w_i*x_i in feature order,
+// p = 1/(1+exp(-s)), e = y - p; gradient record (vid, e*x_i) per feature in
+// (row, feature) order.
+__global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
                              const float *__restrict__ fval, const float *__restrict__ label, uint64_t r0, uint64_t nr,
                              const uint32_t *__restrict__ vid_row, const float *__restrict__ rows,
-                             float *__restrict__ contrib, uint32_t *__restrict__ keys, uint32_t *__restrict__ idx,
+                             float *__restrict__ contrib, uint32_t *__restrict__ keys,
                              float *__restrict__ err2, uint64_t nz0) {
-  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t j = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (j >= nr) return;
   const uint64_t r = r0 + j;
   const uint64_t a = row_off[r], b = row_off[r + 1];
   float sum = 0;
-  for (uint64_t i = a; i < b; i++) {
-    const float w = rows[(uint64_t)vid_row[fvid[i]] * 2];
-    const float prod = w * fval[i];
-    sum += prod;
+  for (uint64_t c = a; c < b; c += 64) {
+    const int m = (int)min<uint64_t>(64, b - c);
+    float prod = 0.f;
+    if (lane < m) {
+      const float w = weight(vid_row, rows, fvid[c + lane]);
+      prod = w * fval[c + lane];
+    }
+    sum = ordered_add(sum, prod, m);
   }
   const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
   const float error = label[r] - predict;
-  for (uint64_t i = a; i < b; i++) {
-    contrib[i - nz0] = error * fval[i];
-    keys[i - nz0] = (uint32_t)fvid[i];
-    idx[i - nz0] = (uint32_t)(i - nz0);
+  for (uint64_t c = a + lane; c < b; c += 64) {
+    contrib[c - nz0] = error * fval[c];
+    keys[c - nz0] = (uint32_t)fvid[c];
   }
-  err2[r] = error * error;
+  if (lane == 0) err2[r] = error * error;
 }
 
-__global__ void k_lr_push(const uint32_t *__restrict__ uniq, const uint32_t *__restrict__ cnt,
-                          const uint32_t *__restrict__ off, const uint32_t *__restrict__ nruns,
-                          const uint32_t *__restrict__ sidx, const float *__restrict__ contrib,
-                          const uint32_t *__restrict__ vid_row, float *__restrict__ rows, float lr, float fudge) {
-  const uint32_t R = *nruns;
+// Per pushed key (a run of the sorted records): s = sum of e*x_i in record
+// order (fp32, sequential like `grads[i].val += ...`), mean = s/count
+// (lr.cpp:32-38); then either AdaGrad on the shard row (lr.cpp:68-75) or, in
+// sharded mode, the mean into the push request at local[vid].
+constexpr uint32_t kLrShort = 32;
+
+struct LrReduce {
+  const uint32_t *uniq, *cnt, *off, *nruns;
+  const float *val;  // contributions sorted by key (stable)
+  const uint32_t *vid_row;
+  float *rows;
+  float lr, fudge;
+  const int32_t *local;
+  float *grads;
+  uint32_t *nlong, *longs;
+};
+
+__device__ __forceinline__ void lr_apply(const LrReduce &a, uint32_t r, float s, uint32_t c) {
+  const float m = float(s / c);
+  if (a.grads) {
+    a.grads[a.local[a.uniq[r]]] = m;
+    return;
+  }
+  float *row = a.rows + (uint64_t)a.vid_row[a.uniq[r]] * 2;
+  const float g2 = row[1] + m * m;
+  row[1] = g2;
+  const float step = a.lr * m;
+  row[0] = row[0] + step / sqrtf(g2 + a.fudge);
+}
+
+__global__ __launch_bounds__(256) void k_lr_reduce_short(LrReduce a) {
+  const uint32_t R = *a.nruns;
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < R; r += gridDim.x * blockDim.x) {
-    const uint32_t o = off[r], c = cnt[r];
+    const uint32_t o = a.off[r], c = a.cnt[r];
+    if (c > kLrShort) {
+      a.longs[atomicAdd(a.nlong, 1u)] = r;
+      continue;
+    }
     float s = 0;
-    for (uint32_t i = o; i < o + c; i++) s += contrib[sidx[i]];
-    const float m = float(s / c);
-    float *row = rows + (uint64_t)vid_row[uniq[r]] * 2;
-    const float g2 = row[1] + m * m;
-    row[1] = g2;
-    const float step = lr * m;
-    row[0] = row[0] + step / sqrtf(g2 + fudge);
+    for (uint32_t i = o; i < o + c; i++) s += a.val[i];
+    lr_apply(a, r, s, c);
   }
 }
 
-__global__ void k_lr_predict(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
+// Long runs (hot features): the exact sequential fp32 chain is the bound, so
+// keep it fed — the wave stages 512 records at a time into LDS with
+// coalesced loads (next chunk's loads in flight) and lane 0 runs the add
+// chain from LDS.
+constexpr uint32_t kLrStage = 512;
+__global__ __launch_bounds__(256) void k_lr_reduce_long(LrReduce a) {
+  __shared__ float4 stage[4][kLrStage / 4];
+  const int lane = threadIdx.x & 63;
+  float4 *b4 = stage[threadIdx.x >> 6];
+  float *b = (float *)b4;
+  const uint32_t NL = *a.nlong;
+  for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < NL; q += gridDim.x * 4) {
+    const uint32_t r = a.longs[q];
+    const uint32_t o = a.off[r], c = a.cnt[r];
+    float s = 0;
+    float x[kLrStage / 64];
+#pragma unroll
+    for (uint32_t u = 0; u < kLrStage / 64; u++) {
+      const uint32_t k = u * 64 + lane;
+      x[u] = k < c ? a.val[o + k] : 0.f;
+    }
+    for (uint32_t i = 0; i < c; i += kLrStage) {
+      const uint32_t n = min(kLrStage, c - i);
+#pragma unroll
+      for (uint32_t u = 0; u < kLrStage / 64; u++) b[u * 64 + lane] = x[u];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // prefetch the next chunk while lane 0 sums this one
+#pragma unroll
+      for (uint32_t u = 0; u < kLrStage / 64; u++) {
+        const uint32_t k = i + kLrStage + u * 64 + lane;
+        x[u] = k < c ? a.val[o + k] : 0.f;
+      }
+      if (lane == 0) {
+        uint32_t k = 0;
+        for (; k + 16 <= n; k += 16) {
+          const float4 v0 = b4[k / 4], v1 = b4[k / 4 + 1], v2 = b4[k / 4 + 2], v3 = b4[k / 4 + 3];
+          s += v0.x; s += v0.y; s += v0.z; s += v0.w;
+          s += v1.x; s += v1.y; s += v1.z; s += v1.w;
+          s += v2.x; s += v2.y; s += v2.z; s += v2.w;
+          s += v3.x; s += v3.y; s += v3.z; s += v3.w;
+        }
+        for (; k < n; k++) s += b[k];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) lr_apply(a, r, s, c);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lr_predict(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
                              const float *__restrict__ fval, uint64_t nr, const uint32_t *__restrict__ vid_row,
                              const float *__restrict__ rows, float *__restrict__ pred) {
-  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (r >= nr) return;
+  const uint64_t a = row_off[r], b = row_off[r + 1];
   float sum = 0;
-  for (uint64_t i = row_off[r]; i < row_off[r + 1]; i++) {
-    const float prod = rows[(uint64_t)vid_row[fvid[i]] * 2] * fval[i];
-    sum += prod;
+  for (uint64_t c = a; c < b; c += 64) {
+    const int m = (int)min<uint64_t>(64, b - c);
+    float prod = 0.f;
+    if (lane < m) prod = weight(vid_row, rows, fvid[c + lane]) * fval[c + lane];
+    sum = ordered_add(sum, prod, m);
   }
-  pred[r] = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
+  if (lane == 0) pred[r] = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
+}
+
+// pulled weights [U] (request order K) into the worker cache; local[vid] = u
+__global__ void k_lr_install(const int32_t *__restrict__ K, uint64_t U, const float *__restrict__ vals,
+                             float *__restrict__ wcache, int32_t *__restrict__ local) {
+  uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  wcache[K[u]] = vals[u];
+  if (local) local[K[u]] = (int32_t)u;
+}
+
+__global__ void k_lr_keys(const int32_t *__restrict__ K, uint64_t n, const uint64_t *__restrict__ vkeys,
+                          uint64_t *__restrict__ out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = vkeys[K[i]];
 }
 
 inline unsigned nblk(uint64_t n, unsigned bs = 256) { return (unsigned)std::max<uint64_t>(1, (n + bs - 1) / bs); }
@@ -131,10 +251,17 @@ struct swps_lr {
   std::vector<uint64_t> vocab_keys;  // vid order = first-pull order
   bool loaded = false, inited = false;
   uint64_t cursor = 0, nbatches = 0;
-  DevMem d_label, d_row_off, d_fvid, d_fval, d_vid_row, d_contrib, d_keys, d_idx, d_keys_s, d_idx_s, d_uniq, d_cnt,
-      d_off, d_nruns, d_err2, d_tmp, d_pred;
+  DevMem d_label, d_row_off, d_fvid, d_fval, d_vid_row, d_contrib, d_keys, d_keys_s, d_val_s, d_uniq, d_cnt,
+      d_off, d_nruns, d_err2, d_tmp, d_pred, d_longs;
   uint32_t *h_small = nullptr;
   LTimer timer;
+  // sharded mode (swps_lr_shard): per-batch key sets ordered by owner rank
+  bool sharded = false;
+  int32_t rank = 0, world = 1;
+  std::vector<int32_t> allK, init_order;  // vids
+  std::vector<uint64_t> kofs, bU, bcounts, icounts;
+  DevMem d_K, d_vkeys, d_init_order, d_wcache, d_local, d_serve_rows;
+  uint64_t serve_n = 0;
   int B1() const { return cfg.minibatch + 1; }
 };
 
@@ -166,30 +293,39 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   return SWPS_OK;
 }
 
-int lr_batch(swps_lr *l) {
+int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr) {
   const uint64_t nr = l->label.size();
   const uint64_t bi = l->cursor % l->nbatches;
   const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1());
   const uint64_t nz0 = l->row_off[r0], nnz = l->row_off[r1] - nz0;
   hipStream_t s = l->s;
   float *rows = l->t->rows.as<float>();
+  const uint32_t *vid_row = l->d_vid_row.as<uint32_t>();
   l->cursor++;
+  if (l->sharded) {  // install the owners' pull values; read weights from the cache
+    const uint64_t U = l->bU[bi];
+    if (U)
+      k_lr_install<<<nblk(U), 256, 0, s>>>(l->d_K.as<int32_t>() + l->kofs[bi], U, d_vals, l->d_wcache.as<float>(),
+                                           l->d_local.as<int32_t>());
+    SWPS_HIP(hipGetLastError());
+    rows = l->d_wcache.as<float>();
+    vid_row = nullptr;
+  }
   if (nnz == 0) return SWPS_OK;
   SWPS_TRY(l->d_contrib.ensure(nnz * 4));
   SWPS_TRY(l->d_keys.ensure(nnz * 4));
-  SWPS_TRY(l->d_idx.ensure(nnz * 4));
   SWPS_TRY(l->d_keys_s.ensure(nnz * 4));
-  SWPS_TRY(l->d_idx_s.ensure(nnz * 4));
+  SWPS_TRY(l->d_val_s.ensure(nnz * 4));
+  SWPS_TRY(l->d_longs.ensure((nnz + 1) * 4));
   SWPS_TRY(l->d_uniq.ensure(nnz * 4));
   SWPS_TRY(l->d_cnt.ensure((nnz + 1) * 4));
   SWPS_TRY(l->d_off.ensure((nnz + 1) * 4));
   SWPS_TRY(l->d_nruns.ensure(16));
   hipEvent_t e0 = l->timer.begin(s);
-  k_lr_forward<<<nblk(r1 - r0), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), l->d_fvid.as<int32_t>(),
-                                             l->d_fval.as<float>(), l->d_label.as<float>(), r0, r1 - r0,
-                                             l->d_vid_row.as<uint32_t>(), rows, l->d_contrib.as<float>(),
-                                             l->d_keys.as<uint32_t>(), l->d_idx.as<uint32_t>(), l->d_err2.as<float>(),
-                                             nz0);
+  k_lr_forward<<<nblk((r1 - r0) * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), l->d_fvid.as<int32_t>(),
+                                                    l->d_fval.as<float>(), l->d_label.as<float>(), r0, r1 - r0,
+                                                    vid_row, rows, l->d_contrib.as<float>(),
+                                                    l->d_keys.as<uint32_t>(), l->d_err2.as<float>(), nz0);
   SWPS_HIP(hipGetLastError());
   l->timer.end(0, e0, s);
   int bits = 1;
@@ -197,7 +333,7 @@ int lr_batch(swps_lr *l) {
   hipEvent_t e1 = l->timer.begin(s);
   size_t b1 = 0, b2 = 0, b3 = 0;
   SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(),
-                                              l->d_idx.as<uint32_t>(), l->d_idx_s.as<uint32_t>(), (int)nnz, 0, bits,
+                                              l->d_contrib.as<float>(), l->d_val_s.as<float>(), (int)nnz, 0, bits,
                                               s));
   SWPS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, l->d_keys_s.as<uint32_t>(), l->d_uniq.as<uint32_t>(),
                                                  l->d_cnt.as<uint32_t>(), l->d_nruns.as<uint32_t>(), (int)nnz, s));
@@ -206,7 +342,7 @@ int lr_batch(swps_lr *l) {
   SWPS_TRY(l->d_tmp.ensure(std::max(b1, std::max(b2, b3))));
   size_t tb = l->d_tmp.bytes;
   SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(l->d_tmp.p, tb, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(),
-                                              l->d_idx.as<uint32_t>(), l->d_idx_s.as<uint32_t>(), (int)nnz, 0, bits,
+                                              l->d_contrib.as<float>(), l->d_val_s.as<float>(), (int)nnz, 0, bits,
                                               s));
   tb = l->d_tmp.bytes;
   SWPS_HIP(hipcub::DeviceRunLengthEncode::Encode(l->d_tmp.p, tb, l->d_keys_s.as<uint32_t>(), l->d_uniq.as<uint32_t>(),
@@ -216,10 +352,15 @@ int lr_batch(swps_lr *l) {
                                             (int)nnz, s));
   l->timer.end(1, e1, s);
   hipEvent_t e3 = l->timer.begin(s);
-  k_lr_push<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(
-      l->d_uniq.as<uint32_t>(), l->d_cnt.as<uint32_t>(), l->d_off.as<uint32_t>(), l->d_nruns.as<uint32_t>(),
-      l->d_idx_s.as<uint32_t>(), l->d_contrib.as<float>(), l->d_vid_row.as<uint32_t>(), rows,
-      l->t->cfg.learning_rate, l->t->cfg.fudge);
+  // the run counter lives past the last possible long-run index
+  uint32_t *nlong = l->d_longs.as<uint32_t>() + nnz;
+  SWPS_HIP(hipMemsetAsync(nlong, 0, 4, s));
+  LrReduce ra{l->d_uniq.as<uint32_t>(), l->d_cnt.as<uint32_t>(), l->d_off.as<uint32_t>(), l->d_nruns.as<uint32_t>(),
+              l->d_val_s.as<float>(), l->d_vid_row.as<uint32_t>(), l->t->rows.as<float>(), l->t->cfg.learning_rate,
+              l->t->cfg.fudge, l->d_local.as<int32_t>(), l->sharded ? d_grads : nullptr, nlong,
+              l->d_longs.as<uint32_t>()};
+  k_lr_reduce_short<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(ra);
+  k_lr_reduce_long<<<(unsigned)std::min<uint64_t>(nblk(nnz * 64 / kLrShort), 2048), 256, 0, s>>>(ra);
   SWPS_HIP(hipGetLastError());
   l->timer.end(3, e3, s);
   return SWPS_OK;
@@ -335,6 +476,7 @@ int swps_lr_init(swps_lr *l) {
 }
 
 int swps_lr_train_batches(swps_lr *l, uint64_t count) {
+  if (l->sharded) return fail(SWPS_E_STATE, "sharded: drive swps_lr_request/serve_pull/step/serve_push");
   if (!l->inited) return fail(SWPS_E_STATE, "call swps_lr_init first");
   if (l->nbatches == 0) return SWPS_OK;
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
@@ -344,19 +486,24 @@ int swps_lr_train_batches(swps_lr *l, uint64_t count) {
 
 // lr.cpp:175-236: per epoch the mean of (y-p)^2 over the trained rows,
 // accumulated in row order in double like `total_error`.
-int swps_lr_train(swps_lr *l, int32_t niters, double *err_out) {
-  if (l->cursor % std::max<uint64_t>(1, l->nbatches)) return fail(SWPS_E_STATE, "not at an epoch boundary");
+int swps_lr_epoch_error(swps_lr *l, double *err) {
   const uint64_t nr = l->label.size();
   std::vector<float> e2(nr);
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  if (nr) SWPS_HIP(hipMemcpyAsync(e2.data(), l->d_err2.p, nr * 4, hipMemcpyDeviceToHost, l->s));
+  SWPS_HIP(hipStreamSynchronize(l->s));
+  double tot = 0;
+  for (uint64_t r = 0; r < nr; r++) tot += e2[r];
+  *err = nr ? tot / (double)nr : 0.0;
+  return SWPS_OK;
+}
+
+int swps_lr_train(swps_lr *l, int32_t niters, double *err_out) {
+  if (l->sharded) return fail(SWPS_E_STATE, "sharded: drive swps_lr_request/serve_pull/step/serve_push");
+  if (l->cursor % std::max<uint64_t>(1, l->nbatches)) return fail(SWPS_E_STATE, "not at an epoch boundary");
   for (int it = 0; it < niters; it++) {
     SWPS_TRY(swps_lr_train_batches(l, l->nbatches));
-    if (err_out) {
-      SWPS_HIP(hipMemcpyAsync(e2.data(), l->d_err2.p, nr * 4, hipMemcpyDeviceToHost, l->s));
-      SWPS_HIP(hipStreamSynchronize(l->s));
-      double tot = 0;
-      for (uint64_t r = 0; r < nr; r++) tot += e2[r];
-      err_out[it] = nr ? tot / (double)nr : 0.0;
-    }
+    if (err_out) SWPS_TRY(swps_lr_epoch_error(l, &err_out[it]));
   }
   return swps_lr_sync(l);
 }
@@ -374,8 +521,9 @@ int swps_lr_predict(swps_lr *l, float *pred_out, float *target_out, uint64_t cap
   if (cap < nr) return fail(SWPS_E_CFG, "buffer too small");
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
   SWPS_TRY(l->d_pred.ensure(std::max<uint64_t>(1, nr) * 4));
-  k_lr_predict<<<nblk(nr), 256, 0, l->s>>>(l->d_row_off.as<uint64_t>(), l->d_fvid.as<int32_t>(), l->d_fval.as<float>(),
-                                            nr, l->d_vid_row.as<uint32_t>(), l->t->rows.as<float>(),
+  k_lr_predict<<<nblk(nr * 64), 256, 0, l->s>>>(l->d_row_off.as<uint64_t>(), l->d_fvid.as<int32_t>(), l->d_fval.as<float>(),
+                                            nr, l->sharded ? nullptr : l->d_vid_row.as<uint32_t>(),
+                                            l->sharded ? l->d_wcache.as<float>() : l->t->rows.as<float>(),
                                             l->d_pred.as<float>());
   SWPS_HIP(hipGetLastError());
   if (nr) SWPS_HIP(hipMemcpyAsync(pred_out, l->d_pred.p, nr * 4, hipMemcpyDeviceToHost, l->s));
@@ -427,5 +575,159 @@ int swps_lr_kernel_times(swps_lr *l, double *out, int32_t reset) {
   }
   return SWPS_OK;
 }
+
+// ============================================================================
+// Key-sharded LR over several GPUs (one process per GPU; the caller moves the
+// payloads, swiftmpi_amd/dist.py).  Key -> owner = BasicHashFrag node - 1
+// (cluster/hashfrag.h:33-56).  Per batch: request (the batch's unique
+// features, grouped by owner) -> serve_pull (owner: weights) -> step
+// (install, forward, mean gradients in request order) -> serve_push (owner:
+// AdaGrad once per source rank, in rank order; lr.cpp:58-81).
+// ============================================================================
+
+int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
+  if (!l->loaded) return fail(SWPS_E_STATE, "load data first");
+  if (l->inited) return fail(SWPS_E_STATE, "shard before swps_lr_init / the first pull");
+  if (world < 1 || rank < 0 || rank >= world) return fail(SWPS_E_CFG, "bad rank/world");
+  if (l->cfg.init_ref)
+    return fail(SWPS_E_UNSUPPORTED, "sharded mode initialises on the owners (init_ref = 0, SWPS_INIT_HASH): the "
+                                    "reference's float-LCG order depends on message arrival");
+  std::vector<uint32_t> map(frag_num);
+  SWPS_TRY(swps_hashfrag_table(frag_num, world, map.data()));
+  const uint64_t V = l->vocab_keys.size(), nb = l->nbatches, nr = l->label.size();
+  std::vector<int32_t> owner(V);
+  for (uint64_t i = 0; i < V; i++) owner[i] = (int32_t)map[fmix64(l->vocab_keys[i]) % (uint64_t)frag_num] - 1;
+  // per batch: unique vids in owner order, then vid order (counting sort by owner)
+  std::vector<uint64_t> stamp(V, ~0ULL);
+  std::vector<int32_t> uniq;
+  std::vector<uint64_t> start(world + 1);
+  l->allK.clear();
+  l->kofs.assign(nb, 0);
+  l->bU.assign(nb, 0);
+  l->bcounts.assign(nb * world, 0);
+  for (uint64_t bi = 0; bi < nb; bi++) {
+    const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1());
+    uniq.clear();
+    for (uint64_t i = l->row_off[r0]; i < l->row_off[r1]; i++) {
+      const int32_t v = l->fvid[i];
+      if (stamp[v] != bi) {
+        stamp[v] = bi;
+        uniq.push_back(v);
+      }
+    }
+    std::sort(uniq.begin(), uniq.end());
+    uint64_t *cnt = &l->bcounts[bi * world];
+    for (int32_t v : uniq) cnt[owner[v]]++;
+    start[0] = 0;
+    for (int r = 0; r < world; r++) start[r + 1] = start[r] + cnt[r];
+    l->kofs[bi] = l->allK.size();
+    l->bU[bi] = uniq.size();
+    l->allK.resize(l->allK.size() + uniq.size());
+    int32_t *dst = l->allK.data() + l->kofs[bi];
+    for (int32_t v : uniq) dst[start[owner[v]]++] = v;
+  }
+  l->init_order.resize(V);
+  for (uint64_t i = 0; i < V; i++) l->init_order[i] = (int32_t)i;
+  std::stable_sort(l->init_order.begin(), l->init_order.end(),
+                   [&](int32_t a, int32_t b) { return owner[a] < owner[b]; });
+  l->icounts.assign(world, 0);
+  for (uint64_t i = 0; i < V; i++) l->icounts[owner[i]]++;
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  SWPS_TRY(upload(l->d_K, l->allK, l->s));
+  SWPS_TRY(upload(l->d_vkeys, l->vocab_keys, l->s));
+  SWPS_TRY(upload(l->d_init_order, l->init_order, l->s));
+  SWPS_TRY(l->d_wcache.ensure(std::max<uint64_t>(V, 1) * 4));
+  SWPS_TRY(l->d_local.ensure(std::max<uint64_t>(V, 1) * 4));
+  SWPS_HIP(hipMemsetAsync(l->d_wcache.p, 0, std::max<uint64_t>(V, 1) * 4, l->s));
+  SWPS_HIP(hipStreamSynchronize(l->s));
+  l->rank = rank;
+  l->world = world;
+  l->sharded = true;
+  return SWPS_OK;
+}
+
+int swps_lr_batch_counts(swps_lr *l, uint64_t *out, uint64_t cap, uint64_t *nb) {
+  if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
+  *nb = l->nbatches;
+  if (cap < l->bcounts.size()) return fail(SWPS_E_CFG, "buffer too small");
+  std::copy(l->bcounts.begin(), l->bcounts.end(), out);
+  return SWPS_OK;
+}
+
+int swps_lr_request(swps_lr *l, int32_t init, uint64_t *counts, uint64_t *d_keys, uint64_t *n) {
+  if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  if (init) {
+    std::copy(l->icounts.begin(), l->icounts.end(), counts);
+    *n = l->vocab_keys.size();
+    if (d_keys && *n)
+      k_lr_keys<<<nblk(*n), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), *n, l->d_vkeys.as<uint64_t>(), d_keys);
+  } else {
+    if (l->nbatches == 0) return fail(SWPS_E_STATE, "no batches");
+    const uint64_t bi = l->cursor % l->nbatches;
+    std::copy(l->bcounts.begin() + bi * l->world, l->bcounts.begin() + (bi + 1) * l->world, counts);
+    *n = l->bU[bi];
+    if (d_keys && *n)
+      k_lr_keys<<<nblk(*n), 256, 0, l->s>>>(l->d_K.as<int32_t>() + l->kofs[bi], *n, l->d_vkeys.as<uint64_t>(), d_keys);
+  }
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+int swps_lr_serve_pull(swps_lr *l, const uint64_t *d_keys, const uint64_t *src_counts, int32_t insert,
+                       float *d_vals) {
+  if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  uint64_t n = 0;
+  for (int r = 0; r < l->world; r++) n += src_counts[r];
+  SWPS_TRY(l->d_serve_rows.ensure(std::max<uint64_t>(n, 1) * 4));
+  uint32_t *rows = l->d_serve_rows.as<uint32_t>();
+  if (insert) {  // keys are distinct within a source, not across sources
+    uint64_t off = 0;
+    for (int r = 0; r < l->world; r++) {
+      SWPS_TRY(table_find_or_insert(l->t, d_keys + off, src_counts[r], rows + off, l->s));
+      off += src_counts[r];
+    }
+  } else {
+    SWPS_TRY(table_lookup(l->t, d_keys, n, rows, l->s));
+  }
+  SWPS_TRY(table_copy_pull(l->t, rows, n, d_vals, l->s));
+  l->serve_n = n;
+  return SWPS_OK;
+}
+
+int swps_lr_install(swps_lr *l, const float *d_vals) {
+  if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  const uint64_t V = l->vocab_keys.size();
+  if (V)
+    k_lr_install<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals, l->d_wcache.as<float>(),
+                                            nullptr);
+  SWPS_HIP(hipGetLastError());
+  l->inited = true;
+  return SWPS_OK;
+}
+
+int swps_lr_step(swps_lr *l, const float *d_vals, float *d_grads) {
+  if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
+  if (!l->inited) return fail(SWPS_E_STATE, "install the first full pull first");
+  if (l->nbatches == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  return lr_batch(l, d_vals, d_grads);
+}
+
+int swps_lr_serve_push(swps_lr *l, const float *d_grads, const uint64_t *src_counts) {
+  if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  uint64_t off = 0;
+  for (int r = 0; r < l->world; r++) {  // one AdaGrad step per source, in rank order
+    SWPS_TRY(table_push_rows(l->t, l->d_serve_rows.as<uint32_t>() + off, src_counts[r], d_grads + off, l->s));
+    off += src_counts[r];
+  }
+  if (off != l->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
+  return SWPS_OK;
+}
+
+void *swps_lr_stream(swps_lr *l) { return (void *)l->s; }
 
 }  // extern "C"

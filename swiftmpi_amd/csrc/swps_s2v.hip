@@ -311,6 +311,8 @@ struct swps_s2v {
   uint64_t nlines = 0, ntok = 0, misses = 0, rand_calls = 0, max_recs = 0, max_docs = 0;
   uint64_t lstate_end = 2008;
   bool loaded = false;
+  // doc sharding (swps_s2v_shard): keep the lines whose sentence id this rank owns
+  int32_t shard_rank = 0, shard_world = 1, shard_frag = 0;
   uint64_t cursor = 0;
   // device
   DevMem d_tok_row, d_doc_tok, d_doc_rec, d_doc_lcg, d_vocab_row, d_starts, d_init, d_exptab, d_rec, d_out, d_err,
@@ -377,8 +379,30 @@ void s2v_unigram_starts(const std::vector<std::pair<uint64_t, int32_t>> &vc, uin
 // The host schedule: Sent2Vec::train's loop (sent2vec.cpp:95-103) replayed
 // over the parsed corpus.  tok_keys/line_off describe every line, sent_ids
 // the BKDR hash of each line (sent2vec.cpp:75).
+int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std::vector<uint64_t> &line_off,
+                   const std::vector<uint64_t> &sent_ids);
+
+// Documents are independent and the word table is read-only:
+// a rank trains exactly the lines whose sentence id BasicHashFrag assigns to
+// it (hashfrag.h:33-56), with no exchange.
 int s2v_ingest(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std::vector<uint64_t> &line_off,
                const std::vector<uint64_t> &sent_ids) {
+  if (m->shard_world <= 1) return s2v_ingest_all(m, tok_keys, line_off, sent_ids);
+  std::vector<uint32_t> map(m->shard_frag);
+  SWPS_TRY(swps_hashfrag_table(m->shard_frag, m->shard_world, map.data()));
+  std::vector<uint64_t> k2, off2{0}, id2;
+  const uint64_t nl = line_off.size() - 1;
+  for (uint64_t l = 0; l < nl; l++) {
+    if ((int32_t)map[fmix64(sent_ids[l]) % (uint64_t)m->shard_frag] - 1 != m->shard_rank) continue;
+    k2.insert(k2.end(), tok_keys.begin() + line_off[l], tok_keys.begin() + line_off[l + 1]);
+    off2.push_back(k2.size());
+    id2.push_back(sent_ids[l]);
+  }
+  return s2v_ingest_all(m, k2, off2, id2);
+}
+
+int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std::vector<uint64_t> &line_off,
+                   const std::vector<uint64_t> &sent_ids) {
   const uint64_t nl = line_off.size() - 1;
   const int D = m->D, B = m->cfg.minibatch, N = m->N, S = 2 * m->W + m->N + 1;
   const uint64_t T = m->cfg.unigram_size;
@@ -657,6 +681,15 @@ int swps_s2v_load_text(swps_s2v *m, const char *path) {
   free(buf);
   fclose(f);
   return s2v_ingest(m, keys, off, ids);
+}
+
+int swps_s2v_shard(swps_s2v *m, int32_t rank, int32_t world, int32_t frag_num) {
+  if (m->loaded) return fail(SWPS_E_STATE, "shard before loading the corpus");
+  if (world < 1 || rank < 0 || rank >= world || frag_num < world) return fail(SWPS_E_CFG, "bad rank/world/frag_num");
+  m->shard_rank = rank;
+  m->shard_world = world;
+  m->shard_frag = frag_num;
+  return SWPS_OK;
 }
 
 int swps_s2v_load_tokens(swps_s2v *m, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,

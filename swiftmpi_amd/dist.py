@@ -1,4 +1,4 @@
-"""Key-sharded multi-GPU word2vec: one process per GPU, the reference's
+"""Key-sharded multi-GPU word2vec and LR: one process per GPU, the reference's
 worker+server-per-rank layout with the ZeroMQ request /
 response path (transfer/transfer.h:86-241) replaced by three all-to-all-v
 exchanges per minibatch over torch.distributed — RCCL over xGMI with the
@@ -20,7 +20,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import Word2Vec, capi
+from . import LR, Word2Vec, capi
 from .capi import check, ptr
 
 
@@ -65,20 +65,14 @@ class Exchanger:
         return int(t.item())
 
 
-class ShardedWord2Vec:
-    """Word2Vec over key-sharded HBM tables on several GPUs (one per rank).
+class _ShardedApp:
+    """Lockstep driver of a sharded app context (swps_<app>_request /
+    serve_pull / step / serve_push).  Subclasses set the handle `self.h`,
+    the C prefix `self.pfx`, the value width per key `self.width`, and the
+    value / gradient tensor dtypes."""
 
-    The table passed in is this rank's shard (create it with init="hash":
-    owners initialise keys on their first pull)."""
-
-    def __init__(self, table, group=None, frag_num=1000, **kw):
-        kw.setdefault("init", "table")
-        self.w = Word2Vec(table, **kw)
-        # push payload: fp64 (the reference's wire format) unless fast mode (fp32 table, fp32 intermediates)
-        fast = table.dtype == "f32" and not kw.get("fp64_intermediates", True)
-        self.grad_dtype = torch.float32 if fast else torch.float64
+    def _setup(self, table, group, frag_num):
         self.table = table
-        self.D = table.dim
         self.dev = torch.device("cuda", table.device)
         self.ex = Exchanger(group, self.dev)
         self.rank, self.world = self.ex.rank, self.ex.world
@@ -86,25 +80,18 @@ class ShardedWord2Vec:
         self.cursor = 0
         self._ext = None
 
-    # -- setup -----------------------------------------------------------------
-    def load_text(self, path):
-        self.w.load_text(path)
-        self._shard()
+    def _fn(self, name):
+        return getattr(capi.lib(), "swps_%s_%s" % (self.pfx, name))
 
-    def load_tokens(self, word_ids, line_off, word_keys):
-        self.w.load_tokens(word_ids, line_off, word_keys)
-        self._shard()
-
-    def _shard(self):
-        check(capi.lib().swps_w2v_shard(self.w.h, self.rank, self.world, self.frag_num))
-        nb = self.w.info()["batches"]
-        cnt = np.zeros(nb * self.world, dtype=np.uint64)
+    def _shard(self, nb):
+        check(self._fn("shard")(self.h, self.rank, self.world, self.frag_num))
+        cnt = np.zeros(max(nb * self.world, 1), dtype=np.uint64)
         n = ctypes.c_uint64()
-        check(capi.lib().swps_w2v_batch_counts(self.w.h, ptr(cnt), len(cnt), ctypes.byref(n)))
+        check(self._fn("batch_counts")(self.h, ptr(cnt), len(cnt), ctypes.byref(n)))
         self.nb = nb
         self.steps_per_epoch = self.ex.max(nb)
         mat = np.zeros((self.steps_per_epoch, self.world), dtype=np.int64)
-        mat[:nb] = cnt.reshape(nb, self.world).astype(np.int64)
+        mat[:nb] = cnt[:nb * self.world].reshape(nb, self.world).astype(np.int64)
         g = self.ex.all_gather_matrix(mat)  # [src][step][dst]
         self.send_counts = g[self.rank]                 # [step][dst]
         self.recv_counts = g[:, :, self.rank].T.copy()  # [step][src]
@@ -113,17 +100,13 @@ class ShardedWord2Vec:
         if self.ex.backend != "nccl":
             return None
         if self._ext is None:
-            self._ext = torch.cuda.ExternalStream(self.w.stream(), device=self.dev)
+            self._ext = torch.cuda.ExternalStream(self._fn("stream")(self.h), device=self.dev)
         return self._ext
-
-    def _sync_for_host(self):
-        if self.ex.backend != "nccl":
-            self.w.sync()
 
     def _exchange(self, send, sc, rc, width):
         s = self._stream()
         if s is None:
-            self._sync_for_host()
+            check(self._fn("sync")(self.h))  # gloo stages through the host
             return self.ex.a2a(send, sc, rc, width)
         with torch.cuda.stream(s):  # RCCL ordered after / before the library's kernels
             return self.ex.a2a(send, sc, rc, width)
@@ -135,27 +118,26 @@ class ShardedWord2Vec:
         with torch.cuda.stream(s):
             return torch.empty(n, dtype=dtype, device=self.dev)
 
-    # -- the first full pull (word2vec_global.h:557-562) ------------------------
-    def init(self):
-        L = capi.lib()
+    def full_pull(self):
+        """Pull every key of the local data (the reference's first full pull)
+        into the worker cache, inserting keys new to their owners."""
         counts = np.zeros(self.world, dtype=np.uint64)
         n = ctypes.c_uint64()
-        check(L.swps_w2v_request(self.w.h, 1, ptr(counts), None, ctypes.byref(n)))
+        check(self._fn("request")(self.h, 1, ptr(counts), None, ctypes.byref(n)))
         keys = self._empty(n.value, torch.int64)
-        check(L.swps_w2v_request(self.w.h, 1, ptr(counts), ptr(keys), ctypes.byref(n)))
+        check(self._fn("request")(self.h, 1, ptr(counts), ptr(keys), ctypes.byref(n)))
         sc = counts.astype(np.int64)
         rc = self.ex.all_gather_matrix(sc[None, :])[:, 0, self.rank].copy()  # [src]
         rkeys = self._exchange(keys, sc, rc, 1)
-        vals = self._empty(int(rc.sum()) * 2 * self.D, self.table.torch_dtype)
+        vals = self._empty(int(rc.sum()) * self.width, self.val_dtype)
         rcu = rc.astype(np.uint64)
-        check(L.swps_w2v_serve_pull(self.w.h, ptr(rkeys), ptr(rcu), 1, ptr(vals)))
-        mine = self._exchange(vals, rc, sc, 2 * self.D)
-        check(L.swps_w2v_install_init(self.w.h, ptr(mine)))
-        self.w.sync()
+        check(self._fn("serve_pull")(self.h, ptr(rkeys), ptr(rcu), 1, ptr(vals)))
+        mine = self._exchange(vals, rc, sc, self.width)
+        check(self._fn(self.install_fn)(self.h, ptr(mine)))
+        check(self._fn("sync")(self.h))
 
-    # -- one lockstep minibatch ------------------------------------------------
     def step(self):
-        L = capi.lib()
+        """One lockstep minibatch on every rank."""
         s = self.cursor % self.steps_per_epoch
         sc, rc = self.send_counts[s], self.recv_counts[s]
         nsend = int(sc.sum())
@@ -164,17 +146,17 @@ class ShardedWord2Vec:
         if mine and nsend:
             counts = np.zeros(self.world, dtype=np.uint64)
             n = ctypes.c_uint64()
-            check(L.swps_w2v_request(self.w.h, 0, ptr(counts), ptr(keys), ctypes.byref(n)))
+            check(self._fn("request")(self.h, 0, ptr(counts), ptr(keys), ctypes.byref(n)))
         rkeys = self._exchange(keys, sc, rc, 1)
-        vals = self._empty(int(rc.sum()) * 2 * self.D, self.table.torch_dtype)
+        vals = self._empty(int(rc.sum()) * self.width, self.val_dtype)
         rcu = rc.astype(np.uint64)
-        check(L.swps_w2v_serve_pull(self.w.h, ptr(rkeys), ptr(rcu), 0, ptr(vals)))
-        my_vals = self._exchange(vals, rc, sc, 2 * self.D)
-        grads = self._empty(nsend * 2 * self.D, self.grad_dtype)
+        check(self._fn("serve_pull")(self.h, ptr(rkeys), ptr(rcu), 0, ptr(vals)))
+        my_vals = self._exchange(vals, rc, sc, self.width)
+        grads = self._empty(nsend * self.width, self.grad_dtype)
         if mine:
-            check(L.swps_w2v_step(self.w.h, ptr(my_vals) if nsend else None, ptr(grads) if nsend else None))
-        rgrads = self._exchange(grads, sc, rc, 2 * self.D)
-        check(L.swps_w2v_serve_push(self.w.h, ptr(rgrads), ptr(rcu)))
+            check(self._fn("step")(self.h, ptr(my_vals) if nsend else None, ptr(grads) if nsend else None))
+        rgrads = self._exchange(grads, sc, rc, self.width)
+        check(self._fn("serve_push")(self.h, ptr(rgrads), ptr(rcu)))
         self.cursor += 1
 
     def train_steps(self, n):
@@ -183,13 +165,48 @@ class ShardedWord2Vec:
 
     train_batches = train_steps
 
+    def sync(self):
+        check(self._fn("sync")(self.h))
+        torch.cuda.synchronize(self.dev)
+
+
+class ShardedWord2Vec(_ShardedApp):
+    """Word2Vec over key-sharded HBM tables on several GPUs (one per rank).
+
+    The table passed in is this rank's shard (create it with init="hash":
+    owners initialise keys on their first pull)."""
+
+    pfx = "w2v"
+    install_fn = "install_init"
+
+    def __init__(self, table, group=None, frag_num=1000, **kw):
+        kw.setdefault("init", "table")
+        self.w = Word2Vec(table, **kw)
+        self.h = self.w.h
+        self._setup(table, group, frag_num)
+        self.D = table.dim
+        self.width = 2 * self.D
+        self.val_dtype = table.torch_dtype
+        # push payload: fp64 (the reference's wire format) unless fast mode (fp32 table, fp32 intermediates)
+        fast = table.dtype == "f32" and not kw.get("fp64_intermediates", True)
+        self.grad_dtype = torch.float32 if fast else torch.float64
+
+    # -- setup -----------------------------------------------------------------
+    def load_text(self, path):
+        self.w.load_text(path)
+        self._shard(self.w.info()["batches"])
+
+    def load_tokens(self, word_ids, line_off, word_keys):
+        self.w.load_tokens(word_ids, line_off, word_keys)
+        self._shard(self.w.info()["batches"])
+
+    def init(self):
+        """The first full pull (word2vec_global.h:557-562)."""
+        self.full_pull()
+
     def train(self, niters=1):
         self.train_steps(niters * self.steps_per_epoch)
         self.sync()
-
-    def sync(self):
-        self.w.sync()
-        torch.cuda.synchronize(self.dev)
 
     def stats(self):
         return self.w.stats()
@@ -210,3 +227,64 @@ class ShardedWord2Vec:
             return keys, np.zeros((0, 4 * self.D))
         kt = torch.as_tensor(keys.astype(np.int64), device=self.dev)
         return keys, self.table.export(kt).double().cpu().numpy()
+
+
+class ShardedLR(_ShardedApp):
+    """Sparse LR over key-sharded HBM tables (BASELINE config 3): one fp32
+    weight per feature key, owners apply AdaGrad per source rank in rank
+    order (lr.cpp:58-81).  The table must be created with init="hash"."""
+
+    pfx = "lr"
+    install_fn = "install"
+    width = 1
+    val_dtype = torch.float32
+    grad_dtype = torch.float32
+
+    def __init__(self, table, group=None, frag_num=2000, minibatch=200, profile=False):
+        self.m = LR(table, minibatch=minibatch, init_ref=False, profile=profile)
+        self.h = self.m.h
+        self._setup(table, group, frag_num)
+
+    def load_text(self, path):
+        self.m.load_text(path)
+        self._shard(self.m.info()["batches"])
+
+    def load_csr(self, labels, row_off, feat, vals):
+        self.m.load_csr(labels, row_off, feat, vals)
+        self._shard(self.m.info()["batches"])
+
+    def init(self):
+        """The first full pull of every local feature (lr.cpp:161-166)."""
+        self.full_pull()
+
+    def train(self, niters=1):
+        """niters epochs in lockstep; per-epoch mean squared error of the
+        local rows (lr.cpp:231)."""
+        err = np.zeros(niters)
+        for it in range(niters):
+            self.train_steps(self.steps_per_epoch)
+            e = ctypes.c_double()
+            check(capi.lib().swps_lr_epoch_error(self.h, ctypes.byref(e)))
+            err[it] = e.value
+        self.sync()
+        return err
+
+    def predict(self):
+        """Refresh the worker cache with a full pull, then predict the local rows."""
+        self.full_pull()
+        return self.m.predict()
+
+    def info(self):
+        return self.m.info()
+
+    def kernel_times(self, reset=False):
+        return self.m.kernel_times(reset)
+
+    def shard_weights(self):
+        """(keys, w, g2) of the feature keys this rank owns, sorted by key."""
+        keys = np.sort(self.table.keys())
+        if len(keys) == 0:
+            return keys, np.zeros(0, np.float32), np.zeros(0, np.float32)
+        kt = torch.as_tensor(keys.astype(np.int64), device=self.dev)
+        rows = self.table.export(kt).cpu().numpy().reshape(len(keys), 2)
+        return keys, rows[:, 0].copy(), rows[:, 1].copy()

@@ -75,3 +75,22 @@ def gpu(lib):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def gloo1():
+    """A world-1 gloo process group for the sharded paths (torn down after
+    the test if this fixture created it)."""
+    import socket
+
+    import torch.distributed as dist
+    own = not dist.is_initialized()
+    if own:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    yield dist
+    if own:
+        dist.destroy_process_group()

@@ -124,3 +124,36 @@ def test_s2v_bench_shape_properties(lib, gpu):
     st = outs[0][1]
     assert st["docs"] == nd and st["positions"] == int(off[-1])
     assert st["tgt_rows"] >= st["positions"]  # the positive target is never skipped
+
+
+def test_s2v_doc_sharding_partitions_docs(lib, gpu, tmp_path):
+    """Config 5's layout: with swps_s2v_shard every rank keeps exactly the
+    sentences whose id BasicHashFrag maps to it — the ranks' outputs partition
+    the corpus, and world 1 is the unsharded run bit for bit."""
+    corpus = int_corpus(str(tmp_path / "c.txt"), 300, 150, seed=8)
+    dump = word_dump(str(tmp_path / "w.txt"), 150, 16, seed=9)
+
+    def run(rank, world):
+        t = lib.Table("w2v", dim=16, capacity=256, dtype="f64")
+        s = lib.Sent2Vec(t, window=3, negative=4, minibatch=20, niters=1, unigram_size=10 ** 6)
+        s.load_word_vector(dump)
+        if world:
+            s.shard(rank, world, 1000)
+        s.load_text(corpus)
+        s.train()
+        return s.docs()
+
+    ids0, v0, _ = run(0, 0)
+    ids1, v1, _ = run(0, 1)
+    assert np.array_equal(ids0, ids1) and np.array_equal(v0, v1)
+    world = 3
+    fm = lib.hashfrag_table(1000, world)
+    seen = []
+    for r in range(world):
+        ids, vecs, _ = run(r, world)
+        assert len(ids) > 0 and np.isfinite(vecs).all()
+        assert (lib.to_node_id(ids, 1000, fm) - 1 == r).all()
+        seen.append(ids)
+    allids = np.concatenate(seen)
+    assert len(np.unique(allids)) == len(allids) == len(ids0)
+    assert set(allids.tolist()) == set(ids0.tolist())
