@@ -82,6 +82,9 @@ def main():
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--frag-num", type=int, default=1000)
     ap.add_argument("--sharded", action="store_true", help="use the key-sharded multi-GPU path even at N=1")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="sharded path: strict pull/learn/push order (default in --parity mode); otherwise the "
+                         "pipelined driver overlaps minibatch i+1's pull and i's push with learning i")
     ap.add_argument("--cpu-lines", type=int, default=2500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity", action="store_true",
@@ -136,7 +139,7 @@ def main():
                      device=local, init="hash", seed=1)
         if sharded:  # key-sharded over the ranks (BasicHashFrag), RCCL all-to-all per minibatch
             from swiftmpi_amd.dist import ShardedWord2Vec
-            w = ShardedWord2Vec(t, frag_num=args.frag_num, **kw)
+            w = ShardedWord2Vec(t, frag_num=args.frag_num, pipeline=pipelined, **kw)
         else:
             w = sw.Word2Vec(t, init="ref", **kw)
         w.load_tokens(ids, off, keys)
@@ -155,6 +158,7 @@ def main():
         return dt, {k: s1[k] - s0[k] for k in s1 if k not in ("lstate", "fstate")}
 
     parity_main = args.parity
+    pipelined = sharded and not (args.lockstep or parity_main)
     t, w = build(fp64_intermediates=parity_main)
     info = w.info()
     w.train_batches(args.warmup)
@@ -226,8 +230,10 @@ def main():
                                                                   args.negative, args.sample, args.minibatch,
                                                                   args.line_len),
                    "global_batch": args.minibatch * world,
-                   "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num %d), %s all-to-all-v"
-                                   % (world, args.frag_num, "RCCL" if backend == "nccl" else "gloo"))
+                   "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num %d), %s all-to-all-v, %s"
+                                   % (world, args.frag_num, "RCCL" if backend == "nccl" else "gloo",
+                                      "pipelined: pull(i+1)/push(i) overlap learn(i), staleness 1" if pipelined
+                                      else "lockstep pull/learn/push"))
                    if sharded else "1 GPU, one HBM shard",
                    "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"]},
         "roofline": {"bound": "hbm", "kernel": "k_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,

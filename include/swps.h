@@ -209,7 +209,12 @@ int swps_w2v_install_init(swps_w2v *w, const void *d_vals);
  * (the reference's wire format) unless the table is SWPS_F32 with
  * fp64_intermediates = 0 (fast mode), then fp32 (half the exchange bytes). */
 int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads);
-int swps_w2v_serve_push(swps_w2v *w, const void *d_grads, const uint64_t *src_counts);
+/* d_keys: the keys received for the matching serve_pull (src_counts as there) */
+int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads, const uint64_t *src_counts);
+/* Issue request / serve_pull / serve_push on `stream` (a hipStream_t of the
+ * context's device; NULL = the compute stream, the default).  The caller
+ * orders the two streams (the pipelined driver in swiftmpi_amd/dist.py). */
+int swps_w2v_set_serve_stream(swps_w2v *w, void *stream);
 
 /* ---- host-only helpers (no device needed; used by the CPU test-suite) ---- */
 /* run-length form of gen_unigram_table (word2vec_global.h:467-497): start slot
@@ -319,7 +324,7 @@ int swps_lr_serve_pull(swps_lr *l, const uint64_t *d_keys, const uint64_t *src_c
                        float *d_vals);
 int swps_lr_install(swps_lr *l, const float *d_vals);
 int swps_lr_step(swps_lr *l, const float *d_vals, float *d_grads);
-int swps_lr_serve_push(swps_lr *l, const float *d_grads, const uint64_t *src_counts);
+int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads, const uint64_t *src_counts);
 
 #ifdef __cplusplus
 }

@@ -716,15 +716,19 @@ int swps_lr_step(swps_lr *l, const float *d_vals, float *d_grads) {
   return lr_batch(l, d_vals, d_grads);
 }
 
-int swps_lr_serve_push(swps_lr *l, const float *d_grads, const uint64_t *src_counts) {
+// d_keys: the keys of the matching serve_pull (the push request carries its keys)
+int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads, const uint64_t *src_counts) {
   if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  uint64_t n = 0;
+  for (int r = 0; r < l->world; r++) n += src_counts[r];
+  if (n != l->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
+  SWPS_TRY(table_lookup(l->t, d_keys, n, l->d_serve_rows.as<uint32_t>(), l->s));
   uint64_t off = 0;
   for (int r = 0; r < l->world; r++) {  // one AdaGrad step per source, in rank order
     SWPS_TRY(table_push_rows(l->t, l->d_serve_rows.as<uint32_t>() + off, src_counts[r], d_grads + off, l->s));
     off += src_counts[r];
   }
-  if (off != l->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
   return SWPS_OK;
 }
 

@@ -793,8 +793,8 @@ struct swps_w2v {
   std::vector<uint64_t> bcounts;   // [nb][world] keys requested per owner per batch
   std::vector<uint64_t> icounts;   // [world] init request per owner
   std::vector<int32_t> init_order; // vids grouped by owner
-  DevMem d_vkeys, d_init_order, d_serve_rows;
-  uint64_t serve_n = 0;
+  DevMem d_vkeys, d_init_order, d_serve_rows, d_push_rows;
+  hipStream_t ss = nullptr;  // serve stream (request / serve_pull / serve_push); nullptr = s
   std::vector<uint32_t> plan_P;     // kept positions per batch of the current epoch
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
@@ -1427,6 +1427,7 @@ int swps_w2v_train_epochs(swps_w2v *w, int32_t niters) {
 int swps_w2v_sync(swps_w2v *w) {
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   SWPS_HIP(hipStreamSynchronize(w->s));
+  if (w->ss) SWPS_HIP(hipStreamSynchronize(w->ss));
   w->timer.resolve();
   return SWPS_OK;
 }
@@ -1588,20 +1589,29 @@ int swps_w2v_batch_counts(swps_w2v *w, uint64_t *out, uint64_t cap, uint64_t *nb
   return SWPS_OK;
 }
 
+// Server-side work (request, serve_pull, serve_push) is issued on the serve
+// stream when one is set — the pipelined driver overlaps it, and the RCCL
+// exchanges ordered on it, with the compute stream's minibatch.
+int swps_w2v_set_serve_stream(swps_w2v *w, void *stream) {
+  w->ss = (hipStream_t)stream;
+  return SWPS_OK;
+}
+
 int swps_w2v_request(swps_w2v *w, int32_t init, uint64_t *counts, uint64_t *d_keys, uint64_t *n) {
   if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  hipStream_t ss = w->ss ? w->ss : w->s;
   if (init) {
     std::copy(w->icounts.begin(), w->icounts.end(), counts);
     *n = w->vocab_keys.size();
-    if (d_keys) k_vid_keys<<<nblk(*n), 256, 0, w->s>>>(w->d_init_order.as<int32_t>(), *n, w->d_vkeys.as<uint64_t>(), d_keys);
+    if (d_keys) k_vid_keys<<<nblk(*n), 256, 0, ss>>>(w->d_init_order.as<int32_t>(), *n, w->d_vkeys.as<uint64_t>(), d_keys);
   } else {
     const uint64_t bi = w->cursor % w->batches.size();
     const auto &b = w->batches[bi];
     std::copy(w->bcounts.begin() + bi * w->world, w->bcounts.begin() + (bi + 1) * w->world, counts);
     *n = b.U;
     if (d_keys && b.U)
-      k_vid_keys<<<nblk(b.U), 256, 0, w->s>>>(w->d_K.as<int32_t>() + b.kofs, b.U, w->d_vkeys.as<uint64_t>(), d_keys);
+      k_vid_keys<<<nblk(b.U), 256, 0, ss>>>(w->d_K.as<int32_t>() + b.kofs, b.U, w->d_vkeys.as<uint64_t>(), d_keys);
   }
   SWPS_HIP(hipGetLastError());
   return SWPS_OK;
@@ -1611,6 +1621,7 @@ int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src
                         void *d_vals) {
   if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  hipStream_t ss = w->ss ? w->ss : w->s;
   uint64_t n = 0;
   for (int r = 0; r < w->world; r++) n += src_counts[r];
   SWPS_TRY(w->d_serve_rows.ensure(std::max<uint64_t>(n, 1) * 4));
@@ -1618,14 +1629,13 @@ int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src
   if (insert) {  // keys are distinct within a source, not across sources
     uint64_t off = 0;
     for (int r = 0; r < w->world; r++) {
-      SWPS_TRY(table_find_or_insert(w->t, d_keys + off, src_counts[r], rows + off, w->s));
+      SWPS_TRY(table_find_or_insert(w->t, d_keys + off, src_counts[r], rows + off, ss));
       off += src_counts[r];
     }
   } else {
-    SWPS_TRY(table_lookup(w->t, d_keys, n, rows, w->s));
+    SWPS_TRY(table_lookup(w->t, d_keys, n, rows, ss));
   }
-  SWPS_TRY(table_copy_pull(w->t, rows, n, d_vals, w->s));
-  w->serve_n = n;
+  SWPS_TRY(table_copy_pull(w->t, rows, n, d_vals, ss));
   return SWPS_OK;
 }
 
@@ -1655,18 +1665,24 @@ int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads) {
   return run_batch<float, float>(w, d_vals, (float *)d_grads);
 }
 
-int swps_w2v_serve_push(swps_w2v *w, const void *d_grads, const uint64_t *src_counts) {
+// d_keys: the keys of the matching serve_pull (the push request carries its
+// keys, as the reference's push Request does, global_push_access.h:48-67).
+int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads, const uint64_t *src_counts) {
   if (!w->sharded) return fail(SWPS_E_STATE, "not sharded");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  hipStream_t ss = w->ss ? w->ss : w->s;
+  uint64_t n = 0;
+  for (int r = 0; r < w->world; r++) n += src_counts[r];
+  SWPS_TRY(w->d_push_rows.ensure(std::max<uint64_t>(n, 1) * 4));
+  SWPS_TRY(table_lookup(w->t, d_keys, n, w->d_push_rows.as<uint32_t>(), ss));
   const bool g32 = !w->f64 && !w->cfg.fp64_intermediates;  // fast mode: fp32 push payload
   const size_t gsz = g32 ? 4 : 8;
   uint64_t off = 0;
   for (int r = 0; r < w->world; r++) {  // one AdaGrad step per source, in rank order
-    SWPS_TRY(table_push_rows(w->t, w->d_serve_rows.as<uint32_t>() + off, src_counts[r],
-                             (const char *)d_grads + off * 2 * w->D * gsz, w->s, g32));
+    SWPS_TRY(table_push_rows(w->t, w->d_push_rows.as<uint32_t>() + off, src_counts[r],
+                             (const char *)d_grads + off * 2 * w->D * gsz, ss, g32));
     off += src_counts[r];
   }
-  if (off != w->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
   return SWPS_OK;
 }
 

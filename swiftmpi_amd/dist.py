@@ -96,67 +96,81 @@ class _ShardedApp:
         self.send_counts = g[self.rank]                 # [step][dst]
         self.recv_counts = g[:, :, self.rank].T.copy()  # [step][src]
 
-    def _stream(self):
-        if self.ex.backend != "nccl":
-            return None
+    def _cstream(self):
+        """The library's compute stream as a torch stream."""
         if self._ext is None:
             self._ext = torch.cuda.ExternalStream(self._fn("stream")(self.h), device=self.dev)
         return self._ext
 
-    def _exchange(self, send, sc, rc, width):
-        s = self._stream()
-        if s is None:
-            check(self._fn("sync")(self.h))  # gloo stages through the host
-            return self.ex.a2a(send, sc, rc, width)
-        with torch.cuda.stream(s):  # RCCL ordered after / before the library's kernels
+    def _a2a(self, stream, send, sc, rc, width):
+        # RCCL (or gloo's host staging) ordered after / before the library's
+        # kernels on `stream`
+        with torch.cuda.stream(stream):
             return self.ex.a2a(send, sc, rc, width)
 
-    def _empty(self, n, dtype):
-        s = self._stream()
-        if s is None:
-            return torch.empty(n, dtype=dtype, device=self.dev)
-        with torch.cuda.stream(s):
+    def _empty(self, stream, n, dtype):
+        with torch.cuda.stream(stream):
             return torch.empty(n, dtype=dtype, device=self.dev)
 
     def full_pull(self):
         """Pull every key of the local data (the reference's first full pull)
         into the worker cache, inserting keys new to their owners."""
+        C = self._cstream()
         counts = np.zeros(self.world, dtype=np.uint64)
         n = ctypes.c_uint64()
         check(self._fn("request")(self.h, 1, ptr(counts), None, ctypes.byref(n)))
-        keys = self._empty(n.value, torch.int64)
+        keys = self._empty(C, n.value, torch.int64)
         check(self._fn("request")(self.h, 1, ptr(counts), ptr(keys), ctypes.byref(n)))
         sc = counts.astype(np.int64)
         rc = self.ex.all_gather_matrix(sc[None, :])[:, 0, self.rank].copy()  # [src]
-        rkeys = self._exchange(keys, sc, rc, 1)
-        vals = self._empty(int(rc.sum()) * self.width, self.val_dtype)
+        rkeys = self._a2a(C, keys, sc, rc, 1)
+        vals = self._empty(C, int(rc.sum()) * self.width, self.val_dtype)
         rcu = rc.astype(np.uint64)
         check(self._fn("serve_pull")(self.h, ptr(rkeys), ptr(rcu), 1, ptr(vals)))
-        mine = self._exchange(vals, rc, sc, self.width)
+        mine = self._a2a(C, vals, rc, sc, self.width)
         check(self._fn(self.install_fn)(self.h, ptr(mine)))
         check(self._fn("sync")(self.h))
 
-    def step(self):
-        """One lockstep minibatch on every rank."""
-        s = self.cursor % self.steps_per_epoch
+    # -- the two halves of a minibatch's exchange ------------------------------
+    def _pull_phase(self, s, S):
+        """Request keys of step s, owners serve them, values back (on S)."""
         sc, rc = self.send_counts[s], self.recv_counts[s]
         nsend = int(sc.sum())
-        keys = self._empty(nsend, torch.int64)
-        mine = s < self.nb
-        if mine and nsend:
+        keys = self._empty(S, nsend, torch.int64)
+        if s < self.nb and nsend:
             counts = np.zeros(self.world, dtype=np.uint64)
             n = ctypes.c_uint64()
             check(self._fn("request")(self.h, 0, ptr(counts), ptr(keys), ctypes.byref(n)))
-        rkeys = self._exchange(keys, sc, rc, 1)
-        vals = self._empty(int(rc.sum()) * self.width, self.val_dtype)
+        rkeys = self._a2a(S, keys, sc, rc, 1)
+        vals = self._empty(S, int(rc.sum()) * self.width, self.val_dtype)
         rcu = rc.astype(np.uint64)
         check(self._fn("serve_pull")(self.h, ptr(rkeys), ptr(rcu), 0, ptr(vals)))
-        my_vals = self._exchange(vals, rc, sc, self.width)
-        grads = self._empty(nsend * self.width, self.grad_dtype)
-        if mine:
+        my_vals = self._a2a(S, vals, rc, sc, self.width)
+        return my_vals, rkeys
+
+    def _push_phase(self, s, grads, rkeys, S):
+        """Mean gradients of step s to the owners, AdaGrad per source (on S)."""
+        sc, rc = self.send_counts[s], self.recv_counts[s]
+        rgrads = self._a2a(S, grads, sc, rc, self.width)
+        rcu = rc.astype(np.uint64)
+        check(self._fn("serve_push")(self.h, ptr(rkeys), ptr(rgrads), ptr(rcu)))
+
+    def _learn(self, s, my_vals, stream):
+        nsend = int(self.send_counts[s].sum())
+        grads = self._empty(stream, nsend * self.width, self.grad_dtype)
+        if s < self.nb:
             check(self._fn("step")(self.h, ptr(my_vals) if nsend else None, ptr(grads) if nsend else None))
-        rgrads = self._exchange(grads, sc, rc, self.width)
-        check(self._fn("serve_push")(self.h, ptr(rgrads), ptr(rcu)))
+        return grads
+
+    def step(self):
+        """One lockstep minibatch on every rank: pull, learn, push, in order
+        (every pull sees every earlier push — the reference's semantics for
+        one worker)."""
+        C = self._cstream()
+        s = self.cursor % self.steps_per_epoch
+        my_vals, rkeys = self._pull_phase(s, C)
+        grads = self._learn(s, my_vals, C)
+        self._push_phase(s, grads, rkeys, C)
         self.cursor += 1
 
     def train_steps(self, n):
@@ -179,7 +193,7 @@ class ShardedWord2Vec(_ShardedApp):
     pfx = "w2v"
     install_fn = "install_init"
 
-    def __init__(self, table, group=None, frag_num=1000, **kw):
+    def __init__(self, table, group=None, frag_num=1000, pipeline=False, **kw):
         kw.setdefault("init", "table")
         self.w = Word2Vec(table, **kw)
         self.h = self.w.h
@@ -190,6 +204,53 @@ class ShardedWord2Vec(_ShardedApp):
         # push payload: fp64 (the reference's wire format) unless fast mode (fp32 table, fp32 intermediates)
         fast = table.dtype == "f32" and not kw.get("fp64_intermediates", True)
         self.grad_dtype = torch.float32 if fast else torch.float64
+        self.pipeline = pipeline
+        self._S = None
+        self._next = None
+
+    def step(self):
+        if not self.pipeline:
+            return super().step()
+        return self._step_pipelined()
+
+    def _step_pipelined(self):
+        """Bounded-staleness minibatch (overlap minibatch
+        i+1's pull with step i).  The serve stream S runs the exchanges and the
+        owners' serve kernels while the compute stream C learns:
+
+            C:  learn(i) ------------------------------> learn(i+1) ...
+            S:  pull(i+1) [sees pushes <= i-1] -> wait learn(i) -> push(i)
+
+        so minibatch i+1 reads rows that lack only step i's updates (every
+        rank's).  Deterministic: the order on each stream is fixed, and the
+        prefetch is issued whatever the caller's chunking of steps."""
+        C = self._cstream()
+        if self._S is None:
+            self._S = torch.cuda.Stream(device=self.dev)
+            check(capi.lib().swps_w2v_set_serve_stream(self.h, ctypes.c_void_p(self._S.cuda_stream)))
+        S = self._S
+        s = self.cursor % self.steps_per_epoch
+        if self._next is None:  # prologue: nothing prefetched yet
+            S.wait_stream(C)
+            self._next = self._pull_phase(s, S) + (self._record(S),)
+        my_vals, rkeys, ev = self._next
+        C.wait_event(ev)
+        my_vals.record_stream(C)            # produced on S before ev
+        grads = self._learn(s, my_vals, C)  # allocated on C, its first writer
+        eg = self._record(C)
+        nvals, nkeys = self._pull_phase((self.cursor + 1) % self.steps_per_epoch, S)
+        ev_next = self._record(S)           # learn(i+1) waits for the pull only
+        S.wait_event(eg)
+        grads.record_stream(S)
+        self._push_phase(s, grads, rkeys, S)
+        self._next = (nvals, nkeys, ev_next)
+        self.cursor += 1
+
+    @staticmethod
+    def _record(stream):
+        e = torch.cuda.Event()
+        e.record(stream)
+        return e
 
     # -- setup -----------------------------------------------------------------
     def load_text(self, path):

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--fast", action="store_true", help="fp32 intermediates (fp32 push payload)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="pipelined driver: check run-to-run bit-identity instead of equality with lockstep")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     ngpu = torch.cuda.device_count()
@@ -48,12 +50,26 @@ def main():
     kw = dict(window=4, negative=4, minibatch=17, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=not args.fast)
     D = 16
     # sharded
-    t = sw.Table("w2v", dim=D, capacity=4096, dtype=args.dtype, learning_rate=0.7, init="hash", seed=7, device=dev)
-    sh = ShardedWord2Vec(t, frag_num=1000, **kw)
-    sh.load_text(path)
-    sh.init()
-    sh.train(args.epochs)
-    keys, rows = sh.shard_rows()
+    def sharded_run():
+        t = sw.Table("w2v", dim=D, capacity=4096, dtype=args.dtype, learning_rate=0.7, init="hash", seed=7,
+                     device=dev)
+        sh = ShardedWord2Vec(t, frag_num=1000, pipeline=args.pipeline, **kw)
+        sh.load_text(path)
+        sh.init()
+        sh.train(args.epochs)
+        return sh, sh.shard_rows()
+
+    sh, (keys, rows) = sharded_run()
+    if args.pipeline:
+        _, (k2, r2) = sharded_run()
+        o1, o2 = np.argsort(keys), np.argsort(k2)  # row order = insertion order, which is racy
+        assert np.array_equal(keys[o1], k2[o2]) and np.array_equal(rows[o1], r2[o2]), "pipelined run not reproducible"
+        assert np.isfinite(rows).all()
+        if rank == 0:
+            print("DIST PIPELINE OK world=%d owned=%d steps/epoch=%d" % (world, len(keys), sh.steps_per_epoch))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     # every rank's own single-GPU training
     t1 = sw.Table("w2v", dim=D, capacity=4096, dtype=args.dtype, learning_rate=0.7, init="hash", seed=7, device=dev)
     w1 = sw.Word2Vec(t1, init="table", **kw)
