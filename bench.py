@@ -75,7 +75,8 @@ def main():
     ap.add_argument("--sample", type=float, default=1e-5)
     ap.add_argument("--alpha", type=float, default=0.05)
     ap.add_argument("--lr", type=float, default=0.7)
-    ap.add_argument("--minibatch", type=int, default=1000)
+    ap.add_argument("--minibatch", type=int, default=5000,
+                    help="worker.minibatch in lines (the reference demo: apps/word2vec/demo.conf:11)")
     ap.add_argument("--tokens", type=int, default=17005207)
     ap.add_argument("--vocab", type=int, default=253854)
     ap.add_argument("--line-len", type=int, default=1000)
@@ -191,13 +192,20 @@ def main():
     step_bytes = (2 * es * D * (d["ctx_rows"] + d["tgt_rows"]) + d["pulled"] * 4 * es * D +
                   d["pushed"] * (10 * es * D + 8))
     step_gbs = step_bytes / dt / 1e9
+    # HBM traffic of the same kernel from the committed PMC passes of this exact
+    # command (scripts/gpu_profile.sh -> scripts/pmc_summary.py); null otherwise
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_fast.json")
-    if os.path.exists(pmc) and not parity_main and args.dim == 300 and args.minibatch == 1000:
+    pmc_name = "r01_pmc_w2v_fast.json"
+    pmc = os.path.join(ROOT, "profiles", pmc_name)
+    mine = dict(minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, steps=args.steps, warmup=args.warmup,
+                mode="fast", world=world)
+    if os.path.exists(pmc) and not parity_main:
         prof = json.load(open(pmc))
-        for k, v in prof["kernels"].items():
-            if k.startswith("k_forward") and "hbm_bytes_corrected" in v:
-                traffic, traffic_src = v["hbm_bytes_corrected"], "profiles/r01_pmc_fast.json (FETCH_SIZE*2 + WRITE_SIZE)"
+        if prof.get("config") == mine:
+            for k, v in prof["kernels"].items():
+                if k.startswith("k_forward"):
+                    traffic = v["hbm_bytes_corrected"]
+                    traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch)" % pmc_name
 
     parity_leg = None
     if rank == 0 and world == 1 and not parity_main and not args.no_parity_leg:
@@ -240,6 +248,7 @@ def main():
                      "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1),
+                     "launches": fwd_n,
                      "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS},
         "kernel_ms": {k: v[0] for k, v in kt.items()},
         "parity_mode": parity_leg,
