@@ -243,7 +243,8 @@ def main():
                                       "pipelined: pull(i+1)/push(i) overlap learn(i), staleness 1" if pipelined
                                       else "lockstep pull/learn/push"))
                    if sharded else "1 GPU, one HBM shard",
-                   "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"]},
+                   "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"],
+                   "pulled_keys_per_step": d["pulled"] / args.steps},
         "roofline": {"bound": "hbm", "kernel": "k_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,

@@ -432,18 +432,25 @@ __global__ void k_item_counts(const uint32_t *__restrict__ seg, uint32_t U, uint
   cnt[j] = (c + CH - 1) / CH;
 }
 
-// item descriptors {first record, end record | kind << 31, (key, kind) index j, chunk}
+// item descriptors {first record, end record | kind << 31, (key, kind) index j, chunk}:
+// one thread per item (hot keys have thousands of chunks), j found by binary
+// search over the item offsets ioff[0..2U].
 __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__restrict__ ioff, uint32_t U,
-                            uint32_t CH, uint4 *__restrict__ desc) {
-  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 2ull * U) return;
-  const uint32_t u = (uint32_t)(j >> 1), kind = (uint32_t)(j & 1);
-  const uint32_t s = seg[(2 * kind) * U + u], e = seg[(2 * kind + 1) * U + u];
-  const uint32_t o = ioff[j], n = ioff[j + 1] - o;
-  for (uint32_t k = 0; k < n; k++) {
-    const uint32_t cs = s + k * CH;
-    desc[o + k] = make_uint4(cs, min(cs + CH, e) | (kind << 31), (uint32_t)j, k);
+                            uint32_t CH, uint64_t max_items, uint4 *__restrict__ desc) {
+  const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= max_items || item >= ioff[2ull * U]) return;
+  uint32_t lo = 0, hi = 2 * U;  // largest j with ioff[j] <= item
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ioff[mid] <= item)
+      lo = mid;
+    else
+      hi = mid;
   }
+  const uint32_t jj = lo, u = jj >> 1, kind = jj & 1, k = (uint32_t)item - ioff[jj];
+  const uint32_t s = seg[(2 * kind) * U + u], e = seg[(2 * kind + 1) * U + u];
+  const uint32_t cs = s + k * CH;
+  desc[item] = make_uint4(cs, min(cs + CH, e) | (kind << 31), jj, k);
 }
 
 template <typename A> struct GatherArgs {
@@ -1210,8 +1217,8 @@ template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals 
       const uint64_t max_items = 2ULL * U + M / kChunk + 1;
       SWPS_TRY(w->d_partial.ensure(max_items * D * sizeof(A)));
       SWPS_TRY(w->d_desc.ensure(max_items * 16));
-      k_item_desc<<<nblk(2ULL * U), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk,
-                                                 w->d_desc.as<uint4>());
+      k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk,
+                                                   max_items, w->d_desc.as<uint4>());
       SWPS_HIP(hipGetLastError());
       GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
                        w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), HOFF, (uint32_t)P, D,
