@@ -83,9 +83,9 @@ def main():
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--frag-num", type=int, default=1000)
     ap.add_argument("--sharded", action="store_true", help="use the key-sharded multi-GPU path even at N=1")
-    ap.add_argument("--lockstep", action="store_true",
-                    help="sharded path: strict pull/learn/push order (default in --parity mode); otherwise the "
-                         "pipelined driver overlaps minibatch i+1's pull and i's push with learning i")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="sharded path: the bounded-staleness driver (pull(i+1)/push(i) overlap learn(i)) instead "
+                         "of the default lockstep pull/learn/push order (exact reference semantics)")
     ap.add_argument("--cpu-lines", type=int, default=2500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity", action="store_true",
@@ -159,7 +159,7 @@ def main():
         return dt, {k: s1[k] - s0[k] for k in s1 if k not in ("lstate", "fstate")}
 
     parity_main = args.parity
-    pipelined = sharded and not (args.lockstep or parity_main)
+    pipelined = sharded and args.pipeline
     t, w = build(fp64_intermediates=parity_main)
     info = w.info()
     w.train_batches(args.warmup)

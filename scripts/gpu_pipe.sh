@@ -8,5 +8,5 @@ step pytest_w2v 600 python -m pytest tests/test_w2v_gpu.py -m gpu -q -p no:cache
 step dist2_fast 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29515 tests/dist_w2v_check.py --backend gloo --dtype f32 --fast || exit $?
 step dist3_pipe 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29516 tests/dist_w2v_check.py --backend gloo --dtype f32 --fast --pipeline || exit $?
 step dist2_lr 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29521 tests/dist_lr_check.py --backend gloo || exit $?
-step bench_sharded1_lock 600 python bench.py --sharded --lockstep --steps 20 --warmup 3 --no-cpu-baseline --no-parity-leg || exit $?
-step bench_sharded1_pipe 600 python bench.py --sharded --steps 20 --warmup 3 --no-cpu-baseline --no-parity-leg || exit $?
+step bench_sharded1_lock 600 python bench.py --sharded --steps 20 --warmup 3 --no-cpu-baseline --no-parity-leg || exit $?
+step bench_sharded1_pipe 600 python bench.py --sharded --pipeline --steps 20 --warmup 3 --no-cpu-baseline --no-parity-leg || exit $?

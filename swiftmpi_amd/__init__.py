@@ -142,7 +142,10 @@ class Table:
             self.h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (AttributeError, TypeError):  # interpreter shutdown: modules already torn down
+            pass
 
     @property
     def torch_dtype(self):
@@ -231,7 +234,10 @@ class Word2Vec:
             self.h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (AttributeError, TypeError):  # interpreter shutdown: modules already torn down
+            pass
 
     def load_text(self, path):
         check(capi.lib().swps_w2v_load_text(self.h, path.encode()))
@@ -371,7 +377,10 @@ class Sent2Vec:
             self.h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (AttributeError, TypeError):  # interpreter shutdown: modules already torn down
+            pass
 
     def load_text(self, path):
         self._create()
@@ -462,7 +471,10 @@ class LR:
             self.h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (AttributeError, TypeError):  # interpreter shutdown: modules already torn down
+            pass
 
     def load_text(self, path):
         check(capi.lib().swps_lr_load_text(self.h, path.encode()))

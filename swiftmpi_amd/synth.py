@@ -49,3 +49,57 @@ def criteo(rows, seed=3, bits=CRITEO_BITS):
     labels = (rng.random(rows) < 1.0 / (1.0 + np.exp(-z))).astype(np.float32)
     row_off = np.arange(0, rows * CRITEO_SLOTS + 1, CRITEO_SLOTS, dtype=np.uint64)
     return labels, row_off, feat.ravel(), vals.ravel()
+
+
+def analogy_corpus(path, entities=40, relations=4, lines=3000, segments=12, ctx_words=3, noise_vocab=400,
+                   seed=11):
+    """A planted-analogy corpus (text8 and questions-words.txt are not
+    available offline): target words "e<i>_r<j>" occur amid entity-context
+    words "ce<i>_<k>", relation-context words "cr<j>_<k>" and Zipfian noise,
+    so a trained v vector of e<i>_r<j> is close to an entity part plus a
+    relation part and  v(e_a r_y) - v(e_a r_x) + v(e_b r_x) ~ v(e_b r_y).
+    Writes `lines` lines of `segments` segments each; returns the question
+    list [(a, b, c, expected)] of word strings."""
+    rng = np.random.default_rng(seed)
+    zp = 1.0 / np.arange(1, noise_vocab + 1)
+    zp /= zp.sum()
+    with open(path, "w") as f:
+        for _ in range(lines):
+            words = []
+            for _ in range(segments):
+                i, j = int(rng.integers(entities)), int(rng.integers(relations))
+                seg = ["ce%d_%d" % (i, k) for k in rng.integers(0, ctx_words, 2)]
+                seg += ["cr%d_%d" % (j, k) for k in rng.integers(0, ctx_words, 2)]
+                seg += ["n%d" % k for k in rng.choice(noise_vocab, 2, p=zp)]
+                rng.shuffle(seg)
+                seg.insert(3, "e%d_r%d" % (i, j))
+                words += seg
+            f.write(" ".join(words) + "\n")
+    qs = []
+    for a in range(entities):
+        for b in range(entities):
+            if a == b:
+                continue
+            for x in range(relations):
+                for y in range(relations):
+                    if x != y:
+                        qs.append(("e%d_r%d" % (a, x), "e%d_r%d" % (a, y), "e%d_r%d" % (b, x), "e%d_r%d" % (b, y)))
+    return qs
+
+
+def analogy_accuracy(vecs, index, questions, candidates):
+    """questions-words style top-1 accuracy: for (a, b, c, d) predict
+    argmax cos(x, b - a + c) over `candidates` (word strings) excluding a, b,
+    c.  vecs: [V, D] word vectors; index: word -> row."""
+    cand = np.array([index[w] for w in candidates])
+    m = vecs[cand].astype(np.float64)
+    m /= np.linalg.norm(m, axis=1, keepdims=True) + 1e-30
+    pos = {int(r): k for k, r in enumerate(cand)}
+    ok = 0
+    for a, b, c, d in questions:
+        q = vecs[index[b]] - vecs[index[a]] + vecs[index[c]]
+        s = m @ q
+        for w in (a, b, c):
+            s[pos[index[w]]] = -np.inf
+        ok += int(cand[int(np.argmax(s))] == index[d])
+    return ok / max(len(questions), 1)
