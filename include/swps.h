@@ -209,6 +209,12 @@ int swps_w2v_install_init(swps_w2v *w, const void *d_vals);
  * (the reference's wire format) unless the table is SWPS_F32 with
  * fp64_intermediates = 0 (fast mode), then fp32 (half the exchange bytes). */
 int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads);
+/* Prepare the next minibatch's parameter-independent half (epoch plan, local
+ * key map, learn_instance's draws as position/gradient records, the sorted
+ * inverted index) on the compute stream; swps_w2v_step / train_batches do it
+ * themselves when it was not done.  Issued right after a step, it overlaps
+ * that step's push and the next pull (sharded mode). */
+int swps_w2v_prep(swps_w2v *w);
 /* d_keys: the keys received for the matching serve_pull (src_counts as there) */
 int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads, const uint64_t *src_counts);
 /* Issue request / serve_pull / serve_push on `stream` (a hipStream_t of the

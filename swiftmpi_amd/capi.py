@@ -102,6 +102,7 @@ PROTOS = {
     "swps_w2v_step": (ctypes.c_int, [_p, _p, _p]),
     "swps_w2v_serve_push": (ctypes.c_int, [_p, _p, _p, _p]),
     "swps_w2v_set_serve_stream": (ctypes.c_int, [_p, _p]),
+    "swps_w2v_prep": (ctypes.c_int, [_p]),
     "swps_unigram_starts": (ctypes.c_int, [_p, _p, _u64, _u64, _p]),
     "swps_glibc_rand": (ctypes.c_int, [ctypes.c_uint32, _u64, _u64, _p]),
     "swps_s2v_create": (ctypes.c_int, [_p, ctypes.POINTER(S2VCfg), ctypes.POINTER(_p)]),

@@ -803,6 +803,12 @@ struct swps_w2v {
   DevMem d_vkeys, d_init_order, d_serve_rows, d_push_rows;
   hipStream_t ss = nullptr;  // serve stream (request / serve_pull / serve_push); nullptr = s
   std::vector<uint32_t> plan_P;     // kept positions per batch of the current epoch
+  // the prepared (parameter-independent) half of the next minibatch
+  struct Prepped {
+    bool valid = false, records = false, sorted = false;
+    uint64_t bi = 0, P = 0, nt = 0, HOFF = 0, M = 0, max_items = 0;
+    uint32_t U = 0;
+  } pb;
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
   // negative trace
@@ -1102,36 +1108,46 @@ int plan_epoch(swps_w2v *w) {
   return SWPS_OK;
 }
 
-template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals = nullptr, A *d_grads = nullptr) {
+// ---- one minibatch, in two halves ------------------------------------------
+// prep_batch: everything that depends only on the corpus, the RNG streams and
+// the batch's key set — the epoch plan, the local key map, the position and
+// gradient records (learn_instance's draws) and the inverted index (sorted
+// records, segments, chunk descriptors).  learn_batch: everything that reads
+// parameters — pull (or install of the owners' values), forward, gathered
+// gradient sums, push.  The sharded driver issues prep(i+1) right after
+// learn(i) on the compute stream, so it runs while minibatch i's push and
+// i+1's pull cross the fabric (exact lockstep semantics kept).
+__global__ void k_set_local(const int32_t *__restrict__ K, uint32_t U, int32_t *__restrict__ local) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < U) local[K[u]] = (int32_t)u;
+}
+
+int prep_batch(swps_w2v *w) {
+  if (w->pb.valid) return SWPS_OK;
   const uint64_t nb = w->batches.size();
   if (w->cursor % nb == 0) SWPS_TRY(plan_epoch(w));
   const uint64_t bi = w->cursor % nb;
   const swps_w2v::Batch &B = w->batches[bi];
   hipStream_t s = w->s;
   Timer &tm = w->timer;
-  const int D = w->D, W = w->W, N = w->N;
+  const int W = w->W, N = w->N;
   const uint64_t t0 = (uint64_t)w->line_off[B.l0], t1 = (uint64_t)w->line_off[B.l1];
   const uint64_t nt = t1 - t0;
   const uint32_t U = B.U;
   const int32_t *K = w->d_K.as<int32_t>() + B.kofs;
-  // ---- pull (global_pull_access.h:28-107 + server.h:129-154) ----
-  if (U) {
-    hipEvent_t e = tm.begin(s);
-    if (d_vals)  // sharded: values pulled from the owners
-      k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
-                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 1);
-    else
-      k_pull<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(), D,
-                                                       w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
-                                                       w->d_local.as<int32_t>(), 1);
-    SWPS_HIP(hipGetLastError());
-    tm.end(KT_PULL, e, s);
-  }
   const uint64_t P = w->plan_P[bi];
-  w->st_batches++;
-  w->st_kept += P;
-  w->st_words += nt;
-  w->st_pulled += U;
+  auto &pb = w->pb;
+  pb = swps_w2v::Prepped();
+  pb.bi = bi;
+  pb.P = P;
+  pb.U = U;
+  pb.nt = nt;
+  // local key map of the batch (the grads[key] slots the pull resets,
+  // global_pull_access.h:88-97); cleared again by the push
+  if (U) {
+    k_set_local<<<nblk(U), 256, 0, s>>>(K, U, w->d_local.as<int32_t>());
+    SWPS_HIP(hipGetLastError());
+  }
   const bool tracing = w->trace.size() < w->trace_cap;
   if (P > 0 && (U > 0 || tracing)) {
     // ---- position records + gradient records (learn_instance's draws) ----
@@ -1141,13 +1157,10 @@ template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals 
     if (M >= (1ULL << 31)) return fail(SWPS_E_UNSUPPORTED, "minibatch too large (2^31 gradient records)");
     SWPS_TRY(w->d_pos_tok.ensure(P * 4));
     SWPS_TRY(w->d_rec.ensure(P * RS * 4));
-    SWPS_TRY(w->d_neu1.ensure(P * D * sizeof(A)));
-    SWPS_TRY(w->d_neu1e.ensure(P * D * sizeof(A)));
     SWPS_TRY(w->d_pkeys.ensure(M * 4));
     SWPS_TRY(w->d_pvals.ensure(M * 4));
     SWPS_TRY(w->d_pkeys_s.ensure(M * 4));
     SWPS_TRY(w->d_pvals_s.ensure(M * 4));
-    SWPS_TRY(w->d_pg.ensure(HOFF * 4));
     if (tracing) SWPS_TRY(w->d_trace.ensure(std::max<uint64_t>(1, P * N) * 4));
     RecArgs ra{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(),
                w->d_pos_tok.as<int32_t>(), (uint32_t)P, w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(),
@@ -1160,19 +1173,9 @@ template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals 
     k_records<<<nblk(P), 256, 0, s>>>(ra);
     SWPS_HIP(hipGetLastError());
     tm.end(KT_REC, er, s);
-    // ---- forward (learn_instance) ----
-    FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
-                     w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                     w->d_pg.as<float>()};
-    hipEvent_t ef = tm.begin(s);
-    switch (w->NCH) {
-      case 1: launch_forward<1>(fa, s); break;
-      case 2: launch_forward<2>(fa, s); break;
-      case 3: launch_forward<3>(fa, s); break;
-      default: launch_forward<4>(fa, s); break;
-    }
-    SWPS_HIP(hipGetLastError());
-    tm.end(KT_FWD, ef, s);
+    pb.records = true;
+    pb.HOFF = HOFF;
+    pb.M = M;
     if (tracing) {
       std::vector<int32_t> tr(P * N);
       if (!tr.empty()) {
@@ -1212,38 +1215,91 @@ template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals 
       ib = w->d_tmp.bytes;
       SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, ib, w->d_icnt.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
                                                 (int)(2 * U + 1), s));
-      tm.end(KT_SORT, es, s);
-      // ---- chunked segmented gradient sums ----
       const uint64_t max_items = 2ULL * U + M / kChunk + 1;
-      SWPS_TRY(w->d_partial.ensure(max_items * D * sizeof(A)));
       SWPS_TRY(w->d_desc.ensure(max_items * 16));
       k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk,
                                                    max_items, w->d_desc.as<uint4>());
       SWPS_HIP(hipGetLastError());
-      GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
-                       w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), HOFF, (uint32_t)P, D,
-                       w->d_partial.as<A>()};
-      const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(max_items * 64), 16384);
-      hipEvent_t eg = tm.begin(s);
-      switch (w->NCH) {
-        case 1: launch_gather<1, T, A>(ga, ggrid, s); break;
-        case 2: launch_gather<2, T, A>(ga, ggrid, s); break;
-        case 3: launch_gather<3, T, A>(ga, ggrid, s); break;
-        default: launch_gather<4, T, A>(ga, ggrid, s); break;
-      }
-      SWPS_HIP(hipGetLastError());
-      tm.end(KT_GATHER, eg, s);
-      w->st_pairs += M;
+      tm.end(KT_SORT, es, s);
+      pb.sorted = true;
+      pb.max_items = max_items;
     }
+  }
+  if (U > 0 && !pb.sorted) {  // no records: the push sees empty segments
+    SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
+    SWPS_HIP(hipMemsetAsync(w->d_seg.p, 0, (uint64_t)U * 16, s));
+    SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
+    SWPS_HIP(hipMemsetAsync(w->d_ioff.p, 0, (2ULL * U + 1) * 4, s));
+  }
+  pb.valid = true;
+  return SWPS_OK;
+}
+
+template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_vals = nullptr, A *d_grads = nullptr) {
+  SWPS_TRY(prep_batch(w));
+  const auto pb = w->pb;
+  const swps_w2v::Batch &B = w->batches[pb.bi];
+  hipStream_t s = w->s;
+  Timer &tm = w->timer;
+  const int D = w->D, W = w->W, N = w->N;
+  const uint32_t U = pb.U;
+  const uint64_t P = pb.P;
+  const int32_t *K = w->d_K.as<int32_t>() + B.kofs;
+  // ---- pull (global_pull_access.h:28-107 + server.h:129-154) ----
+  if (U) {
+    hipEvent_t e = tm.begin(s);
+    if (d_vals)  // sharded: values pulled from the owners
+      k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
+                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0);
+    else
+      k_pull<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(), D,
+                                                       w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
+                                                       w->d_local.as<int32_t>(), 0);
+    SWPS_HIP(hipGetLastError());
+    tm.end(KT_PULL, e, s);
+  }
+  w->st_batches++;
+  w->st_kept += P;
+  w->st_words += pb.nt;
+  w->st_pulled += U;
+  if (pb.records) {
+    // ---- forward (learn_instance) ----
+    SWPS_TRY(w->d_neu1.ensure(P * D * sizeof(A)));
+    SWPS_TRY(w->d_neu1e.ensure(P * D * sizeof(A)));
+    SWPS_TRY(w->d_pg.ensure(pb.HOFF * 4));
+    FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
+                     w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
+                     w->d_pg.as<float>()};
+    hipEvent_t ef = tm.begin(s);
+    switch (w->NCH) {
+      case 1: launch_forward<1>(fa, s); break;
+      case 2: launch_forward<2>(fa, s); break;
+      case 3: launch_forward<3>(fa, s); break;
+      default: launch_forward<4>(fa, s); break;
+    }
+    SWPS_HIP(hipGetLastError());
+    tm.end(KT_FWD, ef, s);
+  }
+  if (pb.sorted) {
+    // ---- chunked segmented gradient sums ----
+    SWPS_TRY(w->d_partial.ensure(pb.max_items * D * sizeof(A)));
+    GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
+                     w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
+                     w->d_partial.as<A>()};
+    const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(pb.max_items * 64), 16384);
+    hipEvent_t eg = tm.begin(s);
+    switch (w->NCH) {
+      case 1: launch_gather<1, T, A>(ga, ggrid, s); break;
+      case 2: launch_gather<2, T, A>(ga, ggrid, s); break;
+      case 3: launch_gather<3, T, A>(ga, ggrid, s); break;
+      default: launch_gather<4, T, A>(ga, ggrid, s); break;
+    }
+    SWPS_HIP(hipGetLastError());
+    tm.end(KT_GATHER, eg, s);
+    w->st_pairs += pb.M;
   }
   if (U > 0) {
     // ---- push: mean + AdaGrad (also clears the local index map) ----
-    if (P == 0) {
-      SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
-      SWPS_HIP(hipMemsetAsync(w->d_seg.p, 0, (uint64_t)U * 16, s));
-      SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
-      SWPS_HIP(hipMemsetAsync(w->d_ioff.p, 0, (2ULL * U + 1) * 4, s));
-    }
     PushArgs<T, A> pa{K, U, w->d_vid_row.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
                       w->d_partial.as<A>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
                       (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads};
@@ -1258,8 +1314,13 @@ template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals 
     tm.end(KT_PUSH, ep, s);
     w->st_pushed += U;
   }
+  w->pb.valid = false;
   w->cursor++;
   return SWPS_OK;
+}
+
+template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals = nullptr, A *d_grads = nullptr) {
+  return learn_batch<T, A>(w, d_vals, d_grads);
 }
 
 }  // namespace
@@ -1661,6 +1722,12 @@ int swps_w2v_install_init(swps_w2v *w, const void *d_vals) {
   SWPS_HIP(hipGetLastError());
   w->inited = true;
   return SWPS_OK;
+}
+
+int swps_w2v_prep(swps_w2v *w) {
+  if (!w->inited) return fail(SWPS_E_STATE, "init first");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  return prep_batch(w);
 }
 
 int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads) {

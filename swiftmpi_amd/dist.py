@@ -193,7 +193,7 @@ class ShardedWord2Vec(_ShardedApp):
     pfx = "w2v"
     install_fn = "install_init"
 
-    def __init__(self, table, group=None, frag_num=1000, pipeline=False, **kw):
+    def __init__(self, table, group=None, frag_num=1000, pipeline=False, overlap=True, **kw):
         kw.setdefault("init", "table")
         self.w = Word2Vec(table, **kw)
         self.h = self.w.h
@@ -205,13 +205,54 @@ class ShardedWord2Vec(_ShardedApp):
         fast = table.dtype == "f32" and not kw.get("fp64_intermediates", True)
         self.grad_dtype = torch.float32 if fast else torch.float64
         self.pipeline = pipeline
+        self.overlap = overlap
         self._S = None
         self._next = None
 
-    def step(self):
-        if not self.pipeline:
-            return super().step()
-        return self._step_pipelined()
+    def step(self, prep_next=True):
+        if self.pipeline:
+            return self._step_pipelined()
+        if self.overlap:
+            return self._step_overlapped(prep_next)
+        return super().step()
+
+    def train_steps(self, n):
+        for k in range(n):
+            self.step(prep_next=k + 1 < n)
+
+    train_batches = train_steps
+
+    def _serve_stream(self):
+        if self._S is None:
+            self._S = torch.cuda.Stream(device=self.dev)
+            self._S.wait_stream(self._cstream())  # after init's full pull
+            check(capi.lib().swps_w2v_set_serve_stream(self.h, ctypes.c_void_p(self._S.cuda_stream)))
+        return self._S
+
+    def _step_overlapped(self, prep_next):
+        """Lockstep minibatch (exact: every pull sees every earlier push) with
+        the exchanges on a serve stream S, and the next minibatch's
+        parameter-independent half (swps_w2v_prep: records, sort, index)
+        issued on the compute stream C right after this one's learn — so it
+        runs while this push and the next pull cross the fabric:
+
+            S:  pull(i) ......... wait learn(i) -> push(i) -> pull(i+1) ...
+            C:  wait pull(i) -> learn(i) -> prep(i+1) -> wait pull(i+1) -> ...
+        """
+        C, S = self._cstream(), self._serve_stream()
+        s = self.cursor % self.steps_per_epoch
+        my_vals, rkeys = self._pull_phase(s, S)
+        C.wait_event(self._record(S))
+        my_vals.record_stream(C)            # produced on S before the event
+        grads = self._learn(s, my_vals, C)  # allocated on C, its first writer
+        eg = self._record(C)
+        nxt = (self.cursor + 1) % self.steps_per_epoch
+        if prep_next and nxt < self.nb:
+            check(capi.lib().swps_w2v_prep(self.h))
+        S.wait_event(eg)
+        grads.record_stream(S)
+        self._push_phase(s, grads, rkeys, S)
+        self.cursor += 1
 
     def _step_pipelined(self):
         """Bounded-staleness minibatch (overlap minibatch
@@ -224,11 +265,7 @@ class ShardedWord2Vec(_ShardedApp):
         so minibatch i+1 reads rows that lack only step i's updates (every
         rank's).  Deterministic: the order on each stream is fixed, and the
         prefetch is issued whatever the caller's chunking of steps."""
-        C = self._cstream()
-        if self._S is None:
-            self._S = torch.cuda.Stream(device=self.dev)
-            check(capi.lib().swps_w2v_set_serve_stream(self.h, ctypes.c_void_p(self._S.cuda_stream)))
-        S = self._S
+        C, S = self._cstream(), self._serve_stream()
         s = self.cursor % self.steps_per_epoch
         if self._next is None:  # prologue: nothing prefetched yet
             S.wait_stream(C)

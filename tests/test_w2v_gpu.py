@@ -176,8 +176,9 @@ def test_fast_mode_close_to_parity_mode(lib, oracle_mod, gpu, tmp_path):
     assert np.median(rel) < 1e-5 and np.quantile(rel, 0.99) < 1e-2
 
 
-@pytest.mark.parametrize("dtype,fp64i", [("f64", True), ("f32", True), ("f32", False)])
-def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i):
+@pytest.mark.parametrize("dtype,fp64i,overlap", [("f64", True, True), ("f32", True, True), ("f32", False, True),
+                                                ("f32", False, False)])
+def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i, overlap):
     """The sharded request / serve / step / push path with one rank (gloo,
     world 1) reproduces the single-GPU path bit for bit — in fast mode too,
     where the push payload is fp32."""
@@ -195,10 +196,11 @@ def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i):
         dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
     try:
         t = lib.Table("w2v", dim=16, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
-        sh = ShardedWord2Vec(t, **kw)
+        sh = ShardedWord2Vec(t, overlap=overlap, **kw)
         sh.load_text(path)
         sh.init()
         sh.train(2)
+        assert sh.stats()["lstate"] == w1_lstate(lib, path, dtype, kw)
         t1 = lib.Table("w2v", dim=16, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
         w1 = lib.Word2Vec(t1, init="table", **kw)
         w1.load_text(path)
@@ -212,6 +214,15 @@ def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+def w1_lstate(lib, path, dtype, kw):
+    t = lib.Table("w2v", dim=16, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
+    w = lib.Word2Vec(t, init="table", **kw)
+    w.load_text(path)
+    w.init()
+    w.train(2)
+    return w.stats()["lstate"]
 
 
 def _sharded_run(lib, path, kw, pipeline, epochs=3, D=16, seed=3, lr=0.1):
