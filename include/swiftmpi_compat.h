@@ -292,11 +292,14 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
 
 /* ---- app level ------------------------------------------------------------ */
 
-/* Word2Vec<MiniBatch> (word2vec_global.h:541-748): train() = the first full
- * pull + niters epochs of the minibatch loop, all on the GPU. */
+/* Word2Vec<MiniBatch> (word2vec_global.h:541-748, w2v.cpp): train() = the
+ * first full pull + niters epochs of the minibatch loop, all on the GPU.
+ * local = true: word2vec.h's Word2Vec<MiniBatch> (w2v_local.cpp) — atoi keys,
+ * per-minibatch vocab and unigram table. */
 class Word2VecApp {
  public:
-  Word2VecApp(const std::string &path, int niters, swps_table *t = nullptr, int fp64_intermediates = 1)
+  Word2VecApp(const std::string &path, int niters, swps_table *t = nullptr, int fp64_intermediates = 1,
+              bool local = false)
       : _path(path), _niters(niters) {
     swps_w2v_cfg c;
     c.window = global_config().get("word2vec", "window").to_int32();
@@ -306,12 +309,13 @@ class Word2VecApp {
     c.sample = global_config().get("word2vec", "sample").to_float();
     c.alpha = global_config().get("word2vec", "learning_rate").to_float();
     c.unigram_size = 100000000ULL;
-    c.key_mode = SWPS_KEY_BKDR;
+    c.key_mode = local ? SWPS_KEY_ATOI : SWPS_KEY_BKDR;
     c.init_mode = SWPS_W2V_INIT_REF;
     c.rand_seed = 1;
     c.rand_offset = 2;
     c.fp64_intermediates = fp64_intermediates;
     c.profile = 0;
+    c.minibatch_vocab = local ? 1 : 0;
     swps_check(swps_w2v_create(t ? t : global_swps_table(), &c, &_w));
   }
   ~Word2VecApp() { swps_w2v_destroy(_w); }

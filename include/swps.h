@@ -143,6 +143,11 @@ typedef struct {
   int32_t fp64_intermediates;  /* 1: neu1/neu1e and gradient sums kept in fp64 like the reference's Vec
                                 * (parity mode for fp32 tables); 0: fp32 (fast mode). fp64 tables: always */
   int32_t profile;             /* 1: time kernels with HIP events */
+  int32_t minibatch_vocab;     /* 0: apps/word2vec/word2vec_global.h (w2v.cpp): one vocab and unigram
+                                * table for the corpus, a full-vocab worker cache, B+3-line gather windows;
+                                * 1: apps/word2vec/word2vec.h's MiniBatch (w2v_local.cpp): per-minibatch
+                                * vocab and table (std::map order), B+1-line windows, to_sample over the
+                                * never-reset _num_words */
 } swps_w2v_cfg;
 
 /* The table must use SWPS_LAYOUT_W2V; ctx is bound to the table's device. */

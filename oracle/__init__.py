@@ -28,7 +28,8 @@ class W2VCfg(ctypes.Structure):
     _fields_ = [("dim", ctypes.c_int32), ("window", ctypes.c_int32), ("negative", ctypes.c_int32),
                 ("min_sentence_length", ctypes.c_int32), ("minibatch", ctypes.c_int32),
                 ("storage_f32", ctypes.c_int32), ("sample", ctypes.c_float), ("alpha", ctypes.c_float),
-                ("lr", ctypes.c_float), ("table_size", ctypes.c_uint64), ("key_mode", ctypes.c_int32)]
+                ("lr", ctypes.c_float), ("table_size", ctypes.c_uint64), ("key_mode", ctypes.c_int32),
+                ("minibatch_vocab", ctypes.c_int32)]
 
 
 class S2VCfg(ctypes.Structure):
@@ -155,12 +156,15 @@ def libc_rand(n, seed=1, skip=0):
 
 
 class W2V:
-    """Reference-semantics CBOW-NS trainer (word2vec_global.h, nthreads = 1)."""
+    """Reference-semantics CBOW-NS trainer (word2vec_global.h, nthreads = 1);
+    minibatch_vocab=True: word2vec.h's MiniBatch (w2v_local.cpp) — per-minibatch
+    vocab and unigram table."""
 
     def __init__(self, corpus_path, dim, window=5, negative=5, min_sentence_length=1, minibatch=100,
-                 sample=1e-5, alpha=0.05, lr=0.7, table_size=int(1e8), storage_f32=False, key_mode=0):
+                 sample=1e-5, alpha=0.05, lr=0.7, table_size=int(1e8), storage_f32=False, key_mode=0,
+                 minibatch_vocab=False):
         c = W2VCfg(dim, window, negative, min_sentence_length, minibatch, int(storage_f32), sample, alpha, lr,
-                   table_size, key_mode)
+                   table_size, key_mode, int(minibatch_vocab))
         self.dim = dim
         self.h = lib().orc_w2v_create(corpus_path.encode(), ctypes.byref(c))
         if not self.h:

@@ -183,7 +183,8 @@ struct W2VCfg {
   int32_t dim, window, negative, min_sentence_length, minibatch, storage_f32;
   float sample, alpha, lr;
   uint64_t table_size;
-  int32_t key_mode;  // 0 = BKDR (word2vec_global.h:205), 1 = atoi (word2vec.h:206)
+  int32_t key_mode;        // 0 = BKDR (word2vec_global.h:205), 1 = atoi (word2vec.h:206)
+  int32_t minibatch_vocab; // 1 = word2vec.h's MiniBatch (w2v_local.cpp): per-minibatch vocab + table
 };
 
 struct Row {
@@ -221,6 +222,13 @@ struct W2V {
   // optional trace of negative draws (vids) for the first `trace_cap` draws
   std::vector<int64_t> neg_trace;
   size_t trace_cap = 0;
+  // word2vec.h MiniBatch state (minibatch_vocab): the minibatch's counts in
+  // std::map order, its unigram table (keys), and `_num_words`, which
+  // gather_keys increments for every gathered word and nothing resets
+  // 
+  std::map<uint64_t, int> bfreq;
+  std::vector<uint64_t> btable;
+  size_t num_words = 0;
 
   int D() const { return cfg.dim; }
   bool f32() const { return cfg.storage_f32 != 0; }
@@ -323,6 +331,40 @@ struct W2V {
     return flcg_next(frng) > ran;
   }
 
+  // word2vec.h:621-629 to_sample: freq over the minibatch's counts and the
+  // never-reset `_num_words` (an int in the reference)
+  bool to_sample_local(uint64_t word) {
+    if (cfg.sample < 0) return true;
+    auto it = bfreq.find(word);
+    if (it == bfreq.end()) throw std::runtime_error("trained word outside the minibatch vocab (reference UB)");
+    const int tw = (int)num_words;
+    float freq = float(it->second) / tw;
+    float ran = (float)(1 - std::sqrt((double)(cfg.sample / freq)));
+    return flcg_next(frng) > ran;
+  }
+
+  // word2vec.h:398-425 gen_unigram_table over the minibatch vocab (_wordids
+  // and the normaliser both in std::map key order), literal T-entry loop
+  void gen_batch_table() {
+    std::vector<uint64_t> ids;
+    for (auto &kv : bfreq) ids.push_back(kv.first);
+    const uint64_t T = cfg.table_size;
+    btable.assign(T, 0);
+    double pw = 0, power = 0.75;
+    for (auto &kv : bfreq) pw += std::pow(kv.second, power);
+    size_t i = 0;
+    double d1 = std::pow(bfreq[ids[i]], power) / (double)pw;
+    for (uint64_t a = 0; a < T; a++) {
+      btable[a] = ids[i];
+      if ((int64_t)a / (double)T > d1) {
+        i++;
+        if (i >= ids.size()) throw std::runtime_error("unigram table walked past the vocab (reference UB)");
+        d1 += std::pow(bfreq[ids[i]], power) / (double)pw;
+      }
+      if (i >= bfreq.size()) i = bfreq.size() - 1;
+    }
+  }
+
   Row &cache_row(uint64_t k) {
     auto it = cache.find(k);
     if (it == cache.end()) {  // dense_hash_map::operator[] inserts zeros
@@ -353,9 +395,10 @@ struct W2V {
     (void)b;
     int n = (int)w.size();
     std::vector<double> neu1(Dd), neu1e(Dd), tmp(Dd);
+    const bool local = cfg.minibatch_vocab != 0;
     for (int pos = 0; pos < n; pos++) {
       uint64_t word = w[pos];
-      if (!to_sample(word)) continue;
+      if (!(local ? to_sample_local(word) : to_sample(word))) continue;
       kept++;
       std::fill(neu1.begin(), neu1.end(), 0.0);
       std::fill(neu1e.begin(), neu1e.end(), 0.0);
@@ -375,12 +418,12 @@ struct W2V {
           label = 1;
         } else {
           uint64_t ti = (lcg_next(rng) >> 16) % cfg.table_size;
-          target = wordids[table[ti]];
+          target = local ? btable[ti] : wordids[table[ti]];
           if (target == 0) {
             ti = (lcg_next(rng) >> 16) % cfg.table_size;
-            target = wordids[table[ti]];
+            target = local ? btable[ti] : wordids[table[ti]];
           }
-          if (neg_trace.size() < trace_cap) neg_trace.push_back((int64_t)table[ti]);
+          if (neg_trace.size() < trace_cap) neg_trace.push_back(local ? (int64_t)vid[target] : (int64_t)table[ti]);
           if (target == word) continue;
           label = 0;
         }
@@ -486,6 +529,47 @@ struct W2V {
     }
   }
 
+  // word2vec.h:496-538 train_iter with nthreads = 1 (w2v_local.cpp): per
+  // minibatch, gather_keys reads the next B+1 valid lines (counts, keys,
+  // `_num_words`) and seeks back; fewer than 5 keys ends the epoch; pull;
+  // the minibatch table; then B+1 lines (valid or not) are trained; push all
+  // gathered keys; clear.
+  void train_iter_local() {
+    actual_train_words = 0;
+    size_t p = 0;
+    const int B = cfg.minibatch;
+    while (true) {
+      bfreq.clear();
+      std::unordered_set<uint64_t> K;
+      int count = 0;
+      for (size_t q = p; q < lines.size();) {
+        const Line &ln = lines[q++];
+        if (!ln.valid) continue;
+        for (auto k : ln.words) {
+          num_words++;
+          if (bfreq.find(k) == bfreq.end()) K.insert(k);
+          bfreq[k]++;
+        }
+        if (++count > B) break;
+      }
+      if (K.size() < 5) break;
+      pull(K);
+      gen_batch_table();
+      int lc = 0;
+      while (p < lines.size()) {
+        const Line &ln = lines[p++];
+        learn_instance(ln.words);
+        actual_train_words += ln.words.size();
+        if (++lc > B) break;
+      }
+      push(K);
+      for (auto k : K) {  // MiniBatch::clear (word2vec.h:386-391)
+        cache.erase(k);
+        grads.erase(k);
+      }
+    }
+  }
+
   // word2vec_global.h:591-651 TrainModelThread(0) with nthreads = 1
   void train_iter() {
     actual_train_words = 0;
@@ -523,6 +607,7 @@ typedef struct {
   float sample, alpha, lr;
   uint64_t table_size;
   int32_t key_mode;
+  int32_t minibatch_vocab;
 } orc_w2v_cfg;
 
 const char *orc_last_error(void) { return g_err.c_str(); }
@@ -530,8 +615,8 @@ const char *orc_last_error(void) { return g_err.c_str(); }
 void *orc_w2v_create(const char *corpus_path, const orc_w2v_cfg *c) {
   try {
     W2V *m = new W2V();
-    m->cfg = W2VCfg{c->dim,    c->window, c->negative, c->min_sentence_length, c->minibatch, c->storage_f32,
-                    c->sample, c->alpha,  c->lr,       c->table_size,          c->key_mode};
+    m->cfg = W2VCfg{c->dim,    c->window, c->negative,   c->min_sentence_length, c->minibatch,
+                    c->storage_f32, c->sample, c->alpha, c->lr, c->table_size, c->key_mode, c->minibatch_vocab};
     std::vector<std::string> raw;
     if (!read_lines(corpus_path, raw)) {
       g_err = "cannot open corpus";
@@ -541,6 +626,7 @@ void *orc_w2v_create(const char *corpus_path, const orc_w2v_cfg *c) {
     m->lines.resize(raw.size());
     for (size_t i = 0; i < raw.size(); i++) m->parse(raw[i], m->lines[i]);
     m->gather_all();
+    m->num_words = m->train_words;  // the first gather_keys(file, nlines) (word2vec.h:467-471)
     if (m->local_keys.size() < 5) {  // word2vec_global.h:556: train() returns
       g_err = "fewer than 5 keys";
       delete m;
@@ -644,7 +730,13 @@ uint64_t orc_w2v_negatives(void *h, int64_t *out, uint64_t cap) {
 
 int orc_w2v_train(void *h, int niters) {
   try {
-    for (int i = 0; i < niters; i++) ((W2V *)h)->train_iter();
+    W2V *m = (W2V *)h;
+    for (int i = 0; i < niters; i++) {
+      if (m->cfg.minibatch_vocab)
+        m->train_iter_local();
+      else
+        m->train_iter();
+    }
     return 0;
   } catch (std::exception &e) {
     g_err = e.what();

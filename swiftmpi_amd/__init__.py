@@ -200,12 +200,12 @@ class Word2Vec:
 
     def __init__(self, table, window=5, negative=5, min_sentence_length=1, minibatch=100, sample=1e-5, alpha=0.05,
                  unigram_size=int(1e8), key_mode="bkdr", init="ref", rand_seed=1, rand_offset=2, profile=False,
-                 fp64_intermediates=True):
+                 fp64_intermediates=True, minibatch_vocab=False):
         assert table.layout == "w2v"
         cfg = capi.W2VCfg(window, negative, min_sentence_length, minibatch, sample, alpha, unigram_size,
                           capi.KEY_ATOI if key_mode == "atoi" else capi.KEY_BKDR,
                           capi.W2V_INIT_REF if init == "ref" else capi.W2V_INIT_TABLE, rand_seed, rand_offset,
-                          int(fp64_intermediates), int(profile))
+                          int(fp64_intermediates), int(profile), int(minibatch_vocab))
         h = ctypes.c_void_p()
         check(capi.lib().swps_w2v_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h

@@ -124,6 +124,41 @@ __global__ void k_keep(const int32_t *__restrict__ tok, uint64_t nt, const float
   }
 }
 
+// word2vec.h:621-629 to_sample with per-minibatch counts: freq =
+// count_in_batch / (int)_num_words, where _num_words (never reset) is
+// tw[b] for batch b of this epoch; btok[b] = first token of batch b.
+__global__ void k_keep_mb(const int32_t *__restrict__ bcnt, uint64_t nt, const int64_t *__restrict__ btok,
+                          uint32_t nb, const int32_t *__restrict__ tw, float sample, uint64_t fstate, int sample_on,
+                          int32_t *__restrict__ kflag) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = r * kKeepRun;
+  if (i0 > nt) return;
+  uint64_t y = sample_on ? lcg_jump(fstate, i0, kFlcgA, kLcgC) : 0;
+  uint32_t b = 0, hi = nb;  // batch of token i0
+  while (hi - b > 1) {
+    const uint32_t mid = (b + hi) >> 1;
+    if ((uint64_t)btok[mid] <= i0)
+      b = mid;
+    else
+      hi = mid;
+  }
+  for (uint64_t i = i0; i < i0 + kKeepRun && i <= nt; i++) {
+    if (i == nt) {
+      kflag[i] = 0;
+      break;
+    }
+    int32_t keep = 1;
+    if (sample_on) {
+      while (b + 1 < nb && (uint64_t)btok[b + 1] <= i) b++;
+      y = y * kFlcgA + kLcgC;
+      const float freq = (float)bcnt[i] / (float)tw[b];
+      const float ran = (float)(1 - sqrt((double)(sample / freq)));
+      keep = flcg_value(y) > ran;
+    }
+    kflag[i] = keep;
+  }
+}
+
 // main-LCG draws per line: 1 (learn_instance's initial b) + kept*(1+negative)
 __global__ void k_line_draws(const int64_t *__restrict__ line_off, uint64_t nl, const int32_t *__restrict__ kscan,
                              int N, uint64_t *__restrict__ ldraw) {
@@ -174,6 +209,9 @@ struct RecArgs {
   uint64_t mW;  // floor((2^64-1)/W)
   const int32_t *unigram;
   uint64_t uni_size, mT;
+  const uint64_t *bstarts;  // minibatch-vocab mode: run starts of the batch's table [bU+1] (else nullptr)
+  const int32_t *buk;       // the batch's vids in std::map key order (the table's word order)
+  uint32_t bU;
   const int32_t *local;
   uint32_t U;
   int32_t *rec;     // [P][RS]: word, ctx vid x 2W (-1 = none), target vid x (N+1) (-1 = skipped)
@@ -229,7 +267,20 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
       int32_t tv = word;
       if (d > 0) {
         x = x * kLcgA + kLcgC;
-        tv = a.unigram[fast_mod(x >> 16, a.uni_size, a.mT)];
+        const uint64_t slot = fast_mod(x >> 16, a.uni_size, a.mT);
+        if (a.bstarts) {  // word2vec.h:398-425 table over the minibatch vocab, run-length form
+          uint32_t lo = 0, hi = a.bU;  // largest u with bstarts[u] <= slot
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.bstarts[mid] <= slot)
+              lo = mid;
+            else
+              hi = mid;
+          }
+          tv = a.buk[lo];
+        } else {
+          tv = a.unigram[slot];
+        }
         if (a.trace) a.trace[p * N + d - 1] = tv;
         if (tv == word) tv = -1;
       }
@@ -778,6 +829,8 @@ struct swps_w2v {
   struct Batch {
     uint64_t l0, l1, kofs;
     uint32_t U;
+    uint64_t sofs = 0;    // minibatch-vocab mode: offset of the batch's table run starts
+    uint64_t gathered = 0;  // words its gather_keys counted into _num_words
   };
   std::vector<Batch> batches;
   std::vector<int32_t> allK;
@@ -803,6 +856,12 @@ struct swps_w2v {
   DevMem d_vkeys, d_init_order, d_serve_rows, d_push_rows;
   hipStream_t ss = nullptr;  // serve stream (request / serve_pull / serve_push); nullptr = s
   std::vector<uint32_t> plan_P;     // kept positions per batch of the current epoch
+  // minibatch-vocab mode (word2vec.h MiniBatch, w2v_local.cpp)
+  std::vector<int32_t> allUK;       // per batch: its vids in std::map key order (offset kofs)
+  std::vector<uint64_t> bstarts;    // per batch: U+1 table run starts (offset sofs)
+  std::vector<int32_t> bcnt_tok;    // per trained token: its word's count in its batch
+  uint64_t gather_end = 0;          // words counted by the epoch's final (< 5 keys) gather
+  DevMem d_bstarts, d_UK, d_bcnt_tok, d_tw;
   // the prepared (parameter-independent) half of the next minibatch
   struct Prepped {
     bool valid = false, records = false, sorted = false;
@@ -847,6 +906,9 @@ int ingest(swps_w2v *w, const std::vector<uint64_t> &tok_keys, std::vector<int64
     const int64_t a = w->line_off[l], b = w->line_off[l + 1];
     const bool valid = (b - a) >= w->cfg.min_sentence_length;
     w->line_valid[l] = valid;
+    if (w->cfg.minibatch_vocab && !valid && b > a)
+      return fail(SWPS_E_UNSUPPORTED, "minibatch-vocab mode: a non-empty line shorter than min_sentence_length is "
+                                      "trained but never gathered (word2vec.h:521-523, UB in the reference)");
     if (!valid) continue;
     tw += (uint64_t)(b - a);
     for (int64_t i = a; i < b; i++) {
@@ -974,6 +1036,77 @@ void build_schedule(swps_w2v *w) {
   }
 }
 
+// word2vec.h:496-538 train_iter with nthreads = 1: gather_keys reads the next
+// B+1 valid lines (word2vec.h:323-377; counts into a std::map, every word
+// into _num_words), fewer than 5 keys ends the epoch, then B+1 lines (valid or
+// not) are trained from the same position.  The batch's key set is its
+// std::map key order; its unigram table (run starts) follows that order.
+int build_schedule_mb(swps_w2v *w) {
+  const uint64_t nl = w->line_off.size() - 1;
+  const int B = w->cfg.minibatch;
+  w->batches.clear();
+  w->allK.clear();
+  w->allUK.clear();
+  w->bstarts.clear();
+  w->bcnt_tok.assign(w->tok.size(), 0);
+  std::map<int32_t, int32_t> freq_vid;  // counts per vid, then re-ordered by key
+  uint64_t p = 0;
+  std::vector<std::pair<uint64_t, int32_t>> kv;  // (key, vid)
+  std::unordered_map<int32_t, int32_t> cnt_of;
+  while (true) {
+    cnt_of.clear();
+    uint64_t G = 0;
+    int count = 0;
+    for (uint64_t q = p; q < nl;) {
+      const uint64_t l = q++;
+      if (!w->line_valid[l]) continue;
+      for (int64_t i = w->line_off[l]; i < w->line_off[l + 1]; i++) {
+        cnt_of[w->tok[i]]++;
+        G++;
+      }
+      if (++count > B) break;
+    }
+    if (cnt_of.size() < 5) {
+      w->gather_end = G;
+      break;
+    }
+    swps_w2v::Batch b{p, std::min<uint64_t>(nl, p + (uint64_t)B + 1), w->allK.size(), (uint32_t)cnt_of.size(),
+                      w->bstarts.size(), G};
+    kv.clear();
+    for (auto &c : cnt_of) kv.push_back({w->vocab_keys[c.first], c.first});
+    std::sort(kv.begin(), kv.end());
+    std::vector<uint64_t> keys(kv.size());
+    std::vector<int32_t> cnts(kv.size());
+    for (size_t i = 0; i < kv.size(); i++) {
+      keys[i] = kv[i].first;
+      cnts[i] = cnt_of[kv[i].second];
+      w->allUK.push_back(kv[i].second);
+      w->allK.push_back(kv[i].second);
+    }
+    std::vector<uint64_t> st;
+    unigram_starts(keys.data(), cnts.data(), keys.size(), w->cfg.unigram_size, st);
+    w->bstarts.insert(w->bstarts.end(), st.begin(), st.end());
+    for (uint64_t l = b.l0; l < b.l1; l++)
+      for (int64_t i = w->line_off[l]; i < w->line_off[l + 1]; i++) {
+        auto it = cnt_of.find(w->tok[i]);
+        if (it == cnt_of.end())
+          return fail(SWPS_E_UNSUPPORTED, "a trained word is outside its minibatch's gathered vocab "
+                                          "(to_sample reads past word_freq in the reference)");
+        w->bcnt_tok[i] = it->second;
+      }
+    w->batches.push_back(b);
+    p = b.l1;
+  }
+  if (w->batches.empty()) return fail(SWPS_E_UNSUPPORTED, "no minibatch with 5 keys (word2vec.h:532 breaks)");
+  w->max_tok = w->max_U = w->max_lines = 0;
+  for (auto &b : w->batches) {
+    w->max_tok = std::max<uint64_t>(w->max_tok, (uint64_t)(w->line_off[b.l1] - w->line_off[b.l0]));
+    w->max_U = std::max<uint64_t>(w->max_U, b.U);
+    w->max_lines = std::max<uint64_t>(w->max_lines, b.l1 - b.l0);
+  }
+  return SWPS_OK;
+}
+
 int upload_corpus(swps_w2v *w) {
   hipStream_t s = w->s;
   const uint64_t V = w->vocab_keys.size();
@@ -1000,13 +1133,20 @@ int upload_corpus(swps_w2v *w) {
     ex[i] = e / (e + 1);
   }
   SWPS_TRY(upload(w->d_exptab, ex, s));
-  std::vector<uint64_t> starts;
-  unigram_starts(w->vocab_keys.data(), w->counts.data(), V, w->cfg.unigram_size, starts);
-  SWPS_TRY(upload(w->d_starts, starts, s));
-  SWPS_TRY(w->d_unigram.ensure(w->cfg.unigram_size * 4));
-  k_build_unigram<<<4096, 256, 0, s>>>(w->d_starts.as<uint64_t>(), (uint32_t)V, w->cfg.unigram_size,
-                                       w->d_unigram.as<int32_t>());
-  SWPS_HIP(hipGetLastError());
+  if (w->cfg.minibatch_vocab) {
+    SWPS_TRY(upload(w->d_bstarts, w->bstarts, s));
+    SWPS_TRY(upload(w->d_UK, w->allUK, s));
+    SWPS_TRY(upload(w->d_bcnt_tok, w->bcnt_tok, s));
+    SWPS_TRY(w->d_tw.ensure(w->batches.size() * 4));
+  } else {
+    std::vector<uint64_t> starts;
+    unigram_starts(w->vocab_keys.data(), w->counts.data(), V, w->cfg.unigram_size, starts);
+    SWPS_TRY(upload(w->d_starts, starts, s));
+    SWPS_TRY(w->d_unigram.ensure(w->cfg.unigram_size * 4));
+    k_build_unigram<<<4096, 256, 0, s>>>(w->d_starts.as<uint64_t>(), (uint32_t)V, w->cfg.unigram_size,
+                                         w->d_unigram.as<int32_t>());
+    SWPS_HIP(hipGetLastError());
+  }
   const size_t es = w->f64 ? 8 : 4;
   SWPS_TRY(w->d_cache_h.ensure(V * w->D * es));
   SWPS_TRY(w->d_cache_v.ensure(V * w->D * es));
@@ -1071,8 +1211,28 @@ int plan_epoch(swps_w2v *w) {
   SWPS_TRY(w->d_ldraw.ensure((L + 1) * 8));
   SWPS_TRY(w->d_ldoff.ensure((L + 1) * 8));
   hipEvent_t ek = w->timer.begin(s);
-  k_keep<<<nblk((T + kKeepRun) / kKeepRun), 256, 0, s>>>(w->d_tok.as<int32_t>(), T, w->d_ran.as<float>(), w->fstate, sample_on,
-                                     w->d_kflag.as<int32_t>());
+  std::vector<int32_t> tw;
+  if (w->cfg.minibatch_vocab) {
+    // _num_words when batch b of epoch e trains: the first full gather, e whole
+    // epochs of gathers (incl. each epoch's final short gather), this epoch's
+    // gathers up to b; `int train_words = num_words()` truncates to 32 bits
+    const uint64_t e = w->cursor / nb;
+    uint64_t per_epoch = w->gather_end;
+    for (auto &b : w->batches) per_epoch += b.gathered;
+    uint64_t acc = w->train_words + e * per_epoch;
+    tw.resize(nb);
+    for (uint64_t b = 0; b < nb; b++) {
+      acc += w->batches[b].gathered;
+      tw[b] = (int32_t)(uint32_t)acc;
+    }
+    SWPS_HIP(hipMemcpyAsync(w->d_tw.p, tw.data(), nb * 4, hipMemcpyHostToDevice, s));
+    k_keep_mb<<<nblk((T + kKeepRun) / kKeepRun), 256, 0, s>>>(w->d_bcnt_tok.as<int32_t>(), T, w->d_btok.as<int64_t>(),
+                                                              (uint32_t)nb, w->d_tw.as<int32_t>(), w->cfg.sample,
+                                                              w->fstate, sample_on, w->d_kflag.as<int32_t>());
+  } else {
+    k_keep<<<nblk((T + kKeepRun) / kKeepRun), 256, 0, s>>>(w->d_tok.as<int32_t>(), T, w->d_ran.as<float>(), w->fstate,
+                                                           sample_on, w->d_kflag.as<int32_t>());
+  }
   SWPS_HIP(hipGetLastError());
   size_t tb1 = 0, tb2 = 0;
   SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, w->d_kflag.as<int32_t>(), w->d_kscan.as<int32_t>(),
@@ -1165,7 +1325,10 @@ int prep_batch(swps_w2v *w) {
     RecArgs ra{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(),
                w->d_pos_tok.as<int32_t>(), (uint32_t)P, w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(),
                w->lstate_epoch, W, N, ~0ULL / (uint64_t)W, w->d_unigram.as<int32_t>(), w->cfg.unigram_size,
-               ~0ULL / w->cfg.unigram_size, w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(),
+               ~0ULL / w->cfg.unigram_size,
+               w->cfg.minibatch_vocab ? w->d_bstarts.as<uint64_t>() + B.sofs : nullptr,
+               w->cfg.minibatch_vocab ? w->d_UK.as<int32_t>() + B.kofs : nullptr, U,
+               w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(),
                w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
                w->d_rows_touched.as<unsigned long long>()};
     hipEvent_t er = tm.begin(s);
@@ -1403,7 +1566,10 @@ int swps_w2v_load_text(swps_w2v *w, const char *path) {
   fclose(f);
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   SWPS_TRY(ingest(w, keys, std::move(off)));
-  build_schedule(w);
+  if (w->cfg.minibatch_vocab)
+    SWPS_TRY(build_schedule_mb(w));
+  else
+    build_schedule(w);
   return upload_corpus(w);
 }
 
@@ -1418,7 +1584,10 @@ int swps_w2v_load_tokens(swps_w2v *w, const uint32_t *word_ids, uint64_t ntok, c
   std::vector<int64_t> off(line_off, line_off + nlines + 1);
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   SWPS_TRY(ingest(w, keys, std::move(off)));
-  build_schedule(w);
+  if (w->cfg.minibatch_vocab)
+    SWPS_TRY(build_schedule_mb(w));
+  else
+    build_schedule(w);
   return upload_corpus(w);
 }
 
@@ -1539,6 +1708,7 @@ int swps_w2v_set_params(swps_w2v *w, const double *hv) {
 }
 
 int swps_w2v_unigram_at(swps_w2v *w, const uint64_t *idx, uint64_t n, uint32_t *out) {
+  if (w->cfg.minibatch_vocab) return fail(SWPS_E_STATE, "minibatch-vocab mode has one table per minibatch");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   SWPS_HIP(hipStreamSynchronize(w->s));
   for (uint64_t i = 0; i < n; i++) {

@@ -261,3 +261,74 @@ def test_pipelined_sharded_deterministic_and_close(lib, gpu, gloo1, tmp_path, fp
     assert not np.array_equal(p1, pl)
     assert abs(o1 - ol) <= 0.02 * abs(ol)
     assert ol > o0 + 0.1 and o1 > o0 + 0.1
+
+
+# ---- word2vec.h's MiniBatch (w2v_local.cpp): per-minibatch vocab and table ----
+def make_local(lib, oracle_mod, path, dtype, D=16, W=3, N=4, B=20, sample=1e-3, table=10 ** 6, min_len=1,
+               fp64_intermediates=True):
+    orc = oracle_mod.W2V(path, D, window=W, negative=N, minibatch=B, sample=sample, table_size=table,
+                         min_sentence_length=min_len, storage_f32=(dtype == "f32"), key_mode=1,
+                         minibatch_vocab=True)
+    orc.init_rand(1, 2)
+    t = lib.Table("w2v", dim=D, capacity=orc.vocab_size + 16, dtype=dtype, learning_rate=0.7)
+    w = lib.Word2Vec(t, window=W, negative=N, minibatch=B, sample=sample, unigram_size=table,
+                     min_sentence_length=min_len, key_mode="atoi", init="ref", rand_offset=2,
+                     fp64_intermediates=fp64_intermediates, minibatch_vocab=True)
+    w.load_text(path)
+    w.init()
+    return orc, t, w
+
+
+@pytest.mark.parametrize("sample,B,N,W,extra", [(1e-3, 20, 4, 3, ()), (-1.0, 7, 5, 5, ()), (1e-2, 13, 2, 2, ("",) * 3),
+                                                (1e-4, 1, 3, 4, ("1 2", "3"))])
+def test_minibatch_vocab_f64_matches_oracle(lib, oracle_mod, gpu, tmp_path, sample, B, N, W, extra):
+    """w2v_local.cpp semantics (word2vec.h MiniBatch): per-minibatch std::map
+    vocab and unigram table, B+1-line gather/train windows, to_sample over the
+    never-reset _num_words, a final short gather (< 5 keys) ending the epoch.
+    Negative draws, kept positions, both RNG states bit-exact; fp64 rows
+    within 1e-9."""
+    from conftest import int_corpus
+    path = int_corpus(str(tmp_path / "c.txt"), 160, 120, seed=41)
+    with open(path, "a") as f:  # empty lines (trained, never gathered) and a short tail
+        for ln in extra:
+            f.write(ln + "\n")
+    orc, t, w = make_local(lib, oracle_mod, path, "f64", W=W, N=N, B=B, sample=sample)
+    orc.trace_negatives(100000)
+    w.trace_negatives(100000)
+    orc.train(3)
+    w.train(3)
+    so, sg = orc.stats(), w.stats()
+    assert sg["lstate"] == so["rng"] and sg["fstate"] == so["frng"], (so, sg)
+    assert sg["kept"] == so["kept"] and sg["words"] == 3 * so["actual_train_words"]  # oracle: last epoch
+    assert np.array_equal(w.negatives(100000), orc.negatives(100000))
+    po, pg = orc.get_params(), w.get_params()
+    assert np.allclose(pg, po, rtol=1e-9, atol=1e-12), float(np.abs(pg - po).max())
+
+
+def test_minibatch_vocab_f32_and_sharded(lib, oracle_mod, gpu, gloo1, tmp_path):
+    """fp32 tables within 1e-5 of the oracle's fp32-storage mode; the sharded
+    lockstep driver (world 1) equals the single-GPU run bit for bit."""
+    from conftest import int_corpus
+    from swiftmpi_amd.dist import ShardedWord2Vec
+    path = int_corpus(str(tmp_path / "c.txt"), 200, 150, seed=42)
+    orc, t, w = make_local(lib, oracle_mod, path, "f32", B=25)
+    orc.train(2)
+    w.train(2)
+    po, pg = orc.get_params(), w.get_params()
+    assert np.allclose(pg, po, rtol=1e-5, atol=1e-7), float(np.abs(pg - po).max())
+    kw = dict(window=3, negative=4, minibatch=25, sample=1e-3, unigram_size=10 ** 6, key_mode="atoi",
+              minibatch_vocab=True, fp64_intermediates=False)
+    t1 = lib.Table("w2v", dim=16, capacity=1024, dtype="f32", learning_rate=0.7, init="hash", seed=2)
+    w1 = lib.Word2Vec(t1, init="table", **kw)
+    w1.load_text(path)
+    w1.init()
+    w1.train(2)
+    t2 = lib.Table("w2v", dim=16, capacity=1024, dtype="f32", learning_rate=0.7, init="hash", seed=2)
+    sh = ShardedWord2Vec(t2, **kw)
+    sh.load_text(path)
+    sh.init()
+    sh.train(2)
+    vk, _ = w1.vocab()
+    keys, rows = sh.shard_rows()
+    pos = {int(k): i for i, k in enumerate(keys)}
+    assert np.array_equal(np.stack([rows[pos[int(k)]] for k in vk]), w1.get_params())
