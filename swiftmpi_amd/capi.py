@@ -9,7 +9,7 @@ import os
 
 from . import build as _build
 
-LIB_PATH = _build.LIB
+LIB_PATH = os.environ.get("SWPS_LIB", _build.LIB)  # SWPS_LIB: A/B timing of another in-tree build
 
 SWPS_OK = 0
 ERRORS = {-1: "SWPS_E_OOM", -2: "SWPS_E_BADKEY", -3: "SWPS_E_HIP", -4: "SWPS_E_RCCL", -5: "SWPS_E_CFG",

@@ -40,11 +40,13 @@ struct DevMem {
     p = nullptr;
     bytes = 0;
   }
-  // grow-only; contents are not preserved
+  // grow-only, with 1/8 headroom so per-batch sizes that wander a little
+  // (kept positions differ per epoch) do not reallocate — a hipFree is a
+  // device-wide sync and a fresh hipMalloc maps pages; contents not preserved
   int ensure(size_t b) {
     if (b <= bytes && p) return SWPS_OK;
     release();
-    size_t nb = b ? b : 16;
+    size_t nb = b ? b + b / 8 : 16;
     if (hipMalloc(&p, nb) != hipSuccess) {
       (void)hipGetLastError();
       return fail(SWPS_E_OOM, "hipMalloc of " + std::to_string(nb) + " bytes failed");

@@ -1396,6 +1396,42 @@ constexpr uint32_t kChunk = 128;
 // the two RNG streams (the float LCG advances one draw per processed token,
 // the main LCG 1 + kept*(1+negative) draws per line), never on the
 // parameters, so one pass per epoch replaces per-batch host syncs.
+// Size every per-batch buffer for the epoch's largest batch once, at plan
+// time, so no hipMalloc / hipFree (a device-wide sync) lands inside a step.
+int presize(swps_w2v *w, uint64_t maxP) {
+  if (maxP == 0) return SWPS_OK;
+  const int W = w->W, N = w->N, D = w->D, RS = 2 * W + N + 2;
+  const uint64_t HOFF = maxP * (uint64_t)(N + 1), M = HOFF + maxP * (uint64_t)(2 * W);
+  if (M >= (1ULL << 31)) return SWPS_OK;  // prep_batch reports it
+  const size_t a = (w->f64 || w->cfg.fp64_intermediates) ? 8 : 4;
+  SWPS_TRY(w->d_pos_tok.ensure(maxP * 4));
+  SWPS_TRY(w->d_rec.ensure(maxP * RS * 4));
+  SWPS_TRY(w->d_pkeys.ensure(M * 4));
+  SWPS_TRY(w->d_pvals.ensure(M * 4));
+  SWPS_TRY(w->d_pkeys_s.ensure(M * 4));
+  SWPS_TRY(w->d_pvals_s.ensure(M * 4));
+  SWPS_TRY(w->d_neu1.ensure(maxP * D * a));
+  SWPS_TRY(w->d_neu1e.ensure(maxP * D * a));
+  SWPS_TRY(w->d_pg.ensure(HOFF * 4));
+  const uint64_t U = w->max_U;
+  if (U) {
+    int bits = 1;
+    while ((1ULL << bits) <= U) bits++;
+    size_t sb = 0;
+    SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                                                w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (int)M, 0, bits,
+                                                w->s));
+    SWPS_TRY(w->d_tmp.ensure(sb));
+    const uint64_t max_items = 2ULL * U + M / kChunk + 1;
+    SWPS_TRY(w->d_seg.ensure(U * 16));
+    SWPS_TRY(w->d_icnt.ensure((2ULL * U + 1) * 4));
+    SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
+    SWPS_TRY(w->d_desc.ensure(max_items * 16));
+    SWPS_TRY(w->d_partial.ensure(max_items * D * a));
+  }
+  return SWPS_OK;
+}
+
 int plan_epoch(swps_w2v *w) {
   hipStream_t s = w->s;
   const uint64_t nb = w->batches.size();
@@ -1457,7 +1493,12 @@ int plan_epoch(swps_w2v *w) {
   SWPS_HIP(hipMemcpyAsync(&draws, w->d_ldoff.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipStreamSynchronize(s));
   w->plan_P.resize(nb);
-  for (uint64_t i = 0; i < nb; i++) w->plan_P[i] = (uint32_t)(ks[i + 1] - ks[i]);
+  uint64_t maxP = 0;
+  for (uint64_t i = 0; i < nb; i++) {
+    w->plan_P[i] = (uint32_t)(ks[i + 1] - ks[i]);
+    maxP = std::max<uint64_t>(maxP, w->plan_P[i]);
+  }
+  SWPS_TRY(presize(w, maxP));
   w->lstate_epoch = w->lstate;
   w->lstate = lcg_jump(w->lstate, draws, kLcgA, kLcgC);
   if (sample_on) w->fstate = lcg_jump(w->fstate, T, kFlcgA, kLcgC);
