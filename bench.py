@@ -92,6 +92,8 @@ def main():
                     help="time the fp64-intermediate parity mode instead of the default fast mode")
     ap.add_argument("--no-parity-leg", action="store_true",
                     help="skip the extra parity-mode timing reported beside the fast-mode value")
+    ap.add_argument("--sampler", default="table", choices=["table", "alias"],
+                    help="negative sampler: the reference's unigram table (bit-exact draws) or an alias table")
     ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
                     help="w2v: the headline (config 2); lr: config 3 shape; s2v: config 5 shape")
     ap.add_argument("--lr-batch", type=int, default=65536, help="LR rows per GPU per minibatch (config 3)")
@@ -135,7 +137,7 @@ def main():
 
     def build(fp64_intermediates):
         kw = dict(window=args.window, negative=args.negative, minibatch=args.minibatch, sample=args.sample,
-                  alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates)
+                  alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates, sampler=args.sampler)
         t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
                      device=local, init="hash", seed=1)
         if sharded:  # key-sharded over the ranks (BasicHashFrag), RCCL all-to-all per minibatch
@@ -231,7 +233,8 @@ def main():
         "dtype": ("f32 table, f64 intermediates + accumulate" if parity_main else
                   "f32 table, f32 intermediates, f64 accumulate") if args.dtype == "f32" else "f64",
         "data": "synthetic Zipf(s=1) text8 stand-in, random-init (reference glibc-rand) params",
-        "config": {"mode": "parity (fp64 intermediates)" if parity_main else "fast (fp32 intermediates)",
+        "config": {"mode": ("parity (fp64 intermediates)" if parity_main else "fast (fp32 intermediates)") +
+                           (", alias sampler" if args.sampler == "alias" else ""),
                    "workload": "word2vec CBOW-NS (the reference's 'SGNS' app) text8-shaped corpus %d tokens, "
                                "vocab %d, dim %d, window %d, negative %d, sample %g, minibatch %d lines of %d "
                                "tokens, table in one HBM shard" % (args.tokens, info["vocab"], D, args.window,

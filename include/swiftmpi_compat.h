@@ -316,6 +316,7 @@ class Word2VecApp {
     c.fp64_intermediates = fp64_intermediates;
     c.profile = 0;
     c.minibatch_vocab = local ? 1 : 0;
+    c.sampler = SWPS_SAMPLER_TABLE;
     swps_check(swps_w2v_create(t ? t : global_swps_table(), &c, &_w));
   }
   ~Word2VecApp() { swps_w2v_destroy(_w); }

@@ -148,7 +148,14 @@ typedef struct {
                                 * 1: apps/word2vec/word2vec.h's MiniBatch (w2v_local.cpp): per-minibatch
                                 * vocab and table (std::map order), B+1-line windows, to_sample over the
                                 * never-reset _num_words */
+  int32_t sampler;             /* SWPS_SAMPLER_TABLE (the reference's cumulative unigram^0.75 table,
+                                * bit-exact draws) or SWPS_SAMPLER_ALIAS (Walker/Vose alias table over the
+                                * same weights: V x 8 B instead of table_size x 4 B, one L2-resident read per
+                                * draw; same LCG consumption, different words — a non-parity fast mode) */
 } swps_w2v_cfg;
+
+#define SWPS_SAMPLER_TABLE 0
+#define SWPS_SAMPLER_ALIAS 1
 
 /* The table must use SWPS_LAYOUT_W2V; ctx is bound to the table's device. */
 int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out);

@@ -200,12 +200,13 @@ class Word2Vec:
 
     def __init__(self, table, window=5, negative=5, min_sentence_length=1, minibatch=100, sample=1e-5, alpha=0.05,
                  unigram_size=int(1e8), key_mode="bkdr", init="ref", rand_seed=1, rand_offset=2, profile=False,
-                 fp64_intermediates=True, minibatch_vocab=False):
+                 fp64_intermediates=True, minibatch_vocab=False, sampler="table"):
         assert table.layout == "w2v"
         cfg = capi.W2VCfg(window, negative, min_sentence_length, minibatch, sample, alpha, unigram_size,
                           capi.KEY_ATOI if key_mode == "atoi" else capi.KEY_BKDR,
                           capi.W2V_INIT_REF if init == "ref" else capi.W2V_INIT_TABLE, rand_seed, rand_offset,
-                          int(fp64_intermediates), int(profile), int(minibatch_vocab))
+                          int(fp64_intermediates), int(profile), int(minibatch_vocab),
+                          {"table": 0, "alias": 1}[sampler])
         h = ctypes.c_void_p()
         check(capi.lib().swps_w2v_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h

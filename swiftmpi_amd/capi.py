@@ -40,7 +40,7 @@ class W2VCfg(ctypes.Structure):
     _fields_ = [("window", _i32), ("negative", _i32), ("min_sentence_length", _i32), ("minibatch", _i32),
                 ("sample", ctypes.c_float), ("alpha", ctypes.c_float), ("unigram_size", _u64), ("key_mode", _i32),
                 ("init_mode", _i32), ("rand_seed", ctypes.c_uint32), ("rand_offset", _u64),
-                ("fp64_intermediates", _i32), ("profile", _i32), ("minibatch_vocab", _i32)]
+                ("fp64_intermediates", _i32), ("profile", _i32), ("minibatch_vocab", _i32), ("sampler", _i32)]
 
 
 class LRCfg(ctypes.Structure):

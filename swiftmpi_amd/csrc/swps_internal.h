@@ -106,6 +106,12 @@ __host__ __device__ inline float flcg_value(uint64_t y) {
   return (float)y / 18446744073709551616.0f;
 }
 
+inline uint32_t __float_as_uint_host(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return u;
+}
+
 // ---- host utilities (swps_host.cpp) -----------------------------------------
 uint64_t bkdr(const char *s);
 // glibc random_r TYPE_3 (the generator behind rand()): r[i] = r[i-3] + r[i-31]

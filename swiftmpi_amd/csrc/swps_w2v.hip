@@ -208,6 +208,8 @@ struct RecArgs {
   const uint64_t *bstarts;  // minibatch-vocab mode: run starts of the batch's table [bU+1] (else nullptr)
   const int32_t *buk;       // the batch's vids in std::map key order (the table's word order)
   uint32_t bU;
+  const uint2 *alias;       // SWPS_SAMPLER_ALIAS: {prob bits, alias} per word of the (batch) vocab, else nullptr
+  uint32_t alias_n;
   const int32_t *local;
   uint32_t U;
   int32_t *rec;     // [P][RS]: word, ctx vid x 2W (-1 = none), target vid x (N+1) (-1 = skipped)
@@ -264,7 +266,13 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
       if (d > 0) {
         x = x * kLcgA + kLcgC;
         const uint64_t slot = fast_mod(x >> 16, a.uni_size, a.mT);
-        if (a.bstarts) {  // word2vec.h:398-425 table over the minibatch vocab, run-length form
+        if (a.alias) {  // Walker/Vose alias over unigram^0.75: bucket from the high word, coin from bits 8..31
+          const uint32_t bkt = (uint32_t)(((x >> 32) * (uint64_t)a.alias_n) >> 32);
+          const uint2 e = a.alias[bkt];
+          const float coin = (float)((uint32_t)(x >> 8) & 0xFFFFFFu) * (1.0f / 16777216.0f);
+          const int32_t w = coin < __uint_as_float(e.x) ? (int32_t)bkt : (int32_t)e.y;
+          tv = a.bstarts ? a.buk[w] : w;
+        } else if (a.bstarts) {  // word2vec.h:398-425 table over the minibatch vocab, run-length form
           uint32_t lo = 0, hi = a.bU;  // largest u with bstarts[u] <= slot
           while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -1055,6 +1063,10 @@ struct swps_w2v {
   std::vector<int32_t> bcnt_tok;    // per trained token: its word's count in its batch
   uint64_t gather_end = 0;          // words counted by the epoch's final (< 5 keys) gather
   DevMem d_bstarts, d_UK, d_bcnt_tok, d_tw;
+  // SWPS_SAMPLER_ALIAS: alias tables (global: one over the vocab in vid order;
+  // minibatch-vocab: one per batch over its map order, offset = batch kofs)
+  std::vector<uint2> alias;
+  DevMem d_alias;
   // the prepared (parameter-independent) half of the next minibatch
   struct Prepped {
     bool valid = false, records = false, sorted = false;
@@ -1077,6 +1089,7 @@ int check_cfg(swps_w2v *w) {
   if (c.negative < 0 || c.negative + 1 > 64) return fail(SWPS_E_CFG, "negative must be in [0, 63]");
   if (c.minibatch <= 0) return fail(SWPS_E_CFG, "minibatch must be positive");
   if (c.unigram_size == 0 || c.unigram_size > (1ULL << 31)) return fail(SWPS_E_CFG, "unigram_size out of range");
+  if (c.sampler != SWPS_SAMPLER_TABLE && c.sampler != SWPS_SAMPLER_ALIAS) return fail(SWPS_E_CFG, "unknown sampler");
   const int E = w->f64 ? 2 : 4;
   if (w->D % E != 0) return fail(SWPS_E_UNSUPPORTED, "dim must be a multiple of 16 bytes (4 fp32 / 2 fp64)");
   int nc = w->D / E;
@@ -1229,6 +1242,35 @@ void build_schedule(swps_w2v *w) {
   }
 }
 
+// Vose's alias method over weights count^0.75 (the distribution the
+// reference's unigram table discretises into table_size slots): entry i =
+// {P(keep i) as float bits, alias}; deterministic (stable worklists).
+void build_alias(const int32_t *counts, size_t n, std::vector<uint2> &out) {
+  std::vector<double> q(n);
+  double sum = 0;
+  for (size_t i = 0; i < n; i++) sum += (q[i] = std::pow((double)counts[i], 0.75));
+  std::vector<uint32_t> small, large;
+  for (size_t i = 0; i < n; i++) {
+    q[i] = q[i] * (double)n / sum;
+    (q[i] < 1.0 ? small : large).push_back((uint32_t)i);
+  }
+  const size_t o = out.size();
+  out.resize(o + n);
+  size_t si = 0, li = 0;
+  while (si < small.size() && li < large.size()) {
+    const uint32_t sm = small[si++], lg = large[li];
+    float pr = (float)q[sm];
+    out[o + sm] = make_uint2(__float_as_uint_host(pr), lg);
+    q[lg] -= 1.0 - q[sm];
+    if (q[lg] < 1.0) {
+      li++;
+      small.push_back(lg);
+    }
+  }
+  for (; li < large.size(); li++) out[o + large[li]] = make_uint2(__float_as_uint_host(1.0f), large[li]);
+  for (; si < small.size(); si++) out[o + small[si]] = make_uint2(__float_as_uint_host(1.0f), small[si]);
+}
+
 // word2vec.h:496-538 train_iter with nthreads = 1: gather_keys reads the next
 // B+1 valid lines (word2vec.h:323-377; counts into a std::map, every word
 // into _num_words), fewer than 5 keys ends the epoch, then B+1 lines (valid or
@@ -1241,6 +1283,7 @@ int build_schedule_mb(swps_w2v *w) {
   w->allK.clear();
   w->allUK.clear();
   w->bstarts.clear();
+  w->alias.clear();
   w->bcnt_tok.assign(w->tok.size(), 0);
   std::map<int32_t, int32_t> freq_vid;  // counts per vid, then re-ordered by key
   uint64_t p = 0;
@@ -1279,6 +1322,7 @@ int build_schedule_mb(swps_w2v *w) {
     std::vector<uint64_t> st;
     unigram_starts(keys.data(), cnts.data(), keys.size(), w->cfg.unigram_size, st);
     w->bstarts.insert(w->bstarts.end(), st.begin(), st.end());
+    if (w->cfg.sampler == SWPS_SAMPLER_ALIAS) build_alias(cnts.data(), cnts.size(), w->alias);
     for (uint64_t l = b.l0; l < b.l1; l++)
       for (int64_t i = w->line_off[l]; i < w->line_off[l + 1]; i++) {
         auto it = cnt_of.find(w->tok[i]);
@@ -1326,12 +1370,19 @@ int upload_corpus(swps_w2v *w) {
     ex[i] = e / (e + 1);
   }
   SWPS_TRY(upload(w->d_exptab, ex, s));
+  if (w->cfg.sampler == SWPS_SAMPLER_ALIAS) {
+    if (!w->cfg.minibatch_vocab) {
+      w->alias.clear();
+      build_alias(w->counts.data(), V, w->alias);
+    }
+    SWPS_TRY(upload(w->d_alias, w->alias, s));
+  }
   if (w->cfg.minibatch_vocab) {
     SWPS_TRY(upload(w->d_bstarts, w->bstarts, s));
     SWPS_TRY(upload(w->d_UK, w->allUK, s));
     SWPS_TRY(upload(w->d_bcnt_tok, w->bcnt_tok, s));
     SWPS_TRY(w->d_tw.ensure(w->batches.size() * 4));
-  } else {
+  } else if (w->cfg.sampler != SWPS_SAMPLER_ALIAS) {
     std::vector<uint64_t> starts;
     unigram_starts(w->vocab_keys.data(), w->counts.data(), V, w->cfg.unigram_size, starts);
     SWPS_TRY(upload(w->d_starts, starts, s));
@@ -1565,6 +1616,10 @@ int prep_batch(swps_w2v *w) {
                ~0ULL / w->cfg.unigram_size,
                w->cfg.minibatch_vocab ? w->d_bstarts.as<uint64_t>() + B.sofs : nullptr,
                w->cfg.minibatch_vocab ? w->d_UK.as<int32_t>() + B.kofs : nullptr, U,
+               w->cfg.sampler == SWPS_SAMPLER_ALIAS
+                   ? w->d_alias.as<uint2>() + (w->cfg.minibatch_vocab ? B.kofs : 0)
+                   : nullptr,
+               w->cfg.minibatch_vocab ? U : (uint32_t)w->vocab_keys.size(),
                w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(),
                w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
                w->d_rows_touched.as<unsigned long long>()};
@@ -1946,6 +2001,7 @@ int swps_w2v_set_params(swps_w2v *w, const double *hv) {
 
 int swps_w2v_unigram_at(swps_w2v *w, const uint64_t *idx, uint64_t n, uint32_t *out) {
   if (w->cfg.minibatch_vocab) return fail(SWPS_E_STATE, "minibatch-vocab mode has one table per minibatch");
+  if (w->cfg.sampler == SWPS_SAMPLER_ALIAS) return fail(SWPS_E_STATE, "the alias sampler has no slot table");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   SWPS_HIP(hipStreamSynchronize(w->s));
   for (uint64_t i = 0; i < n; i++) {

@@ -93,3 +93,19 @@ def test_analogy_accuracy_sharded(lib, gpu, gloo1, corpus, reference_acc):
     print("analogy accuracy: reference %.4f  hash-init single GPU %.4f  sharded lockstep %.4f  pipelined %.4f"
           % (reference_acc, acc1, accs[False], accs[True]))
     assert accs[False] > 0.8 and accs[False] == acc1
+
+
+def test_analogy_accuracy_alias_sampler(lib, gpu, corpus, reference_acc):
+    """The alias sampler draws other words than the reference's table (same
+    distribution): the learnt structure matches the reference's accuracy."""
+    path, qs, words = corpus
+    kw = dict(window=W, negative=N, minibatch=B, sample=SAMPLE, unigram_size=10 ** 7, fp64_intermediates=False)
+    t = lib.Table("w2v", dim=D, capacity=4096, dtype="f32", learning_rate=LR)
+    w = lib.Word2Vec(t, init="ref", sampler="alias", **kw)
+    w.load_text(path)
+    w.init()
+    w.train(EPOCHS)
+    vk, _ = w.vocab()
+    acc = accuracy(w.get_params(), vk, lib.bkdr, qs, words)
+    print("analogy accuracy: reference %.4f  gpu fast + alias sampler %.4f" % (reference_acc, acc))
+    assert abs(acc - reference_acc) <= 0.01

@@ -332,3 +332,29 @@ def test_minibatch_vocab_f32_and_sharded(lib, oracle_mod, gpu, gloo1, tmp_path):
     keys, rows = sh.shard_rows()
     pos = {int(k): i for i, k in enumerate(keys)}
     assert np.array_equal(np.stack([rows[pos[int(k)]] for k in vk]), w1.get_params())
+
+
+def test_alias_sampler_distribution(lib, gpu, tmp_path):
+    """SWPS_SAMPLER_ALIAS draws negatives from count^0.75 / sum (the weights
+    the reference's table discretises): empirical frequencies of the traced
+    draws match within 5 sigma for every word, and the LCG stream advances
+    exactly as with the table sampler (one draw per negative)."""
+    path = zipf_corpus(str(tmp_path / "c.txt"), 300, 200, seed=51)
+    kw = dict(window=3, negative=5, minibatch=40, sample=1e-3, unigram_size=10 ** 6)
+    res = {}
+    for sampler in ("table", "alias"):
+        t = lib.Table("w2v", dim=16, capacity=512, dtype="f32", learning_rate=0.7)
+        w = lib.Word2Vec(t, init="ref", sampler=sampler, **kw)
+        w.load_text(path)
+        w.init()
+        w.trace_negatives(10 ** 7)
+        w.train(20)
+        res[sampler] = (w.negatives(10 ** 7), w.stats(), w.vocab()[1])
+    (na, sa, cnt), (nt, st, _) = res["alias"], res["table"]
+    assert sa["lstate"] == st["lstate"] and sa["kept"] == st["kept"]
+    p = cnt.astype(np.float64) ** 0.75
+    p /= p.sum()
+    emp = np.bincount(na, minlength=len(cnt)) / len(na)
+    sigma = np.sqrt(p * (1 - p) / len(na))
+    assert len(na) > 100000
+    assert (np.abs(emp - p) <= 5 * sigma + 1e-9).all(), float(np.max(np.abs(emp - p) / sigma))
