@@ -135,6 +135,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    setup_s = {}
+
     def build(fp64_intermediates):
         kw = dict(window=args.window, negative=args.negative, minibatch=args.minibatch, sample=args.sample,
                   alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates, sampler=args.sampler)
@@ -145,8 +147,11 @@ def main():
             w = ShardedWord2Vec(t, frag_num=args.frag_num, pipeline=pipelined, **kw)
         else:
             w = sw.Word2Vec(t, init="ref", **kw)
+        t0 = time.perf_counter()
         w.load_tokens(ids, off, keys)
+        t1 = time.perf_counter()
         w.init()
+        setup_s.update(ingest=t1 - t0, first_pull=time.perf_counter() - t1)
         return t, w
 
     def timed(w, steps):
@@ -247,7 +252,8 @@ def main():
                                       else "lockstep pull/learn/push"))
                    if sharded else "1 GPU, one HBM shard",
                    "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"],
-                   "pulled_keys_per_step": d["pulled"] / args.steps},
+                   "pulled_keys_per_step": d["pulled"] / args.steps,
+                   "setup_s": dict(setup_s)},
         "roofline": {"bound": "hbm", "kernel": "k_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
