@@ -35,6 +35,7 @@
 #include <unordered_set>
 
 #include "swps_internal.h"
+#include "swps_wave.h"
 
 using namespace swps;
 
@@ -50,11 +51,6 @@ template <> struct RowVec<double> {
   static constexpr int E = 2;
 };
 
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
 
 __device__ __forceinline__ uint64_t mod_magic(uint64_t x, uint64_t d, uint64_t m) {
   const uint64_t q = __umul64hi(x, m);  // underestimates x/d by at most 2
@@ -207,14 +203,19 @@ __global__ __launch_bounds__(256) void k_s2v_docs(S2VDocArgs<T> a) {
             for (int k = 0; k < E; k++) neu1[c][k] += (double)((const T *)&rv[u][c])[k];
       }
     }
-    // positive + negatives (sent2vec.cpp:136-163)
+    // positive + negatives (sent2vec.cpp:136-163), eight at a time: their
+    // per-lane partial dots are reduced together (wave_sum8), lanes 8u..8u+7
+    // then hold target s0+u's dot
+    static_assert(G == 8, "wave_sum8 reduces eight targets");
     for (int s0 = 0; s0 <= N; s0 += G) {
       V hv[G][NCH];
       int32_t id[G];
+      uint32_t tmask = 0;  // wave-uniform: present targets
 #pragma unroll
       for (int u = 0; u < G; u++) {
         id[u] = s0 + u <= N ? r[2 * W + s0 + u] : -1;
         if (id[u] >= 0) {
+          tmask |= 1u << u;
           const V *src = (const V *)(a.rows + (uint64_t)id[u] * 4 * D);
 #pragma unroll
           for (int c = 0; c < NCH; c++)
@@ -235,22 +236,22 @@ __global__ __launch_bounds__(256) void k_s2v_docs(S2VDocArgs<T> a) {
               part[u] += prod;
             }
       }
-#pragma unroll
-      for (int u = 0; u < G; u++)
-        if (id[u] >= 0) part[u] = wsum(part[u]);
+      const double tot = wave_sum8(part, lane);
+      const int label = s0 + (lane >> 3) == 0 ? 1 : 0;
+      float f = 0;
+      f += tot;
+      float gl;
+      if (f > 6)
+        gl = (label - 1) * a.alpha;
+      else if (f < -6)
+        gl = (label - 0) * a.alpha;
+      else
+        gl = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
 #pragma unroll
       for (int u = 0; u < G; u++) {
-        if (id[u] < 0) continue;
+        if (!((tmask >> u) & 1)) continue;
         ntgt++;
-        const int label = s0 + u == 0 ? 1 : 0;
-        float f = 0;
-        f += part[u];
-        if (f > 6)
-          g = (label - 1) * a.alpha;
-        else if (f < -6)
-          g = (label - 0) * a.alpha;
-        else
-          g = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
+        g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl), 8 * u));
         // neu1e += g * h  (Vec operator*(double, Vec): h[i] * (double)g)
 #pragma unroll
         for (int c = 0; c < NCH; c++)
