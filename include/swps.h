@@ -16,6 +16,8 @@
  *                         parameter/global_push_access.h:26-43  (+ accessmethod.h:102-121)
  *   swps_assign/load  SparseTable::assign, ClusterServer::load  sparsetable.h:117, server.h:49-62
  *   swps_dump         SparseTable::output                        sparsetable.h:127-132
+ *   swps_save/restore binary checkpoint (the reference has only the 6-digit text dump of
+ *   swps_w2v_save_state  sparsetable.h:63-70 and cannot resume)
  *   swps_to_node_id   BasicHashFrag::to_node_id                  cluster/hashfrag.h:51-56
  *   swps_w2v_*        Word2Vec<MiniBatch>::train / MiniBatch     apps/word2vec/word2vec_global.h:284-731
  *   swps_lr_*         LR::train / learn_instance / predict       apps/logistic/lr.cpp:157-398
@@ -111,6 +113,12 @@ int swps_table_keys(swps_table *t, uint64_t *keys, uint64_t cap, uint64_t *n);
  * world 1 keeps all. */
 int swps_dump(swps_table *t, const char *path);
 int swps_load(swps_table *t, const char *path, int32_t frag_num, int32_t world, int32_t node_id);
+/* Binary snapshot: every key and every row element bit for bit (incl. the
+ * AdaGrad sums the text dump drops), with a trailing checksum.  restore
+ * verifies the whole file (magic, layout/dtype/dim, checksum) before it
+ * assigns any row, and keeps only node_id's keys like swps_load. */
+int swps_save(swps_table *t, const char *path);
+int swps_restore(swps_table *t, const char *path, int32_t frag_num, int32_t world, int32_t node_id);
 
 /* ---- key -> node map (BasicHashFrag) ------------------------------------ */
 uint64_t swps_fmix64(uint64_t x);                       /* utils/HashFunction.h:16-24 */
@@ -195,6 +203,15 @@ int swps_w2v_kernel_times(swps_w2v *w, double *out14, int32_t reset);
 int swps_w2v_set_profile(swps_w2v *w, int32_t on);
 /* the HIP stream all of this context's work is issued on */
 void *swps_w2v_stream(swps_w2v *w);
+/* Worker checkpoint (with swps_save of its table, an exact resume point at
+ * any batch boundary): batch cursor, both LCG streams at the epoch start,
+ * counters and the worker cache (the stale rows negatives outside the batch
+ * key set read), plus config and corpus fingerprints.  restore_state needs a
+ * fresh context (corpus loaded, not initialised; sharded contexts already
+ * swps_w2v_shard-ed) whose table already holds the vocab rows (swps_restore):
+ * a different corpus or config fails with SWPS_E_CFG. */
+int swps_w2v_save_state(swps_w2v *w, const char *path);
+int swps_w2v_restore_state(swps_w2v *w, const char *path);
 
 /* ---- sharded mode (several GPUs; the caller moves the payloads) ---------
  * Every rank = a worker with its own corpus + a server for the keys whose

@@ -191,6 +191,15 @@ class Table:
     def load(self, path, frag_num=1000, world=1, node_id=0):
         check(capi.lib().swps_load(self.h, path.encode(), frag_num, world, node_id))
 
+    def save(self, path):
+        """Binary snapshot of every key and row, bit for bit (swps_save)."""
+        check(capi.lib().swps_save(self.h, path.encode()))
+
+    def restore(self, path, frag_num=1000, world=1, node_id=0):
+        """Assign the rows of a swps_save snapshot (node_id's keys only when
+        world > 1, as `load`); the file is verified before any row changes."""
+        check(capi.lib().swps_restore(self.h, path.encode(), frag_num, world, node_id))
+
 
 KT_NAMES = ["plan", "forward", "sort", "gather", "push", "pull", "records"]
 
@@ -317,6 +326,25 @@ class Word2Vec:
 
     def stream(self):
         return capi.lib().swps_w2v_stream(self.h)
+
+    def save_state(self, path):
+        """Worker checkpoint: batch cursor, RNG streams, counters, cache."""
+        check(capi.lib().swps_w2v_save_state(self.h, path.encode()))
+
+    def restore_state(self, path):
+        """Resume a fresh context (corpus loaded, not initialised) whose table
+        already holds the vocab rows."""
+        check(capi.lib().swps_w2v_restore_state(self.h, path.encode()))
+
+    def save(self, prefix):
+        """Exact resume point: <prefix>.table (the shard) + <prefix>.w2v."""
+        self.sync()
+        self.table.save(prefix + ".table")
+        self.save_state(prefix + ".w2v")
+
+    def restore(self, prefix):
+        self.table.restore(prefix + ".table")
+        self.restore_state(prefix + ".w2v")
 
 
 class Sent2Vec:

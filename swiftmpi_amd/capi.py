@@ -71,6 +71,8 @@ PROTOS = {
     "swps_table_keys": (ctypes.c_int, [_p, _p, _u64, ctypes.POINTER(_u64)]),
     "swps_dump": (ctypes.c_int, [_p, ctypes.c_char_p]),
     "swps_load": (ctypes.c_int, [_p, ctypes.c_char_p, _i32, _i32, _i32]),
+    "swps_save": (ctypes.c_int, [_p, ctypes.c_char_p]),
+    "swps_restore": (ctypes.c_int, [_p, ctypes.c_char_p, _i32, _i32, _i32]),
     "swps_fmix64": (_u64, [_u64]),
     "swps_bkdr": (_u64, [ctypes.c_char_p]),
     "swps_hashfrag_table": (ctypes.c_int, [_i32, _i32, _p]),
@@ -94,6 +96,8 @@ PROTOS = {
     "swps_w2v_kernel_times": (ctypes.c_int, [_p, _p, _i32]),
     "swps_w2v_set_profile": (ctypes.c_int, [_p, _i32]),
     "swps_w2v_stream": (_p, [_p]),
+    "swps_w2v_save_state": (ctypes.c_int, [_p, ctypes.c_char_p]),
+    "swps_w2v_restore_state": (ctypes.c_int, [_p, ctypes.c_char_p]),
     "swps_w2v_shard": (ctypes.c_int, [_p, _i32, _i32, _i32]),
     "swps_w2v_batch_counts": (ctypes.c_int, [_p, _p, _u64, ctypes.POINTER(_u64)]),
     "swps_w2v_request": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.POINTER(_u64)]),

@@ -104,6 +104,62 @@ bool Config::get(const std::string &sec, const std::string &key, std::string &ou
   return false;
 }
 
+// Running checksum of snapshot payloads: 8-byte words folded with a
+// multiply-xorshift step (each put/get chunk independently, chained), tail
+// bytes one at a time.  Detects bit flips and truncation; not cryptographic.
+uint64_t checksum64(uint64_t h, const void *p, size_t n) {
+  const unsigned char *b = (const unsigned char *)p;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, b + i, 8);
+    h = (h ^ w) * 0x9E3779B97F4A7C15ULL;
+    h ^= h >> 29;
+  }
+  for (; i < n; i++) {
+    h = (h ^ b[i]) * 0x100000001B3ULL;
+    h ^= h >> 29;
+  }
+  return (h ^ (uint64_t)n) * 0xff51afd7ed558ccdULL;
+}
+
+int SnapFile::open(const std::string &p, bool write) {
+  path = p;
+  f = fopen(p.c_str(), write ? "wb" : "rb");
+  if (!f) return fail(SWPS_E_IO, std::string(write ? "cannot write " : "cannot open ") + p);
+  return SWPS_OK;
+}
+
+int SnapFile::put(const void *p, size_t n) {
+  if (n && fwrite(p, 1, n, f) != n) return fail(SWPS_E_IO, "short write to " + path);
+  sum = checksum64(sum, p, n);
+  return SWPS_OK;
+}
+
+int SnapFile::get(void *p, size_t n) {
+  if (n && fread(p, 1, n, f) != n) return fail(SWPS_E_IO, "truncated snapshot " + path);
+  sum = checksum64(sum, p, n);
+  return SWPS_OK;
+}
+
+int SnapFile::finish_write() {
+  const uint64_t s = sum;
+  if (fwrite(&s, 1, 8, f) != 8) return fail(SWPS_E_IO, "short write to " + path);
+  const int bad = fclose(f);
+  f = nullptr;
+  if (bad) return fail(SWPS_E_IO, "cannot close " + path);
+  return SWPS_OK;
+}
+
+int SnapFile::finish_read() {
+  uint64_t s = 0;
+  if (fread(&s, 1, 8, f) != 8) return fail(SWPS_E_IO, "truncated snapshot " + path);
+  if (s != sum) return fail(SWPS_E_IO, "snapshot checksum mismatch in " + path + " (corrupt file)");
+  char extra;
+  if (fread(&extra, 1, 1, f) != 0) return fail(SWPS_E_IO, "trailing bytes after the snapshot checksum in " + path);
+  return SWPS_OK;
+}
+
 }  // namespace swps
 
 extern "C" {

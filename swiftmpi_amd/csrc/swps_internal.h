@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -114,6 +115,26 @@ inline uint32_t __float_as_uint_host(float f) {
 
 // ---- host utilities (swps_host.cpp) -----------------------------------------
 uint64_t bkdr(const char *s);
+uint64_t checksum64(uint64_t h, const void *p, size_t n);
+// binary snapshot files (swps_save / swps_w2v_save_state): every payload byte
+// goes through a running 64-bit checksum, stored after the payload; short
+// reads/writes and checksum mismatches fail with SWPS_E_IO
+struct SnapFile {
+  FILE *f = nullptr;
+  uint64_t sum = 0x5357505353554dULL;
+  std::string path;
+  SnapFile() = default;
+  SnapFile(const SnapFile &) = delete;
+  SnapFile &operator=(const SnapFile &) = delete;
+  ~SnapFile() {
+    if (f) fclose(f);
+  }
+  int open(const std::string &p, bool write);
+  int put(const void *p, size_t n);
+  int get(void *p, size_t n);
+  int finish_write();  // trailing checksum + close
+  int finish_read();   // compare the trailing checksum
+};
 // glibc random_r TYPE_3 (the generator behind rand()): r[i] = r[i-3] + r[i-31]
 struct GlibcRand {
   int32_t r[34];

@@ -600,4 +600,84 @@ int swps_load(swps_table *t, const char *path, int32_t frag_num, int32_t world, 
   return SWPS_OK;
 }
 
+// ---- binary snapshots -------------------------------------------------------
+// The reference can only dump values as text at 6 significant digits and
+// without the AdaGrad sums (sparsetable.h:63-70): a resumed run
+// diverges.  swps_save writes every row element bit for bit:
+//   "SWPSTBL1" | u32 layout | u32 dtype | i32 dim | u32 row_elems | u64 n |
+//   keys u64[n] | rows [n][row_elems] (table dtype) | u64 checksum
+static const char kTableMagic[8] = {'S', 'W', 'P', 'S', 'T', 'B', 'L', '1'};
+
+int swps_save(swps_table *t, const char *path) {
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_TRY(table_check_error(t, t->stream));
+  const uint64_t m = t->host_nrows;
+  std::vector<uint64_t> keys(m);
+  std::vector<char> rows(m * t->row_elems * t->esize);
+  if (m) {
+    SWPS_HIP(hipMemcpy(keys.data(), t->row_key.p, m * 8, hipMemcpyDeviceToHost));
+    SWPS_HIP(hipMemcpy(rows.data(), t->rows.p, rows.size(), hipMemcpyDeviceToHost));
+  }
+  SnapFile f;
+  SWPS_TRY(f.open(path, true));
+  const uint32_t hdr[4] = {(uint32_t)t->cfg.layout, (uint32_t)t->cfg.dtype, (uint32_t)t->cfg.dim,
+                           (uint32_t)t->row_elems};
+  SWPS_TRY(f.put(kTableMagic, 8));
+  SWPS_TRY(f.put(hdr, sizeof(hdr)));
+  SWPS_TRY(f.put(&m, 8));
+  SWPS_TRY(f.put(keys.data(), m * 8));
+  SWPS_TRY(f.put(rows.data(), rows.size()));
+  return f.finish_write();
+}
+
+// Read and verify the whole file before touching the table; then assign the
+// rows (all of them, or those BasicHashFrag gives node_id, as swps_load).
+int swps_restore(swps_table *t, const char *path, int32_t frag_num, int32_t world, int32_t node_id) {
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SnapFile f;
+  SWPS_TRY(f.open(path, false));
+  char magic[8];
+  uint32_t hdr[4];
+  uint64_t m = 0;
+  if (f.get(magic, 8) != SWPS_OK || memcmp(magic, kTableMagic, 8) != 0)
+    return fail(SWPS_E_IO, std::string("not a swps table snapshot: ") + path);
+  SWPS_TRY(f.get(hdr, sizeof(hdr)));
+  if (hdr[0] != (uint32_t)t->cfg.layout || hdr[1] != (uint32_t)t->cfg.dtype || hdr[2] != (uint32_t)t->cfg.dim ||
+      hdr[3] != (uint32_t)t->row_elems)
+    return fail(SWPS_E_CFG, "snapshot (layout " + std::to_string(hdr[0]) + ", dtype " + std::to_string(hdr[1]) +
+                                ", dim " + std::to_string(hdr[2]) + ") does not match the table (layout " +
+                                std::to_string(t->cfg.layout) + ", dtype " + std::to_string(t->cfg.dtype) +
+                                ", dim " + std::to_string(t->cfg.dim) + ")");
+  SWPS_TRY(f.get(&m, 8));
+  const size_t rb = (size_t)t->row_elems * t->esize;
+  if (m > (1ULL << 40) / std::max<size_t>(rb, 1)) return fail(SWPS_E_IO, std::string("corrupt snapshot header: ") + path);
+  std::vector<uint64_t> keys(m);
+  std::vector<char> rows(m * rb);
+  SWPS_TRY(f.get(keys.data(), m * 8));
+  SWPS_TRY(f.get(rows.data(), rows.size()));
+  SWPS_TRY(f.finish_read());
+  if (world > 1 && node_id > 0) {
+    std::vector<uint32_t> map(frag_num);
+    SWPS_TRY(swps_hashfrag_table(frag_num, world, map.data()));
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < m; i++) {
+      if ((int)map[fmix64(keys[i]) % (uint64_t)frag_num] != node_id) continue;
+      if (k != i) {
+        keys[k] = keys[i];
+        memcpy(rows.data() + k * rb, rows.data() + i * rb, rb);
+      }
+      k++;
+    }
+    m = k;
+  }
+  if (!m) return SWPS_OK;
+  if (m > t->cfg.capacity)  // keys new to a partly filled table are caught by the insert
+    return fail(SWPS_E_OOM, "snapshot holds " + std::to_string(m) + " rows; table capacity is " +
+                                std::to_string(t->cfg.capacity));
+  DevMem dk, dv;
+  SWPS_TRY(upload(dk, keys, t->stream));
+  SWPS_TRY(upload(dv, rows, t->stream));
+  return swps_assign(t, dk.as<uint64_t>(), m, dv.p);  // syncs before dk/dv go out of scope
+}
+
 }  // extern "C"

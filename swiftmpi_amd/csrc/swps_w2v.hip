@@ -961,6 +961,7 @@ struct swps_w2v {
   uint64_t lstate = 2008ULL;
   uint64_t fstate = std::numeric_limits<unsigned long>::max() / 2;
   uint64_t lstate_epoch = 0;        // main LCG state at the current epoch's start
+  uint64_t fstate_epoch = 0;        // float LCG state at the current epoch's start
   // sharded mode: keys owned by BasicHashFrag node rank+1
   int rank = 0, world = 1, frag_num = 0;
   bool sharded = false;
@@ -1464,6 +1465,7 @@ int plan_epoch(swps_w2v *w) {
   }
   SWPS_TRY(presize(w, maxP));
   w->lstate_epoch = w->lstate;
+  w->fstate_epoch = w->fstate;
   w->lstate = lcg_jump(w->lstate, draws, kLcgA, kLcgC);
   if (sample_on) w->fstate = lcg_jump(w->fstate, T, kFlcgA, kLcgC);
   return SWPS_OK;
@@ -2133,6 +2135,123 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
                              (const char *)d_grads + off * 2 * w->D * gsz, ss, g32));
     off += src_counts[r];
   }
+  return SWPS_OK;
+}
+
+}  // extern "C"
+
+// ============================================================================
+// Worker checkpoint (swps_w2v_save_state / swps_w2v_restore_state).  With the
+// table snapshot (swps_save) it is an exact resume point at any batch
+// boundary: the epoch plan is a function of the two LCG states at the epoch
+// start, so those are stored instead of the plan, and the worker cache is
+// stored because negatives outside a batch's key set read its stale rows.
+//   "SWPSW2V1" | u64 config fp | u64 corpus fp | u64 V | u32 D | u32 esize |
+//   u64 cursor, lstate0, fstate0, 6 counters, 2 row counters |
+//   cache_h [V][D] | cache_v [V][D] (table dtype) | u64 checksum
+// ============================================================================
+namespace {
+
+const char kW2VMagic[8] = {'S', 'W', 'P', 'S', 'W', '2', 'V', '1'};
+
+uint64_t w2v_config_fp(const swps_w2v *w) {
+  const auto &c = w->cfg;
+  const uint64_t f[] = {(uint64_t)c.window,   (uint64_t)c.negative,         (uint64_t)c.min_sentence_length,
+                        (uint64_t)c.minibatch, __float_as_uint_host(c.sample), __float_as_uint_host(c.alpha),
+                        c.unigram_size,        (uint64_t)c.key_mode,         (uint64_t)c.fp64_intermediates,
+                        (uint64_t)c.minibatch_vocab, (uint64_t)c.sampler,    (uint64_t)w->D,
+                        (uint64_t)w->f64,      (uint64_t)w->sharded,         (uint64_t)w->rank,
+                        (uint64_t)w->world,    (uint64_t)w->frag_num};
+  return checksum64(1, f, sizeof(f));
+}
+
+uint64_t w2v_corpus_fp(const swps_w2v *w) {
+  uint64_t h = checksum64(2, &w->train_words, 8);
+  h = checksum64(h, w->vocab_keys.data(), w->vocab_keys.size() * 8);
+  h = checksum64(h, w->counts.data(), w->counts.size() * 4);
+  h = checksum64(h, w->line_off.data(), w->line_off.size() * 8);
+  return checksum64(h, w->tok.data(), w->tok.size() * 4);
+}
+
+}  // namespace
+
+extern "C" {
+
+int swps_w2v_save_state(swps_w2v *w, const char *path) {
+  if (!w->inited) return fail(SWPS_E_STATE, "nothing to save: the context is not initialised");
+  SWPS_TRY(swps_w2v_sync(w));
+  const uint64_t nb = std::max<uint64_t>(1, w->batches.size());
+  // the current epoch is planned once its first batch was prepared
+  const bool planned = w->cursor % nb != 0 || w->pb.valid;
+  const uint64_t V = w->vocab_keys.size();
+  const uint32_t es = w->f64 ? 8 : 4;
+  uint64_t rt[2] = {0, 0};
+  SWPS_HIP(hipMemcpy(rt, w->d_rows_touched.p, 16, hipMemcpyDeviceToHost));
+  const uint64_t head[] = {w2v_config_fp(w), w2v_corpus_fp(w), V, (uint64_t)w->D | ((uint64_t)es << 32)};
+  const uint64_t st[] = {w->cursor,       planned ? w->lstate_epoch : w->lstate,
+                         planned ? w->fstate_epoch : w->fstate,
+                         w->st_batches,   w->st_kept, w->st_words, w->st_pairs, w->st_pulled, w->st_pushed, rt[0], rt[1]};
+  std::vector<char> cache(V * w->D * es);
+  SnapFile f;
+  SWPS_TRY(f.open(path, true));
+  SWPS_TRY(f.put(kW2VMagic, 8));
+  SWPS_TRY(f.put(head, sizeof(head)));
+  SWPS_TRY(f.put(st, sizeof(st)));
+  for (DevMem *m : {&w->d_cache_h, &w->d_cache_v}) {
+    if (!cache.empty()) SWPS_HIP(hipMemcpy(cache.data(), m->p, cache.size(), hipMemcpyDeviceToHost));
+    SWPS_TRY(f.put(cache.data(), cache.size()));
+  }
+  return f.finish_write();
+}
+
+int swps_w2v_restore_state(swps_w2v *w, const char *path) {
+  if (!w->loaded) return fail(SWPS_E_STATE, "load the corpus first");
+  if (w->inited) return fail(SWPS_E_STATE, "restore_state needs a fresh context (corpus loaded, not initialised)");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  const uint64_t V = w->vocab_keys.size();
+  const uint32_t es = w->f64 ? 8 : 4;
+  SnapFile f;
+  SWPS_TRY(f.open(path, false));
+  char magic[8];
+  uint64_t head[4], st[11];
+  if (f.get(magic, 8) != SWPS_OK || memcmp(magic, kW2VMagic, 8) != 0)
+    return fail(SWPS_E_IO, std::string("not a swps word2vec state snapshot: ") + path);
+  SWPS_TRY(f.get(head, sizeof(head)));
+  SWPS_TRY(f.get(st, sizeof(st)));
+  if (head[0] != w2v_config_fp(w))
+    return fail(SWPS_E_CFG, "snapshot was taken with a different word2vec config (window, negative, minibatch, "
+                            "sample, alpha, dim, dtype, precision mode, sampler or sharding)");
+  if (head[1] != w2v_corpus_fp(w) || head[2] != V || head[3] != ((uint64_t)w->D | ((uint64_t)es << 32)))
+    return fail(SWPS_E_CFG, "snapshot was taken on a different corpus");
+  std::vector<char> ch(V * w->D * es), cv(ch.size());
+  SWPS_TRY(f.get(ch.data(), ch.size()));
+  SWPS_TRY(f.get(cv.data(), cv.size()));
+  SWPS_TRY(f.finish_read());
+  if (!w->sharded) {  // the vocab rows must be in the table already (swps_restore)
+    DevMem dk;
+    SWPS_TRY(upload(dk, w->vocab_keys, w->s));
+    SWPS_TRY(table_lookup(w->t, dk.as<uint64_t>(), V, w->d_vid_row.as<uint32_t>(), w->s));
+    if (table_check_error(w->t, w->s) != SWPS_OK)
+      return fail(SWPS_E_STATE, "the table lacks the worker's vocab rows: swps_restore its table snapshot first");
+  }
+  if (!ch.empty()) {
+    SWPS_HIP(hipMemcpy(w->d_cache_h.p, ch.data(), ch.size(), hipMemcpyHostToDevice));
+    SWPS_HIP(hipMemcpy(w->d_cache_v.p, cv.data(), cv.size(), hipMemcpyHostToDevice));
+  }
+  SWPS_HIP(hipMemcpy(w->d_rows_touched.p, st + 9, 16, hipMemcpyHostToDevice));
+  w->cursor = st[0];
+  w->lstate = st[1];
+  w->fstate = st[2];
+  w->st_batches = st[3];
+  w->st_kept = st[4];
+  w->st_words = st[5];
+  w->st_pairs = st[6];
+  w->st_pulled = st[7];
+  w->st_pushed = st[8];
+  w->pb = swps_w2v::Prepped();
+  const uint64_t nb = std::max<uint64_t>(1, w->batches.size());
+  if (w->cursor % nb != 0) SWPS_TRY(plan_epoch(w));  // mid-epoch: re-plan from the epoch-start states
+  w->inited = true;
   return SWPS_OK;
 }
 

@@ -318,6 +318,30 @@ class ShardedWord2Vec(_ShardedApp):
     def set_profile(self, on):
         self.w.set_profile(on)
 
+    def save(self, prefix):
+        """Per-rank checkpoint <prefix>.rank<r>.{table,w2v,json}: this rank's
+        shard, its worker state and the driver's step cursor.  Lockstep
+        drivers only (a pipelined driver holds a prefetched pull that lacks
+        the last push)."""
+        import json
+        if self._next is not None:
+            raise capi.SwpsError(-6, "save: the pipelined driver holds a prefetched pull")
+        base = "%s.rank%d" % (prefix, self.rank)
+        self.w.save(base)
+        with open(base + ".json", "w") as f:
+            json.dump({"cursor": self.cursor, "world": self.world, "frag_num": self.frag_num}, f)
+
+    def restore(self, prefix):
+        """Resume after load_text/load_tokens (instead of init)."""
+        import json
+        base = "%s.rank%d" % (prefix, self.rank)
+        with open(base + ".json") as f:
+            meta = json.load(f)
+        if meta["world"] != self.world or meta["frag_num"] != self.frag_num:
+            raise capi.SwpsError(-5, "checkpoint of world %d / frag_num %d" % (meta["world"], meta["frag_num"]))
+        self.w.restore(base)
+        self.cursor = meta["cursor"]
+
     def shard_rows(self):
         """(keys, rows [n][4D] fp64) of the keys this rank owns."""
         keys = self.table.keys()
