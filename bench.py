@@ -64,6 +64,63 @@ def cpu_baseline(ids, off, keys, args, lines):
                       "the same corpus, 1 epoch, D=%d; %.1f s" % (lines, words, args.dim, dt)}
 
 
+def cpu_baseline_lr(y, off, f, v, minibatch, lr, rows):
+    """The oracle's LR (lr.cpp semantics, nthreads = 1, fp32) on the first
+    `rows` rows of the same synthetic Criteo-shaped data, one epoch."""
+    import oracle
+    oracle.build()
+    rows = min(rows, len(y))
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "lr.txt")
+        with open(path, "w") as fh:
+            for r in range(rows):
+                a, b = int(off[r]), int(off[r + 1])
+                fh.write("%g %s\n" % (y[r], " ".join("%d:%g" % (k, x) for k, x in zip(f[a:b], v[a:b]))))
+        m = oracle.LR(path, minibatch=minibatch, lr=lr)
+        t0 = time.perf_counter()
+        m.train(1)
+        dt = time.perf_counter() - t0
+    return {"value": rows / dt, "unit": "examples/s", "cores": 1, "kind": "port",
+            "sample": "oracle/swps_oracle.cpp LR (fp32, nthreads=1 semantics) on the first %d rows of the same "
+                      "data, minibatch %d, 1 epoch; %.1f s" % (rows, minibatch, dt)}
+
+
+def cpu_baseline_s2v(toks, off, args, docs):
+    """The oracle's sent2vec (sent2vec.cpp on word2vec.h's MiniBatch,
+    nthreads = 1, fp64) on the first `docs` documents, word vectors for their
+    vocabulary in the reference's dump format."""
+    import oracle
+    oracle.build()
+    docs = min(docs, len(off) - 1)
+    n = int(off[docs])
+    words = np.unique(toks[:n])
+    rng = np.random.default_rng(11)
+    with tempfile.TemporaryDirectory() as d:
+        cpath, wpath = os.path.join(d, "docs.txt"), os.path.join(d, "words.txt")
+        with open(cpath, "w") as fh:
+            for i in range(docs):
+                fh.write(" ".join(str(int(x)) for x in toks[int(off[i]):int(off[i + 1])]) + "\n")
+        # values (U(-0.5,0.5)/D, the reference's init scale) from a pool of 4096 fixed-width
+        # strings so the dump of ~1e5 words x 2D values is written in seconds
+        pool = np.array([b"% .6f " % x for x in (rng.random(4096) - 0.5) / args.dim], dtype="S10")
+        body = pool[rng.integers(0, 4096, (len(words), 2 * args.dim))].view(np.uint8).reshape(len(words), -1).copy()
+        body[:, 10 * args.dim - 1] = ord("\t")
+        body[:, -1] = ord("\n")
+        with open(wpath, "wb") as fh:
+            for k, row in zip(words, body):
+                fh.write(b"%d\t" % int(k) + row.tobytes())
+        m = oracle.S2V(cpath, args.dim, window=args.window, negative=args.negative, minibatch=args.s2v_docs,
+                       niters=1, alpha=args.alpha)
+        m.load_words(wpath)
+        t0 = time.perf_counter()
+        m.train()
+        dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "words/s", "cores": 1, "kind": "port",
+            "sample": "oracle/swps_oracle.cpp sent2vec (fp64, nthreads=1 semantics) on the first %d docs (%d words) "
+                      "of the same corpus, word vectors for their %d distinct words; %.1f s"
+                      % (docs, n, len(words), dt)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,6 +144,8 @@ def main():
                     help="sharded path: the bounded-staleness driver (pull(i+1)/push(i) overlap learn(i)) instead "
                          "of the default lockstep pull/learn/push order (exact reference semantics)")
     ap.add_argument("--cpu-lines", type=int, default=2500)
+    ap.add_argument("--cpu-rows", type=int, default=1000000, help="LR CPU baseline sample (rows)")
+    ap.add_argument("--cpu-docs", type=int, default=3000, help="sent2vec CPU baseline sample (documents)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity", action="store_true",
                     help="time the fp64-intermediate parity mode instead of the default fast mode")
@@ -199,6 +258,19 @@ def main():
     step_bytes = (2 * es * D * (d["ctx_rows"] + d["tgt_rows"]) + d["pulled"] * 4 * es * D +
                   d["pushed"] * (10 * es * D + 8))
     step_gbs = step_bytes / dt / 1e9
+    # the metric's "sparse push/pull HBM GB/s": §8(d) bytes of the pull gather
+    # (read h,v from the table, write the worker cache: 4·D elements per key) and
+    # of the fused mean + AdaGrad push (mean grads 2·D, read h,v,h2,v2 4·D,
+    # write 4·D elements + the count per key), over those kernels' event times
+    # in the profiled pass (sharded mode: the owner-side install / serve kernels
+    # are not in these timers, so the fields are omitted)
+    pp = {}
+    for name, nbytes in (("pull", dp["pulled"] * 4 * es * D), ("push", dp["pushed"] * (10 * es * D + 8))):
+        ms, n = kt.get(name, (0.0, 0))
+        if ms > 0 and not sharded:
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            pp[name] = {"GBps": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": nbytes / max(n, 1),
+                        "avg_launch_ms": ms / max(n, 1)}
     # HBM traffic of the same kernel from the committed PMC passes of this exact
     # command (scripts/gpu_profile.sh -> scripts/pmc_summary.py); null otherwise
     traffic, traffic_src = None, None
@@ -259,7 +331,8 @@ def main():
                      "traffic_source": traffic_src,
                      "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1),
                      "launches": fwd_n,
-                     "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS},
+                     "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
+                     "pull_push": pp or None},
         "kernel_ms": {k: v[0] for k, v in kt.items()},
         "parity_mode": parity_leg,
     }
@@ -314,49 +387,77 @@ def bench_other(args):
         return dt, float(units)
 
     steps, warm = args.steps, args.warmup
+
+    def run_timed(run, sync, n):
+        barrier()
+        t0 = time.perf_counter()
+        run(n)
+        sync()
+        barrier()
+        return time.perf_counter() - t0
+
     if args.app == "lr":
         from swiftmpi_amd.synth import criteo
         B1 = args.lr_batch + 1
-        rows = B1 * (steps + warm)
+        rows = B1 * (2 * steps + warm)  # warmup, the timed pass, a profiled pass
         y, off, f, v = criteo(rows, seed=3 + rank)
-        t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=args.lr if args.lr != 0.7 else 0.05,
-                     init="hash", seed=1, device=local)
+        lr_rate = args.lr if args.lr != 0.7 else 0.05
+        t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=lr_rate, init="hash", seed=1, device=local)
         if dist is not None:
             from swiftmpi_amd.dist import ShardedLR
             m = ShardedLR(t, frag_num=2000, minibatch=args.lr_batch, profile=False)
             m.load_csr(y, off, f, v)
             m.init()
             run = m.train_steps
-            sync = m.sync
         else:
             m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False)
             m.load_csr(y, off, f, v)
             m.init()
             run = m.train_batches
-            sync = m.sync
         run(warm)
-        sync()
-        barrier()
-        t0 = time.perf_counter()
-        run(steps)
-        sync()
-        barrier()
-        dt = time.perf_counter() - t0
+        m.sync()
+        dt = run_timed(run, m.sync, steps)     # the measured region: no event timing inside
+        m.set_profile(True)                    # a second, profiled pass for the per-kernel roofline
+        m.kernel_times(reset=True)
+        run_timed(run, m.sync, steps)
+        kt = m.kernel_times()
+        m.set_profile(False)
         dt, total = finish(dt, steps * B1)
-        nnz_per_row = 39
+        # SURVEY.md §8(d) LR bytes, over the profiled pass's rows [warm+steps, warm+2*steps) batches:
+        # k_lr_forward per example: fvid, fval, weight, contribution, key (4 B each) per feature + 16 B
+        # (row offset, label, err^2); the step: F*28 per example + 32 per unique key of each batch
+        r0, r1 = (warm + steps) * B1, (warm + 2 * steps) * B1
+        nnz = int(off[r1] - off[r0])
+        uniq = sum(len(np.unique(f[off[(warm + steps + k) * B1]:off[(warm + steps + k + 1) * B1]]))
+                   for k in range(steps))
+        fwd_ms, fwd_n = kt["forward"]
+        fwd_bytes = 20 * nnz + 16 * (r1 - r0)
+        fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+        step_gbs = (28 * nnz + 32 * uniq) * world / dt / 1e9
         out = {"metric": "sparse LR trained examples/sec (AdaGrad, key-sharded PS)", "value": total / dt,
                "unit": "examples/s", "n_gpus": world, "steps": steps, "warmup": warm,
                "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": "f32", "data": "synthetic Criteo-shape hashed features (swiftmpi_amd/synth.py criteo)",
-               "config": {"workload": "sparse logistic regression, 39 features/row, 2^24 hashed feature space, "
-                                      "%d rows per GPU per minibatch" % B1,
+               "config": {"workload": "sparse logistic regression (BASELINE config 3 shape), 39 features/row, "
+                                      "2^24 hashed feature space, %d rows per GPU per minibatch, AdaGrad lr %g"
+                                      % (B1, lr_rate),
                           "parallelism": ("key-sharded PS over %d GPU(s), %s all-to-all-v" % (world, backend))
                           if dist is not None else "1 GPU, one HBM shard",
-                          "features_per_s": total * nnz_per_row / dt}}
+                          "features_per_s": total * nnz / max(r1 - r0, 1) / dt,
+                          "unique_keys_per_step": uniq / steps},
+               "roofline": {"bound": "hbm", "kernel": "k_lr_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": None,
+                            "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1),
+                            "launches": fwd_n, "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
+                            "note": "the step is bound by the exact sequential fp32 per-key sums of the hot "
+                                    "features (the reference's order), not by HBM"},
+               "kernel_ms": {k: v[0] for k, v in kt.items() if v[1]}}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_lr(y, off, f, v, args.lr_batch, lr_rate, args.cpu_rows)
     else:
         from swiftmpi_amd.synth import zipf_tokens
         V, D = 1000000, args.dim
-        nd = args.s2v_docs * (steps + warm)
+        nd = args.s2v_docs * (2 * steps + warm)
         rng = np.random.default_rng(5 + rank)
         lens = rng.integers(50, 201, nd)
         off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
@@ -372,22 +473,38 @@ def bench_other(args):
         s2.load_tokens(toks, off, sent)  # each rank generated its own docs: doc-sharded by construction
         s2.train_batches(warm)
         s2.sync()
-        barrier()
         st0 = s2.stats()
-        t0 = time.perf_counter()
-        s2.train_batches(steps)
-        s2.sync()
-        barrier()
-        dt = time.perf_counter() - t0
+        dt = run_timed(s2.train_batches, s2.sync, steps)
         st1 = s2.stats()
+        s2.set_profile(True)
+        s2.kernel_times(reset=True)
+        run_timed(s2.train_batches, s2.sync, steps)
+        st2 = s2.stats()
+        kt = s2.kernel_times()
+        s2.set_profile(False)
         dt, total = finish(dt, st1["positions"] - st0["positions"])
+        # SURVEY.md §8(d) sent2vec bytes of the docs kernel: 4*D per word row read (contexts + targets)
+        # + 8*D per document (its row read and written)
+        rows_read = (st2["ctx_rows"] - st1["ctx_rows"]) + (st2["tgt_rows"] - st1["tgt_rows"])
+        ndocs = st2["docs"] - st1["docs"]
+        doc_ms, doc_n = kt["docs"]
+        doc_bytes = 4 * D * rows_read + 8 * D * ndocs
+        doc_gbs = doc_bytes / (doc_ms * 1e-3) / 1e9 if doc_ms > 0 else 0.0
         out = {"metric": "sent2vec trained words/sec (frozen word table, doc-sharded)", "value": total / dt,
                "unit": "words/s", "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": dt * 1e3 / steps,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 table, f64 math",
                "data": "synthetic Zipf(s=1) docs of 50-200 tokens over V=1M, hash-initialised word table",
-               "config": {"workload": "sent2vec, D=%d, window %d, negative %d, %d docs per minibatch, word table "
-                                      "1M x %d" % (D, args.window, args.negative, args.s2v_docs, D),
-                          "parallelism": "doc-sharded over %d GPU(s), no exchange" % world}}
+               "config": {"workload": "sent2vec (BASELINE config 5 shape), D=%d, window %d, negative %d, %d docs "
+                                      "per minibatch, word table 1M x %d" % (D, args.window, args.negative,
+                                                                              args.s2v_docs, D),
+                          "parallelism": "doc-sharded over %d GPU(s), no exchange (replicas only)" % world},
+               "roofline": {"bound": "hbm", "kernel": "k_s2v_docs", "achieved": doc_gbs, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": doc_gbs / HBM_PEAK_GBS, "traffic": None,
+                            "bytes_per_launch": doc_bytes / max(doc_n, 1), "avg_launch_ms": doc_ms / max(doc_n, 1),
+                            "launches": doc_n},
+               "kernel_ms": {k: v[0] for k, v in kt.items()}}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_s2v(toks, off, args, args.cpu_docs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -338,6 +338,7 @@ int swps_lr_predict(swps_lr *l, float *pred_out, float *target_out, uint64_t cap
 int swps_lr_params(swps_lr *l, uint32_t *keys, float *w, float *g2, uint64_t cap, uint64_t *n);
 int swps_lr_info(swps_lr *l, uint64_t *out4); /* nrows, nkeys, nbatches, nnz */
 int swps_lr_sync(swps_lr *l);
+int swps_lr_set_profile(swps_lr *l, int32_t on); /* per-kernel HIP-event timing on/off (swps_lr_cfg.profile at create) */
 int swps_lr_kernel_times(swps_lr *l, double *out8, int32_t reset);
 /* mean of (y-p)^2 over all rows as of each row's last training (lr.cpp:231) */
 int swps_lr_epoch_error(swps_lr *l, double *err);

@@ -550,6 +550,9 @@ class LR:
         check(capi.lib().swps_lr_params(self.h, ptr(keys), ptr(w), ptr(g2), len(keys), ctypes.byref(m)))
         return keys[:m.value], w[:m.value], g2[:m.value]
 
+    def set_profile(self, on):
+        check(capi.lib().swps_lr_set_profile(self.h, int(on)))
+
     def kernel_times(self, reset=False):
         o = np.zeros(8, dtype=np.float64)
         check(capi.lib().swps_lr_kernel_times(self.h, ptr(o), int(reset)))

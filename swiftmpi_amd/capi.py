@@ -136,6 +136,7 @@ PROTOS = {
     "swps_lr_info": (ctypes.c_int, [_p, _p]),
     "swps_lr_sync": (ctypes.c_int, [_p]),
     "swps_lr_kernel_times": (ctypes.c_int, [_p, _p, _i32]),
+    "swps_lr_set_profile": (ctypes.c_int, [_p, _i32]),
     "swps_lr_epoch_error": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_double)]),
     "swps_lr_stream": (_p, [_p]),
     "swps_lr_shard": (ctypes.c_int, [_p, _i32, _i32, _i32]),

@@ -563,6 +563,12 @@ int swps_lr_info(swps_lr *l, uint64_t *o) {
   return SWPS_OK;
 }
 
+int swps_lr_set_profile(swps_lr *l, int32_t on) {
+  SWPS_TRY(swps_lr_sync(l));
+  l->timer.on = on != 0;
+  return SWPS_OK;
+}
+
 int swps_lr_kernel_times(swps_lr *l, double *out, int32_t reset) {
   SWPS_TRY(swps_lr_sync(l));
   for (int k = 0; k < 4; k++) {

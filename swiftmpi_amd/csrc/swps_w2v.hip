@@ -362,7 +362,19 @@ template <typename T, typename A> struct FwdArgs {
   float alpha;
   A *neu1, *neu1e;
   float *pg;
+  int xcd;  // 1: XCD-contiguous block order (xcd_block)
 };
+
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+// §Workgroup dispatch: b and b+8 share one).  Renumber so each XCD walks one
+// contiguous range of positions: neighbouring kept positions share most of
+// their context rows (the window slides by one token), so those rows are
+// re-read from the XCD's own L2 instead of crossing to HBM/MALL.  A bijection
+// on [0, G) for any G; speed only, never correctness.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
+  const uint32_t q = G >> 3, r = G & 7, x = b & 7, i = b >> 3;
+  return x * q + min(x, r) + i;
+}
 
 // One wave per kept position (the body of learn_instance's position loop,
 // word2vec_global.h:663-718).  Context v rows are loaded in groups of G slots
@@ -376,7 +388,8 @@ __global__ __launch_bounds__(256) void k_forward_b8(FwdArgs<T, A> a) {
   using CT = Chk<T, E>;
   using CA = Chk<A, E>;
   const int lane = threadIdx.x & 63;
-  const int p = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int p = __builtin_amdgcn_readfirstlane((int)(blk * 4 + (threadIdx.x >> 6)));
   if (p >= a.P) return;
   const int D = a.D, W = a.W, N = a.N, NC = D / E;
   const int S = 2 * W + N + 1;  // slots: contexts then targets
@@ -485,7 +498,8 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
   using CT = Chk<T, E>;
   using CA = Chk<A, E>;
   const int lane = threadIdx.x & 63;
-  const int p = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int p = __builtin_amdgcn_readfirstlane((int)(blk * 4 + (threadIdx.x >> 6)));
   if (p >= a.P) return;
   const int D = a.D, W = a.W, N = a.N, NC = D / E;
   const int S = 2 * W + N + 1;  // slots: contexts then targets
@@ -929,6 +943,7 @@ struct swps_w2v {
   swps_w2v_cfg cfg{};
   int D = 0, W = 0, N = 0, NCH = 1;
   bool f64 = false;
+  int xcd_order = 1;  // forward blocks in XCD-contiguous order (SWPS_XCD_ORDER=0 turns it off for A/B timing)
   hipStream_t s = nullptr;
   // host corpus / vocab
   std::vector<int32_t> tok;
@@ -1639,7 +1654,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_TRY(w->d_pg.ensure(pb.HOFF * 4));
     FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
                      w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                     w->d_pg.as<float>()};
+                     w->d_pg.as<float>(), w->xcd_order};
     hipEvent_t ef = tm.begin(s);
     switch (w->NCH) {
       case 1: launch_forward<1>(fa, s); break;
@@ -1711,6 +1726,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   w->f64 = t->cfg.dtype == SWPS_F64;
   w->s = t->stream;
   w->timer.on = cfg->profile != 0;
+  if (const char *e = getenv("SWPS_XCD_ORDER")) w->xcd_order = atoi(e) != 0;
   int rc = check_cfg(w);
   if (!rc && hipHostMalloc((void **)&w->h_small, 64) != hipSuccess) rc = fail(SWPS_E_OOM, "pinned alloc");
   if (!rc) rc = w->d_rows_touched.ensure(16);

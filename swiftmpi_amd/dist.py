@@ -402,6 +402,9 @@ class ShardedLR(_ShardedApp):
     def kernel_times(self, reset=False):
         return self.m.kernel_times(reset)
 
+    def set_profile(self, on):
+        self.m.set_profile(on)
+
     def shard_weights(self):
         """(keys, w, g2) of the feature keys this rank owns, sorted by key."""
         keys = np.sort(self.table.keys())
