@@ -137,148 +137,202 @@ template <typename T> struct S2VDocArgs {
   unsigned long long *rows_read;
 };
 
-// One wave per sentence: learn_instance (sent2vec.cpp:109-181) for every
-// position of every pass, in order.  Lane l owns elements [E*ci, E*ci+E) for
-// ci = l + 64*c; all arithmetic is fp64 like the reference's Vec, products
-// rounded before their adds (-ffp-contract=off).
-template <typename T, int NCH, int G>
-__global__ __launch_bounds__(256) void k_s2v_docs(S2VDocArgs<T> a) {
+// A word-table row slice held by one lane: NCH 16-byte chunks (elements
+// [E*ci, E*ci+E) for ci = lane + 64*c) plus, when TAIL, one scalar at element
+// 64*E*NCH + lane.  D = 300 fp32 is one float4 chunk + a 44-lane float tail
+// (5 registers per row instead of the 8 two whole chunks take), which leaves
+// room to keep two positions' rows in flight.
+template <typename T, int NCH, bool TAIL> struct Slice {
   using V = typename RowVec<T>::V;
+  static constexpr int E = RowVec<T>::E;
+  V v[NCH];
+  T t;
+  __device__ __forceinline__ void load(const T *row, int lane, int D) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+      if ((lane + c * 64) * E < D) v[c] = ((const V *)row)[lane + c * 64];
+    if (TAIL && 64 * E * NCH + lane < D) t = row[64 * E * NCH + lane];
+  }
+  __device__ __forceinline__ double at(int c, int k) const { return (double)((const T *)&v[c])[k]; }
+};
+
+// per-lane fp64 accumulator of the same shape
+template <typename T, int NCH, bool TAIL> struct Acc {
+  static constexpr int E = RowVec<T>::E;
+  double v[NCH][E];
+  double t;
+};
+
+template <typename T, int NCH, bool TAIL, int G> struct DocCtx {
+  using SL = Slice<T, NCH, TAIL>;
+  using AC = Acc<T, NCH, TAIL>;
+  static constexpr int E = RowVec<T>::E;
+  const S2VDocArgs<T> &a;
+  const int32_t *rec;
+  int lane, D, W, N, S;
+
+  // rows of slots [s0, s0+G) of record q: context slots read v, target slots h
+  __device__ __forceinline__ void load(int q, int s0, SL (&rv)[G], int32_t (&id)[G]) const {
+    const int32_t *r = rec + (uint64_t)q * S;
+#pragma unroll
+    for (int u = 0; u < G; u++) {
+      const int slot = s0 + u;
+      id[u] = slot < S ? r[slot] : -1;
+      if (id[u] >= 0) rv[u].load(a.rows + (uint64_t)id[u] * 4 * D + (slot < 2 * W ? D : 0), lane, D);
+    }
+  }
+
+  // learn_instance's work for slots [s0, s0+G): context slots add into neu1
+  // in window order (sent2vec.cpp:125-135); target slots (positive, then the
+  // negatives, :136-163) get their fp64 dots with the finished neu1 reduced
+  // together (wave_sum8), g from the exp table, and neu1e += g*h
+  __device__ __forceinline__ void work(int s0, const SL (&rv)[G], const int32_t (&id)[G], AC &neu1, AC &ne,
+                                       float &g, unsigned long long &nctx, unsigned long long &ntgt) const {
+    const bool tl = TAIL && 64 * E * NCH + lane < D;
+#pragma unroll
+    for (int u = 0; u < G; u++) {
+      if (s0 + u >= 2 * W || id[u] < 0) continue;
+      nctx++;
+#pragma unroll
+      for (int c = 0; c < NCH; c++)
+        if ((lane + c * 64) * E < D)
+#pragma unroll
+          for (int k = 0; k < E; k++) neu1.v[c][k] += rv[u].at(c, k);
+      if (tl) neu1.t += (double)rv[u].t;
+    }
+    if (s0 + G <= 2 * W) return;  // no target in this group
+    double part[G];
+    uint32_t tmask = 0;  // wave-uniform: present targets
+#pragma unroll
+    for (int u = 0; u < G; u++) {
+      double pq = 0.0;
+      if (s0 + u >= 2 * W && id[u] >= 0) {
+        tmask |= 1u << u;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          if ((lane + c * 64) * E < D)
+#pragma unroll
+            for (int k = 0; k < E; k++) {
+              const double prod = neu1.v[c][k] * rv[u].at(c, k);
+              pq += prod;
+            }
+        if (tl) {
+          const double prod = neu1.t * (double)rv[u].t;
+          pq += prod;
+        }
+      }
+      part[u] = pq;
+    }
+    const double tot = wave_sum8(part, lane);
+    // lanes 8u..8u+7 hold slot s0+u's dot
+    const int d = s0 + (lane >> 3) - 2 * W;
+    const int label = d == 0 ? 1 : 0;
+    float f = 0;
+    f += tot;
+    float gl;
+    if (f > 6)
+      gl = (label - 1) * a.alpha;
+    else if (f < -6)
+      gl = (label - 0) * a.alpha;
+    else
+      gl = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
+#pragma unroll
+    for (int u = 0; u < G; u++) {
+      if (!((tmask >> u) & 1)) continue;
+      ntgt++;
+      g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl), 8 * u));
+      // neu1e += g * h  (Vec operator*(double, Vec): h[i] * (double)g)
+#pragma unroll
+      for (int c = 0; c < NCH; c++)
+        if ((lane + c * 64) * E < D)
+#pragma unroll
+          for (int k = 0; k < E; k++) {
+            const double prod = rv[u].at(c, k) * (double)g;
+            ne.v[c][k] += prod;
+          }
+      if (tl) {
+        const double prod = (double)rv[u].t * (double)g;
+        ne.t += prod;
+      }
+    }
+  }
+};
+
+// One wave per sentence: learn_instance (sent2vec.cpp:109-181) for every
+// position of every pass, in order.  All arithmetic is fp64 like the
+// reference's Vec, products rounded before their adds (-ffp-contract=off).
+// The sentence vector is the only loop-carried value, and no row address
+// depends on it, so the rows are software-pipelined across positions: slot
+// group 0 (the first G context rows) of position q+1 is in flight while
+// position q's targets are reduced, and group 1 of q while group 0 is summed —
+// one exposed memory latency per position at most, instead of one per group.
+template <typename T, int NCH, bool TAIL, int G>
+__global__ __launch_bounds__(256) void k_s2v_docs(S2VDocArgs<T> a) {
+  using C = DocCtx<T, NCH, TAIL, G>;
+  using SL = typename C::SL;
+  using AC = typename C::AC;
   constexpr int E = RowVec<T>::E;
+  static_assert(G == 8, "wave_sum8 reduces eight targets");
   const int lane = threadIdx.x & 63;
   const uint64_t j = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (j >= a.nd) return;
   const uint64_t doc = a.d0 + j;
   const int L = (int)(a.doc_tok[doc + 1] - a.doc_tok[doc]);
-  const int D = a.D, W = a.W, N = a.N, NC = D / E, S = 2 * W + N + 1;
-  const int32_t *rec = a.rec + (a.doc_rec[doc] - a.doc_rec[a.d0]) * (uint64_t)S;
-  double sent[NCH][E];
+  const int D = a.D, W = a.W, N = a.N, S = 2 * W + N + 1;
+  const C cx{a, a.rec + (a.doc_rec[doc] - a.doc_rec[a.d0]) * (uint64_t)S, lane, D, W, N, S};
+  const bool tl = TAIL && 64 * E * NCH + lane < D;
+  AC sent;
   // Vec::random: (rand()/(float)RAND_MAX - 0.5)/D
+  auto init = [&](int e) {
+    const float u = (float)a.init[doc * D + e] / (float)2147483647;
+    return ((double)u - 0.5) / (double)D;
+  };
 #pragma unroll
-  for (int c = 0; c < NCH; c++) {
-    const int ci = lane + c * 64;
+  for (int c = 0; c < NCH; c++)
 #pragma unroll
-    for (int k = 0; k < E; k++) {
-      sent[c][k] = 0.0;
-      if (ci < NC) {
-        const float u = (float)a.init[doc * D + ci * E + k] / (float)2147483647;
-        sent[c][k] = ((double)u - 0.5) / (double)D;
-      }
-    }
-  }
+    for (int k = 0; k < E; k++) sent.v[c][k] = (lane + c * 64) * E < D ? init((lane + c * 64) * E + k) : 0.0;
+  sent.t = tl ? init(64 * E * NCH + lane) : 0.0;
   float g = 0.f;
   unsigned long long nctx = 0, ntgt = 0;
-  for (int q = 0; q < L * a.niters; q++) {
-    const int32_t *r = rec + (uint64_t)q * S;
-    double neu1[NCH][E], ne[NCH][E];
+  const int Q = L * a.niters;
+  SL ra[G], rb[G];
+  int32_t ia[G], ib[G];
+  if (Q > 0) cx.load(0, 0, ra, ia);
+  for (int q = 0; q < Q; q++) {
+    AC neu1 = sent, ne;
 #pragma unroll
     for (int c = 0; c < NCH; c++)
 #pragma unroll
-      for (int k = 0; k < E; k++) {
-        neu1[c][k] = sent[c][k];
-        ne[c][k] = 0.0;
-      }
-    // neu1 = sent_vec + context v rows in window order (sent2vec.cpp:125-135)
-    for (int s0 = 0; s0 < 2 * W; s0 += G) {
-      V rv[G][NCH];
-      int32_t id[G];
-#pragma unroll
-      for (int u = 0; u < G; u++) {
-        id[u] = s0 + u < 2 * W ? r[s0 + u] : -1;
-        if (id[u] >= 0) {
-          const V *src = (const V *)(a.rows + (uint64_t)id[u] * 4 * D + D);
-#pragma unroll
-          for (int c = 0; c < NCH; c++)
-            if (lane + c * 64 < NC) rv[u][c] = src[lane + c * 64];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < G; u++) {
-        if (id[u] < 0) continue;
-        nctx++;
-#pragma unroll
-        for (int c = 0; c < NCH; c++)
-          if (lane + c * 64 < NC)
-#pragma unroll
-            for (int k = 0; k < E; k++) neu1[c][k] += (double)((const T *)&rv[u][c])[k];
-      }
-    }
-    // positive + negatives (sent2vec.cpp:136-163), eight at a time: their
-    // per-lane partial dots are reduced together (wave_sum8), lanes 8u..8u+7
-    // then hold target s0+u's dot
-    static_assert(G == 8, "wave_sum8 reduces eight targets");
-    for (int s0 = 0; s0 <= N; s0 += G) {
-      V hv[G][NCH];
-      int32_t id[G];
-      uint32_t tmask = 0;  // wave-uniform: present targets
-#pragma unroll
-      for (int u = 0; u < G; u++) {
-        id[u] = s0 + u <= N ? r[2 * W + s0 + u] : -1;
-        if (id[u] >= 0) {
-          tmask |= 1u << u;
-          const V *src = (const V *)(a.rows + (uint64_t)id[u] * 4 * D);
-#pragma unroll
-          for (int c = 0; c < NCH; c++)
-            if (lane + c * 64 < NC) hv[u][c] = src[lane + c * 64];
-        }
-      }
-      double part[G];
-#pragma unroll
-      for (int u = 0; u < G; u++) {
-        part[u] = 0.0;
-        if (id[u] < 0) continue;
-#pragma unroll
-        for (int c = 0; c < NCH; c++)
-          if (lane + c * 64 < NC)
-#pragma unroll
-            for (int k = 0; k < E; k++) {
-              const double prod = neu1[c][k] * (double)((const T *)&hv[u][c])[k];
-              part[u] += prod;
-            }
-      }
-      const double tot = wave_sum8(part, lane);
-      const int label = s0 + (lane >> 3) == 0 ? 1 : 0;
-      float f = 0;
-      f += tot;
-      float gl;
-      if (f > 6)
-        gl = (label - 1) * a.alpha;
-      else if (f < -6)
-        gl = (label - 0) * a.alpha;
-      else
-        gl = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
-#pragma unroll
-      for (int u = 0; u < G; u++) {
-        if (!((tmask >> u) & 1)) continue;
-        ntgt++;
-        g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl), 8 * u));
-        // neu1e += g * h  (Vec operator*(double, Vec): h[i] * (double)g)
-#pragma unroll
-        for (int c = 0; c < NCH; c++)
-          if (lane + c * 64 < NC)
-#pragma unroll
-            for (int k = 0; k < E; k++) {
-              const double prod = (double)((const T *)&hv[u][c])[k] * (double)g;
-              ne[c][k] += prod;
-            }
-      }
+      for (int k = 0; k < E; k++) ne.v[c][k] = 0.0;
+    ne.t = 0.0;
+    if (S > G) cx.load(q, G, rb, ib);
+    cx.work(0, ra, ia, neu1, ne, g, nctx, ntgt);
+    if (q + 1 < Q) cx.load(q + 1, 0, ra, ia);  // prefetch: group 0 of the next position
+    for (int s0 = G; s0 < S; s0 += G) {
+      if (s0 > G) cx.load(q, s0, rb, ib);
+      cx.work(s0, rb, ib, neu1, ne, g, nctx, ntgt);
     }
     // sent_vec += alpha * neu1e (sent2vec.cpp:164)
 #pragma unroll
     for (int c = 0; c < NCH; c++)
 #pragma unroll
       for (int k = 0; k < E; k++) {
-        const double prod = ne[c][k] * (double)a.alpha;
-        sent[c][k] += prod;
+        const double prod = ne.v[c][k] * (double)a.alpha;
+        sent.v[c][k] += prod;
       }
+    if (tl) {
+      const double prod = ne.t * (double)a.alpha;
+      sent.t += prod;
+    }
   }
 #pragma unroll
   for (int c = 0; c < NCH; c++) {
     const int ci = lane + c * 64;
-    if (ci < NC)
+    if (ci * E < D)
 #pragma unroll
-      for (int k = 0; k < E; k++) a.out[doc * D + ci * E + k] = (T)sent[c][k];
+      for (int k = 0; k < E; k++) a.out[doc * D + ci * E + k] = (T)sent.v[c][k];
   }
+  if (tl) a.out[doc * D + 64 * E * NCH + lane] = (T)sent.t;
   if (lane == 0) {
     a.err[doc] = g * g;
     atomicAdd(&a.rows_read[0], nctx);
@@ -298,6 +352,7 @@ struct swps_s2v {
   swps_table *t = nullptr;
   swps_s2v_cfg cfg{};
   int D = 0, W = 0, N = 0, NCH = 1;
+  bool tail = false;  // row slices: NCH 16-B chunks + a scalar tail (k_s2v_docs)
   bool f64 = false;
   hipStream_t s = nullptr;
   // host schedule (fixed at load)
@@ -555,8 +610,8 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   return SWPS_OK;
 }
 
-template <typename T, int NCH> void launch_docs(const S2VDocArgs<T> &a, hipStream_t s) {
-  k_s2v_docs<T, NCH, 8><<<nblk(a.nd * 64), 256, 0, s>>>(a);
+template <typename T, int NCH, bool TAIL> void launch_docs(const S2VDocArgs<T> &a, hipStream_t s) {
+  k_s2v_docs<T, NCH, TAIL, 8><<<nblk(a.nd * 64), 256, 0, s>>>(a);
 }
 
 template <typename T> int s2v_batch(swps_s2v *m) {
@@ -591,11 +646,14 @@ template <typename T> int s2v_batch(swps_s2v *m) {
                    m->cfg.niters, m->cfg.alpha, m->d_out.as<T>(), m->d_err.as<float>(),
                    m->d_rows_read.as<unsigned long long>()};
   hipEvent_t e1 = ev_begin(m);
-  switch (m->NCH) {
-    case 1: launch_docs<T, 1>(da, s); break;
-    case 2: launch_docs<T, 2>(da, s); break;
-    case 3: launch_docs<T, 3>(da, s); break;
-    default: launch_docs<T, 4>(da, s); break;
+  switch (m->NCH * 2 + (m->tail ? 1 : 0)) {
+    case 2: launch_docs<T, 1, false>(da, s); break;
+    case 3: launch_docs<T, 1, true>(da, s); break;
+    case 4: launch_docs<T, 2, false>(da, s); break;
+    case 5: launch_docs<T, 2, true>(da, s); break;
+    case 6: launch_docs<T, 3, false>(da, s); break;
+    case 7: launch_docs<T, 3, true>(da, s); break;
+    default: launch_docs<T, 4, false>(da, s); break;
   }
   SWPS_HIP(hipGetLastError());
   ev_end(m, ST_DOC, e1);
@@ -629,7 +687,13 @@ int swps_s2v_create(swps_table *t, const swps_s2v_cfg *cfg, swps_s2v **out) {
   m->D = D;
   m->W = cfg->window;
   m->N = cfg->negative;
+  // whole 64-lane chunks, and the remainder as a one-scalar-per-lane tail when it fits in 64 lanes
+  const int full = D / (64 * E), rem = D - full * 64 * E;
   m->NCH = nch;
+  if (full >= 1 && rem > 0 && rem <= 64) {
+    m->NCH = full;
+    m->tail = true;
+  }
   m->f64 = t->cfg.dtype == SWPS_F64;
   m->s = t->stream;
   m->timing = cfg->profile != 0;
