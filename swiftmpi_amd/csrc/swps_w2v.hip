@@ -34,6 +34,7 @@
 #include <limits>
 #include <map>
 #include <unordered_map>
+#include <type_traits>
 #include <unordered_set>
 
 #include "swps_internal.h"
@@ -584,6 +585,133 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
   if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
 }
 
+// Fast mode (fp32 rows, fp32 intermediates) when D = 256*NCH + tail with
+// 0 < tail <= 64 (D = 300: one float4 chunk + a 44-lane float tail): a lane's
+// slice of a row is NCH float4 + one float, 5 registers per row at D = 300
+// instead of the 8 two whole float4 chunks take, so more rows are in flight
+// per CU.  Same memory layout (natural element order) as the chunked form.
+template <int NCH> struct FSlice {
+  float4 v[NCH];
+  float t;
+  __device__ __forceinline__ void ld(const float *row, int lane, bool tl) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) v[c] = ((const float4 *)row)[lane + c * 64];
+    if (tl) t = row[256 * NCH + lane];
+  }
+};
+template <int NCH> struct FAcc {
+  double v[NCH][4];
+  double t;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[c][k] = 0.0;
+    t = 0.0;
+  }
+  __device__ __forceinline__ void add(const FSlice<NCH> &r, bool tl) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      v[c][0] += (double)r.v[c].x;
+      v[c][1] += (double)r.v[c].y;
+      v[c][2] += (double)r.v[c].z;
+      v[c][3] += (double)r.v[c].w;
+    }
+    if (tl) t += (double)r.t;
+  }
+  __device__ __forceinline__ void axpy(double g, const FSlice<NCH> &r, bool tl) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const double p0 = g * (double)r.v[c].x, p1 = g * (double)r.v[c].y, p2 = g * (double)r.v[c].z,
+                   p3 = g * (double)r.v[c].w;
+      v[c][0] += p0;
+      v[c][1] += p1;
+      v[c][2] += p2;
+      v[c][3] += p3;
+    }
+    if (tl) {
+      const double p = g * (double)r.t;
+      t += p;
+    }
+  }
+  __device__ __forceinline__ double dot(const FSlice<NCH> &r, bool tl) const {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const double p0 = v[c][0] * (double)r.v[c].x, p1 = v[c][1] * (double)r.v[c].y,
+                   p2 = v[c][2] * (double)r.v[c].z, p3 = v[c][3] * (double)r.v[c].w;
+      s += p0;
+      s += p1;
+      s += p2;
+      s += p3;
+    }
+    if (tl) {
+      const double p = t * (double)r.t;
+      s += p;
+    }
+    return s;
+  }
+  __device__ __forceinline__ void st(float *row, int lane, bool tl) const {
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+      ((float4 *)row)[lane + c * 64] = make_float4((float)v[c][0], (float)v[c][1], (float)v[c][2], (float)v[c][3]);
+    if (tl) row[256 * NCH + lane] = (float)t;
+  }
+};
+
+// k_forward (fast mode) on FSlice rows.
+template <int NCH, int G>
+__global__ __launch_bounds__(256) void k_forward_t(FwdArgs<float, float> a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int p = __builtin_amdgcn_readfirstlane((int)(blk * 4 + (threadIdx.x >> 6)));
+  if (p >= a.P) return;
+  const int D = a.D, W = a.W, N = a.N;
+  const bool tl = 256 * NCH + lane < D;
+  const int S = 2 * W + N + 1;  // slots: contexts then targets
+  const int32_t *r = a.rec + (uint64_t)p * (S + 1);
+  FAcc<NCH> acc, ne;
+  acc.zero();
+  ne.zero();
+  float gk = 0.f;
+  for (int s0 = 0; s0 < S; s0 += G) {
+    FSlice<NCH> rows[G];
+    int32_t vid[G];
+#pragma unroll
+    for (int q = 0; q < G; q++) {
+      const int slot = s0 + q;
+      vid[q] = slot < S ? r[1 + slot] : -1;
+      if (vid[q] >= 0) rows[q].ld((slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * D, lane, tl);
+    }
+#pragma unroll
+    for (int q = 0; q < G; q++) {
+      const int slot = s0 + q;
+      if (vid[q] < 0) continue;
+      if (slot < 2 * W) {
+        acc.add(rows[q], tl);
+      } else {
+        const int d = slot - 2 * W;
+        const double part = wave_sum_pl(acc.dot(rows[q], tl));
+        float f = 0;
+        f += part;
+        const int label = d == 0 ? 1 : 0;
+        float g;
+        if (f > 6)
+          g = (label - 1) * a.alpha;
+        else if (f < -6)
+          g = (label - 0) * a.alpha;
+        else
+          g = (label - a.exptab[(int)((f + 6) * (1000 / 6 / 2))]) * a.alpha;
+        ne.axpy((double)g, rows[q], tl);
+        if (lane == d) gk = g;
+      }
+    }
+  }
+  acc.st(a.neu1 + (uint64_t)p * D, lane, tl);
+  ne.st(a.neu1e + (uint64_t)p * D, lane, tl);
+  if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
+}
+
 // Segment bounds of each (local key, kind) run in the sorted records:
 // seg[0][u], seg[1][u] = h-record range; seg[2][u], seg[3][u] = v-record range.
 __global__ void k_segments(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, uint64_t M,
@@ -724,6 +852,63 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
       const int ci = lane + c * 64;
       if (ci < NC) CA::st(a.partial + (uint64_t)item * a.D, ci, a.D, acc[c]);
     }
+  }
+}
+
+// k_gather (fast mode) on FSlice rows.
+template <int NCH, int UNR>
+__global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
+  const int lane = threadIdx.x & 63;
+  const bool tl = 256 * NCH + lane < a.D;
+  const uint32_t NI = a.ioff[2 * a.U];
+  for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
+    const uint4 d = a.desc[__builtin_amdgcn_readfirstlane(item)];
+    const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
+    uint32_t p0 = 0, p1 = 0;
+    float g0 = 1.f, g1 = 1.f;
+    // records are slot-major: index = slot*P + p (v records after HOFF)
+    if (lane < (int)n) {
+      const uint32_t pi = a.vals[s + lane];
+      if (kind == 0) {
+        p0 = pi % a.P;
+        g0 = a.pg[pi];
+      } else {
+        p0 = (uint32_t)((pi - a.HOFF) % a.P);
+      }
+    }
+    if (lane + 64 < (int)n) {
+      const uint32_t pi = a.vals[s + 64 + lane];
+      if (kind == 0) {
+        p1 = pi % a.P;
+        g1 = a.pg[pi];
+      } else {
+        p1 = (uint32_t)((pi - a.HOFF) % a.P);
+      }
+    }
+    const float *base = kind == 0 ? a.neu1 : a.neu1e;
+    FAcc<NCH> acc;
+    acc.zero();
+    for (uint32_t r0 = 0; r0 < n; r0 += UNR) {
+      FSlice<NCH> rv[UNR];
+      double gg[UNR];
+#pragma unroll
+      for (int q = 0; q < UNR; q++) {
+        const uint32_t idx = min(r0 + q, n - 1);
+        const uint32_t pr = idx < 64 ? __shfl(p0, (int)idx, 64) : __shfl(p1, (int)(idx - 64), 64);
+        gg[q] = (double)(idx < 64 ? __shfl(g0, (int)idx, 64) : __shfl(g1, (int)(idx - 64), 64));
+        rv[q].ld(base + (uint64_t)pr * a.D, lane, tl);
+      }
+#pragma unroll
+      for (int q = 0; q < UNR; q++) {
+        if (r0 + q < n) {
+          if (kind == 0)
+            acc.axpy(gg[q], rv[q], tl);
+          else
+            acc.add(rv[q], tl);
+        }
+      }
+    }
+    acc.st(a.partial + (uint64_t)item * a.D, lane, tl);
   }
 }
 
@@ -943,6 +1128,7 @@ struct swps_w2v {
   swps_w2v_cfg cfg{};
   int D = 0, W = 0, N = 0, NCH = 1;
   bool f64 = false;
+  bool tail = false;  // fast mode: FSlice kernels (D = 256*NCH + tail, 0 < tail <= 64)
   int xcd_order = 1;  // forward blocks in XCD-contiguous order (SWPS_XCD_ORDER=0 turns it off for A/B timing)
   hipStream_t s = nullptr;
   // host corpus / vocab
@@ -1023,6 +1209,8 @@ int check_cfg(swps_w2v *w) {
   if (w->D % E != 0) return fail(SWPS_E_UNSUPPORTED, "dim must be a multiple of 16 bytes (4 fp32 / 2 fp64)");
   int nc = w->D / E;
   w->NCH = (nc + 63) / 64;
+  if (!w->f64 && w->D > 256 && w->D % 256 != 0 && w->D % 256 <= 64) w->tail = true;
+  if (const char *e = getenv("SWPS_SLICE")) w->tail = w->tail && atoi(e) != 0;  // A/B timing
   if (w->NCH > 4) return fail(SWPS_E_UNSUPPORTED, "dim too large (max 1024 fp32 / 512 fp64)");
   return SWPS_OK;
 }
@@ -1656,12 +1844,24 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                      w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
                      w->d_pg.as<float>(), w->xcd_order};
     hipEvent_t ef = tm.begin(s);
+    if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      if (w->tail) {
+        if (D < 512)
+          k_forward_t<1, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
+        else if (D < 768)
+          k_forward_t<2, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
+        else
+          k_forward_t<3, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
+        goto forward_done;
+      }
+    }
     switch (w->NCH) {
       case 1: launch_forward<1>(fa, s); break;
       case 2: launch_forward<2>(fa, s); break;
       case 3: launch_forward<3>(fa, s); break;
       default: launch_forward<4>(fa, s); break;
     }
+  forward_done:
     SWPS_HIP(hipGetLastError());
     tm.end(KT_FWD, ef, s);
   }
@@ -1673,12 +1873,29 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                      w->d_partial.as<A>()};
     const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(pb.max_items * 64), 16384);
     hipEvent_t eg = tm.begin(s);
+    if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      if (w->tail) {
+        if (D < 512)
+          k_gather_t<1, 8><<<ggrid, 256, 0, s>>>(ga);
+        else if (D < 768)
+          k_gather_t<2, 8><<<ggrid, 256, 0, s>>>(ga);
+        else
+          k_gather_t<3, 8><<<ggrid, 256, 0, s>>>(ga);
+        switch (w->NCH) {  // second level over the partials: layout-independent
+          case 2: k_combine<T, A, 2><<<ggrid, 256, 0, s>>>(ga); break;
+          case 3: k_combine<T, A, 3><<<ggrid, 256, 0, s>>>(ga); break;
+          default: k_combine<T, A, 4><<<ggrid, 256, 0, s>>>(ga); break;
+        }
+        goto gather_done;
+      }
+    }
     switch (w->NCH) {
       case 1: launch_gather<1, T, A>(ga, ggrid, s); break;
       case 2: launch_gather<2, T, A>(ga, ggrid, s); break;
       case 3: launch_gather<3, T, A>(ga, ggrid, s); break;
       default: launch_gather<4, T, A>(ga, ggrid, s); break;
     }
+  gather_done:
     SWPS_HIP(hipGetLastError());
     tm.end(KT_GATHER, eg, s);
     w->st_pairs += pb.M;
