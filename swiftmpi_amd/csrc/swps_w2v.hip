@@ -596,7 +596,7 @@ template <int NCH> struct FSlice {
   __device__ __forceinline__ void ld(const float *row, int lane, bool tl) {
 #pragma unroll
     for (int c = 0; c < NCH; c++) v[c] = ((const float4 *)row)[lane + c * 64];
-    if (tl) t = row[256 * NCH + lane];
+    t = row[256 * NCH + (tl ? lane : 0)];  // lanes past the tail load a valid duplicate: no branch
   }
 };
 template <int NCH> struct FAcc {
@@ -617,7 +617,7 @@ template <int NCH> struct FAcc {
       v[c][2] += (double)r.v[c].z;
       v[c][3] += (double)r.v[c].w;
     }
-    if (tl) t += (double)r.t;
+    t += (double)r.t;  // garbage past the tail is never stored nor dotted
   }
   __device__ __forceinline__ void axpy(double g, const FSlice<NCH> &r, bool tl) {
 #pragma unroll
@@ -629,10 +629,8 @@ template <int NCH> struct FAcc {
       v[c][2] += p2;
       v[c][3] += p3;
     }
-    if (tl) {
-      const double p = g * (double)r.t;
-      t += p;
-    }
+    const double p = g * (double)r.t;
+    t += p;
   }
   __device__ __forceinline__ double dot(const FSlice<NCH> &r, bool tl) const {
     double s = 0.0;
@@ -645,10 +643,8 @@ template <int NCH> struct FAcc {
       s += p2;
       s += p3;
     }
-    if (tl) {
-      const double p = t * (double)r.t;
-      s += p;
-    }
+    const double p = t * (double)r.t;
+    s += tl ? p : 0.0;
     return s;
   }
   __device__ __forceinline__ void st(float *row, int lane, bool tl) const {
@@ -660,8 +656,8 @@ template <int NCH> struct FAcc {
 };
 
 // k_forward (fast mode) on FSlice rows.
-template <int NCH, int G>
-__global__ __launch_bounds__(256) void k_forward_t(FwdArgs<float, float> a) {
+template <int NCH, int G, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_forward_t(FwdArgs<float, float> a) {
   const int lane = threadIdx.x & 63;
   const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const int p = __builtin_amdgcn_readfirstlane((int)(blk * 4 + (threadIdx.x >> 6)));
@@ -680,7 +676,7 @@ __global__ __launch_bounds__(256) void k_forward_t(FwdArgs<float, float> a) {
 #pragma unroll
     for (int q = 0; q < G; q++) {
       const int slot = s0 + q;
-      vid[q] = slot < S ? r[1 + slot] : -1;
+      vid[q] = __builtin_amdgcn_readfirstlane(slot < S ? r[1 + slot] : -1);
       if (vid[q] >= 0) rows[q].ld((slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * D, lane, tl);
     }
 #pragma unroll
@@ -855,49 +851,80 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
   }
 }
 
-// k_gather (fast mode) on FSlice rows.
+// Record info of one gather item: position and g of its records 0..127
+// (lanes hold records lane and 64+lane).
+struct ItemRecs {
+  uint32_t p0, p1;
+  float g0, g1;
+};
+__device__ __forceinline__ uint4 uniform4(uint4 d) {  // wave-uniform value: keep its branches scalar
+  return make_uint4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                    __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
+}
+
+__device__ __forceinline__ ItemRecs item_recs(const GatherArgs<float> &a, uint4 d, int lane) {
+  const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
+  ItemRecs r{0, 0, 1.f, 1.f};
+  // records are slot-major: index = slot*P + p (v records after HOFF)
+  if (lane < (int)n) {
+    const uint32_t pi = a.vals[s + lane];
+    if (kind == 0) {
+      r.p0 = pi % a.P;
+      r.g0 = a.pg[pi];
+    } else {
+      r.p0 = (uint32_t)((pi - a.HOFF) % a.P);
+    }
+  }
+  if (lane + 64 < (int)n) {
+    const uint32_t pi = a.vals[s + 64 + lane];
+    if (kind == 0) {
+      r.p1 = pi % a.P;
+      r.g1 = a.pg[pi];
+    } else {
+      r.p1 = (uint32_t)((pi - a.HOFF) % a.P);
+    }
+  }
+  return r;
+}
+
+// k_gather (fast mode) on FSlice rows, software-pipelined across items: most
+// items are short (Zipf tail keys: a few records), so the next item's
+// descriptor and record info are fetched while this item's rows are in flight
+// instead of after them (desc -> vals -> pg -> rows was four dependent
+// memory round trips per item).
 template <int NCH, int UNR>
 __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
   const int lane = threadIdx.x & 63;
   const bool tl = 256 * NCH + lane < a.D;
   const uint32_t NI = a.ioff[2 * a.U];
-  for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
-    const uint4 d = a.desc[__builtin_amdgcn_readfirstlane(item)];
+  const uint32_t stride = gridDim.x * 4;
+  uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= NI) return;
+  uint4 d = uniform4(a.desc[__builtin_amdgcn_readfirstlane(item)]);
+  ItemRecs ri = item_recs(a, d, lane);
+  for (;;) {
+    const uint32_t nx = item + stride;
+    const bool more = nx < NI;
+    const uint4 dn = uniform4(more ? a.desc[__builtin_amdgcn_readfirstlane(nx)] : make_uint4(0, 0x80000000u, 0, 0));
     const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
-    uint32_t p0 = 0, p1 = 0;
-    float g0 = 1.f, g1 = 1.f;
-    // records are slot-major: index = slot*P + p (v records after HOFF)
-    if (lane < (int)n) {
-      const uint32_t pi = a.vals[s + lane];
-      if (kind == 0) {
-        p0 = pi % a.P;
-        g0 = a.pg[pi];
-      } else {
-        p0 = (uint32_t)((pi - a.HOFF) % a.P);
-      }
-    }
-    if (lane + 64 < (int)n) {
-      const uint32_t pi = a.vals[s + 64 + lane];
-      if (kind == 0) {
-        p1 = pi % a.P;
-        g1 = a.pg[pi];
-      } else {
-        p1 = (uint32_t)((pi - a.HOFF) % a.P);
-      }
-    }
     const float *base = kind == 0 ? a.neu1 : a.neu1e;
     FAcc<NCH> acc;
     acc.zero();
+    ItemRecs rn;
     for (uint32_t r0 = 0; r0 < n; r0 += UNR) {
       FSlice<NCH> rv[UNR];
       double gg[UNR];
 #pragma unroll
       for (int q = 0; q < UNR; q++) {
         const uint32_t idx = min(r0 + q, n - 1);
-        const uint32_t pr = idx < 64 ? __shfl(p0, (int)idx, 64) : __shfl(p1, (int)(idx - 64), 64);
-        gg[q] = (double)(idx < 64 ? __shfl(g0, (int)idx, 64) : __shfl(g1, (int)(idx - 64), 64));
+        // idx is wave-uniform: read the record's position and g with v_readlane (scalar results)
+        const uint32_t pr = idx < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)ri.p0, (int)idx)
+                                     : (uint32_t)__builtin_amdgcn_readlane((int)ri.p1, (int)(idx - 64));
+        gg[q] = (double)__int_as_float(idx < 64 ? __builtin_amdgcn_readlane(__float_as_int(ri.g0), (int)idx)
+                                                : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
         rv[q].ld(base + (uint64_t)pr * a.D, lane, tl);
       }
+      if (r0 == 0) rn = item_recs(a, dn, lane);  // next item's record info, behind this item's first rows
 #pragma unroll
       for (int q = 0; q < UNR; q++) {
         if (r0 + q < n) {
@@ -908,7 +935,12 @@ __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
         }
       }
     }
+    if (n == 0) rn = item_recs(a, dn, lane);
     acc.st(a.partial + (uint64_t)item * a.D, lane, tl);
+    if (!more) break;
+    item = nx;
+    d = dn;
+    ri = rn;
   }
 }
 
@@ -1846,12 +1878,12 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     hipEvent_t ef = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
-        if (D < 512)
-          k_forward_t<1, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
-        else if (D < 768)
-          k_forward_t<2, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
+        if (D < 512) {
+          k_forward_t<1, 4, 1><<<nblk(P * 64), 256, 0, s>>>(fa);  // G = 4: occupancy 7 (A/B: G = 2..8)
+        } else if (D < 768)
+          k_forward_t<2, 8, 1><<<nblk(P * 64), 256, 0, s>>>(fa);
         else
-          k_forward_t<3, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
+          k_forward_t<3, 8, 1><<<nblk(P * 64), 256, 0, s>>>(fa);
         goto forward_done;
       }
     }
