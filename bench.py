@@ -234,8 +234,11 @@ def main():
     words = d["words"]
     w.set_profile(True)                     # a second, profiled pass for the per-kernel roofline
     w.kernel_times(reset=True)
+    gw = getattr(w, "w", w)                 # the per-rank Word2Vec (sharded: its learner)
+    g0 = gw.gather_stats()
     _, dp = timed(w, args.steps)
     kt = w.kernel_times()
+    g1 = gw.gather_stats()
     w.set_profile(False)
     del w, t
     if dist is not None:
@@ -248,14 +251,24 @@ def main():
         total_words = float(words)
 
     D, es = args.dim, (8 if args.dtype == "f64" else 4)
+    ea = 8 if (parity_main or args.dtype == "f64") else 4   # neu1/neu1e/partials element size
     kept = d["kept"]
-    # SURVEY.md §8(d) algorithmic bytes of k_forward: each touched row read once
+    # SURVEY.md §8(d) algorithmic bytes of k_forward: every context/target row
+    # occurrence read (4·D per row in fp32) + neu1, neu1e written (2·D·ea per position)
     ctx_rows, tgt_rows = dp["ctx_rows"], dp["tgt_rows"]
     fwd_ms, fwd_n = kt["forward"]
-    fwd_bytes = es * D * (ctx_rows + tgt_rows)
+    fwd_bytes = es * D * (ctx_rows + tgt_rows) + 2 * ea * D * dp["kept"]
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+    # the dominant kernel by time: the segmented gradient sums (k_gather_t + k_combine
+    # under one timer).  Algorithmic bytes: each gradient record reads its source row
+    # (neu1 or neu1e of its position, D·ea) and its 4-B record index; each item (chunk of
+    # <= 128 records of one key) writes one partial row (D·ea) and reads a 16-B descriptor.
+    g_rec, g_items = g1["records"] - g0["records"], g1["items"] - g0["items"]
+    gat_ms, gat_n = kt["gather"]
+    gat_bytes = g_rec * (D * ea + 4) + g_items * (D * ea + 16)
+    gat_gbs = gat_bytes / (gat_ms * 1e-3) / 1e9 if gat_ms > 0 else 0.0
     # whole step (§8(d) full formula): rows read + gradients written + pull 16D/key + push (40D+8)/key
-    step_bytes = (2 * es * D * (d["ctx_rows"] + d["tgt_rows"]) + d["pulled"] * 4 * es * D +
+    step_bytes = (2 * es * D * (dp["ctx_rows"] + dp["tgt_rows"]) + d["pulled"] * 4 * es * D +
                   d["pushed"] * (10 * es * D + 8))
     step_gbs = step_bytes / dt / 1e9
     # the metric's "sparse push/pull HBM GB/s": §8(d) bytes of the pull gather
@@ -273,7 +286,7 @@ def main():
                         "avg_launch_ms": ms / max(n, 1)}
     # HBM traffic of the same kernel from the committed PMC passes of this exact
     # command (scripts/gpu_profile.sh -> scripts/pmc_summary.py); null otherwise
-    traffic, traffic_src = None, None
+    traffic, traffic_src, fwd_traffic = None, None, None
     pmc_name = "r01_pmc_w2v_fast.json"
     pmc = os.path.join(ROOT, "profiles", pmc_name)
     mine = dict(minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, steps=args.steps, warmup=args.warmup,
@@ -281,10 +294,14 @@ def main():
     if os.path.exists(pmc) and not parity_main:
         prof = json.load(open(pmc))
         if prof.get("config") == mine:
+            gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items()
+                  if k.startswith("k_gather") or k.startswith("k_combine")]
+            if gt:  # per gather-timer launch: k_gather_t + k_combine
+                traffic = sum(gt)
+                traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch, k_gather_t + k_combine)" % pmc_name
             for k, v in prof["kernels"].items():
                 if k.startswith("k_forward"):
-                    traffic = v["hbm_bytes_corrected"]
-                    traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch)" % pmc_name
+                    fwd_traffic = v["hbm_bytes_corrected"]
 
     parity_leg = None
     if rank == 0 and world == 1 and not parity_main and not args.no_parity_leg:
@@ -326,11 +343,22 @@ def main():
                    "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"],
                    "pulled_keys_per_step": d["pulled"] / args.steps,
                    "setup_s": dict(setup_s)},
-        "roofline": {"bound": "hbm", "kernel": "k_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": traffic,
+        "roofline": {"bound": "hbm", "kernel": "k_gather_t + k_combine (segmented gradient sums)",
+                     "achieved": gat_gbs, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": gat_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1),
-                     "launches": fwd_n,
+                     "bytes_per_launch": gat_bytes / max(gat_n, 1), "avg_launch_ms": gat_ms / max(gat_n, 1),
+                     "launches": gat_n, "records_per_launch": g_rec / max(gat_n, 1),
+                     "items_per_launch": g_items / max(gat_n, 1),
+                     # k_forward: its row-occurrence bytes exceed its HBM traffic (hot Zipf rows
+                     # hit in L2/MALL), so its "achieved" can pass the HBM peak; hbm_GBps is the
+                     # PMC-measured HBM rate of the same launches
+                     "forward": {"kernel": "k_forward_t", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
+                                 "bytes_per_launch": fwd_bytes / max(fwd_n, 1),
+                                 "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n,
+                                 "traffic": fwd_traffic,
+                                 "hbm_GBps": (fwd_traffic / (fwd_ms / max(fwd_n, 1) * 1e-3) / 1e9
+                                              if fwd_traffic and fwd_ms > 0 else None)},
                      "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
                      "pull_push": pp or None},
         "kernel_ms": {k: v[0] for k, v in kt.items()},

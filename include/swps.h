@@ -185,8 +185,13 @@ int swps_w2v_train_batches(swps_w2v *w, uint64_t count);
 int swps_w2v_train_epochs(swps_w2v *w, int32_t niters);
 int swps_w2v_sync(swps_w2v *w);
 /* cumulative stats: [batches, kept positions, train words, gradient records, lstate, fstate,
- *  pulled keys, pushed keys, context rows read, target rows read] */
+ *  pulled keys, pushed keys, context rows read, target rows read]; the two row counts
+ *  (roofline accounting) advance only while swps_w2v_set_profile is on */
 int swps_w2v_stats(swps_w2v *w, uint64_t *out10);
+/* cumulative work of the segmented gradient sums (k_gather + k_combine), for the
+ * roofline: [gradient records summed (key in the batch), gather items (chunks of <= 128
+ * records of one key and kind)] (no reference counterpart: measurement only) */
+int swps_w2v_gather_stats(swps_w2v *w, uint64_t *out2);
 /* rows of all vocab keys in vid order, host buffer [V][4D] fp64 */
 int swps_w2v_get_params(swps_w2v *w, double *out);
 /* set h,v of all vocab keys (vid order, host [V][2D] fp64), zero h2/v2, refresh the cache */

@@ -291,6 +291,12 @@ class Word2Vec:
         return dict(zip(["batches", "kept", "words", "pairs", "lstate", "fstate", "pulled", "pushed", "ctx_rows",
                          "tgt_rows"], [int(x) for x in o]))
 
+    def gather_stats(self):
+        """Cumulative gather work: gradient records summed and gather items (chunks)."""
+        o = np.zeros(2, dtype=np.uint64)
+        check(capi.lib().swps_w2v_gather_stats(self.h, ptr(o)))
+        return {"records": int(o[0]), "items": int(o[1])}
+
     def get_params(self):
         V = self.info()["vocab"]
         out = np.zeros((V, 4 * self.dim), dtype=np.float64)

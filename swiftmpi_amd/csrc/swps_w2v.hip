@@ -226,12 +226,19 @@ struct RecArgs {
 // line — and writes the position record plus the (local key, record index)
 // gradient records (key U = not in the batch's pulled key set: dropped, as the
 // reference's pull reset drops them).
+// The [RS]-int position records are built in LDS (thread stride RS) and
+// stored by the whole block as one contiguous run: per-thread stores at a
+// 4*RS-byte stride wrote partial cache lines (PMC: 1.25 GB written per batch
+// for 0.28 GB of records and gradient records).
 __global__ __launch_bounds__(256) void k_records(RecArgs a) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  extern __shared__ int32_t srec[];
+  const uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x;
+  const uint64_t p = p0 + threadIdx.x;
+  const int RS = 2 * a.W + a.N + 2;
   int nctx = 0, ntgt = 0;
   if (p < a.P) {
     const uint64_t P = a.P;
-    const int W = a.W, N = a.N, RS = 2 * W + N + 2;
+    const int W = a.W, N = a.N;
     const uint64_t HOFF = P * (uint64_t)(N + 1);
     const uint64_t t = (uint64_t)a.pos_tok[p];
     const int32_t l = a.tok_line[t];
@@ -242,7 +249,7 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
     uint64_t x = lcg_jump(a.lstate, a.ldoff[l] + 1 + rank * (uint64_t)(N + 1), kLcgA, kLcgC);
     x = x * kLcgA + kLcgC;
     const int b = (int)fast_mod(x, (uint64_t)W, a.mW);
-    int32_t *r = a.rec + p * RS;
+    int32_t *r = srec + threadIdx.x * RS;
     r[0] = word;
     for (int j = 0; j < 2 * W; j++) {
       int32_t cv = -1;
@@ -302,6 +309,12 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
       a.pvals[k] = (uint32_t)k;
     }
   }
+  __syncthreads();
+  {
+    const uint32_t n = (uint32_t)min<uint64_t>(blockDim.x, a.P - min(p0, a.P)) * (uint32_t)RS;
+    int32_t *dst = a.rec + p0 * RS;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = srec[i];
+  }
   // rows the forward will read (roofline accounting), one atomic per wave
   unsigned long long c = (unsigned long long)nctx, g = (unsigned long long)ntgt;
 #pragma unroll
@@ -309,7 +322,7 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
     c += __shfl_xor(c, off, 64);
     g += __shfl_xor(g, off, 64);
   }
-  if ((threadIdx.x & 63) == 0 && (c | g)) {
+  if (a.rows_touched && (threadIdx.x & 63) == 0 && (c | g)) {  // profiled passes only
     atomicAdd(&a.rows_touched[0], c);
     atomicAdd(&a.rows_touched[1], g);
   }
@@ -364,6 +377,7 @@ template <typename T, typename A> struct FwdArgs {
   A *neu1, *neu1e;
   float *pg;
   int xcd;  // 1: XCD-contiguous block order (xcd_block)
+  int ld;   // neu1/neu1e row stride in elements (D rounded up to 128 B: whole cache lines per row)
 };
 
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
@@ -484,8 +498,8 @@ __global__ __launch_bounds__(256) void k_forward_b8(FwdArgs<T, A> a) {
   for (int c = 0; c < NCH; c++) {
     const int ci = lane + c * 64;
     if (ci < NC) {
-      CA::st(a.neu1 + (uint64_t)p * D, ci, D, acc[c]);
-      CA::st(a.neu1e + (uint64_t)p * D, ci, D, ne[c]);
+      CA::st(a.neu1 + (uint64_t)p * a.ld, ci, D, acc[c]);
+      CA::st(a.neu1e + (uint64_t)p * a.ld, ci, D, ne[c]);
     }
   }
 }
@@ -578,8 +592,8 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
   for (int c = 0; c < NCH; c++) {
     const int ci = lane + c * 64;
     if (ci < NC) {
-      CA::st(a.neu1 + (uint64_t)p * D, ci, D, acc[c]);
-      CA::st(a.neu1e + (uint64_t)p * D, ci, D, ne[c]);
+      CA::st(a.neu1 + (uint64_t)p * a.ld, ci, D, acc[c]);
+      CA::st(a.neu1e + (uint64_t)p * a.ld, ci, D, ne[c]);
     }
   }
   if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
@@ -703,8 +717,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
     }
   }
-  acc.st(a.neu1 + (uint64_t)p * D, lane, tl);
-  ne.st(a.neu1e + (uint64_t)p * D, lane, tl);
+  acc.st(a.neu1 + (uint64_t)p * a.ld, lane, tl);
+  ne.st(a.neu1e + (uint64_t)p * a.ld, lane, tl);
   if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
 }
 
@@ -723,16 +737,31 @@ __global__ void k_segments(const uint32_t *__restrict__ keys, const uint32_t *__
   if (last) seg[(2 * kind + 1) * U + k] = (uint32_t)(i + 1);
 }
 
-__global__ void k_item_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t *__restrict__ cnt) {
+// In profiled passes (gstats != nullptr) also accumulates the gather's work
+// (records summed, items = chunks) into gstats[0..1] for the roofline
+// accounting: one atomic per wave (same-address atomics: 5 -> 170 us, so
+// never in unprofiled steps).
+__global__ void k_item_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t *__restrict__ cnt,
+                              unsigned long long *__restrict__ gstats) {
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j > 2ull * U) return;
-  if (j == 2ull * U) {
-    cnt[j] = 0;
-    return;
+  unsigned long long rc = 0, ic = 0;
+  if (j == 2ull * U) cnt[j] = 0;
+  if (j < 2ull * U) {
+    const uint32_t u = (uint32_t)(j >> 1), kind = (uint32_t)(j & 1);
+    const uint32_t c = seg[(2 * kind + 1) * U + u] - seg[(2 * kind) * U + u];
+    cnt[j] = (c + CH - 1) / CH;
+    rc = c;
+    ic = (c + CH - 1) / CH;
   }
-  const uint32_t u = (uint32_t)(j >> 1), kind = (uint32_t)(j & 1);
-  const uint32_t c = seg[(2 * kind + 1) * U + u] - seg[(2 * kind) * U + u];
-  cnt[j] = (c + CH - 1) / CH;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    rc += __shfl_xor(rc, off, 64);
+    ic += __shfl_xor(ic, off, 64);
+  }
+  if (gstats && (threadIdx.x & 63) == 0 && rc) {
+    atomicAdd(&gstats[0], rc);
+    atomicAdd(&gstats[1], ic);
+  }
 }
 
 // item descriptors {first record, end record | kind << 31, (key, kind) index j, chunk}:
@@ -766,6 +795,7 @@ template <typename A> struct GatherArgs {
   uint32_t P;
   int D;
   A *partial;
+  int ld;  // neu1/neu1e row stride (FwdArgs::ld)
 };
 
 // One wave per chunk of <= 128 records of one (key, kind): the fp64 sum, in
@@ -818,7 +848,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
         const uint32_t idx = min(r0 + q, n - 1);
         const uint32_t pr = idx < 64 ? __shfl(p0, (int)idx, 64) : __shfl(p1, (int)(idx - 64), 64);
         gg[q] = (double)(idx < 64 ? __shfl(g0, (int)idx, 64) : __shfl(g1, (int)(idx - 64), 64));
-        const A *src = base + (uint64_t)pr * a.D;
+        const A *src = base + (uint64_t)pr * a.ld;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
           const int ci = lane + c * 64;
@@ -922,7 +952,7 @@ __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
                                      : (uint32_t)__builtin_amdgcn_readlane((int)ri.p1, (int)(idx - 64));
         gg[q] = (double)__int_as_float(idx < 64 ? __builtin_amdgcn_readlane(__float_as_int(ri.g0), (int)idx)
                                                 : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
-        rv[q].ld(base + (uint64_t)pr * a.D, lane, tl);
+        rv[q].ld(base + (uint64_t)pr * a.ld, lane, tl);
       }
       if (r0 == 0) rn = item_recs(a, dn, lane);  // next item's record info, behind this item's first rows
 #pragma unroll
@@ -1066,6 +1096,81 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
   }
 }
 
+// k_push (fast mode, fp32 rows and partials, single GPU) on FSlice rows: both
+// halves' first partial and their w / w2 rows are loaded together before any
+// arithmetic (k_push walks chunk x half with a dependent load -> store round
+// trip each, and its second 64-lane chunk keeps 11 lanes busy at D = 300).
+// Same per-element arithmetic and partial order as k_push: bit-identical.
+template <int NCH>
+__global__ __launch_bounds__(256) void k_push_t(PushArgs<float, float> a) {
+  constexpr int PU = 8;
+  const int lane = threadIdx.x & 63;
+  const int D = a.D;
+  const bool tl = 256 * NCH + lane < D;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < a.U; u += (uint64_t)gridDim.x * 4) {
+    const int32_t vid = a.K[u];
+    if (lane == 0) a.local[vid] = -1;
+    const uint32_t s0 = a.seg[0 * a.U + u], s1 = a.seg[1 * a.U + u], s2 = a.seg[2 * a.U + u], s3 = a.seg[3 * a.U + u];
+    const uint32_t cnt[2] = {s1 - s0, s3 - s2};
+    if (cnt[0] == 0 && cnt[1] == 0) continue;
+    float *row = a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
+    uint32_t i0[2], i1[2];
+    FSlice<NCH> wr[2], w2r[2], pf[2];
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      i0[half] = a.ioff[2 * u + half];
+      i1[half] = a.ioff[2 * u + half + 1];
+      if (cnt[half]) {
+        pf[half].ld(a.partial + (uint64_t)i0[half] * D, lane, tl);
+        wr[half].ld(row + half * D, lane, tl);
+        w2r[half].ld(row + (2 + half) * D, lane, tl);
+      }
+    }
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      if (cnt[half] == 0) continue;
+      FAcc<NCH> acc;
+      acc.zero();
+      acc.add(pf[half], tl);
+      const uint32_t stride = (i1[half] - i0[half]) > kGroup ? kGroup : 1;
+      for (uint32_t it0 = i0[half] + stride; it0 < i1[half]; it0 += PU * stride) {
+        FSlice<NCH> pv[PU];
+#pragma unroll
+        for (int q = 0; q < PU; q++)
+          pv[q].ld(a.partial + (uint64_t)min(it0 + q * stride, i1[half] - 1) * D, lane, tl);
+#pragma unroll
+        for (int q = 0; q < PU; q++)
+          if (it0 + q * stride < i1[half]) acc.add(pv[q], tl);
+      }
+      const double inv = (double)cnt[half];
+      float *w = row + half * D, *w2 = row + (2 + half) * D;
+      auto upd = [&](double sum, float wv, float w2v, float &wo, float &w2o) {
+        const double g = (double)(float)(sum / inv);  // the mean in the push payload's type
+        const double acc2 = (double)w2v + g * g;
+        const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
+        w2o = (float)acc2;
+        wo = (float)((double)wv + step);
+      };
+#pragma unroll
+      for (int c = 0; c < NCH; c++) {
+        float4 wo, w2o;
+        upd(acc.v[c][0], wr[half].v[c].x, w2r[half].v[c].x, wo.x, w2o.x);
+        upd(acc.v[c][1], wr[half].v[c].y, w2r[half].v[c].y, wo.y, w2o.y);
+        upd(acc.v[c][2], wr[half].v[c].z, w2r[half].v[c].z, wo.z, w2o.z);
+        upd(acc.v[c][3], wr[half].v[c].w, w2r[half].v[c].w, wo.w, w2o.w);
+        ((float4 *)w2)[lane + c * 64] = w2o;
+        ((float4 *)w)[lane + c * 64] = wo;
+      }
+      if (tl) {
+        float wo, w2o;
+        upd(acc.t, wr[half].t, w2r[half].t, wo, w2o);
+        w2[256 * NCH + lane] = w2o;
+        w[256 * NCH + lane] = wo;
+      }
+    }
+  }
+}
+
 // requester side of a sharded pull: the owners' pull values [U][h|v] (K order)
 // into the worker cache (global_pull_access.h:88-97: params[key] = val)
 template <typename T>
@@ -1104,6 +1209,14 @@ inline unsigned nblk(uint64_t threads, unsigned bs = 256) { return (unsigned)std
 
 // ---- per-kernel HIP-event timing ----------------------------------------
 enum { KT_KEEP = 0, KT_FWD, KT_SORT, KT_GATHER, KT_PUSH, KT_PULL, KT_REC, KT_N };
+
+// neu1/neu1e row stride: D elements rounded up to whole 128-B cache lines, so
+// the forward writes and the gather reads full lines only (1200-B fp32 rows at
+// D = 300 straddled 10-11 lines: PMC showed 28 % extra forward write bytes).
+inline int row_ld(int D, size_t es, bool pad = true) {
+  const int q = pad ? (int)(128 / es) : 1;
+  return (D + q - 1) / q * q;
+}
 
 struct Timer {
   bool on = false;
@@ -1162,6 +1275,8 @@ struct swps_w2v {
   bool f64 = false;
   bool tail = false;  // fast mode: FSlice kernels (D = 256*NCH + tail, 0 < tail <= 64)
   int xcd_order = 1;  // forward blocks in XCD-contiguous order (SWPS_XCD_ORDER=0 turns it off for A/B timing)
+  int push_t = 1;     // fast mode: k_push_t (SWPS_PUSH_T=0: k_push, for A/B timing)
+  bool row_pad = true;  // neu1/neu1e rows padded to 128 B (SWPS_ROW_PAD=0: D-strided, for A/B timing)
   hipStream_t s = nullptr;
   // host corpus / vocab
   std::vector<int32_t> tok;
@@ -1188,7 +1303,7 @@ struct swps_w2v {
       d_local, d_K;
   DevMem d_btok, d_bounds;
   DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_pos_tok, d_rec, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
-      d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_desc, d_tmp, d_trace, d_rows_touched;
+      d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_desc, d_tmp, d_trace, d_rows_touched, d_gstats;
   uint64_t *h_small = nullptr;  // pinned readback
   // RNG (utils/random.h:44-47, seed 2008)
   uint64_t lstate = 2008ULL;
@@ -1610,8 +1725,8 @@ int presize(swps_w2v *w, uint64_t maxP) {
   SWPS_TRY(w->d_pvals.ensure(M * 4));
   SWPS_TRY(w->d_pkeys_s.ensure(M * 4));
   SWPS_TRY(w->d_pvals_s.ensure(M * 4));
-  SWPS_TRY(w->d_neu1.ensure(maxP * D * a));
-  SWPS_TRY(w->d_neu1e.ensure(maxP * D * a));
+  SWPS_TRY(w->d_neu1.ensure(maxP * row_ld(D, a, w->row_pad) * a));
+  SWPS_TRY(w->d_neu1e.ensure(maxP * row_ld(D, a, w->row_pad) * a));
   SWPS_TRY(w->d_pg.ensure(HOFF * 4));
   const uint64_t U = w->max_U;
   if (U) {
@@ -1772,10 +1887,10 @@ int prep_batch(swps_w2v *w) {
                w->cfg.minibatch_vocab ? U : (uint32_t)w->vocab_keys.size(),
                w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(),
                w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
-               w->d_rows_touched.as<unsigned long long>()};
+               tm.on ? w->d_rows_touched.as<unsigned long long>() : nullptr};
     hipEvent_t er = tm.begin(s);
     k_positions<<<nblk(nt), 256, 0, s>>>(w->d_kscan.as<int32_t>(), t0, nt, w->d_pos_tok.as<int32_t>());
-    k_records<<<nblk(P), 256, 0, s>>>(ra);
+    k_records<<<nblk(P), 256, 256 * RS * sizeof(int32_t), s>>>(ra);
     SWPS_HIP(hipGetLastError());
     tm.end(KT_REC, er, s);
     pb.records = true;
@@ -1811,7 +1926,8 @@ int prep_batch(swps_w2v *w) {
       SWPS_HIP(hipGetLastError());
       SWPS_TRY(w->d_icnt.ensure((2ULL * U + 1) * 4));
       SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
-      k_item_counts<<<nblk(2ULL * U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, w->d_icnt.as<uint32_t>());
+      k_item_counts<<<nblk(2ULL * U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, w->d_icnt.as<uint32_t>(),
+                                                    tm.on ? w->d_gstats.as<unsigned long long>() : nullptr);
       SWPS_HIP(hipGetLastError());
       size_t ib = 0;
       SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, ib, w->d_icnt.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
@@ -1869,12 +1985,13 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
   w->st_pulled += U;
   if (pb.records) {
     // ---- forward (learn_instance) ----
-    SWPS_TRY(w->d_neu1.ensure(P * D * sizeof(A)));
-    SWPS_TRY(w->d_neu1e.ensure(P * D * sizeof(A)));
+    const int ld = row_ld(D, sizeof(A), w->row_pad);
+    SWPS_TRY(w->d_neu1.ensure(P * ld * sizeof(A)));
+    SWPS_TRY(w->d_neu1e.ensure(P * ld * sizeof(A)));
     SWPS_TRY(w->d_pg.ensure(pb.HOFF * 4));
     FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
                      w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                     w->d_pg.as<float>(), w->xcd_order};
+                     w->d_pg.as<float>(), w->xcd_order, ld};
     hipEvent_t ef = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
@@ -1902,7 +2019,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_TRY(w->d_partial.ensure(pb.max_items * D * sizeof(A)));
     GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
-                     w->d_partial.as<A>()};
+                     w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad)};
     const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(pb.max_items * 64), 16384);
     hipEvent_t eg = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
@@ -1938,12 +2055,24 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       w->d_partial.as<A>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
                       (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads};
     hipEvent_t ep = tm.begin(s);
+    if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      if (w->tail && !d_grads && w->push_t) {
+        if (D < 512)
+          k_push_t<1><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);
+        else if (D < 768)
+          k_push_t<2><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);
+        else
+          k_push_t<3><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);
+        goto push_done;
+      }
+    }
     switch (w->NCH) {
       case 1: launch_push<1>(pa, s); break;
       case 2: launch_push<2>(pa, s); break;
       case 3: launch_push<3>(pa, s); break;
       default: launch_push<4>(pa, s); break;
     }
+  push_done:
     SWPS_HIP(hipGetLastError());
     tm.end(KT_PUSH, ep, s);
     w->st_pushed += U;
@@ -1976,10 +2105,14 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   w->s = t->stream;
   w->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_XCD_ORDER")) w->xcd_order = atoi(e) != 0;
+  if (const char *e = getenv("SWPS_PUSH_T")) w->push_t = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
   int rc = check_cfg(w);
   if (!rc && hipHostMalloc((void **)&w->h_small, 64) != hipSuccess) rc = fail(SWPS_E_OOM, "pinned alloc");
   if (!rc) rc = w->d_rows_touched.ensure(16);
   if (!rc && hipMemset(w->d_rows_touched.p, 0, 16) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
+  if (!rc) rc = w->d_gstats.ensure(16);
+  if (!rc && hipMemset(w->d_gstats.p, 0, 16) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
   if (!rc) {
     uint64_t A[kMaxJump + 1], C[kMaxJump + 1];
     for (int k = 0; k <= kMaxJump; k++) {
@@ -2155,6 +2288,12 @@ int swps_w2v_stats(swps_w2v *w, uint64_t *o) {
   SWPS_HIP(hipMemcpy(rt, w->d_rows_touched.p, 16, hipMemcpyDeviceToHost));
   o[8] = rt[0];
   o[9] = rt[1];
+  return SWPS_OK;
+}
+
+int swps_w2v_gather_stats(swps_w2v *w, uint64_t *out2) {
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  SWPS_HIP(hipMemcpy(out2, w->d_gstats.p, 16, hipMemcpyDeviceToHost));
   return SWPS_OK;
 }
 
