@@ -1276,6 +1276,8 @@ struct swps_w2v {
   bool tail = false;  // fast mode: FSlice kernels (D = 256*NCH + tail, 0 < tail <= 64)
   int xcd_order = 1;  // forward blocks in XCD-contiguous order (SWPS_XCD_ORDER=0 turns it off for A/B timing)
   int push_t = 1;     // fast mode: k_push_t (SWPS_PUSH_T=0: k_push, for A/B timing)
+  int gather_unr = 8;         // k_gather_t rows in flight per wave (SWPS_GATHER_UNR: 4, 8, 16; A/B timing)
+  uint32_t gather_grid = 65536;  // k_gather_t / k_combine grid cap in blocks (SWPS_GATHER_GRID; A/B: 2048..65536 -> 65536 best)
   bool row_pad = true;  // neu1/neu1e rows padded to 128 B (SWPS_ROW_PAD=0: D-strided, for A/B timing)
   hipStream_t s = nullptr;
   // host corpus / vocab
@@ -2020,12 +2022,18 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
                      w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad)};
-    const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(pb.max_items * 64), 16384);
+    const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(pb.max_items * 64), (uint64_t)w->gather_grid);
     hipEvent_t eg = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
-        if (D < 512)
-          k_gather_t<1, 8><<<ggrid, 256, 0, s>>>(ga);
+        if (D < 512) {
+          if (w->gather_unr == 4)
+            k_gather_t<1, 4><<<ggrid, 256, 0, s>>>(ga);
+          else if (w->gather_unr == 16)
+            k_gather_t<1, 16><<<ggrid, 256, 0, s>>>(ga);
+          else
+            k_gather_t<1, 8><<<ggrid, 256, 0, s>>>(ga);
+        }
         else if (D < 768)
           k_gather_t<2, 8><<<ggrid, 256, 0, s>>>(ga);
         else
@@ -2107,6 +2115,8 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_XCD_ORDER")) w->xcd_order = atoi(e) != 0;
   if (const char *e = getenv("SWPS_PUSH_T")) w->push_t = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_GATHER_UNR")) w->gather_unr = atoi(e);
+  if (const char *e = getenv("SWPS_GATHER_GRID")) w->gather_grid = std::max(64, atoi(e));
   int rc = check_cfg(w);
   if (!rc && hipHostMalloc((void **)&w->h_small, 64) != hipSuccess) rc = fail(SWPS_E_OOM, "pinned alloc");
   if (!rc) rc = w->d_rows_touched.ensure(16);
