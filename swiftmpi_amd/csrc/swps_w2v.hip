@@ -75,6 +75,43 @@ __global__ void k_build_unigram(const uint64_t *__restrict__ starts, uint32_t V,
   }
 }
 
+// Coarse index over the run-length unigram table: idx[b] = the word holding
+// slot b << shift (the same "largest i with starts[i] <= a" as
+// k_build_unigram), b in [0, nb].  A draw then binary-searches starts[] only
+// between idx[b] and idx[b+1] (a few runs at 1024 slots per bucket) — 2.4 MB
+// of L2-resident index instead of one random 4-B read into the 400-MB table.
+__global__ void k_build_uidx(const uint64_t *__restrict__ starts, uint32_t V, int shift, uint64_t nb1,
+                             int32_t *__restrict__ idx) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb1) return;
+  const uint64_t a = b << shift;
+  uint32_t lo = 0, hi = V;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (starts[mid] <= a)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  idx[b] = (int32_t)lo;
+}
+
+constexpr int kUShift = 10;  // unigram coarse index: 1024 slots per bucket
+
+__device__ __forceinline__ int32_t unigram_lookup(const uint64_t *__restrict__ starts, const int32_t *__restrict__ idx,
+                                                  int shift, uint32_t V, uint64_t slot) {
+  const uint64_t b = slot >> shift;
+  uint32_t lo = (uint32_t)idx[b], hi = min((uint32_t)idx[b + 1] + 1u, V);
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (starts[mid] <= slot)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return (int32_t)lo;
+}
+
 // cache <- table rows (h, v) for the listed vids; local[vid] = u when set_local
 template <typename T>
 __global__ __launch_bounds__(256) void k_pull(const int32_t *__restrict__ K, uint32_t U,
@@ -210,6 +247,10 @@ struct RecArgs {
   const uint64_t *bstarts;  // minibatch-vocab mode: run starts of the batch's table [bU+1] (else nullptr)
   const int32_t *buk;       // the batch's vids in std::map key order (the table's word order)
   uint32_t bU;
+  const uint64_t *ustarts;  // run-length unigram table + its coarse index (k_build_uidx), or nullptr: read unigram[]
+  const int32_t *uidx;
+  int ushift;
+  uint32_t uV;
   const uint2 *alias;       // SWPS_SAMPLER_ALIAS: {prob bits, alias} per word of the (batch) vocab, else nullptr
   uint32_t alias_n;
   const int32_t *local;
@@ -291,6 +332,8 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
               hi = mid;
           }
           tv = a.buk[lo];
+        } else if (a.uidx) {
+          tv = unigram_lookup(a.ustarts, a.uidx, a.ushift, a.uV, slot);
         } else {
           tv = a.unigram[slot];
         }
@@ -1278,6 +1321,7 @@ struct swps_w2v {
   int push_t = 1;     // fast mode: k_push_t (SWPS_PUSH_T=0: k_push, for A/B timing)
   int gather_unr = 8;         // k_gather_t rows in flight per wave (SWPS_GATHER_UNR: 4, 8, 16; A/B timing)
   uint32_t gather_grid = 65536;  // k_gather_t / k_combine grid cap in blocks (SWPS_GATHER_GRID; A/B: 2048..65536 -> 65536 best)
+  bool uni_index = true;  // negatives via the coarse-indexed run-length table (SWPS_UNI_INDEX=0: the 1e8-slot table)
   bool row_pad = true;  // neu1/neu1e rows padded to 128 B (SWPS_ROW_PAD=0: D-strided, for A/B timing)
   hipStream_t s = nullptr;
   // host corpus / vocab
@@ -1301,6 +1345,7 @@ struct swps_w2v {
   uint64_t max_tok = 0, max_U = 0, max_lines = 0;
   uint64_t cursor = 0;  // next global batch index
   // device
+  DevMem d_uidx;
   DevMem d_tok, d_tok_line, d_line_off, d_ran, d_exptab, d_unigram, d_starts, d_vid_row, d_cache_h, d_cache_v,
       d_local, d_K;
   DevMem d_btok, d_bounds;
@@ -1656,6 +1701,11 @@ int upload_corpus(swps_w2v *w) {
     k_build_unigram<<<4096, 256, 0, s>>>(w->d_starts.as<uint64_t>(), (uint32_t)V, w->cfg.unigram_size,
                                          w->d_unigram.as<int32_t>());
     SWPS_HIP(hipGetLastError());
+    const uint64_t nb1 = ((w->cfg.unigram_size - 1) >> kUShift) + 2;
+    SWPS_TRY(w->d_uidx.ensure(nb1 * 4));
+    k_build_uidx<<<nblk(nb1), 256, 0, s>>>(w->d_starts.as<uint64_t>(), (uint32_t)V, kUShift, nb1,
+                                           w->d_uidx.as<int32_t>());
+    SWPS_HIP(hipGetLastError());
   }
   const size_t es = w->f64 ? 8 : 4;
   SWPS_TRY(w->d_cache_h.ensure(V * w->D * es));
@@ -1877,12 +1927,16 @@ int prep_batch(swps_w2v *w) {
     SWPS_TRY(w->d_pkeys_s.ensure(M * 4));
     SWPS_TRY(w->d_pvals_s.ensure(M * 4));
     if (tracing) SWPS_TRY(w->d_trace.ensure(std::max<uint64_t>(1, P * N) * 4));
+    const bool use_uidx = !w->cfg.minibatch_vocab && w->cfg.sampler != SWPS_SAMPLER_ALIAS && w->uni_index &&
+                          w->d_uidx.p != nullptr;
     RecArgs ra{w->d_tok.as<int32_t>(), w->d_tok_line.as<int32_t>(), w->d_line_off.as<int64_t>(),
                w->d_pos_tok.as<int32_t>(), (uint32_t)P, w->d_kscan.as<int32_t>(), w->d_ldoff.as<uint64_t>(),
                w->lstate_epoch, W, N, ~0ULL / (uint64_t)W, w->d_unigram.as<int32_t>(), w->cfg.unigram_size,
                ~0ULL / w->cfg.unigram_size,
                w->cfg.minibatch_vocab ? w->d_bstarts.as<uint64_t>() + B.sofs : nullptr,
                w->cfg.minibatch_vocab ? w->d_UK.as<int32_t>() + B.kofs : nullptr, U,
+               use_uidx ? w->d_starts.as<uint64_t>() : nullptr, use_uidx ? w->d_uidx.as<int32_t>() : nullptr,
+               kUShift, (uint32_t)w->vocab_keys.size(),
                w->cfg.sampler == SWPS_SAMPLER_ALIAS
                    ? w->d_alias.as<uint2>() + (w->cfg.minibatch_vocab ? B.kofs : 0)
                    : nullptr,
@@ -2115,6 +2169,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_XCD_ORDER")) w->xcd_order = atoi(e) != 0;
   if (const char *e = getenv("SWPS_PUSH_T")) w->push_t = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_UNI_INDEX")) w->uni_index = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_GATHER_UNR")) w->gather_unr = atoi(e);
   if (const char *e = getenv("SWPS_GATHER_GRID")) w->gather_grid = std::max(64, atoi(e));
   int rc = check_cfg(w);
