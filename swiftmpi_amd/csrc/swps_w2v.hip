@@ -1382,6 +1382,18 @@ struct swps_w2v {
     uint64_t bi = 0, P = 0, nt = 0, HOFF = 0, M = 0, max_items = 0;
     uint32_t U = 0;
   } pb;
+  // overlapped single-GPU driver (train_overlapped): the second set of the
+  // parameter-independent per-batch buffers, swapped with the members above,
+  // and the stream prep(i+1) runs on while learn(i) runs on s
+  static constexpr int kPrepBufs = 12;
+  DevMem alt[kPrepBufs];
+  bool alt_local_ready = false;
+  int overlap = 0;  // SWPS_OVERLAP=1: train_overlapped (same-box A/B: 4.25e8 sequential vs 4.24e8 / 4.02e8
+                    // overlapped — forward and gather already fill every CU and the HBM, so prep only stretches)
+  hipStream_t s_prep = nullptr;
+  hipEvent_t ev_learn = nullptr, ev_prep = nullptr;
+  DevMem *prep_set[kPrepBufs] = {&d_pos_tok, &d_rec, &d_pkeys, &d_pvals, &d_pkeys_s, &d_pvals_s,
+                                 &d_tmp,     &d_seg, &d_icnt,  &d_ioff,  &d_desc,    &d_local};
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
   // negative trace
@@ -2150,6 +2162,67 @@ template <typename T, typename A> int run_batch(swps_w2v *w, const void *d_vals 
 
 }  // namespace
 
+void swap_prep_set(swps_w2v *w) {
+  for (int k = 0; k < swps_w2v::kPrepBufs; k++) {
+    std::swap(w->prep_set[k]->p, w->alt[k].p);
+    std::swap(w->prep_set[k]->bytes, w->alt[k].bytes);
+  }
+}
+
+// Single-GPU minibatch loop with prep(i+1) (epoch plan, local key map,
+// records, radix sort, chunk index — parameter-independent, SURVEY.md §3.2's
+// draws) on s_prep into the second buffer set while learn(i) (pull, forward,
+// gather, push) runs on s.  prep(i+1) waits for learn(i-1), the last user of
+// that set (its push also clears that set's local-key map); learn(i+1) waits
+// for prep(i+1).  Every kernel sees the same inputs as in the sequential
+// loop, so results are bit-identical (tests: SWPS_OVERLAP=0 vs 1).  Nothing
+// is left prepared when the call returns.
+template <typename T, typename A> int train_overlapped(swps_w2v *w, uint64_t count) {
+  if (!w->s_prep) {
+    SWPS_HIP(hipStreamCreateWithFlags(&w->s_prep, hipStreamNonBlocking));
+    SWPS_HIP(hipEventCreateWithFlags(&w->ev_learn, hipEventDisableTiming));
+    SWPS_HIP(hipEventCreateWithFlags(&w->ev_prep, hipEventDisableTiming));
+  }
+  const uint64_t V = w->vocab_keys.size();
+  if (!w->alt_local_ready) {
+    DevMem &al = w->alt[swps_w2v::kPrepBufs - 1];
+    SWPS_TRY(al.ensure(V * 4));
+    SWPS_HIP(hipMemsetAsync(al.p, 0xFF, V * 4, w->s));
+    w->alt_local_ready = true;
+  }
+  const hipStream_t s = w->s;
+  bool prep_pending = false;  // batch i's prep ran on s_prep (ev_prep)
+  for (uint64_t i = 0; i < count; i++) {
+    if (!w->pb.valid) SWPS_TRY(prep_batch(w));  // inline on s (first batch of the call)
+    const swps_w2v::Prepped cur = w->pb;
+    swps_w2v::Prepped next;
+    if (i + 1 < count) {
+      SWPS_HIP(hipEventRecord(w->ev_learn, s));  // learn(i-1) done -> the other set is free
+      SWPS_HIP(hipStreamWaitEvent(w->s_prep, w->ev_learn, 0));
+      swap_prep_set(w);
+      w->s = w->s_prep;
+      w->cursor++;
+      w->pb = swps_w2v::Prepped();
+      const int rc = prep_batch(w);
+      next = w->pb;
+      w->cursor--;
+      w->s = s;
+      swap_prep_set(w);
+      SWPS_TRY(rc);
+    }
+    if (prep_pending) SWPS_HIP(hipStreamWaitEvent(s, w->ev_prep, 0));
+    if (i + 1 < count) SWPS_HIP(hipEventRecord(w->ev_prep, w->s_prep));
+    prep_pending = i + 1 < count;
+    w->pb = cur;
+    SWPS_TRY((learn_batch<T, A>(w)));
+    if (prep_pending) {
+      swap_prep_set(w);
+      w->pb = next;
+    }
+  }
+  return SWPS_OK;
+}
+
 extern "C" {
 
 int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
@@ -2170,6 +2243,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_PUSH_T")) w->push_t = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_UNI_INDEX")) w->uni_index = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_OVERLAP")) w->overlap = atoi(e);  // A/B timing
   if (const char *e = getenv("SWPS_GATHER_UNR")) w->gather_unr = atoi(e);
   if (const char *e = getenv("SWPS_GATHER_GRID")) w->gather_grid = std::max(64, atoi(e));
   int rc = check_cfg(w);
@@ -2201,6 +2275,12 @@ int swps_w2v_destroy(swps_w2v *w) {
   if (!w) return SWPS_OK;
   (void)hipSetDevice(w->t->cfg.device);
   (void)hipStreamSynchronize(w->s);
+  if (w->s_prep) {
+    (void)hipStreamSynchronize(w->s_prep);
+    (void)hipStreamDestroy(w->s_prep);
+  }
+  if (w->ev_learn) (void)hipEventDestroy(w->ev_learn);
+  if (w->ev_prep) (void)hipEventDestroy(w->ev_prep);
   if (w->h_small) (void)hipHostFree(w->h_small);
   delete w;
   (void)hipGetLastError();  // leave no sticky error from the calls above
@@ -2314,6 +2394,11 @@ int swps_w2v_init(swps_w2v *w) {
 int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
   if (!w->inited) return fail(SWPS_E_STATE, "call swps_w2v_init first");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  if (w->overlap && count > 1 && !w->cfg.minibatch_vocab && w->trace.size() >= w->trace_cap && !w->pb.valid) {
+    if (w->f64) return train_overlapped<double, double>(w, count);
+    if (w->cfg.fp64_intermediates) return train_overlapped<float, double>(w, count);
+    return train_overlapped<float, float>(w, count);
+  }
   for (uint64_t i = 0; i < count; i++) {
     if (w->f64)
       SWPS_TRY((run_batch<double, double>(w)));

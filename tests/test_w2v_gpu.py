@@ -389,3 +389,35 @@ def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch):
         assert np.array_equal(outs[0], outs[k]), k
         assert np.array_equal(negs[0], negs[k]), k
     assert len(negs[0]) > 1000
+
+
+@pytest.mark.parametrize("dtype,fp64i", [("f32", False), ("f32", True), ("f64", True)])
+def test_overlapped_driver_bit_identical(lib, gpu, monkeypatch, dtype, fp64i):
+    """prep(i+1) on a second stream into a second buffer set while learn(i)
+    runs (SWPS_OVERLAP=1, opt-in) == the sequential loop, bit for bit,
+    across epoch boundaries and uneven train_batches chunks; RNG states and
+    counters equal too."""
+    rng = np.random.default_rng(5)
+    V, lines, L = 2000, 90, 300
+    p = 1.0 / np.arange(1, V + 1)
+    p /= p.sum()
+    ids = np.minimum(np.searchsorted(np.cumsum(p), rng.random(lines * L)), V - 1).astype(np.uint32)
+    off = np.arange(0, lines * L + 1, L, dtype=np.uint64)
+    keys = np.array([lib.bkdr("w%d" % i) for i in range(V)], dtype=np.uint64)
+    res = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("SWPS_OVERLAP", ov)
+        t = lib.Table("w2v", dim=64 if dtype == "f64" else 300, capacity=V, dtype=dtype, learning_rate=0.7)
+        w = lib.Word2Vec(t, window=5, negative=5, minibatch=20, sample=1e-3, unigram_size=10 ** 6,
+                         fp64_intermediates=fp64i)
+        w.load_tokens(ids, off, keys)
+        w.init()
+        nb = w.info()["batches"]
+        for chunk in (1, 3, nb, 2 * nb + 1, 2):
+            w.train_batches(chunk)
+        w.sync()
+        st = w.stats()
+        res.append((w.get_params(), {k: st[k] for k in ("batches", "kept", "words", "lstate", "fstate",
+                                                        "pulled", "pushed")}))
+    assert res[0][1] == res[1][1]
+    assert np.array_equal(res[0][0], res[1][0])
