@@ -41,27 +41,62 @@ def word_keys(lib, vocab):
     return np.array([lib.bkdr("w%d" % i) for i in range(vocab)], dtype=np.uint64)
 
 
+_W2V_CPU_WORKER = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+import oracle
+path, dim, window, negative, minibatch, sample, alpha, lr = sys.argv[2:10]
+m = oracle.W2V(path, int(dim), window=int(window), negative=int(negative), minibatch=int(minibatch),
+               sample=float(sample), alpha=float(alpha), lr=float(lr), table_size=int(1e8))
+m.init_rand(1, 2)
+t0 = time.perf_counter()
+m.train(1)
+dt = time.perf_counter() - t0
+print(json.dumps({"words": m.stats()["actual_train_words"], "dt": dt}))
+"""
+
+
 def cpu_baseline(ids, off, keys, args, lines):
-    """The oracle (single-threaded C++ port of the reference algorithm, fp64
-    like the reference) on the first `lines` lines of the same corpus."""
+    """The oracle (C++ port of the reference algorithm, fp64 like the
+    reference, nthreads = 1 semantics) as `--cpu-procs` independent processes,
+    one per host core, each on its own `lines`-line slice of the same corpus:
+    the reference's MPI ranks each train their own file (apps/word2vec/
+    README.md:37-46); the ranks' ZeroMQ parameter exchange is left out, so
+    this is an upper bound on the reference's multi-core throughput.  Started
+    as child processes (fresh interpreters), never forked from this GPU
+    process."""
+    import subprocess
     import oracle
     oracle.build()
+    procs = max(1, args.cpu_procs)
+    nl = len(off) - 1
+    per = max(1, min(lines, nl // procs))
     with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "sample.txt")
-        with open(path, "w") as f:
-            for l in range(lines):
-                a, b = int(off[l]), int(off[l + 1])
-                f.write(" ".join("w%d" % x for x in ids[a:b]) + "\n")
-        m = oracle.W2V(path, args.dim, window=args.window, negative=args.negative, minibatch=args.minibatch,
-                       sample=args.sample, alpha=args.alpha, lr=args.lr, table_size=int(1e8))
-        m.init_rand(1, 2)
+        runs = []
+        for r in range(procs):
+            path = os.path.join(d, "sample%d.txt" % r)
+            with open(path, "w") as f:
+                for l in range(r * per, (r + 1) * per):
+                    a, b = int(off[l]), int(off[l + 1])
+                    f.write(" ".join("w%d" % x for x in ids[a:b]) + "\n")
+            runs.append(path)
+        env = dict(os.environ, OMP_NUM_THREADS="1")
         t0 = time.perf_counter()
-        m.train(1)
-        dt = time.perf_counter() - t0
-        words = m.stats()["actual_train_words"]
-    return {"value": words / dt, "unit": "words/s", "cores": 1, "kind": "port",
-            "sample": "oracle/swps_oracle.cpp (fp64, nthreads=1 semantics) on the first %d lines (%d words) of "
-                      "the same corpus, 1 epoch, D=%d; %.1f s" % (lines, words, args.dim, dt)}
+        ps = [subprocess.Popen([sys.executable, "-c", _W2V_CPU_WORKER, ROOT, path, str(args.dim), str(args.window),
+                                str(args.negative), str(args.minibatch), str(args.sample), str(args.alpha),
+                                str(args.lr)], stdout=subprocess.PIPE, env=env) for path in runs]
+        res = [json.loads(p.communicate()[0].decode().strip().splitlines()[-1]) for p in ps]
+        wall = time.perf_counter() - t0
+        if any(p.returncode for p in ps):
+            raise RuntimeError("cpu baseline worker failed")
+    words = sum(r["words"] for r in res)
+    slowest = max(r["dt"] for r in res)
+    return {"value": words / slowest, "unit": "words/s", "cores": procs, "kind": "port",
+            "sample": "oracle/swps_oracle.cpp (fp64, nthreads=1 semantics) as %d concurrent processes, each on its "
+                      "own %d-line slice (%d words in all) of the same corpus, 1 epoch, D=%d, no parameter "
+                      "exchange between them; slowest process %.1f s (wall %.1f s incl. setup); single-process "
+                      "rate %.3g words/s" % (procs, per, words, args.dim, slowest, wall,
+                                               res[0]["words"] / res[0]["dt"])}
 
 
 def cpu_baseline_lr(y, off, f, v, minibatch, lr, rows):
@@ -124,6 +159,8 @@ def cpu_baseline_s2v(toks, off, args, docs):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--cpu-procs", type=int, default=8,
+                    help="concurrent single-threaded oracle processes for the w2v cpu_baseline (host cores used)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dim", type=int, default=300)
