@@ -117,7 +117,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_pull(const int32_t *__restrict__ K, uint32_t U,
                                               const uint32_t *__restrict__ vid_row, const T *__restrict__ rows,
                                               int D, T *__restrict__ cache_h, T *__restrict__ cache_v,
-                                              int32_t *__restrict__ local, int set_local) {
+                                              int32_t *__restrict__ local, int set_local, int cs) {
   using V = typename V16<T>::V;
   constexpr int E = V16<T>::E;
   const int lane = threadIdx.x & 63;
@@ -125,8 +125,8 @@ __global__ __launch_bounds__(256) void k_pull(const int32_t *__restrict__ K, uin
   for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += (uint64_t)gridDim.x * 4) {
     const int32_t vid = K ? K[u] : (int32_t)u;
     const V *src = (const V *)(rows + (uint64_t)vid_row[vid] * 4 * D);
-    V *dh = (V *)(cache_h + (uint64_t)vid * D);
-    V *dv = (V *)(cache_v + (uint64_t)vid * D);
+    V *dh = (V *)(cache_h + (uint64_t)vid * cs);  // cs: the cache row stride (swps_w2v::cs)
+    V *dv = (V *)(cache_v + (uint64_t)vid * cs);
     for (int c = lane; c < NC; c += 64) {
       dh[c] = src[c];
       dv[c] = src[NC + c];
@@ -421,6 +421,7 @@ template <typename T, typename A> struct FwdArgs {
   float *pg;
   int xcd;  // 1: XCD-contiguous block order (xcd_block)
   int ld;   // neu1/neu1e row stride in elements (D rounded up to 128 B: whole cache lines per row)
+  int cs;   // worker-cache row stride in elements (the same rounding)
 };
 
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(256) void k_forward_b8(FwdArgs<T, A> a) {
       const int slot = s0 + q;
       vid[q] = slot < S ? r[1 + slot] : -1;
       if (vid[q] >= 0) {
-        const T *src = (slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * D;
+        const T *src = (slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * a.cs;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
           const int ci = lane + c * 64;
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
       const int slot = s0 + q;
       vid[q] = slot < S ? r[1 + slot] : -1;
       if (vid[q] >= 0) {
-        const T *src = (slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * D;
+        const T *src = (slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * a.cs;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
           const int ci = lane + c * 64;
@@ -734,7 +735,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (int q = 0; q < G; q++) {
       const int slot = s0 + q;
       vid[q] = __builtin_amdgcn_readfirstlane(slot < S ? r[1 + slot] : -1);
-      if (vid[q] >= 0) rows[q].ld((slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * D, lane, tl);
+      if (vid[q] >= 0) rows[q].ld((slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * a.cs, lane, tl);
     }
 #pragma unroll
     for (int q = 0; q < G; q++) {
@@ -1219,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_push_t(PushArgs<float, float> a) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_install(const int32_t *__restrict__ K, uint32_t U, const T *__restrict__ vals,
                                                  int D, T *__restrict__ cache_h, T *__restrict__ cache_v,
-                                                 int32_t *__restrict__ local, int set_local) {
+                                                 int32_t *__restrict__ local, int set_local, int cs) {
   using V = typename V16<T>::V;
   constexpr int E = V16<T>::E;
   const int lane = threadIdx.x & 63;
@@ -1227,8 +1228,8 @@ __global__ __launch_bounds__(256) void k_install(const int32_t *__restrict__ K, 
   for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += (uint64_t)gridDim.x * 4) {
     const int32_t vid = K[u];
     const V *src = (const V *)(vals + u * 2 * D);
-    V *dh = (V *)(cache_h + (uint64_t)vid * D);
-    V *dv = (V *)(cache_v + (uint64_t)vid * D);
+    V *dh = (V *)(cache_h + (uint64_t)vid * cs);  // cs: the cache row stride (swps_w2v::cs)
+    V *dv = (V *)(cache_v + (uint64_t)vid * cs);
     for (int c = lane; c < NC; c += 64) {
       dh[c] = src[c];
       dv[c] = src[NC + c];
@@ -1321,6 +1322,8 @@ struct swps_w2v {
   int push_t = 1;     // fast mode: k_push_t (SWPS_PUSH_T=0: k_push, for A/B timing)
   int gather_unr = 8;         // k_gather_t rows in flight per wave (SWPS_GATHER_UNR: 4, 8, 16; A/B timing)
   uint32_t gather_grid = 65536;  // k_gather_t / k_combine grid cap in blocks (SWPS_GATHER_GRID; A/B: 2048..65536 -> 65536 best)
+  bool cache_pad = true;  // worker-cache rows padded to 128 B (SWPS_CACHE_PAD=0: D-strided, for A/B timing)
+  int cs = 0;              // worker-cache row stride in elements (set with the cache allocation)
   bool uni_index = true;  // negatives via the coarse-indexed run-length table (SWPS_UNI_INDEX=0: the 1e8-slot table)
   bool row_pad = true;  // neu1/neu1e rows padded to 128 B (SWPS_ROW_PAD=0: D-strided, for A/B timing)
   hipStream_t s = nullptr;
@@ -1720,8 +1723,9 @@ int upload_corpus(swps_w2v *w) {
     SWPS_HIP(hipGetLastError());
   }
   const size_t es = w->f64 ? 8 : 4;
-  SWPS_TRY(w->d_cache_h.ensure(V * w->D * es));
-  SWPS_TRY(w->d_cache_v.ensure(V * w->D * es));
+  w->cs = row_ld(w->D, es, w->cache_pad);
+  SWPS_TRY(w->d_cache_h.ensure(V * w->cs * es));
+  SWPS_TRY(w->d_cache_v.ensure(V * w->cs * es));
   SWPS_TRY(w->d_local.ensure(V * 4));
   SWPS_HIP(hipMemsetAsync(w->d_local.p, 0xFF, V * 4, s));
   SWPS_TRY(w->d_vid_row.ensure(V * 4));
@@ -1733,7 +1737,7 @@ template <typename T> int pull_all(swps_w2v *w) {
   const uint64_t V = w->vocab_keys.size();
   k_pull<T><<<nblk(V * 64), 256, 0, w->s>>>(nullptr, (uint32_t)V, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(),
                                             w->D, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(), w->d_local.as<int32_t>(),
-                                            0);
+                                            0, w->cs);
   SWPS_HIP(hipGetLastError());
   SWPS_HIP(hipStreamSynchronize(w->s));
   return SWPS_OK;
@@ -2039,11 +2043,11 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     hipEvent_t e = tm.begin(s);
     if (d_vals)  // sharded: values pulled from the owners
       k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
-                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0);
+                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0, w->cs);
     else
       k_pull<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(), D,
                                                        w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
-                                                       w->d_local.as<int32_t>(), 0);
+                                                       w->d_local.as<int32_t>(), 0, w->cs);
     SWPS_HIP(hipGetLastError());
     tm.end(KT_PULL, e, s);
   }
@@ -2059,7 +2063,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_TRY(w->d_pg.ensure(pb.HOFF * 4));
     FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
                      w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                     w->d_pg.as<float>(), w->xcd_order, ld};
+                     w->d_pg.as<float>(), w->xcd_order, ld, w->cs};
     hipEvent_t ef = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
@@ -2243,6 +2247,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_PUSH_T")) w->push_t = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_UNI_INDEX")) w->uni_index = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_CACHE_PAD")) w->cache_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_OVERLAP")) w->overlap = atoi(e);  // A/B timing
   if (const char *e = getenv("SWPS_GATHER_UNR")) w->gather_unr = atoi(e);
   if (const char *e = getenv("SWPS_GATHER_GRID")) w->gather_grid = std::max(64, atoi(e));
@@ -2646,11 +2651,11 @@ int swps_w2v_install_init(swps_w2v *w, const void *d_vals) {
   if (w->f64)
     k_install<double><<<nblk(V * 64), 256, 0, w->s>>>(w->d_init_order.as<int32_t>(), (uint32_t)V,
                                                       (const double *)d_vals, w->D, w->d_cache_h.as<double>(),
-                                                      w->d_cache_v.as<double>(), w->d_local.as<int32_t>(), 0);
+                                                      w->d_cache_v.as<double>(), w->d_local.as<int32_t>(), 0, w->cs);
   else
     k_install<float><<<nblk(V * 64), 256, 0, w->s>>>(w->d_init_order.as<int32_t>(), (uint32_t)V,
                                                      (const float *)d_vals, w->D, w->d_cache_h.as<float>(),
-                                                     w->d_cache_v.as<float>(), w->d_local.as<int32_t>(), 0);
+                                                     w->d_cache_v.as<float>(), w->d_local.as<int32_t>(), 0, w->cs);
   SWPS_HIP(hipGetLastError());
   w->inited = true;
   return SWPS_OK;
@@ -2752,7 +2757,8 @@ int swps_w2v_save_state(swps_w2v *w, const char *path) {
   SWPS_TRY(f.put(head, sizeof(head)));
   SWPS_TRY(f.put(st, sizeof(st)));
   for (DevMem *m : {&w->d_cache_h, &w->d_cache_v}) {
-    if (!cache.empty()) SWPS_HIP(hipMemcpy(cache.data(), m->p, cache.size(), hipMemcpyDeviceToHost));
+    if (!cache.empty())  // unpadded [V][D] in the file whatever the device row stride
+      SWPS_HIP(hipMemcpy2D(cache.data(), w->D * es, m->p, (size_t)w->cs * es, w->D * es, V, hipMemcpyDeviceToHost));
     SWPS_TRY(f.put(cache.data(), cache.size()));
   }
   return f.finish_write();
@@ -2789,8 +2795,10 @@ int swps_w2v_restore_state(swps_w2v *w, const char *path) {
       return fail(SWPS_E_STATE, "the table lacks the worker's vocab rows: swps_restore its table snapshot first");
   }
   if (!ch.empty()) {
-    SWPS_HIP(hipMemcpy(w->d_cache_h.p, ch.data(), ch.size(), hipMemcpyHostToDevice));
-    SWPS_HIP(hipMemcpy(w->d_cache_v.p, cv.data(), cv.size(), hipMemcpyHostToDevice));
+    SWPS_HIP(hipMemcpy2D(w->d_cache_h.p, (size_t)w->cs * es, ch.data(), w->D * es, w->D * es, V,
+                         hipMemcpyHostToDevice));
+    SWPS_HIP(hipMemcpy2D(w->d_cache_v.p, (size_t)w->cs * es, cv.data(), w->D * es, w->D * es, V,
+                         hipMemcpyHostToDevice));
   }
   SWPS_HIP(hipMemcpy(w->d_rows_touched.p, st + 9, 16, hipMemcpyHostToDevice));
   w->cursor = st[0];
