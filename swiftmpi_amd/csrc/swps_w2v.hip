@@ -127,9 +127,10 @@ __global__ __launch_bounds__(256) void k_pull(const int32_t *__restrict__ K, uin
     const V *src = (const V *)(rows + (uint64_t)vid_row[vid] * 4 * D);
     V *dh = (V *)(cache_h + (uint64_t)vid * cs);  // cs: the cache row stride (swps_w2v::cs)
     V *dv = (V *)(cache_v + (uint64_t)vid * cs);
-    for (int c = lane; c < NC; c += 64) {
-      dh[c] = src[c];
-      dv[c] = src[NC + c];
+    for (int c = lane; c < cs / E; c += 64) {  // the pad too (zeros): whole-line stores
+      const bool in = c < NC;
+      dh[c] = in ? src[c] : V{};
+      dv[c] = in ? src[NC + c] : V{};
     }
     if (set_local && lane == 0) local[vid] = (int32_t)u;
   }
@@ -1019,6 +1020,9 @@ __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
 }
 
 constexpr uint32_t kGroup = 16;  // hot keys: partials are pre-summed in groups of 16
+// k_combine walks every item to find the few hot-group leaders: a small grid
+// with a stride loop beats dispatching one wave per item
+constexpr unsigned kCombineGrid = 1024;
 
 // Hot (key, kind) runs with more than kGroup chunks: each group leader sums
 // its group's partials in chunk order into its own slot (second level).
@@ -1230,9 +1234,10 @@ __global__ __launch_bounds__(256) void k_install(const int32_t *__restrict__ K, 
     const V *src = (const V *)(vals + u * 2 * D);
     V *dh = (V *)(cache_h + (uint64_t)vid * cs);  // cs: the cache row stride (swps_w2v::cs)
     V *dv = (V *)(cache_v + (uint64_t)vid * cs);
-    for (int c = lane; c < NC; c += 64) {
-      dh[c] = src[c];
-      dv[c] = src[NC + c];
+    for (int c = lane; c < cs / E; c += 64) {  // the pad too (zeros): whole-line stores
+      const bool in = c < NC;
+      dh[c] = in ? src[c] : V{};
+      dv[c] = in ? src[NC + c] : V{};
     }
     if (set_local && lane == 0) local[vid] = (int32_t)u;
   }
@@ -1765,7 +1770,7 @@ template <int NCH, typename T, typename A> void launch_forward(const FwdArgs<T, 
 template <int NCH, typename T, typename A> void launch_gather(const GatherArgs<A> &a, unsigned grid, hipStream_t s) {
   constexpr int UNR = sizeof(A) * V16<T>::E > 16 ? 4 : 8;
   k_gather<T, A, NCH, UNR><<<grid, 256, 0, s>>>(a);
-  k_combine<T, A, NCH><<<grid, 256, 0, s>>>(a);
+  k_combine<T, A, NCH><<<std::min(grid, kCombineGrid), 256, 0, s>>>(a);
 }
 template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A> &a, hipStream_t s) {
   if (a.grads)
@@ -2109,9 +2114,9 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
         else
           k_gather_t<3, 8><<<ggrid, 256, 0, s>>>(ga);
         switch (w->NCH) {  // second level over the partials: layout-independent
-          case 2: k_combine<T, A, 2><<<ggrid, 256, 0, s>>>(ga); break;
-          case 3: k_combine<T, A, 3><<<ggrid, 256, 0, s>>>(ga); break;
-          default: k_combine<T, A, 4><<<ggrid, 256, 0, s>>>(ga); break;
+          case 2: k_combine<T, A, 2><<<std::min(ggrid, kCombineGrid), 256, 0, s>>>(ga); break;
+          case 3: k_combine<T, A, 3><<<std::min(ggrid, kCombineGrid), 256, 0, s>>>(ga); break;
+          default: k_combine<T, A, 4><<<std::min(ggrid, kCombineGrid), 256, 0, s>>>(ga); break;
         }
         goto gather_done;
       }
