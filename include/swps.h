@@ -50,9 +50,15 @@ int swps_version(void);
 /* ---- parameter table (server shard in HBM) ------------------------------ */
 /* Layouts: one row per key.
  *   SWPS_LAYOUT_W2V : [h(D) | v(D) | h2sum(D) | v2sum(D)]   (WParam, word2vec_global.h:34-48)
- *     pull value  = [h(D) | v(D)]                           (WLocalParam)
- *     push value  = [mean h_grad(D) | mean v_grad(D)] fp64  (WLocalGrad wire, :122-134)
+ *     pull value  = [h(D) | v(D)]                           (WLocalParam's values)
+ *     push value  = [mean h_grad(D) | mean v_grad(D)] fp64  (WLocalGrad's mean, :122-134)
  *     push rule   = AdaGrad ascent                          (:176-185)
+ *   Value BLOCKS, not the reference's byte stream: its BinaryBuffer wire
+ *   interleaves h[i], v[i] per element (word2vec_global.h:129-132, 144-147)
+ *   after each key.  The element type matches the wire's (fp64); a bridge to
+ *   reference peers must (de)interleave — swiftmpi_compat.h's WLocalParam /
+ *   WLocalGrad do, see INTEGRATION.md. */
+/*
  *   SWPS_LAYOUT_LR  : [w | grad2sum]                         (LRParam, lr.cpp:7-10)
  *     pull value  = [w]; push value = [mean grad] fp32;  AdaGrad (lr.cpp:68-75)
  */

@@ -1,5 +1,8 @@
 // Host-side utilities of libswps: error state, BKDR key hashing, glibc rand()
 // emulation, the hash-frag node map and the reference config file format.
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <fstream>
 
@@ -123,11 +126,22 @@ uint64_t checksum64(uint64_t h, const void *p, size_t n) {
   return (h ^ (uint64_t)n) * 0xff51afd7ed558ccdULL;
 }
 
+// Writes go to <path>.tmp; finish_write flushes and fsyncs it, renames it
+// over <path> and fsyncs the directory, so a crash at any point leaves either
+// the previous snapshot or the new one, never a torn file (an unfinished
+// writer removes its temporary).
 int SnapFile::open(const std::string &p, bool write) {
   path = p;
-  f = fopen(p.c_str(), write ? "wb" : "rb");
-  if (!f) return fail(SWPS_E_IO, std::string(write ? "cannot write " : "cannot open ") + p);
+  writing = write;
+  tmp = write ? p + ".tmp" : p;
+  f = fopen(tmp.c_str(), write ? "wb" : "rb");
+  if (!f) return fail(SWPS_E_IO, std::string(write ? "cannot write " : "cannot open ") + tmp);
   return SWPS_OK;
+}
+
+SnapFile::~SnapFile() {
+  if (f) fclose(f);
+  if (writing && !committed) (void)std::remove(tmp.c_str());
 }
 
 int SnapFile::put(const void *p, size_t n) {
@@ -144,10 +158,20 @@ int SnapFile::get(void *p, size_t n) {
 
 int SnapFile::finish_write() {
   const uint64_t s = sum;
-  if (fwrite(&s, 1, 8, f) != 8) return fail(SWPS_E_IO, "short write to " + path);
+  if (fwrite(&s, 1, 8, f) != 8) return fail(SWPS_E_IO, "short write to " + tmp);
+  if (fflush(f) != 0 || fsync(fileno(f)) != 0) return fail(SWPS_E_IO, "cannot flush " + tmp);
   const int bad = fclose(f);
   f = nullptr;
-  if (bad) return fail(SWPS_E_IO, "cannot close " + path);
+  if (bad) return fail(SWPS_E_IO, "cannot close " + tmp);
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) return fail(SWPS_E_IO, "cannot rename " + tmp + " to " + path);
+  committed = true;
+  const size_t slash = path.find_last_of('/');
+  const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : path.substr(0, slash));
+  const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+  if (dfd >= 0) {  // make the rename itself durable
+    (void)fsync(dfd);
+    ::close(dfd);
+  }
   return SWPS_OK;
 }
 

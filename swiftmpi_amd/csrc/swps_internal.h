@@ -122,17 +122,16 @@ uint64_t checksum64(uint64_t h, const void *p, size_t n);
 struct SnapFile {
   FILE *f = nullptr;
   uint64_t sum = 0x5357505353554dULL;
-  std::string path;
+  std::string path, tmp;
+  bool writing = false, committed = false;
   SnapFile() = default;
   SnapFile(const SnapFile &) = delete;
   SnapFile &operator=(const SnapFile &) = delete;
-  ~SnapFile() {
-    if (f) fclose(f);
-  }
+  ~SnapFile();
   int open(const std::string &p, bool write);
   int put(const void *p, size_t n);
   int get(void *p, size_t n);
-  int finish_write();  // trailing checksum + close
+  int finish_write();  // trailing checksum, fsync, atomic rename over path
   int finish_read();   // compare the trailing checksum
 };
 // glibc random_r TYPE_3 (the generator behind rand()): r[i] = r[i-3] + r[i-31]
@@ -166,6 +165,8 @@ struct swps_table {
   swps::DevMem counters;  // [0] = nrows (u32), [1] = error flag
   swps::DevMem scratch;   // per-call row indices
   uint32_t host_nrows = 0;
+  uint64_t snap_sum = 0;  // checksum of the snapshot last saved from / restored into this table (0: none);
+                          // worker-state snapshots record it so a resume pairs the two files of one save
 };
 
 namespace swps {

@@ -1,0 +1,24 @@
+// Stable key/value radix sort for the per-minibatch inverted indexes.
+//
+// rocPRIM picks a block merge sort below 1M items: at the B = 100 minibatch
+// (≈0.6M gradient records, 15-bit keys) that is ~20 kernels per sort — 37 %
+// of the step on the trace (profiles/r02_b100_*).  Onesweep sorts the same
+// keys in one histogram kernel plus one kernel per 8-bit digit, so the merge
+// path is switched off (MergeSortLimit = 0; inputs that fit one block still
+// get the single-block sort).  Same stable order, so same results.
+#pragma once
+#include <rocprim/device/device_radix_sort.hpp>
+
+namespace swps {
+
+using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                               rocprim::default_config, 0>;
+
+// tmp == nullptr: *bytes = the temporary storage needed
+template <typename K, typename V>
+inline hipError_t sort_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, const V *vin, V *vout, uint64_t n,
+                             int bits, hipStream_t s) {
+  return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);
+}
+
+}  // namespace swps

@@ -23,6 +23,8 @@ using namespace swps;
 
 namespace {
 
+constexpr uint32_t kFullRow = 0xFFFFFFFEu;  // slot claimed but the shard was full (no row)
+
 __device__ __forceinline__ uint64_t slot_hash(uint64_t key) { return splitmix64(key ^ 0x5851f42d4c957f2dULL); }
 
 __global__ void k_find_or_insert(const uint64_t *__restrict__ keys, uint64_t n, uint64_t *tkeys, uint32_t *slot_row,
@@ -46,18 +48,24 @@ __global__ void k_find_or_insert(const uint64_t *__restrict__ keys, uint64_t n, 
           uint32_t r = atomicAdd(&counters[0], 1u);
           if (r >= cap) {
             atomicOr(&counters[1], 1u);
+            __hip_atomic_store(&slot_row[s], kFullRow, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
           } else {
-            slot_row[s] = r;
             row_key[r] = key;
             row = r;
             isnew = 1;
+            // published after the row's key: a thread that finds this key
+            // (the same key twice in one call) waits for it below
+            __hip_atomic_store(&slot_row[s], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
           }
           break;
         }
         k = old;
       }
       if (k == key) {
-        row = slot_row[s];
+        uint32_t r;
+        while ((r = __hip_atomic_load(&slot_row[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == kNoRow)
+          __builtin_amdgcn_s_sleep(1);  // the inserting thread is between its CAS and the store above
+        if (r != kFullRow) row = r;
         break;
       }
       s = (s + 1) & mask;
@@ -604,9 +612,13 @@ int swps_load(swps_table *t, const char *path, int32_t frag_num, int32_t world, 
 // The reference can only dump values as text at 6 significant digits and
 // without the AdaGrad sums (sparsetable.h:63-70): a resumed run
 // diverges.  swps_save writes every row element bit for bit:
-//   "SWPSTBL1" | u32 layout | u32 dtype | i32 dim | u32 row_elems | u64 n |
+//   "SWPSTBL2" | u32 layout | u32 dtype | i32 dim | u32 row_elems |
+//   f32 learning_rate | f32 fudge (the push rule's constants: a resume with
+//   another server learning rate is not the same run) | u64 n |
 //   keys u64[n] | rows [n][row_elems] (table dtype) | u64 checksum
-static const char kTableMagic[8] = {'S', 'W', 'P', 'S', 'T', 'B', 'L', '1'};
+// The checksum is kept in swps_table::snap_sum; swps_w2v_save_state records
+// it, so a worker state resumes only against the table file of the same save.
+static const char kTableMagic[8] = {'S', 'W', 'P', 'S', 'T', 'B', 'L', '2'};
 
 int swps_save(swps_table *t, const char *path) {
   SWPS_HIP(hipSetDevice(t->cfg.device));
@@ -620,14 +632,18 @@ int swps_save(swps_table *t, const char *path) {
   }
   SnapFile f;
   SWPS_TRY(f.open(path, true));
-  const uint32_t hdr[4] = {(uint32_t)t->cfg.layout, (uint32_t)t->cfg.dtype, (uint32_t)t->cfg.dim,
-                           (uint32_t)t->row_elems};
+  const uint32_t hdr[6] = {(uint32_t)t->cfg.layout, (uint32_t)t->cfg.dtype, (uint32_t)t->cfg.dim,
+                           (uint32_t)t->row_elems, __float_as_uint_host(t->cfg.learning_rate),
+                           __float_as_uint_host(t->cfg.fudge)};
   SWPS_TRY(f.put(kTableMagic, 8));
   SWPS_TRY(f.put(hdr, sizeof(hdr)));
   SWPS_TRY(f.put(&m, 8));
   SWPS_TRY(f.put(keys.data(), m * 8));
   SWPS_TRY(f.put(rows.data(), rows.size()));
-  return f.finish_write();
+  const uint64_t sum = f.sum;
+  SWPS_TRY(f.finish_write());
+  t->snap_sum = sum;
+  return SWPS_OK;
 }
 
 // Read and verify the whole file before touching the table; then assign the
@@ -637,11 +653,17 @@ int swps_restore(swps_table *t, const char *path, int32_t frag_num, int32_t worl
   SnapFile f;
   SWPS_TRY(f.open(path, false));
   char magic[8];
-  uint32_t hdr[4];
+  uint32_t hdr[6];
   uint64_t m = 0;
-  if (f.get(magic, 8) != SWPS_OK || memcmp(magic, kTableMagic, 8) != 0)
+  if (f.get(magic, 8) != SWPS_OK || memcmp(magic, kTableMagic, 7) != 0)
     return fail(SWPS_E_IO, std::string("not a swps table snapshot: ") + path);
+  if (magic[7] != kTableMagic[7])
+    return fail(SWPS_E_IO, std::string("table snapshot format version ") + magic[7] + " (this library reads " +
+                               kTableMagic[7] + "): " + path);
   SWPS_TRY(f.get(hdr, sizeof(hdr)));
+  if (hdr[4] != __float_as_uint_host(t->cfg.learning_rate) || hdr[5] != __float_as_uint_host(t->cfg.fudge))
+    return fail(SWPS_E_CFG, std::string("snapshot was taken with another push rule (server learning rate / AdaGrad "
+                                        "fudge) than this table's: ") + path);
   if (hdr[0] != (uint32_t)t->cfg.layout || hdr[1] != (uint32_t)t->cfg.dtype || hdr[2] != (uint32_t)t->cfg.dim ||
       hdr[3] != (uint32_t)t->row_elems)
     return fail(SWPS_E_CFG, "snapshot (layout " + std::to_string(hdr[0]) + ", dtype " + std::to_string(hdr[1]) +
@@ -655,7 +677,9 @@ int swps_restore(swps_table *t, const char *path, int32_t frag_num, int32_t worl
   std::vector<char> rows(m * rb);
   SWPS_TRY(f.get(keys.data(), m * 8));
   SWPS_TRY(f.get(rows.data(), rows.size()));
+  const uint64_t sum = f.sum;
   SWPS_TRY(f.finish_read());
+  t->snap_sum = sum;
   if (world > 1 && node_id > 0) {
     std::vector<uint32_t> map(frag_num);
     SWPS_TRY(swps_hashfrag_table(frag_num, world, map.data()));

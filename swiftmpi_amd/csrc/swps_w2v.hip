@@ -38,6 +38,7 @@
 #include <unordered_set>
 
 #include "swps_internal.h"
+#include "swps_sort.h"
 #include "swps_wave.h"
 
 using namespace swps;
@@ -45,6 +46,8 @@ using namespace swps;
 namespace {
 
 constexpr int kMaxJump = 64;
+// forward slot entry tag: a table row index (not a worker-cache vid); see slot_row
+constexpr int32_t kTabRow = 0x40000000;
 __constant__ uint64_t c_jumpA[kMaxJump + 1];
 __constant__ uint64_t c_jumpC[kMaxJump + 1];
 
@@ -215,14 +218,6 @@ __global__ void k_bounds(const int32_t *__restrict__ kscan, const int64_t *__res
   if (i < n) out[i] = kscan[btok[i]];
 }
 
-// kept token indices of a batch in order
-__global__ void k_positions(const int32_t *__restrict__ kscan, uint64_t t0, uint64_t nt, int32_t *__restrict__ pos_tok) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nt) return;
-  const int32_t a = kscan[t0 + i];
-  if (kscan[t0 + i + 1] != a) pos_tok[a - kscan[t0]] = (int32_t)(t0 + i);
-}
-
 // x mod d for a fixed divisor d < 2^63 with the precomputed m = floor((2^64-1)/d):
 // q = mulhi(x, m) underestimates x/d by at most 2, so two corrections are exact.
 __device__ __forceinline__ uint64_t fast_mod(uint64_t x, uint64_t d, uint64_t m) {
@@ -256,7 +251,9 @@ struct RecArgs {
   uint32_t alias_n;
   const int32_t *local;
   uint32_t U;
-  int32_t *rec;     // [P][RS]: word, ctx vid x 2W (-1 = none), target vid x (N+1) (-1 = skipped)
+  const uint32_t *vid_row;  // direct table reads (single GPU): slots of pulled keys hold kTabRow | table row
+  int32_t *rec;     // [P][RS]: word, ctx x 2W (-1 = none), target x (N+1) (-1 = skipped); each a cache vid
+                    // or kTabRow | table row (slot_row)
   uint32_t *pkeys, *pvals;  // slot-major: h record (p,d) at d*P+p; v record (p,j) at (N+1)*P + j*P+p
   int32_t *trace;
   unsigned long long *rows_touched;
@@ -301,13 +298,17 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
         const int c = pos - W + aa;
         if (c >= 0 && c < n) cv = a.tok[ls + c];
       }
-      r[1 + j] = cv;
       uint32_t key = a.U;
+      int32_t src = cv;
       if (cv >= 0) {
         nctx++;
         const int32_t u = a.local[cv];
-        if (u >= 0) key = (uint32_t)u;
+        if (u >= 0) {
+          key = (uint32_t)u;
+          if (a.vid_row) src = kTabRow | (int32_t)a.vid_row[cv];
+        }
       }
+      r[1 + j] = src;
       const uint64_t k = HOFF + (uint64_t)j * P + p;
       a.pkeys[k] = key;
       a.pvals[k] = (uint32_t)k;
@@ -341,13 +342,17 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
         if (a.trace) a.trace[p * N + d - 1] = tv;
         if (tv == word) tv = -1;
       }
-      r[1 + 2 * W + d] = tv;
       uint32_t key = a.U;
+      int32_t src = tv;
       if (tv >= 0) {
         ntgt++;
         const int32_t u = a.local[tv];
-        if (u >= 0) key = (uint32_t)u;
+        if (u >= 0) {
+          key = (uint32_t)u;
+          if (a.vid_row) src = kTabRow | (int32_t)a.vid_row[tv];
+        }
       }
+      r[1 + 2 * W + d] = src;
       const uint64_t k = (uint64_t)d * P + p;
       a.pkeys[k] = key;
       a.pvals[k] = (uint32_t)k;
@@ -415,6 +420,7 @@ template <typename T, typename A> struct FwdArgs {
   const int32_t *rec;
   int P;
   const T *cache_h, *cache_v;
+  const T *tab;  // the table's rows [cap][4D]: source of rows tagged kTabRow (single-GPU direct reads)
   const float *exptab;
   int D, W, N;
   float alpha;
@@ -424,6 +430,17 @@ template <typename T, typename A> struct FwdArgs {
   int ld;   // neu1/neu1e row stride in elements (D rounded up to 128 B: whole cache lines per row)
   int cs;   // worker-cache row stride in elements (the same rounding)
 };
+
+// Source row of a forward slot: a record entry tagged kTabRow is a row index
+// into the table (the batch's pulled keys: the table row IS the value the
+// pull would have copied — the push of this batch has not run yet); any other
+// entry >= 0 is a vid into the worker cache (stale rows of keys outside the
+// batch key set, global_pull_access.h:88-97).
+template <typename T, typename A>
+__device__ __forceinline__ const T *slot_row(const FwdArgs<T, A> &a, int32_t e, bool ctx) {
+  if (e & kTabRow) return a.tab + (uint64_t)(e & ~kTabRow) * 4 * a.D + (ctx ? a.D : 0);
+  return (ctx ? a.cache_v : a.cache_h) + (uint64_t)e * a.cs;
+}
 
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
 // §Workgroup dispatch: b and b+8 share one).  Renumber so each XCD walks one
@@ -475,7 +492,7 @@ __global__ __launch_bounds__(256) void k_forward_b8(FwdArgs<T, A> a) {
       const int slot = s0 + q;
       vid[q] = slot < S ? r[1 + slot] : -1;
       if (vid[q] >= 0) {
-        const T *src = (slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * a.cs;
+        const T *src = slot_row(a, vid[q], slot < 2 * W);
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
           const int ci = lane + c * 64;
@@ -581,7 +598,7 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
       const int slot = s0 + q;
       vid[q] = slot < S ? r[1 + slot] : -1;
       if (vid[q] >= 0) {
-        const T *src = (slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * a.cs;
+        const T *src = slot_row(a, vid[q], slot < 2 * W);
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
           const int ci = lane + c * 64;
@@ -656,6 +673,11 @@ template <int NCH> struct FSlice {
 #pragma unroll
     for (int c = 0; c < NCH; c++) v[c] = ((const float4 *)row)[lane + c * 64];
     t = row[256 * NCH + (tl ? lane : 0)];  // lanes past the tail load a valid duplicate: no branch
+  }
+  __device__ __forceinline__ void st(float *row, int lane, bool tl) const {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) ((float4 *)row)[lane + c * 64] = v[c];
+    if (tl) row[256 * NCH + lane] = t;
   }
 };
 template <int NCH> struct FAcc {
@@ -736,7 +758,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (int q = 0; q < G; q++) {
       const int slot = s0 + q;
       vid[q] = __builtin_amdgcn_readfirstlane(slot < S ? r[1 + slot] : -1);
-      if (vid[q] >= 0) rows[q].ld((slot < 2 * W ? a.cache_v : a.cache_h) + (uint64_t)vid[q] * a.cs, lane, tl);
+      if (vid[q] >= 0) rows[q].ld(slot_row(a, vid[q], slot < 2 * W), lane, tl);
     }
 #pragma unroll
     for (int q = 0; q < G; q++) {
@@ -765,48 +787,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   acc.st(a.neu1 + (uint64_t)p * a.ld, lane, tl);
   ne.st(a.neu1e + (uint64_t)p * a.ld, lane, tl);
   if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
-}
-
-// Segment bounds of each (local key, kind) run in the sorted records:
-// seg[0][u], seg[1][u] = h-record range; seg[2][u], seg[3][u] = v-record range.
-__global__ void k_segments(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, uint64_t M,
-                           uint64_t HOFF, uint32_t U, uint32_t *__restrict__ seg) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M) return;
-  const uint32_t k = keys[i];
-  if (k >= U) return;
-  const int kind = vals[i] >= HOFF;
-  const bool first = i == 0 || keys[i - 1] != k || (int)(vals[i - 1] >= HOFF) != kind;
-  const bool last = i + 1 == M || keys[i + 1] != k || (int)(vals[i + 1] >= HOFF) != kind;
-  if (first) seg[(2 * kind) * U + k] = (uint32_t)i;
-  if (last) seg[(2 * kind + 1) * U + k] = (uint32_t)(i + 1);
-}
-
-// In profiled passes (gstats != nullptr) also accumulates the gather's work
-// (records summed, items = chunks) into gstats[0..1] for the roofline
-// accounting: one atomic per wave (same-address atomics: 5 -> 170 us, so
-// never in unprofiled steps).
-__global__ void k_item_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t *__restrict__ cnt,
-                              unsigned long long *__restrict__ gstats) {
-  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long rc = 0, ic = 0;
-  if (j == 2ull * U) cnt[j] = 0;
-  if (j < 2ull * U) {
-    const uint32_t u = (uint32_t)(j >> 1), kind = (uint32_t)(j & 1);
-    const uint32_t c = seg[(2 * kind + 1) * U + u] - seg[(2 * kind) * U + u];
-    cnt[j] = (c + CH - 1) / CH;
-    rc = c;
-    ic = (c + CH - 1) / CH;
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    rc += __shfl_xor(rc, off, 64);
-    ic += __shfl_xor(ic, off, 64);
-  }
-  if (gstats && (threadIdx.x & 63) == 0 && rc) {
-    atomicAdd(&gstats[0], rc);
-    atomicAdd(&gstats[1], ic);
-  }
 }
 
 // item descriptors {first record, end record | kind << 31, (key, kind) index j, chunk}:
@@ -1069,6 +1049,8 @@ template <typename T, typename A> struct PushArgs {
   int D;
   double lr, fudge;
   A *grads;  // TO_GRADS: mean gradients [U][2D] in the intermediate type (the push request payload)
+  T *cache_h, *cache_v;  // direct table reads (single GPU): every pushed key's pre-update h, v rows go to
+  int cs;                // the worker cache (the value its pull would have left there), row stride cs
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
@@ -1088,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
     if (lane == 0) a.local[vid] = -1;
     const uint32_t hc = a.seg[1 * a.U + u] - a.seg[0 * a.U + u];
     const uint32_t vc = a.seg[3 * a.U + u] - a.seg[2 * a.U + u];
-    if (hc == 0 && vc == 0 && !TO_GRADS) continue;
+    if (hc == 0 && vc == 0 && !TO_GRADS && !a.cache_h) continue;
     T *row = TO_GRADS ? nullptr : a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -1096,6 +1078,10 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
       if (ci >= NC) continue;
       for (int half = 0; half < 2; half++) {
         const uint32_t cnt = half ? vc : hc;
+        if (!TO_GRADS && a.cache_h) {  // the pulled (pre-update) value stays in the worker cache
+          using V = typename V16<T>::V;
+          ((V *)((half ? a.cache_v : a.cache_h) + (uint64_t)vid * a.cs))[ci] = ((const V *)(row + half * D))[ci];
+        }
         if (cnt == 0) {
           if (TO_GRADS)
 #pragma unroll
@@ -1160,7 +1146,7 @@ __global__ __launch_bounds__(256) void k_push_t(PushArgs<float, float> a) {
     if (lane == 0) a.local[vid] = -1;
     const uint32_t s0 = a.seg[0 * a.U + u], s1 = a.seg[1 * a.U + u], s2 = a.seg[2 * a.U + u], s3 = a.seg[3 * a.U + u];
     const uint32_t cnt[2] = {s1 - s0, s3 - s2};
-    if (cnt[0] == 0 && cnt[1] == 0) continue;
+    if (cnt[0] == 0 && cnt[1] == 0 && !a.cache_h) continue;
     float *row = a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
     uint32_t i0[2], i1[2];
     FSlice<NCH> wr[2], w2r[2], pf[2];
@@ -1168,11 +1154,15 @@ __global__ __launch_bounds__(256) void k_push_t(PushArgs<float, float> a) {
     for (int half = 0; half < 2; half++) {
       i0[half] = a.ioff[2 * u + half];
       i1[half] = a.ioff[2 * u + half + 1];
+      if (cnt[half] || a.cache_h) wr[half].ld(row + half * D, lane, tl);
       if (cnt[half]) {
         pf[half].ld(a.partial + (uint64_t)i0[half] * D, lane, tl);
-        wr[half].ld(row + half * D, lane, tl);
         w2r[half].ld(row + (2 + half) * D, lane, tl);
       }
+    }
+    if (a.cache_h) {  // the pulled (pre-update) value stays in the worker cache
+      wr[0].st(a.cache_h + (uint64_t)vid * a.cs, lane, tl);
+      wr[1].st(a.cache_v + (uint64_t)vid * a.cs, lane, tl);
     }
 #pragma unroll
     for (int half = 0; half < 2; half++) {
@@ -1806,9 +1796,8 @@ int presize(swps_w2v *w, uint64_t maxP) {
     int bits = 1;
     while ((1ULL << bits) <= U) bits++;
     size_t sb = 0;
-    SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
-                                                w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (int)M, 0, bits,
-                                                w->s));
+    SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                                            w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, w->s));
     SWPS_TRY(w->d_tmp.ensure(sb));
     const uint64_t max_items = 2ULL * U + M / kChunk + 1;
     SWPS_TRY(w->d_seg.ensure(U * 16));
@@ -1908,6 +1897,73 @@ __global__ void k_set_local(const int32_t *__restrict__ K, uint32_t U, int32_t *
   if (u < U) local[K[u]] = (int32_t)u;
 }
 
+// k_set_local and k_positions in one launch (thread i does both jobs' i-th item)
+__global__ void k_batch_setup(const int32_t *__restrict__ K, uint32_t U, int32_t *__restrict__ local,
+                              const int32_t *__restrict__ kscan, uint64_t t0, uint64_t nt,
+                              int32_t *__restrict__ pos_tok) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < U) local[K[i]] = (int32_t)i;
+  if (i < nt && pos_tok) {
+    const int32_t a = kscan[t0 + i];
+    if (kscan[t0 + i + 1] != a) pos_tok[a - kscan[t0]] = (int32_t)(t0 + i);
+  }
+}
+
+// Segment bounds and chunk counts of every (local key, kind) run of the
+// sorted records by binary search — one thread per key instead of one per
+// record plus a memset (records of key u: its h records, index < HOFF, then
+// its v records, each run in index order: the sort is stable).
+// seg[0][u], seg[1][u] = h-record range; seg[2][u], seg[3][u] = v-record range;
+// cnt[2u + kind] = chunks of <= CH records; cnt[2U] = 0 (the scan's tail).
+// Profiled passes (gstats) also add the records / items to gstats[0..1].
+__global__ void k_seg_counts(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, uint32_t M,
+                             uint32_t HOFF, uint32_t U, uint32_t CH, uint32_t *__restrict__ seg,
+                             uint32_t *__restrict__ cnt, unsigned long long *__restrict__ gstats) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long rc = 0, ic = 0;
+  if (u == U) cnt[2 * U] = 0;
+  if (u < U) {
+    auto lower = [&](uint32_t key) {
+      uint32_t lo = 0, hi = M;
+      while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (keys[mid] < key)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      return lo;
+    };
+    const uint32_t a = lower(u), b = lower(u + 1);
+    uint32_t lo = a, hi = b;  // first v record of the run
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1);
+      if (vals[mid] < HOFF)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    seg[u] = a;
+    seg[U + u] = lo;
+    seg[2 * U + u] = lo;
+    seg[3 * U + u] = b;
+    const uint32_t ch = (lo - a + CH - 1) / CH, cv = (b - lo + CH - 1) / CH;
+    cnt[2 * u] = ch;
+    cnt[2 * u + 1] = cv;
+    rc = b - a;
+    ic = ch + cv;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    rc += __shfl_xor(rc, off, 64);
+    ic += __shfl_xor(ic, off, 64);
+  }
+  if (gstats && (threadIdx.x & 63) == 0 && rc) {
+    atomicAdd(&gstats[0], rc);
+    atomicAdd(&gstats[1], ic);
+  }
+}
+
 int prep_batch(swps_w2v *w) {
   if (w->pb.valid) return SWPS_OK;
   const uint64_t nb = w->batches.size();
@@ -1929,13 +1985,18 @@ int prep_batch(swps_w2v *w) {
   pb.U = U;
   pb.nt = nt;
   // local key map of the batch (the grads[key] slots the pull resets,
-  // global_pull_access.h:88-97); cleared again by the push
-  if (U) {
-    k_set_local<<<nblk(U), 256, 0, s>>>(K, U, w->d_local.as<int32_t>());
+  // global_pull_access.h:88-97; cleared again by the push) and the batch's
+  // kept token indices, in one launch
+  const bool tracing = w->trace.size() < w->trace_cap;
+  const bool recs = P > 0 && (U > 0 || tracing);
+  if (recs) SWPS_TRY(w->d_pos_tok.ensure(P * 4));
+  if (U || recs) {
+    k_batch_setup<<<nblk(std::max<uint64_t>(U, recs ? nt : 0)), 256, 0, s>>>(
+        K, U, w->d_local.as<int32_t>(), w->d_kscan.as<int32_t>(), t0, recs ? nt : 0,
+        recs ? w->d_pos_tok.as<int32_t>() : nullptr);
     SWPS_HIP(hipGetLastError());
   }
-  const bool tracing = w->trace.size() < w->trace_cap;
-  if (P > 0 && (U > 0 || tracing)) {
+  if (recs) {
     // ---- position records + gradient records (learn_instance's draws) ----
     const uint64_t HOFF = P * (uint64_t)(N + 1);
     const uint64_t M = HOFF + P * (uint64_t)(2 * W);
@@ -1962,11 +2023,10 @@ int prep_batch(swps_w2v *w) {
                    ? w->d_alias.as<uint2>() + (w->cfg.minibatch_vocab ? B.kofs : 0)
                    : nullptr,
                w->cfg.minibatch_vocab ? U : (uint32_t)w->vocab_keys.size(),
-               w->d_local.as<int32_t>(), U, w->d_rec.as<int32_t>(),
+               w->d_local.as<int32_t>(), U, w->sharded ? nullptr : w->d_vid_row.as<uint32_t>(), w->d_rec.as<int32_t>(),
                w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
                tm.on ? w->d_rows_touched.as<unsigned long long>() : nullptr};
     hipEvent_t er = tm.begin(s);
-    k_positions<<<nblk(nt), 256, 0, s>>>(w->d_kscan.as<int32_t>(), t0, nt, w->d_pos_tok.as<int32_t>());
     k_records<<<nblk(P), 256, 256 * RS * sizeof(int32_t), s>>>(ra);
     SWPS_HIP(hipGetLastError());
     tm.end(KT_REC, er, s);
@@ -1988,23 +2048,18 @@ int prep_batch(swps_w2v *w) {
       while ((1ULL << bits) <= U) bits++;
       hipEvent_t es = tm.begin(s);
       size_t sb = 0;
-      SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
-                                                  w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (int)M, 0,
-                                                  bits, s));
+      SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                                              w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, s));
       SWPS_TRY(w->d_tmp.ensure(sb));
       sb = w->d_tmp.bytes;
-      SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(w->d_tmp.p, sb, w->d_pkeys.as<uint32_t>(),
-                                                  w->d_pkeys_s.as<uint32_t>(), w->d_pvals.as<uint32_t>(),
-                                                  w->d_pvals_s.as<uint32_t>(), (int)M, 0, bits, s));
+      SWPS_HIP(sort_pairs(w->d_tmp.p, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                                              w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, s));
       SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
-      SWPS_HIP(hipMemsetAsync(w->d_seg.p, 0, (uint64_t)U * 16, s));
-      k_segments<<<nblk(M), 256, 0, s>>>(w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, HOFF, U,
-                                         w->d_seg.as<uint32_t>());
-      SWPS_HIP(hipGetLastError());
       SWPS_TRY(w->d_icnt.ensure((2ULL * U + 1) * 4));
       SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
-      k_item_counts<<<nblk(2ULL * U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, w->d_icnt.as<uint32_t>(),
-                                                    tm.on ? w->d_gstats.as<unsigned long long>() : nullptr);
+      k_seg_counts<<<nblk((uint64_t)U + 1), 256, 0, s>>>(
+          w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (uint32_t)M, (uint32_t)HOFF, U, kChunk,
+          w->d_seg.as<uint32_t>(), w->d_icnt.as<uint32_t>(), tm.on ? w->d_gstats.as<unsigned long long>() : nullptr);
       SWPS_HIP(hipGetLastError());
       size_t ib = 0;
       SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, ib, w->d_icnt.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
@@ -2044,15 +2099,14 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
   const uint64_t P = pb.P;
   const int32_t *K = w->d_K.as<int32_t>() + B.kofs;
   // ---- pull (global_pull_access.h:28-107 + server.h:129-154) ----
-  if (U) {
+  // Single GPU: no copy — the forward reads the batch's keys straight from
+  // the table rows (k_records tagged them kTabRow) and the push leaves their
+  // pre-update values in the worker cache, which is exactly the state the
+  // reference's pull leaves behind.  Sharded: install the owners' values.
+  if (U && d_vals) {
     hipEvent_t e = tm.begin(s);
-    if (d_vals)  // sharded: values pulled from the owners
-      k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
-                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0, w->cs);
-    else
-      k_pull<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>(), D,
-                                                       w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
-                                                       w->d_local.as<int32_t>(), 0, w->cs);
+    k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
+                                                        w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0, w->cs);
     SWPS_HIP(hipGetLastError());
     tm.end(KT_PULL, e, s);
   }
@@ -2066,7 +2120,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_TRY(w->d_neu1.ensure(P * ld * sizeof(A)));
     SWPS_TRY(w->d_neu1e.ensure(P * ld * sizeof(A)));
     SWPS_TRY(w->d_pg.ensure(pb.HOFF * 4));
-    FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(),
+    FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(), w->t->rows.as<T>(),
                      w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
                      w->d_pg.as<float>(), w->xcd_order, ld, w->cs};
     hipEvent_t ef = tm.begin(s);
@@ -2136,7 +2190,8 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     // ---- push: mean + AdaGrad (also clears the local index map) ----
     PushArgs<T, A> pa{K, U, w->d_vid_row.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
                       w->d_partial.as<A>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
-                      (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads};
+                      (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads,
+                      d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail && !d_grads && w->push_t) {
@@ -2403,6 +2458,7 @@ int swps_w2v_init(swps_w2v *w) {
 
 int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
   if (!w->inited) return fail(SWPS_E_STATE, "call swps_w2v_init first");
+  if (w->sharded) return fail(SWPS_E_STATE, "sharded context: drive it with request / serve_pull / step / serve_push");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   if (w->overlap && count > 1 && !w->cfg.minibatch_vocab && w->trace.size() >= w->trace_cap && !w->pb.valid) {
     if (w->f64) return train_overlapped<double, double>(w, count);
@@ -2710,13 +2766,16 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
 // boundary: the epoch plan is a function of the two LCG states at the epoch
 // start, so those are stored instead of the plan, and the worker cache is
 // stored because negatives outside a batch's key set read its stale rows.
-//   "SWPSW2V1" | u64 config fp | u64 corpus fp | u64 V | u32 D | u32 esize |
+//   "SWPSW2V2" | u64 config fp | u64 corpus fp | u64 V | u32 D | u32 esize |
+//   u64 table snapshot checksum (swps_table::snap_sum of the swps_save that
+//   goes with this state; restore_state requires the table to have been
+//   swps_restore-d from exactly that file) |
 //   u64 cursor, lstate0, fstate0, 6 counters, 2 row counters |
 //   cache_h [V][D] | cache_v [V][D] (table dtype) | u64 checksum
 // ============================================================================
 namespace {
 
-const char kW2VMagic[8] = {'S', 'W', 'P', 'S', 'W', '2', 'V', '1'};
+const char kW2VMagic[8] = {'S', 'W', 'P', 'S', 'W', '2', 'V', '2'};
 
 uint64_t w2v_config_fp(const swps_w2v *w) {
   const auto &c = w->cfg;
@@ -2725,7 +2784,8 @@ uint64_t w2v_config_fp(const swps_w2v *w) {
                         c.unigram_size,        (uint64_t)c.key_mode,         (uint64_t)c.fp64_intermediates,
                         (uint64_t)c.minibatch_vocab, (uint64_t)c.sampler,    (uint64_t)w->D,
                         (uint64_t)w->f64,      (uint64_t)w->sharded,         (uint64_t)w->rank,
-                        (uint64_t)w->world,    (uint64_t)w->frag_num};
+                        (uint64_t)w->world,    (uint64_t)w->frag_num,
+                        __float_as_uint_host(w->t->cfg.learning_rate), __float_as_uint_host(w->t->cfg.fudge)};
   return checksum64(1, f, sizeof(f));
 }
 
@@ -2751,7 +2811,10 @@ int swps_w2v_save_state(swps_w2v *w, const char *path) {
   const uint32_t es = w->f64 ? 8 : 4;
   uint64_t rt[2] = {0, 0};
   SWPS_HIP(hipMemcpy(rt, w->d_rows_touched.p, 16, hipMemcpyDeviceToHost));
-  const uint64_t head[] = {w2v_config_fp(w), w2v_corpus_fp(w), V, (uint64_t)w->D | ((uint64_t)es << 32)};
+  if (!w->t->snap_sum)
+    return fail(SWPS_E_STATE, "save the table first (swps_save): the worker state is tied to that table snapshot");
+  const uint64_t head[] = {w2v_config_fp(w), w2v_corpus_fp(w), V, (uint64_t)w->D | ((uint64_t)es << 32),
+                           w->t->snap_sum};
   const uint64_t st[] = {w->cursor,       planned ? w->lstate_epoch : w->lstate,
                          planned ? w->fstate_epoch : w->fstate,
                          w->st_batches,   w->st_kept, w->st_words, w->st_pairs, w->st_pulled, w->st_pushed, rt[0], rt[1]};
@@ -2778,7 +2841,7 @@ int swps_w2v_restore_state(swps_w2v *w, const char *path) {
   SnapFile f;
   SWPS_TRY(f.open(path, false));
   char magic[8];
-  uint64_t head[4], st[11];
+  uint64_t head[5], st[11];
   if (f.get(magic, 8) != SWPS_OK || memcmp(magic, kW2VMagic, 8) != 0)
     return fail(SWPS_E_IO, std::string("not a swps word2vec state snapshot: ") + path);
   SWPS_TRY(f.get(head, sizeof(head)));
@@ -2788,6 +2851,9 @@ int swps_w2v_restore_state(swps_w2v *w, const char *path) {
                             "sample, alpha, dim, dtype, precision mode, sampler or sharding)");
   if (head[1] != w2v_corpus_fp(w) || head[2] != V || head[3] != ((uint64_t)w->D | ((uint64_t)es << 32)))
     return fail(SWPS_E_CFG, "snapshot was taken on a different corpus");
+  if (head[4] != w->t->snap_sum)
+    return fail(SWPS_E_STATE, "the table was not restored from the table snapshot saved with this worker state "
+                              "(swps_restore <prefix>.table of the same save first)");
   std::vector<char> ch(V * w->D * es), cv(ch.size());
   SWPS_TRY(f.get(ch.data(), ch.size()));
   SWPS_TRY(f.get(cv.data(), cv.size()));

@@ -64,6 +64,27 @@ class Exchanger:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return int(t.item())
 
+    def min(self, x):
+        return -self.max(-x)
+
+
+def _write_json_atomic(path, obj):
+    """<path>.tmp, fsync, rename over <path>, fsync the directory (a crash
+    leaves the old file or the new one, never a torn one)."""
+    import json
+    import os
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+    fd = os.open(os.path.dirname(os.path.abspath(path)), os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
 
 class _ShardedApp:
     """Lockstep driver of a sharded app context (swps_<app>_request /
@@ -320,25 +341,47 @@ class ShardedWord2Vec(_ShardedApp):
 
     def save(self, prefix):
         """Per-rank checkpoint <prefix>.rank<r>.{table,w2v,json}: this rank's
-        shard, its worker state and the driver's step cursor.  Lockstep
-        drivers only (a pipelined driver holds a prefetched pull that lacks
-        the last push)."""
-        import json
+        shard, its worker state (tied to that shard file by its checksum) and
+        the driver's step cursor, all tagged with one generation id; after
+        every rank has written its files, rank 0 writes <prefix>.commit —
+        a save without a commit marker (a crash mid-save) is never resumed.
+        Lockstep drivers only (a pipelined driver holds a prefetched pull that
+        lacks the last push)."""
+        import os
         if self._next is not None:
             raise capi.SwpsError(-6, "save: the pipelined driver holds a prefetched pull")
+        self.sync()
+        gen = self.ex.max(int.from_bytes(os.urandom(7), "little") if self.rank == 0 else 0)
         base = "%s.rank%d" % (prefix, self.rank)
         self.w.save(base)
-        with open(base + ".json", "w") as f:
-            json.dump({"cursor": self.cursor, "world": self.world, "frag_num": self.frag_num}, f)
+        _write_json_atomic(base + ".json", {"cursor": self.cursor, "world": self.world, "frag_num": self.frag_num,
+                                            "generation": gen})
+        self.ex.max(0)  # barrier: every rank's files are durable
+        if self.rank == 0:
+            _write_json_atomic(prefix + ".commit", {"generation": gen, "world": self.world, "cursor": self.cursor})
+        self.ex.max(0)
 
     def restore(self, prefix):
-        """Resume after load_text/load_tokens (instead of init)."""
+        """Resume after load_text/load_tokens (instead of init).  Every rank
+        must find the committed generation in its own files and all ranks the
+        same cursor (mismatched counts would desynchronise the all-to-alls)."""
         import json
+        import os
         base = "%s.rank%d" % (prefix, self.rank)
+        if not os.path.exists(prefix + ".commit"):
+            raise capi.SwpsError(-8, "no commit marker %s.commit: the save did not complete" % prefix)
+        with open(prefix + ".commit") as f:
+            commit = json.load(f)
         with open(base + ".json") as f:
             meta = json.load(f)
-        if meta["world"] != self.world or meta["frag_num"] != self.frag_num:
+        if meta["world"] != self.world or meta["frag_num"] != self.frag_num or commit["world"] != self.world:
             raise capi.SwpsError(-5, "checkpoint of world %d / frag_num %d" % (meta["world"], meta["frag_num"]))
+        if meta.get("generation") != commit["generation"]:
+            raise capi.SwpsError(-5, "rank %d files belong to another save than %s.commit" % (self.rank, prefix))
+        lo, hi = self.ex.min(meta["cursor"]), self.ex.max(meta["cursor"])
+        if lo != hi or hi != commit["cursor"]:
+            raise capi.SwpsError(-5, "ranks resume at different cursors (%d..%d, commit %d)" % (lo, hi,
+                                                                                           commit["cursor"]))
         self.w.restore(base)
         self.cursor = meta["cursor"]
 

@@ -165,6 +165,21 @@ def test_w2v_restore_preconditions(lib, gpu, tmp_path):
     # an already-initialised worker
     with pytest.raises(lib.SwpsError, match="fresh"):
         a.restore_state(prefix + ".w2v")
+    # the table file of ANOTHER save (later step) with this worker state
+    a.train_batches(2)
+    a.save(prefix + "2")
+    t = lib.Table("w2v", dim=16, capacity=2000, dtype="f32")
+    t.restore(prefix + "2.table")
+    w = lib.Word2Vec(t, init="table", **kw)
+    w.load_text(path)
+    with pytest.raises(lib.SwpsError, match="table snapshot"):
+        w.restore_state(prefix + ".w2v")
+    # a table whose push rule (server learning rate) differs from the snapshot's
+    with pytest.raises(lib.SwpsError, match="push rule"):
+        lib.Table("w2v", dim=16, capacity=2000, dtype="f32", learning_rate=0.5).restore(prefix + ".table")
+    # saves are atomic: no temporary is left behind, and a failed write keeps the old file
+    import glob
+    assert not glob.glob(prefix + "*.tmp")
 
 
 def test_lr_resume_from_table_snapshot(lib, gpu, tmp_path):
@@ -221,6 +236,12 @@ def test_sharded_w2v_resume_world1(lib, gpu, gloo1, tmp_path):
     b = make()
     b.restore(prefix)
     b.train_steps(3 * b.steps_per_epoch - b.cursor)
+    # a save without its commit marker (a crash between the ranks' files and the marker) is refused
+    import os
+    os.rename(prefix + ".commit", prefix + ".commit.bak")
+    with pytest.raises(lib.SwpsError, match="commit"):
+        make().restore(prefix)
+    os.rename(prefix + ".commit.bak", prefix + ".commit")
     b.sync()
     kr, rr = ref.shard_rows()
     kb, rb = b.shard_rows()

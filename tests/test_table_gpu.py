@@ -63,3 +63,18 @@ def test_w2v_dump_format_and_sharded_load(lib, gpu, tmp_path):
         t2 = lib.Table("w2v", dim=D, capacity=100, dtype="f32")
         t2.load(path, frag_num=1000, world=2, node_id=node)
         assert sorted(int(k) for k in t2.keys()) == [i + 1 for i in range(50) if owners[i] == node]
+
+
+def test_duplicate_keys_in_one_pull_share_a_row(lib, gpu):
+    """The reference's key sets are std::unordered_set (distinct); a caller
+    that repeats a key in one pull still gets one row for it — the inserting
+    thread publishes the row after its CAS, and a duplicate waits for it —
+    never a spurious zero row or an OOM."""
+    t = lib.Table("w2v", dim=8, capacity=64, dtype="f32", init="hash", seed=7)
+    base = torch.arange(100, 132, dtype=torch.int64, device=gpu)
+    keys = torch.cat([base, base, base[:7]])  # each key 2-3 times, in one call
+    v = t.pull(keys)
+    assert t.size() == 32
+    assert torch.equal(v[:32], v[32:64]) and torch.equal(v[:7], v[64:])
+    assert v.abs().sum(dim=1).min() > 0  # every copy got the initialised row
+    assert torch.equal(t.pull(base), v[:32])
