@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+XGMI_PEAK_GBS = 7 * 153.0  # per GPU: 7 xGMI links x ~153 GB/s
 
 
 def make_corpus(tokens, vocab, line_len, seed):
@@ -188,6 +189,8 @@ def main():
                     help="time the fp64-intermediate parity mode instead of the default fast mode")
     ap.add_argument("--no-parity-leg", action="store_true",
                     help="skip the extra parity-mode timing reported beside the fast-mode value")
+    ap.add_argument("--b100-steps", type=int, default=200,
+                    help="minibatches of the extra B = 100 leg (SURVEY.md §8(d) config 1's minibatch); 0 = skip")
     ap.add_argument("--sampler", default="table", choices=["table", "alias"],
                     help="negative sampler: the reference's unigram table (bit-exact draws) or an alias table")
     ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
@@ -233,8 +236,8 @@ def main():
 
     setup_s = {}
 
-    def build(fp64_intermediates):
-        kw = dict(window=args.window, negative=args.negative, minibatch=args.minibatch, sample=args.sample,
+    def build(fp64_intermediates, minibatch=None):
+        kw = dict(window=args.window, negative=args.negative, minibatch=minibatch or args.minibatch, sample=args.sample,
                   alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates, sampler=args.sampler)
         t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
                      device=local, init="hash", seed=1)
@@ -273,10 +276,15 @@ def main():
     w.kernel_times(reset=True)
     gw = getattr(w, "w", w)                 # the per-rank Word2Vec (sharded: its learner)
     g0 = gw.gather_stats()
-    _, dp = timed(w, args.steps)
+    if sharded:
+        w.set_exchange_profile(True)
+    dpt, dp = timed(w, args.steps)
     kt = w.kernel_times()
     g1 = gw.gather_stats()
+    xs = w.exchange_stats() if sharded else None
     w.set_profile(False)
+    if sharded:
+        w.set_exchange_profile(False)
     del w, t
     if dist is not None:
         tt = torch.tensor([dt, float(words)], dtype=torch.float64, device="cuda")
@@ -308,29 +316,47 @@ def main():
     step_bytes = (2 * es * D * (dp["ctx_rows"] + dp["tgt_rows"]) + d["pulled"] * 4 * es * D +
                   d["pushed"] * (10 * es * D + 8))
     step_gbs = step_bytes / dt / 1e9
-    # the metric's "sparse push/pull HBM GB/s": §8(d) bytes of the pull gather
-    # (read h,v from the table, write the worker cache: 4·D elements per key) and
-    # of the fused mean + AdaGrad push (mean grads 2·D, read h,v,h2,v2 4·D,
-    # write 4·D elements + the count per key), over those kernels' event times
-    # in the profiled pass (sharded mode: the owner-side install / serve kernels
-    # are not in these timers, so the fields are omitted)
+    # the metric's "sparse push/pull HBM GB/s".  Single GPU: the pull is no
+    # kernel of its own — the forward reads the batch's keys straight from the
+    # table rows (counted in roofline.forward) and the push leaves their
+    # pre-update h, v in the worker cache.  Push (§8(d) + that cache write):
+    # mean grads 2·D, read h,v,h2,v2 4·D, write 4·D, cache h,v 2·D elements
+    # + the count per key, over the push kernel's event time in the profiled
+    # pass (sharded mode: the owner-side install / serve kernels are not in
+    # these timers, so the fields are omitted)
     pp = {}
-    for name, nbytes in (("pull", dp["pulled"] * 4 * es * D), ("push", dp["pushed"] * (10 * es * D + 8))):
+    for name, nbytes in (("pull", dp["pulled"] * 4 * es * D), ("push", dp["pushed"] * (12 * es * D + 8))):
         ms, n = kt.get(name, (0.0, 0))
         if ms > 0 and not sharded:
             gbs = nbytes / (ms * 1e-3) / 1e9
             pp[name] = {"GBps": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": nbytes / max(n, 1),
                         "avg_launch_ms": ms / max(n, 1)}
+    if not sharded and "pull" not in pp:
+        pp["pull"] = "fused: k_forward reads the pulled keys' table rows directly; k_push writes their cache rows"
+    # xGMI: bytes this rank's all-to-alls sent to other ranks per step, over the
+    # exchanges' event time on their stream, against 7 links x 153 GB/s
+    exchange = None
+    if xs is not None:
+        xg = xs["bytes_remote"] / (xs["ms"] * 1e-3) / 1e9 if xs["ms"] > 0 else 0.0
+        exchange = {"bytes_remote_per_step": xs["bytes_remote"] / args.steps,
+                    "bytes_total_per_step": xs["bytes_total"] / args.steps,
+                    "a2a_per_step": xs["calls"] / args.steps, "ms_per_step": xs["ms"] / args.steps,
+                    "share_of_step": xs["ms"] / (dpt * 1e3) if dpt > 0 else None,
+                    "GBps": xg, "peak": XGMI_PEAK_GBS, "frac": xg / XGMI_PEAK_GBS,
+                    "note": "remote bytes (keys 8 B, rows and grads %d B per remote key) / all-to-all time "
+                            "(events on the exchange stream, profiled pass); world %d" % (2 * D * es, world)}
     # HBM traffic of the same kernel from the committed PMC passes of this exact
     # command (scripts/gpu_profile.sh -> scripts/pmc_summary.py); null otherwise
     traffic, traffic_src, fwd_traffic = None, None, None
-    pmc_name = "r01_pmc_w2v_fast.json"
+    # (per-launch bytes do not depend on --steps / --warmup: only the workload
+    # keys must match)
+    pmc_name = "r02_pmc_w2v_fast.json"
     pmc = os.path.join(ROOT, "profiles", pmc_name)
-    mine = dict(minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, steps=args.steps, warmup=args.warmup,
-                mode="fast", world=world)
+    mine = dict(minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, mode="fast", world=world,
+                tokens=args.tokens, vocab=args.vocab, line_len=args.line_len)
     if os.path.exists(pmc) and not parity_main:
         prof = json.load(open(pmc))
-        if prof.get("config") == mine:
+        if {k: prof.get("config", {}).get(k) for k in mine} == mine:
             gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items()
                   if k.startswith("k_gather") or k.startswith("k_combine")]
             if gt:  # per gather-timer launch: k_gather_t + k_combine
@@ -349,6 +375,19 @@ def main():
         parity_leg = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
                       "mode": "fp64 neu1/neu1e + gradient partials (reference-parity mode)"}
         del w2, t2
+    # SURVEY.md §8(d) config 1's minibatch (B = 100 lines of the same
+    # 1000-token lines), same mode as the headline, timed the same way over
+    # --b100-steps minibatches (the driver-visible small-batch number)
+    b100_leg = None
+    if rank == 0 and world == 1 and not sharded and args.b100_steps > 0 and args.minibatch != 100:
+        t3, w3 = build(fp64_intermediates=parity_main, minibatch=100)
+        w3.train_batches(10)
+        w3.sync()
+        bdt, bd = timed(w3, args.b100_steps)
+        b100_leg = {"value": bd["words"] / bdt, "unit": "words/s", "minibatch": 100, "steps": args.b100_steps,
+                    "warmup": 10, "ms_per_step": bdt * 1e3 / args.b100_steps,
+                    "kept_positions_per_s": bd["kept"] / bdt, "pulled_keys_per_step": bd["pulled"] / args.b100_steps}
+        del w3, t3
 
     out = {
         "metric": "SGNS trained words/sec at 1/8 GPUs; sparse push/pull HBM GB/s vs peak",
@@ -400,6 +439,8 @@ def main():
                      "pull_push": pp or None},
         "kernel_ms": {k: v[0] for k, v in kt.items()},
         "parity_mode": parity_leg,
+        "minibatch_100": b100_leg,
+        "exchange": exchange,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ids, off, keys, args, args.cpu_lines)

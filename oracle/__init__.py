@@ -101,6 +101,22 @@ def lib():
         L.orc_s2v_docs.argtypes = [_p, _p, _p, _p]
         L.orc_s2v_stats.argtypes = [_p, _p]
         L.orc_s2v_word_rows.argtypes = [_p, _p, _u64, _p]
+        L.orc_w2vm_create.restype = _p
+        L.orc_w2vm_create.argtypes = [_p, ctypes.c_int, ctypes.POINTER(W2VCfg), _u64]
+        L.orc_w2vm_destroy.argtypes = [_p]
+        L.orc_w2vm_train.argtypes = [_p, ctypes.c_int]
+        L.orc_w2vm_train_steps.argtypes = [_p, _u64]
+        L.orc_w2vm_num_keys.restype = _u64
+        L.orc_w2vm_num_keys.argtypes = [_p]
+        L.orc_w2vm_params.argtypes = [_p, _p, _p]
+        L.orc_w2vm_rank_stats.argtypes = [_p, ctypes.c_int, _p]
+        L.orc_lrm_create.restype = _p
+        L.orc_lrm_create.argtypes = [_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, _u64]
+        L.orc_lrm_destroy.argtypes = [_p]
+        L.orc_lrm_train.argtypes = [_p, ctypes.c_int]
+        L.orc_lrm_num_keys.restype = _u64
+        L.orc_lrm_num_keys.argtypes = [_p]
+        L.orc_lrm_params.argtypes = [_p, _p, _p, _p]
         _lib = L
     return _lib
 
@@ -324,6 +340,83 @@ class S2V:
         out = np.zeros((len(keys), 2 * self.dim), dtype=np.float64)
         rc = lib().orc_s2v_word_rows(self.h, _ptr(keys), len(keys), _ptr(out))
         return out, rc == 0
+
+
+def _cstrings(paths):
+    arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+    return ctypes.cast(arr, ctypes.c_void_p), arr
+
+
+class W2VMulti:
+    """Lockstep multi-rank word2vec (swps_oracle.cpp W2VMulti): one worker per
+    corpus path, one server map, hash-initialised keys (the sharded tables'
+    SWPS_INIT_HASH with `seed`), every rank's push its own AdaGrad step in
+    rank order."""
+
+    def __init__(self, paths, dim, window=5, negative=5, min_sentence_length=1, minibatch=100, sample=1e-5,
+                 alpha=0.05, lr=0.7, table_size=int(1e8), storage_f32=False, seed=0):
+        c = W2VCfg(dim, window, negative, min_sentence_length, minibatch, int(storage_f32), sample, alpha, lr,
+                   table_size, 0, 0)
+        self.dim = dim
+        pp, self._keep = _cstrings(paths)
+        self.h = lib().orc_w2vm_create(pp, len(paths), ctypes.byref(c), seed)
+        if not self.h:
+            raise RuntimeError(lib().orc_last_error().decode())
+        self.R = len(paths)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_w2vm_destroy(self.h)
+            self.h = None
+
+    def train(self, niters=1):
+        if lib().orc_w2vm_train(self.h, niters) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def train_steps(self, n):
+        """The next n lockstep steps (one minibatch per rank each; epochs wrap)."""
+        if lib().orc_w2vm_train_steps(self.h, n) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def params(self):
+        """(keys ascending, rows [n][4D] = h | v | h2sum | v2sum)"""
+        n = int(lib().orc_w2vm_num_keys(self.h))
+        keys = np.zeros(n, dtype=np.uint64)
+        rows = np.zeros((n, 4 * self.dim), dtype=np.float64)
+        lib().orc_w2vm_params(self.h, _ptr(keys), _ptr(rows))
+        return keys, rows
+
+    def rank_stats(self, r):
+        out = np.zeros(6, dtype=np.uint64)
+        lib().orc_w2vm_rank_stats(self.h, r, _ptr(out))
+        return dict(zip(["kept", "pushes", "pulls", "actual_train_words", "rng", "frng"], [int(x) for x in out]))
+
+
+class LRMulti:
+    """Lockstep multi-rank sparse LR (swps_oracle.cpp LRMulti)."""
+
+    def __init__(self, paths, minibatch=200, lr=0.05, seed=0):
+        pp, self._keep = _cstrings(paths)
+        self.h = lib().orc_lrm_create(pp, len(paths), minibatch, lr, seed)
+        if not self.h:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_lrm_destroy(self.h)
+            self.h = None
+
+    def train(self, niters):
+        if lib().orc_lrm_train(self.h, niters) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def params(self):
+        n = int(lib().orc_lrm_num_keys(self.h))
+        keys = np.zeros(n, dtype=np.uint32)
+        w = np.zeros(n, dtype=np.float32)
+        g2 = np.zeros(n, dtype=np.float32)
+        lib().orc_lrm_params(self.h, _ptr(keys), _ptr(w), _ptr(g2))
+        return keys, w, g2
 
 
 def logloss_accuracy(p, y, eps=1e-15):

@@ -209,6 +209,7 @@ struct W2V {
   size_t train_words = 0;
   std::vector<uint32_t> table;  // unigram table as indices into wordids
   std::unordered_map<uint64_t, SParam> server;
+  std::unordered_map<uint64_t, SParam> *srv = &server;  // the multi-rank oracle shares one server
   std::unordered_map<uint64_t, Row> cache;
   std::unordered_map<uint64_t, Grad> grads;
   std::unordered_map<uint64_t, uint32_t> vid;
@@ -312,7 +313,7 @@ struct W2V {
 
   void full_pull_to_cache() {
     for (auto k : local_keys) {
-      auto &p = server[k];
+      auto &p = (*srv)[k];
       cache[k] = Row{p.h, p.v};
       Grad g;
       g.hg.assign(D(), 0);
@@ -484,8 +485,8 @@ struct W2V {
   void pull(const std::unordered_set<uint64_t> &K) {
     pulls++;
     for (auto k : K) {
-      auto it = server.find(k);
-      if (it == server.end()) throw std::runtime_error("pull of a key the full pull never inserted");
+      auto it = srv->find(k);
+      if (it == srv->end()) throw std::runtime_error("pull of a key the full pull never inserted");
       cache[k] = Row{it->second.h, it->second.v};
       Grad g;
       g.hg.assign(D(), 0);
@@ -513,8 +514,8 @@ struct W2V {
       std::fill(g.hg.begin(), g.hg.end(), 0.0);
       std::fill(g.vg.begin(), g.vg.end(), 0.0);
       g.hc = g.vc = 0;
-      auto sit = server.find(k);
-      if (sit == server.end()) throw std::runtime_error("push of an unknown key");
+      auto sit = srv->find(k);
+      if (sit == srv->end()) throw std::runtime_error("push of an unknown key");
       SParam &p = sit->second;
       for (int i = 0; i < D(); i++) {
         double h2 = p.h2[i] + hg[i] * hg[i];
@@ -568,6 +569,56 @@ struct W2V {
         grads.erase(k);
       }
     }
+  }
+
+  // The batches of one train_iter epoch as steps (the GPU schedule's
+  // batches): step 0 = line 1, trained on the stale cache with no key set;
+  // step j >= 1 = pull K_j, the lines up to the next minibatch boundary (or
+  // the early stop), push K_j.
+  struct Step {
+    size_t l0, l1;
+    bool hasK;
+    std::unordered_set<uint64_t> K;
+  };
+  std::vector<Step> epoch_steps() {
+    std::vector<Step> out;
+    int line_counter = 0;
+    size_t cur = 0, li = 0, start = 0;
+    bool hasK = false;
+    std::unordered_set<uint64_t> K;
+    auto emit = [&](size_t end) {
+      out.push_back(Step{start, end, hasK, hasK ? K : std::unordered_set<uint64_t>()});
+      start = end;
+    };
+    while (li < lines.size()) {
+      cur += lines[li++].words.size();
+      line_counter++;
+      if (line_counter == 1) {
+        emit(li);
+        K = gather_window(li);
+        hasK = true;
+      }
+      if (line_counter % cfg.minibatch == 0) {
+        emit(li);
+        K = gather_window(li);
+      }
+      if (cur > train_words) break;
+    }
+    emit(li);
+    return out;
+  }
+  // one step of a lockstep multi-rank run, in three phases
+  void step_pull(const Step &st) {
+    if (st.hasK) pull(st.K);
+  }
+  void step_learn(const Step &st) {
+    for (size_t l = st.l0; l < st.l1; l++) {
+      learn_instance(lines[l].words);
+      actual_train_words += lines[l].words.size();
+    }
+  }
+  void step_push(const Step &st) {
+    if (st.hasK) push(st.K);
   }
 
   // word2vec_global.h:591-651 TrainModelThread(0) with nthreads = 1
@@ -975,6 +1026,269 @@ uint64_t orc_lr_pull_order(void *h, uint32_t *out, uint64_t cap) {
   for (auto k : K0)
     if (n < cap) out[n++] = k;
   return n;
+}
+
+}  // extern "C"
+
+// =============================================================================
+// Multi-rank lockstep restatement.  R workers — each a
+// reference MPI rank with its own corpus, vocab, unigram table, RNG streams
+// (global_random() is per process, random.h:44-47) and worker cache — and ONE
+// server map standing for the union of the key-sharded servers.  A key is
+// initialised on the first pull that reaches its owner by the hash rule of the
+// product's sharded tables (SWPS_INIT_HASH: the reference's rand() order would
+// depend on message arrival).  Step s of an epoch: every rank pulls its batch-s
+// key set (so every pull sees every push of steps < s), every rank learns its
+// batch-s lines, then every rank's mean-gradient push is applied as its own
+// AdaGrad step in rank order — cluster/server.h:156-176 applies each worker's
+// push request as it arrives; the lockstep order fixes the arrival order.
+// Ranks with fewer batches per epoch idle in the later steps.
+// =============================================================================
+namespace {
+
+static inline uint64_t orc_splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ULL;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+// u in [0, 1) from (seed, key, element) — the sharded tables' init hash
+static inline float orc_unit_hash(uint64_t seed, uint64_t key, uint64_t i) {
+  uint64_t z = orc_splitmix64(seed ^ orc_splitmix64(key + 0x632be59bd9b4e019ULL * (i + 1)));
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+struct W2VMulti {
+  std::vector<W2V *> ranks;
+  std::unordered_map<uint64_t, SParam> server;
+  uint64_t seed = 0;
+  ~W2VMulti() {
+    for (auto *m : ranks) delete m;
+  }
+  void init_key(uint64_t k, int D, bool f32) {
+    if (server.count(k)) return;
+    SParam p;
+    p.h.assign(D, 0);
+    p.v.assign(D, 0);
+    p.h2.assign(D, 0);
+    p.v2.assign(D, 0);
+    for (int e = 0; e < 2 * D; e++) {
+      double x = store_round(((double)orc_unit_hash(seed, k, e) - 0.5) / (double)D, f32);
+      (e < D ? p.h[e] : p.v[e - D]) = x;
+    }
+    server[k] = p;
+  }
+  void full_pulls() {  // every rank's first full pull (word2vec_global.h:557-562)
+    for (auto *m : ranks) {
+      for (auto k : m->local_keys) init_key(k, m->D(), m->f32());
+      m->full_pull_to_cache();
+    }
+  }
+  std::vector<std::vector<W2V::Step>> st;
+  size_t maxs = 0, cursor = 0;  // steps per epoch (the longest rank's), global step
+  void plan() {
+    if (!st.empty()) return;
+    for (auto *m : ranks) {
+      st.push_back(m->epoch_steps());
+      maxs = std::max(maxs, st.back().size());
+    }
+  }
+  void train_steps(size_t n) {  // the next n lockstep steps, epochs wrapping
+    plan();
+    for (size_t k = 0; k < n; k++, cursor++) {
+      const size_t s = cursor % maxs;
+      if (s == 0)
+        for (auto *m : ranks) m->actual_train_words = 0;
+      for (size_t r = 0; r < ranks.size(); r++)
+        if (s < st[r].size()) ranks[r]->step_pull(st[r][s]);
+      for (size_t r = 0; r < ranks.size(); r++)
+        if (s < st[r].size()) ranks[r]->step_learn(st[r][s]);
+      for (size_t r = 0; r < ranks.size(); r++)
+        if (s < st[r].size()) ranks[r]->step_push(st[r][s]);
+    }
+  }
+  void train(int niters) {
+    plan();
+    train_steps((size_t)niters * maxs);
+  }
+};
+
+// sparse LR, the same lockstep over R workers (lr.cpp:157-238 per rank, one
+// server map, hash init w = u on the first pull, AdaGrad per source in rank order)
+struct LRMulti {
+  std::vector<LR *> ranks;
+  std::unordered_map<uint32_t, LRParam> server;
+  uint64_t seed = 0;
+  ~LRMulti() {
+    for (auto *m : ranks) delete m;
+  }
+  // a rank's batches of an epoch: B+1 valid lines each (lr.cpp:308-354)
+  static std::vector<std::pair<size_t, size_t>> batches(const LR &m) {
+    std::vector<std::pair<size_t, size_t>> out;
+    for (size_t li = 0; li < m.ins.size();) {
+      size_t end = std::min(m.ins.size(), li + (size_t)m.minibatch + 1);
+      out.emplace_back(li, end);
+      li = end;
+    }
+    return out;
+  }
+  void pull(LR &m, const std::unordered_set<uint32_t> &K) {
+    for (auto k : K) {
+      auto it = server.find(k);
+      if (it == server.end()) {
+        LRParam p;
+        p.val = orc_unit_hash(seed, k, 0);
+        it = server.emplace(k, p).first;
+      }
+      m.cache[k] = it->second.val;
+      m.grads[k] = LRGrad();
+    }
+  }
+  void push(LR &m, const std::unordered_set<uint32_t> &K) {
+    for (auto k : K) {
+      auto it = m.grads.find(k);
+      if (it == m.grads.end()) continue;
+      LRGrad g = it->second;
+      it->second = LRGrad();
+      if (g.count == 0) continue;
+      float mg = float(g.val / g.count);
+      LRParam &p = server[k];
+      p.g2 += mg * mg;
+      p.val += m.lr * mg / float(std::sqrt(p.g2 + 1e-6f));
+    }
+  }
+  void train(int niters) {
+    std::vector<std::vector<std::pair<size_t, size_t>>> bs;
+    size_t maxs = 0;
+    for (auto *m : ranks) {
+      std::unordered_set<uint32_t> K0;
+      for (auto &x : m->ins)
+        for (auto &f : x.feas) K0.insert(f.first);
+      pull(*m, K0);
+      bs.push_back(batches(*m));
+      maxs = std::max(maxs, bs.back().size());
+    }
+    std::vector<std::unordered_set<uint32_t>> K(ranks.size());
+    for (int it = 0; it < niters; it++)
+      for (size_t s = 0; s < maxs; s++) {
+        for (size_t r = 0; r < ranks.size(); r++) {
+          if (s >= bs[r].size()) continue;
+          LR &m = *ranks[r];
+          K[r].clear();
+          for (size_t j = bs[r][s].first; j < bs[r][s].second; j++)
+            for (auto &f : m.ins[j].feas) K[r].insert(f.first);
+          m.cache.clear();
+          m.grads.clear();
+          pull(m, K[r]);
+        }
+        for (size_t r = 0; r < ranks.size(); r++)
+          if (s < bs[r].size())
+            for (size_t j = bs[r][s].first; j < bs[r][s].second; j++) ranks[r]->learn(ranks[r]->ins[j]);
+        for (size_t r = 0; r < ranks.size(); r++)
+          if (s < bs[r].size()) push(*ranks[r], K[r]);
+      }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+void *orc_w2vm_create(const char **paths, int R, const orc_w2v_cfg *c, uint64_t seed) {
+  W2VMulti *mm = new W2VMulti();
+  mm->seed = seed;
+  for (int r = 0; r < R; r++) {
+    W2V *m = (W2V *)orc_w2v_create(paths[r], c);
+    if (!m) {
+      delete mm;
+      return nullptr;
+    }
+    m->srv = &mm->server;
+    mm->ranks.push_back(m);
+  }
+  try {
+    mm->full_pulls();
+  } catch (std::exception &e) {
+    g_err = e.what();
+    delete mm;
+    return nullptr;
+  }
+  return mm;
+}
+void orc_w2vm_destroy(void *h) { delete (W2VMulti *)h; }
+int orc_w2vm_train(void *h, int niters) {
+  try {
+    ((W2VMulti *)h)->train(niters);
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+int orc_w2vm_train_steps(void *h, uint64_t n) {
+  try {
+    ((W2VMulti *)h)->train_steps(n);
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+uint64_t orc_w2vm_num_keys(void *h) { return ((W2VMulti *)h)->server.size(); }
+// every server key (ascending) with its row [h | v | h2 | v2]
+void orc_w2vm_params(void *h, uint64_t *keys, double *rows) {
+  W2VMulti *mm = (W2VMulti *)h;
+  std::vector<uint64_t> ks;
+  for (auto &kv : mm->server) ks.push_back(kv.first);
+  std::sort(ks.begin(), ks.end());
+  const int D = mm->ranks[0]->D();
+  for (size_t i = 0; i < ks.size(); i++) {
+    keys[i] = ks[i];
+    const SParam &p = mm->server[ks[i]];
+    double *o = rows + i * 4 * D;
+    std::copy(p.h.begin(), p.h.end(), o);
+    std::copy(p.v.begin(), p.v.end(), o + D);
+    std::copy(p.h2.begin(), p.h2.end(), o + 2 * D);
+    std::copy(p.v2.begin(), p.v2.end(), o + 3 * D);
+  }
+}
+// per-rank [kept, pushes, pulls, actual_train_words, rng, frng]
+void orc_w2vm_rank_stats(void *h, int r, uint64_t *out) { orc_w2v_stats(((W2VMulti *)h)->ranks[r], out); }
+
+void *orc_lrm_create(const char **paths, int R, int minibatch, float lr, uint64_t seed) {
+  LRMulti *mm = new LRMulti();
+  mm->seed = seed;
+  for (int r = 0; r < R; r++) {
+    LR *m = (LR *)orc_lr_create(paths[r], minibatch, lr);
+    if (!m) {
+      delete mm;
+      return nullptr;
+    }
+    mm->ranks.push_back(m);
+  }
+  return mm;
+}
+void orc_lrm_destroy(void *h) { delete (LRMulti *)h; }
+int orc_lrm_train(void *h, int niters) {
+  try {
+    ((LRMulti *)h)->train(niters);
+    return 0;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+uint64_t orc_lrm_num_keys(void *h) { return ((LRMulti *)h)->server.size(); }
+void orc_lrm_params(void *h, uint32_t *keys, float *w, float *g2) {
+  LRMulti *mm = (LRMulti *)h;
+  std::vector<uint32_t> ks;
+  for (auto &kv : mm->server) ks.push_back(kv.first);
+  std::sort(ks.begin(), ks.end());
+  for (size_t i = 0; i < ks.size(); i++) {
+    keys[i] = ks[i];
+    w[i] = mm->server[ks[i]].val;
+    g2[i] = mm->server[ks[i]].g2;
+  }
 }
 
 }  // extern "C"

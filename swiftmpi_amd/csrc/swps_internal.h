@@ -165,6 +165,7 @@ struct swps_table {
   swps::DevMem counters;  // [0] = nrows (u32), [1] = error flag
   swps::DevMem scratch;   // per-call row indices
   uint32_t host_nrows = 0;
+  swps::DevMem push_scratch, sort_tmp;  // table_push_sources: (row, position) pairs and their sort
   uint64_t snap_sum = 0;  // checksum of the snapshot last saved from / restored into this table (0: none);
                           // worker-state snapshots record it so a resume pairs the two files of one save
 };
@@ -181,4 +182,8 @@ int table_get_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_va
 int table_copy_pull(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s);
 int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
                     bool grads_f32 = false);
+// several sources' pushes concatenated in rank order (keys distinct within a
+// source): each row gets its sources' AdaGrad steps in that order, one pass
+int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
+                       bool grads_f32 = false);
 }  // namespace swps

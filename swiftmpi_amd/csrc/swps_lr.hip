@@ -730,12 +730,8 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
   for (int r = 0; r < l->world; r++) n += src_counts[r];
   if (n != l->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
   SWPS_TRY(table_lookup(l->t, d_keys, n, l->d_serve_rows.as<uint32_t>(), l->s));
-  uint64_t off = 0;
-  for (int r = 0; r < l->world; r++) {  // one AdaGrad step per source, in rank order
-    SWPS_TRY(table_push_rows(l->t, l->d_serve_rows.as<uint32_t>() + off, src_counts[r], d_grads + off, l->s));
-    off += src_counts[r];
-  }
-  return SWPS_OK;
+  // one AdaGrad step per source, in rank order, all sources in one pass
+  return table_push_sources(l->t, l->d_serve_rows.as<uint32_t>(), n, d_grads, l->s);
 }
 
 void *swps_lr_stream(swps_lr *l) { return (void *)l->s; }

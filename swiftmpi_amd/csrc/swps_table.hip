@@ -16,8 +16,10 @@
 #include <cstdio>
 #include <fstream>
 #include <sstream>
+#include <type_traits>
 
 #include "swps_internal.h"
+#include "swps_sort.h"
 
 using namespace swps;
 
@@ -217,6 +219,82 @@ __global__ void k_push_lr(const uint32_t *__restrict__ rows_idx, uint64_t n, con
 
 inline unsigned blocks_for(uint64_t threads, unsigned bs = 256) { return (unsigned)((threads + bs - 1) / bs); }
 
+// ---- several sources' pushes in one pass (sharded serve_push) -------------
+// The owner receives the mean gradients of every source rank for its keys,
+// concatenated in rank order; each source's keys are distinct, a key may come
+// from several sources.  The reference applies each worker's push request as
+// its own AdaGrad step, in arrival order (cluster/server.h:156-176); here the
+// order is the rank order.  Instead of one launch per source re-reading and
+// re-writing a hot row once per source, the (row, position) pairs are
+// stable-sorted by row and one wave per distinct row applies its pushes in
+// position (= rank) order with the row held in registers: the same
+// arithmetic, element for element (every intermediate rounded to the table
+// type, as the per-source form stores it), one read and one write per row.
+__global__ void k_push_keys(const uint32_t *__restrict__ rows_idx, uint64_t n, uint32_t cap,
+                            uint32_t *__restrict__ key, uint32_t *__restrict__ pos) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = rows_idx[i];
+  key[i] = r == kNoRow ? cap : r;  // unknown keys (the lookup flagged them) sort last and are skipped
+  pos[i] = (uint32_t)i;
+}
+
+template <typename T, typename G, int E>
+__global__ void k_push_w2v_multi(const uint32_t *__restrict__ rows_s, const uint32_t *__restrict__ pos_s,
+                                 uint64_t n, uint32_t cap, const G *__restrict__ grads, T *__restrict__ rows, int D,
+                                 double lr, double fudge) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= n) return;
+  const uint32_t r = rows_s[w];
+  if (r >= cap || (w > 0 && rows_s[w - 1] == r)) return;  // only the head of each row's run works
+  uint64_t e = w + 1;
+  while (e < n && rows_s[e] == r) e++;
+  using PT = Pack<T, E>;
+  using PG = Pack<G, E>;
+  T *row = rows + (uint64_t)r * 4 * D;
+  for (int c = lane; c < D / E; c += 64) {
+    PT h = ((PT *)row)[c], v = ((PT *)(row + D))[c], h2 = ((PT *)(row + 2 * D))[c], v2 = ((PT *)(row + 3 * D))[c];
+    for (uint64_t j = w; j < e; j++) {
+      const G *g = grads + (uint64_t)pos_s[j] * 2 * D;
+      const PG gh = ((const PG *)g)[c], gv = ((const PG *)(g + D))[c];
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const double a = (double)gh.v[k], b = (double)gv.v[k];
+        const double h2n = (double)h2.v[k] + a * a;
+        const double v2n = (double)v2.v[k] + b * b;
+        h.v[k] = (T)((double)h.v[k] + (a * lr) / sqrt(h2n + fudge));
+        v.v[k] = (T)((double)v.v[k] + (b * lr) / sqrt(v2n + fudge));
+        h2.v[k] = (T)h2n;
+        v2.v[k] = (T)v2n;
+      }
+    }
+    ((PT *)(row + 2 * D))[c] = h2;
+    ((PT *)(row + 3 * D))[c] = v2;
+    ((PT *)row)[c] = h;
+    ((PT *)(row + D))[c] = v;
+  }
+}
+
+template <typename T>
+__global__ void k_push_lr_multi(const uint32_t *__restrict__ rows_s, const uint32_t *__restrict__ pos_s, uint64_t n,
+                                uint32_t cap, const float *__restrict__ grads, T *__restrict__ rows, T lr, T fudge) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = rows_s[i];
+  if (r >= cap || (i > 0 && rows_s[i - 1] == r)) return;
+  T *row = rows + (uint64_t)r * 2;
+  T w = row[0], g2 = row[1];
+  for (uint64_t j = i; j < n && rows_s[j] == r; j++) {  // k_push_lr's steps, in source order
+    const T m = (T)grads[pos_s[j]];
+    g2 = g2 + m * m;
+    const T step = lr * m;
+    w = w + step / (T)sqrt(g2 + fudge);
+  }
+  row[1] = g2;
+  row[0] = w;
+}
+
 }  // namespace
 
 namespace swps {
@@ -341,6 +419,57 @@ int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const voi
     else
       k_push_lr<float><<<blocks_for(n), 256, 0, s>>>(d_rows, n, (const float *)d_grads, t->rows.as<float>(),
                                                      t->cfg.learning_rate, t->cfg.fudge);
+  }
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
+                       bool grads_f32) {
+  if (n == 0) return SWPS_OK;
+  if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 pushed keys in one call");
+  const uint32_t cap = (uint32_t)t->cfg.capacity;
+  int bits = 1;
+  while ((1ULL << bits) <= cap) bits++;
+  SWPS_TRY(t->push_scratch.ensure(n * 16));
+  uint32_t *key = t->push_scratch.as<uint32_t>(), *pos = key + n, *key_s = pos + n, *pos_s = key_s + n;
+  k_push_keys<<<blocks_for(n), 256, 0, s>>>(d_rows, n, cap, key, pos);
+  SWPS_HIP(hipGetLastError());
+  size_t sb = 0;
+  SWPS_HIP(sort_pairs(nullptr, sb, key, key_s, pos, pos_s, n, bits, s));
+  SWPS_TRY(t->sort_tmp.ensure(sb));
+  sb = t->sort_tmp.bytes;
+  SWPS_HIP(sort_pairs(t->sort_tmp.p, sb, key, key_s, pos, pos_s, n, bits, s));
+  if (t->cfg.layout == SWPS_LAYOUT_W2V) {
+    const double lr = (double)t->cfg.learning_rate, fudge = (double)t->cfg.fudge;
+    const int D = t->cfg.dim;
+    auto go = [&](auto *rows, const auto *g) {
+      using T = std::remove_pointer_t<decltype(rows)>;
+      using G = std::remove_cv_t<std::remove_pointer_t<decltype(g)>>;
+      constexpr int E = 16 / sizeof(T);
+      if (D % E == 0)
+        k_push_w2v_multi<T, G, E><<<blocks_for(n * 64), 256, 0, s>>>(key_s, pos_s, n, cap, g, rows, D, lr, fudge);
+      else
+        k_push_w2v_multi<T, G, 1><<<blocks_for(n * 64), 256, 0, s>>>(key_s, pos_s, n, cap, g, rows, D, lr, fudge);
+    };
+    if (t->cfg.dtype == SWPS_F64) {
+      if (grads_f32)
+        go(t->rows.as<double>(), (const float *)d_grads);
+      else
+        go(t->rows.as<double>(), (const double *)d_grads);
+    } else {
+      if (grads_f32)
+        go(t->rows.as<float>(), (const float *)d_grads);
+      else
+        go(t->rows.as<float>(), (const double *)d_grads);
+    }
+  } else if (t->cfg.dtype == SWPS_F64) {
+    k_push_lr_multi<double><<<blocks_for(n), 256, 0, s>>>(key_s, pos_s, n, cap, (const float *)d_grads,
+                                                          t->rows.as<double>(), (double)t->cfg.learning_rate,
+                                                          (double)t->cfg.fudge);
+  } else {
+    k_push_lr_multi<float><<<blocks_for(n), 256, 0, s>>>(key_s, pos_s, n, cap, (const float *)d_grads,
+                                                         t->rows.as<float>(), t->cfg.learning_rate, t->cfg.fudge);
   }
   SWPS_HIP(hipGetLastError());
   return SWPS_OK;

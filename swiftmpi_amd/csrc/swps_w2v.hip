@@ -2748,14 +2748,8 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
   SWPS_TRY(w->d_push_rows.ensure(std::max<uint64_t>(n, 1) * 4));
   SWPS_TRY(table_lookup(w->t, d_keys, n, w->d_push_rows.as<uint32_t>(), ss));
   const bool g32 = !w->f64 && !w->cfg.fp64_intermediates;  // fast mode: fp32 push payload
-  const size_t gsz = g32 ? 4 : 8;
-  uint64_t off = 0;
-  for (int r = 0; r < w->world; r++) {  // one AdaGrad step per source, in rank order
-    SWPS_TRY(table_push_rows(w->t, w->d_push_rows.as<uint32_t>() + off, src_counts[r],
-                             (const char *)d_grads + off * 2 * w->D * gsz, ss, g32));
-    off += src_counts[r];
-  }
-  return SWPS_OK;
+  // one AdaGrad step per source, in rank order, all sources in one pass
+  return table_push_sources(w->t, w->d_push_rows.as<uint32_t>(), n, d_grads, ss, g32);
 }
 
 }  // extern "C"

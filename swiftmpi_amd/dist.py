@@ -100,6 +100,7 @@ class _ShardedApp:
         self.frag_num = frag_num
         self.cursor = 0
         self._ext = None
+        self._xprof = None
 
     def _fn(self, name):
         return getattr(capi.lib(), "swps_%s_%s" % (self.pfx, name))
@@ -127,7 +128,37 @@ class _ShardedApp:
         # RCCL (or gloo's host staging) ordered after / before the library's
         # kernels on `stream`
         with torch.cuda.stream(stream):
-            return self.ex.a2a(send, sc, rc, width)
+            if self._xprof is None:
+                return self.ex.a2a(send, sc, rc, width)
+            # exchange accounting (bench.py's xGMI roofline): bytes this rank
+            # sends to other ranks, and the exchange's time on its stream
+            es = send.element_size() * width
+            remote = sum(int(c) for d, c in enumerate(sc) if d != self.rank) * es
+            self._xprof["bytes_remote"] += remote
+            self._xprof["bytes_total"] += int(sum(int(c) for c in sc)) * es
+            self._xprof["calls"] += 1
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            out = self.ex.a2a(send, sc, rc, width)
+            e1.record(stream)
+            self._xprof["events"].append((e0, e1))
+            return out
+
+    def set_exchange_profile(self, on):
+        """Count the bytes every all-to-all sends and time it with events on
+        its stream (off: no events in the exchange path)."""
+        self._xprof = {"bytes_remote": 0, "bytes_total": 0, "calls": 0, "events": [], "ms": 0.0} if on else None
+
+    def exchange_stats(self):
+        """{bytes_remote, bytes_total, calls, ms} since set_exchange_profile(True)."""
+        if self._xprof is None:
+            return None
+        torch.cuda.synchronize(self.dev)
+        x = self._xprof
+        x["ms"] += sum(a.elapsed_time(b) for a, b in x["events"])
+        x["events"] = []
+        return {k: x[k] for k in ("bytes_remote", "bytes_total", "calls", "ms")}
 
     def _empty(self, stream, n, dtype):
         with torch.cuda.stream(stream):
