@@ -10,6 +10,8 @@
  *   GlobalPullAccess<Key,Val,Grad>     parameter/global_pull_access.h:15-118
  *   GlobalPushAccess<Key,Val,Grad>     parameter/global_push_access.h:15-106
  *   Cluster<Worker,Server,Key>         cluster/cluster.h:9-140 (initialize/finalize)
+ *   ClusterServer<Key,Param,PullVal,Grad,PullM,PushM>  cluster/server.h:20-101
+ *   PullAccessMethod / PushAccessMethod parameter/accessmethod.h:7-35
  *   Word2VecApp                        apps/word2vec/word2vec_global.h:541-748 + w2v.cpp
  *   Sent2VecApp                        apps/sent2vec/sent2vec.cpp:14-257
  *   LRApp                              apps/logistic/lr.cpp:133-509
@@ -142,6 +144,54 @@ inline swps_table *&global_swps_table() {
   return t;
 }
 
+/* ---- parameter/accessmethod.h ---------------------------------------------
+ * The reference's server runs the app's access-method objects per key on
+ * the CPU; here the owner GPU applies one of the library's device rules to
+ * whole batches.  An app's access-method classes keep their reference shape
+ * (they may still derive from these bases and define init_param /
+ * get_pull_value / apply_push_value, which are not called) and select the
+ * device rule through two constants, inherited unless overridden:
+ *   PullM::init_mode = SWPS_INIT_HASH (or SWPS_INIT_ZERO)  (init_param)
+ *   PushM::push_rule = SWPS_PUSH_ADAGRAD (or SWPS_PUSH_SGD) (apply_push_value)
+ * AdaGrad is what all three reference apps implement
+ * (word2vec_global.h:176-185, lr.cpp:68-75). */
+template <typename Key, typename Param, typename PullVal> class PullAccessMethod {
+ public:
+  typedef Key key_t;
+  typedef Param param_t;
+  typedef PullVal pull_t;
+  static const int32_t init_mode = SWPS_INIT_HASH;
+  virtual ~PullAccessMethod() {}
+};
+template <typename Key, typename Param, typename Grad> class PushAccessMethod {
+ public:
+  typedef Key key_t;
+  typedef Param param_t;
+  typedef Grad grad_t;
+  static const int32_t push_rule = SWPS_PUSH_ADAGRAD;
+  virtual ~PushAccessMethod() {}
+};
+
+/* ---- cluster/server.h ClusterServer --------------------------------------
+ * The server half of a rank: its HBM shard's layout comes from the pull
+ * value's codec (PullCodec<PullVal>::layout), its miss initialisation and
+ * push rule from the access methods.  Cluster<Worker, ClusterServer<...>,
+ * Key> creates the shard; load() keeps the keys this rank owns
+ * (server.h:49-62). */
+template <typename Key, typename Param, typename PullVal, typename Grad, typename PullM, typename PushM>
+class ClusterServer {
+ public:
+  typedef Key key_t;
+  typedef Param param_t;
+  typedef PullVal pull_t;
+  typedef Grad grad_t;
+  typedef PullM pull_access_t;
+  typedef PushM push_access_t;
+  static int32_t layout() { return PullCodec<PullVal>::layout; }
+  static int32_t init_mode() { return PullM::init_mode; }
+  static int32_t push_rule() { return PushM::push_rule; }
+};
+
 /* ---- parameter/param.h ---------------------------------------------------- */
 template <typename Key, typename Param, typename Grad> class LocalParamCache {
  public:
@@ -171,8 +221,11 @@ template <typename Key, typename Param, typename Grad> class LocalParamCache {
 /* ---- parameter/global_pull_access.h --------------------------------------
  * pull_with_barrier: params[key] = pulled value, grads[key] reset
  * (global_pull_access.h:88-97).  Keys new to the shard are initialised by it
- * (accessmethod.h:63-70).  An empty key set returns at once (the reference
- * blocks forever, global_pull_access.h:33-42). */
+ * (accessmethod.h:63-70).  On a multi-rank Cluster the keys go to their
+ * BasicHashFrag owners inside the library (swps_table_route): every rank
+ * calls pull / push in the same sequence, an empty key set included (the
+ * reference blocks forever on one, global_pull_access.h:33-42; here it
+ * joins the exchange and returns). */
 template <typename Key, typename Val, typename Grad> class GlobalPullAccess {
  public:
   typedef LocalParamCache<Key, Val, Grad> param_cache_t;
@@ -181,7 +234,6 @@ template <typename Key, typename Val, typename Grad> class GlobalPullAccess {
   explicit GlobalPullAccess(swps_table *t = nullptr) : _t(t) {}
 
   void pull_with_barrier(const std::unordered_set<Key> &keys, param_cache_t &cache) {
-    if (keys.empty()) return;
     swps_table *t = _t ? _t : global_swps_table();
     if (!t) throw SwpsError(SWPS_E_STATE, "no shard: create a Cluster first");
     std::vector<uint64_t> k;
@@ -227,7 +279,7 @@ template <typename Key, typename Val, typename Grad> class GlobalPushAccess {
       g.resize(k.size() * (size_t)push);
       PushCodec<Grad>::encode(it->second, &g[(k.size() - 1) * push]);
     }
-    if (!k.empty()) swps_check(swps_push_h(t, k.data(), k.size(), g.data()));
+    swps_check(swps_push_h(t, k.data(), k.size(), g.data()));  // n = 0 still joins a routed exchange
   }
 
  private:
@@ -244,50 +296,97 @@ template <class Key, class Val, class Grad> GlobalPushAccess<Key, Val, Grad> &gl
 }
 
 /* ---- cluster/cluster.h ----------------------------------------------------
- * One process per GPU.  The shard's shape comes from the config keys the
- * reference's server reads: [word2vec] len_vec (W2V layout) and
- * [server] initial_learning_rate.  Rank / device from the launcher's
- * RANK / LOCAL_RANK (torchrun, mpirun -x) instead of MPI_Comm_rank. */
+ * One process per GPU.  Rank / world / device from the launcher's
+ * environment (torchrun: RANK, WORLD_SIZE, LOCAL_RANK; mpirun:
+ * OMPI_COMM_WORLD_RANK / _SIZE / _LOCAL_RANK) instead of MPI_Comm_rank.
+ * With world > 1 (or SWPS_ROUTE=1) the shard is key-sharded over a
+ * communicator (swps_table_route): RCCL over xGMI, its unique id
+ * bootstrapped over TCP at MASTER_ADDR:SWPS_BOOTSTRAP_PORT (default
+ * MASTER_PORT + 1), or SWPS_TRANSPORT=tcp for the library's TCP star
+ * (several ranks on one GPU).  frag_num = [server] frag_num (the
+ * reference's hash-frag size; 1000 when absent).  The shard's shape:
+ * [word2vec] len_vec (W2V layout) and [server] initial_learning_rate. */
 struct W2VServer {
   static int32_t layout() { return SWPS_LAYOUT_W2V; }
+  static int32_t init_mode() { return SWPS_INIT_HASH; }
+  static int32_t push_rule() { return SWPS_PUSH_ADAGRAD; }
 };
 struct LRServer {
   static int32_t layout() { return SWPS_LAYOUT_LR; }
+  static int32_t init_mode() { return SWPS_INIT_HASH; }
+  static int32_t push_rule() { return SWPS_PUSH_ADAGRAD; }
 };
 struct ClusterWorker {};
+
+inline int env_int(const char *a, const char *b, int dflt) {
+  const char *v = std::getenv(a);
+  if (!v && b) v = std::getenv(b);
+  return v ? std::atoi(v) : dflt;
+}
 
 template <class WorkerT, class ServerT, class KeyT> class Cluster {
  public:
   explicit Cluster(uint64_t capacity = 1u << 22, int32_t dtype = SWPS_F32) {
-    const char *lr = std::getenv("LOCAL_RANK");
+    _rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", 0);
+    _world = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1);
+    const int dev = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", 0);
     swps_table_cfg c;
-    c.device = lr ? std::atoi(lr) : 0;
+    c.device = dev;
     c.layout = ServerT::layout();
     c.dtype = dtype;
     c.dim = c.layout == SWPS_LAYOUT_W2V ? global_config().get("word2vec", "len_vec").to_int32() : 1;
     c.capacity = capacity;
     c.learning_rate = global_config().get("server", "initial_learning_rate").to_float();
     c.fudge = 1e-6f;
-    c.init_mode = SWPS_INIT_HASH;
+    c.init_mode = ServerT::init_mode();
     c.seed = 0;
+    c.push_rule = ServerT::push_rule();
     swps_check(swps_table_create(&c, &_t));
     global_swps_table() = _t;
+    if (_world > 1 || env_int("SWPS_ROUTE", nullptr, 0)) {
+      const char *addr = std::getenv("MASTER_ADDR");
+      const int port = env_int("SWPS_BOOTSTRAP_PORT", nullptr, env_int("MASTER_PORT", nullptr, 29500) + 1);
+      const int timeout = env_int("SWPS_BOOTSTRAP_TIMEOUT_MS", nullptr, 120000);
+      const char *tr = std::getenv("SWPS_TRANSPORT");
+      if (tr && std::string(tr) == "tcp") {
+        swps_check(swps_comm_create_tcp(addr ? addr : "127.0.0.1", port, _rank, _world, dev, timeout, &_comm));
+      } else {
+        std::vector<uint8_t> id(SWPS_COMM_ID_BYTES);
+        swps_check(swps_comm_bootstrap_tcp(addr ? addr : "127.0.0.1", port, _rank, _world, timeout, id.data()));
+        swps_check(swps_comm_create_rccl(id.data(), _rank, _world, dev, &_comm));
+      }
+      const int frag = global_config().has("server", "frag_num")
+                           ? global_config().get("server", "frag_num").to_int32()
+                           : 1000;
+      swps_check(swps_table_route(_t, _comm, frag));
+    }
   }
   ~Cluster() {
     if (global_swps_table() == _t) global_swps_table() = nullptr;
     swps_table_destroy(_t);
+    swps_comm_destroy(_comm);
   }
   void initialize() {}
-  /* SparseTable::output (sparsetable.h:127-132) to `path` */
+  /* The worker is done: keep serving the other ranks until all are
+   * (swps_finish), then SparseTable::output (sparsetable.h:127-132) of this
+   * rank's shard to `path` (world > 1: `path`.<rank>). */
   void finalize(const std::string &path = "") {
-    if (!path.empty()) swps_check(swps_dump(_t, path.c_str()));
+    swps_check(swps_finish(_t));
+    if (path.empty()) return;
+    const std::string p = _world > 1 ? path + "." + std::to_string(_rank) : path;
+    swps_check(swps_dump(_t, p.c_str()));
   }
   swps_table *table() { return _t; }
+  int rank() const { return _rank; }
+  int world() const { return _world; }
+  bool routed() const { return _comm != nullptr; }
 
  private:
   Cluster(const Cluster &);
   Cluster &operator=(const Cluster &);
   swps_table *_t = nullptr;
+  swps_comm *_comm = nullptr;
+  int _rank = 0, _world = 1;
 };
 
 /* ---- app level ------------------------------------------------------------ */

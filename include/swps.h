@@ -72,6 +72,12 @@ int swps_version(void);
 #define SWPS_INIT_ZERO 0
 #define SWPS_INIT_HASH 1 /* W2V: (u-0.5)/D, LR: u in [0,1); u from (seed,key,i) */
 
+/* push rule (PushAccessMethod::apply_push_value, accessmethod.h:26-35) */
+#define SWPS_PUSH_ADAGRAD 0 /* W2V word2vec_global.h:176-185, LR lr.cpp:68-75: g2 += g*g;
+                             * w += lr*g/sqrt(g2+fudge) — every reference app's rule */
+#define SWPS_PUSH_SGD 1     /* w += lr*g (the accumulators are left alone); PS level only:
+                             * the app contexts (swps_w2v_*, swps_lr_*) reject such tables */
+
 typedef struct swps_table swps_table;
 
 typedef struct {
@@ -84,6 +90,7 @@ typedef struct {
   float fudge;        /* AdaGrad fudge factor (reference: 1e-6f) */
   int32_t init_mode;  /* SWPS_INIT_* */
   uint64_t seed;
+  int32_t push_rule;  /* SWPS_PUSH_* (0 = AdaGrad) */
 } swps_table_cfg;
 
 int swps_table_create(const swps_table_cfg *cfg, swps_table **out);
@@ -106,6 +113,16 @@ int swps_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_g
  * (include/swiftmpi_compat.h: GlobalPullAccess / GlobalPushAccess). */
 int swps_pull_h(swps_table *t, const uint64_t *keys, uint64_t n, void *vals);
 int swps_push_h(swps_table *t, const uint64_t *keys, uint64_t n, const void *grads);
+/* Stream-ordered forms of swps_pull / swps_push on a local (unrouted) table:
+ * issued on `stream` (a hipStream_t of the table's device; NULL = the
+ * table's own stream) with no host sync.  Table-full / unknown-key errors are
+ * latched on the device and reported by the next swps_table_sync or
+ * swps_barrier.  The table's scratch buffers are shared: calls on different
+ * streams must be ordered by the caller (events).  A routed table
+ * (swps_table_route) needs the per-owner key counts on the host, so these
+ * forms sync once per call there, like swps_pull / swps_push. */
+int swps_pull_async(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals, void *stream);
+int swps_push_async(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads, void *stream);
 /* Overwrite / read full rows (table dtype, d_rows[n][row elems]). */
 int swps_assign(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_rows);
 int swps_export(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_rows);
@@ -132,6 +149,67 @@ uint64_t swps_bkdr(const char *s);                      /* utils/string.h:130-13
 int swps_hashfrag_table(int32_t frag_num, int32_t num_nodes, uint32_t *out); /* hashfrag.h:33-49 */
 int swps_to_node_id(const uint64_t *keys, uint64_t n, int32_t frag_num, const uint32_t *table,
                     int32_t *out);                      /* hashfrag.h:51-56 (host) */
+
+/* ---- communicator (replaces src/transfer + the MPI bootstrap) ------------
+ * One process per GPU.  Two transports:
+ *   RCCL (xGMI): swps_comm_create_rccl from a 128-byte unique id that rank 0
+ *     makes (swps_comm_unique_id) and the caller distributes — with
+ *     swps_comm_bootstrap_tcp (rank 0 serves it on addr:port; the launcher's
+ *     MASTER_ADDR / MASTER_PORT) or any channel of its own.  Payloads move
+ *     device to device with ncclSend / ncclRecv groups.
+ *   host: the caller's all-gather and all-to-all-v callbacks on host buffers
+ *     (MPI, gloo, sockets, ...); payloads are staged through host memory.
+ *     Lets several ranks share one GPU (RCCL refuses that). */
+typedef struct swps_comm swps_comm;
+#define SWPS_COMM_ID_BYTES 128
+typedef struct {
+  void *ctx;
+  /* every rank contributes `bytes` bytes; out receives world*bytes, rank order */
+  int (*allgather)(void *ctx, const void *in, void *out, uint64_t bytes);
+  /* send holds the blocks for ranks 0..world-1 back to back (send_bytes[r]
+   * each); recv receives the blocks from ranks 0..world-1 (recv_bytes[r]) */
+  int (*alltoallv)(void *ctx, const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes);
+} swps_transport;
+
+int swps_comm_unique_id(uint8_t *id); /* ncclGetUniqueId: one rank calls it */
+/* rank 0 makes the id and sends it to every other rank over TCP (it listens
+ * on port; the others connect to addr:port, retrying for up to timeout_ms);
+ * every rank returns with the same id */
+int swps_comm_bootstrap_tcp(const char *addr, int32_t port, int32_t rank, int32_t world, int32_t timeout_ms,
+                            uint8_t *id);
+int swps_comm_create_rccl(const uint8_t *id, int32_t rank, int32_t world, int32_t device, swps_comm **out);
+int swps_comm_create_host(const swps_transport *tr, int32_t rank, int32_t world, int32_t device, swps_comm **out);
+/* the library's own host transport: TCP, a star through rank 0 (it listens
+ * on addr:port; the others connect, retrying for up to timeout_ms).  For
+ * jobs without RCCL: several ranks on one GPU, host-only interconnects. */
+int swps_comm_create_tcp(const char *addr, int32_t port, int32_t rank, int32_t world, int32_t device,
+                         int32_t timeout_ms, swps_comm **out);
+int swps_comm_destroy(swps_comm *c);
+int swps_comm_info(swps_comm *c, int32_t *rank, int32_t *world);
+
+/* ---- key-sharded table (the GPU-to-shard map, src/cluster) --------------
+ * swps_table_route binds a local shard to a communicator: this table then
+ * serves the keys BasicHashFrag (hashfrag.h:33-56, S = world) maps to node
+ * rank+1, and swps_pull / swps_push / swps_pull_h / swps_push_h /
+ * swps_*_async become COLLECTIVE: keys are grouped by owner, exchanged
+ * (all-to-all-v), owners find-or-insert / apply the push rule, pull values
+ * come back in the caller's key order (GlobalPullAccess::pull_with_barrier,
+ * global_pull_access.h:46-107; GlobalPushAccess::push_with_barrier,
+ * global_push_access.h:48-96; the server handlers server.h:129-176).  An
+ * owner applies the pushes of several sources for one key as separate steps
+ * in source-rank order (the reference: one step per worker request).
+ * Every rank must make the same sequence of calls; n = 0 is allowed and
+ * still joins the exchange.  A rank whose worker is done calls swps_finish:
+ * it keeps serving the other ranks' pulls / pushes and returns once every
+ * rank has called it (the reference's servers outlive their workers). */
+int swps_table_route(swps_table *t, swps_comm *c, int32_t frag_num);
+int swps_finish(swps_table *t);
+/* routed: every rank's earlier calls on this table have retired (all ranks
+ * call it); local: swps_table_sync.  Reports latched device errors. */
+int swps_barrier(swps_table *t);
+/* routed-call counters: [rounds, keys sent, keys sent to other ranks,
+ * payload bytes sent, payload bytes sent to other ranks, keys served] */
+int swps_route_stats(swps_table *t, uint64_t *out6);
 
 /* ---- word2vec CBOW negative sampling (apps/word2vec) --------------------- */
 typedef struct swps_w2v swps_w2v;

@@ -121,10 +121,11 @@ class Table:
     """One HBM parameter shard (SparseTable + server access methods)."""
 
     def __init__(self, layout="w2v", dim=100, capacity=1 << 20, dtype="f32", learning_rate=0.7, fudge=1e-6,
-                 init="hash", seed=0, device=0):
+                 init="hash", seed=0, device=0, push_rule="adagrad"):
         cfg = capi.TableCfg(device, capi.LAYOUT_W2V if layout == "w2v" else capi.LAYOUT_LR,
                             capi.F64 if dtype == "f64" else capi.F32, dim, capacity, learning_rate, fudge,
-                            capi.INIT_HASH if init == "hash" else capi.INIT_ZERO, seed)
+                            capi.INIT_HASH if init == "hash" else capi.INIT_ZERO, seed,
+                            {"adagrad": capi.PUSH_ADAGRAD, "sgd": capi.PUSH_SGD}[push_rule])
         h = ctypes.c_void_p()
         check(capi.lib().swps_table_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -199,6 +200,35 @@ class Table:
         """Assign the rows of a swps_save snapshot (node_id's keys only when
         world > 1, as `load`); the file is verified before any row changes."""
         check(capi.lib().swps_restore(self.h, path.encode(), frag_num, world, node_id))
+
+    # ---- key-sharded mode (swps_table_route): pull / push become collective ----
+    def route(self, comm, frag_num=1000):
+        check(capi.lib().swps_table_route(self.h, comm.h, frag_num))
+        self._comm = comm  # the communicator must outlive the routed table
+
+    def finish(self):
+        check(capi.lib().swps_finish(self.h))
+
+    def barrier(self):
+        check(capi.lib().swps_barrier(self.h))
+
+    def route_stats(self):
+        out = np.zeros(6, dtype=np.uint64)
+        check(capi.lib().swps_route_stats(self.h, ptr(out)))
+        return dict(zip(["rounds", "keys_sent", "keys_remote", "bytes_sent", "bytes_remote", "keys_served"],
+                        (int(x) for x in out)))
+
+    def pull_h(self, keys):
+        """Host keys (uint64) -> host pull values in the wire type (W2V fp64, LR fp32)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros((len(keys), self.pull_elems), dtype=np.float64 if self.layout == "w2v" else np.float32)
+        check(capi.lib().swps_pull_h(self.h, ptr(keys), len(keys), ptr(out)))
+        return out
+
+    def push_h(self, keys, grads):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        grads = np.ascontiguousarray(grads, dtype=np.float64 if self.layout == "w2v" else np.float32)
+        check(capi.lib().swps_push_h(self.h, ptr(keys), len(keys), ptr(grads)))
 
 
 KT_NAMES = ["plan", "forward", "sort", "gather", "push", "pull", "records"]

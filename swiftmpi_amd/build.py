@@ -24,7 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # before the add (x86-64 without FMA); contracting into fma would change bits.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}", "-I" + INCLUDE, "-I" + CSRC,
           "-Wall", "-Wno-unused-result"]
-LDFLAGS = ["-shared", f"--offload-arch={ARCH}"]
+LDFLAGS = ["-shared", f"--offload-arch={ARCH}", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def sources():
@@ -62,6 +62,8 @@ def build(force=False, verbose=False):
     os.makedirs(LIBDIR, exist_ok=True)
     srcs = sources()
     hdrs = headers()
+    if not force and not _stale(LIB, srcs + hdrs):
+        return LIB  # the in-tree library is newer than every source (e.g. on the GPU box: no build/ there)
     todo = [s for s in srcs if force or _stale(_obj(s), [s] + hdrs)]
     if todo:
         workers = min(len(todo), int(os.environ.get("MAX_JOBS", "8")), 16)

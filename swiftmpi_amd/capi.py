@@ -19,6 +19,13 @@ F32, F64 = 0, 1
 INIT_ZERO, INIT_HASH = 0, 1
 KEY_BKDR, KEY_ATOI = 0, 1
 W2V_INIT_REF, W2V_INIT_TABLE = 0, 1
+PUSH_ADAGRAD, PUSH_SGD = 0, 1
+COMM_ID_BYTES = 128
+
+# swps_transport callbacks (host all-gather / all-to-all-v)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
 
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -33,7 +40,12 @@ class SwpsError(RuntimeError):
 
 class TableCfg(ctypes.Structure):
     _fields_ = [("device", _i32), ("layout", _i32), ("dtype", _i32), ("dim", _i32), ("capacity", _u64),
-                ("learning_rate", ctypes.c_float), ("fudge", ctypes.c_float), ("init_mode", _i32), ("seed", _u64)]
+                ("learning_rate", ctypes.c_float), ("fudge", ctypes.c_float), ("init_mode", _i32), ("seed", _u64),
+                ("push_rule", _i32)]
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
 class W2VCfg(ctypes.Structure):
@@ -65,6 +77,19 @@ PROTOS = {
     "swps_pull": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_push": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_pull_h": (ctypes.c_int, [_p, _p, _u64, _p]),
+    "swps_pull_async": (ctypes.c_int, [_p, _p, _u64, _p, _p]),
+    "swps_push_async": (ctypes.c_int, [_p, _p, _u64, _p, _p]),
+    "swps_comm_unique_id": (ctypes.c_int, [_p]),
+    "swps_comm_bootstrap_tcp": (ctypes.c_int, [ctypes.c_char_p, _i32, _i32, _i32, _i32, _p]),
+    "swps_comm_create_rccl": (ctypes.c_int, [_p, _i32, _i32, _i32, ctypes.POINTER(_p)]),
+    "swps_comm_create_host": (ctypes.c_int, [ctypes.POINTER(Transport), _i32, _i32, _i32, ctypes.POINTER(_p)]),
+    "swps_comm_create_tcp": (ctypes.c_int, [ctypes.c_char_p, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_p)]),
+    "swps_comm_destroy": (ctypes.c_int, [_p]),
+    "swps_comm_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "swps_table_route": (ctypes.c_int, [_p, _p, _i32]),
+    "swps_finish": (ctypes.c_int, [_p]),
+    "swps_barrier": (ctypes.c_int, [_p]),
+    "swps_route_stats": (ctypes.c_int, [_p, _p]),
     "swps_push_h": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_assign": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_export": (ctypes.c_int, [_p, _p, _u64, _p]),

@@ -1,0 +1,82 @@
+"""Communicators for the library's own key-sharded table (swps_comm_*,
+swps_table_route): RCCL from a bootstrap, or a host transport whose
+all-gather / all-to-all-v callbacks run over a torch.distributed process
+group (gloo: several ranks sharing one GPU in tests — RCCL refuses that).
+
+The library issues the exchanges itself (include/swps.h "communicator");
+this module only builds the handle."""
+import ctypes
+import traceback
+
+import numpy as np
+
+from . import capi
+from .capi import check
+
+
+class Comm:
+    def __init__(self, handle, rank, world, keep=()):
+        self.h = handle
+        self.rank, self.world = rank, world
+        self._keep = keep  # ctypes callbacks must outlive the handle
+
+    @classmethod
+    def rccl(cls, rank, world, device=0, addr="127.0.0.1", port=29611, timeout_ms=60000):
+        """RCCL communicator; rank 0 serves the unique id over TCP (addr:port)."""
+        uid = (ctypes.c_uint8 * capi.COMM_ID_BYTES)()
+        check(capi.lib().swps_comm_bootstrap_tcp(addr.encode(), port, rank, world, timeout_ms, uid))
+        h = ctypes.c_void_p()
+        check(capi.lib().swps_comm_create_rccl(uid, rank, world, device, ctypes.byref(h)))
+        return cls(h, rank, world)
+
+    @classmethod
+    def host(cls, group=None, device=0):
+        """Host transport over a torch.distributed group (gloo)."""
+        import torch
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+
+        def allgather(_ctx, src, dst, nbytes):
+            try:
+                t = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(src)).copy())
+                outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(outs, t, group=group)
+                flat = torch.cat(outs).numpy()
+                ctypes.memmove(dst, flat.ctypes.data, flat.size)
+                return 0
+            except Exception:  # noqa: BLE001 — an exception must not cross the C boundary
+                traceback.print_exc()
+                return 1
+
+        def alltoallv(_ctx, src, sbytes, dst, rbytes):
+            try:
+                sb = [int(sbytes[r]) for r in range(world)]
+                rb = [int(rbytes[r]) for r in range(world)]
+                n = sum(sb)
+                send = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * max(n, 1)).from_address(src))[:n].copy())
+                recv = torch.empty(sum(rb), dtype=torch.uint8)
+                dist.all_to_all_single(recv, send, rb, sb, group=group)
+                if recv.numel():
+                    ctypes.memmove(dst, recv.numpy().ctypes.data, recv.numel())
+                return 0
+            except Exception:  # noqa: BLE001
+                traceback.print_exc()
+                return 1
+
+        ag = capi.ALLGATHER_FN(allgather)
+        a2a = capi.ALLTOALLV_FN(alltoallv)
+        tr = capi.Transport(None, ag, a2a)
+        h = ctypes.c_void_p()
+        check(capi.lib().swps_comm_create_host(ctypes.byref(tr), rank, world, device, ctypes.byref(h)))
+        return cls(h, rank, world, keep=(ag, a2a, tr))
+
+    def close(self):
+        if getattr(self, "h", None):
+            capi.lib().swps_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except (AttributeError, TypeError):
+            pass

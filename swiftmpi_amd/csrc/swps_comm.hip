@@ -1,0 +1,648 @@
+// Communicator and key-sharded table: the reference's src/transfer (ZeroMQ
+// request/response, transfer.h:86-241), src/cluster (rank <-> server route,
+// hashfrag.h:33-56) and the server's pull / push handlers (server.h:129-176)
+// as owner-routed all-to-all exchanges, issued by the library itself:
+//   RCCL (ncclSend / ncclRecv groups over xGMI, device buffers, on the
+//   table's stream), or the caller's host callbacks (payloads staged
+//   through host memory: several ranks on one GPU, CPU-side transports).
+//
+// One routed call = one "round":
+//   1. owner of each key = BasicHashFrag node - 1 (k_owner); a stable radix
+//      sort by owner groups the keys (position order kept inside a group);
+//      per-owner counts come back to the host (the only sync of a round)
+//   2. header all-gather {op, counts[world]} from every rank: each rank
+//      learns what it receives and checks that all active ranks agree on the
+//      op (a rank inside swps_finish contributes op FINISH and no keys)
+//   3. all-to-all-v of keys (and, for a push, of the mean gradients)
+//   4. owners: find-or-insert + pull values (pull) or lookup + the push rule
+//      applied per source in rank order (push; table_push_sources)
+//   5. pull: all-to-all-v of the values back, un-permuted to key order.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <memory>
+#include <thread>
+
+#include "swps_internal.h"
+#include "swps_sort.h"
+
+using namespace swps;
+
+struct TcpStar;
+struct swps_comm {
+  int32_t rank = 0, world = 1, device = 0;
+  bool rccl = false;
+  ncclComm_t nc = nullptr;
+  swps_transport tr{};
+  TcpStar *tcp = nullptr;  // swps_comm_create_tcp's transport state (owned)
+  DevMem d_hdr;  // RCCL header all-gather buffers
+};
+
+namespace {
+
+enum { kOpPull = 0, kOpPush = 1, kOpFinish = 2 };
+
+#define SWPS_NCCL(call)                                                                                   \
+  do {                                                                                                    \
+    ncclResult_t r_ = (call);                                                                             \
+    if (r_ != ncclSuccess) return ::swps::fail(SWPS_E_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+inline unsigned nblocks(uint64_t threads, unsigned bs = 256) {
+  return (unsigned)std::max<uint64_t>(1, (threads + bs - 1) / bs);
+}
+
+// owner rank of each key: node_id(key) - 1 (hashfrag.h:51-56)
+__global__ void k_owner(const uint64_t *__restrict__ keys, uint64_t n, const uint32_t *__restrict__ map,
+                        uint32_t frag_num, uint32_t *__restrict__ owner, uint32_t *__restrict__ pos) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  owner[i] = map[fmix64(keys[i]) % frag_num] - 1;
+  pos[i] = (uint32_t)i;
+}
+
+// per-owner counts of the owner-sorted keys (one thread per owner, binary search)
+__global__ void k_owner_counts(const uint32_t *__restrict__ owner_s, uint64_t n, int world,
+                               uint64_t *__restrict__ cnt) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= world) return;
+  auto lower = [&](uint32_t v) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (owner_s[mid] < v)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return lo;
+  };
+  cnt[r] = lower((uint32_t)r + 1) - lower((uint32_t)r);
+}
+
+// out[i] = in[perm[i]] for rows of wb bytes (16-B, 4-B or byte lanes)
+__global__ void k_gather_rows(const uint32_t *__restrict__ perm, uint64_t n, const char *__restrict__ in,
+                              char *__restrict__ out, uint64_t wb) {
+  const uint64_t row = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const char *src = in + (uint64_t)perm[row] * wb;
+  char *dst = out + row * wb;
+  if (wb % 16 == 0) {
+    for (uint64_t c = lane; c < wb / 16; c += 64) ((uint4 *)dst)[c] = ((const uint4 *)src)[c];
+  } else if (wb % 4 == 0) {
+    for (uint64_t c = lane; c < wb / 4; c += 64) ((uint32_t *)dst)[c] = ((const uint32_t *)src)[c];
+  } else {
+    for (uint64_t c = lane; c < wb; c += 64) dst[c] = src[c];
+  }
+}
+
+// out[perm[i]] = in[i]
+__global__ void k_scatter_rows(const uint32_t *__restrict__ perm, uint64_t n, const char *__restrict__ in,
+                               char *__restrict__ out, uint64_t wb) {
+  const uint64_t row = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const char *src = in + row * wb;
+  char *dst = out + (uint64_t)perm[row] * wb;
+  if (wb % 16 == 0) {
+    for (uint64_t c = lane; c < wb / 16; c += 64) ((uint4 *)dst)[c] = ((const uint4 *)src)[c];
+  } else if (wb % 4 == 0) {
+    for (uint64_t c = lane; c < wb / 4; c += 64) ((uint32_t *)dst)[c] = ((const uint32_t *)src)[c];
+  } else {
+    for (uint64_t c = lane; c < wb; c += 64) dst[c] = src[c];
+  }
+}
+
+// all-gather of a small host block (the round header)
+int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipStream_t s) {
+  if (c->world == 1) {
+    memcpy(out, in, bytes);
+    return SWPS_OK;
+  }
+  if (!c->rccl) {
+    if (c->tr.allgather(c->tr.ctx, in, out, bytes) != 0) return fail(SWPS_E_RCCL, "host transport all-gather failed");
+    return SWPS_OK;
+  }
+  SWPS_TRY(c->d_hdr.ensure(bytes * (c->world + 1)));
+  char *d = c->d_hdr.as<char>();
+  SWPS_HIP(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, s));
+  SWPS_NCCL(ncclAllGather(d, d + bytes, bytes, ncclChar, c->nc, s));
+  SWPS_HIP(hipMemcpyAsync(out, d + bytes, bytes * c->world, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  return SWPS_OK;
+}
+
+// all-to-all-v of device buffers (byte counts per peer, blocks in rank order)
+int comm_alltoallv(swps_table *t, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
+                   const std::vector<uint64_t> &rb, hipStream_t s) {
+  swps_comm *c = t->comm;
+  uint64_t st = 0, rt = 0;
+  for (int r = 0; r < c->world; r++) {
+    st += sb[r];
+    rt += rb[r];
+  }
+  if (c->world == 1) {
+    if (st) SWPS_HIP(hipMemcpyAsync(d_recv, d_send, st, hipMemcpyDeviceToDevice, s));
+    return SWPS_OK;
+  }
+  if (c->rccl) {
+    SWPS_NCCL(ncclGroupStart());
+    uint64_t so = 0, ro = 0;
+    for (int r = 0; r < c->world; r++) {
+      if (sb[r]) SWPS_NCCL(ncclSend((const char *)d_send + so, sb[r], ncclChar, r, c->nc, s));
+      if (rb[r]) SWPS_NCCL(ncclRecv((char *)d_recv + ro, rb[r], ncclChar, r, c->nc, s));
+      so += sb[r];
+      ro += rb[r];
+    }
+    SWPS_NCCL(ncclGroupEnd());
+    return SWPS_OK;
+  }
+  t->h_send.resize(std::max<uint64_t>(st, 1));
+  t->h_recv.resize(std::max<uint64_t>(rt, 1));
+  if (st) SWPS_HIP(hipMemcpyAsync(t->h_send.data(), d_send, st, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  if (c->tr.alltoallv(c->tr.ctx, t->h_send.data(), sb.data(), t->h_recv.data(), rb.data()) != 0)
+    return fail(SWPS_E_RCCL, "host transport all-to-all-v failed");
+  if (rt) SWPS_HIP(hipMemcpyAsync(d_recv, t->h_recv.data(), rt, hipMemcpyHostToDevice, s));
+  SWPS_HIP(hipStreamSynchronize(s));  // h_recv is reused by the next exchange
+  return SWPS_OK;
+}
+
+// One round.  op: kOpPull (d_io = values out, table dtype [n][pull elems]),
+// kOpPush (d_io = mean gradients in, the push wire type [n][push elems]) or
+// kOpFinish (n = 0).  Returns the op every active rank ran (or kOpFinish when
+// all ranks are finishing) in *ran.
+int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void *d_io, hipStream_t s, int *ran) {
+  swps_comm *c = t->comm;
+  const int world = c->world;
+  const size_t pb = (size_t)t->pull_elems * t->esize;
+  const size_t gb = (size_t)t->push_elems * (t->cfg.layout == SWPS_LAYOUT_W2V ? 8 : 4);
+  if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 keys in one routed call");
+  // ---- 1. group by owner ----
+  std::vector<int64_t> hdr(2 + world, 0);
+  hdr[0] = op;
+  uint32_t *perm = nullptr;
+  uint64_t *keys_s = nullptr;
+  if (n) {
+    SWPS_TRY(t->r_owner.ensure(n * 4));
+    SWPS_TRY(t->r_pos.ensure(n * 4));
+    SWPS_TRY(t->r_owner_s.ensure(n * 4));
+    SWPS_TRY(t->r_perm.ensure(n * 4));
+    SWPS_TRY(t->r_keys.ensure(n * 8));
+    SWPS_TRY(t->r_cnt.ensure(world * 8));
+    k_owner<<<nblocks(n), 256, 0, s>>>(d_keys, n, t->frag_map.as<uint32_t>(), (uint32_t)t->frag_num,
+                                        t->r_owner.as<uint32_t>(), t->r_pos.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+    int bits = 1;
+    while ((1 << bits) < world) bits++;
+    size_t sb = 0;
+    SWPS_HIP(sort_pairs(nullptr, sb, t->r_owner.as<uint32_t>(), t->r_owner_s.as<uint32_t>(), t->r_pos.as<uint32_t>(),
+                        t->r_perm.as<uint32_t>(), n, bits, s));
+    SWPS_TRY(t->r_tmp.ensure(sb));
+    sb = t->r_tmp.bytes;
+    SWPS_HIP(sort_pairs(t->r_tmp.p, sb, t->r_owner.as<uint32_t>(), t->r_owner_s.as<uint32_t>(),
+                        t->r_pos.as<uint32_t>(), t->r_perm.as<uint32_t>(), n, bits, s));
+    perm = t->r_perm.as<uint32_t>();
+    keys_s = t->r_keys.as<uint64_t>();
+    k_gather_rows<<<nblocks(n * 64), 256, 0, s>>>(perm, n, (const char *)d_keys, (char *)keys_s, 8);
+    k_owner_counts<<<nblocks(world), 256, 0, s>>>(t->r_owner_s.as<uint32_t>(), n, world, t->r_cnt.as<uint64_t>());
+    SWPS_HIP(hipGetLastError());
+    SWPS_HIP(hipMemcpyAsync(hdr.data() + 2, t->r_cnt.p, world * 8, hipMemcpyDeviceToHost, s));
+    SWPS_HIP(hipStreamSynchronize(s));
+  }
+  // ---- 2. header all-gather ----
+  std::vector<int64_t> all((size_t)world * (2 + world));
+  SWPS_TRY(comm_allgather(c, hdr.data(), all.data(), (2 + world) * 8, s));
+  int agreed = kOpFinish;
+  for (int r = 0; r < world; r++) {
+    const int o = (int)all[(size_t)r * (2 + world)];
+    if (o == kOpFinish) continue;
+    if (agreed != kOpFinish && agreed != o)
+      return fail(SWPS_E_STATE, "ranks disagree on the routed call (one pulls while another pushes)");
+    agreed = o;
+  }
+  *ran = agreed;
+  if (agreed == kOpFinish) return SWPS_OK;
+  if (op != kOpFinish && op != agreed) return fail(SWPS_E_STATE, "ranks disagree on the routed call");
+  std::vector<uint64_t> send_k(world), recv_k(world);
+  uint64_t nrecv = 0, remote = 0;
+  for (int r = 0; r < world; r++) {
+    send_k[r] = (uint64_t)all[(size_t)c->rank * (2 + world) + 2 + r];
+    recv_k[r] = (uint64_t)all[(size_t)r * (2 + world) + 2 + c->rank];
+    nrecv += recv_k[r];
+    if (r != c->rank) remote += send_k[r];
+  }
+  // ---- 3. keys (+ gradients) to their owners ----
+  SWPS_TRY(t->r_rkeys.ensure(std::max<uint64_t>(nrecv, 1) * 8));
+  auto scaled = [&](const std::vector<uint64_t> &k, uint64_t w) {
+    std::vector<uint64_t> b(world);
+    for (int r = 0; r < world; r++) b[r] = k[r] * w;
+    return b;
+  };
+  SWPS_TRY(comm_alltoallv(t, keys_s, scaled(send_k, 8), t->r_rkeys.p, scaled(recv_k, 8), s));
+  const size_t vb = agreed == kOpPull ? pb : gb;
+  SWPS_TRY(t->r_rows.ensure(std::max<uint64_t>(nrecv, 1) * 4));
+  SWPS_TRY(t->r_rbuf.ensure(std::max<uint64_t>(nrecv, 1) * vb));
+  SWPS_TRY(t->r_buf.ensure(std::max<uint64_t>(n, 1) * vb));
+  t->rstats[0]++;
+  t->rstats[1] += n;
+  t->rstats[2] += remote;
+  t->rstats[5] += nrecv;
+  if (agreed == kOpPush) {
+    if (n) k_gather_rows<<<nblocks(n * 64), 256, 0, s>>>(perm, n, (const char *)d_io, t->r_buf.as<char>(), gb);
+    SWPS_HIP(hipGetLastError());
+    SWPS_TRY(comm_alltoallv(t, t->r_buf.p, scaled(send_k, gb), t->r_rbuf.p, scaled(recv_k, gb), s));
+    t->rstats[3] += n * (8 + gb);
+    t->rstats[4] += remote * (8 + gb);
+    // ---- 4. owner: the push rule, one step per source in rank order ----
+    if (nrecv) {
+      SWPS_TRY(table_lookup(t, t->r_rkeys.as<uint64_t>(), nrecv, t->r_rows.as<uint32_t>(), s));
+      SWPS_TRY(table_push_sources(t, t->r_rows.as<uint32_t>(), nrecv, t->r_rbuf.p, s));
+    }
+    return SWPS_OK;
+  }
+  // ---- 4. owner: find-or-insert (init_param on a miss) + pull values ----
+  if (nrecv) {
+    SWPS_TRY(table_find_or_insert(t, t->r_rkeys.as<uint64_t>(), nrecv, t->r_rows.as<uint32_t>(), s));
+    SWPS_TRY(table_copy_pull(t, t->r_rows.as<uint32_t>(), nrecv, t->r_rbuf.p, s));
+  }
+  // ---- 5. values back to the requesters, then to the caller's key order ----
+  SWPS_TRY(comm_alltoallv(t, t->r_rbuf.p, scaled(recv_k, pb), t->r_buf.p, scaled(send_k, pb), s));
+  t->rstats[3] += n * 8 + nrecv * pb;
+  t->rstats[4] += remote * 8;
+  for (int r = 0; r < world; r++)
+    if (r != c->rank) t->rstats[4] += recv_k[r] * pb;
+  if (n) k_scatter_rows<<<nblocks(n * 64), 256, 0, s>>>(perm, n, t->r_buf.as<char>(), (char *)d_io, pb);
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
+int tcp_send_all(int fd, const void *p, size_t n) {
+  const char *b = (const char *)p;
+  while (n) {
+    const ssize_t k = ::send(fd, b, n, MSG_NOSIGNAL);
+    if (k <= 0) return -1;
+    b += k;
+    n -= (size_t)k;
+  }
+  return 0;
+}
+
+int tcp_recv_all(int fd, void *p, size_t n, int timeout_ms) {
+  char *b = (char *)p;
+  while (n) {
+    pollfd pf{fd, POLLIN, 0};
+    if (::poll(&pf, 1, timeout_ms) <= 0) return -1;
+    const ssize_t k = ::recv(fd, b, n, 0);
+    if (k <= 0) return -1;
+    b += k;
+    n -= (size_t)k;
+  }
+  return 0;
+}
+
+// ---- native TCP host transport (swps_comm_create_tcp) ----------------------
+// A star through rank 0: every rank keeps one socket to rank 0, which
+// relays the all-gather and the all-to-all-v blocks.  For jobs without RCCL
+// (several ranks on one GPU — RCCL refuses duplicate devices — or host-only
+// interconnects); the exchanges of a routed table are small next to its
+// compute at the sizes this is meant for.
+}  // namespace
+
+struct TcpStar {
+  int rank = 0, world = 1;
+  std::vector<int> fd;  // rank 0: fd[r] for r >= 1; others: fd[0] = the socket to rank 0
+  int timeout_ms = 600000;
+  ~TcpStar() {
+    for (int f : fd)
+      if (f >= 0) ::close(f);
+  }
+};
+
+namespace {
+
+int star_allgather(void *ctx, const void *in, void *out, uint64_t bytes) {
+  TcpStar *t = (TcpStar *)ctx;
+  char *o = (char *)out;
+  if (t->rank != 0) {
+    if (tcp_send_all(t->fd[0], in, bytes)) return 1;
+    return tcp_recv_all(t->fd[0], o, bytes * t->world, t->timeout_ms) ? 1 : 0;
+  }
+  memcpy(o, in, bytes);
+  for (int r = 1; r < t->world; r++)
+    if (tcp_recv_all(t->fd[r], o + (uint64_t)r * bytes, bytes, t->timeout_ms)) return 1;
+  for (int r = 1; r < t->world; r++)
+    if (tcp_send_all(t->fd[r], o, bytes * t->world)) return 1;
+  return 0;
+}
+
+int star_alltoallv(void *ctx, const void *send, const uint64_t *sb, void *recv, const uint64_t *rb) {
+  TcpStar *t = (TcpStar *)ctx;
+  const int W = t->world;
+  uint64_t st = 0, rt = 0;
+  for (int r = 0; r < W; r++) {
+    st += sb[r];
+    rt += rb[r];
+  }
+  if (t->rank != 0) {
+    if (tcp_send_all(t->fd[0], sb, W * 8) || (st && tcp_send_all(t->fd[0], send, st))) return 1;
+    return (rt && tcp_recv_all(t->fd[0], recv, rt, t->timeout_ms)) ? 1 : 0;
+  }
+  // rank 0: every source's counts and payload, then each destination's blocks in source order
+  std::vector<std::vector<uint64_t>> cnt(W, std::vector<uint64_t>(W));
+  std::vector<std::vector<char>> pay(W);
+  cnt[0].assign(sb, sb + W);
+  pay[0].assign((const char *)send, (const char *)send + st);
+  for (int r = 1; r < W; r++) {
+    if (tcp_recv_all(t->fd[r], cnt[r].data(), W * 8, t->timeout_ms)) return 1;
+    uint64_t n = 0;
+    for (int d = 0; d < W; d++) n += cnt[r][d];
+    pay[r].resize(n);
+    if (n && tcp_recv_all(t->fd[r], pay[r].data(), n, t->timeout_ms)) return 1;
+  }
+  std::vector<uint64_t> off(W, 0);  // per source: offset of its block for destination d
+  for (int d = 0; d < W; d++) {
+    std::vector<char> blk;
+    for (int src = 0; src < W; src++) {
+      uint64_t o = 0;
+      for (int k = 0; k < d; k++) o += cnt[src][k];
+      blk.insert(blk.end(), pay[src].begin() + o, pay[src].begin() + o + cnt[src][d]);
+    }
+    if (d == 0) {
+      if (blk.size() != rt) return 1;
+      if (rt) memcpy(recv, blk.data(), rt);
+    } else if (!blk.empty() && tcp_send_all(t->fd[d], blk.data(), blk.size())) {
+      return 1;
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+namespace swps {
+
+int routed_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals, hipStream_t s) {
+  if (t->finished) return fail(SWPS_E_STATE, "pull after swps_finish");
+  int ran = 0;
+  SWPS_TRY(route_round(t, kOpPull, d_keys, n, d_vals, s, &ran));
+  if (ran != kOpPull) return fail(SWPS_E_STATE, "routed pull while every other rank has finished");
+  return SWPS_OK;
+}
+
+int routed_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads, hipStream_t s) {
+  if (t->finished) return fail(SWPS_E_STATE, "push after swps_finish");
+  int ran = 0;
+  SWPS_TRY(route_round(t, kOpPush, d_keys, n, const_cast<void *>(d_grads), s, &ran));
+  if (ran != kOpPush) return fail(SWPS_E_STATE, "routed push while every other rank has finished");
+  return SWPS_OK;
+}
+
+}  // namespace swps
+
+extern "C" {
+
+int swps_comm_unique_id(uint8_t *id) {
+  if (!id) return fail(SWPS_E_CFG, "null id");
+  ncclUniqueId u;
+  SWPS_NCCL(ncclGetUniqueId(&u));
+  memcpy(id, u.internal, SWPS_COMM_ID_BYTES);
+  return SWPS_OK;
+}
+
+int swps_comm_bootstrap_tcp(const char *addr, int32_t port, int32_t rank, int32_t world, int32_t timeout_ms,
+                            uint8_t *id) {
+  if (!addr || !id || world < 1 || rank < 0 || rank >= world || port <= 0 || port > 65535)
+    return fail(SWPS_E_CFG, "bad bootstrap arguments");
+  if (world == 1) return swps_comm_unique_id(id);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons((uint16_t)port);
+  if (inet_pton(AF_INET, addr, &sa.sin_addr) != 1) return fail(SWPS_E_CFG, std::string("bad IPv4 address ") + addr);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  if (rank == 0) {
+    SWPS_TRY(swps_comm_unique_id(id));
+    const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (ls < 0) return fail(SWPS_E_IO, "socket");
+    const int one = 1;
+    setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    if (::bind(ls, (sockaddr *)&sa, sizeof(sa)) != 0 || ::listen(ls, world) != 0) {
+      ::close(ls);
+      return fail(SWPS_E_IO, "bootstrap: cannot listen on " + std::string(addr) + ":" + std::to_string(port));
+    }
+    int served = 0, rc = SWPS_OK;
+    while (served < world - 1) {
+      const int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
+                           deadline - std::chrono::steady_clock::now()).count();
+      pollfd pf{ls, POLLIN, 0};
+      if (left <= 0 || ::poll(&pf, 1, left) <= 0) {
+        rc = fail(SWPS_E_IO, "bootstrap: timed out waiting for ranks");
+        break;
+      }
+      const int fd = ::accept(ls, nullptr, nullptr);
+      if (fd < 0) continue;
+      const int bad = tcp_send_all(fd, id, SWPS_COMM_ID_BYTES);
+      ::close(fd);
+      if (bad) {
+        rc = fail(SWPS_E_IO, "bootstrap: send failed");
+        break;
+      }
+      served++;
+    }
+    ::close(ls);
+    return rc;
+  }
+  for (;;) {
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) return fail(SWPS_E_IO, "socket");
+    if (::connect(fd, (sockaddr *)&sa, sizeof(sa)) == 0) {
+      const int bad = tcp_recv_all(fd, id, SWPS_COMM_ID_BYTES, std::max(timeout_ms, 1));
+      ::close(fd);
+      if (bad) return fail(SWPS_E_IO, "bootstrap: receive failed");
+      return SWPS_OK;
+    }
+    ::close(fd);
+    if (std::chrono::steady_clock::now() >= deadline)
+      return fail(SWPS_E_IO, "bootstrap: cannot reach rank 0 at " + std::string(addr) + ":" + std::to_string(port));
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
+}
+
+int swps_comm_create_rccl(const uint8_t *id, int32_t rank, int32_t world, int32_t device, swps_comm **out) {
+  if (!id || !out || world < 1 || rank < 0 || rank >= world) return fail(SWPS_E_CFG, "bad communicator arguments");
+  *out = nullptr;
+  SWPS_HIP(hipSetDevice(device));
+  ncclUniqueId u;
+  memcpy(u.internal, id, SWPS_COMM_ID_BYTES);
+  ncclComm_t nc;
+  SWPS_NCCL(ncclCommInitRank(&nc, world, u, rank));
+  swps_comm *c = new swps_comm();
+  c->rank = rank;
+  c->world = world;
+  c->device = device;
+  c->rccl = true;
+  c->nc = nc;
+  *out = c;
+  return SWPS_OK;
+}
+
+int swps_comm_create_host(const swps_transport *tr, int32_t rank, int32_t world, int32_t device, swps_comm **out) {
+  if (!tr || !out || world < 1 || rank < 0 || rank >= world) return fail(SWPS_E_CFG, "bad communicator arguments");
+  if (world > 1 && (!tr->allgather || !tr->alltoallv)) return fail(SWPS_E_CFG, "transport callbacks missing");
+  swps_comm *c = new swps_comm();
+  c->rank = rank;
+  c->world = world;
+  c->device = device;
+  c->tr = *tr;
+  *out = c;
+  return SWPS_OK;
+}
+
+int swps_comm_create_tcp(const char *addr, int32_t port, int32_t rank, int32_t world, int32_t device,
+                         int32_t timeout_ms, swps_comm **out) {
+  if (!addr || !out || world < 1 || rank < 0 || rank >= world || port <= 0 || port > 65535)
+    return fail(SWPS_E_CFG, "bad communicator arguments");
+  *out = nullptr;
+  std::unique_ptr<TcpStar> st(new TcpStar());
+  st->rank = rank;
+  st->world = world;
+  st->timeout_ms = std::max(timeout_ms, 1000);
+  if (world > 1) {
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons((uint16_t)port);
+    if (inet_pton(AF_INET, addr, &sa.sin_addr) != 1) return fail(SWPS_E_CFG, std::string("bad IPv4 address ") + addr);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    const int one = 1;
+    if (rank == 0) {
+      st->fd.assign(world, -1);
+      const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+      if (ls < 0) return fail(SWPS_E_IO, "socket");
+      setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+      if (::bind(ls, (sockaddr *)&sa, sizeof(sa)) != 0 || ::listen(ls, world) != 0) {
+        ::close(ls);
+        return fail(SWPS_E_IO, "tcp transport: cannot listen on " + std::string(addr) + ":" + std::to_string(port));
+      }
+      for (int got = 1; got < world;) {
+        const int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
+                             deadline - std::chrono::steady_clock::now()).count();
+        pollfd pf{ls, POLLIN, 0};
+        if (left <= 0 || ::poll(&pf, 1, left) <= 0) {
+          ::close(ls);
+          return fail(SWPS_E_IO, "tcp transport: timed out waiting for ranks");
+        }
+        const int fd = ::accept(ls, nullptr, nullptr);
+        if (fd < 0) continue;
+        int32_t r = -1;
+        if (tcp_recv_all(fd, &r, 4, st->timeout_ms) || r <= 0 || r >= world || st->fd[r] >= 0) {
+          ::close(fd);
+          ::close(ls);
+          return fail(SWPS_E_IO, "tcp transport: bad hello");
+        }
+        setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+        st->fd[r] = fd;
+        got++;
+      }
+      ::close(ls);
+    } else {
+      for (;;) {
+        const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        if (fd < 0) return fail(SWPS_E_IO, "socket");
+        if (::connect(fd, (sockaddr *)&sa, sizeof(sa)) == 0) {
+          setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          const int32_t r = rank;
+          if (tcp_send_all(fd, &r, 4)) {
+            ::close(fd);
+            return fail(SWPS_E_IO, "tcp transport: hello failed");
+          }
+          st->fd.assign(1, fd);
+          break;
+        }
+        ::close(fd);
+        if (std::chrono::steady_clock::now() >= deadline)
+          return fail(SWPS_E_IO, "tcp transport: cannot reach rank 0 at " + std::string(addr) + ":" +
+                                     std::to_string(port));
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      }
+    }
+  }
+  swps_transport tr{st.get(), star_allgather, star_alltoallv};
+  swps_comm *c = nullptr;
+  SWPS_TRY(swps_comm_create_host(&tr, rank, world, device, &c));
+  c->tcp = st.release();
+  *out = c;
+  return SWPS_OK;
+}
+
+int swps_comm_destroy(swps_comm *c) {
+  if (!c) return SWPS_OK;
+  (void)hipSetDevice(c->device);
+  if (c->nc) (void)ncclCommDestroy(c->nc);
+  delete c->tcp;
+  delete c;
+  return SWPS_OK;
+}
+
+int swps_comm_info(swps_comm *c, int32_t *rank, int32_t *world) {
+  if (!c) return fail(SWPS_E_CFG, "null communicator");
+  if (rank) *rank = c->rank;
+  if (world) *world = c->world;
+  return SWPS_OK;
+}
+
+int swps_table_route(swps_table *t, swps_comm *c, int32_t frag_num) {
+  if (!t || !c) return fail(SWPS_E_CFG, "null argument");
+  if (c->device != t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");
+  if (frag_num < c->world) return fail(SWPS_E_CFG, "frag_num < world (hashfrag.h divides by frag_num / world)");
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  std::vector<uint32_t> map(frag_num);
+  SWPS_TRY(swps_hashfrag_table(frag_num, c->world, map.data()));
+  SWPS_TRY(upload(t->frag_map, map, t->stream));
+  SWPS_HIP(hipStreamSynchronize(t->stream));
+  t->comm = c;
+  t->frag_num = frag_num;
+  t->finished = false;
+  return SWPS_OK;
+}
+
+int swps_finish(swps_table *t) {
+  if (!t) return fail(SWPS_E_CFG, "null table");
+  if (!t->comm) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  t->finished = true;
+  for (;;) {  // serve the other ranks' rounds until every rank is finishing
+    int ran = 0;
+    SWPS_TRY(route_round(t, kOpFinish, nullptr, 0, nullptr, t->stream, &ran));
+    if (ran == kOpFinish) break;
+  }
+  SWPS_HIP(hipStreamSynchronize(t->stream));
+  return table_check_error(t, t->stream);
+}
+
+int swps_barrier(swps_table *t) {
+  if (!t) return fail(SWPS_E_CFG, "null table");
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  SWPS_HIP(hipDeviceSynchronize());
+  if (t->comm && t->comm->world > 1) {
+    std::vector<int64_t> all(t->comm->world);
+    const int64_t one = 1;
+    SWPS_TRY(comm_allgather(t->comm, &one, all.data(), 8, t->stream));
+  }
+  return table_check_error(t, t->stream);
+}
+
+int swps_route_stats(swps_table *t, uint64_t *out6) {
+  if (!t || !out6) return fail(SWPS_E_CFG, "null argument");
+  for (int i = 0; i < 6; i++) out6[i] = t->rstats[i];
+  return SWPS_OK;
+}
+
+}  // extern "C"

@@ -168,6 +168,15 @@ struct swps_table {
   swps::DevMem push_scratch, sort_tmp;  // table_push_sources: (row, position) pairs and their sort
   uint64_t snap_sum = 0;  // checksum of the snapshot last saved from / restored into this table (0: none);
                           // worker-state snapshots record it so a resume pairs the two files of one save
+  swps::DevMem isnew;     // find_or_insert: per-key "inserted by this call" flags
+  // key-sharded mode (swps_table_route, swps_comm.hip)
+  swps_comm *comm = nullptr;
+  int32_t frag_num = 0;
+  swps::DevMem frag_map;  // u32[frag_num]: frag -> node id (1..world)
+  swps::DevMem r_owner, r_pos, r_owner_s, r_perm, r_keys, r_buf, r_rkeys, r_rbuf, r_rows, r_tmp, r_cnt;
+  std::vector<char> h_send, h_recv;  // host staging (host transport)
+  uint64_t rstats[6] = {0, 0, 0, 0, 0, 0};
+  bool finished = false;
 };
 
 namespace swps {
@@ -186,4 +195,11 @@ int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const voi
 // source): each row gets its sources' AdaGrad steps in that order, one pass
 int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
                        bool grads_f32 = false);
+// latched device error flags (table full, unknown key) -> error code, no sync
+int table_error_code(uint32_t flags);
+// key-sharded pull / push (swps_comm.hip): collective over t->comm
+int routed_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals, hipStream_t s);
+int routed_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads, hipStream_t s);
+// app contexts take plain local AdaGrad shards only
+int check_app_table(swps_table *t);
 }  // namespace swps

@@ -374,6 +374,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (!t || !cfg || !out) return fail(SWPS_E_CFG, "null argument");
   *out = nullptr;
   if (t->cfg.layout != SWPS_LAYOUT_LR) return fail(SWPS_E_CFG, "table layout must be SWPS_LAYOUT_LR");
+  SWPS_TRY(check_app_table(t));
   if (t->cfg.dtype != SWPS_F32) return fail(SWPS_E_UNSUPPORTED, "LR runs in the reference's fp32 (SWPS_F32)");
   if (cfg->minibatch <= 0) return fail(SWPS_E_CFG, "minibatch must be positive");
   SWPS_HIP(hipSetDevice(t->cfg.device));

@@ -670,6 +670,7 @@ int swps_s2v_create(swps_table *t, const swps_s2v_cfg *cfg, swps_s2v **out) {
   if (!t || !cfg || !out) return fail(SWPS_E_CFG, "null argument");
   *out = nullptr;
   if (t->cfg.layout != SWPS_LAYOUT_W2V) return fail(SWPS_E_CFG, "word table layout must be SWPS_LAYOUT_W2V");
+  if (t->comm) return fail(SWPS_E_UNSUPPORTED, "sent2vec reads a local (replicated) word table, not a routed one");
   if (cfg->window <= 0 || 2 * cfg->window > 64) return fail(SWPS_E_CFG, "window must be in [1, 32]");
   if (cfg->negative < 0 || cfg->negative > 62) return fail(SWPS_E_CFG, "negative must be in [0, 62]");
   if (cfg->minibatch <= 0) return fail(SWPS_E_CFG, "minibatch must be positive");

@@ -170,7 +170,7 @@ template <typename T, int E> struct alignas(sizeof(T) * E) Pack {
 
 template <typename T, typename G, int E>
 __global__ void k_push_w2v(const uint32_t *__restrict__ rows_idx, uint64_t n, const G *__restrict__ grads,
-                           T *__restrict__ rows, int D, double lr, double fudge) {
+                           T *__restrict__ rows, int D, double lr, double fudge, int rule) {
   uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   int lane = threadIdx.x & 63;
   if (w >= n) return;
@@ -182,7 +182,18 @@ __global__ void k_push_w2v(const uint32_t *__restrict__ rows_idx, uint64_t n, co
   const G *g = grads + w * 2 * D;
   for (int c = lane; c < D / E; c += 64) {
     const PG gh = ((const PG *)g)[c], gv = ((const PG *)(g + D))[c];
-    PT h = ((PT *)row)[c], v = ((PT *)(row + D))[c], h2 = ((PT *)(row + 2 * D))[c], v2 = ((PT *)(row + 3 * D))[c];
+    PT h = ((PT *)row)[c], v = ((PT *)(row + D))[c];
+    if (rule == SWPS_PUSH_SGD) {
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        h.v[k] = (T)((double)h.v[k] + (double)gh.v[k] * lr);
+        v.v[k] = (T)((double)v.v[k] + (double)gv.v[k] * lr);
+      }
+      ((PT *)row)[c] = h;
+      ((PT *)(row + D))[c] = v;
+      continue;
+    }
+    PT h2 = ((PT *)(row + 2 * D))[c], v2 = ((PT *)(row + 3 * D))[c];
 #pragma unroll
     for (int k = 0; k < E; k++) {
       const double a = (double)gh.v[k], b = (double)gv.v[k];
@@ -204,13 +215,17 @@ __global__ void k_push_w2v(const uint32_t *__restrict__ rows_idx, uint64_t n, co
 // (fp32 for SWPS_F32, exactly the reference's float arithmetic).
 template <typename T>
 __global__ void k_push_lr(const uint32_t *__restrict__ rows_idx, uint64_t n, const float *__restrict__ grads,
-                          T *__restrict__ rows, T lr, T fudge) {
+                          T *__restrict__ rows, T lr, T fudge, int rule) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t r = rows_idx[i];
   if (r == kNoRow) return;
   T m = (T)grads[i];
   T *row = rows + (uint64_t)r * 2;
+  if (rule == SWPS_PUSH_SGD) {
+    row[0] = row[0] + lr * m;
+    return;
+  }
   T g2 = row[1] + m * m;
   row[1] = g2;
   T step = lr * m;
@@ -242,7 +257,7 @@ __global__ void k_push_keys(const uint32_t *__restrict__ rows_idx, uint64_t n, u
 template <typename T, typename G, int E>
 __global__ void k_push_w2v_multi(const uint32_t *__restrict__ rows_s, const uint32_t *__restrict__ pos_s,
                                  uint64_t n, uint32_t cap, const G *__restrict__ grads, T *__restrict__ rows, int D,
-                                 double lr, double fudge) {
+                                 double lr, double fudge, int rule) {
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (w >= n) return;
@@ -258,6 +273,14 @@ __global__ void k_push_w2v_multi(const uint32_t *__restrict__ rows_s, const uint
     for (uint64_t j = w; j < e; j++) {
       const G *g = grads + (uint64_t)pos_s[j] * 2 * D;
       const PG gh = ((const PG *)g)[c], gv = ((const PG *)(g + D))[c];
+      if (rule == SWPS_PUSH_SGD) {
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+          h.v[k] = (T)((double)h.v[k] + (double)gh.v[k] * lr);
+          v.v[k] = (T)((double)v.v[k] + (double)gv.v[k] * lr);
+        }
+        continue;
+      }
 #pragma unroll
       for (int k = 0; k < E; k++) {
         const double a = (double)gh.v[k], b = (double)gv.v[k];
@@ -278,7 +301,8 @@ __global__ void k_push_w2v_multi(const uint32_t *__restrict__ rows_s, const uint
 
 template <typename T>
 __global__ void k_push_lr_multi(const uint32_t *__restrict__ rows_s, const uint32_t *__restrict__ pos_s, uint64_t n,
-                                uint32_t cap, const float *__restrict__ grads, T *__restrict__ rows, T lr, T fudge) {
+                                uint32_t cap, const float *__restrict__ grads, T *__restrict__ rows, T lr, T fudge,
+                                int rule) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t r = rows_s[i];
@@ -287,6 +311,10 @@ __global__ void k_push_lr_multi(const uint32_t *__restrict__ rows_s, const uint3
   T w = row[0], g2 = row[1];
   for (uint64_t j = i; j < n && rows_s[j] == r; j++) {  // k_push_lr's steps, in source order
     const T m = (T)grads[pos_s[j]];
+    if (rule == SWPS_PUSH_SGD) {
+      w = w + lr * m;
+      continue;
+    }
     g2 = g2 + m * m;
     const T step = lr * m;
     w = w + step / (T)sqrt(g2 + fudge);
@@ -299,6 +327,12 @@ __global__ void k_push_lr_multi(const uint32_t *__restrict__ rows_s, const uint3
 
 namespace swps {
 
+int table_error_code(uint32_t flags) {
+  if (flags & 1) return fail(SWPS_E_OOM, "table capacity exhausted");
+  if (flags & 4) return fail(SWPS_E_BADKEY, "key ~0 is the table's empty key");
+  return fail(SWPS_E_BADKEY, "new key should be inited before (push of an unknown key)");
+}
+
 int table_check_error(swps_table *t, hipStream_t s) {
   uint32_t h[2];
   SWPS_HIP(hipMemcpyAsync(h, t->counters.p, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -307,31 +341,49 @@ int table_check_error(swps_table *t, hipStream_t s) {
   if (h[1]) {
     uint32_t z = 0;
     SWPS_HIP(hipMemcpy((uint32_t *)t->counters.p + 1, &z, 4, hipMemcpyHostToDevice));
-    if (h[1] & 1) return fail(SWPS_E_OOM, "table capacity exhausted");
-    if (h[1] & 4) return fail(SWPS_E_BADKEY, "key ~0 is the table's empty key");
-    return fail(SWPS_E_BADKEY, "new key should be inited before (push of an unknown key)");
+    return table_error_code(h[1]);
   }
+  return SWPS_OK;
+}
+
+// find-or-insert + init_param of the new keys, stream-ordered (errors latched
+// in counters[1]); `isnew` is the table's own scratch
+static int find_or_insert_async(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out,
+                                hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  SWPS_TRY(t->isnew.ensure(n));
+  uint8_t *isnew = t->isnew.as<uint8_t>();
+  k_find_or_insert<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(),
+                                                  t->row_key.as<uint64_t>(), t->counters.as<uint32_t>(), t->mask,
+                                                  t->cfg.capacity, d_rows_out, isnew);
+  SWPS_HIP(hipGetLastError());
+  if (t->cfg.dtype == SWPS_F64)
+    k_init_rows<double><<<blocks_for(n * 64), 256, 0, s>>>(d_keys, d_rows_out, isnew, n, t->rows.as<double>(),
+                                                           t->row_elems, t->cfg.layout, t->cfg.dim,
+                                                           t->cfg.init_mode, t->cfg.seed);
+  else
+    k_init_rows<float><<<blocks_for(n * 64), 256, 0, s>>>(d_keys, d_rows_out, isnew, n, t->rows.as<float>(),
+                                                          t->row_elems, t->cfg.layout, t->cfg.dim,
+                                                          t->cfg.init_mode, t->cfg.seed);
+  SWPS_HIP(hipGetLastError());
   return SWPS_OK;
 }
 
 int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s) {
   if (n == 0) return SWPS_OK;
-  DevMem isnew;
-  SWPS_TRY(isnew.ensure(n));
-  k_find_or_insert<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(),
-                                                  t->row_key.as<uint64_t>(), t->counters.as<uint32_t>(), t->mask,
-                                                  t->cfg.capacity, d_rows_out, isnew.as<uint8_t>());
-  SWPS_HIP(hipGetLastError());
-  if (t->cfg.dtype == SWPS_F64)
-    k_init_rows<double><<<blocks_for(n * 64), 256, 0, s>>>(d_keys, d_rows_out, isnew.as<uint8_t>(), n,
-                                                           t->rows.as<double>(), t->row_elems, t->cfg.layout,
-                                                           t->cfg.dim, t->cfg.init_mode, t->cfg.seed);
-  else
-    k_init_rows<float><<<blocks_for(n * 64), 256, 0, s>>>(d_keys, d_rows_out, isnew.as<uint8_t>(), n,
-                                                          t->rows.as<float>(), t->row_elems, t->cfg.layout,
-                                                          t->cfg.dim, t->cfg.init_mode, t->cfg.seed);
-  SWPS_HIP(hipGetLastError());
-  return table_check_error(t, s);  // also keeps `isnew` alive until the kernels retire
+  SWPS_TRY(find_or_insert_async(t, d_keys, n, d_rows_out, s));
+  return table_check_error(t, s);
+}
+
+int check_app_table(swps_table *t) {
+  if (!t) return fail(SWPS_E_CFG, "null table");
+  if (t->cfg.push_rule != SWPS_PUSH_ADAGRAD)
+    return fail(SWPS_E_UNSUPPORTED, "app contexts apply the reference apps' AdaGrad rule: the table's push_rule "
+                                    "must be SWPS_PUSH_ADAGRAD");
+  if (t->comm)
+    return fail(SWPS_E_UNSUPPORTED, "app contexts need a local shard (swps_w2v_shard / swps_lr_shard route their "
+                                    "own exchange), not a table bound by swps_table_route");
+  return SWPS_OK;
 }
 
 int table_lookup(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s) {
@@ -385,12 +437,12 @@ int table_copy_pull(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_v
 
 template <typename T, typename G>
 void launch_push_w2v(const uint32_t *d_rows, uint64_t n, const G *g, T *rows, int D, double lr, double fudge,
-                     hipStream_t s) {
+                     int rule, hipStream_t s) {
   constexpr int E = 16 / sizeof(T);
   if (D % E == 0)
-    k_push_w2v<T, G, E><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, g, rows, D, lr, fudge);
+    k_push_w2v<T, G, E><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, g, rows, D, lr, fudge, rule);
   else
-    k_push_w2v<T, G, 1><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, g, rows, D, lr, fudge);
+    k_push_w2v<T, G, 1><<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, g, rows, D, lr, fudge, rule);
 }
 
 // the push rule on known rows (W2V: mean gradients [n][2D], fp64 or, with
@@ -403,22 +455,23 @@ int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const voi
     const int D = t->cfg.dim;
     if (t->cfg.dtype == SWPS_F64) {
       if (grads_f32)
-        launch_push_w2v(d_rows, n, (const float *)d_grads, t->rows.as<double>(), D, lr, fudge, s);
+        launch_push_w2v(d_rows, n, (const float *)d_grads, t->rows.as<double>(), D, lr, fudge, t->cfg.push_rule, s);
       else
-        launch_push_w2v(d_rows, n, (const double *)d_grads, t->rows.as<double>(), D, lr, fudge, s);
+        launch_push_w2v(d_rows, n, (const double *)d_grads, t->rows.as<double>(), D, lr, fudge, t->cfg.push_rule, s);
     } else {
       if (grads_f32)
-        launch_push_w2v(d_rows, n, (const float *)d_grads, t->rows.as<float>(), D, lr, fudge, s);
+        launch_push_w2v(d_rows, n, (const float *)d_grads, t->rows.as<float>(), D, lr, fudge, t->cfg.push_rule, s);
       else
-        launch_push_w2v(d_rows, n, (const double *)d_grads, t->rows.as<float>(), D, lr, fudge, s);
+        launch_push_w2v(d_rows, n, (const double *)d_grads, t->rows.as<float>(), D, lr, fudge, t->cfg.push_rule, s);
     }
   } else {
     if (t->cfg.dtype == SWPS_F64)
       k_push_lr<double><<<blocks_for(n), 256, 0, s>>>(d_rows, n, (const float *)d_grads, t->rows.as<double>(),
-                                                      (double)t->cfg.learning_rate, (double)t->cfg.fudge);
+                                                      (double)t->cfg.learning_rate, (double)t->cfg.fudge,
+                                                      t->cfg.push_rule);
     else
       k_push_lr<float><<<blocks_for(n), 256, 0, s>>>(d_rows, n, (const float *)d_grads, t->rows.as<float>(),
-                                                     t->cfg.learning_rate, t->cfg.fudge);
+                                                     t->cfg.learning_rate, t->cfg.fudge, t->cfg.push_rule);
   }
   SWPS_HIP(hipGetLastError());
   return SWPS_OK;
@@ -448,9 +501,11 @@ int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const 
       using G = std::remove_cv_t<std::remove_pointer_t<decltype(g)>>;
       constexpr int E = 16 / sizeof(T);
       if (D % E == 0)
-        k_push_w2v_multi<T, G, E><<<blocks_for(n * 64), 256, 0, s>>>(key_s, pos_s, n, cap, g, rows, D, lr, fudge);
+        k_push_w2v_multi<T, G, E><<<blocks_for(n * 64), 256, 0, s>>>(key_s, pos_s, n, cap, g, rows, D, lr, fudge,
+                                                                       t->cfg.push_rule);
       else
-        k_push_w2v_multi<T, G, 1><<<blocks_for(n * 64), 256, 0, s>>>(key_s, pos_s, n, cap, g, rows, D, lr, fudge);
+        k_push_w2v_multi<T, G, 1><<<blocks_for(n * 64), 256, 0, s>>>(key_s, pos_s, n, cap, g, rows, D, lr, fudge,
+                                                                       t->cfg.push_rule);
     };
     if (t->cfg.dtype == SWPS_F64) {
       if (grads_f32)
@@ -466,10 +521,11 @@ int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const 
   } else if (t->cfg.dtype == SWPS_F64) {
     k_push_lr_multi<double><<<blocks_for(n), 256, 0, s>>>(key_s, pos_s, n, cap, (const float *)d_grads,
                                                           t->rows.as<double>(), (double)t->cfg.learning_rate,
-                                                          (double)t->cfg.fudge);
+                                                          (double)t->cfg.fudge, t->cfg.push_rule);
   } else {
     k_push_lr_multi<float><<<blocks_for(n), 256, 0, s>>>(key_s, pos_s, n, cap, (const float *)d_grads,
-                                                         t->rows.as<float>(), t->cfg.learning_rate, t->cfg.fudge);
+                                                         t->rows.as<float>(), t->cfg.learning_rate, t->cfg.fudge,
+                                                         t->cfg.push_rule);
   }
   SWPS_HIP(hipGetLastError());
   return SWPS_OK;
@@ -486,6 +542,7 @@ int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
   if (cfg->dtype != SWPS_F32 && cfg->dtype != SWPS_F64) return fail(SWPS_E_CFG, "unknown dtype");
   if (cfg->layout == SWPS_LAYOUT_W2V && cfg->dim <= 0) return fail(SWPS_E_CFG, "dim must be positive");
   if (cfg->capacity == 0 || cfg->capacity >= 0xFFFFFFF0ULL) return fail(SWPS_E_CFG, "capacity out of range");
+  if (cfg->push_rule != SWPS_PUSH_ADAGRAD && cfg->push_rule != SWPS_PUSH_SGD) return fail(SWPS_E_CFG, "unknown push rule");
   SWPS_HIP(hipSetDevice(cfg->device));
   swps_table *t = new swps_table();
   t->cfg = *cfg;
@@ -539,8 +596,8 @@ int swps_table_destroy(swps_table *t) {
 
 int swps_table_sync(swps_table *t) {
   SWPS_HIP(hipSetDevice(t->cfg.device));
-  SWPS_HIP(hipStreamSynchronize(t->stream));
-  return SWPS_OK;
+  SWPS_HIP(hipDeviceSynchronize());  // async calls may have used caller streams
+  return table_check_error(t, t->stream);
 }
 
 int swps_table_size(swps_table *t, uint64_t *n) {
@@ -557,31 +614,37 @@ int swps_table_row_elems(swps_table *t, int32_t *row, int32_t *pull, int32_t *pu
   return SWPS_OK;
 }
 
-int swps_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals) {
-  if (n == 0) return SWPS_OK;
+int swps_pull_async(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals, void *stream) {
+  hipStream_t s = stream ? (hipStream_t)stream : t->stream;
   SWPS_HIP(hipSetDevice(t->cfg.device));
+  if (t->comm) return routed_pull(t, d_keys, n, d_vals, s);
+  if (n == 0) return SWPS_OK;
   SWPS_TRY(t->scratch.ensure(n * 4));
   uint32_t *rows = t->scratch.as<uint32_t>();
-  SWPS_TRY(table_find_or_insert(t, d_keys, n, rows, t->stream));
-  if (t->cfg.dtype == SWPS_F64)
-    k_copy_rows_out<double><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, t->rows.as<double>(), t->row_elems,
-                                                                       t->pull_elems, (double *)d_vals);
-  else
-    k_copy_rows_out<float><<<blocks_for(n * 64), 256, 0, t->stream>>>(rows, n, t->rows.as<float>(), t->row_elems,
-                                                                      t->pull_elems, (float *)d_vals);
-  SWPS_HIP(hipGetLastError());
-  SWPS_HIP(hipStreamSynchronize(t->stream));
-  return SWPS_OK;
+  SWPS_TRY(find_or_insert_async(t, d_keys, n, rows, s));
+  return table_copy_pull(t, rows, n, d_vals, s);
+}
+
+int swps_push_async(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads, void *stream) {
+  hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  if (t->comm) return routed_push(t, d_keys, n, d_grads, s);
+  if (n == 0) return SWPS_OK;
+  SWPS_TRY(t->scratch.ensure(n * 4));
+  uint32_t *rows = t->scratch.as<uint32_t>();
+  SWPS_TRY(table_lookup(t, d_keys, n, rows, s));
+  return table_push_rows(t, rows, n, d_grads, s);
+}
+
+int swps_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals) {
+  if (n == 0 && !t->comm) return SWPS_OK;
+  SWPS_TRY(swps_pull_async(t, d_keys, n, d_vals, nullptr));
+  return table_check_error(t, t->stream);
 }
 
 int swps_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads) {
-  if (n == 0) return SWPS_OK;
-  SWPS_HIP(hipSetDevice(t->cfg.device));
-  SWPS_TRY(t->scratch.ensure(n * 4));
-  uint32_t *rows = t->scratch.as<uint32_t>();
-  SWPS_TRY(table_lookup(t, d_keys, n, rows, t->stream));
-  SWPS_TRY(table_push_rows(t, rows, n, d_grads, t->stream));
-  SWPS_HIP(hipGetLastError());
+  if (n == 0 && !t->comm) return SWPS_OK;
+  SWPS_TRY(swps_push_async(t, d_keys, n, d_grads, nullptr));
   return table_check_error(t, t->stream);
 }
 
@@ -609,7 +672,7 @@ int swps_export(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_rows)
 // Host-pointer forms for FFI callers without device memory: the reference's
 // wire types (W2V fp64 [h|v] / [h_grad|v_grad], LR fp32), staged through HBM.
 int swps_pull_h(swps_table *t, const uint64_t *keys, uint64_t n, void *vals) {
-  if (n == 0) return SWPS_OK;
+  if (n == 0 && !t->comm) return SWPS_OK;
   SWPS_HIP(hipSetDevice(t->cfg.device));
   const int P = t->pull_elems;
   DevMem dk, dv;
@@ -636,7 +699,7 @@ int swps_pull_h(swps_table *t, const uint64_t *keys, uint64_t n, void *vals) {
 }
 
 int swps_push_h(swps_table *t, const uint64_t *keys, uint64_t n, const void *grads) {
-  if (n == 0) return SWPS_OK;
+  if (n == 0 && !t->comm) return SWPS_OK;
   SWPS_HIP(hipSetDevice(t->cfg.device));
   const size_t gb = n * t->push_elems * (t->cfg.layout == SWPS_LAYOUT_W2V ? 8 : 4);
   DevMem dk, dg;

@@ -2293,6 +2293,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (!t || !cfg || !out) return fail(SWPS_E_CFG, "null argument");
   *out = nullptr;
   if (t->cfg.layout != SWPS_LAYOUT_W2V) return fail(SWPS_E_CFG, "table layout must be SWPS_LAYOUT_W2V");
+  SWPS_TRY(check_app_table(t));
   SWPS_HIP(hipSetDevice(t->cfg.device));
   swps_w2v *w = new swps_w2v();
   w->t = t;

@@ -39,6 +39,7 @@ struct WLocalGrad {
 namespace swift_snails {
 template <> struct PullCodec<WLocalParam> {
   typedef double wire_t;
+  static const int32_t layout = SWPS_LAYOUT_W2V;
   static int elems() { return 2 * g_dim; }
   static void decode(const double *w, WLocalParam &p) {
     p.h.assign(w, w + g_dim);
@@ -58,13 +59,35 @@ template <> struct PushCodec<WLocalGrad> {  // the mean, word2vec_global.h:122-1
 
 typedef LocalParamCache<uint64_t, WLocalParam, WLocalGrad> cache_t;
 
+// the reference app's access-method classes keep their shape
+// (word2vec_global.h:158-191); the device applies the rule they select
+class WPullAccessMethod : public PullAccessMethod<uint64_t, WLocalParam, WLocalParam> {};
+class WPushAccessMethod : public PushAccessMethod<uint64_t, WLocalParam, WLocalGrad> {};
+typedef ClusterServer<uint64_t, WLocalParam, WLocalParam, WLocalGrad, WPullAccessMethod, WPushAccessMethod> server_t;
+
+// rank r's keys: overlapping sets, so owners see several sources per key
+static bool has_key(uint64_t i, int r) { return (i + (uint64_t)r) % 3 != 0; }
+static uint64_t key_of(uint64_t i) { return i * 2654435761ULL; }
+static void grads_of(uint64_t k, int r, std::vector<double> &g1, std::vector<double> &g2, std::vector<double> &g3) {
+  for (int i = 0; i < g_dim; i++) {
+    g1[i] = std::sin((double)(k % 97) + i + r);
+    g2[i] = std::cos((double)(k % 89) * i - r);
+    g3[i] = 0.25 * i - 1.0 + 0.1 * r;
+  }
+}
+
+// PS-level client (the reference apps' pull / learn / push cycle with a
+// host learn step): on one rank, or key-sharded over several (RANK /
+// WORLD_SIZE; every rank's push is its own AdaGrad step, in rank order)
 static int ps_client() {
   g_dim = global_config().get("word2vec", "len_vec").to_int32();
   const double lr = global_config().get("server", "initial_learning_rate").to_float();
-  Cluster<ClusterWorker, W2VServer, uint64_t> cluster(4096, SWPS_F64);
+  Cluster<ClusterWorker, server_t, uint64_t> cluster(4096, SWPS_F64);
   cluster.initialize();
+  const int rank = cluster.rank(), world = cluster.world();
   std::unordered_set<uint64_t> keys;
-  for (uint64_t k = 1; k <= 300; k++) keys.insert(k * 2654435761ULL);
+  for (uint64_t i = 1; i <= 300; i++)
+    if (has_key(i, rank)) keys.insert(key_of(i));
   cache_t cache, again;
   cache.init_keys(keys);
   global_pull_access<uint64_t, WLocalParam, WLocalGrad>().pull_with_barrier(keys, cache);
@@ -78,45 +101,60 @@ static int ps_client() {
         return 1;
       }
   }
-  // accumulate two gradients per key, push the mean, check AdaGrad
-  std::map<uint64_t, std::vector<double> > mh, mv;
+  // accumulate two gradients per key, push the mean
+  std::vector<double> g1(g_dim), g2(g_dim), g3(g_dim);
   for (auto k : keys) {
-    std::vector<double> g1(g_dim), g2(g_dim), g3(g_dim);
-    for (int i = 0; i < g_dim; i++) {
-      g1[i] = std::sin((double)(k % 97) + i);
-      g2[i] = std::cos((double)(k % 89) * i);
-      g3[i] = 0.25 * i - 1.0;
-    }
+    grads_of(k, rank, g1, g2, g3);
     cache.grads()[k].accu_h(g1);
     cache.grads()[k].accu_h(g2);
     cache.grads()[k].accu_v(g3);
-    std::vector<double> h(g_dim), v(g_dim);
-    for (int i = 0; i < g_dim; i++) {
-      h[i] = (g1[i] + g2[i]) / 2;
-      v[i] = g3[i];
-    }
-    mh[k] = h;
-    mv[k] = v;
   }
   global_push_access<uint64_t, WLocalParam, WLocalGrad>().push_with_barrier(keys, cache);
   cache_t after;
   after.init_keys(keys);
   global_pull_access<uint64_t, WLocalParam, WLocalGrad>().pull_with_barrier(keys, after);
+  // expected: word2vec_global.h:176-185 from h2 = v2 = 0, one step per rank
+  // holding the key, ranks in order
   const double fudge = (double)1e-6f;
   double worst = 0;
-  for (auto k : keys) {
-    for (int i = 0; i < g_dim; i++) {  // word2vec_global.h:176-185 from h2 = v2 = 0
-      const double eh = again.params()[k].h[i] + lr * mh[k][i] / std::sqrt(mh[k][i] * mh[k][i] + fudge);
-      const double ev = again.params()[k].v[i] + lr * mv[k][i] / std::sqrt(mv[k][i] * mv[k][i] + fudge);
-      worst = std::fmax(worst, std::fabs(after.params()[k].h[i] - eh));
-      worst = std::fmax(worst, std::fabs(after.params()[k].v[i] - ev));
+  for (uint64_t ii = 1; ii <= 300; ii++) {
+    if (!has_key(ii, rank)) continue;
+    const uint64_t k = key_of(ii);
+    for (int i = 0; i < g_dim; i++) {
+      double h = again.params()[k].h[i], v = again.params()[k].v[i], h2 = 0, v2 = 0;
+      for (int r = 0; r < world; r++) {
+        if (!has_key(ii, r)) continue;
+        grads_of(k, r, g1, g2, g3);
+        const double a = (g1[i] + g2[i]) / 2, b = g3[i];
+        h2 = h2 + a * a;
+        v2 = v2 + b * b;
+        h = h + (a * lr) / std::sqrt(h2 + fudge);
+        v = v + (b * lr) / std::sqrt(v2 + fudge);
+      }
+      worst = std::fmax(worst, std::fabs(after.params()[k].h[i] - h));
+      worst = std::fmax(worst, std::fabs(after.params()[k].v[i] - v));
     }
     if (cache.grads()[k].h_count != 0) {
       std::printf("FAIL grads not reset\n");
       return 1;
     }
   }
-  std::printf("ps ok keys=%zu max|diff|=%.3g\n", keys.size(), worst);
+  // the last rank keeps working after the others finished: their shards
+  // still serve it (swps_finish)
+  if (world > 1 && rank == world - 1) {
+    cache_t late;
+    late.init_keys(keys);
+    global_pull_access<uint64_t, WLocalParam, WLocalGrad>().pull_with_barrier(keys, late);
+    for (auto k : keys)
+      for (int i = 0; i < g_dim; i++)
+        if (late.params()[k].h[i] != after.params()[k].h[i]) {
+          std::printf("FAIL late pull\n");
+          return 1;
+        }
+  }
+  cluster.finalize();
+  std::printf("ps ok rank=%d world=%d routed=%d keys=%zu max|diff|=%.3g\n", rank, world, (int)cluster.routed(),
+              keys.size(), worst);
   return worst < 1e-12 ? 0 : 1;
 }
 

@@ -66,7 +66,50 @@ def test_compat_ps_client(compat_bin, gpu, tmp_path):
     conf = tmp_path / "demo.conf"
     conf.write_text(W2V_CONF)
     out = _run(compat_bin, "ps", "-config", str(conf))
-    assert "ps ok" in out
+    assert "ps ok" in out and "routed=0" in out
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_compat_ps_client_routed_rccl_world1(compat_bin, gpu, tmp_path):
+    """The multi-rank code path (owner routing, RCCL exchange) at world 1."""
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF)
+    env = dict(os.environ, SWPS_ROUTE="1", MASTER_ADDR="127.0.0.1", SWPS_BOOTSTRAP_PORT=str(_free_port()))
+    r = subprocess.run([compat_bin, "ps", "-config", str(conf)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "routed=1" in r.stdout
+
+
+@pytest.mark.gpu
+def test_compat_ps_client_two_ranks(compat_bin, gpu, tmp_path):
+    """Two C++ ranks on one GPU over the library's TCP transport: keys shared
+    by both ranks get both pushes as separate AdaGrad steps in rank order;
+    the last rank pulls again after rank 0 finished (rank 0 keeps serving)."""
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF + "[server]\nfrag_num: 1000\n")
+    port = str(_free_port())
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   SWPS_BOOTSTRAP_PORT=port, SWPS_TRANSPORT="tcp", HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([compat_bin, "ps", "-config", str(conf)], stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, env=env))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        outs.append((p.returncode, o, e))
+    for rc, o, e in outs:
+        assert rc == 0, o + e
+        assert "routed=1" in o and "world=2" in o
 
 
 @pytest.mark.gpu

@@ -1,0 +1,138 @@
+"""The library's own key-sharded table (swps_table_route + swps_comm_*):
+RCCL at world 1 through the full routed code path, two gloo ranks on one GPU
+against one unrouted table (tests/dist_route_check.py), the SGD push rule,
+the stream-ordered forms, and the app contexts refusing routed / non-AdaGrad
+tables."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _keys(rng, n, V=5000):
+    return (np.unique(rng.integers(0, V, n)).astype(np.uint64) * np.uint64(104729) + np.uint64(3))
+
+
+@pytest.mark.parametrize("layout,dtype", [("w2v", "f32"), ("w2v", "f64"), ("lr", "f32")])
+def test_rccl_world1_routed_equals_local(lib, gpu, layout, dtype):
+    import swiftmpi_amd as sw
+    from swiftmpi_amd.comm import Comm
+    D = 20 if layout == "w2v" else 1
+    kw = dict(dim=D, capacity=20000, dtype=dtype, learning_rate=0.7, init="hash", seed=4)
+    comm = Comm.rccl(0, 1, port=_port())
+    a, b = sw.Table(layout, **kw), sw.Table(layout, **kw)
+    a.route(comm, frag_num=1000)
+    rng = np.random.default_rng(2)
+    for _ in range(5):
+        k = _keys(rng, 3000)
+        rng.shuffle(k)
+        pa, pb = a.pull_h(k), b.pull_h(k)
+        assert np.array_equal(pa, pb)
+        g = rng.normal(0, 0.2, (len(k), a.push_elems)).astype(np.float64 if layout == "w2v" else np.float32)
+        a.push_h(k, g)
+        b.push_h(k, g)
+    a.barrier()
+    a.finish()
+    st = a.route_stats()
+    assert st["rounds"] == 10 and st["keys_remote"] == 0 and st["keys_sent"] == st["keys_served"]
+    keys = np.sort(b.keys())
+    assert np.array_equal(np.sort(a.keys()), keys)
+    kk = torch.as_tensor(keys.astype(np.int64), device="cuda")
+    assert torch.equal(a.export(kk), b.export(kk))
+    a.close()
+    b.close()
+    comm.close()
+
+
+def test_routed_two_ranks_host_transport(lib, gpu):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist_route_check.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    print(r.stdout[-6000:])
+    print("\n".join(ln for ln in r.stderr.splitlines() if "rank0" in ln or "Error" in ln)[-6000:])
+    assert r.returncode == 0 and "ROUTE OK" in r.stdout
+
+
+def test_sgd_push_rule(lib, gpu):
+    import swiftmpi_amd as sw
+    rng = np.random.default_rng(3)
+    k = _keys(rng, 500)
+    for layout, dt in (("w2v", np.float64), ("lr", np.float32)):
+        t = sw.Table(layout, dim=8, capacity=1000, dtype="f64" if layout == "w2v" else "f32", learning_rate=0.5,
+                     init="hash", seed=1, push_rule="sgd")
+        before = t.pull_h(k)
+        g = rng.normal(0, 1, before.shape).astype(dt)
+        t.push_h(k, g)
+        after = t.pull_h(k)
+        want = (before.astype(np.float64) + g.astype(np.float64) * np.float64(np.float32(0.5))).astype(dt)
+        if layout == "w2v":
+            assert np.array_equal(after, want)
+            rows = t.export(torch.as_tensor(k.astype(np.int64), device="cuda")).cpu().numpy()
+            assert not rows[:, 16:].any()  # the AdaGrad sums stay untouched
+        else:
+            want = (before + np.float32(0.5) * g).astype(np.float32)
+            assert np.array_equal(after, want)
+        t.close()
+
+
+def test_async_forms_and_latched_errors(lib, gpu):
+    import swiftmpi_amd as sw
+    from swiftmpi_amd import capi
+    t = sw.Table("w2v", dim=16, capacity=100, dtype="f32", init="hash", seed=2)
+    s = torch.cuda.Stream()
+    k = torch.arange(1, 51, dtype=torch.int64, device="cuda")
+    out = torch.empty((50, 32), dtype=torch.float32, device="cuda")
+    capi.check(capi.lib().swps_pull_async(t.h, capi.ptr(k), 50, capi.ptr(out), ctypes_stream(s)))
+    g = torch.full((50, 32), 0.1, dtype=torch.float64, device="cuda")
+    capi.check(capi.lib().swps_push_async(t.h, capi.ptr(k), 50, capi.ptr(g), ctypes_stream(s)))
+    t.barrier()
+    ref = sw.Table("w2v", dim=16, capacity=100, dtype="f32", init="hash", seed=2)
+    want = ref.pull(k)
+    assert torch.equal(out, want)
+    ref.push(k, g)
+    assert torch.equal(t.export(k), ref.export(k))
+    # a push of unknown keys is latched and reported by the next sync
+    bad = torch.arange(1000, 1010, dtype=torch.int64, device="cuda")
+    capi.check(capi.lib().swps_push_async(t.h, capi.ptr(bad), 10, capi.ptr(g), ctypes_stream(s)))
+    with pytest.raises(capi.SwpsError) as e:
+        t.barrier()
+    assert e.value.code == -2
+    t.close()
+    ref.close()
+
+
+def ctypes_stream(s):
+    import ctypes
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def test_app_contexts_refuse_routed_or_sgd_tables(lib, gpu):
+    import swiftmpi_amd as sw
+    from swiftmpi_amd import capi
+    t = sw.Table("w2v", dim=16, capacity=100, push_rule="sgd")
+    with pytest.raises(capi.SwpsError) as e:
+        sw.Word2Vec(t)
+    assert e.value.code == -7
+    t.close()
+    t = sw.Table("lr", capacity=100, push_rule="sgd")
+    with pytest.raises(capi.SwpsError):
+        sw.LR(t)
+    t.close()
