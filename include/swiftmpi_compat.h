@@ -143,6 +143,20 @@ inline swps_table *&global_swps_table() {
   static swps_table *t = nullptr;
   return t;
 }
+/* The multi-rank job's communicator (null on one rank), its frag_num, and
+ * the shard's configuration (Cluster sets them). */
+inline swps_comm *&global_swps_comm() {
+  static swps_comm *c = nullptr;
+  return c;
+}
+inline int &global_frag_num() {
+  static int f = 1000;
+  return f;
+}
+inline swps_table_cfg &global_swps_cfg() {
+  static swps_table_cfg c;
+  return c;
+}
 
 /* ---- parameter/accessmethod.h ---------------------------------------------
  * The reference's server runs the app's access-method objects per key on
@@ -343,6 +357,7 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
     c.push_rule = ServerT::push_rule();
     swps_check(swps_table_create(&c, &_t));
     global_swps_table() = _t;
+    global_swps_cfg() = c;
     if (_world > 1 || env_int("SWPS_ROUTE", nullptr, 0)) {
       const char *addr = std::getenv("MASTER_ADDR");
       const int port = env_int("SWPS_BOOTSTRAP_PORT", nullptr, env_int("MASTER_PORT", nullptr, 29500) + 1);
@@ -359,10 +374,13 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
                            ? global_config().get("server", "frag_num").to_int32()
                            : 1000;
       swps_check(swps_table_route(_t, _comm, frag));
+      global_swps_comm() = _comm;
+      global_frag_num() = frag;
     }
   }
   ~Cluster() {
     if (global_swps_table() == _t) global_swps_table() = nullptr;
+    if (global_swps_comm() == _comm) global_swps_comm() = nullptr;
     swps_table_destroy(_t);
     swps_comm_destroy(_comm);
   }
@@ -394,7 +412,9 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
 /* Word2Vec<MiniBatch> (word2vec_global.h:541-748, w2v.cpp): train() = the
  * first full pull + niters epochs of the minibatch loop, all on the GPU.
  * local = true: word2vec.h's Word2Vec<MiniBatch> (w2v_local.cpp) — atoi keys,
- * per-minibatch vocab and unigram table. */
+ * per-minibatch vocab and unigram table.  On a multi-rank Cluster each rank
+ * trains its own corpus file and the library runs the key-sharded exchange
+ * (swps_w2v_shard_comm; the owners initialise keys, SWPS_INIT_HASH). */
 class Word2VecApp {
  public:
   Word2VecApp(const std::string &path, int niters, swps_table *t = nullptr, int fp64_intermediates = 1,
@@ -416,11 +436,14 @@ class Word2VecApp {
     c.profile = 0;
     c.minibatch_vocab = local ? 1 : 0;
     c.sampler = SWPS_SAMPLER_TABLE;
+    _comm = t ? nullptr : global_swps_comm();
+    if (_comm) c.init_mode = SWPS_W2V_INIT_TABLE;
     swps_check(swps_w2v_create(t ? t : global_swps_table(), &c, &_w));
   }
   ~Word2VecApp() { swps_w2v_destroy(_w); }
   void train() {
     swps_check(swps_w2v_load_text(_w, _path.c_str()));
+    if (_comm) swps_check(swps_w2v_shard_comm(_w, _comm, global_frag_num()));
     swps_check(swps_w2v_init(_w));
     swps_check(swps_w2v_train_epochs(_w, _niters));
   }
@@ -432,14 +455,26 @@ class Word2VecApp {
   std::string _path;
   int _niters;
   swps_w2v *_w = nullptr;
+  swps_comm *_comm = nullptr;
 };
 
 /* Sent2Vec (sent2vec.cpp:14-195): load_word_vector then train(); the
- * sentence vectors go to `out_path` in the reference's format. */
+ * sentence vectors go to `out_path` in the reference's format.  On a
+ * multi-rank Cluster: replicas — every rank loads the whole (read-only) word
+ * table into a local copy and trains the documents BasicHashFrag gives it
+ * (swps_s2v_shard; sentence vectors to `out_path`.<rank>). */
 class Sent2VecApp {
  public:
   Sent2VecApp(const std::string &path, const std::string &out_path, int niters, swps_table *t = nullptr)
       : _path(path), _out(out_path), _t(t ? t : global_swps_table()) {
+    _comm = t ? nullptr : global_swps_comm();
+    if (_comm) {  // a local replica of the word table
+      swps_table_cfg c = global_swps_cfg();
+      swps_check(swps_table_create(&c, &_own));
+      _t = _own;
+      swps_check(swps_comm_info(_comm, &_rank, &_world));
+      _out = _out.empty() ? _out : _out + "." + std::to_string(_rank);
+    }
     _c.window = global_config().get("word2vec", "window").to_int32();
     _c.negative = global_config().get("word2vec", "negative").to_int32();
     _c.min_sentence_length = global_config().get("word2vec", "min_sentence_length").to_int32();
@@ -454,6 +489,7 @@ class Sent2VecApp {
   }
   ~Sent2VecApp() {
     if (_s) swps_s2v_destroy(_s);
+    if (_own) swps_table_destroy(_own);
   }
   /* ClusterServer::load (server.h:49-62) + the WParam it constructs first */
   void load_word_vector(const std::string &path) {
@@ -467,6 +503,7 @@ class Sent2VecApp {
   }
   void train() {
     swps_check(swps_s2v_create(_t, &_c, &_s));
+    if (_comm) swps_check(swps_s2v_shard(_s, _rank, _world, global_frag_num()));
     swps_check(swps_s2v_load_text(_s, _path.c_str()));
     swps_check(swps_s2v_train(_s));
     if (!_out.empty()) swps_check(swps_s2v_dump(_s, _out.c_str()));
@@ -480,19 +517,28 @@ class Sent2VecApp {
   swps_table *_t;
   swps_s2v_cfg _c;
   swps_s2v *_s = nullptr;
+  swps_comm *_comm = nullptr;
+  swps_table *_own = nullptr;
+  int32_t _rank = 0, _world = 1;
 };
 
 /* LR (lr.cpp:133-411): train(niters) returns the per-epoch mean squared
- * error the reference logs (lr.cpp:231); predict() the probabilities. */
+ * error the reference logs (lr.cpp:231); predict() the probabilities.  On a
+ * multi-rank Cluster the library runs the key-sharded exchange
+ * (swps_lr_shard_comm): train / predict are collective, errors are this
+ * rank's rows'. */
 class LRApp {
  public:
   LRApp(const std::string &path, swps_table *t = nullptr) {
+    swps_comm *comm = t ? nullptr : global_swps_comm();
     swps_lr_cfg c;
     c.minibatch = global_config().get("worker", "minibatch").to_int32();
-    c.init_ref = 1;
+    c.init_ref = comm ? 0 : 1;
     c.profile = 0;
+    c.fast_sums = 0;
     swps_check(swps_lr_create(t ? t : global_swps_table(), &c, &_l));
     swps_check(swps_lr_load_text(_l, path.c_str()));
+    if (comm) swps_check(swps_lr_shard_comm(_l, comm, global_frag_num()));
     swps_check(swps_lr_init(_l));
   }
   ~LRApp() { swps_lr_destroy(_l); }

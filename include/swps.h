@@ -339,6 +339,20 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
  * context's device; NULL = the compute stream, the default).  The caller
  * orders the two streams (the pipelined driver in swiftmpi_amd/dist.py). */
 int swps_w2v_set_serve_stream(swps_w2v *w, void *stream);
+/* Library-driven sharded mode: swps_w2v_shard for comm's rank / world, and
+ * the library runs the exchange itself over `comm` — swps_w2v_init is the
+ * first full pull, swps_w2v_train_batches / _epochs run lockstep minibatches
+ * (collective: every rank calls them with the same count; ranks with fewer
+ * minibatches per epoch run empty steps, steps per epoch = the maximum over
+ * ranks), with the server work and exchanges on a second stream and the next
+ * minibatch's parameter-independent half overlapping them.  The table may be
+ * the local shard or one routed over the same comm. */
+int swps_w2v_shard_comm(swps_w2v *w, swps_comm *comm, int32_t frag_num);
+/* exchange accounting of the library-driven mode: out4 = [bytes sent to other
+ * ranks, bytes sent in all, exchanges, ms of exchange on the serve stream]
+ * since the last reset; on = 1 / 0 switches the (per-exchange syncing) event
+ * timing on / off and resets, -1 only reads */
+int swps_w2v_exchange_stats(swps_w2v *w, int32_t on, double *out4);
 
 /* ---- host-only helpers (no device needed; used by the CPU test-suite) ---- */
 /* run-length form of gen_unigram_table (word2vec_global.h:467-497): start slot
@@ -411,6 +425,9 @@ typedef struct {
   int32_t minibatch;  /* worker.minibatch: a batch is B+1 valid lines (lr.cpp:308-354) */
   int32_t init_ref;   /* 1: first-pull init from the float LCG in _local_keys order (lr.cpp:48-50) */
   int32_t profile;
+  int32_t fast_sums;  /* 0: each key's gradient sum is the reference's sequential fp32 chain in record
+                       * order (bit-exact); 1: fp64 sums, long runs tree-reduced across a wave (fast
+                       * mode: deterministic, not bit-exact — within 1e-5 of the oracle) */
 } swps_lr_cfg;
 
 int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out);
@@ -450,6 +467,10 @@ int swps_lr_serve_pull(swps_lr *l, const uint64_t *d_keys, const uint64_t *src_c
 int swps_lr_install(swps_lr *l, const float *d_vals);
 int swps_lr_step(swps_lr *l, const float *d_vals, float *d_grads);
 int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads, const uint64_t *src_counts);
+/* library-driven sharded LR over `comm` (as swps_w2v_shard_comm): swps_lr_init,
+ * swps_lr_train / train_batches and swps_lr_predict (a full pull first)
+ * become collective; swps_lr_train's errors are this rank's rows'. */
+int swps_lr_shard_comm(swps_lr *l, swps_comm *comm, int32_t frag_num);
 
 #ifdef __cplusplus
 }

@@ -253,6 +253,19 @@ class Word2Vec:
         self.table = table
         self.dim = table.dim
 
+    def shard_comm(self, comm, frag_num=1000):
+        """Library-driven key-sharded mode (swps_w2v_shard_comm): after load_*,
+        init() is the first full pull and train_batches / train run lockstep
+        minibatches over `comm` (collective).  The table must use init="hash"
+        and this context init="table"."""
+        check(capi.lib().swps_w2v_shard_comm(self.h, comm.h, frag_num))
+        self._comm = comm
+
+    def exchange_stats(self, on=-1):
+        out = np.zeros(4)
+        check(capi.lib().swps_w2v_exchange_stats(self.h, on, ptr(out)))
+        return dict(zip(["bytes_remote", "bytes_total", "calls", "ms"], out.tolist()))
+
     @classmethod
     def from_config(cls, config, table_kwargs=None, **kw):
         """Build a Table + Word2Vec from the reference's demo.conf keys."""
@@ -521,14 +534,20 @@ class Sent2Vec:
 class LR:
     """Sparse logistic regression with server-side AdaGrad (lr.cpp:133-411)."""
 
-    def __init__(self, table, minibatch=200, init_ref=True, profile=False):
+    def __init__(self, table, minibatch=200, init_ref=True, profile=False, fast_sums=False):
         assert table.layout == "lr"
-        cfg = capi.LRCfg(minibatch, int(init_ref), int(profile))
+        cfg = capi.LRCfg(minibatch, int(init_ref), int(profile), int(fast_sums))
         h = ctypes.c_void_p()
         check(capi.lib().swps_lr_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
         table._deps.add(self)
         self.table = table
+
+    def shard_comm(self, comm, frag_num=2000):
+        """Library-driven key-sharded LR (swps_lr_shard_comm): init / train /
+        train_batches / predict become collective over `comm`."""
+        check(capi.lib().swps_lr_shard_comm(self.h, comm.h, frag_num))
+        self._comm = comm
 
     def close(self):
         if getattr(self, "h", None):

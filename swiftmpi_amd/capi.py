@@ -56,7 +56,7 @@ class W2VCfg(ctypes.Structure):
 
 
 class LRCfg(ctypes.Structure):
-    _fields_ = [("minibatch", _i32), ("init_ref", _i32), ("profile", _i32)]
+    _fields_ = [("minibatch", _i32), ("init_ref", _i32), ("profile", _i32), ("fast_sums", _i32)]
 
 
 class S2VCfg(ctypes.Structure):
@@ -133,6 +133,9 @@ PROTOS = {
     "swps_w2v_serve_push": (ctypes.c_int, [_p, _p, _p, _p]),
     "swps_w2v_set_serve_stream": (ctypes.c_int, [_p, _p]),
     "swps_w2v_prep": (ctypes.c_int, [_p]),
+    "swps_w2v_shard_comm": (ctypes.c_int, [_p, _p, _i32]),
+    "swps_w2v_exchange_stats": (ctypes.c_int, [_p, _i32, _p]),
+    "swps_lr_shard_comm": (ctypes.c_int, [_p, _p, _i32]),
     "swps_unigram_starts": (ctypes.c_int, [_p, _p, _u64, _u64, _p]),
     "swps_glibc_rand": (ctypes.c_int, [ctypes.c_uint32, _u64, _u64, _p]),
     "swps_s2v_create": (ctypes.c_int, [_p, ctypes.POINTER(S2VCfg), ctypes.POINTER(_p)]),

@@ -30,6 +30,13 @@ class Comm:
         return cls(h, rank, world)
 
     @classmethod
+    def tcp(cls, rank, world, device=0, addr="127.0.0.1", port=29612, timeout_ms=60000):
+        """The library's own TCP star transport (several ranks may share a GPU)."""
+        h = ctypes.c_void_p()
+        check(capi.lib().swps_comm_create_tcp(addr.encode(), port, rank, world, device, timeout_ms, ctypes.byref(h)))
+        return cls(h, rank, world)
+
+    @classmethod
     def host(cls, group=None, device=0):
         """Host transport over a torch.distributed group (gloo)."""
         import torch

@@ -121,61 +121,6 @@ __global__ void k_scatter_rows(const uint32_t *__restrict__ perm, uint64_t n, co
   }
 }
 
-// all-gather of a small host block (the round header)
-int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipStream_t s) {
-  if (c->world == 1) {
-    memcpy(out, in, bytes);
-    return SWPS_OK;
-  }
-  if (!c->rccl) {
-    if (c->tr.allgather(c->tr.ctx, in, out, bytes) != 0) return fail(SWPS_E_RCCL, "host transport all-gather failed");
-    return SWPS_OK;
-  }
-  SWPS_TRY(c->d_hdr.ensure(bytes * (c->world + 1)));
-  char *d = c->d_hdr.as<char>();
-  SWPS_HIP(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, s));
-  SWPS_NCCL(ncclAllGather(d, d + bytes, bytes, ncclChar, c->nc, s));
-  SWPS_HIP(hipMemcpyAsync(out, d + bytes, bytes * c->world, hipMemcpyDeviceToHost, s));
-  SWPS_HIP(hipStreamSynchronize(s));
-  return SWPS_OK;
-}
-
-// all-to-all-v of device buffers (byte counts per peer, blocks in rank order)
-int comm_alltoallv(swps_table *t, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
-                   const std::vector<uint64_t> &rb, hipStream_t s) {
-  swps_comm *c = t->comm;
-  uint64_t st = 0, rt = 0;
-  for (int r = 0; r < c->world; r++) {
-    st += sb[r];
-    rt += rb[r];
-  }
-  if (c->world == 1) {
-    if (st) SWPS_HIP(hipMemcpyAsync(d_recv, d_send, st, hipMemcpyDeviceToDevice, s));
-    return SWPS_OK;
-  }
-  if (c->rccl) {
-    SWPS_NCCL(ncclGroupStart());
-    uint64_t so = 0, ro = 0;
-    for (int r = 0; r < c->world; r++) {
-      if (sb[r]) SWPS_NCCL(ncclSend((const char *)d_send + so, sb[r], ncclChar, r, c->nc, s));
-      if (rb[r]) SWPS_NCCL(ncclRecv((char *)d_recv + ro, rb[r], ncclChar, r, c->nc, s));
-      so += sb[r];
-      ro += rb[r];
-    }
-    SWPS_NCCL(ncclGroupEnd());
-    return SWPS_OK;
-  }
-  t->h_send.resize(std::max<uint64_t>(st, 1));
-  t->h_recv.resize(std::max<uint64_t>(rt, 1));
-  if (st) SWPS_HIP(hipMemcpyAsync(t->h_send.data(), d_send, st, hipMemcpyDeviceToHost, s));
-  SWPS_HIP(hipStreamSynchronize(s));
-  if (c->tr.alltoallv(c->tr.ctx, t->h_send.data(), sb.data(), t->h_recv.data(), rb.data()) != 0)
-    return fail(SWPS_E_RCCL, "host transport all-to-all-v failed");
-  if (rt) SWPS_HIP(hipMemcpyAsync(d_recv, t->h_recv.data(), rt, hipMemcpyHostToDevice, s));
-  SWPS_HIP(hipStreamSynchronize(s));  // h_recv is reused by the next exchange
-  return SWPS_OK;
-}
-
 // One round.  op: kOpPull (d_io = values out, table dtype [n][pull elems]),
 // kOpPush (d_io = mean gradients in, the push wire type [n][push elems]) or
 // kOpFinish (n = 0).  Returns the op every active rank ran (or kOpFinish when
@@ -247,7 +192,7 @@ int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void 
     for (int r = 0; r < world; r++) b[r] = k[r] * w;
     return b;
   };
-  SWPS_TRY(comm_alltoallv(t, keys_s, scaled(send_k, 8), t->r_rkeys.p, scaled(recv_k, 8), s));
+  SWPS_TRY(comm_alltoallv(t->comm, keys_s, scaled(send_k, 8), t->r_rkeys.p, scaled(recv_k, 8), s, t->stage));
   const size_t vb = agreed == kOpPull ? pb : gb;
   SWPS_TRY(t->r_rows.ensure(std::max<uint64_t>(nrecv, 1) * 4));
   SWPS_TRY(t->r_rbuf.ensure(std::max<uint64_t>(nrecv, 1) * vb));
@@ -259,7 +204,7 @@ int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void 
   if (agreed == kOpPush) {
     if (n) k_gather_rows<<<nblocks(n * 64), 256, 0, s>>>(perm, n, (const char *)d_io, t->r_buf.as<char>(), gb);
     SWPS_HIP(hipGetLastError());
-    SWPS_TRY(comm_alltoallv(t, t->r_buf.p, scaled(send_k, gb), t->r_rbuf.p, scaled(recv_k, gb), s));
+    SWPS_TRY(comm_alltoallv(t->comm, t->r_buf.p, scaled(send_k, gb), t->r_rbuf.p, scaled(recv_k, gb), s, t->stage));
     t->rstats[3] += n * (8 + gb);
     t->rstats[4] += remote * (8 + gb);
     // ---- 4. owner: the push rule, one step per source in rank order ----
@@ -275,7 +220,7 @@ int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void 
     SWPS_TRY(table_copy_pull(t, t->r_rows.as<uint32_t>(), nrecv, t->r_rbuf.p, s));
   }
   // ---- 5. values back to the requesters, then to the caller's key order ----
-  SWPS_TRY(comm_alltoallv(t, t->r_rbuf.p, scaled(recv_k, pb), t->r_buf.p, scaled(send_k, pb), s));
+  SWPS_TRY(comm_alltoallv(t->comm, t->r_rbuf.p, scaled(recv_k, pb), t->r_buf.p, scaled(send_k, pb), s, t->stage));
   t->rstats[3] += n * 8 + nrecv * pb;
   t->rstats[4] += remote * 8;
   for (int r = 0; r < world; r++)
@@ -389,6 +334,67 @@ int star_alltoallv(void *ctx, const void *send, const uint64_t *sb, void *recv, 
 }  // namespace
 
 namespace swps {
+
+// all-gather of a small host block (round headers, count matrices)
+int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipStream_t s) {
+  if (c->world == 1) {
+    memcpy(out, in, bytes);
+    return SWPS_OK;
+  }
+  if (!c->rccl) {
+    if (c->tr.allgather(c->tr.ctx, in, out, bytes) != 0) return fail(SWPS_E_RCCL, "host transport all-gather failed");
+    return SWPS_OK;
+  }
+  SWPS_TRY(c->d_hdr.ensure(bytes * (c->world + 1)));
+  char *d = c->d_hdr.as<char>();
+  SWPS_HIP(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, s));
+  SWPS_NCCL(ncclAllGather(d, d + bytes, bytes, ncclChar, c->nc, s));
+  SWPS_HIP(hipMemcpyAsync(out, d + bytes, bytes * c->world, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  return SWPS_OK;
+}
+
+// all-to-all-v of device buffers (byte counts per peer, blocks in rank
+// order), ordered on stream s: RCCL send/recv groups, or host staging
+// through `st` and the transport's callback (synchronous)
+int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
+                   const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg) {
+  uint64_t st = 0, rt = 0;
+  for (int r = 0; r < c->world; r++) {
+    st += sb[r];
+    rt += rb[r];
+  }
+  if (c->world == 1) {
+    if (st) SWPS_HIP(hipMemcpyAsync(d_recv, d_send, st, hipMemcpyDeviceToDevice, s));
+    return SWPS_OK;
+  }
+  if (c->rccl) {
+    SWPS_NCCL(ncclGroupStart());
+    uint64_t so = 0, ro = 0;
+    for (int r = 0; r < c->world; r++) {
+      if (sb[r]) SWPS_NCCL(ncclSend((const char *)d_send + so, sb[r], ncclChar, r, c->nc, s));
+      if (rb[r]) SWPS_NCCL(ncclRecv((char *)d_recv + ro, rb[r], ncclChar, r, c->nc, s));
+      so += sb[r];
+      ro += rb[r];
+    }
+    SWPS_NCCL(ncclGroupEnd());
+    return SWPS_OK;
+  }
+  stg.send.resize(std::max<uint64_t>(st, 1));
+  stg.recv.resize(std::max<uint64_t>(rt, 1));
+  if (st) SWPS_HIP(hipMemcpyAsync(stg.send.data(), d_send, st, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  if (c->tr.alltoallv(c->tr.ctx, stg.send.data(), sb.data(), stg.recv.data(), rb.data()) != 0)
+    return fail(SWPS_E_RCCL, "host transport all-to-all-v failed");
+  if (rt) SWPS_HIP(hipMemcpyAsync(d_recv, stg.recv.data(), rt, hipMemcpyHostToDevice, s));
+  SWPS_HIP(hipStreamSynchronize(s));  // stg.recv is reused by the next exchange
+  return SWPS_OK;
+}
+
+int comm_rank(const swps_comm *c) { return c->rank; }
+int comm_world(const swps_comm *c) { return c->world; }
+int comm_device(const swps_comm *c) { return c->device; }
+bool comm_is_rccl(const swps_comm *c) { return c->rccl; }
 
 int routed_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals, hipStream_t s) {
   if (t->finished) return fail(SWPS_E_STATE, "pull after swps_finish");

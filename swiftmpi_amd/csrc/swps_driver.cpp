@@ -1,0 +1,194 @@
+// Library-driven sharded app loop (swps_w2v_shard_comm / swps_lr_shard_comm):
+// the lockstep minibatch exchange of SURVEY.md §8(e) issued by the library
+// over its own communicator, so a C/C++ host (include/swiftmpi_compat.h's
+// Word2VecApp / LRApp) trains on several GPUs without moving payloads itself.
+// Per minibatch i, every rank (weak scaling: its own corpus; owner of the
+// keys BasicHashFrag gives node rank+1):
+//   serve stream S:  request(i) -> a2a keys -> serve_pull -> a2a values
+//   compute stream C:   wait -> step(i): install, learn, mean gradients
+//                       -> prep(i+1): records, sort, index (param-free)
+//   S:  wait step(i) -> a2a gradients -> serve_push (one AdaGrad step per
+//       source, in rank order; server.h:156-176)
+// so every pull sees every earlier push (the reference's single-worker
+// semantics, lockstep) and prep(i+1) overlaps push(i) / pull(i+1).  Ranks
+// whose corpora have fewer minibatches run empty steps (steps_per_epoch =
+// the maximum over ranks); per-step key counts come from the static batch
+// schedules and are exchanged once at setup, so no step needs a handshake.
+// The same protocol as swiftmpi_amd/dist.py's Python driver.
+#include <algorithm>
+
+#include "swps_internal.h"
+
+namespace swps {
+
+ShardDriver::~ShardDriver() {
+  if (ev_pull) (void)hipEventDestroy(ev_pull);
+  if (ev_learn) (void)hipEventDestroy(ev_learn);
+  if (ev_x0) (void)hipEventDestroy(ev_x0);
+  if (ev_x1) (void)hipEventDestroy(ev_x1);
+  if (S && S != ops.cs) {
+    (void)hipStreamSynchronize(S);
+    (void)hipStreamDestroy(S);
+  }
+}
+
+int ShardDriver::setup() {
+  rank = comm_rank(c);
+  world = comm_world(c);
+  // apps whose server work cannot move to another stream run everything on theirs
+  if (ops.set_serve_stream)
+    SWPS_HIP(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
+  else
+    S = ops.cs;
+  SWPS_HIP(hipEventCreateWithFlags(&ev_pull, hipEventDisableTiming));
+  SWPS_HIP(hipEventCreateWithFlags(&ev_learn, hipEventDisableTiming));
+  SWPS_HIP(hipEventCreate(&ev_x0));
+  SWPS_HIP(hipEventCreate(&ev_x1));
+  uint64_t n = 0;
+  std::vector<uint64_t> bc(1);
+  (void)ops.batch_counts(ops.h, bc.data(), 0, &n);  // "buffer too small", but *n = the batch count
+  nb = n;
+  bc.assign(std::max<uint64_t>(nb * world, 1), 0);
+  SWPS_TRY(ops.batch_counts(ops.h, bc.data(), bc.size(), &n));
+  // steps per epoch = max over ranks; then everyone's [step][dst] counts
+  std::vector<int64_t> nbs(world);
+  const int64_t mine = (int64_t)nb;
+  SWPS_TRY(comm_allgather(c, &mine, nbs.data(), 8, ops.cs));
+  spe = 0;
+  for (auto v : nbs) spe = std::max<uint64_t>(spe, (uint64_t)v);
+  std::vector<uint64_t> mat(spe * world, 0), all(spe * world * world);
+  std::copy(bc.begin(), bc.begin() + nb * world, mat.begin());
+  if (spe) SWPS_TRY(comm_allgather(c, mat.data(), all.data(), spe * world * 8, ops.cs));
+  send.assign(spe * world, 0);
+  recv.assign(spe * world, 0);
+  for (uint64_t st = 0; st < spe; st++)
+    for (int r = 0; r < world; r++) {
+      send[st * world + r] = all[((uint64_t)rank * spe + st) * world + r];  // I send to r
+      recv[st * world + r] = all[((uint64_t)r * spe + st) * world + rank];  // r sends to me
+    }
+  // size the step buffers once (a grow inside a step would free memory in flight)
+  uint64_t ms = 1, mr = 1;
+  for (uint64_t st = 0; st < spe; st++) {
+    uint64_t ns = 0, nr = 0;
+    for (int r = 0; r < world; r++) {
+      ns += send[st * world + r];
+      nr += recv[st * world + r];
+    }
+    ms = std::max(ms, ns);
+    mr = std::max(mr, nr);
+  }
+  const uint64_t vb = ops.width * ops.val_bytes, gb = ops.width * ops.grad_bytes;
+  SWPS_TRY(keys.ensure(ms * 8));
+  SWPS_TRY(myvals.ensure(ms * vb));
+  SWPS_TRY(grads.ensure(ms * gb));
+  SWPS_TRY(rkeys.ensure(mr * 8));
+  SWPS_TRY(vals.ensure(mr * vb));
+  SWPS_TRY(rgrads.ensure(mr * gb));
+  step_keys = ms;
+  step_rkeys = mr;
+  return SWPS_OK;
+}
+
+static std::vector<uint64_t> scaled(const uint64_t *k, int world, uint64_t w) {
+  std::vector<uint64_t> b(world);
+  for (int r = 0; r < world; r++) b[r] = k[r] * w;
+  return b;
+}
+
+int ShardDriver::exchange(const void *d_send, const uint64_t *sk, void *d_recv, const uint64_t *rk, uint64_t w,
+                          hipStream_t s) {
+  if (xprof) {
+    SWPS_HIP(hipEventRecord(ev_x0, s));
+    for (int r = 0; r < world; r++) {
+      bytes_total += sk[r] * w;
+      if (r != rank) bytes_remote += sk[r] * w;
+    }
+    calls++;
+  }
+  SWPS_TRY(comm_alltoallv(c, d_send, scaled(sk, world, w), d_recv, scaled(rk, world, w), s, stage));
+  if (xprof) {
+    SWPS_HIP(hipEventRecord(ev_x1, s));
+    SWPS_HIP(hipEventSynchronize(ev_x1));  // profiled runs only
+    float ms = 0;
+    SWPS_HIP(hipEventElapsedTime(&ms, ev_x0, ev_x1));
+    xms += ms;
+  }
+  return SWPS_OK;
+}
+
+int ShardDriver::full_pull() {
+  SWPS_TRY(sync());  // the full pull reuses the step buffers
+  std::vector<uint64_t> cnt(world), all((size_t)world * world);
+  uint64_t n = 0;
+  SWPS_TRY(ops.request(ops.h, 1, cnt.data(), nullptr, &n));
+  DevMem &fk = fp_keys, &frk = fp_rkeys, &fv = fp_vals, &fmv = fp_myvals;  // full-vocab sized, freed after
+  SWPS_TRY(fk.ensure(std::max<uint64_t>(n, 1) * 8));
+  SWPS_TRY(ops.request(ops.h, 1, cnt.data(), fk.as<uint64_t>(), &n));
+  SWPS_TRY(comm_allgather(c, cnt.data(), all.data(), world * 8, ops.cs));
+  std::vector<uint64_t> rc(world);
+  uint64_t nr = 0;
+  for (int r = 0; r < world; r++) nr += (rc[r] = all[(size_t)r * world + rank]);
+  SWPS_TRY(frk.ensure(std::max<uint64_t>(nr, 1) * 8));
+  SWPS_TRY(fv.ensure(std::max<uint64_t>(nr, 1) * ops.width * ops.val_bytes));
+  SWPS_TRY(fmv.ensure(std::max<uint64_t>(n, 1) * ops.width * ops.val_bytes));
+  SWPS_TRY(exchange(fk.p, cnt.data(), frk.p, rc.data(), 8, ops.cs));
+  SWPS_TRY(ops.serve_pull(ops.h, frk.as<uint64_t>(), rc.data(), 1, fv.p));
+  SWPS_TRY(exchange(fv.p, rc.data(), fmv.p, cnt.data(), ops.width * ops.val_bytes, ops.cs));
+  SWPS_TRY(ops.install(ops.h, fmv.p));
+  SWPS_HIP(hipStreamSynchronize(ops.cs));
+  fk.release();
+  frk.release();
+  fv.release();
+  fmv.release();
+  // server-side work of the steps goes to S from here on
+  if (ops.set_serve_stream) SWPS_TRY(ops.set_serve_stream(ops.h, S));
+  return SWPS_OK;
+}
+
+int ShardDriver::steps(uint64_t count) {
+  const uint64_t vb = ops.width * ops.val_bytes, gb = ops.width * ops.grad_bytes;
+  for (uint64_t k = 0; k < count; k++) {
+    const uint64_t st = cursor % spe;
+    const uint64_t *sk = &send[st * world], *rk = &recv[st * world];
+    uint64_t ns = 0, nr = 0;
+    for (int r = 0; r < world; r++) {
+      ns += sk[r];
+      nr += rk[r];
+    }
+    if (ns > step_keys || nr > step_rkeys) return fail(SWPS_E_STATE, "step larger than the setup's schedule");
+    const bool mine = st < nb;
+    // ---- S: pull(i) (C's earlier work on these buffers is ordered by events) ----
+    SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+    if (mine && ns) {
+      std::vector<uint64_t> cnt(world);
+      uint64_t n = 0;
+      SWPS_TRY(ops.request(ops.h, 0, cnt.data(), keys.as<uint64_t>(), &n));
+    }
+    SWPS_TRY(exchange(keys.p, sk, rkeys.p, rk, 8, S));
+    SWPS_TRY(ops.serve_pull(ops.h, rkeys.as<uint64_t>(), rk, 0, vals.p));
+    SWPS_TRY(exchange(vals.p, rk, myvals.p, sk, vb, S));
+    SWPS_HIP(hipEventRecord(ev_pull, S));
+    // ---- C: learn(i), then prep(i+1) ----
+    SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_pull, 0));
+    if (mine) SWPS_TRY(ops.step(ops.h, ns ? myvals.p : nullptr, ns ? grads.p : nullptr));
+    SWPS_HIP(hipEventRecord(ev_learn, ops.cs));
+    const uint64_t nxt = (cursor + 1) % spe;
+    if (ops.prep && k + 1 < count && nxt < nb) SWPS_TRY(ops.prep(ops.h));
+    // ---- S: push(i) ----
+    SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+    SWPS_TRY(exchange(grads.p, sk, rgrads.p, rk, gb, S));
+    SWPS_TRY(ops.serve_push(ops.h, rkeys.as<uint64_t>(), rgrads.p, rk));
+    cursor++;
+  }
+  SWPS_HIP(hipEventRecord(ev_learn, S));  // the next call's C work waits for this push
+  SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_learn, 0));
+  return SWPS_OK;
+}
+
+int ShardDriver::sync() {
+  SWPS_HIP(hipStreamSynchronize(S));
+  SWPS_HIP(hipStreamSynchronize(ops.cs));
+  return SWPS_OK;
+}
+
+}  // namespace swps

@@ -64,6 +64,11 @@ template <typename T> int upload(DevMem &m, const std::vector<T> &v, hipStream_t
   return SWPS_OK;
 }
 
+// host staging buffers of a host-transport exchange
+struct HostStage {
+  std::vector<char> send, recv;
+};
+
 // ---- hashing / RNG (host + device) ----------------------------------------
 __host__ __device__ inline uint64_t fmix64(uint64_t x) {  // utils/HashFunction.h:16-24
   x ^= x >> 33;
@@ -174,7 +179,7 @@ struct swps_table {
   int32_t frag_num = 0;
   swps::DevMem frag_map;  // u32[frag_num]: frag -> node id (1..world)
   swps::DevMem r_owner, r_pos, r_owner_s, r_perm, r_keys, r_buf, r_rkeys, r_rbuf, r_rows, r_tmp, r_cnt;
-  std::vector<char> h_send, h_recv;  // host staging (host transport)
+  swps::HostStage stage;  // host staging (host transport)
   uint64_t rstats[6] = {0, 0, 0, 0, 0, 0};
   bool finished = false;
 };
@@ -200,6 +205,54 @@ int table_error_code(uint32_t flags);
 // key-sharded pull / push (swps_comm.hip): collective over t->comm
 int routed_pull(swps_table *t, const uint64_t *d_keys, uint64_t n, void *d_vals, hipStream_t s);
 int routed_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_grads, hipStream_t s);
-// app contexts take plain local AdaGrad shards only
+// app contexts take AdaGrad shards only
 int check_app_table(swps_table *t);
+// communicator exchanges (swps_comm.hip), ordered on stream s
+int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipStream_t s);
+int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
+                   const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg);
+int comm_rank(const swps_comm *c);
+int comm_world(const swps_comm *c);
+int comm_device(const swps_comm *c);
+bool comm_is_rccl(const swps_comm *c);
+
+// ---- library-driven sharded app loop (swps_driver.cpp) ---------------------
+// An app context's sharded-mode entry points (swps_<app>_request /
+// serve_pull / step / serve_push ...) and payload widths.
+struct AppOps {
+  void *h = nullptr;
+  hipStream_t cs = nullptr;  // the app's compute stream
+  uint64_t width = 0, val_bytes = 0, grad_bytes = 0;
+  int (*batch_counts)(void *, uint64_t *, uint64_t, uint64_t *) = nullptr;
+  int (*request)(void *, int32_t, uint64_t *, uint64_t *, uint64_t *) = nullptr;
+  int (*serve_pull)(void *, const uint64_t *, const uint64_t *, int32_t, void *) = nullptr;
+  int (*install)(void *, const void *) = nullptr;
+  int (*step)(void *, const void *, void *) = nullptr;
+  int (*serve_push)(void *, const uint64_t *, const void *, const uint64_t *) = nullptr;
+  int (*prep)(void *) = nullptr;                      // optional: the next step's param-free half
+  int (*set_serve_stream)(void *, void *) = nullptr;  // optional: server work on the driver's stream
+};
+
+struct ShardDriver {
+  AppOps ops;
+  swps_comm *c = nullptr;
+  int rank = 0, world = 1;
+  uint64_t nb = 0, spe = 0, cursor = 0;  // own batches, steps per epoch (max over ranks), steps run
+  std::vector<uint64_t> send, recv;      // [step][rank] key counts
+  DevMem keys, rkeys, vals, myvals, grads, rgrads;  // per step, sized at setup for the largest step
+  DevMem fp_keys, fp_rkeys, fp_vals, fp_myvals;      // the full pull's (whole local vocab)
+  uint64_t step_keys = 0, step_rkeys = 0;
+  HostStage stage;
+  hipStream_t S = nullptr;
+  hipEvent_t ev_pull = nullptr, ev_learn = nullptr, ev_x0 = nullptr, ev_x1 = nullptr;
+  bool xprof = false;  // exchange accounting: bytes and event-timed exchanges (syncs per exchange)
+  uint64_t bytes_total = 0, bytes_remote = 0, calls = 0;
+  double xms = 0;
+  ~ShardDriver();
+  int setup();
+  int full_pull();
+  int steps(uint64_t count);
+  int sync();
+  int exchange(const void *d_send, const uint64_t *sk, void *d_recv, const uint64_t *rk, uint64_t w, hipStream_t s);
+};
 }  // namespace swps

@@ -23,6 +23,8 @@
 #include <unordered_set>
 
 #include "swps_internal.h"
+#include "swps_sort.h"
+#include "swps_wave.h"
 
 using namespace swps;
 
@@ -90,10 +92,12 @@ struct LrReduce {
   const int32_t *local;
   float *grads;
   uint32_t *nlong, *longs;
+  int fast;  // swps_lr_cfg.fast_sums: fp64 sums (tree-reduced for long runs) instead of the fp32 chain
 };
 
-__device__ __forceinline__ void lr_apply(const LrReduce &a, uint32_t r, float s, uint32_t c) {
-  const float m = float(s / c);
+// mean = s / count in fp32 (lr.cpp:32-38); fast mode passes the fp64 sum
+__device__ __forceinline__ void lr_apply(const LrReduce &a, uint32_t r, float s, uint32_t c, double s64 = 0.0) {
+  const float m = a.fast ? (float)(s64 / (double)c) : float(s / c);
   if (a.grads) {
     a.grads[a.local[a.uniq[r]]] = m;
     return;
@@ -111,6 +115,12 @@ __global__ __launch_bounds__(256) void k_lr_reduce_short(LrReduce a) {
     const uint32_t o = a.off[r], c = a.cnt[r];
     if (c > kLrShort) {
       a.longs[atomicAdd(a.nlong, 1u)] = r;
+      continue;
+    }
+    if (a.fast) {
+      double s = 0;
+      for (uint32_t i = o; i < o + c; i++) s += (double)a.val[i];
+      lr_apply(a, r, 0.f, c, s);
       continue;
     }
     float s = 0;
@@ -133,6 +143,20 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long(LrReduce a) {
   for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < NL; q += gridDim.x * 4) {
     const uint32_t r = a.longs[q];
     const uint32_t o = a.off[r], c = a.cnt[r];
+    if (a.fast) {  // every lane sums a strided slice in fp64, then one fixed-order wave reduction
+      double s4[4] = {0.0, 0.0, 0.0, 0.0};
+      uint32_t k = lane;
+      for (; k + 192 < c; k += 256) {
+        s4[0] += (double)a.val[o + k];
+        s4[1] += (double)a.val[o + k + 64];
+        s4[2] += (double)a.val[o + k + 128];
+        s4[3] += (double)a.val[o + k + 192];
+      }
+      for (; k < c; k += 64) s4[0] += (double)a.val[o + k];
+      const double tot = wave_sum_pl((s4[0] + s4[1]) + (s4[2] + s4[3]));
+      if (lane == 0) lr_apply(a, r, 0.f, c, tot);
+      continue;
+    }
     float s = 0;
     float x[kLrStage / 64];
 #pragma unroll
@@ -261,6 +285,7 @@ struct swps_lr {
   std::vector<int32_t> allK, init_order;  // vids
   std::vector<uint64_t> kofs, bU, bcounts, icounts;
   DevMem d_K, d_vkeys, d_init_order, d_wcache, d_local, d_serve_rows;
+  swps::ShardDriver *drv = nullptr;  // swps_lr_shard_comm: the library drives the exchange
   uint64_t serve_n = 0;
   int B1() const { return cfg.minibatch + 1; }
 };
@@ -332,18 +357,16 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   while ((1ULL << bits) <= l->vocab_keys.size()) bits++;
   hipEvent_t e1 = l->timer.begin(s);
   size_t b1 = 0, b2 = 0, b3 = 0;
-  SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(),
-                                              l->d_contrib.as<float>(), l->d_val_s.as<float>(), (int)nnz, 0, bits,
-                                              s));
+  SWPS_HIP(sort_pairs(nullptr, b1, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(), l->d_contrib.as<float>(),
+                      l->d_val_s.as<float>(), nnz, bits, s));
   SWPS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, l->d_keys_s.as<uint32_t>(), l->d_uniq.as<uint32_t>(),
                                                  l->d_cnt.as<uint32_t>(), l->d_nruns.as<uint32_t>(), (int)nnz, s));
   SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b3, l->d_cnt.as<uint32_t>(), l->d_off.as<uint32_t>(),
                                             (int)nnz, s));
   SWPS_TRY(l->d_tmp.ensure(std::max(b1, std::max(b2, b3))));
   size_t tb = l->d_tmp.bytes;
-  SWPS_HIP(hipcub::DeviceRadixSort::SortPairs(l->d_tmp.p, tb, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(),
-                                              l->d_contrib.as<float>(), l->d_val_s.as<float>(), (int)nnz, 0, bits,
-                                              s));
+  SWPS_HIP(sort_pairs(l->d_tmp.p, tb, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(), l->d_contrib.as<float>(),
+                      l->d_val_s.as<float>(), nnz, bits, s));
   tb = l->d_tmp.bytes;
   SWPS_HIP(hipcub::DeviceRunLengthEncode::Encode(l->d_tmp.p, tb, l->d_keys_s.as<uint32_t>(), l->d_uniq.as<uint32_t>(),
                                                  l->d_cnt.as<uint32_t>(), l->d_nruns.as<uint32_t>(), (int)nnz, s));
@@ -358,7 +381,7 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   LrReduce ra{l->d_uniq.as<uint32_t>(), l->d_cnt.as<uint32_t>(), l->d_off.as<uint32_t>(), l->d_nruns.as<uint32_t>(),
               l->d_val_s.as<float>(), l->d_vid_row.as<uint32_t>(), l->t->rows.as<float>(), l->t->cfg.learning_rate,
               l->t->cfg.fudge, l->d_local.as<int32_t>(), l->sharded ? d_grads : nullptr, nlong,
-              l->d_longs.as<uint32_t>()};
+              l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
   k_lr_reduce_short<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(ra);
   k_lr_reduce_long<<<(unsigned)std::min<uint64_t>(nblk(nnz * 64 / kLrShort), 2048), 256, 0, s>>>(ra);
   SWPS_HIP(hipGetLastError());
@@ -397,6 +420,7 @@ int swps_lr_destroy(swps_lr *l) {
   (void)hipStreamSynchronize(l->s);
   l->timer.resolve();
   if (l->h_small) (void)hipHostFree(l->h_small);
+  delete l->drv;
   delete l;
   (void)hipGetLastError();  // leave no sticky error from the calls above
   return SWPS_OK;
@@ -455,6 +479,10 @@ int swps_lr_load_csr(swps_lr *l, const float *labels, uint64_t nrows, const uint
 int swps_lr_init(swps_lr *l) {
   if (!l->loaded) return fail(SWPS_E_STATE, "load data first");
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  if (l->drv) return l->drv->full_pull();  // the first full pull, over the communicator
+  if (l->t->comm)
+    return fail(SWPS_E_UNSUPPORTED, "the table is key-sharded (swps_table_route): drive the context with "
+                                    "swps_lr_shard_comm");
   const uint64_t V = l->vocab_keys.size();
   DevMem dk;
   SWPS_TRY(upload(dk, l->vocab_keys, l->s));
@@ -477,6 +505,10 @@ int swps_lr_init(swps_lr *l) {
 }
 
 int swps_lr_train_batches(swps_lr *l, uint64_t count) {
+  if (l->drv) {
+    SWPS_HIP(hipSetDevice(l->t->cfg.device));
+    return l->drv->steps(count);  // collective
+  }
   if (l->sharded) return fail(SWPS_E_STATE, "sharded: drive swps_lr_request/serve_pull/step/serve_push");
   if (!l->inited) return fail(SWPS_E_STATE, "call swps_lr_init first");
   if (l->nbatches == 0) return SWPS_OK;
@@ -500,6 +532,15 @@ int swps_lr_epoch_error(swps_lr *l, double *err) {
 }
 
 int swps_lr_train(swps_lr *l, int32_t niters, double *err_out) {
+  if (l->drv) {  // lockstep epochs of steps_per_epoch steps; error of this rank's rows
+    if (l->drv->spe && l->drv->cursor % l->drv->spe) return fail(SWPS_E_STATE, "not at an epoch boundary");
+    for (int it = 0; it < niters; it++) {
+      SWPS_TRY(l->drv->steps(l->drv->spe));
+      SWPS_TRY(l->drv->sync());
+      if (err_out) SWPS_TRY(swps_lr_epoch_error(l, &err_out[it]));
+    }
+    return swps_lr_sync(l);
+  }
   if (l->sharded) return fail(SWPS_E_STATE, "sharded: drive swps_lr_request/serve_pull/step/serve_push");
   if (l->cursor % std::max<uint64_t>(1, l->nbatches)) return fail(SWPS_E_STATE, "not at an epoch boundary");
   for (int it = 0; it < niters; it++) {
@@ -511,6 +552,7 @@ int swps_lr_train(swps_lr *l, int32_t niters, double *err_out) {
 
 int swps_lr_sync(swps_lr *l) {
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  if (l->drv) SWPS_TRY(l->drv->sync());
   SWPS_HIP(hipStreamSynchronize(l->s));
   l->timer.resolve();
   return SWPS_OK;
@@ -521,6 +563,10 @@ int swps_lr_predict(swps_lr *l, float *pred_out, float *target_out, uint64_t cap
   const uint64_t nr = l->label.size();
   if (cap < nr) return fail(SWPS_E_CFG, "buffer too small");
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  if (l->drv) {  // refresh the worker cache with a full pull (collective)
+    SWPS_TRY(l->drv->sync());
+    SWPS_TRY(l->drv->full_pull());
+  }
   SWPS_TRY(l->d_pred.ensure(std::max<uint64_t>(1, nr) * 4));
   k_lr_predict<<<nblk(nr * 64), 256, 0, l->s>>>(l->d_row_off.as<uint64_t>(), l->d_fvid.as<int32_t>(), l->d_fval.as<float>(),
                                             nr, l->sharded ? nullptr : l->d_vid_row.as<uint32_t>(),
@@ -733,6 +779,42 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
   SWPS_TRY(table_lookup(l->t, d_keys, n, l->d_serve_rows.as<uint32_t>(), l->s));
   // one AdaGrad step per source, in rank order, all sources in one pass
   return table_push_sources(l->t, l->d_serve_rows.as<uint32_t>(), n, d_grads, l->s);
+}
+
+int swps_lr_shard_comm(swps_lr *l, swps_comm *c, int32_t frag_num) {
+  if (!c) return fail(SWPS_E_CFG, "null communicator");
+  if (comm_device(c) != l->t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");
+  if (l->t->comm && l->t->comm != c) return fail(SWPS_E_CFG, "the table is routed over another communicator");
+  SWPS_TRY(swps_lr_shard(l, comm_rank(c), comm_world(c), frag_num));
+  ShardDriver *d = new ShardDriver();
+  d->c = c;
+  AppOps &o = d->ops;
+  o.h = l;
+  o.cs = l->s;
+  o.width = 1;
+  o.val_bytes = 4;
+  o.grad_bytes = 4;
+  o.batch_counts = [](void *h, uint64_t *out, uint64_t cap, uint64_t *nb) {
+    return swps_lr_batch_counts((swps_lr *)h, out, cap, nb);
+  };
+  o.request = [](void *h, int32_t init, uint64_t *cnt, uint64_t *k, uint64_t *n) {
+    return swps_lr_request((swps_lr *)h, init, cnt, k, n);
+  };
+  o.serve_pull = [](void *h, const uint64_t *k, const uint64_t *sc, int32_t ins, void *v) {
+    return swps_lr_serve_pull((swps_lr *)h, k, sc, ins, (float *)v);
+  };
+  o.install = [](void *h, const void *v) { return swps_lr_install((swps_lr *)h, (const float *)v); };
+  o.step = [](void *h, const void *v, void *g) { return swps_lr_step((swps_lr *)h, (const float *)v, (float *)g); };
+  o.serve_push = [](void *h, const uint64_t *k, const void *g, const uint64_t *sc) {
+    return swps_lr_serve_push((swps_lr *)h, k, (const float *)g, sc);
+  };
+  const int rc = d->setup();
+  if (rc) {
+    delete d;
+    return rc;
+  }
+  l->drv = d;
+  return SWPS_OK;
 }
 
 void *swps_lr_stream(swps_lr *l) { return (void *)l->s; }

@@ -380,9 +380,6 @@ int check_app_table(swps_table *t) {
   if (t->cfg.push_rule != SWPS_PUSH_ADAGRAD)
     return fail(SWPS_E_UNSUPPORTED, "app contexts apply the reference apps' AdaGrad rule: the table's push_rule "
                                     "must be SWPS_PUSH_ADAGRAD");
-  if (t->comm)
-    return fail(SWPS_E_UNSUPPORTED, "app contexts need a local shard (swps_w2v_shard / swps_lr_shard route their "
-                                    "own exchange), not a table bound by swps_table_route");
   return SWPS_OK;
 }
 

@@ -789,11 +789,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
 }
 
+constexpr uint32_t kGroupDesc = 16;  // = kGroup (k_combine's group size)
+
 // item descriptors {first record, end record | kind << 31, (key, kind) index j, chunk}:
 // one thread per item (hot keys have thousands of chunks), j found by binary
 // search over the item offsets ioff[0..2U].
 __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__restrict__ ioff, uint32_t U,
-                            uint32_t CH, uint64_t max_items, uint4 *__restrict__ desc) {
+                            uint32_t CH, uint64_t max_items, uint4 *__restrict__ desc, uint32_t *__restrict__ lead) {
   const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= max_items || item >= ioff[2ull * U]) return;
   uint32_t lo = 0, hi = 2 * U;  // largest j with ioff[j] <= item
@@ -808,6 +810,10 @@ __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__
   const uint32_t s = seg[(2 * kind) * U + u], e = seg[(2 * kind + 1) * U + u];
   const uint32_t cs = s + k * CH;
   desc[item] = make_uint4(cs, min(cs + CH, e) | (kind << 31), jj, k);
+  // hot (key, kind) runs of more than kGroup chunks: k_combine pre-sums each
+  // group of kGroup partials into its leader (the list order does not
+  // matter: every leader writes only its own slot)
+  if (lead && ioff[jj + 1] - ioff[jj] > kGroupDesc && k % kGroupDesc == 0) lead[1 + atomicAdd(&lead[0], 1u)] = (uint32_t)item;
 }
 
 template <typename A> struct GatherArgs {
@@ -821,6 +827,8 @@ template <typename A> struct GatherArgs {
   int D;
   A *partial;
   int ld;  // neu1/neu1e row stride (FwdArgs::ld)
+  const uint32_t *lead;  // hot-group leaders (k_item_desc): [0] = count, then items
+  uint32_t max_items;    // capacity of desc / partial: a bound on ioff[2U] every reader clamps to
 };
 
 // One wave per chunk of <= 128 records of one (key, kind): the fp64 sum, in
@@ -834,7 +842,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
   using CA = Chk<A, E>;
   const int lane = threadIdx.x & 63;
   const int NC = a.D / E;
-  const uint32_t NI = a.ioff[2 * a.U];
+  const uint32_t NI = min(a.ioff[2 * a.U], a.max_items);
   for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
     const uint4 d = a.desc[__builtin_amdgcn_readfirstlane(item)];
     const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
@@ -951,7 +959,7 @@ template <int NCH, int UNR>
 __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
   const int lane = threadIdx.x & 63;
   const bool tl = 256 * NCH + lane < a.D;
-  const uint32_t NI = a.ioff[2 * a.U];
+  const uint32_t NI = min(a.ioff[2 * a.U], a.max_items);
   const uint32_t stride = gridDim.x * 4;
   uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= NI) return;
@@ -1000,8 +1008,7 @@ __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
 }
 
 constexpr uint32_t kGroup = 16;  // hot keys: partials are pre-summed in groups of 16
-// k_combine walks every item to find the few hot-group leaders: a small grid
-// with a stride loop beats dispatching one wave per item
+// k_combine: a stride loop over the leader list k_item_desc collected
 constexpr unsigned kCombineGrid = 1024;
 
 // Hot (key, kind) runs with more than kGroup chunks: each group leader sums
@@ -1012,12 +1019,12 @@ __global__ __launch_bounds__(256) void k_combine(GatherArgs<A> a) {
   using CA = Chk<A, E>;
   const int lane = threadIdx.x & 63;
   const int NC = a.D / E;
-  const uint32_t NI = a.ioff[2 * a.U];
-  for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
+  const uint32_t NL = min(a.lead[0], a.max_items / 8 + 1);
+  for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < NL; q += gridDim.x * 4) {
+    const uint32_t item = a.lead[1 + __builtin_amdgcn_readfirstlane(q)];
     const uint4 d = a.desc[__builtin_amdgcn_readfirstlane(item)];
-    const uint32_t j = d.z, k = d.w;
-    const uint32_t i1 = a.ioff[j + 1], nchunk = i1 - a.ioff[j];
-    if (nchunk <= kGroup || (k % kGroup) != 0) continue;
+    const uint32_t j = d.z;
+    const uint32_t i1 = a.ioff[j + 1];
     const uint32_t end = min(item + kGroup, i1);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -1025,15 +1032,15 @@ __global__ __launch_bounds__(256) void k_combine(GatherArgs<A> a) {
       if (ci >= NC) continue;
       typename CA::R rv[kGroup];
 #pragma unroll
-      for (uint32_t q = 0; q < kGroup; q++) rv[q] = CA::ld(a.partial + (uint64_t)min(item + q, end - 1) * a.D, ci, a.D);
+      for (uint32_t q2 = 0; q2 < kGroup; q2++) rv[q2] = CA::ld(a.partial + (uint64_t)min(item + q2, end - 1) * a.D, ci, a.D);
       double sum[E];
 #pragma unroll
       for (int kk = 0; kk < E; kk++) sum[kk] = 0.0;
 #pragma unroll
-      for (uint32_t q = 0; q < kGroup; q++)
-        if (item + q < end)
+      for (uint32_t q2 = 0; q2 < kGroup; q2++)
+        if (item + q2 < end)
 #pragma unroll
-          for (int kk = 0; kk < E; kk++) sum[kk] += CA::at(rv[q], kk);
+          for (int kk = 0; kk < E; kk++) sum[kk] += CA::at(rv[q2], kk);
       CA::st(a.partial + (uint64_t)item * a.D, ci, a.D, sum);
     }
   }
@@ -1349,6 +1356,8 @@ struct swps_w2v {
   DevMem d_btok, d_bounds;
   DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_pos_tok, d_rec, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
       d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_desc, d_tmp, d_trace, d_rows_touched, d_gstats;
+  swps::ShardDriver *drv = nullptr;  // swps_w2v_shard_comm: the library drives the exchange
+  DevMem d_lead;  // hot-group leaders of the batch's gather items: [0] = count, then item indices
   uint64_t *h_small = nullptr;  // pinned readback
   // RNG (utils/random.h:44-47, seed 2008)
   uint64_t lstate = 2008ULL;
@@ -1383,15 +1392,15 @@ struct swps_w2v {
   // overlapped single-GPU driver (train_overlapped): the second set of the
   // parameter-independent per-batch buffers, swapped with the members above,
   // and the stream prep(i+1) runs on while learn(i) runs on s
-  static constexpr int kPrepBufs = 12;
+  static constexpr int kPrepBufs = 13;
   DevMem alt[kPrepBufs];
   bool alt_local_ready = false;
   int overlap = 0;  // SWPS_OVERLAP=1: train_overlapped (same-box A/B: 4.25e8 sequential vs 4.24e8 / 4.02e8
                     // overlapped — forward and gather already fill every CU and the HBM, so prep only stretches)
   hipStream_t s_prep = nullptr;
   hipEvent_t ev_learn = nullptr, ev_prep = nullptr;
-  DevMem *prep_set[kPrepBufs] = {&d_pos_tok, &d_rec, &d_pkeys, &d_pvals, &d_pkeys_s, &d_pvals_s,
-                                 &d_tmp,     &d_seg, &d_icnt,  &d_ioff,  &d_desc,    &d_local};
+  DevMem *prep_set[kPrepBufs] = {&d_pos_tok, &d_rec,  &d_pkeys, &d_pvals, &d_pkeys_s, &d_pvals_s, &d_tmp,
+                                 &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_local};
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
   // negative trace
@@ -1757,10 +1766,15 @@ template <int NCH, typename T, typename A> void launch_forward(const FwdArgs<T, 
   else
     k_forward<T, A, NCH, 8><<<nblk((uint64_t)a.P * 64), 256, 0, s>>>(a);
 }
-template <int NCH, typename T, typename A> void launch_gather(const GatherArgs<A> &a, unsigned grid, hipStream_t s) {
+// at most max_items / kGroup leaders, 4 per block
+inline unsigned combine_grid(uint64_t max_items) {
+  return (unsigned)std::min<uint64_t>(kCombineGrid, max_items / kGroup / 4 + 1);
+}
+template <int NCH, typename T, typename A>
+void launch_gather(const GatherArgs<A> &a, unsigned grid, unsigned cgrid, hipStream_t s) {
   constexpr int UNR = sizeof(A) * V16<T>::E > 16 ? 4 : 8;
   k_gather<T, A, NCH, UNR><<<grid, 256, 0, s>>>(a);
-  k_combine<T, A, NCH><<<std::min(grid, kCombineGrid), 256, 0, s>>>(a);
+  k_combine<T, A, NCH><<<cgrid, 256, 0, s>>>(a);
 }
 template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A> &a, hipStream_t s) {
   if (a.grads)
@@ -1900,53 +1914,52 @@ __global__ void k_set_local(const int32_t *__restrict__ K, uint32_t U, int32_t *
 // k_set_local and k_positions in one launch (thread i does both jobs' i-th item)
 __global__ void k_batch_setup(const int32_t *__restrict__ K, uint32_t U, int32_t *__restrict__ local,
                               const int32_t *__restrict__ kscan, uint64_t t0, uint64_t nt,
-                              int32_t *__restrict__ pos_tok) {
+                              int32_t *__restrict__ pos_tok, uint4 *__restrict__ seg0, uint32_t *__restrict__ lead) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < U) local[K[i]] = (int32_t)i;
+  if (seg0 && i < U) seg0[i] = make_uint4(0, 0, 0, 0);  // seg[4][U] u32 = U x 16 B: keys without records
+  if (lead && i == 0) lead[0] = 0;
   if (i < nt && pos_tok) {
     const int32_t a = kscan[t0 + i];
     if (kscan[t0 + i + 1] != a) pos_tok[a - kscan[t0]] = (int32_t)(t0 + i);
   }
 }
 
-// Segment bounds and chunk counts of every (local key, kind) run of the
-// sorted records by binary search — one thread per key instead of one per
-// record plus a memset (records of key u: its h records, index < HOFF, then
-// its v records, each run in index order: the sort is stable).
-// seg[0][u], seg[1][u] = h-record range; seg[2][u], seg[3][u] = v-record range;
-// cnt[2u + kind] = chunks of <= CH records; cnt[2U] = 0 (the scan's tail).
-// Profiled passes (gstats) also add the records / items to gstats[0..1].
-__global__ void k_seg_counts(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, uint32_t M,
-                             uint32_t HOFF, uint32_t U, uint32_t CH, uint32_t *__restrict__ seg,
-                             uint32_t *__restrict__ cnt, unsigned long long *__restrict__ gstats) {
+// Segment bounds of every (local key, kind) run of the sorted records, one
+// thread per record (records of key u: its h records, index < HOFF, then its
+// v records, each run in index order: the sort is stable).  seg[0][u],
+// seg[1][u] = h-record range; seg[2][u], seg[3][u] = v-record range; keys
+// without records keep the zeros k_batch_setup wrote.
+__global__ void k_seg_bounds(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, uint32_t M,
+                             uint32_t HOFF, uint32_t U, uint32_t *__restrict__ seg) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const uint32_t u = keys[i];
+  if (u >= U) return;  // "no key" records sort last
+  const bool first = i == 0 || keys[i - 1] != u, last = i + 1 == M || keys[i + 1] != u;
+  const bool isv = vals[i] >= HOFF;
+  if (first) seg[u] = i;
+  if (last) seg[3 * U + u] = i + 1;
+  // the h/v split: the first v record, or the run's end when it has none
+  if ((first && isv) || (!first && isv && vals[i - 1] < HOFF)) {
+    seg[U + u] = i;
+    seg[2 * U + u] = i;
+  } else if (last && !isv) {
+    seg[U + u] = i + 1;
+    seg[2 * U + u] = i + 1;
+  }
+}
+
+// chunks of <= CH records per (key, kind) from the bounds; cnt[2U] = 0 (the
+// scan's tail).  Profiled passes (gstats) also add the records / items to
+// gstats[0..1].
+__global__ void k_seg_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t *__restrict__ cnt,
+                             unsigned long long *__restrict__ gstats) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long rc = 0, ic = 0;
   if (u == U) cnt[2 * U] = 0;
   if (u < U) {
-    auto lower = [&](uint32_t key) {
-      uint32_t lo = 0, hi = M;
-      while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        if (keys[mid] < key)
-          lo = mid + 1;
-        else
-          hi = mid;
-      }
-      return lo;
-    };
-    const uint32_t a = lower(u), b = lower(u + 1);
-    uint32_t lo = a, hi = b;  // first v record of the run
-    while (lo < hi) {
-      const uint32_t mid = lo + ((hi - lo) >> 1);
-      if (vals[mid] < HOFF)
-        lo = mid + 1;
-      else
-        hi = mid;
-    }
-    seg[u] = a;
-    seg[U + u] = lo;
-    seg[2 * U + u] = lo;
-    seg[3 * U + u] = b;
+    const uint32_t a = seg[u], lo = seg[U + u], b = seg[3 * U + u];
     const uint32_t ch = (lo - a + CH - 1) / CH, cv = (b - lo + CH - 1) / CH;
     cnt[2 * u] = ch;
     cnt[2 * u + 1] = cv;
@@ -1990,10 +2003,17 @@ int prep_batch(swps_w2v *w) {
   const bool tracing = w->trace.size() < w->trace_cap;
   const bool recs = P > 0 && (U > 0 || tracing);
   if (recs) SWPS_TRY(w->d_pos_tok.ensure(P * 4));
+  const bool will_sort = recs && U > 0;
+  if (will_sort) {  // zeroed by k_batch_setup: keys without records keep empty segments
+    SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
+    // leaders: at most 2 per 17 items (a run of kGroup + 1 chunks has two)
+    SWPS_TRY(w->d_lead.ensure(((2ULL * U + P * (uint64_t)(N + 1 + 2 * W) / kChunk + 1) / 8 + 2) * 4));
+  }
   if (U || recs) {
     k_batch_setup<<<nblk(std::max<uint64_t>(U, recs ? nt : 0)), 256, 0, s>>>(
         K, U, w->d_local.as<int32_t>(), w->d_kscan.as<int32_t>(), t0, recs ? nt : 0,
-        recs ? w->d_pos_tok.as<int32_t>() : nullptr);
+        recs ? w->d_pos_tok.as<int32_t>() : nullptr, will_sort ? w->d_seg.as<uint4>() : nullptr,
+        will_sort ? w->d_lead.as<uint32_t>() : nullptr);
     SWPS_HIP(hipGetLastError());
   }
   if (recs) {
@@ -2054,12 +2074,12 @@ int prep_batch(swps_w2v *w) {
       sb = w->d_tmp.bytes;
       SWPS_HIP(sort_pairs(w->d_tmp.p, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
                                               w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, s));
-      SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
       SWPS_TRY(w->d_icnt.ensure((2ULL * U + 1) * 4));
       SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
-      k_seg_counts<<<nblk((uint64_t)U + 1), 256, 0, s>>>(
-          w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (uint32_t)M, (uint32_t)HOFF, U, kChunk,
-          w->d_seg.as<uint32_t>(), w->d_icnt.as<uint32_t>(), tm.on ? w->d_gstats.as<unsigned long long>() : nullptr);
+      k_seg_bounds<<<nblk(M), 256, 0, s>>>(w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (uint32_t)M,
+                                            (uint32_t)HOFF, U, w->d_seg.as<uint32_t>());
+      k_seg_counts<<<nblk((uint64_t)U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, w->d_icnt.as<uint32_t>(),
+                                                          tm.on ? w->d_gstats.as<unsigned long long>() : nullptr);
       SWPS_HIP(hipGetLastError());
       size_t ib = 0;
       SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, ib, w->d_icnt.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
@@ -2071,7 +2091,7 @@ int prep_batch(swps_w2v *w) {
       const uint64_t max_items = 2ULL * U + M / kChunk + 1;
       SWPS_TRY(w->d_desc.ensure(max_items * 16));
       k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk,
-                                                   max_items, w->d_desc.as<uint4>());
+                                                   max_items, w->d_desc.as<uint4>(), w->d_lead.as<uint32_t>());
       SWPS_HIP(hipGetLastError());
       tm.end(KT_SORT, es, s);
       pb.sorted = true;
@@ -2150,8 +2170,10 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_TRY(w->d_partial.ensure(pb.max_items * D * sizeof(A)));
     GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
-                     w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad)};
+                     w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad), w->d_lead.as<uint32_t>(),
+                     (uint32_t)pb.max_items};
     const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(pb.max_items * 64), (uint64_t)w->gather_grid);
+    const unsigned cgrid = combine_grid(pb.max_items);
     hipEvent_t eg = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
@@ -2168,18 +2190,18 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
         else
           k_gather_t<3, 8><<<ggrid, 256, 0, s>>>(ga);
         switch (w->NCH) {  // second level over the partials: layout-independent
-          case 2: k_combine<T, A, 2><<<std::min(ggrid, kCombineGrid), 256, 0, s>>>(ga); break;
-          case 3: k_combine<T, A, 3><<<std::min(ggrid, kCombineGrid), 256, 0, s>>>(ga); break;
-          default: k_combine<T, A, 4><<<std::min(ggrid, kCombineGrid), 256, 0, s>>>(ga); break;
+          case 2: k_combine<T, A, 2><<<cgrid, 256, 0, s>>>(ga); break;
+          case 3: k_combine<T, A, 3><<<cgrid, 256, 0, s>>>(ga); break;
+          default: k_combine<T, A, 4><<<cgrid, 256, 0, s>>>(ga); break;
         }
         goto gather_done;
       }
     }
     switch (w->NCH) {
-      case 1: launch_gather<1, T, A>(ga, ggrid, s); break;
-      case 2: launch_gather<2, T, A>(ga, ggrid, s); break;
-      case 3: launch_gather<3, T, A>(ga, ggrid, s); break;
-      default: launch_gather<4, T, A>(ga, ggrid, s); break;
+      case 1: launch_gather<1, T, A>(ga, ggrid, cgrid, s); break;
+      case 2: launch_gather<2, T, A>(ga, ggrid, cgrid, s); break;
+      case 3: launch_gather<3, T, A>(ga, ggrid, cgrid, s); break;
+      default: launch_gather<4, T, A>(ga, ggrid, cgrid, s); break;
     }
   gather_done:
     SWPS_HIP(hipGetLastError());
@@ -2348,6 +2370,7 @@ int swps_w2v_destroy(swps_w2v *w) {
   if (w->ev_learn) (void)hipEventDestroy(w->ev_learn);
   if (w->ev_prep) (void)hipEventDestroy(w->ev_prep);
   if (w->h_small) (void)hipHostFree(w->h_small);
+  delete w->drv;
   delete w;
   (void)hipGetLastError();  // leave no sticky error from the calls above
   return SWPS_OK;
@@ -2434,6 +2457,10 @@ int swps_w2v_info(swps_w2v *w, uint64_t *o) {
 int swps_w2v_init(swps_w2v *w) {
   if (!w->loaded) return fail(SWPS_E_STATE, "load a corpus first");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  if (w->drv) return w->drv->full_pull();  // the first full pull, over the communicator
+  if (w->t->comm)
+    return fail(SWPS_E_UNSUPPORTED, "the table is key-sharded (swps_table_route): drive the context with "
+                                    "swps_w2v_shard_comm");
   const uint64_t V = w->vocab_keys.size();
   DevMem dk;
   SWPS_TRY(upload(dk, w->vocab_keys, w->s));
@@ -2459,6 +2486,10 @@ int swps_w2v_init(swps_w2v *w) {
 
 int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
   if (!w->inited) return fail(SWPS_E_STATE, "call swps_w2v_init first");
+  if (w->drv) {
+    SWPS_HIP(hipSetDevice(w->t->cfg.device));
+    return w->drv->steps(count);  // collective: `count` lockstep steps on every rank
+  }
   if (w->sharded) return fail(SWPS_E_STATE, "sharded context: drive it with request / serve_pull / step / serve_push");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   if (w->overlap && count > 1 && !w->cfg.minibatch_vocab && w->trace.size() >= w->trace_cap && !w->pb.valid) {
@@ -2478,6 +2509,11 @@ int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
 }
 
 int swps_w2v_train_epochs(swps_w2v *w, int32_t niters) {
+  if (w->drv) {
+    if (w->drv->spe && w->drv->cursor % w->drv->spe) return fail(SWPS_E_STATE, "not at an epoch boundary");
+    SWPS_TRY(swps_w2v_train_batches(w, (uint64_t)niters * w->drv->spe));
+    return swps_w2v_sync(w);
+  }
   if (w->cursor % std::max<size_t>(1, w->batches.size()) != 0) return fail(SWPS_E_STATE, "not at an epoch boundary");
   SWPS_TRY(swps_w2v_train_batches(w, (uint64_t)niters * w->batches.size()));
   return swps_w2v_sync(w);
@@ -2485,6 +2521,7 @@ int swps_w2v_train_epochs(swps_w2v *w, int32_t niters) {
 
 int swps_w2v_sync(swps_w2v *w) {
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  if (w->drv) SWPS_TRY(w->drv->sync());
   SWPS_HIP(hipStreamSynchronize(w->s));
   if (w->ss) SWPS_HIP(hipStreamSynchronize(w->ss));
   w->timer.resolve();
@@ -2751,6 +2788,61 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
   const bool g32 = !w->f64 && !w->cfg.fp64_intermediates;  // fast mode: fp32 push payload
   // one AdaGrad step per source, in rank order, all sources in one pass
   return table_push_sources(w->t, w->d_push_rows.as<uint32_t>(), n, d_grads, ss, g32);
+}
+
+int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
+  if (!c) return fail(SWPS_E_CFG, "null communicator");
+  if (comm_device(c) != w->t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");
+  if (w->t->comm && w->t->comm != c) return fail(SWPS_E_CFG, "the table is routed over another communicator");
+  SWPS_TRY(swps_w2v_shard(w, comm_rank(c), comm_world(c), frag_num));
+  ShardDriver *d = new ShardDriver();
+  d->c = c;
+  AppOps &o = d->ops;
+  o.h = w;
+  o.cs = w->s;
+  o.width = 2 * (uint64_t)w->D;
+  o.val_bytes = w->f64 ? 8 : 4;
+  o.grad_bytes = (w->f64 || w->cfg.fp64_intermediates) ? 8 : 4;
+  o.batch_counts = [](void *h, uint64_t *out, uint64_t cap, uint64_t *nb) {
+    return swps_w2v_batch_counts((swps_w2v *)h, out, cap, nb);
+  };
+  o.request = [](void *h, int32_t init, uint64_t *cnt, uint64_t *k, uint64_t *n) {
+    return swps_w2v_request((swps_w2v *)h, init, cnt, k, n);
+  };
+  o.serve_pull = [](void *h, const uint64_t *k, const uint64_t *sc, int32_t ins, void *v) {
+    return swps_w2v_serve_pull((swps_w2v *)h, k, sc, ins, v);
+  };
+  o.install = [](void *h, const void *v) { return swps_w2v_install_init((swps_w2v *)h, v); };
+  o.step = [](void *h, const void *v, void *g) { return swps_w2v_step((swps_w2v *)h, v, g); };
+  o.serve_push = [](void *h, const uint64_t *k, const void *g, const uint64_t *sc) {
+    return swps_w2v_serve_push((swps_w2v *)h, k, g, sc);
+  };
+  o.prep = [](void *h) { return swps_w2v_prep((swps_w2v *)h); };
+  o.set_serve_stream = [](void *h, void *s) { return swps_w2v_set_serve_stream((swps_w2v *)h, s); };
+  const int rc = d->setup();
+  if (rc) {
+    delete d;
+    return rc;
+  }
+  w->drv = d;
+  return SWPS_OK;
+}
+
+int swps_w2v_exchange_stats(swps_w2v *w, int32_t on, double *out4) {
+  if (!w->drv) return fail(SWPS_E_STATE, "not driven by swps_w2v_shard_comm");
+  SWPS_TRY(w->drv->sync());
+  if (out4) {
+    out4[0] = (double)w->drv->bytes_remote;
+    out4[1] = (double)w->drv->bytes_total;
+    out4[2] = (double)w->drv->calls;
+    out4[3] = w->drv->xms;
+  }
+  if (on >= 0) {
+    w->drv->xprof = on != 0;
+    w->drv->bytes_remote = w->drv->bytes_total = w->drv->calls = 0;
+    w->drv->xms = 0;
+  }
+  return SWPS_OK;
 }
 
 }  // extern "C"

@@ -436,8 +436,8 @@ class ShardedLR(_ShardedApp):
     val_dtype = torch.float32
     grad_dtype = torch.float32
 
-    def __init__(self, table, group=None, frag_num=2000, minibatch=200, profile=False):
-        self.m = LR(table, minibatch=minibatch, init_ref=False, profile=profile)
+    def __init__(self, table, group=None, frag_num=2000, minibatch=200, profile=False, fast_sums=False):
+        self.m = LR(table, minibatch=minibatch, init_ref=False, profile=profile, fast_sums=fast_sums)
         self.h = self.m.h
         self._setup(table, group, frag_num)
 

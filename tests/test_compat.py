@@ -113,6 +113,41 @@ def test_compat_ps_client_two_ranks(compat_bin, gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_compat_w2v_main_two_ranks_matches_python_driver(compat_bin, lib, gpu, tmp_path):
+    """apps/word2vec/w2v.cpp's main on two C++ ranks (one GPU, TCP transport):
+    each rank trains its own corpus, the library runs the key-sharded
+    exchange (swps_w2v_shard_comm) — every rank's dumped shard equals the one
+    the Python driver over gloo produces (tests/dist_w2v_dump.py)."""
+    import sys
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF)
+    data = [zipf_corpus(str(tmp_path / ("c%d.txt" % r)), 70 + 25 * r, 200, seed=51 + r) for r in range(2)]
+    cpp_out = str(tmp_path / "cpp_param.txt")
+    port = str(_free_port())
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   SWPS_BOOTSTRAP_PORT=port, SWPS_TRANSPORT="tcp", HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([compat_bin, "w2v", "-config", str(conf), "-data", data[rank], "-niters", "2",
+                                       "-output", cpp_out], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True, env=env))
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        assert p.returncode == 0, o + e
+    py_out = str(tmp_path / "py_param.txt")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(ROOT, "tests", "dist_w2v_dump.py"), "--data", ",".join(data), "--out", py_out],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    for rank in range(2):
+        a = sorted(open("%s.%d" % (cpp_out, rank)).read().splitlines())
+        b = sorted(open("%s.%d" % (py_out, rank)).read().splitlines())
+        assert len(a) > 0 and a == b, rank
+
+
+@pytest.mark.gpu
 def test_compat_w2v_and_s2v_mains_match_python(compat_bin, lib, gpu, tmp_path):
     conf = tmp_path / "demo.conf"
     conf.write_text(W2V_CONF)

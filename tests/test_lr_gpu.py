@@ -100,3 +100,63 @@ def test_lr_criteo_shape_properties(lib, gpu):
         ws.append(m.params()[1])
     assert np.array_equal(errs[0], errs[1]) and np.array_equal(ws[0], ws[1])
     assert np.isfinite(ws[0]).all() and errs[0][2] < errs[0][0]
+
+
+@pytest.mark.parametrize("B", [200, 1604])
+def test_lr_fast_sums_within_1e5_of_oracle(lib, oracle_mod, gpu, B):
+    """Fast mode (fp64 per-key sums, long runs tree-reduced over a wave
+    instead of the reference's sequential fp32 chain): weights and AdaGrad
+    sums within 1e-5 relative of the oracle after 5 epochs, epoch errors
+    within 1e-5, log-loss within 1 % of the reference binary's, and run to
+    run bit-identical."""
+    orc = oracle_mod.LR(DATA, B, 0.05)
+    e_o = orc.train(5)
+    ko, wo, go = orc.params()
+    runs = []
+    for _ in range(2):
+        t = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+        m = lib.LR(t, minibatch=B, fast_sums=True)
+        m.load_text(DATA)
+        m.init()
+        e = m.train(5)
+        runs.append((e, m.params(), m.predict()))
+    (e_g, (kg, wg, gg), (p, tgt)), (e_2, (_, w2, _), _) = runs
+    assert np.array_equal(e_g, e_2) and np.array_equal(wg, w2)
+    assert np.array_equal(ko, kg)
+    assert np.allclose(wg, wo, rtol=1e-5, atol=1e-6), np.abs(wg - wo).max()
+    assert np.allclose(gg, go, rtol=1e-5, atol=1e-7)
+    assert np.allclose(e_g, e_o, rtol=1e-5)
+
+
+def test_lr_fast_sums_reference_quality(lib, oracle_mod, gpu):
+    q = json.load(open(os.path.join(GOLDEN, "lr_reference_quality.json")))
+    for ep, exp in q["epochs"].items():
+        t = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+        m = lib.LR(t, minibatch=200, fast_sums=True)
+        m.load_text(DATA)
+        m.init()
+        m.train(int(ep))
+        p, tg = m.predict()
+        p6 = np.array([float("%g" % x) for x in p], dtype=np.float32)
+        ll, acc = oracle_mod.logloss_accuracy(p6, tg)
+        assert abs(ll - exp["logloss"]) / exp["logloss"] < 0.01
+
+
+def test_lr_fast_sums_criteo_shape_close_to_exact(lib, gpu):
+    """At the Criteo shape (hot categorical features: runs of thousands of
+    records — the long-run path), fast sums stay within 1e-5 of the exact
+    fp32-chain mode after 3 epochs, relative to the weights' scale (the fp32
+    chain's own rounding over runs of thousands of records is ~1e-6 of it;
+    the small-data bar against the oracle is element-wise)."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(20000, seed=3)
+    ws = []
+    for fast in (False, True):
+        t = lib.Table("lr", capacity=1 << 20, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+        m = lib.LR(t, minibatch=4095, init_ref=False, fast_sums=fast)
+        m.load_csr(y, off, f, v)
+        m.init()
+        m.train(3)
+        ws.append(m.params()[1])
+    assert np.abs(ws[1] - ws[0]).max() <= 1e-5 * np.abs(ws[0]).max(), (np.abs(ws[1] - ws[0]).max(),
+                                                                       np.abs(ws[0]).max())

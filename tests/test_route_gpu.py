@@ -136,3 +136,49 @@ def test_app_contexts_refuse_routed_or_sgd_tables(lib, gpu):
     with pytest.raises(capi.SwpsError):
         sw.LR(t)
     t.close()
+
+
+def test_native_sharded_driver_equals_python_driver(lib, gpu):
+    """swps_w2v_shard_comm / swps_lr_shard_comm (the library runs the
+    exchange over its TCP transport) == the Python driver over gloo, bit for
+    bit, two ranks on one GPU (tests/dist_native_check.py)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist_native_check.py"), "--tcp-port", str(_port())]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    print(r.stdout[-6000:])
+    print("\n".join(ln for ln in r.stderr.splitlines() if "rank0" in ln or "Error" in ln)[-6000:])
+    assert r.returncode == 0 and "NATIVE OK" in r.stdout
+
+
+def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path):
+    """The library-driven loop over RCCL at world 1 == the unsharded context
+    with the same hash init (the exchange is a self-copy)."""
+    import swiftmpi_amd as sw
+    from swiftmpi_amd.comm import Comm
+    from conftest import zipf_corpus
+    path = zipf_corpus(str(tmp_path / "c.txt"), 120, 300, seed=12)
+    kw = dict(window=3, negative=4, minibatch=23, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=False)
+    comm = Comm.rccl(0, 1, port=_port())
+    ta = sw.Table("w2v", dim=24, capacity=2048, dtype="f32", init="hash", seed=7)
+    a = sw.Word2Vec(ta, init="table", **kw)
+    a.load_text(path)
+    a.shard_comm(comm, frag_num=1000)
+    a.init()
+    a.exchange_stats(on=1)
+    a.train(2)
+    xs = a.exchange_stats()
+    tb = sw.Table("w2v", dim=24, capacity=2048, dtype="f32", init="hash", seed=7)
+    b = sw.Word2Vec(tb, init="table", **kw)
+    b.load_text(path)
+    b.init()
+    b.train(2)
+    vk, _ = b.vocab()
+    kk = torch.as_tensor(vk.astype(np.int64), device="cuda")
+    assert torch.equal(ta.export(kk), tb.export(kk))  # every key lives on the one rank
+    assert a.stats()["lstate"] == b.stats()["lstate"]
+    assert xs["bytes_remote"] == 0 and xs["bytes_total"] > 0 and xs["calls"] > 0
+    a.close()
+    b.close()
+    comm.close()
