@@ -436,6 +436,7 @@ class Word2VecApp {
     c.profile = 0;
     c.minibatch_vocab = local ? 1 : 0;
     c.sampler = SWPS_SAMPLER_TABLE;
+    c.host_ingest = 0;
     _comm = t ? nullptr : global_swps_comm();
     if (_comm) c.init_mode = SWPS_W2V_INIT_TABLE;
     swps_check(swps_w2v_create(t ? t : global_swps_table(), &c, &_w));

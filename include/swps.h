@@ -244,6 +244,9 @@ typedef struct {
                                 * bit-exact draws) or SWPS_SAMPLER_ALIAS (Walker/Vose alias table over the
                                 * same weights: V x 8 B instead of table_size x 4 B, one L2-resident read per
                                 * draw; same LCG consumption, different words — a non-parity fast mode) */
+  int32_t host_ingest;         /* 0: corpus ingest on the GPU (tokenize, hash, vocab counts, the minibatch
+                                * key sets; bit-identical to the host restatement); 1: on the host (kept
+                                * for A/B and parity tests; minibatch_vocab mode always ingests on the host) */
 } swps_w2v_cfg;
 
 #define SWPS_SAMPLER_TABLE 0
@@ -258,6 +261,11 @@ int swps_w2v_destroy(swps_w2v *w);
 int swps_w2v_load_text(swps_w2v *w, const char *path);
 int swps_w2v_load_tokens(swps_w2v *w, const uint32_t *word_ids, uint64_t ntok, const uint64_t *line_off,
                          uint64_t nlines, const uint64_t *word_keys, uint64_t nwords);
+/* introspection (tests): every token's vid and line (host arrays of cap >= ntok) */
+int swps_w2v_corpus(swps_w2v *w, int32_t *vid, int32_t *line, uint64_t cap);
+/* batch b of the epoch schedule: its lines [lines2[0], lines2[1]) and its gathered key set (vids,
+ * ascending; sharded contexts: grouped by owner) into out[cap], count via *n */
+int swps_w2v_batch_keys(swps_w2v *w, uint64_t b, int32_t *out, uint64_t cap, uint64_t *n, uint64_t *lines2);
 /* vocab in _wordids order (vid order): keys[V], counts[V]; V via *n */
 int swps_w2v_vocab(swps_w2v *w, uint64_t *keys, int32_t *counts, uint64_t cap, uint64_t *n);
 int swps_w2v_info(swps_w2v *w, uint64_t *out8); /* V, train_words, nlines, ntok, nbatches, max_batch_tok, lstate, fstate */

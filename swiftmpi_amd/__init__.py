@@ -239,13 +239,13 @@ class Word2Vec:
 
     def __init__(self, table, window=5, negative=5, min_sentence_length=1, minibatch=100, sample=1e-5, alpha=0.05,
                  unigram_size=int(1e8), key_mode="bkdr", init="ref", rand_seed=1, rand_offset=2, profile=False,
-                 fp64_intermediates=True, minibatch_vocab=False, sampler="table"):
+                 fp64_intermediates=True, minibatch_vocab=False, sampler="table", host_ingest=False):
         assert table.layout == "w2v"
         cfg = capi.W2VCfg(window, negative, min_sentence_length, minibatch, sample, alpha, unigram_size,
                           capi.KEY_ATOI if key_mode == "atoi" else capi.KEY_BKDR,
                           capi.W2V_INIT_REF if init == "ref" else capi.W2V_INIT_TABLE, rand_seed, rand_offset,
                           int(fp64_intermediates), int(profile), int(minibatch_vocab),
-                          {"table": 0, "alias": 1}[sampler])
+                          {"table": 0, "alias": 1}[sampler], int(host_ingest))
         h = ctypes.c_void_p()
         check(capi.lib().swps_w2v_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -315,6 +315,23 @@ class Word2Vec:
         n = ctypes.c_uint64()
         check(capi.lib().swps_w2v_vocab(self.h, ptr(keys), ptr(counts), V, ctypes.byref(n)))
         return keys, counts
+
+    def corpus(self):
+        """(vid per token, line per token) — introspection for the ingest tests."""
+        n = self.info()["tokens"]
+        vid = np.zeros(max(n, 1), dtype=np.int32)
+        line = np.zeros(max(n, 1), dtype=np.int32)
+        check(capi.lib().swps_w2v_corpus(self.h, ptr(vid), ptr(line), len(vid)))
+        return vid[:n], line[:n]
+
+    def batch_keys(self, b):
+        """(l0, l1, sorted vids of the gathered key set) of schedule batch b."""
+        n = ctypes.c_uint64()
+        lines = np.zeros(2, dtype=np.uint64)
+        capi.lib().swps_w2v_batch_keys(self.h, b, None, 0, ctypes.byref(n), ptr(lines))
+        out = np.zeros(max(n.value, 1), dtype=np.int32)
+        check(capi.lib().swps_w2v_batch_keys(self.h, b, ptr(out), len(out), ctypes.byref(n), ptr(lines)))
+        return int(lines[0]), int(lines[1]), out[:n.value]
 
     def init(self):
         check(capi.lib().swps_w2v_init(self.h))

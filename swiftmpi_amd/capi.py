@@ -52,7 +52,8 @@ class W2VCfg(ctypes.Structure):
     _fields_ = [("window", _i32), ("negative", _i32), ("min_sentence_length", _i32), ("minibatch", _i32),
                 ("sample", ctypes.c_float), ("alpha", ctypes.c_float), ("unigram_size", _u64), ("key_mode", _i32),
                 ("init_mode", _i32), ("rand_seed", ctypes.c_uint32), ("rand_offset", _u64),
-                ("fp64_intermediates", _i32), ("profile", _i32), ("minibatch_vocab", _i32), ("sampler", _i32)]
+                ("fp64_intermediates", _i32), ("profile", _i32), ("minibatch_vocab", _i32), ("sampler", _i32),
+                ("host_ingest", _i32)]
 
 
 class LRCfg(ctypes.Structure):
@@ -108,6 +109,8 @@ PROTOS = {
     "swps_w2v_load_tokens": (ctypes.c_int, [_p, _p, _u64, _p, _u64, _p, _u64]),
     "swps_w2v_vocab": (ctypes.c_int, [_p, _p, _p, _u64, ctypes.POINTER(_u64)]),
     "swps_w2v_info": (ctypes.c_int, [_p, _p]),
+    "swps_w2v_corpus": (ctypes.c_int, [_p, _p, _p, _u64]),
+    "swps_w2v_batch_keys": (ctypes.c_int, [_p, _u64, _p, _u64, ctypes.POINTER(_u64), _p]),
     "swps_w2v_init": (ctypes.c_int, [_p]),
     "swps_w2v_train_batches": (ctypes.c_int, [_p, _u64]),
     "swps_w2v_train_epochs": (ctypes.c_int, [_p, _i32]),

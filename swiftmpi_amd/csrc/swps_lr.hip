@@ -51,8 +51,8 @@ __device__ __forceinline__ float ordered_add(float acc, float x, int m) {
 __global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
                              const float *__restrict__ fval, const float *__restrict__ label, uint64_t r0, uint64_t nr,
                              const uint32_t *__restrict__ vid_row, const float *__restrict__ rows,
-                             float *__restrict__ contrib, uint32_t *__restrict__ keys,
-                             float *__restrict__ err2, uint64_t nz0) {
+                             float *__restrict__ contrib_s, const uint32_t *__restrict__ slot,
+                             float *__restrict__ err2) {
   const uint64_t j = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (j >= nr) return;
@@ -70,11 +70,81 @@ __global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__
   }
   const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
   const float error = label[r] - predict;
-  for (uint64_t c = a + lane; c < b; c += 64) {
-    contrib[c - nz0] = error * fval[c];
-    keys[c - nz0] = (uint32_t)fvid[c];
-  }
+  // the contribution goes straight to its place in the batch's key-sorted
+  // order (a static permutation of the batch's features, built at load)
+  for (uint64_t c = a + lane; c < b; c += 64) contrib_s[slot[c]] = error * fval[c];
   if (lane == 0) err2[r] = error * error;
+}
+
+// ---- the static per-batch index (built once at load; lr_index) -------------
+// The batch's records are its rows' features in (row, feature) order; their
+// stable key-sorted order, the runs (one per pushed key) and the run bounds
+// depend only on the data, never on the weights: sorted once for the whole
+// corpus with (batch << 32 | vid) keys instead of once per minibatch.
+__global__ void k_lr_idx_keys(const uint64_t *__restrict__ row_off, uint64_t nr, uint64_t B1,
+                              const int32_t *__restrict__ fvid, uint64_t *__restrict__ key, uint32_t *__restrict__ idx) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nr) return;
+  const uint64_t b = r / B1;
+  for (uint64_t c = row_off[r]; c < row_off[r + 1]; c++) {
+    key[c] = (b << 32) | (uint32_t)fvid[c];
+    idx[c] = (uint32_t)c;
+  }
+}
+
+// slot of record c = its position in the sorted order, relative to its batch's
+// first record; run heads -> run key, relative start
+__global__ void k_lr_idx_slots(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ perm, uint64_t n,
+                               const uint64_t *__restrict__ bnz0, uint32_t *__restrict__ slot,
+                               uint32_t *__restrict__ head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t z0 = bnz0[ks[i] >> 32];
+  slot[perm[i]] = (uint32_t)(i - z0);
+  head[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_lr_idx_runs(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ head,
+                              const uint32_t *__restrict__ rid1, uint64_t n, const uint64_t *__restrict__ bnz0,
+                              uint64_t *__restrict__ rkey, uint32_t *__restrict__ uniq, uint32_t *__restrict__ off) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !head[i]) return;
+  const uint32_t r = rid1[i] - 1;
+  rkey[r] = ks[i];
+  uniq[r] = (uint32_t)ks[i];
+  off[r] = (uint32_t)(i - bnz0[ks[i] >> 32]);
+}
+
+// run lengths from the starts (a run never crosses its batch: the next run's
+// start in the same batch, else the batch's record count)
+__global__ void k_lr_idx_cnt(const uint64_t *__restrict__ rkey, const uint32_t *__restrict__ off, uint64_t R,
+                             const uint64_t *__restrict__ bnz0, uint32_t *__restrict__ cnt) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint64_t b = rkey[r] >> 32;
+  const uint64_t end = (r + 1 < R && (rkey[r + 1] >> 32) == b) ? off[r + 1] : bnz0[b + 1] - bnz0[b];
+  cnt[r] = (uint32_t)(end - off[r]);
+}
+
+// first run of every batch (lower bound of b << 32), and its run count
+__global__ void k_lr_idx_bruns(const uint64_t *__restrict__ rkey, uint64_t R, uint64_t nb, uint64_t *__restrict__ brun,
+                               uint32_t *__restrict__ bnruns) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nb) return;
+  auto lb = [&](uint64_t v) {
+    uint64_t lo = 0, hi = R;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (rkey[mid] < v)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return lo;
+  };
+  const uint64_t a = lb(b << 32);
+  brun[b] = a;
+  if (b < nb) bnruns[b] = (uint32_t)(lb((b + 1) << 32) - a);
 }
 
 // Per pushed key (a run of the sorted records): s = sum of e*x_i in record
@@ -275,8 +345,12 @@ struct swps_lr {
   std::vector<uint64_t> vocab_keys;  // vid order = first-pull order
   bool loaded = false, inited = false;
   uint64_t cursor = 0, nbatches = 0;
-  DevMem d_label, d_row_off, d_fvid, d_fval, d_vid_row, d_contrib, d_keys, d_keys_s, d_val_s, d_uniq, d_cnt,
-      d_off, d_nruns, d_err2, d_tmp, d_pred, d_longs;
+  DevMem d_label, d_row_off, d_fvid, d_fval, d_vid_row, d_val_s, d_err2, d_tmp, d_pred, d_longs;
+  // the static per-batch index (lr_index): slot of every record in its batch's key-sorted order; the runs
+  // (pushed keys) of all batches: vid, start and length relative to the batch; first run and run count per batch
+  DevMem d_slot, d_ruk, d_roff, d_rcnt, d_bnruns;
+  std::vector<uint64_t> brun;
+  uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
   LTimer timer;
   // sharded mode (swps_lr_shard): per-batch key sets ordered by owner rank
@@ -295,6 +369,83 @@ namespace {
 // lr.cpp:161-166: the first gather collects every feature of every valid row
 // into `_local_keys` (std::unordered_set<unsigned>); the first pull visits it
 // in iteration order, initialising each miss with global_random().gen_float().
+template <typename T> int lr_scan_incl(const T *in, T *out, uint64_t n, DevMem &tmp, hipStream_t s) {
+  size_t b = 0;
+  SWPS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b, in, out, (int)n, s));
+  SWPS_TRY(tmp.ensure(b));
+  b = tmp.bytes;
+  SWPS_HIP(hipcub::DeviceScan::InclusiveSum(tmp.p, b, in, out, (int)n, s));
+  return SWPS_OK;
+}
+
+// The static per-batch index (see k_lr_idx_*): one (batch << 32 | vid) radix
+// sort of every record of the corpus at load time.
+int lr_index(swps_lr *l) {
+  hipStream_t s = l->s;
+  const uint64_t nr = l->label.size(), nb = l->nbatches, B1 = (uint64_t)l->B1();
+  const uint64_t n = l->row_off[nr];
+  if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 features per rank");
+  std::vector<uint64_t> bnz0(nb + 1);
+  l->max_bnnz = 0;
+  for (uint64_t b = 0; b <= nb; b++) bnz0[b] = l->row_off[std::min<uint64_t>(nr, b * B1)];
+  for (uint64_t b = 0; b < nb; b++) l->max_bnnz = std::max<uint64_t>(l->max_bnnz, bnz0[b + 1] - bnz0[b]);
+  DevMem d_bnz0, key, idx, ks, perm, head, rid1, rkey, tmp;
+  SWPS_TRY(upload(d_bnz0, bnz0, s));
+  SWPS_TRY(l->d_slot.ensure(std::max<uint64_t>(n, 1) * 4));
+  SWPS_TRY(l->d_bnruns.ensure(std::max<uint64_t>(nb, 1) * 4));
+  l->brun.assign(nb + 1, 0);
+  if (n == 0) return SWPS_OK;
+  SWPS_TRY(key.ensure(n * 8));
+  SWPS_TRY(idx.ensure(n * 4));
+  SWPS_TRY(ks.ensure(n * 8));
+  SWPS_TRY(perm.ensure(n * 4));
+  k_lr_idx_keys<<<nblk(nr), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), nr, B1, l->d_fvid.as<int32_t>(),
+                                          key.as<uint64_t>(), idx.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  int vbits = 1;
+  while ((1ULL << vbits) <= l->vocab_keys.size()) vbits++;
+  int bbits = 1;
+  while ((1ULL << bbits) <= nb) bbits++;
+  // stable on (batch, vid): the batch's records stay in (row, feature) order inside a key,
+  // the order the per-minibatch sort produced (lr.cpp:358-375's accumulation order)
+  size_t sb = 0;
+  SWPS_HIP(sort_pairs(nullptr, sb, key.as<uint64_t>(), ks.as<uint64_t>(), idx.as<uint32_t>(), perm.as<uint32_t>(), n,
+                      32 + bbits, s));
+  SWPS_TRY(tmp.ensure(sb));
+  sb = tmp.bytes;
+  SWPS_HIP(sort_pairs(tmp.p, sb, key.as<uint64_t>(), ks.as<uint64_t>(), idx.as<uint32_t>(), perm.as<uint32_t>(), n,
+                      32 + bbits, s));
+  (void)vbits;
+  key.release();
+  idx.release();
+  SWPS_TRY(head.ensure(n * 4));
+  SWPS_TRY(rid1.ensure(n * 4));
+  k_lr_idx_slots<<<nblk(n), 256, 0, s>>>(ks.as<uint64_t>(), perm.as<uint32_t>(), n, d_bnz0.as<uint64_t>(),
+                                          l->d_slot.as<uint32_t>(), head.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  SWPS_TRY(lr_scan_incl(head.as<uint32_t>(), rid1.as<uint32_t>(), n, tmp, s));
+  uint32_t R = 0;
+  SWPS_HIP(hipMemcpyAsync(&R, rid1.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  SWPS_TRY(rkey.ensure((uint64_t)R * 8));
+  SWPS_TRY(l->d_ruk.ensure((uint64_t)R * 4));
+  SWPS_TRY(l->d_roff.ensure((uint64_t)R * 4));
+  SWPS_TRY(l->d_rcnt.ensure((uint64_t)R * 4));
+  k_lr_idx_runs<<<nblk(n), 256, 0, s>>>(ks.as<uint64_t>(), head.as<uint32_t>(), rid1.as<uint32_t>(), n,
+                                         d_bnz0.as<uint64_t>(), rkey.as<uint64_t>(), l->d_ruk.as<uint32_t>(),
+                                         l->d_roff.as<uint32_t>());
+  k_lr_idx_cnt<<<nblk(R), 256, 0, s>>>(rkey.as<uint64_t>(), l->d_roff.as<uint32_t>(), R, d_bnz0.as<uint64_t>(),
+                                        l->d_rcnt.as<uint32_t>());
+  DevMem d_brun;
+  SWPS_TRY(d_brun.ensure((nb + 1) * 8));
+  k_lr_idx_bruns<<<nblk(nb + 1), 256, 0, s>>>(rkey.as<uint64_t>(), R, nb, d_brun.as<uint64_t>(),
+                                               l->d_bnruns.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  SWPS_HIP(hipMemcpyAsync(l->brun.data(), d_brun.p, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  return SWPS_OK;
+}
+
 int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   std::unordered_set<uint32_t> K0;
   for (auto f : feat) K0.insert(f);
@@ -313,6 +464,7 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   SWPS_TRY(upload(l->d_fval, l->fval, s));
   SWPS_TRY(l->d_vid_row.ensure(std::max<size_t>(1, l->vocab_keys.size()) * 4));
   SWPS_TRY(l->d_err2.ensure(std::max<uint64_t>(1, nr) * 4));
+  SWPS_TRY(lr_index(l));
   SWPS_HIP(hipStreamSynchronize(s));
   l->loaded = true;
   return SWPS_OK;
@@ -337,51 +489,24 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     vid_row = nullptr;
   }
   if (nnz == 0) return SWPS_OK;
-  SWPS_TRY(l->d_contrib.ensure(nnz * 4));
-  SWPS_TRY(l->d_keys.ensure(nnz * 4));
-  SWPS_TRY(l->d_keys_s.ensure(nnz * 4));
-  SWPS_TRY(l->d_val_s.ensure(nnz * 4));
-  SWPS_TRY(l->d_longs.ensure((nnz + 1) * 4));
-  SWPS_TRY(l->d_uniq.ensure(nnz * 4));
-  SWPS_TRY(l->d_cnt.ensure((nnz + 1) * 4));
-  SWPS_TRY(l->d_off.ensure((nnz + 1) * 4));
-  SWPS_TRY(l->d_nruns.ensure(16));
+  SWPS_TRY(l->d_val_s.ensure(l->max_bnnz * 4));
+  SWPS_TRY(l->d_longs.ensure((l->max_bnnz + 1) * 4));
   hipEvent_t e0 = l->timer.begin(s);
   k_lr_forward<<<nblk((r1 - r0) * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), l->d_fvid.as<int32_t>(),
                                                     l->d_fval.as<float>(), l->d_label.as<float>(), r0, r1 - r0,
-                                                    vid_row, rows, l->d_contrib.as<float>(),
-                                                    l->d_keys.as<uint32_t>(), l->d_err2.as<float>(), nz0);
+                                                    vid_row, rows, l->d_val_s.as<float>(), l->d_slot.as<uint32_t>(),
+                                                    l->d_err2.as<float>());
   SWPS_HIP(hipGetLastError());
   l->timer.end(0, e0, s);
-  int bits = 1;
-  while ((1ULL << bits) <= l->vocab_keys.size()) bits++;
-  hipEvent_t e1 = l->timer.begin(s);
-  size_t b1 = 0, b2 = 0, b3 = 0;
-  SWPS_HIP(sort_pairs(nullptr, b1, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(), l->d_contrib.as<float>(),
-                      l->d_val_s.as<float>(), nnz, bits, s));
-  SWPS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, l->d_keys_s.as<uint32_t>(), l->d_uniq.as<uint32_t>(),
-                                                 l->d_cnt.as<uint32_t>(), l->d_nruns.as<uint32_t>(), (int)nnz, s));
-  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b3, l->d_cnt.as<uint32_t>(), l->d_off.as<uint32_t>(),
-                                            (int)nnz, s));
-  SWPS_TRY(l->d_tmp.ensure(std::max(b1, std::max(b2, b3))));
-  size_t tb = l->d_tmp.bytes;
-  SWPS_HIP(sort_pairs(l->d_tmp.p, tb, l->d_keys.as<uint32_t>(), l->d_keys_s.as<uint32_t>(), l->d_contrib.as<float>(),
-                      l->d_val_s.as<float>(), nnz, bits, s));
-  tb = l->d_tmp.bytes;
-  SWPS_HIP(hipcub::DeviceRunLengthEncode::Encode(l->d_tmp.p, tb, l->d_keys_s.as<uint32_t>(), l->d_uniq.as<uint32_t>(),
-                                                 l->d_cnt.as<uint32_t>(), l->d_nruns.as<uint32_t>(), (int)nnz, s));
-  tb = l->d_tmp.bytes;
-  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(l->d_tmp.p, tb, l->d_cnt.as<uint32_t>(), l->d_off.as<uint32_t>(),
-                                            (int)nnz, s));
-  l->timer.end(1, e1, s);
   hipEvent_t e3 = l->timer.begin(s);
   // the run counter lives past the last possible long-run index
-  uint32_t *nlong = l->d_longs.as<uint32_t>() + nnz;
+  uint32_t *nlong = l->d_longs.as<uint32_t>() + l->max_bnnz;
   SWPS_HIP(hipMemsetAsync(nlong, 0, 4, s));
-  LrReduce ra{l->d_uniq.as<uint32_t>(), l->d_cnt.as<uint32_t>(), l->d_off.as<uint32_t>(), l->d_nruns.as<uint32_t>(),
-              l->d_val_s.as<float>(), l->d_vid_row.as<uint32_t>(), l->t->rows.as<float>(), l->t->cfg.learning_rate,
-              l->t->cfg.fudge, l->d_local.as<int32_t>(), l->sharded ? d_grads : nullptr, nlong,
-              l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
+  const uint64_t q0 = l->brun[bi];
+  LrReduce ra{l->d_ruk.as<uint32_t>() + q0, l->d_rcnt.as<uint32_t>() + q0, l->d_roff.as<uint32_t>() + q0,
+              l->d_bnruns.as<uint32_t>() + bi, l->d_val_s.as<float>(), l->d_vid_row.as<uint32_t>(),
+              l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, l->d_local.as<int32_t>(),
+              l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
   k_lr_reduce_short<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(ra);
   k_lr_reduce_long<<<(unsigned)std::min<uint64_t>(nblk(nnz * 64 / kLrShort), 2048), 256, 0, s>>>(ra);
   SWPS_HIP(hipGetLastError());

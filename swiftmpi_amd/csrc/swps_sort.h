@@ -21,4 +21,10 @@ inline hipError_t sort_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, co
   return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);
 }
 
+// keys-only form (same onesweep configuration)
+template <typename K>
+inline hipError_t sort_keys(void *tmp, size_t &bytes, const K *kin, K *kout, uint64_t n, int bits, hipStream_t s) {
+  return rocprim::radix_sort_keys<OnesweepCfg>(tmp, bytes, kin, kout, (size_t)n, 0u, (unsigned)bits, s);
+}
+
 }  // namespace swps

@@ -1330,8 +1330,11 @@ struct swps_w2v {
   bool row_pad = true;  // neu1/neu1e rows padded to 128 B (SWPS_ROW_PAD=0: D-strided, for A/B timing)
   hipStream_t s = nullptr;
   // host corpus / vocab
-  std::vector<int32_t> tok;
+  std::vector<int32_t> tok;       // host ingest only (the GPU ingest leaves tokens in d_tok)
   std::vector<int32_t> tok_line;
+  uint64_t ntok = 0;              // corpus tokens
+  uint64_t tok_fp = 0;            // device-computed fingerprint of d_tok (checkpoint corpus check)
+  bool tok_on_device = false;     // d_tok / d_tok_line / d_K were built by the GPU ingest
   std::vector<int64_t> line_off;
   std::vector<uint8_t> line_valid;
   std::vector<uint64_t> vocab_keys;
@@ -1481,6 +1484,8 @@ int ingest(swps_w2v *w, const std::vector<uint64_t> &tok_keys, std::vector<int64
       w->tok[i] = it->second;
       w->tok_line[i] = (int32_t)l;
     }
+  w->ntok = nt;
+  w->tok_on_device = false;
   w->loaded = true;
   return SWPS_OK;
 }
@@ -1674,13 +1679,495 @@ int build_schedule_mb(swps_w2v *w) {
   return SWPS_OK;
 }
 
+// ============================================================================
+// Corpus ingest on the GPU (word2vec_global.h:215-227
+// parse_instance, :385-444 gather_keys with nthreads = 1, :335-381 the
+// minibatch windows).  Same results as the host restatement above (ingest +
+// build_schedule), bit for bit; the host keeps only per-line and per-word
+// work (line validity, the std::unordered_set iteration order of the V
+// distinct keys, the batch boundaries):
+//   tokenize   text bytes -> token starts (scan), BKDR / atoi per token
+//   vocab      stable radix sort of (key, position); per run: count over valid
+//              lines and first valid position (integer atomics: exact);
+//              host inserts the V keys into std::unordered_set in first-
+//              occurrence order (its iteration order = the vid order) and
+//              sends back vid per run; tok[position] = vid
+//   schedule   (batch << 32 | vid) for every token of every batch's B+3-line
+//              window, radix sort, unique -> each batch's sorted key set
+// ============================================================================
+__global__ void k_tok_fp(const int32_t *__restrict__ tok, uint64_t n, unsigned long long *__restrict__ out) {
+  unsigned long long acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    acc += splitmix64((uint64_t)(uint32_t)tok[i] ^ (i * 0x9E3779B97F4A7C15ULL));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);  // a wrapping integer sum: order-independent
+}
+
+int tok_fingerprint(swps_w2v *w) {
+  DevMem d;
+  SWPS_TRY(d.ensure(8));
+  SWPS_HIP(hipMemsetAsync(d.p, 0, 8, w->s));
+  if (w->ntok) k_tok_fp<<<1024, 256, 0, w->s>>>(w->d_tok.as<int32_t>(), w->ntok, d.as<unsigned long long>());
+  SWPS_HIP(hipGetLastError());
+  uint64_t h = 0;
+  SWPS_HIP(hipMemcpyAsync(&h, d.p, 8, hipMemcpyDeviceToHost, w->s));
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  w->tok_fp = h ^ w->ntok;
+  return SWPS_OK;
+}
+
+// per byte: token start (not a delimiter, after a delimiter or at 0) and
+// newline flags; element nb is 0 so the exclusive scans end with the totals
+__global__ void k_text_flags(const char *__restrict__ t, uint64_t nb, uint32_t *__restrict__ st,
+                             uint32_t *__restrict__ nl) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nb) return;
+  if (i == nb) {
+    st[i] = 0;
+    nl[i] = 0;
+    return;
+  }
+  const char c = t[i], p = i ? t[i - 1] : '\n';
+  st[i] = (c != ' ' && c != '\n' && (p == ' ' || p == '\n')) ? 1u : 0u;
+  nl[i] = c == '\n' ? 1u : 0u;
+}
+
+// token start positions, and line_off[l + 1] = first token after newline l
+__global__ void k_text_index(const char *__restrict__ t, uint64_t nb, const uint32_t *__restrict__ st,
+                             const uint32_t *__restrict__ tix, const uint32_t *__restrict__ lix,
+                             uint64_t *__restrict__ tstart, int64_t *__restrict__ line_off) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  if (st[i]) tstart[tix[i]] = i;
+  if (t[i] == '\n') line_off[lix[i] + 1] = (int64_t)tix[i + 1];
+}
+
+// BKDRHash (string.h:130-137: signed char) or atoi (word2vec.h:206) of one token
+__global__ void k_text_keys(const char *__restrict__ t, uint64_t nb, const uint64_t *__restrict__ tstart, uint64_t n,
+                            int atoi_mode, uint64_t *__restrict__ keys) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  uint64_t i = tstart[k];
+  if (!atoi_mode) {
+    uint64_t h = 0;
+    for (; i < nb && t[i] != ' ' && t[i] != '\n'; i++) h = h * 13131ULL + (uint64_t)(int64_t)(signed char)t[i];
+    keys[k] = h;
+    return;
+  }
+  // glibc atoi = (int)strtol(s, 0, 10): leading isspace, sign, digits; strtol saturates
+  uint64_t e = i;
+  while (e < nb && t[e] != ' ' && t[e] != '\n') e++;
+  while (i < e && (t[i] == '\t' || t[i] == '\v' || t[i] == '\f' || t[i] == '\r')) i++;
+  bool neg = false;
+  if (i < e && (t[i] == '+' || t[i] == '-')) neg = t[i++] == '-';
+  const uint64_t lim = neg ? 9223372036854775808ULL : 9223372036854775807ULL;
+  uint64_t v = 0;
+  bool ovf = false;
+  for (; i < e && t[i] >= '0' && t[i] <= '9'; i++) {
+    const uint64_t d = (uint64_t)(t[i] - '0');
+    if (ovf || v > (lim - d) / 10)
+      ovf = true;
+    else
+      v = v * 10 + d;
+  }
+  if (ovf) v = lim;
+  const int64_t sv = neg ? (int64_t)(0 - v) : (int64_t)v;
+  keys[k] = (uint64_t)(int64_t)(int32_t)sv;
+}
+
+__global__ void k_gather_keys(const uint32_t *__restrict__ ids, uint64_t n, const uint64_t *__restrict__ wk,
+                              uint64_t nw, uint64_t *__restrict__ keys, uint32_t *__restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t id = ids[i];
+  if (id >= nw) {
+    *bad = 1;
+    keys[i] = 0;
+  } else {
+    keys[i] = wk[id];
+  }
+}
+
+// line of every token (upper bound in line_off) and its validity
+__global__ void k_tok_lines(const int64_t *__restrict__ off, uint64_t nl, uint64_t n, int min_len,
+                            int32_t *__restrict__ tline, uint32_t *__restrict__ pos) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  uint64_t lo = 0, hi = nl;  // largest l with off[l] <= t (empty lines share an offset: take the last)
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)off[mid] <= t)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  tline[t] = (int32_t)lo;
+  pos[t] = (uint32_t)t;
+}
+
+__global__ void k_run_heads(const uint64_t *__restrict__ k, uint64_t n, uint32_t *__restrict__ head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_run_stats(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ ps,
+                            const uint32_t *__restrict__ rid1, const uint32_t *__restrict__ head, uint64_t n,
+                            const int32_t *__restrict__ tline, const int64_t *__restrict__ off, int min_len,
+                            uint64_t *__restrict__ ukey, uint32_t *__restrict__ cnt, uint32_t *__restrict__ first) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = rid1[i] - 1, p = ps[i];
+  if (head[i]) ukey[r] = ks[i];
+  const int32_t l = tline[p];
+  if (off[l + 1] - off[l] >= min_len) {
+    atomicAdd(&cnt[r], 1u);
+    atomicMin(&first[r], p);
+  }
+}
+
+__global__ void k_tok_vid(const uint32_t *__restrict__ ps, const uint32_t *__restrict__ rid1, uint64_t n,
+                          const int32_t *__restrict__ vid_of_run, int32_t *__restrict__ tok) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) tok[ps[i]] = vid_of_run[rid1[i] - 1];
+}
+
+// (batch << 32 | vid) of every token of every batch's gather window; tokens
+// of invalid lines (never gathered) get the sentinel, which sorts last
+__global__ void k_sched_keys(const uint64_t *__restrict__ eoff, const int64_t *__restrict__ ta, uint32_t nb,
+                             uint64_t E, const int32_t *__restrict__ tok, const int32_t *__restrict__ tline,
+                             const uint8_t *__restrict__ valid, uint64_t *__restrict__ out) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  uint32_t lo = 0, hi = nb;  // batch: largest b with eoff[b] <= e
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (eoff[mid] <= e)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const uint64_t t = (uint64_t)ta[lo] + (e - eoff[lo]);
+  out[e] = valid[tline[t]] ? ((uint64_t)lo << 32) | (uint32_t)tok[t] : ~0ULL;
+}
+
+__global__ void k_uniq_flags(const uint64_t *__restrict__ k, uint64_t n, uint32_t *__restrict__ f) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = (k[i] != ~0ULL && (i == 0 || k[i] != k[i - 1])) ? 1u : 0u;
+}
+
+__global__ void k_uniq_scatter(const uint64_t *__restrict__ k, const uint32_t *__restrict__ f,
+                               const uint32_t *__restrict__ at, uint64_t n, uint64_t *__restrict__ uk,
+                               int32_t *__restrict__ K) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && f[i]) {
+    uk[at[i]] = k[i];
+    K[at[i]] = (int32_t)(uint32_t)k[i];
+  }
+}
+
+// kofs[b] = first unique key of batch b (lower bound of b << 32)
+__global__ void k_batch_kofs(const uint64_t *__restrict__ uk, uint64_t nu, uint32_t nb, uint64_t *__restrict__ kofs) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nb) return;
+  const uint64_t v = (uint64_t)b << 32;
+  uint64_t lo = 0, hi = nu;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (uk[mid] < v)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  kofs[b] = lo;
+}
+
+template <typename T> int exclusive_scan(const T *in, T *out, uint64_t n, DevMem &tmp, hipStream_t s) {
+  size_t b = 0;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b, in, out, (int)n, s));
+  SWPS_TRY(tmp.ensure(b));
+  b = tmp.bytes;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, b, in, out, (int)n, s));
+  return SWPS_OK;
+}
+template <typename T> int inclusive_scan(const T *in, T *out, uint64_t n, DevMem &tmp, hipStream_t s) {
+  size_t b = 0;
+  SWPS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b, in, out, (int)n, s));
+  SWPS_TRY(tmp.ensure(b));
+  b = tmp.bytes;
+  SWPS_HIP(hipcub::DeviceScan::InclusiveSum(tmp.p, b, in, out, (int)n, s));
+  return SWPS_OK;
+}
+
+// Vocab + tokens from device keys [ntok] (consumed) and host line offsets.
+int ingest_gpu(swps_w2v *w, DevMem &d_keys, uint64_t nt, std::vector<int64_t> &&line_off) {
+  hipStream_t s = w->s;
+  const uint64_t nl = line_off.size() - 1;
+  if (nt >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 tokens per rank");
+  w->line_off = std::move(line_off);
+  w->line_valid.assign(nl, 0);
+  uint64_t tw = 0;
+  for (uint64_t l = 0; l < nl; l++) {
+    const int64_t len = w->line_off[l + 1] - w->line_off[l];
+    w->line_valid[l] = len >= w->cfg.min_sentence_length;
+    if (w->line_valid[l]) tw += (uint64_t)len;
+  }
+  SWPS_TRY(upload(w->d_line_off, w->line_off, s));
+  SWPS_TRY(w->d_tok.ensure(std::max<uint64_t>(nt, 1) * 4));
+  SWPS_TRY(w->d_tok_line.ensure(std::max<uint64_t>(nt, 1) * 4));
+  DevMem pos, ks, ps, head, rid1, tmp;
+  SWPS_TRY(pos.ensure(std::max<uint64_t>(nt, 1) * 4));
+  SWPS_TRY(ks.ensure(std::max<uint64_t>(nt, 1) * 8));
+  SWPS_TRY(ps.ensure(std::max<uint64_t>(nt, 1) * 4));
+  if (nt) {
+    k_tok_lines<<<nblk(nt), 256, 0, s>>>(w->d_line_off.as<int64_t>(), nl, nt, w->cfg.min_sentence_length,
+                                          w->d_tok_line.as<int32_t>(), pos.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+    size_t sb = 0;
+    SWPS_HIP(sort_pairs(nullptr, sb, d_keys.as<uint64_t>(), ks.as<uint64_t>(), pos.as<uint32_t>(), ps.as<uint32_t>(),
+                        nt, 64, s));
+    SWPS_TRY(tmp.ensure(sb));
+    sb = tmp.bytes;
+    SWPS_HIP(sort_pairs(tmp.p, sb, d_keys.as<uint64_t>(), ks.as<uint64_t>(), pos.as<uint32_t>(), ps.as<uint32_t>(), nt,
+                        64, s));
+    d_keys.release();
+    pos.release();
+    SWPS_TRY(head.ensure(nt * 4));
+    SWPS_TRY(rid1.ensure(nt * 4));
+    k_run_heads<<<nblk(nt), 256, 0, s>>>(ks.as<uint64_t>(), nt, head.as<uint32_t>());
+    SWPS_TRY(inclusive_scan(head.as<uint32_t>(), rid1.as<uint32_t>(), nt, tmp, s));
+  }
+  uint32_t nruns = 0;
+  if (nt) SWPS_HIP(hipMemcpyAsync(&nruns, rid1.as<uint32_t>() + nt - 1, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  DevMem ukey, cnt, first;
+  SWPS_TRY(ukey.ensure(std::max<uint32_t>(nruns, 1) * 8));
+  SWPS_TRY(cnt.ensure(std::max<uint32_t>(nruns, 1) * 4));
+  SWPS_TRY(first.ensure(std::max<uint32_t>(nruns, 1) * 4));
+  SWPS_HIP(hipMemsetAsync(cnt.p, 0, std::max<uint32_t>(nruns, 1) * 4, s));
+  SWPS_HIP(hipMemsetAsync(first.p, 0xFF, std::max<uint32_t>(nruns, 1) * 4, s));
+  if (nt) {
+    k_run_stats<<<nblk(nt), 256, 0, s>>>(ks.as<uint64_t>(), ps.as<uint32_t>(), rid1.as<uint32_t>(),
+                                          head.as<uint32_t>(), nt, w->d_tok_line.as<int32_t>(),
+                                          w->d_line_off.as<int64_t>(), w->cfg.min_sentence_length,
+                                          ukey.as<uint64_t>(), cnt.as<uint32_t>(), first.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+  }
+  ks.release();
+  head.release();
+  std::vector<uint64_t> hk(nruns);
+  std::vector<uint32_t> hc(nruns), hf(nruns);
+  if (nruns) {
+    SWPS_HIP(hipMemcpyAsync(hk.data(), ukey.p, nruns * 8ULL, hipMemcpyDeviceToHost, s));
+    SWPS_HIP(hipMemcpyAsync(hc.data(), cnt.p, nruns * 4ULL, hipMemcpyDeviceToHost, s));
+    SWPS_HIP(hipMemcpyAsync(hf.data(), first.p, nruns * 4ULL, hipMemcpyDeviceToHost, s));
+  }
+  SWPS_HIP(hipStreamSynchronize(s));
+  // _local_keys: std::unordered_set filled in first-occurrence order over the
+  // valid lines; its iteration order is the vid order (ingest() above)
+  std::vector<uint32_t> order;
+  order.reserve(nruns);
+  for (uint32_t r = 0; r < nruns; r++) {
+    if (hc[r] == 0)
+      return fail(SWPS_E_UNSUPPORTED, "a word occurs only in lines shorter than min_sentence_length "
+                                      "(to_sample reads past word_freq in the reference)");
+    order.push_back(r);
+  }
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hf[a] < hf[b]; });
+  std::unordered_set<uint64_t> local_keys;
+  for (uint32_t r : order) local_keys.insert(hk[r]);
+  if (local_keys.size() < 5) return fail(SWPS_E_UNSUPPORTED, "fewer than 5 keys (word2vec_global.h:556 returns)");
+  w->train_words = tw;
+  w->vocab_keys.assign(local_keys.begin(), local_keys.end());
+  const uint64_t V = w->vocab_keys.size();
+  std::vector<std::pair<uint64_t, int32_t>> kv(V);
+  for (uint64_t i = 0; i < V; i++) {
+    if (w->vocab_keys[i] == 0)
+      return fail(SWPS_E_UNSUPPORTED, "a vocab key hashes to 0 (the reference redraws such negatives)");
+    kv[i] = {w->vocab_keys[i], (int32_t)i};
+  }
+  std::sort(kv.begin(), kv.end());  // runs are in ascending key order too
+  std::vector<int32_t> vid_of_run(nruns);
+  w->counts.assign(V, 0);
+  for (uint32_t r = 0; r < nruns; r++) {
+    vid_of_run[r] = kv[r].second;
+    w->counts[kv[r].second] = (int32_t)hc[r];
+  }
+  DevMem dv;
+  SWPS_TRY(upload(dv, vid_of_run, s));
+  if (nt) {
+    k_tok_vid<<<nblk(nt), 256, 0, s>>>(ps.as<uint32_t>(), rid1.as<uint32_t>(), nt, dv.as<int32_t>(),
+                                        w->d_tok.as<int32_t>());
+    SWPS_HIP(hipGetLastError());
+  }
+  SWPS_HIP(hipStreamSynchronize(s));
+  w->tok.clear();
+  w->tok_line.clear();
+  w->ntok = nt;
+  w->tok_on_device = true;
+  w->loaded = true;
+  return SWPS_OK;
+}
+
+// build_schedule (above) with the windows' key sets made on the device
+int schedule_gpu(swps_w2v *w) {
+  hipStream_t s = w->s;
+  const uint64_t nl = w->line_off.size() - 1;
+  const int B = w->cfg.minibatch;
+  w->batches.clear();
+  std::vector<int64_t> ta;     // window token start per batch (batches without a key set: empty)
+  std::vector<uint64_t> eoff;  // window element offsets
+  eoff.push_back(0);
+  auto window_end = [&](uint64_t li) {  // the line after the B+3-valid-line window from li
+    int count = 0;
+    for (int task = 0; task < 3; task++)
+      while (li < nl) {
+        const uint64_t l = li++;
+        if (!w->line_valid[l]) continue;
+        if (++count > B) break;
+      }
+    return li;
+  };
+  uint64_t wa = 0, we = 0;
+  bool haveK = false;
+  auto emit = [&](uint64_t l0, uint64_t l1, bool withK) {
+    w->batches.push_back(swps_w2v::Batch{l0, l1, 0, 0});
+    const int64_t a = withK ? w->line_off[wa] : 0, e = withK ? w->line_off[we] : 0;
+    ta.push_back(a);
+    eoff.push_back(eoff.back() + (uint64_t)(e - a));
+  };
+  uint64_t start = 0, cur = 0, line_counter = 0, last = 0;
+  for (uint64_t li = 0; li < nl; li++) {
+    cur += (uint64_t)(w->line_off[li + 1] - w->line_off[li]);
+    line_counter++;
+    last = li + 1;
+    if (line_counter == 1) {
+      emit(start, li + 1, haveK);
+      wa = li + 1;
+      we = window_end(li + 1);
+      haveK = true;
+      start = li + 1;
+    }
+    if (line_counter % (uint64_t)B == 0) {
+      emit(start, li + 1, haveK);
+      wa = li + 1;
+      we = window_end(li + 1);
+      start = li + 1;
+    }
+    if (cur > w->train_words) break;
+  }
+  emit(start, last, haveK);
+  const uint32_t nb = (uint32_t)w->batches.size();
+  const uint64_t E = eoff.back();
+  DevMem d_eoff, d_ta, d_valid, keys, keys_s, flags, at, uk, tmp, kofs;
+  SWPS_TRY(upload(d_eoff, eoff, s));
+  SWPS_TRY(upload(d_ta, ta, s));
+  SWPS_TRY(upload(d_valid, w->line_valid, s));
+  uint64_t nu = 0;
+  if (E) {
+    SWPS_TRY(keys.ensure(E * 8));
+    SWPS_TRY(keys_s.ensure(E * 8));
+    k_sched_keys<<<nblk(E), 256, 0, s>>>(d_eoff.as<uint64_t>(), d_ta.as<int64_t>(), nb, E, w->d_tok.as<int32_t>(),
+                                          w->d_tok_line.as<int32_t>(), d_valid.as<uint8_t>(), keys.as<uint64_t>());
+    SWPS_HIP(hipGetLastError());
+    size_t sb = 0;
+    SWPS_HIP(sort_keys(nullptr, sb, keys.as<uint64_t>(), keys_s.as<uint64_t>(), E, 64, s));
+    SWPS_TRY(tmp.ensure(sb));
+    sb = tmp.bytes;
+    SWPS_HIP(sort_keys(tmp.p, sb, keys.as<uint64_t>(), keys_s.as<uint64_t>(), E, 64, s));
+    keys.release();
+    SWPS_TRY(flags.ensure((E + 1) * 4));
+    SWPS_TRY(at.ensure((E + 1) * 4));
+    k_uniq_flags<<<nblk(E), 256, 0, s>>>(keys_s.as<uint64_t>(), E, flags.as<uint32_t>());
+    SWPS_HIP(hipMemsetAsync(flags.as<uint32_t>() + E, 0, 4, s));
+    SWPS_TRY(exclusive_scan(flags.as<uint32_t>(), at.as<uint32_t>(), E + 1, tmp, s));
+    uint32_t n32 = 0;
+    SWPS_HIP(hipMemcpyAsync(&n32, at.as<uint32_t>() + E, 4, hipMemcpyDeviceToHost, s));
+    SWPS_HIP(hipStreamSynchronize(s));
+    nu = n32;
+    SWPS_TRY(uk.ensure(std::max<uint64_t>(nu, 1) * 8));
+    SWPS_TRY(w->d_K.ensure(std::max<uint64_t>(nu, 1) * 4));
+    k_uniq_scatter<<<nblk(E), 256, 0, s>>>(keys_s.as<uint64_t>(), flags.as<uint32_t>(), at.as<uint32_t>(), E,
+                                            uk.as<uint64_t>(), w->d_K.as<int32_t>());
+    SWPS_HIP(hipGetLastError());
+  } else {
+    SWPS_TRY(w->d_K.ensure(4));
+    SWPS_TRY(uk.ensure(8));
+  }
+  SWPS_TRY(kofs.ensure((nb + 1ULL) * 8));
+  k_batch_kofs<<<nblk(nb + 1ULL), 256, 0, s>>>(uk.as<uint64_t>(), nu, nb, kofs.as<uint64_t>());
+  SWPS_HIP(hipGetLastError());
+  std::vector<uint64_t> hk(nb + 1);
+  SWPS_HIP(hipMemcpyAsync(hk.data(), kofs.p, (nb + 1ULL) * 8, hipMemcpyDeviceToHost, s));
+  w->allK.resize(nu);
+  if (nu) SWPS_HIP(hipMemcpyAsync(w->allK.data(), w->d_K.p, nu * 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  w->max_tok = w->max_U = w->max_lines = 0;
+  for (uint32_t b = 0; b < nb; b++) {
+    auto &bt = w->batches[b];
+    bt.kofs = hk[b];
+    bt.U = (uint32_t)(hk[b + 1] - hk[b]);
+    w->max_tok = std::max<uint64_t>(w->max_tok, (uint64_t)(w->line_off[bt.l1] - w->line_off[bt.l0]));
+    w->max_U = std::max<uint64_t>(w->max_U, bt.U);
+    w->max_lines = std::max<uint64_t>(w->max_lines, bt.l1 - bt.l0);
+  }
+  return SWPS_OK;
+}
+
+// text file -> device keys + line offsets (load_text's split on ' ' and '\n'
+// only; a file holding a NUL byte takes the host path, whose lines end at
+// their first NUL like the reference's std::string(cline))
+int tokenize_gpu(swps_w2v *w, const std::vector<char> &text, DevMem &d_keys, uint64_t &nt,
+                 std::vector<int64_t> &line_off) {
+  hipStream_t s = w->s;
+  const uint64_t nb = text.size();
+  DevMem d_text, st, nlf, tix, lix, tstart, d_off, tmp;
+  SWPS_TRY(d_text.ensure(std::max<uint64_t>(nb, 1)));
+  if (nb) SWPS_HIP(hipMemcpyAsync(d_text.p, text.data(), nb, hipMemcpyHostToDevice, s));
+  SWPS_TRY(st.ensure((nb + 1) * 4));
+  SWPS_TRY(nlf.ensure((nb + 1) * 4));
+  SWPS_TRY(tix.ensure((nb + 1) * 4));
+  SWPS_TRY(lix.ensure((nb + 1) * 4));
+  k_text_flags<<<nblk(nb + 1), 256, 0, s>>>(d_text.as<char>(), nb, st.as<uint32_t>(), nlf.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  SWPS_TRY(exclusive_scan(st.as<uint32_t>(), tix.as<uint32_t>(), nb + 1, tmp, s));
+  SWPS_TRY(exclusive_scan(nlf.as<uint32_t>(), lix.as<uint32_t>(), nb + 1, tmp, s));
+  uint32_t tot[2];
+  SWPS_HIP(hipMemcpyAsync(&tot[0], tix.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipMemcpyAsync(&tot[1], lix.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  nt = tot[0];
+  const uint64_t nnl = tot[1];
+  const uint64_t nlines = nnl + ((nb && text[nb - 1] != '\n') ? 1 : 0);
+  SWPS_TRY(tstart.ensure(std::max<uint64_t>(nt, 1) * 8));
+  SWPS_TRY(d_off.ensure((nlines + 2) * 8));
+  SWPS_HIP(hipMemsetAsync(d_off.p, 0, 8, s));
+  if (nb)
+    k_text_index<<<nblk(nb), 256, 0, s>>>(d_text.as<char>(), nb, st.as<uint32_t>(), tix.as<uint32_t>(),
+                                           lix.as<uint32_t>(), tstart.as<uint64_t>(), d_off.as<int64_t>());
+  SWPS_HIP(hipGetLastError());
+  SWPS_TRY(d_keys.ensure(std::max<uint64_t>(nt, 1) * 8));
+  if (nt)
+    k_text_keys<<<nblk(nt), 256, 0, s>>>(d_text.as<char>(), nb, tstart.as<uint64_t>(), nt,
+                                          w->cfg.key_mode == SWPS_KEY_ATOI, d_keys.as<uint64_t>());
+  SWPS_HIP(hipGetLastError());
+  line_off.assign(nlines + 1, 0);
+  if (nnl) SWPS_HIP(hipMemcpyAsync(line_off.data(), d_off.p, (nnl + 1) * 8, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  line_off[nlines] = (int64_t)nt;  // a last line without '\n'
+  return SWPS_OK;
+}
+
 int upload_corpus(swps_w2v *w) {
   hipStream_t s = w->s;
   const uint64_t V = w->vocab_keys.size();
-  SWPS_TRY(upload(w->d_tok, w->tok, s));
-  SWPS_TRY(upload(w->d_tok_line, w->tok_line, s));
+  if (!w->tok_on_device) {
+    SWPS_TRY(upload(w->d_tok, w->tok, s));
+    SWPS_TRY(upload(w->d_tok_line, w->tok_line, s));
+    SWPS_TRY(upload(w->d_K, w->allK, s));
+  }
   SWPS_TRY(upload(w->d_line_off, w->line_off, s));
-  SWPS_TRY(upload(w->d_K, w->allK, s));
+  SWPS_TRY(tok_fingerprint(w));
   std::vector<int64_t> btok;  // token offset of every batch start + the epoch end
   for (auto &b : w->batches) btok.push_back(w->line_off[b.l0]);
   btok.push_back(w->line_off[w->batches.back().l1]);
@@ -2378,6 +2865,26 @@ int swps_w2v_destroy(swps_w2v *w) {
 
 // LineFileReader + split(" ") + BKDRHash / atoi (word2vec_global.h:215-227)
 int swps_w2v_load_text(swps_w2v *w, const char *path) {
+  if (!w->cfg.minibatch_vocab && !w->cfg.host_ingest) {  // the GPU ingest (no NUL bytes in the file)
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(SWPS_E_IO, std::string("no such file or directory: ") + path);
+    std::vector<char> text;
+    char chunk[1 << 16];
+    size_t k;
+    while ((k = fread(chunk, 1, sizeof(chunk), f)) > 0) text.insert(text.end(), chunk, chunk + k);
+    fclose(f);
+    if (!memchr(text.data(), 0, text.size())) {
+      SWPS_HIP(hipSetDevice(w->t->cfg.device));
+      DevMem d_keys;
+      uint64_t nt = 0;
+      std::vector<int64_t> off;
+      SWPS_TRY(tokenize_gpu(w, text, d_keys, nt, off));
+      std::vector<char>().swap(text);
+      SWPS_TRY(ingest_gpu(w, d_keys, nt, std::move(off)));
+      SWPS_TRY(schedule_gpu(w));
+      return upload_corpus(w);
+    }
+  }
   FILE *f = fopen(path, "rb");
   if (!f) return fail(SWPS_E_IO, std::string("no such file or directory: ") + path);
   std::vector<uint64_t> keys;
@@ -2415,19 +2922,68 @@ int swps_w2v_load_text(swps_w2v *w, const char *path) {
 int swps_w2v_load_tokens(swps_w2v *w, const uint32_t *word_ids, uint64_t ntok, const uint64_t *line_off,
                          uint64_t nlines, const uint64_t *word_keys, uint64_t nwords) {
   if (line_off[0] != 0 || line_off[nlines] != ntok) return fail(SWPS_E_CFG, "line_off must span [0, ntok]");
+  std::vector<int64_t> off(line_off, line_off + nlines + 1);
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  if (!w->cfg.minibatch_vocab && !w->cfg.host_ingest) {  // the GPU ingest
+    DevMem d_ids, d_wk, d_keys, d_bad;
+    SWPS_TRY(d_ids.ensure(std::max<uint64_t>(ntok, 1) * 4));
+    SWPS_TRY(d_wk.ensure(std::max<uint64_t>(nwords, 1) * 8));
+    SWPS_TRY(d_keys.ensure(std::max<uint64_t>(ntok, 1) * 8));
+    SWPS_TRY(d_bad.ensure(4));
+    if (ntok) SWPS_HIP(hipMemcpyAsync(d_ids.p, word_ids, ntok * 4, hipMemcpyHostToDevice, w->s));
+    if (nwords) SWPS_HIP(hipMemcpyAsync(d_wk.p, word_keys, nwords * 8, hipMemcpyHostToDevice, w->s));
+    SWPS_HIP(hipMemsetAsync(d_bad.p, 0, 4, w->s));
+    if (ntok)
+      k_gather_keys<<<nblk(ntok), 256, 0, w->s>>>(d_ids.as<uint32_t>(), ntok, d_wk.as<uint64_t>(), nwords,
+                                                   d_keys.as<uint64_t>(), d_bad.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+    uint32_t bad = 0;
+    SWPS_HIP(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, w->s));
+    SWPS_HIP(hipStreamSynchronize(w->s));
+    if (bad) return fail(SWPS_E_CFG, "word id out of range");
+    d_ids.release();
+    d_wk.release();
+    SWPS_TRY(ingest_gpu(w, d_keys, ntok, std::move(off)));
+    SWPS_TRY(schedule_gpu(w));
+    return upload_corpus(w);
+  }
   std::vector<uint64_t> keys(ntok);
   for (uint64_t i = 0; i < ntok; i++) {
     if (word_ids[i] >= nwords) return fail(SWPS_E_CFG, "word id out of range");
     keys[i] = word_keys[word_ids[i]];
   }
-  std::vector<int64_t> off(line_off, line_off + nlines + 1);
-  SWPS_HIP(hipSetDevice(w->t->cfg.device));
   SWPS_TRY(ingest(w, keys, std::move(off)));
   if (w->cfg.minibatch_vocab)
     SWPS_TRY(build_schedule_mb(w));
   else
     build_schedule(w);
   return upload_corpus(w);
+}
+
+int swps_w2v_corpus(swps_w2v *w, int32_t *vid, int32_t *line, uint64_t cap) {
+  if (!w->loaded) return fail(SWPS_E_STATE, "load a corpus first");
+  if (cap < w->ntok) return fail(SWPS_E_CFG, "buffer too small");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  if (w->ntok) {
+    SWPS_HIP(hipMemcpyAsync(vid, w->d_tok.p, w->ntok * 4, hipMemcpyDeviceToHost, w->s));
+    SWPS_HIP(hipMemcpyAsync(line, w->d_tok_line.p, w->ntok * 4, hipMemcpyDeviceToHost, w->s));
+  }
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  return SWPS_OK;
+}
+
+int swps_w2v_batch_keys(swps_w2v *w, uint64_t b, int32_t *out, uint64_t cap, uint64_t *n, uint64_t *lines2) {
+  if (!w->loaded) return fail(SWPS_E_STATE, "load a corpus first");
+  if (b >= w->batches.size()) return fail(SWPS_E_CFG, "no such batch");
+  const auto &bt = w->batches[b];
+  *n = bt.U;
+  if (lines2) {
+    lines2[0] = bt.l0;
+    lines2[1] = bt.l1;
+  }
+  if (cap < bt.U) return fail(SWPS_E_CFG, "buffer too small");
+  std::copy(w->allK.begin() + bt.kofs, w->allK.begin() + bt.kofs + bt.U, out);
+  return SWPS_OK;
 }
 
 int swps_w2v_vocab(swps_w2v *w, uint64_t *keys, int32_t *counts, uint64_t cap, uint64_t *n) {
@@ -2444,7 +3000,7 @@ int swps_w2v_info(swps_w2v *w, uint64_t *o) {
   o[0] = w->vocab_keys.size();
   o[1] = w->train_words;
   o[2] = w->line_off.empty() ? 0 : w->line_off.size() - 1;
-  o[3] = w->tok.size();
+  o[3] = w->ntok;
   o[4] = w->batches.size();
   o[5] = w->max_tok;
   o[6] = w->lstate;
@@ -2881,7 +3437,7 @@ uint64_t w2v_corpus_fp(const swps_w2v *w) {
   h = checksum64(h, w->vocab_keys.data(), w->vocab_keys.size() * 8);
   h = checksum64(h, w->counts.data(), w->counts.size() * 4);
   h = checksum64(h, w->line_off.data(), w->line_off.size() * 8);
-  return checksum64(h, w->tok.data(), w->tok.size() * 4);
+  return checksum64(h, &w->tok_fp, 8);
 }
 
 }  // namespace
