@@ -318,10 +318,11 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
       if (d > 0) {
         x = x * kLcgA + kLcgC;
         const uint64_t slot = fast_mod(x >> 16, a.uni_size, a.mT);
-        if (a.alias) {  // Walker/Vose alias over unigram^0.75: bucket from the high word, coin from bits 8..31
+        if (a.alias) {  // Walker/Vose alias over unigram^0.75: bucket from the LCG's high word; the
+                        // coin from a mix of the whole state (the LCG's low bits have short periods)
           const uint32_t bkt = (uint32_t)(((x >> 32) * (uint64_t)a.alias_n) >> 32);
           const uint2 e = a.alias[bkt];
-          const float coin = (float)((uint32_t)(x >> 8) & 0xFFFFFFu) * (1.0f / 16777216.0f);
+          const float coin = (float)(uint32_t)(splitmix64(x) >> 40) * (1.0f / 16777216.0f);
           const int32_t w = coin < __uint_as_float(e.x) ? (int32_t)bkt : (int32_t)e.y;
           tv = a.bstarts ? a.buk[w] : w;
         } else if (a.bstarts) {  // word2vec.h:398-425 table over the minibatch vocab, run-length form
@@ -365,6 +366,137 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = srec[i];
   }
   // rows the forward will read (roofline accounting), one atomic per wave
+  unsigned long long c = (unsigned long long)nctx, g = (unsigned long long)ntgt;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    c += __shfl_xor(c, off, 64);
+    g += __shfl_xor(g, off, 64);
+  }
+  if (a.rows_touched && (threadIdx.x & 63) == 0 && (c | g)) {  // profiled passes only
+    atomicAdd(&a.rows_touched[0], c);
+    atomicAdd(&a.rows_touched[1], g);
+  }
+}
+
+// Main-LCG jump by k draws with per-bit constants (x -> A_i x + C_i jumps
+// 2^i draws; powers of one affine map commute): the per-thread doubling loop
+// of lcg_jump squared the same (A, C) pairs in every thread.
+__constant__ uint64_t c_p2A[64];
+__constant__ uint64_t c_p2C[64];
+__device__ __forceinline__ uint64_t lcg_jump_p2(uint64_t x, uint64_t k) {
+  for (int i = 0; k; i++, k >>= 1)
+    if (k & 1) x = c_p2A[i] * x + c_p2C[i];
+  return x;
+}
+
+// k_records for the common case — compile-time window W and negatives N, the
+// reference's table sampler through the coarse index, one global vocab —
+// restructured so each thread's independent loads are in flight together
+// (all 2W context words, then all their local / row lookups; the N draws
+// first, then the N unigram searches advanced in lockstep) instead of one
+// dependent chain per slot.  Identical outputs to k_records.
+template <int W, int N>
+__global__ __launch_bounds__(256) void k_records_t(RecArgs a) {
+  extern __shared__ int32_t srec[];
+  constexpr int RS = 2 * W + N + 2;
+  const uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x;
+  const uint64_t p = p0 + threadIdx.x;
+  int nctx = 0, ntgt = 0;
+  if (p < a.P) {
+    const uint64_t P = a.P;
+    const uint64_t HOFF = P * (uint64_t)(N + 1);
+    const uint64_t t = (uint64_t)a.pos_tok[p];
+    const int32_t l = a.tok_line[t];
+    const int64_t ls = a.line_off[l];
+    const int n = (int)(a.line_off[l + 1] - ls), pos = (int)((int64_t)t - ls);
+    const int32_t word = a.tok[t];
+    const uint64_t rank = (uint64_t)(a.kscan[t] - a.kscan[ls]);
+    uint64_t x = lcg_jump_p2(a.lstate, a.ldoff[l] + 1 + rank * (uint64_t)(N + 1));
+    x = x * kLcgA + kLcgC;
+    const int b = (int)fast_mod(x, (uint64_t)W, a.mW);
+    int32_t *r = srec + threadIdx.x * RS;
+    r[0] = word;
+    // ---- contexts: a = b .. 2W-b (a != W) inside the line ----
+    int32_t cv[2 * W];
+#pragma unroll
+    for (int j = 0; j < 2 * W; j++) {
+      cv[j] = -1;
+      if (j < 2 * (W - b)) {
+        int aa = b + j;
+        if (aa >= W) aa++;
+        const int c = pos - W + aa;
+        if (c >= 0 && c < n) cv[j] = a.tok[ls + c];
+      }
+    }
+    int32_t cu[2 * W];
+#pragma unroll
+    for (int j = 0; j < 2 * W; j++) cu[j] = cv[j] >= 0 ? a.local[cv[j]] : -1;
+    int32_t cs[2 * W];
+#pragma unroll
+    for (int j = 0; j < 2 * W; j++) cs[j] = (cu[j] >= 0 && a.vid_row) ? (kTabRow | (int32_t)a.vid_row[cv[j]]) : cv[j];
+    // ---- targets: the word, then N draws from the unigram table ----
+    uint64_t slot[N + 1];
+    uint32_t lo[N + 1], hi[N + 1];
+#pragma unroll
+    for (int d = 1; d <= N; d++) {
+      x = x * kLcgA + kLcgC;
+      slot[d] = fast_mod(x >> 16, a.uni_size, a.mT);
+      const uint64_t bk = slot[d] >> a.ushift;
+      lo[d] = (uint32_t)a.uidx[bk];
+      hi[d] = min((uint32_t)a.uidx[bk + 1] + 1u, a.uV);
+    }
+    for (bool more = true; more;) {  // the N binary searches (unigram_lookup) step together
+      more = false;
+#pragma unroll
+      for (int d = 1; d <= N; d++) {
+        if (hi[d] - lo[d] > 1) {
+          const uint32_t mid = (lo[d] + hi[d]) >> 1;
+          if (a.ustarts[mid] <= slot[d])
+            lo[d] = mid;
+          else
+            hi[d] = mid;
+          more |= hi[d] - lo[d] > 1;
+        }
+      }
+    }
+    int32_t tv[N + 1];
+    tv[0] = word;
+#pragma unroll
+    for (int d = 1; d <= N; d++) {
+      tv[d] = (int32_t)lo[d];
+      if (a.trace) a.trace[p * N + d - 1] = tv[d];
+      if (tv[d] == word) tv[d] = -1;
+    }
+    int32_t tu[N + 1];
+#pragma unroll
+    for (int d = 0; d <= N; d++) tu[d] = tv[d] >= 0 ? a.local[tv[d]] : -1;
+    int32_t ts[N + 1];
+#pragma unroll
+    for (int d = 0; d <= N; d++) ts[d] = (tu[d] >= 0 && a.vid_row) ? (kTabRow | (int32_t)a.vid_row[tv[d]]) : tv[d];
+    // ---- stores: position record (LDS), gradient records (slot-major) ----
+#pragma unroll
+    for (int j = 0; j < 2 * W; j++) {
+      nctx += cv[j] >= 0;
+      r[1 + j] = cs[j];
+      const uint64_t k = HOFF + (uint64_t)j * P + p;
+      a.pkeys[k] = cu[j] >= 0 ? (uint32_t)cu[j] : a.U;
+      a.pvals[k] = (uint32_t)k;
+    }
+#pragma unroll
+    for (int d = 0; d <= N; d++) {
+      ntgt += tv[d] >= 0;
+      r[1 + 2 * W + d] = ts[d];
+      const uint64_t k = (uint64_t)d * P + p;
+      a.pkeys[k] = tu[d] >= 0 ? (uint32_t)tu[d] : a.U;
+      a.pvals[k] = (uint32_t)k;
+    }
+  }
+  __syncthreads();
+  {
+    const uint32_t nn = (uint32_t)min<uint64_t>(blockDim.x, a.P - min(p0, a.P)) * (uint32_t)RS;
+    int32_t *dst = a.rec + p0 * RS;
+    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) dst[i] = srec[i];
+  }
   unsigned long long c = (unsigned long long)nctx, g = (unsigned long long)ntgt;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -1360,6 +1492,7 @@ struct swps_w2v {
   DevMem d_kflag, d_kscan, d_ldraw, d_ldoff, d_pos_tok, d_rec, d_neu1, d_neu1e, d_pkeys, d_pvals, d_pkeys_s,
       d_pvals_s, d_pg, d_seg, d_icnt, d_ioff, d_partial, d_desc, d_tmp, d_trace, d_rows_touched, d_gstats;
   swps::ShardDriver *drv = nullptr;  // swps_w2v_shard_comm: the library drives the exchange
+  bool rec_generic = false;          // SWPS_REC_GENERIC=1: the generic k_records (A/B, tests)
   DevMem d_lead;  // hot-group leaders of the batch's gather items: [0] = count, then item indices
   uint64_t *h_small = nullptr;  // pinned readback
   // RNG (utils/random.h:44-47, seed 2008)
@@ -1806,24 +1939,45 @@ __global__ void k_tok_lines(const int64_t *__restrict__ off, uint64_t nl, uint64
   pos[t] = (uint32_t)t;
 }
 
-__global__ void k_run_heads(const uint64_t *__restrict__ k, uint64_t n, uint32_t *__restrict__ head) {
+// run heads of the sorted keys, and whether each sorted token lies in a valid
+// (gathered) line
+__global__ void k_run_heads(const uint64_t *__restrict__ k, const uint32_t *__restrict__ ps, uint64_t n,
+                            const int32_t *__restrict__ tline, const int64_t *__restrict__ off, int min_len,
+                            uint32_t *__restrict__ head, uint32_t *__restrict__ valid) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) head[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+  if (i > n) return;
+  if (i == n) {
+    valid[n] = 0;  // the exclusive scan's tail
+    return;
+  }
+  head[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+  const int32_t l = tline[ps[i]];
+  valid[i] = off[l + 1] - off[l] >= min_len ? 1u : 0u;
 }
 
-__global__ void k_run_stats(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ ps,
-                            const uint32_t *__restrict__ rid1, const uint32_t *__restrict__ head, uint64_t n,
-                            const int32_t *__restrict__ tline, const int64_t *__restrict__ off, int min_len,
-                            uint64_t *__restrict__ ukey, uint32_t *__restrict__ cnt, uint32_t *__restrict__ first) {
+__global__ void k_run_starts(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ head,
+                             const uint32_t *__restrict__ rid1, uint64_t n, uint64_t *__restrict__ ukey,
+                             uint32_t *__restrict__ rstart) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t r = rid1[i] - 1, p = ps[i];
-  if (head[i]) ukey[r] = ks[i];
-  const int32_t l = tline[p];
-  if (off[l + 1] - off[l] >= min_len) {
-    atomicAdd(&cnt[r], 1u);
-    atomicMin(&first[r], p);
-  }
+  if (i >= n || !head[i]) return;
+  const uint32_t r = rid1[i] - 1;
+  ukey[r] = ks[i];
+  rstart[r] = (uint32_t)i;
+}
+
+// per run (one thread, no atomics: a hot word's run has millions of tokens):
+// tokens in valid lines = difference of the valid-flag scan; first valid
+// position = the first valid element (the sort is stable: positions ascend)
+__global__ void k_run_stats(const uint32_t *__restrict__ rstart, uint32_t R, uint64_t n,
+                            const uint32_t *__restrict__ vscan, const uint32_t *__restrict__ valid,
+                            const uint32_t *__restrict__ ps, uint32_t *__restrict__ cnt, uint32_t *__restrict__ first) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint64_t s = rstart[r], e = r + 1 < R ? rstart[r + 1] : n;
+  cnt[r] = vscan[e] - vscan[s];
+  uint64_t i = s;
+  while (i < e && !valid[i]) i++;
+  first[r] = i < e ? ps[i] : 0xFFFFFFFFu;
 }
 
 __global__ void k_tok_vid(const uint32_t *__restrict__ ps, const uint32_t *__restrict__ rid1, uint64_t n,
@@ -1915,7 +2069,7 @@ int ingest_gpu(swps_w2v *w, DevMem &d_keys, uint64_t nt, std::vector<int64_t> &&
   SWPS_TRY(upload(w->d_line_off, w->line_off, s));
   SWPS_TRY(w->d_tok.ensure(std::max<uint64_t>(nt, 1) * 4));
   SWPS_TRY(w->d_tok_line.ensure(std::max<uint64_t>(nt, 1) * 4));
-  DevMem pos, ks, ps, head, rid1, tmp;
+  DevMem pos, ks, ps, head, rid1, valid, vscan, tmp;
   SWPS_TRY(pos.ensure(std::max<uint64_t>(nt, 1) * 4));
   SWPS_TRY(ks.ensure(std::max<uint64_t>(nt, 1) * 8));
   SWPS_TRY(ps.ensure(std::max<uint64_t>(nt, 1) * 4));
@@ -1934,23 +2088,29 @@ int ingest_gpu(swps_w2v *w, DevMem &d_keys, uint64_t nt, std::vector<int64_t> &&
     pos.release();
     SWPS_TRY(head.ensure(nt * 4));
     SWPS_TRY(rid1.ensure(nt * 4));
-    k_run_heads<<<nblk(nt), 256, 0, s>>>(ks.as<uint64_t>(), nt, head.as<uint32_t>());
+    SWPS_TRY(valid.ensure((nt + 1) * 4));
+    SWPS_TRY(vscan.ensure((nt + 1) * 4));
+    k_run_heads<<<nblk(nt + 1), 256, 0, s>>>(ks.as<uint64_t>(), ps.as<uint32_t>(), nt, w->d_tok_line.as<int32_t>(),
+                                              w->d_line_off.as<int64_t>(), w->cfg.min_sentence_length,
+                                              head.as<uint32_t>(), valid.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
     SWPS_TRY(inclusive_scan(head.as<uint32_t>(), rid1.as<uint32_t>(), nt, tmp, s));
+    SWPS_TRY(exclusive_scan(valid.as<uint32_t>(), vscan.as<uint32_t>(), nt + 1, tmp, s));
   }
   uint32_t nruns = 0;
   if (nt) SWPS_HIP(hipMemcpyAsync(&nruns, rid1.as<uint32_t>() + nt - 1, 4, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipStreamSynchronize(s));
-  DevMem ukey, cnt, first;
+  DevMem ukey, cnt, first, rstart;
   SWPS_TRY(ukey.ensure(std::max<uint32_t>(nruns, 1) * 8));
   SWPS_TRY(cnt.ensure(std::max<uint32_t>(nruns, 1) * 4));
   SWPS_TRY(first.ensure(std::max<uint32_t>(nruns, 1) * 4));
-  SWPS_HIP(hipMemsetAsync(cnt.p, 0, std::max<uint32_t>(nruns, 1) * 4, s));
-  SWPS_HIP(hipMemsetAsync(first.p, 0xFF, std::max<uint32_t>(nruns, 1) * 4, s));
+  SWPS_TRY(rstart.ensure(std::max<uint32_t>(nruns, 1) * 4));
   if (nt) {
-    k_run_stats<<<nblk(nt), 256, 0, s>>>(ks.as<uint64_t>(), ps.as<uint32_t>(), rid1.as<uint32_t>(),
-                                          head.as<uint32_t>(), nt, w->d_tok_line.as<int32_t>(),
-                                          w->d_line_off.as<int64_t>(), w->cfg.min_sentence_length,
-                                          ukey.as<uint64_t>(), cnt.as<uint32_t>(), first.as<uint32_t>());
+    k_run_starts<<<nblk(nt), 256, 0, s>>>(ks.as<uint64_t>(), head.as<uint32_t>(), rid1.as<uint32_t>(), nt,
+                                           ukey.as<uint64_t>(), rstart.as<uint32_t>());
+    k_run_stats<<<nblk(nruns), 256, 0, s>>>(rstart.as<uint32_t>(), nruns, nt, vscan.as<uint32_t>(),
+                                             valid.as<uint32_t>(), ps.as<uint32_t>(), cnt.as<uint32_t>(),
+                                             first.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
   }
   ks.release();
@@ -2232,6 +2392,111 @@ template <typename T> int pull_all(swps_w2v *w) {
   SWPS_HIP(hipGetLastError());
   SWPS_HIP(hipStreamSynchronize(w->s));
   return SWPS_OK;
+}
+
+// Vec::randInit (vec1.h:229-232) for every vocab key on the GPU: rand() is
+// glibc's additive generator o[i] = o[i-31] + o[i-3] (mod 2^32, output o >> 1;
+// GlibcRand in swps_host.cpp), linear in its state, so output m is
+// sum_j a_j o[3+j] with sum_j a_j x^j = x^(m-3) mod (x^31 - x^28 - 1):
+// every thread jumps to its own run of outputs (square-and-multiply on
+// 31-coefficient polynomials) and then steps the recurrence.  Output k
+// (after `skip` earlier calls) is element k % 2D of key k / 2D's [h | v],
+// (rand()/(float)RAND_MAX - 0.5) / D, written straight into the table row.
+struct Poly31 {
+  uint32_t c[31];
+};
+__device__ void poly_mulmod(const Poly31 &a, const Poly31 &b, Poly31 &out) {
+  uint32_t t[61];
+  for (int i = 0; i < 61; i++) t[i] = 0;
+  for (int i = 0; i < 31; i++)
+    for (int j = 0; j < 31; j++) t[i + j] += a.c[i] * b.c[j];
+  for (int d = 60; d >= 31; d--) {  // x^d = x^(d-3) + x^(d-31)
+    t[d - 3] += t[d];
+    t[d - 31] += t[d];
+  }
+  for (int i = 0; i < 31; i++) out.c[i] = t[i];
+}
+
+constexpr uint64_t kRandRun = 8192;  // outputs per thread
+
+template <typename T>
+__global__ __launch_bounds__(64) void k_rand_init(const uint32_t *__restrict__ base, uint64_t first, uint64_t total,
+                                                   int D, const uint32_t *__restrict__ vid_row, T *__restrict__ rows) {
+  const uint64_t k0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRandRun;
+  if (k0 >= total) return;
+  // o[m] for the 31 values before output k0: m = first + k0 - 31 + d, d = 0..30
+  const uint64_t m0 = first + k0 - 31;
+  Poly31 r, x;  // r = x^(m0-3) mod P
+  for (int i = 0; i < 31; i++) {
+    r.c[i] = i == 0 ? 1u : 0u;
+    x.c[i] = i == 1 ? 1u : 0u;
+  }
+  for (uint64_t e = m0 - 3; e; e >>= 1) {
+    if (e & 1) poly_mulmod(r, x, r);
+    poly_mulmod(x, x, x);
+  }
+  uint32_t ring[31];
+  for (int d = 0; d < 31; d++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 31; j++) v += r.c[j] * base[j];
+    ring[d] = v;
+    const uint32_t top = r.c[30];  // r <- x * r mod P
+    for (int j = 30; j > 0; j--) r.c[j] = r.c[j - 1];
+    r.c[0] = top;
+    r.c[28] += top;
+  }
+  const uint64_t k1 = min(total, k0 + kRandRun);
+  int h = 0;  // ring[h] = o[i-31], ring[(h+28)%31] = o[i-3]
+  for (uint64_t k = k0; k < k1; k++) {
+    const int h28 = h + 28 >= 31 ? h + 28 - 31 : h + 28;
+    const uint32_t v = ring[h] + ring[h28];
+    ring[h] = v;
+    h = h + 1 == 31 ? 0 : h + 1;
+    const float f = (float)(int32_t)(v >> 1) / (float)2147483647;
+    const uint64_t key = k / (2 * (uint64_t)D), el = k % (2 * (uint64_t)D);
+    rows[(uint64_t)vid_row[key] * 4 * D + el] = (T)(((double)f - 0.5) / (double)(size_t)D);
+  }
+}
+
+template <typename T>
+__global__ void k_zero_sums(const uint32_t *__restrict__ vid_row, uint64_t V, int D, T *__restrict__ rows) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= V * 2 * (uint64_t)D) return;
+  const uint64_t key = i / (2 * (uint64_t)D), el = i % (2 * (uint64_t)D);
+  rows[(uint64_t)vid_row[key] * 4 * D + 2 * D + el] = (T)0;
+}
+
+template <typename T> int rand_init_gpu(swps_w2v *w) {
+  const uint64_t V = w->vocab_keys.size();
+  const int D = w->D;
+  // o[3..33] after srand(seed) (GlibcRand's seeding, swps_host.cpp)
+  std::vector<uint32_t> base(31);
+  {
+    int32_t s0[34];
+    uint32_t seed = w->cfg.rand_seed ? w->cfg.rand_seed : 1;
+    s0[0] = (int32_t)seed;
+    for (int i = 1; i < 31; i++) {
+      int64_t hi = s0[i - 1] / 127773, lo = s0[i - 1] % 127773;
+      int64_t v = 16807 * lo - 2836 * hi;
+      if (v < 0) v += 2147483647;
+      s0[i] = (int32_t)v;
+    }
+    for (int i = 31; i < 34; i++) s0[i] = s0[i - 31];
+    for (int j = 0; j < 31; j++) base[j] = (uint32_t)s0[3 + j];
+  }
+  const uint64_t total = V * 2 * (uint64_t)D;
+  const uint64_t first = 344 + w->cfg.rand_offset;  // o index of the first output used
+  DevMem d_base;
+  SWPS_TRY(upload(d_base, base, w->s));
+  const uint64_t nthr = (total + kRandRun - 1) / kRandRun;
+  if (total) {
+    k_rand_init<T><<<nblk(nthr, 64), 64, 0, w->s>>>(d_base.as<uint32_t>(), first, total, D,
+                                                    w->d_vid_row.as<uint32_t>(), w->t->rows.as<T>());
+    k_zero_sums<T><<<nblk(total), 256, 0, w->s>>>(w->d_vid_row.as<uint32_t>(), V, D, w->t->rows.as<T>());
+  }
+  SWPS_HIP(hipGetLastError());
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  return pull_all<T>(w);
 }
 
 template <typename T> int set_hv(swps_w2v *w, const double *hv) {
@@ -2534,7 +2799,10 @@ int prep_batch(swps_w2v *w) {
                w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
                tm.on ? w->d_rows_touched.as<unsigned long long>() : nullptr};
     hipEvent_t er = tm.begin(s);
-    k_records<<<nblk(P), 256, 256 * RS * sizeof(int32_t), s>>>(ra);
+    if (W == 5 && N == 5 && use_uidx && !w->rec_generic)
+      k_records_t<5, 5><<<nblk(P), 256, 256 * RS * sizeof(int32_t), s>>>(ra);
+    else
+      k_records<<<nblk(P), 256, 256 * RS * sizeof(int32_t), s>>>(ra);
     SWPS_HIP(hipGetLastError());
     tm.end(KT_REC, er, s);
     pb.records = true;
@@ -2820,6 +3088,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_CACHE_PAD")) w->cache_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_OVERLAP")) w->overlap = atoi(e);  // A/B timing
   if (const char *e = getenv("SWPS_GATHER_UNR")) w->gather_unr = atoi(e);
+  if (const char *e = getenv("SWPS_REC_GENERIC")) w->rec_generic = atoi(e) != 0;
   if (const char *e = getenv("SWPS_GATHER_GRID")) w->gather_grid = std::max(64, atoi(e));
   int rc = check_cfg(w);
   if (!rc && hipHostMalloc((void **)&w->h_small, 64) != hipSuccess) rc = fail(SWPS_E_OOM, "pinned alloc");
@@ -2833,8 +3102,15 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
       A[k] = lcg_jump(1, k, kLcgA, kLcgC) - lcg_jump(0, k, kLcgA, kLcgC);
       C[k] = lcg_jump(0, k, kLcgA, kLcgC);
     }
+    uint64_t PA[64], PC[64];  // jumps by 2^i draws
+    for (int i = 0; i < 64; i++) {
+      PA[i] = lcg_jump(1, 1ULL << i, kLcgA, kLcgC) - lcg_jump(0, 1ULL << i, kLcgA, kLcgC);
+      PC[i] = lcg_jump(0, 1ULL << i, kLcgA, kLcgC);
+    }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_jumpA), A, sizeof(A)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_jumpC), C, sizeof(C)) != hipSuccess)
+        hipMemcpyToSymbol(HIP_SYMBOL(c_jumpC), C, sizeof(C)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_p2A), PA, sizeof(PA)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_p2C), PC, sizeof(PC)) != hipSuccess)
       rc = fail(SWPS_E_HIP, "constant upload");
   }
   if (rc) {
@@ -3023,16 +3299,9 @@ int swps_w2v_init(swps_w2v *w) {
   SWPS_TRY(table_find_or_insert(w->t, dk.as<uint64_t>(), V, w->d_vid_row.as<uint32_t>(), w->s));
   if (w->cfg.init_mode == SWPS_W2V_INIT_REF) {
     // Vec::randInit (vec1.h:229-232): (rand()/(float)RAND_MAX - 0.5)/D, h then
-    // v per key, keys in _local_keys order, after rand_offset earlier calls.
-    GlibcRand r(w->cfg.rand_seed);
-    for (uint64_t i = 0; i < w->cfg.rand_offset; i++) (void)r.next();
-    const int D = w->D;
-    std::vector<double> hv(V * 2 * D);
-    for (uint64_t i = 0; i < V * 2 * D; i++) {
-      float x = r.next() / (float)2147483647;
-      hv[i] = ((double)x - 0.5) / (double)(size_t)D;
-    }
-    SWPS_TRY(w->f64 ? set_hv<double>(w, hv.data()) : set_hv<float>(w, hv.data()));
+    // v per key, keys in _local_keys order, after rand_offset earlier calls —
+    // generated on the GPU by jump-ahead (rand_init_gpu)
+    SWPS_TRY(w->f64 ? rand_init_gpu<double>(w) : rand_init_gpu<float>(w));
   } else {
     SWPS_TRY(w->f64 ? pull_all<double>(w) : pull_all<float>(w));
   }

@@ -95,17 +95,33 @@ def test_analogy_accuracy_sharded(lib, gpu, gloo1, corpus, reference_acc):
     assert accs[False] > 0.8 and accs[False] == acc1
 
 
-def test_analogy_accuracy_alias_sampler(lib, gpu, corpus, reference_acc):
-    """The alias sampler draws other words than the reference's table (same
-    distribution): the learnt structure matches the reference's accuracy."""
-    path, qs, words = corpus
+def test_analogy_accuracy_alias_sampler(lib, gpu, oracle_mod, tmp_path):
+    """The alias sampler draws other words than the reference's table (the
+    same unigram^0.75 distribution), so a single corpus compares two random
+    draws: the seed-to-seed spread of the reference itself is ~1 pt here.
+    Over three planted-analogy corpora (different seeds) the mean accuracy
+    must match the reference's mean within 0.5 pt (north star)."""
+    from swiftmpi_amd.synth import analogy_corpus
+    ref, ali = [], []
     kw = dict(window=W, negative=N, minibatch=B, sample=SAMPLE, unigram_size=10 ** 7, fp64_intermediates=False)
-    t = lib.Table("w2v", dim=D, capacity=4096, dtype="f32", learning_rate=LR)
-    w = lib.Word2Vec(t, init="ref", sampler="alias", **kw)
-    w.load_text(path)
-    w.init()
-    w.train(EPOCHS)
-    vk, _ = w.vocab()
-    acc = accuracy(w.get_params(), vk, lib.bkdr, qs, words)
-    print("analogy accuracy: reference %.4f  gpu fast + alias sampler %.4f" % (reference_acc, acc))
-    assert abs(acc - reference_acc) <= 0.01
+    for seed in (11, 12, 13):
+        path = str(tmp_path / ("a%d.txt" % seed))
+        qs = analogy_corpus(path, lines=2000, seed=seed)
+        words = sorted({x for q in qs for x in q})
+        o = oracle_mod.W2V(path, D, window=W, negative=N, minibatch=B, sample=SAMPLE, table_size=10 ** 7, lr=LR,
+                           alpha=0.05)
+        o.init_rand(1, 2)
+        o.train(EPOCHS)
+        vk, _ = o.vocab()
+        ref.append(accuracy(o.get_params(), vk, oracle_mod.bkdr, qs, words))
+        t = lib.Table("w2v", dim=D, capacity=4096, dtype="f32", learning_rate=LR)
+        w = lib.Word2Vec(t, init="ref", sampler="alias", **kw)
+        w.load_text(path)
+        w.init()
+        w.train(EPOCHS)
+        vk, _ = w.vocab()
+        ali.append(accuracy(w.get_params(), vk, lib.bkdr, qs, words))
+    print("analogy accuracy per seed: reference %s  alias %s  means %.4f / %.4f"
+          % (np.round(ref, 4), np.round(ali, 4), np.mean(ref), np.mean(ali)))
+    assert min(ref) > 0.8
+    assert abs(np.mean(ali) - np.mean(ref)) <= 0.005

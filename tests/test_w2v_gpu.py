@@ -424,3 +424,22 @@ def test_overlapped_driver_bit_identical(lib, gpu, monkeypatch, dtype, fp64i):
                                                         "pulled", "pushed")}))
     assert res[0][1] == res[1][1]
     assert np.array_equal(res[0][0], res[1][0])
+
+
+def test_specialised_records_kernel_bit_identical(lib, gpu, tmp_path, monkeypatch):
+    """k_records_t<5, 5> (the W = 5, N = 5 table-sampler path: independent
+    loads batched, per-bit LCG jump constants) writes exactly what the
+    generic k_records writes: same negatives, same trained rows."""
+    path = zipf_corpus(str(tmp_path / "c.txt"), 150, 400, seed=23)
+    outs = []
+    for generic in ("1", "0"):
+        monkeypatch.setenv("SWPS_REC_GENERIC", generic)
+        t = lib.Table("w2v", dim=16, capacity=1000, dtype="f64", learning_rate=0.7)
+        w = lib.Word2Vec(t, window=5, negative=5, minibatch=17, sample=1e-3, unigram_size=10 ** 6)
+        w.load_text(path)
+        w.init()
+        w.trace_negatives(100000)
+        w.train(2)
+        outs.append((w.negatives(100000), w.get_params(), w.stats()["lstate"]))
+    assert np.array_equal(outs[0][0], outs[1][0]) and len(outs[0][0]) > 0
+    assert np.array_equal(outs[0][1], outs[1][1]) and outs[0][2] == outs[1][2]
