@@ -12,8 +12,10 @@ gradients with AdaGrad — all on the GPU through libswps.so.
 N > 1: every rank trains its own corpus of the same size (the reference's
 per-rank local data) and serves the keys BasicHashFrag assigns to it; each
 minibatch pulls rows from and pushes mean gradients to the owning GPUs with
-RCCL all-to-all-v (swiftmpi_amd/dist.py).  Weak scaling.  Rank 0 prints one
-JSON line.
+RCCL all-to-all-v issued by the library itself (swps_w2v_shard_comm; its RCCL
+id bootstrapped over TCP at MASTER_ADDR:MASTER_PORT+1), or with
+--driver python by swiftmpi_amd/dist.py over torch.distributed.  Weak
+scaling.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -178,6 +180,9 @@ def main():
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--frag-num", type=int, default=1000)
     ap.add_argument("--sharded", action="store_true", help="use the key-sharded multi-GPU path even at N=1")
+    ap.add_argument("--driver", default="native", choices=["python", "native"],
+                    help="sharded exchange: swiftmpi_amd/dist.py over torch.distributed, or the library's own "
+                         "(swps_w2v_shard_comm over RCCL / its TCP transport)")
     ap.add_argument("--pipeline", action="store_true",
                     help="sharded path: the bounded-staleness driver (pull(i+1)/push(i) overlap learn(i)) instead "
                          "of the default lockstep pull/learn/push order (exact reference semantics)")
@@ -237,13 +242,26 @@ def main():
             dist.barrier()
 
     setup_s = {}
+    _comm = []
+
+    def native_comm():  # one communicator per process, reused by every leg
+        if not _comm:
+            from swiftmpi_amd.comm import Comm
+            port = int(os.environ.get("MASTER_PORT", "29533")) + 1
+            addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+            _comm.append(Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
+                         else Comm.tcp(rank, world, local, addr=addr, port=port))
+        return _comm[0]
 
     def build(fp64_intermediates, minibatch=None):
         kw = dict(window=args.window, negative=args.negative, minibatch=minibatch or args.minibatch, sample=args.sample,
                   alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates, sampler=args.sampler)
         t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
                      device=local, init="hash", seed=1)
-        if sharded:  # key-sharded over the ranks (BasicHashFrag), RCCL all-to-all per minibatch
+        if sharded and args.driver == "native":  # the library's own exchange
+            from swiftmpi_amd.dist import NativeShardedWord2Vec
+            w = NativeShardedWord2Vec(t, native_comm(), frag_num=args.frag_num, **kw)
+        elif sharded:  # key-sharded over the ranks (BasicHashFrag), RCCL all-to-all per minibatch
             from swiftmpi_amd.dist import ShardedWord2Vec
             w = ShardedWord2Vec(t, frag_num=args.frag_num, pipeline=pipelined, **kw)
         else:
@@ -414,7 +432,9 @@ def main():
                                                                   args.line_len),
                    "global_batch": args.minibatch * world,
                    "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num %d), %s all-to-all-v, %s"
-                                   % (world, args.frag_num, "RCCL" if backend == "nccl" else "gloo",
+                                   % (world, args.frag_num,
+                                      ("library-issued RCCL" if backend == "nccl" else "library TCP transport")
+                                      if args.driver == "native" else ("RCCL" if backend == "nccl" else "gloo"),
                                       "pipelined: pull(i+1)/push(i) overlap learn(i), staleness 1" if pipelined
                                       else "lockstep pull/learn/push"))
                    if sharded else "1 GPU, one HBM shard",

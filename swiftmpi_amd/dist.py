@@ -487,3 +487,53 @@ class ShardedLR(_ShardedApp):
         kt = torch.as_tensor(keys.astype(np.int64), device=self.dev)
         rows = self.table.export(kt).cpu().numpy().reshape(len(keys), 2)
         return keys, rows[:, 0].copy(), rows[:, 1].copy()
+
+
+class NativeShardedWord2Vec:
+    """The library-driven sharded loop (swps_w2v_shard_comm, src/swps_driver.cpp)
+    behind ShardedWord2Vec's interface (what bench.py --driver native uses):
+    the library issues the three all-to-all-v per minibatch itself over its
+    own communicator — RCCL when every rank has its own GPU, its TCP
+    transport when ranks share one."""
+
+    def __init__(self, table, comm, frag_num=1000, **kw):
+        kw.setdefault("init", "table")
+        self.w = Word2Vec(table, **kw)
+        self.table, self.comm, self.frag_num = table, comm, frag_num
+
+    def load_tokens(self, word_ids, line_off, word_keys):
+        self.w.load_tokens(word_ids, line_off, word_keys)
+        self.w.shard_comm(self.comm, self.frag_num)
+
+    def load_text(self, path):
+        self.w.load_text(path)
+        self.w.shard_comm(self.comm, self.frag_num)
+
+    def init(self):
+        self.w.init()
+
+    def train_batches(self, n):
+        self.w.train_batches(n)
+
+    train_steps = train_batches
+
+    def sync(self):
+        self.w.sync()
+
+    def stats(self):
+        return self.w.stats()
+
+    def info(self):
+        return self.w.info()
+
+    def kernel_times(self, reset=False):
+        return self.w.kernel_times(reset)
+
+    def set_profile(self, on):
+        self.w.set_profile(on)
+
+    def set_exchange_profile(self, on):
+        self.w.exchange_stats(on=1 if on else 0)
+
+    def exchange_stats(self):
+        return self.w.exchange_stats()
