@@ -249,8 +249,16 @@ def main():
             from swiftmpi_amd.comm import Comm
             port = int(os.environ.get("MASTER_PORT", "29533")) + 1
             addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-            _comm.append(Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
-                         else Comm.tcp(rank, world, local, addr=addr, port=port))
+            try:
+                c = (Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
+                     else Comm.tcp(rank, world, local, addr=addr, port=port))
+                ok = 1
+            except Exception as e:  # noqa: BLE001 — reported, and every rank falls back together
+                print("native communicator failed on rank %d: %s" % (rank, e), file=sys.stderr, flush=True)
+                c, ok = None, 0
+            t = torch.tensor([ok], dtype=torch.int32, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            _comm.append(c if int(t.item()) else None)
         return _comm[0]
 
     def build(fp64_intermediates, minibatch=None):
@@ -258,7 +266,7 @@ def main():
                   alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates, sampler=args.sampler)
         t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
                      device=local, init="hash", seed=1)
-        if sharded and args.driver == "native":  # the library's own exchange
+        if sharded and args.driver == "native" and native_comm() is not None:  # the library's own exchange
             from swiftmpi_amd.dist import NativeShardedWord2Vec
             w = NativeShardedWord2Vec(t, native_comm(), frag_num=args.frag_num, **kw)
         elif sharded:  # key-sharded over the ranks (BasicHashFrag), RCCL all-to-all per minibatch
@@ -434,7 +442,8 @@ def main():
                    "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num %d), %s all-to-all-v, %s"
                                    % (world, args.frag_num,
                                       ("library-issued RCCL" if backend == "nccl" else "library TCP transport")
-                                      if args.driver == "native" else ("RCCL" if backend == "nccl" else "gloo"),
+                                      if args.driver == "native" and _comm and _comm[0] is not None
+                                      else ("RCCL" if backend == "nccl" else "gloo"),
                                       "pipelined: pull(i+1)/push(i) overlap learn(i), staleness 1" if pipelined
                                       else "lockstep pull/learn/push"))
                    if sharded else "1 GPU, one HBM shard",
@@ -531,7 +540,27 @@ def bench_other(args):
         y, off, f, v = criteo(rows, seed=3 + rank)
         lr_rate = args.lr if args.lr != 0.7 else 0.05
         t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=lr_rate, init="hash", seed=1, device=local)
-        if dist is not None:
+        comm = None
+        if dist is not None and args.driver == "native":  # the library issues the exchange
+            from swiftmpi_amd.comm import Comm
+            port = int(os.environ.get("MASTER_PORT", "29533")) + 1
+            addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+            try:
+                comm = (Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
+                        else Comm.tcp(rank, world, local, addr=addr, port=port))
+            except Exception as e:  # noqa: BLE001 — every rank falls back to the Python driver together
+                print("native communicator failed on rank %d: %s" % (rank, e), file=sys.stderr, flush=True)
+            ok = torch.tensor([int(comm is not None)], dtype=torch.int32, device="cuda")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if not int(ok.item()):
+                comm = None
+        if comm is not None:
+            m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
+            m.load_csr(y, off, f, v)
+            m.shard_comm(comm, frag_num=2000)
+            m.init()
+            run = m.train_batches
+        elif dist is not None:
             from swiftmpi_amd.dist import ShardedLR
             m = ShardedLR(t, frag_num=2000, minibatch=args.lr_batch, profile=False, fast_sums=not args.lr_exact)
             m.load_csr(y, off, f, v)
@@ -569,7 +598,8 @@ def bench_other(args):
                "config": {"workload": "sparse logistic regression (BASELINE config 3 shape), 39 features/row, "
                                       "2^24 hashed feature space, %d rows per GPU per minibatch, AdaGrad lr %g"
                                       % (B1, lr_rate),
-                          "parallelism": ("key-sharded PS over %d GPU(s), %s all-to-all-v" % (world, backend))
+                          "parallelism": ("key-sharded PS over %d GPU(s), %s all-to-all-v%s"
+                                          % (world, backend, ", library-issued" if comm is not None else ""))
                           if dist is not None else "1 GPU, one HBM shard",
                           "mode": "exact (sequential fp32 per-key sums, bit-exact with the reference)" if args.lr_exact
                           else "fast (fp64 per-key sums, wave tree-reduced; within 1e-5 of the oracle)",

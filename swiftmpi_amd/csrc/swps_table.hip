@@ -560,7 +560,13 @@ int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
   t->nslots = ns;
   t->mask = ns - 1;
   int rc = SWPS_OK;
-  if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) rc = fail(SWPS_E_HIP, "stream");
+  // the shard's stream (every app context's compute stream) at the highest priority, so helper streams
+  // (the overlapped prep, RCCL exchanges) yield CUs to it (SWPS_TABLE_PRIO=0: default priority, A/B)
+  int plo = 0, phi = 0;
+  const char *pe = getenv("SWPS_TABLE_PRIO");
+  if (hipDeviceGetStreamPriorityRange(&plo, &phi) != hipSuccess) plo = phi = 0;
+  if (pe && atoi(pe) == 0) phi = 0;
+  if (hipStreamCreateWithPriority(&t->stream, hipStreamNonBlocking, phi) != hipSuccess) rc = fail(SWPS_E_HIP, "stream");
   if (!rc) rc = t->keys.ensure(ns * 8);
   if (!rc) rc = t->slot_row.ensure(ns * 4);
   if (!rc) rc = t->row_key.ensure(cfg->capacity * 8);

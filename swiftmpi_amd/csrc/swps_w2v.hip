@@ -1531,8 +1531,11 @@ struct swps_w2v {
   static constexpr int kPrepBufs = 13;
   DevMem alt[kPrepBufs];
   bool alt_local_ready = false;
-  int overlap = 0;  // SWPS_OVERLAP=1: train_overlapped (same-box A/B: 4.25e8 sequential vs 4.24e8 / 4.02e8
-                    // overlapped — forward and gather already fill every CU and the HBM, so prep only stretches)
+  // train_overlapped: -1 = auto (on for minibatches of at most kOverlapTok tokens: at B = 100 lines the
+  // prep chain — records, sort, index: ~12 short latency-bound launches — hides behind the learn, 0.41 ->
+  // 0.36 ms/step; at B = 5000 forward and gather already fill every CU and the HBM: 4.25e8 sequential vs
+  // 4.24e8 / 4.02e8 overlapped); SWPS_OVERLAP=0/1 forces it
+  int overlap = -1;
   hipStream_t s_prep = nullptr;
   hipEvent_t ev_learn = nullptr, ev_prep = nullptr;
   DevMem *prep_set[kPrepBufs] = {&d_pos_tok, &d_rec,  &d_pkeys, &d_pvals, &d_pkeys_s, &d_pvals_s, &d_tmp,
@@ -2535,6 +2538,7 @@ template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A>
     k_push<T, A, NCH, false><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
 }
 constexpr uint32_t kChunk = 128;
+constexpr uint64_t kOverlapTok = 1000000;  // auto-overlap threshold (tokens per minibatch)
 
 // Subsample masks and main-LCG offsets for a whole epoch.  They depend only on
 // the two RNG streams (the float LCG advances one draw per processed token,
@@ -3020,7 +3024,15 @@ void swap_prep_set(swps_w2v *w) {
 // is left prepared when the call returns.
 template <typename T, typename A> int train_overlapped(swps_w2v *w, uint64_t count) {
   if (!w->s_prep) {
-    SWPS_HIP(hipStreamCreateWithFlags(&w->s_prep, hipStreamNonBlocking));
+    // the prep stream at the lowest priority: its short kernels fill the gaps the learn kernels leave
+    // instead of competing with them for CUs (SWPS_PREP_PRIO=0: default priority, A/B)
+    int lo = 0, hi = 0;
+    SWPS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const char *pe = getenv("SWPS_PREP_PRIO");
+    if (pe && atoi(pe) == 0)
+      SWPS_HIP(hipStreamCreateWithFlags(&w->s_prep, hipStreamNonBlocking));
+    else
+      SWPS_HIP(hipStreamCreateWithPriority(&w->s_prep, hipStreamNonBlocking, lo));
     SWPS_HIP(hipEventCreateWithFlags(&w->ev_learn, hipEventDisableTiming));
     SWPS_HIP(hipEventCreateWithFlags(&w->ev_prep, hipEventDisableTiming));
   }
@@ -3317,7 +3329,8 @@ int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
   }
   if (w->sharded) return fail(SWPS_E_STATE, "sharded context: drive it with request / serve_pull / step / serve_push");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
-  if (w->overlap && count > 1 && !w->cfg.minibatch_vocab && w->trace.size() >= w->trace_cap && !w->pb.valid) {
+  const bool ov = w->overlap > 0 || (w->overlap < 0 && w->max_tok <= kOverlapTok);
+  if (ov && count > 1 && !w->cfg.minibatch_vocab && w->trace.size() >= w->trace_cap && !w->pb.valid) {
     if (w->f64) return train_overlapped<double, double>(w, count);
     if (w->cfg.fp64_intermediates) return train_overlapped<float, double>(w, count);
     return train_overlapped<float, float>(w, count);
