@@ -37,7 +37,7 @@ def make_corpus(tokens, vocab, line_len, seed):
     """Zipf(s=1) over `vocab` word ids, `tokens` tokens in lines of `line_len`
     (the synthetic text8 stand-in)."""
     from swiftmpi_amd.synth import zipf_tokens
-    return zipf_tokens(tokens, vocab, line_len, seed)
+    return zipf_tokens(tokens, vocab, line_len, seed, progress=tokens > (1 << 26))
 
 
 def word_keys(lib, vocab):
@@ -234,6 +234,7 @@ def main():
         torch.cuda.set_device(local)
 
     ids, off = make_corpus(args.tokens, args.vocab, args.line_len, seed=8 + rank)
+    print("corpus: %d tokens" % len(ids), file=sys.stderr, flush=True)
     keys = word_keys(sw, args.vocab)
 
     def barrier():
@@ -617,11 +618,11 @@ def bench_other(args):
     else:
         from swiftmpi_amd.synth import zipf_tokens
         V, D = 1000000, args.dim
-        nd = args.s2v_docs * (2 * steps + warm)
+        nd = args.s2v_docs * (steps + warm)  # the profiled pass wraps to the corpus start
         rng = np.random.default_rng(5 + rank)
         lens = rng.integers(50, 201, nd)
         off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
-        ids, _ = zipf_tokens(int(off[-1]), V, 100, seed=5 + rank)
+        ids, _ = zipf_tokens(int(off[-1]), V, 100, seed=5 + rank, progress=True)
         toks = ids.astype(np.uint64) + 1
         sent = (np.arange(nd, dtype=np.uint64) + np.uint64(nd * rank + 1)) * np.uint64(2654435761)
         t = sw.Table("w2v", dim=D, capacity=V + 1024, dtype="f32", init="hash", seed=3, device=local)

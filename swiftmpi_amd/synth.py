@@ -4,9 +4,11 @@ generation only — nothing in this module is on the compute path."""
 import numpy as np
 
 
-def zipf_tokens(tokens, vocab, line_len, seed, s=1.0):
+def zipf_tokens(tokens, vocab, line_len, seed, s=1.0, progress=False):
     """Zipf(s) over `vocab` word ids, `tokens` tokens in lines of `line_len`
-    (config 1/2/4: the text8 stand-in).  Returns (ids uint32, line_off uint64)."""
+    (config 1/2/4: the text8 stand-in).  Returns (ids uint32, line_off uint64).
+    progress: a line on stderr per 16M tokens (long generations stay visibly alive)."""
+    import sys
     rng = np.random.default_rng(seed)
     cdf = np.cumsum(1.0 / np.arange(1, vocab + 1) ** s)
     cdf /= cdf[-1]
@@ -15,6 +17,8 @@ def zipf_tokens(tokens, vocab, line_len, seed, s=1.0):
     for a in range(0, tokens, step):
         b = min(tokens, a + step)
         ids[a:b] = np.minimum(np.searchsorted(cdf, rng.random(b - a), side="right"), vocab - 1)
+        if progress:
+            print("synth: %d / %d tokens" % (b, tokens), file=sys.stderr, flush=True)
     off = np.arange(0, tokens, line_len, dtype=np.uint64)
     off = np.append(off, np.uint64(tokens))
     return ids, off
