@@ -7,6 +7,8 @@
 // path is switched off (MergeSortLimit = 0; inputs that fit one block still
 // get the single-block sort).  Same stable order, so same results.
 #pragma once
+#include <cstdlib>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 namespace swps {
@@ -14,10 +16,37 @@ namespace swps {
 using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                rocprim::default_config, 0>;
 
-// tmp == nullptr: *bytes = the temporary storage needed
+// Wider digits for 17-20-bit keys: the bench minibatch's local key indices
+// (U ~ 2^18) sort in 2 onesweep passes of 9 bits instead of 3 of 8 (same
+// stable order, so same results).  Block shape of rocPRIM's gfx950 default.
+template <unsigned RB>
+using OnesweepWide = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, RB,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+
+// tmp == nullptr: *bytes = the temporary storage needed (same `bits` for both calls)
+inline bool sort_wide() {  // SWPS_SORT_WIDE=0: the default 8-bit digits only (A/B, tests)
+  static const bool on = [] {
+    const char *e = getenv("SWPS_SORT_WIDE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <typename K, typename V>
 inline hipError_t sort_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, const V *vin, V *vout, uint64_t n,
                              int bits, hipStream_t s) {
+  if (!sort_wide())
+    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
+                                                  s);
+  if (sizeof(K) == 4 && sizeof(V) == 4 && bits > 16 && bits <= 18)
+    return rocprim::radix_sort_pairs<OnesweepWide<9>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
+                                                      s);
+  if (sizeof(K) == 4 && sizeof(V) == 4 && bits > 18 && bits <= 20)
+    return rocprim::radix_sort_pairs<OnesweepWide<10>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                       (unsigned)bits, s);
   return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);
 }
 

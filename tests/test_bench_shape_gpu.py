@@ -165,3 +165,26 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode):
     print("single batch D=%d %s: max rel %.3g (median %.3g) over %d elements"
           % (D, mode, rel.max(), np.median(rel), rel.size))
     assert rel.max() <= (1e-5 if mode == "parity" else FAST_TOL_BATCH), float(rel.max())
+
+
+def test_wide_digit_sort_bit_identical_at_bench_scale(lib, gpu, monkeypatch):
+    """The bench corpus's minibatch key indices need 18 bits: they sort in two
+    9-bit onesweep passes (swps_sort.h) instead of three 8-bit ones.  Same
+    stable order: three 5000-line batches train to the same bits either way."""
+    res = []
+    for wide in ("0", "1"):
+        monkeypatch.setenv("SWPS_SORT_WIDE", wide)
+        import subprocess
+        import sys
+        code = ("import sys, numpy as np; sys.path.insert(0, %r); import swiftmpi_amd as sw; "
+                "from swiftmpi_amd.synth import zipf_tokens; ids, off = zipf_tokens(17005207, 253854, 1000, seed=8); "
+                "keys = np.array([sw.bkdr('w%%d' %% i) for i in range(253854)], dtype=np.uint64); "
+                "t = sw.Table('w2v', dim=300, capacity=260000, dtype='f32', init='hash', seed=1); "
+                "w = sw.Word2Vec(t, minibatch=5000, sample=1e-5, init='table', fp64_intermediates=False); "
+                "w.load_tokens(ids, off, keys); w.init(); w.train_batches(3); p = w.get_params(); "
+                "import hashlib; print('H', hashlib.sha256(p.tobytes()).hexdigest(), w.stats()['pairs'])"
+                % str(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))))
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append([l for l in r.stdout.splitlines() if l.startswith("H ")][-1])
+    assert res[0] == res[1], res
