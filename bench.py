@@ -304,12 +304,12 @@ def main():
     w.set_profile(True)                     # a second, profiled pass for the per-kernel roofline
     w.kernel_times(reset=True)
     gw = getattr(w, "w", w)                 # the per-rank Word2Vec (sharded: its learner)
-    g0 = gw.gather_stats()
+    g0 = gw.sum_stats()
     if sharded:
         w.set_exchange_profile(True)
     dpt, dp = timed(w, args.steps)
     kt = w.kernel_times()
-    g1 = gw.gather_stats()
+    g1 = gw.sum_stats()
     xs = w.exchange_stats() if sharded else None
     w.set_profile(False)
     if sharded:
@@ -333,14 +333,31 @@ def main():
     fwd_ms, fwd_n = kt["forward"]
     fwd_bytes = es * D * (ctx_rows + tgt_rows) + 2 * ea * D * dp["kept"]
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
-    # the dominant kernel by time: the segmented gradient sums (k_gather_t + k_combine
-    # under one timer).  Algorithmic bytes: each gradient record reads its source row
-    # (neu1 or neu1e of its position, D·ea) and its 4-B record index; each item (chunk of
-    # <= 128 records of one key) writes one partial row (D·ea) and reads a 16-B descriptor.
+    # the dominant kernel by time: the segmented gradient sums + AdaGrad push.
+    # Algorithmic bytes: each gradient record reads its source row (neu1 or neu1e of its
+    # position, D·ea) and its 4-B record index; each item (chunk of <= 128 records of one
+    # key) that goes through a partial writes it (D·ea + a 16-B descriptor read) and the
+    # push reads it back (D·ea); each pushed key reads h,v,h2,v2 (4·D·es), writes them
+    # (4·D·es) and its pre-update h,v to the worker cache (2·D·es) + 8 B of bounds.
+    # Fused push (k_push_tg, the fast-mode default): k_gather_t + k_combine sum only the
+    # multi-chunk runs, k_push_tg sums the single-chunk runs itself -> the group is
+    # k_gather_t + k_combine + k_push_tg, timed by the gather and push timers.
+    # Otherwise the group is k_gather_t + k_combine alone (the push is reported below).
     g_rec, g_items = g1["records"] - g0["records"], g1["items"] - g0["items"]
+    g_mrec, g_mitems = g1["multi_records"] - g0["multi_records"], g1["multi_items"] - g0["multi_items"]
+    fused = g1["batches"] > g0["batches"] and g1["fused"] - g0["fused"] == g1["batches"] - g0["batches"]
     gat_ms, gat_n = kt["gather"]
-    gat_bytes = g_rec * (D * ea + 4) + g_items * (D * ea + 16)
-    gat_gbs = gat_bytes / (gat_ms * 1e-3) / 1e9 if gat_ms > 0 else 0.0
+    push_ms, push_n = kt.get("push", (0.0, 0))
+    if fused:
+        sum_kernel = "k_gather_t + k_combine + k_push_tg (segmented gradient sums + fused AdaGrad push)"
+        gat_bytes = (g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) +
+                     dp["pushed"] * (10 * es * D + 8))
+        sum_ms = gat_ms + push_ms
+    else:
+        sum_kernel = "k_gather_t + k_combine (segmented gradient sums)"
+        gat_bytes = g_rec * (D * ea + 4) + g_items * (D * ea + 16)
+        sum_ms = gat_ms
+    gat_gbs = gat_bytes / (sum_ms * 1e-3) / 1e9 if sum_ms > 0 else 0.0
     # whole step (§8(d) full formula): rows read + gradients written + pull 16D/key + push (40D+8)/key
     step_bytes = (2 * es * D * (dp["ctx_rows"] + dp["tgt_rows"]) + d["pulled"] * 4 * es * D +
                   d["pushed"] * (10 * es * D + 8))
@@ -356,7 +373,7 @@ def main():
     pp = {}
     for name, nbytes in (("pull", dp["pulled"] * 4 * es * D), ("push", dp["pushed"] * (12 * es * D + 8))):
         ms, n = kt.get(name, (0.0, 0))
-        if ms > 0 and not sharded:
+        if ms > 0 and not sharded and not (fused and name == "push"):
             gbs = nbytes / (ms * 1e-3) / 1e9
             pp[name] = {"GBps": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": nbytes / max(n, 1),
                         "avg_launch_ms": ms / max(n, 1)}
@@ -386,11 +403,11 @@ def main():
     if os.path.exists(pmc) and not parity_main:
         prof = json.load(open(pmc))
         if {k: prof.get("config", {}).get(k) for k in mine} == mine:
-            gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items()
-                  if k.startswith("k_gather") or k.startswith("k_combine")]
-            if gt:  # per gather-timer launch: k_gather_t + k_combine
-                traffic = sum(gt)
-                traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch, k_gather_t + k_combine)" % pmc_name
+            grp = ("k_gather", "k_combine") + (("k_push_tg",) if fused else ())
+            gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items() if k.startswith(grp)]
+            if gt and (not fused or any(k.startswith("k_push_tg") for k in prof["kernels"])):
+                traffic = sum(gt)  # per step: one launch of each kernel of the group
+                traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch, %s)" % (pmc_name, " + ".join(grp))
             for k, v in prof["kernels"].items():
                 if k.startswith("k_forward"):
                     fwd_traffic = v["hbm_bytes_corrected"]
@@ -451,13 +468,16 @@ def main():
                    "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"],
                    "pulled_keys_per_step": d["pulled"] / args.steps,
                    "setup_s": dict(setup_s)},
-        "roofline": {"bound": "hbm", "kernel": "k_gather_t + k_combine (segmented gradient sums)",
+        "roofline": {"bound": "hbm", "kernel": sum_kernel,
                      "achieved": gat_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": gat_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "bytes_per_launch": gat_bytes / max(gat_n, 1), "avg_launch_ms": gat_ms / max(gat_n, 1),
+                     "bytes_per_launch": gat_bytes / max(gat_n, 1), "avg_launch_ms": sum_ms / max(gat_n, 1),
                      "launches": gat_n, "records_per_launch": g_rec / max(gat_n, 1),
                      "items_per_launch": g_items / max(gat_n, 1),
+                     "partial_items_per_launch": (g_mitems if fused else g_items) / max(gat_n, 1),
+                     "gather_ms_per_launch": gat_ms / max(gat_n, 1),
+                     "push_ms_per_launch": push_ms / max(push_n, 1),
                      # k_forward: its row-occurrence bytes exceed its HBM traffic (hot Zipf rows
                      # hit in L2/MALL), so its "achieved" can pass the HBM peak; hbm_GBps is the
                      # PMC-measured HBM rate of the same launches

@@ -357,6 +357,14 @@ class Word2Vec:
         check(capi.lib().swps_w2v_gather_stats(self.h, ptr(o)))
         return {"records": int(o[0]), "items": int(o[1])}
 
+    def sum_stats(self):
+        """Cumulative gradient-sum work split by kernel: all records / items, the
+        multi-chunk runs' records / items (k_gather_t's share when the push is fused),
+        fused pushes and batches with sums."""
+        o = np.zeros(6, dtype=np.uint64)
+        check(capi.lib().swps_w2v_sum_stats(self.h, ptr(o)))
+        return dict(zip(["records", "items", "multi_records", "multi_items", "fused", "batches"], [int(x) for x in o]))
+
     def get_params(self):
         V = self.info()["vocab"]
         out = np.zeros((V, 4 * self.dim), dtype=np.float64)

@@ -117,6 +117,7 @@ PROTOS = {
     "swps_w2v_sync": (ctypes.c_int, [_p]),
     "swps_w2v_stats": (ctypes.c_int, [_p, _p]),
     "swps_w2v_gather_stats": (ctypes.c_int, [_p, _p]),
+    "swps_w2v_sum_stats": (ctypes.c_int, [_p, _p]),
     "swps_w2v_get_params": (ctypes.c_int, [_p, _p]),
     "swps_w2v_set_params": (ctypes.c_int, [_p, _p]),
     "swps_w2v_unigram_at": (ctypes.c_int, [_p, _p, _u64, _p]),

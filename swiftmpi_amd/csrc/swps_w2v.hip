@@ -926,18 +926,55 @@ constexpr uint32_t kGroupDesc = 16;  // = kGroup (k_combine's group size)
 // item descriptors {first record, end record | kind << 31, (key, kind) index j, chunk}:
 // one thread per item (hot keys have thousands of chunks), j found by binary
 // search over the item offsets ioff[0..2U].
+struct MultiOrder {  // k_item_desc: sort keys of the multi-chunk items by their first record's position
+  uint32_t *key, *item;  // [max_items]: coarse position (kMultiPad for the rest) and item index; null = unsorted
+  const uint32_t *vals;  // the sorted records
+  uint32_t P;
+  uint64_t HOFF;
+  int shift;  // coarse position = p >> shift (< kMultiPad)
+};
+constexpr uint32_t kMultiPad = 0xFFFFu;  // 16-bit sort keys: items outside the multi list sort last
+
 __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__restrict__ ioff, uint32_t U,
-                            uint32_t CH, uint64_t max_items, uint4 *__restrict__ desc, uint32_t *__restrict__ lead) {
+                            uint32_t CH, uint64_t max_items, uint4 *__restrict__ desc, uint32_t *__restrict__ lead,
+                            uint32_t *__restrict__ multi, MultiOrder mo) {
   const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (item >= max_items || item >= ioff[2ull * U]) return;
+  const bool live = item < max_items && item < ioff[2ull * U];
   uint32_t lo = 0, hi = 2 * U;  // largest j with ioff[j] <= item
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (ioff[mid] <= item)
-      lo = mid;
-    else
-      hi = mid;
+  if (live)
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ioff[mid] <= item)
+        lo = mid;
+      else
+        hi = mid;
+    }
+  if (multi) {
+    // items of (key, kind) runs with more than one chunk, for k_gather_t when
+    // k_push_tg sums the single-chunk runs itself (list order is irrelevant:
+    // every item writes only its own partial slot); one atomic per wave
+    const bool m = live && ioff[lo + 1] - ioff[lo] > 1;
+    if (mo.key && item < max_items) {
+      uint32_t key = kMultiPad;
+      if (m) {  // the chunk's first record: index slot*P + p (v records after HOFF)
+        const uint32_t jj = lo, u = jj >> 1, kind = jj & 1, k = (uint32_t)item - ioff[jj];
+        const uint32_t pi = mo.vals[seg[(2 * kind) * U + u] + k * CH];
+        key = (uint32_t)((kind ? (uint64_t)pi - mo.HOFF : (uint64_t)pi) % mo.P) >> mo.shift;
+      }
+      mo.key[item] = key;
+      mo.item[item] = (uint32_t)item;
+    }
+    const uint64_t bal = __ballot(m);
+    if (bal) {
+      const int lane = threadIdx.x & 63;
+      const int first = __ffsll((long long)bal) - 1;
+      uint32_t base = 0;
+      if (lane == first) base = atomicAdd(&multi[0], (uint32_t)__popcll(bal));
+      base = (uint32_t)__shfl((int)base, first, 64);
+      if (m && !mo.key) multi[1 + base + (uint32_t)__popcll(bal & ((1ULL << lane) - 1))] = (uint32_t)item;
+    }
   }
+  if (!live) return;
   const uint32_t jj = lo, u = jj >> 1, kind = jj & 1, k = (uint32_t)item - ioff[jj];
   const uint32_t s = seg[(2 * kind) * U + u], e = seg[(2 * kind + 1) * U + u];
   const uint32_t cs = s + k * CH;
@@ -961,6 +998,7 @@ template <typename A> struct GatherArgs {
   int ld;  // neu1/neu1e row stride (FwdArgs::ld)
   const uint32_t *lead;  // hot-group leaders (k_item_desc): [0] = count, then items
   uint32_t max_items;    // capacity of desc / partial: a bound on ioff[2U] every reader clamps to
+  const uint32_t *multi;  // k_gather_t: only these items ([0] = count; the multi-chunk runs'), or null = all
 };
 
 // One wave per chunk of <= 128 records of one (key, kind): the fp64 sum, in
@@ -1057,29 +1095,34 @@ __device__ __forceinline__ uint4 uniform4(uint4 d) {  // wave-uniform value: kee
                     __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
 }
 
-__device__ __forceinline__ ItemRecs item_recs(const GatherArgs<float> &a, uint4 d, int lane) {
-  const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
+__device__ __forceinline__ ItemRecs run_recs(const uint32_t *vals, const float *pg, uint32_t P, uint64_t HOFF,
+                                             uint32_t s, uint32_t n, uint32_t kind, int lane) {
   ItemRecs r{0, 0, 1.f, 1.f};
   // records are slot-major: index = slot*P + p (v records after HOFF)
   if (lane < (int)n) {
-    const uint32_t pi = a.vals[s + lane];
+    const uint32_t pi = vals[s + lane];
     if (kind == 0) {
-      r.p0 = pi % a.P;
-      r.g0 = a.pg[pi];
+      r.p0 = pi % P;
+      r.g0 = pg[pi];
     } else {
-      r.p0 = (uint32_t)((pi - a.HOFF) % a.P);
+      r.p0 = (uint32_t)((pi - HOFF) % P);
     }
   }
   if (lane + 64 < (int)n) {
-    const uint32_t pi = a.vals[s + 64 + lane];
+    const uint32_t pi = vals[s + 64 + lane];
     if (kind == 0) {
-      r.p1 = pi % a.P;
-      r.g1 = a.pg[pi];
+      r.p1 = pi % P;
+      r.g1 = pg[pi];
     } else {
-      r.p1 = (uint32_t)((pi - a.HOFF) % a.P);
+      r.p1 = (uint32_t)((pi - HOFF) % P);
     }
   }
   return r;
+}
+
+__device__ __forceinline__ ItemRecs item_recs(const GatherArgs<float> &a, uint4 d, int lane) {
+  const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
+  return run_recs(a.vals, a.pg, a.P, a.HOFF, s, n, kind, lane);
 }
 
 // k_gather (fast mode) on FSlice rows, software-pipelined across items: most
@@ -1091,16 +1134,19 @@ template <int NCH, int UNR>
 __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
   const int lane = threadIdx.x & 63;
   const bool tl = 256 * NCH + lane < a.D;
-  const uint32_t NI = min(a.ioff[2 * a.U], a.max_items);
+  const uint32_t NI = min(a.multi ? a.multi[0] : a.ioff[2 * a.U], a.max_items);
   const uint32_t stride = gridDim.x * 4;
-  uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (item >= NI) return;
-  uint4 d = uniform4(a.desc[__builtin_amdgcn_readfirstlane(item)]);
+  uint32_t qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= NI) return;
+  auto item_at = [&](uint32_t q) { return a.multi ? a.multi[1 + __builtin_amdgcn_readfirstlane(q)] : q; };
+  uint32_t item = __builtin_amdgcn_readfirstlane(item_at(qi));
+  uint4 d = uniform4(a.desc[item]);
   ItemRecs ri = item_recs(a, d, lane);
   for (;;) {
-    const uint32_t nx = item + stride;
-    const bool more = nx < NI;
-    const uint4 dn = uniform4(more ? a.desc[__builtin_amdgcn_readfirstlane(nx)] : make_uint4(0, 0x80000000u, 0, 0));
+    const uint32_t qn = qi + stride;
+    const bool more = qn < NI;
+    const uint32_t nx = more ? __builtin_amdgcn_readfirstlane(item_at(qn)) : 0;
+    const uint4 dn = uniform4(more ? a.desc[nx] : make_uint4(0, 0x80000000u, 0, 0));
     const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
     const float *base = kind == 0 ? a.neu1 : a.neu1e;
     FAcc<NCH> acc;
@@ -1133,6 +1179,7 @@ __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
     if (n == 0) rn = item_recs(a, dn, lane);
     acc.st(a.partial + (uint64_t)item * a.D, lane, tl);
     if (!more) break;
+    qi = qn;
     item = nx;
     d = dn;
     ri = rn;
@@ -1190,6 +1237,13 @@ template <typename T, typename A> struct PushArgs {
   A *grads;  // TO_GRADS: mean gradients [U][2D] in the intermediate type (the push request payload)
   T *cache_h, *cache_v;  // direct table reads (single GPU): every pushed key's pre-update h, v rows go to
   int cs;                // the worker cache (the value its pull would have left there), row stride cs
+  // k_push_tg: the sorted records and the forward's rows, to sum single-chunk runs in place
+  const uint32_t *vals;
+  const float *pg;
+  const A *neu1, *neu1e;
+  uint64_t HOFF;
+  uint32_t P;
+  int ld;
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
@@ -1318,6 +1372,127 @@ __global__ __launch_bounds__(256) void k_push_t(PushArgs<float, float> a) {
 #pragma unroll
         for (int q = 0; q < PU; q++)
           if (it0 + q * stride < i1[half]) acc.add(pv[q], tl);
+      }
+      const double inv = (double)cnt[half];
+      float *w = row + half * D, *w2 = row + (2 + half) * D;
+      auto upd = [&](double sum, float wv, float w2v, float &wo, float &w2o) {
+        const double g = (double)(float)(sum / inv);  // the mean in the push payload's type
+        const double acc2 = (double)w2v + g * g;
+        const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
+        w2o = (float)acc2;
+        wo = (float)((double)wv + step);
+      };
+#pragma unroll
+      for (int c = 0; c < NCH; c++) {
+        float4 wo, w2o;
+        upd(acc.v[c][0], wr[half].v[c].x, w2r[half].v[c].x, wo.x, w2o.x);
+        upd(acc.v[c][1], wr[half].v[c].y, w2r[half].v[c].y, wo.y, w2o.y);
+        upd(acc.v[c][2], wr[half].v[c].z, w2r[half].v[c].z, wo.z, w2o.z);
+        upd(acc.v[c][3], wr[half].v[c].w, w2r[half].v[c].w, wo.w, w2o.w);
+        ((float4 *)w2)[lane + c * 64] = w2o;
+        ((float4 *)w)[lane + c * 64] = wo;
+      }
+      if (tl) {
+        float wo, w2o;
+        upd(acc.t, wr[half].t, w2r[half].t, wo, w2o);
+        w2[256 * NCH + lane] = w2o;
+        w[256 * NCH + lane] = wo;
+      }
+    }
+  }
+}
+
+// k_push_t with the gather of single-chunk runs folded in: a (key, kind) run of
+// at most kChunk records is summed here, straight from the forward's neu1 /
+// neu1e rows (the same fp64 sum in record order, rounded to the fp32 partial
+// it would have stored), so k_gather_t only runs the multi-chunk items and
+// the single-chunk partials are never written nor re-read.  Bit-identical to
+// k_gather_t + k_combine + k_push_t.
+template <int NCH, int UNR, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_push_tg(PushArgs<float, float> a) {
+  constexpr int PU = 8;
+  const int lane = threadIdx.x & 63;
+  const int D = a.D;
+  const bool tl = 256 * NCH + lane < D;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < a.U; u += (uint64_t)gridDim.x * 4) {
+    const int32_t vid = a.K[u];
+    if (lane == 0) a.local[vid] = -1;
+    const uint32_t sg[4] = {a.seg[0 * a.U + u], a.seg[1 * a.U + u], a.seg[2 * a.U + u], a.seg[3 * a.U + u]};
+    const uint32_t cnt[2] = {sg[1] - sg[0], sg[3] - sg[2]};
+    if (cnt[0] == 0 && cnt[1] == 0 && !a.cache_h) continue;
+    float *row = a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
+    uint32_t i0[2], i1[2];
+    bool one[2];
+    FSlice<NCH> wr[2], w2r[2], pf[2];
+    ItemRecs ri[2];
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      i0[half] = a.ioff[2 * u + half];
+      i1[half] = a.ioff[2 * u + half + 1];
+      one[half] = i1[half] - i0[half] == 1;
+      if (cnt[half] || a.cache_h) wr[half].ld(row + half * D, lane, tl);
+      if (cnt[half]) {
+        if (one[half])
+          ri[half] = run_recs(a.vals, a.pg, a.P, a.HOFF, sg[2 * half], cnt[half], half, lane);
+        else
+          pf[half].ld(a.partial + (uint64_t)i0[half] * D, lane, tl);
+        w2r[half].ld(row + (2 + half) * D, lane, tl);
+      }
+    }
+    if (a.cache_h) {  // the pulled (pre-update) value stays in the worker cache
+      wr[0].st(a.cache_h + (uint64_t)vid * a.cs, lane, tl);
+      wr[1].st(a.cache_v + (uint64_t)vid * a.cs, lane, tl);
+    }
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      if (cnt[half] == 0) continue;
+      FAcc<NCH> acc;
+      acc.zero();
+      if (one[half]) {
+        const uint32_t n = cnt[half];
+        const float *base = half == 0 ? a.neu1 : a.neu1e;
+        FAcc<NCH> c;
+        c.zero();
+        for (uint32_t r0 = 0; r0 < n; r0 += UNR) {
+          FSlice<NCH> rv[UNR];
+          float gf[UNR];
+#pragma unroll
+          for (int q = 0; q < UNR; q++) {
+            const uint32_t idx = min(r0 + q, n - 1);
+            const uint32_t pr = idx < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)ri[half].p0, (int)idx)
+                                         : (uint32_t)__builtin_amdgcn_readlane((int)ri[half].p1, (int)(idx - 64));
+            gf[q] = __int_as_float(idx < 64
+                                               ? __builtin_amdgcn_readlane(__float_as_int(ri[half].g0), (int)idx)
+                                               : __builtin_amdgcn_readlane(__float_as_int(ri[half].g1), (int)(idx - 64)));
+            rv[q].ld(base + (uint64_t)pr * a.ld, lane, tl);
+          }
+#pragma unroll
+          for (int q = 0; q < UNR; q++) {
+            if (r0 + q < n) {
+              if (half == 0)
+                c.axpy((double)gf[q], rv[q], tl);
+              else
+                c.add(rv[q], tl);
+            }
+          }
+        }
+#pragma unroll
+        for (int cc = 0; cc < NCH; cc++)
+#pragma unroll
+          for (int k = 0; k < 4; k++) acc.v[cc][k] = (double)(float)c.v[cc][k];  // the fp32 partial
+        acc.t = (double)(float)c.t;
+      } else {
+        acc.add(pf[half], tl);
+        const uint32_t stride = (i1[half] - i0[half]) > kGroup ? kGroup : 1;
+        for (uint32_t it0 = i0[half] + stride; it0 < i1[half]; it0 += PU * stride) {
+          FSlice<NCH> pv[PU];
+#pragma unroll
+          for (int q = 0; q < PU; q++)
+            pv[q].ld(a.partial + (uint64_t)min(it0 + q * stride, i1[half] - 1) * D, lane, tl);
+#pragma unroll
+          for (int q = 0; q < PU; q++)
+            if (it0 + q * stride < i1[half]) acc.add(pv[q], tl);
+        }
       }
       const double inv = (double)cnt[half];
       float *w = row + half * D, *w2 = row + (2 + half) * D;
@@ -1494,6 +1669,11 @@ struct swps_w2v {
   swps::ShardDriver *drv = nullptr;  // swps_w2v_shard_comm: the library drives the exchange
   bool rec_generic = false;          // SWPS_REC_GENERIC=1: the generic k_records (A/B, tests)
   DevMem d_lead;  // hot-group leaders of the batch's gather items: [0] = count, then item indices
+  DevMem d_multi;  // items of multi-chunk runs (k_gather_t's work when k_push_tg runs): [0] = count, then items
+  int fused_push = 1;
+  int push_tg_var = 0;
+  int multi_sort = 1;                 // order the multi-chunk items by position (SWPS_MULTI_SORT=0: off; A/B)
+  uint64_t multi_sort_min = 65536;    // ... for batches of at least this many kept positions (SWPS_MULTI_SORT_MIN)  // k_push_tg variant (SWPS_PUSH_TG: 0 = UNR 8, 1 = UNR 8 at occupancy 4, 2 = UNR 4; A/B)  // fast mode: k_push_tg sums single-chunk runs itself (SWPS_FUSED_PUSH=0: k_gather_t + k_push_t)
   uint64_t *h_small = nullptr;  // pinned readback
   // RNG (utils/random.h:44-47, seed 2008)
   uint64_t lstate = 2008ULL;
@@ -1528,7 +1708,7 @@ struct swps_w2v {
   // overlapped single-GPU driver (train_overlapped): the second set of the
   // parameter-independent per-batch buffers, swapped with the members above,
   // and the stream prep(i+1) runs on while learn(i) runs on s
-  static constexpr int kPrepBufs = 13;
+  static constexpr int kPrepBufs = 14;
   DevMem alt[kPrepBufs];
   bool alt_local_ready = false;
   // train_overlapped: -1 = auto (on for minibatches of at most kOverlapTok tokens: at B = 100 lines the
@@ -1539,9 +1719,10 @@ struct swps_w2v {
   hipStream_t s_prep = nullptr;
   hipEvent_t ev_learn = nullptr, ev_prep = nullptr;
   DevMem *prep_set[kPrepBufs] = {&d_pos_tok, &d_rec,  &d_pkeys, &d_pvals, &d_pkeys_s, &d_pvals_s, &d_tmp,
-                                 &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_local};
+                                 &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_multi, &d_local};
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
+  uint64_t st_sums = 0, st_fused = 0;  // batches with gradient sums; of those, pushed by k_push_tg
   // negative trace
   uint64_t trace_cap = 0;
   std::vector<int64_t> trace;
@@ -2575,6 +2756,16 @@ int presize(swps_w2v *w, uint64_t maxP) {
     SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
     SWPS_TRY(w->d_desc.ensure(max_items * 16));
     SWPS_TRY(w->d_partial.ensure(max_items * D * a));
+    SWPS_TRY(w->d_multi.ensure((max_items + 1) * 4));
+    if (w->multi_sort && maxP >= w->multi_sort_min) {  // the multi-item order sort (prep_batch)
+      SWPS_TRY(w->d_pkeys.ensure(max_items * 4));
+      SWPS_TRY(w->d_pvals.ensure(max_items * 4));
+      SWPS_TRY(w->d_icnt.ensure(max_items * 4));
+      size_t mb = 0;
+      SWPS_HIP(sort_pairs(nullptr, mb, w->d_pkeys.as<uint32_t>(), w->d_icnt.as<uint32_t>(), w->d_pvals.as<uint32_t>(),
+                          w->d_multi.as<uint32_t>(), max_items, 16, w->s));
+      SWPS_TRY(w->d_tmp.ensure(mb));
+    }
   }
   return SWPS_OK;
 }
@@ -2670,11 +2861,13 @@ __global__ void k_set_local(const int32_t *__restrict__ K, uint32_t U, int32_t *
 // k_set_local and k_positions in one launch (thread i does both jobs' i-th item)
 __global__ void k_batch_setup(const int32_t *__restrict__ K, uint32_t U, int32_t *__restrict__ local,
                               const int32_t *__restrict__ kscan, uint64_t t0, uint64_t nt,
-                              int32_t *__restrict__ pos_tok, uint4 *__restrict__ seg0, uint32_t *__restrict__ lead) {
+                              int32_t *__restrict__ pos_tok, uint4 *__restrict__ seg0, uint32_t *__restrict__ lead,
+                              uint32_t *__restrict__ multi) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < U) local[K[i]] = (int32_t)i;
   if (seg0 && i < U) seg0[i] = make_uint4(0, 0, 0, 0);  // seg[4][U] u32 = U x 16 B: keys without records
   if (lead && i == 0) lead[0] = 0;
+  if (multi && i == 0) multi[0] = 0;
   if (i < nt && pos_tok) {
     const int32_t a = kscan[t0 + i];
     if (kscan[t0 + i + 1] != a) pos_tok[a - kscan[t0]] = (int32_t)(t0 + i);
@@ -2712,7 +2905,7 @@ __global__ void k_seg_bounds(const uint32_t *__restrict__ keys, const uint32_t *
 __global__ void k_seg_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t *__restrict__ cnt,
                              unsigned long long *__restrict__ gstats) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long rc = 0, ic = 0;
+  unsigned long long rc = 0, ic = 0, mr = 0, mi = 0;
   if (u == U) cnt[2 * U] = 0;
   if (u < U) {
     const uint32_t a = seg[u], lo = seg[U + u], b = seg[3 * U + u];
@@ -2721,15 +2914,21 @@ __global__ void k_seg_counts(const uint32_t *__restrict__ seg, uint32_t U, uint3
     cnt[2 * u + 1] = cv;
     rc = b - a;
     ic = ch + cv;
+    mr = (ch > 1 ? lo - a : 0) + (cv > 1 ? b - lo : 0);  // multi-chunk runs: k_gather_t's share when fused
+    mi = (ch > 1 ? ch : 0) + (cv > 1 ? cv : 0);
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     rc += __shfl_xor(rc, off, 64);
     ic += __shfl_xor(ic, off, 64);
+    mr += __shfl_xor(mr, off, 64);
+    mi += __shfl_xor(mi, off, 64);
   }
   if (gstats && (threadIdx.x & 63) == 0 && rc) {
     atomicAdd(&gstats[0], rc);
     atomicAdd(&gstats[1], ic);
+    atomicAdd(&gstats[2], mr);
+    atomicAdd(&gstats[3], mi);
   }
 }
 
@@ -2764,12 +2963,13 @@ int prep_batch(swps_w2v *w) {
     SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
     // leaders: at most 2 per 17 items (a run of kGroup + 1 chunks has two)
     SWPS_TRY(w->d_lead.ensure(((2ULL * U + P * (uint64_t)(N + 1 + 2 * W) / kChunk + 1) / 8 + 2) * 4));
+    SWPS_TRY(w->d_multi.ensure((2ULL * U + P * (uint64_t)(N + 1 + 2 * W) / kChunk + 2) * 4));
   }
   if (U || recs) {
     k_batch_setup<<<nblk(std::max<uint64_t>(U, recs ? nt : 0)), 256, 0, s>>>(
         K, U, w->d_local.as<int32_t>(), w->d_kscan.as<int32_t>(), t0, recs ? nt : 0,
         recs ? w->d_pos_tok.as<int32_t>() : nullptr, will_sort ? w->d_seg.as<uint4>() : nullptr,
-        will_sort ? w->d_lead.as<uint32_t>() : nullptr);
+        will_sort ? w->d_lead.as<uint32_t>() : nullptr, will_sort ? w->d_multi.as<uint32_t>() : nullptr);
     SWPS_HIP(hipGetLastError());
   }
   if (recs) {
@@ -2849,8 +3049,34 @@ int prep_batch(swps_w2v *w) {
                                                 (int)(2 * U + 1), s));
       const uint64_t max_items = 2ULL * U + M / kChunk + 1;
       SWPS_TRY(w->d_desc.ensure(max_items * 16));
+      // multi-chunk items in the order of their first record's position when
+      // the batch's neu1 / neu1e rows outgrow the Infinity Cache: concurrently
+      // running gather waves then read nearby positions, so a row's ~6
+      // re-reads (by the records of its other keys) hit the cache
+      MultiOrder mo{};
+      const bool msort = w->multi_sort && P >= w->multi_sort_min;
+      if (msort) {
+        SWPS_TRY(w->d_pkeys.ensure(max_items * 4));
+        SWPS_TRY(w->d_pvals.ensure(max_items * 4));
+        SWPS_TRY(w->d_icnt.ensure(max_items * 4));
+        int shift = 0;
+        while ((P >> shift) >= kMultiPad) shift++;
+        mo = MultiOrder{w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(),
+                        (uint32_t)P, HOFF, shift};
+      }
       k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk,
-                                                   max_items, w->d_desc.as<uint4>(), w->d_lead.as<uint32_t>());
+                                                   max_items, w->d_desc.as<uint4>(), w->d_lead.as<uint32_t>(),
+                                                   w->d_multi.as<uint32_t>(), mo);
+      SWPS_HIP(hipGetLastError());
+      if (msort) {  // stable: equal coarse positions keep item order
+        size_t mb = 0;
+        SWPS_HIP(sort_pairs(nullptr, mb, w->d_pkeys.as<uint32_t>(), w->d_icnt.as<uint32_t>(),
+                            w->d_pvals.as<uint32_t>(), w->d_multi.as<uint32_t>() + 1, max_items, 16, s));
+        SWPS_TRY(w->d_tmp.ensure(mb));
+        mb = w->d_tmp.bytes;
+        SWPS_HIP(sort_pairs(w->d_tmp.p, mb, w->d_pkeys.as<uint32_t>(), w->d_icnt.as<uint32_t>(),
+                            w->d_pvals.as<uint32_t>(), w->d_multi.as<uint32_t>() + 1, max_items, 16, s));
+      }
       SWPS_HIP(hipGetLastError());
       tm.end(KT_SORT, es, s);
       pb.sorted = true;
@@ -2924,14 +3150,19 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_HIP(hipGetLastError());
     tm.end(KT_FWD, ef, s);
   }
+  // fast mode, single GPU: the push sums the single-chunk runs itself (k_push_tg)
+  const bool fused = std::is_same<T, float>::value && std::is_same<A, float>::value && w->tail && !d_grads &&
+                     w->push_t && w->fused_push && D < 512 && pb.sorted;
   if (pb.sorted) {
     // ---- chunked segmented gradient sums ----
     SWPS_TRY(w->d_partial.ensure(pb.max_items * D * sizeof(A)));
     GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
                      w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad), w->d_lead.as<uint32_t>(),
-                     (uint32_t)pb.max_items};
-    const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(pb.max_items * 64), (uint64_t)w->gather_grid);
+                     (uint32_t)pb.max_items, fused ? w->d_multi.as<uint32_t>() : nullptr};
+    // multi-chunk items: at most M / kChunk full chunks plus one partial chunk per run of > kChunk records
+    const uint64_t gitems = fused ? std::min<uint64_t>(pb.max_items, 2 * pb.M / kChunk + 1) : pb.max_items;
+    const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(gitems * 64), (uint64_t)w->gather_grid);
     const unsigned cgrid = combine_grid(pb.max_items);
     hipEvent_t eg = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
@@ -2966,15 +3197,28 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_HIP(hipGetLastError());
     tm.end(KT_GATHER, eg, s);
     w->st_pairs += pb.M;
+    w->st_sums++;
+    w->st_fused += fused;
   }
   if (U > 0) {
     // ---- push: mean + AdaGrad (also clears the local index map) ----
     PushArgs<T, A> pa{K, U, w->d_vid_row.as<uint32_t>(), w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
                       w->d_partial.as<A>(), w->t->rows.as<T>(), w->d_local.as<int32_t>(), D,
                       (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads,
-                      d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs};
+                      d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs,
+                      w->d_pvals_s.as<uint32_t>(), w->d_pg.as<float>(), w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
+                      pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad)};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      if (fused) {
+        if (w->push_tg_var == 1)
+          k_push_tg<1, 8, 4><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);  // occupancy 4, 5 VGPRs spilled
+        else if (w->push_tg_var == 2)
+          k_push_tg<1, 4, 1><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);
+        else
+          k_push_tg<1, 8, 1><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);  // 135 VGPRs, occupancy 3
+        goto push_done;
+      }
       if (w->tail && !d_grads && w->push_t) {
         if (D < 512)
           k_push_t<1><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);
@@ -3095,6 +3339,10 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   w->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_XCD_ORDER")) w->xcd_order = atoi(e) != 0;
   if (const char *e = getenv("SWPS_PUSH_T")) w->push_t = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_FUSED_PUSH")) w->fused_push = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_PUSH_TG")) w->push_tg_var = atoi(e);          // A/B timing
+  if (const char *e = getenv("SWPS_MULTI_SORT")) w->multi_sort = atoi(e);        // A/B timing
+  if (const char *e = getenv("SWPS_MULTI_SORT_MIN")) w->multi_sort_min = strtoull(e, nullptr, 10);
   if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_UNI_INDEX")) w->uni_index = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_CACHE_PAD")) w->cache_pad = atoi(e) != 0;  // A/B timing
@@ -3106,8 +3354,8 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (!rc && hipHostMalloc((void **)&w->h_small, 64) != hipSuccess) rc = fail(SWPS_E_OOM, "pinned alloc");
   if (!rc) rc = w->d_rows_touched.ensure(16);
   if (!rc && hipMemset(w->d_rows_touched.p, 0, 16) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
-  if (!rc) rc = w->d_gstats.ensure(16);
-  if (!rc && hipMemset(w->d_gstats.p, 0, 16) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
+  if (!rc) rc = w->d_gstats.ensure(32);
+  if (!rc && hipMemset(w->d_gstats.p, 0, 32) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
   if (!rc) {
     uint64_t A[kMaxJump + 1], C[kMaxJump + 1];
     for (int k = 0; k <= kMaxJump; k++) {
@@ -3386,6 +3634,14 @@ int swps_w2v_stats(swps_w2v *w, uint64_t *o) {
 int swps_w2v_gather_stats(swps_w2v *w, uint64_t *out2) {
   SWPS_HIP(hipStreamSynchronize(w->s));
   SWPS_HIP(hipMemcpy(out2, w->d_gstats.p, 16, hipMemcpyDeviceToHost));
+  return SWPS_OK;
+}
+
+int swps_w2v_sum_stats(swps_w2v *w, uint64_t *out6) {
+  SWPS_HIP(hipStreamSynchronize(w->s));
+  SWPS_HIP(hipMemcpy(out6, w->d_gstats.p, 32, hipMemcpyDeviceToHost));
+  out6[4] = w->st_fused;
+  out6[5] = w->st_sums;
   return SWPS_OK;
 }
 

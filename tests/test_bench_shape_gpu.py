@@ -167,13 +167,23 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode):
     assert rel.max() <= (1e-5 if mode == "parity" else FAST_TOL_BATCH), float(rel.max())
 
 
-def test_wide_digit_sort_bit_identical_at_bench_scale(lib, gpu, monkeypatch):
-    """The bench corpus's minibatch key indices need 18 bits: they sort in two
-    9-bit onesweep passes (swps_sort.h) instead of three 8-bit ones.  Same
-    stable order: three 5000-line batches train to the same bits either way."""
+@pytest.mark.parametrize("env", ["SWPS_SORT_WIDE", "SWPS_FUSED_PUSH", "SWPS_MULTI_SORT"])
+def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env):
+    """Three 5000-line batches of the bench corpus train to the same bits with
+    either setting of:
+    * SWPS_SORT_WIDE — the minibatch key indices need 18 bits: they sort in two
+      9-bit onesweep passes (swps_sort.h) instead of three 8-bit ones (same
+      stable order);
+    * SWPS_FUSED_PUSH — k_push_tg sums the single-chunk (key, kind) runs itself
+      and k_gather_t / k_combine only the multi-chunk ones (hot keys of
+      thousands of records: the second level runs), vs every run through a
+      partial;
+    * SWPS_MULTI_SORT — the multi-chunk items run in the order of their first
+      record's position (Infinity-Cache reuse of the neu1 / neu1e rows) instead
+      of item order."""
     res = []
-    for wide in ("0", "1"):
-        monkeypatch.setenv("SWPS_SORT_WIDE", wide)
+    for val in ("0", "1"):
+        monkeypatch.setenv(env, val)
         import subprocess
         import sys
         code = ("import sys, numpy as np; sys.path.insert(0, %r); import swiftmpi_amd as sw; "

@@ -361,7 +361,8 @@ def test_alias_sampler_distribution(lib, gpu, tmp_path):
 
 
 def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch):
-    """k_push_t (compact-slice push) == k_push, padded == D-strided neu1/neu1e
+    """k_push_t (compact-slice push) == k_push, k_push_tg (single-chunk runs
+    summed inside the push, three variants) == k_gather_t + k_push_t, padded == D-strided neu1/neu1e
     rows, 128-B padded == D-strided worker-cache rows, and negatives from the
     coarse-indexed run-length unigram table == the
     1e8-slot table, bit for bit, at the bench's D = 300 (tail) shape in fast mode."""
@@ -373,12 +374,19 @@ def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch):
     off = np.arange(0, lines * L + 1, L, dtype=np.uint64)
     keys = np.array([lib.bkdr("w%d" % i) for i in range(V)], dtype=np.uint64)
     outs, negs = [], []
-    for push_t, pad, uidx, cpad in (("1", "1", "1", "1"), ("0", "1", "1", "1"), ("1", "0", "1", "1"),
-                                    ("1", "1", "0", "1"), ("1", "1", "1", "0")):
+    variants = (("1", "1", "1", "1", "1", "0"), ("0", "1", "1", "1", "1", "0"), ("1", "0", "1", "1", "1", "0"),
+                ("1", "1", "0", "1", "1", "0"), ("1", "1", "1", "0", "1", "0"), ("1", "1", "1", "1", "0", "0"),
+                ("1", "1", "1", "1", "1", "1"), ("1", "1", "1", "1", "1", "2"), ("1", "1", "1", "1", "1", "sort"))
+    for push_t, pad, uidx, cpad, fused, tgv in variants:
+        # "sort": the multi-chunk gather items in position order even for these small batches
+        monkeypatch.setenv("SWPS_MULTI_SORT_MIN", "0" if tgv == "sort" else "65536")
+        tgv = "0" if tgv == "sort" else tgv
         monkeypatch.setenv("SWPS_PUSH_T", push_t)
         monkeypatch.setenv("SWPS_ROW_PAD", pad)
         monkeypatch.setenv("SWPS_UNI_INDEX", uidx)
         monkeypatch.setenv("SWPS_CACHE_PAD", cpad)
+        monkeypatch.setenv("SWPS_FUSED_PUSH", fused)
+        monkeypatch.setenv("SWPS_PUSH_TG", tgv)
         t = lib.Table("w2v", dim=300, capacity=V, dtype="f32", learning_rate=0.7)
         w = lib.Word2Vec(t, window=5, negative=5, minibatch=20, sample=1e-3, unigram_size=10 ** 8,
                          fp64_intermediates=False)
@@ -388,7 +396,7 @@ def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch):
         w.train(1)
         outs.append(w.get_params())
         negs.append(w.negatives(200000))
-    for k in (1, 2, 3, 4):
+    for k in range(1, len(variants)):
         assert np.array_equal(outs[0], outs[k]), k
         assert np.array_equal(negs[0], negs[k]), k
     assert len(negs[0]) > 1000
