@@ -2,13 +2,15 @@
 // (apps/logistic/lr.cpp:157-238, nthreads = 1 semantics) as HIP kernels.
 //
 // Per minibatch (B+1 valid rows, lr.cpp:308-354 gather == train window):
-//   k_lr_forward   one thread per row: s = sum w_i*x_i (fp32, feature order),
-//                  p = 1/(1+exp(-s)), e = y - p; one gradient record e*x_i per
-//                  nonzero, keyed by the feature's vid   (lr.cpp:358-375)
-//   radix sort     records by vid (stable: row order, then feature order)
-//   run-length     unique vids + counts of the batch = the pushed key set
-//   k_lr_push      per key: fp32 sum in record order, mean = sum/count
-//                  (lr.cpp:32-38), AdaGrad fp32 (lr.cpp:68-75) on the shard row
+//   k_lr_forward   one wave per row: s = sum w_i*x_i (fp32, feature order),
+//                  p = 1/(1+exp(-s)), e = y - p stored per row (lr.cpp:358-375)
+//   k_lr_reduce_*  per pushed key (a run of the batch's records in their static
+//                  key-sorted order, built once at load): the gradient records
+//                  e[row]*x_i summed in record order (fp32 chain, or fp64 in
+//                  fast_sums mode), mean = sum/count (lr.cpp:32-38), AdaGrad fp32
+//                  (lr.cpp:68-75) on the shard row
+// The records' (row, x_i) in key-sorted order are static (srow / sval), so the
+// forward writes one error per row instead of scattering a record per feature.
 // Every weight read in a batch belongs to that batch's key set, which the
 // reference pulls at the start of the batch and the server only changes at the
 // push: reading the shard rows directly is the same snapshot, so no copy.
@@ -35,6 +37,11 @@ namespace {
 __device__ __forceinline__ float weight(const uint32_t *__restrict__ vid_row, const float *__restrict__ w, int32_t v) {
   return vid_row ? w[(uint64_t)vid_row[v] * 2] : w[v];
 }
+// the training loop's form: fidx = the feature's shard row (single GPU, stride 2: precomputed
+// vid_row[vid] per record, one dependent random load less) or its vid (cache, stride 1)
+__device__ __forceinline__ float weight_at(const float *__restrict__ w, uint32_t fidx, int stride) {
+  return w[(uint64_t)fidx * stride];
+}
 
 // Ordered fp32 sum of one value per lane (lanes [0, m)) added to acc in lane
 // order — the reference's sequential `sum += ...` (bit-exact), with the loads
@@ -48,10 +55,9 @@ __device__ __forceinline__ float ordered_add(float acc, float x, int m) {
 // feature k of the row (64 at a time), s = sum w_i*x_i in feature order,
 // p = 1/(1+exp(-s)), e = y - p; gradient record (vid, e*x_i) per feature in
 // (row, feature) order.
-__global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
+__global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__ row_off, const uint32_t *__restrict__ fidx,
                              const float *__restrict__ fval, const float *__restrict__ label, uint64_t r0, uint64_t nr,
-                             const uint32_t *__restrict__ vid_row, const float *__restrict__ rows,
-                             float *__restrict__ contrib_s, const uint32_t *__restrict__ slot,
+                             const float *__restrict__ rows, int stride, float *__restrict__ err,
                              float *__restrict__ err2) {
   const uint64_t j = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
@@ -63,17 +69,18 @@ __global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__
     const int m = (int)min<uint64_t>(64, b - c);
     float prod = 0.f;
     if (lane < m) {
-      const float w = weight(vid_row, rows, fvid[c + lane]);
+      const float w = weight_at(rows, fidx[c + lane], stride);
       prod = w * fval[c + lane];
     }
     sum = ordered_add(sum, prod, m);
   }
   const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
   const float error = label[r] - predict;
-  // the contribution goes straight to its place in the batch's key-sorted
-  // order (a static permutation of the batch's features, built at load)
-  for (uint64_t c = a + lane; c < b; c += 64) contrib_s[slot[c]] = error * fval[c];
-  if (lane == 0) err2[r] = error * error;
+  // the gradient records e*x_i are formed by the reduce from the static sorted (row, x_i)
+  if (lane == 0) {
+    err[r] = error;
+    err2[r] = error * error;
+  }
 }
 
 // ---- the static per-batch index (built once at load; lr_index) -------------
@@ -92,16 +99,30 @@ __global__ void k_lr_idx_keys(const uint64_t *__restrict__ row_off, uint64_t nr,
   }
 }
 
-// slot of record c = its position in the sorted order, relative to its batch's
-// first record; run heads -> run key, relative start
+// row of every record
+__global__ void k_lr_rowid(const uint64_t *__restrict__ row_off, uint64_t nr, uint32_t *__restrict__ rid) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nr) return;
+  for (uint64_t c = row_off[r]; c < row_off[r + 1]; c++) rid[c] = (uint32_t)r;
+}
+
+// the records in sorted order: their row and x_i; run heads
 __global__ void k_lr_idx_slots(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ perm, uint64_t n,
-                               const uint64_t *__restrict__ bnz0, uint32_t *__restrict__ slot,
-                               uint32_t *__restrict__ head) {
+                               const uint32_t *__restrict__ rid, const float *__restrict__ fval,
+                               uint32_t *__restrict__ srow, float *__restrict__ sval, uint32_t *__restrict__ head) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t z0 = bnz0[ks[i] >> 32];
-  slot[perm[i]] = (uint32_t)(i - z0);
+  const uint32_t c = perm[i];
+  srow[i] = rid[c];
+  sval[i] = fval[c];
   head[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1u : 0u;
+}
+
+// shard row of every record's feature / every run's key (single GPU)
+__global__ void k_lr_map_rows(const int32_t *__restrict__ vid, uint64_t n, const uint32_t *__restrict__ vid_row,
+                              uint32_t *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = vid_row[vid[i]];
 }
 
 __global__ void k_lr_idx_runs(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ head,
@@ -155,8 +176,8 @@ constexpr uint32_t kLrShort = 32;
 
 struct LrReduce {
   const uint32_t *uniq, *cnt, *off, *nruns;
-  const float *val;  // contributions sorted by key (stable)
-  const uint32_t *vid_row;
+  const float *val;      // the batch's gradient records e*x_i in key-sorted order (k_lr_records)
+  const uint32_t *urow;  // shard row per run (single GPU)
   float *rows;
   float lr, fudge;
   const int32_t *local;
@@ -172,11 +193,21 @@ __device__ __forceinline__ void lr_apply(const LrReduce &a, uint32_t r, float s,
     a.grads[a.local[a.uniq[r]]] = m;
     return;
   }
-  float *row = a.rows + (uint64_t)a.vid_row[a.uniq[r]] * 2;
+  float *row = a.rows + (uint64_t)a.urow[r] * 2;
   const float g2 = row[1] + m * m;
   row[1] = g2;
   const float step = a.lr * m;
   row[0] = row[0] + step / sqrtf(g2 + a.fudge);
+}
+
+__device__ __forceinline__ float lr_rec(const LrReduce &a, uint32_t i) { return a.val[i]; }
+
+// the batch's gradient records in key-sorted order: e[row]*x_i (fp32 product, = the
+// reference's error * x) from the static sorted (row, x_i); e is L2-resident (4 B per row)
+__global__ void k_lr_records(const uint32_t *__restrict__ srow, const float *__restrict__ sval, uint64_t n,
+                             const float *__restrict__ err, float *__restrict__ val) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) val[i] = err[srow[i]] * sval[i];
 }
 
 __global__ __launch_bounds__(256) void k_lr_reduce_short(LrReduce a) {
@@ -189,12 +220,12 @@ __global__ __launch_bounds__(256) void k_lr_reduce_short(LrReduce a) {
     }
     if (a.fast) {
       double s = 0;
-      for (uint32_t i = o; i < o + c; i++) s += (double)a.val[i];
+      for (uint32_t i = o; i < o + c; i++) s += (double)lr_rec(a, i);
       lr_apply(a, r, 0.f, c, s);
       continue;
     }
     float s = 0;
-    for (uint32_t i = o; i < o + c; i++) s += a.val[i];
+    for (uint32_t i = o; i < o + c; i++) s += lr_rec(a, i);
     lr_apply(a, r, s, c);
   }
 }
@@ -217,12 +248,12 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long(LrReduce a) {
       double s4[4] = {0.0, 0.0, 0.0, 0.0};
       uint32_t k = lane;
       for (; k + 192 < c; k += 256) {
-        s4[0] += (double)a.val[o + k];
-        s4[1] += (double)a.val[o + k + 64];
-        s4[2] += (double)a.val[o + k + 128];
-        s4[3] += (double)a.val[o + k + 192];
+        s4[0] += (double)lr_rec(a, o + k);
+        s4[1] += (double)lr_rec(a, o + k + 64);
+        s4[2] += (double)lr_rec(a, o + k + 128);
+        s4[3] += (double)lr_rec(a, o + k + 192);
       }
-      for (; k < c; k += 64) s4[0] += (double)a.val[o + k];
+      for (; k < c; k += 64) s4[0] += (double)lr_rec(a, o + k);
       const double tot = wave_sum_pl((s4[0] + s4[1]) + (s4[2] + s4[3]));
       if (lane == 0) lr_apply(a, r, 0.f, c, tot);
       continue;
@@ -232,7 +263,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long(LrReduce a) {
 #pragma unroll
     for (uint32_t u = 0; u < kLrStage / 64; u++) {
       const uint32_t k = u * 64 + lane;
-      x[u] = k < c ? a.val[o + k] : 0.f;
+      x[u] = k < c ? lr_rec(a, o + k) : 0.f;
     }
     for (uint32_t i = 0; i < c; i += kLrStage) {
       const uint32_t n = min(kLrStage, c - i);
@@ -245,7 +276,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long(LrReduce a) {
 #pragma unroll
       for (uint32_t u = 0; u < kLrStage / 64; u++) {
         const uint32_t k = i + kLrStage + u * 64 + lane;
-        x[u] = k < c ? a.val[o + k] : 0.f;
+        x[u] = k < c ? lr_rec(a, o + k) : 0.f;
       }
       if (lane == 0) {
         uint32_t k = 0;
@@ -345,10 +376,12 @@ struct swps_lr {
   std::vector<uint64_t> vocab_keys;  // vid order = first-pull order
   bool loaded = false, inited = false;
   uint64_t cursor = 0, nbatches = 0;
-  DevMem d_label, d_row_off, d_fvid, d_fval, d_vid_row, d_val_s, d_err2, d_tmp, d_pred, d_longs;
-  // the static per-batch index (lr_index): slot of every record in its batch's key-sorted order; the runs
+  DevMem d_label, d_row_off, d_fvid, d_fval, d_vid_row, d_err, d_err2, d_val_s, d_tmp, d_pred, d_longs;
+  DevMem d_frow, d_urow;  // single GPU: shard row per record's feature / per run (built at the first batch)
+  bool rows_mapped = false;
+  // the static per-batch index (lr_index): every batch's records in key-sorted order (row, x_i); the runs
   // (pushed keys) of all batches: vid, start and length relative to the batch; first run and run count per batch
-  DevMem d_slot, d_ruk, d_roff, d_rcnt, d_bnruns;
+  DevMem d_srow, d_sval, d_ruk, d_roff, d_rcnt, d_bnruns;
   std::vector<uint64_t> brun;
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
@@ -391,7 +424,8 @@ int lr_index(swps_lr *l) {
   for (uint64_t b = 0; b < nb; b++) l->max_bnnz = std::max<uint64_t>(l->max_bnnz, bnz0[b + 1] - bnz0[b]);
   DevMem d_bnz0, key, idx, ks, perm, head, rid1, rkey, tmp;
   SWPS_TRY(upload(d_bnz0, bnz0, s));
-  SWPS_TRY(l->d_slot.ensure(std::max<uint64_t>(n, 1) * 4));
+  SWPS_TRY(l->d_srow.ensure(std::max<uint64_t>(n, 1) * 4));
+  SWPS_TRY(l->d_sval.ensure(std::max<uint64_t>(n, 1) * 4));
   SWPS_TRY(l->d_bnruns.ensure(std::max<uint64_t>(nb, 1) * 4));
   l->brun.assign(nb + 1, 0);
   if (n == 0) return SWPS_OK;
@@ -420,8 +454,10 @@ int lr_index(swps_lr *l) {
   idx.release();
   SWPS_TRY(head.ensure(n * 4));
   SWPS_TRY(rid1.ensure(n * 4));
-  k_lr_idx_slots<<<nblk(n), 256, 0, s>>>(ks.as<uint64_t>(), perm.as<uint32_t>(), n, d_bnz0.as<uint64_t>(),
-                                          l->d_slot.as<uint32_t>(), head.as<uint32_t>());
+  k_lr_rowid<<<nblk(nr), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), nr, rid1.as<uint32_t>());
+  k_lr_idx_slots<<<nblk(n), 256, 0, s>>>(ks.as<uint64_t>(), perm.as<uint32_t>(), n, rid1.as<uint32_t>(),
+                                          l->d_fval.as<float>(), l->d_srow.as<uint32_t>(), l->d_sval.as<float>(),
+                                          head.as<uint32_t>());
   SWPS_HIP(hipGetLastError());
   SWPS_TRY(lr_scan_incl(head.as<uint32_t>(), rid1.as<uint32_t>(), n, tmp, s));
   uint32_t R = 0;
@@ -463,8 +499,10 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   SWPS_TRY(upload(l->d_fvid, l->fvid, s));
   SWPS_TRY(upload(l->d_fval, l->fval, s));
   SWPS_TRY(l->d_vid_row.ensure(std::max<size_t>(1, l->vocab_keys.size()) * 4));
+  SWPS_TRY(l->d_err.ensure(std::max<uint64_t>(1, nr) * 4));
   SWPS_TRY(l->d_err2.ensure(std::max<uint64_t>(1, nr) * 4));
   SWPS_TRY(lr_index(l));
+  l->rows_mapped = false;
   SWPS_HIP(hipStreamSynchronize(s));
   l->loaded = true;
   return SWPS_OK;
@@ -477,7 +515,8 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const uint64_t nz0 = l->row_off[r0], nnz = l->row_off[r1] - nz0;
   hipStream_t s = l->s;
   float *rows = l->t->rows.as<float>();
-  const uint32_t *vid_row = l->d_vid_row.as<uint32_t>();
+  const uint32_t *fidx = l->d_frow.as<uint32_t>();
+  int stride = 2;
   l->cursor++;
   if (l->sharded) {  // install the owners' pull values; read weights from the cache
     const uint64_t U = l->bU[bi];
@@ -486,16 +525,26 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
                                            l->d_local.as<int32_t>());
     SWPS_HIP(hipGetLastError());
     rows = l->d_wcache.as<float>();
-    vid_row = nullptr;
+    fidx = (const uint32_t *)l->d_fvid.as<int32_t>();
+    stride = 1;
+  } else if (!l->rows_mapped) {  // the shard rows of every record's feature and every run's key, once
+    const uint64_t n = l->row_off[nr], R = l->brun[l->nbatches];
+    SWPS_TRY(l->d_frow.ensure(std::max<uint64_t>(n, 1) * 4));
+    SWPS_TRY(l->d_urow.ensure(std::max<uint64_t>(R, 1) * 4));
+    k_lr_map_rows<<<nblk(n), 256, 0, s>>>(l->d_fvid.as<int32_t>(), n, l->d_vid_row.as<uint32_t>(),
+                                          l->d_frow.as<uint32_t>());
+    k_lr_map_rows<<<nblk(R), 256, 0, s>>>((const int32_t *)l->d_ruk.as<uint32_t>(), R, l->d_vid_row.as<uint32_t>(),
+                                          l->d_urow.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+    l->rows_mapped = true;
+    fidx = l->d_frow.as<uint32_t>();
   }
   if (nnz == 0) return SWPS_OK;
-  SWPS_TRY(l->d_val_s.ensure(l->max_bnnz * 4));
   SWPS_TRY(l->d_longs.ensure((l->max_bnnz + 1) * 4));
   hipEvent_t e0 = l->timer.begin(s);
-  k_lr_forward<<<nblk((r1 - r0) * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), l->d_fvid.as<int32_t>(),
-                                                    l->d_fval.as<float>(), l->d_label.as<float>(), r0, r1 - r0,
-                                                    vid_row, rows, l->d_val_s.as<float>(), l->d_slot.as<uint32_t>(),
-                                                    l->d_err2.as<float>());
+  k_lr_forward<<<nblk((r1 - r0) * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(),
+                                                    l->d_label.as<float>(), r0, r1 - r0, rows, stride,
+                                                    l->d_err.as<float>(), l->d_err2.as<float>());
   SWPS_HIP(hipGetLastError());
   l->timer.end(0, e0, s);
   hipEvent_t e3 = l->timer.begin(s);
@@ -503,8 +552,12 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   uint32_t *nlong = l->d_longs.as<uint32_t>() + l->max_bnnz;
   SWPS_HIP(hipMemsetAsync(nlong, 0, 4, s));
   const uint64_t q0 = l->brun[bi];
+  SWPS_TRY(l->d_val_s.ensure(l->max_bnnz * 4));
+  k_lr_records<<<nblk(nnz), 256, 0, s>>>(l->d_srow.as<uint32_t>() + nz0, l->d_sval.as<float>() + nz0, nnz,
+                                          l->d_err.as<float>(), l->d_val_s.as<float>());
   LrReduce ra{l->d_ruk.as<uint32_t>() + q0, l->d_rcnt.as<uint32_t>() + q0, l->d_roff.as<uint32_t>() + q0,
-              l->d_bnruns.as<uint32_t>() + bi, l->d_val_s.as<float>(), l->d_vid_row.as<uint32_t>(),
+              l->d_bnruns.as<uint32_t>() + bi, l->d_val_s.as<float>(),
+              l->sharded ? nullptr : l->d_urow.as<uint32_t>() + q0,
               l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, l->d_local.as<int32_t>(),
               l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
   k_lr_reduce_short<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(ra);
@@ -612,6 +665,7 @@ int swps_lr_init(swps_lr *l) {
   DevMem dk;
   SWPS_TRY(upload(dk, l->vocab_keys, l->s));
   SWPS_TRY(table_find_or_insert(l->t, dk.as<uint64_t>(), V, l->d_vid_row.as<uint32_t>(), l->s));
+  l->rows_mapped = false;  // vid_row changed: k_lr_map_rows again at the next batch
   if (l->cfg.init_ref) {
     // LRPullAccessMethod::init_param (lr.cpp:48-50): w = gen_float() per miss
     std::vector<float> rows(V * 2, 0.f);

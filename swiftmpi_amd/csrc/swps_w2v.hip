@@ -936,7 +936,7 @@ struct MultiOrder {  // k_item_desc: sort keys of the multi-chunk items by their
 constexpr uint32_t kMultiPad = 0xFFFFu;  // 16-bit sort keys: items outside the multi list sort last
 
 __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__restrict__ ioff, uint32_t U,
-                            uint32_t CH, uint64_t max_items, uint4 *__restrict__ desc, uint32_t *__restrict__ lead,
+                            uint32_t CH, uint32_t CHM, uint64_t max_items, uint4 *__restrict__ desc, uint32_t *__restrict__ lead,
                             uint32_t *__restrict__ multi, MultiOrder mo) {
   const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = item < max_items && item < ioff[2ull * U];
@@ -958,7 +958,7 @@ __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__
       uint32_t key = kMultiPad;
       if (m) {  // the chunk's first record: index slot*P + p (v records after HOFF)
         const uint32_t jj = lo, u = jj >> 1, kind = jj & 1, k = (uint32_t)item - ioff[jj];
-        const uint32_t pi = mo.vals[seg[(2 * kind) * U + u] + k * CH];
+        const uint32_t pi = mo.vals[seg[(2 * kind) * U + u] + k * CHM];
         key = (uint32_t)((kind ? (uint64_t)pi - mo.HOFF : (uint64_t)pi) % mo.P) >> mo.shift;
       }
       mo.key[item] = key;
@@ -977,8 +977,9 @@ __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__
   if (!live) return;
   const uint32_t jj = lo, u = jj >> 1, kind = jj & 1, k = (uint32_t)item - ioff[jj];
   const uint32_t s = seg[(2 * kind) * U + u], e = seg[(2 * kind + 1) * U + u];
-  const uint32_t cs = s + k * CH;
-  desc[item] = make_uint4(cs, min(cs + CH, e) | (kind << 31), jj, k);
+  const uint32_t ck = ioff[jj + 1] - ioff[jj] > 1 ? CHM : CH;  // single-item runs hold up to CH records
+  const uint32_t cs = s + k * ck;
+  desc[item] = make_uint4(cs, min(cs + ck, e) | (kind << 31), jj, k);
   // hot (key, kind) runs of more than kGroup chunks: k_combine pre-sums each
   // group of kGroup partials into its leader (the list order does not
   // matter: every leader writes only its own slot)
@@ -1523,6 +1524,114 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
+// k_push_tg with one wave per (key, half): the h half (h, h2sum: the target
+// records' g*neu1 sums) and the v half (v, v2sum: the context records' neu1e
+// sums) of a key's AdaGrad update touch disjoint elements, so they run as
+// independent waves — half the live registers per wave (occupancy) and twice
+// the waves.  Same arithmetic per element: bit-identical to k_push_tg.
+template <int NCH, int UNR>
+__global__ __launch_bounds__(256) void k_push_th(PushArgs<float, float> a) {
+  constexpr int PU = 8;
+  const int lane = threadIdx.x & 63;
+  const int D = a.D;
+  const bool tl = 256 * NCH + lane < D;
+  const uint64_t n2 = 2ull * a.U;
+  for (uint64_t uh = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); uh < n2; uh += (uint64_t)gridDim.x * 4) {
+    const uint64_t u = uh >> 1;
+    const int half = (int)(uh & 1);
+    const int32_t vid = a.K[u];
+    if (lane == 0 && half == 0) a.local[vid] = -1;
+    const uint32_t s0 = a.seg[(2 * half) * a.U + u], s1 = a.seg[(2 * half + 1) * a.U + u];
+    const uint32_t cnt = s1 - s0;
+    if (cnt == 0 && !a.cache_h) continue;
+    float *row = a.rows + (uint64_t)a.vid_row[vid] * 4 * D;
+    const uint32_t i0 = a.ioff[2 * u + half], i1 = a.ioff[2 * u + half + 1];
+    const bool one = i1 - i0 == 1;
+    FSlice<NCH> wr, w2r, pf;
+    ItemRecs ri;
+    wr.ld(row + half * D, lane, tl);
+    if (cnt) {
+      if (one)
+        ri = run_recs(a.vals, a.pg, a.P, a.HOFF, s0, cnt, half, lane);
+      else
+        pf.ld(a.partial + (uint64_t)i0 * D, lane, tl);
+      w2r.ld(row + (2 + half) * D, lane, tl);
+    }
+    if (a.cache_h) wr.st((half ? a.cache_v : a.cache_h) + (uint64_t)vid * a.cs, lane, tl);  // pre-update value
+    if (cnt == 0) continue;
+    FAcc<NCH> acc;
+    acc.zero();
+    if (one) {
+      const float *base = half == 0 ? a.neu1 : a.neu1e;
+      FAcc<NCH> c;
+      c.zero();
+      for (uint32_t r0 = 0; r0 < cnt; r0 += UNR) {
+        FSlice<NCH> rv[UNR];
+        float gf[UNR];
+#pragma unroll
+        for (int q = 0; q < UNR; q++) {
+          const uint32_t idx = min(r0 + q, cnt - 1);
+          const uint32_t pr = idx < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)ri.p0, (int)idx)
+                                       : (uint32_t)__builtin_amdgcn_readlane((int)ri.p1, (int)(idx - 64));
+          gf[q] = __int_as_float(idx < 64 ? __builtin_amdgcn_readlane(__float_as_int(ri.g0), (int)idx)
+                                          : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
+          rv[q].ld(base + (uint64_t)pr * a.ld, lane, tl);
+        }
+#pragma unroll
+        for (int q = 0; q < UNR; q++) {
+          if (r0 + q < cnt) {
+            if (half == 0)
+              c.axpy((double)gf[q], rv[q], tl);
+            else
+              c.add(rv[q], tl);
+          }
+        }
+      }
+#pragma unroll
+      for (int cc = 0; cc < NCH; cc++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc.v[cc][k] = (double)(float)c.v[cc][k];  // the fp32 partial
+      acc.t = (double)(float)c.t;
+    } else {
+      acc.add(pf, tl);
+      const uint32_t stride = (i1 - i0) > kGroup ? kGroup : 1;
+      for (uint32_t it0 = i0 + stride; it0 < i1; it0 += PU * stride) {
+        FSlice<NCH> pv[PU];
+#pragma unroll
+        for (int q = 0; q < PU; q++) pv[q].ld(a.partial + (uint64_t)min(it0 + q * stride, i1 - 1) * D, lane, tl);
+#pragma unroll
+        for (int q = 0; q < PU; q++)
+          if (it0 + q * stride < i1) acc.add(pv[q], tl);
+      }
+    }
+    const double inv = (double)cnt;
+    float *w = row + half * D, *w2 = row + (2 + half) * D;
+    auto upd = [&](double sum, float wv, float w2v, float &wo, float &w2o) {
+      const double g = (double)(float)(sum / inv);  // the mean in the push payload's type
+      const double acc2 = (double)w2v + g * g;
+      const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
+      w2o = (float)acc2;
+      wo = (float)((double)wv + step);
+    };
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      float4 wo, w2o;
+      upd(acc.v[c][0], wr.v[c].x, w2r.v[c].x, wo.x, w2o.x);
+      upd(acc.v[c][1], wr.v[c].y, w2r.v[c].y, wo.y, w2o.y);
+      upd(acc.v[c][2], wr.v[c].z, w2r.v[c].z, wo.z, w2o.z);
+      upd(acc.v[c][3], wr.v[c].w, w2r.v[c].w, wo.w, w2o.w);
+      ((float4 *)w2)[lane + c * 64] = w2o;
+      ((float4 *)w)[lane + c * 64] = wo;
+    }
+    if (tl) {
+      float wo, w2o;
+      upd(acc.t, wr.t, w2r.t, wo, w2o);
+      w2[256 * NCH + lane] = w2o;
+      w[256 * NCH + lane] = wo;
+    }
+  }
+}
+
 // requester side of a sharded pull: the owners' pull values [U][h|v] (K order)
 // into the worker cache (global_pull_access.h:88-97: params[key] = val)
 template <typename T>
@@ -1672,6 +1781,7 @@ struct swps_w2v {
   DevMem d_multi;  // items of multi-chunk runs (k_gather_t's work when k_push_tg runs): [0] = count, then items
   int fused_push = 1;
   int push_tg_var = 0;
+  uint32_t multi_chunk = 0;  // SWPS_MULTI_CHUNK: chunk size of multi-chunk runs (1..128; 0 = by batch size)
   int multi_sort = 1;                 // order the multi-chunk items by position (SWPS_MULTI_SORT=0: off; A/B)
   uint64_t multi_sort_min = 65536;    // ... for batches of at least this many kept positions (SWPS_MULTI_SORT_MIN)  // k_push_tg variant (SWPS_PUSH_TG: 0 = UNR 8, 1 = UNR 8 at occupancy 4, 2 = UNR 4; A/B)  // fast mode: k_push_tg sums single-chunk runs itself (SWPS_FUSED_PUSH=0: k_gather_t + k_push_t)
   uint64_t *h_small = nullptr;  // pinned readback
@@ -2718,7 +2828,10 @@ template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A>
   else
     k_push<T, A, NCH, false><<<nblk((uint64_t)a.U * 64), 256, 0, s>>>(a);
 }
-constexpr uint32_t kChunk = 128;
+constexpr uint32_t kChunk = 128;  // a (key, kind) run of at most kChunk records is one item
+// chunk size of the longer runs: kChunk (SWPS_MULTI_CHUNK sets 1..128 for A/B: 32 and 16 at
+// B = 100 lines were 4 % and 7 % slower — more partials and second-level groups, no latency win)
+inline uint32_t multi_chunk(const swps_w2v *w, uint64_t) { return w->multi_chunk ? w->multi_chunk : kChunk; }
 constexpr uint64_t kOverlapTok = 1000000;  // auto-overlap threshold (tokens per minibatch)
 
 // Subsample masks and main-LCG offsets for a whole epoch.  They depend only on
@@ -2750,7 +2863,8 @@ int presize(swps_w2v *w, uint64_t maxP) {
     SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
                                             w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, w->s));
     SWPS_TRY(w->d_tmp.ensure(sb));
-    const uint64_t max_items = 2ULL * U + M / kChunk + 1;
+    const uint64_t max_items = 2ULL * U + M / multi_chunk(w, maxP) + 1;
+    SWPS_TRY(w->d_lead.ensure((max_items / 8 + 2) * 4));
     SWPS_TRY(w->d_seg.ensure(U * 16));
     SWPS_TRY(w->d_icnt.ensure((2ULL * U + 1) * 4));
     SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
@@ -2902,14 +3016,16 @@ __global__ void k_seg_bounds(const uint32_t *__restrict__ keys, const uint32_t *
 // chunks of <= CH records per (key, kind) from the bounds; cnt[2U] = 0 (the
 // scan's tail).  Profiled passes (gstats) also add the records / items to
 // gstats[0..1].
-__global__ void k_seg_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t *__restrict__ cnt,
-                             unsigned long long *__restrict__ gstats) {
+__global__ void k_seg_counts(const uint32_t *__restrict__ seg, uint32_t U, uint32_t CH, uint32_t CHM,
+                             uint32_t *__restrict__ cnt, unsigned long long *__restrict__ gstats) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long rc = 0, ic = 0, mr = 0, mi = 0;
   if (u == U) cnt[2 * U] = 0;
   if (u < U) {
     const uint32_t a = seg[u], lo = seg[U + u], b = seg[3 * U + u];
-    const uint32_t ch = (lo - a + CH - 1) / CH, cv = (b - lo + CH - 1) / CH;
+    // a run of <= CH records is one item; longer runs are chunks of CHM <= CH
+    const uint32_t nh = lo - a, nv = b - lo;
+    const uint32_t ch = nh <= CH ? (nh > 0) : (nh + CHM - 1) / CHM, cv = nv <= CH ? (nv > 0) : (nv + CHM - 1) / CHM;
     cnt[2 * u] = ch;
     cnt[2 * u + 1] = cv;
     rc = b - a;
@@ -2962,8 +3078,9 @@ int prep_batch(swps_w2v *w) {
   if (will_sort) {  // zeroed by k_batch_setup: keys without records keep empty segments
     SWPS_TRY(w->d_seg.ensure((uint64_t)U * 16));
     // leaders: at most 2 per 17 items (a run of kGroup + 1 chunks has two)
-    SWPS_TRY(w->d_lead.ensure(((2ULL * U + P * (uint64_t)(N + 1 + 2 * W) / kChunk + 1) / 8 + 2) * 4));
-    SWPS_TRY(w->d_multi.ensure((2ULL * U + P * (uint64_t)(N + 1 + 2 * W) / kChunk + 2) * 4));
+    const uint64_t mi = 2ULL * U + P * (uint64_t)(N + 1 + 2 * W) / multi_chunk(w, P) + 1;  // max items
+    SWPS_TRY(w->d_lead.ensure((mi / 8 + 2) * 4));
+    SWPS_TRY(w->d_multi.ensure((mi + 1) * 4));
   }
   if (U || recs) {
     k_batch_setup<<<nblk(std::max<uint64_t>(U, recs ? nt : 0)), 256, 0, s>>>(
@@ -3037,7 +3154,8 @@ int prep_batch(swps_w2v *w) {
       SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
       k_seg_bounds<<<nblk(M), 256, 0, s>>>(w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (uint32_t)M,
                                             (uint32_t)HOFF, U, w->d_seg.as<uint32_t>());
-      k_seg_counts<<<nblk((uint64_t)U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, w->d_icnt.as<uint32_t>(),
+      const uint32_t chm = multi_chunk(w, P);
+      k_seg_counts<<<nblk((uint64_t)U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, chm, w->d_icnt.as<uint32_t>(),
                                                           tm.on ? w->d_gstats.as<unsigned long long>() : nullptr);
       SWPS_HIP(hipGetLastError());
       size_t ib = 0;
@@ -3047,7 +3165,7 @@ int prep_batch(swps_w2v *w) {
       ib = w->d_tmp.bytes;
       SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(w->d_tmp.p, ib, w->d_icnt.as<uint32_t>(), w->d_ioff.as<uint32_t>(),
                                                 (int)(2 * U + 1), s));
-      const uint64_t max_items = 2ULL * U + M / kChunk + 1;
+      const uint64_t max_items = 2ULL * U + M / chm + 1;
       SWPS_TRY(w->d_desc.ensure(max_items * 16));
       // multi-chunk items in the order of their first record's position when
       // the batch's neu1 / neu1e rows outgrow the Infinity Cache: concurrently
@@ -3064,7 +3182,7 @@ int prep_batch(swps_w2v *w) {
         mo = MultiOrder{w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(),
                         (uint32_t)P, HOFF, shift};
       }
-      k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk,
+      k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk, chm,
                                                    max_items, w->d_desc.as<uint4>(), w->d_lead.as<uint32_t>(),
                                                    w->d_multi.as<uint32_t>(), mo);
       SWPS_HIP(hipGetLastError());
@@ -3160,8 +3278,9 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
                      w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad), w->d_lead.as<uint32_t>(),
                      (uint32_t)pb.max_items, fused ? w->d_multi.as<uint32_t>() : nullptr};
-    // multi-chunk items: at most M / kChunk full chunks plus one partial chunk per run of > kChunk records
-    const uint64_t gitems = fused ? std::min<uint64_t>(pb.max_items, 2 * pb.M / kChunk + 1) : pb.max_items;
+    // multi-chunk items: at most M / chm full chunks plus one partial chunk per run of > kChunk records
+    const uint64_t gitems =
+        fused ? std::min<uint64_t>(pb.max_items, pb.M / multi_chunk(w, P) + pb.M / kChunk + 1) : pb.max_items;
     const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(gitems * 64), (uint64_t)w->gather_grid);
     const unsigned cgrid = combine_grid(pb.max_items);
     hipEvent_t eg = tm.begin(s);
@@ -3211,7 +3330,11 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (fused) {
-        if (w->push_tg_var == 1)
+        if (w->push_tg_var == 3)
+          k_push_th<1, 8><<<nblk((uint64_t)U * 128), 256, 0, s>>>(pa);
+        else if (w->push_tg_var == 4)
+          k_push_th<1, 16><<<nblk((uint64_t)U * 128), 256, 0, s>>>(pa);
+        else if (w->push_tg_var == 1)
           k_push_tg<1, 8, 4><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);  // occupancy 4, 5 VGPRs spilled
         else if (w->push_tg_var == 2)
           k_push_tg<1, 4, 1><<<nblk((uint64_t)U * 64), 256, 0, s>>>(pa);
@@ -3342,6 +3465,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_FUSED_PUSH")) w->fused_push = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_PUSH_TG")) w->push_tg_var = atoi(e);          // A/B timing
   if (const char *e = getenv("SWPS_MULTI_SORT")) w->multi_sort = atoi(e);        // A/B timing
+  if (const char *e = getenv("SWPS_MULTI_CHUNK")) w->multi_chunk = (uint32_t)std::min(128, std::max(0, atoi(e)));
   if (const char *e = getenv("SWPS_MULTI_SORT_MIN")) w->multi_sort_min = strtoull(e, nullptr, 10);
   if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_UNI_INDEX")) w->uni_index = atoi(e) != 0;  // A/B timing
