@@ -602,16 +602,30 @@ def bench_other(args):
         m.set_profile(False)
         dt, total = finish(dt, steps * B1)
         # SURVEY.md §8(d) LR bytes, over the profiled pass's rows [warm+steps, warm+2*steps) batches:
-        # k_lr_forward per example: fvid, fval, weight, contribution, key (4 B each) per feature + 16 B
-        # (row offset, label, err^2); the step: F*28 per example + 32 per unique key of each batch
+        # k_lr_forward: per feature its shard row index, x_i and weight (4 B each); per example 20 B
+        # (row offset, label, e, e^2).  Push (k_lr_records + k_lr_reduce_*, the push timer): per
+        # feature the sorted (row, x_i), the gathered e and the record written then read back (20 B);
+        # per unique key its run (key, count, offset, shard row: 16 B) + the [w | g2] row read and
+        # written (16 B).
         r0, r1 = (warm + steps) * B1, (warm + 2 * steps) * B1
         nnz = int(off[r1] - off[r0])
         uniq = sum(len(np.unique(f[off[(warm + steps + k) * B1]:off[(warm + steps + k + 1) * B1]]))
                    for k in range(steps))
         fwd_ms, fwd_n = kt["forward"]
-        fwd_bytes = 20 * nnz + 16 * (r1 - r0)
+        fwd_bytes = 12 * nnz + 20 * (r1 - r0)
         fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
-        step_gbs = (28 * nnz + 32 * uniq) * world / dt / 1e9
+        push_ms, push_n = kt.get("push", (0.0, 0))
+        push_bytes = 20 * nnz + 32 * uniq
+        push_gbs = push_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
+        step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
+        kf = {"kernel": "k_lr_forward", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
+              "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
+        kp = {"kernel": "k_lr_records + k_lr_reduce_short + k_lr_reduce_long%s (per-key mean + AdaGrad push)"
+                        % ("" if args.lr_exact else "_fast"),
+              "achieved": push_gbs, "frac": push_gbs / HBM_PEAK_GBS,
+              "bytes_per_launch": push_bytes / max(push_n, 1), "avg_launch_ms": push_ms / max(push_n, 1),
+              "launches": push_n}
+        dom, other = (kp, kf) if push_ms >= fwd_ms else (kf, kp)
         out = {"metric": "sparse LR trained examples/sec (AdaGrad, key-sharded PS)", "value": total / dt,
                "unit": "examples/s", "n_gpus": world, "steps": steps, "warmup": warm,
                "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -626,12 +640,11 @@ def bench_other(args):
                           else "fast (fp64 per-key sums, wave tree-reduced; within 1e-5 of the oracle)",
                           "features_per_s": total * nnz / max(r1 - r0, 1) / dt,
                           "unique_keys_per_step": uniq / steps},
-               "roofline": {"bound": "hbm", "kernel": "k_lr_forward", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": fwd_gbs / HBM_PEAK_GBS, "traffic": None,
-                            "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1),
-                            "launches": fwd_n, "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
-                            "note": "a 65k-row step is ~76 MB of algorithmic traffic: launch/sort latency, not "
-                                    "HBM, bounds it"},
+               "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s", traffic=None,
+                                step_GBps=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS, other=other,
+                                note="a 65k-row step is ~80 MB of algorithmic traffic in 4-B random accesses "
+                                     "(weights, e gathers, row read-modify-writes): access latency, not HBM "
+                                     "bandwidth, bounds it"),
                "kernel_ms": {k: v[0] for k, v in kt.items() if v[1]}}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_lr(y, off, f, v, args.lr_batch, lr_rate, args.cpu_rows)

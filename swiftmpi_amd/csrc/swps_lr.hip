@@ -297,6 +297,35 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long(LrReduce a) {
   }
 }
 
+// fast_sums, long runs (hot features: up to one record per row of the batch):
+// one 256-thread block per run, 8 loads in flight per thread, fp64 partial per
+// thread -> wave sums -> the 4 wave sums added in wave order (fixed order:
+// deterministic run to run).
+__global__ __launch_bounds__(256) void k_lr_reduce_long_fast(LrReduce a) {
+  __shared__ double ws[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t NL = *a.nlong;
+  for (uint32_t q = blockIdx.x; q < NL; q += gridDim.x) {
+    const uint32_t r = a.longs[q];
+    const uint32_t o = a.off[r], c = a.cnt[r];
+    double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    uint32_t k = t;
+    for (; k + 7 * 256 < c; k += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = a.val[o + k + j * 256];
+#pragma unroll
+      for (int j = 0; j < 8; j++) s8[j] += (double)v[j];
+    }
+    for (; k < c; k += 256) s8[0] += (double)a.val[o + k];
+    const double tot = wave_sum_pl(((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7])));
+    if (lane == 0) ws[wv] = tot;
+    __syncthreads();
+    if (t == 0) lr_apply(a, r, 0.f, c, ((ws[0] + ws[1]) + (ws[2] + ws[3])));
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void k_lr_predict(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
                              const float *__restrict__ fval, uint64_t nr, const uint32_t *__restrict__ vid_row,
                              const float *__restrict__ rows, float *__restrict__ pred) {
@@ -561,7 +590,10 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
               l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, l->d_local.as<int32_t>(),
               l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
   k_lr_reduce_short<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(ra);
-  k_lr_reduce_long<<<(unsigned)std::min<uint64_t>(nblk(nnz * 64 / kLrShort), 2048), 256, 0, s>>>(ra);
+  if (l->cfg.fast_sums)
+    k_lr_reduce_long_fast<<<(unsigned)std::min<uint64_t>(nblk(nnz * 256 / kLrShort), 4096), 256, 0, s>>>(ra);
+  else
+    k_lr_reduce_long<<<(unsigned)std::min<uint64_t>(nblk(nnz * 64 / kLrShort), 2048), 256, 0, s>>>(ra);
   SWPS_HIP(hipGetLastError());
   l->timer.end(3, e3, s);
   return SWPS_OK;
