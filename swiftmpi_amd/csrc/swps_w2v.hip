@@ -1245,6 +1245,7 @@ template <typename T, typename A> struct PushArgs {
   uint64_t HOFF;
   uint32_t P;
   int ld;
+  const uint32_t *krow;  // k_push_thp: shard row per batch key (k_batch_setup)
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
@@ -1632,6 +1633,147 @@ __global__ __launch_bounds__(256) void k_push_th(PushArgs<float, float> a) {
   }
 }
 
+// k_push_th software-pipelined across (key, half) items, like k_gather_t:
+// a wave walks a stride of items; the next item's bounds / key / shard row are
+// loaded at the top and its record info right behind this item's row loads,
+// so the per-item chain (bounds -> records -> g -> rows, key -> shard row ->
+// w rows) overlaps the previous item's traffic.  Same arithmetic: bit-identical.
+struct PHead {
+  uint32_t s0, s1, i0, i1;
+  int32_t vid;
+  uint32_t row;
+};
+template <int NCH, int UNR>
+__global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
+  constexpr int PU = 8;
+  const int lane = threadIdx.x & 63;
+  const int D = a.D;
+  const bool tl = 256 * NCH + lane < D;
+  const uint64_t n2 = 2ull * a.U;
+  const uint64_t stride = (uint64_t)gridDim.x * 4;
+  uint64_t uh = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (uh >= n2) return;
+  auto head = [&](uint64_t x) {
+    const uint64_t u = x >> 1;
+    const int half = (int)(x & 1);
+    PHead h;
+    h.s0 = __builtin_amdgcn_readfirstlane(a.seg[(2 * half) * a.U + u]);
+    h.s1 = __builtin_amdgcn_readfirstlane(a.seg[(2 * half + 1) * a.U + u]);
+    h.i0 = __builtin_amdgcn_readfirstlane(a.ioff[2 * u + half]);
+    h.i1 = __builtin_amdgcn_readfirstlane(a.ioff[2 * u + half + 1]);
+    h.vid = __builtin_amdgcn_readfirstlane(a.K[u]);
+    h.row = __builtin_amdgcn_readfirstlane(a.krow[u]);
+    return h;
+  };
+  PHead h = head(uh);
+  ItemRecs ri{0, 0, 1.f, 1.f};
+  if (h.s1 > h.s0 && h.i1 - h.i0 == 1) ri = run_recs(a.vals, a.pg, a.P, a.HOFF, h.s0, h.s1 - h.s0, (int)(uh & 1), lane);
+  for (;;) {
+    const uint64_t nx = uh + stride;
+    const bool more = nx < n2;
+    PHead hn{0, 0, 0, 0, 0, 0};
+    if (more) hn = head(nx);
+    const int half = (int)(uh & 1);
+    if (lane == 0 && half == 0) a.local[h.vid] = -1;
+    const uint32_t cnt = h.s1 - h.s0;
+    const bool one = h.i1 - h.i0 == 1;
+    float *row = a.rows + (uint64_t)h.row * 4 * D;
+    FSlice<NCH> wr, w2r, pf;
+    ItemRecs rn{0, 0, 1.f, 1.f};
+    bool rn_done = false;
+    auto next_recs = [&]() {
+      if (more && hn.s1 > hn.s0 && hn.i1 - hn.i0 == 1)
+        rn = run_recs(a.vals, a.pg, a.P, a.HOFF, hn.s0, hn.s1 - hn.s0, (int)(nx & 1), lane);
+      rn_done = true;
+    };
+    if (cnt || a.cache_h) wr.ld(row + half * D, lane, tl);
+    if (cnt) {
+      if (!one) pf.ld(a.partial + (uint64_t)h.i0 * D, lane, tl);
+      w2r.ld(row + (2 + half) * D, lane, tl);
+    }
+    if (a.cache_h) wr.st((half ? a.cache_v : a.cache_h) + (uint64_t)h.vid * a.cs, lane, tl);  // pre-update value
+    if (cnt) {
+      FAcc<NCH> acc;
+      acc.zero();
+      if (one) {
+        const float *base = half == 0 ? a.neu1 : a.neu1e;
+        FAcc<NCH> c;
+        c.zero();
+        for (uint32_t r0 = 0; r0 < cnt; r0 += UNR) {
+          FSlice<NCH> rv[UNR];
+          float gf[UNR];
+#pragma unroll
+          for (int q = 0; q < UNR; q++) {
+            const uint32_t idx = min(r0 + q, cnt - 1);
+            const uint32_t pr = idx < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)ri.p0, (int)idx)
+                                         : (uint32_t)__builtin_amdgcn_readlane((int)ri.p1, (int)(idx - 64));
+            gf[q] = __int_as_float(idx < 64 ? __builtin_amdgcn_readlane(__float_as_int(ri.g0), (int)idx)
+                                            : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
+            rv[q].ld(base + (uint64_t)pr * a.ld, lane, tl);
+          }
+          if (r0 == 0) next_recs();  // behind this item's first rows
+#pragma unroll
+          for (int q = 0; q < UNR; q++) {
+            if (r0 + q < cnt) {
+              if (half == 0)
+                c.axpy((double)gf[q], rv[q], tl);
+              else
+                c.add(rv[q], tl);
+            }
+          }
+        }
+#pragma unroll
+        for (int cc = 0; cc < NCH; cc++)
+#pragma unroll
+          for (int k = 0; k < 4; k++) acc.v[cc][k] = (double)(float)c.v[cc][k];  // the fp32 partial
+        acc.t = (double)(float)c.t;
+      } else {
+        next_recs();
+        acc.add(pf, tl);
+        const uint32_t st = (h.i1 - h.i0) > kGroup ? kGroup : 1;
+        for (uint32_t it0 = h.i0 + st; it0 < h.i1; it0 += PU * st) {
+          FSlice<NCH> pv[PU];
+#pragma unroll
+          for (int q = 0; q < PU; q++) pv[q].ld(a.partial + (uint64_t)min(it0 + q * st, h.i1 - 1) * D, lane, tl);
+#pragma unroll
+          for (int q = 0; q < PU; q++)
+            if (it0 + q * st < h.i1) acc.add(pv[q], tl);
+        }
+      }
+      const double inv = (double)cnt;
+      float *w = row + half * D, *w2 = row + (2 + half) * D;
+      auto upd = [&](double sum, float wv, float w2v, float &wo, float &w2o) {
+        const double g = (double)(float)(sum / inv);  // the mean in the push payload's type
+        const double acc2 = (double)w2v + g * g;
+        const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
+        w2o = (float)acc2;
+        wo = (float)((double)wv + step);
+      };
+#pragma unroll
+      for (int c = 0; c < NCH; c++) {
+        float4 wo, w2o;
+        upd(acc.v[c][0], wr.v[c].x, w2r.v[c].x, wo.x, w2o.x);
+        upd(acc.v[c][1], wr.v[c].y, w2r.v[c].y, wo.y, w2o.y);
+        upd(acc.v[c][2], wr.v[c].z, w2r.v[c].z, wo.z, w2o.z);
+        upd(acc.v[c][3], wr.v[c].w, w2r.v[c].w, wo.w, w2o.w);
+        ((float4 *)w2)[lane + c * 64] = w2o;
+        ((float4 *)w)[lane + c * 64] = wo;
+      }
+      if (tl) {
+        float wo, w2o;
+        upd(acc.t, wr.t, w2r.t, wo, w2o);
+        w2[256 * NCH + lane] = w2o;
+        w[256 * NCH + lane] = wo;
+      }
+    }
+    if (!rn_done) next_recs();
+    if (!more) break;
+    uh = nx;
+    h = hn;
+    ri = rn;
+  }
+}
+
 // requester side of a sharded pull: the owners' pull values [U][h|v] (K order)
 // into the worker cache (global_pull_access.h:88-97: params[key] = val)
 template <typename T>
@@ -1778,12 +1920,16 @@ struct swps_w2v {
   swps::ShardDriver *drv = nullptr;  // swps_w2v_shard_comm: the library drives the exchange
   bool rec_generic = false;          // SWPS_REC_GENERIC=1: the generic k_records (A/B, tests)
   DevMem d_lead;  // hot-group leaders of the batch's gather items: [0] = count, then item indices
-  DevMem d_multi;  // items of multi-chunk runs (k_gather_t's work when k_push_tg runs): [0] = count, then items
-  int fused_push = 1;
-  int push_tg_var = 0;
-  uint32_t multi_chunk = 0;  // SWPS_MULTI_CHUNK: chunk size of multi-chunk runs (1..128; 0 = by batch size)
+  DevMem d_multi;  // items of multi-chunk runs (k_gather_t's work when the push is fused): [0] = count, then items
+  DevMem d_krow;   // per batch key: its shard row (vid_row[K[u]]), for k_push_thp
+  int fused_push = 1;  // fast mode: the push sums single-chunk runs itself (SWPS_FUSED_PUSH=0: k_gather_t + k_push_t)
+  int push_tg_var = 5;  // fused push kernel (SWPS_PUSH_TG, A/B): 5 = k_push_thp (default), 0 = k_push_tg UNR 8,
+                        // 1 = k_push_tg at occupancy 4, 2 = k_push_tg UNR 4, 3 = k_push_th, 4 = k_push_th UNR 16
+  uint32_t push_grid = 0;
+  int fwd_g = 4;  // k_forward_t rows in flight per wave (SWPS_FWD_G: 4, 8, 16; A/B)  // k_push_thp grid cap in blocks (SWPS_PUSH_GRID; 0 = by batch size)
+  uint32_t multi_chunk = 0;  // SWPS_MULTI_CHUNK: chunk size of multi-chunk runs (1..128; 0 = kChunk)
   int multi_sort = 1;                 // order the multi-chunk items by position (SWPS_MULTI_SORT=0: off; A/B)
-  uint64_t multi_sort_min = 65536;    // ... for batches of at least this many kept positions (SWPS_MULTI_SORT_MIN)  // k_push_tg variant (SWPS_PUSH_TG: 0 = UNR 8, 1 = UNR 8 at occupancy 4, 2 = UNR 4; A/B)  // fast mode: k_push_tg sums single-chunk runs itself (SWPS_FUSED_PUSH=0: k_gather_t + k_push_t)
+  uint64_t multi_sort_min = 65536;    // ... for batches of at least this many kept positions (SWPS_MULTI_SORT_MIN)
   uint64_t *h_small = nullptr;  // pinned readback
   // RNG (utils/random.h:44-47, seed 2008)
   uint64_t lstate = 2008ULL;
@@ -1818,7 +1964,7 @@ struct swps_w2v {
   // overlapped single-GPU driver (train_overlapped): the second set of the
   // parameter-independent per-batch buffers, swapped with the members above,
   // and the stream prep(i+1) runs on while learn(i) runs on s
-  static constexpr int kPrepBufs = 14;
+  static constexpr int kPrepBufs = 15;
   DevMem alt[kPrepBufs];
   bool alt_local_ready = false;
   // train_overlapped: -1 = auto (on for minibatches of at most kOverlapTok tokens: at B = 100 lines the
@@ -1829,7 +1975,7 @@ struct swps_w2v {
   hipStream_t s_prep = nullptr;
   hipEvent_t ev_learn = nullptr, ev_prep = nullptr;
   DevMem *prep_set[kPrepBufs] = {&d_pos_tok, &d_rec,  &d_pkeys, &d_pvals, &d_pkeys_s, &d_pvals_s, &d_tmp,
-                                 &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_multi, &d_local};
+                                 &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_multi, &d_krow, &d_local};
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
   uint64_t st_sums = 0, st_fused = 0;  // batches with gradient sums; of those, pushed by k_push_tg
@@ -2976,9 +3122,11 @@ __global__ void k_set_local(const int32_t *__restrict__ K, uint32_t U, int32_t *
 __global__ void k_batch_setup(const int32_t *__restrict__ K, uint32_t U, int32_t *__restrict__ local,
                               const int32_t *__restrict__ kscan, uint64_t t0, uint64_t nt,
                               int32_t *__restrict__ pos_tok, uint4 *__restrict__ seg0, uint32_t *__restrict__ lead,
-                              uint32_t *__restrict__ multi) {
+                              uint32_t *__restrict__ multi, const uint32_t *__restrict__ vid_row,
+                              uint32_t *__restrict__ krow) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < U) local[K[i]] = (int32_t)i;
+  if (krow && i < U) krow[i] = vid_row[K[i]];  // the batch keys' shard rows (k_push_thp)
   if (seg0 && i < U) seg0[i] = make_uint4(0, 0, 0, 0);  // seg[4][U] u32 = U x 16 B: keys without records
   if (lead && i == 0) lead[0] = 0;
   if (multi && i == 0) multi[0] = 0;
@@ -3082,11 +3230,15 @@ int prep_batch(swps_w2v *w) {
     SWPS_TRY(w->d_lead.ensure((mi / 8 + 2) * 4));
     SWPS_TRY(w->d_multi.ensure((mi + 1) * 4));
   }
+  // the fused push's per-key shard rows (single GPU)
+  const bool krow = U > 0 && !w->sharded && w->tail && w->fused_push && w->push_tg_var == 5;
+  if (krow) SWPS_TRY(w->d_krow.ensure((uint64_t)U * 4));
   if (U || recs) {
     k_batch_setup<<<nblk(std::max<uint64_t>(U, recs ? nt : 0)), 256, 0, s>>>(
         K, U, w->d_local.as<int32_t>(), w->d_kscan.as<int32_t>(), t0, recs ? nt : 0,
         recs ? w->d_pos_tok.as<int32_t>() : nullptr, will_sort ? w->d_seg.as<uint4>() : nullptr,
-        will_sort ? w->d_lead.as<uint32_t>() : nullptr, will_sort ? w->d_multi.as<uint32_t>() : nullptr);
+        will_sort ? w->d_lead.as<uint32_t>() : nullptr, will_sort ? w->d_multi.as<uint32_t>() : nullptr,
+        w->d_vid_row.as<uint32_t>(), krow ? w->d_krow.as<uint32_t>() : nullptr);
     SWPS_HIP(hipGetLastError());
   }
   if (recs) {
@@ -3250,7 +3402,12 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
         if (D < 512) {
-          k_forward_t<1, 4, 1><<<nblk(P * 64), 256, 0, s>>>(fa);  // G = 4: occupancy 7 (A/B: G = 2..8)
+          if (w->fwd_g == 8)
+            k_forward_t<1, 8, 1><<<nblk(P * 64), 256, 0, s>>>(fa);
+          else if (w->fwd_g == 16)
+            k_forward_t<1, 16, 1><<<nblk(P * 64), 256, 0, s>>>(fa);
+          else
+            k_forward_t<1, 4, 1><<<nblk(P * 64), 256, 0, s>>>(fa);  // G = 4: occupancy 7 (A/B: G = 2..8)
         } else if (D < 768)
           k_forward_t<2, 8, 1><<<nblk(P * 64), 256, 0, s>>>(fa);
         else
@@ -3326,11 +3483,17 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads,
                       d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs,
                       w->d_pvals_s.as<uint32_t>(), w->d_pg.as<float>(), w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                      pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad)};
+                      pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad), w->d_krow.as<uint32_t>()};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (fused) {
-        if (w->push_tg_var == 3)
+        if (w->push_tg_var == 5)
+          // small batches are latency-bound: several items per wave, and the idle CUs run the prep stream
+          // (A/B at B = 100 lines: 2048 blocks 0.317 ms/step, 4096 0.323, one item per wave 0.331); large ones want every item in flight
+          k_push_thp<1, 8><<<(unsigned)std::min<uint64_t>(nblk((uint64_t)U * 128),
+                                                          w->push_grid ? w->push_grid : (U < 65536 ? 2048 : ~0u)),
+                             256, 0, s>>>(pa);
+        else if (w->push_tg_var == 3)
           k_push_th<1, 8><<<nblk((uint64_t)U * 128), 256, 0, s>>>(pa);
         else if (w->push_tg_var == 4)
           k_push_th<1, 16><<<nblk((uint64_t)U * 128), 256, 0, s>>>(pa);
@@ -3464,6 +3627,8 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_PUSH_T")) w->push_t = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_FUSED_PUSH")) w->fused_push = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_PUSH_TG")) w->push_tg_var = atoi(e);          // A/B timing
+  if (const char *e = getenv("SWPS_FWD_G")) w->fwd_g = atoi(e);
+  if (const char *e = getenv("SWPS_PUSH_GRID")) w->push_grid = (uint32_t)std::max(0, atoi(e));
   if (const char *e = getenv("SWPS_MULTI_SORT")) w->multi_sort = atoi(e);        // A/B timing
   if (const char *e = getenv("SWPS_MULTI_CHUNK")) w->multi_chunk = (uint32_t)std::min(128, std::max(0, atoi(e)));
   if (const char *e = getenv("SWPS_MULTI_SORT_MIN")) w->multi_sort_min = strtoull(e, nullptr, 10);

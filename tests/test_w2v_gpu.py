@@ -376,7 +376,7 @@ def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch):
     outs, negs = [], []
     variants = (("1", "1", "1", "1", "1", "0"), ("0", "1", "1", "1", "1", "0"), ("1", "0", "1", "1", "1", "0"),
                 ("1", "1", "0", "1", "1", "0"), ("1", "1", "1", "0", "1", "0"), ("1", "1", "1", "1", "0", "0"),
-                ("1", "1", "1", "1", "1", "1"), ("1", "1", "1", "1", "1", "2"), ("1", "1", "1", "1", "1", "3"), ("1", "1", "1", "1", "1", "4"),
+                ("1", "1", "1", "1", "1", "1"), ("1", "1", "1", "1", "1", "2"), ("1", "1", "1", "1", "1", "3"), ("1", "1", "1", "1", "1", "4"), ("1", "1", "1", "1", "1", "5"),
                 ("1", "1", "1", "1", "1", "sort"))
     for push_t, pad, uidx, cpad, fused, tgv in variants:
         # "sort": the multi-chunk gather items in position order even for these small batches
