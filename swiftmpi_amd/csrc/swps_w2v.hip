@@ -254,7 +254,7 @@ struct RecArgs {
   const uint32_t *vid_row;  // direct table reads (single GPU): slots of pulled keys hold kTabRow | table row
   int32_t *rec;     // [P][RS]: word, ctx x 2W (-1 = none), target x (N+1) (-1 = skipped); each a cache vid
                     // or kTabRow | table row (slot_row)
-  uint32_t *pkeys, *pvals;  // slot-major: h record (p,d) at d*P+p; v record (p,j) at (N+1)*P + j*P+p
+  uint32_t *pkeys, *pvals;  // position-major: h record (p,d) at p*(N+1)+d; v record (p,j) at (N+1)*P + p*2W+j
   int32_t *trace;
   unsigned long long *rows_touched;
 };
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
         }
       }
       r[1 + j] = src;
-      const uint64_t k = HOFF + (uint64_t)j * P + p;
+      const uint64_t k = HOFF + p * (uint64_t)(2 * W) + j;
       a.pkeys[k] = key;
       a.pvals[k] = (uint32_t)k;
     }
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
         }
       }
       r[1 + 2 * W + d] = src;
-      const uint64_t k = (uint64_t)d * P + p;
+      const uint64_t k = p * (uint64_t)(N + 1) + d;
       a.pkeys[k] = key;
       a.pvals[k] = (uint32_t)k;
     }
@@ -473,12 +473,12 @@ __global__ __launch_bounds__(256) void k_records_t(RecArgs a) {
     int32_t ts[N + 1];
 #pragma unroll
     for (int d = 0; d <= N; d++) ts[d] = (tu[d] >= 0 && a.vid_row) ? (kTabRow | (int32_t)a.vid_row[tv[d]]) : tv[d];
-    // ---- stores: position record (LDS), gradient records (slot-major) ----
+    // ---- stores: position record (LDS), gradient records (position-major) ----
 #pragma unroll
     for (int j = 0; j < 2 * W; j++) {
       nctx += cv[j] >= 0;
       r[1 + j] = cs[j];
-      const uint64_t k = HOFF + (uint64_t)j * P + p;
+      const uint64_t k = HOFF + p * (uint64_t)(2 * W) + j;
       a.pkeys[k] = cu[j] >= 0 ? (uint32_t)cu[j] : a.U;
       a.pvals[k] = (uint32_t)k;
     }
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void k_records_t(RecArgs a) {
     for (int d = 0; d <= N; d++) {
       ntgt += tv[d] >= 0;
       r[1 + 2 * W + d] = ts[d];
-      const uint64_t k = (uint64_t)d * P + p;
+      const uint64_t k = p * (uint64_t)(N + 1) + d;
       a.pkeys[k] = tu[d] >= 0 ? (uint32_t)tu[d] : a.U;
       a.pvals[k] = (uint32_t)k;
     }
@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256) void k_forward_b8(FwdArgs<T, A> a) {
             ne[c][k] += prod;
           }
     }
-    if ((lane & 7) == 0 && d >= 0 && d <= N) a.pg[(uint64_t)d * a.P + p] = (tmask >> (lane >> 3)) & 1 ? g : 0.f;
+    if ((lane & 7) == 0 && d >= 0 && d <= N) a.pg[(uint64_t)p * (N + 1) + d] = (tmask >> (lane >> 3)) & 1 ? g : 0.f;
   }
 #pragma unroll
   for (int c = 0; c < NCH; c++) {
@@ -790,7 +790,7 @@ __global__ __launch_bounds__(256) void k_forward(FwdArgs<T, A> a) {
       CA::st(a.neu1e + (uint64_t)p * a.ld, ci, D, ne[c]);
     }
   }
-  if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
+  if (lane <= N) a.pg[(uint64_t)p * (N + 1) + lane] = gk;
 }
 
 // Fast mode (fp32 rows, fp32 intermediates) when D = 256*NCH + tail with
@@ -918,7 +918,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   acc.st(a.neu1 + (uint64_t)p * a.ld, lane, tl);
   ne.st(a.neu1e + (uint64_t)p * a.ld, lane, tl);
-  if (lane <= N) a.pg[(uint64_t)lane * a.P + p] = gk;
+  if (lane <= N) a.pg[(uint64_t)p * (N + 1) + lane] = gk;
 }
 
 constexpr uint32_t kGroupDesc = 16;  // = kGroup (k_combine's group size)
@@ -929,7 +929,7 @@ constexpr uint32_t kGroupDesc = 16;  // = kGroup (k_combine's group size)
 struct MultiOrder {  // k_item_desc: sort keys of the multi-chunk items by their first record's position
   uint32_t *key, *item;  // [max_items]: coarse position (kMultiPad for the rest) and item index; null = unsorted
   const uint32_t *vals;  // the sorted records
-  uint32_t P;
+  uint32_t SH, SV;  // record slots per position: N+1 targets (h), 2W contexts (v)
   uint64_t HOFF;
   int shift;  // coarse position = p >> shift (< kMultiPad)
 };
@@ -956,10 +956,10 @@ __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__
     const bool m = live && ioff[lo + 1] - ioff[lo] > 1;
     if (mo.key && item < max_items) {
       uint32_t key = kMultiPad;
-      if (m) {  // the chunk's first record: index slot*P + p (v records after HOFF)
+      if (m) {  // the chunk's first record: index p*SH + d (h), HOFF + p*SV + j (v)
         const uint32_t jj = lo, u = jj >> 1, kind = jj & 1, k = (uint32_t)item - ioff[jj];
         const uint32_t pi = mo.vals[seg[(2 * kind) * U + u] + k * CHM];
-        key = (uint32_t)((kind ? (uint64_t)pi - mo.HOFF : (uint64_t)pi) % mo.P) >> mo.shift;
+        key = (kind ? (uint32_t)((uint64_t)pi - mo.HOFF) / mo.SV : pi / mo.SH) >> mo.shift;
       }
       mo.key[item] = key;
       mo.item[item] = (uint32_t)item;
@@ -1000,6 +1000,7 @@ template <typename A> struct GatherArgs {
   const uint32_t *lead;  // hot-group leaders (k_item_desc): [0] = count, then items
   uint32_t max_items;    // capacity of desc / partial: a bound on ioff[2U] every reader clamps to
   const uint32_t *multi;  // k_gather_t: only these items ([0] = count; the multi-chunk runs'), or null = all
+  uint32_t SH, SV;        // record slots per position: N+1 (h records), 2W (v records)
 };
 
 // One wave per chunk of <= 128 records of one (key, kind): the fp64 sum, in
@@ -1019,23 +1020,23 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
     const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
     uint32_t p0 = 0, p1 = 0;
     float g0 = 1.f, g1 = 1.f;
-    // records are slot-major: index = slot*P + p (v records after HOFF)
+    // records are position-major: index = p*SH + d (h), HOFF + p*SV + j (v)
     if (lane < (int)n) {
       const uint32_t pi = a.vals[s + lane];
       if (kind == 0) {
-        p0 = pi % a.P;
+        p0 = pi / a.SH;
         g0 = a.pg[pi];
       } else {
-        p0 = (uint32_t)((pi - a.HOFF) % a.P);
+        p0 = (uint32_t)(pi - a.HOFF) / a.SV;
       }
     }
     if (lane + 64 < (int)n) {
       const uint32_t pi = a.vals[s + 64 + lane];
       if (kind == 0) {
-        p1 = pi % a.P;
+        p1 = pi / a.SH;
         g1 = a.pg[pi];
       } else {
-        p1 = (uint32_t)((pi - a.HOFF) % a.P);
+        p1 = (uint32_t)(pi - a.HOFF) / a.SV;
       }
     }
     const A *base = kind == 0 ? a.neu1 : a.neu1e;
@@ -1096,26 +1097,26 @@ __device__ __forceinline__ uint4 uniform4(uint4 d) {  // wave-uniform value: kee
                     __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
 }
 
-__device__ __forceinline__ ItemRecs run_recs(const uint32_t *vals, const float *pg, uint32_t P, uint64_t HOFF,
-                                             uint32_t s, uint32_t n, uint32_t kind, int lane) {
+__device__ __forceinline__ ItemRecs run_recs(const uint32_t *vals, const float *pg, uint32_t SH, uint32_t SV,
+                                             uint64_t HOFF, uint32_t s, uint32_t n, uint32_t kind, int lane) {
   ItemRecs r{0, 0, 1.f, 1.f};
-  // records are slot-major: index = slot*P + p (v records after HOFF)
+  // records are position-major: index = p*SH + d (h), HOFF + p*SV + j (v)
   if (lane < (int)n) {
     const uint32_t pi = vals[s + lane];
     if (kind == 0) {
-      r.p0 = pi % P;
+      r.p0 = pi / SH;
       r.g0 = pg[pi];
     } else {
-      r.p0 = (uint32_t)((pi - HOFF) % P);
+      r.p0 = (uint32_t)(pi - HOFF) / SV;
     }
   }
   if (lane + 64 < (int)n) {
     const uint32_t pi = vals[s + 64 + lane];
     if (kind == 0) {
-      r.p1 = pi % P;
+      r.p1 = pi / SH;
       r.g1 = pg[pi];
     } else {
-      r.p1 = (uint32_t)((pi - HOFF) % P);
+      r.p1 = (uint32_t)(pi - HOFF) / SV;
     }
   }
   return r;
@@ -1123,7 +1124,7 @@ __device__ __forceinline__ ItemRecs run_recs(const uint32_t *vals, const float *
 
 __device__ __forceinline__ ItemRecs item_recs(const GatherArgs<float> &a, uint4 d, int lane) {
   const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
-  return run_recs(a.vals, a.pg, a.P, a.HOFF, s, n, kind, lane);
+  return run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, s, n, kind, lane);
 }
 
 // k_gather (fast mode) on FSlice rows, software-pipelined across items: most
@@ -1246,6 +1247,7 @@ template <typename T, typename A> struct PushArgs {
   uint32_t P;
   int ld;
   const uint32_t *krow;  // k_push_thp: shard row per batch key (k_batch_setup)
+  uint32_t SH, SV;       // record slots per position (GatherArgs)
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
@@ -1435,7 +1437,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (cnt[half] || a.cache_h) wr[half].ld(row + half * D, lane, tl);
       if (cnt[half]) {
         if (one[half])
-          ri[half] = run_recs(a.vals, a.pg, a.P, a.HOFF, sg[2 * half], cnt[half], half, lane);
+          ri[half] = run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, sg[2 * half], cnt[half], half, lane);
         else
           pf[half].ld(a.partial + (uint64_t)i0[half] * D, lane, tl);
         w2r[half].ld(row + (2 + half) * D, lane, tl);
@@ -1553,7 +1555,7 @@ __global__ __launch_bounds__(256) void k_push_th(PushArgs<float, float> a) {
     wr.ld(row + half * D, lane, tl);
     if (cnt) {
       if (one)
-        ri = run_recs(a.vals, a.pg, a.P, a.HOFF, s0, cnt, half, lane);
+        ri = run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, s0, cnt, half, lane);
       else
         pf.ld(a.partial + (uint64_t)i0 * D, lane, tl);
       w2r.ld(row + (2 + half) * D, lane, tl);
@@ -1667,7 +1669,7 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
   };
   PHead h = head(uh);
   ItemRecs ri{0, 0, 1.f, 1.f};
-  if (h.s1 > h.s0 && h.i1 - h.i0 == 1) ri = run_recs(a.vals, a.pg, a.P, a.HOFF, h.s0, h.s1 - h.s0, (int)(uh & 1), lane);
+  if (h.s1 > h.s0 && h.i1 - h.i0 == 1) ri = run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, h.s0, h.s1 - h.s0, (int)(uh & 1), lane);
   for (;;) {
     const uint64_t nx = uh + stride;
     const bool more = nx < n2;
@@ -1683,7 +1685,7 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
     bool rn_done = false;
     auto next_recs = [&]() {
       if (more && hn.s1 > hn.s0 && hn.i1 - hn.i0 == 1)
-        rn = run_recs(a.vals, a.pg, a.P, a.HOFF, hn.s0, hn.s1 - hn.s0, (int)(nx & 1), lane);
+        rn = run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, hn.s0, hn.s1 - hn.s0, (int)(nx & 1), lane);
       rn_done = true;
     };
     if (cnt || a.cache_h) wr.ld(row + half * D, lane, tl);
@@ -3332,7 +3334,7 @@ int prep_batch(swps_w2v *w) {
         int shift = 0;
         while ((P >> shift) >= kMultiPad) shift++;
         mo = MultiOrder{w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(),
-                        (uint32_t)P, HOFF, shift};
+                        (uint32_t)(N + 1), (uint32_t)(2 * W), HOFF, shift};
       }
       k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk, chm,
                                                    max_items, w->d_desc.as<uint4>(), w->d_lead.as<uint32_t>(),
@@ -3434,7 +3436,8 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
                      w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad), w->d_lead.as<uint32_t>(),
-                     (uint32_t)pb.max_items, fused ? w->d_multi.as<uint32_t>() : nullptr};
+                     (uint32_t)pb.max_items, fused ? w->d_multi.as<uint32_t>() : nullptr, (uint32_t)(N + 1),
+                     (uint32_t)(2 * W)};
     // multi-chunk items: at most M / chm full chunks plus one partial chunk per run of > kChunk records
     const uint64_t gitems =
         fused ? std::min<uint64_t>(pb.max_items, pb.M / multi_chunk(w, P) + pb.M / kChunk + 1) : pb.max_items;
@@ -3483,7 +3486,8 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads,
                       d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs,
                       w->d_pvals_s.as<uint32_t>(), w->d_pg.as<float>(), w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                      pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad), w->d_krow.as<uint32_t>()};
+                      pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad), w->d_krow.as<uint32_t>(),
+                      (uint32_t)(N + 1), (uint32_t)(2 * W)};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (fused) {
