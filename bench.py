@@ -339,9 +339,9 @@ def main():
     # key) that goes through a partial writes it (D·ea + a 16-B descriptor read) and the
     # push reads it back (D·ea); each pushed key reads h,v,h2,v2 (4·D·es), writes them
     # (4·D·es) and its pre-update h,v to the worker cache (2·D·es) + 8 B of bounds.
-    # Fused push (k_push_tg, the fast-mode default): k_gather_t + k_combine sum only the
-    # multi-chunk runs, k_push_tg sums the single-chunk runs itself -> the group is
-    # k_gather_t + k_combine + k_push_tg, timed by the gather and push timers.
+    # Fused push (k_push_thp, the fast-mode default): k_gather_t + k_combine sum only the
+    # multi-chunk runs, k_push_thp sums the single-chunk runs itself -> the group is
+    # k_gather_t + k_combine + k_push_thp, timed by the gather and push timers.
     # Otherwise the group is k_gather_t + k_combine alone (the push is reported below).
     g_rec, g_items = g1["records"] - g0["records"], g1["items"] - g0["items"]
     g_mrec, g_mitems = g1["multi_records"] - g0["multi_records"], g1["multi_items"] - g0["multi_items"]
@@ -349,7 +349,7 @@ def main():
     gat_ms, gat_n = kt["gather"]
     push_ms, push_n = kt.get("push", (0.0, 0))
     if fused:
-        sum_kernel = "k_gather_t + k_combine + k_push_tg (segmented gradient sums + fused AdaGrad push)"
+        sum_kernel = "k_gather_t + k_combine + k_push_thp (segmented gradient sums + fused AdaGrad push)"
         gat_bytes = (g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) +
                      dp["pushed"] * (10 * es * D + 8))
         sum_ms = gat_ms + push_ms
@@ -403,9 +403,9 @@ def main():
     if os.path.exists(pmc) and not parity_main:
         prof = json.load(open(pmc))
         if {k: prof.get("config", {}).get(k) for k in mine} == mine:
-            grp = ("k_gather", "k_combine") + (("k_push_tg",) if fused else ())
+            grp = ("k_gather", "k_combine") + (("k_push_tg", "k_push_th") if fused else ())
             gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items() if k.startswith(grp)]
-            if gt and (not fused or any(k.startswith("k_push_tg") for k in prof["kernels"])):
+            if gt and (not fused or any(k.startswith(grp[2:]) for k in prof["kernels"])):
                 traffic = sum(gt)  # per step: one launch of each kernel of the group
                 traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch, %s)" % (pmc_name, " + ".join(grp))
             for k, v in prof["kernels"].items():
