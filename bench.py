@@ -345,10 +345,17 @@ def main():
     # Otherwise the group is k_gather_t + k_combine alone (the push is reported below).
     g_rec, g_items = g1["records"] - g0["records"], g1["items"] - g0["items"]
     g_mrec, g_mitems = g1["multi_records"] - g0["multi_records"], g1["multi_items"] - g0["multi_items"]
-    fused = g1["batches"] > g0["batches"] and g1["fused"] - g0["fused"] == g1["batches"] - g0["batches"]
+    nbat = g1["batches"] - g0["batches"]
+    fused = nbat > 0 and g1["fused"] - g0["fused"] == nbat
+    fused_g = nbat > 0 and g1.get("fused_grads", 0) - g0.get("fused_grads", 0) == nbat
     gat_ms, gat_n = kt["gather"]
     push_ms, push_n = kt.get("push", (0.0, 0))
-    if fused:
+    if fused_g:  # sharded learner: the fused push stops at the mean gradients (2·D·ea written per key)
+        sum_kernel = ("k_gather_t + k_combine + k_push_thp<TO_GRADS> (segmented gradient sums + fused mean "
+                      "gradients of the push payload)")
+        gat_bytes = g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) + dp["pushed"] * (2 * D * ea + 8)
+        sum_ms = gat_ms + push_ms
+    elif fused:
         sum_kernel = "k_gather_t + k_combine + k_push_thp (segmented gradient sums + fused AdaGrad push)"
         gat_bytes = (g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) +
                      dp["pushed"] * (10 * es * D + 8))
@@ -373,7 +380,7 @@ def main():
     pp = {}
     for name, nbytes in (("pull", dp["pulled"] * 4 * es * D), ("push", dp["pushed"] * (12 * es * D + 8))):
         ms, n = kt.get(name, (0.0, 0))
-        if ms > 0 and not sharded and not (fused and name == "push"):
+        if ms > 0 and not sharded and not ((fused or fused_g) and name == "push"):
             gbs = nbytes / (ms * 1e-3) / 1e9
             pp[name] = {"GBps": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": nbytes / max(n, 1),
                         "avg_launch_ms": ms / max(n, 1)}
@@ -403,9 +410,9 @@ def main():
     if os.path.exists(pmc) and not parity_main:
         prof = json.load(open(pmc))
         if {k: prof.get("config", {}).get(k) for k in mine} == mine:
-            grp = ("k_gather", "k_combine") + (("k_push_tg", "k_push_th") if fused else ())
+            grp = ("k_gather", "k_combine") + (("k_push_tg", "k_push_th") if (fused or fused_g) else ())
             gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items() if k.startswith(grp)]
-            if gt and (not fused or any(k.startswith(grp[2:]) for k in prof["kernels"])):
+            if gt and (not (fused or fused_g) or any(k.startswith(grp[2:]) for k in prof["kernels"])):
                 traffic = sum(gt)  # per step: one launch of each kernel of the group
                 traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch, %s)" % (pmc_name, " + ".join(grp))
             for k, v in prof["kernels"].items():

@@ -286,9 +286,10 @@ int swps_w2v_stats(swps_w2v *w, uint64_t *out10);
 int swps_w2v_gather_stats(swps_w2v *w, uint64_t *out2);
 /* the same split by who sums them, for the roofline of the fused sums + push: [gradient
  * records, items, records of multi-chunk (key, kind) runs (k_gather_t's share when the push
- * is fused), items of those runs, batches pushed by the fused k_push_tg, batches with
- * gradient sums] (measurement only) */
-int swps_w2v_sum_stats(swps_w2v *w, uint64_t *out6);
+ * is fused), items of those runs, batches pushed by the fused in-place k_push_thp, batches
+ * with gradient sums, batches whose mean gradients (sharded learner) came from the fused
+ * k_push_thp, 0] (measurement only) */
+int swps_w2v_sum_stats(swps_w2v *w, uint64_t *out8);
 /* rows of all vocab keys in vid order, host buffer [V][4D] fp64 */
 int swps_w2v_get_params(swps_w2v *w, double *out);
 /* set h,v of all vocab keys (vid order, host [V][2D] fp64), zero h2/v2, refresh the cache */

@@ -361,9 +361,10 @@ class Word2Vec:
         """Cumulative gradient-sum work split by kernel: all records / items, the
         multi-chunk runs' records / items (k_gather_t's share when the push is fused),
         fused pushes and batches with sums."""
-        o = np.zeros(6, dtype=np.uint64)
+        o = np.zeros(8, dtype=np.uint64)
         check(capi.lib().swps_w2v_sum_stats(self.h, ptr(o)))
-        return dict(zip(["records", "items", "multi_records", "multi_items", "fused", "batches"], [int(x) for x in o]))
+        return dict(zip(["records", "items", "multi_records", "multi_items", "fused", "batches", "fused_grads"],
+                        [int(x) for x in o[:7]]))
 
     def get_params(self):
         V = self.info()["vocab"]

@@ -1001,6 +1001,7 @@ template <typename A> struct GatherArgs {
   uint32_t max_items;    // capacity of desc / partial: a bound on ioff[2U] every reader clamps to
   const uint32_t *multi;  // k_gather_t: only these items ([0] = count; the multi-chunk runs'), or null = all
   uint32_t SH, SV;        // record slots per position: N+1 (h records), 2W (v records)
+  const uint32_t *order;  // k_gather: all items in this order ([1..]: the multi-item sort's output), or null
 };
 
 // One wave per chunk of <= 128 records of one (key, kind): the fp64 sum, in
@@ -1015,7 +1016,9 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs<A> a) {
   const int lane = threadIdx.x & 63;
   const int NC = a.D / E;
   const uint32_t NI = min(a.ioff[2 * a.U], a.max_items);
-  for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < NI; item += gridDim.x * 4) {
+  for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < NI; q += gridDim.x * 4) {
+    // the multi-chunk items first, in first-record position order (Infinity-Cache reuse), then the rest
+    const uint32_t item = a.order ? __builtin_amdgcn_readfirstlane(a.order[1 + q]) : q;
     const uint4 d = a.desc[__builtin_amdgcn_readfirstlane(item)];
     const uint32_t s = d.x, e = d.y & 0x7FFFFFFFu, kind = d.y >> 31, n = e - s;
     uint32_t p0 = 0, p1 = 0;
@@ -1140,7 +1143,9 @@ __global__ __launch_bounds__(256) void k_gather_t(GatherArgs<float> a) {
   const uint32_t stride = gridDim.x * 4;
   uint32_t qi = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (qi >= NI) return;
-  auto item_at = [&](uint32_t q) { return a.multi ? a.multi[1 + __builtin_amdgcn_readfirstlane(q)] : q; };
+  // the multi-chunk items only (fused push), or every item in multi-first position order, or item order
+  const uint32_t *list = a.multi ? a.multi : a.order;
+  auto item_at = [&](uint32_t q) { return list ? list[1 + __builtin_amdgcn_readfirstlane(q)] : q; };
   uint32_t item = __builtin_amdgcn_readfirstlane(item_at(qi));
   uint4 d = uniform4(a.desc[item]);
   ItemRecs ri = item_recs(a, d, lane);
@@ -1645,7 +1650,10 @@ struct PHead {
   int32_t vid;
   uint32_t row;
 };
-template <int NCH, int UNR>
+// TO_GRADS (sharded learner): stop at the mean and write the push payload
+// [U][h|v] (fp32), zeros for an empty half, as k_push<..., true> does; the
+// owner applies AdaGrad (swps_w2v_serve_push).
+template <int NCH, int UNR, bool TO_GRADS = false>
 __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
   constexpr int PU = 8;
   const int lane = threadIdx.x & 63;
@@ -1664,7 +1672,7 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
     h.i0 = __builtin_amdgcn_readfirstlane(a.ioff[2 * u + half]);
     h.i1 = __builtin_amdgcn_readfirstlane(a.ioff[2 * u + half + 1]);
     h.vid = __builtin_amdgcn_readfirstlane(a.K[u]);
-    h.row = __builtin_amdgcn_readfirstlane(a.krow[u]);
+    h.row = TO_GRADS ? 0u : __builtin_amdgcn_readfirstlane(a.krow[u]);
     return h;
   };
   PHead h = head(uh);
@@ -1679,7 +1687,8 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
     if (lane == 0 && half == 0) a.local[h.vid] = -1;
     const uint32_t cnt = h.s1 - h.s0;
     const bool one = h.i1 - h.i0 == 1;
-    float *row = a.rows + (uint64_t)h.row * 4 * D;
+    float *row = TO_GRADS ? nullptr : a.rows + (uint64_t)h.row * 4 * D;
+    float *gout = TO_GRADS ? a.grads + ((uh >> 1) * 2 + half) * (uint64_t)D : nullptr;
     FSlice<NCH> wr, w2r, pf;
     ItemRecs rn{0, 0, 1.f, 1.f};
     bool rn_done = false;
@@ -1688,12 +1697,19 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
         rn = run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, hn.s0, hn.s1 - hn.s0, (int)(nx & 1), lane);
       rn_done = true;
     };
-    if (cnt || a.cache_h) wr.ld(row + half * D, lane, tl);
-    if (cnt) {
-      if (!one) pf.ld(a.partial + (uint64_t)h.i0 * D, lane, tl);
-      w2r.ld(row + (2 + half) * D, lane, tl);
+    if (!TO_GRADS) {
+      if (cnt || a.cache_h) wr.ld(row + half * D, lane, tl);
+      if (cnt) w2r.ld(row + (2 + half) * D, lane, tl);
     }
-    if (a.cache_h) wr.st((half ? a.cache_v : a.cache_h) + (uint64_t)h.vid * a.cs, lane, tl);  // pre-update value
+    if (cnt && !one) pf.ld(a.partial + (uint64_t)h.i0 * D, lane, tl);
+    if (!TO_GRADS && a.cache_h) wr.st((half ? a.cache_v : a.cache_h) + (uint64_t)h.vid * a.cs, lane, tl);
+    if (TO_GRADS && cnt == 0) {  // an empty half: zero mean
+      FSlice<NCH> z;
+#pragma unroll
+      for (int c = 0; c < NCH; c++) z.v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      z.t = 0.f;
+      z.st(gout, lane, tl);
+    }
     if (cnt) {
       FAcc<NCH> acc;
       acc.zero();
@@ -1743,29 +1759,39 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
         }
       }
       const double inv = (double)cnt;
-      float *w = row + half * D, *w2 = row + (2 + half) * D;
-      auto upd = [&](double sum, float wv, float w2v, float &wo, float &w2o) {
-        const double g = (double)(float)(sum / inv);  // the mean in the push payload's type
-        const double acc2 = (double)w2v + g * g;
-        const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
-        w2o = (float)acc2;
-        wo = (float)((double)wv + step);
-      };
+      if (TO_GRADS) {  // the mean in the push payload's type
+        FSlice<NCH> m;
 #pragma unroll
-      for (int c = 0; c < NCH; c++) {
-        float4 wo, w2o;
-        upd(acc.v[c][0], wr.v[c].x, w2r.v[c].x, wo.x, w2o.x);
-        upd(acc.v[c][1], wr.v[c].y, w2r.v[c].y, wo.y, w2o.y);
-        upd(acc.v[c][2], wr.v[c].z, w2r.v[c].z, wo.z, w2o.z);
-        upd(acc.v[c][3], wr.v[c].w, w2r.v[c].w, wo.w, w2o.w);
-        ((float4 *)w2)[lane + c * 64] = w2o;
-        ((float4 *)w)[lane + c * 64] = wo;
-      }
-      if (tl) {
-        float wo, w2o;
-        upd(acc.t, wr.t, w2r.t, wo, w2o);
-        w2[256 * NCH + lane] = w2o;
-        w[256 * NCH + lane] = wo;
+        for (int c = 0; c < NCH; c++)
+          m.v[c] = make_float4((float)(acc.v[c][0] / inv), (float)(acc.v[c][1] / inv), (float)(acc.v[c][2] / inv),
+                               (float)(acc.v[c][3] / inv));
+        m.t = (float)(acc.t / inv);
+        m.st(gout, lane, tl);
+      } else {
+        float *w = row + half * D, *w2 = row + (2 + half) * D;
+        auto upd = [&](double sum, float wv, float w2v, float &wo, float &w2o) {
+          const double g = (double)(float)(sum / inv);  // the mean in the push payload's type
+          const double acc2 = (double)w2v + g * g;
+          const double step = (g * a.lr) / sqrt(acc2 + a.fudge);
+          w2o = (float)acc2;
+          wo = (float)((double)wv + step);
+        };
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+          float4 wo, w2o;
+          upd(acc.v[c][0], wr.v[c].x, w2r.v[c].x, wo.x, w2o.x);
+          upd(acc.v[c][1], wr.v[c].y, w2r.v[c].y, wo.y, w2o.y);
+          upd(acc.v[c][2], wr.v[c].z, w2r.v[c].z, wo.z, w2o.z);
+          upd(acc.v[c][3], wr.v[c].w, w2r.v[c].w, wo.w, w2o.w);
+          ((float4 *)w2)[lane + c * 64] = w2o;
+          ((float4 *)w)[lane + c * 64] = wo;
+        }
+        if (tl) {
+          float wo, w2o;
+          upd(acc.t, wr.t, w2r.t, wo, w2o);
+          w2[256 * NCH + lane] = w2o;
+          w[256 * NCH + lane] = wo;
+        }
       }
     }
     if (!rn_done) next_recs();
@@ -1959,7 +1985,7 @@ struct swps_w2v {
   DevMem d_alias;
   // the prepared (parameter-independent) half of the next minibatch
   struct Prepped {
-    bool valid = false, records = false, sorted = false;
+    bool valid = false, records = false, sorted = false, msorted = false;
     uint64_t bi = 0, P = 0, nt = 0, HOFF = 0, M = 0, max_items = 0;
     uint32_t U = 0;
   } pb;
@@ -1980,7 +2006,8 @@ struct swps_w2v {
                                  &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_multi, &d_krow, &d_local};
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
-  uint64_t st_sums = 0, st_fused = 0;  // batches with gradient sums; of those, pushed by k_push_tg
+  uint64_t st_sums = 0, st_fused = 0, st_fused_g = 0;  // batches with gradient sums; of those, fused in-place
+                                                       // pushes / fused mean-gradient (sharded) pushes
   // negative trace
   uint64_t trace_cap = 0;
   std::vector<int64_t> trace;
@@ -3340,6 +3367,7 @@ int prep_batch(swps_w2v *w) {
                                                    max_items, w->d_desc.as<uint4>(), w->d_lead.as<uint32_t>(),
                                                    w->d_multi.as<uint32_t>(), mo);
       SWPS_HIP(hipGetLastError());
+      pb.msorted = msort;
       if (msort) {  // stable: equal coarse positions keep item order
         size_t mb = 0;
         SWPS_HIP(sort_pairs(nullptr, mb, w->d_pkeys.as<uint32_t>(), w->d_icnt.as<uint32_t>(),
@@ -3428,8 +3456,11 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     tm.end(KT_FWD, ef, s);
   }
   // fast mode, single GPU: the push sums the single-chunk runs itself (k_push_tg)
-  const bool fused = std::is_same<T, float>::value && std::is_same<A, float>::value && w->tail && !d_grads &&
-                     w->push_t && w->fused_push && D < 512 && pb.sorted;
+  const bool fast_tail = std::is_same<T, float>::value && std::is_same<A, float>::value && w->tail &&
+                         w->fused_push && D < 512 && pb.sorted;
+  const bool fused_ip = fast_tail && !d_grads && w->push_t;        // in-place AdaGrad (single GPU)
+  const bool fused_g = fast_tail && d_grads && w->push_tg_var == 5;  // the sharded learner's mean gradients
+  const bool fused = fused_ip || fused_g;
   if (pb.sorted) {
     // ---- chunked segmented gradient sums ----
     SWPS_TRY(w->d_partial.ensure(pb.max_items * D * sizeof(A)));
@@ -3437,7 +3468,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
                      w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad), w->d_lead.as<uint32_t>(),
                      (uint32_t)pb.max_items, fused ? w->d_multi.as<uint32_t>() : nullptr, (uint32_t)(N + 1),
-                     (uint32_t)(2 * W)};
+                     (uint32_t)(2 * W), !fused && pb.msorted ? w->d_multi.as<uint32_t>() : nullptr};
     // multi-chunk items: at most M / chm full chunks plus one partial chunk per run of > kChunk records
     const uint64_t gitems =
         fused ? std::min<uint64_t>(pb.max_items, pb.M / multi_chunk(w, P) + pb.M / kChunk + 1) : pb.max_items;
@@ -3477,7 +3508,8 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     tm.end(KT_GATHER, eg, s);
     w->st_pairs += pb.M;
     w->st_sums++;
-    w->st_fused += fused;
+    w->st_fused += fused_ip;
+    w->st_fused_g += fused_g;
   }
   if (U > 0) {
     // ---- push: mean + AdaGrad (also clears the local index map) ----
@@ -3490,6 +3522,12 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       (uint32_t)(N + 1), (uint32_t)(2 * W)};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      if (fused_g) {
+        k_push_thp<1, 8, true><<<(unsigned)std::min<uint64_t>(nblk((uint64_t)U * 128),
+                                                             w->push_grid ? w->push_grid : (U < 65536 ? 2048 : ~0u)),
+                                 256, 0, s>>>(pa);
+        goto push_done;
+      }
       if (fused) {
         if (w->push_tg_var == 5)
           // small batches are latency-bound: several items per wave, and the idle CUs run the prep stream
@@ -3930,11 +3968,13 @@ int swps_w2v_gather_stats(swps_w2v *w, uint64_t *out2) {
   return SWPS_OK;
 }
 
-int swps_w2v_sum_stats(swps_w2v *w, uint64_t *out6) {
+int swps_w2v_sum_stats(swps_w2v *w, uint64_t *out8) {
   SWPS_HIP(hipStreamSynchronize(w->s));
-  SWPS_HIP(hipMemcpy(out6, w->d_gstats.p, 32, hipMemcpyDeviceToHost));
-  out6[4] = w->st_fused;
-  out6[5] = w->st_sums;
+  SWPS_HIP(hipMemcpy(out8, w->d_gstats.p, 32, hipMemcpyDeviceToHost));
+  out8[4] = w->st_fused;
+  out8[5] = w->st_sums;
+  out8[6] = w->st_fused_g;
+  out8[7] = 0;
   return SWPS_OK;
 }
 

@@ -167,8 +167,11 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode):
     assert rel.max() <= (1e-5 if mode == "parity" else FAST_TOL_BATCH), float(rel.max())
 
 
-@pytest.mark.parametrize("env", ["SWPS_SORT_WIDE", "SWPS_FUSED_PUSH", "SWPS_MULTI_SORT"])
-def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env):
+@pytest.mark.parametrize("env,fixed,fp64i", [("SWPS_SORT_WIDE", "", False), ("SWPS_FUSED_PUSH", "", False),
+                                             ("SWPS_MULTI_SORT", "", False),
+                                             ("SWPS_MULTI_SORT", "SWPS_FUSED_PUSH=0", False),
+                                             ("SWPS_MULTI_SORT", "", True)])
+def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed, fp64i):
     """Three 5000-line batches of the bench corpus train to the same bits with
     either setting of:
     * SWPS_SORT_WIDE — the minibatch key indices need 18 bits: they sort in two
@@ -180,8 +183,12 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env):
       partial;
     * SWPS_MULTI_SORT — the multi-chunk items run in the order of their first
       record's position (Infinity-Cache reuse of the neu1 / neu1e rows) instead
-      of item order."""
+      of item order — with the fused push (multi-chunk items only), without it
+      (every item through k_gather_t, the sharded path's kernels) and in parity
+      mode (the generic k_gather)."""
     res = []
+    for k_v in fixed.split():
+        monkeypatch.setenv(*k_v.split("="))
     for val in ("0", "1"):
         monkeypatch.setenv(env, val)
         import subprocess
@@ -190,10 +197,11 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env):
                 "from swiftmpi_amd.synth import zipf_tokens; ids, off = zipf_tokens(17005207, 253854, 1000, seed=8); "
                 "keys = np.array([sw.bkdr('w%%d' %% i) for i in range(253854)], dtype=np.uint64); "
                 "t = sw.Table('w2v', dim=300, capacity=260000, dtype='f32', init='hash', seed=1); "
-                "w = sw.Word2Vec(t, minibatch=5000, sample=1e-5, init='table', fp64_intermediates=False); "
+                "w = sw.Word2Vec(t, minibatch=5000, sample=1e-5, init='table', fp64_intermediates=%s); "
                 "w.load_tokens(ids, off, keys); w.init(); w.train_batches(3); p = w.get_params(); "
                 "import hashlib; print('H', hashlib.sha256(p.tobytes()).hexdigest(), w.stats()['pairs'])"
-                % str(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))))
+                % (str(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))),
+                   fp64i))
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         res.append([l for l in r.stdout.splitlines() if l.startswith("H ")][-1])

@@ -176,12 +176,15 @@ def test_fast_mode_close_to_parity_mode(lib, oracle_mod, gpu, tmp_path):
     assert np.median(rel) < 1e-5 and np.quantile(rel, 0.99) < 1e-2
 
 
-@pytest.mark.parametrize("dtype,fp64i,overlap", [("f64", True, True), ("f32", True, True), ("f32", False, True),
-                                                ("f32", False, False)])
-def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i, overlap):
+@pytest.mark.parametrize("dtype,fp64i,overlap,D", [("f64", True, True, 16), ("f32", True, True, 16),
+                                                  ("f32", False, True, 16), ("f32", False, False, 16),
+                                                  ("f32", False, True, 300), ("f32", False, False, 300)])
+def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i, overlap, D):
     """The sharded request / serve / step / push path with one rank (gloo,
     world 1) reproduces the single-GPU path bit for bit — in fast mode too,
-    where the push payload is fp32."""
+    where the push payload is fp32, and at D = 300, where the learner's mean
+    gradients come from the fused k_push_thp<TO_GRADS> and the single GPU's
+    update from the in-place k_push_thp."""
     import torch.distributed as dist
     from swiftmpi_amd.dist import ShardedWord2Vec
     path = zipf_corpus(str(tmp_path / "c.txt"), 120, 300, seed=31)
@@ -195,13 +198,13 @@ def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i, overl
         s.close()
         dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
     try:
-        t = lib.Table("w2v", dim=16, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
+        t = lib.Table("w2v", dim=D, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
         sh = ShardedWord2Vec(t, overlap=overlap, **kw)
         sh.load_text(path)
         sh.init()
         sh.train(2)
         assert sh.stats()["lstate"] == w1_lstate(lib, path, dtype, kw)
-        t1 = lib.Table("w2v", dim=16, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
+        t1 = lib.Table("w2v", dim=D, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
         w1 = lib.Word2Vec(t1, init="table", **kw)
         w1.load_text(path)
         w1.init()
