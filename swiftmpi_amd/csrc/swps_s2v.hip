@@ -65,10 +65,12 @@ struct S2VRecArgs {
   const uint64_t *doc_tok;    // [ndocs+1] token offsets
   const uint64_t *doc_rec;    // [ndocs+1] record offsets (niters * tokens)
   const uint64_t *doc_lcg;    // [ndocs] main-LCG state before the sentence
-  uint64_t d0, nd;            // sentences of this minibatch
-  const uint32_t *vocab_row;  // minibatch vocab (std::map order) -> word-table row
-  const uint64_t *starts;     // unigram run starts of the minibatch vocab [U+1]
-  uint32_t U;
+  uint64_t d0, nd;            // sentences of this launch (one or several consecutive minibatches)
+  const uint32_t *vocab_row;  // concatenated minibatch vocabs (std::map order) -> word-table row
+  const uint64_t *starts;     // concatenated unigram run starts of the minibatch vocabs
+  const uint32_t *doc_batch;  // minibatch of every sentence
+  const uint64_t *bv0, *bs0;  // per minibatch: offset of its vocab / its run starts
+  const uint32_t *bU;         // per minibatch: vocab size
   uint64_t T, mT;  // unigram table size, floor((2^64-1)/T)
   int W, N, niters;
   uint64_t mW;
@@ -88,6 +90,10 @@ __global__ __launch_bounds__(256) void k_s2v_records(S2VRecArgs a) {
   const int W = a.W, N = a.N, S = 2 * W + N + 1;
   const uint64_t per_iter = 1 + (uint64_t)L * (N + 1);
   const uint64_t r0 = a.doc_rec[doc] - a.doc_rec[a.d0];
+  const uint32_t bi = a.doc_batch[doc];  // the sentence's minibatch: its vocab and unigram table
+  const uint32_t *vocab_row = a.vocab_row + a.bv0[bi];
+  const uint64_t *starts = a.starts + a.bs0[bi];
+  const uint32_t U = a.bU[bi];
   for (int q = lane; q < L * a.niters; q += 64) {
     const int it = q / L, p = q - it * L;
     uint64_t x = lcg_jump(a.doc_lcg[doc], (uint64_t)it * per_iter + 1 + (uint64_t)p * (N + 1), kLcgA, kLcgC);
@@ -109,15 +115,15 @@ __global__ __launch_bounds__(256) void k_s2v_records(S2VRecArgs a) {
     for (int d = 1; d <= N; d++) {
       x = x * kLcgA + kLcgC;
       const uint64_t slot = mod_magic(x >> 16, a.T, a.mT);
-      uint32_t lo = 0, hi = a.U;  // largest i with starts[i] <= slot
+      uint32_t lo = 0, hi = U;  // largest i with starts[i] <= slot
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (a.starts[mid] <= slot)
+        if (starts[mid] <= slot)
           lo = mid;
         else
           hi = mid;
       }
-      const uint32_t row = a.vocab_row[lo];
+      const uint32_t row = vocab_row[lo];
       r[2 * W + d] = row == word ? -1 : (int32_t)row;
     }
   }
@@ -373,6 +379,11 @@ struct swps_s2v {
   // device
   DevMem d_tok_row, d_doc_tok, d_doc_rec, d_doc_lcg, d_vocab_row, d_starts, d_init, d_exptab, d_rec, d_out, d_err,
       d_rows_read;
+  DevMem d_doc_batch, d_bv0, d_bs0, d_bU;  // sentence -> minibatch; per minibatch vocab / run-start offsets, size
+  // consecutive minibatches per launch, up to this many sentences (SWPS_S2V_GROUP; 0 = one minibatch):
+  // the word table is read-only while training and every miss was inserted at load, so the
+  // minibatches are independent and one launch over several fills the GPU (no per-minibatch tail)
+  uint64_t group_docs = 262144;  // A/B on the config-5 shape: per minibatch 2.62e8 words/s, 65,536 3.02e8, 262,144 3.06e8
   // stats and HIP-event kernel timing
   uint64_t st_batches = 0, st_docs = 0, st_pos = 0;
   bool timing = false;
@@ -483,6 +494,7 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   std::vector<uint64_t> starts_all;
   std::vector<int32_t> init;  // [docs][D] rand() outputs
   std::vector<uint64_t> doc_tok_keys;
+  std::vector<uint32_t> doc_batch;  // sentence -> minibatch
   m->batches.clear();
   m->doc_id.clear();
   m->doc_tok.assign(1, 0);
@@ -554,6 +566,7 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     }
     b.d1 = m->doc_id.size();
     b.recs = m->doc_rec[b.d1] - m->doc_rec[b.d0];
+    doc_batch.resize(b.d1, (uint32_t)m->batches.size());
     m->max_recs = std::max(m->max_recs, b.recs);
     m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
     m->batches.push_back(b);
@@ -589,6 +602,25 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     SWPS_TRY(table_check_error(m->t, s));  // syncs; every key is present by now
   }
   SWPS_TRY(upload(m->d_starts, starts_all, s));
+  {
+    std::vector<uint64_t> bv0, bs0;
+    std::vector<uint32_t> bU;
+    for (auto &b : m->batches) {
+      bv0.push_back(b.v0);
+      bs0.push_back(b.s0);
+      bU.push_back(b.U);
+    }
+    if (doc_batch.empty()) doc_batch.push_back(0);
+    if (bv0.empty()) {
+      bv0.push_back(0);
+      bs0.push_back(0);
+      bU.push_back(0);
+    }
+    SWPS_TRY(upload(m->d_doc_batch, doc_batch, s));
+    SWPS_TRY(upload(m->d_bv0, bv0, s));
+    SWPS_TRY(upload(m->d_bs0, bs0, s));
+    SWPS_TRY(upload(m->d_bU, bU, s));
+  }
   SWPS_TRY(upload(m->d_doc_tok, m->doc_tok, s));
   SWPS_TRY(upload(m->d_doc_rec, m->doc_rec, s));
   SWPS_TRY(upload(m->d_doc_lcg, m->doc_lcg, s));
@@ -614,22 +646,28 @@ template <typename T, int NCH, bool TAIL> void launch_docs(const S2VDocArgs<T> &
   k_s2v_docs<T, NCH, TAIL, 8><<<nblk(a.nd * 64), 256, 0, s>>>(a);
 }
 
-template <typename T> int s2v_batch(swps_s2v *m) {
-  const swps_s2v::Batch &b = m->batches[m->cursor];
+// minibatches [c0, c1) (consecutive, no wrap) in one records + docs launch
+template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1) {
   hipStream_t s = m->s;
-  const uint64_t nd = b.d1 - b.d0;
-  m->cursor++;
-  m->st_batches++;
+  const uint64_t d0 = m->batches[c0].d0, d1 = m->batches[c1 - 1].d1, nd = d1 - d0;
+  uint64_t recs = 0;
+  for (uint64_t c = c0; c < c1; c++) recs += m->batches[c].recs;
+  m->st_batches += c1 - c0;
   if (nd == 0) return SWPS_OK;
+  const int S = 2 * m->W + m->N + 1;
+  SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(recs, 1) * (uint64_t)S * 4));
   S2VRecArgs ra{m->d_tok_row.as<uint32_t>(),
                 m->d_doc_tok.as<uint64_t>(),
                 m->d_doc_rec.as<uint64_t>(),
                 m->d_doc_lcg.as<uint64_t>(),
-                b.d0,
+                d0,
                 nd,
-                m->d_vocab_row.as<uint32_t>() + b.v0,
-                m->d_starts.as<uint64_t>() + b.s0,
-                b.U,
+                m->d_vocab_row.as<uint32_t>(),
+                m->d_starts.as<uint64_t>(),
+                m->d_doc_batch.as<uint32_t>(),
+                m->d_bv0.as<uint64_t>(),
+                m->d_bs0.as<uint64_t>(),
+                m->d_bU.as<uint32_t>(),
                 m->cfg.unigram_size,
                 ~0ULL / m->cfg.unigram_size,
                 m->W,
@@ -641,7 +679,7 @@ template <typename T> int s2v_batch(swps_s2v *m) {
   k_s2v_records<<<nblk(nd * 64), 256, 0, s>>>(ra);
   SWPS_HIP(hipGetLastError());
   ev_end(m, ST_REC, e0);
-  S2VDocArgs<T> da{m->d_rec.as<int32_t>(), m->d_doc_tok.as<uint64_t>(), m->d_doc_rec.as<uint64_t>(), b.d0, nd,
+  S2VDocArgs<T> da{m->d_rec.as<int32_t>(), m->d_doc_tok.as<uint64_t>(), m->d_doc_rec.as<uint64_t>(), d0, nd,
                    m->d_init.as<int32_t>(), m->t->rows.as<T>(), m->d_exptab.as<float>(), m->D, m->W, m->N,
                    m->cfg.niters, m->cfg.alpha, m->d_out.as<T>(), m->d_err.as<float>(),
                    m->d_rows_read.as<unsigned long long>()};
@@ -658,7 +696,7 @@ template <typename T> int s2v_batch(swps_s2v *m) {
   SWPS_HIP(hipGetLastError());
   ev_end(m, ST_DOC, e1);
   m->st_docs += nd;
-  m->st_pos += b.recs;
+  m->st_pos += recs;
   return SWPS_OK;
 }
 
@@ -698,6 +736,7 @@ int swps_s2v_create(swps_table *t, const swps_s2v_cfg *cfg, swps_s2v **out) {
   m->f64 = t->cfg.dtype == SWPS_F64;
   m->s = t->stream;
   m->timing = cfg->profile != 0;
+  if (const char *e = getenv("SWPS_S2V_GROUP")) m->group_docs = strtoull(e, nullptr, 10);  // A/B timing
   int rc = m->d_rows_read.ensure(16);
   if (!rc && hipMemset(m->d_rows_read.p, 0, 16) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
   if (rc) {
@@ -783,9 +822,20 @@ int swps_s2v_train_batches(swps_s2v *m, uint64_t count) {
   if (!m->loaded) return fail(SWPS_E_STATE, "load a corpus first");
   if (m->batches.empty()) return SWPS_OK;
   SWPS_HIP(hipSetDevice(m->t->cfg.device));
-  for (uint64_t i = 0; i < count; i++) {
-    if (m->cursor == m->batches.size()) m->cursor = 0;  // another pass over the corpus
-    SWPS_TRY(m->f64 ? s2v_batch<double>(m) : s2v_batch<float>(m));
+  const uint64_t nb = m->batches.size();
+  for (uint64_t i = 0; i < count;) {
+    if (m->cursor == nb) m->cursor = 0;  // another pass over the corpus
+    // consecutive minibatches up to group_docs sentences, never across the corpus end
+    const uint64_t c0 = m->cursor;
+    uint64_t c1 = c0 + 1, docs = m->batches[c0].d1 - m->batches[c0].d0;
+    while (c1 < nb && i + (c1 - c0) < count &&
+           docs + (m->batches[c1].d1 - m->batches[c1].d0) <= m->group_docs) {
+      docs += m->batches[c1].d1 - m->batches[c1].d0;
+      c1++;
+    }
+    SWPS_TRY(m->f64 ? s2v_group<double>(m, c0, c1) : s2v_group<float>(m, c0, c1));
+    m->cursor = c1;
+    i += c1 - c0;
   }
   return SWPS_OK;
 }
