@@ -210,7 +210,9 @@ int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void 
     // ---- 4. owner: the push rule, one step per source in rank order ----
     if (nrecv) {
       SWPS_TRY(table_lookup(t, t->r_rkeys.as<uint64_t>(), nrecv, t->r_rows.as<uint32_t>(), s));
-      SWPS_TRY(table_push_sources(t, t->r_rows.as<uint32_t>(), nrecv, t->r_rbuf.p, s));
+      int nsrc = 0;
+      for (int r = 0; r < world; r++) nsrc += recv_k[r] > 0;
+      SWPS_TRY(table_push_sources(t, t->r_rows.as<uint32_t>(), nrecv, t->r_rbuf.p, s, false, nsrc <= 1));
     }
     return SWPS_OK;
   }

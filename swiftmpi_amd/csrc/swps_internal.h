@@ -171,6 +171,7 @@ struct swps_table {
   swps::DevMem scratch;   // per-call row indices
   uint32_t host_nrows = 0;
   swps::DevMem push_scratch, sort_tmp;  // table_push_sources: (row, position) pairs and their sort
+  bool slice_push = true;  // table_push_sources: k_push_w2v_multi_t for fp32 D = 256k + t (SWPS_SLICE_PUSH=0: off)
   uint64_t snap_sum = 0;  // checksum of the snapshot last saved from / restored into this table (0: none);
                           // worker-state snapshots record it so a resume pairs the two files of one save
   swps::DevMem isnew;     // find_or_insert: per-key "inserted by this call" flags
@@ -198,8 +199,9 @@ int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const voi
                     bool grads_f32 = false);
 // several sources' pushes concatenated in rank order (keys distinct within a
 // source): each row gets its sources' AdaGrad steps in that order, one pass
+// distinct: one source (no row repeats): no grouping sort
 int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
-                       bool grads_f32 = false);
+                       bool grads_f32 = false, bool distinct = false);
 // latched device error flags (table full, unknown key) -> error code, no sync
 int table_error_code(uint32_t flags);
 // key-sharded pull / push (swps_comm.hip): collective over t->comm

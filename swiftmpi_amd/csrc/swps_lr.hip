@@ -988,8 +988,10 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
   for (int r = 0; r < l->world; r++) n += src_counts[r];
   if (n != l->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
   SWPS_TRY(table_lookup(l->t, d_keys, n, l->d_serve_rows.as<uint32_t>(), l->s));
+  int nsrc = 0;
+  for (int r = 0; r < l->world; r++) nsrc += src_counts[r] > 0;
   // one AdaGrad step per source, in rank order, all sources in one pass
-  return table_push_sources(l->t, l->d_serve_rows.as<uint32_t>(), n, d_grads, l->s);
+  return table_push_sources(l->t, l->d_serve_rows.as<uint32_t>(), n, d_grads, l->s, false, nsrc <= 1);
 }
 
 int swps_lr_shard_comm(swps_lr *l, swps_comm *c, int32_t frag_num) {

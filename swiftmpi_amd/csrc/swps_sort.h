@@ -26,7 +26,27 @@ using OnesweepWide = rocprim::radix_sort_config<
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
 
-// tmp == nullptr: *bytes = the temporary storage needed (same `bits` for both calls)
+// Small inputs (< kSmallSort items: the B = 100 minibatch's ~0.6M records, a sharded
+// step's ~0.2M served keys): the default tile (1024 x 16 items) leaves a handful of
+// workgroups per onesweep pass; 256 x 8-item tiles give the passes 8x the workgroups.
+template <unsigned RB>
+using OnesweepSmall = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 8>, rocprim::kernel_config<256, 8>, RB,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+constexpr uint64_t kSmallSort = 1u << 20;
+// Off by default: same-box A/B at B = 100 lines 0.322 ms/step default tiles vs 0.324 small
+// (the small-tile passes overlap the learn stream and slow its kernels); SWPS_SORT_SMALL=1 on.
+inline int sort_small_mode() {
+  static const int on = [] {
+    const char *e = getenv("SWPS_SORT_SMALL");
+    return e ? atoi(e) : 0;
+  }();
+  return on;
+}
+
+// tmp == nullptr: *bytes = the temporary storage needed (same `bits` and `n` for both calls)
 inline bool sort_wide() {  // SWPS_SORT_WIDE=0: the default 8-bit digits only (A/B, tests)
   static const bool on = [] {
     const char *e = getenv("SWPS_SORT_WIDE");
@@ -41,6 +61,13 @@ inline hipError_t sort_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, co
   if (!sort_wide())
     return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
                                                   s);
+  if (n < kSmallSort && sort_small_mode()) {
+    if (bits > 16 && bits <= 20)  // two passes of 9 or 10 bits
+      return rocprim::radix_sort_pairs<OnesweepSmall<10>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                          (unsigned)bits, s);
+    return rocprim::radix_sort_pairs<OnesweepSmall<8>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                       (unsigned)bits, s);
+  }
   if (sizeof(K) == 4 && sizeof(V) == 4 && bits > 16 && bits <= 18)
     return rocprim::radix_sort_pairs<OnesweepWide<9>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
                                                       s);

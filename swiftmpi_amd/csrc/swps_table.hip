@@ -299,6 +299,83 @@ __global__ void k_push_w2v_multi(const uint32_t *__restrict__ rows_s, const uint
   }
 }
 
+// k_push_w2v_multi for fp32 rows and fp32 mean gradients (the fast-mode push payload) when
+// D = 256*NCH + tail, 0 < tail <= 64 (D = 300): a lane holds NCH float4 chunks plus one
+// scalar of each quarter [h | v | h2 | v2], so the whole row is one register pass (the
+// float4 form runs a second, 11-lane pass at D = 300).  pos_s == nullptr: the rows are
+// distinct (one source), entry w's gradients are at w.  Same per-element arithmetic in
+// the same source order: bit-identical.
+template <int NCH>
+__global__ __launch_bounds__(256) void k_push_w2v_multi_t(const uint32_t *__restrict__ rows_s,
+                                                          const uint32_t *__restrict__ pos_s, uint64_t n, uint32_t cap,
+                                                          const float *__restrict__ grads, float *__restrict__ rows,
+                                                          int D, double lr, double fudge, int rule) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= n) return;
+  const uint32_t r = rows_s[w];
+  if (r >= cap) return;
+  uint64_t e = w + 1;
+  if (pos_s) {
+    if (w > 0 && rows_s[w - 1] == r) return;  // only the head of each row's run works
+    while (e < n && rows_s[e] == r) e++;
+  }
+  const bool tl = 256 * NCH + lane < D;
+  const int ti = 256 * NCH + (tl ? lane : 0);  // lanes past the tail read a valid duplicate, never store it
+  float *row = rows + (uint64_t)r * 4 * D;
+  float4 q[4][NCH];
+  float qt[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) q[k][c] = ((const float4 *)(row + k * D))[lane + c * 64];
+    qt[k] = row[k * D + ti];
+  }
+  auto ada = [&](float &x, float &x2, float gv) {
+    const double a = (double)gv;
+    const double x2n = (double)x2 + a * a;
+    x = (float)((double)x + (a * lr) / sqrt(x2n + fudge));
+    x2 = (float)x2n;
+  };
+  auto sgd = [&](float &x, float gv) { x = (float)((double)x + (double)gv * lr); };
+  for (uint64_t j = w; j < e; j++) {
+    const float *g = grads + (pos_s ? (uint64_t)pos_s[j] : j) * 2 * D;
+    float4 gh[NCH], gv[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      gh[c] = ((const float4 *)g)[lane + c * 64];
+      gv[c] = ((const float4 *)(g + D))[lane + c * 64];
+    }
+    const float ght = g[ti], gvt = g[D + ti];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      if (rule == SWPS_PUSH_SGD) {
+        sgd(q[0][c].x, gh[c].x); sgd(q[0][c].y, gh[c].y); sgd(q[0][c].z, gh[c].z); sgd(q[0][c].w, gh[c].w);
+        sgd(q[1][c].x, gv[c].x); sgd(q[1][c].y, gv[c].y); sgd(q[1][c].z, gv[c].z); sgd(q[1][c].w, gv[c].w);
+      } else {
+        ada(q[0][c].x, q[2][c].x, gh[c].x); ada(q[0][c].y, q[2][c].y, gh[c].y);
+        ada(q[0][c].z, q[2][c].z, gh[c].z); ada(q[0][c].w, q[2][c].w, gh[c].w);
+        ada(q[1][c].x, q[3][c].x, gv[c].x); ada(q[1][c].y, q[3][c].y, gv[c].y);
+        ada(q[1][c].z, q[3][c].z, gv[c].z); ada(q[1][c].w, q[3][c].w, gv[c].w);
+      }
+    }
+    if (rule == SWPS_PUSH_SGD) {
+      sgd(qt[0], ght);
+      sgd(qt[1], gvt);
+    } else {
+      ada(qt[0], qt[2], ght);
+      ada(qt[1], qt[3], gvt);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (rule == SWPS_PUSH_SGD && k >= 2) break;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) ((float4 *)(row + k * D))[lane + c * 64] = q[k][c];
+    if (tl) row[k * D + ti] = qt[k];
+  }
+}
+
 template <typename T>
 __global__ void k_push_lr_multi(const uint32_t *__restrict__ rows_s, const uint32_t *__restrict__ pos_s, uint64_t n,
                                 uint32_t cap, const float *__restrict__ grads, T *__restrict__ rows, T lr, T fudge,
@@ -475,10 +552,37 @@ int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const voi
 }
 
 int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
-                       bool grads_f32) {
+                       bool grads_f32, bool distinct) {
   if (n == 0) return SWPS_OK;
   if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 pushed keys in one call");
   const uint32_t cap = (uint32_t)t->cfg.capacity;
+  // fast-mode payload on fp32 rows of D = 256*NCH + tail: the register-pass kernel
+  const int D0 = t->cfg.dim;
+  const int nch = D0 / 256, tail = D0 - 256 * nch;
+  const bool slice = t->cfg.layout == SWPS_LAYOUT_W2V && t->cfg.dtype == SWPS_F32 && grads_f32 && nch >= 1 &&
+                     nch <= 3 && tail > 0 && tail <= 64 && t->slice_push;
+  auto go_slice = [&](const uint32_t *rows_s, const uint32_t *pos_s) {
+    const double lr = (double)t->cfg.learning_rate, fudge = (double)t->cfg.fudge;
+    const float *g = (const float *)d_grads;
+    float *rows = t->rows.as<float>();
+    if (nch == 1)
+      k_push_w2v_multi_t<1><<<blocks_for(n * 64), 256, 0, s>>>(rows_s, pos_s, n, cap, g, rows, D0, lr, fudge,
+                                                                t->cfg.push_rule);
+    else if (nch == 2)
+      k_push_w2v_multi_t<2><<<blocks_for(n * 64), 256, 0, s>>>(rows_s, pos_s, n, cap, g, rows, D0, lr, fudge,
+                                                                t->cfg.push_rule);
+    else
+      k_push_w2v_multi_t<3><<<blocks_for(n * 64), 256, 0, s>>>(rows_s, pos_s, n, cap, g, rows, D0, lr, fudge,
+                                                                t->cfg.push_rule);
+  };
+  if (distinct) {  // one source: every row once, no grouping sort
+    if (slice) {
+      go_slice(d_rows, nullptr);
+      SWPS_HIP(hipGetLastError());
+      return SWPS_OK;
+    }
+    return table_push_rows(t, d_rows, n, d_grads, s, grads_f32);
+  }
   int bits = 1;
   while ((1ULL << bits) <= cap) bits++;
   SWPS_TRY(t->push_scratch.ensure(n * 16));
@@ -490,7 +594,9 @@ int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const 
   SWPS_TRY(t->sort_tmp.ensure(sb));
   sb = t->sort_tmp.bytes;
   SWPS_HIP(sort_pairs(t->sort_tmp.p, sb, key, key_s, pos, pos_s, n, bits, s));
-  if (t->cfg.layout == SWPS_LAYOUT_W2V) {
+  if (slice) {
+    go_slice(key_s, pos_s);
+  } else if (t->cfg.layout == SWPS_LAYOUT_W2V) {
     const double lr = (double)t->cfg.learning_rate, fudge = (double)t->cfg.fudge;
     const int D = t->cfg.dim;
     auto go = [&](auto *rows, const auto *g) {
@@ -543,6 +649,7 @@ int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
   SWPS_HIP(hipSetDevice(cfg->device));
   swps_table *t = new swps_table();
   t->cfg = *cfg;
+  if (const char *e = getenv("SWPS_SLICE_PUSH")) t->slice_push = atoi(e) != 0;  // A/B timing, tests
   if (t->cfg.fudge == 0.0f) t->cfg.fudge = 1e-6f;
   t->esize = cfg->dtype == SWPS_F64 ? 8 : 4;
   if (cfg->layout == SWPS_LAYOUT_W2V) {

@@ -3034,10 +3034,13 @@ int presize(swps_w2v *w, uint64_t maxP) {
   if (U) {
     int bits = 1;
     while ((1ULL << bits) <= U) bits++;
-    size_t sb = 0;
-    SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
-                                            w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, w->s));
-    SWPS_TRY(w->d_tmp.ensure(sb));
+    // smaller batches of the epoch may take the small-tile sort (swps_sort.h): size for both
+    for (uint64_t n : {M, std::min<uint64_t>(M, kSmallSort - 1)}) {
+      size_t sb = 0;
+      SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                          w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), n, bits, w->s));
+      SWPS_TRY(w->d_tmp.ensure(sb));
+    }
     const uint64_t max_items = 2ULL * U + M / multi_chunk(w, maxP) + 1;
     SWPS_TRY(w->d_lead.ensure((max_items / 8 + 2) * 4));
     SWPS_TRY(w->d_seg.ensure(U * 16));
@@ -3050,10 +3053,12 @@ int presize(swps_w2v *w, uint64_t maxP) {
       SWPS_TRY(w->d_pkeys.ensure(max_items * 4));
       SWPS_TRY(w->d_pvals.ensure(max_items * 4));
       SWPS_TRY(w->d_icnt.ensure(max_items * 4));
-      size_t mb = 0;
-      SWPS_HIP(sort_pairs(nullptr, mb, w->d_pkeys.as<uint32_t>(), w->d_icnt.as<uint32_t>(), w->d_pvals.as<uint32_t>(),
-                          w->d_multi.as<uint32_t>(), max_items, 16, w->s));
-      SWPS_TRY(w->d_tmp.ensure(mb));
+      for (uint64_t n : {max_items, std::min<uint64_t>(max_items, kSmallSort - 1)}) {
+        size_t mb = 0;
+        SWPS_HIP(sort_pairs(nullptr, mb, w->d_pkeys.as<uint32_t>(), w->d_icnt.as<uint32_t>(),
+                            w->d_pvals.as<uint32_t>(), w->d_multi.as<uint32_t>(), n, 16, w->s));
+        SWPS_TRY(w->d_tmp.ensure(mb));
+      }
     }
   }
   return SWPS_OK;
@@ -4213,8 +4218,10 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
   SWPS_TRY(w->d_push_rows.ensure(std::max<uint64_t>(n, 1) * 4));
   SWPS_TRY(table_lookup(w->t, d_keys, n, w->d_push_rows.as<uint32_t>(), ss));
   const bool g32 = !w->f64 && !w->cfg.fp64_intermediates;  // fast mode: fp32 push payload
+  int nsrc = 0;
+  for (int r = 0; r < w->world; r++) nsrc += src_counts[r] > 0;
   // one AdaGrad step per source, in rank order, all sources in one pass
-  return table_push_sources(w->t, w->d_push_rows.as<uint32_t>(), n, d_grads, ss, g32);
+  return table_push_sources(w->t, w->d_push_rows.as<uint32_t>(), n, d_grads, ss, g32, nsrc <= 1);
 }
 
 int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {

@@ -47,10 +47,13 @@ def gather(obj, world):
 
 def check_w2v(sw, rank, world, dev, tmp, mode, epochs):
     from swiftmpi_amd.dist import ShardedWord2Vec
-    dtype, fp64i = {"f64": ("f64", True), "parity": ("f32", True), "fast": ("f32", False)}[mode]
+    dtype, fp64i = {"f64": ("f64", True), "parity": ("f32", True), "fast": ("f32", False),
+                    "fast300": ("f32", False)}[mode]
     paths = [w2v_corpus(os.path.join(tmp, "c%d.txt" % r), r) for r in range(world)]
     kw = dict(window=4, negative=4, minibatch=17, sample=1e-3, unigram_size=10 ** 6)
-    D, seed = 16, 9
+    # fast300: the bench's D = 300 kernels (k_push_thp<TO_GRADS> on the learner, the
+    # register-pass k_push_w2v_multi_t on the owners, several sources per hot row)
+    D, seed = (300 if mode == "fast300" else 16), 9
     t = sw.Table("w2v", dim=D, capacity=4096, dtype=dtype, learning_rate=0.7, init="hash", seed=seed, device=dev)
     sh = ShardedWord2Vec(t, frag_num=1000, fp64_intermediates=fp64i, **kw)
     sh.load_text(paths[rank])
@@ -60,7 +63,8 @@ def check_w2v(sw, rank, world, dev, tmp, mode, epochs):
     # steps a tiny hot vocabulary turns fp32 rounding into exp-table bucket
     # flips (tests/test_bench_shape_gpu.py), which compare nothing about the
     # exchange; f64 / parity: whole epochs
-    nsteps = 3 if mode == "fast" else epochs * sh.steps_per_epoch
+    fast = mode.startswith("fast")
+    nsteps = 3 if fast else epochs * sh.steps_per_epoch
     sh.train_steps(nsteps)
     sh.sync()
     keys, rows = sh.shard_rows()
@@ -80,7 +84,7 @@ def check_w2v(sw, rank, world, dev, tmp, mode, epochs):
             owned[kk] = rr
     assert sorted(owned) == [int(k) for k in ok_keys], "key sets differ"
     got = np.array([owned[int(k)] for k in ok_keys])
-    if mode != "fast":  # at an epoch boundary (the library plans, and jumps its LCGs, a whole epoch ahead)
+    if not fast:  # at an epoch boundary (the library plans, and jumps its LCGs, a whole epoch ahead)
         for r in range(world):
             so = orc.rank_stats(r)
             assert (objs[r][2], objs[r][3]) == (so["rng"], so["frng"]), "rank %d RNG streams diverged" % r
