@@ -348,18 +348,21 @@ def main():
     nbat = g1["batches"] - g0["batches"]
     fused = nbat > 0 and g1["fused"] - g0["fused"] == nbat
     fused_g = nbat > 0 and g1.get("fused_grads", 0) - g0.get("fused_grads", 0) == nbat
+    # small batches run the multi-chunk gather on a side stream beside the push: the push timer
+    # (push start .. the multi-chunk halves' push end) then spans the whole group
+    split = nbat > 0 and g1.get("split", 0) - g0.get("split", 0) == nbat
     gat_ms, gat_n = kt["gather"]
     push_ms, push_n = kt.get("push", (0.0, 0))
     if fused_g:  # sharded learner: the fused push stops at the mean gradients (2·D·ea written per key)
         sum_kernel = ("k_gather_t + k_combine + k_push_thp<TO_GRADS> (segmented gradient sums + fused mean "
                       "gradients of the push payload)")
         gat_bytes = g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) + dp["pushed"] * (2 * D * ea + 8)
-        sum_ms = gat_ms + push_ms
+        sum_ms = push_ms if split else gat_ms + push_ms
     elif fused:
         sum_kernel = "k_gather_t + k_combine + k_push_thp (segmented gradient sums + fused AdaGrad push)"
         gat_bytes = (g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) +
                      dp["pushed"] * (10 * es * D + 8))
-        sum_ms = gat_ms + push_ms
+        sum_ms = push_ms if split else gat_ms + push_ms
     else:
         sum_kernel = "k_gather_t + k_combine (segmented gradient sums)"
         gat_bytes = g_rec * (D * ea + 4) + g_items * (D * ea + 16)

@@ -288,7 +288,8 @@ int swps_w2v_gather_stats(swps_w2v *w, uint64_t *out2);
  * records, items, records of multi-chunk (key, kind) runs (k_gather_t's share when the push
  * is fused), items of those runs, batches pushed by the fused in-place k_push_thp, batches
  * with gradient sums, batches whose mean gradients (sharded learner) came from the fused
- * k_push_thp, 0] (measurement only) */
+ * k_push_thp, batches whose multi-chunk gather ran beside the push on a side stream]
+ * (measurement only) */
 int swps_w2v_sum_stats(swps_w2v *w, uint64_t *out8);
 /* rows of all vocab keys in vid order, host buffer [V][4D] fp64 */
 int swps_w2v_get_params(swps_w2v *w, double *out);

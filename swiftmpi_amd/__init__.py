@@ -363,8 +363,8 @@ class Word2Vec:
         fused pushes and batches with sums."""
         o = np.zeros(8, dtype=np.uint64)
         check(capi.lib().swps_w2v_sum_stats(self.h, ptr(o)))
-        return dict(zip(["records", "items", "multi_records", "multi_items", "fused", "batches", "fused_grads"],
-                        [int(x) for x in o[:7]]))
+        return dict(zip(["records", "items", "multi_records", "multi_items", "fused", "batches", "fused_grads",
+                         "split"], [int(x) for x in o]))
 
     def get_params(self):
         V = self.info()["vocab"]

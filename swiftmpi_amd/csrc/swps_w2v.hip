@@ -1653,7 +1653,9 @@ struct PHead {
 // TO_GRADS (sharded learner): stop at the mean and write the push payload
 // [U][h|v] (fp32), zeros for an empty half, as k_push<..., true> does; the
 // owner applies AdaGrad (swps_w2v_serve_push).
-template <int NCH, int UNR, bool TO_GRADS = false>
+// MODE 0: every (key, half); 1: all but the multi-chunk halves (they wait for k_gather_t's
+// partials while this runs beside it, on another stream); 2: only the multi-chunk halves.
+template <int NCH, int UNR, bool TO_GRADS = false, int MODE = 0>
 __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
   constexpr int PU = 8;
   const int lane = threadIdx.x & 63;
@@ -1684,7 +1686,16 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
     PHead hn{0, 0, 0, 0, 0, 0};
     if (more) hn = head(nx);
     const int half = (int)(uh & 1);
-    if (lane == 0 && half == 0) a.local[h.vid] = -1;
+    const bool multi = h.i1 - h.i0 > 1;
+    if ((MODE == 1 && multi) || (MODE == 2 && !multi)) {  // the other pass's item
+      if (more && hn.s1 > hn.s0 && hn.i1 - hn.i0 == 1 && MODE != 2)
+        ri = run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, hn.s0, hn.s1 - hn.s0, (int)(nx & 1), lane);
+      if (!more) break;
+      uh = nx;
+      h = hn;
+      continue;
+    }
+    if (lane == 0 && half == 0 && MODE != 2) a.local[h.vid] = -1;
     const uint32_t cnt = h.s1 - h.s0;
     const bool one = h.i1 - h.i0 == 1;
     float *row = TO_GRADS ? nullptr : a.rows + (uint64_t)h.row * 4 * D;
@@ -1954,7 +1965,11 @@ struct swps_w2v {
   int push_tg_var = 5;  // fused push kernel (SWPS_PUSH_TG, A/B): 5 = k_push_thp (default), 0 = k_push_tg UNR 8,
                         // 1 = k_push_tg at occupancy 4, 2 = k_push_tg UNR 4, 3 = k_push_th, 4 = k_push_th UNR 16
   uint32_t push_grid = 0;
-  int fwd_g = 4;  // k_forward_t rows in flight per wave (SWPS_FWD_G: 4, 8, 16; A/B)  // k_push_thp grid cap in blocks (SWPS_PUSH_GRID; 0 = by batch size)
+  int fwd_g = 4;
+  int split_push = 0;  // SWPS_SPLIT_PUSH: 1 = gather beside the push always, -1 = below 64 k keys, 0 = never
+                      // (default: same-box A/B at B = 100 lines 0.321 ms/step in one stream vs 0.349 split)
+  hipStream_t s_side = nullptr;
+  hipEvent_t ev_fwd = nullptr, ev_gat = nullptr;  // k_forward_t rows in flight per wave (SWPS_FWD_G: 4, 8, 16; A/B)  // k_push_thp grid cap in blocks (SWPS_PUSH_GRID; 0 = by batch size)
   uint32_t multi_chunk = 0;  // SWPS_MULTI_CHUNK: chunk size of multi-chunk runs (1..128; 0 = kChunk)
   int multi_sort = 1;                 // order the multi-chunk items by position (SWPS_MULTI_SORT=0: off; A/B)
   uint64_t multi_sort_min = 65536;    // ... for batches of at least this many kept positions (SWPS_MULTI_SORT_MIN)
@@ -2006,7 +2021,7 @@ struct swps_w2v {
                                  &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_multi, &d_krow, &d_local};
   // stats
   uint64_t st_batches = 0, st_kept = 0, st_words = 0, st_pairs = 0, st_pulled = 0, st_pushed = 0;
-  uint64_t st_sums = 0, st_fused = 0, st_fused_g = 0;  // batches with gradient sums; of those, fused in-place
+  uint64_t st_sums = 0, st_fused = 0, st_fused_g = 0, st_split = 0;  // batches with gradient sums; of those, fused in-place
                                                        // pushes / fused mean-gradient (sharded) pushes
   // negative trace
   uint64_t trace_cap = 0;
@@ -3466,6 +3481,22 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
   const bool fused_ip = fast_tail && !d_grads && w->push_t;        // in-place AdaGrad (single GPU)
   const bool fused_g = fast_tail && d_grads && w->push_tg_var == 5;  // the sharded learner's mean gradients
   const bool fused = fused_ip || fused_g;
+  // small batches: the multi-chunk gather (latency-bound, a few hundred items) runs on a side stream
+  // beside the push of every other (key, half); the multi-chunk halves are pushed after it
+  const bool split = fused && w->push_tg_var == 5 && (w->split_push > 0 || (w->split_push < 0 && U < 65536));
+  hipStream_t gs = s;  // the gather's stream
+  if (split) {
+    if (!w->s_side) {
+      int lo = 0, hi = 0;
+      SWPS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      SWPS_HIP(hipStreamCreateWithPriority(&w->s_side, hipStreamNonBlocking, hi));
+      SWPS_HIP(hipEventCreateWithFlags(&w->ev_fwd, hipEventDisableTiming));
+      SWPS_HIP(hipEventCreateWithFlags(&w->ev_gat, hipEventDisableTiming));
+    }
+    SWPS_HIP(hipEventRecord(w->ev_fwd, s));
+    SWPS_HIP(hipStreamWaitEvent(w->s_side, w->ev_fwd, 0));
+    gs = w->s_side;
+  }
   if (pb.sorted) {
     // ---- chunked segmented gradient sums ----
     SWPS_TRY(w->d_partial.ensure(pb.max_items * D * sizeof(A)));
@@ -3479,25 +3510,25 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
         fused ? std::min<uint64_t>(pb.max_items, pb.M / multi_chunk(w, P) + pb.M / kChunk + 1) : pb.max_items;
     const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(gitems * 64), (uint64_t)w->gather_grid);
     const unsigned cgrid = combine_grid(pb.max_items);
-    hipEvent_t eg = tm.begin(s);
+    hipEvent_t eg = tm.begin(gs);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
         if (D < 512) {
           if (w->gather_unr == 4)
-            k_gather_t<1, 4><<<ggrid, 256, 0, s>>>(ga);
+            k_gather_t<1, 4><<<ggrid, 256, 0, gs>>>(ga);
           else if (w->gather_unr == 16)
-            k_gather_t<1, 16><<<ggrid, 256, 0, s>>>(ga);
+            k_gather_t<1, 16><<<ggrid, 256, 0, gs>>>(ga);
           else
-            k_gather_t<1, 8><<<ggrid, 256, 0, s>>>(ga);
+            k_gather_t<1, 8><<<ggrid, 256, 0, gs>>>(ga);
         }
         else if (D < 768)
-          k_gather_t<2, 8><<<ggrid, 256, 0, s>>>(ga);
+          k_gather_t<2, 8><<<ggrid, 256, 0, gs>>>(ga);
         else
-          k_gather_t<3, 8><<<ggrid, 256, 0, s>>>(ga);
+          k_gather_t<3, 8><<<ggrid, 256, 0, gs>>>(ga);
         switch (w->NCH) {  // second level over the partials: layout-independent
-          case 2: k_combine<T, A, 2><<<cgrid, 256, 0, s>>>(ga); break;
-          case 3: k_combine<T, A, 3><<<cgrid, 256, 0, s>>>(ga); break;
-          default: k_combine<T, A, 4><<<cgrid, 256, 0, s>>>(ga); break;
+          case 2: k_combine<T, A, 2><<<cgrid, 256, 0, gs>>>(ga); break;
+          case 3: k_combine<T, A, 3><<<cgrid, 256, 0, gs>>>(ga); break;
+          default: k_combine<T, A, 4><<<cgrid, 256, 0, gs>>>(ga); break;
         }
         goto gather_done;
       }
@@ -3510,7 +3541,8 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     }
   gather_done:
     SWPS_HIP(hipGetLastError());
-    tm.end(KT_GATHER, eg, s);
+    tm.end(KT_GATHER, eg, gs);
+    if (split) SWPS_HIP(hipEventRecord(w->ev_gat, gs));
     w->st_pairs += pb.M;
     w->st_sums++;
     w->st_fused += fused_ip;
@@ -3527,10 +3559,23 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       (uint32_t)(N + 1), (uint32_t)(2 * W)};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      const unsigned pgrid = (unsigned)std::min<uint64_t>(nblk((uint64_t)U * 128),
+                                                          w->push_grid ? w->push_grid : (U < 65536 ? 2048 : ~0u));
+      if (split) {  // every other (key, half) beside the gather, then the multi-chunk halves
+        if (fused_g)
+          k_push_thp<1, 8, true, 1><<<pgrid, 256, 0, s>>>(pa);
+        else
+          k_push_thp<1, 8, false, 1><<<pgrid, 256, 0, s>>>(pa);
+        SWPS_HIP(hipStreamWaitEvent(s, w->ev_gat, 0));
+        if (fused_g)
+          k_push_thp<1, 8, true, 2><<<pgrid, 256, 0, s>>>(pa);
+        else
+          k_push_thp<1, 8, false, 2><<<pgrid, 256, 0, s>>>(pa);
+        w->st_split++;
+        goto push_done;
+      }
       if (fused_g) {
-        k_push_thp<1, 8, true><<<(unsigned)std::min<uint64_t>(nblk((uint64_t)U * 128),
-                                                             w->push_grid ? w->push_grid : (U < 65536 ? 2048 : ~0u)),
-                                 256, 0, s>>>(pa);
+        k_push_thp<1, 8, true><<<pgrid, 256, 0, s>>>(pa);
         goto push_done;
       }
       if (fused) {
@@ -3675,6 +3720,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_FUSED_PUSH")) w->fused_push = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_PUSH_TG")) w->push_tg_var = atoi(e);          // A/B timing
   if (const char *e = getenv("SWPS_FWD_G")) w->fwd_g = atoi(e);
+  if (const char *e = getenv("SWPS_SPLIT_PUSH")) w->split_push = atoi(e);
   if (const char *e = getenv("SWPS_PUSH_GRID")) w->push_grid = (uint32_t)std::max(0, atoi(e));
   if (const char *e = getenv("SWPS_MULTI_SORT")) w->multi_sort = atoi(e);        // A/B timing
   if (const char *e = getenv("SWPS_MULTI_CHUNK")) w->multi_chunk = (uint32_t)std::min(128, std::max(0, atoi(e)));
@@ -3726,8 +3772,14 @@ int swps_w2v_destroy(swps_w2v *w) {
     (void)hipStreamSynchronize(w->s_prep);
     (void)hipStreamDestroy(w->s_prep);
   }
+  if (w->s_side) {
+    (void)hipStreamSynchronize(w->s_side);
+    (void)hipStreamDestroy(w->s_side);
+  }
   if (w->ev_learn) (void)hipEventDestroy(w->ev_learn);
   if (w->ev_prep) (void)hipEventDestroy(w->ev_prep);
+  if (w->ev_fwd) (void)hipEventDestroy(w->ev_fwd);
+  if (w->ev_gat) (void)hipEventDestroy(w->ev_gat);
   if (w->h_small) (void)hipHostFree(w->h_small);
   delete w->drv;
   delete w;
@@ -3979,7 +4031,7 @@ int swps_w2v_sum_stats(swps_w2v *w, uint64_t *out8) {
   out8[4] = w->st_fused;
   out8[5] = w->st_sums;
   out8[6] = w->st_fused_g;
-  out8[7] = 0;
+  out8[7] = w->st_split;
   return SWPS_OK;
 }
 

@@ -170,7 +170,7 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode):
 @pytest.mark.parametrize("env,fixed,fp64i", [("SWPS_SORT_WIDE", "", False), ("SWPS_FUSED_PUSH", "", False),
                                              ("SWPS_MULTI_SORT", "", False),
                                              ("SWPS_MULTI_SORT", "SWPS_FUSED_PUSH=0", False),
-                                             ("SWPS_MULTI_SORT", "", True)])
+                                             ("SWPS_MULTI_SORT", "", True), ("SWPS_SPLIT_PUSH", "", False)])
 def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed, fp64i):
     """Three 5000-line batches of the bench corpus train to the same bits with
     either setting of:
@@ -185,7 +185,10 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed,
       record's position (Infinity-Cache reuse of the neu1 / neu1e rows) instead
       of item order — with the fused push (multi-chunk items only), without it
       (every item through k_gather_t, the sharded path's kernels) and in parity
-      mode (the generic k_gather)."""
+      mode (the generic k_gather);
+    * SWPS_SPLIT_PUSH — the multi-chunk gather (and its second level) on a
+      side stream beside the push of the other (key, half) items, the
+      multi-chunk halves pushed after it, vs everything in one stream."""
     res = []
     for k_v in fixed.split():
         monkeypatch.setenv(*k_v.split("="))
