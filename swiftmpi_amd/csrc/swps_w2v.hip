@@ -561,6 +561,7 @@ template <typename T, typename A> struct FwdArgs {
   int xcd;  // 1: XCD-contiguous block order (xcd_block)
   int ld;   // neu1/neu1e row stride in elements (D rounded up to 128 B: whole cache lines per row)
   int cs;   // worker-cache row stride in elements (the same rounding)
+  int full;  // k_forward_t: neu1/neu1e stores cover the row pad (zeros): whole lines (SWPS_FULL_LINES)
 };
 
 // Source row of a forward slot: a record entry tagged kTabRow is a row index
@@ -811,6 +812,14 @@ template <int NCH> struct FSlice {
     for (int c = 0; c < NCH; c++) ((float4 *)row)[lane + c * 64] = v[c];
     if (tl) row[256 * NCH + lane] = t;
   }
+  // the same into a row of ld >= D elements whose pad (elements D..ld) is written as zeros:
+  // whole-line stores (a partial last line is a masked write that HBM completes as a
+  // read-modify-write of its ECC word; measured on the cache rows: pull 0.19 -> 0.16 ms)
+  __device__ __forceinline__ void st_full(float *row, int lane, bool tl, int ld) const {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) ((float4 *)row)[lane + c * 64] = v[c];
+    if (256 * NCH + lane < ld) row[256 * NCH + lane] = tl ? t : 0.f;
+  }
 };
 template <int NCH> struct FAcc {
   double v[NCH][4];
@@ -866,6 +875,12 @@ template <int NCH> struct FAcc {
       ((float4 *)row)[lane + c * 64] = make_float4((float)v[c][0], (float)v[c][1], (float)v[c][2], (float)v[c][3]);
     if (tl) row[256 * NCH + lane] = (float)t;
   }
+  __device__ __forceinline__ void st_full(float *row, int lane, bool tl, int ld) const {  // FSlice::st_full
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+      ((float4 *)row)[lane + c * 64] = make_float4((float)v[c][0], (float)v[c][1], (float)v[c][2], (float)v[c][3]);
+    if (256 * NCH + lane < ld) row[256 * NCH + lane] = tl ? (float)t : 0.f;
+  }
 };
 
 // k_forward (fast mode) on FSlice rows.
@@ -916,8 +931,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
     }
   }
-  acc.st(a.neu1 + (uint64_t)p * a.ld, lane, tl);
-  ne.st(a.neu1e + (uint64_t)p * a.ld, lane, tl);
+  acc.st_full(a.neu1 + (uint64_t)p * a.ld, lane, tl, a.full ? a.ld : a.D);
+  ne.st_full(a.neu1e + (uint64_t)p * a.ld, lane, tl, a.full ? a.ld : a.D);
   if (lane <= N) a.pg[(uint64_t)p * (N + 1) + lane] = gk;
 }
 
@@ -1253,6 +1268,7 @@ template <typename T, typename A> struct PushArgs {
   int ld;
   const uint32_t *krow;  // k_push_thp: shard row per batch key (k_batch_setup)
   uint32_t SH, SV;       // record slots per position (GatherArgs)
+  int full;              // cache-row stores cover the pad too (zeros): SWPS_FULL_LINES
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
@@ -1363,8 +1379,8 @@ __global__ __launch_bounds__(256) void k_push_t(PushArgs<float, float> a) {
       }
     }
     if (a.cache_h) {  // the pulled (pre-update) value stays in the worker cache
-      wr[0].st(a.cache_h + (uint64_t)vid * a.cs, lane, tl);
-      wr[1].st(a.cache_v + (uint64_t)vid * a.cs, lane, tl);
+      wr[0].st_full(a.cache_h + (uint64_t)vid * a.cs, lane, tl, a.full ? a.cs : D);
+      wr[1].st_full(a.cache_v + (uint64_t)vid * a.cs, lane, tl, a.full ? a.cs : D);
     }
 #pragma unroll
     for (int half = 0; half < 2; half++) {
@@ -1449,8 +1465,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
     }
     if (a.cache_h) {  // the pulled (pre-update) value stays in the worker cache
-      wr[0].st(a.cache_h + (uint64_t)vid * a.cs, lane, tl);
-      wr[1].st(a.cache_v + (uint64_t)vid * a.cs, lane, tl);
+      wr[0].st_full(a.cache_h + (uint64_t)vid * a.cs, lane, tl, a.full ? a.cs : D);
+      wr[1].st_full(a.cache_v + (uint64_t)vid * a.cs, lane, tl, a.full ? a.cs : D);
     }
 #pragma unroll
     for (int half = 0; half < 2; half++) {
@@ -1565,7 +1581,7 @@ __global__ __launch_bounds__(256) void k_push_th(PushArgs<float, float> a) {
         pf.ld(a.partial + (uint64_t)i0 * D, lane, tl);
       w2r.ld(row + (2 + half) * D, lane, tl);
     }
-    if (a.cache_h) wr.st((half ? a.cache_v : a.cache_h) + (uint64_t)vid * a.cs, lane, tl);  // pre-update value
+    if (a.cache_h) wr.st_full((half ? a.cache_v : a.cache_h) + (uint64_t)vid * a.cs, lane, tl, a.full ? a.cs : D);
     if (cnt == 0) continue;
     FAcc<NCH> acc;
     acc.zero();
@@ -1713,7 +1729,8 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
       if (cnt) w2r.ld(row + (2 + half) * D, lane, tl);
     }
     if (cnt && !one) pf.ld(a.partial + (uint64_t)h.i0 * D, lane, tl);
-    if (!TO_GRADS && a.cache_h) wr.st((half ? a.cache_v : a.cache_h) + (uint64_t)h.vid * a.cs, lane, tl);
+    if (!TO_GRADS && a.cache_h)  // the pre-update value, pad as zeros (whole lines)
+      wr.st_full((half ? a.cache_v : a.cache_h) + (uint64_t)h.vid * a.cs, lane, tl, a.full ? a.cs : D);
     if (TO_GRADS && cnt == 0) {  // an empty half: zero mean
       FSlice<NCH> z;
 #pragma unroll
@@ -1966,6 +1983,7 @@ struct swps_w2v {
                         // 1 = k_push_tg at occupancy 4, 2 = k_push_tg UNR 4, 3 = k_push_th, 4 = k_push_th UNR 16
   uint32_t push_grid = 0;
   int fwd_g = 4;
+  int full_lines = 1;  // neu1/neu1e and cache-row stores write the row pad as zeros (SWPS_FULL_LINES=0: off; A/B)
   int split_push = 0;  // SWPS_SPLIT_PUSH: 1 = gather beside the push always, -1 = below 64 k keys, 0 = never
                       // (default: same-box A/B at B = 100 lines 0.321 ms/step in one stream vs 0.349 split)
   hipStream_t s_side = nullptr;
@@ -3447,7 +3465,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_TRY(w->d_pg.ensure(pb.HOFF * 4));
     FwdArgs<T, A> fa{w->d_rec.as<int32_t>(), (int)P, w->d_cache_h.as<T>(), w->d_cache_v.as<T>(), w->t->rows.as<T>(),
                      w->d_exptab.as<float>(), D, W, N, w->cfg.alpha, w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                     w->d_pg.as<float>(), w->xcd_order, ld, w->cs};
+                     w->d_pg.as<float>(), w->xcd_order, ld, w->cs, w->full_lines};
     hipEvent_t ef = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
@@ -3556,7 +3574,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs,
                       w->d_pvals_s.as<uint32_t>(), w->d_pg.as<float>(), w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
                       pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad), w->d_krow.as<uint32_t>(),
-                      (uint32_t)(N + 1), (uint32_t)(2 * W)};
+                      (uint32_t)(N + 1), (uint32_t)(2 * W), w->full_lines};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       const unsigned pgrid = (unsigned)std::min<uint64_t>(nblk((uint64_t)U * 128),
@@ -3720,6 +3738,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_FUSED_PUSH")) w->fused_push = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_PUSH_TG")) w->push_tg_var = atoi(e);          // A/B timing
   if (const char *e = getenv("SWPS_FWD_G")) w->fwd_g = atoi(e);
+  if (const char *e = getenv("SWPS_FULL_LINES")) w->full_lines = atoi(e) != 0;
   if (const char *e = getenv("SWPS_SPLIT_PUSH")) w->split_push = atoi(e);
   if (const char *e = getenv("SWPS_PUSH_GRID")) w->push_grid = (uint32_t)std::max(0, atoi(e));
   if (const char *e = getenv("SWPS_MULTI_SORT")) w->multi_sort = atoi(e);        // A/B timing

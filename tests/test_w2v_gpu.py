@@ -380,13 +380,16 @@ def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch):
     variants = (("1", "1", "1", "1", "1", "0"), ("0", "1", "1", "1", "1", "0"), ("1", "0", "1", "1", "1", "0"),
                 ("1", "1", "0", "1", "1", "0"), ("1", "1", "1", "0", "1", "0"), ("1", "1", "1", "1", "0", "0"),
                 ("1", "1", "1", "1", "1", "1"), ("1", "1", "1", "1", "1", "2"), ("1", "1", "1", "1", "1", "3"), ("1", "1", "1", "1", "1", "4"), ("1", "1", "1", "1", "1", "5"),
-                ("1", "1", "1", "1", "1", "sort"), ("1", "1", "1", "1", "1", "split"), ("1", "1", "1", "1", "1", "nosplit"))
+                ("1", "1", "1", "1", "1", "sort"), ("1", "1", "1", "1", "1", "split"), ("1", "1", "1", "1", "1", "nosplit"),
+                ("1", "1", "1", "1", "1", "nofull"))
     for push_t, pad, uidx, cpad, fused, tgv in variants:
         # "sort": the multi-chunk gather items in position order even for these small batches
         monkeypatch.setenv("SWPS_MULTI_SORT_MIN", "0" if tgv == "sort" else "65536")
         # split / nosplit: the multi-chunk gather beside the push on a side stream, or after it
         monkeypatch.setenv("SWPS_SPLIT_PUSH", {"split": "1", "nosplit": "0"}.get(tgv, "-1"))
-        tgv = {"sort": "0", "split": "5", "nosplit": "5"}.get(tgv, tgv)
+        # nofull: neu1/neu1e and cache rows stored without their zero pad (partial last lines)
+        monkeypatch.setenv("SWPS_FULL_LINES", "0" if tgv == "nofull" else "1")
+        tgv = {"sort": "0", "split": "5", "nosplit": "5", "nofull": "5"}.get(tgv, tgv)
         monkeypatch.setenv("SWPS_PUSH_T", push_t)
         monkeypatch.setenv("SWPS_ROW_PAD", pad)
         monkeypatch.setenv("SWPS_UNI_INDEX", uidx)
