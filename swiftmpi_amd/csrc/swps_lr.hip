@@ -83,6 +83,63 @@ __global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__
   }
 }
 
+// k_lr_forward with R rows per wave (rows of at most 2*(64/R) features): L = 64/R lanes per
+// row, two features per lane (f and f+L).  The examples are latency-bound chains (offsets ->
+// feature indices -> weights -> the ordered sum), so R rows per wave put R times the chains
+// in flight per wave slot; the R ordered sums run interleaved.  Same products, same
+// feature-order fp32 sums as k_lr_forward: bit-identical.
+template <int R>
+__global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict__ row_off,
+                                                      const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
+                                                      const float *__restrict__ label, uint64_t r0, uint64_t nr,
+                                                      const float *__restrict__ rows, int stride,
+                                                      float *__restrict__ err, float *__restrict__ err2) {
+  constexpr int L = 64 / R;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / L, k = lane - sub * L;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (wave * R >= nr) return;
+  const uint64_t j = wave * R + (uint64_t)sub;
+  const bool act = sub < R && j < nr;
+  int m = 0;
+  float p0 = 0.f, p1 = 0.f, y = 0.f;
+  if (act) {
+    const uint64_t r = r0 + j;
+    const uint64_t a = row_off[r];
+    m = (int)(row_off[r + 1] - a);
+    y = label[r];
+    if (k < m) p0 = weight_at(rows, fidx[a + k], stride) * fval[a + k];
+    if (k + L < m) p1 = weight_at(rows, fidx[a + k + L], stride) * fval[a + k + L];
+  }
+  int mq[R];
+  int mmax = 0;
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    mq[q] = __builtin_amdgcn_readlane(m, q * L);  // 0 for rows past the batch
+    mmax = max(mmax, mq[q]);
+  }
+  float sum[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) sum[q] = 0.f;
+  for (int f = 0; f < mmax; f++) {  // feature order, R chains interleaved
+    const int src = f < L ? __float_as_int(p0) : __float_as_int(p1);
+    const int fl = f < L ? f : f - L;
+#pragma unroll
+    for (int q = 0; q < R; q++)
+      if (f < mq[q]) sum[q] += __int_as_float(__builtin_amdgcn_readlane(src, q * L + fl));
+  }
+  if (act && k == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < R; q++)
+      if (q == sub) s = sum[q];
+    const float predict = (float)(1. / (1. + (double)(float)exp((double)(-s))));
+    const float error = y - predict;
+    err[r0 + j] = error;
+    err2[r0 + j] = error * error;
+  }
+}
+
 // ---- the static per-batch index (built once at load; lr_index) -------------
 // The batch's records are its rows' features in (row, feature) order; their
 // stable key-sorted order, the runs (one per pushed key) and the run bounds
@@ -412,6 +469,8 @@ struct swps_lr {
   // (pushed keys) of all batches: vid, start and length relative to the batch; first run and run count per batch
   DevMem d_srow, d_sval, d_ruk, d_roff, d_rcnt, d_bnruns;
   std::vector<uint64_t> brun;
+  std::vector<uint32_t> bmaxf;  // longest row (features) per batch: k_lr_forward_r's row packing
+  int rows_per_wave = 1;        // SWPS_LR_PACK: 0 = one row per wave (k_lr_forward), 2 = at most 2, 1 = by length
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
   LTimer timer;
@@ -450,6 +509,9 @@ int lr_index(swps_lr *l) {
   std::vector<uint64_t> bnz0(nb + 1);
   l->max_bnnz = 0;
   for (uint64_t b = 0; b <= nb; b++) bnz0[b] = l->row_off[std::min<uint64_t>(nr, b * B1)];
+  l->bmaxf.assign(nb, 0);
+  for (uint64_t r = 0; r < nr; r++)
+    l->bmaxf[r / B1] = std::max<uint32_t>(l->bmaxf[r / B1], (uint32_t)(l->row_off[r + 1] - l->row_off[r]));
   for (uint64_t b = 0; b < nb; b++) l->max_bnnz = std::max<uint64_t>(l->max_bnnz, bnz0[b + 1] - bnz0[b]);
   DevMem d_bnz0, key, idx, ks, perm, head, rid1, rkey, tmp;
   SWPS_TRY(upload(d_bnz0, bnz0, s));
@@ -571,9 +633,20 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   if (nnz == 0) return SWPS_OK;
   SWPS_TRY(l->d_longs.ensure((l->max_bnnz + 1) * 4));
   hipEvent_t e0 = l->timer.begin(s);
-  k_lr_forward<<<nblk((r1 - r0) * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(),
-                                                    l->d_label.as<float>(), r0, r1 - r0, rows, stride,
-                                                    l->d_err.as<float>(), l->d_err2.as<float>());
+  const uint64_t nrb = r1 - r0;
+  const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
+  if (l->rows_per_wave && mf <= 42 && l->rows_per_wave != 2)
+    k_lr_forward_r<3><<<nblk((nrb + 2) / 3 * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(),
+                                                                l->d_label.as<float>(), r0, nrb, rows, stride,
+                                                                l->d_err.as<float>(), l->d_err2.as<float>());
+  else if (l->rows_per_wave && mf <= 64)
+    k_lr_forward_r<2><<<nblk((nrb + 1) / 2 * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(),
+                                                                l->d_label.as<float>(), r0, nrb, rows, stride,
+                                                                l->d_err.as<float>(), l->d_err2.as<float>());
+  else
+    k_lr_forward<<<nblk(nrb * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(),
+                                                 l->d_label.as<float>(), r0, nrb, rows, stride, l->d_err.as<float>(),
+                                                 l->d_err2.as<float>());
   SWPS_HIP(hipGetLastError());
   l->timer.end(0, e0, s);
   hipEvent_t e3 = l->timer.begin(s);
@@ -616,6 +689,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   l->cfg = *cfg;
   l->s = t->stream;
   l->timer.on = cfg->profile != 0;
+  if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;
     return fail(SWPS_E_OOM, "pinned alloc");

@@ -160,3 +160,29 @@ def test_lr_fast_sums_criteo_shape_close_to_exact(lib, gpu):
         ws.append(m.params()[1])
     assert np.abs(ws[1] - ws[0]).max() <= 1e-5 * np.abs(ws[0]).max(), (np.abs(ws[1] - ws[0]).max(),
                                                                        np.abs(ws[0]).max())
+
+
+@pytest.mark.parametrize("fast", [False, True])
+def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
+    """k_lr_forward_r (3 or 2 rows per wave, by the batch's longest row) ==
+    one row per wave, bit for bit: Criteo-shaped rows (39 features: 3 per
+    wave) and the reference's data.txt (its own row lengths)."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(9000, seed=5)
+    res = []
+    for pack in ("0", "1", "2"):
+        monkeypatch.setenv("SWPS_LR_PACK", pack)
+        t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+        m = lib.LR(t, minibatch=1000, init_ref=False, fast_sums=fast)
+        m.load_csr(y, off, f, v)
+        m.init()
+        e = m.train(2)
+        t2 = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+        m2 = lib.LR(t2, minibatch=200, fast_sums=fast)
+        m2.load_text(DATA)
+        m2.init()
+        e2 = m2.train(2)
+        res.append((e, m.params()[1], e2, m2.params()[1]))
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert np.array_equal(a, b)
