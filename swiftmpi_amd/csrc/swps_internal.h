@@ -171,6 +171,7 @@ struct swps_table {
   swps::DevMem scratch;   // per-call row indices
   uint32_t host_nrows = 0;
   swps::DevMem push_scratch, sort_tmp;  // table_push_sources: (row, position) pairs and their sort
+  bool distinct_push = true;  // table_push_sources: one source skips the grouping sort (SWPS_PUSH_DISTINCT=0: off)
   bool slice_push = true;  // table_push_sources: k_push_w2v_multi_t for fp32 D = 256k + t (SWPS_SLICE_PUSH=0: off)
   uint64_t snap_sum = 0;  // checksum of the snapshot last saved from / restored into this table (0: none);
                           // worker-state snapshots record it so a resume pairs the two files of one save

@@ -575,7 +575,7 @@ int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const 
       k_push_w2v_multi_t<3><<<blocks_for(n * 64), 256, 0, s>>>(rows_s, pos_s, n, cap, g, rows, D0, lr, fudge,
                                                                 t->cfg.push_rule);
   };
-  if (distinct) {  // one source: every row once, no grouping sort
+  if (distinct && t->distinct_push) {  // one source: every row once, no grouping sort
     if (slice) {
       go_slice(d_rows, nullptr);
       SWPS_HIP(hipGetLastError());
@@ -650,6 +650,7 @@ int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
   swps_table *t = new swps_table();
   t->cfg = *cfg;
   if (const char *e = getenv("SWPS_SLICE_PUSH")) t->slice_push = atoi(e) != 0;  // A/B timing, tests
+  if (const char *e = getenv("SWPS_PUSH_DISTINCT")) t->distinct_push = atoi(e) != 0;  // A/B: the multi-source path
   if (t->cfg.fudge == 0.0f) t->cfg.fudge = 1e-6f;
   t->esize = cfg->dtype == SWPS_F64 ? 8 : 4;
   if (cfg->layout == SWPS_LAYOUT_W2V) {
