@@ -16,6 +16,7 @@
 // schedules and are exchanged once at setup, so no step needs a handshake.
 // The same protocol as swiftmpi_amd/dist.py's Python driver.
 #include <algorithm>
+#include <cstdlib>
 
 #include "swps_internal.h"
 
@@ -36,9 +37,19 @@ int ShardDriver::setup() {
   rank = comm_rank(c);
   world = comm_world(c);
   // apps whose server work cannot move to another stream run everything on theirs
-  if (ops.set_serve_stream)
-    SWPS_HIP(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
-  else
+  if (ops.set_serve_stream) {
+    // the serve stream (exchanges, owner kernels) at the highest priority, so prep(i+1) on the
+    // compute stream does not delay the critical push -> pull chain: same-box A/B at world 1
+    // (--sharded) 4.0e8 -> 4.29e8 words/s; SWPS_SERVE_PRIO=0: default priority
+    const char *e = getenv("SWPS_SERVE_PRIO");
+    if (!(e && atoi(e) == 0)) {
+      int lo = 0, hi = 0;
+      SWPS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      SWPS_HIP(hipStreamCreateWithPriority(&S, hipStreamNonBlocking, hi));
+    } else {
+      SWPS_HIP(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
+    }
+  } else
     S = ops.cs;
   SWPS_HIP(hipEventCreateWithFlags(&ev_pull, hipEventDisableTiming));
   SWPS_HIP(hipEventCreateWithFlags(&ev_learn, hipEventDisableTiming));
