@@ -3664,15 +3664,18 @@ void swap_prep_set(swps_w2v *w) {
 // is left prepared when the call returns.
 template <typename T, typename A> int train_overlapped(swps_w2v *w, uint64_t count) {
   if (!w->s_prep) {
-    // the prep stream at the lowest priority: its short kernels fill the gaps the learn kernels leave
-    // instead of competing with them for CUs (SWPS_PREP_PRIO=0: default priority, A/B)
     int lo = 0, hi = 0;
     SWPS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    // the prep chain is short latency-bound launches: at the highest priority they take CUs as
+    // soon as they are issued instead of queueing behind the learn kernels (same-box A/B at
+    // B = 100 lines: highest 0.317 ms/step, lowest 0.321); SWPS_PREP_PRIO=0 default, 1 lowest
     const char *pe = getenv("SWPS_PREP_PRIO");
     if (pe && atoi(pe) == 0)
       SWPS_HIP(hipStreamCreateWithFlags(&w->s_prep, hipStreamNonBlocking));
-    else
+    else if (pe && atoi(pe) == 1)
       SWPS_HIP(hipStreamCreateWithPriority(&w->s_prep, hipStreamNonBlocking, lo));
+    else
+      SWPS_HIP(hipStreamCreateWithPriority(&w->s_prep, hipStreamNonBlocking, hi));
     SWPS_HIP(hipEventCreateWithFlags(&w->ev_learn, hipEventDisableTiming));
     SWPS_HIP(hipEventCreateWithFlags(&w->ev_prep, hipEventDisableTiming));
   }
