@@ -97,6 +97,19 @@ int ShardDriver::setup() {
   SWPS_TRY(rgrads.ensure(mr * gb));
   step_keys = ms;
   step_rkeys = mr;
+  // per-slot received keys (SWPS_KEY_CACHE=0: off), when they fit in 2 GiB
+  rk_off.assign(spe + 1, 0);
+  for (uint64_t st = 0; st < spe; st++) {
+    uint64_t nr = 0;
+    for (int r = 0; r < world; r++) nr += recv[st * world + r];
+    rk_off[st + 1] = rk_off[st] + nr;
+  }
+  const char *kc = getenv("SWPS_KEY_CACHE");
+  key_cache = !(kc && atoi(kc) == 0) && rk_off[spe] * 8 <= (2ULL << 30);
+  if (key_cache) {
+    SWPS_TRY(rk_cache.ensure(std::max<uint64_t>(rk_off[spe], 1) * 8));
+    rk_valid.assign(spe, 0);
+  }
   return SWPS_OK;
 }
 
@@ -170,13 +183,20 @@ int ShardDriver::steps(uint64_t count) {
     const bool mine = st < nb;
     // ---- S: pull(i) (C's earlier work on these buffers is ordered by events) ----
     SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
-    if (mine && ns) {
-      std::vector<uint64_t> cnt(world);
-      uint64_t n = 0;
-      SWPS_TRY(ops.request(ops.h, 0, cnt.data(), keys.as<uint64_t>(), &n));
+    // every rank runs the same steps, so every rank takes the same branch (the exchange is collective)
+    const bool kc = key_cache && rk_valid[st];
+    uint64_t *rkp = key_cache ? rk_cache.as<uint64_t>() + rk_off[st] : rkeys.as<uint64_t>();
+    if (!kc) {
+      if (mine && ns) {
+        std::vector<uint64_t> cnt(world);
+        uint64_t n = 0;
+        SWPS_TRY(ops.request(ops.h, 0, cnt.data(), keys.as<uint64_t>(), &n));
+      }
+      SWPS_TRY(exchange(keys.p, sk, rkp, rk, 8, S));
+      if (key_cache) rk_valid[st] = 1;
     }
-    SWPS_TRY(exchange(keys.p, sk, rkeys.p, rk, 8, S));
-    SWPS_TRY(ops.serve_pull(ops.h, rkeys.as<uint64_t>(), rk, 0, vals.p));
+    if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, key_cache ? (int64_t)st : -1));
+    SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, vals.p));
     SWPS_TRY(exchange(vals.p, rk, myvals.p, sk, vb, S));
     SWPS_HIP(hipEventRecord(ev_pull, S));
     // ---- C: learn(i), then prep(i+1) ----
@@ -188,7 +208,8 @@ int ShardDriver::steps(uint64_t count) {
     // ---- S: push(i) ----
     SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
     SWPS_TRY(exchange(grads.p, sk, rgrads.p, rk, gb, S));
-    SWPS_TRY(ops.serve_push(ops.h, rkeys.as<uint64_t>(), rgrads.p, rk));
+    SWPS_TRY(ops.serve_push(ops.h, rkp, rgrads.p, rk));
+    if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, -1));
     cursor++;
   }
   SWPS_HIP(hipEventRecord(ev_learn, S));  // the next call's C work waits for this push

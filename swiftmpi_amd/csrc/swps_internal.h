@@ -201,8 +201,11 @@ int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const voi
 // several sources' pushes concatenated in rank order (keys distinct within a
 // source): each row gets its sources' AdaGrad steps in that order, one pass
 // distinct: one source (no row repeats): no grouping sort
+// sort_cache / sort_valid: the grouping sort's output for these same rows, kept across calls (a
+// static per-step key set): reused when *sort_valid, else computed, stored and *sort_valid set
 int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
-                       bool grads_f32 = false, bool distinct = false);
+                       bool grads_f32 = false, bool distinct = false, swps::DevMem *sort_cache = nullptr,
+                       bool *sort_valid = nullptr);
 // latched device error flags (table full, unknown key) -> error code, no sync
 int table_error_code(uint32_t flags);
 // key-sharded pull / push (swps_comm.hip): collective over t->comm
@@ -234,6 +237,9 @@ struct AppOps {
   int (*serve_push)(void *, const uint64_t *, const void *, const uint64_t *) = nullptr;
   int (*prep)(void *) = nullptr;                      // optional: the next step's param-free half
   int (*set_serve_stream)(void *, void *) = nullptr;  // optional: server work on the driver's stream
+  // optional: the step slot (position in the epoch) the next serve_pull / serve_push belong to, -1 =
+  // none; their received keys are the same every epoch, so the app may cache per-slot lookups
+  int (*set_slot)(void *, int64_t) = nullptr;
 };
 
 struct ShardDriver {
@@ -245,6 +251,12 @@ struct ShardDriver {
   DevMem keys, rkeys, vals, myvals, grads, rgrads;  // per step, sized at setup for the largest step
   DevMem fp_keys, fp_rkeys, fp_vals, fp_myvals;      // the full pull's (whole local vocab)
   uint64_t step_keys = 0, step_rkeys = 0;
+  // the keys each owner receives at a step are the same every epoch (static batch schedules): the
+  // first epoch's key exchange fills rk_cache[slot], later epochs skip the request and the exchange
+  DevMem rk_cache;
+  std::vector<uint64_t> rk_off;  // [spe] element offsets into rk_cache
+  std::vector<char> rk_valid;    // [spe]
+  bool key_cache = false;
   HostStage stage;
   hipStream_t S = nullptr;
   hipEvent_t ev_pull = nullptr, ev_learn = nullptr, ev_x0 = nullptr, ev_x1 = nullptr;

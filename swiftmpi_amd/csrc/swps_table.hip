@@ -552,7 +552,7 @@ int table_push_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const voi
 }
 
 int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_grads, hipStream_t s,
-                       bool grads_f32, bool distinct) {
+                       bool grads_f32, bool distinct, DevMem *sort_cache, bool *sort_valid) {
   if (n == 0) return SWPS_OK;
   if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 pushed keys in one call");
   const uint32_t cap = (uint32_t)t->cfg.capacity;
@@ -585,15 +585,28 @@ int table_push_sources(swps_table *t, const uint32_t *d_rows, uint64_t n, const 
   }
   int bits = 1;
   while ((1ULL << bits) <= cap) bits++;
-  SWPS_TRY(t->push_scratch.ensure(n * 16));
-  uint32_t *key = t->push_scratch.as<uint32_t>(), *pos = key + n, *key_s = pos + n, *pos_s = key_s + n;
-  k_push_keys<<<blocks_for(n), 256, 0, s>>>(d_rows, n, cap, key, pos);
-  SWPS_HIP(hipGetLastError());
-  size_t sb = 0;
-  SWPS_HIP(sort_pairs(nullptr, sb, key, key_s, pos, pos_s, n, bits, s));
-  SWPS_TRY(t->sort_tmp.ensure(sb));
-  sb = t->sort_tmp.bytes;
-  SWPS_HIP(sort_pairs(t->sort_tmp.p, sb, key, key_s, pos, pos_s, n, bits, s));
+  uint32_t *key_s = nullptr, *pos_s = nullptr;
+  if (sort_cache && sort_valid && *sort_valid) {  // the same rows as an earlier call: its grouping
+    key_s = sort_cache->as<uint32_t>();
+    pos_s = key_s + n;
+  } else {
+    SWPS_TRY(t->push_scratch.ensure(n * 16));
+    uint32_t *key = t->push_scratch.as<uint32_t>(), *pos = key + n;
+    key_s = pos + n;
+    pos_s = key_s + n;
+    k_push_keys<<<blocks_for(n), 256, 0, s>>>(d_rows, n, cap, key, pos);
+    SWPS_HIP(hipGetLastError());
+    size_t sb = 0;
+    SWPS_HIP(sort_pairs(nullptr, sb, key, key_s, pos, pos_s, n, bits, s));
+    SWPS_TRY(t->sort_tmp.ensure(sb));
+    sb = t->sort_tmp.bytes;
+    SWPS_HIP(sort_pairs(t->sort_tmp.p, sb, key, key_s, pos, pos_s, n, bits, s));
+    if (sort_cache && sort_valid) {
+      SWPS_TRY(sort_cache->ensure(n * 8));
+      SWPS_HIP(hipMemcpyAsync(sort_cache->p, key_s, n * 8, hipMemcpyDeviceToDevice, s));  // key_s | pos_s
+      *sort_valid = true;
+    }
+  }
   if (slice) {
     go_slice(key_s, pos_s);
   } else if (t->cfg.layout == SWPS_LAYOUT_W2V) {

@@ -27,6 +27,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <memory>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -2005,6 +2006,15 @@ struct swps_w2v {
   std::vector<int32_t> init_order; // vids grouped by owner
   DevMem d_vkeys, d_init_order, d_serve_rows, d_push_rows;
   hipStream_t ss = nullptr;  // serve stream (request / serve_pull / serve_push); nullptr = s
+  // the library driver's step slot (AppOps::set_slot): the keys served at a slot are the same every
+  // epoch, so their row lookups and the push's grouping sort are kept per slot
+  int64_t slot = -1;
+  struct SlotRows {
+    DevMem rows, sorted;
+    uint64_t n = 0;
+    bool sorted_valid = false;
+  };
+  std::vector<std::unique_ptr<SlotRows>> slot_rows;
   std::vector<uint32_t> plan_P;     // kept positions per batch of the current epoch
   // minibatch-vocab mode (word2vec.h MiniBatch, w2v_local.cpp)
   std::vector<int32_t> allUK;       // per batch: its vids in std::map key order (offset kofs)
@@ -4236,6 +4246,17 @@ int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src
   for (int r = 0; r < w->world; r++) n += src_counts[r];
   SWPS_TRY(w->d_serve_rows.ensure(std::max<uint64_t>(n, 1) * 4));
   uint32_t *rows = w->d_serve_rows.as<uint32_t>();
+  if (!insert && w->slot >= 0) {  // a driver step slot: the same keys every epoch
+    while ((uint64_t)w->slot >= w->slot_rows.size()) w->slot_rows.emplace_back(new swps_w2v::SlotRows());
+    auto &e = *w->slot_rows[w->slot];
+    if (e.n != n || !e.rows.p) {
+      SWPS_TRY(e.rows.ensure(std::max<uint64_t>(n, 1) * 4));
+      SWPS_TRY(table_lookup(w->t, d_keys, n, e.rows.as<uint32_t>(), ss));
+      e.n = n;
+      e.sorted_valid = false;
+    }
+    return table_copy_pull(w->t, e.rows.as<uint32_t>(), n, d_vals, ss);
+  }
   if (insert) {  // keys are distinct within a source, not across sources
     uint64_t off = 0;
     for (int r = 0; r < w->world; r++) {
@@ -4289,11 +4310,17 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
   hipStream_t ss = w->ss ? w->ss : w->s;
   uint64_t n = 0;
   for (int r = 0; r < w->world; r++) n += src_counts[r];
-  SWPS_TRY(w->d_push_rows.ensure(std::max<uint64_t>(n, 1) * 4));
-  SWPS_TRY(table_lookup(w->t, d_keys, n, w->d_push_rows.as<uint32_t>(), ss));
   const bool g32 = !w->f64 && !w->cfg.fp64_intermediates;  // fast mode: fp32 push payload
   int nsrc = 0;
   for (int r = 0; r < w->world; r++) nsrc += src_counts[r] > 0;
+  if (w->slot >= 0 && (uint64_t)w->slot < w->slot_rows.size() && w->slot_rows[w->slot]->n == n &&
+      w->slot_rows[w->slot]->rows.p) {  // this slot's pull looked the same keys up
+    auto &e = *w->slot_rows[w->slot];
+    return table_push_sources(w->t, e.rows.as<uint32_t>(), n, d_grads, ss, g32, nsrc <= 1, &e.sorted,
+                              &e.sorted_valid);
+  }
+  SWPS_TRY(w->d_push_rows.ensure(std::max<uint64_t>(n, 1) * 4));
+  SWPS_TRY(table_lookup(w->t, d_keys, n, w->d_push_rows.as<uint32_t>(), ss));
   // one AdaGrad step per source, in rank order, all sources in one pass
   return table_push_sources(w->t, w->d_push_rows.as<uint32_t>(), n, d_grads, ss, g32, nsrc <= 1);
 }
@@ -4327,6 +4354,10 @@ int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
   };
   o.prep = [](void *h) { return swps_w2v_prep((swps_w2v *)h); };
   o.set_serve_stream = [](void *h, void *s) { return swps_w2v_set_serve_stream((swps_w2v *)h, s); };
+  o.set_slot = [](void *h, int64_t slot) {
+    ((swps_w2v *)h)->slot = slot;
+    return (int)SWPS_OK;
+  };
   const int rc = d->setup();
   if (rc) {
     delete d;
