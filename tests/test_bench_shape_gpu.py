@@ -209,3 +209,32 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed,
         assert r.returncode == 0, r.stderr[-2000:]
         res.append([l for l in r.stdout.splitlines() if l.startswith("H ")][-1])
     assert res[0] == res[1], res
+
+
+def test_config4_per_rank_shape(lib, gpu):
+    """BASELINE config 4's per-rank share on one GPU (125M-token Zipf corpus,
+    V = 1M, D = 300, the bench kernels in fast mode): two 5000-line batches
+    train deterministically (50k sampled rows bit-identical run to run),
+    rows stay finite, and the kept / trained word counts are consistent."""
+    import torch
+    from swiftmpi_amd.synth import zipf_tokens
+    V = 1000000
+    ids, off = zipf_tokens(125000000, V, 1000, seed=9)
+    keys = np.array([lib.bkdr("w%d" % i) for i in range(V)], dtype=np.uint64)
+    sample = torch.as_tensor(keys[np.random.default_rng(1).choice(V, 50000, replace=False)].astype(np.int64),
+                             device="cuda")
+    outs = []
+    for _ in range(2):
+        t = lib.Table("w2v", dim=300, capacity=V + 1024, dtype="f32", learning_rate=0.7, init="hash", seed=1)
+        w = lib.Word2Vec(t, minibatch=5000, sample=1e-5, init="table", fp64_intermediates=False)
+        w.load_tokens(ids, off, keys)
+        w.init()
+        w.train_batches(2)
+        w.sync()
+        outs.append((t.export(sample).cpu().numpy(), w.stats()))
+        del w, t
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.isfinite(outs[0][0]).all()
+    st = outs[0][1]
+    assert st["batches"] == 2 and 0 < st["kept"] < st["words"] <= 2 * 5001 * 1000
+    assert st["pairs"] > 10 * st["kept"]
