@@ -393,6 +393,52 @@ int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t>
   return SWPS_OK;
 }
 
+// all-to-all-v with explicit byte displacements: peer r gets sb[r] bytes from d_send + so[r] and
+// sends rb[r] bytes that land at d_recv + ro[r] (a part of a larger exchange, e.g. half of every
+// peer's segment)
+int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb,
+                        const std::vector<uint64_t> &so, void *d_recv, const std::vector<uint64_t> &rb,
+                        const std::vector<uint64_t> &ro, hipStream_t s, HostStage &stg) {
+  uint64_t st = 0, rt = 0;
+  for (int r = 0; r < c->world; r++) {
+    st += sb[r];
+    rt += rb[r];
+  }
+  if (c->world == 1) {
+    if (sb[0]) SWPS_HIP(hipMemcpyAsync((char *)d_recv + ro[0], (const char *)d_send + so[0], sb[0],
+                                       hipMemcpyDeviceToDevice, s));
+    return SWPS_OK;
+  }
+  if (c->rccl) {
+    SWPS_NCCL(ncclGroupStart());
+    for (int r = 0; r < c->world; r++) {
+      if (sb[r]) SWPS_NCCL(ncclSend((const char *)d_send + so[r], sb[r], ncclChar, r, c->nc, s));
+      if (rb[r]) SWPS_NCCL(ncclRecv((char *)d_recv + ro[r], rb[r], ncclChar, r, c->nc, s));
+    }
+    SWPS_NCCL(ncclGroupEnd());
+    return SWPS_OK;
+  }
+  stg.send.resize(std::max<uint64_t>(st, 1));
+  stg.recv.resize(std::max<uint64_t>(rt, 1));
+  uint64_t o = 0;
+  for (int r = 0; r < c->world; r++) {  // pack the segments for the host transport
+    if (sb[r])
+      SWPS_HIP(hipMemcpyAsync(stg.send.data() + o, (const char *)d_send + so[r], sb[r], hipMemcpyDeviceToHost, s));
+    o += sb[r];
+  }
+  SWPS_HIP(hipStreamSynchronize(s));
+  if (c->tr.alltoallv(c->tr.ctx, stg.send.data(), sb.data(), stg.recv.data(), rb.data()) != 0)
+    return fail(SWPS_E_RCCL, "host transport all-to-all-v failed");
+  o = 0;
+  for (int r = 0; r < c->world; r++) {
+    if (rb[r])
+      SWPS_HIP(hipMemcpyAsync((char *)d_recv + ro[r], stg.recv.data() + o, rb[r], hipMemcpyHostToDevice, s));
+    o += rb[r];
+  }
+  SWPS_HIP(hipStreamSynchronize(s));  // stg.recv is reused by the next exchange
+  return SWPS_OK;
+}
+
 int comm_rank(const swps_comm *c) { return c->rank; }
 int comm_world(const swps_comm *c) { return c->world; }
 int comm_device(const swps_comm *c) { return c->device; }

@@ -106,6 +106,10 @@ int ShardDriver::setup() {
   }
   const char *kc = getenv("SWPS_KEY_CACHE");
   key_cache = !(kc && atoi(kc) == 0) && rk_off[spe] * 8 <= (2ULL << 30);
+  // the gradient exchange in two all-to-alls (first halves of every segment as soon as the learner
+  // has them, the rest after it), for apps whose learner computes them in two passes
+  const char *sg = getenv("SWPS_SPLIT_GRADS");
+  split_grads = ops.half_event != nullptr && !(sg && atoi(sg) == 0);
   if (key_cache) {
     SWPS_TRY(rk_cache.ensure(std::max<uint64_t>(rk_off[spe], 1) * 8));
     rk_valid.assign(spe, 0);
@@ -130,6 +134,28 @@ int ShardDriver::exchange(const void *d_send, const uint64_t *sk, void *d_recv, 
     calls++;
   }
   SWPS_TRY(comm_alltoallv(c, d_send, scaled(sk, world, w), d_recv, scaled(rk, world, w), s, stage));
+  if (xprof) {
+    SWPS_HIP(hipEventRecord(ev_x1, s));
+    SWPS_HIP(hipEventSynchronize(ev_x1));  // profiled runs only
+    float ms = 0;
+    SWPS_HIP(hipEventElapsedTime(&ms, ev_x0, ev_x1));
+    xms += ms;
+  }
+  return SWPS_OK;
+}
+
+int ShardDriver::exchange_disp(const void *d_send, const std::vector<uint64_t> &sb, const std::vector<uint64_t> &so,
+                               void *d_recv, const std::vector<uint64_t> &rb, const std::vector<uint64_t> &ro,
+                               hipStream_t s) {
+  if (xprof) {
+    SWPS_HIP(hipEventRecord(ev_x0, s));
+    for (int r = 0; r < world; r++) {
+      bytes_total += sb[r];
+      if (r != rank) bytes_remote += sb[r];
+    }
+    calls++;
+  }
+  SWPS_TRY(comm_alltoallv_disp(c, d_send, sb, so, d_recv, rb, ro, s, stage));
   if (xprof) {
     SWPS_HIP(hipEventRecord(ev_x1, s));
     SWPS_HIP(hipEventSynchronize(ev_x1));  // profiled runs only
@@ -206,8 +232,36 @@ int ShardDriver::steps(uint64_t count) {
     const uint64_t nxt = (cursor + 1) % spe;
     if (ops.prep && k + 1 < count && nxt < nb) SWPS_TRY(ops.prep(ops.h));
     // ---- S: push(i) ----
-    SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
-    SWPS_TRY(exchange(grads.p, sk, rgrads.p, rk, gb, S));
+    // split_grads is the same on every rank (build, environment, world), so every rank issues the
+    // same two collectives; eh (the learner ran its two passes) only decides when the first starts
+    hipEvent_t eh = (mine && ops.half_event) ? (hipEvent_t)ops.half_event(ops.h) : nullptr;
+    if (split_grads && world > 1) {
+      // first halves of every peer's segment (counts floor(n/2), the learner's split), then the rest
+      std::vector<uint64_t> sb(world), so(world), rb(world), ro(world);
+      uint64_t a = 0, b = 0;
+      for (int r = 0; r < world; r++) {
+        sb[r] = (sk[r] / 2) * gb;
+        so[r] = a * gb;
+        rb[r] = (rk[r] / 2) * gb;
+        ro[r] = b * gb;
+        a += sk[r];
+        b += rk[r];
+      }
+      if (eh) SWPS_HIP(hipStreamWaitEvent(S, eh, 0));
+      else SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+      SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S));
+      for (int r = 0; r < world; r++) {
+        so[r] += sb[r];
+        ro[r] += rb[r];
+        sb[r] = (sk[r] - sk[r] / 2) * gb;
+        rb[r] = (rk[r] - rk[r] / 2) * gb;
+      }
+      SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+      SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S));
+    } else {
+      SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+      SWPS_TRY(exchange(grads.p, sk, rgrads.p, rk, gb, S));
+    }
     SWPS_TRY(ops.serve_push(ops.h, rkp, rgrads.p, rk));
     if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, -1));
     cursor++;

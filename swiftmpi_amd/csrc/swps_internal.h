@@ -217,6 +217,9 @@ int check_app_table(swps_table *t);
 int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipStream_t s);
 int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
                    const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg);
+int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb,
+                        const std::vector<uint64_t> &so, void *d_recv, const std::vector<uint64_t> &rb,
+                        const std::vector<uint64_t> &ro, hipStream_t s, HostStage &stg);
 int comm_rank(const swps_comm *c);
 int comm_world(const swps_comm *c);
 int comm_device(const swps_comm *c);
@@ -240,6 +243,9 @@ struct AppOps {
   // optional: the step slot (position in the epoch) the next serve_pull / serve_push belong to, -1 =
   // none; their received keys are the same every epoch, so the app may cache per-slot lookups
   int (*set_slot)(void *, int64_t) = nullptr;
+  // optional: after step(), the event (hipEvent_t) recorded once the first half of every owner's
+  // keys has its gradients (the rest follow in a second pass), or nullptr: one all-to-all
+  void *(*half_event)(void *) = nullptr;
 };
 
 struct ShardDriver {
@@ -257,6 +263,7 @@ struct ShardDriver {
   std::vector<uint64_t> rk_off;  // [spe] element offsets into rk_cache
   std::vector<char> rk_valid;    // [spe]
   bool key_cache = false;
+  bool split_grads = false;  // the gradient all-to-all in two halves (AppOps::half_event)
   HostStage stage;
   hipStream_t S = nullptr;
   hipEvent_t ev_pull = nullptr, ev_learn = nullptr, ev_x0 = nullptr, ev_x1 = nullptr;
@@ -269,5 +276,7 @@ struct ShardDriver {
   int steps(uint64_t count);
   int sync();
   int exchange(const void *d_send, const uint64_t *sk, void *d_recv, const uint64_t *rk, uint64_t w, hipStream_t s);
+  int exchange_disp(const void *d_send, const std::vector<uint64_t> &sb, const std::vector<uint64_t> &so,
+                    void *d_recv, const std::vector<uint64_t> &rb, const std::vector<uint64_t> &ro, hipStream_t s);
 };
 }  // namespace swps

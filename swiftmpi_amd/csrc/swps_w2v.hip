@@ -1248,6 +1248,7 @@ __global__ __launch_bounds__(256) void k_combine(GatherArgs<A> a) {
   }
 }
 
+constexpr int kMaxSplitOwners = 64;
 template <typename T, typename A> struct PushArgs {
   const int32_t *K;
   uint32_t U;
@@ -1270,6 +1271,12 @@ template <typename T, typename A> struct PushArgs {
   const uint32_t *krow;  // k_push_thp: shard row per batch key (k_batch_setup)
   uint32_t SH, SV;       // record slots per position (GatherArgs)
   int full;              // cache-row stores cover the pad too (zeros): SWPS_FULL_LINES
+  // k_push_thp<TO_GRADS> in two passes (sharded learner, world > 1): pass 1 = the first
+  // ohalf[r] keys of every owner r's key range [obnd[r], obnd[r+1]) (K is grouped by owner),
+  // pass 2 = the rest; 0 = every key.  Their all-to-alls then overlap pass 2.
+  int gpass;
+  uint32_t nown;
+  uint32_t obnd[kMaxSplitOwners + 1], ohalf[kMaxSplitOwners];
 };
 
 // Mean gradient (word2vec_global.h:122-134) + AdaGrad ascent
@@ -1704,7 +1711,15 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
     if (more) hn = head(nx);
     const int half = (int)(uh & 1);
     const bool multi = h.i1 - h.i0 > 1;
-    if ((MODE == 1 && multi) || (MODE == 2 && !multi)) {  // the other pass's item
+    bool other = (MODE == 1 && multi) || (MODE == 2 && !multi);
+    if (TO_GRADS && a.gpass) {  // the key's owner range: its first ohalf keys go in pass 1
+      const uint32_t u = (uint32_t)(uh >> 1);
+      uint32_t r = 0;
+      while (r + 1 < a.nown && a.obnd[r + 1] <= u) r++;
+      const bool first = u - a.obnd[r] < a.ohalf[r];
+      other = other || (first != (a.gpass == 1));
+    }
+    if (other) {  // the other pass's item
       if (more && hn.s1 > hn.s0 && hn.i1 - hn.i0 == 1 && MODE != 2)
         ri = run_recs(a.vals, a.pg, a.SH, a.SV, a.HOFF, hn.s0, hn.s1 - hn.s0, (int)(nx & 1), lane);
       if (!more) break;
@@ -1985,6 +2000,9 @@ struct swps_w2v {
   uint32_t push_grid = 0;
   int fwd_g = 4;
   int full_lines = 1;  // neu1/neu1e and cache-row stores write the row pad as zeros (SWPS_FULL_LINES=0: off; A/B)
+  int split_grads = 1;  // sharded learner (world > 1): mean gradients in two owner-half passes (SWPS_SPLIT_GRADS=0: one)
+  hipEvent_t ev_half = nullptr;  // recorded between the two passes of the last step
+  bool half_ready = false;       // the last step ran the two passes (the driver takes and clears it)
   int split_push = 0;  // SWPS_SPLIT_PUSH: 1 = gather beside the push always, -1 = below 64 k keys, 0 = never
                       // (default: same-box A/B at B = 100 lines 0.321 ms/step in one stream vs 0.349 split)
   hipStream_t s_side = nullptr;
@@ -3603,7 +3621,29 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
         goto push_done;
       }
       if (fused_g) {
-        k_push_thp<1, 8, true><<<pgrid, 256, 0, s>>>(pa);
+        const int world = w->world;
+        if (w->split_grads && world > 1 && world <= kMaxSplitOwners) {
+          // two passes, each owner's first half of keys first: the driver sends those gradients
+          // (ev_half) while the second pass runs
+          if (!w->ev_half) SWPS_HIP(hipEventCreateWithFlags(&w->ev_half, hipEventDisableTiming));
+          pa.nown = (uint32_t)world;
+          uint32_t acc = 0;
+          for (int r = 0; r < world; r++) {
+            const uint64_t c = w->bcounts[pb.bi * world + r];
+            pa.obnd[r] = acc;
+            pa.ohalf[r] = (uint32_t)(c / 2);
+            acc += (uint32_t)c;
+          }
+          pa.obnd[world] = acc;
+          pa.gpass = 1;
+          k_push_thp<1, 8, true><<<pgrid, 256, 0, s>>>(pa);
+          SWPS_HIP(hipEventRecord(w->ev_half, s));
+          pa.gpass = 2;
+          k_push_thp<1, 8, true><<<pgrid, 256, 0, s>>>(pa);
+          w->half_ready = true;
+        } else {
+          k_push_thp<1, 8, true><<<pgrid, 256, 0, s>>>(pa);
+        }
         goto push_done;
       }
       if (fused) {
@@ -3753,6 +3793,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_FWD_G")) w->fwd_g = atoi(e);
   if (const char *e = getenv("SWPS_FULL_LINES")) w->full_lines = atoi(e) != 0;
   if (const char *e = getenv("SWPS_SPLIT_PUSH")) w->split_push = atoi(e);
+  if (const char *e = getenv("SWPS_SPLIT_GRADS")) w->split_grads = atoi(e) != 0;
   if (const char *e = getenv("SWPS_PUSH_GRID")) w->push_grid = (uint32_t)std::max(0, atoi(e));
   if (const char *e = getenv("SWPS_MULTI_SORT")) w->multi_sort = atoi(e);        // A/B timing
   if (const char *e = getenv("SWPS_MULTI_CHUNK")) w->multi_chunk = (uint32_t)std::min(128, std::max(0, atoi(e)));
@@ -3811,6 +3852,7 @@ int swps_w2v_destroy(swps_w2v *w) {
   if (w->ev_learn) (void)hipEventDestroy(w->ev_learn);
   if (w->ev_prep) (void)hipEventDestroy(w->ev_prep);
   if (w->ev_fwd) (void)hipEventDestroy(w->ev_fwd);
+  if (w->ev_half) (void)hipEventDestroy(w->ev_half);
   if (w->ev_gat) (void)hipEventDestroy(w->ev_gat);
   if (w->h_small) (void)hipHostFree(w->h_small);
   delete w->drv;
@@ -4354,6 +4396,12 @@ int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
   };
   o.prep = [](void *h) { return swps_w2v_prep((swps_w2v *)h); };
   o.set_serve_stream = [](void *h, void *s) { return swps_w2v_set_serve_stream((swps_w2v *)h, s); };
+  o.half_event = [](void *h) -> void * {
+    swps_w2v *x = (swps_w2v *)h;
+    const bool r = x->half_ready;
+    x->half_ready = false;
+    return r ? (void *)x->ev_half : nullptr;
+  };
   o.set_slot = [](void *h, int64_t slot) {
     ((swps_w2v *)h)->slot = slot;
     return (int)SWPS_OK;
