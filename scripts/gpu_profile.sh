@@ -42,10 +42,12 @@ cp gpurun_out/prof_lr/run_kernel_stats.csv "$OUT/${TAG}_lr_kernel_stats.csv"
 grep '^{' gpurun_out/prof_lr.log | tail -1 > "$OUT/${TAG}_bench_lr_traced.json"
 ls -la "$OUT"
 # sent2vec (config-5 per-rank shape) and word2vec at config 4's per-rank shape (V = 1M, 125M tokens)
-run bench_s2v 600 python3 $R/bench.py --app s2v --steps 32 --warmup 8 || exit $?
+run bench_s2v 900 python3 $R/bench.py --app s2v --steps 150 --warmup 3 || exit $?  # 8192 x 153 = 1.25M docs: config 5 per rank
 grep '^{' gpurun_out/bench_s2v.log | tail -1 > "$OUT/${TAG}_bench_s2v_config5_per_rank.json"
 run bench_c4 900 python3 $R/bench.py --tokens 125000000 --vocab 1000000 --steps 20 --warmup 5 --no-parity-leg --b100-steps 0 --no-cpu-baseline || exit $?
 grep '^{' gpurun_out/bench_c4.log | tail -1 > "$OUT/${TAG}_bench_w2v_config4_per_rank.json"
+run bench_sharded 600 python3 $R/bench.py --sharded --steps 20 --warmup 5 --b100-steps 0 --no-parity-leg --no-cpu-baseline || exit $?
+grep '^{' gpurun_out/bench_sharded.log | tail -1 > "$OUT/${TAG}_bench_w2v_sharded_native_world1.json"
 run bench_default 900 python3 $R/bench.py --steps 20 --warmup 5 || exit $?
 grep '^{' gpurun_out/bench_default.log | tail -1 > "$OUT/${TAG}_bench_w2v_default.json"
 ls -la "$OUT"
