@@ -630,8 +630,8 @@ def bench_other(args):
         step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
         kf = {"kernel": "k_lr_forward", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
               "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
-        kp = {"kernel": "k_lr_records + k_lr_reduce_short + k_lr_reduce_long%s (per-key mean + AdaGrad push)"
-                        % ("" if args.lr_exact else "_fast"),
+        kp = {"kernel": ("k_lr_records + k_lr_reduce_short + k_lr_reduce_long" if args.lr_exact
+                         else "k_lr_records + k_lr_reduce_fused") + " (per-key mean + AdaGrad push)",
               "achieved": push_gbs, "frac": push_gbs / HBM_PEAK_GBS,
               "bytes_per_launch": push_bytes / max(push_n, 1), "avg_launch_ms": push_ms / max(push_n, 1),
               "launches": push_n}

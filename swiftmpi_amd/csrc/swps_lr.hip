@@ -383,6 +383,47 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long_fast(LrReduce a) {
   }
 }
 
+// fast_sums in one launch: the batch's long runs (> kLrShort records) come from a static list
+// built at load (the run lengths depend only on the data), so the first LB blocks reduce them
+// (one block per run, as k_lr_reduce_long_fast) while the other blocks take the short runs (a
+// thread per run, as k_lr_reduce_short): no counter reset, no dependency between the two, one
+// launch instead of three.  Same sums in the same order: bit-identical.
+__global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint32_t *__restrict__ slong,
+                                                         uint32_t NL, uint32_t LB) {
+  __shared__ double ws[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (blockIdx.x < LB) {
+    for (uint32_t q = blockIdx.x; q < NL; q += LB) {
+      const uint32_t r = slong[q];
+      const uint32_t o = a.off[r], c = a.cnt[r];
+      double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      uint32_t k = t;
+      for (; k + 7 * 256 < c; k += 8 * 256) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = a.val[o + k + j * 256];
+#pragma unroll
+        for (int j = 0; j < 8; j++) s8[j] += (double)v[j];
+      }
+      for (; k < c; k += 256) s8[0] += (double)a.val[o + k];
+      const double tot = wave_sum_pl(((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7])));
+      if (lane == 0) ws[wv] = tot;
+      __syncthreads();
+      if (t == 0) lr_apply(a, r, 0.f, c, ((ws[0] + ws[1]) + (ws[2] + ws[3])));
+      __syncthreads();
+    }
+    return;
+  }
+  const uint32_t R = *a.nruns;
+  for (uint32_t r = (blockIdx.x - LB) * blockDim.x + t; r < R; r += (gridDim.x - LB) * blockDim.x) {
+    const uint32_t o = a.off[r], c = a.cnt[r];
+    if (c > kLrShort) continue;  // a long run: the first LB blocks
+    double sum = 0;
+    for (uint32_t i = o; i < o + c; i++) sum += (double)a.val[i];
+    lr_apply(a, r, 0.f, c, sum);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_lr_predict(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
                              const float *__restrict__ fval, uint64_t nr, const uint32_t *__restrict__ vid_row,
                              const float *__restrict__ rows, float *__restrict__ pred) {
@@ -469,6 +510,9 @@ struct swps_lr {
   // (pushed keys) of all batches: vid, start and length relative to the batch; first run and run count per batch
   DevMem d_srow, d_sval, d_ruk, d_roff, d_rcnt, d_bnruns;
   std::vector<uint64_t> brun;
+  std::vector<uint64_t> blong;  // [nb+1] offsets of each batch's long runs in d_slong (k_lr_reduce_fused)
+  DevMem d_slong;
+  int fused_reduce = 1;         // fast sums: k_lr_reduce_fused (SWPS_LR_FUSED=0: memset + short + long; A/B)
   std::vector<uint32_t> bmaxf;  // longest row (features) per batch: k_lr_forward_r's row packing
   int rows_per_wave = 1;        // SWPS_LR_PACK: 0 = one row per wave (k_lr_forward), 2 = at most 2, 1 = by length
   uint64_t max_bnnz = 0;
@@ -570,6 +614,22 @@ int lr_index(swps_lr *l) {
   SWPS_HIP(hipGetLastError());
   SWPS_HIP(hipMemcpyAsync(l->brun.data(), d_brun.p, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipStreamSynchronize(s));
+  // every batch's long runs (> kLrShort records), relative to its first run: k_lr_reduce_fused
+  {
+    std::vector<uint32_t> cnt(R);
+    if (R) SWPS_HIP(hipMemcpy(cnt.data(), l->d_rcnt.p, (uint64_t)R * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> lst;
+    l->blong.assign(nb + 1, 0);
+    for (uint64_t b = 0; b < nb; b++) {
+      l->blong[b] = lst.size();
+      for (uint64_t q = l->brun[b]; q < l->brun[b + 1]; q++)
+        if (cnt[q] > kLrShort) lst.push_back((uint32_t)(q - l->brun[b]));
+    }
+    l->blong[nb] = lst.size();
+    if (lst.empty()) lst.push_back(0);
+    SWPS_TRY(upload(l->d_slong, lst, s));
+    SWPS_HIP(hipStreamSynchronize(s));
+  }
   return SWPS_OK;
 }
 
@@ -652,7 +712,8 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   hipEvent_t e3 = l->timer.begin(s);
   // the run counter lives past the last possible long-run index
   uint32_t *nlong = l->d_longs.as<uint32_t>() + l->max_bnnz;
-  SWPS_HIP(hipMemsetAsync(nlong, 0, 4, s));
+  const bool fused = l->cfg.fast_sums && l->fused_reduce && !l->blong.empty();
+  if (!fused) SWPS_HIP(hipMemsetAsync(nlong, 0, 4, s));
   const uint64_t q0 = l->brun[bi];
   SWPS_TRY(l->d_val_s.ensure(l->max_bnnz * 4));
   k_lr_records<<<nblk(nnz), 256, 0, s>>>(l->d_srow.as<uint32_t>() + nz0, l->d_sval.as<float>() + nz0, nnz,
@@ -662,6 +723,15 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
               l->sharded ? nullptr : l->d_urow.as<uint32_t>() + q0,
               l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, l->d_local.as<int32_t>(),
               l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
+  if (fused) {
+    const uint32_t NL = (uint32_t)(l->blong[bi + 1] - l->blong[bi]);
+    const uint32_t LB = std::min<uint32_t>(NL, 2048);
+    const unsigned sblocks = (unsigned)std::min<uint64_t>(nblk(nnz), 4096);
+    k_lr_reduce_fused<<<LB + sblocks, 256, 0, s>>>(ra, l->d_slong.as<uint32_t>() + l->blong[bi], NL, LB);
+    SWPS_HIP(hipGetLastError());
+    l->timer.end(3, e3, s);
+    return SWPS_OK;
+  }
   k_lr_reduce_short<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(ra);
   if (l->cfg.fast_sums)
     k_lr_reduce_long_fast<<<(unsigned)std::min<uint64_t>(nblk(nnz * 256 / kLrShort), 4096), 256, 0, s>>>(ra);
@@ -690,6 +760,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   l->s = t->stream;
   l->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
+  if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;
     return fail(SWPS_E_OOM, "pinned alloc");

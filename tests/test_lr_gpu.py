@@ -186,3 +186,22 @@ def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
     for r in res[1:]:
         for a, b in zip(res[0], r):
             assert np.array_equal(a, b)
+
+
+def test_lr_fused_reduce_bit_identical(lib, gpu, monkeypatch):
+    """Fast sums: k_lr_reduce_fused (static long-run list, one launch) == the
+    short / long pair with the runtime long list, bit for bit (Criteo shape
+    with hot features: long runs present)."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(20000, seed=7)
+    res = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("SWPS_LR_FUSED", fused)
+        t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+        m = lib.LR(t, minibatch=4095, init_ref=False, fast_sums=True)
+        m.load_csr(y, off, f, v)
+        m.init()
+        e = m.train(2)
+        res.append((e, m.params()[1], m.params()[2]))
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
