@@ -1274,6 +1274,7 @@ template <typename T, typename A> struct PushArgs {
   // k_push_thp<TO_GRADS> in two passes (sharded learner, world > 1): pass 1 = the first
   // ohalf[r] keys of every owner r's key range [obnd[r], obnd[r+1]) (K is grouped by owner),
   // pass 2 = the rest; 0 = every key.  Their all-to-alls then overlap pass 2.
+  uint32_t group;  // runs of more than `group` partials read k_combine's group leaders (kGroup), else all
   int gpass;
   uint32_t nown;
   uint32_t obnd[kMaxSplitOwners + 1], ohalf[kMaxSplitOwners];
@@ -1315,7 +1316,7 @@ __global__ __launch_bounds__(256) void k_push(PushArgs<T, A> a) {
           continue;
         }
         const uint32_t i0 = a.ioff[2 * u + half], i1 = a.ioff[2 * u + half + 1];
-        const uint32_t stride = (i1 - i0) > kGroup ? kGroup : 1;
+        const uint32_t stride = (i1 - i0) > a.group ? kGroup : 1;
         double sum[E];
 #pragma unroll
         for (int k = 0; k < E; k++) sum[k] = 0.0;
@@ -1396,7 +1397,7 @@ __global__ __launch_bounds__(256) void k_push_t(PushArgs<float, float> a) {
       FAcc<NCH> acc;
       acc.zero();
       acc.add(pf[half], tl);
-      const uint32_t stride = (i1[half] - i0[half]) > kGroup ? kGroup : 1;
+      const uint32_t stride = (i1[half] - i0[half]) > a.group ? kGroup : 1;
       for (uint32_t it0 = i0[half] + stride; it0 < i1[half]; it0 += PU * stride) {
         FSlice<NCH> pv[PU];
 #pragma unroll
@@ -1516,7 +1517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         acc.t = (double)(float)c.t;
       } else {
         acc.add(pf[half], tl);
-        const uint32_t stride = (i1[half] - i0[half]) > kGroup ? kGroup : 1;
+        const uint32_t stride = (i1[half] - i0[half]) > a.group ? kGroup : 1;
         for (uint32_t it0 = i0[half] + stride; it0 < i1[half]; it0 += PU * stride) {
           FSlice<NCH> pv[PU];
 #pragma unroll
@@ -1626,7 +1627,7 @@ __global__ __launch_bounds__(256) void k_push_th(PushArgs<float, float> a) {
       acc.t = (double)(float)c.t;
     } else {
       acc.add(pf, tl);
-      const uint32_t stride = (i1 - i0) > kGroup ? kGroup : 1;
+      const uint32_t stride = (i1 - i0) > a.group ? kGroup : 1;
       for (uint32_t it0 = i0 + stride; it0 < i1; it0 += PU * stride) {
         FSlice<NCH> pv[PU];
 #pragma unroll
@@ -1792,7 +1793,7 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
       } else {
         next_recs();
         acc.add(pf, tl);
-        const uint32_t st = (h.i1 - h.i0) > kGroup ? kGroup : 1;
+        const uint32_t st = (h.i1 - h.i0) > a.group ? kGroup : 1;
         for (uint32_t it0 = h.i0 + st; it0 < h.i1; it0 += PU * st) {
           FSlice<NCH> pv[PU];
 #pragma unroll
@@ -1999,6 +2000,11 @@ struct swps_w2v {
                         // 1 = k_push_tg at occupancy 4, 2 = k_push_tg UNR 4, 3 = k_push_th, 4 = k_push_th UNR 16
   uint32_t push_grid = 0;
   int fwd_g = 4;
+  // k_combine pre-sums hot runs' partials in groups of kGroup: 1 always, 0 never (the push reads every
+  // partial), 2 (default) when the batch has at least combine_min records -- measured: -2.6% without it at
+  // B = 5000 (21M records), +1.6% at B = 100 (0.4M), where its launch costs more than the re-reads
+  int combine = 2;
+  uint64_t combine_min = 1ull << 22;
   int full_lines = 1;  // neu1/neu1e and cache-row stores write the row pad as zeros (SWPS_FULL_LINES=0: off; A/B)
   int split_grads = 1;  // sharded learner (world > 1): mean gradients in two owner-half passes (SWPS_SPLIT_GRADS=0: one)
   hipEvent_t ev_half = nullptr;  // recorded between the two passes of the last step
@@ -3049,6 +3055,9 @@ template <int NCH, typename T, typename A> void launch_forward(const FwdArgs<T, 
     k_forward<T, A, NCH, 8><<<nblk((uint64_t)a.P * 64), 256, 0, s>>>(a);
 }
 // at most max_items / kGroup leaders, 4 per block
+inline bool use_combine(const swps_w2v *w, uint64_t M) {
+  return w->combine == 1 || (w->combine == 2 && M >= w->combine_min);
+}
 inline unsigned combine_grid(uint64_t max_items) {
   return (unsigned)std::min<uint64_t>(kCombineGrid, max_items / kGroup / 4 + 1);
 }
@@ -3056,7 +3065,7 @@ template <int NCH, typename T, typename A>
 void launch_gather(const GatherArgs<A> &a, unsigned grid, unsigned cgrid, hipStream_t s) {
   constexpr int UNR = sizeof(A) * V16<T>::E > 16 ? 4 : 8;
   k_gather<T, A, NCH, UNR><<<grid, 256, 0, s>>>(a);
-  k_combine<T, A, NCH><<<cgrid, 256, 0, s>>>(a);
+  if (cgrid) k_combine<T, A, NCH><<<cgrid, 256, 0, s>>>(a);
 }
 template <int NCH, typename T, typename A> void launch_push(const PushArgs<T, A> &a, hipStream_t s) {
   if (a.grads)
@@ -3555,7 +3564,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     const uint64_t gitems =
         fused ? std::min<uint64_t>(pb.max_items, pb.M / multi_chunk(w, P) + pb.M / kChunk + 1) : pb.max_items;
     const unsigned ggrid = (unsigned)std::min<uint64_t>(nblk(gitems * 64), (uint64_t)w->gather_grid);
-    const unsigned cgrid = combine_grid(pb.max_items);
+    const unsigned cgrid = use_combine(w, pb.M) ? combine_grid(pb.max_items) : 0;  // 0: no second level
     hipEvent_t eg = tm.begin(gs);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->tail) {
@@ -3571,7 +3580,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
           k_gather_t<2, 8><<<ggrid, 256, 0, gs>>>(ga);
         else
           k_gather_t<3, 8><<<ggrid, 256, 0, gs>>>(ga);
-        switch (w->NCH) {  // second level over the partials: layout-independent
+        if (cgrid) switch (w->NCH) {  // second level over the partials: layout-independent
           case 2: k_combine<T, A, 2><<<cgrid, 256, 0, gs>>>(ga); break;
           case 3: k_combine<T, A, 3><<<cgrid, 256, 0, gs>>>(ga); break;
           default: k_combine<T, A, 4><<<cgrid, 256, 0, gs>>>(ga); break;
@@ -3602,7 +3611,8 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs,
                       w->d_pvals_s.as<uint32_t>(), w->d_pg.as<float>(), w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
                       pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad), w->d_krow.as<uint32_t>(),
-                      (uint32_t)(N + 1), (uint32_t)(2 * W), w->full_lines};
+                      (uint32_t)(N + 1), (uint32_t)(2 * W), w->full_lines,
+                      use_combine(w, pb.M) ? kGroup : 0xFFFFFFFFu};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       const unsigned pgrid = (unsigned)std::min<uint64_t>(nblk((uint64_t)U * 128),
@@ -3791,6 +3801,8 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_FUSED_PUSH")) w->fused_push = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_PUSH_TG")) w->push_tg_var = atoi(e);          // A/B timing
   if (const char *e = getenv("SWPS_FWD_G")) w->fwd_g = atoi(e);
+  if (const char *e = getenv("SWPS_COMBINE")) w->combine = atoi(e);
+  if (const char *e = getenv("SWPS_COMBINE_MIN")) w->combine_min = strtoull(e, nullptr, 10);
   if (const char *e = getenv("SWPS_FULL_LINES")) w->full_lines = atoi(e) != 0;
   if (const char *e = getenv("SWPS_SPLIT_PUSH")) w->split_push = atoi(e);
   if (const char *e = getenv("SWPS_SPLIT_GRADS")) w->split_grads = atoi(e) != 0;

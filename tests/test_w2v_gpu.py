@@ -56,6 +56,20 @@ def test_train_f64_matches_oracle(lib, oracle_mod, gpu, tmp_path, sample, B, N, 
     assert np.allclose(pg, po, rtol=1e-9, atol=1e-12), np.abs(pg - po).max()
 
 
+@pytest.mark.parametrize("combine", ["1", "0"])
+def test_train_f64_matches_oracle_combine(lib, oracle_mod, gpu, tmp_path, monkeypatch, combine):
+    """Hot runs' partials summed in groups by k_combine (forced on; the default
+    only above 4M records per batch) or one by one in the push: both within the
+    f64 tolerance of the oracle."""
+    monkeypatch.setenv("SWPS_COMBINE", combine)
+    path = zipf_corpus(str(tmp_path / "c.txt"), 203, 350, seed=11)
+    orc, t, w = make(lib, oracle_mod, path, "f64", B=60, N=5, W=5, sample=-1.0)
+    orc.train(2)
+    w.train(2)
+    po, pg = orc.get_params(), w.get_params()
+    assert np.allclose(pg, po, rtol=1e-9, atol=1e-12), np.abs(pg - po).max()
+
+
 def test_train_f32_matches_oracle_f32(lib, oracle_mod, gpu, tmp_path):
     path = zipf_corpus(str(tmp_path / "c.txt"), 251, 500, seed=13)
     orc, t, w = make(lib, oracle_mod, path, "f32", D=32, B=30, N=5, W=5, sample=1e-3)
@@ -363,12 +377,16 @@ def test_alias_sampler_distribution(lib, gpu, tmp_path):
     assert (np.abs(emp - p) <= 5 * sigma + 1e-9).all(), float(np.max(np.abs(emp - p) / sigma))
 
 
-def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch):
+@pytest.mark.parametrize("combine", ["1", "0"])
+def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch, combine):
     """k_push_t (compact-slice push) == k_push, k_push_tg (single-chunk runs
     summed inside the push, three variants) == k_gather_t + k_push_t, padded == D-strided neu1/neu1e
     rows, 128-B padded == D-strided worker-cache rows, and negatives from the
     coarse-indexed run-length unigram table == the
-    1e8-slot table, bit for bit, at the bench's D = 300 (tail) shape in fast mode."""
+    1e8-slot table, bit for bit, at the bench's D = 300 (tail) shape in fast mode --
+    with hot runs' partials pre-summed by k_combine (SWPS_COMBINE=1, the default
+    for large batches) and read one by one by the push (0, small batches)."""
+    monkeypatch.setenv("SWPS_COMBINE", combine)
     rng = np.random.default_rng(21)
     V, lines, L = 3000, 60, 400
     p = 1.0 / np.arange(1, V + 1)
