@@ -1998,8 +1998,8 @@ struct swps_w2v {
   int fused_push = 1;  // fast mode: the push sums single-chunk runs itself (SWPS_FUSED_PUSH=0: k_gather_t + k_push_t)
   int push_tg_var = 5;  // fused push kernel (SWPS_PUSH_TG, A/B): 5 = k_push_thp (default), 0 = k_push_tg UNR 8,
                         // 1 = k_push_tg at occupancy 4, 2 = k_push_tg UNR 4, 3 = k_push_th, 4 = k_push_th UNR 16
-  uint32_t push_grid = 0;
-  int fwd_g = 4;
+  uint32_t push_grid = 0;  // k_push_thp grid cap in blocks (SWPS_PUSH_GRID; 0 = by batch size)
+  int fwd_g = 4;           // k_forward_t rows in flight per wave (SWPS_FWD_G: 4, 8, 16; A/B)
   // k_combine pre-sums hot runs' partials in groups of kGroup: 1 always, 0 never (the push reads every
   // partial), 2 (default) when the batch has at least combine_min records -- measured: -2.6% without it at
   // B = 5000 (21M records), +1.6% at B = 100 (0.4M), where its launch costs more than the re-reads
@@ -2012,7 +2012,7 @@ struct swps_w2v {
   int split_push = 0;  // SWPS_SPLIT_PUSH: 1 = gather beside the push always, -1 = below 64 k keys, 0 = never
                       // (default: same-box A/B at B = 100 lines 0.321 ms/step in one stream vs 0.349 split)
   hipStream_t s_side = nullptr;
-  hipEvent_t ev_fwd = nullptr, ev_gat = nullptr;  // k_forward_t rows in flight per wave (SWPS_FWD_G: 4, 8, 16; A/B)  // k_push_thp grid cap in blocks (SWPS_PUSH_GRID; 0 = by batch size)
+  hipEvent_t ev_fwd = nullptr, ev_gat = nullptr;
   uint32_t multi_chunk = 0;  // SWPS_MULTI_CHUNK: chunk size of multi-chunk runs (1..128; 0 = kChunk)
   int multi_sort = 1;                 // order the multi-chunk items by position (SWPS_MULTI_SORT=0: off; A/B)
   uint64_t multi_sort_min = 65536;    // ... for batches of at least this many kept positions (SWPS_MULTI_SORT_MIN)
