@@ -272,8 +272,8 @@ template <typename T, int NCH, bool TAIL, int G> struct DocCtx {
 // group 0 (the first G context rows) of position q+1 is in flight while
 // position q's targets are reduced, and group 1 of q while group 0 is summed —
 // one exposed memory latency per position at most, instead of one per group.
-template <typename T, int NCH, bool TAIL, int G>
-__global__ __launch_bounds__(256) void k_s2v_docs(S2VDocArgs<T> a) {
+template <typename T, int NCH, bool TAIL, int G, int WPE = 1>  // WPE: occupancy floor (1 = none)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_s2v_docs(S2VDocArgs<T> a) {
   using C = DocCtx<T, NCH, TAIL, G>;
   using SL = typename C::SL;
   using AC = typename C::AC;
@@ -642,8 +642,14 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   return SWPS_OK;
 }
 
-template <typename T, int NCH, bool TAIL> void launch_docs(const S2VDocArgs<T> &a, hipStream_t s) {
-  k_s2v_docs<T, NCH, TAIL, 8><<<nblk(a.nd * 64), 256, 0, s>>>(a);
+template <typename T, int NCH, bool TAIL> void launch_docs(const S2VDocArgs<T> &a, hipStream_t s, int wpe) {
+  // one sentence per wave is a serial chain (one exposed latency per position): 4 waves per SIMD
+  // (143 -> 128 VGPRs, 38 spilled) beat 3 by 8 % at D = 300; 5 (180 spilled) lose 26 %.
+  // SWPS_S2V_WPE=1: the unconstrained allocation (A/B)
+  if (NCH == 1 && wpe == 4)
+    k_s2v_docs<T, NCH, TAIL, 8, 4><<<nblk(a.nd * 64), 256, 0, s>>>(a);
+  else
+    k_s2v_docs<T, NCH, TAIL, 8><<<nblk(a.nd * 64), 256, 0, s>>>(a);
 }
 
 // minibatches [c0, c1) (consecutive, no wrap) in one records + docs launch
@@ -684,14 +690,18 @@ template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1) {
                    m->cfg.niters, m->cfg.alpha, m->d_out.as<T>(), m->d_err.as<float>(),
                    m->d_rows_read.as<unsigned long long>()};
   hipEvent_t e1 = ev_begin(m);
+  static const int wpe = [] {
+    const char *e = getenv("SWPS_S2V_WPE");
+    return e ? atoi(e) : 4;
+  }();
   switch (m->NCH * 2 + (m->tail ? 1 : 0)) {
-    case 2: launch_docs<T, 1, false>(da, s); break;
-    case 3: launch_docs<T, 1, true>(da, s); break;
-    case 4: launch_docs<T, 2, false>(da, s); break;
-    case 5: launch_docs<T, 2, true>(da, s); break;
-    case 6: launch_docs<T, 3, false>(da, s); break;
-    case 7: launch_docs<T, 3, true>(da, s); break;
-    default: launch_docs<T, 4, false>(da, s); break;
+    case 2: launch_docs<T, 1, false>(da, s, wpe); break;
+    case 3: launch_docs<T, 1, true>(da, s, wpe); break;
+    case 4: launch_docs<T, 2, false>(da, s, wpe); break;
+    case 5: launch_docs<T, 2, true>(da, s, wpe); break;
+    case 6: launch_docs<T, 3, false>(da, s, wpe); break;
+    case 7: launch_docs<T, 3, true>(da, s, wpe); break;
+    default: launch_docs<T, 4, false>(da, s, wpe); break;
   }
   SWPS_HIP(hipGetLastError());
   ev_end(m, ST_DOC, e1);
