@@ -3511,8 +3511,6 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
             k_forward_t<1, 8, 1><<<nblk(P * 64), 256, 0, s>>>(fa);
           else if (w->fwd_g == 16)
             k_forward_t<1, 16, 1><<<nblk(P * 64), 256, 0, s>>>(fa);
-          else if (w->fwd_g == 48)  // G = 4 at 8 waves per SIMD (A/B)
-            k_forward_t<1, 4, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
           else
             k_forward_t<1, 4, 1><<<nblk(P * 64), 256, 0, s>>>(fa);  // G = 4: occupancy 7 (A/B: G = 2..8)
         } else if (D < 768)
