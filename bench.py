@@ -190,10 +190,13 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=1000000, help="LR CPU baseline sample (rows)")
     ap.add_argument("--cpu-docs", type=int, default=3000, help="sent2vec CPU baseline sample (documents)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--parity", action="store_true",
-                    help="time the fp64-intermediate parity mode instead of the default fast mode")
+    ap.add_argument("--precision", default="bfp40", choices=["bfp40", "bfp32", "fast", "parity"],
+                    help="fp32-table intermediates: bfp40 (block-floating-point neu1/neu1e, int32 + int8 "
+                         "mantissas per row exponent, fp64 sums: within the north star's 1e-5 single-batch bar; "
+                         "the default), bfp32 (int32 mantissas), fast (fp32), parity (fp64)")
+    ap.add_argument("--parity", action="store_true", help="= --precision parity")
     ap.add_argument("--no-parity-leg", action="store_true",
-                    help="skip the extra parity-mode timing reported beside the fast-mode value")
+                    help="skip the extra parity- and fast-mode timings reported beside the headline")
     ap.add_argument("--b100-steps", type=int, default=200,
                     help="minibatches of the extra B = 100 leg (SURVEY.md §8(d) config 1's minibatch); 0 = skip")
     ap.add_argument("--sampler", default="table", choices=["table", "alias"],
@@ -293,9 +296,15 @@ def main():
         s1 = w.stats()
         return dt, {k: s1[k] - s0[k] for k in s1 if k not in ("lstate", "fstate")}
 
-    parity_main = args.parity
+    if args.parity:
+        args.precision = "parity"
+    prec = args.precision
+    parity_main = prec == "parity"
+    bfp_main = prec.startswith("bfp") and args.dtype == "f32"
+    rb = 1 if prec == "bfp40" else 0  # BFP residual bytes per element
+    INTER = {"bfp40": "bfp40", "bfp32": "bfp32", "fast": False, "parity": True}
     pipelined = sharded and args.pipeline
-    t, w = build(fp64_intermediates=parity_main)
+    t, w = build(fp64_intermediates=INTER[prec])
     info = w.info()
     w.train_batches(args.warmup)
     w.sync()
@@ -325,13 +334,17 @@ def main():
         total_words = float(words)
 
     D, es = args.dim, (8 if args.dtype == "f64" else 4)
-    ea = 8 if (parity_main or args.dtype == "f64") else 4   # neu1/neu1e/partials element size
+    ea = 8 if (parity_main or args.dtype == "f64") else 4   # neu1/neu1e element size
+    # BFP modes: a record reads its position's mantissas (4 B, + the int8 residual in bfp40) per
+    # element and the row scale (4 B); partials and the mean-gradient payload are fp64
+    rec_row = D * (4 + rb) + 4 if bfp_main else D * ea
+    pa = 8 if bfp_main else ea
     kept = d["kept"]
     # SURVEY.md §8(d) algorithmic bytes of k_forward: every context/target row
     # occurrence read (4·D per row in fp32) + neu1, neu1e written (2·D·ea per position)
     ctx_rows, tgt_rows = dp["ctx_rows"], dp["tgt_rows"]
     fwd_ms, fwd_n = kt["forward"]
-    fwd_bytes = es * D * (ctx_rows + tgt_rows) + 2 * ea * D * dp["kept"]
+    fwd_bytes = es * D * (ctx_rows + tgt_rows) + 2 * rec_row * dp["kept"]
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
     # the dominant kernel by time: the segmented gradient sums + AdaGrad push.
     # Algorithmic bytes: each gradient record reads its source row (neu1 or neu1e of its
@@ -353,14 +366,15 @@ def main():
     split = nbat > 0 and g1.get("split", 0) - g0.get("split", 0) == nbat
     gat_ms, gat_n = kt["gather"]
     push_ms, push_n = kt.get("push", (0.0, 0))
-    if fused_g:  # sharded learner: the fused push stops at the mean gradients (2·D·ea written per key)
-        sum_kernel = ("k_gather_t + k_combine + k_push_thp<TO_GRADS> (segmented gradient sums + fused mean "
-                      "gradients of the push payload)")
-        gat_bytes = g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) + dp["pushed"] * (2 * D * ea + 8)
+    kn = ("k_gather_b", "k_combine_b", "k_push_b") if bfp_main else ("k_gather_t", "k_combine", "k_push_thp")
+    if fused_g:  # sharded learner: the fused push stops at the mean gradients (2·D·pa written per key)
+        sum_kernel = ("%s + %s + %s<TO_GRADS> (segmented gradient sums + fused mean "
+                      "gradients of the push payload)" % kn)
+        gat_bytes = g_rec * (rec_row + 4) + g_mitems * (2 * D * pa + 16) + dp["pushed"] * (2 * D * pa + 8)
         sum_ms = push_ms if split else gat_ms + push_ms
     elif fused:
-        sum_kernel = "k_gather_t + k_combine + k_push_thp (segmented gradient sums + fused AdaGrad push)"
-        gat_bytes = (g_rec * (D * ea + 4) + g_mitems * (2 * D * ea + 16) +
+        sum_kernel = "%s + %s + %s (segmented gradient sums + fused AdaGrad push)" % kn
+        gat_bytes = (g_rec * (rec_row + 4) + g_mitems * (2 * D * pa + 16) +
                      dp["pushed"] * (10 * es * D + 8))
         sum_ms = push_ms if split else gat_ms + push_ms
     else:
@@ -406,14 +420,15 @@ def main():
     traffic, traffic_src, fwd_traffic = None, None, None
     # (per-launch bytes do not depend on --steps / --warmup: only the workload
     # keys must match)
-    pmc_name = "r02_pmc_w2v_fast.json"
+    pmc_name = "r03_pmc_w2v_%s.json" % prec
     pmc = os.path.join(ROOT, "profiles", pmc_name)
-    mine = dict(minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, mode="fast", world=world,
-                tokens=args.tokens, vocab=args.vocab, line_len=args.line_len)
+    mine = dict(minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, mode=prec, world=world,
+                tokens=args.tokens, vocab=args.vocab, line_len=args.line_len, sharded=bool(sharded))
     if os.path.exists(pmc) and not parity_main:
         prof = json.load(open(pmc))
         if {k: prof.get("config", {}).get(k) for k in mine} == mine:
-            grp = ("k_gather", "k_combine") + (("k_push_tg", "k_push_th") if (fused or fused_g) else ())
+            grp = (("k_gather_b", "k_combine_b") + (("k_push_b",) if (fused or fused_g) else ()) if bfp_main else
+                   ("k_gather", "k_combine") + (("k_push_tg", "k_push_th") if (fused or fused_g) else ()))
             gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items() if k.startswith(grp)]
             if gt and (not (fused or fused_g) or any(k.startswith(grp[2:]) for k in prof["kernels"])):
                 traffic = sum(gt)  # per step: one launch of each kernel of the group
@@ -422,7 +437,7 @@ def main():
                 if k.startswith("k_forward"):
                     fwd_traffic = v["hbm_bytes_corrected"]
 
-    parity_leg = None
+    parity_leg, fast_leg = None, None
     if rank == 0 and world == 1 and not parity_main and not args.no_parity_leg:
         t2, w2 = build(fp64_intermediates=True)
         w2.train_batches(args.warmup)
@@ -431,12 +446,20 @@ def main():
         parity_leg = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
                       "mode": "fp64 neu1/neu1e + gradient partials (reference-parity mode)"}
         del w2, t2
+    if rank == 0 and world == 1 and bfp_main and not args.no_parity_leg:
+        t2, w2 = build(fp64_intermediates=False)
+        w2.train_batches(args.warmup)
+        w2.sync()
+        pdt, pd = timed(w2, args.steps)
+        fast_leg = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
+                    "mode": "fp32 neu1/neu1e + partials (fast mode: outside the 1e-5 single-batch bar at D = 100)"}
+        del w2, t2
     # SURVEY.md §8(d) config 1's minibatch (B = 100 lines of the same
     # 1000-token lines), same mode as the headline, timed the same way over
     # --b100-steps minibatches (the driver-visible small-batch number)
     b100_leg = None
     if rank == 0 and world == 1 and not sharded and args.b100_steps > 0 and args.minibatch != 100:
-        t3, w3 = build(fp64_intermediates=parity_main, minibatch=100)
+        t3, w3 = build(fp64_intermediates=INTER[prec], minibatch=100)
         w3.train_batches(10)
         w3.sync()
         bdt, bd = timed(w3, args.b100_steps)
@@ -456,10 +479,17 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("f32 table, f64 intermediates + accumulate" if parity_main else
-                  "f32 table, f32 intermediates, f64 accumulate") if args.dtype == "f32" else "f64",
+        "dtype": {"parity": "f32 table, f64 intermediates + accumulate",
+                  "bfp40": "f32 table, block-fp intermediates (int32+int8 mantissas/row exponent), f64 accumulate",
+                  "bfp32": "f32 table, block-fp intermediates (int32 mantissas/row exponent), f64 accumulate",
+                  "fast": "f32 table, f32 intermediates, f64 accumulate"}[prec] if args.dtype == "f32" else "f64",
         "data": "synthetic Zipf(s=1) text8 stand-in, random-init (reference glibc-rand) params",
-        "config": {"mode": ("parity (fp64 intermediates)" if parity_main else "fast (fp32 intermediates)") +
+        "config": {"mode": {"parity": "parity (fp64 intermediates)",
+                            "bfp40": "bfp40 (block-fp neu1/neu1e: int32 + int8 mantissas, one exponent per row; "
+                                     "fp64 sums and mean)",
+                            "bfp32": "bfp32 (block-fp neu1/neu1e: int32 mantissas, one exponent per row; "
+                                     "fp64 sums and mean)",
+                            "fast": "fast (fp32 intermediates)"}[prec] +
                            (", alias sampler" if args.sampler == "alias" else ""),
                    "workload": "word2vec CBOW-NS (the reference's 'SGNS' app) text8-shaped corpus %d tokens, "
                                "vocab %d, dim %d, window %d, negative %d, sample %g, minibatch %d lines of %d "
@@ -491,7 +521,7 @@ def main():
                      # k_forward: its row-occurrence bytes exceed its HBM traffic (hot Zipf rows
                      # hit in L2/MALL), so its "achieved" can pass the HBM peak; hbm_GBps is the
                      # PMC-measured HBM rate of the same launches
-                     "forward": {"kernel": "k_forward_t", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
+                     "forward": {"kernel": "k_forward_b" if bfp_main else "k_forward_t", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
                                  "bytes_per_launch": fwd_bytes / max(fwd_n, 1),
                                  "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n,
                                  "traffic": fwd_traffic,
@@ -501,6 +531,7 @@ def main():
                      "pull_push": pp or None},
         "kernel_ms": {k: v[0] for k, v in kt.items()},
         "parity_mode": parity_leg,
+        "fast_mode": fast_leg,
         "minibatch_100": b100_leg,
         "exchange": exchange,
     }

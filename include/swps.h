@@ -232,8 +232,13 @@ typedef struct {
   int32_t init_mode;           /* SWPS_W2V_INIT_* */
   uint32_t rand_seed;          /* glibc srand seed (reference: 1) */
   uint64_t rand_offset;        /* rand() calls before the first pull (reference: 2 port binds) */
-  int32_t fp64_intermediates;  /* 1: neu1/neu1e and gradient sums kept in fp64 like the reference's Vec
-                                * (parity mode for fp32 tables); 0: fp32 (fast mode). fp64 tables: always */
+  int32_t fp64_intermediates;  /* fp32 tables, the type of learn_instance's intermediates neu1/neu1e:
+                                * SWPS_INTER_FP64 (1): fp64 like the reference's Vec (parity mode);
+                                * SWPS_INTER_FP32 (0): fp32 (fast mode); SWPS_INTER_BFP40 (2) / _BFP32 (3):
+                                * block floating point rows — int32 (+ int8) mantissas under one exponent
+                                * per row, 5 (4) B/element, 2^-40 (2^-32) of the row's largest element —
+                                * with fp64 sums, mean and push payload (dim % 4 == 0, dim <= 512).
+                                * fp64 tables: always fp64 */
   int32_t profile;             /* 1: time kernels with HIP events */
   int32_t minibatch_vocab;     /* 0: apps/word2vec/word2vec_global.h (w2v.cpp): one vocab and unigram
                                 * table for the corpus, a full-vocab worker cache, B+3-line gather windows;
@@ -248,6 +253,11 @@ typedef struct {
                                 * key sets; bit-identical to the host restatement); 1: on the host (kept
                                 * for A/B and parity tests; minibatch_vocab mode always ingests on the host) */
 } swps_w2v_cfg;
+
+#define SWPS_INTER_FP32 0
+#define SWPS_INTER_FP64 1
+#define SWPS_INTER_BFP40 2
+#define SWPS_INTER_BFP32 3
 
 #define SWPS_SAMPLER_TABLE 0
 #define SWPS_SAMPLER_ALIAS 1
@@ -339,8 +349,8 @@ int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src
                         void *d_vals);
 int swps_w2v_install_init(swps_w2v *w, const void *d_vals);
 /* d_grads: mean gradients [U][h|v] in the context's intermediate type — fp64
- * (the reference's wire format) unless the table is SWPS_F32 with
- * fp64_intermediates = 0 (fast mode), then fp32 (half the exchange bytes). */
+ * (the reference's wire format; SWPS_INTER_FP64 and the BFP modes) unless the table is
+ * SWPS_F32 with SWPS_INTER_FP32 (fast mode), then fp32 (half the exchange bytes). */
 int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads);
 /* Prepare the next minibatch's parameter-independent half (epoch plan, local
  * key map, learn_instance's draws as position/gradient records, the sorted

@@ -65,6 +65,7 @@ def lib():
         L.orc_w2v_create.restype = _p
         L.orc_w2v_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(W2VCfg)]
         L.orc_w2v_destroy.argtypes = [_p]
+        L.orc_set_diag_round.argtypes = [ctypes.c_int]
         for n in ("orc_w2v_vocab_size", "orc_w2v_train_words"):
             getattr(L, n).restype = _u64
             getattr(L, n).argtypes = [_p]

@@ -196,7 +196,79 @@ struct SParam {
 struct Grad {
   std::vector<double> hg, vg;
   int hc = 0, vc = 0;
+  std::vector<double> hp, vp;  // orc_diag_round bit 2: the current 128-record chunk's partial
 };
+
+// Diagnostic only (scripts/diag_fast.py): emulate one fp32 rounding of the
+// GPU's fp32-intermediate kernels at a time, to attribute their distance from
+// this oracle.  bit 0: g*neu1 formed from neu1 rounded to fp32; bit 1: neu1e
+// rounded to fp32 before accu_v; bit 2: every 128-record chunk of a (key,
+// kind) run summed alone and rounded to fp32 (k_gather_t partials; a run of
+// <= 128 records is one chunk); bit 3: the mean rounded to fp32; bit 4: bits
+// 0 and 1 keep a bf16 residual (x = fp32 hi + bf16 lo, the hi/lo storage).
+// 0 = the reference's arithmetic.
+static int orc_diag_round = 0;
+static inline double diag_bf16(float x) {  // round to nearest even bf16
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  u = (u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u;
+  float y;
+  memcpy(&y, &u, 4);
+  return (double)y;
+}
+static inline double diag_r(double x, int bit) {
+  if (!((orc_diag_round >> bit) & 1)) return x;
+  const float hi = (float)x;
+  if (bit <= 1 && (orc_diag_round & 16)) return (double)hi + diag_bf16((float)(x - (double)hi));
+  if (bit <= 1 && (orc_diag_round & 32) && hi != 0.f) {  // int16 residual in units of ulp(hi) / 2^16
+    int e;
+    std::frexp(hi, &e);
+    const double u = std::ldexp(1.0, e - 24 - 16);
+    double q = std::nearbyint((x - (double)hi) / u);
+    q = std::max(-32768.0, std::min(32767.0, q));
+    return (double)hi + q * u;
+  }
+  return (double)hi;
+}
+// a whole neu1 / neu1e row: bit 6 = int16 residual in units of 2^-16 ulp of the row's largest
+// element (one scale per row; bit 7: int8, 2^-8 ulp), else element-wise diag_r
+static inline void diag_row(const std::vector<double> &x, std::vector<double> &out, int bit) {
+  out = x;
+  if (!((orc_diag_round >> bit) & 1)) return;
+  if (orc_diag_round & (256 | 512)) {  // bits 8 / 9: block floating point, int32 / int40 mantissas, one exponent
+    double mx = 0;
+    for (double v : x) mx = std::max(mx, std::fabs(v));
+    if (mx == 0) return;
+    int e;
+    std::frexp(mx, &e);
+    const int mb = (orc_diag_round & 256) ? 31 : 39;
+    const double u = std::ldexp(1.0, e - mb);
+    for (size_t i = 0; i < x.size(); i++) out[i] = std::nearbyint(x[i] / u) * u;
+    return;
+  }
+  if (!(orc_diag_round & 64)) {
+    for (auto &v : out) v = diag_r(v, bit);
+    return;
+  }
+  int emax = -1000;
+  for (double v : x) {
+    const float hi = (float)v;
+    if (hi != 0.f) {
+      int e;
+      std::frexp(hi, &e);
+      emax = std::max(emax, e);
+    }
+  }
+  const int rb = (orc_diag_round & 128) ? 8 : 16;  // bit 7: an int8 residual instead of int16
+  const double u = std::ldexp(1.0, std::max(emax - 24 - rb, -149));
+  const double qm = rb == 8 ? 127.0 : 32767.0;
+  for (size_t i = 0; i < x.size(); i++) {
+    const float hi = (float)x[i];
+    double q = std::nearbyint((x[i] - (double)hi) / u);
+    q = std::max(-qm, std::min(qm, q));
+    out[i] = (double)hi + q * u;
+  }
+}
 
 static inline double store_round(double x, bool f32) { return f32 ? (double)(float)x : x; }
 
@@ -376,6 +448,16 @@ struct W2V {
     }
     return it->second;
   }
+  std::vector<double> &chunk_part(std::vector<double> &p) {
+    if (p.empty()) p.assign(D(), 0);
+    return p;
+  }
+  static void flush_part(std::vector<double> &p, std::vector<double> &tot) {
+    for (size_t i = 0; i < p.size(); i++) {
+      tot[i] += (double)(float)p[i];
+      p[i] = 0;
+    }
+  }
   Grad &grad_row(uint64_t k) {
     auto it = grads.find(k);
     if (it == grads.end()) {
@@ -395,7 +477,7 @@ struct W2V {
     int b = (int)(lcg_next(rng) % (uint64_t)W);
     (void)b;
     int n = (int)w.size();
-    std::vector<double> neu1(Dd), neu1e(Dd), tmp(Dd);
+    std::vector<double> neu1(Dd), neu1e(Dd), tmp(Dd), n1r, n1er;
     const bool local = cfg.minibatch_vocab != 0;
     for (int pos = 0; pos < n; pos++) {
       uint64_t word = w[pos];
@@ -411,6 +493,7 @@ struct W2V {
         Row &r = cache_row(w[c]);
         for (int i = 0; i < Dd; i++) neu1[i] += r.v[i];
       }
+      diag_row(neu1, n1r, 0);
       for (int d = 0; d < N + 1; d++) {
         uint64_t target;
         int label;
@@ -448,18 +531,23 @@ struct W2V {
         }
         Grad &gr = grad_row(target);
         gr.hc++;
+        std::vector<double> &hacc = (orc_diag_round & 4) ? chunk_part(gr.hp) : gr.hg;
         for (int i = 0; i < Dd; i++) {
-          double p = (double)g * neu1[i];
-          gr.hg[i] += p;
+          double p = (double)g * n1r[i];
+          hacc[i] += p;
         }
+        if ((orc_diag_round & 4) && gr.hc % 128 == 0) flush_part(gr.hp, gr.hg);
       }
+      diag_row(neu1e, n1er, 1);
       for (int a = b; a < W * 2 + 1 - b; a++) {
         if (a == W) continue;
         int c = pos - W + a;
         if (c < 0 || c >= n) continue;
         Grad &gr = grad_row(w[c]);
         gr.vc++;
-        for (int i = 0; i < Dd; i++) gr.vg[i] += neu1e[i];
+        std::vector<double> &vacc = (orc_diag_round & 4) ? chunk_part(gr.vp) : gr.vg;
+        for (int i = 0; i < Dd; i++) vacc[i] += n1er[i];
+        if ((orc_diag_round & 4) && gr.vc % 128 == 0) flush_part(gr.vp, gr.vg);
       }
     }
   }
@@ -506,11 +594,15 @@ struct W2V {
       auto git = grads.find(k);
       if (git == grads.end()) continue;
       Grad &g = git->second;
+      if (orc_diag_round & 4) {
+        if (g.hc % 128) flush_part(g.hp, g.hg);
+        if (g.vc % 128) flush_part(g.vp, g.vg);
+      }
       std::vector<double> hg = g.hg, vg = g.vg;
       if (g.hc > 0)
-        for (auto &x : hg) x /= g.hc;
+        for (auto &x : hg) x = diag_r(x / g.hc, 3);
       if (g.vc > 0)
-        for (auto &x : vg) x /= g.vc;
+        for (auto &x : vg) x = diag_r(x / g.vc, 3);
       std::fill(g.hg.begin(), g.hg.end(), 0.0);
       std::fill(g.vg.begin(), g.vg.end(), 0.0);
       g.hc = g.vc = 0;
@@ -693,6 +785,7 @@ void *orc_w2v_create(const char *corpus_path, const orc_w2v_cfg *c) {
 }
 
 void orc_w2v_destroy(void *h) { delete (W2V *)h; }
+void orc_set_diag_round(int bits) { orc_diag_round = bits; }
 
 uint64_t orc_w2v_vocab_size(void *h) { return ((W2V *)h)->wordids.size(); }
 uint64_t orc_w2v_train_words(void *h) { return ((W2V *)h)->train_words; }

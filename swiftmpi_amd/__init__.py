@@ -234,8 +234,16 @@ class Table:
 KT_NAMES = ["plan", "forward", "sort", "gather", "push", "pull", "records"]
 
 
+INTERMEDIATES = {False: 0, True: 1, "fp32": 0, "fp64": 1, "bfp40": 2, "bfp32": 3, 0: 0, 1: 1, 2: 2, 3: 3}
+
+
 class Word2Vec:
-    """CBOW negative-sampling word2vec (Word2Vec<MiniBatch>, word2vec_global.h:541-748)."""
+    """CBOW negative-sampling word2vec (Word2Vec<MiniBatch>, word2vec_global.h:541-748).
+
+    fp64_intermediates (fp32 tables): True / "fp64" = parity mode (neu1/neu1e and
+    sums in fp64), False / "fp32" = fast mode (fp32 intermediates), "bfp40" /
+    "bfp32" = block-floating-point neu1/neu1e rows (int32 + int8 / int32
+    mantissas, one exponent per row) with fp64 sums (swps_w2v_bfp.h)."""
 
     def __init__(self, table, window=5, negative=5, min_sentence_length=1, minibatch=100, sample=1e-5, alpha=0.05,
                  unigram_size=int(1e8), key_mode="bkdr", init="ref", rand_seed=1, rand_offset=2, profile=False,
@@ -244,7 +252,7 @@ class Word2Vec:
         cfg = capi.W2VCfg(window, negative, min_sentence_length, minibatch, sample, alpha, unigram_size,
                           capi.KEY_ATOI if key_mode == "atoi" else capi.KEY_BKDR,
                           capi.W2V_INIT_REF if init == "ref" else capi.W2V_INIT_TABLE, rand_seed, rand_offset,
-                          int(fp64_intermediates), int(profile), int(minibatch_vocab),
+                          INTERMEDIATES[fp64_intermediates], int(profile), int(minibatch_vocab),
                           {"table": 0, "alias": 1}[sampler], int(host_ingest))
         h = ctypes.c_void_p()
         check(capi.lib().swps_w2v_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))

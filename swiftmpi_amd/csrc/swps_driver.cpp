@@ -168,6 +168,9 @@ int ShardDriver::exchange_disp(const void *d_send, const std::vector<uint64_t> &
 
 int ShardDriver::full_pull() {
   SWPS_TRY(sync());  // the full pull reuses the step buffers
+  // its request / serve_pull run on ops.cs like its exchanges (a second full pull would otherwise
+  // find them on the serve stream S set below, unordered with the exchanges)
+  if (ops.set_serve_stream) SWPS_TRY(ops.set_serve_stream(ops.h, nullptr));
   std::vector<uint64_t> cnt(world), all((size_t)world * world);
   uint64_t n = 0;
   SWPS_TRY(ops.request(ops.h, 1, cnt.data(), nullptr, &n));

@@ -1143,6 +1143,7 @@ int swps_lr_shard_comm(swps_lr *l, swps_comm *c, int32_t frag_num) {
   if (!c) return fail(SWPS_E_CFG, "null communicator");
   if (comm_device(c) != l->t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");
   if (l->t->comm && l->t->comm != c) return fail(SWPS_E_CFG, "the table is routed over another communicator");
+  if (l->drv) return fail(SWPS_E_STATE, "swps_lr_shard_comm was already called on this context");
   SWPS_TRY(swps_lr_shard(l, comm_rank(c), comm_world(c), frag_num));
   ShardDriver *d = new ShardDriver();
   d->c = c;

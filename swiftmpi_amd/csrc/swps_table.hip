@@ -90,6 +90,9 @@ __global__ void k_lookup(const uint64_t *__restrict__ keys, uint64_t n, const ui
     uint64_t k = tkeys[s];
     if (k == key) {
       row = slot_row[s];
+      // a key whose insert found the shard full owns its slot but no row: a miss (the
+      // insert already latched the table-full error), never a row index
+      if (row == kFullRow) row = kNoRow;
       break;
     }
     if (k == kEmptyKey) break;

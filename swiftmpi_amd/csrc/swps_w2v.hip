@@ -1847,6 +1847,33 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
   }
 }
 
+#include "swps_w2v_bfp.h"
+
+// (NCH, NT) lane layout of the BFP-mode kernels for dim D (swps_w2v_bfp.h), as 10*NCH + NT
+inline int bfp_shape(int D) {
+  const int nch = D / 256, rem = D % 256;
+  if (rem == 0) return 10 * nch;
+  if (rem <= 128) return 10 * nch + (rem + 63) / 64;
+  return 10 * (nch + 1);
+}
+#define SWPS_BFP_SHAPES(code, F, RB) \
+  switch (code) {                     \
+    case 1: F(0, 1, RB); break;       \
+    case 2: F(0, 2, RB); break;       \
+    case 10: F(1, 0, RB); break;      \
+    case 11: F(1, 1, RB); break;      \
+    case 12: F(1, 2, RB); break;      \
+    default: F(2, 0, RB); break;      \
+  }
+// every (NCH, NT, RB) instantiation of F for context w's dim and residual bytes
+#define SWPS_BFP_DISPATCH(w, F)                    \
+  do {                                             \
+    if ((w)->bfp_rb)                               \
+      SWPS_BFP_SHAPES(bfp_shape((w)->D), F, 1)     \
+    else                                           \
+      SWPS_BFP_SHAPES(bfp_shape((w)->D), F, 0)     \
+  } while (0)
+
 // requester side of a sharded pull: the owners' pull values [U][h|v] (K order)
 // into the worker cache (global_pull_access.h:88-97: params[key] = val)
 template <typename T>
@@ -1894,6 +1921,9 @@ inline int row_ld(int D, size_t es, bool pad = true) {
   const int q = pad ? (int)(128 / es) : 1;
   return (D + q - 1) / q * q;
 }
+
+// fp64 intermediates (parity mode): neu1/neu1e, partials and the push payload in fp64
+inline bool inter64(const swps_w2v_cfg &c) { return c.fp64_intermediates == SWPS_INTER_FP64; }
 
 struct Timer {
   bool on = false;
@@ -1951,6 +1981,8 @@ struct swps_w2v {
   int D = 0, W = 0, N = 0, NCH = 1;
   bool f64 = false;
   bool tail = false;  // fast mode: FSlice kernels (D = 256*NCH + tail, 0 < tail <= 64)
+  bool bfp = false;  // fp32 table, fp64_intermediates = SWPS_INTER_BFP40 / _BFP32: the BFP-row kernels (swps_w2v_bfp.h)
+  int bfp_rb = 0;    // ... with an int8 residual per element (BFP40: 1) or not (BFP32: 0)
   int xcd_order = 1;  // forward blocks in XCD-contiguous order (SWPS_XCD_ORDER=0 turns it off for A/B timing)
   int push_t = 1;     // fast mode: k_push_t (SWPS_PUSH_T=0: k_push, for A/B timing)
   int gather_unr = 8;         // k_gather_t rows in flight per wave (SWPS_GATHER_UNR: 4, 8, 16; A/B timing)
@@ -2097,6 +2129,13 @@ int check_cfg(swps_w2v *w) {
   if (!w->f64 && w->D > 256 && w->D % 256 != 0 && w->D % 256 <= 64) w->tail = true;
   if (const char *e = getenv("SWPS_SLICE")) w->tail = w->tail && atoi(e) != 0;  // A/B timing
   if (w->NCH > 4) return fail(SWPS_E_UNSUPPORTED, "dim too large (max 1024 fp32 / 512 fp64)");
+  if (c.fp64_intermediates < SWPS_INTER_FP32 || c.fp64_intermediates > SWPS_INTER_BFP32)
+    return fail(SWPS_E_CFG, "fp64_intermediates must be SWPS_INTER_FP32, _FP64, _BFP40 or _BFP32");
+  if (!w->f64 && (c.fp64_intermediates == SWPS_INTER_BFP40 || c.fp64_intermediates == SWPS_INTER_BFP32)) {
+    if (w->D > kBfpMaxD) return fail(SWPS_E_UNSUPPORTED, "BFP intermediates: dim at most 512");
+    w->bfp = true;
+    w->bfp_rb = c.fp64_intermediates == SWPS_INTER_BFP40 ? 1 : 0;
+  }
   return SWPS_OK;
 }
 
@@ -3090,15 +3129,16 @@ int presize(swps_w2v *w, uint64_t maxP) {
   const int W = w->W, N = w->N, D = w->D, RS = 2 * W + N + 2;
   const uint64_t HOFF = maxP * (uint64_t)(N + 1), M = HOFF + maxP * (uint64_t)(2 * W);
   if (M >= (1ULL << 31)) return SWPS_OK;  // prep_batch reports it
-  const size_t a = (w->f64 || w->cfg.fp64_intermediates) ? 8 : 4;
+  const size_t a = (w->f64 || w->cfg.fp64_intermediates) ? 8 : 4;  // partials (split mode: fp64 too)
+  const uint64_t nrow = w->bfp ? (uint64_t)bfp_ld(D, w->bfp_rb) * 4 : (uint64_t)row_ld(D, a, w->row_pad) * a;
   SWPS_TRY(w->d_pos_tok.ensure(maxP * 4));
   SWPS_TRY(w->d_rec.ensure(maxP * RS * 4));
   SWPS_TRY(w->d_pkeys.ensure(M * 4));
   SWPS_TRY(w->d_pvals.ensure(M * 4));
   SWPS_TRY(w->d_pkeys_s.ensure(M * 4));
   SWPS_TRY(w->d_pvals_s.ensure(M * 4));
-  SWPS_TRY(w->d_neu1.ensure(maxP * row_ld(D, a, w->row_pad) * a));
-  SWPS_TRY(w->d_neu1e.ensure(maxP * row_ld(D, a, w->row_pad) * a));
+  SWPS_TRY(w->d_neu1.ensure(maxP * nrow));
+  SWPS_TRY(w->d_neu1e.ensure(maxP * nrow));
   SWPS_TRY(w->d_pg.ensure(HOFF * 4));
   const uint64_t U = w->max_U;
   if (U) {
@@ -3335,7 +3375,7 @@ int prep_batch(swps_w2v *w) {
     SWPS_TRY(w->d_multi.ensure((mi + 1) * 4));
   }
   // the fused push's per-key shard rows (single GPU)
-  const bool krow = U > 0 && !w->sharded && w->tail && w->fused_push && w->push_tg_var == 5;
+  const bool krow = U > 0 && !w->sharded && (w->bfp || (w->tail && w->fused_push && w->push_tg_var == 5));
   if (krow) SWPS_TRY(w->d_krow.ensure((uint64_t)U * 4));
   if (U || recs) {
     k_batch_setup<<<nblk(std::max<uint64_t>(U, recs ? nt : 0)), 256, 0, s>>>(
@@ -3496,7 +3536,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
   w->st_pulled += U;
   if (pb.records) {
     // ---- forward (learn_instance) ----
-    const int ld = row_ld(D, sizeof(A), w->row_pad);
+    const int ld = w->bfp ? bfp_ld(D, w->bfp_rb) : row_ld(D, sizeof(A), w->row_pad);
     SWPS_TRY(w->d_neu1.ensure(P * ld * sizeof(A)));
     SWPS_TRY(w->d_neu1e.ensure(P * ld * sizeof(A)));
     SWPS_TRY(w->d_pg.ensure(pb.HOFF * 4));
@@ -3505,6 +3545,12 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                      w->d_pg.as<float>(), w->xcd_order, ld, w->cs, w->full_lines};
     hipEvent_t ef = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      if (w->bfp) {
+#define SWPS_F(a_, b_, r_) k_forward_b<a_, b_, r_, 4><<<nblk(P * 64), 256, 0, s>>>(fa)
+        SWPS_BFP_DISPATCH(w, SWPS_F);
+#undef SWPS_F
+        goto forward_done;
+      }
       if (w->tail) {
         if (D < 512) {
           if (w->fwd_g == 8)
@@ -3532,13 +3578,14 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
   }
   // fast mode, single GPU: the push sums the single-chunk runs itself (k_push_tg)
   const bool fast_tail = std::is_same<T, float>::value && std::is_same<A, float>::value && w->tail &&
-                         w->fused_push && D < 512 && pb.sorted;
-  const bool fused_ip = fast_tail && !d_grads && w->push_t;        // in-place AdaGrad (single GPU)
-  const bool fused_g = fast_tail && d_grads && w->push_tg_var == 5;  // the sharded learner's mean gradients
+                         w->fused_push && D < 512 && pb.sorted && !w->bfp;
+  const bool sp = std::is_same<T, float>::value && std::is_same<A, float>::value && w->bfp;  // BFP rows
+  const bool fused_ip = (fast_tail && !d_grads && w->push_t) || (sp && !d_grads);  // in-place AdaGrad (single GPU)
+  const bool fused_g = (fast_tail && d_grads && w->push_tg_var == 5) || (sp && d_grads);  // the sharded learner's mean gradients
   const bool fused = fused_ip || fused_g;
   // small batches: the multi-chunk gather (latency-bound, a few hundred items) runs on a side stream
   // beside the push of every other (key, half); the multi-chunk halves are pushed after it
-  const bool split = fused && w->push_tg_var == 5 && (w->split_push > 0 || (w->split_push < 0 && U < 65536));
+  const bool split = !sp && fused && w->push_tg_var == 5 && (w->split_push > 0 || (w->split_push < 0 && U < 65536));
   hipStream_t gs = s;  // the gather's stream
   if (split) {
     if (!w->s_side) {
@@ -3554,10 +3601,10 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
   }
   if (pb.sorted) {
     // ---- chunked segmented gradient sums ----
-    SWPS_TRY(w->d_partial.ensure(pb.max_items * D * sizeof(A)));
+    SWPS_TRY(w->d_partial.ensure(pb.max_items * D * (sp ? 8 : sizeof(A))));
     GatherArgs<A> ga{w->d_desc.as<uint4>(), w->d_ioff.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), U,
                      w->d_neu1.as<A>(), w->d_neu1e.as<A>(), w->d_pg.as<float>(), pb.HOFF, (uint32_t)P, D,
-                     w->d_partial.as<A>(), row_ld(D, sizeof(A), w->row_pad), w->d_lead.as<uint32_t>(),
+                     w->d_partial.as<A>(), sp ? bfp_ld(D, w->bfp_rb) : row_ld(D, sizeof(A), w->row_pad), w->d_lead.as<uint32_t>(),
                      (uint32_t)pb.max_items, fused ? w->d_multi.as<uint32_t>() : nullptr, (uint32_t)(N + 1),
                      (uint32_t)(2 * W), !fused && pb.msorted ? w->d_multi.as<uint32_t>() : nullptr};
     // multi-chunk items: at most M / chm full chunks plus one partial chunk per run of > kChunk records
@@ -3567,6 +3614,14 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     const unsigned cgrid = use_combine(w, pb.M) ? combine_grid(pb.max_items) : 0;  // 0: no second level
     hipEvent_t eg = tm.begin(gs);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
+      if (sp) {
+        double *part = w->d_partial.as<double>();
+#define SWPS_F(a_, b_, r_) k_gather_b<a_, b_, r_, 8><<<ggrid, 256, 0, gs>>>(ga, part)
+        SWPS_BFP_DISPATCH(w, SWPS_F);
+#undef SWPS_F
+        if (cgrid) k_combine_b<<<cgrid, 256, 0, gs>>>(ga, part);
+        goto gather_done;
+      }
       if (w->tail) {
         if (D < 512) {
           if (w->gather_unr == 4)
@@ -3610,13 +3665,47 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
                       (double)w->t->cfg.learning_rate, (double)w->t->cfg.fudge, d_grads,
                       d_vals ? nullptr : w->d_cache_h.as<T>(), d_vals ? nullptr : w->d_cache_v.as<T>(), w->cs,
                       w->d_pvals_s.as<uint32_t>(), w->d_pg.as<float>(), w->d_neu1.as<A>(), w->d_neu1e.as<A>(),
-                      pb.HOFF, (uint32_t)P, row_ld(D, sizeof(A), w->row_pad), w->d_krow.as<uint32_t>(),
+                      pb.HOFF, (uint32_t)P, sp ? bfp_ld(D, w->bfp_rb) : row_ld(D, sizeof(A), w->row_pad), w->d_krow.as<uint32_t>(),
                       (uint32_t)(N + 1), (uint32_t)(2 * W), w->full_lines,
                       use_combine(w, pb.M) ? kGroup : 0xFFFFFFFFu};
     hipEvent_t ep = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       const unsigned pgrid = (unsigned)std::min<uint64_t>(nblk((uint64_t)U * 128),
                                                           w->push_grid ? w->push_grid : (U < 65536 ? 2048 : ~0u));
+      if (sp) {
+        const double *part = w->d_partial.as<double>();
+        double *g64 = (double *)d_grads;  // BFP mode: the fp64 push payload
+        if (!d_grads) {
+#define SWPS_F(a_, b_, r_) k_push_b<a_, b_, r_, 8, false><<<pgrid, 256, 0, s>>>(pa, part, nullptr)
+          SWPS_BFP_DISPATCH(w, SWPS_F);
+#undef SWPS_F
+          goto push_done;
+        }
+#define SWPS_F(a_, b_, r_) k_push_b<a_, b_, r_, 8, true><<<pgrid, 256, 0, s>>>(pa, part, g64)
+        const int world = w->world;
+        if (w->split_grads && world > 1 && world <= kMaxSplitOwners) {  // two owner-half passes (below)
+          if (!w->ev_half) SWPS_HIP(hipEventCreateWithFlags(&w->ev_half, hipEventDisableTiming));
+          pa.nown = (uint32_t)world;
+          uint32_t acc = 0;
+          for (int r = 0; r < world; r++) {
+            const uint64_t c = w->bcounts[pb.bi * world + r];
+            pa.obnd[r] = acc;
+            pa.ohalf[r] = (uint32_t)(c / 2);
+            acc += (uint32_t)c;
+          }
+          pa.obnd[world] = acc;
+          pa.gpass = 1;
+          SWPS_BFP_DISPATCH(w, SWPS_F);
+          SWPS_HIP(hipEventRecord(w->ev_half, s));
+          pa.gpass = 2;
+          SWPS_BFP_DISPATCH(w, SWPS_F);
+          w->half_ready = true;
+        } else {
+          SWPS_BFP_DISPATCH(w, SWPS_F);
+        }
+#undef SWPS_F
+        goto push_done;
+      }
       if (split) {  // every other (key, half) beside the gather, then the multi-chunk halves
         if (fused_g)
           k_push_thp<1, 8, true, 1><<<pgrid, 256, 0, s>>>(pa);
@@ -4054,13 +4143,13 @@ int swps_w2v_train_batches(swps_w2v *w, uint64_t count) {
   const bool ov = w->overlap > 0 || (w->overlap < 0 && w->max_tok <= kOverlapTok);
   if (ov && count > 1 && !w->cfg.minibatch_vocab && w->trace.size() >= w->trace_cap && !w->pb.valid) {
     if (w->f64) return train_overlapped<double, double>(w, count);
-    if (w->cfg.fp64_intermediates) return train_overlapped<float, double>(w, count);
+    if (inter64(w->cfg)) return train_overlapped<float, double>(w, count);
     return train_overlapped<float, float>(w, count);
   }
   for (uint64_t i = 0; i < count; i++) {
     if (w->f64)
       SWPS_TRY((run_batch<double, double>(w)));
-    else if (w->cfg.fp64_intermediates)
+    else if (inter64(w->cfg))
       SWPS_TRY((run_batch<float, double>(w)));
     else
       SWPS_TRY((run_batch<float, float>(w)));
@@ -4352,8 +4441,8 @@ int swps_w2v_step(swps_w2v *w, const void *d_vals, void *d_grads) {
   if (!w->inited) return fail(SWPS_E_STATE, "init first");
   SWPS_HIP(hipSetDevice(w->t->cfg.device));
   if (w->f64) return run_batch<double, double>(w, d_vals, (double *)d_grads);
-  if (w->cfg.fp64_intermediates) return run_batch<float, double>(w, d_vals, (double *)d_grads);
-  return run_batch<float, float>(w, d_vals, (float *)d_grads);
+  if (inter64(w->cfg)) return run_batch<float, double>(w, d_vals, (double *)d_grads);
+  return run_batch<float, float>(w, d_vals, (float *)d_grads);  // fast, or BFP (d_grads: the fp64 payload)
 }
 
 // d_keys: the keys of the matching serve_pull (the push request carries its
@@ -4383,6 +4472,7 @@ int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
   if (!c) return fail(SWPS_E_CFG, "null communicator");
   if (comm_device(c) != w->t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");
   if (w->t->comm && w->t->comm != c) return fail(SWPS_E_CFG, "the table is routed over another communicator");
+  if (w->drv) return fail(SWPS_E_STATE, "swps_w2v_shard_comm was already called on this context");
   SWPS_TRY(swps_w2v_shard(w, comm_rank(c), comm_world(c), frag_num));
   ShardDriver *d = new ShardDriver();
   d->c = c;
@@ -4489,6 +4579,8 @@ extern "C" {
 
 int swps_w2v_save_state(swps_w2v *w, const char *path) {
   if (!w->inited) return fail(SWPS_E_STATE, "nothing to save: the context is not initialised");
+  if (w->drv && w->drv->spe && w->drv->cursor % w->drv->spe != 0)
+    return fail(SWPS_E_STATE, "a library-driven sharded context saves at epoch boundaries (swps_w2v_train_epochs)");
   SWPS_TRY(swps_w2v_sync(w));
   const uint64_t nb = std::max<uint64_t>(1, w->batches.size());
   // the current epoch is planned once its first batch was prepared
@@ -4570,6 +4662,14 @@ int swps_w2v_restore_state(swps_w2v *w, const char *path) {
   w->pb = swps_w2v::Prepped();
   const uint64_t nb = std::max<uint64_t>(1, w->batches.size());
   if (w->cursor % nb != 0) SWPS_TRY(plan_epoch(w));  // mid-epoch: re-plan from the epoch-start states
+  if (w->drv) {
+    // the library driver's lockstep step count is not this rank's batch count (ranks with fewer
+    // batches idle to the epoch's end), so its saves are at epoch boundaries (save_state), where
+    // it is epochs * spe; its server work then goes to the serve stream, as after full_pull
+    if (w->cursor % nb != 0) return fail(SWPS_E_STATE, "library-driven sharded state not at an epoch boundary");
+    w->drv->cursor = w->cursor / nb * w->drv->spe;
+    if (w->drv->ops.set_serve_stream) SWPS_TRY(w->drv->ops.set_serve_stream(w, w->drv->S));
+  }
   w->inited = true;
   return SWPS_OK;
 }

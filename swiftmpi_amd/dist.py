@@ -375,7 +375,8 @@ class ShardedWord2Vec(_ShardedApp):
         shard, its worker state (tied to that shard file by its checksum) and
         the driver's step cursor, all tagged with one generation id; after
         every rank has written its files, rank 0 writes <prefix>.commit —
-        a save without a commit marker (a crash mid-save) is never resumed.
+        a save without a commit marker (a crash mid-save) is never resumed;
+        rank 0 removes the previous marker before any rank writes.
         Lockstep drivers only (a pipelined driver holds a prefetched pull that
         lacks the last push)."""
         import os
@@ -383,6 +384,11 @@ class ShardedWord2Vec(_ShardedApp):
             raise capi.SwpsError(-6, "save: the pipelined driver holds a prefetched pull")
         self.sync()
         gen = self.ex.max(int.from_bytes(os.urandom(7), "little") if self.rank == 0 else 0)
+        # an earlier save's marker must not vouch for files this save is about to replace: a crash
+        # between a rank's new shard and its new .json would otherwise resume mixed generations
+        if self.rank == 0 and os.path.exists(prefix + ".commit"):
+            os.remove(prefix + ".commit")
+        self.ex.max(0)  # barrier: no rank writes while the old marker exists
         base = "%s.rank%d" % (prefix, self.rank)
         self.w.save(base)
         _write_json_atomic(base + ".json", {"cursor": self.cursor, "world": self.world, "frag_num": self.frag_num,

@@ -60,10 +60,11 @@ def main():
     kw = dict(window=4, negative=4, minibatch=19, sample=1e-3, unigram_size=10 ** 6)
     # fast300: the bench kernels (D = 300): the learner's mean gradients in two owner-half passes,
     # the native driver's gradient exchange in two halves (the first behind the second pass)
-    for mode in ("f64", "parity", "fast", "fast300"):
+    # bfp300: the BFP-row kernels (bfp40) (fp64 push payload, two owner-half passes)
+    for mode in ("f64", "parity", "fast", "fast300", "bfp300"):
         dtype, fp64i = {"f64": ("f64", True), "parity": ("f32", True), "fast": ("f32", False),
-                        "fast300": ("f32", False)}[mode]
-        tk = dict(dim=300 if mode == "fast300" else 16, capacity=4096, dtype=dtype, learning_rate=0.7, init="hash",
+                        "fast300": ("f32", False), "bfp300": ("f32", "bfp40")}[mode]
+        tk = dict(dim=300 if mode.endswith("300") else 16, capacity=4096, dtype=dtype, learning_rate=0.7, init="hash",
                   seed=3, device=dev)
         ta = sw.Table("w2v", **tk)
         py = ShardedWord2Vec(ta, frag_num=1000, fp64_intermediates=fp64i, **kw)

@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("modes", ["f64,parity", "fast,lr", "fast300"])
+@pytest.mark.parametrize("modes", ["f64,parity", "fast,lr", "fast300", "bfp300"])
 def test_shared_keys_two_ranks_match_lockstep_oracle(lib, oracle_mod, gpu, modes):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",

@@ -182,3 +182,47 @@ def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path):
     a.close()
     b.close()
     comm.close()
+
+
+def test_native_sharded_resume_rccl_world1(lib, gpu, tmp_path):
+    """A library-driven sharded context (swps_w2v_shard_comm) saves at an epoch
+    boundary and a fresh context resumes it bit for bit: restore_state sets the
+    driver's lockstep cursor and serve stream.  A mid-epoch save
+    and a second shard_comm are refused."""
+    import swiftmpi_amd as sw
+    from swiftmpi_amd.comm import Comm
+    from conftest import zipf_corpus
+    path = zipf_corpus(str(tmp_path / "c.txt"), 120, 300, seed=14)
+    kw = dict(window=3, negative=4, minibatch=23, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates="bfp40")
+    comm = Comm.rccl(0, 1, port=_port())
+
+    def make():
+        t = sw.Table("w2v", dim=24, capacity=2048, dtype="f32", init="hash", seed=7)
+        w = sw.Word2Vec(t, init="table", **kw)
+        w.load_text(path)
+        w.shard_comm(comm, frag_num=1000)
+        return t, w
+    ta, a = make()
+    with pytest.raises(lib.SwpsError, match="already"):
+        a.shard_comm(comm, frag_num=1000)
+    a.init()
+    a.train(3)
+    tb, b = make()
+    b.init()
+    b.train(1)
+    b.train_batches(1)
+    with pytest.raises(lib.SwpsError, match="epoch"):
+        b.save(str(tmp_path / "mid"))
+    b.train_batches(b.info()["batches"] - 1)
+    prefix = str(tmp_path / "ck")
+    b.save(prefix)
+    tc, c = make()
+    c.restore(prefix)
+    c.train(1)
+    vk, _ = a.vocab()
+    kk = torch.as_tensor(vk.astype(np.int64), device="cuda")
+    assert torch.equal(ta.export(kk), tc.export(kk))
+    assert a.stats()["lstate"] == c.stats()["lstate"]
+    for w in (a, b, c):
+        w.close()
+    comm.close()

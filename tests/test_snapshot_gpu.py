@@ -100,6 +100,7 @@ def _w2v(lib, path, dtype, init, **kw):
 
 
 @pytest.mark.parametrize("dtype,fp64i,extra", [("f64", True, {}), ("f32", True, {}), ("f32", False, {}),
+                                               ("f32", "bfp40", {}),
                                                ("f32", False, {"sampler": "alias"}),
                                                ("f64", True, {"minibatch_vocab": True, "key_mode": "atoi"})])
 @pytest.mark.parametrize("stop", ["epoch", "mid"])
@@ -242,6 +243,23 @@ def test_sharded_w2v_resume_world1(lib, gpu, gloo1, tmp_path):
     with pytest.raises(lib.SwpsError, match="commit"):
         make().restore(prefix)
     os.rename(prefix + ".commit.bak", prefix + ".commit")
+    # a second save that dies after this rank's new shard + worker state but before its .json
+    # (ADVICE r2): the old marker is gone, so the mixed files are never resumed
+    import swiftmpi_amd.dist as sd
+    real = sd._write_json_atomic
+
+    def crash(path, obj):
+        if path.endswith(".json"):
+            raise OSError("killed between the table write and the json write")
+        real(path, obj)
+    sd._write_json_atomic = crash
+    try:
+        with pytest.raises(OSError):
+            a.save(prefix)
+    finally:
+        sd._write_json_atomic = real
+    with pytest.raises(lib.SwpsError, match="commit"):
+        make().restore(prefix)
     b.sync()
     kr, rr = ref.shard_rows()
     kb, rb = b.shard_rows()

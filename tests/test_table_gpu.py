@@ -45,6 +45,29 @@ def test_capacity_exhausted_is_error(lib, gpu):
     assert "OOM" in str(e.value)
 
 
+def test_full_table_overflow_key_is_never_a_row(lib, gpu):
+    """A key whose insert found the table full owns a hash slot but no row
+    (kFullRow): a later pull or push of it must fail as a miss, never read
+    or write row 0xFFFFFFFE, and the stored keys keep working."""
+    t = lib.Table("lr", capacity=4, dtype="f32")
+    with pytest.raises(lib.SwpsError):
+        t.pull(torch.arange(10, dtype=torch.int64, device=gpu))
+    stored = sorted(int(x) for x in t.keys())
+    assert len(stored) == 4
+    over = [x for x in range(10) if x not in stored]
+    ko = torch.tensor(over[:1], dtype=torch.int64, device=gpu)
+    with pytest.raises(lib.SwpsError) as e:
+        t.push(ko, torch.ones(1, 1, dtype=torch.float32, device=gpu))
+    assert "BADKEY" in str(e.value)
+    with pytest.raises(lib.SwpsError):
+        t.pull(ko)
+    ks = torch.tensor(stored, dtype=torch.int64, device=gpu)
+    before = t.pull(ks).clone()
+    t.push(ks, torch.full((4, 1), 0.5, dtype=torch.float32, device=gpu))
+    after = t.pull(ks)
+    assert torch.isfinite(after).all() and not torch.equal(before, after)
+
+
 def test_w2v_dump_format_and_sharded_load(lib, gpu, tmp_path):
     D = 4
     t = lib.Table("w2v", dim=D, capacity=100, dtype="f32", init="hash", seed=1)

@@ -192,7 +192,8 @@ def test_fast_mode_close_to_parity_mode(lib, oracle_mod, gpu, tmp_path):
 
 @pytest.mark.parametrize("dtype,fp64i,overlap,D", [("f64", True, True, 16), ("f32", True, True, 16),
                                                   ("f32", False, True, 16), ("f32", False, False, 16),
-                                                  ("f32", False, True, 300), ("f32", False, False, 300)])
+                                                  ("f32", False, True, 300), ("f32", False, False, 300),
+                                                  ("f32", "bfp40", True, 300), ("f32", "bfp40", True, 100)])
 def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i, overlap, D):
     """The sharded request / serve / step / push path with one rank (gloo,
     world 1) reproduces the single-GPU path bit for bit — in fast mode too,
@@ -429,7 +430,7 @@ def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch, combine):
     assert len(negs[0]) > 1000
 
 
-@pytest.mark.parametrize("dtype,fp64i", [("f32", False), ("f32", True), ("f64", True)])
+@pytest.mark.parametrize("dtype,fp64i", [("f32", False), ("f32", True), ("f64", True), ("f32", "bfp40")])
 def test_overlapped_driver_bit_identical(lib, gpu, monkeypatch, dtype, fp64i):
     """prep(i+1) on a second stream into a second buffer set while learn(i)
     runs (SWPS_OVERLAP=1, opt-in) == the sequential loop, bit for bit,
