@@ -33,6 +33,31 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 XGMI_PEAK_GBS = 7 * 153.0  # per GPU: 7 xGMI links x ~153 GB/s
 
 
+def pmc_traffic(config, groups):
+    """HBM bytes per launch of kernel groups (one launch of each kernel per
+    step), from the committed PMC summary of this exact workload
+    (profiles/r03_pmc_*.json, written by scripts/pmc_summary.py from separate
+    rocprofv3 --pmc passes of the same command; read requests counted by size
+    + WRITE_SIZE).  groups: name -> kernel base names (template arguments
+    dropped).  Returns ({name: bytes or None}, source or None)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r03_pmc_*.json"))):
+        try:
+            prof = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if {k: prof.get("config", {}).get(k) for k in config} != config:
+            continue
+        res = {}
+        for name, bases in groups.items():
+            vals = [v["hbm_bytes"] for k, v in prof["kernels"].items()
+                    if k.split("<")[0] in bases and v.get("hbm_bytes") is not None]
+            res[name] = sum(vals) if vals else None
+        src = "profiles/%s (32/64/128-B read requests + WRITE_SIZE per launch)" % os.path.basename(path)
+        return res, src
+    return {name: None for name in groups}, None
+
+
 def make_corpus(tokens, vocab, line_len, seed):
     """Zipf(s=1) over `vocab` word ids, `tokens` tokens in lines of `line_len`
     (the synthetic text8 stand-in)."""
@@ -417,25 +442,20 @@ def main():
                             "(events on the exchange stream, profiled pass); world %d" % (2 * D * es, world)}
     # HBM traffic of the same kernel from the committed PMC passes of this exact
     # command (scripts/gpu_profile.sh -> scripts/pmc_summary.py); null otherwise
-    traffic, traffic_src, fwd_traffic = None, None, None
     # (per-launch bytes do not depend on --steps / --warmup: only the workload
     # keys must match)
-    pmc_name = "r03_pmc_w2v_%s.json" % prec
-    pmc = os.path.join(ROOT, "profiles", pmc_name)
-    mine = dict(minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, mode=prec, world=world,
-                tokens=args.tokens, vocab=args.vocab, line_len=args.line_len, sharded=bool(sharded))
-    if os.path.exists(pmc) and not parity_main:
-        prof = json.load(open(pmc))
-        if {k: prof.get("config", {}).get(k) for k in mine} == mine:
-            grp = (("k_gather_b", "k_combine_b") + (("k_push_b",) if (fused or fused_g) else ()) if bfp_main else
-                   ("k_gather", "k_combine") + (("k_push_tg", "k_push_th") if (fused or fused_g) else ()))
-            gt = [v["hbm_bytes_corrected"] for k, v in prof["kernels"].items() if k.startswith(grp)]
-            if gt and (not (fused or fused_g) or any(k.startswith(grp[2:]) for k in prof["kernels"])):
-                traffic = sum(gt)  # per step: one launch of each kernel of the group
-                traffic_src = "profiles/%s (2*FETCH_SIZE + WRITE_SIZE per launch, %s)" % (pmc_name, " + ".join(grp))
-            for k, v in prof["kernels"].items():
-                if k.startswith("k_forward"):
-                    fwd_traffic = v["hbm_bytes_corrected"]
+    mine = dict(app="w2v", minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, mode=prec, world=world,
+                tokens=args.tokens, vocab=args.vocab, line_len=args.line_len, sharded=bool(sharded),
+                sampler=args.sampler)
+    if bfp_main:
+        grp = ("k_gather_b", "k_combine_b", "k_push_b")
+    elif parity_main or args.dtype == "f64":
+        grp = ("k_gather", "k_combine") + (("k_push_thp", "k_push_tg") if (fused or fused_g) else ())
+    else:
+        grp = ("k_gather_t", "k_combine") + (("k_push_thp", "k_push_tg") if (fused or fused_g) else ())
+    tr, traffic_src = pmc_traffic(mine, {"sum": grp, "forward": ("k_forward_t", "k_forward_b", "k_forward_b8",
+                                                                  "k_forward")})
+    traffic, fwd_traffic = tr["sum"], tr["forward"]
 
     parity_leg, fast_leg = None, None
     if rank == 0 and world == 1 and not parity_main and not args.no_parity_leg:
@@ -518,15 +538,18 @@ def main():
                      "partial_items_per_launch": (g_mitems if fused else g_items) / max(gat_n, 1),
                      "gather_ms_per_launch": gat_ms / max(gat_n, 1),
                      "push_ms_per_launch": push_ms / max(push_n, 1),
-                     # k_forward: its row-occurrence bytes exceed its HBM traffic (hot Zipf rows
-                     # hit in L2/MALL), so its "achieved" can pass the HBM peak; hbm_GBps is the
-                     # PMC-measured HBM rate of the same launches
-                     "forward": {"kernel": "k_forward_b" if bfp_main else "k_forward_t", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
-                                 "bytes_per_launch": fwd_bytes / max(fwd_n, 1),
+                     # k_forward: its row-occurrence bytes count every context/target row read,
+                     # most of them L2 / Infinity-Cache hits (hot Zipf rows), so they are no
+                     # roofline quantity (row_bytes_GBps); its roofline fraction is the
+                     # PMC-measured memory-side traffic of the same launches over their time
+                     "forward": {"kernel": "k_forward_b" if bfp_main else "k_forward_t",
+                                 "row_bytes_GBps": fwd_gbs, "row_bytes_per_launch": fwd_bytes / max(fwd_n, 1),
                                  "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n,
                                  "traffic": fwd_traffic,
                                  "hbm_GBps": (fwd_traffic / (fwd_ms / max(fwd_n, 1) * 1e-3) / 1e9
-                                              if fwd_traffic and fwd_ms > 0 else None)},
+                                              if fwd_traffic and fwd_ms > 0 else None),
+                                 "frac": (fwd_traffic / (fwd_ms / max(fwd_n, 1) * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                          if fwd_traffic and fwd_ms > 0 else None)},
                      "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
                      "pull_push": pp or None},
         "kernel_ms": {k: v[0] for k, v in kt.items()},
@@ -666,6 +689,17 @@ def bench_other(args):
               "achieved": push_gbs, "frac": push_gbs / HBM_PEAK_GBS,
               "bytes_per_launch": push_bytes / max(push_n, 1), "avg_launch_ms": push_ms / max(push_n, 1),
               "launches": push_n}
+        tr, tsrc = pmc_traffic(dict(app="lr", lr_batch=args.lr_batch, exact=bool(args.lr_exact), world=world,
+                                    sharded=dist is not None),
+                               {"forward": ("k_lr_forward_r", "k_lr_forward"),
+                                "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
+                                         "k_lr_reduce_long_fast")})
+        for kd, name in ((kf, "forward"), (kp, "push")):
+            kd["traffic"] = tr[name]
+            kd["traffic_source"] = tsrc
+            if tr[name] and kd["avg_launch_ms"] > 0:
+                kd["hbm_GBps"] = tr[name] / (kd["avg_launch_ms"] * 1e-3) / 1e9
+                kd["hbm_frac"] = kd["hbm_GBps"] / HBM_PEAK_GBS
         dom, other = (kp, kf) if push_ms >= fwd_ms else (kf, kp)
         out = {"metric": "sparse LR trained examples/sec (AdaGrad, key-sharded PS)", "value": total / dt,
                "unit": "examples/s", "n_gpus": world, "steps": steps, "warmup": warm,
@@ -681,7 +715,7 @@ def bench_other(args):
                           else "fast (fp64 per-key sums, wave tree-reduced; within 1e-5 of the oracle)",
                           "features_per_s": total * nnz / max(r1 - r0, 1) / dt,
                           "unique_keys_per_step": uniq / steps},
-               "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s", traffic=None,
+               "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
                                 step_GBps=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS, other=other,
                                 note="a 65k-row step is ~80 MB of algorithmic traffic in 4-B random accesses "
                                      "(weights, e gathers, row read-modify-writes): access latency, not HBM "
@@ -725,6 +759,7 @@ def bench_other(args):
         doc_ms, doc_n = kt["docs"]
         doc_bytes = 4 * D * rows_read + 8 * D * ndocs
         doc_gbs = doc_bytes / (doc_ms * 1e-3) / 1e9 if doc_ms > 0 else 0.0
+        tr, tsrc = pmc_traffic(dict(app="s2v", s2v_docs=args.s2v_docs, dim=D, world=world), {"docs": ("k_s2v_docs",)})
         out = {"metric": "sent2vec trained words/sec (frozen word table, doc-sharded)", "value": total / dt,
                "unit": "words/s", "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": dt * 1e3 / steps,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 table, f64 math",
@@ -734,7 +769,10 @@ def bench_other(args):
                                                                               args.s2v_docs, D),
                           "parallelism": "doc-sharded over %d GPU(s), no exchange (replicas only)" % world},
                "roofline": {"bound": "hbm", "kernel": "k_s2v_docs", "achieved": doc_gbs, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": doc_gbs / HBM_PEAK_GBS, "traffic": None,
+                            "unit": "GB/s", "frac": doc_gbs / HBM_PEAK_GBS, "traffic": tr["docs"],
+                            "traffic_source": tsrc,
+                            "hbm_GBps": (tr["docs"] / (doc_ms / max(doc_n, 1) * 1e-3) / 1e9
+                                         if tr["docs"] and doc_ms > 0 else None),
                             "bytes_per_launch": doc_bytes / max(doc_n, 1), "avg_launch_ms": doc_ms / max(doc_n, 1),
                             "launches": doc_n},
                "kernel_ms": {k: v[0] for k, v in kt.items()}}

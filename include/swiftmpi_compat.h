@@ -157,24 +157,37 @@ inline swps_table_cfg &global_swps_cfg() {
   static swps_table_cfg c;
   return c;
 }
+/* BasicHashFrag node id of this rank's shard (rank + 1, hashfrag.h:33-56) and the node count */
+inline std::pair<int, int> &global_node() {
+  static std::pair<int, int> n(1, 1);
+  return n;
+}
 
 /* ---- parameter/accessmethod.h ---------------------------------------------
  * The reference's server runs the app's access-method objects per key on
- * the CPU; here the owner GPU applies one of the library's device rules to
- * whole batches.  An app's access-method classes keep their reference shape
- * (they may still derive from these bases and define init_param /
- * get_pull_value / apply_push_value, which are not called) and select the
- * device rule through two constants, inherited unless overridden:
- *   PullM::init_mode = SWPS_INIT_HASH (or SWPS_INIT_ZERO)  (init_param)
- *   PushM::push_rule = SWPS_PUSH_ADAGRAD (or SWPS_PUSH_SGD) (apply_push_value)
- * AdaGrad is what all three reference apps implement
- * (word2vec_global.h:176-185, lr.cpp:68-75). */
+ * the CPU (accessmethod.h:16-33); here the owner GPU applies one of the
+ * library's device rules to whole batches.  An app's access-method classes
+ * keep their reference shape and select the device rule through two
+ * constants:
+ *   PullM::init_mode = SWPS_INIT_HASH or SWPS_INIT_ZERO       (init_param)
+ *   PushM::push_rule = SWPS_PUSH_ADAGRAD or SWPS_PUSH_SGD     (apply_push_value)
+ * A class that leaves them unset inherits "unspecified", which resolves to
+ * the rule every reference app implements (AdaGrad, word2vec_global.h:
+ * 176-185 / lr.cpp:68-75; hashed random init) — unless the class defines its
+ * own init_param / get_pull_value / apply_push_value body: the library cannot
+ * run host bodies on the device, so such a class must state the rule its
+ * body computes (one line, e.g. `static const int32_t push_rule =
+ * SWPS_PUSH_ADAGRAD;` in the reference's WPushAccessMethod), and creating
+ * its ClusterServer otherwise throws SwpsError(SWPS_E_UNSUPPORTED).  A rule
+ * value the library lacks fails the same way (swps_table_create). */
+const int32_t SWPS_RULE_UNSPECIFIED = -1;
+
 template <typename Key, typename Param, typename PullVal> class PullAccessMethod {
  public:
   typedef Key key_t;
   typedef Param param_t;
   typedef PullVal pull_t;
-  static const int32_t init_mode = SWPS_INIT_HASH;
+  static const int32_t init_mode = SWPS_RULE_UNSPECIFIED;
   virtual ~PullAccessMethod() {}
 };
 template <typename Key, typename Param, typename Grad> class PushAccessMethod {
@@ -182,16 +195,43 @@ template <typename Key, typename Param, typename Grad> class PushAccessMethod {
   typedef Key key_t;
   typedef Param param_t;
   typedef Grad grad_t;
-  static const int32_t push_rule = SWPS_PUSH_ADAGRAD;
+  static const int32_t push_rule = SWPS_RULE_UNSPECIFIED;
   virtual ~PushAccessMethod() {}
 };
+
+namespace detail {
+/* does M (or a base between it and the library's) define a host body? */
+template <class M> struct has_init_param {
+  template <class U> static char test(decltype(&U::init_param));
+  template <class U> static long test(...);
+  static const bool value = sizeof(test<M>(nullptr)) == 1;
+};
+template <class M> struct has_get_pull_value {
+  template <class U> static char test(decltype(&U::get_pull_value));
+  template <class U> static long test(...);
+  static const bool value = sizeof(test<M>(nullptr)) == 1;
+};
+template <class M> struct has_apply_push_value {
+  template <class U> static char test(decltype(&U::apply_push_value));
+  template <class U> static long test(...);
+  static const bool value = sizeof(test<M>(nullptr)) == 1;
+};
+inline int32_t resolve_rule(int32_t declared, bool host_body, int32_t dflt, const char *what) {
+  if (declared != SWPS_RULE_UNSPECIFIED) return declared;
+  if (host_body)
+    throw SwpsError(SWPS_E_UNSUPPORTED, std::string("the access method defines its own ") + what +
+                                            " body, which the library cannot run on the device: declare the rule "
+                                            "it computes (see swiftmpi_compat.h, parameter/accessmethod.h)");
+  return dflt;
+}
+}  // namespace detail
 
 /* ---- cluster/server.h ClusterServer --------------------------------------
  * The server half of a rank: its HBM shard's layout comes from the pull
  * value's codec (PullCodec<PullVal>::layout), its miss initialisation and
  * push rule from the access methods.  Cluster<Worker, ClusterServer<...>,
- * Key> creates the shard; load() keeps the keys this rank owns
- * (server.h:49-62). */
+ * Key> creates the shard; load() assigns the dump's keys this rank owns
+ * (server.h:49-62), global_server<server_t>().load(path) as in lr.cpp:297-300. */
 template <typename Key, typename Param, typename PullVal, typename Grad, typename PullM, typename PushM>
 class ClusterServer {
  public:
@@ -202,8 +242,16 @@ class ClusterServer {
   typedef PullM pull_access_t;
   typedef PushM push_access_t;
   static int32_t layout() { return PullCodec<PullVal>::layout; }
-  static int32_t init_mode() { return PullM::init_mode; }
-  static int32_t push_rule() { return PushM::push_rule; }
+  static int32_t init_mode() {
+    return detail::resolve_rule(PullM::init_mode,
+                                detail::has_init_param<PullM>::value || detail::has_get_pull_value<PullM>::value,
+                                SWPS_INIT_HASH, "init_param / get_pull_value");
+  }
+  static int32_t push_rule() {
+    return detail::resolve_rule(PushM::push_rule, detail::has_apply_push_value<PushM>::value, SWPS_PUSH_ADAGRAD,
+                                "apply_push_value");
+  }
+  void load(const std::string &path);  // defined after Cluster's globals
 };
 
 /* ---- parameter/param.h ---------------------------------------------------- */
@@ -358,6 +406,9 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
     swps_check(swps_table_create(&c, &_t));
     global_swps_table() = _t;
     global_swps_cfg() = c;
+    global_node() = std::make_pair(_rank + 1, _world);
+    global_frag_num() = global_config().has("server", "frag_num") ? global_config().get("server", "frag_num").to_int32()
+                                                                  : 1000;
     if (_world > 1 || env_int("SWPS_ROUTE", nullptr, 0)) {
       const char *addr = std::getenv("MASTER_ADDR");
       const int port = env_int("SWPS_BOOTSTRAP_PORT", nullptr, env_int("MASTER_PORT", nullptr, 29500) + 1);
@@ -370,12 +421,8 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
         swps_check(swps_comm_bootstrap_tcp(addr ? addr : "127.0.0.1", port, _rank, _world, timeout, id.data()));
         swps_check(swps_comm_create_rccl(id.data(), _rank, _world, dev, &_comm));
       }
-      const int frag = global_config().has("server", "frag_num")
-                           ? global_config().get("server", "frag_num").to_int32()
-                           : 1000;
-      swps_check(swps_table_route(_t, _comm, frag));
+      swps_check(swps_table_route(_t, _comm, global_frag_num()));
       global_swps_comm() = _comm;
-      global_frag_num() = frag;
     }
   }
   ~Cluster() {
@@ -387,12 +434,12 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
   void initialize() {}
   /* The worker is done: keep serving the other ranks until all are
    * (swps_finish), then SparseTable::output (sparsetable.h:127-132) of this
-   * rank's shard to `path` (world > 1: `path`.<rank>). */
+   * rank's shard to exactly `path` (cluster.h:41-50; the reference's mains
+   * make it per rank themselves, w2v.cpp:54-56). */
   void finalize(const std::string &path = "") {
     swps_check(swps_finish(_t));
     if (path.empty()) return;
-    const std::string p = _world > 1 ? path + "." + std::to_string(_rank) : path;
-    swps_check(swps_dump(_t, p.c_str()));
+    swps_check(swps_dump(_t, path.c_str()));
   }
   swps_table *table() { return _t; }
   int rank() const { return _rank; }
@@ -406,6 +453,19 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
   swps_comm *_comm = nullptr;
   int _rank = 0, _world = 1;
 };
+
+/* server.h:49-62: every "key param" record of the dump whose BasicHashFrag
+ * node is this rank's is assigned to the shard (the others are skipped). */
+template <typename Key, typename Param, typename PullVal, typename Grad, typename PullM, typename PushM>
+void ClusterServer<Key, Param, PullVal, Grad, PullM, PushM>::load(const std::string &path) {
+  swps_table *t = global_swps_table();
+  if (!t) throw SwpsError(SWPS_E_STATE, "no shard: create a Cluster first");
+  swps_check(swps_load(t, path.c_str(), global_frag_num(), global_node().second, global_node().first));
+}
+template <class ServerT> ServerT &global_server() {
+  static ServerT s;
+  return s;
+}
 
 /* ---- app level ------------------------------------------------------------ */
 
@@ -463,7 +523,8 @@ class Word2VecApp {
  * sentence vectors go to `out_path` in the reference's format.  On a
  * multi-rank Cluster: replicas — every rank loads the whole (read-only) word
  * table into a local copy and trains the documents BasicHashFrag gives it
- * (swps_s2v_shard; sentence vectors to `out_path`.<rank>). */
+ * (swps_s2v_shard); its sentence vectors go to exactly `out_path`, as the
+ * reference's Sent2Vec writes them (sent2vec.cpp:24,46). */
 class Sent2VecApp {
  public:
   Sent2VecApp(const std::string &path, const std::string &out_path, int niters, swps_table *t = nullptr)
@@ -474,7 +535,6 @@ class Sent2VecApp {
       swps_check(swps_table_create(&c, &_own));
       _t = _own;
       swps_check(swps_comm_info(_comm, &_rank, &_world));
-      _out = _out.empty() ? _out : _out + "." + std::to_string(_rank);
     }
     _c.window = global_config().get("word2vec", "window").to_int32();
     _c.negative = global_config().get("word2vec", "negative").to_int32();
@@ -524,31 +584,41 @@ class Sent2VecApp {
 };
 
 /* LR (lr.cpp:133-411): train(niters) returns the per-epoch mean squared
- * error the reference logs (lr.cpp:231); predict() the probabilities.  On a
- * multi-rank Cluster the library runs the key-sharded exchange
+ * error the reference logs (lr.cpp:231); predict() the probabilities.  As in
+ * the reference the first pull happens at the first train / predict, so a
+ * load_param (lr.cpp:297-300: ClusterServer::load of a dump) before it leaves
+ * the loaded keys as they are and initialises only the others (gen_float in
+ * first-pull order, lr.cpp:48-50) — the predict mode of lr.cpp:498-504.  On
+ * a multi-rank Cluster the library runs the key-sharded exchange
  * (swps_lr_shard_comm): train / predict are collective, errors are this
  * rank's rows'. */
 class LRApp {
  public:
-  LRApp(const std::string &path, swps_table *t = nullptr) {
+  LRApp(const std::string &path, swps_table *t = nullptr) : _t(t ? t : global_swps_table()) {
     swps_comm *comm = t ? nullptr : global_swps_comm();
     swps_lr_cfg c;
     c.minibatch = global_config().get("worker", "minibatch").to_int32();
     c.init_ref = comm ? 0 : 1;
     c.profile = 0;
     c.fast_sums = 0;
-    swps_check(swps_lr_create(t ? t : global_swps_table(), &c, &_l));
+    swps_check(swps_lr_create(_t, &c, &_l));
     swps_check(swps_lr_load_text(_l, path.c_str()));
     if (comm) swps_check(swps_lr_shard_comm(_l, comm, global_frag_num()));
-    swps_check(swps_lr_init(_l));
   }
   ~LRApp() { swps_lr_destroy(_l); }
+  /* lr.cpp:297-300: the dump's keys this rank owns (server.h:49-62) */
+  void load_param(const std::string &path) {
+    if (_inited) throw SwpsError(SWPS_E_STATE, "load_param after the first pull");
+    swps_check(swps_load(_t, path.c_str(), global_frag_num(), global_node().second, global_node().first));
+  }
   std::vector<double> train(int niters) {
+    init();
     std::vector<double> err((size_t)niters);
     swps_check(swps_lr_train(_l, niters, err.data()));
     return err;
   }
   std::vector<float> predict() {
+    init();
     uint64_t info[4];
     swps_check(swps_lr_info(_l, info));
     std::vector<float> p(info[0] ? info[0] : 1);
@@ -556,11 +626,27 @@ class LRApp {
     p.resize(info[0]);
     return p;
   }
+  /* lr.cpp:240-295: one probability per line (`outfile << predict <<
+   * std::endl`, ostream precision 6).  Like the reference (it reads _path,
+   * lr.cpp:247) the rows are the context's own data; `dataset` is unused. */
+  void predict(const std::string &dataset, const std::string &out) {
+    (void)dataset;
+    const std::vector<float> p = predict();
+    std::ofstream f(out.c_str());
+    if (!f) throw SwpsError(SWPS_E_IO, "cannot open " + out);
+    for (float x : p) f << x << std::endl;
+  }
 
  private:
+  void init() {
+    if (!_inited) swps_check(swps_lr_init(_l));
+    _inited = true;
+  }
   LRApp(const LRApp &);
   LRApp &operator=(const LRApp &);
+  swps_table *_t;
   swps_lr *_l = nullptr;
+  bool _inited = false;
 };
 
 }  // namespace swift_snails

@@ -83,6 +83,7 @@ def lib():
         L.orc_lr_create.restype = _p
         L.orc_lr_create.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_float]
         L.orc_lr_destroy.argtypes = [_p]
+        L.orc_lr_set_sum_f64.argtypes = [_p, ctypes.c_int]
         L.orc_lr_num_instances.restype = _u64
         L.orc_lr_num_instances.argtypes = [_p]
         L.orc_lr_train.argtypes = [_p, ctypes.c_int, _p]
@@ -254,10 +255,15 @@ class W2V:
 class LR:
     """Reference-semantics sparse logistic regression (lr.cpp, nthreads = 1)."""
 
-    def __init__(self, path, minibatch=200, lr=0.05):
+    def __init__(self, path, minibatch=200, lr=0.05, sum_f64=False):
+        """sum_f64: NOT the reference — each key's gradient terms summed in
+        fp64 (mean = float(sum/count)), the definition the rebuild's
+        fast_sums mode implements; its distance from the default mode is the
+        reference's own fp32-chain rounding."""
         self.h = lib().orc_lr_create(path.encode(), minibatch, lr)
         if not self.h:
             raise RuntimeError(lib().orc_last_error().decode())
+        lib().orc_lr_set_sum_f64(self.h, int(sum_f64))
 
     def __del__(self):
         if getattr(self, "h", None):

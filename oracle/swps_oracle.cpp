@@ -937,12 +937,18 @@ struct LRParam {
 };
 struct LRGrad {
   float val = 0;
+  double val64 = 0;  // sum_f64: the same terms summed in fp64 (the rebuild's fast_sums definition)
   int count = 0;
 };
 
 struct LR {
   int minibatch = 200;
   float lr = 0.05f;
+  // not the reference: each key's mean from an fp64 sum of its fp32 terms,
+  // mean = float(sum / count) — what the rebuild's fast_sums computes (up to
+  // summation order); the distance between the two oracle modes is the
+  // reference's own fp32-chain rounding
+  bool sum_f64 = false;
   std::vector<std::string> raw;
   std::vector<LRIns> ins;  // valid lines only
   std::unordered_set<uint32_t> all_keys;
@@ -974,7 +980,7 @@ struct LR {
       LRGrad g = it->second;
       it->second = LRGrad();
       if (g.count == 0) throw std::runtime_error("zero-count push (reference stream desync, lr.cpp:34-35)");
-      float m = float(g.val / g.count);
+      float m = sum_f64 ? float(g.val64 / (double)g.count) : float(g.val / g.count);
       LRParam &p = server[k];
       p.g2 += m * m;
       p.val += lr * m / float(std::sqrt(p.g2 + 1e-6f));
@@ -994,6 +1000,7 @@ struct LR {
       float grad = error * f.second;
       LRGrad &g = grads[f.first];
       g.val += grad;
+      g.val64 += (double)grad;
       g.count++;
     }
     return error * error;
@@ -1043,6 +1050,8 @@ struct LR {
 }  // namespace
 
 extern "C" {
+
+void orc_lr_set_sum_f64(void *h, int on) { ((LR *)h)->sum_f64 = on != 0; }
 
 void *orc_lr_create(const char *path, int minibatch, float lr) {
   try {

@@ -1,53 +1,71 @@
 #!/bin/bash
-# rocprofv3 evidence for the bench line, written to gpurun_out/profiles_$TAG/
-# (copy into profiles/ afterwards):
-#   * kernel-trace + stats of the headline command (the driver's --steps 20
-#     --warmup 5; the extra legs off so the profiled pass's launches are the
-#     last ones of each kernel) -> <tag>_w2v_fast_kernel_stats.csv and the
-#     bench JSON line of that same traced process -> <tag>_bench_w2v_traced.json
-#   * FETCH_SIZE and WRITE_SIZE in separate --pmc passes of the same command
-#     (never combined with other tracing) -> <tag>_pmc_w2v_fast.json
-#   * the B = 100 minibatch, parity mode and LR (config 3) kernel stats
+# rocprofv3 evidence for the bench lines, per leg, written to
+# gpurun_out/profiles_$TAG/ (copy into profiles/ afterwards):
+#   <tag>_<leg>_kernel_stats.csv   kernel-trace + stats of the leg's command
+#   <tag>_bench_<leg>_traced.json  the bench JSON line of that traced process
+#   <tag>_pmc_<leg>.json           separate --pmc passes of the same command
+#                                  (read requests by size; WRITE_SIZE; for the
+#                                  headline also FETCH_SIZE as a cross-check),
+#                                  summarised by scripts/pmc_summary.py
+#   <tag>_bench_<leg>.json         the same command without the profiler, its
+#                                  roofline.traffic read from that summary
+# LEGS selects legs (default: all).  Each step runs under its own time limit;
+# the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 OUT=gpurun_out/profiles_$TAG
-mkdir -p gpurun_out "$OUT"
+mkdir -p gpurun_out "$OUT" profiles
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 R=$(pwd)
 cd /tmp && export TMPDIR=/tmp && cd "$R"
+LEGS=${LEGS:-"w2v_bfp40 w2v_b100 w2v_parity w2v_fast lr s2v w2v_config4 w2v_sharded"}
+READS="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
 run() {  # name timeout args...
   local name=$1 to=$2; shift 2
-  echo "== $name"
+  echo "== $name $(date +%T)"
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"; tail -2 "gpurun_out/$name.log" | cut -c1-400
   return $rc
 }
-B="$R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-parity-leg --b100-steps 0"
-run prof_fast 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fast -o run -- python3 $B || exit $?
-cp gpurun_out/prof_fast/run_kernel_stats.csv "$OUT/${TAG}_w2v_fast_kernel_stats.csv"
-grep '^{' gpurun_out/prof_fast.log | tail -1 > "$OUT/${TAG}_bench_w2v_traced.json"
-run pmc_fetch_fast 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_fast -o run -- python3 $B || exit $?
-run pmc_write_fast 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_fast -o run -- python3 $B || exit $?
-python3 scripts/pmc_summary.py gpurun_out/pmc_fetch_fast gpurun_out/pmc_write_fast "$OUT/${TAG}_pmc_w2v_fast.json" \
-  --last 16 --cmd "python3 bench.py --gpus 1 --steps 20 --warmup 5 (legs off)" \
-  --config '{"minibatch": 5000, "dim": 300, "dtype": "f32", "mode": "fast", "world": 1, "tokens": 17005207, "vocab": 253854, "line_len": 1000}' || exit $?
-run prof_b100 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_b100 -o run -- python3 $R/bench.py --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline --no-parity-leg || exit $?
-cp gpurun_out/prof_b100/run_kernel_stats.csv "$OUT/${TAG}_w2v_b100_kernel_stats.csv"
-grep '^{' gpurun_out/prof_b100.log | tail -1 > "$OUT/${TAG}_bench_w2v_b100_traced.json"
-run prof_parity 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_parity -o run -- python3 $B --parity || exit $?
-cp gpurun_out/prof_parity/run_kernel_stats.csv "$OUT/${TAG}_w2v_parity_kernel_stats.csv"
-run prof_lr 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lr -o run -- python3 $R/bench.py --app lr --steps 20 --warmup 3 --no-cpu-baseline || exit $?
-cp gpurun_out/prof_lr/run_kernel_stats.csv "$OUT/${TAG}_lr_kernel_stats.csv"
-grep '^{' gpurun_out/prof_lr.log | tail -1 > "$OUT/${TAG}_bench_lr_traced.json"
-ls -la "$OUT"
-# sent2vec (config-5 per-rank shape) and word2vec at config 4's per-rank shape (V = 1M, 125M tokens)
-run bench_s2v 900 python3 $R/bench.py --app s2v --steps 150 --warmup 3 || exit $?  # 8192 x 153 = 1.25M docs: config 5 per rank
-grep '^{' gpurun_out/bench_s2v.log | tail -1 > "$OUT/${TAG}_bench_s2v_config5_per_rank.json"
-run bench_c4 900 python3 $R/bench.py --tokens 125000000 --vocab 1000000 --steps 20 --warmup 5 --no-parity-leg --b100-steps 0 --no-cpu-baseline || exit $?
-grep '^{' gpurun_out/bench_c4.log | tail -1 > "$OUT/${TAG}_bench_w2v_config4_per_rank.json"
-run bench_sharded 600 python3 $R/bench.py --sharded --steps 20 --warmup 5 --b100-steps 0 --no-parity-leg --no-cpu-baseline || exit $?
-grep '^{' gpurun_out/bench_sharded.log | tail -1 > "$OUT/${TAG}_bench_w2v_sharded_native_world1.json"
-run bench_default 900 python3 $R/bench.py --steps 20 --warmup 5 || exit $?
-grep '^{' gpurun_out/bench_default.log | tail -1 > "$OUT/${TAG}_bench_w2v_default.json"
+W2V="bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-parity-leg --b100-steps 0"
+W2VCFG='"app": "w2v", "dim": 300, "dtype": "f32", "world": 1, "line_len": 1000, "sampler": "table"'
+TEXT8='"tokens": 17005207, "vocab": 253854'
+leg() {  # name last(N|launches) config-json args...
+  local name=$1 last=$2 cfg=$3; shift 3
+  run prof_$name 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$name -o run -- python3 "$@" || exit $?
+  cp gpurun_out/prof_$name/run_kernel_stats.csv "$OUT/${TAG}_${name}_kernel_stats.csv"
+  grep '^{' gpurun_out/prof_$name.log | tail -1 > "$OUT/${TAG}_bench_${name}_traced.json"
+  if [ "$last" = launches ]; then
+    last=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['roofline']['launches'])" "$OUT/${TAG}_bench_${name}_traced.json") || exit 1
+  fi
+  local dirs="gpurun_out/pmc_rd_$name gpurun_out/pmc_wr_$name"
+  run pmc_rd_$name 900 rocprofv3 --pmc $READS --kernel-trace --output-format csv -d gpurun_out/pmc_rd_$name -o run -- python3 "$@" || exit $?
+  run pmc_wr_$name 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_wr_$name -o run -- python3 "$@" || exit $?
+  if [ -n "$FETCH" ]; then
+    run pmc_fe_$name 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fe_$name -o run -- python3 "$@" || exit $?
+    dirs="$dirs gpurun_out/pmc_fe_$name"
+  fi
+  python3 scripts/pmc_summary.py "$OUT/${TAG}_pmc_${name}.json" $dirs --last "$last" --cmd "python3 $*" --config "$cfg" || exit $?
+  cp "$OUT/${TAG}_pmc_${name}.json" profiles/
+  run bench_$name 900 python3 "$@" || exit $?
+  grep '^{' gpurun_out/bench_$name.log | tail -1 > "$OUT/${TAG}_bench_${name}.json"
+}
+for L in $LEGS; do
+  case $L in
+    w2v_bfp40) FETCH=1 leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": false}" $W2V ;;
+    w2v_b100) leg $L 200 "{$W2VCFG, $TEXT8, \"minibatch\": 100, \"mode\": \"bfp40\", \"sharded\": false}" \
+                bench.py --gpus 1 --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline --no-parity-leg ;;
+    w2v_parity) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"parity\", \"sharded\": false}" $W2V --parity ;;
+    w2v_fast) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"fast\", \"sharded\": false}" $W2V --precision fast ;;
+    lr) leg $L 20 '{"app": "lr", "lr_batch": 65536, "exact": false, "world": 1, "sharded": false}' \
+          bench.py --app lr --steps 20 --warmup 3 --no-cpu-baseline ;;
+    s2v) leg $L launches '{"app": "s2v", "s2v_docs": 8192, "dim": 300, "world": 1}' \
+           bench.py --app s2v --steps 150 --warmup 3 --no-cpu-baseline ;;
+    w2v_config4) leg $L 20 "{$W2VCFG, \"tokens\": 125000000, \"vocab\": 1000000, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": false}" \
+                   $W2V --tokens 125000000 --vocab 1000000 ;;
+    w2v_sharded) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": true}" $W2V --sharded ;;
+    *) echo "unknown leg $L"; exit 2 ;;
+  esac
+done
 ls -la "$OUT"

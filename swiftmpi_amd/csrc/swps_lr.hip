@@ -841,19 +841,44 @@ int swps_lr_init(swps_lr *l) {
   const uint64_t V = l->vocab_keys.size();
   DevMem dk;
   SWPS_TRY(upload(dk, l->vocab_keys, l->s));
+  // keys the table already holds (ClusterServer::load of a dump before the
+  // first pull, lr.cpp:297-300 -> server.h:49-62) are found by the reference's
+  // pull, not initialised: they keep their rows and draw nothing
+  std::vector<uint32_t> pre;
+  uint64_t held = 0;
+  SWPS_TRY(swps_table_size(l->t, &held));
+  if (l->cfg.init_ref && held) {
+    DevMem dp;
+    SWPS_TRY(dp.ensure(std::max<uint64_t>(1, V) * 4));
+    SWPS_TRY(table_lookup(l->t, dk.as<uint64_t>(), V, dp.as<uint32_t>(), l->s));
+    pre.resize(V);
+    if (V) SWPS_HIP(hipMemcpyAsync(pre.data(), dp.p, V * 4, hipMemcpyDeviceToHost, l->s));
+    SWPS_HIP(hipStreamSynchronize(l->s));
+  }
   SWPS_TRY(table_find_or_insert(l->t, dk.as<uint64_t>(), V, l->d_vid_row.as<uint32_t>(), l->s));
   l->rows_mapped = false;  // vid_row changed: k_lr_map_rows again at the next batch
   if (l->cfg.init_ref) {
-    // LRPullAccessMethod::init_param (lr.cpp:48-50): w = gen_float() per miss
-    std::vector<float> rows(V * 2, 0.f);
+    // LRPullAccessMethod::init_param (lr.cpp:48-50): w = gen_float() per miss, in first-pull order
+    std::vector<uint32_t> vid_row(V), rid;
+    if (V) SWPS_HIP(hipMemcpyAsync(vid_row.data(), l->d_vid_row.p, V * 4, hipMemcpyDeviceToHost, l->s));
+    SWPS_HIP(hipStreamSynchronize(l->s));
+    std::vector<float> rows;
+    rows.reserve(V * 2);
+    rid.reserve(V);
     uint64_t y = std::numeric_limits<unsigned long>::max() / 2;
     for (uint64_t i = 0; i < V; i++) {
+      if (!pre.empty() && pre[i] != kNoRow) continue;
       y = y * kFlcgA + kLcgC;
-      rows[2 * i] = flcg_value(y);
+      rows.push_back(flcg_value(y));
+      rows.push_back(0.f);
+      rid.push_back(vid_row[i]);
     }
-    DevMem dr;
-    SWPS_TRY(upload(dr, rows, l->s));
-    SWPS_TRY(table_set_rows(l->t, l->d_vid_row.as<uint32_t>(), V, dr.p, l->s));
+    if (!rid.empty()) {
+      DevMem dr, dri;
+      SWPS_TRY(upload(dr, rows, l->s));
+      SWPS_TRY(upload(dri, rid, l->s));
+      SWPS_TRY(table_set_rows(l->t, dri.as<uint32_t>(), rid.size(), dr.p, l->s));
+    }
     SWPS_HIP(hipStreamSynchronize(l->s));
   }
   l->inited = true;

@@ -661,7 +661,12 @@ int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
   if (cfg->dtype != SWPS_F32 && cfg->dtype != SWPS_F64) return fail(SWPS_E_CFG, "unknown dtype");
   if (cfg->layout == SWPS_LAYOUT_W2V && cfg->dim <= 0) return fail(SWPS_E_CFG, "dim must be positive");
   if (cfg->capacity == 0 || cfg->capacity >= 0xFFFFFFF0ULL) return fail(SWPS_E_CFG, "capacity out of range");
-  if (cfg->push_rule != SWPS_PUSH_ADAGRAD && cfg->push_rule != SWPS_PUSH_SGD) return fail(SWPS_E_CFG, "unknown push rule");
+  if (cfg->push_rule != SWPS_PUSH_ADAGRAD && cfg->push_rule != SWPS_PUSH_SGD)
+    return fail(SWPS_E_UNSUPPORTED, "push rule " + std::to_string(cfg->push_rule) +
+                                        ": the library implements SWPS_PUSH_ADAGRAD and SWPS_PUSH_SGD only");
+  if (cfg->init_mode != SWPS_INIT_ZERO && cfg->init_mode != SWPS_INIT_HASH)
+    return fail(SWPS_E_UNSUPPORTED, "init mode " + std::to_string(cfg->init_mode) +
+                                        ": the library implements SWPS_INIT_ZERO and SWPS_INIT_HASH only");
   SWPS_HIP(hipSetDevice(cfg->device));
   swps_table *t = new swps_table();
   t->cfg = *cfg;

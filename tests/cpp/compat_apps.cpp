@@ -5,8 +5,11 @@
 //
 //   compat_apps w2v    -config C -data D -niters N -output O
 //   compat_apps s2v    -config C -data D -niters N -wordvec W -output O
-//   compat_apps lr     -config C -data D -niters N -output O   (per-epoch MSE)
+//   compat_apps lr     -config C -data D -niters N -output O [-param P]
+//                      (per-epoch MSE; -param: the trained shard's dump, lr.cpp:488-492)
+//   compat_apps lrpredict -config C -data D -param P -output O  (lr.cpp:498-504)
 //   compat_apps ps     -config C                               (PS-level client)
+//   compat_apps rules  -config C -case K   (access-method rule resolution)
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -64,6 +67,43 @@ typedef LocalParamCache<uint64_t, WLocalParam, WLocalGrad> cache_t;
 class WPullAccessMethod : public PullAccessMethod<uint64_t, WLocalParam, WLocalParam> {};
 class WPushAccessMethod : public PushAccessMethod<uint64_t, WLocalParam, WLocalGrad> {};
 typedef ClusterServer<uint64_t, WLocalParam, WLocalParam, WLocalGrad, WPullAccessMethod, WPushAccessMethod> server_t;
+
+// access methods with their own host bodies (word2vec_global.h:158-191 shape)
+class BodyPushAccessMethod : public PushAccessMethod<uint64_t, WLocalParam, WLocalGrad> {
+ public:
+  void apply_push_value(const uint64_t &, WLocalParam &, const WLocalGrad &) {}
+};
+class DeclaredPushAccessMethod : public PushAccessMethod<uint64_t, WLocalParam, WLocalGrad> {
+ public:
+  static const int32_t push_rule = SWPS_PUSH_ADAGRAD;  // what its body computes
+  void apply_push_value(const uint64_t &, WLocalParam &, const WLocalGrad &) {}
+};
+class UnknownPushAccessMethod : public PushAccessMethod<uint64_t, WLocalParam, WLocalGrad> {
+ public:
+  static const int32_t push_rule = 7;  // a rule the library lacks
+};
+class BodyPullAccessMethod : public PullAccessMethod<uint64_t, WLocalParam, WLocalParam> {
+ public:
+  void init_param(const uint64_t &, WLocalParam &) {}
+};
+
+// rule resolution of a ClusterServer: prints the resolved rules (errors exit 3)
+template <class PullM, class PushM> static int rules_of() {
+  typedef ClusterServer<uint64_t, WLocalParam, WLocalParam, WLocalGrad, PullM, PushM> s_t;
+  std::printf("init_mode=%d push_rule=%d\n", (int)s_t::init_mode(), (int)s_t::push_rule());
+  g_dim = global_config().get("word2vec", "len_vec").to_int32();
+  Cluster<ClusterWorker, s_t, uint64_t> cluster(64);
+  cluster.finalize();
+  return 0;
+}
+static int rules(const std::string &k) {
+  if (k == "plain") return rules_of<WPullAccessMethod, WPushAccessMethod>();
+  if (k == "push_body") return rules_of<WPullAccessMethod, BodyPushAccessMethod>();
+  if (k == "push_declared") return rules_of<WPullAccessMethod, DeclaredPushAccessMethod>();
+  if (k == "push_unknown") return rules_of<WPullAccessMethod, UnknownPushAccessMethod>();
+  if (k == "pull_body") return rules_of<BodyPullAccessMethod, WPushAccessMethod>();
+  return 2;
+}
 
 // rank r's keys: overlapping sets, so owners see several sources per key
 static bool has_key(uint64_t i, int r) { return (i + (uint64_t)r) % 3 != 0; }
@@ -167,13 +207,15 @@ int main(int argc, char **argv) {
     global_config().load_conf(a["-config"]);
     global_config().parse();
     if (mode == "ps") return ps_client();
+    if (mode == "rules") return rules(a["-case"]);
     const int niters = std::atoi(a["-niters"].c_str());
     if (mode == "w2v") {  // apps/word2vec/w2v.cpp:5-61
       Cluster<ClusterWorker, W2VServer, uint64_t> cluster;
       cluster.initialize();
       Word2VecApp w2v(a["-data"], niters);
       w2v.train();
-      cluster.finalize(a["-output"]);
+      const std::string out = a["-output"] + "-" + std::to_string(cluster.rank()) + ".txt";  // w2v.cpp:54
+      cluster.finalize(out);
     } else if (mode == "s2v") {  // apps/sent2vec/sent2vec.cpp:198-257
       Cluster<ClusterWorker, W2VServer, uint64_t> cluster;
       cluster.initialize();
@@ -188,6 +230,14 @@ int main(int argc, char **argv) {
       FILE *f = std::fopen(a["-output"].c_str(), "w");
       for (double e : err) std::fprintf(f, "%.17g\n", e);
       std::fclose(f);
+      cluster.finalize(a["-param"]);  // lr.cpp:488-492 (no dump when -param is absent)
+    } else if (mode == "lrpredict") {  // apps/logistic/lr.cpp:498-504 (predict mode)
+      Cluster<ClusterWorker, LRServer, uint32_t> cluster;
+      cluster.initialize();
+      LRApp lr(a["-data"]);
+      lr.load_param(a["-param"]);
+      lr.predict(a["-data"], a["-output"]);
+      cluster.finalize();
     } else {
       return 2;
     }

@@ -141,8 +141,8 @@ def test_compat_w2v_main_two_ranks_matches_python_driver(compat_bin, lib, gpu, t
                         os.path.join(ROOT, "tests", "dist_w2v_dump.py"), "--data", ",".join(data), "--out", py_out],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    for rank in range(2):
-        a = sorted(open("%s.%d" % (cpp_out, rank)).read().splitlines())
+    for rank in range(2):  # w2v.cpp:54-56: the main names its rank's file, finalize writes exactly that
+        a = sorted(open("%s-%d.txt" % (cpp_out, rank)).read().splitlines())
         b = sorted(open("%s.%d" % (py_out, rank)).read().splitlines())
         assert len(a) > 0 and a == b, rank
 
@@ -154,6 +154,7 @@ def test_compat_w2v_and_s2v_mains_match_python(compat_bin, lib, gpu, tmp_path):
     corpus = zipf_corpus(str(tmp_path / "c.txt"), 90, 200, seed=41)
     cpp_dump = str(tmp_path / "cpp_param.txt")
     _run(compat_bin, "w2v", "-config", str(conf), "-data", corpus, "-niters", "2", "-output", cpp_dump)
+    cpp_dump += "-0.txt"
     t = lib.Table("w2v", dim=16, capacity=1 << 22, dtype="f32", learning_rate=0.7)
     w = lib.Word2Vec(t, window=3, negative=4, minibatch=20, sample=1e-3, alpha=0.05)
     w.load_text(corpus)
@@ -195,3 +196,59 @@ def test_compat_lr_main_matches_python(compat_bin, lib, gpu, tmp_path):
     m.init()
     err = m.train(4)
     assert np.array_equal(np.loadtxt(out), err)
+
+
+@pytest.mark.parametrize("case,code", [("push_body", 3), ("push_unknown", 3), ("pull_body", 3)])
+def test_compat_access_method_rules_fail_loudly(compat_bin, tmp_path, case, code):
+    """An access method with its own apply_push_value / init_param body and
+    no declared rule, or a rule the library lacks, fails with
+    SWPS_E_UNSUPPORTED before any GPU work (accessmethod.h:16-33: the library
+    cannot run host bodies on the device)."""
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF)
+    r = subprocess.run([compat_bin, "rules", "-config", str(conf), "-case", case], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == code and "error -7" in r.stderr, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,rules", [("plain", "init_mode=1 push_rule=0"), ("push_declared", "init_mode=1 push_rule=0")])
+def test_compat_access_method_rules_resolve(compat_bin, gpu, tmp_path, case, rules):
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF)
+    out = _run(compat_bin, "rules", "-config", str(conf), "-case", case)
+    assert rules in out
+
+
+@pytest.mark.gpu
+def test_compat_lr_train_dump_then_predict_mode(compat_bin, lib, gpu, tmp_path):
+    """lr.cpp's two modes: train and finalize(param path) dumps the shard;
+    the predict mode (load_param, then predict) reproduces the Python
+    mirror's predictions from that dump, one per line at ostream precision 6
+    (lr.cpp:240-300,488-504)."""
+    conf = tmp_path / "demo.conf"
+    conf.write_text(LR_CONF)
+    data = os.path.join(GOLDEN, "lr_data.txt")
+    param = str(tmp_path / "param.txt")
+    _run(compat_bin, "lr", "-config", str(conf), "-data", data, "-niters", "3", "-output", str(tmp_path / "e.txt"),
+         "-param", param)
+    pred = str(tmp_path / "pred.txt")
+    _run(compat_bin, "lrpredict", "-config", str(conf), "-data", data, "-param", param, "-output", pred)
+    t = lib.Table("lr", capacity=1 << 22, dtype="f32", learning_rate=0.05)
+    t.load(param)
+    m = lib.LR(t, minibatch=200)
+    m.load_text(data)
+    m.init()
+    p, _ = m.predict()
+    lines = open(pred).read().splitlines()
+    assert len(lines) == len(p) > 0
+    assert lines == ["%g" % x for x in p]
+    # the dump covers every key of the data: nothing is re-initialised, so the
+    # predictions equal those of the trained model itself (to the dump's 6 digits)
+    t2 = lib.Table("lr", capacity=1 << 22, dtype="f32", learning_rate=0.05)
+    m2 = lib.LR(t2, minibatch=200)
+    m2.load_text(data)
+    m2.init()
+    m2.train(3)
+    p2, _ = m2.predict()
+    assert np.allclose(p, p2, rtol=1e-4, atol=1e-6)

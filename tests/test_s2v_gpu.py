@@ -157,3 +157,94 @@ def test_s2v_doc_sharding_partitions_docs(lib, gpu, tmp_path):
     allids = np.concatenate(seen)
     assert len(np.unique(allids)) == len(allids) == len(ids0)
     assert set(allids.tolist()) == set(ids0.tolist())
+
+
+@pytest.mark.parametrize("dtype,D", [("f64", 300), ("f32", 300), ("f64", 100), ("f32", 100)])
+def test_s2v_bench_dim_matches_oracle(lib, oracle_mod, gpu, tmp_path, dtype, D):
+    """The benchmarked dimension (config 5: D = 300, W = N = 5, docs of 50-200
+    tokens) against the oracle, the dump covering every word of the docs
+    (sent2vec.cpp:119-179: neu1 = sent_vec + sum of context v, sent_vec +=
+    alpha * neu1e).  D = 300 instantiates the scalar-tail docs kernels
+    (k_s2v_docs<float, 1, true> fp32, <double, 2, true> fp64) that D = 16 / 32
+    never reach; D = 100 the partial-chunk ones.  fp64 within 1e-9, fp32 within
+    1e-5 of the oracle's fp32-storage mode (full array)."""
+    orc, t, s = run_pair(lib, oracle_mod, tmp_path, dtype=dtype, D=D, W=5, N=5, B=40, niters=2, vocab=1500,
+                         dump_vocab=1500, nlines=160, lo=50, hi=200, seed=11)
+    io, vo, _ = orc.docs()
+    ig, vg, _ = s.docs()
+    assert len(io) == len(ig) > 100 and np.array_equal(io, ig)
+    info, so = s.info(), orc.stats()
+    assert info["lstate"] == so["rng"] and info["rand_calls"] == so["rand_calls"]
+    if dtype == "f64":
+        assert np.allclose(vg, vo, rtol=1e-9, atol=1e-12), np.abs(vg - vo).max()
+    else:
+        rel = np.abs(vg - vo) / np.maximum(np.abs(vo), 1e-3)
+        assert rel.max() < 1e-5, rel.max()
+
+
+def _zipf_docs(rng, V, nd, lo=50, hi=200):
+    p = 1.0 / np.arange(1, V + 1)
+    cdf = np.cumsum(p / p.sum())
+    lens = rng.integers(lo, hi + 1, nd)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    toks = (np.minimum(np.searchsorted(cdf, rng.random(int(off[-1]))), V - 1) + 1).astype(np.uint64)
+    return toks, off
+
+
+def test_s2v_config5_shape(lib, oracle_mod, gpu, tmp_path):
+    """BASELINE config 5's per-rank shape: a hash-initialised 1M x 300 fp32
+    word table (every word pulled once: the frozen word table), 60k docs of
+    50-200 Zipf(1M) tokens in minibatches of 4096 — run to run bit-identical,
+    finite, every position counted — and an oracle-sized slice of the same
+    docs (the first 120) trained on the same word rows (a full-precision dump
+    of the words they use, loaded by both) within 1e-5 of the oracle."""
+    import torch
+    rng = np.random.default_rng(5)
+    V, nd, D = 1_000_000, 60_000, 300
+    toks, off = _zipf_docs(rng, V, nd)
+    ids = np.arange(1, nd + 1, dtype=np.uint64) * 2654435761
+    t = lib.Table("w2v", dim=D, capacity=V + 16, dtype="f32", init="hash", seed=3)
+    keys = torch.arange(1, V + 1, dtype=torch.int64, device="cuda")
+    for k0 in range(0, V, 1 << 18):
+        t.pull(keys[k0:k0 + (1 << 18)])
+    outs = []
+    for _ in range(2):
+        s = lib.Sent2Vec(t, window=5, negative=5, minibatch=4096, niters=1)
+        s.load_tokens(toks, off, ids)
+        s.train()
+        outs.append((s.docs()[1], s.stats()))
+        del s
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.isfinite(outs[0][0]).all()
+    st = outs[0][1]
+    assert st["docs"] == nd and st["positions"] == int(off[-1])
+    assert st["tgt_rows"] >= st["positions"]
+    # the oracle slice: the first 120 docs as text, the rows of their words dumped at full precision
+    ns = 120
+    corpus = str(tmp_path / "slice.txt")
+    with open(corpus, "w") as f:
+        for i in range(ns):
+            f.write(" ".join(str(int(x)) for x in toks[int(off[i]):int(off[i + 1])]) + "\n")
+    words = np.unique(toks[:int(off[ns])])
+    rows = t.export(torch.as_tensor(words.astype(np.int64), device="cuda")).cpu().numpy()
+    dump = str(tmp_path / "words.txt")
+    with open(dump, "w") as f:
+        for k, r in zip(words, rows):  # WParam operator<< order: v then h (word2vec_global.h:102-111)
+            f.write("%d\t%s\t%s\n" % (k, " ".join("%.9g" % x for x in r[D:2 * D]),
+                                      " ".join("%.9g" % x for x in r[:D])))
+    orc = oracle_mod.S2V(corpus, D, window=5, negative=5, minibatch=4096, niters=1, table_size=10 ** 8,
+                         storage_f32=True, rand_offset=2)
+    orc.load_words(dump)
+    orc.train()
+    t2 = lib.Table("w2v", dim=D, capacity=len(words) + 64, dtype="f32")
+    s2 = lib.Sent2Vec(t2, window=5, negative=5, minibatch=4096, niters=1, rand_offset=2)
+    s2.load_word_vector(dump)
+    s2.load_text(corpus)
+    s2.train()
+    io, vo, _ = orc.docs()
+    ig, vg, _ = s2.docs()
+    assert len(io) == ns and np.array_equal(io, ig)
+    assert np.array_equal(t2.export(torch.as_tensor(words.astype(np.int64), device="cuda")).cpu().numpy()[:, :2 * D],
+                          rows[:, :2 * D])  # the word rows the slice trained on are the 1M table's
+    rel = np.abs(vg - vo) / np.maximum(np.abs(vo), 1e-3)
+    assert rel.max() < 1e-5, rel.max()
