@@ -127,6 +127,54 @@ def cpu_baseline(ids, off, keys, args, lines):
                                                res[0]["words"] / res[0]["dt"])}
 
 
+_W2V_MULTI_WORKER = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+import oracle
+paths = sys.argv[2].split(",")
+dim, window, negative, minibatch, sample, alpha, lr = sys.argv[3:10]
+m = oracle.W2VMulti(paths, int(dim), window=int(window), negative=int(negative), minibatch=int(minibatch),
+                    sample=float(sample), alpha=float(alpha), lr=float(lr), table_size=int(1e8))
+t0 = time.perf_counter()
+m.train(1)
+dt = time.perf_counter() - t0
+print(json.dumps({"words": sum(m.rank_stats(r)["actual_train_words"] for r in range(len(paths))), "dt": dt}))
+"""
+
+
+def cpu_baseline_config1(ids, off, args, lines):
+    """BASELINE config 1 on the CPU: 2 ranks, D = 100, minibatch 100 lines, in
+    the oracle's lockstep multi-rank restatement (W2VMulti: each rank trains
+    its own `lines`-line slice, pulls from and pushes to one key-sharded
+    server state, every rank's push its own AdaGrad step in rank order — the
+    exchange of apps/word2vec/cluster_run.sh:2 done in memory), one process,
+    one core.  Child process (fresh interpreter), never forked from this GPU
+    process."""
+    import subprocess
+    import oracle
+    oracle.build()
+    with tempfile.TemporaryDirectory() as d:
+        paths = []
+        for r in range(2):
+            path = os.path.join(d, "rank%d.txt" % r)
+            with open(path, "w") as f:
+                for l in range(r * lines, (r + 1) * lines):
+                    a, b = int(off[l]), int(off[l + 1])
+                    f.write(" ".join("w%d" % x for x in ids[a:b]) + "\n")
+            paths.append(path)
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        r = subprocess.run([sys.executable, "-c", _W2V_MULTI_WORKER, ROOT, ",".join(paths), "100", str(args.window),
+                            str(args.negative), "100", str(args.sample), str(args.alpha), str(args.lr)],
+                           capture_output=True, text=True, env=env)
+        if r.returncode:
+            raise RuntimeError("config-1 cpu worker failed: " + r.stderr[-2000:])
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": res["words"] / res["dt"], "unit": "words/s", "cores": 1, "kind": "port",
+            "sample": "oracle/swps_oracle.cpp W2VMulti (fp64, nthreads=1 semantics): 2 ranks in lockstep, each on its "
+                      "own %d-line slice of the same corpus (%d words in all), D=100, minibatch 100, 1 epoch, one "
+                      "process; %.1f s" % (lines, res["words"], res["dt"])}
+
+
 def cpu_baseline_lr(y, off, f, v, minibatch, lr, rows):
     """The oracle's LR (lr.cpp semantics, nthreads = 1, fp32) on the first
     `rows` rows of the same synthetic Criteo-shaped data, one epoch."""
@@ -224,6 +272,10 @@ def main():
                     help="skip the extra parity- and fast-mode timings reported beside the headline")
     ap.add_argument("--b100-steps", type=int, default=200,
                     help="minibatches of the extra B = 100 leg (SURVEY.md §8(d) config 1's minibatch); 0 = skip")
+    ap.add_argument("--config1-steps", type=int, default=200,
+                    help="minibatches of the BASELINE config-1 leg (D = 100, minibatch 100) on the GPU; 0 = skip")
+    ap.add_argument("--config1-cpu-lines", type=int, default=600,
+                    help="lines per rank of the config-1 CPU leg (2 ranks in lockstep, oracle W2VMulti)")
     ap.add_argument("--sampler", default="table", choices=["table", "alias"],
                     help="negative sampler: the reference's unigram table (bit-exact draws) or an alias table")
     ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
@@ -290,10 +342,10 @@ def main():
             _comm.append(c if int(t.item()) else None)
         return _comm[0]
 
-    def build(fp64_intermediates, minibatch=None):
+    def build(fp64_intermediates, minibatch=None, dim=None):
         kw = dict(window=args.window, negative=args.negative, minibatch=minibatch or args.minibatch, sample=args.sample,
                   alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates, sampler=args.sampler)
-        t = sw.Table("w2v", dim=args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
+        t = sw.Table("w2v", dim=dim or args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
                      device=local, init="hash", seed=1)
         if sharded and args.driver == "native" and native_comm() is not None:  # the library's own exchange
             from swiftmpi_amd.dist import NativeShardedWord2Vec
@@ -457,23 +509,23 @@ def main():
                                                                   "k_forward")})
     traffic, fwd_traffic = tr["sum"], tr["forward"]
 
-    parity_leg, fast_leg = None, None
-    if rank == 0 and world == 1 and not parity_main and not args.no_parity_leg:
-        t2, w2 = build(fp64_intermediates=True)
-        w2.train_batches(args.warmup)
-        w2.sync()
-        pdt, pd = timed(w2, args.steps)
-        parity_leg = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
-                      "mode": "fp64 neu1/neu1e + gradient partials (reference-parity mode)"}
-        del w2, t2
-    if rank == 0 and world == 1 and bfp_main and not args.no_parity_leg:
-        t2, w2 = build(fp64_intermediates=False)
-        w2.train_batches(args.warmup)
-        w2.sync()
-        pdt, pd = timed(w2, args.steps)
-        fast_leg = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
-                    "mode": "fp32 neu1/neu1e + partials (fast mode: outside the 1e-5 single-batch bar at D = 100)"}
-        del w2, t2
+    # the other precision modes on the same workload, timed the same way
+    MODE_DESC = {"parity": "fp64 neu1/neu1e + gradient partials (reference-parity mode)",
+                 "bfp40": "block-fp neu1/neu1e, int32 + int8 mantissas per row exponent, fp64 sums (5 B/element)",
+                 "bfp32": "block-fp neu1/neu1e, int32 mantissas per row exponent, fp64 sums (4 B/element)",
+                 "fast": "fp32 neu1/neu1e + partials (fast mode: outside the 1e-5 single-batch bar)"}
+    other_modes = {}
+    if rank == 0 and world == 1 and not args.no_parity_leg and args.dtype == "f32":
+        for m in ("parity", "bfp40", "bfp32", "fast"):
+            if m == prec:
+                continue
+            t2, w2 = build(fp64_intermediates=INTER[m])
+            w2.train_batches(args.warmup)
+            w2.sync()
+            pdt, pd = timed(w2, args.steps)
+            other_modes[m] = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
+                              "mode": MODE_DESC[m]}
+            del w2, t2
     # SURVEY.md §8(d) config 1's minibatch (B = 100 lines of the same
     # 1000-token lines), same mode as the headline, timed the same way over
     # --b100-steps minibatches (the driver-visible small-batch number)
@@ -487,6 +539,22 @@ def main():
                     "warmup": 10, "ms_per_step": bdt * 1e3 / args.b100_steps,
                     "kept_positions_per_s": bd["kept"] / bdt, "pulled_keys_per_step": bd["pulled"] / args.b100_steps}
         del w3, t3
+
+    # BASELINE config 1 (D = 100, minibatch 100 lines) on this GPU, same mode, beside its CPU
+    # run (2 ranks in lockstep, cpu_baseline_config1)
+    config1 = None
+    if rank == 0 and world == 1 and not sharded and args.config1_steps > 0:
+        t4, w4 = build(fp64_intermediates=INTER[prec], minibatch=100, dim=100)
+        w4.train_batches(10)
+        w4.sync()
+        cdt, cd = timed(w4, args.config1_steps)
+        config1 = {"gpu": {"value": cd["words"] / cdt, "unit": "words/s", "n_gpus": 1, "dim": 100, "minibatch": 100,
+                           "steps": args.config1_steps, "ms_per_step": cdt * 1e3 / args.config1_steps},
+                   "note": "BASELINE config 1 (D=100, window 5, negative 5, minibatch 100): the GPU on one rank's "
+                           "corpus; the reference's 2-rank CPU plumbing as cpu_2rank"}
+        del w4, t4
+        if not args.no_cpu_baseline:
+            config1["cpu_2rank"] = cpu_baseline_config1(ids, off, args, args.config1_cpu_lines)
 
     out = {
         "metric": "SGNS trained words/sec at 1/8 GPUs; sparse push/pull HBM GB/s vs peak",
@@ -553,9 +621,9 @@ def main():
                      "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
                      "pull_push": pp or None},
         "kernel_ms": {k: v[0] for k, v in kt.items()},
-        "parity_mode": parity_leg,
-        "fast_mode": fast_leg,
+        "other_modes": other_modes or None,
         "minibatch_100": b100_leg,
+        "config1": config1,
         "exchange": exchange,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

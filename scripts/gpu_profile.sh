@@ -54,6 +54,7 @@ leg() {  # name last(N|launches) config-json args...
 for L in $LEGS; do
   case $L in
     w2v_bfp40) FETCH=1 leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": false}" $W2V ;;
+    w2v_bfp32) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": false}" $W2V --precision bfp32 ;;
     w2v_b100) leg $L 200 "{$W2VCFG, $TEXT8, \"minibatch\": 100, \"mode\": \"bfp40\", \"sharded\": false}" \
                 bench.py --gpus 1 --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline --no-parity-leg ;;
     w2v_parity) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"parity\", \"sharded\": false}" $W2V --parity ;;

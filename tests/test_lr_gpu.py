@@ -234,11 +234,11 @@ def test_lr_config3_batches_match_oracle(lib, oracle_mod, gpu, criteo_text, fast
     Exact mode (the reference's sequential fp32 chain): weights, AdaGrad sums
     and epoch errors within 1e-5 relative of the oracle.  fast_sums (fp64
     per-key sums): within 1e-5 of the oracle's fp64-sum variant (same
-    definition, summation order aside); against the reference oracle the
-    weights stay within 1e-5 and each AdaGrad sum within 1e-5 plus the
-    reference's own fp32-chain rounding, measured as the distance between the
-    two oracle modes (a hot key's mean of ~3e4 cancelling fp32 terms carries
-    ~1e-4 relative rounding in the reference)."""
+    definition, summation order aside); against the reference oracle every
+    weight and AdaGrad sum within 1e-5 plus the reference's own fp32-chain
+    rounding, measured as the distance between the two oracle modes (a hot
+    key's mean of ~3e4 cancelling fp32 terms carries up to ~1e-4 relative
+    rounding in the reference: 3e-6 absolute on a weight was seen)."""
     orc = oracle_mod.LR(criteo_text, 65536, 0.05)
     e_o = orc.train(2)
     ko, wo, go = orc.params()
@@ -250,8 +250,8 @@ def test_lr_config3_batches_match_oracle(lib, oracle_mod, gpu, criteo_text, fast
     e_g = m.train(2)
     kg, wg, gg = m.params()
     assert len(ko) > 100000 and np.array_equal(ko, kg)
-    assert np.allclose(wg, wo, rtol=1e-5, atol=1e-6), np.abs(wg - wo).max()
     if not fast:
+        assert np.allclose(wg, wo, rtol=1e-5, atol=1e-6), np.abs(wg - wo).max()
         assert np.allclose(gg, go, rtol=1e-5, atol=1e-7), np.abs(gg - go).max()
         assert np.allclose(e_g, e_o, rtol=1e-5)
         return
@@ -262,6 +262,7 @@ def test_lr_config3_batches_match_oracle(lib, oracle_mod, gpu, criteo_text, fast
     assert np.allclose(wg, w64, rtol=1e-5, atol=1e-6), np.abs(wg - w64).max()
     assert np.allclose(gg, g64, rtol=1e-5, atol=1e-7), np.abs(gg - g64).max()
     assert np.allclose(e_g, e_64, rtol=1e-5)
-    ref_round = np.abs(g64.astype(np.float64) - go)
-    assert (np.abs(gg.astype(np.float64) - go) <= ref_round + 1e-5 * np.abs(go) + 1e-7).all()
+    for got, f64, ref, atol in ((wg, w64, wo, 1e-6), (gg, g64, go, 1e-7)):
+        ref_round = np.abs(f64.astype(np.float64) - ref)  # the reference's own fp32-chain rounding
+        assert (np.abs(got.astype(np.float64) - ref) <= ref_round + 1e-5 * np.abs(ref) + atol).all()
     assert np.allclose(e_g, e_o, rtol=1e-5)
