@@ -263,10 +263,11 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=1000000, help="LR CPU baseline sample (rows)")
     ap.add_argument("--cpu-docs", type=int, default=3000, help="sent2vec CPU baseline sample (documents)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", default="bfp40", choices=["bfp40", "bfp32", "fast", "parity"],
-                    help="fp32-table intermediates: bfp40 (block-floating-point neu1/neu1e, int32 + int8 "
-                         "mantissas per row exponent, fp64 sums: within the north star's 1e-5 single-batch bar; "
-                         "the default), bfp32 (int32 mantissas), fast (fp32), parity (fp64)")
+    ap.add_argument("--precision", default="bfp32", choices=["bfp40", "bfp32", "fast", "parity"],
+                    help="fp32-table intermediates: bfp32 (block-floating-point neu1/neu1e, int32 mantissas per "
+                         "row exponent, fp64 sums and mean: within the north star's 1e-5 single-batch bar at fp32's "
+                         "4 B per element; the default), bfp40 (+ an int8 residual: 1e-5 after two batches too), "
+                         "fast (fp32), parity (fp64)")
     ap.add_argument("--parity", action="store_true", help="= --precision parity")
     ap.add_argument("--no-parity-leg", action="store_true",
                     help="skip the extra parity- and fast-mode timings reported beside the headline")

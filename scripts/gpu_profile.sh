@@ -18,7 +18,7 @@ mkdir -p gpurun_out "$OUT" profiles
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 R=$(pwd)
 cd /tmp && export TMPDIR=/tmp && cd "$R"
-LEGS=${LEGS:-"w2v_bfp40 w2v_b100 w2v_parity w2v_fast lr s2v w2v_config4 w2v_sharded"}
+LEGS=${LEGS:-"w2v_bfp32 w2v_bfp40 w2v_b100 w2v_parity w2v_fast lr s2v w2v_config4 w2v_sharded"}
 READS="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
 run() {  # name timeout args...
   local name=$1 to=$2; shift 2
@@ -53,9 +53,9 @@ leg() {  # name last(N|launches) config-json args...
 }
 for L in $LEGS; do
   case $L in
-    w2v_bfp40) FETCH=1 leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": false}" $W2V ;;
-    w2v_bfp32) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": false}" $W2V --precision bfp32 ;;
-    w2v_b100) leg $L 200 "{$W2VCFG, $TEXT8, \"minibatch\": 100, \"mode\": \"bfp40\", \"sharded\": false}" \
+    w2v_bfp32) FETCH=1 leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": false}" $W2V ;;
+    w2v_bfp40) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": false}" $W2V --precision bfp40 ;;
+    w2v_b100) leg $L 200 "{$W2VCFG, $TEXT8, \"minibatch\": 100, \"mode\": \"bfp32\", \"sharded\": false}" \
                 bench.py --gpus 1 --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline --no-parity-leg --config1-steps 0 ;;
     w2v_parity) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"parity\", \"sharded\": false}" $W2V --parity ;;
     w2v_fast) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"fast\", \"sharded\": false}" $W2V --precision fast ;;
@@ -63,9 +63,9 @@ for L in $LEGS; do
           bench.py --app lr --steps 20 --warmup 3 --no-cpu-baseline ;;
     s2v) leg $L launches '{"app": "s2v", "s2v_docs": 8192, "dim": 300, "world": 1}' \
            bench.py --app s2v --steps 150 --warmup 3 --no-cpu-baseline ;;
-    w2v_config4) leg $L 20 "{$W2VCFG, \"tokens\": 125000000, \"vocab\": 1000000, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": false}" \
+    w2v_config4) leg $L 20 "{$W2VCFG, \"tokens\": 125000000, \"vocab\": 1000000, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": false}" \
                    $W2V --tokens 125000000 --vocab 1000000 ;;
-    w2v_sharded) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": true}" $W2V --sharded ;;
+    w2v_sharded) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": true}" $W2V --sharded ;;
     *) echo "unknown leg $L"; exit 2 ;;
   esac
 done
