@@ -50,6 +50,8 @@ leg() {  # name last(N|launches) config-json args...
   cp "$OUT/${TAG}_pmc_${name}.json" profiles/
   run bench_$name 900 python3 "$@" || exit $?
   grep '^{' gpurun_out/bench_$name.log | tail -1 > "$OUT/${TAG}_bench_${name}.json"
+  # the per-dispatch traces are tens of MB each: only the summaries travel back
+  rm -rf gpurun_out/prof_$name gpurun_out/pmc_rd_$name gpurun_out/pmc_wr_$name gpurun_out/pmc_fe_$name
 }
 for L in $LEGS; do
   case $L in

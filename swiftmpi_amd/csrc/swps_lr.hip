@@ -93,7 +93,8 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
                                                       const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
                                                       const float *__restrict__ label, uint64_t r0, uint64_t nr,
                                                       const float *__restrict__ rows, int stride,
-                                                      float *__restrict__ err, float *__restrict__ err2) {
+                                                      float *__restrict__ err, float *__restrict__ err2,
+                                                      int diag = 0) {
   constexpr int L = 64 / R;
   const int lane = threadIdx.x & 63;
   const int sub = lane / L, k = lane - sub * L;
@@ -108,8 +109,23 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
     const uint64_t a = row_off[r];
     m = (int)(row_off[r + 1] - a);
     y = label[r];
-    if (k < m) p0 = weight_at(rows, fidx[a + k], stride) * fval[a + k];
-    if (k + L < m) p1 = weight_at(rows, fidx[a + k + L], stride) * fval[a + k + L];
+    if (diag & 1) {  // SWPS_LR_DIAG timing experiment only: no weight gather (w = x)
+      if (k < m) p0 = fval[a + k];
+      if (k + L < m) p1 = fval[a + k + L];
+    } else {
+      if (k < m) p0 = weight_at(rows, fidx[a + k], stride) * fval[a + k];
+      if (k + L < m) p1 = weight_at(rows, fidx[a + k + L], stride) * fval[a + k + L];
+    }
+  }
+  if (diag & 2) {  // timing experiment only: no ordered chain (a wave tree sum per row)
+    float t = p0 + p1;
+    for (int o = 1; o < L; o <<= 1) t += __shfl_xor(t, o);
+    if (act && k == 0) {
+      const float predict = (float)(1. / (1. + (double)(float)exp((double)(-t))));
+      err[r0 + j] = y - predict;
+      err2[r0 + j] = (y - predict) * (y - predict);
+    }
+    return;
   }
   int mq[R];
   int mmax = 0;
@@ -138,6 +154,52 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
     err[r0 + j] = error;
     err2[r0 + j] = error * error;
   }
+}
+
+// One lane per example: the lane sums its own row in feature order (lr.cpp:
+// 358-375, fp32 products and adds, -ffp-contract=off: bit-identical to the
+// cross-lane forms above) — no readlane chain.  Per chunk of CH features the
+// lane issues every index and value load, then every weight gather, then the
+// ordered adds, so a row of <= CH features is three memory round trips.  The
+// index/value loads of a wave touch 64 rows' lines at once; a lane's next
+// features hit the same lines in L1.  (Measured by SWPS_LR_DIAG on the
+// cross-lane k_lr_forward_r<3>: the ordered readlane chain alone was ~12 of
+// its ~34 us per 65,537-row batch.)
+template <int CH>
+__global__ __launch_bounds__(64) void k_lr_forward_l(const uint64_t *__restrict__ row_off,
+                                                     const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
+                                                     const float *__restrict__ label, uint64_t r0, uint64_t nr,
+                                                     const float *__restrict__ rows, int stride,
+                                                     float *__restrict__ err, float *__restrict__ err2) {
+  const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= nr) return;
+  const uint64_t r = r0 + j;
+  const uint64_t a = row_off[r], b = row_off[r + 1];
+  float sum = 0.f;
+  for (uint64_t c = a; c < b; c += CH) {
+    const int m = (int)min<uint64_t>(CH, b - c);
+    uint32_t id[CH];
+    float x[CH], w[CH];
+#pragma unroll
+    for (int k = 0; k < CH; k++)
+      if (k < m) {
+        id[k] = fidx[c + k];
+        x[k] = fval[c + k];
+      }
+#pragma unroll
+    for (int k = 0; k < CH; k++)
+      if (k < m) w[k] = weight_at(rows, id[k], stride);
+#pragma unroll
+    for (int k = 0; k < CH; k++)
+      if (k < m) {
+        const float prod = w[k] * x[k];
+        sum += prod;
+      }
+  }
+  const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
+  const float error = label[r] - predict;
+  err[r] = error;
+  err2[r] = error * error;
 }
 
 // ---- the static per-batch index (built once at load; lr_index) -------------
@@ -514,7 +576,9 @@ struct swps_lr {
   DevMem d_slong;
   int fused_reduce = 1;         // fast sums: k_lr_reduce_fused (SWPS_LR_FUSED=0: memset + short + long; A/B)
   std::vector<uint32_t> bmaxf;  // longest row (features) per batch: k_lr_forward_r's row packing
-  int rows_per_wave = 1;        // SWPS_LR_PACK: 0 = one row per wave (k_lr_forward), 2 = at most 2, 1 = by length
+  int rows_per_wave = 1;        // SWPS_LR_PACK: 1 = a lane per row (k_lr_forward_l), 0 = one row per wave
+                                // (k_lr_forward), 3 = 3 or 2 rows per wave by length, 2 = at most 2
+  int fwd_diag = 0;             // SWPS_LR_DIAG: forward timing experiments (1: no weight gather, 2: no ordered chain)
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
   LTimer timer;
@@ -695,10 +759,16 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   hipEvent_t e0 = l->timer.begin(s);
   const uint64_t nrb = r1 - r0;
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
-  if (l->rows_per_wave && mf <= 42 && l->rows_per_wave != 2)
+  if (l->rows_per_wave == 1)  // a lane per row (default)
+    k_lr_forward_l<40><<<(unsigned)((nrb + 63) / 64), 64, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx,
+                                                                  l->d_fval.as<float>(), l->d_label.as<float>(), r0,
+                                                                  nrb, rows, stride, l->d_err.as<float>(),
+                                                                  l->d_err2.as<float>());
+  else if (l->rows_per_wave && mf <= 42 && l->rows_per_wave != 2)
     k_lr_forward_r<3><<<nblk((nrb + 2) / 3 * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(),
                                                                 l->d_label.as<float>(), r0, nrb, rows, stride,
-                                                                l->d_err.as<float>(), l->d_err2.as<float>());
+                                                                l->d_err.as<float>(), l->d_err2.as<float>(),
+                                                                l->fwd_diag);
   else if (l->rows_per_wave && mf <= 64)
     k_lr_forward_r<2><<<nblk((nrb + 1) / 2 * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(),
                                                                 l->d_label.as<float>(), r0, nrb, rows, stride,
@@ -760,6 +830,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   l->s = t->stream;
   l->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
+  if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;

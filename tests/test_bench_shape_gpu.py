@@ -24,8 +24,12 @@ AdaGrad):
             * two epochs: full-array max within BFP_TOL_MAX and p99.99
               within 1e-6 (chaotic: see below; emulated 1.1e-4 / 4.8e-5).
   bfp32   the same with int32 mantissas only (4 B per element, fast mode's
-          bytes): one minibatch within 1e-5 (emulated 2.3e-7); two chained
-          minibatches and two epochs within the fast bars.
+          bytes) — the bench's headline mode (k_forward_b / k_gather_b /
+          k_push_b <1,1,0> at D = 300): one minibatch within 1e-5 (emulated
+          1.2e-7 / 2.3e-7); two chained minibatches within FAST_TOL_BATCH
+          (measured 1.8e-5 / 8.4e-6); two epochs max within BFP32_TOL_MAX and
+          p99.9 within BFP32_TOL_P999 (measured 1.4e-3 / 9.0e-4, p99.9
+          2.0e-6 / 1.6e-6 — the emulation's 1.4e-3 / 9.0e-4).
   fast    fp32 table, fp32 neu1/neu1e and partials — k_forward_t<1,4,1> /
           k_gather_t<1,8> / k_push_thp<1,8> at D = 300 (256 + a 44-lane
           tail), the generic fp32 kernels at D = 100 — vs the oracle's
@@ -69,6 +73,10 @@ FAST_TOL_BATCH = 2e-4
 # 4.8e-5 (D = 100), p99.99 9.5e-8 / 1.0e-7.
 BFP_TOL_MAX = 1e-3
 BFP_TOL_P9999 = 1e-6
+# bfp32 after two epochs: the same chaos started from ~2^-32 perturbations
+# (measured max 1.4e-3 at D = 300, 9.0e-4 at D = 100; p99.9 2.0e-6 / 1.6e-6)
+BFP32_TOL_MAX = 1e-2
+BFP32_TOL_P999 = 1e-5
 MODES = {"f64": ("f64", True), "parity": ("f32", True), "fast": ("f32", False), "bfp40": ("f32", "bfp40"),
          "bfp32": ("f32", "bfp32")}
 
@@ -156,6 +164,8 @@ def test_bench_kernels_match_oracle(lib, gpu, bench_corpus, oracles, D, mode):
         assert rel.max() <= 1e-5, float(rel.max())
     elif mode == "bfp40":
         assert rel.max() <= BFP_TOL_MAX and np.quantile(rel, 0.9999) <= BFP_TOL_P9999, float(rel.max())
+    elif mode == "bfp32":
+        assert rel.max() <= BFP32_TOL_MAX and np.quantile(rel, 0.999) <= BFP32_TOL_P999, float(rel.max())
     else:
         assert np.quantile(rel, 0.999) <= FAST_TOL_P999 and rel.max() <= FAST_TOL_MAX, float(rel.max())
 

@@ -164,13 +164,14 @@ def test_lr_fast_sums_criteo_shape_close_to_exact(lib, gpu):
 
 @pytest.mark.parametrize("fast", [False, True])
 def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
-    """k_lr_forward_r (3 or 2 rows per wave, by the batch's longest row) ==
-    one row per wave, bit for bit: Criteo-shaped rows (39 features: 3 per
-    wave) and the reference's data.txt (its own row lengths)."""
+    """k_lr_forward_l (a lane per row, the default) == k_lr_forward_r (3 or 2
+    rows per wave, by the batch's longest row) == one row per wave, bit for
+    bit: Criteo-shaped rows (39 features: 3 per wave) and the reference's
+    data.txt (its own row lengths, some longer than one 40-feature chunk)."""
     from swiftmpi_amd.synth import criteo
     y, off, f, v = criteo(9000, seed=5)
     res = []
-    for pack in ("0", "1", "2"):
+    for pack in ("0", "1", "2", "3"):
         monkeypatch.setenv("SWPS_LR_PACK", pack)
         t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
         m = lib.LR(t, minibatch=1000, init_ref=False, fast_sums=fast)
@@ -182,7 +183,19 @@ def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
         m2.load_text(DATA)
         m2.init()
         e2 = m2.train(2)
-        res.append((e, m.params()[1], e2, m2.params()[1]))
+        # ragged rows of 1..130 features (several 40-feature chunks per lane)
+        rng = np.random.default_rng(9)
+        lens = rng.integers(1, 131, 3000)
+        roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        feat = rng.integers(0, 5000, int(roff[-1])).astype(np.uint32)
+        vals = rng.random(int(roff[-1])).astype(np.float32)
+        yl = (rng.random(3000) < 0.5).astype(np.float32)
+        t3 = lib.Table("lr", capacity=1 << 14, dtype="f32", learning_rate=0.05, init="hash", seed=2)
+        m3 = lib.LR(t3, minibatch=500, init_ref=False, fast_sums=fast)
+        m3.load_csr(yl, roff, feat, vals)
+        m3.init()
+        e3 = m3.train(2)
+        res.append((e, m.params()[1], e2, m2.params()[1], e3, m3.params()[1]))
     for r in res[1:]:
         for a, b in zip(res[0], r):
             assert np.array_equal(a, b)
