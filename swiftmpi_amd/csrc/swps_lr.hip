@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__
 // feature indices -> weights -> the ordered sum), so R rows per wave put R times the chains
 // in flight per wave slot; the R ordered sums run interleaved.  Same products, same
 // feature-order fp32 sums as k_lr_forward: bit-identical.
-template <int R>
+template <int R, bool LDS_SUM = false>
 __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict__ row_off,
                                                       const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
                                                       const float *__restrict__ label, uint64_t r0, uint64_t nr,
@@ -124,6 +124,36 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
       const float predict = (float)(1. / (1. + (double)(float)exp((double)(-t))));
       err[r0 + j] = y - predict;
       err2[r0 + j] = (y - predict) * (y - predict);
+    }
+    return;
+  }
+  if (LDS_SUM) {
+    // the ordered sums through LDS: every lane stores its two products, then one lane per row
+    // reads its row's products back in feature order (4 per ds_read) and adds them sequentially
+    // — the same fp32 adds in the same order as the readlane chain below, without its
+    // per-feature readlane latency
+    __shared__ float4 sp[4][R][(2 * L + 3) / 4];
+    float *row = (float *)sp[threadIdx.x >> 6][sub < R ? sub : 0];
+    if (sub < R) {
+      row[k] = p0;
+      row[k + L] = p1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (act && k == 0) {
+      float s = 0.f;
+      const float4 *r4 = (const float4 *)row;
+      for (int f4 = 0; f4 * 4 < m; f4++) {
+        const float4 v = r4[f4];
+        s += v.x;
+        if (f4 * 4 + 1 < m) s += v.y;
+        if (f4 * 4 + 2 < m) s += v.z;
+        if (f4 * 4 + 3 < m) s += v.w;
+      }
+      const float predict = (float)(1. / (1. + (double)(float)exp((double)(-s))));
+      const float error = y - predict;
+      err[r0 + j] = error;
+      err2[r0 + j] = error * error;
     }
     return;
   }
@@ -576,8 +606,9 @@ struct swps_lr {
   DevMem d_slong;
   int fused_reduce = 1;         // fast sums: k_lr_reduce_fused (SWPS_LR_FUSED=0: memset + short + long; A/B)
   std::vector<uint32_t> bmaxf;  // longest row (features) per batch: k_lr_forward_r's row packing
-  int rows_per_wave = 1;        // SWPS_LR_PACK: 1 = a lane per row (k_lr_forward_l), 0 = one row per wave
-                                // (k_lr_forward), 3 = 3 or 2 rows per wave by length, 2 = at most 2
+  int rows_per_wave = 1;        // SWPS_LR_PACK: 1 = 3 or 2 rows per wave by length, ordered sums through LDS
+                                // (the default; longer rows: one per wave); 3 = the same with readlane chains;
+                                // 2 = at most 2 (readlane); 4 = a lane per row (k_lr_forward_l); 0 = a row per wave
   int fwd_diag = 0;             // SWPS_LR_DIAG: forward timing experiments (1: no weight gather, 2: no ordered chain)
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
@@ -759,7 +790,17 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   hipEvent_t e0 = l->timer.begin(s);
   const uint64_t nrb = r1 - r0;
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
-  if (l->rows_per_wave == 1)  // a lane per row (default)
+  if (l->rows_per_wave == 1 && mf <= 42)  // 3 rows per wave, the ordered sums through LDS (default)
+    k_lr_forward_r<3, true><<<nblk((nrb + 2) / 3 * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx,
+                                                                      l->d_fval.as<float>(), l->d_label.as<float>(),
+                                                                      r0, nrb, rows, stride, l->d_err.as<float>(),
+                                                                      l->d_err2.as<float>());
+  else if (l->rows_per_wave == 1 && mf <= 64)
+    k_lr_forward_r<2, true><<<nblk((nrb + 1) / 2 * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx,
+                                                                      l->d_fval.as<float>(), l->d_label.as<float>(),
+                                                                      r0, nrb, rows, stride, l->d_err.as<float>(),
+                                                                      l->d_err2.as<float>());
+  else if (l->rows_per_wave == 4)  // a lane per row
     k_lr_forward_l<40><<<(unsigned)((nrb + 63) / 64), 64, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx,
                                                                   l->d_fval.as<float>(), l->d_label.as<float>(), r0,
                                                                   nrb, rows, stride, l->d_err.as<float>(),

@@ -124,7 +124,8 @@ template <int NCH, int NT, int RB> struct BRow {
   uint32_t r[LaneMap<NCH, NT>::NC];
   int32_t mt[LaneMap<NCH, NT>::NTT];
   int32_t rt[LaneMap<NCH, NT>::NTT];
-  __device__ __forceinline__ void ld(const float *row, const LaneMap<NCH, NT> &mp, int D) {
+  // stl >= 0: this lane's last tail load fetches element stl instead (the row scale; ScaleLane)
+  __device__ __forceinline__ void ld(const float *row, const LaneMap<NCH, NT> &mp, int D, int stl = -1) {
     const int8_t *lo = (const int8_t *)(row + D);
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -133,12 +134,33 @@ template <int NCH, int NT, int RB> struct BRow {
     }
 #pragma unroll
     for (int k = 0; k < NT; k++) {
-      mt[k] = ((const int32_t *)row)[mp.te[k]];
+      mt[k] = ((const int32_t *)row)[k == NT - 1 && stl >= 0 ? stl : mp.te[k]];
       if (RB) rt[k] = lo[mp.te[k]];
     }
   }
 };
 template <int RB> __device__ __forceinline__ float bfp_scale(const float *row, int D) { return row[D + RB * D / 4]; }
+
+// bfp32 rows whose last tail leaves lanes free (D = 300: elements 256..299 on lanes 0..43): the
+// first free lane loads the row scale (float D) with the tail, and the record's scale is a
+// readlane of it — one memory instruction per record less than a separate scale load.
+template <int NCH, int NT, int RB> struct ScaleLane {
+  int lane = -1;  // wave-uniform: the lane carrying the scale, or -1 (separate load)
+  int stl = -1;   // this lane's tail index override
+  __device__ __forceinline__ ScaleLane(int l, int D) {
+    if (RB == 0 && NT > 0) {
+      const int f = D - 256 * NCH - 64 * (NT - 1);
+      if (f >= 0 && f < 64) {
+        lane = f;
+        stl = l == f ? D : -1;
+      }
+    }
+  }
+  __device__ __forceinline__ float scale(const BRow<NCH, NT, RB> &r, const float *row, int D) const {
+    if (NT > 0 && lane >= 0) return __int_as_float(__builtin_amdgcn_readlane(r.mt[NT > 0 ? NT - 1 : 0], lane));
+    return bfp_scale<RB>(row, D);
+  }
+};
 
 // fp64 row accumulator of the forward (neu1, neu1e), stored as a BFP row
 template <int NCH, int NT> struct DAcc {
@@ -377,6 +399,7 @@ __global__ __launch_bounds__(256) void k_gather_b(GatherArgs<float> a, double *_
   const int lane = threadIdx.x & 63;
   const int D = a.D;
   const LaneMap<NCH, NT> m(lane, D);
+  const ScaleLane<NCH, NT, RB> sl(lane, D);
   const uint32_t NI = min(a.multi[0], a.max_items);
   const uint32_t stride = gridDim.x * 4;
   uint32_t qi = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -406,8 +429,8 @@ __global__ __launch_bounds__(256) void k_gather_b(GatherArgs<float> a, double *_
         gg[q] = __int_as_float(idx < 64 ? __builtin_amdgcn_readlane(__float_as_int(ri.g0), (int)idx)
                                         : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
         const float *row = base + (uint64_t)pr * a.ld;
-        rv[q].ld(row, m, D);
-        sc[q] = bfp_scale<RB>(row, D);
+        rv[q].ld(row, m, D, sl.stl);
+        sc[q] = sl.scale(rv[q], row, D);
       }
       if (r0 == 0) rn = item_recs(a, dn, lane);  // next item's record info, behind this item's first rows
 #pragma unroll
@@ -464,13 +487,15 @@ __global__ __launch_bounds__(256) void k_combine_b(GatherArgs<float> a, double *
 // worker cache.  TO_GRADS (sharded learner): the fp64 mean is the push payload
 // [U][h|v] (the reference's wire type), zeros for an empty half; a.gpass as in
 // k_push_thp.
-template <int NCH, int NT, int RB, int UNR, bool TO_GRADS>
-__global__ __launch_bounds__(256) void k_push_b(PushArgs<float, float> a, const double *__restrict__ partial,
-                                                double *__restrict__ grads) {
+// WPE: a minimum of waves per SIMD the register allocation must allow (1 = unconstrained).
+template <int NCH, int NT, int RB, int UNR, bool TO_GRADS, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_push_b(
+    PushArgs<float, float> a, const double *__restrict__ partial, double *__restrict__ grads) {
   constexpr int PU = 4;
   const int lane = threadIdx.x & 63;
   const int D = a.D;
   const LaneMap<NCH, NT> m(lane, D);
+  const ScaleLane<NCH, NT, RB> sl(lane, D);
   const uint64_t n2 = 2ull * a.U;
   const uint64_t stride = (uint64_t)gridDim.x * 4;
   uint64_t uh = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -546,8 +571,8 @@ __global__ __launch_bounds__(256) void k_push_b(PushArgs<float, float> a, const 
           gf[q] = __int_as_float(idx < 64 ? __builtin_amdgcn_readlane(__float_as_int(ri.g0), (int)idx)
                                           : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
           const float *prow = base + (uint64_t)pr * a.ld;
-          rv[q].ld(prow, m, D);
-          sc[q] = bfp_scale<RB>(prow, D);
+          rv[q].ld(prow, m, D, sl.stl);
+          sc[q] = sl.scale(rv[q], prow, D);
         }
         if (r0 == 0) {  // the next item's record info, behind this item's first rows
           if (more) rn = recs_of(hn, nx);

@@ -164,14 +164,16 @@ def test_lr_fast_sums_criteo_shape_close_to_exact(lib, gpu):
 
 @pytest.mark.parametrize("fast", [False, True])
 def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
-    """k_lr_forward_l (a lane per row, the default) == k_lr_forward_r (3 or 2
-    rows per wave, by the batch's longest row) == one row per wave, bit for
-    bit: Criteo-shaped rows (39 features: 3 per wave) and the reference's
-    data.txt (its own row lengths, some longer than one 40-feature chunk)."""
+    """k_lr_forward_r with the ordered sums through LDS (the default: 3 or 2
+    rows per wave by the batch's longest row) == the same with readlane
+    chains == 2 rows per wave == k_lr_forward_l (a lane per row) == one row
+    per wave, bit for bit: Criteo-shaped rows (39 features: 3 per wave), the
+    reference's data.txt (its own row lengths) and ragged rows of 1-130
+    features (longer than one 40-feature chunk; one row per wave past 64)."""
     from swiftmpi_amd.synth import criteo
     y, off, f, v = criteo(9000, seed=5)
     res = []
-    for pack in ("0", "1", "2", "3"):
+    for pack in ("0", "1", "2", "3", "4"):
         monkeypatch.setenv("SWPS_LR_PACK", pack)
         t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
         m = lib.LR(t, minibatch=1000, init_ref=False, fast_sums=fast)
