@@ -88,13 +88,16 @@ __global__ __launch_bounds__(256) void k_lr_forward(const uint64_t *__restrict__
 // feature indices -> weights -> the ordered sum), so R rows per wave put R times the chains
 // in flight per wave slot; the R ordered sums run interleaved.  Same products, same
 // feature-order fp32 sums as k_lr_forward: bit-identical.
-template <int R, bool LDS_SUM = false>
+// SCAT (with LDS_SUM): the forward also writes the batch's gradient records e*x_i into their
+// key-sorted slots (spos, static), the job of k_lr_records — same fp32 products, no second pass
+template <int R, bool LDS_SUM = false, bool SCAT = false>
 __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict__ row_off,
                                                       const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
                                                       const float *__restrict__ label, uint64_t r0, uint64_t nr,
                                                       const float *__restrict__ rows, int stride,
                                                       float *__restrict__ err, float *__restrict__ err2,
-                                                      int diag = 0) {
+                                                      int diag = 0, const uint32_t *__restrict__ spos = nullptr,
+                                                      uint64_t nz0 = 0, float *__restrict__ val = nullptr) {
   constexpr int L = 64 / R;
   const int lane = threadIdx.x & 63;
   const int sub = lane / L, k = lane - sub * L;
@@ -103,12 +106,23 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
   const uint64_t j = wave * R + (uint64_t)sub;
   const bool act = sub < R && j < nr;
   int m = 0;
-  float p0 = 0.f, p1 = 0.f, y = 0.f;
+  float p0 = 0.f, p1 = 0.f, y = 0.f, x0 = 0.f, x1 = 0.f;
+  uint32_t q0 = 0, q1 = 0;
   if (act) {
     const uint64_t r = r0 + j;
     const uint64_t a = row_off[r];
     m = (int)(row_off[r + 1] - a);
     y = label[r];
+    if (SCAT) {
+      if (k < m) {
+        x0 = fval[a + k];
+        q0 = spos[a + k];
+      }
+      if (k + L < m) {
+        x1 = fval[a + k + L];
+        q1 = spos[a + k + L];
+      }
+    }
     if (diag & 1) {  // SWPS_LR_DIAG timing experiment only: no weight gather (w = x)
       if (k < m) p0 = fval[a + k];
       if (k + L < m) p1 = fval[a + k + L];
@@ -140,6 +154,7 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    float error = 0.f;
     if (act && k == 0) {
       float s = 0.f;
       const float4 *r4 = (const float4 *)row;
@@ -151,9 +166,14 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
         if (f4 * 4 + 3 < m) s += v.w;
       }
       const float predict = (float)(1. / (1. + (double)(float)exp((double)(-s))));
-      const float error = y - predict;
+      error = y - predict;
       err[r0 + j] = error;
       err2[r0 + j] = error * error;
+    }
+    if (SCAT) {  // the row's e to its lanes (lane sub*L holds it), then one record per feature
+      const float e = __int_as_float(__builtin_amdgcn_ds_bpermute((sub < R ? sub : 0) * L * 4, __float_as_int(error)));
+      if (act && k < m) val[q0 - nz0] = e * x0;
+      if (act && k + L < m) val[q1 - nz0] = e * x1;
     }
     return;
   }
@@ -258,12 +278,14 @@ __global__ void k_lr_rowid(const uint64_t *__restrict__ row_off, uint64_t nr, ui
 // the records in sorted order: their row and x_i; run heads
 __global__ void k_lr_idx_slots(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ perm, uint64_t n,
                                const uint32_t *__restrict__ rid, const float *__restrict__ fval,
-                               uint32_t *__restrict__ srow, float *__restrict__ sval, uint32_t *__restrict__ head) {
+                               uint32_t *__restrict__ srow, float *__restrict__ sval, uint32_t *__restrict__ head,
+                               uint32_t *__restrict__ spos) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t c = perm[i];
   srow[i] = rid[c];
   sval[i] = fval[c];
+  spos[c] = (uint32_t)i;  // the inverse: feature c's slot in the key-sorted record order
   head[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1u : 0u;
 }
 
@@ -600,7 +622,7 @@ struct swps_lr {
   bool rows_mapped = false;
   // the static per-batch index (lr_index): every batch's records in key-sorted order (row, x_i); the runs
   // (pushed keys) of all batches: vid, start and length relative to the batch; first run and run count per batch
-  DevMem d_srow, d_sval, d_ruk, d_roff, d_rcnt, d_bnruns;
+  DevMem d_srow, d_sval, d_spos, d_ruk, d_roff, d_rcnt, d_bnruns;
   std::vector<uint64_t> brun;
   std::vector<uint64_t> blong;  // [nb+1] offsets of each batch's long runs in d_slong (k_lr_reduce_fused)
   DevMem d_slong;
@@ -609,6 +631,7 @@ struct swps_lr {
   int rows_per_wave = 1;        // SWPS_LR_PACK: 1 = 3 or 2 rows per wave by length, ordered sums through LDS
                                 // (the default; longer rows: one per wave); 3 = the same with readlane chains;
                                 // 2 = at most 2 (readlane); 4 = a lane per row (k_lr_forward_l); 0 = a row per wave
+  int fwd_records = 1;          // SWPS_LR_FWD_RECORDS=0: k_lr_records forms the records instead of the forward
   int fwd_diag = 0;             // SWPS_LR_DIAG: forward timing experiments (1: no weight gather, 2: no ordered chain)
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
@@ -655,6 +678,7 @@ int lr_index(swps_lr *l) {
   DevMem d_bnz0, key, idx, ks, perm, head, rid1, rkey, tmp;
   SWPS_TRY(upload(d_bnz0, bnz0, s));
   SWPS_TRY(l->d_srow.ensure(std::max<uint64_t>(n, 1) * 4));
+  SWPS_TRY(l->d_spos.ensure(std::max<uint64_t>(n, 1) * 4));
   SWPS_TRY(l->d_sval.ensure(std::max<uint64_t>(n, 1) * 4));
   SWPS_TRY(l->d_bnruns.ensure(std::max<uint64_t>(nb, 1) * 4));
   l->brun.assign(nb + 1, 0);
@@ -687,7 +711,7 @@ int lr_index(swps_lr *l) {
   k_lr_rowid<<<nblk(nr), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), nr, rid1.as<uint32_t>());
   k_lr_idx_slots<<<nblk(n), 256, 0, s>>>(ks.as<uint64_t>(), perm.as<uint32_t>(), n, rid1.as<uint32_t>(),
                                           l->d_fval.as<float>(), l->d_srow.as<uint32_t>(), l->d_sval.as<float>(),
-                                          head.as<uint32_t>());
+                                          head.as<uint32_t>(), l->d_spos.as<uint32_t>());
   SWPS_HIP(hipGetLastError());
   SWPS_TRY(lr_scan_incl(head.as<uint32_t>(), rid1.as<uint32_t>(), n, tmp, s));
   uint32_t R = 0;
@@ -790,7 +814,17 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   hipEvent_t e0 = l->timer.begin(s);
   const uint64_t nrb = r1 - r0;
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
-  if (l->rows_per_wave == 1 && mf <= 42)  // 3 rows per wave, the ordered sums through LDS (default)
+  SWPS_TRY(l->d_val_s.ensure(l->max_bnnz * 4));
+  const bool scat = l->fwd_records && l->rows_per_wave == 1 && mf <= 64;  // the forward writes the records
+  if (scat && mf <= 42)  // 3 rows per wave, the ordered sums through LDS, records scattered (default)
+    k_lr_forward_r<3, true, true><<<nblk((nrb + 2) / 3 * 64), 256, 0, s>>>(
+        l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(), l->d_label.as<float>(), r0, nrb, rows, stride,
+        l->d_err.as<float>(), l->d_err2.as<float>(), 0, l->d_spos.as<uint32_t>(), nz0, l->d_val_s.as<float>());
+  else if (scat)
+    k_lr_forward_r<2, true, true><<<nblk((nrb + 1) / 2 * 64), 256, 0, s>>>(
+        l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(), l->d_label.as<float>(), r0, nrb, rows, stride,
+        l->d_err.as<float>(), l->d_err2.as<float>(), 0, l->d_spos.as<uint32_t>(), nz0, l->d_val_s.as<float>());
+  else if (l->rows_per_wave == 1 && mf <= 42)  // the same without the records (k_lr_records forms them)
     k_lr_forward_r<3, true><<<nblk((nrb + 2) / 3 * 64), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), fidx,
                                                                       l->d_fval.as<float>(), l->d_label.as<float>(),
                                                                       r0, nrb, rows, stride, l->d_err.as<float>(),
@@ -826,9 +860,9 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const bool fused = l->cfg.fast_sums && l->fused_reduce && !l->blong.empty();
   if (!fused) SWPS_HIP(hipMemsetAsync(nlong, 0, 4, s));
   const uint64_t q0 = l->brun[bi];
-  SWPS_TRY(l->d_val_s.ensure(l->max_bnnz * 4));
-  k_lr_records<<<nblk(nnz), 256, 0, s>>>(l->d_srow.as<uint32_t>() + nz0, l->d_sval.as<float>() + nz0, nnz,
-                                          l->d_err.as<float>(), l->d_val_s.as<float>());
+  if (!scat)
+    k_lr_records<<<nblk(nnz), 256, 0, s>>>(l->d_srow.as<uint32_t>() + nz0, l->d_sval.as<float>() + nz0, nnz,
+                                            l->d_err.as<float>(), l->d_val_s.as<float>());
   LrReduce ra{l->d_ruk.as<uint32_t>() + q0, l->d_rcnt.as<uint32_t>() + q0, l->d_roff.as<uint32_t>() + q0,
               l->d_bnruns.as<uint32_t>() + bi, l->d_val_s.as<float>(),
               l->sharded ? nullptr : l->d_urow.as<uint32_t>() + q0,
@@ -871,7 +905,8 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   l->s = t->stream;
   l->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
-  if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);       // timing experiments (wrong results)
+  if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);
+  if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;

@@ -156,9 +156,12 @@ template <int NCH, int NT, int RB> struct ScaleLane {
       }
     }
   }
-  __device__ __forceinline__ float scale(const BRow<NCH, NT, RB> &r, const float *row, int D) const {
+  // at load time: the separate scale load when no lane carries it (issued with the row's loads)
+  __device__ __forceinline__ float ld(const float *row, int D) const { return lane >= 0 ? 0.f : bfp_scale<RB>(row, D); }
+  // at use time (after the loads, so the readlane does not stall the next rows' loads)
+  __device__ __forceinline__ float get(const BRow<NCH, NT, RB> &r, float loaded) const {
     if (NT > 0 && lane >= 0) return __int_as_float(__builtin_amdgcn_readlane(r.mt[NT > 0 ? NT - 1 : 0], lane));
-    return bfp_scale<RB>(row, D);
+    return loaded;
   }
 };
 
@@ -430,14 +433,14 @@ __global__ __launch_bounds__(256) void k_gather_b(GatherArgs<float> a, double *_
                                         : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
         const float *row = base + (uint64_t)pr * a.ld;
         rv[q].ld(row, m, D, sl.stl);
-        sc[q] = sl.scale(rv[q], row, D);
+        sc[q] = sl.ld(row, D);
       }
       if (r0 == 0) rn = item_recs(a, dn, lane);  // next item's record info, behind this item's first rows
 #pragma unroll
       for (int q = 0; q < UNR; q++) {
         if (r0 + q < n) {
-          const float g = kind == 0 ? gg[q] : 1.f;
-          acc.axpy(coef_m<RB>(g, sc[q]), g * sc[q], rv[q]);
+          const float g = kind == 0 ? gg[q] : 1.f, u = sl.get(rv[q], sc[q]);
+          acc.axpy(coef_m<RB>(g, u), g * u, rv[q]);
         }
       }
     }
@@ -572,7 +575,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                           : __builtin_amdgcn_readlane(__float_as_int(ri.g1), (int)(idx - 64)));
           const float *prow = base + (uint64_t)pr * a.ld;
           rv[q].ld(prow, m, D, sl.stl);
-          sc[q] = sl.scale(rv[q], prow, D);
+          sc[q] = sl.ld(prow, D);
         }
         if (r0 == 0) {  // the next item's record info, behind this item's first rows
           if (more) rn = recs_of(hn, nx);
@@ -581,8 +584,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int q = 0; q < UNR; q++) {
           if (r0 + q < cnt) {
-            const float g = half == 0 ? gf[q] : 1.f;
-            acc.axpy(coef_m<RB>(g, sc[q]), g * sc[q], rv[q]);
+            const float g = half == 0 ? gf[q] : 1.f, u = sl.get(rv[q], sc[q]);
+            acc.axpy(coef_m<RB>(g, u), g * u, rv[q]);
           }
         }
       }

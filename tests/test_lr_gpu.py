@@ -281,3 +281,32 @@ def test_lr_config3_batches_match_oracle(lib, oracle_mod, gpu, criteo_text, fast
         ref_round = np.abs(f64.astype(np.float64) - ref)  # the reference's own fp32-chain rounding
         assert (np.abs(got.astype(np.float64) - ref) <= ref_round + 1e-5 * np.abs(ref) + atol).all()
     assert np.allclose(e_g, e_o, rtol=1e-5)
+
+
+@pytest.mark.parametrize("fast", [False, True])
+def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, fast):
+    """The forward writing the batch's gradient records e*x_i straight into
+    their static key-sorted slots == k_lr_records forming them after it, bit
+    for bit (Criteo shape: 3 rows per wave; ragged rows up to 60 features: 2
+    per wave)."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(20000, seed=7)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(1, 61, 4000)
+    roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    feat = rng.integers(0, 3000, int(roff[-1])).astype(np.uint32)
+    vals = rng.random(int(roff[-1])).astype(np.float32)
+    yl = (rng.random(4000) < 0.5).astype(np.float32)
+    res = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("SWPS_LR_FWD_RECORDS", on)
+        out = []
+        for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
+            t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+            m = lib.LR(t, minibatch=B, init_ref=False, fast_sums=fast)
+            m.load_csr(*data)
+            m.init()
+            out += [m.train(2), m.params()[1], m.params()[2]]
+        res.append(out)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
