@@ -375,10 +375,21 @@ __device__ __forceinline__ float lr_rec(const LrReduce &a, uint32_t i) { return 
 
 // the batch's gradient records in key-sorted order: e[row]*x_i (fp32 product, = the
 // reference's error * x) from the static sorted (row, x_i); e is L2-resident (4 B per row)
-__global__ void k_lr_records(const uint32_t *__restrict__ srow, const float *__restrict__ sval, uint64_t n,
-                             const float *__restrict__ err, float *__restrict__ val) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) val[i] = err[srow[i]] * sval[i];
+// Four records per thread with 16-B loads and stores: srow / sval / val are indexed by the
+// records' absolute position i (val shifted by nz0 & 3 so that its 16-B groups line up with
+// theirs); [i0, i1) is the batch's range.
+__global__ void k_lr_records(const uint32_t *__restrict__ srow, const float *__restrict__ sval, uint64_t i0,
+                             uint64_t i1, const float *__restrict__ err, float *__restrict__ val) {
+  const uint64_t g = (i0 >> 2) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-B group
+  const uint64_t b = g << 2;
+  if (b >= i1) return;
+  if (b >= i0 && b + 4 <= i1) {
+    const uint4 r = ((const uint4 *)srow)[g];
+    const float4 x = ((const float4 *)sval)[g];
+    ((float4 *)val)[g - (i0 >> 2)] = make_float4(err[r.x] * x.x, err[r.y] * x.y, err[r.z] * x.z, err[r.w] * x.w);
+    return;
+  }
+  for (uint64_t i = max(b, i0); i < min(b + 4, i1); i++) val[i - ((i0 >> 2) << 2)] = err[srow[i]] * sval[i];
 }
 
 __global__ __launch_bounds__(256) void k_lr_reduce_short(LrReduce a) {
@@ -468,6 +479,31 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long(LrReduce a) {
   }
 }
 
+// A thread's fp64 share of a long run: accumulator j gets the thread's elements t + j*256,
+// t + 2048 + j*256, ... in that order (then the tail into accumulator 0); 32 loads in flight
+// while whole groups of 32 remain, then 8 — the same additions in the same order as 8 at a
+// time throughout (bit-identical), with four times the loads in flight on hot runs.
+__device__ __forceinline__ double long_share(const float *__restrict__ val, uint32_t o, uint32_t c, int t) {
+  double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  uint32_t k = t;
+  for (; k + 31 * 256 < c; k += 32 * 256) {
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) v[j] = val[o + k + j * 256];
+#pragma unroll
+    for (int j = 0; j < 32; j++) s8[j & 7] += (double)v[j];
+  }
+  for (; k + 7 * 256 < c; k += 8 * 256) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = val[o + k + j * 256];
+#pragma unroll
+    for (int j = 0; j < 8; j++) s8[j] += (double)v[j];
+  }
+  for (; k < c; k += 256) s8[0] += (double)val[o + k];
+  return ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+}
+
 // fast_sums, long runs (hot features: up to one record per row of the batch):
 // one 256-thread block per run, 8 loads in flight per thread, fp64 partial per
 // thread -> wave sums -> the 4 wave sums added in wave order (fixed order:
@@ -479,17 +515,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long_fast(LrReduce a) {
   for (uint32_t q = blockIdx.x; q < NL; q += gridDim.x) {
     const uint32_t r = a.longs[q];
     const uint32_t o = a.off[r], c = a.cnt[r];
-    double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    uint32_t k = t;
-    for (; k + 7 * 256 < c; k += 8 * 256) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = a.val[o + k + j * 256];
-#pragma unroll
-      for (int j = 0; j < 8; j++) s8[j] += (double)v[j];
-    }
-    for (; k < c; k += 256) s8[0] += (double)a.val[o + k];
-    const double tot = wave_sum_pl(((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7])));
+    const double tot = wave_sum_pl(long_share(a.val, o, c, t));
     if (lane == 0) ws[wv] = tot;
     __syncthreads();
     if (t == 0) lr_apply(a, r, 0.f, c, ((ws[0] + ws[1]) + (ws[2] + ws[3])));
@@ -510,17 +536,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
     for (uint32_t q = blockIdx.x; q < NL; q += LB) {
       const uint32_t r = slong[q];
       const uint32_t o = a.off[r], c = a.cnt[r];
-      double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-      uint32_t k = t;
-      for (; k + 7 * 256 < c; k += 8 * 256) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = a.val[o + k + j * 256];
-#pragma unroll
-        for (int j = 0; j < 8; j++) s8[j] += (double)v[j];
-      }
-      for (; k < c; k += 256) s8[0] += (double)a.val[o + k];
-      const double tot = wave_sum_pl(((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7])));
+      const double tot = wave_sum_pl(long_share(a.val, o, c, t));
       if (lane == 0) ws[wv] = tot;
       __syncthreads();
       if (t == 0) lr_apply(a, r, 0.f, c, ((ws[0] + ws[1]) + (ws[2] + ws[3])));
@@ -631,7 +647,7 @@ struct swps_lr {
   int rows_per_wave = 1;        // SWPS_LR_PACK: 1 = 3 or 2 rows per wave by length, ordered sums through LDS
                                 // (the default; longer rows: one per wave); 3 = the same with readlane chains;
                                 // 2 = at most 2 (readlane); 4 = a lane per row (k_lr_forward_l); 0 = a row per wave
-  int fwd_records = 1;          // SWPS_LR_FWD_RECORDS=0: k_lr_records forms the records instead of the forward
+  int fwd_records = 0;          // SWPS_LR_FWD_RECORDS=1: the forward scatters the records (A/B: 66.6 vs 53.4 us per step, off)
   int fwd_diag = 0;             // SWPS_LR_DIAG: forward timing experiments (1: no weight gather, 2: no ordered chain)
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
@@ -814,7 +830,7 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   hipEvent_t e0 = l->timer.begin(s);
   const uint64_t nrb = r1 - r0;
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
-  SWPS_TRY(l->d_val_s.ensure(l->max_bnnz * 4));
+  SWPS_TRY(l->d_val_s.ensure((l->max_bnnz + 4) * 4));
   const bool scat = l->fwd_records && l->rows_per_wave == 1 && mf <= 64;  // the forward writes the records
   if (scat && mf <= 42)  // 3 rows per wave, the ordered sums through LDS, records scattered (default)
     k_lr_forward_r<3, true, true><<<nblk((nrb + 2) / 3 * 64), 256, 0, s>>>(
@@ -860,11 +876,13 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const bool fused = l->cfg.fast_sums && l->fused_reduce && !l->blong.empty();
   if (!fused) SWPS_HIP(hipMemsetAsync(nlong, 0, 4, s));
   const uint64_t q0 = l->brun[bi];
+  // the batch's records from val_s + (nz0 & 3): their 16-B groups line up with srow / sval's
+  float *val = l->d_val_s.as<float>() + (scat ? 0 : (nz0 & 3));
   if (!scat)
-    k_lr_records<<<nblk(nnz), 256, 0, s>>>(l->d_srow.as<uint32_t>() + nz0, l->d_sval.as<float>() + nz0, nnz,
-                                            l->d_err.as<float>(), l->d_val_s.as<float>());
+    k_lr_records<<<(unsigned)(((nz0 + nnz + 3) / 4 - nz0 / 4 + 255) / 256), 256, 0, s>>>(
+        l->d_srow.as<uint32_t>(), l->d_sval.as<float>(), nz0, nz0 + nnz, l->d_err.as<float>(), val - (nz0 & 3));
   LrReduce ra{l->d_ruk.as<uint32_t>() + q0, l->d_rcnt.as<uint32_t>() + q0, l->d_roff.as<uint32_t>() + q0,
-              l->d_bnruns.as<uint32_t>() + bi, l->d_val_s.as<float>(),
+              l->d_bnruns.as<uint32_t>() + bi, val,
               l->sharded ? nullptr : l->d_urow.as<uint32_t>() + q0,
               l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, l->d_local.as<int32_t>(),
               l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
