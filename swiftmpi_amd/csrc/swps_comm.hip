@@ -356,6 +356,30 @@ int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipS
   return SWPS_OK;
 }
 
+template <typename V>
+__global__ void k_scatter_rows(const V *__restrict__ src, const uint32_t *__restrict__ pos, uint64_t n, uint32_t rv,
+                               V *__restrict__ dst) {
+  // one wave per row, rv V-elements per row
+  const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const V *a = src + i * rv;
+  V *b = dst + (uint64_t)pos[i] * rv;
+  for (uint32_t e = lane; e < rv; e += 64) b[e] = a[e];
+}
+
+int scatter_rows(const void *src, const uint32_t *pos, uint64_t n, uint64_t row_bytes, void *dst, hipStream_t s) {
+  if (!n) return SWPS_OK;
+  const unsigned blocks = (unsigned)((n * 64 + 255) / 256);
+  if (row_bytes % 16 == 0)
+    k_scatter_rows<uint4><<<blocks, 256, 0, s>>>((const uint4 *)src, pos, n, (uint32_t)(row_bytes / 16), (uint4 *)dst);
+  else
+    k_scatter_rows<uint32_t><<<blocks, 256, 0, s>>>((const uint32_t *)src, pos, n, (uint32_t)(row_bytes / 4),
+                                                    (uint32_t *)dst);
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
 // all-to-all-v of device buffers (byte counts per peer, blocks in rank
 // order), ordered on stream s: RCCL send/recv groups, or host staging
 // through `st` and the transport's callback (synchronous)

@@ -17,6 +17,7 @@
 // The same protocol as swiftmpi_amd/dist.py's Python driver.
 #include <algorithm>
 #include <cstdlib>
+#include <memory>
 
 #include "swps_internal.h"
 
@@ -114,6 +115,86 @@ int ShardDriver::setup() {
     SWPS_TRY(rk_cache.ensure(std::max<uint64_t>(rk_off[spe], 1) * 8));
     rk_valid.assign(spe, 0);
   }
+  const char *spl = getenv("SWPS_SPLIT_PULL");
+  split_pull = key_cache && ops.late_mask && ops.set_slot && spe > 1 && !(spl && atoi(spl) == 0);
+  if (split_pull)
+    for (uint64_t st = 0; st < spe; st++) sp.emplace_back(new SplitSlot());
+  return SWPS_OK;
+}
+
+// The early / late partition of slot st's pull, once (its second epoch): the owner flags the keys
+// it serves at st that it also served at st-1 (late), sends the flags back to the requesters,
+// and both sides keep their halves of the slot (keys and counts per peer; value positions).
+int ShardDriver::split_prepare(uint64_t st) {
+  const uint64_t prev = (st + spe - 1) % spe;
+  const uint64_t *sk = &send[st * world], *rk = &recv[st * world];
+  uint64_t n = 0, m = 0;
+  for (int r = 0; r < world; r++) {
+    n += rk[r];
+    m += sk[r];
+  }
+  SWPS_TRY(sync());  // one-time per slot: the buffers below may grow
+  DevMem flags, myflags;
+  SWPS_TRY(flags.ensure(std::max<uint64_t>(n, 1)));
+  SWPS_TRY(myflags.ensure(std::max<uint64_t>(m, 1)));
+  SWPS_TRY(ops.late_mask(ops.h, (int64_t)(3 * st), (int64_t)(3 * prev), flags.as<uint8_t>(), n));
+  SWPS_TRY(exchange(flags.p, rk, myflags.p, sk, 1, S));  // the owners' flags to their requesters
+  std::vector<uint8_t> hf(n), hm(m);
+  std::vector<uint64_t> keys(n);
+  if (n) SWPS_HIP(hipMemcpyAsync(hf.data(), flags.p, n, hipMemcpyDeviceToHost, S));
+  if (n) SWPS_HIP(hipMemcpyAsync(keys.data(), rk_cache.as<uint64_t>() + rk_off[st], n * 8, hipMemcpyDeviceToHost, S));
+  if (m) SWPS_HIP(hipMemcpyAsync(hm.data(), myflags.p, m, hipMemcpyDeviceToHost, S));
+  SWPS_HIP(hipStreamSynchronize(S));
+  SplitSlot &e = *sp[st];
+  e.es.assign(world, 0);
+  e.ls.assign(world, 0);
+  e.ed.assign(world, 0);
+  e.ld.assign(world, 0);
+  std::vector<uint64_t> ek, lk;
+  uint64_t o = 0;
+  for (int r = 0; r < world; r++)  // owner: my served keys, per source
+    for (uint64_t j = 0; j < rk[r]; j++, o++) {
+      if (hf[o]) {
+        lk.push_back(keys[o]);
+        e.ls[r]++;
+      } else {
+        ek.push_back(keys[o]);
+        e.es[r]++;
+      }
+    }
+  std::vector<uint32_t> pe, pl;
+  o = 0;
+  for (int r = 0; r < world; r++)  // requester: my keys at each owner, in my value order
+    for (uint64_t j = 0; j < sk[r]; j++, o++) {
+      if (hm[o]) {
+        pl.push_back((uint32_t)o);
+        e.ld[r]++;
+      } else {
+        pe.push_back((uint32_t)o);
+        e.ed[r]++;
+      }
+    }
+  e.ne = pe.size();
+  e.nl = pl.size();
+  SWPS_TRY(upload(e.ek, ek, S));
+  SWPS_TRY(upload(e.lk, lk, S));
+  SWPS_TRY(upload(e.pe, pe, S));
+  SWPS_TRY(upload(e.pl, pl, S));
+  const uint64_t vb = ops.width * ops.val_bytes;
+  SWPS_TRY(evals.ensure(std::max<uint64_t>(e.ne, 1) * vb));
+  SWPS_TRY(lvals.ensure(std::max<uint64_t>(e.nl, 1) * vb));
+  SWPS_HIP(hipStreamSynchronize(S));
+  e.ready = true;
+  return SWPS_OK;
+}
+
+// slot st's early values: served and exchanged into evals (S)
+int ShardDriver::serve_early(uint64_t st) {
+  SplitSlot &e = *sp[st];
+  const uint64_t vb = ops.width * ops.val_bytes;
+  SWPS_TRY(ops.set_slot(ops.h, (int64_t)(3 * st + 1)));
+  SWPS_TRY(ops.serve_pull(ops.h, e.ek.as<uint64_t>(), e.es.data(), 0, vals.p));
+  SWPS_TRY(exchange(vals.p, e.es.data(), evals.p, e.ed.data(), vb, S));
   return SWPS_OK;
 }
 
@@ -224,9 +305,31 @@ int ShardDriver::steps(uint64_t count) {
       SWPS_TRY(exchange(keys.p, sk, rkp, rk, 8, S));
       if (key_cache) rk_valid[st] = 1;
     }
-    if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, key_cache ? (int64_t)st : -1));
-    SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, vals.p));
-    SWPS_TRY(exchange(vals.p, rk, myvals.p, sk, vb, S));
+    // slot ids of the app's per-slot caches: 3*st the whole key set (pull and push), 3*st + 1 its
+    // early and 3*st + 2 its late part
+    const uint64_t prev = (st + spe - 1) % spe;
+    bool split = false;
+    if (split_pull && kc && rk_valid[prev]) {  // the slot's keys and both slots' row lookups exist
+      if (sp[st]->ready)
+        split = true;
+      else
+        SWPS_TRY(split_prepare(st));  // collective: every rank reaches it at the same step
+    }
+    if (split) {
+      SplitSlot &e = *sp[st];
+      if (!(early_pending && early_slot == st)) SWPS_TRY(serve_early(st));
+      early_pending = false;
+      SWPS_TRY(ops.set_slot(ops.h, (int64_t)(3 * st + 2)));
+      SWPS_TRY(ops.serve_pull(ops.h, e.lk.as<uint64_t>(), e.ls.data(), 0, vals.p));
+      SWPS_TRY(exchange(vals.p, e.ls.data(), lvals.p, e.ld.data(), vb, S));
+      SWPS_TRY(scatter_rows(lvals.p, e.pl.as<uint32_t>(), e.nl, vb, myvals.p, S));
+      SWPS_TRY(scatter_rows(evals.p, e.pe.as<uint32_t>(), e.ne, vb, myvals.p, S));
+      split_steps++;
+    } else {
+      if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, key_cache ? (int64_t)(3 * st) : -1));
+      SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, vals.p));
+      SWPS_TRY(exchange(vals.p, rk, myvals.p, sk, vb, S));
+    }
     SWPS_HIP(hipEventRecord(ev_pull, S));
     // ---- C: learn(i), then prep(i+1) ----
     SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_pull, 0));
@@ -234,6 +337,13 @@ int ShardDriver::steps(uint64_t count) {
     SWPS_HIP(hipEventRecord(ev_learn, ops.cs));
     const uint64_t nxt = (cursor + 1) % spe;
     if (ops.prep && k + 1 < count && nxt < nb) SWPS_TRY(ops.prep(ops.h));
+    // ---- S: the next step's early pull, while this one learns (its rows cannot change at push(i)) ----
+    if (split_pull && k + 1 < count && sp[nxt]->ready && rk_valid[nxt] && rk_valid[st]) {
+      SWPS_TRY(serve_early(nxt));
+      early_pending = true;
+      early_slot = nxt;
+    }
+    if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, key_cache ? (int64_t)(3 * st) : -1));  // push(i)'s keys
     // ---- S: push(i) ----
     // split_grads is the same on every rank (build, environment, world), so every rank issues the
     // same two collectives; eh (the learner ran its two passes) only decides when the first starts

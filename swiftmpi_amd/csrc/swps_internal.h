@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "swps.h"
@@ -215,6 +216,8 @@ int routed_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d
 int check_app_table(swps_table *t);
 // communicator exchanges (swps_comm.hip), ordered on stream s
 int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipStream_t s);
+// dst rows pos[i] = src rows i (row_bytes each, a multiple of 4), ordered on s
+int scatter_rows(const void *src, const uint32_t *pos, uint64_t n, uint64_t row_bytes, void *dst, hipStream_t s);
 int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
                    const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg);
 int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb,
@@ -246,6 +249,9 @@ struct AppOps {
   // optional: after step(), the event (hipEvent_t) recorded once the first half of every owner's
   // keys has its gradients (the rest follow in a second pass), or nullptr: one all-to-all
   void *(*half_event)(void *) = nullptr;
+  // optional: d_flags[j] = 1 when the j-th of the n keys served at slot `cur` (set_slot ids) was
+  // also served at slot `prev`, from the rows cached for both (0: no push of `prev` touches it)
+  int (*late_mask)(void *, int64_t cur, int64_t prev, uint8_t *d_flags, uint64_t n) = nullptr;
 };
 
 struct ShardDriver {
@@ -264,6 +270,27 @@ struct ShardDriver {
   std::vector<char> rk_valid;    // [spe]
   bool key_cache = false;
   bool split_grads = false;  // the gradient all-to-all in two halves (AppOps::half_event)
+  // Early / late pulls (AppOps::late_mask; SWPS_SPLIT_PULL=0 off): of the keys an owner serves at
+  // slot st, those that no rank pulled at slot st-1 receive no push at st-1, so push(st-1) cannot
+  // change their rows: they are served and exchanged while step st-1 learns, and only the rest
+  // waits for push(st-1).  Per slot, from its second epoch on (the key cache and both slots' row
+  // lookups exist by then).  Same values in the same positions: bit-identical to lockstep.
+  struct SplitSlot {
+    bool ready = false;
+    DevMem ek, lk;                // owner: the early / late keys, per source in rank order
+    std::vector<uint64_t> es, ls;  // owner: early / late counts per source (what I send)
+    std::vector<uint64_t> ed, ld;  // requester: early / late counts per owner (what I receive)
+    DevMem pe, pl;                // requester: my values' positions (K order) of the early / late values
+    uint64_t ne = 0, nl = 0;      // requester: totals
+  };
+  bool split_pull = false;
+  std::vector<std::unique_ptr<SplitSlot>> sp;  // [spe]
+  DevMem evals, lvals;  // requester: early values (received while the previous step learns), late values
+  bool early_pending = false;
+  uint64_t early_slot = 0;
+  uint64_t split_steps = 0;  // steps whose pull was split (stats)
+  int split_prepare(uint64_t st);
+  int serve_early(uint64_t st);
   HostStage stage;
   hipStream_t S = nullptr;
   hipEvent_t ev_pull = nullptr, ev_learn = nullptr, ev_x0 = nullptr, ev_x1 = nullptr;

@@ -1904,6 +1904,19 @@ __global__ void k_vid_keys(const int32_t *__restrict__ K, uint64_t n, const uint
   if (i < n) out[i] = vkeys[K[i]];
 }
 
+// owner side of the early / late pull split (AppOps::late_mask): stamp the table rows served
+// at one slot, then flag the rows of another slot that carry the stamp
+__global__ void k_stamp_rows(const uint32_t *__restrict__ rows, uint64_t n, uint32_t cap, uint32_t stamp,
+                             uint32_t *__restrict__ mark) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && rows[i] < cap) mark[rows[i]] = stamp;
+}
+__global__ void k_flag_rows(const uint32_t *__restrict__ rows, uint64_t n, uint32_t cap, uint32_t stamp,
+                            const uint32_t *__restrict__ mark, uint8_t *__restrict__ flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = rows[i] >= cap || mark[rows[i]] == stamp;  // an unknown row: late (safe)
+}
+
 __global__ void k_trace_copy(const int32_t *__restrict__ src, uint64_t n, int32_t *__restrict__ dst) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = src[i];
@@ -2062,6 +2075,8 @@ struct swps_w2v {
   std::vector<uint64_t> icounts;   // [world] init request per owner
   std::vector<int32_t> init_order; // vids grouped by owner
   DevMem d_vkeys, d_init_order, d_serve_rows, d_push_rows;
+  DevMem d_mark;          // late_mask: a stamp per table row
+  uint32_t mark_stamp = 0;
   hipStream_t ss = nullptr;  // serve stream (request / serve_pull / serve_push); nullptr = s
   // the library driver's step slot (AppOps::set_slot): the keys served at a slot are the same every
   // epoch, so their row lookups and the push's grouping sort are kept per slot
@@ -4477,6 +4492,28 @@ int swps_w2v_serve_push(swps_w2v *w, const uint64_t *d_keys, const void *d_grads
   return table_push_sources(w->t, w->d_push_rows.as<uint32_t>(), n, d_grads, ss, g32, nsrc <= 1);
 }
 
+// flags[j] = 1 when the j-th key served at slot `cur` (its cached row lookups) was served at slot
+// `prev` too: a push of slot prev may change its row, so its pull must follow that push
+static int w2v_late_mask(swps_w2v *w, int64_t cur, int64_t prev, uint8_t *d_flags, uint64_t n) {
+  if (cur < 0 || prev < 0 || (uint64_t)cur >= w->slot_rows.size() || (uint64_t)prev >= w->slot_rows.size())
+    return fail(SWPS_E_STATE, "late_mask: slot rows not cached");
+  auto &ec = *w->slot_rows[cur], &ep = *w->slot_rows[prev];
+  if (ec.n != n || (n && !ec.rows.p) || (ep.n && !ep.rows.p)) return fail(SWPS_E_STATE, "late_mask: slot rows not cached");
+  SWPS_HIP(hipSetDevice(w->t->cfg.device));
+  hipStream_t ss = w->ss ? w->ss : w->s;
+  const uint32_t cap = (uint32_t)w->t->cfg.capacity;
+  if (!w->d_mark.p) {
+    SWPS_TRY(w->d_mark.ensure((uint64_t)cap * 4));
+    SWPS_HIP(hipMemsetAsync(w->d_mark.p, 0, (uint64_t)cap * 4, ss));
+  }
+  const uint32_t stamp = ++w->mark_stamp;
+  if (ep.n) k_stamp_rows<<<nblk(ep.n), 256, 0, ss>>>(ep.rows.as<uint32_t>(), ep.n, cap, stamp, w->d_mark.as<uint32_t>());
+  if (n)
+    k_flag_rows<<<nblk(n), 256, 0, ss>>>(ec.rows.as<uint32_t>(), n, cap, stamp, w->d_mark.as<uint32_t>(), d_flags);
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
 int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
   if (!c) return fail(SWPS_E_CFG, "null communicator");
   if (comm_device(c) != w->t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");
@@ -4516,6 +4553,9 @@ int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
   o.set_slot = [](void *h, int64_t slot) {
     ((swps_w2v *)h)->slot = slot;
     return (int)SWPS_OK;
+  };
+  o.late_mask = [](void *h, int64_t cur, int64_t prev, uint8_t *f, uint64_t n) {
+    return w2v_late_mask((swps_w2v *)h, cur, prev, f, n);
   };
   const int rc = d->setup();
   if (rc) {

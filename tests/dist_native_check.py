@@ -70,7 +70,7 @@ def main():
         py = ShardedWord2Vec(ta, frag_num=1000, fp64_intermediates=fp64i, **kw)
         py.load_text(path)
         py.init()
-        steps = 2 * py.steps_per_epoch + 1
+        steps = 3 * py.steps_per_epoch + 2  # the split pull runs from the third epoch on
         py.train_steps(steps)
         py.sync()
         tb = sw.Table("w2v", **tk)

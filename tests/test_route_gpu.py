@@ -154,7 +154,9 @@ def test_native_sharded_driver_equals_python_driver(lib, gpu):
 
 def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path):
     """The library-driven loop over RCCL at world 1 == the unsharded context
-    with the same hash init (the exchange is a self-copy)."""
+    with the same hash init (the exchange is a self-copy), over four epochs:
+    from the third on, every slot's pull is split into the keys the previous
+    slot did not touch (served during the previous step's learn) and the rest."""
     import swiftmpi_amd as sw
     from swiftmpi_amd.comm import Comm
     from conftest import zipf_corpus
@@ -167,13 +169,13 @@ def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path):
     a.shard_comm(comm, frag_num=1000)
     a.init()
     a.exchange_stats(on=1)
-    a.train(2)
+    a.train(4)  # epochs 3-4 pull each slot's keys in an early and a late part
     xs = a.exchange_stats()
     tb = sw.Table("w2v", dim=24, capacity=2048, dtype="f32", init="hash", seed=7)
     b = sw.Word2Vec(tb, init="table", **kw)
     b.load_text(path)
     b.init()
-    b.train(2)
+    b.train(4)
     vk, _ = b.vocab()
     kk = torch.as_tensor(vk.astype(np.int64), device="cuda")
     assert torch.equal(ta.export(kk), tb.export(kk))  # every key lives on the one rank
