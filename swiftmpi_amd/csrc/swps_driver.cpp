@@ -115,8 +115,10 @@ int ShardDriver::setup() {
     SWPS_TRY(rk_cache.ensure(std::max<uint64_t>(rk_off[spe], 1) * 8));
     rk_valid.assign(spe, 0);
   }
+  // on by default at world > 1 (at world 1 the exchange is one local copy: nothing to hide;
+  // same-box A/B at world 1 with an assembly pass: 4.13e8 -> 3.95e8 words/s); SWPS_SPLIT_PULL=0 / 1
   const char *spl = getenv("SWPS_SPLIT_PULL");
-  split_pull = key_cache && ops.late_mask && ops.set_slot && spe > 1 && !(spl && atoi(spl) == 0);
+  split_pull = key_cache && ops.late_mask && ops.set_slot && spe > 1 && (spl ? atoi(spl) != 0 : world > 1);
   if (split_pull)
     for (uint64_t st = 0; st < spe; st++) sp.emplace_back(new SplitSlot());
   return SWPS_OK;
@@ -181,20 +183,23 @@ int ShardDriver::split_prepare(uint64_t st) {
   SWPS_TRY(upload(e.pe, pe, S));
   SWPS_TRY(upload(e.pl, pl, S));
   const uint64_t vb = ops.width * ops.val_bytes;
-  SWPS_TRY(evals.ensure(std::max<uint64_t>(e.ne, 1) * vb));
+  SWPS_TRY(evals[0].ensure(std::max<uint64_t>(e.ne, 1) * vb));
+  SWPS_TRY(evals[1].ensure(std::max<uint64_t>(e.ne, 1) * vb));
   SWPS_TRY(lvals.ensure(std::max<uint64_t>(e.nl, 1) * vb));
   SWPS_HIP(hipStreamSynchronize(S));
   e.ready = true;
   return SWPS_OK;
 }
 
-// slot st's early values: served and exchanged into evals (S)
+// slot st's early values: served and exchanged into evals[ebuf] (S); the buffers alternate
 int ShardDriver::serve_early(uint64_t st) {
   SplitSlot &e = *sp[st];
   const uint64_t vb = ops.width * ops.val_bytes;
   SWPS_TRY(ops.set_slot(ops.h, (int64_t)(3 * st + 1)));
   SWPS_TRY(ops.serve_pull(ops.h, e.ek.as<uint64_t>(), e.es.data(), 0, vals.p));
-  SWPS_TRY(exchange(vals.p, e.es.data(), evals.p, e.ed.data(), vb, S));
+  SWPS_TRY(exchange(vals.p, e.es.data(), evals[ebuf].p, e.ed.data(), vb, S));
+  early_buf = ebuf;
+  ebuf ^= 1;
   return SWPS_OK;
 }
 
@@ -322,8 +327,14 @@ int ShardDriver::steps(uint64_t count) {
       SWPS_TRY(ops.set_slot(ops.h, (int64_t)(3 * st + 2)));
       SWPS_TRY(ops.serve_pull(ops.h, e.lk.as<uint64_t>(), e.ls.data(), 0, vals.p));
       SWPS_TRY(exchange(vals.p, e.ls.data(), lvals.p, e.ld.data(), vb, S));
-      SWPS_TRY(scatter_rows(lvals.p, e.pl.as<uint32_t>(), e.nl, vb, myvals.p, S));
-      SWPS_TRY(scatter_rows(evals.p, e.pe.as<uint32_t>(), e.ne, vb, myvals.p, S));
+      const void *ev = evals[early_buf].p;
+      if (ops.install_parts) {  // the step installs both parts itself (no assembly pass)
+        if (mine && ns)
+          SWPS_TRY(ops.install_parts(ops.h, ev, e.pe.as<uint32_t>(), e.ne, lvals.p, e.pl.as<uint32_t>(), e.nl));
+      } else {
+        SWPS_TRY(scatter_rows(lvals.p, e.pl.as<uint32_t>(), e.nl, vb, myvals.p, S));
+        SWPS_TRY(scatter_rows(ev, e.pe.as<uint32_t>(), e.ne, vb, myvals.p, S));
+      }
       split_steps++;
     } else {
       if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, key_cache ? (int64_t)(3 * st) : -1));

@@ -252,6 +252,10 @@ struct AppOps {
   // optional: d_flags[j] = 1 when the j-th of the n keys served at slot `cur` (set_slot ids) was
   // also served at slot `prev`, from the rows cached for both (0: no push of `prev` touches it)
   int (*late_mask)(void *, int64_t cur, int64_t prev, uint8_t *d_flags, uint64_t n) = nullptr;
+  // optional: the next step() takes its pull values in two parts (value i of part q belongs to the
+  // batch's key pos_q[i]) instead of one array in key order
+  int (*install_parts)(void *, const void *, const uint32_t *, uint64_t, const void *, const uint32_t *,
+                       uint64_t) = nullptr;
 };
 
 struct ShardDriver {
@@ -285,9 +289,13 @@ struct ShardDriver {
   };
   bool split_pull = false;
   std::vector<std::unique_ptr<SplitSlot>> sp;  // [spe]
-  DevMem evals, lvals;  // requester: early values (received while the previous step learns), late values
+  // requester: early values (received while the previous step learns; two buffers, since the
+  // step may still be installing one slot's when the next slot's arrive), late values
+  DevMem evals[2], lvals;
+  int ebuf = 0;  // the buffer serve_early writes next
   bool early_pending = false;
   uint64_t early_slot = 0;
+  int early_buf = 0;
   uint64_t split_steps = 0;  // steps whose pull was split (stats)
   int split_prepare(uint64_t st);
   int serve_early(uint64_t st);

@@ -1898,6 +1898,29 @@ __global__ __launch_bounds__(256) void k_install(const int32_t *__restrict__ K, 
   }
 }
 
+// k_install of a split pull's part (ShardDriver early / late values): value i belongs to the
+// batch's key pos[i] (K order) — the same rows written as by k_install of the assembled values
+template <typename T>
+__global__ __launch_bounds__(256) void k_install_idx(const int32_t *__restrict__ K, const uint32_t *__restrict__ pos,
+                                                     uint32_t n, const T *__restrict__ vals, int D,
+                                                     T *__restrict__ cache_h, T *__restrict__ cache_v, int cs) {
+  using V = typename V16<T>::V;
+  constexpr int E = V16<T>::E;
+  const int lane = threadIdx.x & 63;
+  const int NC = D / E;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += (uint64_t)gridDim.x * 4) {
+    const int32_t vid = K[pos[i]];
+    const V *src = (const V *)(vals + i * 2 * D);
+    V *dh = (V *)(cache_h + (uint64_t)vid * cs);
+    V *dv = (V *)(cache_v + (uint64_t)vid * cs);
+    for (int c = lane; c < cs / E; c += 64) {
+      const bool in = c < NC;
+      dh[c] = in ? src[c] : V{};
+      dv[c] = in ? src[NC + c] : V{};
+    }
+  }
+}
+
 __global__ void k_vid_keys(const int32_t *__restrict__ K, uint64_t n, const uint64_t *__restrict__ vkeys,
                            uint64_t *__restrict__ out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2076,6 +2099,12 @@ struct swps_w2v {
   std::vector<int32_t> init_order; // vids grouped by owner
   DevMem d_vkeys, d_init_order, d_serve_rows, d_push_rows;
   DevMem d_mark;          // late_mask: a stamp per table row
+  // the next step's pull values in two parts (AppOps::install_parts; consumed by that step)
+  struct Parts {
+    const void *vals[2] = {nullptr, nullptr};
+    const uint32_t *pos[2] = {nullptr, nullptr};
+    uint64_t n[2] = {0, 0};
+  } parts;
   uint32_t mark_stamp = 0;
   hipStream_t ss = nullptr;  // serve stream (request / serve_pull / serve_push); nullptr = s
   // the library driver's step slot (AppOps::set_slot): the keys served at a slot are the same every
@@ -3541,8 +3570,17 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
   // reference's pull leaves behind.  Sharded: install the owners' values.
   if (U && d_vals) {
     hipEvent_t e = tm.begin(s);
-    k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
-                                                        w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0, w->cs);
+    if (w->parts.n[0] + w->parts.n[1] == U) {  // a split pull: the early and the late values
+      for (int q = 0; q < 2; q++)
+        if (w->parts.n[q])
+          k_install_idx<T><<<nblk((uint64_t)w->parts.n[q] * 64), 256, 0, s>>>(
+              K, w->parts.pos[q], (uint32_t)w->parts.n[q], (const T *)w->parts.vals[q], D, w->d_cache_h.as<T>(),
+              w->d_cache_v.as<T>(), w->cs);
+    } else {
+      k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
+                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0, w->cs);
+    }
+    w->parts = swps_w2v::Parts{};
     SWPS_HIP(hipGetLastError());
     tm.end(KT_PULL, e, s);
   }
@@ -4556,6 +4594,17 @@ int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
   };
   o.late_mask = [](void *h, int64_t cur, int64_t prev, uint8_t *f, uint64_t n) {
     return w2v_late_mask((swps_w2v *)h, cur, prev, f, n);
+  };
+  o.install_parts = [](void *h, const void *v0, const uint32_t *p0, uint64_t n0, const void *v1, const uint32_t *p1,
+                       uint64_t n1) {
+    auto &q = ((swps_w2v *)h)->parts;
+    q.vals[0] = v0;
+    q.pos[0] = p0;
+    q.n[0] = n0;
+    q.vals[1] = v1;
+    q.pos[1] = p1;
+    q.n[1] = n1;
+    return (int)SWPS_OK;
   };
   const int rc = d->setup();
   if (rc) {
