@@ -115,10 +115,12 @@ int ShardDriver::setup() {
     SWPS_TRY(rk_cache.ensure(std::max<uint64_t>(rk_off[spe], 1) * 8));
     rk_valid.assign(spe, 0);
   }
-  // on by default at world > 1 (at world 1 the exchange is one local copy: nothing to hide;
-  // same-box A/B at world 1 with an assembly pass: 4.13e8 -> 3.95e8 words/s); SWPS_SPLIT_PULL=0 / 1
+  // opt-in (SWPS_SPLIT_PULL=1): forced at world 1 it costs 4.19e8 -> 4.05e8 words/s (same box;
+  // 4.13e8 -> 3.95e8 with an assembly pass instead of the two-part install), and at the bench's
+  // text8 shape only 6.6 % of a minibatch's keys are early, so at N = 8 it would hide ~25 MB of a
+  // 1.1 GB exchange; at config 4's shape (34 % early) it hides ~0.4 GB per step
   const char *spl = getenv("SWPS_SPLIT_PULL");
-  split_pull = key_cache && ops.late_mask && ops.set_slot && spe > 1 && (spl ? atoi(spl) != 0 : world > 1);
+  split_pull = key_cache && ops.late_mask && ops.set_slot && spe > 1 && spl && atoi(spl) != 0;
   if (split_pull)
     for (uint64_t st = 0; st < spe; st++) sp.emplace_back(new SplitSlot());
   return SWPS_OK;

@@ -47,6 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tcp-port", type=int, default=29561)
     a = ap.parse_args()
+    os.environ["SWPS_SPLIT_PULL"] = "1"  # the native driver's early / late pulls (opt-in) from the third epoch
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     import swiftmpi_amd as sw

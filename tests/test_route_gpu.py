@@ -162,7 +162,7 @@ def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path, monkeypatch):
     from conftest import zipf_corpus
     path = zipf_corpus(str(tmp_path / "c.txt"), 120, 300, seed=12)
     kw = dict(window=3, negative=4, minibatch=23, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=False)
-    monkeypatch.setenv("SWPS_SPLIT_PULL", "1")  # on by default at world > 1 only
+    monkeypatch.setenv("SWPS_SPLIT_PULL", "1")  # the early / late pulls (opt-in)
     comm = Comm.rccl(0, 1, port=_port())
     ta = sw.Table("w2v", dim=24, capacity=2048, dtype="f32", init="hash", seed=7)
     a = sw.Word2Vec(ta, init="table", **kw)
