@@ -456,7 +456,8 @@ def main():
                      dp["pushed"] * (10 * es * D + 8))
         sum_ms = push_ms if split else gat_ms + push_ms
     else:
-        sum_kernel = "k_gather_t + k_combine (segmented gradient sums)"
+        sum_kernel = ("k_gather + k_combine" if (parity_main or args.dtype == "f64") else "k_gather_t + k_combine") + \
+            " (segmented gradient sums)"
         gat_bytes = g_rec * (D * ea + 4) + g_items * (D * ea + 16)
         sum_ms = gat_ms
     gat_gbs = gat_bytes / (sum_ms * 1e-3) / 1e9 if sum_ms > 0 else 0.0

@@ -14,6 +14,7 @@
 // Every weight read in a batch belongs to that batch's key set, which the
 // reference pulls at the start of the batch and the server only changes at the
 // push: reading the shard rows directly is the same snapshot, so no copy.
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -607,6 +608,17 @@ struct LTimer {
     (void)hipEventRecord(e, s);
     pending.push_back({k, {b, e}});
   }
+  // events for hipExtLaunchKernelGGL: stamped by the GPU at the kernel's own start / end, so a
+  // short kernel's time does not include the stream's gaps around it (as rocprof measures it)
+  hipEvent_t ext() {
+    if (!on) return nullptr;
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void ext_end(int k, hipEvent_t b, hipEvent_t e) {
+    if (b && e) pending.push_back({k, {b, e}});
+  }
   void resolve() {
     for (auto &q : pending) {
       float t = 0;
@@ -832,7 +844,17 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
   SWPS_TRY(l->d_val_s.ensure((l->max_bnnz + 4) * 4));
   const bool scat = l->fwd_records && l->rows_per_wave == 1 && mf <= 64;  // the forward writes the records
-  if (scat && mf <= 42)  // 3 rows per wave, the ordered sums through LDS, records scattered (default)
+  if (!scat && l->rows_per_wave == 1 && mf <= 42) {  // the default, its own start / end stamps when profiled
+    hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
+    hipExtLaunchKernelGGL(k_lr_forward_r<3, true>, dim3((unsigned)nblk((nrb + 2) / 3 * 64)), dim3(256), 0, s, fb, fe, 0,
+                          (const uint64_t *)l->d_row_off.as<uint64_t>(), fidx, (const float *)l->d_fval.as<float>(),
+                          (const float *)l->d_label.as<float>(), r0, nrb, (const float *)rows, stride,
+                          l->d_err.as<float>(), l->d_err2.as<float>(), 0, (const uint32_t *)nullptr, (uint64_t)0,
+                          (float *)nullptr);
+    l->timer.ext_end(0, fb, fe);
+    if (fb) (void)hipEventDestroy(e0);
+    e0 = nullptr;
+  } else if (scat && mf <= 42)  // 3 rows per wave, the ordered sums through LDS, records scattered (default)
     k_lr_forward_r<3, true, true><<<nblk((nrb + 2) / 3 * 64), 256, 0, s>>>(
         l->d_row_off.as<uint64_t>(), fidx, l->d_fval.as<float>(), l->d_label.as<float>(), r0, nrb, rows, stride,
         l->d_err.as<float>(), l->d_err2.as<float>(), 0, l->d_spos.as<uint32_t>(), nz0, l->d_val_s.as<float>());
@@ -878,9 +900,14 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const uint64_t q0 = l->brun[bi];
   // the batch's records from val_s + (nz0 & 3): their 16-B groups line up with srow / sval's
   float *val = l->d_val_s.as<float>() + (scat ? 0 : (nz0 & 3));
-  if (!scat)
-    k_lr_records<<<(unsigned)(((nz0 + nnz + 3) / 4 - nz0 / 4 + 255) / 256), 256, 0, s>>>(
-        l->d_srow.as<uint32_t>(), l->d_sval.as<float>(), nz0, nz0 + nnz, l->d_err.as<float>(), val - (nz0 & 3));
+  hipEvent_t pb = nullptr;  // the push group's start stamp (the records kernel's start)
+  if (!scat) {
+    pb = l->timer.ext();
+    hipExtLaunchKernelGGL(k_lr_records, dim3((unsigned)(((nz0 + nnz + 3) / 4 - nz0 / 4 + 255) / 256)), dim3(256), 0, s,
+                          pb, (hipEvent_t) nullptr, 0, (const uint32_t *)l->d_srow.as<uint32_t>(),
+                          (const float *)l->d_sval.as<float>(), nz0, nz0 + nnz, (const float *)l->d_err.as<float>(),
+                          val - (nz0 & 3));
+  }
   LrReduce ra{l->d_ruk.as<uint32_t>() + q0, l->d_rcnt.as<uint32_t>() + q0, l->d_roff.as<uint32_t>() + q0,
               l->d_bnruns.as<uint32_t>() + bi, val,
               l->sharded ? nullptr : l->d_urow.as<uint32_t>() + q0,
@@ -890,11 +917,21 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     const uint32_t NL = (uint32_t)(l->blong[bi + 1] - l->blong[bi]);
     const uint32_t LB = std::min<uint32_t>(NL, 2048);
     const unsigned sblocks = (unsigned)std::min<uint64_t>(nblk(nnz), 4096);
+    if (pb) {  // records .. reduce, stamped by the kernels themselves
+      hipEvent_t pe = l->timer.ext();
+      hipExtLaunchKernelGGL(k_lr_reduce_fused, dim3(LB + sblocks), dim3(256), 0, s, (hipEvent_t) nullptr, pe, 0, ra,
+                            (const uint32_t *)(l->d_slong.as<uint32_t>() + l->blong[bi]), NL, LB);
+      SWPS_HIP(hipGetLastError());
+      l->timer.ext_end(3, pb, pe);
+      if (e3) (void)hipEventDestroy(e3);
+      return SWPS_OK;
+    }
     k_lr_reduce_fused<<<LB + sblocks, 256, 0, s>>>(ra, l->d_slong.as<uint32_t>() + l->blong[bi], NL, LB);
     SWPS_HIP(hipGetLastError());
     l->timer.end(3, e3, s);
     return SWPS_OK;
   }
+  if (pb) (void)hipEventDestroy(pb);  // exact mode: the stream events below
   k_lr_reduce_short<<<(unsigned)std::min<uint64_t>(nblk(nnz), 4096), 256, 0, s>>>(ra);
   if (l->cfg.fast_sums)
     k_lr_reduce_long_fast<<<(unsigned)std::min<uint64_t>(nblk(nnz * 256 / kLrShort), 4096), 256, 0, s>>>(ra);
