@@ -374,6 +374,21 @@ __device__ __forceinline__ void lr_apply(const LrReduce &a, uint32_t r, float s,
 
 __device__ __forceinline__ float lr_rec(const LrReduce &a, uint32_t i) { return a.val[i]; }
 
+// A short run's records added in record order (fp64 for fast sums, fp32 for the exact chain),
+// their loads issued 8 at a time instead of one per add: the same additions in the same order.
+template <typename S> __device__ __forceinline__ S short_sum(const float *__restrict__ val, uint32_t o, uint32_t c) {
+  S s = 0;
+  for (uint32_t i = 0; i < c; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = i + j < c ? val[o + i + j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (i + j < c) s += (S)v[j];
+  }
+  return s;
+}
+
 // the batch's gradient records in key-sorted order: e[row]*x_i (fp32 product, = the
 // reference's error * x) from the static sorted (row, x_i); e is L2-resident (4 B per row)
 // Four records per thread with 16-B loads and stores: srow / sval / val are indexed by the
@@ -402,14 +417,10 @@ __global__ __launch_bounds__(256) void k_lr_reduce_short(LrReduce a) {
       continue;
     }
     if (a.fast) {
-      double s = 0;
-      for (uint32_t i = o; i < o + c; i++) s += (double)lr_rec(a, i);
-      lr_apply(a, r, 0.f, c, s);
+      lr_apply(a, r, 0.f, c, short_sum<double>(a.val, o, c));
       continue;
     }
-    float s = 0;
-    for (uint32_t i = o; i < o + c; i++) s += lr_rec(a, i);
-    lr_apply(a, r, s, c);
+    lr_apply(a, r, short_sum<float>(a.val, o, c), c);
   }
 }
 
@@ -549,9 +560,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
   for (uint32_t r = (blockIdx.x - LB) * blockDim.x + t; r < R; r += (gridDim.x - LB) * blockDim.x) {
     const uint32_t o = a.off[r], c = a.cnt[r];
     if (c > kLrShort) continue;  // a long run: the first LB blocks
-    double sum = 0;
-    for (uint32_t i = o; i < o + c; i++) sum += (double)a.val[i];
-    lr_apply(a, r, 0.f, c, sum);
+    lr_apply(a, r, 0.f, c, short_sum<double>(a.val, o, c));
   }
 }
 
