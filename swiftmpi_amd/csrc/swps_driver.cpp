@@ -213,6 +213,13 @@ static std::vector<uint64_t> scaled(const uint64_t *k, int world, uint64_t w) {
 
 int ShardDriver::exchange(const void *d_send, const uint64_t *sk, void *d_recv, const uint64_t *rk, uint64_t w,
                           hipStream_t s) {
+  if (world == 1 && d_send == d_recv) {  // an aliased world-1 exchange: nothing moves
+    if (xprof) {
+      bytes_total += sk[0] * w;
+      calls++;
+    }
+    return SWPS_OK;
+  }
   if (xprof) {
     SWPS_HIP(hipEventRecord(ev_x0, s));
     for (int r = 0; r < world; r++) {
@@ -298,6 +305,11 @@ int ShardDriver::steps(uint64_t count) {
     }
     if (ns > step_keys || nr > step_rkeys) return fail(SWPS_E_STATE, "step larger than the setup's schedule");
     const bool mine = st < nb;
+    // world 1: the owner's values are the learner's and its gradients the owner's, in the same
+    // order — no self-copy (the exchange below sees send == recv); not with the split pull, whose
+    // early serve rewrites vals while the step may still be installing them
+    const bool alias = world == 1 && !split_pull;
+    void *mv = alias ? vals.p : myvals.p, *rg = alias ? grads.p : rgrads.p;
     // ---- S: pull(i) (C's earlier work on these buffers is ordered by events) ----
     SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
     // every rank runs the same steps, so every rank takes the same branch (the exchange is collective)
@@ -341,12 +353,12 @@ int ShardDriver::steps(uint64_t count) {
     } else {
       if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, key_cache ? (int64_t)(3 * st) : -1));
       SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, vals.p));
-      SWPS_TRY(exchange(vals.p, rk, myvals.p, sk, vb, S));
+      SWPS_TRY(exchange(vals.p, rk, mv, sk, vb, S));
     }
     SWPS_HIP(hipEventRecord(ev_pull, S));
     // ---- C: learn(i), then prep(i+1) ----
     SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_pull, 0));
-    if (mine) SWPS_TRY(ops.step(ops.h, ns ? myvals.p : nullptr, ns ? grads.p : nullptr));
+    if (mine) SWPS_TRY(ops.step(ops.h, ns ? mv : nullptr, ns ? grads.p : nullptr));
     SWPS_HIP(hipEventRecord(ev_learn, ops.cs));
     const uint64_t nxt = (cursor + 1) % spe;
     if (ops.prep && k + 1 < count && nxt < nb) SWPS_TRY(ops.prep(ops.h));
@@ -386,9 +398,9 @@ int ShardDriver::steps(uint64_t count) {
       SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S));
     } else {
       SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
-      SWPS_TRY(exchange(grads.p, sk, rgrads.p, rk, gb, S));
+      SWPS_TRY(exchange(grads.p, sk, rg, rk, gb, S));
     }
-    SWPS_TRY(ops.serve_push(ops.h, rkp, rgrads.p, rk));
+    SWPS_TRY(ops.serve_push(ops.h, rkp, rg, rk));
     if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, -1));
     cursor++;
   }

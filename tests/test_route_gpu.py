@@ -152,17 +152,20 @@ def test_native_sharded_driver_equals_python_driver(lib, gpu):
     assert r.returncode == 0 and "NATIVE OK" in r.stdout
 
 
-def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path, monkeypatch):
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path, monkeypatch, split):
     """The library-driven loop over RCCL at world 1 == the unsharded context
-    with the same hash init (the exchange is a self-copy), over four epochs:
-    from the third on, every slot's pull is split into the keys the previous
-    slot did not touch (served during the previous step's learn) and the rest."""
+    with the same hash init, over four epochs: without the split the owner's
+    buffers are the learner's (no self-copy); with it, from the third epoch
+    on, every slot's pull is split into the keys the previous slot did not
+    touch (served during the previous step's learn) and the rest."""
     import swiftmpi_amd as sw
     from swiftmpi_amd.comm import Comm
     from conftest import zipf_corpus
     path = zipf_corpus(str(tmp_path / "c.txt"), 120, 300, seed=12)
     kw = dict(window=3, negative=4, minibatch=23, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=False)
-    monkeypatch.setenv("SWPS_SPLIT_PULL", "1")  # the early / late pulls (opt-in)
+    # split 1: the early / late pulls (opt-in); split 0: world 1's aliased exchange (no self-copy)
+    monkeypatch.setenv("SWPS_SPLIT_PULL", split)
     comm = Comm.rccl(0, 1, port=_port())
     ta = sw.Table("w2v", dim=24, capacity=2048, dtype="f32", init="hash", seed=7)
     a = sw.Word2Vec(ta, init="table", **kw)
