@@ -1,0 +1,60 @@
+"""Host-side measurement tooling (no GPU): scripts/pmc_summary.py's HBM-byte
+arithmetic on synthetic rocprofv3 counter CSVs, and bench.py's lookup of the
+committed summary for a workload."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def _csv(d, rows):
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "run_counter_collection.csv"), "w") as f:
+        f.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n")
+        for r in rows:
+            f.write("%d,\"%s\",%s,%s\n" % r)
+
+
+def test_pmc_summary_read_requests_by_size(tmp_path):
+    k = "void (anonymous namespace)::k_push_b<1, 1, 0, 8, false, 4>((anonymous namespace)::PushArgs<float, float>)"
+    rd, wr, fe = str(tmp_path / "rd"), str(tmp_path / "wr"), str(tmp_path / "fe")
+    rows = []
+    for i in range(3):  # 3 launches; the last 2 are the window
+        rows += [(i, k, "TCC_EA0_RDREQ_32B_sum", 10 * (i + 1)), (i, k, "TCC_EA0_RDREQ_64B_sum", 20 * (i + 1)),
+                 (i, k, "TCC_EA0_RDREQ_128B_sum", 1000 * (i + 1)), (i, k, "TCC_EA0_RDREQ_sum", 1030 * (i + 1))]
+    _csv(rd, rows)
+    _csv(wr, [(i, k, "WRITE_SIZE", 4.0 * (i + 1)) for i in range(3)])
+    _csv(fe, [(i, k, "FETCH_SIZE", 64.0 * (i + 1)) for i in range(3)])
+    out = str(tmp_path / "s.json")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), out, rd, wr, fe, "--last", "2",
+                        "--config", '{"app": "w2v"}'], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    s = json.load(open(out))
+    e = s["kernels"]["k_push_b<1, 1, 0, 8, false, 4>"]
+    # launches 2 and 3 averaged: 32*25 + 64*50 + 128*2500 read, 4*2.5 KiB written
+    assert e["read_bytes"] == 32 * 25 + 64 * 50 + 128 * 2500
+    assert e["write_bytes"] == 10.0 * 1024
+    assert e["hbm_bytes"] == e["read_bytes"] + e["write_bytes"]
+    assert abs(e["fetch_ratio"] - e["read_bytes"] / (160.0 * 1024)) < 1e-12
+    assert s["config"] == {"app": "w2v"}
+
+
+def test_bench_pmc_lookup_matches_config_and_kernel_base_names(tmp_path, monkeypatch):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r03_pmc_x.json").write_text(json.dumps({
+        "config": {"app": "w2v", "mode": "bfp32", "sharded": False},
+        "kernels": {"k_gather_b<1, 1, 0, 8>": {"hbm_bytes": 5.0}, "k_push_b<1, 1, 0, 8, false, 4>": {"hbm_bytes": 7.0},
+                    "k_forward_b<1, 1, 0, 4>": {"hbm_bytes": 11.0}, "k_gather_t<1, 8>": {"hbm_bytes": 100.0}}}))
+    monkeypatch.setattr(b, "ROOT", str(tmp_path))
+    res, src = b.pmc_traffic({"app": "w2v", "mode": "bfp32", "sharded": False},
+                             {"sum": ("k_gather_b", "k_combine_b", "k_push_b"), "forward": ("k_forward_b",)})
+    assert res == {"sum": 12.0, "forward": 11.0} and "r03_pmc_x.json" in src
+    res, src = b.pmc_traffic({"app": "w2v", "mode": "bfp32", "sharded": True}, {"sum": ("k_gather_b",)})
+    assert res == {"sum": None} and src is None  # a sharded line never borrows the unsharded counters
