@@ -796,7 +796,9 @@ def bench_other(args):
     else:
         from swiftmpi_amd.synth import zipf_tokens
         V, D = 1000000, args.dim
-        nd = args.s2v_docs * (steps + warm)  # the profiled pass wraps to the corpus start
+        # a minibatch is the next B + 1 documents (sent2vec.cpp on word2vec.h's MiniBatch): the corpus
+        # is exactly steps + warm of them (the profiled pass wraps to the corpus start)
+        nd = (args.s2v_docs + 1) * (steps + warm)
         rng = np.random.default_rng(5 + rank)
         lens = rng.integers(50, 201, nd)
         off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)

@@ -63,10 +63,10 @@ for L in $LEGS; do
     w2v_fast) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"fast\", \"sharded\": false}" $W2V --precision fast ;;
     lr) leg $L 20 '{"app": "lr", "lr_batch": 65536, "exact": false, "world": 1, "sharded": false}' \
           bench.py --app lr --steps 20 --warmup 3 --no-cpu-baseline ;;
-    # 128 + 32 minibatches of 8192 docs: every docs launch (one per 32 minibatches) the same size,
-    # so rocprof's per-launch average and the profiled pass's describe the same launches
+    # 124 + 31 minibatches of 8193 docs: every docs launch (one per 31 minibatches: 262,144 docs at
+    # most) the same size, so rocprof's per-launch average and the profiled pass's agree
     s2v) leg $L launches '{"app": "s2v", "s2v_docs": 8192, "dim": 300, "world": 1}' \
-           bench.py --app s2v --steps 128 --warmup 32 --no-cpu-baseline ;;
+           bench.py --app s2v --steps 124 --warmup 31 --no-cpu-baseline ;;
     w2v_config4) leg $L 20 "{$W2VCFG, \"tokens\": 125000000, \"vocab\": 1000000, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": false}" \
                    $W2V --tokens 125000000 --vocab 1000000 ;;
     w2v_sharded) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": true}" $W2V --sharded ;;
