@@ -38,6 +38,8 @@
 #include <type_traits>
 #include <unordered_set>
 
+#include <hip/hip_ext.h>
+
 #include "swps_internal.h"
 #include "swps_sort.h"
 #include "swps_wave.h"
@@ -1989,6 +1991,15 @@ struct Timer {
     (void)hipEventRecord(e, s);
     pending.push_back({k, {b, e}});
   }
+  // a pair for hipExtLaunchKernelGGL: stamped by the GPU at the kernels' own start / end (no stream
+  // gaps in the time, as rocprof measures it); ext_end registers it in place of begin / end
+  hipEvent_t ext() { return on ? get() : nullptr; }
+  void ext_end(int k, hipEvent_t b, hipEvent_t e) {
+    if (b && e) pending.push_back({k, {b, e}});
+  }
+  void drop(hipEvent_t e) {  // an event begin() recorded that ext stamps replace
+    if (e) pool.push_back(e);
+  }
   void resolve() {  // caller has synchronized the stream
     for (auto &q : pending) {
       float t = 0;
@@ -3668,12 +3679,21 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     const unsigned cgrid = use_combine(w, pb.M) ? combine_grid(pb.max_items) : 0;  // 0: no second level
     hipEvent_t eg = tm.begin(gs);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
-      if (sp) {
+      if (sp) {  // profiled: the kernels' own start / end stamps
         double *part = w->d_partial.as<double>();
-#define SWPS_F(a_, b_, r_) k_gather_b<a_, b_, r_, 8><<<ggrid, 256, 0, gs>>>(ga, part)
+        hipEvent_t gb = tm.ext(), ge = tm.ext();
+#define SWPS_F(a_, b_, r_)                                                                                         \
+  hipExtLaunchKernelGGL(k_gather_b<a_, b_, r_, 8>, dim3(ggrid), dim3(256), 0, gs, gb, cgrid ? (hipEvent_t) nullptr : ge, \
+                        0, ga, part)
         SWPS_BFP_DISPATCH(w, SWPS_F);
 #undef SWPS_F
-        if (cgrid) k_combine_b<<<cgrid, 256, 0, gs>>>(ga, part);
+        if (cgrid)
+          hipExtLaunchKernelGGL(k_combine_b, dim3(cgrid), dim3(256), 0, gs, (hipEvent_t) nullptr, ge, 0, ga, part);
+        if (gb) {
+          tm.ext_end(KT_GATHER, gb, ge);
+          tm.drop(eg);
+          eg = nullptr;
+        }
         goto gather_done;
       }
       if (w->tail) {
@@ -3733,13 +3753,22 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
           // D = 257..320, bfp32: 134 -> 128 VGPRs (2 spilled) for 4 waves per SIMD; small batches only
           // (same-box A/B: B = 100 2.87e8 -> 3.06e8 words/s, B = 5000 -0.1 %); SWPS_PUSH_WPE=1 / 4 forces
           const bool wpe4 = w->push_wpe == 4 || (w->push_wpe == 0 && U < 65536);
+          hipEvent_t pb = tm.ext(), pe = tm.ext();  // profiled: the kernel's own start / end stamps
           if (wpe4 && w->bfp_rb == 0 && bfp_shape(D) == 11) {
-            k_push_b<1, 1, 0, 8, false, 4><<<pgrid, 256, 0, s>>>(pa, part, nullptr);
-            goto push_done;
-          }
-#define SWPS_F(a_, b_, r_) k_push_b<a_, b_, r_, 8, false><<<pgrid, 256, 0, s>>>(pa, part, nullptr)
-          SWPS_BFP_DISPATCH(w, SWPS_F);
+            hipExtLaunchKernelGGL(k_push_b<1, 1, 0, 8, false, 4>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part,
+                                  (double *)nullptr);
+          } else {
+#define SWPS_F(a_, b_, r_)                                                                                    \
+  hipExtLaunchKernelGGL(k_push_b<a_, b_, r_, 8, false>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part, \
+                        (double *)nullptr)
+            SWPS_BFP_DISPATCH(w, SWPS_F);
 #undef SWPS_F
+          }
+          if (pb) {
+            tm.ext_end(KT_PUSH, pb, pe);
+            tm.drop(ep);
+            ep = nullptr;
+          }
           goto push_done;
         }
 #define SWPS_F(a_, b_, r_) k_push_b<a_, b_, r_, 8, true><<<pgrid, 256, 0, s>>>(pa, part, g64)
