@@ -10,6 +10,31 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+_USED_PORTS = set()
+
+
+def free_port():
+    """A free TCP port on 127.0.0.1 not handed out before in this session and
+    not adjacent to one (the library bootstraps RCCL at MASTER_PORT + 1; two
+    bind-to-0 probes in a row may return the same port)."""
+    import random
+    import socket
+    rng = random.Random()
+    while True:
+        p = rng.randrange(20000, 60000)
+        if p in _USED_PORTS or p + 1 in _USED_PORTS or p - 1 in _USED_PORTS:
+            continue
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+        except OSError:
+            continue
+        finally:
+            s.close()
+        _USED_PORTS.add(p)
+        return p
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libswps.so on cuda:0)")
 

@@ -10,11 +10,8 @@ import pytest
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from conftest import free_port
+    return free_port()
 
 
 def _boot(rank, world, port, q):

@@ -70,12 +70,8 @@ def test_compat_ps_client(compat_bin, gpu, tmp_path):
 
 
 def _free_port():
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from conftest import free_port
+    return free_port()
 
 
 @pytest.mark.gpu

@@ -12,11 +12,8 @@ import torch.multiprocessing as mp
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from conftest import free_port
+    return free_port()
 
 
 def _worker(rank, world, port, q):

@@ -16,11 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from conftest import free_port
+    return free_port()
 
 
 @pytest.mark.parametrize("modes", ["f64,parity", "fast,lr", "fast300", "bfp300"])
