@@ -356,6 +356,9 @@ struct LrReduce {
   float *grads;
   uint32_t *nlong, *longs;
   int fast;  // swps_lr_cfg.fast_sums: fp64 sums (tree-reduced for long runs) instead of the fp32 chain
+  // inline records (k_lr_reduce_fused<true>): e[srow[i]] * sval[i] formed by the reduce itself
+  const uint32_t *srow;  // the batch's sorted (row, x_i), from its first record
+  const float *sval, *err;
 };
 
 // mean = s / count in fp32 (lr.cpp:32-38); fast mode passes the fp64 sum
@@ -516,6 +519,58 @@ __device__ __forceinline__ double long_share(const float *__restrict__ val, uint
   return ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
 }
 
+// The same two sums with the records formed inline (e[srow[i]] * sval[i], the fp32 product
+// k_lr_records stores): the (row, x_i) loads of a batch of records first, then their e gathers
+// (L2-resident), then the additions in the same order — bit-identical, without k_lr_records'
+// write and re-read of every record.
+__device__ __forceinline__ double short_sum_inl(const LrReduce &a, uint32_t o, uint32_t c) {
+  double s = 0;
+  for (uint32_t i = 0; i < c; i += 8) {
+    uint32_t rw[8];
+    float x[8], v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const bool in = i + j < c;
+      rw[j] = in ? a.srow[o + i + j] : 0u;
+      x[j] = in ? a.sval[o + i + j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = i + j < c ? a.err[rw[j]] * x[j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (i + j < c) s += (double)v[j];
+  }
+  return s;
+}
+__device__ __forceinline__ double long_share_inl(const LrReduce &a, uint32_t o, uint32_t c, int t) {
+  double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  uint32_t k = t;
+  for (; k + 31 * 256 < c; k += 32 * 256) {
+    uint32_t rw[32];
+    float x[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      rw[j] = a.srow[o + k + j * 256];
+      x[j] = a.sval[o + k + j * 256];
+    }
+#pragma unroll
+    for (int j = 0; j < 32; j++) s8[j & 7] += (double)(a.err[rw[j]] * x[j]);
+  }
+  for (; k + 7 * 256 < c; k += 8 * 256) {
+    uint32_t rw[8];
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      rw[j] = a.srow[o + k + j * 256];
+      x[j] = a.sval[o + k + j * 256];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) s8[j] += (double)(a.err[rw[j]] * x[j]);
+  }
+  for (; k < c; k += 256) s8[0] += (double)(a.err[a.srow[o + k]] * a.sval[o + k]);
+  return ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+}
+
 // fast_sums, long runs (hot features: up to one record per row of the batch):
 // one 256-thread block per run, 8 loads in flight per thread, fp64 partial per
 // thread -> wave sums -> the 4 wave sums added in wave order (fixed order:
@@ -540,6 +595,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_long_fast(LrReduce a) {
 // (one block per run, as k_lr_reduce_long_fast) while the other blocks take the short runs (a
 // thread per run, as k_lr_reduce_short): no counter reset, no dependency between the two, one
 // launch instead of three.  Same sums in the same order: bit-identical.
+template <bool INL>
 __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint32_t *__restrict__ slong,
                                                          uint32_t NL, uint32_t LB) {
   __shared__ double ws[4];
@@ -548,7 +604,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
     for (uint32_t q = blockIdx.x; q < NL; q += LB) {
       const uint32_t r = slong[q];
       const uint32_t o = a.off[r], c = a.cnt[r];
-      const double tot = wave_sum_pl(long_share(a.val, o, c, t));
+      const double tot = wave_sum_pl(INL ? long_share_inl(a, o, c, t) : long_share(a.val, o, c, t));
       if (lane == 0) ws[wv] = tot;
       __syncthreads();
       if (t == 0) lr_apply(a, r, 0.f, c, ((ws[0] + ws[1]) + (ws[2] + ws[3])));
@@ -560,7 +616,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
   for (uint32_t r = (blockIdx.x - LB) * blockDim.x + t; r < R; r += (gridDim.x - LB) * blockDim.x) {
     const uint32_t o = a.off[r], c = a.cnt[r];
     if (c > kLrShort) continue;  // a long run: the first LB blocks
-    lr_apply(a, r, 0.f, c, short_sum<double>(a.val, o, c));
+    lr_apply(a, r, 0.f, c, INL ? short_sum_inl(a, o, c) : short_sum<double>(a.val, o, c));
   }
 }
 
@@ -668,6 +724,7 @@ struct swps_lr {
   int rows_per_wave = 1;        // SWPS_LR_PACK: 1 = 3 or 2 rows per wave by length, ordered sums through LDS
                                 // (the default; longer rows: one per wave); 3 = the same with readlane chains;
                                 // 2 = at most 2 (readlane); 4 = a lane per row (k_lr_forward_l); 0 = a row per wave
+  int inline_records = 0;       // SWPS_LR_INLINE=1: fast sums form the records inside the reduce (A/B)
   int fwd_records = 0;          // SWPS_LR_FWD_RECORDS=1: the forward scatters the records (A/B: 66.6 vs 53.4 us per step, off)
   int fwd_diag = 0;             // SWPS_LR_DIAG: forward timing experiments (1: no weight gather, 2: no ordered chain)
   uint64_t max_bnnz = 0;
@@ -910,7 +967,8 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   // the batch's records from val_s + (nz0 & 3): their 16-B groups line up with srow / sval's
   float *val = l->d_val_s.as<float>() + (scat ? 0 : (nz0 & 3));
   hipEvent_t pb = nullptr;  // the push group's start stamp (the records kernel's start)
-  if (!scat) {
+  const bool inl = fused && !scat && l->inline_records;  // the reduce forms the records itself
+  if (!scat && !inl) {
     pb = l->timer.ext();
     hipExtLaunchKernelGGL(k_lr_records, dim3((unsigned)(((nz0 + nnz + 3) / 4 - nz0 / 4 + 255) / 256)), dim3(256), 0, s,
                           pb, (hipEvent_t) nullptr, 0, (const uint32_t *)l->d_srow.as<uint32_t>(),
@@ -921,21 +979,31 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
               l->d_bnruns.as<uint32_t>() + bi, val,
               l->sharded ? nullptr : l->d_urow.as<uint32_t>() + q0,
               l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, l->d_local.as<int32_t>(),
-              l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums};
+              l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums,
+              l->d_srow.as<uint32_t>() + nz0, l->d_sval.as<float>() + nz0, l->d_err.as<float>()};
   if (fused) {
     const uint32_t NL = (uint32_t)(l->blong[bi + 1] - l->blong[bi]);
     const uint32_t LB = std::min<uint32_t>(NL, 2048);
     const unsigned sblocks = (unsigned)std::min<uint64_t>(nblk(nnz), 4096);
+    if (inl) {  // one kernel: stamped start and end
+      hipEvent_t rb = l->timer.ext(), re = l->timer.ext();
+      hipExtLaunchKernelGGL(k_lr_reduce_fused<true>, dim3(LB + sblocks), dim3(256), 0, s, rb, re, 0, ra,
+                            (const uint32_t *)(l->d_slong.as<uint32_t>() + l->blong[bi]), NL, LB);
+      SWPS_HIP(hipGetLastError());
+      l->timer.ext_end(3, rb, re);
+      if (e3) (void)hipEventDestroy(e3);
+      return SWPS_OK;
+    }
     if (pb) {  // records .. reduce, stamped by the kernels themselves
       hipEvent_t pe = l->timer.ext();
-      hipExtLaunchKernelGGL(k_lr_reduce_fused, dim3(LB + sblocks), dim3(256), 0, s, (hipEvent_t) nullptr, pe, 0, ra,
-                            (const uint32_t *)(l->d_slong.as<uint32_t>() + l->blong[bi]), NL, LB);
+      hipExtLaunchKernelGGL(k_lr_reduce_fused<false>, dim3(LB + sblocks), dim3(256), 0, s, (hipEvent_t) nullptr, pe, 0,
+                            ra, (const uint32_t *)(l->d_slong.as<uint32_t>() + l->blong[bi]), NL, LB);
       SWPS_HIP(hipGetLastError());
       l->timer.ext_end(3, pb, pe);
       if (e3) (void)hipEventDestroy(e3);
       return SWPS_OK;
     }
-    k_lr_reduce_fused<<<LB + sblocks, 256, 0, s>>>(ra, l->d_slong.as<uint32_t>() + l->blong[bi], NL, LB);
+    k_lr_reduce_fused<false><<<LB + sblocks, 256, 0, s>>>(ra, l->d_slong.as<uint32_t>() + l->blong[bi], NL, LB);
     SWPS_HIP(hipGetLastError());
     l->timer.end(3, e3, s);
     return SWPS_OK;
@@ -970,7 +1038,8 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   l->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);
-  if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests       // timing experiments (wrong results)
+  if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests
+  if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;

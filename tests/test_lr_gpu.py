@@ -283,12 +283,14 @@ def test_lr_config3_batches_match_oracle(lib, oracle_mod, gpu, criteo_text, fast
     assert np.allclose(e_g, e_o, rtol=1e-5)
 
 
-@pytest.mark.parametrize("fast", [False, True])
-def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, fast):
-    """The forward writing the batch's gradient records e*x_i straight into
-    their static key-sorted slots == k_lr_records forming them after it, bit
-    for bit (Criteo shape: 3 rows per wave; ragged rows up to 60 features: 2
-    per wave)."""
+@pytest.mark.parametrize("env,fast", [("SWPS_LR_FWD_RECORDS", False), ("SWPS_LR_FWD_RECORDS", True),
+                                      ("SWPS_LR_INLINE", True)])
+def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, env, fast):
+    """Where the batch's gradient records e*x_i are formed — by k_lr_records
+    after the forward (default), by the forward straight into their static
+    key-sorted slots (SWPS_LR_FWD_RECORDS), or inside the fused fast-sums
+    reduce (SWPS_LR_INLINE) — does not change a bit (Criteo shape: 3 rows per
+    wave, hot long runs; ragged rows up to 60 features: 2 per wave)."""
     from swiftmpi_amd.synth import criteo
     y, off, f, v = criteo(20000, seed=7)
     rng = np.random.default_rng(4)
@@ -299,7 +301,7 @@ def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, fast):
     yl = (rng.random(4000) < 0.5).astype(np.float32)
     res = []
     for on in ("0", "1"):
-        monkeypatch.setenv("SWPS_LR_FWD_RECORDS", on)
+        monkeypatch.setenv(env, on)
         out = []
         for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
             t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
