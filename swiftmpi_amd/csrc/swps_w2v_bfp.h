@@ -217,15 +217,17 @@ template <int NCH, int NT> struct DAcc {
   template <int RB>
   __device__ __forceinline__ void st_bfp(float *row, const LaneMap<NCH, NT> &m, int D, int ld, int lane) const {
     constexpr int MB = 31 + 8 * RB;  // bits below 2^e kept
-    uint32_t eb = 0;                 // the largest biased fp64 exponent of this lane's live elements
+    // the largest biased fp64 exponent of this lane's live elements = that of their largest |x|
+    double amax = 0.0;
 #pragma unroll
     for (int c = 0; c < NCH; c++)
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        if (m.ca(c)) eb = max(eb, (uint32_t)(__double2hiint(v[c][k]) >> 20) & 0x7FFu);
+        if (m.ca(c)) amax = fmax(amax, fabs(v[c][k]));
 #pragma unroll
     for (int k = 0; k < NT; k++)
-      if (m.ta(k)) eb = max(eb, (uint32_t)(__double2hiint(t[k]) >> 20) & 0x7FFu);
+      if (m.ta(k)) amax = fmax(amax, fabs(t[k]));
+    const uint32_t eb = (uint32_t)(__double2hiint(amax) >> 20) & 0x7FFu;
     // max|x| < 2^e with e = biased - 1022; keep the scale a normal fp32 (tiny rows: fewer bits, never wrong)
     const int e = max((int)wave_max_i32((int)eb) - 1022, MB - 126);
     const double im = pow2d(31 - e), ir = pow2d(MB - e), hm = pow2d(e - 31);
