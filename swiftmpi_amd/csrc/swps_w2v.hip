@@ -3611,6 +3611,10 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     hipEvent_t ef = tm.begin(s);
     if constexpr (std::is_same<T, float>::value && std::is_same<A, float>::value) {
       if (w->bfp) {
+        if (w->fwd_g == 8 && w->bfp_rb == 0 && bfp_shape(D) == 11) {  // A/B: 8 rows in flight (SWPS_FWD_G=8)
+          k_forward_b<1, 1, 0, 8><<<nblk(P * 64), 256, 0, s>>>(fa);
+          goto forward_done;
+        }
 #define SWPS_F(a_, b_, r_) k_forward_b<a_, b_, r_, 4><<<nblk(P * 64), 256, 0, s>>>(fa)
         SWPS_BFP_DISPATCH(w, SWPS_F);
 #undef SWPS_F
