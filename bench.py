@@ -33,6 +33,25 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 XGMI_PEAK_GBS = 7 * 153.0  # per GPU: 7 xGMI links x ~153 GB/s
 
 
+def lr_tile_pieces(f, off, r0, r1, tile_bits=12, chunk=2048):
+    """The LR row-tile path's pieces and partials for batch rows [r0, r1): records ordered by
+    (tile, key) (stable: row order inside), cut into blocks of `chunk` records per tile; a piece
+    is a key's records inside one block, a partial a piece of a key with several
+    (swps_lr.hip lr_tile_index)."""
+    n = np.diff(off[r0:r1 + 1].astype(np.int64))
+    tile = np.repeat((np.arange(r1 - r0) >> tile_bits), n)
+    feat = f[off[r0]:off[r1]].astype(np.int64)
+    o = np.lexsort((feat, tile))
+    t, k = tile[o], feat[o]
+    start = np.searchsorted(t, t, side="left")  # each tile's first sorted position
+    blk = (np.arange(len(t)) - start) // chunk
+    head = np.ones(len(t), dtype=bool)
+    head[1:] = (t[1:] != t[:-1]) | (blk[1:] != blk[:-1]) | (k[1:] != k[:-1])
+    pk = k[head]
+    _, inv, cnt = np.unique(pk, return_inverse=True, return_counts=True)
+    return int(head.sum()), int((cnt[inv] > 1).sum())
+
+
 def pmc_traffic(config, groups):
     """HBM bytes per launch of kernel groups (one launch of each kernel per
     step), from the committed PMC summary of this exact workload
@@ -747,14 +766,25 @@ def bench_other(args):
                    for k in range(steps))
         fwd_ms, fwd_n = kt["forward"]
         fwd_bytes = 12 * nnz + 20 * (r1 - r0)
+        tiles = not args.lr_exact and os.environ.get("SWPS_LR_TILES", "1") != "0"
         fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
         push_ms, push_n = kt.get("push", (0.0, 0))
-        push_bytes = 20 * nnz + 32 * uniq
+        if tiles:  # row tiles: per feature its (row, x_i) (6 B); per piece its run and slot (8 B), per
+            # partial its fp64 write + read (16 B); per unique key its run (16 B) + the row RMW (16 B)
+            pieces = partials = 0
+            for k in range(steps):
+                pc, pa = lr_tile_pieces(f, off, (warm + steps + k) * B1, (warm + steps + k + 1) * B1)
+                pieces += pc
+                partials += pa
+            push_bytes = 6 * nnz + 8 * pieces + 16 * partials + 32 * uniq
+        else:
+            push_bytes = 20 * nnz + 32 * uniq
         push_gbs = push_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
         step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
         kf = {"kernel": "k_lr_forward", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
               "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
         kp = {"kernel": ("k_lr_records + k_lr_reduce_short + k_lr_reduce_long" if args.lr_exact
+                         else "k_lr_tiles + k_lr_tiles_fin" if tiles
                          else "k_lr_records + k_lr_reduce_fused") + " (per-key mean + AdaGrad push)",
               "achieved": push_gbs, "frac": push_gbs / HBM_PEAK_GBS,
               "bytes_per_launch": push_bytes / max(push_n, 1), "avg_launch_ms": push_ms / max(push_n, 1),
@@ -763,7 +793,7 @@ def bench_other(args):
                                     sharded=dist is not None),
                                {"forward": ("k_lr_forward_r", "k_lr_forward"),
                                 "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
-                                         "k_lr_reduce_long_fast")})
+                                         "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin")})
         for kd, name in ((kf, "forward"), (kp, "push")):
             kd["traffic"] = tr[name]
             kd["traffic_source"] = tsrc
@@ -782,7 +812,8 @@ def bench_other(args):
                                           % (world, backend, ", library-issued" if comm is not None else ""))
                           if dist is not None else "1 GPU, one HBM shard",
                           "mode": "exact (sequential fp32 per-key sums, bit-exact with the reference)" if args.lr_exact
-                          else "fast (fp64 per-key sums, wave tree-reduced; within 1e-5 of the oracle)",
+                          else "fast (fp64 per-key sums%s; within 1e-5 of the oracle)"
+                          % (" through row tiles" if tiles else ", wave tree-reduced"),
                           "features_per_s": total * nnz / max(r1 - r0, 1) / dt,
                           "unique_keys_per_step": uniq / steps},
                "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",

@@ -398,12 +398,16 @@ template <typename S> __device__ __forceinline__ S short_sum(const float *__rest
 // records' absolute position i (val shifted by nz0 & 3 so that its 16-B groups line up with
 // theirs); [i0, i1) is the batch's range.
 __global__ void k_lr_records(const uint32_t *__restrict__ srow, const float *__restrict__ sval, uint64_t i0,
-                             uint64_t i1, const float *__restrict__ err, float *__restrict__ val) {
+                             uint64_t i1, const float *__restrict__ err, float *__restrict__ val, int diag = 0) {
   const uint64_t g = (i0 >> 2) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-B group
   const uint64_t b = g << 2;
   if (b >= i1) return;
   if (b >= i0 && b + 4 <= i1) {
-    const uint4 r = ((const uint4 *)srow)[g];
+    uint4 r = ((const uint4 *)srow)[g];
+    if (diag & 4) {  // SWPS_LR_DIAG timing experiment only: coalesced e reads instead of the gathers
+      const uint32_t c = (uint32_t)(b - i0) & 0xFFFCu;
+      r = make_uint4(c + (r.x >> 31), c + 1, c + 2, c + 3);  // bench batches (>= 65,536 rows) only
+    }
     const float4 x = ((const float4 *)sval)[g];
     ((float4 *)val)[g - (i0 >> 2)] = make_float4(err[r.x] * x.x, err[r.y] * x.y, err[r.z] * x.z, err[r.w] * x.w);
     return;
@@ -620,6 +624,367 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
   }
 }
 
+// ---- fast sums through row tiles (k_lr_tiles + k_lr_tiles_fin) --------------------------
+// The record path's cost is its e gathers (e[row] for every record of the batch, rows in
+// random order within a key's run): 2.56M divergent 4-B reads per Criteo batch.  Cut the batch
+// into tiles of 2^tb rows: the static index orders each batch's records by (tile, key), so a
+// block loads its tile's slice of e into LDS once and reads every record's e from LDS.  A block
+// takes 2,048 consecutive records of one tile (8 per thread, coalesced) and sums each key's
+// records with one block-wide segmented scan; a piece = a key's records inside one block.  A key
+// with a single piece is applied by k_lr_tiles itself; the others get one fp64 partial per piece,
+// added in (tile, record) order by k_lr_tiles_fin.  Same fp32 products e*x_i as the record path,
+// fp64 sums in a fixed order: deterministic, within fp64 rounding of k_lr_reduce_fused.
+constexpr int kTileMaxBits = 12;         // LDS slice: 4,096 rows (16 KB)
+constexpr uint32_t kTileChunk = 2048;    // records per block
+constexpr uint16_t kTileHead = 0x8000;   // trow bit: the record starts a (tile, key) run
+
+struct LrTiles {
+  const uint16_t *trow;   // record's row within its tile | kTileHead
+  const float *tval;      // record's x_i
+  const uint32_t *chunk;  // per block: tile, first record, end record, first piece, end piece
+  const uint32_t *tinfo;  // per piece: run (batch-relative) | 1u << 31 when the run is this one piece
+  const uint32_t *tdst;   // per piece: its partial's slot (batch-relative), or for a whole run on a
+                          // single GPU its key's shard row
+  double *part;
+  const float *err;
+  uint64_t r0, nrb;
+  int tb;
+};
+
+// segmented-sum scan element (a head seen, open run's sum, heads, last head's record):
+// (fp, vp, cp, hp) precedes (f, v, c, h)
+__device__ __forceinline__ void seg_after(bool fp, double vp, int cp, uint32_t hp, bool &f, double &v, int &c,
+                                          uint32_t &h) {
+  if (!f) v = vp + v;
+  f = f || fp;
+  c += cp;
+  h = max(h, hp);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_lr_tiles(LrReduce a, LrTiles t) {
+  __shared__ float es[1 << kTileMaxBits];
+  __shared__ double wv[4];
+  __shared__ int wf[4], wc[4];
+  __shared__ uint32_t wh[4];
+  const uint32_t *ch = t.chunk + (uint64_t)blockIdx.x * 5;
+  const uint32_t tile = ch[0], rec0 = ch[1], rec1 = ch[2], piece0 = ch[3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t i0 = rec0 + (uint32_t)tid * 8;
+  const int n = i0 < rec1 ? (int)min(8u, rec1 - i0) : 0;
+  uint32_t rw[9];
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    rw[j] = j < n ? t.trow[i0 + j] : 0u;
+    x[j] = j < n ? t.tval[i0 + j] : 0.f;
+  }
+  rw[8] = n == 8 && i0 + 8 < rec1 ? t.trow[i0 + 8] : kTileHead;  // the next record: a head ends this thread's last run
+  const uint64_t e0 = (uint64_t)tile << t.tb;
+  const uint32_t ne = (uint32_t)min<uint64_t>(1ull << t.tb, t.nrb - e0);
+  {  // the tile's slice of e: every load in flight, then the LDS stores
+    constexpr int KE = (1 << kTileMaxBits) / 256;
+    float ev[KE];
+#pragma unroll
+    for (int k = 0; k < KE; k++) {
+      const uint32_t i = tid + k * 256;
+      ev[k] = i < ne ? t.err[t.r0 + e0 + i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KE; k++) {
+      const uint32_t i = tid + k * 256;
+      if (i < ne) es[i] = ev[k];
+    }
+  }
+  __syncthreads();
+  double pr[8];
+  bool any = false;
+  double pre = 0, cur = 0;
+  int nh = 0;
+  uint32_t lh = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    pr[j] = j < n ? (double)(es[rw[j] & (kTileHead - 1)] * x[j]) : 0.0;
+    const bool h = j < n && ((rw[j] & kTileHead) || i0 + j == rec0);
+    if (h) {
+      any = true;
+      nh++;
+      lh = i0 + j;
+      cur = pr[j];
+    } else if (j < n) {
+      if (any)
+        cur += pr[j];
+      else
+        pre += pr[j];
+    }
+  }
+  // block-wide exclusive segmented scan: the sum of this thread's open run before its first
+  // record, the heads before it and the last one's record
+  bool f = any;
+  double v = any ? cur : pre;
+  int c = nh;
+  uint32_t hh = lh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double vp = __shfl_up(v, o);
+    const int fp = __shfl_up((int)f, o), cp = __shfl_up(c, o);
+    const uint32_t hp = __shfl_up(hh, o);
+    if (lane >= o) seg_after(fp != 0, vp, cp, hp, f, v, c, hh);
+  }
+  if (lane == 63) {
+    wv[w] = v;
+    wf[w] = f;
+    wc[w] = c;
+    wh[w] = hh;
+  }
+  double ve = __shfl_up(v, 1);
+  int fe = __shfl_up((int)f, 1), ce = __shfl_up(c, 1);
+  uint32_t he = __shfl_up(hh, 1);
+  if (lane == 0) {
+    ve = 0;
+    fe = 0;
+    ce = 0;
+    he = 0;
+  }
+  __syncthreads();
+  bool fw = false;
+  double vw = 0;
+  int cw = 0;
+  uint32_t hw = 0;
+  for (int k = 0; k < w; k++) {
+    bool fk = wf[k] != 0;
+    double vk = wv[k];
+    int ck = wc[k];
+    uint32_t hk = wh[k];
+    seg_after(fw, vw, cw, hw, fk, vk, ck, hk);
+    fw = fk;
+    vw = vk;
+    cw = ck;
+    hw = hk;
+  }
+  bool fx = fe != 0;
+  double run = ve;
+  int cx = ce;
+  uint32_t hs = he;
+  seg_after(fw, vw, cw, hw, fx, run, cx, hs);
+  // this thread's pieces that end here, in record order: (piece, sum, record count)
+  uint32_t p = (uint32_t)cx - 1;  // block-local index of the piece open before this thread's first record
+  uint32_t pj[8], cj[8];
+  double sj[8];
+  bool ej[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const bool h = (rw[j] & kTileHead) || i0 + j == rec0;
+    if (h) {
+      p++;
+      hs = i0 + j;
+      run = pr[j];
+    } else {
+      run = run + pr[j];
+    }
+    ej[j] = j < n && (j + 1 < n ? (rw[j + 1] & kTileHead) != 0 : (n < 8 || (rw[8] & kTileHead) != 0));
+    pj[j] = p;
+    cj[j] = i0 + j - hs + 1;
+    sj[j] = run;
+  }
+  // a piece that is its key's whole run: the mean and AdaGrad; else its partial.  Every stage's
+  // loads in flight together (a piece end at a time would chain the round trips: vmcnt orders
+  // them behind the stores)
+  uint32_t info[8], dst[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    info[j] = ej[j] ? t.tinfo[piece0 + pj[j]] : 0u;
+    dst[j] = ej[j] ? t.tdst[piece0 + pj[j]] : 0u;
+  }
+  if (a.grads) {  // sharded: the mean into the push request at local[vid]
+    uint32_t u[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) u[j] = ej[j] && (info[j] >> 31) ? a.uniq[info[j] & 0x7FFFFFFFu] : 0u;
+    int32_t lo[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) lo[j] = ej[j] && (info[j] >> 31) ? a.local[u[j]] : 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (!ej[j]) continue;
+      if (info[j] >> 31)
+        a.grads[lo[j]] = (float)(sj[j] / (double)cj[j]);
+      else
+        t.part[dst[j]] = sj[j];
+    }
+    return;
+  }
+  float w0[8], g0[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const bool one = ej[j] && (info[j] >> 31);
+    w0[j] = one ? a.rows[(uint64_t)dst[j] * 2] : 0.f;
+    g0[j] = one ? a.rows[(uint64_t)dst[j] * 2 + 1] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    if (!ej[j]) continue;
+    if (info[j] >> 31) {  // lr_apply's AdaGrad step (lr.cpp:68-75) on the shard row
+      const float m = (float)(sj[j] / (double)cj[j]);
+      const float g2 = g0[j] + m * m;
+      const float step = a.lr * m;
+      float *row = a.rows + (uint64_t)dst[j] * 2;
+      row[1] = g2;
+      row[0] = w0[j] + step / sqrtf(g2 + a.fudge);
+    } else {
+      t.part[dst[j]] = sj[j];
+    }
+  }
+}
+
+// keys with several partials, from static per-key records {first slot, partials, records,
+// run (global)} (+ the run's shard row on a single GPU, so the row loads go out with the partial
+// loads): the first LB blocks take the keys with more than kTileFinShort partials (a wave each:
+// lane-strided fp64 adds, then the fixed-order wave sum), the rest a thread per key (its
+// partials added in slot order); then the mean and AdaGrad
+constexpr uint32_t kTileFinShort = 16;
+__device__ __forceinline__ void fin_apply(const LrReduce &a, uint4 rc, uint32_t row, float w, float g, double s,
+                                          uint64_t q0) {
+  const float m = (float)(s / (double)rc.z);
+  if (a.grads) {
+    a.grads[a.local[a.uniq[rc.w - q0]]] = m;
+    return;
+  }
+  const float g2 = g + m * m;
+  const float step = a.lr * m;
+  float *r = a.rows + (uint64_t)row * 2;
+  r[1] = g2;
+  r[0] = w + step / sqrtf(g2 + a.fudge);
+}
+__global__ __launch_bounds__(256) void k_lr_tiles_fin(LrReduce a, const uint4 *__restrict__ ms,
+                                                      const uint32_t *__restrict__ msrow, uint32_t ns,
+                                                      const uint4 *__restrict__ ml, const uint32_t *__restrict__ mlrow,
+                                                      uint32_t nl, uint32_t LB, const double *__restrict__ part,
+                                                      uint64_t q0) {
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x < LB) {
+    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nl; q += LB * 4) {
+      const uint4 rc = ml[q];
+      const uint32_t row = a.grads ? 0u : mlrow[q];
+      double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint32_t k = lane;
+      for (; k + 7 * 64 < rc.y; k += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = part[rc.x + k + j * 64];
+#pragma unroll
+        for (int j = 0; j < 8; j++) s8[j] += v[j];
+      }
+      for (; k < rc.y; k += 64) s8[0] += part[rc.x + k];
+      const double tot = wave_sum_pl(((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7])));
+      if (lane == 0)
+        fin_apply(a, rc, row, a.grads ? 0.f : a.rows[(uint64_t)row * 2], a.grads ? 0.f : a.rows[(uint64_t)row * 2 + 1],
+                  tot, q0);
+    }
+    return;
+  }
+  const uint32_t q = (blockIdx.x - LB) * blockDim.x + threadIdx.x;
+  if (q >= ns) return;
+  const uint4 rc = ms[q];
+  const uint32_t row = a.grads ? 0u : msrow[q];
+  double v[kTileFinShort];
+#pragma unroll
+  for (int j = 0; j < (int)kTileFinShort; j++) v[j] = (uint32_t)j < rc.y ? part[rc.x + j] : 0.0;
+  const float w = a.grads ? 0.f : a.rows[(uint64_t)row * 2], g = a.grads ? 0.f : a.rows[(uint64_t)row * 2 + 1];
+  double s = 0;
+#pragma unroll
+  for (int j = 0; j < (int)kTileFinShort; j++)
+    if ((uint32_t)j < rc.y) s += v[j];
+  fin_apply(a, rc, row, w, g, s, q0);
+}
+
+// ---- the tile index (built at load with the record index; fast sums) ----
+__global__ void k_lr_tile_keys(const uint64_t *__restrict__ row_off, uint64_t nr, uint64_t B1, int tb, int tbits,
+                               const int32_t *__restrict__ fvid, uint64_t *__restrict__ key, uint32_t *__restrict__ idx) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nr) return;
+  const uint64_t b = r / B1, tile = (r - b * B1) >> tb;
+  for (uint64_t c = row_off[r]; c < row_off[r + 1]; c++) {
+    key[c] = (b << (32 + tbits)) | (tile << 32) | (uint32_t)fvid[c];
+    idx[c] = (uint32_t)c;
+  }
+}
+
+// records in (batch, tile, key) order: row within the tile (+ the run-head bit), x_i, piece heads
+__global__ void k_lr_tile_slots(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ perm, uint64_t n,
+                                const uint32_t *__restrict__ rid, uint64_t B1, int tb, const float *__restrict__ fval,
+                                uint16_t *__restrict__ trow, float *__restrict__ tval, uint32_t *__restrict__ head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = perm[i];
+  const bool h = i == 0 || ks[i] != ks[i - 1];
+  trow[i] = (uint16_t)(((rid[c] % B1) & ((1u << tb) - 1)) | (h ? kTileHead : 0));
+  tval[i] = fval[c];
+  head[i] = h ? 1u : 0u;
+}
+__global__ void k_lr_tile_cuts(const uint32_t *__restrict__ cut, uint64_t nc, uint32_t *__restrict__ head) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nc) head[cut[q]] = 1u;
+}
+// pieces: first record and (batch, key); chunk -> its first piece
+__global__ void k_lr_tile_pieces(const uint64_t *__restrict__ ks, const uint32_t *__restrict__ head,
+                                 const uint32_t *__restrict__ pidr, uint64_t n, int tbits,
+                                 uint64_t *__restrict__ tkey2, uint32_t *__restrict__ pid) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !head[i]) return;
+  const uint32_t q = pidr[i] - 1;
+  const uint64_t k = ks[i];
+  tkey2[q] = ((k >> (32 + tbits)) << 32) | (uint32_t)k;  // (batch, key): pieces in record order after a stable sort
+  pid[q] = q;
+}
+__global__ void k_lr_tile_first(const uint32_t *__restrict__ cut, uint64_t nc, const uint32_t *__restrict__ pidr,
+                                uint32_t *__restrict__ piece0) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nc) piece0[q] = pidr[cut[q]] - 1;
+}
+__global__ void k_lr_tile_heads(const uint64_t *__restrict__ k2s, uint64_t S2, uint32_t *__restrict__ head) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < S2) head[j] = (j == 0 || k2s[j] != k2s[j - 1]) ? 1u : 0u;
+}
+// piece -> its slot (position in (batch, key, record) order, batch-relative); run -> first slot
+__global__ void k_lr_tile_link(const uint64_t *__restrict__ k2s, const uint32_t *__restrict__ perm2,
+                               const uint32_t *__restrict__ head, const uint32_t *__restrict__ gid, uint64_t S2,
+                               const uint64_t *__restrict__ bsub, uint32_t *__restrict__ tslot,
+                               uint32_t *__restrict__ pfirst) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= S2) return;
+  tslot[perm2[j]] = (uint32_t)(j - bsub[k2s[j] >> 32]);
+  if (head[j]) pfirst[gid[j] - 1] = (uint32_t)j;
+}
+__global__ void k_lr_tile_np(const uint32_t *__restrict__ pfirst, uint64_t R, uint64_t S2,
+                             const uint64_t *__restrict__ rkey, const uint64_t *__restrict__ bsub,
+                             uint32_t *__restrict__ np, uint32_t *__restrict__ pst) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= R) return;
+  np[g] = (g + 1 < R ? pfirst[g + 1] : (uint32_t)S2) - pfirst[g];
+  pst[g] = (uint32_t)(pfirst[g] - bsub[rkey[g] >> 32]);
+}
+__global__ void k_lr_tile_info(const uint64_t *__restrict__ k2s, const uint32_t *__restrict__ perm2,
+                               const uint32_t *__restrict__ gid, uint64_t S2, const uint64_t *__restrict__ brun,
+                               const uint32_t *__restrict__ np, uint32_t *__restrict__ tinfo,
+                               uint32_t *__restrict__ tgrun) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= S2) return;
+  const uint64_t g = gid[j] - 1;
+  tinfo[perm2[j]] = (uint32_t)(g - brun[k2s[j] >> 32]) | (np[g] == 1 ? 0x80000000u : 0u);
+  tgrun[perm2[j]] = (uint32_t)g;
+}
+__global__ void k_lr_tile_mrow(const uint4 *__restrict__ m, uint64_t n, const uint32_t *__restrict__ urow,
+                               uint32_t *__restrict__ row) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) row[q] = urow[m[q].w];
+}
+// single GPU, once the runs' shard rows are known: a whole-run piece's destination is its row
+__global__ void k_lr_tile_dst(const uint32_t *__restrict__ tinfo, const uint32_t *__restrict__ tslot,
+                              const uint32_t *__restrict__ tgrun, uint64_t S2, const uint32_t *__restrict__ urow,
+                              uint32_t *__restrict__ tdst) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < S2) tdst[p] = (tinfo[p] >> 31) ? urow[tgrun[p]] : tslot[p];
+}
+
 __global__ __launch_bounds__(256) void k_lr_predict(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
                              const float *__restrict__ fval, uint64_t nr, const uint32_t *__restrict__ vid_row,
                              const float *__restrict__ rows, float *__restrict__ pred) {
@@ -726,7 +1091,17 @@ struct swps_lr {
                                 // 2 = at most 2 (readlane); 4 = a lane per row (k_lr_forward_l); 0 = a row per wave
   int inline_records = 0;       // SWPS_LR_INLINE=1: fast sums form the records inside the reduce (A/B)
   int fwd_records = 0;          // SWPS_LR_FWD_RECORDS=1: the forward scatters the records (A/B: 66.6 vs 53.4 us per step, off)
-  int fwd_diag = 0;             // SWPS_LR_DIAG: forward timing experiments (1: no weight gather, 2: no ordered chain)
+  // fast sums through row tiles (k_lr_tiles): SWPS_LR_TILES=0 for the record path (A/B, tests);
+  // SWPS_LR_TILE_BITS shrinks the tiles (tests: many pieces per key)
+  int tiles = 1, tile_bits = kTileMaxBits;
+  bool tiles_ready = false;
+  DevMem d_trow, d_tval, d_tinfo, d_tslot, d_tgrun, d_tdst, d_tchunk, d_tnp, d_tpst, d_tmulti, d_tmlong, d_tpart;
+  DevMem d_tmsrow, d_tmlrow;
+  uint64_t tile_npieces = 0;
+  // [nb+1] offsets of each batch's blocks (4 u32 each) / runs with several pieces / those with many
+  std::vector<uint64_t> bchunk, bmulti, bmlong;  // (blocks: tile, first / end record, first / end piece)
+  uint64_t max_bpiece = 0;
+  int fwd_diag = 0;             // SWPS_LR_DIAG: timing experiments (1: forward without weight gather, 2: without ordered chain, 4: records without e gathers)
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
   LTimer timer;
@@ -752,6 +1127,159 @@ template <typename T> int lr_scan_incl(const T *in, T *out, uint64_t n, DevMem &
   SWPS_TRY(tmp.ensure(b));
   b = tmp.bytes;
   SWPS_HIP(hipcub::DeviceScan::InclusiveSum(tmp.p, b, in, out, (int)n, s));
+  return SWPS_OK;
+}
+
+// The tile index (k_lr_tiles): every batch's records in (tile, key) order; the blocks (2,048
+// consecutive records of one tile); the pieces (a key's records inside one block) with their
+// run, their partial's slot in (key, record) order, and per run its piece count and first slot;
+// per batch the runs with more than one piece.  ks / perm / rid / tmp are lr_index's scratch.
+int lr_tile_index(swps_lr *l, DevMem &ks, DevMem &perm, DevMem &rid, DevMem &rkey, DevMem &d_brun, uint64_t R, int bbits,
+                  DevMem &tmp) {
+  hipStream_t s = l->s;
+  const uint64_t nr = l->label.size(), nb = l->nbatches, B1 = (uint64_t)l->B1();
+  const uint64_t n = l->row_off[nr];
+  const int tb = l->tile_bits;
+  const uint64_t ntile = (B1 + (1ULL << tb) - 1) >> tb;
+  int tbits = 1;
+  while ((1ULL << tbits) < ntile) tbits++;
+  if (32 + tbits + bbits > 64) return SWPS_OK;  // the record path
+  // blocks, from the CSR: batch b's tile t holds the records of rows [b*B1 + t*2^tb, ...), and
+  // the (batch, tile, key) order keeps each (batch, tile) group contiguous
+  std::vector<uint32_t> cut, chunks;
+  l->bchunk.assign(nb + 1, 0);
+  for (uint64_t b = 0; b < nb; b++) {
+    l->bchunk[b] = cut.size();
+    const uint64_t rb0 = b * B1, rb1 = std::min<uint64_t>(nr, rb0 + B1);
+    for (uint64_t tl = 0; rb0 + (tl << tb) < rb1; tl++) {
+      const uint64_t rs = rb0 + (tl << tb), re = std::min<uint64_t>(rb1, rs + (1ULL << tb));
+      for (uint64_t c0 = l->row_off[rs]; c0 < l->row_off[re]; c0 += kTileChunk) {
+        const uint64_t c1 = std::min<uint64_t>(l->row_off[re], c0 + kTileChunk);
+        // record positions in sorted order equal CSR positions at group granularity
+        cut.push_back((uint32_t)c0);
+        chunks.insert(chunks.end(), {(uint32_t)tl, (uint32_t)c0, (uint32_t)c1, 0u, 0u});
+      }
+    }
+  }
+  l->bchunk[nb] = cut.size();
+  DevMem key, idx, head, pidr, d_cut, d_p0;
+  SWPS_TRY(key.ensure(n * 8));
+  SWPS_TRY(idx.ensure(n * 4));
+  k_lr_tile_keys<<<nblk(nr), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), nr, B1, tb, tbits, l->d_fvid.as<int32_t>(),
+                                           key.as<uint64_t>(), idx.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  size_t sb = 0;
+  SWPS_HIP(sort_pairs(nullptr, sb, key.as<uint64_t>(), ks.as<uint64_t>(), idx.as<uint32_t>(), perm.as<uint32_t>(), n,
+                      32 + tbits + bbits, s));
+  SWPS_TRY(tmp.ensure(sb));
+  sb = tmp.bytes;
+  SWPS_HIP(sort_pairs(tmp.p, sb, key.as<uint64_t>(), ks.as<uint64_t>(), idx.as<uint32_t>(), perm.as<uint32_t>(), n,
+                      32 + tbits + bbits, s));
+  key.release();
+  idx.release();
+  k_lr_rowid<<<nblk(nr), 256, 0, s>>>(l->d_row_off.as<uint64_t>(), nr, rid.as<uint32_t>());
+  SWPS_TRY(l->d_trow.ensure(n * 2));
+  SWPS_TRY(l->d_tval.ensure(n * 4));
+  SWPS_TRY(head.ensure(n * 4));
+  SWPS_TRY(pidr.ensure(n * 4));
+  k_lr_tile_slots<<<nblk(n), 256, 0, s>>>(ks.as<uint64_t>(), perm.as<uint32_t>(), n, rid.as<uint32_t>(), B1, tb,
+                                           l->d_fval.as<float>(), l->d_trow.as<uint16_t>(), l->d_tval.as<float>(),
+                                           head.as<uint32_t>());
+  SWPS_TRY(upload(d_cut, cut, s));
+  k_lr_tile_cuts<<<nblk(cut.size()), 256, 0, s>>>(d_cut.as<uint32_t>(), cut.size(), head.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  SWPS_TRY(lr_scan_incl(head.as<uint32_t>(), pidr.as<uint32_t>(), n, tmp, s));
+  uint32_t S2 = 0;
+  SWPS_HIP(hipMemcpyAsync(&S2, pidr.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  DevMem tkey2, k2s, pid, perm2, head2, gid, pfirst, d_bsub, d_bcnt;
+  SWPS_TRY(tkey2.ensure((uint64_t)S2 * 8));
+  SWPS_TRY(k2s.ensure((uint64_t)S2 * 8));
+  SWPS_TRY(pid.ensure((uint64_t)S2 * 4));
+  SWPS_TRY(perm2.ensure((uint64_t)S2 * 4));
+  SWPS_TRY(d_p0.ensure(std::max<uint64_t>(cut.size(), 1) * 4));
+  k_lr_tile_pieces<<<nblk(n), 256, 0, s>>>(ks.as<uint64_t>(), head.as<uint32_t>(), pidr.as<uint32_t>(), n, tbits,
+                                            tkey2.as<uint64_t>(), pid.as<uint32_t>());
+  k_lr_tile_first<<<nblk(cut.size()), 256, 0, s>>>(d_cut.as<uint32_t>(), cut.size(), pidr.as<uint32_t>(),
+                                                    d_p0.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  head.release();
+  pidr.release();
+  sb = 0;  // stable: a key's pieces stay in (tile, record) order
+  SWPS_HIP(sort_pairs(nullptr, sb, tkey2.as<uint64_t>(), k2s.as<uint64_t>(), pid.as<uint32_t>(), perm2.as<uint32_t>(),
+                      S2, 32 + bbits, s));
+  SWPS_TRY(tmp.ensure(sb));
+  sb = tmp.bytes;
+  SWPS_HIP(sort_pairs(tmp.p, sb, tkey2.as<uint64_t>(), k2s.as<uint64_t>(), pid.as<uint32_t>(), perm2.as<uint32_t>(),
+                      S2, 32 + bbits, s));
+  SWPS_TRY(head2.ensure((uint64_t)S2 * 4));
+  SWPS_TRY(gid.ensure((uint64_t)S2 * 4));
+  k_lr_tile_heads<<<nblk(S2), 256, 0, s>>>(k2s.as<uint64_t>(), S2, head2.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  SWPS_TRY(lr_scan_incl(head2.as<uint32_t>(), gid.as<uint32_t>(), S2, tmp, s));
+  uint32_t R2 = 0;
+  SWPS_HIP(hipMemcpyAsync(&R2, gid.as<uint32_t>() + S2 - 1, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  if (R2 != R) return fail(SWPS_E_STATE, "LR tile index: run count mismatch");
+  SWPS_TRY(d_bsub.ensure((nb + 1) * 8));
+  SWPS_TRY(d_bcnt.ensure((nb + 1) * 4));
+  k_lr_idx_bruns<<<nblk(nb + 1), 256, 0, s>>>(k2s.as<uint64_t>(), S2, nb, d_bsub.as<uint64_t>(), d_bcnt.as<uint32_t>());
+  SWPS_TRY(l->d_tslot.ensure((uint64_t)S2 * 4));
+  SWPS_TRY(l->d_tinfo.ensure((uint64_t)S2 * 4));
+  SWPS_TRY(l->d_tgrun.ensure((uint64_t)S2 * 4));
+  SWPS_TRY(l->d_tdst.ensure((uint64_t)S2 * 4));
+  l->tile_npieces = S2;
+  SWPS_TRY(pfirst.ensure(R * 4));
+  SWPS_TRY(l->d_tnp.ensure(R * 4));
+  SWPS_TRY(l->d_tpst.ensure(R * 4));
+  k_lr_tile_link<<<nblk(S2), 256, 0, s>>>(k2s.as<uint64_t>(), perm2.as<uint32_t>(), head2.as<uint32_t>(),
+                                           gid.as<uint32_t>(), S2, d_bsub.as<uint64_t>(), l->d_tslot.as<uint32_t>(),
+                                           pfirst.as<uint32_t>());
+  k_lr_tile_np<<<nblk(R), 256, 0, s>>>(pfirst.as<uint32_t>(), R, S2, rkey.as<uint64_t>(), d_bsub.as<uint64_t>(),
+                                        l->d_tnp.as<uint32_t>(), l->d_tpst.as<uint32_t>());
+  k_lr_tile_info<<<nblk(S2), 256, 0, s>>>(k2s.as<uint64_t>(), perm2.as<uint32_t>(), gid.as<uint32_t>(), S2,
+                                           d_brun.as<uint64_t>(), l->d_tnp.as<uint32_t>(), l->d_tinfo.as<uint32_t>(),
+                                           l->d_tgrun.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  // first piece of every block; the runs with several pieces
+  std::vector<uint64_t> bsub(nb + 1);
+  std::vector<uint32_t> np(R), p0(cut.size()), pst(R), rcnt(R);
+  SWPS_HIP(hipMemcpyAsync(pst.data(), l->d_tpst.p, R * 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipMemcpyAsync(rcnt.data(), l->d_rcnt.p, R * 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipMemcpyAsync(bsub.data(), d_bsub.p, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipMemcpyAsync(np.data(), l->d_tnp.p, R * 4, hipMemcpyDeviceToHost, s));
+  if (!cut.empty()) SWPS_HIP(hipMemcpyAsync(p0.data(), d_p0.p, cut.size() * 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  std::vector<uint32_t> multi, mlong;
+  l->bmulti.assign(nb + 1, 0);
+  l->bmlong.assign(nb + 1, 0);
+  l->max_bpiece = 0;
+  for (uint64_t b = 0; b < nb; b++) {
+    l->bmulti[b] = multi.size() / 4;
+    l->bmlong[b] = mlong.size() / 4;
+    l->max_bpiece = std::max<uint64_t>(l->max_bpiece, bsub[b + 1] - bsub[b]);
+    for (uint64_t q = l->bchunk[b]; q < l->bchunk[b + 1]; q++) {  // first and end piece (global)
+      chunks[q * 5 + 3] = p0[q];
+      chunks[q * 5 + 4] = q + 1 < cut.size() ? p0[q + 1] : S2;
+    }
+    for (uint64_t g = l->brun[b]; g < l->brun[b + 1]; g++)
+      if (np[g] > 1)  // {first slot, partials, records, run}
+        (np[g] > kTileFinShort ? mlong : multi).insert((np[g] > kTileFinShort ? mlong : multi).end(),
+                                                       {pst[g], np[g], rcnt[g], (uint32_t)g});
+  }
+  l->bmulti[nb] = multi.size() / 4;
+  l->bmlong[nb] = mlong.size() / 4;
+  if (multi.empty()) multi.assign(4, 0);
+  if (mlong.empty()) mlong.assign(4, 0);
+  SWPS_TRY(l->d_tmsrow.ensure(multi.size()));  // 4 B per entry: the runs' shard rows (single GPU)
+  SWPS_TRY(l->d_tmlrow.ensure(mlong.size()));
+  SWPS_TRY(upload(l->d_tmlong, mlong, s));
+  if (chunks.empty()) chunks.assign(5, 0);
+  SWPS_TRY(upload(l->d_tchunk, chunks, s));
+  SWPS_TRY(upload(l->d_tmulti, multi, s));
+  SWPS_TRY(l->d_tpart.ensure(std::max<uint64_t>(l->max_bpiece, 1) * 8));
+  SWPS_HIP(hipStreamSynchronize(s));
+  l->tiles_ready = true;
   return SWPS_OK;
 }
 
@@ -843,6 +1371,8 @@ int lr_index(swps_lr *l) {
     SWPS_TRY(upload(l->d_slong, lst, s));
     SWPS_HIP(hipStreamSynchronize(s));
   }
+  l->tiles_ready = false;
+  if (l->cfg.fast_sums && l->tiles) SWPS_TRY(lr_tile_index(l, ks, perm, rid1, rkey, d_brun, R, bbits, tmp));
   return SWPS_OK;
 }
 
@@ -900,6 +1430,20 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     k_lr_map_rows<<<nblk(R), 256, 0, s>>>((const int32_t *)l->d_ruk.as<uint32_t>(), R, l->d_vid_row.as<uint32_t>(),
                                           l->d_urow.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
+    if (l->tiles_ready && l->tile_npieces)
+      k_lr_tile_dst<<<nblk(l->tile_npieces), 256, 0, s>>>(l->d_tinfo.as<uint32_t>(), l->d_tslot.as<uint32_t>(),
+                                                           l->d_tgrun.as<uint32_t>(), l->tile_npieces,
+                                                           l->d_urow.as<uint32_t>(), l->d_tdst.as<uint32_t>());
+    if (l->tiles_ready) {
+      const uint64_t nms = l->bmulti[l->nbatches], nml = l->bmlong[l->nbatches];
+      if (nms)
+        k_lr_tile_mrow<<<nblk(nms), 256, 0, s>>>((const uint4 *)l->d_tmulti.p, nms, l->d_urow.as<uint32_t>(),
+                                                  l->d_tmsrow.as<uint32_t>());
+      if (nml)
+        k_lr_tile_mrow<<<nblk(nml), 256, 0, s>>>((const uint4 *)l->d_tmlong.p, nml, l->d_urow.as<uint32_t>(),
+                                                  l->d_tmlrow.as<uint32_t>());
+    }
+    SWPS_HIP(hipGetLastError());
     l->rows_mapped = true;
     fidx = l->d_frow.as<uint32_t>();
   }
@@ -915,7 +1459,7 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     hipExtLaunchKernelGGL(k_lr_forward_r<3, true>, dim3((unsigned)nblk((nrb + 2) / 3 * 64)), dim3(256), 0, s, fb, fe, 0,
                           (const uint64_t *)l->d_row_off.as<uint64_t>(), fidx, (const float *)l->d_fval.as<float>(),
                           (const float *)l->d_label.as<float>(), r0, nrb, (const float *)rows, stride,
-                          l->d_err.as<float>(), l->d_err2.as<float>(), 0, (const uint32_t *)nullptr, (uint64_t)0,
+                          l->d_err.as<float>(), l->d_err2.as<float>(), l->fwd_diag & 3, (const uint32_t *)nullptr, (uint64_t)0,
                           (float *)nullptr);
     l->timer.ext_end(0, fb, fe);
     if (fb) (void)hipEventDestroy(e0);
@@ -968,19 +1512,48 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   float *val = l->d_val_s.as<float>() + (scat ? 0 : (nz0 & 3));
   hipEvent_t pb = nullptr;  // the push group's start stamp (the records kernel's start)
   const bool inl = fused && !scat && l->inline_records;  // the reduce forms the records itself
-  if (!scat && !inl) {
-    pb = l->timer.ext();
-    hipExtLaunchKernelGGL(k_lr_records, dim3((unsigned)(((nz0 + nnz + 3) / 4 - nz0 / 4 + 255) / 256)), dim3(256), 0, s,
-                          pb, (hipEvent_t) nullptr, 0, (const uint32_t *)l->d_srow.as<uint32_t>(),
-                          (const float *)l->d_sval.as<float>(), nz0, nz0 + nnz, (const float *)l->d_err.as<float>(),
-                          val - (nz0 & 3));
-  }
   LrReduce ra{l->d_ruk.as<uint32_t>() + q0, l->d_rcnt.as<uint32_t>() + q0, l->d_roff.as<uint32_t>() + q0,
               l->d_bnruns.as<uint32_t>() + bi, val,
               l->sharded ? nullptr : l->d_urow.as<uint32_t>() + q0,
               l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, l->d_local.as<int32_t>(),
               l->sharded ? d_grads : nullptr, nlong, l->d_longs.as<uint32_t>(), l->cfg.fast_sums,
               l->d_srow.as<uint32_t>() + nz0, l->d_sval.as<float>() + nz0, l->d_err.as<float>()};
+  if (l->cfg.fast_sums && l->tiles_ready && !scat && !l->inline_records) {  // row tiles (the default)
+    const uint32_t nch = (uint32_t)(l->bchunk[bi + 1] - l->bchunk[bi]);
+    const uint32_t nm = (uint32_t)(l->bmulti[bi + 1] - l->bmulti[bi]);
+    LrTiles tt{l->d_trow.as<uint16_t>(), l->d_tval.as<float>(), l->d_tchunk.as<uint32_t>() + l->bchunk[bi] * 5,
+               l->d_tinfo.as<uint32_t>(), (l->sharded ? l->d_tslot : l->d_tdst).as<uint32_t>(), l->d_tpart.as<double>(),
+               l->d_err.as<float>(),
+               r0, nrb, l->tile_bits};
+    hipEvent_t tb0 = l->timer.ext(), te0 = l->timer.ext();
+    const bool fin = l->bmulti[bi + 1] > l->bmulti[bi] || l->bmlong[bi + 1] > l->bmlong[bi];
+    if (nch) hipExtLaunchKernelGGL(k_lr_tiles, dim3(nch), dim3(256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0, ra, tt);
+    const uint32_t nl = (uint32_t)(l->bmlong[bi + 1] - l->bmlong[bi]);
+    if (nm || nl) {
+      const uint32_t LB = std::min<uint32_t>((nl + 3) / 4, 1024);
+      hipExtLaunchKernelGGL(k_lr_tiles_fin, dim3(LB + (nm ? nblk(nm) : 0)), dim3(256), 0, s,
+                            nch ? (hipEvent_t) nullptr : tb0, te0, 0, ra,
+                            (const uint4 *)l->d_tmulti.p + l->bmulti[bi], (const uint32_t *)l->d_tmsrow.as<uint32_t>() + l->bmulti[bi], nm,
+                            (const uint4 *)l->d_tmlong.p + l->bmlong[bi], (const uint32_t *)l->d_tmlrow.as<uint32_t>() + l->bmlong[bi], nl,
+                            LB, (const double *)l->d_tpart.as<double>(), (uint64_t)q0);
+    }
+    SWPS_HIP(hipGetLastError());
+    if (nch || fin)
+      l->timer.ext_end(3, tb0, te0);
+    else if (tb0) {
+      (void)hipEventDestroy(tb0);
+      (void)hipEventDestroy(te0);
+    }
+    if (e3) (void)hipEventDestroy(e3);
+    return SWPS_OK;
+  }
+  if (!scat && !inl) {
+    pb = l->timer.ext();
+    hipExtLaunchKernelGGL(k_lr_records, dim3((unsigned)(((nz0 + nnz + 3) / 4 - nz0 / 4 + 255) / 256)), dim3(256), 0, s,
+                          pb, (hipEvent_t) nullptr, 0, (const uint32_t *)l->d_srow.as<uint32_t>(),
+                          (const float *)l->d_sval.as<float>(), nz0, nz0 + nnz, (const float *)l->d_err.as<float>(),
+                          val - (nz0 & 3), l->fwd_diag);
+  }
   if (fused) {
     const uint32_t NL = (uint32_t)(l->blong[bi + 1] - l->blong[bi]);
     const uint32_t LB = std::min<uint32_t>(NL, 2048);
@@ -1041,6 +1614,8 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests
   if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
+  if (const char *e = getenv("SWPS_LR_TILES")) l->tiles = atoi(e);                // A/B timing, tests
+  if (const char *e = getenv("SWPS_LR_TILE_BITS")) l->tile_bits = std::min(std::max(atoi(e), 4), kTileMaxBits);
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;
     return fail(SWPS_E_OOM, "pinned alloc");

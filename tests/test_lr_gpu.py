@@ -210,6 +210,7 @@ def test_lr_fused_reduce_bit_identical(lib, gpu, monkeypatch):
     from swiftmpi_amd.synth import criteo
     y, off, f, v = criteo(20000, seed=7)
     res = []
+    monkeypatch.setenv("SWPS_LR_TILES", "0")  # the record path's two reduce forms
     for fused in ("0", "1"):
         monkeypatch.setenv("SWPS_LR_FUSED", fused)
         t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
@@ -300,6 +301,7 @@ def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, env, fast):
     vals = rng.random(int(roff[-1])).astype(np.float32)
     yl = (rng.random(4000) < 0.5).astype(np.float32)
     res = []
+    monkeypatch.setenv("SWPS_LR_TILES", "0")  # the record path (fast sums default: row tiles)
     for on in ("0", "1"):
         monkeypatch.setenv(env, on)
         out = []
@@ -312,3 +314,42 @@ def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, env, fast):
         res.append(out)
     for a, b in zip(res[0], res[1]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("bits", [None, "6", "4"])
+def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits):
+    """Fast sums through row tiles (k_lr_tiles + k_lr_tiles_fin: e read from an LDS slice, a
+    block-wide segmented scan over 2,048 records, one fp64 partial per piece = a key's records
+    inside one block, a key's partials added in record order) against the record path
+    (k_lr_records + k_lr_reduce_fused): the same fp32 products e*x_i, fp64 sums in another fixed
+    order, so the means agree to fp64 rounding and the weights after 2 epochs within 1e-6 of
+    their scale; run to run bit-identical.  Default tiles (4,096 rows: hot keys' runs cross
+    block boundaries) and shrunken ones (64 / 16 rows: nearly every key in many pieces) on
+    Criteo-shaped rows (hot keys) and ragged rows of 1-60 features."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(20000, seed=7)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(1, 61, 4000)
+    roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    feat = rng.integers(0, 3000, int(roff[-1])).astype(np.uint32)
+    vals = rng.random(int(roff[-1])).astype(np.float32)
+    yl = (rng.random(4000) < 0.5).astype(np.float32)
+    if bits:
+        monkeypatch.setenv("SWPS_LR_TILE_BITS", bits)
+    res = []
+    for tiles in ("0", "1", "1"):
+        monkeypatch.setenv("SWPS_LR_TILES", tiles)
+        out = []
+        for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
+            t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+            m = lib.LR(t, minibatch=B, init_ref=False, fast_sums=True)
+            m.load_csr(*data)
+            m.init()
+            out += [m.train(2), m.params()[1], m.params()[2]]
+        res.append(out)
+    for a, b in zip(res[1], res[2]):
+        assert np.array_equal(a, b)
+    for a, b in zip(res[0], res[1]):
+        a = np.asarray(a, dtype=np.float64)
+        b = np.asarray(b, dtype=np.float64)
+        assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max(), (np.abs(a - b).max(), np.abs(a).max())
