@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 XGMI_PEAK_GBS = 7 * 153.0  # per GPU: 7 xGMI links x ~153 GB/s
 
 
-def lr_tile_pieces(f, off, r0, r1, tile_bits=12, chunk=2048):
+def lr_tile_pieces(f, off, r0, r1, tile_bits=12, chunk=1024):
     """The LR row-tile path's pieces and partials for batch rows [r0, r1): records ordered by
     (tile, key) (stable: row order inside), cut into blocks of `chunk` records per tile; a piece
     is a key's records inside one block, a partial a piece of a key with several

@@ -6,9 +6,11 @@
 //                  p = 1/(1+exp(-s)), e = y - p stored per row (lr.cpp:358-375)
 //   k_lr_reduce_*  per pushed key (a run of the batch's records in their static
 //                  key-sorted order, built once at load): the gradient records
-//                  e[row]*x_i summed in record order (fp32 chain, or fp64 in
-//                  fast_sums mode), mean = sum/count (lr.cpp:32-38), AdaGrad fp32
-//                  (lr.cpp:68-75) on the shard row
+//                  e[row]*x_i summed in record order (fp32 chain, exact mode),
+//                  mean = sum/count (lr.cpp:32-38), AdaGrad fp32 (lr.cpp:68-75)
+//                  on the shard row
+//   k_lr_tiles(_fin) fast_sums mode: the same per-key means from fp64 sums over
+//                  row tiles (e read from LDS, one partial per block piece)
 // The records' (row, x_i) in key-sorted order are static (srow / sval), so the
 // forward writes one error per row instead of scattering a record per feature.
 // Every weight read in a batch belongs to that batch's key set, which the
@@ -629,13 +631,13 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
 // random order within a key's run): 2.56M divergent 4-B reads per Criteo batch.  Cut the batch
 // into tiles of 2^tb rows: the static index orders each batch's records by (tile, key), so a
 // block loads its tile's slice of e into LDS once and reads every record's e from LDS.  A block
-// takes 2,048 consecutive records of one tile (8 per thread, coalesced) and sums each key's
+// takes 1,024 consecutive records of one tile (4 per thread, coalesced) and sums each key's
 // records with one block-wide segmented scan; a piece = a key's records inside one block.  A key
 // with a single piece is applied by k_lr_tiles itself; the others get one fp64 partial per piece,
 // added in (tile, record) order by k_lr_tiles_fin.  Same fp32 products e*x_i as the record path,
 // fp64 sums in a fixed order: deterministic, within fp64 rounding of k_lr_reduce_fused.
 constexpr int kTileMaxBits = 12;         // LDS slice: 4,096 rows (16 KB)
-constexpr uint32_t kTileChunk = 2048;    // records per block
+constexpr uint32_t kTileChunk = 1024;    // records per block (SWPS_LR_TILE_CHUNK: 512 / 1024 / 2048 / 4096)
 constexpr uint16_t kTileHead = 0x8000;   // trow bit: the record starts a (tile, key) run
 
 struct LrTiles {
@@ -649,6 +651,7 @@ struct LrTiles {
   const float *err;
   uint64_t r0, nrb;
   int tb;
+  int diag;  // SWPS_LR_DIAG timing experiments only: 8 no piece ends, 16 no e slice fill
 };
 
 // segmented-sum scan element (a head seen, open run's sum, heads, last head's record):
@@ -661,7 +664,8 @@ __device__ __forceinline__ void seg_after(bool fp, double vp, int cp, uint32_t h
   h = max(h, hp);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_lr_tiles(LrReduce a, LrTiles t) {
+template <int RPT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3 : RPT > 4 ? 6 : 8))) void k_lr_tiles(LrReduce a, LrTiles t) {
   __shared__ float es[1 << kTileMaxBits];
   __shared__ double wv[4];
   __shared__ int wf[4], wc[4];
@@ -669,19 +673,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   const uint32_t *ch = t.chunk + (uint64_t)blockIdx.x * 5;
   const uint32_t tile = ch[0], rec0 = ch[1], rec1 = ch[2], piece0 = ch[3];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t i0 = rec0 + (uint32_t)tid * 8;
-  const int n = i0 < rec1 ? (int)min(8u, rec1 - i0) : 0;
-  uint32_t rw[9];
-  float x[8];
+  const uint32_t i0 = rec0 + (uint32_t)tid * RPT;
+  const int n = i0 < rec1 ? (int)min((uint32_t)RPT, rec1 - i0) : 0;
+  uint32_t rw[RPT + 1];
+  float x[RPT];
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < RPT; j++) {
     rw[j] = j < n ? t.trow[i0 + j] : 0u;
     x[j] = j < n ? t.tval[i0 + j] : 0.f;
   }
-  rw[8] = n == 8 && i0 + 8 < rec1 ? t.trow[i0 + 8] : kTileHead;  // the next record: a head ends this thread's last run
+  rw[RPT] = n == RPT && i0 + RPT < rec1 ? t.trow[i0 + RPT] : kTileHead;  // the next record: a head ends this thread's last run
   const uint64_t e0 = (uint64_t)tile << t.tb;
   const uint32_t ne = (uint32_t)min<uint64_t>(1ull << t.tb, t.nrb - e0);
-  {  // the tile's slice of e: every load in flight, then the LDS stores
+  if (!(t.diag & 16)) {  // the tile's slice of e: every load in flight, then the LDS stores
     constexpr int KE = (1 << kTileMaxBits) / 256;
     float ev[KE];
 #pragma unroll
@@ -696,13 +700,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
   }
   __syncthreads();
-  double pr[8];
+  double pr[RPT];
   bool any = false;
   double pre = 0, cur = 0;
   int nh = 0;
   uint32_t lh = 0;
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < RPT; j++) {
     pr[j] = j < n ? (double)(es[rw[j] & (kTileHead - 1)] * x[j]) : 0.0;
     const bool h = j < n && ((rw[j] & kTileHead) || i0 + j == rec0);
     if (h) {
@@ -768,11 +772,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   seg_after(fw, vw, cw, hw, fx, run, cx, hs);
   // this thread's pieces that end here, in record order: (piece, sum, record count)
   uint32_t p = (uint32_t)cx - 1;  // block-local index of the piece open before this thread's first record
-  uint32_t pj[8], cj[8];
-  double sj[8];
-  bool ej[8];
+  uint32_t pj[RPT], cj[RPT];
+  double sj[RPT];
+  bool ej[RPT];
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < RPT; j++) {
     const bool h = (rw[j] & kTileHead) || i0 + j == rec0;
     if (h) {
       p++;
@@ -781,29 +785,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     } else {
       run = run + pr[j];
     }
-    ej[j] = j < n && (j + 1 < n ? (rw[j + 1] & kTileHead) != 0 : (n < 8 || (rw[8] & kTileHead) != 0));
+    ej[j] = j < n && (j + 1 < n ? (rw[j + 1] & kTileHead) != 0 : (n < RPT || (rw[RPT] & kTileHead) != 0));
     pj[j] = p;
     cj[j] = i0 + j - hs + 1;
     sj[j] = run;
   }
+  if (t.diag & 8) {
+    if (sj[0] == 12345.678) t.part[0] = sj[1];  // keeps the sums live
+    return;
+  }
   // a piece that is its key's whole run: the mean and AdaGrad; else its partial.  Every stage's
   // loads in flight together (a piece end at a time would chain the round trips: vmcnt orders
   // them behind the stores)
-  uint32_t info[8], dst[8];
+  uint32_t info[RPT], dst[RPT];
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < RPT; j++) {
     info[j] = ej[j] ? t.tinfo[piece0 + pj[j]] : 0u;
     dst[j] = ej[j] ? t.tdst[piece0 + pj[j]] : 0u;
   }
   if (a.grads) {  // sharded: the mean into the push request at local[vid]
-    uint32_t u[8];
+    uint32_t u[RPT];
 #pragma unroll
-    for (int j = 0; j < 8; j++) u[j] = ej[j] && (info[j] >> 31) ? a.uniq[info[j] & 0x7FFFFFFFu] : 0u;
-    int32_t lo[8];
+    for (int j = 0; j < RPT; j++) u[j] = ej[j] && (info[j] >> 31) ? a.uniq[info[j] & 0x7FFFFFFFu] : 0u;
+    int32_t lo[RPT];
 #pragma unroll
-    for (int j = 0; j < 8; j++) lo[j] = ej[j] && (info[j] >> 31) ? a.local[u[j]] : 0;
+    for (int j = 0; j < RPT; j++) lo[j] = ej[j] && (info[j] >> 31) ? a.local[u[j]] : 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < RPT; j++) {
       if (!ej[j]) continue;
       if (info[j] >> 31)
         a.grads[lo[j]] = (float)(sj[j] / (double)cj[j]);
@@ -812,15 +820,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
     return;
   }
-  float w0[8], g0[8];
+  float w0[RPT], g0[RPT];
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < RPT; j++) {
     const bool one = ej[j] && (info[j] >> 31);
     w0[j] = one ? a.rows[(uint64_t)dst[j] * 2] : 0.f;
     g0[j] = one ? a.rows[(uint64_t)dst[j] * 2 + 1] : 0.f;
   }
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < RPT; j++) {
     if (!ej[j]) continue;
     if (info[j] >> 31) {  // lr_apply's AdaGrad step (lr.cpp:68-75) on the shard row
       const float m = (float)(sj[j] / (double)cj[j]);
@@ -1094,6 +1102,7 @@ struct swps_lr {
   // fast sums through row tiles (k_lr_tiles): SWPS_LR_TILES=0 for the record path (A/B, tests);
   // SWPS_LR_TILE_BITS shrinks the tiles (tests: many pieces per key)
   int tiles = 1, tile_bits = kTileMaxBits;
+  uint32_t tile_chunk = kTileChunk;
   bool tiles_ready = false;
   DevMem d_trow, d_tval, d_tinfo, d_tslot, d_tgrun, d_tdst, d_tchunk, d_tnp, d_tpst, d_tmulti, d_tmlong, d_tpart;
   DevMem d_tmsrow, d_tmlrow;
@@ -1130,7 +1139,7 @@ template <typename T> int lr_scan_incl(const T *in, T *out, uint64_t n, DevMem &
   return SWPS_OK;
 }
 
-// The tile index (k_lr_tiles): every batch's records in (tile, key) order; the blocks (2,048
+// The tile index (k_lr_tiles): every batch's records in (tile, key) order; the blocks (1,024
 // consecutive records of one tile); the pieces (a key's records inside one block) with their
 // run, their partial's slot in (key, record) order, and per run its piece count and first slot;
 // per batch the runs with more than one piece.  ks / perm / rid / tmp are lr_index's scratch.
@@ -1153,8 +1162,8 @@ int lr_tile_index(swps_lr *l, DevMem &ks, DevMem &perm, DevMem &rid, DevMem &rke
     const uint64_t rb0 = b * B1, rb1 = std::min<uint64_t>(nr, rb0 + B1);
     for (uint64_t tl = 0; rb0 + (tl << tb) < rb1; tl++) {
       const uint64_t rs = rb0 + (tl << tb), re = std::min<uint64_t>(rb1, rs + (1ULL << tb));
-      for (uint64_t c0 = l->row_off[rs]; c0 < l->row_off[re]; c0 += kTileChunk) {
-        const uint64_t c1 = std::min<uint64_t>(l->row_off[re], c0 + kTileChunk);
+      for (uint64_t c0 = l->row_off[rs]; c0 < l->row_off[re]; c0 += l->tile_chunk) {
+        const uint64_t c1 = std::min<uint64_t>(l->row_off[re], c0 + l->tile_chunk);
         // record positions in sorted order equal CSR positions at group granularity
         cut.push_back((uint32_t)c0);
         chunks.insert(chunks.end(), {(uint32_t)tl, (uint32_t)c0, (uint32_t)c1, 0u, 0u});
@@ -1524,10 +1533,16 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     LrTiles tt{l->d_trow.as<uint16_t>(), l->d_tval.as<float>(), l->d_tchunk.as<uint32_t>() + l->bchunk[bi] * 5,
                l->d_tinfo.as<uint32_t>(), (l->sharded ? l->d_tslot : l->d_tdst).as<uint32_t>(), l->d_tpart.as<double>(),
                l->d_err.as<float>(),
-               r0, nrb, l->tile_bits};
+               r0, nrb, l->tile_bits, l->fwd_diag};
     hipEvent_t tb0 = l->timer.ext(), te0 = l->timer.ext();
     const bool fin = l->bmulti[bi + 1] > l->bmulti[bi] || l->bmlong[bi + 1] > l->bmlong[bi];
-    if (nch) hipExtLaunchKernelGGL(k_lr_tiles, dim3(nch), dim3(256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0, ra, tt);
+    if (nch) {
+      auto kt = l->tile_chunk == 512    ? k_lr_tiles<2>
+                : l->tile_chunk == 1024 ? k_lr_tiles<4>
+                : l->tile_chunk == 4096 ? k_lr_tiles<16>
+                                        : k_lr_tiles<8>;
+      hipExtLaunchKernelGGL(kt, dim3(nch), dim3(256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0, ra, tt);
+    }
     const uint32_t nl = (uint32_t)(l->bmlong[bi + 1] - l->bmlong[bi]);
     if (nm || nl) {
       const uint32_t LB = std::min<uint32_t>((nl + 3) / 4, 1024);
@@ -1615,6 +1630,10 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_TILES")) l->tiles = atoi(e);                // A/B timing, tests
+  if (const char *e = getenv("SWPS_LR_TILE_CHUNK")) {
+    const int c = atoi(e);
+    l->tile_chunk = c == 512 || c == 2048 || c == 4096 ? (uint32_t)c : kTileChunk;
+  }
   if (const char *e = getenv("SWPS_LR_TILE_BITS")) l->tile_bits = std::min(std::max(atoi(e), 4), kTileMaxBits);
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;

@@ -316,10 +316,11 @@ def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, env, fast):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("bits", [None, "6", "4"])
-def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits):
+@pytest.mark.parametrize("bits,chunk", [(None, None), ("6", None), ("4", None), (None, "512"), (None, "2048"),
+                                        (None, "4096")])
+def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits, chunk):
     """Fast sums through row tiles (k_lr_tiles + k_lr_tiles_fin: e read from an LDS slice, a
-    block-wide segmented scan over 2,048 records, one fp64 partial per piece = a key's records
+    block-wide segmented scan over 1,024 records, one fp64 partial per piece = a key's records
     inside one block, a key's partials added in record order) against the record path
     (k_lr_records + k_lr_reduce_fused): the same fp32 products e*x_i, fp64 sums in another fixed
     order, so the means agree to fp64 rounding and the weights after 2 epochs within 1e-6 of
@@ -336,6 +337,8 @@ def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits):
     yl = (rng.random(4000) < 0.5).astype(np.float32)
     if bits:
         monkeypatch.setenv("SWPS_LR_TILE_BITS", bits)
+    if chunk:  # blocks of 512 / 2,048 / 4,096 records (2 / 8 / 16 per thread; default 1,024)
+        monkeypatch.setenv("SWPS_LR_TILE_CHUNK", chunk)
     res = []
     for tiles in ("0", "1", "1"):
         monkeypatch.setenv("SWPS_LR_TILES", tiles)
