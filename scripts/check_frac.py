@@ -39,7 +39,7 @@ def main(paths):
         for row in csv.DictReader(open(csvp)):
             rows.setdefault(base(row["Name"]), []).append(float(row["AverageNs"]))
         if leg == "lr":
-            grp = GROUPS["lr_push"] if "reduce" in r["kernel"] else GROUPS["lr_forward"]
+            grp = GROUPS["lr_push"] if ("reduce" in r["kernel"] or "tiles" in r["kernel"]) else GROUPS["lr_forward"]
         elif leg == "s2v":
             grp = GROUPS["s2v"]
         else:

@@ -1,0 +1,8 @@
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || exit $rc
+LEGS=lr bash scripts/gpu_profile.sh > gpurun_out/prof_lr.out 2>&1; rc=$?
+tail -3 gpurun_out/prof_lr.out
+exit $rc
