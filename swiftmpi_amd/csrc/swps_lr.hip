@@ -209,6 +209,95 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
   }
 }
 
+// k_lr_forward_r<R, LDS_SUM> with G row groups per wave: every group's loads, then every group's
+// weight gathers, then the ordered sums (the groups' chains interleaved) — G times the memory
+// chains in flight per wave, a G-th of the waves.  Same products, same feature-order fp32 sums:
+// bit-identical (SWPS_LR_FWD_G).
+template <int R, int G>
+__global__ __launch_bounds__(256) void k_lr_forward_g(const uint64_t *__restrict__ row_off,
+                                                      const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
+                                                      const float *__restrict__ label, uint64_t r0, uint64_t nr,
+                                                      const float *__restrict__ rows, int stride,
+                                                      float *__restrict__ err, float *__restrict__ err2) {
+  constexpr int L = 64 / R;
+  __shared__ float4 sp[4][G][R][(2 * L + 3) / 4];
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / L, k = lane - sub * L;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (wave * G * R >= nr) return;
+  uint64_t a[G];
+  int m[G];
+  float y[G];
+  bool act[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    const uint64_t j = (wave * G + g) * R + (uint64_t)sub;
+    act[g] = sub < R && j < nr;
+    a[g] = 0;
+    m[g] = 0;
+    y[g] = 0.f;
+    if (act[g]) {
+      a[g] = row_off[r0 + j];
+      m[g] = (int)(row_off[r0 + j + 1] - a[g]);
+      y[g] = label[r0 + j];
+    }
+  }
+  uint32_t i0[G], i1[G];
+  float x0[G], x1[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    const bool v0 = act[g] && k < m[g], v1 = act[g] && k + L < m[g];
+    i0[g] = v0 ? fidx[a[g] + k] : 0u;
+    x0[g] = v0 ? fval[a[g] + k] : 0.f;
+    i1[g] = v1 ? fidx[a[g] + k + L] : 0u;
+    x1[g] = v1 ? fval[a[g] + k + L] : 0.f;
+  }
+  float w0[G], w1[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    w0[g] = act[g] && k < m[g] ? weight_at(rows, i0[g], stride) : 0.f;
+    w1[g] = act[g] && k + L < m[g] ? weight_at(rows, i1[g], stride) : 0.f;
+  }
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    float *row = (float *)sp[threadIdx.x >> 6][g][sub < R ? sub : 0];
+    if (sub < R) {
+      row[k] = act[g] && k < m[g] ? w0[g] * x0[g] : 0.f;
+      row[k + L] = act[g] && k + L < m[g] ? w1[g] * x1[g] : 0.f;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (k != 0 || sub >= R) return;
+  float sum[G];
+  int mm = 0;
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    sum[g] = 0.f;
+    mm = max(mm, act[g] ? m[g] : 0);
+  }
+  for (int f4 = 0; f4 * 4 < mm; f4++) {
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      if (!act[g] || f4 * 4 >= m[g]) continue;
+      const float4 v = ((const float4 *)sp[threadIdx.x >> 6][g][sub])[f4];
+      sum[g] += v.x;
+      if (f4 * 4 + 1 < m[g]) sum[g] += v.y;
+      if (f4 * 4 + 2 < m[g]) sum[g] += v.z;
+      if (f4 * 4 + 3 < m[g]) sum[g] += v.w;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    if (!act[g]) continue;
+    const uint64_t j = (wave * G + g) * R + (uint64_t)sub;
+    const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum[g]))));
+    const float error = y[g] - predict;
+    err[r0 + j] = error;
+    err2[r0 + j] = error * error;
+  }
+}
+
 // One lane per example: the lane sums its own row in feature order (lr.cpp:
 // 358-375, fp32 products and adds, -ffp-contract=off: bit-identical to the
 // cross-lane forms above) — no readlane chain.  Per chunk of CH features the
@@ -1110,6 +1199,7 @@ struct swps_lr {
   // [nb+1] offsets of each batch's blocks (4 u32 each) / runs with several pieces / those with many
   std::vector<uint64_t> bchunk, bmulti, bmlong;  // (blocks: tile, first / end record, first / end piece)
   uint64_t max_bpiece = 0;
+  int fwd_groups = 2;            // SWPS_LR_FWD_G: row groups per wave in the forward (1, 2, 4; A/B: 2)
   int fwd_diag = 0;             // SWPS_LR_DIAG: timing experiments (1: forward without weight gather, 2: without ordered chain, 4: records without e gathers)
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
@@ -1463,7 +1553,18 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
   SWPS_TRY(l->d_val_s.ensure((l->max_bnnz + 4) * 4));
   const bool scat = l->fwd_records && l->rows_per_wave == 1 && mf <= 64;  // the forward writes the records
-  if (!scat && l->rows_per_wave == 1 && mf <= 42) {  // the default, its own start / end stamps when profiled
+  if (!scat && l->rows_per_wave == 1 && mf <= 42 && l->fwd_groups > 1 && !l->fwd_diag) {  // G groups per wave
+    hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
+    auto kf = l->fwd_groups == 4 ? k_lr_forward_g<3, 4> : k_lr_forward_g<3, 2>;
+    const uint64_t G = l->fwd_groups == 4 ? 4 : 2;
+    hipExtLaunchKernelGGL(kf, dim3((unsigned)nblk((nrb + 3 * G - 1) / (3 * G) * 64)), dim3(256), 0, s, fb, fe, 0,
+                          (const uint64_t *)l->d_row_off.as<uint64_t>(), fidx, (const float *)l->d_fval.as<float>(),
+                          (const float *)l->d_label.as<float>(), r0, nrb, (const float *)rows, stride,
+                          l->d_err.as<float>(), l->d_err2.as<float>());
+    l->timer.ext_end(0, fb, fe);
+    if (fb) (void)hipEventDestroy(e0);
+    e0 = nullptr;
+  } else if (!scat && l->rows_per_wave == 1 && mf <= 42) {  // its own start / end stamps when profiled
     hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
     hipExtLaunchKernelGGL(k_lr_forward_r<3, true>, dim3((unsigned)nblk((nrb + 2) / 3 * 64)), dim3(256), 0, s, fb, fe, 0,
                           (const uint64_t *)l->d_row_off.as<uint64_t>(), fidx, (const float *)l->d_fval.as<float>(),
@@ -1626,6 +1727,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   l->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);
+  if (const char *e = getenv("SWPS_LR_FWD_G")) l->fwd_groups = atoi(e);  // A/B, tests
   if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests
   if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests

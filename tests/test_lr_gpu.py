@@ -356,3 +356,37 @@ def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits, chunk):
         a = np.asarray(a, dtype=np.float64)
         b = np.asarray(b, dtype=np.float64)
         assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max(), (np.abs(a - b).max(), np.abs(a).max())
+
+
+@pytest.mark.parametrize("groups", ["2", "4"])
+def test_lr_forward_groups_bit_identical(lib, gpu, monkeypatch, groups):
+    """k_lr_forward_g (2 / 4 groups of 3 rows per wave, every group's loads and gathers issued
+    before the ordered sums) == k_lr_forward_r<3> bit for bit: Criteo-shaped rows (39 features),
+    the reference's data.txt and ragged rows of 1-42 features, fast and exact sums."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(9001, seed=5)
+    rng = np.random.default_rng(6)
+    lens = rng.integers(1, 43, 3001)
+    roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    feat = rng.integers(0, 4000, int(roff[-1])).astype(np.uint32)
+    vals = rng.random(int(roff[-1])).astype(np.float32)
+    yl = (rng.random(3001) < 0.5).astype(np.float32)
+    res = []
+    for g in ("1", groups):
+        monkeypatch.setenv("SWPS_LR_FWD_G", g)
+        out = []
+        for fast in (False, True):
+            for data, B in (((y, off, f, v), 1000), ((yl, roff, feat, vals), 499)):
+                t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+                m = lib.LR(t, minibatch=B, init_ref=False, fast_sums=fast)
+                m.load_csr(*data)
+                m.init()
+                out += [m.train(2), m.params()[1]]
+            t2 = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+            m2 = lib.LR(t2, minibatch=200, fast_sums=fast)
+            m2.load_text(DATA)
+            m2.init()
+            out += [m2.train(2), m2.params()[1]]
+        res.append(out)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
