@@ -774,18 +774,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3
   rw[RPT] = n == RPT && i0 + RPT < rec1 ? t.trow[i0 + RPT] : kTileHead;  // the next record: a head ends this thread's last run
   const uint64_t e0 = (uint64_t)tile << t.tb;
   const uint32_t ne = (uint32_t)min<uint64_t>(1ull << t.tb, t.nrb - e0);
-  if (!(t.diag & 16)) {  // the tile's slice of e: every load in flight, then the LDS stores
-    constexpr int KE = (1 << kTileMaxBits) / 256;
-    float ev[KE];
+  if (!(t.diag & 16)) {  // the tile's slice of e: 16-B loads from the aligned base below it, all in
+    // flight, then the LDS stores (err is allocated with 4 floats of slack past its last row)
+    constexpr int KE = ((1 << kTileMaxBits) + 4 + 1023) / 1024;
+    const uint64_t g0 = t.r0 + e0, gb = g0 & ~3ull;
+    const int sh = (int)(g0 - gb);
+    const uint32_t nq = (ne + sh + 3) / 4;
+    float4 ev[KE];
 #pragma unroll
     for (int k = 0; k < KE; k++) {
-      const uint32_t i = tid + k * 256;
-      ev[k] = i < ne ? t.err[t.r0 + e0 + i] : 0.f;
+      const uint32_t q = tid + k * 256;
+      ev[k] = q < nq ? ((const float4 *)(t.err + gb))[q] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int k = 0; k < KE; k++) {
-      const uint32_t i = tid + k * 256;
-      if (i < ne) es[i] = ev[k];
+      const int i = (int)(tid + k * 256) * 4 - sh;
+      if (i >= 0 && i < (int)ne) es[i] = ev[k].x;
+      if (i + 1 >= 0 && i + 1 < (int)ne) es[i + 1] = ev[k].y;
+      if (i + 2 >= 0 && i + 2 < (int)ne) es[i + 2] = ev[k].z;
+      if (i + 3 >= 0 && i + 3 < (int)ne) es[i + 3] = ev[k].w;
     }
   }
   __syncthreads();
@@ -1492,7 +1499,7 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   SWPS_TRY(upload(l->d_fvid, l->fvid, s));
   SWPS_TRY(upload(l->d_fval, l->fval, s));
   SWPS_TRY(l->d_vid_row.ensure(std::max<size_t>(1, l->vocab_keys.size()) * 4));
-  SWPS_TRY(l->d_err.ensure(std::max<uint64_t>(1, nr) * 4));
+  SWPS_TRY(l->d_err.ensure((std::max<uint64_t>(1, nr) + 4) * 4));  // + slack: k_lr_tiles' 16-B loads
   SWPS_TRY(l->d_err2.ensure(std::max<uint64_t>(1, nr) * 4));
   SWPS_TRY(lr_index(l));
   l->rows_mapped = false;
