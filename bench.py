@@ -791,7 +791,7 @@ def bench_other(args):
               "launches": push_n}
         tr, tsrc = pmc_traffic(dict(app="lr", lr_batch=args.lr_batch, exact=bool(args.lr_exact), world=world,
                                     sharded=dist is not None),
-                               {"forward": ("k_lr_forward_r", "k_lr_forward"),
+                               {"forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_g"),
                                 "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
                                          "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin")})
         for kd, name in ((kf, "forward"), (kp, "push")):

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GROUPS = {  # kernel base names of each roofline group
     "w2v": ("k_gather_b", "k_combine_b", "k_push_b", "k_gather_t", "k_combine", "k_push_thp", "k_gather", "k_push",
             "k_push_tg"),
-    "lr_forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_l"),
+    "lr_forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_l", "k_lr_forward_g"),
     "lr_push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long", "k_lr_reduce_long_fast",
                 "k_lr_tiles", "k_lr_tiles_fin"),
     "s2v": ("k_s2v_docs",),
