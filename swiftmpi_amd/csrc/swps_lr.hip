@@ -753,12 +753,13 @@ __device__ __forceinline__ void seg_after(bool fp, double vp, int cp, uint32_t h
   h = max(h, hp);
 }
 
-template <int RPT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3 : RPT > 4 ? 6 : 8))) void k_lr_tiles(LrReduce a, LrTiles t) {
+template <int RPT, int BS = 256>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3 : RPT > 4 ? 6 : 8))) void k_lr_tiles(LrReduce a, LrTiles t) {
+  constexpr int NW = BS / 64;
   __shared__ float es[1 << kTileMaxBits];
-  __shared__ double wv[4];
-  __shared__ int wf[4], wc[4];
-  __shared__ uint32_t wh[4];
+  __shared__ double wv[NW];
+  __shared__ int wf[NW], wc[NW];
+  __shared__ uint32_t wh[NW];
   const uint32_t *ch = t.chunk + (uint64_t)blockIdx.x * 5;
   const uint32_t tile = ch[0], rec0 = ch[1], rec1 = ch[2], piece0 = ch[3];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -776,19 +777,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3
   const uint32_t ne = (uint32_t)min<uint64_t>(1ull << t.tb, t.nrb - e0);
   if (!(t.diag & 16)) {  // the tile's slice of e: 16-B loads from the aligned base below it, all in
     // flight, then the LDS stores (err is allocated with 4 floats of slack past its last row)
-    constexpr int KE = ((1 << kTileMaxBits) + 4 + 1023) / 1024;
+    constexpr int KE = ((1 << kTileMaxBits) + 4 + 4 * BS - 1) / (4 * BS);
     const uint64_t g0 = t.r0 + e0, gb = g0 & ~3ull;
     const int sh = (int)(g0 - gb);
     const uint32_t nq = (ne + sh + 3) / 4;
     float4 ev[KE];
 #pragma unroll
     for (int k = 0; k < KE; k++) {
-      const uint32_t q = tid + k * 256;
+      const uint32_t q = tid + k * BS;
       ev[k] = q < nq ? ((const float4 *)(t.err + gb))[q] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int k = 0; k < KE; k++) {
-      const int i = (int)(tid + k * 256) * 4 - sh;
+      const int i = (int)(tid + k * BS) * 4 - sh;
       if (i >= 0 && i < (int)ne) es[i] = ev[k].x;
       if (i + 1 >= 0 && i + 1 < (int)ne) es[i + 1] = ev[k].y;
       if (i + 2 >= 0 && i + 2 < (int)ne) es[i + 2] = ev[k].z;
@@ -1198,7 +1199,7 @@ struct swps_lr {
   // fast sums through row tiles (k_lr_tiles): SWPS_LR_TILES=0 for the record path (A/B, tests);
   // SWPS_LR_TILE_BITS shrinks the tiles (tests: many pieces per key)
   int tiles = 1, tile_bits = kTileMaxBits;
-  uint32_t tile_chunk = kTileChunk;
+  uint32_t tile_chunk = kTileChunk, tile_threads = 256;
   bool tiles_ready = false;
   DevMem d_trow, d_tval, d_tinfo, d_tslot, d_tgrun, d_tdst, d_tchunk, d_tnp, d_tpst, d_tmulti, d_tmlong, d_tpart;
   DevMem d_tmsrow, d_tmlrow;
@@ -1645,11 +1646,14 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     hipEvent_t tb0 = l->timer.ext(), te0 = l->timer.ext();
     const bool fin = l->bmulti[bi + 1] > l->bmulti[bi] || l->bmlong[bi + 1] > l->bmlong[bi];
     if (nch) {
-      auto kt = l->tile_chunk == 512    ? k_lr_tiles<2>
+      const bool b512 = l->tile_threads == 512;  // 4 records per thread, 512 threads: 2,048-record blocks
+      auto kt = b512                    ? k_lr_tiles<4, 512>
+                : l->tile_chunk == 512  ? k_lr_tiles<2>
                 : l->tile_chunk == 1024 ? k_lr_tiles<4>
                 : l->tile_chunk == 4096 ? k_lr_tiles<16>
                                         : k_lr_tiles<8>;
-      hipExtLaunchKernelGGL(kt, dim3(nch), dim3(256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0, ra, tt);
+      hipExtLaunchKernelGGL(kt, dim3(nch), dim3(b512 ? 512 : 256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0,
+                            ra, tt);
     }
     const uint32_t nl = (uint32_t)(l->bmlong[bi + 1] - l->bmlong[bi]);
     if (nm || nl) {
@@ -1742,6 +1746,10 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_TILE_CHUNK")) {
     const int c = atoi(e);
     l->tile_chunk = c == 512 || c == 2048 || c == 4096 ? (uint32_t)c : kTileChunk;
+  }
+  if (const char *e = getenv("SWPS_LR_TILE_THREADS")) {  // 512: blocks of 2,048 records, 4 per thread (A/B)
+    l->tile_threads = atoi(e) == 512 ? 512 : 256;
+    if (l->tile_threads == 512) l->tile_chunk = 2048;
   }
   if (const char *e = getenv("SWPS_LR_TILE_BITS")) l->tile_bits = std::min(std::max(atoi(e), 4), kTileMaxBits);
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {

@@ -317,7 +317,7 @@ def test_lr_forward_records_bit_identical(lib, gpu, monkeypatch, env, fast):
 
 
 @pytest.mark.parametrize("bits,chunk", [(None, None), ("6", None), ("4", None), (None, "512"), (None, "2048"),
-                                        (None, "4096")])
+                                        (None, "4096"), (None, "t512")])
 def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits, chunk):
     """Fast sums through row tiles (k_lr_tiles + k_lr_tiles_fin: e read from an LDS slice, a
     block-wide segmented scan over 1,024 records, one fp64 partial per piece = a key's records
@@ -337,7 +337,9 @@ def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits, chunk):
     yl = (rng.random(4000) < 0.5).astype(np.float32)
     if bits:
         monkeypatch.setenv("SWPS_LR_TILE_BITS", bits)
-    if chunk:  # blocks of 512 / 2,048 / 4,096 records (2 / 8 / 16 per thread; default 1,024)
+    if chunk == "t512":  # 512-thread blocks of 2,048 records
+        monkeypatch.setenv("SWPS_LR_TILE_THREADS", "512")
+    elif chunk:  # blocks of 512 / 2,048 / 4,096 records (2 / 8 / 16 per thread; default 1,024)
         monkeypatch.setenv("SWPS_LR_TILE_CHUNK", chunk)
     res = []
     for tiles in ("0", "1", "1"):
