@@ -58,3 +58,36 @@ def test_bench_pmc_lookup_matches_config_and_kernel_base_names(tmp_path, monkeyp
     assert res == {"sum": 12.0, "forward": 11.0} and "r03_pmc_x.json" in src
     res, src = b.pmc_traffic({"app": "w2v", "mode": "bfp32", "sharded": True}, {"sum": ("k_gather_b",)})
     assert res == {"sum": None} and src is None  # a sharded line never borrows the unsharded counters
+
+
+def test_bench_lr_tile_pieces_matches_a_loop_restatement():
+    """bench.lr_tile_pieces (the LR row-tile path's pieces and partials, for its algorithmic
+    bytes) against a plain loop over the same definition: records in (tile, key) order, row
+    order inside a key; blocks of `chunk` records per tile; a piece = a key's records in one
+    block; partials = the pieces of keys with more than one."""
+    import importlib.util
+    import numpy as np
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 9, 700)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    f = (rng.zipf(1.3, int(off[-1])) % 50).astype(np.uint32)
+    for r0, r1, tb, ch in ((0, 700, 6, 16), (100, 613, 5, 7), (0, 700, 12, 1024)):
+        recs = []
+        for r in range(r0, r1):
+            for c in range(int(off[r]), int(off[r + 1])):
+                recs.append((((r - r0) >> tb), int(f[c]), r))
+        recs.sort(key=lambda t: (t[0], t[1], t[2]))
+        pieces, seen, start, prev = [], {}, {}, None
+        for pos, (t, k, _) in enumerate(recs):
+            start.setdefault(t, pos)
+            blk = (pos - start[t]) // ch
+            if (t, blk, k) != prev:
+                pieces.append(k)
+                prev = (t, blk, k)
+        for k in pieces:
+            seen[k] = seen.get(k, 0) + 1
+        exp = (len(pieces), sum(n for n in seen.values() if n > 1))
+        assert b.lr_tile_pieces(f, off, r0, r1, tile_bits=tb, chunk=ch) == exp
