@@ -352,8 +352,12 @@ int ShardDriver::steps(uint64_t count) {
       split_steps++;
     } else {
       if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, key_cache ? (int64_t)(3 * st) : -1));
-      SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, vals.p));
-      SWPS_TRY(exchange(vals.p, rk, mv, sk, vb, S));
+      if (alias && key_cache && ops.pull_in_place && ops.set_slot) {  // world 1: the step reads the shard
+        SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, nullptr));
+      } else {
+        SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, vals.p));
+        SWPS_TRY(exchange(vals.p, rk, mv, sk, vb, S));
+      }
     }
     SWPS_HIP(hipEventRecord(ev_pull, S));
     // ---- C: learn(i), then prep(i+1) ----

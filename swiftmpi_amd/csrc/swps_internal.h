@@ -239,6 +239,9 @@ struct AppOps {
   int (*request)(void *, int32_t, uint64_t *, uint64_t *, uint64_t *) = nullptr;
   int (*serve_pull)(void *, const uint64_t *, const uint64_t *, int32_t, void *) = nullptr;
   int (*install)(void *, const void *) = nullptr;
+  // optional: at world 1 with the key cache, serve_pull(..., nullptr) only looks the slot's rows up
+  // and the step's install reads them from the shard in place (no value copy)
+  bool pull_in_place = false;
   int (*step)(void *, const void *, void *) = nullptr;
   int (*serve_push)(void *, const uint64_t *, const void *, const uint64_t *) = nullptr;
   int (*prep)(void *) = nullptr;                      // optional: the next step's param-free half

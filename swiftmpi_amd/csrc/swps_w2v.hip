@@ -1878,17 +1878,20 @@ inline int bfp_shape(int D) {
 
 // requester side of a sharded pull: the owners' pull values [U][h|v] (K order)
 // into the worker cache (global_pull_access.h:88-97: params[key] = val)
+// srow != nullptr (world 1, the pull read in place): value u is the table row srow[u] of vals
+// (the shard rows, [h | v | h2 | v2]: its first 2D elements)
 template <typename T>
 __global__ __launch_bounds__(256) void k_install(const int32_t *__restrict__ K, uint32_t U, const T *__restrict__ vals,
                                                  int D, T *__restrict__ cache_h, T *__restrict__ cache_v,
-                                                 int32_t *__restrict__ local, int set_local, int cs) {
+                                                 int32_t *__restrict__ local, int set_local, int cs,
+                                                 const uint32_t *__restrict__ srow = nullptr) {
   using V = typename V16<T>::V;
   constexpr int E = V16<T>::E;
   const int lane = threadIdx.x & 63;
   const int NC = D / E;
   for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += (uint64_t)gridDim.x * 4) {
     const int32_t vid = K[u];
-    const V *src = (const V *)(vals + u * 2 * D);
+    const V *src = (const V *)(vals + (srow ? (uint64_t)srow[u] * 4 : u * 2) * D);
     V *dh = (V *)(cache_h + (uint64_t)vid * cs);  // cs: the cache row stride (swps_w2v::cs)
     V *dv = (V *)(cache_v + (uint64_t)vid * cs);
     for (int c = lane; c < cs / E; c += 64) {  // the pad too (zeros): whole-line stores
@@ -2111,6 +2114,7 @@ struct swps_w2v {
   DevMem d_vkeys, d_init_order, d_serve_rows, d_push_rows;
   DevMem d_mark;          // late_mask: a stamp per table row
   // the next step's pull values in two parts (AppOps::install_parts; consumed by that step)
+  const uint32_t *pull_rows = nullptr;  // world 1: the slot's shard rows, read in place by the step's install
   struct Parts {
     const void *vals[2] = {nullptr, nullptr};
     const uint32_t *pos[2] = {nullptr, nullptr};
@@ -3587,10 +3591,15 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
           k_install_idx<T><<<nblk((uint64_t)w->parts.n[q] * 64), 256, 0, s>>>(
               K, w->parts.pos[q], (uint32_t)w->parts.n[q], (const T *)w->parts.vals[q], D, w->d_cache_h.as<T>(),
               w->d_cache_v.as<T>(), w->cs);
+    } else if (w->pull_rows) {  // world 1: straight from the shard rows the serve looked up
+      k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, w->t->rows.as<T>(), D, w->d_cache_h.as<T>(),
+                                                          w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0, w->cs,
+                                                          w->pull_rows);
     } else {
       k_install<T><<<nblk((uint64_t)U * 64), 256, 0, s>>>(K, U, (const T *)d_vals, D, w->d_cache_h.as<T>(),
                                                           w->d_cache_v.as<T>(), w->d_local.as<int32_t>(), 0, w->cs);
     }
+    w->pull_rows = nullptr;
     w->parts = swps_w2v::Parts{};
     SWPS_HIP(hipGetLastError());
     tm.end(KT_PULL, e, s);
@@ -4493,8 +4502,14 @@ int swps_w2v_serve_pull(swps_w2v *w, const uint64_t *d_keys, const uint64_t *src
       e.n = n;
       e.sorted_valid = false;
     }
+    if (!d_vals && n) {  // the driver's in-place pull (AppOps::pull_in_place): the step's install reads
+      if (w->world != 1) return fail(SWPS_E_STATE, "an in-place pull needs world 1");
+      w->pull_rows = e.rows.as<uint32_t>();  // these rows of the shard itself
+      return SWPS_OK;
+    }
     return table_copy_pull(w->t, e.rows.as<uint32_t>(), n, d_vals, ss);
   }
+  if (!d_vals && n) return fail(SWPS_E_STATE, "serve_pull without a value buffer needs a world-1 driver step slot");
   if (insert) {  // keys are distinct within a source, not across sources
     uint64_t off = 0;
     for (int r = 0; r < w->world; r++) {
@@ -4609,6 +4624,9 @@ int swps_w2v_shard_comm(swps_w2v *w, swps_comm *c, int32_t frag_num) {
     return swps_w2v_serve_pull((swps_w2v *)h, k, sc, ins, v);
   };
   o.install = [](void *h, const void *v) { return swps_w2v_install_init((swps_w2v *)h, v); };
+  // world 1: the step installs from the shard (serve_pull with no value buffer); SWPS_PULL_IN_PLACE=0: off (A/B)
+  const char *pip = getenv("SWPS_PULL_IN_PLACE");
+  o.pull_in_place = !(pip && atoi(pip) == 0);
   o.step = [](void *h, const void *v, void *g) { return swps_w2v_step((swps_w2v *)h, v, g); };
   o.serve_push = [](void *h, const uint64_t *k, const void *g, const uint64_t *sc) {
     return swps_w2v_serve_push((swps_w2v *)h, k, g, sc);
