@@ -381,6 +381,20 @@ __global__ void k_lr_idx_slots(const uint64_t *__restrict__ ks, const uint32_t *
   head[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1u : 0u;
 }
 
+// every record's run (global index): the forward's staged weights (SWPS_LR_STAGE)
+__global__ void k_lr_idx_frun(const uint32_t *__restrict__ perm, const uint32_t *__restrict__ rid1, uint64_t n,
+                              uint32_t *__restrict__ frun) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) frun[perm[i]] = rid1[i] - 1;
+}
+// the batch's weights, one per run (key), dense: the forward gathers from these 4 B x runs
+// (L2-resident) instead of the shard's 8-B rows across the table
+__global__ void k_lr_stage(const uint32_t *__restrict__ urow, uint32_t nruns, const float *__restrict__ rows,
+                           float *__restrict__ wd) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < nruns) wd[r] = rows[(uint64_t)urow[r] * 2];
+}
+
 // shard row of every record's feature / every run's key (single GPU)
 __global__ void k_lr_map_rows(const int32_t *__restrict__ vid, uint64_t n, const uint32_t *__restrict__ vid_row,
                               uint32_t *__restrict__ out) {
@@ -1207,6 +1221,9 @@ struct swps_lr {
   // [nb+1] offsets of each batch's blocks (4 u32 each) / runs with several pieces / those with many
   std::vector<uint64_t> bchunk, bmulti, bmlong;  // (blocks: tile, first / end record, first / end piece)
   uint64_t max_bpiece = 0;
+  int stage = 0;                // SWPS_LR_STAGE: the forward reads the batch's weights staged densely (k_lr_stage)
+  DevMem d_frun, d_wstage;
+  uint64_t max_bruns = 0;
   int fwd_groups = 2;            // SWPS_LR_FWD_G: row groups per wave in the forward (1, 2, 4; A/B: 2)
   int fwd_diag = 0;             // SWPS_LR_DIAG: timing experiments (1: forward without weight gather, 2: without ordered chain, 4: records without e gathers)
   uint64_t max_bnnz = 0;
@@ -1443,6 +1460,9 @@ int lr_index(swps_lr *l) {
                                           head.as<uint32_t>(), l->d_spos.as<uint32_t>());
   SWPS_HIP(hipGetLastError());
   SWPS_TRY(lr_scan_incl(head.as<uint32_t>(), rid1.as<uint32_t>(), n, tmp, s));
+  SWPS_TRY(l->d_frun.ensure(n * 4));
+  k_lr_idx_frun<<<nblk(n), 256, 0, s>>>(perm.as<uint32_t>(), rid1.as<uint32_t>(), n, l->d_frun.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
   uint32_t R = 0;
   SWPS_HIP(hipMemcpyAsync(&R, rid1.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipStreamSynchronize(s));
@@ -1462,6 +1482,8 @@ int lr_index(swps_lr *l) {
   SWPS_HIP(hipGetLastError());
   SWPS_HIP(hipMemcpyAsync(l->brun.data(), d_brun.p, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipStreamSynchronize(s));
+  l->max_bruns = 0;
+  for (uint64_t b = 0; b < nb; b++) l->max_bruns = std::max<uint64_t>(l->max_bruns, l->brun[b + 1] - l->brun[b]);
   // every batch's long runs (> kLrShort records), relative to its first run: k_lr_reduce_fused
   {
     std::vector<uint32_t> cnt(R);
@@ -1565,10 +1587,24 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
     auto kf = l->fwd_groups == 4 ? k_lr_forward_g<3, 4> : k_lr_forward_g<3, 2>;
     const uint64_t G = l->fwd_groups == 4 ? 4 : 2;
-    hipExtLaunchKernelGGL(kf, dim3((unsigned)nblk((nrb + 3 * G - 1) / (3 * G) * 64)), dim3(256), 0, s, fb, fe, 0,
-                          (const uint64_t *)l->d_row_off.as<uint64_t>(), fidx, (const float *)l->d_fval.as<float>(),
-                          (const float *)l->d_label.as<float>(), r0, nrb, (const float *)rows, stride,
-                          l->d_err.as<float>(), l->d_err2.as<float>());
+    const float *fw = rows;
+    const uint32_t *fi = fidx;
+    int fs = stride;
+    const uint32_t nruns = (uint32_t)(l->brun[bi + 1] - l->brun[bi]);
+    if (l->stage && !l->sharded && nruns) {  // the batch's weights staged densely (stamped with the forward)
+      SWPS_TRY(l->d_wstage.ensure((uint64_t)l->max_bruns * 4));
+      hipExtLaunchKernelGGL(k_lr_stage, dim3(nblk(nruns)), dim3(256), 0, s, fb, (hipEvent_t) nullptr, 0,
+                            (const uint32_t *)(l->d_urow.as<uint32_t>() + l->brun[bi]), nruns, (const float *)rows,
+                            l->d_wstage.as<float>());
+      fw = l->d_wstage.as<float>() - l->brun[bi];  // indexed by the records' global run
+      fi = l->d_frun.as<uint32_t>();
+      fs = 1;
+    }
+    hipExtLaunchKernelGGL(kf, dim3((unsigned)nblk((nrb + 3 * G - 1) / (3 * G) * 64)), dim3(256), 0, s,
+                          l->stage && !l->sharded && nruns ? (hipEvent_t) nullptr : fb, fe, 0,
+                          (const uint64_t *)l->d_row_off.as<uint64_t>(), fi, (const float *)l->d_fval.as<float>(),
+                          (const float *)l->d_label.as<float>(), r0, nrb, fw, fs, l->d_err.as<float>(),
+                          l->d_err2.as<float>());
     l->timer.ext_end(0, fb, fe);
     if (fb) (void)hipEventDestroy(e0);
     e0 = nullptr;
@@ -1739,6 +1775,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);
   if (const char *e = getenv("SWPS_LR_FWD_G")) l->fwd_groups = atoi(e);  // A/B, tests
+  if (const char *e = getenv("SWPS_LR_STAGE")) l->stage = atoi(e);        // A/B, tests
   if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests
   if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
