@@ -213,18 +213,27 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
 // weight gathers, then the ordered sums (the groups' chains interleaved) — G times the memory
 // chains in flight per wave, a G-th of the waves.  Same products, same feature-order fp32 sums:
 // bit-identical (SWPS_LR_FWD_G).
+// hrow != nullptr (single GPU): the batch's kLrHot hottest keys' shard rows; fidx codes a record of
+// one of them as kLrHotBit | rank, and the block reads its weight from LDS (loaded once per block)
+constexpr int kLrHot = 256;
+constexpr uint32_t kLrHotBit = 0x80000000u;
 template <int R, int G>
 __global__ __launch_bounds__(256) void k_lr_forward_g(const uint64_t *__restrict__ row_off,
                                                       const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
                                                       const float *__restrict__ label, uint64_t r0, uint64_t nr,
                                                       const float *__restrict__ rows, int stride,
-                                                      float *__restrict__ err, float *__restrict__ err2) {
+                                                      float *__restrict__ err, float *__restrict__ err2,
+                                                      const uint32_t *__restrict__ hrow = nullptr, uint32_t nhot = 0) {
   constexpr int L = 64 / R;
   __shared__ float4 sp[4][G][R][(2 * L + 3) / 4];
+  __shared__ float wh[kLrHot];
+  // the hot weights' loads go out first; their LDS stores and the block barrier come after this
+  // thread's own index loads (every wave reaches the barrier: rows past the batch are inactive)
+  const float hw = hrow && threadIdx.x < nhot ? rows[(uint64_t)hrow[threadIdx.x] * 2] : 0.f;
   const int lane = threadIdx.x & 63;
   const int sub = lane / L, k = lane - sub * L;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (wave * G * R >= nr) return;
+  if (!hrow && wave * G * R >= nr) return;
   uint64_t a[G];
   int m[G];
   float y[G];
@@ -252,11 +261,21 @@ __global__ __launch_bounds__(256) void k_lr_forward_g(const uint64_t *__restrict
     i1[g] = v1 ? fidx[a[g] + k + L] : 0u;
     x1[g] = v1 ? fval[a[g] + k + L] : 0.f;
   }
+  if (hrow) {
+    if (threadIdx.x < nhot) wh[threadIdx.x] = hw;
+    __syncthreads();
+  }
   float w0[G], w1[G];
 #pragma unroll
   for (int g = 0; g < G; g++) {
-    w0[g] = act[g] && k < m[g] ? weight_at(rows, i0[g], stride) : 0.f;
-    w1[g] = act[g] && k + L < m[g] ? weight_at(rows, i1[g], stride) : 0.f;
+    if (hrow) {
+      w0[g] = act[g] && k < m[g] ? ((i0[g] & kLrHotBit) ? wh[i0[g] & (kLrHotBit - 1)] : rows[(uint64_t)i0[g] * 2]) : 0.f;
+      w1[g] = act[g] && k + L < m[g] ? ((i1[g] & kLrHotBit) ? wh[i1[g] & (kLrHotBit - 1)] : rows[(uint64_t)i1[g] * 2])
+                                     : 0.f;
+    } else {
+      w0[g] = act[g] && k < m[g] ? weight_at(rows, i0[g], stride) : 0.f;
+      w1[g] = act[g] && k + L < m[g] ? weight_at(rows, i1[g], stride) : 0.f;
+    }
   }
 #pragma unroll
   for (int g = 0; g < G; g++) {
@@ -393,6 +412,22 @@ __global__ void k_lr_stage(const uint32_t *__restrict__ urow, uint32_t nruns, co
                            float *__restrict__ wd) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < nruns) wd[r] = rows[(uint64_t)urow[r] * 2];
+}
+
+// single GPU, once the shard rows are known: a record of one of its batch's hot keys is coded
+// kLrHotBit | rank (k_lr_forward_g reads it from LDS), any other by its key's shard row; the hot
+// keys' shard rows per batch
+__global__ void k_lr_hot_codes(const uint32_t *__restrict__ frun, const int32_t *__restrict__ hot_of_run,
+                               const uint32_t *__restrict__ frow, uint64_t n, uint32_t *__restrict__ code) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const int32_t h = hot_of_run[frun[c]];
+  code[c] = h >= 0 ? (kLrHotBit | (uint32_t)h) : frow[c];
+}
+__global__ void k_lr_hot_rows(const uint32_t *__restrict__ hgrun, uint64_t n, const uint32_t *__restrict__ urow,
+                              uint32_t *__restrict__ hrow) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) hrow[q] = urow[hgrun[q]];
 }
 
 // shard row of every record's feature / every run's key (single GPU)
@@ -1223,6 +1258,9 @@ struct swps_lr {
   uint64_t max_bpiece = 0;
   int stage = 0;                // SWPS_LR_STAGE: the forward reads the batch's weights staged densely (k_lr_stage)
   DevMem d_frun, d_wstage;
+  int hot = 0;  // SWPS_LR_HOT: the forward reads the batch's hot keys' weights from LDS (k_lr_forward_g)
+  DevMem d_hot_of_run, d_hgrun, d_hrow, d_fhot;
+  std::vector<uint32_t> bnhot;
   uint64_t max_bruns = 0;
   int fwd_groups = 2;            // SWPS_LR_FWD_G: row groups per wave in the forward (1, 2, 4; A/B: 2)
   int fwd_diag = 0;             // SWPS_LR_DIAG: timing experiments (1: forward without weight gather, 2: without ordered chain, 4: records without e gathers)
@@ -1498,6 +1536,27 @@ int lr_index(swps_lr *l) {
     l->blong[nb] = lst.size();
     if (lst.empty()) lst.push_back(0);
     SWPS_TRY(upload(l->d_slong, lst, s));
+    // every batch's kLrHot most frequent keys (runs of at least 8 records): the forward's LDS weights
+    std::vector<int32_t> hot_of_run(std::max<uint64_t>(R, 1), -1);
+    std::vector<uint32_t> hgrun(std::max<uint64_t>(nb, 1) * kLrHot, 0);
+    l->bnhot.assign(nb, 0);
+    std::vector<uint32_t> ord;
+    for (uint64_t b = 0; b < nb; b++) {
+      ord.clear();
+      for (uint64_t q = l->brun[b]; q < l->brun[b + 1]; q++)
+        if (cnt[q] >= 8) ord.push_back((uint32_t)q);
+      const size_t h = std::min<size_t>(ord.size(), kLrHot);
+      std::partial_sort(ord.begin(), ord.begin() + h, ord.end(), [&](uint32_t x, uint32_t y) {
+        return cnt[x] != cnt[y] ? cnt[x] > cnt[y] : x < y;
+      });
+      for (size_t i = 0; i < h; i++) {
+        hot_of_run[ord[i]] = (int32_t)i;
+        hgrun[b * kLrHot + i] = ord[i];
+      }
+      l->bnhot[b] = (uint32_t)h;
+    }
+    SWPS_TRY(upload(l->d_hot_of_run, hot_of_run, s));
+    SWPS_TRY(upload(l->d_hgrun, hgrun, s));
     SWPS_HIP(hipStreamSynchronize(s));
   }
   l->tiles_ready = false;
@@ -1559,6 +1618,14 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     k_lr_map_rows<<<nblk(R), 256, 0, s>>>((const int32_t *)l->d_ruk.as<uint32_t>(), R, l->d_vid_row.as<uint32_t>(),
                                           l->d_urow.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
+    if (l->hot && !l->bnhot.empty()) {
+      SWPS_TRY(l->d_fhot.ensure(std::max<uint64_t>(n, 1) * 4));
+      SWPS_TRY(l->d_hrow.ensure(std::max<uint64_t>(l->nbatches, 1) * kLrHot * 4));
+      k_lr_hot_codes<<<nblk(n), 256, 0, s>>>(l->d_frun.as<uint32_t>(), l->d_hot_of_run.as<int32_t>(),
+                                              l->d_frow.as<uint32_t>(), n, l->d_fhot.as<uint32_t>());
+      k_lr_hot_rows<<<nblk(l->nbatches * kLrHot), 256, 0, s>>>(l->d_hgrun.as<uint32_t>(), l->nbatches * kLrHot,
+                                                                l->d_urow.as<uint32_t>(), l->d_hrow.as<uint32_t>());
+    }
     if (l->tiles_ready && l->tile_npieces)
       k_lr_tile_dst<<<nblk(l->tile_npieces), 256, 0, s>>>(l->d_tinfo.as<uint32_t>(), l->d_tslot.as<uint32_t>(),
                                                            l->d_tgrun.as<uint32_t>(), l->tile_npieces,
@@ -1600,11 +1667,15 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
       fi = l->d_frun.as<uint32_t>();
       fs = 1;
     }
+    const bool hot = l->hot && !l->sharded && !(l->stage && nruns) && !l->bnhot.empty() && l->bnhot[bi];
+    if (hot) fi = l->d_fhot.as<uint32_t>();
     hipExtLaunchKernelGGL(kf, dim3((unsigned)nblk((nrb + 3 * G - 1) / (3 * G) * 64)), dim3(256), 0, s,
                           l->stage && !l->sharded && nruns ? (hipEvent_t) nullptr : fb, fe, 0,
                           (const uint64_t *)l->d_row_off.as<uint64_t>(), fi, (const float *)l->d_fval.as<float>(),
                           (const float *)l->d_label.as<float>(), r0, nrb, fw, fs, l->d_err.as<float>(),
-                          l->d_err2.as<float>());
+                          l->d_err2.as<float>(),
+                          hot ? (const uint32_t *)(l->d_hrow.as<uint32_t>() + bi * kLrHot) : (const uint32_t *)nullptr,
+                          hot ? l->bnhot[bi] : 0u);
     l->timer.ext_end(0, fb, fe);
     if (fb) (void)hipEventDestroy(e0);
     e0 = nullptr;
@@ -1776,6 +1847,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);
   if (const char *e = getenv("SWPS_LR_FWD_G")) l->fwd_groups = atoi(e);  // A/B, tests
   if (const char *e = getenv("SWPS_LR_STAGE")) l->stage = atoi(e);        // A/B, tests
+  if (const char *e = getenv("SWPS_LR_HOT")) l->hot = atoi(e);            // A/B, tests
   if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests
   if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests

@@ -360,13 +360,15 @@ def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits, chunk):
         assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max(), (np.abs(a - b).max(), np.abs(a).max())
 
 
-@pytest.mark.parametrize("groups,stage", [("2", "1"), ("4", "1"), ("2", "0")])
-def test_lr_forward_groups_bit_identical(lib, gpu, monkeypatch, groups, stage):
+@pytest.mark.parametrize("groups,stage,hot", [("2", "0", "1"), ("4", "0", "1"), ("2", "1", "0"), ("2", "0", "0")])
+def test_lr_forward_groups_bit_identical(lib, gpu, monkeypatch, groups, stage, hot):
     """k_lr_forward_g (2 / 4 groups of 3 rows per wave, every group's loads and gathers issued
-    before the ordered sums; reading the batch's weights staged densely by k_lr_stage, or the
-    shard rows) == k_lr_forward_r<3> on the shard rows, bit for bit: Criteo-shaped rows (39
-    features), the reference's data.txt and ragged rows of 1-42 features, fast and exact sums."""
+    before the ordered sums; the batch's 256 hottest keys' weights from LDS, or the batch's
+    weights staged densely by k_lr_stage, or the shard rows) == k_lr_forward_r<3> on the shard
+    rows, bit for bit: Criteo-shaped rows (39 features), the reference's data.txt and ragged rows
+    of 1-42 features, fast and exact sums."""
     monkeypatch.setenv("SWPS_LR_STAGE", stage)
+    monkeypatch.setenv("SWPS_LR_HOT", hot)
     from swiftmpi_amd.synth import criteo
     y, off, f, v = criteo(9001, seed=5)
     rng = np.random.default_rng(6)
