@@ -1258,7 +1258,7 @@ struct swps_lr {
   uint64_t max_bpiece = 0;
   int stage = 0;                // SWPS_LR_STAGE: the forward reads the batch's weights staged densely (k_lr_stage)
   DevMem d_frun, d_wstage;
-  int hot = 0;  // SWPS_LR_HOT: the forward reads the batch's hot keys' weights from LDS (k_lr_forward_g)
+  int hot = 1;  // SWPS_LR_HOT: the forward reads the batch's hot keys' weights from LDS (k_lr_forward_g)
   DevMem d_hot_of_run, d_hgrun, d_hrow, d_fhot;
   std::vector<uint32_t> bnhot;
   uint64_t max_bruns = 0;
