@@ -55,12 +55,14 @@ def lr_tile_pieces(f, off, r0, r1, tile_bits=12, chunk=1024):
 def pmc_traffic(config, groups):
     """HBM bytes per launch of kernel groups (one launch of each kernel per
     step), from the committed PMC summary of this exact workload
-    (profiles/r03_pmc_*.json, written by scripts/pmc_summary.py from separate
+    (profiles/rNN_pmc_*.json, written by scripts/pmc_summary.py from separate
     rocprofv3 --pmc passes of the same command; read requests counted by size
     + WRITE_SIZE).  groups: name -> kernel base names (template arguments
     dropped).  Returns ({name: bytes or None}, source or None)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r03_pmc_*.json"))):
+    # the newest round's summaries first (profiles/rNN_pmc_<leg>.json)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_*.json")),
+                       key=lambda q: (-int(os.path.basename(q)[1:3]), q)):
         try:
             prof = json.load(open(path))
         except (OSError, ValueError):
@@ -196,23 +198,19 @@ def cpu_baseline_config1(ids, off, args, lines):
 
 def cpu_baseline_lr(y, off, f, v, minibatch, lr, rows):
     """The oracle's LR (lr.cpp semantics, nthreads = 1, fp32) on the first
-    `rows` rows of the same synthetic Criteo-shaped data, one epoch."""
+    `rows` rows of the same synthetic Criteo-shaped data, one epoch (the rows
+    handed over as arrays: the parse is not part of the timed training)."""
     import oracle
     oracle.build()
     rows = min(rows, len(y))
-    with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "lr.txt")
-        with open(path, "w") as fh:
-            for r in range(rows):
-                a, b = int(off[r]), int(off[r + 1])
-                fh.write("%g %s\n" % (y[r], " ".join("%d:%g" % (k, x) for k, x in zip(f[a:b], v[a:b]))))
-        m = oracle.LR(path, minibatch=minibatch, lr=lr)
-        t0 = time.perf_counter()
-        m.train(1)
-        dt = time.perf_counter() - t0
+    n = int(off[rows])
+    m = oracle.LR.from_csr(y[:rows], off[:rows + 1], f[:n], v[:n], minibatch=minibatch, lr=lr)
+    t0 = time.perf_counter()
+    m.train(1)
+    dt = time.perf_counter() - t0
     return {"value": rows / dt, "unit": "examples/s", "cores": 1, "kind": "port",
-            "sample": "oracle/swps_oracle.cpp LR (fp32, nthreads=1 semantics) on the first %d rows of the same "
-                      "data, minibatch %d, 1 epoch; %.1f s" % (rows, minibatch, dt)}
+            "sample": "oracle/swps_oracle.cpp LR (fp32, nthreads=1 semantics) on the first %d rows (%d features) "
+                      "of the same data, minibatch %d, 1 epoch; %.1f s" % (rows, n, minibatch, dt)}
 
 
 def cpu_baseline_s2v(toks, off, args, docs):
@@ -304,6 +302,9 @@ def main():
     ap.add_argument("--lr-exact", action="store_true",
                     help="LR: the reference's sequential fp32 per-key sums (bit-exact) instead of fast fp64 sums")
     ap.add_argument("--s2v-docs", type=int, default=8192, help="sent2vec documents per minibatch")
+    ap.add_argument("--no-app-legs", action="store_true",
+                    help="skip the LR (config 3) and sent2vec (config 5) legs of the default line")
+    ap.add_argument("--app-steps", type=int, default=20, help="timed LR minibatches of the default line's lr leg")
     args = ap.parse_args()
     if args.app != "w2v":
         return bench_other(args)
@@ -647,8 +648,23 @@ def main():
         "config1": config1,
         "exchange": exchange,
     }
+    if _comm and _comm[0] is not None:  # the library's own communicator: what its transport reports
+        kind, nranks = _comm[0].transport()
+        out["transport"] = kind
+        out["rccl_ranks" if kind == "rccl" else "transport_ranks"] = nranks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ids, off, keys, args, args.cpu_lines)
+    # BASELINE configs 3 and 5 at their per-GPU shapes beside the headline (each with its own
+    # roofline and CPU baseline): the driver's default line carries every app of the hot path
+    if rank == 0 and world == 1 and not sharded and not args.no_app_legs:
+        del ids, off
+        one = (0, 1, local, None, None)
+        la = argparse.Namespace(**vars(args))
+        la.steps, la.warmup = args.app_steps, 3
+        out["lr"] = bench_lr(la, one, corpus_batches=10, cpu_rows=10 * (args.lr_batch + 1))
+        sa = argparse.Namespace(**vars(args))
+        sa.steps, sa.warmup = 31, 31  # one launch of 31 minibatches (swps_s2v group_docs) per pass
+        out["s2v"] = bench_s2v(sa, one, corpus_batches=31)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -679,9 +695,18 @@ def bench_other(args):
     """Config 3 (sparse LR, Criteo shape, key-sharded over the GPUs) and
     config 5 (sent2vec, doc-sharded, word table replicated) — one JSON line
     each, same timing contract as the headline."""
+    ctx = _dist_init(args)
+    rank, dist = ctx[0], ctx[3]
+    out = bench_lr(args, ctx) if args.app == "lr" else bench_s2v(args, ctx)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _other_helpers(ctx):
     import torch
-    import swiftmpi_amd as sw
-    rank, world, local, dist, backend = _dist_init(args)
+    dist = ctx[3]
 
     def barrier():
         torch.cuda.synchronize()
@@ -697,8 +722,6 @@ def bench_other(args):
             return float(mx[0]), float(tt[1])
         return dt, float(units)
 
-    steps, warm = args.steps, args.warmup
-
     def run_timed(run, sync, n):
         barrier()
         t0 = time.perf_counter()
@@ -706,186 +729,281 @@ def bench_other(args):
         sync()
         barrier()
         return time.perf_counter() - t0
+    return finish, run_timed
 
-    if args.app == "lr":
-        from swiftmpi_amd.synth import criteo
-        B1 = args.lr_batch + 1
-        rows = B1 * (2 * steps + warm)  # warmup, the timed pass, a profiled pass
-        y, off, f, v = criteo(rows, seed=3 + rank)
-        lr_rate = args.lr if args.lr != 0.7 else 0.05
-        t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=lr_rate, init="hash", seed=1, device=local)
-        comm = None
-        if dist is not None and args.driver == "native":  # the library issues the exchange
-            from swiftmpi_amd.comm import Comm
-            port = int(os.environ.get("MASTER_PORT", "29533")) + 1
-            addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-            try:
-                comm = (Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
-                        else Comm.tcp(rank, world, local, addr=addr, port=port))
-            except Exception as e:  # noqa: BLE001 — every rank falls back to the Python driver together
-                print("native communicator failed on rank %d: %s" % (rank, e), file=sys.stderr, flush=True)
-            ok = torch.tensor([int(comm is not None)], dtype=torch.int32, device="cuda")
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if not int(ok.item()):
-                comm = None
-        if comm is not None:
-            m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
-            m.load_csr(y, off, f, v)
-            m.shard_comm(comm, frag_num=2000)
-            m.init()
-            run = m.train_batches
-        elif dist is not None:
-            from swiftmpi_amd.dist import ShardedLR
-            m = ShardedLR(t, frag_num=2000, minibatch=args.lr_batch, profile=False, fast_sums=not args.lr_exact)
-            m.load_csr(y, off, f, v)
-            m.init()
-            run = m.train_steps
-        else:
-            m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
-            m.load_csr(y, off, f, v)
-            m.init()
-            run = m.train_batches
-        run(warm)
-        m.sync()
-        dt = run_timed(run, m.sync, steps)     # the measured region: no event timing inside
-        m.set_profile(True)                    # a second, profiled pass for the per-kernel roofline
-        m.kernel_times(reset=True)
-        run_timed(run, m.sync, steps)
-        kt = m.kernel_times()
-        m.set_profile(False)
-        dt, total = finish(dt, steps * B1)
-        # SURVEY.md §8(d) LR bytes, over the profiled pass's rows [warm+steps, warm+2*steps) batches:
-        # k_lr_forward: per feature its shard row index, x_i and weight (4 B each); per example 20 B
-        # (row offset, label, e, e^2).  Push (k_lr_records + k_lr_reduce_*, the push timer): per
-        # feature the sorted (row, x_i), the gathered e and the record written then read back (20 B);
-        # per unique key its run (key, count, offset, shard row: 16 B) + the [w | g2] row read and
-        # written (16 B).
-        r0, r1 = (warm + steps) * B1, (warm + 2 * steps) * B1
-        nnz = int(off[r1] - off[r0])
-        uniq = sum(len(np.unique(f[off[(warm + steps + k) * B1]:off[(warm + steps + k + 1) * B1]]))
-                   for k in range(steps))
-        fwd_ms, fwd_n = kt["forward"]
-        fwd_bytes = 12 * nnz + 20 * (r1 - r0)
-        tiles = not args.lr_exact and os.environ.get("SWPS_LR_TILES", "1") != "0"
-        fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
-        push_ms, push_n = kt.get("push", (0.0, 0))
-        if tiles:  # row tiles: per feature its (row, x_i) (6 B); per piece its run and slot (8 B), per
-            # partial its fp64 write + read (16 B); per unique key its run (16 B) + the row RMW (16 B)
-            pieces = partials = 0
-            for k in range(steps):
-                pc, pa = lr_tile_pieces(f, off, (warm + steps + k) * B1, (warm + steps + k + 1) * B1)
-                pieces += pc
-                partials += pa
-            push_bytes = 6 * nnz + 8 * pieces + 16 * partials + 32 * uniq
-        else:
-            push_bytes = 20 * nnz + 32 * uniq
-        push_gbs = push_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
-        step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
-        kf = {"kernel": "k_lr_forward", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
-              "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
-        kp = {"kernel": ("k_lr_records + k_lr_reduce_short + k_lr_reduce_long" if args.lr_exact
-                         else "k_lr_tiles + k_lr_tiles_fin" if tiles
-                         else "k_lr_records + k_lr_reduce_fused") + " (per-key mean + AdaGrad push)",
-              "achieved": push_gbs, "frac": push_gbs / HBM_PEAK_GBS,
-              "bytes_per_launch": push_bytes / max(push_n, 1), "avg_launch_ms": push_ms / max(push_n, 1),
-              "launches": push_n}
-        tr, tsrc = pmc_traffic(dict(app="lr", lr_batch=args.lr_batch, exact=bool(args.lr_exact), world=world,
-                                    sharded=dist is not None),
-                               {"forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_g"),
-                                "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
-                                         "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin")})
-        for kd, name in ((kf, "forward"), (kp, "push")):
-            kd["traffic"] = tr[name]
-            kd["traffic_source"] = tsrc
-            if tr[name] and kd["avg_launch_ms"] > 0:
-                kd["hbm_GBps"] = tr[name] / (kd["avg_launch_ms"] * 1e-3) / 1e9
-                kd["hbm_frac"] = kd["hbm_GBps"] / HBM_PEAK_GBS
-        dom, other = (kp, kf) if push_ms >= fwd_ms else (kf, kp)
-        out = {"metric": "sparse LR trained examples/sec (AdaGrad, key-sharded PS)", "value": total / dt,
-               "unit": "examples/s", "n_gpus": world, "steps": steps, "warmup": warm,
-               "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-               "dtype": "f32", "data": "synthetic Criteo-shape hashed features (swiftmpi_amd/synth.py criteo)",
-               "config": {"workload": "sparse logistic regression (BASELINE config 3 shape), 39 features/row, "
-                                      "2^24 hashed feature space, %d rows per GPU per minibatch, AdaGrad lr %g"
-                                      % (B1, lr_rate),
-                          "parallelism": ("key-sharded PS over %d GPU(s), %s all-to-all-v%s"
-                                          % (world, backend, ", library-issued" if comm is not None else ""))
-                          if dist is not None else "1 GPU, one HBM shard",
-                          "mode": "exact (sequential fp32 per-key sums, bit-exact with the reference)" if args.lr_exact
-                          else "fast (fp64 per-key sums%s; within 1e-5 of the oracle)"
-                          % (" through row tiles" if tiles else ", wave tree-reduced"),
-                          "features_per_s": total * nnz / max(r1 - r0, 1) / dt,
-                          "unique_keys_per_step": uniq / steps},
-               "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
-                                step_GBps=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS, other=other,
-                                note="a 65k-row step is ~80 MB of algorithmic traffic in 4-B random accesses "
-                                     "(weights, e gathers, row read-modify-writes): access latency, not HBM "
-                                     "bandwidth, bounds it"),
-               "kernel_ms": {k: v[0] for k, v in kt.items() if v[1]}}
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_lr(y, off, f, v, args.lr_batch, lr_rate, args.cpu_rows)
+
+def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
+    """BASELINE config 3's per-GPU shape: one result dict (the JSON line of
+    --app lr, or the default line's `lr` object).  corpus_batches: minibatches
+    of synthetic data (default warmup + 2 x steps: every pass trains new rows;
+    fewer wrap around, like further epochs)."""
+    import swiftmpi_amd as sw
+    from swiftmpi_amd.synth import criteo
+    rank, world, local, dist, backend = ctx
+    finish, run_timed = _other_helpers(ctx)
+    steps, warm = args.steps, args.warmup
+    B1 = args.lr_batch + 1
+    nb = corpus_batches or (2 * steps + warm)
+    y, off, f, v = criteo(B1 * nb, seed=3 + rank)
+    lr_rate = args.lr if args.lr != 0.7 else 0.05
+    t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=lr_rate, init="hash", seed=1, device=local)
+    comm = None
+    if dist is not None and args.driver == "native":  # the library issues the exchange
+        from swiftmpi_amd.comm import Comm
+        import torch
+        port = int(os.environ.get("MASTER_PORT", "29533")) + 1
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        try:
+            comm = (Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
+                    else Comm.tcp(rank, world, local, addr=addr, port=port))
+        except Exception as e:  # noqa: BLE001 — every rank falls back to the Python driver together
+            print("native communicator failed on rank %d: %s" % (rank, e), file=sys.stderr, flush=True)
+        ok = torch.tensor([int(comm is not None)], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()):
+            comm = None
+    if comm is not None:
+        m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
+        m.load_csr(y, off, f, v)
+        m.shard_comm(comm, frag_num=2000)
+        m.init()
+        run = m.train_batches
+    elif dist is not None:
+        from swiftmpi_amd.dist import ShardedLR
+        m = ShardedLR(t, frag_num=2000, minibatch=args.lr_batch, profile=False, fast_sums=not args.lr_exact)
+        m.load_csr(y, off, f, v)
+        m.init()
+        run = m.train_steps
     else:
-        from swiftmpi_amd.synth import zipf_tokens
-        V, D = 1000000, args.dim
-        # a minibatch is the next B + 1 documents (sent2vec.cpp on word2vec.h's MiniBatch): the corpus
-        # is exactly steps + warm of them (the profiled pass wraps to the corpus start)
-        nd = (args.s2v_docs + 1) * (steps + warm)
-        rng = np.random.default_rng(5 + rank)
-        lens = rng.integers(50, 201, nd)
-        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
-        ids, _ = zipf_tokens(int(off[-1]), V, 100, seed=5 + rank, progress=True)
-        toks = ids.astype(np.uint64) + 1
-        sent = (np.arange(nd, dtype=np.uint64) + np.uint64(nd * rank + 1)) * np.uint64(2654435761)
-        t = sw.Table("w2v", dim=D, capacity=V + 1024, dtype="f32", init="hash", seed=3, device=local)
-        keys = torch.arange(1, V + 1, dtype=torch.int64, device="cuda")
-        t.pull(keys)  # the frozen word table (replicated on every GPU)
-        del keys
-        s2 = sw.Sent2Vec(t, window=args.window, negative=args.negative, minibatch=args.s2v_docs, niters=1,
-                         alpha=args.alpha)
-        s2.load_tokens(toks, off, sent)  # each rank generated its own docs: doc-sharded by construction
-        s2.train_batches(warm)
-        s2.sync()
-        st0 = s2.stats()
-        dt = run_timed(s2.train_batches, s2.sync, steps)
-        st1 = s2.stats()
-        s2.set_profile(True)
-        s2.kernel_times(reset=True)
-        run_timed(s2.train_batches, s2.sync, steps)
-        st2 = s2.stats()
-        kt = s2.kernel_times()
-        s2.set_profile(False)
-        dt, total = finish(dt, st1["positions"] - st0["positions"])
-        # SURVEY.md §8(d) sent2vec bytes of the docs kernel: 4*D per word row read (contexts + targets)
-        # + 8*D per document (its row read and written)
-        rows_read = (st2["ctx_rows"] - st1["ctx_rows"]) + (st2["tgt_rows"] - st1["tgt_rows"])
-        ndocs = st2["docs"] - st1["docs"]
-        doc_ms, doc_n = kt["docs"]
-        doc_bytes = 4 * D * rows_read + 8 * D * ndocs
-        doc_gbs = doc_bytes / (doc_ms * 1e-3) / 1e9 if doc_ms > 0 else 0.0
-        tr, tsrc = pmc_traffic(dict(app="s2v", s2v_docs=args.s2v_docs, dim=D, world=world), {"docs": ("k_s2v_docs",)})
-        out = {"metric": "sent2vec trained words/sec (frozen word table, doc-sharded)", "value": total / dt,
-               "unit": "words/s", "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": dt * 1e3 / steps,
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 table, f64 math",
-               "data": "synthetic Zipf(s=1) docs of 50-200 tokens over V=1M, hash-initialised word table",
-               "config": {"workload": "sent2vec (BASELINE config 5 shape), D=%d, window %d, negative %d, %d docs "
-                                      "per minibatch, word table 1M x %d" % (D, args.window, args.negative,
-                                                                              args.s2v_docs, D),
-                          "parallelism": "doc-sharded over %d GPU(s), no exchange (replicas only)" % world},
-               "roofline": {"bound": "hbm", "kernel": "k_s2v_docs", "achieved": doc_gbs, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": doc_gbs / HBM_PEAK_GBS, "traffic": tr["docs"],
-                            "traffic_source": tsrc,
-                            "hbm_GBps": (tr["docs"] / (doc_ms / max(doc_n, 1) * 1e-3) / 1e9
-                                         if tr["docs"] and doc_ms > 0 else None),
-                            "bytes_per_launch": doc_bytes / max(doc_n, 1), "avg_launch_ms": doc_ms / max(doc_n, 1),
-                            "launches": doc_n},
-               "kernel_ms": {k: v[0] for k, v in kt.items()}}
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_s2v(toks, off, args, args.cpu_docs)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
+        m.load_csr(y, off, f, v)
+        m.init()
+        run = m.train_batches
+    run(warm)
+    m.sync()
+    dt = run_timed(run, m.sync, steps)     # the measured region: no event timing inside
+    m.set_profile(True)                    # a second, profiled pass for the per-kernel roofline
+    m.kernel_times(reset=True)
+    run_timed(run, m.sync, steps)
+    kt = m.kernel_times()
+    m.set_profile(False)
+    xport = comm.transport() if comm is not None else None
+    m.close()
+    t.close()
+    if comm is not None:
+        comm.close()
+    dt, total = finish(dt, steps * B1)
+    # SURVEY.md §8(d) LR bytes, over the profiled pass's batches (warm + steps + k) mod nb:
+    # k_lr_forward: per feature its shard row index, x_i and weight (4 B each); per example 20 B
+    # (row offset, label, e, e^2).  Push (k_lr_records + k_lr_reduce_*, the push timer): per
+    # feature the sorted (row, x_i), the gathered e and the record written then read back (20 B);
+    # per unique key its run (key, count, offset, shard row: 16 B) + the [w | g2] row read and
+    # written (16 B).
+    pbat = [(warm + steps + k) % nb for k in range(steps)]
+    nnz = sum(int(off[(b + 1) * B1] - off[b * B1]) for b in pbat)
+    uniq = sum(len(np.unique(f[off[b * B1]:off[(b + 1) * B1]])) for b in pbat)
+    fwd_ms, fwd_n = kt["forward"]
+    fwd_bytes = 12 * nnz + 20 * steps * B1
+    tiles = not args.lr_exact and os.environ.get("SWPS_LR_TILES", "1") != "0"
+    fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+    push_ms, push_n = kt.get("push", (0.0, 0))
+    if tiles:  # row tiles: per feature its (row, x_i) (6 B); per piece its run and slot (8 B), per
+        # partial its fp64 write + read (16 B); per unique key its run (16 B) + the row RMW (16 B)
+        pieces = partials = 0
+        for b in pbat:
+            pc, pa = lr_tile_pieces(f, off, b * B1, (b + 1) * B1)
+            pieces += pc
+            partials += pa
+        push_bytes = 6 * nnz + 8 * pieces + 16 * partials + 32 * uniq
+    else:
+        push_bytes = 20 * nnz + 32 * uniq
+    push_gbs = push_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
+    step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
+    kf = {"kernel": "k_lr_forward", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
+          "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
+    kp = {"kernel": ("k_lr_records + k_lr_reduce_short + k_lr_reduce_long" if args.lr_exact
+                     else "k_lr_tiles + k_lr_tiles_fin" if tiles
+                     else "k_lr_records + k_lr_reduce_fused") + " (per-key mean + AdaGrad push)",
+          "achieved": push_gbs, "frac": push_gbs / HBM_PEAK_GBS,
+          "bytes_per_launch": push_bytes / max(push_n, 1), "avg_launch_ms": push_ms / max(push_n, 1),
+          "launches": push_n}
+    tr, tsrc = pmc_traffic(dict(app="lr", lr_batch=args.lr_batch, exact=bool(args.lr_exact), world=world,
+                                sharded=dist is not None),
+                           {"forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_g"),
+                            "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
+                                     "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin")})
+    for kd, name in ((kf, "forward"), (kp, "push")):
+        kd["traffic"] = tr[name]
+        kd["traffic_source"] = tsrc
+        if tr[name] and kd["avg_launch_ms"] > 0:
+            kd["hbm_GBps"] = tr[name] / (kd["avg_launch_ms"] * 1e-3) / 1e9
+            kd["hbm_frac"] = kd["hbm_GBps"] / HBM_PEAK_GBS
+    dom, other = (kp, kf) if push_ms >= fwd_ms else (kf, kp)
+    out = {"metric": "sparse LR trained examples/sec (AdaGrad, key-sharded PS)", "value": total / dt,
+           "unit": "examples/s", "n_gpus": world, "steps": steps, "warmup": warm,
+           "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32", "data": "synthetic Criteo-shape hashed features (swiftmpi_amd/synth.py criteo)",
+           "config": {"workload": "sparse logistic regression (BASELINE config 3 shape), 39 features/row, "
+                                  "2^24 hashed feature space, %d rows per GPU per minibatch, AdaGrad lr %g, "
+                                  "%d minibatches of data" % (B1, lr_rate, nb),
+                      "parallelism": ("key-sharded PS over %d GPU(s), %s all-to-all-v%s"
+                                      % (world, backend, ", library-issued" if comm is not None else ""))
+                      if dist is not None else "1 GPU, one HBM shard",
+                      "mode": "exact (sequential fp32 per-key sums, bit-exact with the reference)" if args.lr_exact
+                      else "fast (fp64 per-key sums%s; within 1e-5 of the oracle)"
+                      % (" through row tiles" if tiles else ", wave tree-reduced"),
+                      "features_per_s": total * nnz / max(steps * B1, 1) / dt,
+                      "unique_keys_per_step": uniq / steps},
+           "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
+                            step_GBps=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS, other=other),
+           "kernel_ms": {k: v[0] for k, v in kt.items() if v[1]}}
+    if xport is not None:
+        out["rccl_ranks" if xport[0] == "rccl" else "transport_ranks"] = xport[1]
+        out["transport"] = xport[0]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_lr(y, off, f, v, args.lr_batch, lr_rate,
+                                              cpu_rows if cpu_rows is not None else args.cpu_rows)
+    return out
+
+
+def bench_s2v(args, ctx, corpus_batches=None):
+    """BASELINE config 5's per-GPU share: one result dict (the JSON line of
+    --app s2v, or the default line's `s2v` object).  corpus_batches: minibatches
+    of synthetic documents (default warmup + steps; fewer wrap around)."""
+    import torch
+    import swiftmpi_amd as sw
+    from swiftmpi_amd.synth import zipf_tokens
+    rank, world, local, dist, backend = ctx
+    finish, run_timed = _other_helpers(ctx)
+    steps, warm = args.steps, args.warmup
+    V, D = 1000000, args.dim
+    # a minibatch is the next B + 1 documents (sent2vec.cpp on word2vec.h's MiniBatch); the
+    # passes wrap to the corpus start
+    nd = (args.s2v_docs + 1) * (corpus_batches or (steps + warm))
+    rng = np.random.default_rng(5 + rank)
+    lens = rng.integers(50, 201, nd)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    ids, _ = zipf_tokens(int(off[-1]), V, 100, seed=5 + rank, progress=True)
+    toks = ids.astype(np.uint64) + 1
+    sent = (np.arange(nd, dtype=np.uint64) + np.uint64(nd * rank + 1)) * np.uint64(2654435761)
+    t = sw.Table("w2v", dim=D, capacity=V + 1024, dtype="f32", init="hash", seed=3, device=local)
+    keys = torch.arange(1, V + 1, dtype=torch.int64, device="cuda")
+    t.pull(keys)  # the frozen word table (replicated on every GPU)
+    del keys
+    s2 = sw.Sent2Vec(t, window=args.window, negative=args.negative, minibatch=args.s2v_docs, niters=1,
+                     alpha=args.alpha)
+    s2.load_tokens(toks, off, sent)  # each rank generated its own docs: doc-sharded by construction
+    s2.train_batches(warm)
+    s2.sync()
+    st0 = s2.stats()
+    dt = run_timed(s2.train_batches, s2.sync, steps)
+    st1 = s2.stats()
+    s2.set_profile(True)
+    s2.kernel_times(reset=True)
+    run_timed(s2.train_batches, s2.sync, steps)
+    st2 = s2.stats()
+    kt = s2.kernel_times()
+    s2.set_profile(False)
+    s2.close()
+    t.close()
+    dt, total = finish(dt, st1["positions"] - st0["positions"])
+    # SURVEY.md §8(d) sent2vec bytes of the docs kernel: 4*D per word row read (contexts + targets)
+    # + 8*D per document (its row read and written)
+    rows_read = (st2["ctx_rows"] - st1["ctx_rows"]) + (st2["tgt_rows"] - st1["tgt_rows"])
+    ndocs = st2["docs"] - st1["docs"]
+    doc_ms, doc_n = kt["docs"]
+    doc_bytes = 4 * D * rows_read + 8 * D * ndocs
+    doc_gbs = doc_bytes / (doc_ms * 1e-3) / 1e9 if doc_ms > 0 else 0.0
+    tr, tsrc = pmc_traffic(dict(app="s2v", s2v_docs=args.s2v_docs, dim=D, world=world), {"docs": ("k_s2v_docs",)})
+    out = {"metric": "sent2vec trained words/sec (frozen word table, doc-sharded)", "value": total / dt,
+           "unit": "words/s", "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": dt * 1e3 / steps,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 table, f64 math",
+           "data": "synthetic Zipf(s=1) docs of 50-200 tokens over V=1M, hash-initialised word table",
+           "config": {"workload": "sent2vec (BASELINE config 5 shape), D=%d, window %d, negative %d, %d docs "
+                                  "per minibatch, word table 1M x %d, %d documents"
+                                  % (D, args.window, args.negative, args.s2v_docs, D, nd),
+                      "parallelism": "doc-sharded over %d GPU(s), no exchange (replicas only)" % world},
+           "roofline": {"bound": "hbm", "kernel": "k_s2v_docs", "achieved": doc_gbs, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": doc_gbs / HBM_PEAK_GBS, "traffic": tr["docs"],
+                        "traffic_source": tsrc,
+                        "hbm_GBps": (tr["docs"] / (doc_ms / max(doc_n, 1) * 1e-3) / 1e9
+                                     if tr["docs"] and doc_ms > 0 else None),
+                        "bytes_per_launch": doc_bytes / max(doc_n, 1), "avg_launch_ms": doc_ms / max(doc_n, 1),
+                        "launches": doc_n},
+           "kernel_ms": {k: v[0] for k, v in kt.items()}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_s2v(toks, off, args, args.cpu_docs)
+    return out
+
+
+def _free_port_pair():
+    """A port P on 127.0.0.1 with P and P + 1 both free (torch.distributed's
+    store at MASTER_PORT, the library's bootstrap at MASTER_PORT + 1)."""
+    import random
+    import socket
+    rng = random.Random()
+    while True:
+        p = rng.randrange(20000, 60000)
+        socks = []
+        try:
+            for q in (p, p + 1):
+                sk = socket.socket()
+                socks.append(sk)
+                sk.bind(("127.0.0.1", q))
+            return p
+        except OSError:
+            continue
+        finally:
+            for sk in socks:
+                sk.close()
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment):
+    start N rank processes of this script — one per GPU, RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as torch.distributed.run would —
+    and wait for them.  This process never touches the GPU (child processes,
+    no exec).  Rank 0 prints the JSON line; if any rank fails the others are
+    stopped and the first failing exit code is returned."""
+    import subprocess
+    port = _free_port_pair()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in procs:  # the others would wait forever in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def _launcher():
+    """Resolve --gpus against the environment before anything imports torch."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None and int(ws) != a.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d: launch one rank per GPU with --gpus equal to the world size"
+              % (ws, a.gpus), file=sys.stderr, flush=True)
+        return 2
+    if ws is None and a.gpus > 1:
+        return launch_ranks(a.gpus, sys.argv[1:])
+    return None
 
 
 if __name__ == "__main__":
+    _rc = _launcher()
+    if _rc is not None:
+        sys.exit(_rc)
     main()

@@ -46,6 +46,10 @@ extern "C" {
 
 const char *swps_last_error(void);
 int swps_version(void);
+/* sha256 (hex) of the sources the library was built from: every file of
+ * swiftmpi_amd/csrc/ and include/, by name then content (swiftmpi_amd/build.py
+ * source_hash); a prebuilt library is checked against the checked-out tree */
+const char *swps_build_hash(void);
 
 /* ---- parameter table (server shard in HBM) ------------------------------ */
 /* Layouts: one row per key.
@@ -186,6 +190,12 @@ int swps_comm_create_tcp(const char *addr, int32_t port, int32_t rank, int32_t w
                          int32_t timeout_ms, swps_comm **out);
 int swps_comm_destroy(swps_comm *c);
 int swps_comm_info(swps_comm *c, int32_t *rank, int32_t *world);
+/* the communicator's transport (SWPS_COMM_RCCL / _TCP / _HOST) and its rank count as the
+ * transport reports it (RCCL: ncclCommCount) */
+#define SWPS_COMM_RCCL 1
+#define SWPS_COMM_TCP 2
+#define SWPS_COMM_HOST 3
+int swps_comm_transport(swps_comm *c, int32_t *kind, int32_t *ranks);
 
 /* ---- key-sharded table (the GPU-to-shard map, src/cluster) --------------
  * swps_table_route binds a local shard to a communicator: this table then

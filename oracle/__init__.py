@@ -82,6 +82,8 @@ def lib():
         L.orc_w2v_stats.argtypes = [_p, _p]
         L.orc_lr_create.restype = _p
         L.orc_lr_create.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_float]
+        L.orc_lr_create_csr.restype = _p
+        L.orc_lr_create_csr.argtypes = [_p, _u64, _p, _p, _p, ctypes.c_int, ctypes.c_float]
         L.orc_lr_destroy.argtypes = [_p]
         L.orc_lr_set_sum_f64.argtypes = [_p, ctypes.c_int]
         L.orc_lr_num_instances.restype = _u64
@@ -264,6 +266,17 @@ class LR:
         if not self.h:
             raise RuntimeError(lib().orc_last_error().decode())
         lib().orc_lr_set_sum_f64(self.h, int(sum_f64))
+
+    @classmethod
+    def from_csr(cls, labels, row_off, feat, vals, minibatch=200, lr=0.05):
+        """The same instances from CSR arrays (labels f32, row_off u64, feat u32, vals f32)."""
+        self = cls.__new__(cls)
+        a = [np.ascontiguousarray(x, dtype=t) for x, t in
+             ((labels, np.float32), (row_off, np.uint64), (feat, np.uint32), (vals, np.float32))]
+        self.h = lib().orc_lr_create_csr(_ptr(a[0]), len(a[0]), _ptr(a[1]), _ptr(a[2]), _ptr(a[3]), minibatch, lr)
+        if not self.h:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return self
 
     def __del__(self):
         if getattr(self, "h", None):

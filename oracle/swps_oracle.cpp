@@ -1073,6 +1073,25 @@ void *orc_lr_create(const char *path, int minibatch, float lr) {
     return nullptr;
   }
 }
+// the same instances from CSR arrays (bench.py's CPU baseline: no text round trip of millions
+// of synthetic rows; the training is lr.cpp's either way)
+void *orc_lr_create_csr(const float *labels, uint64_t nrows, const uint64_t *row_off, const uint32_t *feat,
+                        const float *vals, int minibatch, float lr) {
+  try {
+    LR *m = new LR();
+    m->minibatch = minibatch;
+    m->lr = lr;
+    m->ins.resize(nrows);
+    for (uint64_t r = 0; r < nrows; r++) {
+      m->ins[r].target = labels[r];
+      for (uint64_t j = row_off[r]; j < row_off[r + 1]; j++) m->ins[r].feas.emplace_back(feat[j], vals[j]);
+    }
+    return m;
+  } catch (std::exception &e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
 void orc_lr_destroy(void *h) { delete (LR *)h; }
 uint64_t orc_lr_num_instances(void *h) { return ((LR *)h)->ins.size(); }
 

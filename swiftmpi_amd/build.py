@@ -37,6 +37,48 @@ def headers():
     return hs
 
 
+HASH_MARK = "SWPS_BUILD_HASH:"
+
+
+def source_hash():
+    """sha256 over every source and header the library is built from (name, then content)."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in (CSRC, INCLUDE):
+        for f in sorted(os.listdir(d)):
+            p = os.path.join(d, f)
+            if os.path.isfile(p) and f.endswith((".hip", ".cpp", ".h")):
+                h.update(f.encode() + b"\0")
+                h.update(open(p, "rb").read())
+    return h.hexdigest()
+
+
+def library_hash(path=LIB):
+    """The source hash stamped into a built library (read from its bytes, no load), or None."""
+    try:
+        blob = open(path, "rb").read()
+    except OSError:
+        return None
+    i = blob.find(HASH_MARK.encode())
+    return blob[i + len(HASH_MARK):i + len(HASH_MARK) + 64].decode() if i >= 0 else None
+
+
+def _hash_obj(digest):
+    """A one-function object exporting swps_build_hash() = digest (rebuilt when the sources change)."""
+    src = os.path.join(OBJDIR, "swps_build_hash.cpp")
+    obj = src + ".o"
+    text = ('extern "C" const char *swps_build_hash(void) {\n'
+            '  static const char stamp[] = "%s%s";\n'
+            '  return stamp + %d;\n}\n' % (HASH_MARK, digest, len(HASH_MARK)))
+    if not os.path.exists(src) or open(src).read() != text or not os.path.exists(obj):
+        with open(src, "w") as f:
+            f.write(text)
+        r = subprocess.run(["g++", "-O2", "-fPIC", "-c", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("build-hash object: " + r.stderr)
+    return obj
+
+
 def _obj(src):
     return os.path.join(OBJDIR, os.path.basename(src) + ".o")
 
@@ -62,8 +104,9 @@ def build(force=False, verbose=False):
     os.makedirs(LIBDIR, exist_ok=True)
     srcs = sources()
     hdrs = headers()
-    if not force and not _stale(LIB, srcs + hdrs):
-        return LIB  # the in-tree library is newer than every source (e.g. on the GPU box: no build/ there)
+    digest = source_hash()
+    if not force and not _stale(LIB, srcs + hdrs) and library_hash() == digest:
+        return LIB  # the in-tree library was built from exactly these sources (e.g. on the GPU box)
     todo = [s for s in srcs if force or _stale(_obj(s), [s] + hdrs)]
     if todo:
         workers = min(len(todo), int(os.environ.get("MAX_JOBS", "8")), 16)
@@ -71,8 +114,8 @@ def build(force=False, verbose=False):
             for obj in ex.map(_compile, todo):
                 if verbose:
                     print("compiled", obj)
-    objs = [_obj(s) for s in srcs]
-    if force or todo or _stale(LIB, objs):
+    objs = [_obj(s) for s in srcs] + [_hash_obj(digest)]
+    if force or todo or _stale(LIB, objs) or library_hash() != digest:
         cmd = [HIPCC] + LDFLAGS + objs + ["-o", LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

@@ -70,6 +70,7 @@ class S2VCfg(ctypes.Structure):
 PROTOS = {
     "swps_last_error": (ctypes.c_char_p, []),
     "swps_version": (ctypes.c_int, []),
+    "swps_build_hash": (ctypes.c_char_p, []),
     "swps_table_create": (ctypes.c_int, [ctypes.POINTER(TableCfg), ctypes.POINTER(_p)]),
     "swps_table_destroy": (ctypes.c_int, [_p]),
     "swps_table_size": (ctypes.c_int, [_p, ctypes.POINTER(_u64)]),
@@ -87,6 +88,7 @@ PROTOS = {
     "swps_comm_create_tcp": (ctypes.c_int, [ctypes.c_char_p, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_p)]),
     "swps_comm_destroy": (ctypes.c_int, [_p]),
     "swps_comm_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "swps_comm_transport": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "swps_table_route": (ctypes.c_int, [_p, _p, _i32]),
     "swps_finish": (ctypes.c_int, [_p]),
     "swps_barrier": (ctypes.c_int, [_p]),

@@ -77,6 +77,12 @@ class Comm:
         check(capi.lib().swps_comm_create_host(ctypes.byref(tr), rank, world, device, ctypes.byref(h)))
         return cls(h, rank, world, keep=(ag, a2a, tr))
 
+    def transport(self):
+        """("rccl" | "tcp" | "host", the rank count the transport reports — RCCL: ncclCommCount)."""
+        k, n = ctypes.c_int32(), ctypes.c_int32()
+        check(capi.lib().swps_comm_transport(self.h, ctypes.byref(k), ctypes.byref(n)))
+        return {1: "rccl", 2: "tcp", 3: "host"}[k.value], n.value
+
     def close(self):
         if getattr(self, "h", None):
             capi.lib().swps_comm_destroy(self.h)

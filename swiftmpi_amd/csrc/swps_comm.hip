@@ -676,6 +676,15 @@ int swps_comm_info(swps_comm *c, int32_t *rank, int32_t *world) {
   return SWPS_OK;
 }
 
+int swps_comm_transport(swps_comm *c, int32_t *kind, int32_t *ranks) {
+  if (!c) return fail(SWPS_E_CFG, "null communicator");
+  int32_t n = c->world;
+  if (c->nc) SWPS_NCCL(ncclCommCount(c->nc, &n));  // what RCCL itself reports for the communicator
+  if (kind) *kind = c->rccl ? SWPS_COMM_RCCL : c->tcp ? SWPS_COMM_TCP : SWPS_COMM_HOST;
+  if (ranks) *ranks = n;
+  return SWPS_OK;
+}
+
 int swps_table_route(swps_table *t, swps_comm *c, int32_t frag_num) {
   if (!t || !c) return fail(SWPS_E_CFG, "null argument");
   if (c->device != t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");

@@ -1861,6 +1861,9 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
     if (l->tile_threads == 512) l->tile_chunk = 2048;
   }
   if (const char *e = getenv("SWPS_LR_TILE_BITS")) l->tile_bits = std::min(std::max(atoi(e), 4), kTileMaxBits);
+  // hot codes carry kLrHotBit (bit 31) in the word that otherwise holds a shard row: only while
+  // every row index stays below it
+  if (t->cfg.capacity > (uint64_t)kLrHotBit) l->hot = 0;
   if (hipHostMalloc((void **)&l->h_small, 64) != hipSuccess) {
     delete l;
     return fail(SWPS_E_OOM, "pinned alloc");
@@ -1950,7 +1953,7 @@ int swps_lr_init(swps_lr *l) {
   if (l->cfg.init_ref && held) {
     DevMem dp;
     SWPS_TRY(dp.ensure(std::max<uint64_t>(1, V) * 4));
-    SWPS_TRY(table_lookup(l->t, dk.as<uint64_t>(), V, dp.as<uint32_t>(), l->s));
+    SWPS_TRY(table_probe(l->t, dk.as<uint64_t>(), V, dp.as<uint32_t>(), l->s));  // misses are expected
     pre.resize(V);
     if (V) SWPS_HIP(hipMemcpyAsync(pre.data(), dp.p, V * 4, hipMemcpyDeviceToHost, l->s));
     SWPS_HIP(hipStreamSynchronize(l->s));

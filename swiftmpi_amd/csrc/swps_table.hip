@@ -471,6 +471,15 @@ int table_lookup(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_
   return SWPS_OK;
 }
 
+// table_lookup that latches nothing: a key the table lacks is a kNoRow answer, not an error
+int table_probe(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  k_lookup<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(), t->mask,
+                                          d_rows_out, nullptr);
+  SWPS_HIP(hipGetLastError());
+  return SWPS_OK;
+}
+
 int table_set_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, const void *d_vals, hipStream_t s) {
   if (n == 0) return SWPS_OK;
   if (t->cfg.dtype == SWPS_F64)

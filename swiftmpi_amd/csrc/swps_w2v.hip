@@ -1891,11 +1891,14 @@ __global__ __launch_bounds__(256) void k_install(const int32_t *__restrict__ K, 
   const int NC = D / E;
   for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < U; u += (uint64_t)gridDim.x * 4) {
     const int32_t vid = K[u];
-    const V *src = (const V *)(vals + (srow ? (uint64_t)srow[u] * 4 : u * 2) * D);
+    // a key the shard holds no row for (full table: table_copy_pull's zero row) installs zeros
+    const uint32_t sr = srow ? srow[u] : 0u;
+    const bool have = !srow || sr != kNoRow;
+    const V *src = (const V *)(vals + (srow ? (uint64_t)(have ? sr : 0u) * 4 : u * 2) * D);
     V *dh = (V *)(cache_h + (uint64_t)vid * cs);  // cs: the cache row stride (swps_w2v::cs)
     V *dv = (V *)(cache_v + (uint64_t)vid * cs);
     for (int c = lane; c < cs / E; c += 64) {  // the pad too (zeros): whole-line stores
-      const bool in = c < NC;
+      const bool in = have && c < NC;
       dh[c] = in ? src[c] : V{};
       dv[c] = in ? src[NC + c] : V{};
     }

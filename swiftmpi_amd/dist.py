@@ -254,7 +254,8 @@ class ShardedWord2Vec(_ShardedApp):
         self.width = 2 * self.D
         self.val_dtype = table.torch_dtype
         # push payload: fp64 (the reference's wire format) unless fast mode (fp32 table, fp32 intermediates)
-        fast = table.dtype == "f32" and not kw.get("fp64_intermediates", True)
+        from . import INTERMEDIATES
+        fast = table.dtype == "f32" and INTERMEDIATES[kw.get("fp64_intermediates", True)] == 0
         self.grad_dtype = torch.float32 if fast else torch.float64
         self.pipeline = pipeline
         self.overlap = overlap

@@ -48,7 +48,8 @@ def gather(obj, world):
 def check_w2v(sw, rank, world, dev, tmp, mode, epochs):
     from swiftmpi_amd.dist import ShardedWord2Vec
     dtype, fp64i = {"f64": ("f64", True), "parity": ("f32", True), "fast": ("f32", False),
-                    "fast300": ("f32", False), "bfp300": ("f32", "bfp40")}[mode]
+                    "fast300": ("f32", False), "bfp300": ("f32", "bfp40"),
+                    "fp32str": ("f32", "fp32"), "bfp32str": ("f32", "bfp32")}[mode]
     paths = [w2v_corpus(os.path.join(tmp, "c%d.txt" % r), r) for r in range(world)]
     kw = dict(window=4, negative=4, minibatch=17, sample=1e-3, unigram_size=10 ** 6)
     # fast300: the bench's D = 300 kernels (k_push_thp<TO_GRADS> on the learner, the
@@ -63,7 +64,8 @@ def check_w2v(sw, rank, world, dev, tmp, mode, epochs):
     # steps a tiny hot vocabulary turns fp32 rounding into exp-table bucket
     # flips (tests/test_bench_shape_gpu.py), which compare nothing about the
     # exchange; f64 / parity: whole epochs
-    fast = mode.startswith("fast")
+    # "fp32str" = fast mode selected by name (its push payload must be fp32 like False's)
+    fast = mode.startswith("fast") or mode in ("fp32str", "bfp32str")
     nsteps = 3 if fast else epochs * sh.steps_per_epoch
     sh.train_steps(nsteps)
     sh.sync()

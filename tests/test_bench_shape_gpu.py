@@ -27,7 +27,7 @@ AdaGrad):
           bytes) — the bench's headline mode (k_forward_b / k_gather_b /
           k_push_b <1,1,0> at D = 300): one minibatch within 1e-5 (emulated
           1.2e-7 / 2.3e-7); two chained minibatches within FAST_TOL_BATCH
-          (measured 1.8e-5 / 8.4e-6); two epochs max within BFP32_TOL_MAX and
+          (BFP32_TOL_BATCH2; measured 1.8e-5 / 8.4e-6); two epochs max within BFP32_TOL_MAX and
           p99.9 within BFP32_TOL_P999 (measured 1.4e-3 / 9.0e-4, p99.9
           2.0e-6 / 1.6e-6 — the emulation's 1.4e-3 / 9.0e-4).
   fast    fp32 table, fp32 neu1/neu1e and partials — k_forward_t<1,4,1> /
@@ -75,8 +75,12 @@ BFP_TOL_MAX = 1e-3
 BFP_TOL_P9999 = 1e-6
 # bfp32 after two epochs: the same chaos started from ~2^-32 perturbations
 # (measured max 1.4e-3 at D = 300, 9.0e-4 at D = 100; p99.9 2.0e-6 / 1.6e-6)
-BFP32_TOL_MAX = 1e-2
-BFP32_TOL_P999 = 1e-5
+# — bars about 2x the measured values, so a precision regression of the headline kernels fails
+BFP32_TOL_MAX = 3e-3
+BFP32_TOL_P999 = 5e-6
+# bfp32, two chained minibatches (the second learned from the first's pushed rows): measured
+# 1.8e-5 (D = 300) / 8.4e-6 (D = 100), CPU emulation the same
+BFP32_TOL_BATCH2 = 3e-5
 MODES = {"f64": ("f64", True), "parity": ("f32", True), "fast": ("f32", False), "bfp40": ("f32", "bfp40"),
          "bfp32": ("f32", "bfp32")}
 
@@ -181,8 +185,8 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode, lin
     41 adds a second one-line batch learned from the pushed rows (where fast
     mode's rounding starts to compound).  Full-array max vs the oracle's
     fp32-storage mode: parity and bfp40 within 1e-5 (the north star's
-    single-batch fp32 bar), bfp32 within 1e-5 for the single batch, fast
-    within FAST_TOL_BATCH."""
+    single-batch fp32 bar), bfp32 within 1e-5 for the single batch and
+    BFP32_TOL_BATCH2 for two, fast within FAST_TOL_BATCH."""
     path = corpus(str(tmp_path / "c1.txt"), lines=lines, seed=83)
     c = dict(CFG, minibatch=40)
     orc = oracle_mod.W2V(path, D, window=c["window"], negative=c["negative"], minibatch=c["minibatch"],
@@ -202,8 +206,8 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode, lin
     rel = rel_err(pg, po)
     print("%d lines D=%d %s: max rel %.3g (median %.3g) over %d elements"
           % (lines, D, mode, rel.max(), np.median(rel), rel.size))
-    loose = mode == "fast" or (mode == "bfp32" and lines == 41)
-    assert rel.max() <= (FAST_TOL_BATCH if loose else 1e-5), float(rel.max())
+    tol = FAST_TOL_BATCH if mode == "fast" else BFP32_TOL_BATCH2 if (mode == "bfp32" and lines == 41) else 1e-5
+    assert rel.max() <= tol, float(rel.max())
 
 
 @pytest.mark.parametrize("env,fixed,fp64i", [("SWPS_SORT_WIDE", "", False), ("SWPS_FUSED_PUSH", "", False),
@@ -252,7 +256,7 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed,
 
 def test_config4_per_rank_shape(lib, gpu):
     """BASELINE config 4's per-rank share on one GPU (125M-token Zipf corpus,
-    V = 1M, D = 300, the bench kernels in fast mode): two 5000-line batches
+    V = 1M, D = 300, the headline's bfp32 kernels): two 5000-line batches
     train deterministically (50k sampled rows bit-identical run to run),
     rows stay finite, and the kept / trained word counts are consistent."""
     import torch
@@ -265,7 +269,7 @@ def test_config4_per_rank_shape(lib, gpu):
     outs = []
     for _ in range(2):
         t = lib.Table("w2v", dim=300, capacity=V + 1024, dtype="f32", learning_rate=0.7, init="hash", seed=1)
-        w = lib.Word2Vec(t, minibatch=5000, sample=1e-5, init="table", fp64_intermediates=False)
+        w = lib.Word2Vec(t, minibatch=5000, sample=1e-5, init="table", fp64_intermediates="bfp32")
         w.load_tokens(ids, off, keys)
         w.init()
         w.train_batches(2)

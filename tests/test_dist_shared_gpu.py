@@ -20,7 +20,7 @@ def _port():
     return free_port()
 
 
-@pytest.mark.parametrize("modes", ["f64,parity", "fast,lr", "fast300", "bfp300"])
+@pytest.mark.parametrize("modes", ["f64,parity", "fast,lr", "fast300", "bfp300", "fp32str,bfp32str"])
 def test_shared_keys_two_ranks_match_lockstep_oracle(lib, oracle_mod, gpu, modes):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",

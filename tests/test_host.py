@@ -91,3 +91,12 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".h")):
                 src = open(os.path.join(dirpath, f), errors="replace").read()
                 assert "import oracle" not in src and "from oracle" not in src and "swps_oracle" not in src, f
+
+
+def test_library_built_from_checked_out_sources(lib):
+    """Build provenance: the library in the tree (prebuilt ones travel to the
+    GPU box) carries the hash of exactly the csrc/ + include/ it was built
+    from; a stale library fails here instead of silently testing old code."""
+    from swiftmpi_amd import build, capi
+    assert capi.lib().swps_build_hash().decode() == build.source_hash()
+    assert build.library_hash() == build.source_hash()

@@ -59,6 +59,63 @@ def test_lr_dump_load_roundtrip(lib, gpu, tmp_path):
     assert np.allclose(a[:, 0], b[:, 0], rtol=1e-5) and (b[:, 1] == 0).all()
 
 
+def _gen_float_draws(n):
+    """LRPullAccessMethod::init_param's draws (lr.cpp:48-50 -> random.h gen_float):
+    y = y * 4903917 + 11 from ULONG_MAX / 2, value (float)y / 2^64 (round to nearest even)."""
+    out, y = np.zeros(n, dtype=np.float32), (2 ** 64 - 1) // 2
+    for i in range(n):
+        y = (y * 4903917 + 11) % 2 ** 64
+        b = y.bit_length()
+        q = y
+        if b > 24:
+            sh = b - 24
+            q, r = y >> sh, y & ((1 << sh) - 1)
+            if r > 1 << (sh - 1) or (r == 1 << (sh - 1) and q & 1):
+                q += 1
+            q <<= sh
+        out[i] = np.float32(q / 2.0 ** 64)
+    return out
+
+
+def test_lr_init_after_partial_dump(lib, gpu, tmp_path):
+    """Predict mode on data with features the dump never saw (lr.cpp:297-300 ->
+    server.h:49-62, then the first pull): the dumped keys keep their values, the
+    others get LRPullAccessMethod::init_param's gen_float() draws in first-pull
+    order (lr.cpp:48-50) — the same draws a fresh table gives its first keys —
+    and init does not fail on the misses."""
+    t0 = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+    m0 = lib.LR(t0, minibatch=200)
+    m0.load_text(DATA)
+    m0.init()
+    k0, w0, _ = m0.params()
+    held = np.zeros(len(k0), dtype=bool)
+    held[::3] = True
+    vals = 0.25 + 1e-3 * np.arange(len(k0))
+    path = str(tmp_path / "partial.txt")
+    with open(path, "w") as f:
+        for k, x in zip(k0[held], vals[held]):
+            f.write("%d\t%g\n" % (k, x))
+    t1 = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+    t1.load(path)
+    m1 = lib.LR(t1, minibatch=200)
+    m1.load_text(DATA)
+    m1.init()
+    k1, w1, g1 = m1.params()
+    assert np.array_equal(k0, k1)
+    assert np.array_equal(w1[held], np.array(["%g" % x for x in vals[held]], dtype=np.float32))
+    # the fresh table's draws give each key's first-pull index (vid)
+    seq = _gen_float_draws(len(k0))
+    index = {float(x): i for i, x in enumerate(seq)}
+    assert len(index) == len(seq)
+    vid = np.array([index[float(x)] for x in w0])
+    miss = np.flatnonzero(~held)
+    miss = miss[np.argsort(vid[miss])]
+    assert np.array_equal(w1[miss], seq[:len(miss)])
+    assert (g1 == 0).all()
+    m1.train(1)  # and the held keys train like any other
+    assert np.isfinite(m1.params()[1]).all()
+
+
 @pytest.mark.parametrize("B", [200, 13])
 def test_sharded_lr_world1_equals_unsharded(lib, gpu, gloo1, B):
     """The sharded request / serve / step / push protocol (one rank, gloo)

@@ -60,10 +60,13 @@ def gpu_run(lib, path, fp64i, sharded=False, pipeline=False):
     return vk, np.stack([rows[pos[int(k)]] for k in vk])
 
 
-@pytest.mark.parametrize("mode", ["parity", "fast"])
+MODES = {"parity": True, "fast": False, "bfp40": "bfp40", "bfp32": "bfp32"}
+
+
+@pytest.mark.parametrize("mode", ["parity", "fast", "bfp40", "bfp32"])
 def test_analogy_accuracy_matches_reference(lib, gpu, corpus, reference_acc, mode):
     path, qs, words = corpus
-    vk, rows = gpu_run(lib, path, fp64i=(mode == "parity"))
+    vk, rows = gpu_run(lib, path, fp64i=MODES[mode])
     acc = accuracy(rows, vk, lib.bkdr, qs, words)
     print("analogy accuracy: reference %.4f  gpu %s %.4f" % (reference_acc, mode, acc))
     assert reference_acc > 0.8  # the planted structure is learnt
@@ -127,13 +130,9 @@ def test_analogy_accuracy_alias_sampler(lib, gpu, oracle_mod, tmp_path):
     assert abs(np.mean(ali) - np.mean(ref)) <= 0.005
 
 
-@pytest.mark.parametrize("mode", ["parity", "fast"])
-def test_analogy_accuracy_at_bench_dim(lib, gpu, oracle_mod, corpus, mode):
-    """The same bar at the benchmarked D = 300, where the fast mode runs the
-    bench's own kernels (k_records_t, k_forward_t, the position-ordered
-    k_gather_t and the fused k_push_thp): the oracle at D = 300 (fp64, the
-    reference's semantics, twice the epochs of the D = 32 test) against the
-    GPU within 0.5 pt."""
+@pytest.fixture(scope="module")
+def reference_acc_300(corpus, oracle_mod):
+    """The oracle at D = 300 (fp64, the reference's semantics, twice the epochs of the D = 32 test)."""
     path, qs, words = corpus
     D3 = 300
     o = oracle_mod.W2V(path, D3, window=W, negative=N, minibatch=B, sample=SAMPLE, table_size=10 ** 7, lr=LR,
@@ -143,10 +142,22 @@ def test_analogy_accuracy_at_bench_dim(lib, gpu, oracle_mod, corpus, mode):
     vk, _ = o.vocab()
     idx = {int(k): i for i, k in enumerate(vk)}
     from swiftmpi_amd.synth import analogy_accuracy
-    ref = analogy_accuracy(np.asarray(o.get_params())[:, D3:2 * D3], {w: idx[oracle_mod.bkdr(w)] for w in words},
-                           qs, words)
+    return analogy_accuracy(np.asarray(o.get_params())[:, D3:2 * D3], {w: idx[oracle_mod.bkdr(w)] for w in words},
+                            qs, words)
+
+
+@pytest.mark.parametrize("mode", ["parity", "fast", "bfp40", "bfp32"])
+def test_analogy_accuracy_at_bench_dim(lib, gpu, corpus, reference_acc_300, mode):
+    """The same bar at the benchmarked D = 300, where bfp32 (the headline) runs
+    the bench's own kernels (k_records_t, k_forward_b, the position-ordered
+    k_gather_b and the fused k_push_b), fast mode their fp32 forms: the oracle
+    at D = 300 against the GPU within 0.5 pt."""
+    path, qs, words = corpus
+    D3 = 300
+    ref = reference_acc_300
+    from swiftmpi_amd.synth import analogy_accuracy
     kw = dict(window=W, negative=N, minibatch=B, sample=SAMPLE, unigram_size=10 ** 7,
-              fp64_intermediates=(mode == "parity"))
+              fp64_intermediates=MODES[mode])
     t = lib.Table("w2v", dim=D3, capacity=4096, dtype="f32", learning_rate=LR)
     w = lib.Word2Vec(t, init="ref", **kw)
     w.load_text(path)

@@ -229,3 +229,27 @@ def test_native_sharded_resume_rccl_world1(lib, gpu, tmp_path):
     for w in (a, b, c):
         w.close()
     comm.close()
+
+
+def test_native_sharded_world1_full_table_fails_loudly(lib, gpu, tmp_path):
+    """A shard whose capacity is below the vocabulary: the first
+    full pull reports the table-full error instead of the steps reading a
+    missing row's index past the shard, and the context stays un-initialised
+    (training is refused, not run on rows that do not exist)."""
+    import swiftmpi_amd as sw
+    from swiftmpi_amd.comm import Comm
+    from conftest import zipf_corpus
+    path = zipf_corpus(str(tmp_path / "c.txt"), 80, 300, seed=15)
+    comm = Comm.rccl(0, 1, port=_port())
+    t = sw.Table("w2v", dim=24, capacity=64, dtype="f32", init="hash", seed=7)
+    w = sw.Word2Vec(t, init="table", window=3, negative=4, minibatch=23, sample=1e-3, unigram_size=10 ** 6,
+                    fp64_intermediates="bfp32")
+    w.load_text(path)
+    assert w.info()["vocab"] > 64
+    w.shard_comm(comm, frag_num=1000)
+    with pytest.raises(lib.SwpsError, match="capacity"):
+        w.init()
+    with pytest.raises(lib.SwpsError):
+        w.train(1)
+    w.close()
+    comm.close()

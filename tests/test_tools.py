@@ -91,3 +91,38 @@ def test_bench_lr_tile_pieces_matches_a_loop_restatement():
             seen[k] = seen.get(k, 0) + 1
         exp = (len(pieces), sum(n for n in seen.values() if n > 1))
         assert b.lr_tile_pieces(f, off, r0, r1, tile_bits=tb, chunk=ch) == exp
+
+
+def test_bench_refuses_world_size_that_differs_from_gpus():
+    """The driver's contract: `--gpus N` is the world.  A launcher whose
+    WORLD_SIZE disagrees is refused (rc 2) before anything touches the GPU."""
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=4" in r.stderr
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 2 and "--gpus 1" in r.stderr
+
+
+def test_bench_launcher_spawns_ranks(tmp_path, monkeypatch):
+    """Without WORLD_SIZE, `--gpus N` starts N rank processes of bench.py with
+    torch.distributed.run's variables (a stand-in script records them) and
+    returns the first failing rank's code."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    stub = tmp_path / "stub.py"
+    stub.write_text("import json, os, sys\n"
+                    "d = {k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')}\n"
+                    "open(os.path.join(%r, 'r%%s.json' %% d['RANK']), 'w').write(json.dumps([d, sys.argv[1:]]))\n"
+                    "sys.exit(3 if d['RANK'] == '2' else 0)\n" % str(tmp_path))
+    monkeypatch.setattr(b.os.path, "abspath", lambda p: str(stub) if p == b.__file__ else os.path.realpath(p))
+    rc = b.launch_ranks(3, ["--gpus", "3", "--steps", "2"])
+    assert rc == 3
+    seen = [json.load(open(tmp_path / ("r%d.json" % r))) for r in range(3)]
+    assert [d["RANK"] for d, _ in seen] == ["0", "1", "2"] and {d["WORLD_SIZE"] for d, _ in seen} == {"3"}
+    assert {d["MASTER_ADDR"] for d, _ in seen} == {"127.0.0.1"} and len({d["MASTER_PORT"] for d, _ in seen}) == 1
+    assert all(a == ["--gpus", "3", "--steps", "2"] for _, a in seen)
