@@ -1,0 +1,260 @@
+/*
+ * swiftmpi/swiftmpi.h — what an UNCHANGED reference app sees when it
+ * includes "../../swiftmpi.h" (src/swiftmpi.h): the parameter-server API of
+ * swiftmpi_compat.h (over libswps.so) plus the reference utilities its mains
+ * and app classes call.  Compile a reference app against this tree instead
+ * of its own:
+ *
+ *   g++ -std=c++11 -I- -I<repo>/include -I<repo>/include/swiftmpi/apps/word2vec \
+ *       <ref>/src/apps/logistic/lr.cpp -L<repo>/swiftmpi_amd/lib -lswps -pthread
+ *
+ * (-I- stops the compiler from taking the reference's own headers next to
+ * the source file; the second -I resolves the apps' "../../swiftmpi.h" and
+ * "word2vec_global.h" / "word2vec.h" here.)
+ *
+ * Reference interfaces restated (paths relative to logicxin/SwiftMPI src/):
+ *   GlobalMPI / global_mpi()       utils/mpi.h:7-55 (rank / size from the launcher's environment)
+ *   fms::CMDLine                   utils/CMDLine.h:17-183
+ *   format_string                  utils/string.h:69-89
+ *   LineFileReader                 utils/string.h:91-121
+ *   AsynExec / async_exec          utils/AsynExec.h:17-123
+ *   SpinLock                       utils/SpinLock.h
+ *   LOG / DLOG / CHECK_* / RAW_LOG_*   glog, as utils/common.h pulls it in
+ * Host-side plumbing only: no compute of the hot path lives here.
+ */
+#ifndef SWIFTMPI_SWIFTMPI_H_
+#define SWIFTMPI_SWIFTMPI_H_
+
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "swiftmpi_compat.h"
+
+namespace swift_snails {
+
+/* ---- glog's LOG / CHECK, as the apps use them ------------------------------ */
+namespace detail {
+class LogLine {
+ public:
+  LogLine(const char *sev, bool fatal = false) : _sev(sev), _fatal(fatal) {}
+  ~LogLine() {
+    std::cerr << _sev << " " << _os.str() << std::endl;
+    if (_fatal) std::abort();  // glog's CHECK failure aborts
+  }
+  template <class T> LogLine &operator<<(const T &x) {
+    _os << x;
+    return *this;
+  }
+  LogLine &operator<<(std::ostream &(*f)(std::ostream &)) {
+    _os << f;
+    return *this;
+  }
+
+ private:
+  std::ostringstream _os;
+  const char *_sev;
+  bool _fatal;
+};
+inline void raw_log(const char *sev, const char *fmt, ...) {
+  std::va_list ap;
+  va_start(ap, fmt);
+  std::fprintf(stderr, "%s ", sev);
+  std::vfprintf(stderr, fmt, ap);
+  std::fputc('\n', stderr);
+  va_end(ap);
+}
+}  // namespace detail
+
+#ifndef LOG
+#define LOG(sev) ::swift_snails::detail::LogLine(#sev)
+#define DLOG(sev) ::swift_snails::detail::LogLine(#sev)
+#define CHECK(c) \
+  if (c) {       \
+  } else         \
+    ::swift_snails::detail::LogLine("FATAL check failed: " #c, true)
+#define CHECK_EQ(a, b) CHECK((a) == (b))
+#define CHECK_NE(a, b) CHECK((a) != (b))
+#define CHECK_GT(a, b) CHECK((a) > (b))
+#define CHECK_GE(a, b) CHECK((a) >= (b))
+#define CHECK_LT(a, b) CHECK((a) < (b))
+#define CHECK_LE(a, b) CHECK((a) <= (b))
+#endif
+#define RAW_LOG(sev, ...) ::swift_snails::detail::raw_log(#sev, __VA_ARGS__)
+#define RAW_DLOG(sev, ...) ::swift_snails::detail::raw_log(#sev, __VA_ARGS__)
+#define RAW_LOG_INFO(...) ::swift_snails::detail::raw_log("INFO", __VA_ARGS__)
+#define RAW_LOG_WARNING(...) ::swift_snails::detail::raw_log("WARNING", __VA_ARGS__)
+#define RAW_LOG_ERROR(...) ::swift_snails::detail::raw_log("ERROR", __VA_ARGS__)
+
+/* ---- utils/mpi.h: one process per GPU, rank / size from the launcher -------- */
+class GlobalMPI {
+ public:
+  static void initialize(int, char **) {}
+  int rank() const { return env_int("RANK", "OMPI_COMM_WORLD_RANK", 0); }
+  int size() const { return env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1); }
+  /* a collective over the key-sharded shard (swps_barrier); one rank: its device work retired */
+  void barrier() {
+    if (global_swps_table()) swps_check(swps_barrier(global_swps_table()));
+  }
+};
+inline GlobalMPI &global_mpi() {
+  static GlobalMPI m;
+  return m;
+}
+
+/* ---- utils/string.h ----------------------------------------------------------- */
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wformat-security"  // the apps pass runtime formats (lr.cpp:493)
+#pragma GCC diagnostic ignored "-Wformat-nonliteral"
+template <typename... ARGS> void format_string(std::string &s, const char *format, ARGS... args) {
+  const int len = std::snprintf(NULL, 0, format, args...);
+  CHECK(len >= 0);
+  const size_t old = s.size();
+  s.resize(old + len + 1);
+  std::snprintf(&s[old], (size_t)len + 1, format, args...);
+  s.resize(old + len);
+}
+template <typename... ARGS> std::string format_string(const char *format, ARGS... args) {
+  std::string s;
+  format_string(s, format, args...);
+  return s;
+}
+#pragma GCC diagnostic pop
+
+class LineFileReader {
+ public:
+  LineFileReader() {}
+  explicit LineFileReader(FILE *f) : _file(f) {}
+  ~LineFileReader() { std::free(_buffer); }
+  char *getline() { return getline(_file); }
+  char *getline(FILE *f) { return getdelim(f, '\n'); }
+  char *getdelim(FILE *f, char delim) {
+    ssize_t n = ::getdelim(&_buffer, &_cap, delim, f);
+    if (n < 0) {
+      _length = 0;
+      return NULL;
+    }
+    if (n >= 1 && _buffer[n - 1] == delim) _buffer[--n] = 0;
+    _length = (size_t)n;
+    return _buffer;
+  }
+  char *get() { return _buffer; }
+  size_t length() const { return _length; }
+
+ private:
+  LineFileReader(const LineFileReader &);
+  LineFileReader &operator=(const LineFileReader &);
+  char *_buffer = NULL;
+  size_t _cap = 0, _length = 0;
+  FILE *_file = nullptr;
+};
+
+/* ---- utils/SpinLock.h ------------------------------------------------------- */
+class SpinLock {
+ public:
+  void lock() {
+    while (_f.test_and_set(std::memory_order_acquire)) {
+    }
+  }
+  void unlock() { _f.clear(std::memory_order_release); }
+
+ private:
+  std::atomic_flag _f = ATOMIC_FLAG_INIT;
+};
+
+/* ---- utils/AsynExec.h: the apps' host thread pool --------------------------
+ * async_exec(n, task, channel) runs `task` on n threads and returns when all
+ * are done (AsynExec.h:102-123); nthreads = 1 — the reference's only
+ * deterministic setting — runs it on the caller's thread. */
+class AsynExec {
+ public:
+  typedef std::function<void()> task_t;
+  struct channel_t {};
+  AsynExec() {}
+  explicit AsynExec(int thread_num) : _n(thread_num) {}
+  std::shared_ptr<channel_t> open() { return std::make_shared<channel_t>(); }
+  void set_thread_num(int x) { _n = x; }
+  int thread_num() const { return _n; }
+
+ private:
+  int _n = 0;
+};
+inline void async_exec(int thread_num, AsynExec::task_t &task, std::shared_ptr<AsynExec::channel_t>) {
+  if (thread_num <= 1) {
+    task();
+    return;
+  }
+  std::vector<std::thread> ts;
+  for (int i = 0; i < thread_num; i++) ts.emplace_back([&task] { task(); });
+  for (auto &t : ts) t.join();
+}
+
+}  // namespace swift_snails
+
+/* ---- utils/CMDLine.h ------------------------------------------------------- */
+namespace fms {
+class CMDLine {
+ public:
+  std::string delimiter = ";,";
+  CMDLine(int argc, char **argv) {
+    for (int i = 1; i < argc; i++) {
+      std::string s(argv[i]);
+      if (!name(s)) throw "cannot parse " + s;
+      if (value.count(s)) throw "the parameter " + s + " is already specified";
+      std::string next = i + 1 < argc ? std::string(argv[i + 1]) : std::string("-");
+      if (i + 1 < argc && !name(next)) {
+        value[s] = argv[i + 1];
+        i++;
+      } else {
+        value[s] = "";
+      }
+    }
+  }
+  std::string registerParameter(const std::string &p, const std::string &h) {
+    help[p] = h;
+    return p;
+  }
+  bool hasParameter(const std::string &p) const { return value.count(p) != 0; }
+  void setValue(const std::string &p, const std::string &v) { value[p] = v; }
+  const std::string &getValue(const std::string &p) { return value[p]; }
+  std::string getValue(const std::string &p, const std::string &d) { return hasParameter(p) ? value[p] : d; }
+  double getValue(const std::string &p, const double &d) { return hasParameter(p) ? std::atof(value[p].c_str()) : d; }
+  int getValue(const std::string &p, const int &d) { return hasParameter(p) ? std::atoi(value[p].c_str()) : d; }
+  void print_help() const {
+    for (const auto &h : help) {
+      std::cout << "-" << h.first;
+      for (size_t i = h.first.size() + 1; i < 16; i++) std::cout << " ";
+      std::cout << h.second << std::endl;
+    }
+  }
+  void checkParameters() const {
+    for (const auto &v : value)
+      if (!help.count(v.first)) throw "the parameter " + v.first + " does not exist";
+  }
+
+ private:
+  static bool name(std::string &s) {
+    if (s.empty() || s[0] != '-') return false;
+    s = s.substr(s.size() > 1 && s[1] == '-' ? 2 : 1);
+    return true;
+  }
+  std::map<std::string, std::string> help, value;
+};
+}  // namespace fms
+
+#endif /* SWIFTMPI_SWIFTMPI_H_ */

@@ -32,9 +32,12 @@
 #ifndef SWIFTMPI_COMPAT_H_
 #define SWIFTMPI_COMPAT_H_
 
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
+#include <type_traits>
 #include <limits>
 #include <map>
 #include <stdexcept>
@@ -129,14 +132,140 @@ inline ConfigParser &global_config() {
   return c;
 }
 
+/* ---- utils/Buffer.h BinaryBuffer ------------------------------------------
+ * The byte buffer the reference's apps serialise their pull values and
+ * gradients into (operator<< / >> of basic types, Buffer.h:169-230): the
+ * generic codecs below run an app's own operator<< (BinaryBuffer&, Grad&) /
+ * operator>> to produce and consume the wire values. */
+class BinaryBuffer {
+ public:
+  BinaryBuffer() {}
+  BinaryBuffer(const char *p, size_t n) : _b(p, p + n) {}
+#define SWPS_BB_POD(T)                        \
+  BinaryBuffer &operator<<(const T &x) {      \
+    const char *p = (const char *)&x;         \
+    _b.insert(_b.end(), p, p + sizeof(T));    \
+    return *this;                             \
+  }                                           \
+  BinaryBuffer &operator>>(T &x) {            \
+    if (_r + sizeof(T) > _b.size())           \
+      throw SwpsError(SWPS_E_IO, "BinaryBuffer: read past the end"); \
+    std::memcpy(&x, &_b[_r], sizeof(T));      \
+    _r += sizeof(T);                          \
+    return *this;                             \
+  }
+  SWPS_BB_POD(int16_t)
+  SWPS_BB_POD(uint16_t)
+  SWPS_BB_POD(int32_t)
+  SWPS_BB_POD(uint32_t)
+  SWPS_BB_POD(long)
+  SWPS_BB_POD(unsigned long)
+  SWPS_BB_POD(long long)
+  SWPS_BB_POD(unsigned long long)
+  SWPS_BB_POD(float)
+  SWPS_BB_POD(double)
+  SWPS_BB_POD(bool)
+  SWPS_BB_POD(char)
+#undef SWPS_BB_POD
+  bool read_finished() const { return _r >= _b.size(); }
+  size_t size() const { return _b.size(); }
+  char *buffer() { return _b.empty() ? nullptr : &_b[0]; }
+  const char *buffer() const { return _b.empty() ? nullptr : &_b[0]; }
+  void clear() {
+    _b.clear();
+    _r = 0;
+  }
+
+ private:
+  std::vector<char> _b;
+  size_t _r = 0;
+};
+
+/* ---- utils/random.h Random / global_random() -------------------------------
+ * The reference's two LCGs (random.h:25-37): operator() and gen_float().
+ * A table whose init rule is SWPS_INIT_FLCG continues this float stream on
+ * the device from the state it had when the shard was created. */
+struct Random {
+  explicit Random(unsigned long long seed) : next_random(seed) {}
+  unsigned long long operator()() {
+    next_random = next_random * (unsigned long long)25214903917 + 11;
+    return next_random;
+  }
+  float gen_float() {
+    next_float_random = next_float_random * (unsigned long)4903917 + 11;
+    return float(next_float_random) / std::numeric_limits<unsigned long>::max();
+  }
+  unsigned long float_state() const { return next_float_random; }
+
+ private:
+  unsigned long long next_random = 0;
+  unsigned long next_float_random = std::numeric_limits<unsigned long>::max() / 2;
+};
+inline Random &global_random() {
+  static Random r(2008);
+  return r;
+}
+
 /* ---- wire codecs ----------------------------------------------------------
- * PullCodec<Val>:  typedef wire_t (double for word2vec, float for LR);
- *                  static int elems();  static void decode(const wire_t*, Val&)
- * PushCodec<Grad>: static void encode(Grad&, wire_t*)  — writes the MEAN
- *                  gradient the reference's serializer sends and resets it
- *                  (word2vec_global.h:122-134, lr.cpp:32-38). */
-template <class Val> struct PullCodec;
-template <class Grad> struct PushCodec;
+ * Typed form (a specialisation states the wire directly):
+ *   PullCodec<Val>:  typedef wire_t (double for word2vec, float for LR);
+ *                    static int elems();  static void decode(const wire_t*, Val&)
+ *   PushCodec<Grad>: static void encode(Grad&, wire_t*)  — writes the MEAN
+ *                    gradient the reference's serializer sends and resets it
+ *                    (word2vec_global.h:122-134, lr.cpp:32-38).
+ * Generic form (no specialisation — what an unchanged reference app gets):
+ * the app's own BinaryBuffer operators, exactly as its messages carried the
+ * values (global_pull_access.h:88-97, global_push_access.h:86-90): a pull
+ * value is read with `bb >> val`, a gradient written with `bb << grad` (a
+ * gradient that writes nothing — lr.cpp:34-35 with count 0 — is not pushed)
+ * and then reset with its reset() (global_push_access.h:49, 64) or to
+ * Grad().  Layout: a scalar pull value is the LR layout, anything else the
+ * word2vec one (its wire interleaves h[i], v[i]; the library's value blocks
+ * are converted). */
+namespace detail {
+template <class V> struct is_generic_layout {
+  static const int32_t value = std::is_arithmetic<V>::value ? SWPS_LAYOUT_LR : SWPS_LAYOUT_W2V;
+};
+}  // namespace detail
+template <class Val> struct PullCodec {
+  static const bool generic = true;
+  static const int32_t layout = detail::is_generic_layout<Val>::value;
+};
+template <class Grad> struct PushCodec {
+  static const bool generic = true;
+};
+
+namespace detail {
+template <class C> struct is_generic {
+  template <class U> static char test(decltype(&U::generic));
+  template <class U> static long test(...);
+  static const bool value = sizeof(test<C>(nullptr)) == 1;
+};
+template <class G> struct has_reset {
+  template <class U> static char test(decltype(&U::reset));
+  template <class U> static long test(...);
+  static const bool value = sizeof(test<G>(nullptr)) == 1;
+};
+template <class G> void reset_grad(G &g, std::true_type) { g.reset(); }
+template <class G> void reset_grad(G &g, std::false_type) { g = G(); }
+template <class G> void reset_grad(G &g) { reset_grad(g, std::integral_constant<bool, has_reset<G>::value>()); }
+/* the library's W2V value blocks [a(D) | b(D)] <-> the reference wire's a[i], b[i] pairs */
+inline void interleave(const char *blk, char *wire, size_t keys, int D, size_t es) {
+  for (size_t k = 0; k < keys; k++)
+    for (int i = 0; i < D; i++) {
+      std::memcpy(wire + ((k * D + i) * 2) * es, blk + (k * 2 * D + i) * es, es);
+      std::memcpy(wire + ((k * D + i) * 2 + 1) * es, blk + (k * 2 * D + D + i) * es, es);
+    }
+}
+inline void deinterleave(const char *wire, char *blk, size_t keys, int D, size_t es) {
+  for (size_t k = 0; k < keys; k++)
+    for (int i = 0; i < D; i++) {
+      std::memcpy(blk + (k * 2 * D + i) * es, wire + ((k * D + i) * 2) * es, es);
+      std::memcpy(blk + (k * 2 * D + D + i) * es, wire + ((k * D + i) * 2 + 1) * es, es);
+    }
+}
+inline size_t wire_bytes(int32_t layout) { return layout == SWPS_LAYOUT_W2V ? 8 : 4; }
+}  // namespace detail
 
 /* The shard this process serves and pulls from (one GPU = one shard). */
 inline swps_table *&global_swps_table() {
@@ -224,6 +353,84 @@ inline int32_t resolve_rule(int32_t declared, bool host_body, int32_t dflt, cons
                                             "it computes (see swiftmpi_compat.h, parameter/accessmethod.h)");
   return dflt;
 }
+inline SwpsError unrecognised(const char *what) {
+  return SwpsError(SWPS_E_UNSUPPORTED, std::string("the access method's ") + what +
+                                           " body computes none of the library's device rules: declare the rule "
+                                           "it computes (see swiftmpi_compat.h, parameter/accessmethod.h)");
+}
+template <class G> struct has_bb_read {
+  template <class U> static char test(decltype(std::declval<BinaryBuffer &>() >> std::declval<U &>()) *);
+  template <class U> static long test(...);
+  static const bool value = sizeof(test<G>(nullptr)) == 1;
+};
+inline bool near(float x, float e) { return std::fabs(x - e) <= 1e-6f * std::fmax(1.f, std::fabs(e)); }
+
+/* Recognising an unchanged app's host bodies (an app whose access methods
+ * keep the reference's shape, lr.cpp:45-80, and declare nothing): for a
+ * scalar pull value the bodies are RUN once on the host against probe values
+ * and matched to a device rule — they are never the rule that trains.
+ *   init_param:        0 -> SWPS_INIT_ZERO; the next global_random().gen_float()
+ *                      -> SWPS_INIT_FLCG (global_random() is left as it was)
+ *   apply_push_value:  two steps from Param(), read back through
+ *                      get_pull_value, = AdaGrad (fudge 1e-6f) or SGD with
+ *                      [server] initial_learning_rate
+ * Anything else, or a value type that is not a scalar, fails as before. */
+template <class Key, class Param, class PullVal, class Grad, class PullM, class PushM, bool Scalar =
+                                                                                           std::is_arithmetic<PullVal>::value &&
+                                                                                           has_get_pull_value<PullM>::value>
+struct RuleProbe {
+  static int32_t init_mode() { throw unrecognised("init_param / get_pull_value"); }
+  static int32_t push_rule() { throw unrecognised("apply_push_value"); }
+};
+template <class Key, class Param, class PullVal, class Grad, class PullM, class PushM>
+struct RuleProbe<Key, Param, PullVal, Grad, PullM, PushM, true> {
+  static PullVal read(PullM &m, const Param &p) {
+    PullVal v = PullVal();
+    m.get_pull_value(Key(), p, v);
+    return v;
+  }
+  static int32_t init_mode() { return init_mode(std::integral_constant<bool, has_init_param<PullM>::value>()); }
+  static int32_t init_mode(std::false_type) { return SWPS_INIT_ZERO; }  // Param() as it is
+  static int32_t init_mode(std::true_type) {
+    PullM m;
+    Param p = Param();
+    const Random saved = global_random();
+    Random next = saved;
+    const float draw = next.gen_float();
+    m.init_param(Key(), p);
+    global_random() = saved;
+    const PullVal v = read(m, p);
+    if ((float)v == 0.f) return SWPS_INIT_ZERO;
+    if ((float)v == draw) return SWPS_INIT_FLCG;
+    throw unrecognised("init_param");
+  }
+  static int32_t push_rule() { return push_rule(std::integral_constant<bool, has_bb_read<Grad>::value>()); }
+  static int32_t push_rule(std::false_type) { throw unrecognised("apply_push_value"); }
+  static Grad grad_of(float x) {  // what the server deserialises from the wire (global_push_access.h:86-90)
+    BinaryBuffer bb;
+    bb << x;
+    Grad g = Grad();
+    bb >> g;
+    return g;
+  }
+  static int32_t push_rule(std::true_type) {
+    PushM m;
+    PullM pm;
+    const float lr = global_config().get("server", "initial_learning_rate").to_float();
+    const float fudge = 1e-6f, a = 0.5f, b = -0.25f;
+    Param p = Param();
+    const float v0 = (float)read(pm, p);
+    m.apply_push_value(Key(), p, grad_of(a));
+    const float v1 = (float)read(pm, p);
+    m.apply_push_value(Key(), p, grad_of(b));
+    const float v2 = (float)read(pm, p);
+    const float g2a = a * a, g2b = g2a + b * b;
+    const float ada1 = v0 + lr * a / float(std::sqrt(g2a + fudge));
+    if (near(v1, ada1) && near(v2, ada1 + lr * b / float(std::sqrt(g2b + fudge)))) return SWPS_PUSH_ADAGRAD;
+    if (near(v1, v0 + lr * a) && near(v2, v0 + lr * a + lr * b)) return SWPS_PUSH_SGD;
+    throw unrecognised("apply_push_value");
+  }
+};
 }  // namespace detail
 
 /* ---- cluster/server.h ClusterServer --------------------------------------
@@ -241,15 +448,21 @@ class ClusterServer {
   typedef Grad grad_t;
   typedef PullM pull_access_t;
   typedef PushM push_access_t;
+  typedef detail::RuleProbe<Key, Param, PullVal, Grad, PullM, PushM> probe_t;
   static int32_t layout() { return PullCodec<PullVal>::layout; }
   static int32_t init_mode() {
-    return detail::resolve_rule(PullM::init_mode,
-                                detail::has_init_param<PullM>::value || detail::has_get_pull_value<PullM>::value,
-                                SWPS_INIT_HASH, "init_param / get_pull_value");
+    const bool body = detail::has_init_param<PullM>::value || detail::has_get_pull_value<PullM>::value;
+    if (PullM::init_mode == SWPS_RULE_UNSPECIFIED && body && std::is_arithmetic<PullVal>::value)
+      return probe_t::init_mode();  // an unchanged reference app's bodies (see detail::RuleProbe)
+    return detail::resolve_rule(PullM::init_mode, body, SWPS_INIT_HASH, "init_param / get_pull_value");
   }
+  /* SWPS_INIT_FLCG continues global_random()'s float stream from here */
+  static uint64_t init_seed() { return init_mode() == SWPS_INIT_FLCG ? global_random().float_state() : 0; }
   static int32_t push_rule() {
-    return detail::resolve_rule(PushM::push_rule, detail::has_apply_push_value<PushM>::value, SWPS_PUSH_ADAGRAD,
-                                "apply_push_value");
+    const bool body = detail::has_apply_push_value<PushM>::value;
+    if (PushM::push_rule == SWPS_RULE_UNSPECIFIED && body && std::is_arithmetic<PullVal>::value)
+      return probe_t::push_rule();
+    return detail::resolve_rule(PushM::push_rule, body, SWPS_PUSH_ADAGRAD, "apply_push_value");
   }
   void load(const std::string &path);  // defined after Cluster's globals
 };
@@ -291,7 +504,6 @@ template <typename Key, typename Param, typename Grad> class LocalParamCache {
 template <typename Key, typename Val, typename Grad> class GlobalPullAccess {
  public:
   typedef LocalParamCache<Key, Val, Grad> param_cache_t;
-  typedef typename PullCodec<Val>::wire_t wire_t;
 
   explicit GlobalPullAccess(swps_table *t = nullptr) : _t(t) {}
 
@@ -301,6 +513,12 @@ template <typename Key, typename Val, typename Grad> class GlobalPullAccess {
     std::vector<uint64_t> k;
     k.reserve(keys.size());
     for (const auto &key : keys) k.push_back((uint64_t)key);
+    pull(t, k, cache, std::integral_constant<bool, detail::is_generic<PullCodec<Val> >::value>());
+  }
+
+ private:
+  static void pull(swps_table *t, const std::vector<uint64_t> &k, param_cache_t &cache, std::false_type) {
+    typedef typename PullCodec<Val>::wire_t wire_t;
     const int P = PullCodec<Val>::elems();
     std::vector<wire_t> vals(k.size() * (size_t)P);
     swps_check(swps_pull_h(t, k.data(), k.size(), vals.data()));
@@ -310,8 +528,26 @@ template <typename Key, typename Val, typename Grad> class GlobalPullAccess {
       cache.grads()[key] = Grad();
     }
   }
-
- private:
+  static void pull(swps_table *t, const std::vector<uint64_t> &k, param_cache_t &cache, std::true_type) {
+    int32_t row = 0, P = 0, push = 0;
+    swps_check(swps_table_row_elems(t, &row, &P, &push));
+    const int32_t layout = PullCodec<Val>::layout;
+    const size_t es = detail::wire_bytes(layout), stride = (size_t)P * es;
+    std::vector<char> raw(k.size() * stride + 1), wire;
+    swps_check(swps_pull_h(t, k.data(), k.size(), &raw[0]));
+    const char *src = &raw[0];
+    if (layout == SWPS_LAYOUT_W2V) {  // the reference's wire: h[i], v[i] pairs
+      wire.resize(raw.size());
+      detail::interleave(&raw[0], &wire[0], k.size(), P / 2, es);
+      src = &wire[0];
+    }
+    for (size_t i = 0; i < k.size(); i++) {
+      const Key key = (Key)k[i];
+      BinaryBuffer bb(src + i * stride, stride);
+      bb >> cache.params()[key];  // the app's own deserialiser (global_pull_access.h:88-97)
+      cache.grads()[key] = Grad();
+    }
+  }
   swps_table *_t;
 };
 
@@ -323,7 +559,6 @@ template <typename Key, typename Val, typename Grad> class GlobalPullAccess {
 template <typename Key, typename Val, typename Grad> class GlobalPushAccess {
  public:
   typedef LocalParamCache<Key, Val, Grad> param_cache_t;
-  typedef typename PullCodec<Val>::wire_t wire_t;
 
   explicit GlobalPushAccess(swps_table *t = nullptr) : _t(t) {}
 
@@ -332,6 +567,13 @@ template <typename Key, typename Val, typename Grad> class GlobalPushAccess {
     if (!t) throw SwpsError(SWPS_E_STATE, "no shard: create a Cluster first");
     int32_t row = 0, pull = 0, push = 0;
     swps_check(swps_table_row_elems(t, &row, &pull, &push));
+    push_(t, keys, cache, push, std::integral_constant<bool, detail::is_generic<PushCodec<Grad> >::value>());
+  }
+
+ private:
+  static void push_(swps_table *t, const std::unordered_set<Key> &keys, param_cache_t &cache, int32_t push,
+                    std::false_type) {
+    typedef typename PullCodec<Val>::wire_t wire_t;
     std::vector<uint64_t> k;
     std::vector<wire_t> g;
     for (const auto &key : keys) {
@@ -343,8 +585,32 @@ template <typename Key, typename Val, typename Grad> class GlobalPushAccess {
     }
     swps_check(swps_push_h(t, k.data(), k.size(), g.data()));  // n = 0 still joins a routed exchange
   }
-
- private:
+  static void push_(swps_table *t, const std::unordered_set<Key> &keys, param_cache_t &cache, int32_t push,
+                    std::true_type) {
+    const int32_t layout = PullCodec<Val>::layout;
+    const size_t es = detail::wire_bytes(layout), stride = (size_t)push * es;
+    std::vector<uint64_t> k;
+    BinaryBuffer bb;
+    for (const auto &key : keys) {
+      auto it = cache.grads().find(key);
+      if (it == cache.grads().end()) continue;
+      const size_t before = bb.size();
+      bb << it->second;  // the app's own serialiser: the mean gradient (lr.cpp:32-38)
+      detail::reset_grad(it->second);
+      const size_t nb = bb.size() - before;
+      if (nb == 0) continue;  // nothing to push for this key
+      if (nb != stride)
+        throw SwpsError(SWPS_E_UNSUPPORTED, "a gradient serialises to " + std::to_string(nb) +
+                                                " bytes; the shard's push value is " + std::to_string(stride));
+      k.push_back((uint64_t)key);
+    }
+    std::vector<char> blk(bb.size() + 1);
+    if (layout == SWPS_LAYOUT_W2V)
+      detail::deinterleave(bb.buffer(), &blk[0], k.size(), push / 2, es);
+    else if (bb.size())
+      std::memcpy(&blk[0], bb.buffer(), bb.size());
+    swps_check(swps_push_h(t, k.data(), k.size(), &blk[0]));  // n = 0 still joins a routed exchange
+  }
   swps_table *_t;
 };
 
@@ -371,11 +637,13 @@ template <class Key, class Val, class Grad> GlobalPushAccess<Key, Val, Grad> &gl
 struct W2VServer {
   static int32_t layout() { return SWPS_LAYOUT_W2V; }
   static int32_t init_mode() { return SWPS_INIT_HASH; }
+  static uint64_t init_seed() { return 0; }
   static int32_t push_rule() { return SWPS_PUSH_ADAGRAD; }
 };
 struct LRServer {
   static int32_t layout() { return SWPS_LAYOUT_LR; }
   static int32_t init_mode() { return SWPS_INIT_HASH; }
+  static uint64_t init_seed() { return 0; }
   static int32_t push_rule() { return SWPS_PUSH_ADAGRAD; }
 };
 struct ClusterWorker {};
@@ -388,7 +656,9 @@ inline int env_int(const char *a, const char *b, int dflt) {
 
 template <class WorkerT, class ServerT, class KeyT> class Cluster {
  public:
-  explicit Cluster(uint64_t capacity = 1u << 22, int32_t dtype = SWPS_F32) {
+  /* capacity: keys this rank's shard holds (SWPS_CAPACITY overrides the default) */
+  explicit Cluster(uint64_t capacity = 0, int32_t dtype = SWPS_F32) {
+    if (!capacity) capacity = (uint64_t)env_int("SWPS_CAPACITY", nullptr, 1 << 22);
     _rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", 0);
     _world = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1);
     const int dev = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", 0);
@@ -401,7 +671,7 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
     c.learning_rate = global_config().get("server", "initial_learning_rate").to_float();
     c.fudge = 1e-6f;
     c.init_mode = ServerT::init_mode();
-    c.seed = 0;
+    c.seed = ServerT::init_seed();
     c.push_rule = ServerT::push_rule();
     swps_check(swps_table_create(&c, &_t));
     global_swps_table() = _t;

@@ -75,6 +75,10 @@ const char *swps_build_hash(void);
 /* key initialisation on a pull miss (PullAccessMethod::init_param) */
 #define SWPS_INIT_ZERO 0
 #define SWPS_INIT_HASH 1 /* W2V: (u-0.5)/D, LR: u in [0,1); u from (seed,key,i) */
+#define SWPS_INIT_FLCG 2 /* LR only: w = global_random().gen_float() per new key in the order the
+                          * call lists them (LRPullAccessMethod::init_param, lr.cpp:48-50; random.h:
+                          * 33-36) — the float LCG continues across calls; `seed` = its state before
+                          * the first draw (0: the reference's ULONG_MAX / 2) */
 
 /* push rule (PushAccessMethod::apply_push_value, accessmethod.h:26-35) */
 #define SWPS_PUSH_ADAGRAD 0 /* W2V word2vec_global.h:176-185, LR lr.cpp:68-75: g2 += g*g;

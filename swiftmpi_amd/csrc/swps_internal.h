@@ -177,6 +177,8 @@ struct swps_table {
   uint64_t snap_sum = 0;  // checksum of the snapshot last saved from / restored into this table (0: none);
                           // worker-state snapshots record it so a resume pairs the two files of one save
   swps::DevMem isnew;     // find_or_insert: per-key "inserted by this call" flags
+  swps::DevMem flcg;      // SWPS_INIT_FLCG: [float-LCG state, draws of the current call] (u64 x 2)
+  swps::DevMem flcg_blk;  // SWPS_INIT_FLCG: per-block new-key counts -> offsets
   // key-sharded mode (swps_table_route, swps_comm.hip)
   swps_comm *comm = nullptr;
   int32_t frag_num = 0;

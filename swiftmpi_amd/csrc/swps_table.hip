@@ -130,6 +130,59 @@ __global__ void k_init_rows(const uint64_t *__restrict__ keys, const uint32_t *_
   }
 }
 
+// SWPS_INIT_FLCG (LRPullAccessMethod::init_param = global_random().gen_float(), lr.cpp:48-50): the
+// new keys of one call take consecutive draws of the float LCG in the order the call lists them.
+// Three passes: new keys per 256-key block, the blocks' exclusive offsets (one block), each new
+// key's draw by jump-ahead from the call's start state.
+__global__ __launch_bounds__(256) void k_flcg_counts(const uint8_t *__restrict__ isnew, uint64_t n,
+                                                     uint32_t *__restrict__ blk) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = __syncthreads_count(i < n && isnew[i]);
+  if (threadIdx.x == 0) blk[blockIdx.x] = (uint32_t)c;
+}
+
+__global__ __launch_bounds__(1024) void k_flcg_scan(uint32_t *__restrict__ blk, uint64_t nb,
+                                                    uint64_t *__restrict__ st) {
+  __shared__ uint32_t part[1024];
+  uint64_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nb; b0 += 1024) {  // 1024 blocks at a time, in order
+    const uint64_t b = b0 + threadIdx.x;
+    const uint32_t v = b < nb ? blk[b] : 0u;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+      const uint32_t x = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0u;
+      __syncthreads();
+      part[threadIdx.x] += x;
+      __syncthreads();
+    }
+    if (b < nb) blk[b] = (uint32_t)carry + part[threadIdx.x] - v;
+    carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) st[1] = carry;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_flcg_init(const uint8_t *__restrict__ isnew,
+                                                   const uint32_t *__restrict__ rows_idx, uint64_t n,
+                                                   const uint32_t *__restrict__ blk, const uint64_t *__restrict__ st,
+                                                   T *rows, int R) {
+  __shared__ uint32_t wcnt[4];
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool nw = i < n && isnew[i];
+  const uint64_t m = __ballot(nw);
+  if (lane == 0) wcnt[wv] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (!nw) return;
+  uint32_t r = blk[blockIdx.x] + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
+  for (int q = 0; q < wv; q++) r += wcnt[q];
+  rows[(uint64_t)rows_idx[i] * R] = (T)flcg_value(lcg_jump(st[0], (uint64_t)r + 1, kFlcgA, kLcgC));
+}
+
+__global__ void k_flcg_advance(uint64_t *st) { st[0] = lcg_jump(st[0], st[1], kFlcgA, kLcgC); }
+
 template <typename T>
 __global__ void k_copy_rows_out(const uint32_t *__restrict__ rows_idx, uint64_t n, const T *__restrict__ rows, int R,
                                 int ncopy, T *__restrict__ out) {
@@ -446,6 +499,20 @@ static int find_or_insert_async(swps_table *t, const uint64_t *d_keys, uint64_t 
                                                           t->row_elems, t->cfg.layout, t->cfg.dim,
                                                           t->cfg.init_mode, t->cfg.seed);
   SWPS_HIP(hipGetLastError());
+  if (t->cfg.init_mode == SWPS_INIT_FLCG) {  // the rows are zero: their w from the call-order draws
+    const uint64_t nb = (n + 255) / 256;
+    SWPS_TRY(t->flcg_blk.ensure(nb * 4));
+    uint32_t *blk = t->flcg_blk.as<uint32_t>();
+    uint64_t *st = t->flcg.as<uint64_t>();
+    k_flcg_counts<<<nb, 256, 0, s>>>(isnew, n, blk);
+    k_flcg_scan<<<1, 1024, 0, s>>>(blk, nb, st);
+    if (t->cfg.dtype == SWPS_F64)
+      k_flcg_init<double><<<nb, 256, 0, s>>>(isnew, d_rows_out, n, blk, st, t->rows.as<double>(), t->row_elems);
+    else
+      k_flcg_init<float><<<nb, 256, 0, s>>>(isnew, d_rows_out, n, blk, st, t->rows.as<float>(), t->row_elems);
+    k_flcg_advance<<<1, 1, 0, s>>>(st);
+    SWPS_HIP(hipGetLastError());
+  }
   return SWPS_OK;
 }
 
@@ -673,9 +740,11 @@ int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
   if (cfg->push_rule != SWPS_PUSH_ADAGRAD && cfg->push_rule != SWPS_PUSH_SGD)
     return fail(SWPS_E_UNSUPPORTED, "push rule " + std::to_string(cfg->push_rule) +
                                         ": the library implements SWPS_PUSH_ADAGRAD and SWPS_PUSH_SGD only");
-  if (cfg->init_mode != SWPS_INIT_ZERO && cfg->init_mode != SWPS_INIT_HASH)
+  if (cfg->init_mode != SWPS_INIT_ZERO && cfg->init_mode != SWPS_INIT_HASH && cfg->init_mode != SWPS_INIT_FLCG)
     return fail(SWPS_E_UNSUPPORTED, "init mode " + std::to_string(cfg->init_mode) +
-                                        ": the library implements SWPS_INIT_ZERO and SWPS_INIT_HASH only");
+                                        ": the library implements SWPS_INIT_ZERO, SWPS_INIT_HASH and SWPS_INIT_FLCG");
+  if (cfg->init_mode == SWPS_INIT_FLCG && cfg->layout != SWPS_LAYOUT_LR)
+    return fail(SWPS_E_UNSUPPORTED, "SWPS_INIT_FLCG (LR's gen_float init) needs SWPS_LAYOUT_LR");
   SWPS_HIP(hipSetDevice(cfg->device));
   swps_table *t = new swps_table();
   t->cfg = *cfg;
@@ -710,6 +779,11 @@ int swps_table_create(const swps_table_cfg *cfg, swps_table **out) {
   if (!rc) rc = t->row_key.ensure(cfg->capacity * 8);
   if (!rc) rc = t->rows.ensure(cfg->capacity * (uint64_t)t->row_elems * t->esize);
   if (!rc) rc = t->counters.ensure(16);
+  if (!rc) rc = t->flcg.ensure(16);
+  if (!rc) {  // the float LCG's state before the first draw (random.h:39-40: ULONG_MAX / 2)
+    const uint64_t st[2] = {cfg->seed ? cfg->seed : ~0ULL / 2, 0};
+    if (hipMemcpy(t->flcg.p, st, 16, hipMemcpyHostToDevice) != hipSuccess) rc = fail(SWPS_E_HIP, "memcpy");
+  }
   if (!rc && hipMemsetAsync(t->keys.p, 0xFF, ns * 8, t->stream) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
   if (!rc && hipMemsetAsync(t->slot_row.p, 0xFF, ns * 4, t->stream) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");
   if (!rc && hipMemsetAsync(t->counters.p, 0, 16, t->stream) != hipSuccess) rc = fail(SWPS_E_HIP, "memset");

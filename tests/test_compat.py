@@ -248,3 +248,125 @@ def test_compat_lr_train_dump_then_predict_mode(compat_bin, lib, gpu, tmp_path):
     m2.train(3)
     p2, _ = m2.predict()
     assert np.allclose(p, p2, rtol=1e-4, atol=1e-6)
+
+
+# ---- the reference's own mains, UNCHANGED (tests/cpp/build_ref_apps.py) -----
+LR_REF_CONF = """[ worker ]
+minibatch: 200
+nthreads: 1
+[ server ]
+initial_learning_rate: 0.05
+frag_num: 1000
+out_param_prefix: %s
+"""
+
+
+def _ref_apps():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "cpp"))
+    import build_ref_apps
+    return build_ref_apps
+
+
+def test_reference_mains_compile_unchanged(lib):
+    """apps/word2vec/w2v.cpp, w2v_local.cpp and apps/logistic/lr.cpp, read
+    where they lie under /root/reference, compile with g++ -std=c++11 against
+    include/swiftmpi/ (the reference's include names) and link libswps.so;
+    the binaries run (usage path, no GPU work)."""
+    b = _ref_apps()
+    if not os.path.isdir(b.REF):
+        pytest.skip("no reference tree here (the GPU box uses the binaries built in the build container)")
+    bins = b.build()
+    assert set(bins) == {"w2v", "w2v_local", "lr"}
+    r = subprocess.run([bins["lr"], "-mode"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "missing parameter" in r.stderr and "Train Mode" in r.stdout
+    r = subprocess.run([bins["w2v"]], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "Word2Vec application" in r.stdout
+
+
+def _ref_bin(name):
+    bins = _ref_apps().binaries()
+    if name not in bins:
+        pytest.skip("reference mains not built (tests/cpp/build_ref_apps.py needs /root/reference)")
+    return bins[name]
+
+
+@pytest.mark.gpu
+def test_reference_w2v_main_unchanged_equals_compat_driver(compat_bin, gpu, tmp_path):
+    """w2v.cpp itself (Word2Vec<MiniBatch>, server_t, Cluster, global_mpi)
+    trains on the GPU and dumps exactly what the compat driver's Word2VecApp
+    does (which test_compat_w2v_and_s2v_mains_match_python ties to the Python
+    mirror)."""
+    ref = _ref_bin("w2v")
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF)
+    corpus = zipf_corpus(str(tmp_path / "c.txt"), 90, 200, seed=41)
+    a, b = str(tmp_path / "ref_param"), str(tmp_path / "compat_param")
+    _run(ref, "-config", str(conf), "-data", corpus, "-niters", "2", "-output", a)
+    _run(compat_bin, "w2v", "-config", str(conf), "-data", corpus, "-niters", "2", "-output", b)
+    la, lb = open(a + "-0.txt").read().splitlines(), open(b + "-0.txt").read().splitlines()
+    assert len(la) > 100 and sorted(la) == sorted(lb)
+
+
+@pytest.mark.gpu
+def test_reference_w2v_local_main_unchanged(lib, gpu, tmp_path):
+    """w2v_local.cpp (word2vec.h: atoi keys, a vocabulary and unigram table per
+    minibatch) = the Python mirror's minibatch_vocab mode on the same corpus."""
+    ref = _ref_bin("w2v_local")
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF)
+    corpus = int_corpus(str(tmp_path / "c.txt"), 80, 150, seed=43)
+    out = str(tmp_path / "param")
+    _run(ref, "-config", str(conf), "-data", corpus, "-niters", "2", "-output", out)
+    t = lib.Table("w2v", dim=16, capacity=1 << 22, dtype="f32", learning_rate=0.7)
+    w = lib.Word2Vec(t, window=3, negative=4, minibatch=20, sample=1e-3, alpha=0.05, key_mode="atoi",
+                     minibatch_vocab=True)
+    w.load_text(corpus)
+    w.init()
+    w.train(2)
+    py = str(tmp_path / "py.txt")
+    t.dump(py)
+    la, lb = open(out + "-0.txt").read().splitlines(), open(py).read().splitlines()
+    assert len(la) > 50 and sorted(la) == sorted(lb)
+
+
+@pytest.mark.gpu
+def test_reference_lr_main_unchanged_matches_oracle(lib, oracle_mod, gpu, tmp_path):
+    """lr.cpp itself: its LR class learns on the host through the unchanged
+    PS API (pull_with_barrier / push_with_barrier with its own BinaryBuffer
+    operators) against the HBM shard; its access methods' host bodies are
+    recognised as the device's gen_float init (SWPS_INIT_FLCG) and AdaGrad
+    rules.  The trained dump (server.out_param_prefix + ".txt") matches the
+    oracle's lr.cpp restatement, and predict mode (load_param, predict) gives
+    the Python mirror's predictions from that dump."""
+    ref = _ref_bin("lr")
+    prefix = str(tmp_path / "lr_param")
+    conf = tmp_path / "lr.conf"
+    conf.write_text(LR_REF_CONF % prefix)
+    data = os.path.join(GOLDEN, "lr_data.txt")
+    r = subprocess.run([ref, "-mode", "train", "-config", str(conf), "-dataset", data, "-niters", "3"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    got = {}
+    for line in open(prefix + ".txt"):
+        k, v = line.split("\t")
+        got[int(k)] = float(v)
+    orc = oracle_mod.LR(data, 200, 0.05)
+    orc.train(3)
+    ko, wo, _ = orc.params()
+    assert sorted(got) == [int(k) for k in ko]
+    gw = np.array([got[int(k)] for k in ko])
+    assert np.allclose(gw, wo, rtol=2e-5, atol=1e-6), np.abs(gw - wo).max()
+    pred = str(tmp_path / "pred.txt")
+    r = subprocess.run([ref, "-mode", "predict", "-config", str(conf), "-dataset", data, "-param_path",
+                        prefix + ".txt", "-out_prefix", pred, "-niters", "1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    p_ref = np.loadtxt(pred)
+    t = lib.Table("lr", capacity=1 << 22, dtype="f32", learning_rate=0.05)
+    t.load(prefix + ".txt")
+    m = lib.LR(t, minibatch=200)
+    m.load_text(data)
+    m.init()
+    p, _ = m.predict()
+    assert len(p_ref) == len(p) > 0 and np.allclose(p_ref, p, rtol=1e-5, atol=1e-6)
