@@ -104,7 +104,18 @@ inline void raw_log(const char *sev, const char *fmt, ...) {
 /* ---- utils/mpi.h: one process per GPU, rank / size from the launcher -------- */
 class GlobalMPI {
  public:
-  static void initialize(int, char **) {}
+  /* lr.cpp's main never loads its -config (lr.cpp:413-509 has no load_conf: the reference's
+   * Cluster() then CHECK-fails on the empty config, cluster.h:11-13); the -config of the command
+   * line is loaded here, before the app's own load_conf / parse (which finds the same keys again:
+   * the first definition wins) */
+  static void initialize(int argc, char **argv) {
+    for (int i = 1; i + 1 < argc; i++)
+      if (std::string(argv[i]) == "-config" || std::string(argv[i]) == "--config") {
+        global_config().load_conf(argv[i + 1]);
+        global_config().parse();
+        break;
+      }
+  }
   int rank() const { return env_int("RANK", "OMPI_COMM_WORLD_RANK", 0); }
   int size() const { return env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1); }
   /* a collective over the key-sharded shard (swps_barrier); one rank: its device work retired */

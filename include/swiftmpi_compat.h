@@ -359,7 +359,8 @@ inline SwpsError unrecognised(const char *what) {
                                            "it computes (see swiftmpi_compat.h, parameter/accessmethod.h)");
 }
 template <class G> struct has_bb_read {
-  template <class U> static char test(decltype(std::declval<BinaryBuffer &>() >> std::declval<U &>()) *);
+  template <class U>
+  static char test(typename std::remove_reference<decltype(std::declval<BinaryBuffer &>() >> std::declval<U &>())>::type *);
   template <class U> static long test(...);
   static const bool value = sizeof(test<G>(nullptr)) == 1;
 };
@@ -369,8 +370,9 @@ inline bool near(float x, float e) { return std::fabs(x - e) <= 1e-6f * std::fma
  * keep the reference's shape, lr.cpp:45-80, and declare nothing): for a
  * scalar pull value the bodies are RUN once on the host against probe values
  * and matched to a device rule — they are never the rule that trains.
- *   init_param:        0 -> SWPS_INIT_ZERO; the next global_random().gen_float()
- *                      -> SWPS_INIT_FLCG (global_random() is left as it was)
+ *   init_param:        twice: 0, 0 -> SWPS_INIT_ZERO; the next two
+ *                      global_random().gen_float() draws -> SWPS_INIT_FLCG
+ *                      (global_random() is left as it was)
  *   apply_push_value:  two steps from Param(), read back through
  *                      get_pull_value, = AdaGrad (fudge 1e-6f) or SGD with
  *                      [server] initial_learning_rate
@@ -393,15 +395,16 @@ struct RuleProbe<Key, Param, PullVal, Grad, PullM, PushM, true> {
   static int32_t init_mode(std::false_type) { return SWPS_INIT_ZERO; }  // Param() as it is
   static int32_t init_mode(std::true_type) {
     PullM m;
-    Param p = Param();
+    Param p = Param(), q = Param();
     const Random saved = global_random();
     Random next = saved;
-    const float draw = next.gen_float();
+    const float d1 = next.gen_float(), d2 = next.gen_float();  // two draws: the stream's first is 0.5
     m.init_param(Key(), p);
+    m.init_param(Key(), q);
     global_random() = saved;
-    const PullVal v = read(m, p);
-    if ((float)v == 0.f) return SWPS_INIT_ZERO;
-    if ((float)v == draw) return SWPS_INIT_FLCG;
+    const float v1 = (float)read(m, p), v2 = (float)read(m, q);
+    if (v1 == 0.f && v2 == 0.f) return SWPS_INIT_ZERO;
+    if (v1 == d1 && v2 == d2) return SWPS_INIT_FLCG;
     throw unrecognised("init_param");
   }
   static int32_t push_rule() { return push_rule(std::integral_constant<bool, has_bb_read<Grad>::value>()); }

@@ -47,7 +47,7 @@ extern "C" {
 const char *swps_last_error(void);
 int swps_version(void);
 /* sha256 (hex) of the sources the library was built from: every file of
- * swiftmpi_amd/csrc/ and include/, by name then content (swiftmpi_amd/build.py
+ * swiftmpi_amd/csrc/ and this header, by name then content (swiftmpi_amd/build.py
  * source_hash); a prebuilt library is checked against the checked-out tree */
 const char *swps_build_hash(void);
 

@@ -124,7 +124,8 @@ class Table:
                  init="hash", seed=0, device=0, push_rule="adagrad"):
         cfg = capi.TableCfg(device, capi.LAYOUT_W2V if layout == "w2v" else capi.LAYOUT_LR,
                             capi.F64 if dtype == "f64" else capi.F32, dim, capacity, learning_rate, fudge,
-                            capi.INIT_HASH if init == "hash" else capi.INIT_ZERO, seed,
+                            {"hash": capi.INIT_HASH, "zero": capi.INIT_ZERO, "flcg": capi.INIT_FLCG}.get(init, capi.INIT_ZERO),
+                            seed,
                             {"adagrad": capi.PUSH_ADAGRAD, "sgd": capi.PUSH_SGD}[push_rule])
         h = ctypes.c_void_p()
         check(capi.lib().swps_table_create(ctypes.byref(cfg), ctypes.byref(h)))

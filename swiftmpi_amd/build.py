@@ -32,24 +32,23 @@ def sources():
 
 
 def headers():
+    """The library's own headers and the C ABI it implements (include/swps.h); the C++ drop-in
+    headers over it (swiftmpi_compat.h, swiftmpi/) are not part of the library."""
     hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
-    return hs
+    return hs + [os.path.join(INCLUDE, "swps.h")]
 
 
 HASH_MARK = "SWPS_BUILD_HASH:"
 
 
 def source_hash():
-    """sha256 over every source and header the library is built from (name, then content)."""
+    """sha256 over every source and header the library is built from (csrc/ and include/swps.h;
+    name, then content)."""
     import hashlib
     h = hashlib.sha256()
-    for d in (CSRC, INCLUDE):
-        for f in sorted(os.listdir(d)):
-            p = os.path.join(d, f)
-            if os.path.isfile(p) and f.endswith((".hip", ".cpp", ".h")):
-                h.update(f.encode() + b"\0")
-                h.update(open(p, "rb").read())
+    for p in sorted(sources() + headers(), key=os.path.basename):
+        h.update(os.path.basename(p).encode() + b"\0")
+        h.update(open(p, "rb").read())
     return h.hexdigest()
 
 

@@ -16,7 +16,7 @@ ERRORS = {-1: "SWPS_E_OOM", -2: "SWPS_E_BADKEY", -3: "SWPS_E_HIP", -4: "SWPS_E_R
           -6: "SWPS_E_STATE", -7: "SWPS_E_UNSUPPORTED", -8: "SWPS_E_IO"}
 LAYOUT_W2V, LAYOUT_LR = 0, 1
 F32, F64 = 0, 1
-INIT_ZERO, INIT_HASH = 0, 1
+INIT_ZERO, INIT_HASH, INIT_FLCG = 0, 1, 2
 KEY_BKDR, KEY_ATOI = 0, 1
 W2V_INIT_REF, W2V_INIT_TABLE = 0, 1
 PUSH_ADAGRAD, PUSH_SGD = 0, 1

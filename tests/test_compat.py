@@ -268,6 +268,27 @@ def _ref_apps():
     return build_ref_apps
 
 
+def test_host_body_rules_are_recognised(lib, tmp_path):
+    """Access methods in the reference's shape with host bodies and no declared
+    rule (lr.cpp:45-80's form): the bodies are run on probe values and matched
+    to the device's gen_float init (SWPS_INIT_FLCG) / zero init and AdaGrad /
+    SGD push rules without consuming global_random(); a body that matches no
+    device rule fails with SWPS_E_UNSUPPORTED (-7)."""
+    out = str(tmp_path / "probe")
+    cmd = ["g++", "-std=c++11", "-O1", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I" + os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "cpp", "probe_rules.cpp"), "-L" + os.path.join(ROOT, "swiftmpi_amd", "lib"),
+           "-lswps", "-Wl,-rpath," + os.path.join(ROOT, "swiftmpi_amd", "lib"), "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    conf = tmp_path / "c.conf"
+    conf.write_text(LR_CONF)
+    r = subprocess.run([out, str(conf)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines == ["flcg_adagrad init=2 push=0 seed_ok=1", "zero_sgd init=0 push=1 seed_ok=1",
+                     "half_adagrad error -7", "flcg_momentum error -7"], lines
+
+
 def test_reference_mains_compile_unchanged(lib):
     """apps/word2vec/w2v.cpp, w2v_local.cpp and apps/logistic/lr.cpp, read
     where they lie under /root/reference, compile with g++ -std=c++11 against

@@ -101,3 +101,28 @@ def test_duplicate_keys_in_one_pull_share_a_row(lib, gpu):
     assert torch.equal(v[:32], v[32:64]) and torch.equal(v[:7], v[64:])
     assert v.abs().sum(dim=1).min() > 0  # every copy got the initialised row
     assert torch.equal(t.pull(base), v[:32])
+
+
+def test_flcg_init_continues_gen_float_in_call_order(lib, gpu):
+    """SWPS_INIT_FLCG (LRPullAccessMethod::init_param = global_random().gen_float(),
+    lr.cpp:48-50): the new keys of each pull take the next draws of the float
+    LCG in the order the call lists them; keys already held keep their value
+    and draw nothing; the stream continues across calls (and blocks of keys)."""
+    import torch
+    from test_lr_gpu import _gen_float_draws
+    t = lib.Table("lr", capacity=1 << 16, dtype="f32", learning_rate=0.05, init="flcg")
+    rng = np.random.default_rng(4)
+    k1 = rng.choice(1 << 40, 3000, replace=False).astype(np.int64) + 1
+    k2 = np.concatenate([k1[::7], rng.choice(1 << 40, 1500, replace=False).astype(np.int64) + (1 << 41)])
+    k2 = k2[rng.permutation(len(k2))]
+    v1 = t.pull(torch.as_tensor(k1, device="cuda")).cpu().numpy()[:, 0]
+    v2 = t.pull(torch.as_tensor(k2, device="cuda")).cpu().numpy()[:, 0]
+    draws = _gen_float_draws(3000 + 1500)
+    assert np.array_equal(v1, draws[:3000])
+    old = {int(k): x for k, x in zip(k1, v1)}
+    new = [i for i, k in enumerate(k2) if int(k) not in old]
+    assert len(new) == 1500
+    assert np.array_equal(v2[new], draws[3000:])
+    assert all(v2[i] == old[int(k)] for i, k in enumerate(k2) if int(k) in old)
+    with pytest.raises(lib.SwpsError):
+        lib.Table("w2v", dim=8, capacity=64, init="flcg")  # LR layout only
