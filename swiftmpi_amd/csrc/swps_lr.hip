@@ -317,6 +317,85 @@ __global__ __launch_bounds__(256) void k_lr_forward_g(const uint64_t *__restrict
   }
 }
 
+// Record-contiguous forward (SWPS_LR_FWD_C, the default): a block takes a static chunk of whole rows
+// holding at most RPT*256 records (built on the host at the first batch), so its threads load the
+// chunk's indices and values as contiguous 16-B-aligned runs straight from the chunk's first record —
+// no per-row offset load in front of them — while the rows' offsets and labels load beside them.
+// Products w*x go to LDS in record order; one thread per row then adds its row's products in
+// feature order in fp32 (lr.cpp:358-375, -ffp-contract=off): the same products and the same ordered
+// sum as every other forward form, so bit-identical.  Two dependent memory round trips per record
+// (index -> weight) instead of three, and RPT*256 records per block: a Criteo batch (2.56M records)
+// is ~1,250 blocks of 4 waves, all resident at once.
+constexpr int kLrFwdRpt = 8;
+template <int RPT>
+__global__ __launch_bounds__(256) void k_lr_forward_c(const uint2 *__restrict__ chunks,
+                                                      const uint64_t *__restrict__ row_off,
+                                                      const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
+                                                      const float *__restrict__ label, uint64_t r0,
+                                                      const float *__restrict__ rows, int stride,
+                                                      float *__restrict__ err, float *__restrict__ err2,
+                                                      const uint32_t *__restrict__ hrow, uint32_t nhot) {
+  constexpr int CAP = RPT * 256;
+  __shared__ float prod[CAP];
+  __shared__ float wh[kLrHot];
+  const int tid = threadIdx.x;
+  const float hw = hrow && (uint32_t)tid < nhot ? rows[(uint64_t)hrow[tid] * 2] : 0.f;
+  const uint2 ch = chunks[blockIdx.x];  // first row (batch-relative), rows
+  const uint64_t rf = r0 + ch.x;
+  const uint64_t c0 = row_off[rf], c1 = row_off[rf + ch.y];
+  const uint32_t n = (uint32_t)(c1 - c0);
+  uint32_t f[RPT];
+  float x[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; k++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+    f[k] = i < n ? fidx[c0 + i] : 0u;
+    x[k] = i < n ? fval[c0 + i] : 0.f;
+  }
+  // this thread's row (rows beyond 256 per chunk are looped below)
+  uint64_t ra = 0, rb = 0;
+  float y = 0.f;
+  if ((uint32_t)tid < ch.y) {
+    ra = row_off[rf + tid];
+    rb = row_off[rf + tid + 1];
+    y = label[rf + tid];
+  }
+  if (hrow) {
+    if ((uint32_t)tid < nhot) wh[tid] = hw;
+    __syncthreads();
+  }
+  float w[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; k++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+    if (i >= n)
+      w[k] = 0.f;
+    else if (hrow)
+      w[k] = (f[k] & kLrHotBit) ? wh[f[k] & (kLrHotBit - 1)] : rows[(uint64_t)f[k] * 2];
+    else
+      w[k] = weight_at(rows, f[k], stride);
+  }
+#pragma unroll
+  for (int k = 0; k < RPT; k++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+    if (i < n) prod[i] = w[k] * x[k];
+  }
+  __syncthreads();
+  for (uint32_t r = (uint32_t)tid; r < ch.y; r += 256u) {
+    if (r >= 256u) {
+      ra = row_off[rf + r];
+      rb = row_off[rf + r + 1];
+      y = label[rf + r];
+    }
+    float sum = 0.f;
+    for (uint32_t c = (uint32_t)(ra - c0); c < (uint32_t)(rb - c0); c++) sum += prod[c];
+    const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
+    const float error = y - predict;
+    err[rf + r] = error;
+    err2[rf + r] = error * error;
+  }
+}
+
 // One lane per example: the lane sums its own row in feature order (lr.cpp:
 // 358-375, fp32 products and adds, -ffp-contract=off: bit-identical to the
 // cross-lane forms above) — no readlane chain.  Per chunk of CH features the
@@ -1263,6 +1342,10 @@ struct swps_lr {
   std::vector<uint32_t> bnhot;
   uint64_t max_bruns = 0;
   int fwd_groups = 2;            // SWPS_LR_FWD_G: row groups per wave in the forward (1, 2, 4; A/B: 2)
+  int fwd_c = 1;                 // SWPS_LR_FWD_C: the record-contiguous forward (k_lr_forward_c; 0 = off)
+  int fwd_rpt = 8;               // its records per thread (SWPS_LR_FWD_C = 4 / 16 for A/B; 1 = the default 8)
+  DevMem d_fchunk;               // its static chunks of whole rows (uint2 {first row in batch, rows})
+  std::vector<uint64_t> bfchunk;  // [nb+1] each batch's first chunk
   int fwd_diag = 0;             // SWPS_LR_DIAG: timing experiments (1: forward without weight gather, 2: without ordered chain, 4: records without e gathers)
   uint64_t max_bnnz = 0;
   uint32_t *h_small = nullptr;
@@ -1650,7 +1733,50 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
   SWPS_TRY(l->d_val_s.ensure((l->max_bnnz + 4) * 4));
   const bool scat = l->fwd_records && l->rows_per_wave == 1 && mf <= 64;  // the forward writes the records
-  if (!scat && l->rows_per_wave == 1 && mf <= 42 && l->fwd_groups > 1 && !l->fwd_diag) {  // G groups per wave
+  if (l->fwd_c && !scat && l->rows_per_wave == 1 && !l->fwd_diag && !l->stage && l->bfchunk.empty()) {
+    // the static chunks of whole rows of every batch, once (rows never span chunks; a row longer
+    // than a chunk's capacity turns the form off)
+    std::vector<uint2> ch;
+    l->fwd_rpt = l->fwd_c == 4 || l->fwd_c == 16 ? l->fwd_c : kLrFwdRpt;  // records per thread (A/B: 4, 8, 16)
+    const uint64_t cap = (uint64_t)l->fwd_rpt * 256;
+    l->bfchunk.assign(1, 0);
+    for (uint64_t b = 0; b < l->nbatches && l->fwd_c; b++) {
+      const uint64_t a0 = b * l->B1(), a1 = std::min<uint64_t>(nr, a0 + l->B1());
+      uint64_t first = a0;
+      for (uint64_t r = a0; r < a1; r++) {
+        if (l->row_off[r + 1] - l->row_off[r] > cap) {
+          l->fwd_c = 0;
+          break;
+        }
+        if (l->row_off[r + 1] - l->row_off[first] > cap) {
+          ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(r - first)));
+          first = r;
+        }
+      }
+      if (a1 > first) ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(a1 - first)));
+      l->bfchunk.push_back(ch.size());
+    }
+    if (l->fwd_c) {
+      SWPS_TRY(upload(l->d_fchunk, ch, s));
+      SWPS_HIP(hipStreamSynchronize(s));  // `ch` is a local
+    }
+  }
+  const uint64_t nfc = l->fwd_c && l->bfchunk.size() > bi + 1 ? l->bfchunk[bi + 1] - l->bfchunk[bi] : 0;
+  if (nfc && !scat && l->rows_per_wave == 1 && !l->fwd_diag && !l->stage) {  // record-contiguous chunks of rows
+    hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
+    const bool hot = l->hot && !l->sharded && !l->bnhot.empty() && l->bnhot[bi];
+    auto kc = l->fwd_rpt == 4 ? k_lr_forward_c<4> : l->fwd_rpt == 16 ? k_lr_forward_c<16> : k_lr_forward_c<kLrFwdRpt>;
+    hipExtLaunchKernelGGL(kc, dim3((unsigned)nfc), dim3(256), 0, s, fb, fe, 0,
+                          (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi],
+                          (const uint64_t *)l->d_row_off.as<uint64_t>(), hot ? l->d_fhot.as<uint32_t>() : fidx,
+                          (const float *)l->d_fval.as<float>(), (const float *)l->d_label.as<float>(), r0,
+                          (const float *)rows, stride, l->d_err.as<float>(), l->d_err2.as<float>(),
+                          hot ? (const uint32_t *)(l->d_hrow.as<uint32_t>() + bi * kLrHot) : (const uint32_t *)nullptr,
+                          hot ? l->bnhot[bi] : 0u);
+    l->timer.ext_end(0, fb, fe);
+    if (fb) (void)hipEventDestroy(e0);
+    e0 = nullptr;
+  } else if (!scat && l->rows_per_wave == 1 && mf <= 42 && l->fwd_groups > 1 && !l->fwd_diag) {  // G groups per wave
     hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
     auto kf = l->fwd_groups == 4 ? k_lr_forward_g<3, 4> : k_lr_forward_g<3, 2>;
     const uint64_t G = l->fwd_groups == 4 ? 4 : 2;
@@ -1846,6 +1972,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_DIAG")) l->fwd_diag = atoi(e);
   if (const char *e = getenv("SWPS_LR_FWD_G")) l->fwd_groups = atoi(e);  // A/B, tests
+  if (const char *e = getenv("SWPS_LR_FWD_C")) l->fwd_c = atoi(e);      // A/B, tests
   if (const char *e = getenv("SWPS_LR_STAGE")) l->stage = atoi(e);        // A/B, tests
   if (const char *e = getenv("SWPS_LR_HOT")) l->hot = atoi(e);            // A/B, tests
   if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests

@@ -221,17 +221,20 @@ def test_lr_fast_sums_criteo_shape_close_to_exact(lib, gpu):
 
 @pytest.mark.parametrize("fast", [False, True])
 def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
-    """k_lr_forward_r with the ordered sums through LDS (the default: 3 or 2
-    rows per wave by the batch's longest row) == the same with readlane
-    chains == 2 rows per wave == k_lr_forward_l (a lane per row) == one row
-    per wave, bit for bit: Criteo-shaped rows (39 features: 3 per wave), the
-    reference's data.txt (its own row lengths) and ragged rows of 1-130
-    features (longer than one 40-feature chunk; one row per wave past 64)."""
+    """k_lr_forward_c (the default: whole rows in record-contiguous chunks) ==
+    k_lr_forward_g / _r with the ordered sums through LDS (3 or 2 rows per
+    wave by the batch's longest row) == the same with readlane chains == 2
+    rows per wave == k_lr_forward_l (a lane per row) == one row per wave, bit
+    for bit: Criteo-shaped rows (39 features: 3 per wave), the reference's
+    data.txt (its own row lengths), ragged rows of 1-130 features (longer than
+    one 40-feature chunk; one row per wave past 64) and 1-3-feature rows (over
+    256 rows in one chunk)."""
     from swiftmpi_amd.synth import criteo
     y, off, f, v = criteo(9000, seed=5)
     res = []
-    for pack in ("0", "1", "2", "3", "4"):
+    for pack, fc in (("1", "1"), ("0", "1"), ("1", "0"), ("2", "1"), ("3", "1"), ("4", "1")):
         monkeypatch.setenv("SWPS_LR_PACK", pack)
+        monkeypatch.setenv("SWPS_LR_FWD_C", fc)
         t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
         m = lib.LR(t, minibatch=1000, init_ref=False, fast_sums=fast)
         m.load_csr(y, off, f, v)
@@ -254,7 +257,17 @@ def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
         m3.load_csr(yl, roff, feat, vals)
         m3.init()
         e3 = m3.train(2)
-        res.append((e, m.params()[1], e2, m2.params()[1], e3, m3.params()[1]))
+        # very short rows: a chunk holds more rows than a block has threads
+        lens = rng.integers(1, 4, 6000)
+        roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        feat = rng.integers(0, 3000, int(roff[-1])).astype(np.uint32)
+        vals = rng.random(int(roff[-1])).astype(np.float32)
+        t4 = lib.Table("lr", capacity=1 << 14, dtype="f32", learning_rate=0.05, init="hash", seed=3)
+        m4 = lib.LR(t4, minibatch=2999, init_ref=False, fast_sums=fast)
+        m4.load_csr((rng.random(6000) < 0.5).astype(np.float32), roff, feat, vals)
+        m4.init()
+        e4 = m4.train(2)
+        res.append((e, m.params()[1], e2, m2.params()[1], e3, m3.params()[1], e4, m4.params()[1]))
     for r in res[1:]:
         for a, b in zip(res[0], r):
             assert np.array_equal(a, b)
