@@ -882,7 +882,7 @@ __device__ __forceinline__ void seg_after(bool fp, double vp, int cp, uint32_t h
 }
 
 template <int RPT, int BS = 256>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3 : RPT > 4 ? 6 : 8))) void k_lr_tiles(LrReduce a, LrTiles t) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3 : RPT > 6 ? 6 : 8))) void k_lr_tiles(LrReduce a, LrTiles t) {
   constexpr int NW = BS / 64;
   __shared__ float es[1 << kTileMaxBits];
   __shared__ double wv[NW];
@@ -1883,6 +1883,8 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
       auto kt = b512                    ? k_lr_tiles<4, 512>
                 : l->tile_chunk == 512  ? k_lr_tiles<2>
                 : l->tile_chunk == 1024 ? k_lr_tiles<4>
+                : l->tile_chunk == 1280 ? k_lr_tiles<5>
+                : l->tile_chunk == 1536 ? k_lr_tiles<6>
                 : l->tile_chunk == 4096 ? k_lr_tiles<16>
                                         : k_lr_tiles<8>;
       hipExtLaunchKernelGGL(kt, dim3(nch), dim3(b512 ? 512 : 256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0,
@@ -1981,7 +1983,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_TILES")) l->tiles = atoi(e);                // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_TILE_CHUNK")) {
     const int c = atoi(e);
-    l->tile_chunk = c == 512 || c == 2048 || c == 4096 ? (uint32_t)c : kTileChunk;
+    l->tile_chunk = c == 512 || c == 1280 || c == 1536 || c == 2048 || c == 4096 ? (uint32_t)c : kTileChunk;
   }
   if (const char *e = getenv("SWPS_LR_TILE_THREADS")) {  // 512: blocks of 2,048 records, 4 per thread (A/B)
     l->tile_threads = atoi(e) == 512 ? 512 : 256;
