@@ -819,7 +819,8 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
         push_bytes = 20 * nnz + 32 * uniq
     push_gbs = push_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
     step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
-    kf = {"kernel": "k_lr_forward", "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
+    kf = {"kernel": "k_lr_forward_c" if os.environ.get("SWPS_LR_FWD_C", "1") != "0" else "k_lr_forward_g",
+          "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
           "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
     kp = {"kernel": ("k_lr_records + k_lr_reduce_short + k_lr_reduce_long" if args.lr_exact
                      else "k_lr_tiles + k_lr_tiles_fin" if tiles
@@ -829,7 +830,7 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
           "launches": push_n}
     tr, tsrc = pmc_traffic(dict(app="lr", lr_batch=args.lr_batch, exact=bool(args.lr_exact), world=world,
                                 sharded=dist is not None),
-                           {"forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_g"),
+                           {"forward": ("k_lr_forward_c", "k_lr_forward_r", "k_lr_forward", "k_lr_forward_g"),
                             "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
                                      "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin")})
     for kd, name in ((kf, "forward"), (kp, "push")):

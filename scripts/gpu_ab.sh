@@ -24,10 +24,13 @@ import json, os, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 b = d.get("minibatch_100") or {}
 r = d["roofline"]
-print("%-40s %.4g w/s %.3f ms | b100 %s %s | frac %.3f sum %.3f ms (g %.3f p %.3f)" % (
+km = d.get("kernel_ms", {})
+n = max(r.get("launches", 1), 1)
+print("%-40s %.4g w/s %.3f ms | b100 %s %s | frac %.3f sum %.3f ms (g %.3f p %.3f) sort %.3f rec %.3f fwd %.3f" % (
     os.environ["V"], d["value"], d["ms_per_step"], b.get("value") and "%.4g" % b["value"],
     b.get("ms_per_step") and "%.4f" % b["ms_per_step"], r["frac"], r["avg_launch_ms"],
-    r.get("gather_ms_per_launch", 0), r.get("push_ms_per_launch", 0)), flush=True)
+    r.get("gather_ms_per_launch", 0), r.get("push_ms_per_launch", 0), km.get("sort", 0) / n,
+    km.get("records", 0) / n, km.get("forward", 0) / n), flush=True)
 PY
   done
 done

@@ -12,7 +12,7 @@
 # LEGS selects legs (default: all).  Each step runs under its own time limit;
 # the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 OUT=gpurun_out/profiles_$TAG
 mkdir -p gpurun_out "$OUT" profiles
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -28,7 +28,7 @@ run() {  # name timeout args...
   echo "== $name rc=$rc"; tail -2 "gpurun_out/$name.log" | cut -c1-400
   return $rc
 }
-W2V="bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-parity-leg --b100-steps 0 --config1-steps 0"
+W2V="bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-parity-leg --b100-steps 0 --config1-steps 0 --no-app-legs"
 W2VCFG='"app": "w2v", "dim": 300, "dtype": "f32", "world": 1, "line_len": 1000, "sampler": "table"'
 TEXT8='"tokens": 17005207, "vocab": 253854'
 leg() {  # name last(N|launches) config-json args...
@@ -58,7 +58,7 @@ for L in $LEGS; do
     w2v_bfp32) FETCH=1 leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp32\", \"sharded\": false}" $W2V ;;
     w2v_bfp40) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"bfp40\", \"sharded\": false}" $W2V --precision bfp40 ;;
     w2v_b100) leg $L 200 "{$W2VCFG, $TEXT8, \"minibatch\": 100, \"mode\": \"bfp32\", \"sharded\": false}" \
-                bench.py --gpus 1 --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline --no-parity-leg --config1-steps 0 ;;
+                bench.py --gpus 1 --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline --no-parity-leg --config1-steps 0 --no-app-legs ;;
     w2v_parity) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"parity\", \"sharded\": false}" $W2V --parity ;;
     w2v_fast) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"fast\", \"sharded\": false}" $W2V --precision fast ;;
     lr) leg $L 20 '{"app": "lr", "lr_batch": 65536, "exact": false, "world": 1, "sharded": false}' \

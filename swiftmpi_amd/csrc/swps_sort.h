@@ -10,6 +10,7 @@
 #include <cstdlib>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 namespace swps {
 
@@ -55,9 +56,38 @@ inline bool sort_wide() {  // SWPS_SORT_WIDE=0: the default 8-bit digits only (A
   return on;
 }
 
+// SWPS_SORT_CFG (A/B of the wide sort's tile shape): 0 = 1024 x 16 (rocPRIM's gfx950 default),
+// 1 = 512 x 16, 2 = 1024 x 8, 3 = 256 x 16
+template <unsigned RB, unsigned BS, unsigned IPT>
+using OnesweepShape = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<BS, IPT>, rocprim::kernel_config<BS, IPT>, RB,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+inline int sort_cfg() {
+  static const int c = [] {
+    const char *e = getenv("SWPS_SORT_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  return c;
+}
+
 template <typename K, typename V>
 inline hipError_t sort_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, const V *vin, V *vout, uint64_t n,
                              int bits, hipStream_t s) {
+  if (sort_wide() && sort_cfg() && sizeof(K) == 4 && sizeof(V) == 4 && bits > 16 && bits <= 18) {
+    switch (sort_cfg()) {
+      case 1:
+        return rocprim::radix_sort_pairs<OnesweepShape<9, 512, 16>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                                    (unsigned)bits, s);
+      case 2:
+        return rocprim::radix_sort_pairs<OnesweepShape<9, 1024, 8>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                                    (unsigned)bits, s);
+      default:
+        return rocprim::radix_sort_pairs<OnesweepShape<9, 256, 16>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                                    (unsigned)bits, s);
+    }
+  }
   if (!sort_wide())
     return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
                                                   s);
@@ -72,6 +102,37 @@ inline hipError_t sort_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, co
     return rocprim::radix_sort_pairs<OnesweepWide<9>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
                                                       s);
   if (sizeof(K) == 4 && sizeof(V) == 4 && bits > 18 && bits <= 20)
+    return rocprim::radix_sort_pairs<OnesweepWide<10>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                       (unsigned)bits, s);
+  return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);
+}
+
+// The same with the values 0, 1, 2, ... (a record's index): read from a counting iterator instead of
+// an array the records kernel wrote (SWPS_SORT_IOTA=0: the array, A/B)
+inline bool sort_iota() {
+  static const bool on = [] {
+    const char *e = getenv("SWPS_SORT_IOTA");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+template <typename K>
+inline hipError_t sort_pairs_iota(void *tmp, size_t &bytes, const K *kin, K *kout, uint32_t *vout, uint64_t n,
+                                  int bits, hipStream_t s) {
+  const rocprim::counting_iterator<uint32_t> vin(0u);
+  if (!sort_wide())
+    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);
+  if (n < kSmallSort && sort_small_mode()) {
+    if (bits > 16 && bits <= 20)
+      return rocprim::radix_sort_pairs<OnesweepSmall<10>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                          (unsigned)bits, s);
+    return rocprim::radix_sort_pairs<OnesweepSmall<8>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                       (unsigned)bits, s);
+  }
+  if (sizeof(K) == 4 && bits > 16 && bits <= 18)
+    return rocprim::radix_sort_pairs<OnesweepWide<9>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
+                                                      s);
+  if (sizeof(K) == 4 && bits > 18 && bits <= 20)
     return rocprim::radix_sort_pairs<OnesweepWide<10>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
                                                        (unsigned)bits, s);
   return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);

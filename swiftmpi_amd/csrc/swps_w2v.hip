@@ -260,7 +260,21 @@ struct RecArgs {
   uint32_t *pkeys, *pvals;  // position-major: h record (p,d) at p*(N+1)+d; v record (p,j) at (N+1)*P + p*2W+j
   int32_t *trace;
   unsigned long long *rows_touched;
+  const int2 *tloc;  // per batch token (from t0): {local key, position-record source} (k_tok_local), or nullptr
+  uint64_t t0;
 };
+
+// Per token of the batch: its local key and the source its position-record slot holds (kTabRow |
+// shard row for a pulled key on a single GPU, else its vid) — looked up once per token, so
+// k_records_t reads a position's contexts and word as contiguous entries instead of two random
+// lookups each
+__global__ void k_tok_local(const int32_t *__restrict__ tok, uint64_t nt, const int32_t *__restrict__ local,
+                            const uint32_t *__restrict__ vid_row, int2 *__restrict__ tloc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nt) return;
+  const int32_t v = tok[i], u = local[v];
+  tloc[i] = make_int2(u, (u >= 0 && vid_row) ? (kTabRow | (int32_t)vid_row[v]) : v);
+}
 
 // One thread per kept position: replays learn_instance's LCG draws
 // (word2vec_global.h:669,686-691) from the jumped state — b, the negatives
@@ -314,7 +328,7 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
       r[1 + j] = src;
       const uint64_t k = HOFF + p * (uint64_t)(2 * W) + j;
       a.pkeys[k] = key;
-      a.pvals[k] = (uint32_t)k;
+      if (a.pvals) a.pvals[k] = (uint32_t)k;
     }
     for (int d = 0; d <= N; d++) {
       int32_t tv = word;
@@ -359,7 +373,7 @@ __global__ __launch_bounds__(256) void k_records(RecArgs a) {
       r[1 + 2 * W + d] = src;
       const uint64_t k = p * (uint64_t)(N + 1) + d;
       a.pkeys[k] = key;
-      a.pvals[k] = (uint32_t)k;
+      if (a.pvals) a.pvals[k] = (uint32_t)k;
     }
   }
   __syncthreads();
@@ -420,23 +434,42 @@ __global__ __launch_bounds__(256) void k_records_t(RecArgs a) {
     int32_t *r = srec + threadIdx.x * RS;
     r[0] = word;
     // ---- contexts: a = b .. 2W-b (a != W) inside the line ----
-    int32_t cv[2 * W];
+    int32_t cv[2 * W], cu[2 * W], cs[2 * W];
+    if (a.tloc) {  // the per-token lookups (k_tok_local): contiguous in the line
 #pragma unroll
-    for (int j = 0; j < 2 * W; j++) {
-      cv[j] = -1;
-      if (j < 2 * (W - b)) {
-        int aa = b + j;
-        if (aa >= W) aa++;
-        const int c = pos - W + aa;
-        if (c >= 0 && c < n) cv[j] = a.tok[ls + c];
+      for (int j = 0; j < 2 * W; j++) {
+        cv[j] = -1;
+        cu[j] = -1;
+        cs[j] = -1;
+        if (j < 2 * (W - b)) {
+          int aa = b + j;
+          if (aa >= W) aa++;
+          const int c = pos - W + aa;
+          if (c >= 0 && c < n) {
+            const int2 x = a.tloc[(uint64_t)(ls + c) - a.t0];
+            cv[j] = 0;  // present (its vid is not needed: cs holds the slot's source)
+            cu[j] = x.x;
+            cs[j] = x.y;
+          }
+        }
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2 * W; j++) {
+        cv[j] = -1;
+        if (j < 2 * (W - b)) {
+          int aa = b + j;
+          if (aa >= W) aa++;
+          const int c = pos - W + aa;
+          if (c >= 0 && c < n) cv[j] = a.tok[ls + c];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2 * W; j++) cu[j] = cv[j] >= 0 ? a.local[cv[j]] : -1;
+#pragma unroll
+      for (int j = 0; j < 2 * W; j++)
+        cs[j] = (cu[j] >= 0 && a.vid_row) ? (kTabRow | (int32_t)a.vid_row[cv[j]]) : cv[j];
     }
-    int32_t cu[2 * W];
-#pragma unroll
-    for (int j = 0; j < 2 * W; j++) cu[j] = cv[j] >= 0 ? a.local[cv[j]] : -1;
-    int32_t cs[2 * W];
-#pragma unroll
-    for (int j = 0; j < 2 * W; j++) cs[j] = (cu[j] >= 0 && a.vid_row) ? (kTabRow | (int32_t)a.vid_row[cv[j]]) : cv[j];
     // ---- targets: the word, then N draws from the unigram table ----
     uint64_t slot[N + 1];
     uint32_t lo[N + 1], hi[N + 1];
@@ -471,11 +504,17 @@ __global__ __launch_bounds__(256) void k_records_t(RecArgs a) {
       if (tv[d] == word) tv[d] = -1;
     }
     int32_t tu[N + 1];
-#pragma unroll
-    for (int d = 0; d <= N; d++) tu[d] = tv[d] >= 0 ? a.local[tv[d]] : -1;
     int32_t ts[N + 1];
+    if (a.tloc) {  // the word itself: its token's entry
+      const int2 x = a.tloc[t - a.t0];
+      tu[0] = x.x;
+      ts[0] = x.y;
+    }
 #pragma unroll
-    for (int d = 0; d <= N; d++) ts[d] = (tu[d] >= 0 && a.vid_row) ? (kTabRow | (int32_t)a.vid_row[tv[d]]) : tv[d];
+    for (int d = a.tloc ? 1 : 0; d <= N; d++) tu[d] = tv[d] >= 0 ? a.local[tv[d]] : -1;
+#pragma unroll
+    for (int d = a.tloc ? 1 : 0; d <= N; d++)
+      ts[d] = (tu[d] >= 0 && a.vid_row) ? (kTabRow | (int32_t)a.vid_row[tv[d]]) : tv[d];
     // ---- stores: position record (LDS), gradient records (position-major) ----
 #pragma unroll
     for (int j = 0; j < 2 * W; j++) {
@@ -483,7 +522,7 @@ __global__ __launch_bounds__(256) void k_records_t(RecArgs a) {
       r[1 + j] = cs[j];
       const uint64_t k = HOFF + p * (uint64_t)(2 * W) + j;
       a.pkeys[k] = cu[j] >= 0 ? (uint32_t)cu[j] : a.U;
-      a.pvals[k] = (uint32_t)k;
+      if (a.pvals) a.pvals[k] = (uint32_t)k;
     }
 #pragma unroll
     for (int d = 0; d <= N; d++) {
@@ -491,7 +530,7 @@ __global__ __launch_bounds__(256) void k_records_t(RecArgs a) {
       r[1 + 2 * W + d] = ts[d];
       const uint64_t k = p * (uint64_t)(N + 1) + d;
       a.pkeys[k] = tu[d] >= 0 ? (uint32_t)tu[d] : a.U;
-      a.pvals[k] = (uint32_t)k;
+      if (a.pvals) a.pvals[k] = (uint32_t)k;
     }
   }
   __syncthreads();
@@ -2044,6 +2083,9 @@ struct swps_w2v {
   bool cache_pad = true;  // worker-cache rows padded to 128 B (SWPS_CACHE_PAD=0: D-strided, for A/B timing)
   int cs = 0;              // worker-cache row stride in elements (set with the cache allocation)
   bool uni_index = true;  // negatives via the coarse-indexed run-length table (SWPS_UNI_INDEX=0: the 1e8-slot table)
+  bool seg4 = true;       // k_seg_bounds4: 4 sorted records per thread (SWPS_SEG4=0: one, A/B)
+  bool tok_local = true;  // k_tok_local + k_records_t's per-token lookups (SWPS_TOK_LOCAL=0: off, A/B)
+  DevMem d_tloc;          // its per-token {local, source} of the batch being prepped
   bool row_pad = true;  // neu1/neu1e rows padded to 128 B (SWPS_ROW_PAD=0: D-strided, for A/B timing)
   hipStream_t s = nullptr;
   // host corpus / vocab
@@ -3209,10 +3251,12 @@ int presize(swps_w2v *w, uint64_t maxP) {
     while ((1ULL << bits) <= U) bits++;
     // smaller batches of the epoch may take the small-tile sort (swps_sort.h): size for both
     for (uint64_t n : {M, std::min<uint64_t>(M, kSmallSort - 1)}) {
-      size_t sb = 0;
+      size_t sb = 0, si = 0;
       SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
                           w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), n, bits, w->s));
-      SWPS_TRY(w->d_tmp.ensure(sb));
+      SWPS_HIP(sort_pairs_iota(nullptr, si, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                               w->d_pvals_s.as<uint32_t>(), n, bits, w->s));
+      SWPS_TRY(w->d_tmp.ensure(std::max(sb, si)));
     }
     const uint64_t max_items = 2ULL * U + M / multi_chunk(w, maxP) + 1;
     SWPS_TRY(w->d_lead.ensure((max_items / 8 + 2) * 4));
@@ -3368,6 +3412,48 @@ __global__ void k_seg_bounds(const uint32_t *__restrict__ keys, const uint32_t *
   }
 }
 
+// k_seg_bounds with 4 consecutive records per thread (16-B loads of the sorted keys and their
+// record indices; the neighbours on either side from the next / previous thread's words): the same
+// bounds, a quarter of the threads and load instructions
+__global__ __launch_bounds__(256) void k_seg_bounds4(const uint32_t *__restrict__ keys,
+                                                     const uint32_t *__restrict__ vals, uint32_t M, uint32_t HOFF,
+                                                     uint32_t U, uint32_t *__restrict__ seg) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, i0 = q * 4;
+  if (i0 >= M) return;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;  // past either end: no key
+  uint32_t k[6], v[5];
+  if (i0 + 4 <= M) {
+    const uint4 kk = ((const uint4 *)keys)[q], vv = ((const uint4 *)vals)[q];
+    k[1] = kk.x, k[2] = kk.y, k[3] = kk.z, k[4] = kk.w;
+    v[1] = vv.x, v[2] = vv.y, v[3] = vv.z, v[4] = vv.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      k[j + 1] = i0 + j < M ? keys[i0 + j] : kNone;
+      v[j + 1] = i0 + j < M ? vals[i0 + j] : 0u;
+    }
+  }
+  k[0] = i0 ? keys[i0 - 1] : kNone;
+  v[0] = i0 ? vals[i0 - 1] : 0u;
+  k[5] = i0 + 4 < M ? keys[i0 + 4] : kNone;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t i = i0 + j, u = k[j + 1];
+    if (i >= M || u >= U) continue;  // "no key" records sort last
+    const bool first = k[j] != u, last = k[j + 2] != u;
+    const bool isv = v[j + 1] >= HOFF;
+    if (first) seg[u] = i;
+    if (last) seg[3 * U + u] = i + 1;
+    if ((first && isv) || (!first && isv && v[j] < HOFF)) {
+      seg[U + u] = i;
+      seg[2 * U + u] = i;
+    } else if (last && !isv) {
+      seg[U + u] = i + 1;
+      seg[2 * U + u] = i + 1;
+    }
+  }
+}
+
 // chunks of <= CH records per (key, kind) from the bounds; cnt[2U] = 0 (the
 // scan's tail).  Profiled passes (gstats) also add the records / items to
 // gstats[0..1].
@@ -3476,8 +3562,16 @@ int prep_batch(swps_w2v *w) {
                    : nullptr,
                w->cfg.minibatch_vocab ? U : (uint32_t)w->vocab_keys.size(),
                w->d_local.as<int32_t>(), U, w->sharded ? nullptr : w->d_vid_row.as<uint32_t>(), w->d_rec.as<int32_t>(),
-               w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), tracing ? w->d_trace.as<int32_t>() : nullptr,
-               tm.on ? w->d_rows_touched.as<unsigned long long>() : nullptr};
+               w->d_pkeys.as<uint32_t>(), sort_iota() ? nullptr : w->d_pvals.as<uint32_t>(),
+               tracing ? w->d_trace.as<int32_t>() : nullptr,
+               tm.on ? w->d_rows_touched.as<unsigned long long>() : nullptr, nullptr, t0};
+    if (W == 5 && N == 5 && use_uidx && !w->rec_generic && w->tok_local) {  // k_records_t reads per-token lookups
+      SWPS_TRY(w->d_tloc.ensure(std::max<uint64_t>(nt, 1) * 8));
+      k_tok_local<<<nblk(nt), 256, 0, s>>>(w->d_tok.as<int32_t>() + t0, nt, w->d_local.as<int32_t>(),
+                                           w->sharded ? nullptr : w->d_vid_row.as<uint32_t>(), w->d_tloc.as<int2>());
+      SWPS_HIP(hipGetLastError());
+      ra.tloc = w->d_tloc.as<int2>();
+    }
     hipEvent_t er = tm.begin(s);
     if (W == 5 && N == 5 && use_uidx && !w->rec_generic)
       k_records_t<5, 5><<<nblk(P), 256, 256 * RS * sizeof(int32_t), s>>>(ra);
@@ -3503,16 +3597,29 @@ int prep_batch(swps_w2v *w) {
       while ((1ULL << bits) <= U) bits++;
       hipEvent_t es = tm.begin(s);
       size_t sb = 0;
-      SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
-                                              w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, s));
-      SWPS_TRY(w->d_tmp.ensure(sb));
-      sb = w->d_tmp.bytes;
-      SWPS_HIP(sort_pairs(w->d_tmp.p, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
-                                              w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, s));
+      if (sort_iota()) {  // the values are the record indices 0..M-1 (the records kernel wrote none)
+        SWPS_HIP(sort_pairs_iota(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                                 w->d_pvals_s.as<uint32_t>(), M, bits, s));
+        SWPS_TRY(w->d_tmp.ensure(sb));
+        sb = w->d_tmp.bytes;
+        SWPS_HIP(sort_pairs_iota(w->d_tmp.p, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                                 w->d_pvals_s.as<uint32_t>(), M, bits, s));
+      } else {
+        SWPS_HIP(sort_pairs(nullptr, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                            w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, s));
+        SWPS_TRY(w->d_tmp.ensure(sb));
+        sb = w->d_tmp.bytes;
+        SWPS_HIP(sort_pairs(w->d_tmp.p, sb, w->d_pkeys.as<uint32_t>(), w->d_pkeys_s.as<uint32_t>(),
+                            w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), M, bits, s));
+      }
       SWPS_TRY(w->d_icnt.ensure((2ULL * U + 1) * 4));
       SWPS_TRY(w->d_ioff.ensure((2ULL * U + 1) * 4));
-      k_seg_bounds<<<nblk(M), 256, 0, s>>>(w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (uint32_t)M,
-                                            (uint32_t)HOFF, U, w->d_seg.as<uint32_t>());
+      if (w->seg4)
+        k_seg_bounds4<<<nblk((M + 3) / 4), 256, 0, s>>>(w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(),
+                                                        (uint32_t)M, (uint32_t)HOFF, U, w->d_seg.as<uint32_t>());
+      else
+        k_seg_bounds<<<nblk(M), 256, 0, s>>>(w->d_pkeys_s.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(), (uint32_t)M,
+                                              (uint32_t)HOFF, U, w->d_seg.as<uint32_t>());
       const uint32_t chm = multi_chunk(w, P);
       k_seg_counts<<<nblk((uint64_t)U + 1), 256, 0, s>>>(w->d_seg.as<uint32_t>(), U, kChunk, chm, w->d_icnt.as<uint32_t>(),
                                                           tm.on ? w->d_gstats.as<unsigned long long>() : nullptr);
@@ -4007,6 +4114,8 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_MULTI_SORT_MIN")) w->multi_sort_min = strtoull(e, nullptr, 10);
   if (const char *e = getenv("SWPS_ROW_PAD")) w->row_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_UNI_INDEX")) w->uni_index = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_SEG4")) w->seg4 = atoi(e) != 0;            // A/B timing
+  if (const char *e = getenv("SWPS_TOK_LOCAL")) w->tok_local = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_CACHE_PAD")) w->cache_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_OVERLAP")) w->overlap = atoi(e);  // A/B timing
   if (const char *e = getenv("SWPS_GATHER_UNR")) w->gather_unr = atoi(e);

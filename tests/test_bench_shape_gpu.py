@@ -213,7 +213,10 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode, lin
 @pytest.mark.parametrize("env,fixed,fp64i", [("SWPS_SORT_WIDE", "", False), ("SWPS_FUSED_PUSH", "", False),
                                              ("SWPS_MULTI_SORT", "", False),
                                              ("SWPS_MULTI_SORT", "SWPS_FUSED_PUSH=0", False),
-                                             ("SWPS_MULTI_SORT", "", True), ("SWPS_SPLIT_PUSH", "", False)])
+                                             ("SWPS_MULTI_SORT", "", True), ("SWPS_SPLIT_PUSH", "", False),
+                                             ("SWPS_SORT_IOTA", "", False), ("SWPS_SORT_CFG", "", False),
+                                             ("SWPS_SEG4", "", False), ("SWPS_TOK_LOCAL", "", False),
+                                             ("SWPS_TOK_LOCAL", "", "'bfp32'")])
 def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed, fp64i):
     """Three 5000-line batches of the bench corpus train to the same bits with
     either setting of:
@@ -231,7 +234,14 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed,
       mode (the generic k_gather);
     * SWPS_SPLIT_PUSH — the multi-chunk gather (and its second level) on a
       side stream beside the push of the other (key, half) items, the
-      multi-chunk halves pushed after it, vs everything in one stream."""
+      multi-chunk halves pushed after it, vs everything in one stream;
+    * SWPS_SORT_IOTA — the sort's values (the record indices) read from a
+      counting iterator vs an array the records kernel wrote;
+    * SWPS_SORT_CFG — the wide sort's tile shape (1024 x 16 vs 512 x 16);
+    * SWPS_SEG4 — the segment bounds 4 sorted records per thread vs one;
+    * SWPS_TOK_LOCAL — k_records_t's contexts and word through the per-token
+      lookups of k_tok_local vs random local / row lookups (fast mode and the
+      headline's bfp32)."""
     res = []
     for k_v in fixed.split():
         monkeypatch.setenv(*k_v.split("="))
