@@ -33,11 +33,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 XGMI_PEAK_GBS = 7 * 153.0  # per GPU: 7 xGMI links x ~153 GB/s
 
 
-def lr_tile_pieces(f, off, r0, r1, tile_bits=12, chunk=1024):
+LR_TILE_CHUNK = int(os.environ.get("SWPS_LR_TILE_CHUNK", "1536"))  # swps_lr.hip kTileChunk (records per block)
+
+
+def lr_tile_pieces(f, off, r0, r1, tile_bits=12, chunk=None):
     """The LR row-tile path's pieces and partials for batch rows [r0, r1): records ordered by
     (tile, key) (stable: row order inside), cut into blocks of `chunk` records per tile; a piece
     is a key's records inside one block, a partial a piece of a key with several
     (swps_lr.hip lr_tile_index)."""
+    chunk = chunk or LR_TILE_CHUNK
     n = np.diff(off[r0:r1 + 1].astype(np.int64))
     tile = np.repeat((np.arange(r1 - r0) >> tile_bits), n)
     feat = f[off[r0]:off[r1]].astype(np.int64)

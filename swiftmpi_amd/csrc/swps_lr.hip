@@ -854,7 +854,10 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
 // added in (tile, record) order by k_lr_tiles_fin.  Same fp32 products e*x_i as the record path,
 // fp64 sums in a fixed order: deterministic, within fp64 rounding of k_lr_reduce_fused.
 constexpr int kTileMaxBits = 12;         // LDS slice: 4,096 rows (16 KB)
-constexpr uint32_t kTileChunk = 1024;    // records per block (SWPS_LR_TILE_CHUNK: 512 / 1024 / 2048 / 4096)
+// records per block (SWPS_LR_TILE_CHUNK: 512 / 1024 / 1280 / 1536 / 1792 / 2048 / 4096; same-box A/B at the
+// Criteo batch, round 4: 1024 -> 1536 took the tiles group from 28.0 to 25.1 us — 1,664 blocks of
+// 6 records per thread instead of 2,497 of 4, so every block is resident at once)
+constexpr uint32_t kTileChunk = 1536;
 constexpr uint16_t kTileHead = 0x8000;   // trow bit: the record starts a (tile, key) run
 
 struct LrTiles {
@@ -882,7 +885,7 @@ __device__ __forceinline__ void seg_after(bool fp, double vp, int cp, uint32_t h
 }
 
 template <int RPT, int BS = 256>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3 : RPT > 6 ? 6 : 8))) void k_lr_tiles(LrReduce a, LrTiles t) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RPT > 8 ? 3 : 8))) void k_lr_tiles(LrReduce a, LrTiles t) {
   constexpr int NW = BS / 64;
   __shared__ float es[1 << kTileMaxBits];
   __shared__ double wv[NW];
@@ -1885,6 +1888,7 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
                 : l->tile_chunk == 1024 ? k_lr_tiles<4>
                 : l->tile_chunk == 1280 ? k_lr_tiles<5>
                 : l->tile_chunk == 1536 ? k_lr_tiles<6>
+                : l->tile_chunk == 1792 ? k_lr_tiles<7>
                 : l->tile_chunk == 4096 ? k_lr_tiles<16>
                                         : k_lr_tiles<8>;
       hipExtLaunchKernelGGL(kt, dim3(nch), dim3(b512 ? 512 : 256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0,
@@ -1983,7 +1987,8 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_TILES")) l->tiles = atoi(e);                // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_TILE_CHUNK")) {
     const int c = atoi(e);
-    l->tile_chunk = c == 512 || c == 1280 || c == 1536 || c == 2048 || c == 4096 ? (uint32_t)c : kTileChunk;
+    l->tile_chunk = c == 512 || c == 1024 || c == 1280 || c == 1536 || c == 1792 || c == 2048 || c == 4096 ? (uint32_t)c
+                                                                                                           : kTileChunk;
   }
   if (const char *e = getenv("SWPS_LR_TILE_THREADS")) {  // 512: blocks of 2,048 records, 4 per thread (A/B)
     l->tile_threads = atoi(e) == 512 ? 512 : 256;

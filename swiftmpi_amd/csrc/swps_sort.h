@@ -19,7 +19,9 @@ using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim:
 
 // Wider digits for 17-20-bit keys: the bench minibatch's local key indices
 // (U ~ 2^18) sort in 2 onesweep passes of 9 bits instead of 3 of 8 (same
-// stable order, so same results).  Block shape of rocPRIM's gfx950 default.
+// stable order, so same results).  Block shape of rocPRIM's gfx950 default
+// (same-box A/B at the bench batch, round 4: 512 x 16, 1024 x 8 and 256 x 16 tiles
+// within 0.5 % of it).
 template <unsigned RB>
 using OnesweepWide = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
@@ -56,38 +58,9 @@ inline bool sort_wide() {  // SWPS_SORT_WIDE=0: the default 8-bit digits only (A
   return on;
 }
 
-// SWPS_SORT_CFG (A/B of the wide sort's tile shape): 0 = 1024 x 16 (rocPRIM's gfx950 default),
-// 1 = 512 x 16, 2 = 1024 x 8, 3 = 256 x 16
-template <unsigned RB, unsigned BS, unsigned IPT>
-using OnesweepShape = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<BS, IPT>, rocprim::kernel_config<BS, IPT>, RB,
-                                        rocprim::block_radix_rank_algorithm::match>,
-    0>;
-inline int sort_cfg() {
-  static const int c = [] {
-    const char *e = getenv("SWPS_SORT_CFG");
-    return e ? atoi(e) : 0;
-  }();
-  return c;
-}
-
 template <typename K, typename V>
 inline hipError_t sort_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, const V *vin, V *vout, uint64_t n,
                              int bits, hipStream_t s) {
-  if (sort_wide() && sort_cfg() && sizeof(K) == 4 && sizeof(V) == 4 && bits > 16 && bits <= 18) {
-    switch (sort_cfg()) {
-      case 1:
-        return rocprim::radix_sort_pairs<OnesweepShape<9, 512, 16>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
-                                                                    (unsigned)bits, s);
-      case 2:
-        return rocprim::radix_sort_pairs<OnesweepShape<9, 1024, 8>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
-                                                                    (unsigned)bits, s);
-      default:
-        return rocprim::radix_sort_pairs<OnesweepShape<9, 256, 16>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
-                                                                    (unsigned)bits, s);
-    }
-  }
   if (!sort_wide())
     return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
                                                   s);

@@ -992,13 +992,24 @@ struct MultiOrder {  // k_item_desc: sort keys of the multi-chunk items by their
 };
 constexpr uint32_t kMultiPad = 0xFFFFu;  // 16-bit sort keys: items outside the multi list sort last
 
+// the (key, kind) run of every item without a search: each run with items marks its first item
+// (run_of zeroed before), then an inclusive max-scan carries the mark over the run's other items
+__global__ void k_item_heads(const uint32_t *__restrict__ ioff, uint32_t R, uint32_t *__restrict__ run_of) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= R) return;
+  const uint32_t a = ioff[j];
+  if (ioff[j + 1] > a) run_of[a] = j;
+}
+
 __global__ void k_item_desc(const uint32_t *__restrict__ seg, const uint32_t *__restrict__ ioff, uint32_t U,
                             uint32_t CH, uint32_t CHM, uint64_t max_items, uint4 *__restrict__ desc, uint32_t *__restrict__ lead,
-                            uint32_t *__restrict__ multi, MultiOrder mo) {
+                            uint32_t *__restrict__ multi, MultiOrder mo, const uint32_t *__restrict__ run_of = nullptr) {
   const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = item < max_items && item < ioff[2ull * U];
   uint32_t lo = 0, hi = 2 * U;  // largest j with ioff[j] <= item
-  if (live)
+  if (live && run_of)
+    lo = run_of[item];
+  else if (live)
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
       if (ioff[mid] <= item)
@@ -2085,6 +2096,11 @@ struct swps_w2v {
   bool uni_index = true;  // negatives via the coarse-indexed run-length table (SWPS_UNI_INDEX=0: the 1e8-slot table)
   bool seg4 = true;       // k_seg_bounds4: 4 sorted records per thread (SWPS_SEG4=0: one, A/B)
   bool tok_local = true;  // k_tok_local + k_records_t's per-token lookups (SWPS_TOK_LOCAL=0: off, A/B)
+  // k_item_desc's runs by k_item_heads + max-scan instead of a binary search (SWPS_ITEM_HEADS=1; off:
+  // same-box A/B, round 4, 2 reps: B = 5000 unchanged, B = 100 3.01e8 -> 2.92e8 words/s — four more
+  // launches on the prep stream)
+  bool item_heads = false;
+  DevMem d_irun;           // its item -> run map
   DevMem d_tloc;          // its per-token {local, source} of the batch being prepped
   bool row_pad = true;  // neu1/neu1e rows padded to 128 B (SWPS_ROW_PAD=0: D-strided, for A/B timing)
   hipStream_t s = nullptr;
@@ -3648,9 +3664,23 @@ int prep_batch(swps_w2v *w) {
         mo = MultiOrder{w->d_pkeys.as<uint32_t>(), w->d_pvals.as<uint32_t>(), w->d_pvals_s.as<uint32_t>(),
                         (uint32_t)(N + 1), (uint32_t)(2 * W), HOFF, shift};
       }
+      const uint32_t *run_of = nullptr;
+      if (w->item_heads) {  // every item's run by a max-scan of the runs' first items (no binary search)
+        SWPS_TRY(w->d_irun.ensure(max_items * 4));
+        SWPS_HIP(hipMemsetAsync(w->d_irun.p, 0, max_items * 4, s));
+        k_item_heads<<<nblk(2ULL * U), 256, 0, s>>>(w->d_ioff.as<uint32_t>(), 2 * U, w->d_irun.as<uint32_t>());
+        size_t hb = 0;
+        SWPS_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, hb, w->d_irun.as<uint32_t>(), w->d_irun.as<uint32_t>(),
+                                                   hipcub::Max(), (int)max_items, s));
+        SWPS_TRY(w->d_tmp.ensure(hb));
+        hb = w->d_tmp.bytes;
+        SWPS_HIP(hipcub::DeviceScan::InclusiveScan(w->d_tmp.p, hb, w->d_irun.as<uint32_t>(), w->d_irun.as<uint32_t>(),
+                                                   hipcub::Max(), (int)max_items, s));
+        run_of = w->d_irun.as<uint32_t>();
+      }
       k_item_desc<<<nblk(max_items), 256, 0, s>>>(w->d_seg.as<uint32_t>(), w->d_ioff.as<uint32_t>(), U, kChunk, chm,
                                                    max_items, w->d_desc.as<uint4>(), w->d_lead.as<uint32_t>(),
-                                                   w->d_multi.as<uint32_t>(), mo);
+                                                   w->d_multi.as<uint32_t>(), mo, run_of);
       SWPS_HIP(hipGetLastError());
       pb.msorted = msort;
       if (msort) {  // stable: equal coarse positions keep item order
@@ -4116,6 +4146,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_UNI_INDEX")) w->uni_index = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_SEG4")) w->seg4 = atoi(e) != 0;            // A/B timing
   if (const char *e = getenv("SWPS_TOK_LOCAL")) w->tok_local = atoi(e) != 0;  // A/B timing
+  if (const char *e = getenv("SWPS_ITEM_HEADS")) w->item_heads = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_CACHE_PAD")) w->cache_pad = atoi(e) != 0;  // A/B timing
   if (const char *e = getenv("SWPS_OVERLAP")) w->overlap = atoi(e);  // A/B timing
   if (const char *e = getenv("SWPS_GATHER_UNR")) w->gather_unr = atoi(e);

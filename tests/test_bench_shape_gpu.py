@@ -214,9 +214,9 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode, lin
                                              ("SWPS_MULTI_SORT", "", False),
                                              ("SWPS_MULTI_SORT", "SWPS_FUSED_PUSH=0", False),
                                              ("SWPS_MULTI_SORT", "", True), ("SWPS_SPLIT_PUSH", "", False),
-                                             ("SWPS_SORT_IOTA", "", False), ("SWPS_SORT_CFG", "", False),
+                                             ("SWPS_SORT_IOTA", "", False),
                                              ("SWPS_SEG4", "", False), ("SWPS_TOK_LOCAL", "", False),
-                                             ("SWPS_TOK_LOCAL", "", "'bfp32'")])
+                                             ("SWPS_TOK_LOCAL", "", "'bfp32'"), ("SWPS_ITEM_HEADS", "", False)])
 def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed, fp64i):
     """Three 5000-line batches of the bench corpus train to the same bits with
     either setting of:
@@ -237,11 +237,12 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed,
       multi-chunk halves pushed after it, vs everything in one stream;
     * SWPS_SORT_IOTA — the sort's values (the record indices) read from a
       counting iterator vs an array the records kernel wrote;
-    * SWPS_SORT_CFG — the wide sort's tile shape (1024 x 16 vs 512 x 16);
     * SWPS_SEG4 — the segment bounds 4 sorted records per thread vs one;
     * SWPS_TOK_LOCAL — k_records_t's contexts and word through the per-token
       lookups of k_tok_local vs random local / row lookups (fast mode and the
-      headline's bfp32)."""
+      headline's bfp32);
+    * SWPS_ITEM_HEADS — k_item_desc's (key, kind) run of each item from a
+      max-scan of the runs' first items vs a binary search."""
     res = []
     for k_v in fixed.split():
         monkeypatch.setenv(*k_v.split("="))
