@@ -13,7 +13,7 @@ step() {  # name timeout cmd...
   tail -5 "gpurun_out/$name.log"
   return $rc
 }
-step pytest_gpu 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+step pytest_gpu ${PYTEST_TO:-1000} python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
