@@ -74,6 +74,17 @@ def main():
         if rd is not None and "FETCH_SIZE" in cs and cs["FETCH_SIZE"] > 0:
             e["fetch_ratio"] = rd / (cs["FETCH_SIZE"] * 1024.0)
         e["hbm_bytes"] = rd + wr if rd is not None and wr is not None else None
+        if cs.get("SQ_WAVE_CYCLES"):  # MI355X_MICROARCH.md: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ≈ WAVE_CYCLES
+            wc = cs["SQ_WAVE_CYCLES"]
+            for c, name in (("SQ_WAIT_ANY", "parked_frac"), ("SQ_WAIT_INST_ANY", "issue_stall_frac"),
+                            ("SQ_ACTIVE_INST_ANY", "active_frac")):
+                if c in cs:
+                    e[name] = cs[c] / wc  # parked = s_waitcnt / barrier (memory latency); issue stall = pipe
+            if cs.get("SQ_WAVES"):
+                e["quad_cycles_per_wave"] = wc / cs["SQ_WAVES"]
+                for c in ("SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+                    if c in cs:
+                        e[c.replace("SQ_INSTS_", "").lower() + "_per_wave"] = cs[c] / cs["SQ_WAVES"]
         kernels[k] = e
     out = {"source": "rocprofv3 --pmc <pass> --kernel-trace (one run per pass) -- " + a.cmd,
            "passes": [sorted(load(d).keys()) for d in a.dirs],
@@ -86,7 +97,12 @@ def main():
            "kernels": kernels}
     with open(a.out, "w") as fo:
         json.dump(out, fo, indent=1)
-    for k, v in sorted(kernels.items(), key=lambda kv: -(kv[1]["hbm_bytes"] or 0))[:10]:
+    for k, v in sorted(kernels.items(), key=lambda kv: -(kv[1]["hbm_bytes"] or kv[1].get("SQ_WAVE_CYCLES", 0)))[:10]:
+        if "parked_frac" in v:
+            print("%-44s waves %d  parked %.2f  issue-stall %.2f  active %.2f  qcyc/wave %.0f" % (
+                k, v.get("SQ_WAVES", 0), v["parked_frac"], v.get("issue_stall_frac", 0), v.get("active_frac", 0),
+                v.get("quad_cycles_per_wave", 0)))
+            continue
         print("%-44s hbm %.4g GB  read %s  write %s  fetch_ratio %s" % (
             k, (v["hbm_bytes"] or 0) / 1e9, v["read_bytes"], v["write_bytes"], v.get("fetch_ratio")))
 
