@@ -194,6 +194,8 @@ constexpr uint64_t kEmptyKey = ~0ULL;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 // table internals used by the app contexts (same library)
 int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s);
+int table_find_or_insert_placed(swps_table *t, const uint64_t *d_keys, uint64_t n, const uint32_t *place,
+                                uint32_t *d_rows_out, hipStream_t s);
 int table_lookup(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s);
 int table_probe(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s);
 int table_check_error(swps_table *t, hipStream_t s);

@@ -1309,6 +1309,17 @@ struct swps_lr {
   std::vector<int32_t> fvid;
   std::vector<float> fval;
   std::vector<uint64_t> vocab_keys;  // vid order = first-pull order
+  // the table layout of the single-GPU init: vid -> rank of its new row (SWPS_LR_PLACE=1: by
+  // (batch, row tile, key) of first appearance, 2: by (batch, key); 0, the default: the insert's own
+  // order).  Same-box A/B at the Criteo step, round 4: the forward's L2-miss reads fell 47.3 ->
+  // 38.5 MB (13.7 -> 13.3 us) but the row tiles' rose 27.8 -> 30.4 MB and the finisher's 8.3 ->
+  // 9.6 MB (push 24.7 -> 25.7 us): 1.645e9 -> 1.63e9 examples/s, so off
+  std::vector<uint32_t> vid_place;
+  int place = 0;
+  // SWPS_LR_XCD=1: the row tiles' blocks by key octile per XCD (lr_xcd_order); off by default — the
+  // natural order already deals block j of every tile to XCD j % 8 at the Criteo batch (104 blocks
+  // per tile), and the octile order measured 24.7 -> 25.3 us (A/B, round 4)
+  int xcd = 0;
   bool loaded = false, inited = false;
   uint64_t cursor = 0, nbatches = 0;
   DevMem d_label, d_row_off, d_fvid, d_fval, d_vid_row, d_err, d_err2, d_val_s, d_tmp, d_pred, d_longs;
@@ -1376,6 +1387,34 @@ template <typename T> int lr_scan_incl(const T *in, T *out, uint64_t n, DevMem &
   b = tmp.bytes;
   SWPS_HIP(hipcub::DeviceScan::InclusiveSum(tmp.p, b, in, out, (int)n, s));
   return SWPS_OK;
+}
+
+// XCD-aware block order for the row tiles: the dispatcher deals blocks round-robin over the 8
+// XCDs (blocks b and b + 8 share one; MI355X_MICROARCH.md), and a tile's blocks walk its records
+// in key order, so the j-th of a tile's n blocks covers about the j/n-th stretch of the key space
+// in every tile.  Blocks [q0, q1) of a block table (E u32 each) are reordered so that block slot i
+// takes a block of key octile i % 8 (octile = j * 8 / n within its tile) while such blocks remain:
+// one XCD then holds the pieces of one stretch of keys from every tile — their partial slots
+// (in key order) and their rows (in first-appearance order by key, lr_ingest) stay within one L2
+// instead of being split between eight.  Speed only: every block's work is independent of its slot.
+template <typename T>
+void lr_xcd_order(std::vector<T> &v, int E, uint64_t q0, uint64_t q1, const std::vector<uint32_t> &oct) {
+  constexpr int kXcd = 8;
+  std::vector<std::vector<uint64_t>> qs(kXcd);
+  for (uint64_t q = q0; q < q1; q++) qs[oct[q - q0] % kXcd].push_back(q);
+  std::vector<size_t> at(kXcd, 0);
+  std::vector<T> out;
+  out.reserve((q1 - q0) * E);
+  for (uint64_t i = 0; i < q1 - q0; i++) {
+    int x = (int)(i % kXcd);
+    if (at[x] == qs[x].size()) {  // that octile's blocks are done: the queue with the most left
+      for (int y = 0; y < kXcd; y++)
+        if (qs[y].size() - at[y] > qs[x].size() - at[x]) x = y;
+    }
+    const uint64_t q = qs[x][at[x]++];
+    out.insert(out.end(), v.begin() + q * E, v.begin() + (q + 1) * E);
+  }
+  std::copy(out.begin(), out.end(), v.begin() + q0 * E);
 }
 
 // The tile index (k_lr_tiles): every batch's records in (tile, key) order; the blocks (1,024
@@ -1517,6 +1556,18 @@ int lr_tile_index(swps_lr *l, DevMem &ks, DevMem &perm, DevMem &rid, DevMem &rke
   }
   l->bmulti[nb] = multi.size() / 4;
   l->bmlong[nb] = mlong.size() / 4;
+  if (l->xcd)
+    for (uint64_t b = 0; b < nb; b++) {  // key octile of each block within its tile
+      const uint64_t q0 = l->bchunk[b], q1 = l->bchunk[b + 1];
+      std::vector<uint32_t> oct(q1 - q0);
+      for (uint64_t q = q0; q < q1;) {
+        uint64_t e = q;
+        while (e < q1 && chunks[e * 5] == chunks[q * 5]) e++;
+        for (uint64_t j = q; j < e; j++) oct[j - q0] = (uint32_t)((j - q) * 8 / (e - q));
+        q = e;
+      }
+      lr_xcd_order(chunks, 5, q0, q1, oct);
+    }
   if (multi.empty()) multi.assign(4, 0);
   if (mlong.empty()) mlong.assign(4, 0);
   SWPS_TRY(l->d_tmsrow.ensure(multi.size()));  // 4 B per entry: the runs' shard rows (single GPU)
@@ -1661,6 +1712,28 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   for (size_t i = 0; i < feat.size(); i++) l->fvid[i] = vid[feat[i]];
   const uint64_t nr = l->label.size();
   l->nbatches = nr ? (nr + l->B1() - 1) / l->B1() : 0;
+  // the rows the single-GPU init gives the keys (swps_lr_init): in the order the keys first appear,
+  // by (batch, row tile), then by key.  A batch's keys seen for the first time — most of its
+  // ~144k keys on Criteo-like data after the first batches — then sit in one dense run of rows that
+  // its forward and its row tiles walk in key order, and the keys of the first batches (the
+  // frequent ones) in a few MB: the weight gathers and row updates share 128-B lines instead of
+  // touching one line per key in a table of millions of rows
+  l->vid_place.clear();
+  if (l->place) {
+    const uint64_t B1 = l->B1(), V = l->vocab_keys.size();
+    const uint64_t ntile = (B1 + (1ULL << l->tile_bits) - 1) >> l->tile_bits;
+    std::vector<uint64_t> grp(V, ~0ull);
+    for (uint64_t r = 0; r < nr; r++) {
+      const uint64_t g = l->place == 2 ? r / B1 : (r / B1) * ntile + ((r % B1) >> l->tile_bits);
+      for (uint64_t c = l->row_off[r]; c < l->row_off[r + 1]; c++)
+        if (grp[l->fvid[c]] == ~0ull) grp[l->fvid[c]] = g;
+    }
+    std::vector<std::pair<uint64_t, uint32_t>> ord(V);
+    for (uint64_t i = 0; i < V; i++) ord[i] = {(grp[i] << 32) | (uint32_t)l->vocab_keys[i], (uint32_t)i};
+    std::sort(ord.begin(), ord.end());
+    l->vid_place.resize(V);
+    for (uint64_t j = 0; j < V; j++) l->vid_place[ord[j].second] = (uint32_t)j;
+  }
   hipStream_t s = l->s;
   SWPS_TRY(upload(l->d_label, l->label, s));
   SWPS_TRY(upload(l->d_row_off, l->row_off, s));
@@ -1985,6 +2058,8 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests
   if (const char *e = getenv("SWPS_LR_TILES")) l->tiles = atoi(e);                // A/B timing, tests
+  if (const char *e = getenv("SWPS_LR_PLACE")) l->place = atoi(e);                // A/B, tests
+  if (const char *e = getenv("SWPS_LR_XCD")) l->xcd = atoi(e);                    // A/B, tests
   if (const char *e = getenv("SWPS_LR_TILE_CHUNK")) {
     const int c = atoi(e);
     l->tile_chunk = c == 512 || c == 1024 || c == 1280 || c == 1536 || c == 1792 || c == 2048 || c == 4096 ? (uint32_t)c
@@ -2092,7 +2167,11 @@ int swps_lr_init(swps_lr *l) {
     if (V) SWPS_HIP(hipMemcpyAsync(pre.data(), dp.p, V * 4, hipMemcpyDeviceToHost, l->s));
     SWPS_HIP(hipStreamSynchronize(l->s));
   }
-  SWPS_TRY(table_find_or_insert(l->t, dk.as<uint64_t>(), V, l->d_vid_row.as<uint32_t>(), l->s));
+  if (l->vid_place.size() == V)  // rows in first-appearance order (lr_ingest); init in pull order
+    SWPS_TRY(table_find_or_insert_placed(l->t, dk.as<uint64_t>(), V, l->vid_place.data(),
+                                         l->d_vid_row.as<uint32_t>(), l->s));
+  else
+    SWPS_TRY(table_find_or_insert(l->t, dk.as<uint64_t>(), V, l->d_vid_row.as<uint32_t>(), l->s));
   l->rows_mapped = false;  // vid_row changed: k_lr_map_rows again at the next batch
   if (l->cfg.init_ref) {
     // LRPullAccessMethod::init_param (lr.cpp:48-50): w = gen_float() per miss, in first-pull order

@@ -78,6 +78,65 @@ __global__ void k_find_or_insert(const uint64_t *__restrict__ keys, uint64_t n, 
   if (out_new) out_new[i] = isnew;
 }
 
+// table_find_or_insert_placed, step 1: a key the table holds gets its row; a new key claims its
+// slot (out = the slot index, isnew = 1) and gets its row from step 2.  The keys of one call are
+// distinct (the caller's contract): a key found claimed but unpublished is an error, never a wait.
+__global__ void k_claim_slots(const uint64_t *__restrict__ keys, uint64_t n, uint64_t *tkeys, const uint32_t *slot_row,
+                              uint32_t *counters, uint64_t mask, uint32_t *out, uint8_t *isnew) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t key = keys[i];
+  uint32_t r = kNoRow;
+  uint8_t nw = 0;
+  if (key == kEmptyKey) {
+    atomicOr(&counters[1], 4u);
+  } else {
+    uint64_t s = slot_hash(key) & mask;
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+      uint64_t k = __hip_atomic_load(&tkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == kEmptyKey) {
+        const unsigned long long old =
+            atomicCAS((unsigned long long *)&tkeys[s], (unsigned long long)kEmptyKey, (unsigned long long)key);
+        if (old == kEmptyKey) {
+          r = (uint32_t)s;
+          nw = 1;
+          break;
+        }
+        k = old;
+      }
+      if (k == key) {
+        r = __hip_atomic_load(&slot_row[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (r == kNoRow) atomicOr(&counters[1], 2u);  // the same key twice in one call
+        if (r == kFullRow || r == kNoRow) r = kNoRow;
+        break;
+      }
+      s = (s + 1) & mask;
+    }
+    if (r == kNoRow && !nw) atomicOr(&counters[1], 1u);
+  }
+  out[i] = r;
+  isnew[i] = nw;
+}
+
+// step 2: the new keys' rows (assigned on the host in placement order) published into their slots
+__global__ void k_publish_rows(const uint64_t *__restrict__ keys, uint64_t n, const uint32_t *__restrict__ newrow,
+                               uint32_t *slot_row, uint64_t *row_key, uint32_t *counters, uint64_t cap, uint32_t *out,
+                               uint8_t *isnew) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !isnew[i]) return;
+  const uint32_t s = out[i], r = newrow[i];
+  if (r >= cap) {
+    atomicOr(&counters[1], 1u);
+    __hip_atomic_store(&slot_row[s], kFullRow, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    out[i] = kNoRow;
+    isnew[i] = 0;
+    return;
+  }
+  row_key[r] = keys[i];
+  __hip_atomic_store(&slot_row[s], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  out[i] = r;
+}
+
 __global__ void k_lookup(const uint64_t *__restrict__ keys, uint64_t n, const uint64_t *__restrict__ tkeys,
                          const uint32_t *__restrict__ slot_row, uint64_t mask, uint32_t *out_rows,
                          uint32_t *counters) {
@@ -479,17 +538,10 @@ int table_check_error(swps_table *t, hipStream_t s) {
   return SWPS_OK;
 }
 
-// find-or-insert + init_param of the new keys, stream-ordered (errors latched
-// in counters[1]); `isnew` is the table's own scratch
-static int find_or_insert_async(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out,
-                                hipStream_t s) {
-  if (n == 0) return SWPS_OK;
-  SWPS_TRY(t->isnew.ensure(n));
-  uint8_t *isnew = t->isnew.as<uint8_t>();
-  k_find_or_insert<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(),
-                                                  t->row_key.as<uint64_t>(), t->counters.as<uint32_t>(), t->mask,
-                                                  t->cfg.capacity, d_rows_out, isnew);
-  SWPS_HIP(hipGetLastError());
+// init_param of a call's new keys (isnew), stream-ordered: the table's init mode; SWPS_INIT_FLCG
+// draws in call order
+static int init_new_rows(swps_table *t, const uint64_t *d_keys, uint64_t n, const uint32_t *d_rows_out,
+                         const uint8_t *isnew, hipStream_t s) {
   if (t->cfg.dtype == SWPS_F64)
     k_init_rows<double><<<blocks_for(n * 64), 256, 0, s>>>(d_keys, d_rows_out, isnew, n, t->rows.as<double>(),
                                                            t->row_elems, t->cfg.layout, t->cfg.dim,
@@ -516,10 +568,62 @@ static int find_or_insert_async(swps_table *t, const uint64_t *d_keys, uint64_t 
   return SWPS_OK;
 }
 
+// find-or-insert + init_param of the new keys, stream-ordered (errors latched
+// in counters[1]); `isnew` is the table's own scratch
+static int find_or_insert_async(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out,
+                                hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  SWPS_TRY(t->isnew.ensure(n));
+  uint8_t *isnew = t->isnew.as<uint8_t>();
+  k_find_or_insert<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(),
+                                                  t->row_key.as<uint64_t>(), t->counters.as<uint32_t>(), t->mask,
+                                                  t->cfg.capacity, d_rows_out, isnew);
+  SWPS_HIP(hipGetLastError());
+  return init_new_rows(t, d_keys, n, d_rows_out, isnew, s);
+}
+
 int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s) {
   if (n == 0) return SWPS_OK;
   SWPS_TRY(find_or_insert_async(t, d_keys, n, d_rows_out, s));
   return table_check_error(t, s);
+}
+
+// find-or-insert of n DISTINCT keys whose new rows are laid out in placement order: the new key i
+// gets the next free row after every new key j with place[j] < place[i] (place: a permutation of
+// 0..n-1, host memory).  Found keys keep their rows; init_param runs in call order, as in
+// table_find_or_insert (an SWPS_INIT_FLCG table draws in the order of d_keys, not of place).
+int table_find_or_insert_placed(swps_table *t, const uint64_t *d_keys, uint64_t n, const uint32_t *place,
+                                uint32_t *d_rows_out, hipStream_t s) {
+  if (n == 0) return SWPS_OK;
+  if (t->mask >= 0xFFFFFFFFull) return table_find_or_insert(t, d_keys, n, d_rows_out, s);
+  SWPS_TRY(t->isnew.ensure(n));
+  uint8_t *isnew = t->isnew.as<uint8_t>();
+  k_claim_slots<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(),
+                                               t->counters.as<uint32_t>(), t->mask, d_rows_out, isnew);
+  SWPS_HIP(hipGetLastError());
+  std::vector<uint8_t> nw(n);
+  uint32_t base = 0;
+  SWPS_HIP(hipMemcpyAsync(nw.data(), isnew, n, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipMemcpyAsync(&base, t->counters.p, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  std::vector<uint32_t> order(n, 0xFFFFFFFFu), newrow(n, 0);
+  for (uint64_t i = 0; i < n; i++) {
+    if (place[i] >= n || order[place[i]] != 0xFFFFFFFFu) return fail(SWPS_E_CFG, "placement is not a permutation");
+    order[place[i]] = (uint32_t)i;
+  }
+  uint64_t next = base;
+  for (uint64_t j = 0; j < n; j++)
+    if (nw[order[j]]) newrow[order[j]] = (uint32_t)std::min<uint64_t>(next++, 0xFFFFFFFFull);
+  DevMem dn;
+  SWPS_TRY(upload(dn, newrow, s));
+  k_publish_rows<<<blocks_for(n), 256, 0, s>>>(d_keys, n, dn.as<uint32_t>(), t->slot_row.as<uint32_t>(),
+                                                t->row_key.as<uint64_t>(), t->counters.as<uint32_t>(),
+                                                t->cfg.capacity, d_rows_out, isnew);
+  SWPS_HIP(hipGetLastError());
+  const uint32_t nrows = (uint32_t)std::min<uint64_t>(next, 0xFFFFFFFFull);
+  SWPS_HIP(hipMemcpyAsync(t->counters.p, &nrows, 4, hipMemcpyHostToDevice, s));
+  SWPS_TRY(init_new_rows(t, d_keys, n, d_rows_out, isnew, s));
+  return table_check_error(t, s);  // synchronises: nrows and dn outlive their copies
 }
 
 int check_app_table(swps_table *t) {

@@ -273,6 +273,39 @@ def test_lr_rows_per_wave_bit_identical(lib, gpu, monkeypatch, fast):
             assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("fast", [False, True])
+def test_lr_row_placement_bit_identical(lib, gpu, monkeypatch, fast):
+    """The single-GPU init's row layout (keys' rows in first-appearance order by
+    (batch, row tile, key): SWPS_LR_PLACE) and the XCD-aware block order of the
+    row tiles (key octiles, SWPS_LR_XCD), both off by default (measured
+    slower), change where rows live and which block runs where, never a
+    result: errors and weights bit for bit with both off, one on, both on,
+    and the (batch, key) layout — Criteo shape with 16 row tiles per batch,
+    under the three init modes (reference gen_float draws in pull order, the
+    table's SWPS_INIT_FLCG draws in call order, key hash)."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(12000, seed=11)
+    monkeypatch.setenv("SWPS_LR_TILE_BITS", "8")  # 4,096-row batches: 16 tiles
+    res = []
+    for place, xcd in (("0", "0"), ("1", "1"), ("1", "0"), ("0", "1"), ("2", "0")):
+        monkeypatch.setenv("SWPS_LR_PLACE", place)
+        monkeypatch.setenv("SWPS_LR_XCD", xcd)
+        out = []
+        for init, ref in (("hash", False), ("flcg", False), ("hash", True)):
+            t = lib.Table("lr", capacity=1 << 19, dtype="f32", learning_rate=0.05, init=init, seed=1)
+            m = lib.LR(t, minibatch=4095, init_ref=ref, fast_sums=fast)
+            m.load_csr(y, off, f, v)
+            m.init()
+            out.append(m.train(2))
+            out.append(m.params()[1])
+            m.close()
+            t.close()
+        res.append(out)
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert np.array_equal(a, b)
+
+
 def test_lr_fused_reduce_bit_identical(lib, gpu, monkeypatch):
     """Fast sums: k_lr_reduce_fused (static long-run list, one launch) == the
     short / long pair with the runtime long list, bit for bit (Criteo shape
