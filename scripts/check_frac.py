@@ -1,9 +1,9 @@
 """Recompute each committed bench line's roofline fraction from the rocprof
-kernel-stats CSV of the same leg (profiles/r03_<leg>_kernel_stats.csv):
+kernel-stats CSV of the same leg (profiles/rNN_<leg>_kernel_stats.csv):
 algorithmic bytes per launch (the line's bytes_per_launch) / the summed
 average durations of the group's kernels / 8 TB/s, against the line's frac.
 
-    python scripts/check_frac.py [profiles/r03_bench_<leg>.json ...]"""
+    python scripts/check_frac.py [profiles/rNN_bench_<leg>.json ...]"""
 import csv
 import glob
 import json
@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GROUPS = {  # kernel base names of each roofline group
     "w2v": ("k_gather_b", "k_combine_b", "k_push_b", "k_gather_t", "k_combine", "k_push_thp", "k_gather", "k_push",
             "k_push_tg"),
-    "lr_forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_l", "k_lr_forward_g"),
+    "lr_forward": ("k_lr_forward_r", "k_lr_forward", "k_lr_forward_l", "k_lr_forward_g", "k_lr_forward_c"),
     "lr_push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long", "k_lr_reduce_long_fast",
                 "k_lr_tiles", "k_lr_tiles_fin"),
     "s2v": ("k_s2v_docs",),
@@ -29,8 +29,11 @@ def base(name):
 def main(paths):
     bad = 0
     for p in paths:
+        tag = os.path.basename(p)[:3]  # rNN
         leg = os.path.basename(p)[len("r03_bench_"):-len(".json")]
-        csvp = os.path.join(os.path.dirname(p), "r03_%s_kernel_stats.csv" % leg)
+        if leg.endswith("_traced"):  # the line of the traced process itself
+            leg = leg[:-len("_traced")]
+        csvp = os.path.join(os.path.dirname(p), "%s_%s_kernel_stats.csv" % (tag, leg))
         if not os.path.exists(csvp):
             continue
         b = json.load(open(p))
@@ -63,6 +66,7 @@ def main(paths):
 
 
 if __name__ == "__main__":
-    ps = sys.argv[1:] or sorted(x for x in glob.glob(os.path.join(ROOT, "profiles", "r03_bench_*.json"))
+    tag = max(os.path.basename(x)[:3] for x in glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_*.json")))
+    ps = sys.argv[1:] or sorted(x for x in glob.glob(os.path.join(ROOT, "profiles", tag + "_bench_*.json"))
                                 if not x.endswith("_traced.json"))
     sys.exit(1 if main(ps) else 0)
