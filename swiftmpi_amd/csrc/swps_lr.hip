@@ -1257,7 +1257,7 @@ inline unsigned nblk(uint64_t n, unsigned bs = 256) { return (unsigned)std::max<
 
 struct LTimer {
   bool on = false;
-  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;  // k >= 16: timer k - 16, not counted
   double ms[4] = {0};
   uint64_t cnt[4] = {0};
   hipEvent_t begin(hipStream_t s) {
@@ -1285,12 +1285,17 @@ struct LTimer {
   void ext_end(int k, hipEvent_t b, hipEvent_t e) {
     if (b && e) pending.push_back({k, {b, e}});
   }
+  // a further kernel of the same launch group: its own stamped time added, the launch not counted
+  // again (a group's kernels summed, as rocprof sums them, without the gaps between them)
+  void ext_more(int k, hipEvent_t b, hipEvent_t e) {
+    if (b && e) pending.push_back({k + 16, {b, e}});
+  }
   void resolve() {
     for (auto &q : pending) {
       float t = 0;
       (void)hipEventElapsedTime(&t, q.second.first, q.second.second);
-      ms[q.first] += t;
-      cnt[q.first]++;
+      ms[q.first & 15] += t;
+      if (q.first < 16) cnt[q.first]++;
       (void)hipEventDestroy(q.second.first);
       (void)hipEventDestroy(q.second.second);
     }
@@ -1952,8 +1957,14 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
                l->d_tinfo.as<uint32_t>(), (l->sharded ? l->d_tslot : l->d_tdst).as<uint32_t>(), l->d_tpart.as<double>(),
                l->d_err.as<float>(),
                r0, nrb, l->tile_bits, l->fwd_diag};
-    hipEvent_t tb0 = l->timer.ext(), te0 = l->timer.ext();
+    // each kernel stamped by itself: the group's time is the sum of the two kernels' (not the span
+    // from the first one's start to the second one's end, which holds the dispatch gap between them)
+    hipEvent_t tb0 = l->timer.ext(), te0 = l->timer.ext(), tb1 = nullptr, te1 = nullptr;
     const bool fin = l->bmulti[bi + 1] > l->bmulti[bi] || l->bmlong[bi + 1] > l->bmlong[bi];
+    if (nch && fin) {
+      tb1 = l->timer.ext();
+      te1 = l->timer.ext();
+    }
     if (nch) {
       const bool b512 = l->tile_threads == 512;  // 4 records per thread, 512 threads: 2,048-record blocks
       auto kt = b512                    ? k_lr_tiles<4, 512>
@@ -1964,22 +1975,22 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
                 : l->tile_chunk == 1792 ? k_lr_tiles<7>
                 : l->tile_chunk == 4096 ? k_lr_tiles<16>
                                         : k_lr_tiles<8>;
-      hipExtLaunchKernelGGL(kt, dim3(nch), dim3(b512 ? 512 : 256), 0, s, tb0, fin ? (hipEvent_t) nullptr : te0, 0,
-                            ra, tt);
+      hipExtLaunchKernelGGL(kt, dim3(nch), dim3(b512 ? 512 : 256), 0, s, tb0, te0, 0, ra, tt);
     }
     const uint32_t nl = (uint32_t)(l->bmlong[bi + 1] - l->bmlong[bi]);
     if (nm || nl) {
       const uint32_t LB = std::min<uint32_t>((nl + 3) / 4, 1024);
       hipExtLaunchKernelGGL(k_lr_tiles_fin, dim3(LB + (nm ? nblk(nm) : 0)), dim3(256), 0, s,
-                            nch ? (hipEvent_t) nullptr : tb0, te0, 0, ra,
+                            nch ? tb1 : tb0, nch ? te1 : te0, 0, ra,
                             (const uint4 *)l->d_tmulti.p + l->bmulti[bi], (const uint32_t *)l->d_tmsrow.as<uint32_t>() + l->bmulti[bi], nm,
                             (const uint4 *)l->d_tmlong.p + l->bmlong[bi], (const uint32_t *)l->d_tmlrow.as<uint32_t>() + l->bmlong[bi], nl,
                             LB, (const double *)l->d_tpart.as<double>(), (uint64_t)q0);
     }
     SWPS_HIP(hipGetLastError());
-    if (nch || fin)
+    if (nch || fin) {
       l->timer.ext_end(3, tb0, te0);
-    else if (tb0) {
+      l->timer.ext_more(3, tb1, te1);
+    } else if (tb0) {
       (void)hipEventDestroy(tb0);
       (void)hipEventDestroy(te0);
     }
