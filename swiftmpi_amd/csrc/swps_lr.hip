@@ -213,10 +213,29 @@ __global__ __launch_bounds__(256) void k_lr_forward_r(const uint64_t *__restrict
 // weight gathers, then the ordered sums (the groups' chains interleaved) — G times the memory
 // chains in flight per wave, a G-th of the waves.  Same products, same feature-order fp32 sums:
 // bit-identical (SWPS_LR_FWD_G).
-// hrow != nullptr (single GPU): the batch's kLrHot hottest keys' shard rows; fidx codes a record of
-// one of them as kLrHotBit | rank, and the block reads its weight from LDS (loaded once per block)
-constexpr int kLrHot = 256;
+// hrow != nullptr (single GPU): the batch's nhot (<= kLrHot) hottest keys' shard rows; fidx codes a
+// record of one of them as kLrHotBit | rank, and the block reads its weight from LDS (loaded once per
+// block, kLrHotPT per thread)
+constexpr int kLrHot = 1024;
+constexpr int kLrHotPT = kLrHot / 256;
 constexpr uint32_t kLrHotBit = 0x80000000u;
+struct HotW {  // a thread's share of the block's hot weights: loads first, LDS stores later
+  float v[kLrHotPT];
+  __device__ __forceinline__ void ld(const float *rows, const uint32_t *hrow, uint32_t nhot, int tid) {
+#pragma unroll
+    for (int j = 0; j < kLrHotPT; j++) {
+      const uint32_t q = (uint32_t)tid + 256u * j;
+      v[j] = hrow && q < nhot ? rows[(uint64_t)hrow[q] * 2] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void st(float *wh, uint32_t nhot, int tid) const {
+#pragma unroll
+    for (int j = 0; j < kLrHotPT; j++) {
+      const uint32_t q = (uint32_t)tid + 256u * j;
+      if (q < nhot) wh[q] = v[j];
+    }
+  }
+};
 template <int R, int G>
 __global__ __launch_bounds__(256) void k_lr_forward_g(const uint64_t *__restrict__ row_off,
                                                       const uint32_t *__restrict__ fidx, const float *__restrict__ fval,
@@ -229,7 +248,8 @@ __global__ __launch_bounds__(256) void k_lr_forward_g(const uint64_t *__restrict
   __shared__ float wh[kLrHot];
   // the hot weights' loads go out first; their LDS stores and the block barrier come after this
   // thread's own index loads (every wave reaches the barrier: rows past the batch are inactive)
-  const float hw = hrow && threadIdx.x < nhot ? rows[(uint64_t)hrow[threadIdx.x] * 2] : 0.f;
+  HotW hw;
+  hw.ld(rows, hrow, nhot, threadIdx.x);
   const int lane = threadIdx.x & 63;
   const int sub = lane / L, k = lane - sub * L;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -262,7 +282,7 @@ __global__ __launch_bounds__(256) void k_lr_forward_g(const uint64_t *__restrict
     x1[g] = v1 ? fval[a[g] + k + L] : 0.f;
   }
   if (hrow) {
-    if (threadIdx.x < nhot) wh[threadIdx.x] = hw;
+    hw.st(wh, nhot, threadIdx.x);
     __syncthreads();
   }
   float w0[G], w1[G];
@@ -339,7 +359,8 @@ __global__ __launch_bounds__(256) void k_lr_forward_c(const uint2 *__restrict__ 
   __shared__ float prod[CAP];
   __shared__ float wh[kLrHot];
   const int tid = threadIdx.x;
-  const float hw = hrow && (uint32_t)tid < nhot ? rows[(uint64_t)hrow[tid] * 2] : 0.f;
+  HotW hw;
+  hw.ld(rows, hrow, nhot, tid);
   const uint2 ch = chunks[blockIdx.x];  // first row (batch-relative), rows
   const uint64_t rf = r0 + ch.x;
   const uint64_t c0 = row_off[rf], c1 = row_off[rf + ch.y];
@@ -361,7 +382,7 @@ __global__ __launch_bounds__(256) void k_lr_forward_c(const uint2 *__restrict__ 
     y = label[rf + tid];
   }
   if (hrow) {
-    if ((uint32_t)tid < nhot) wh[tid] = hw;
+    hw.st(wh, nhot, tid);
     __syncthreads();
   }
   float w[RPT];
@@ -1357,6 +1378,9 @@ struct swps_lr {
   int stage = 0;                // SWPS_LR_STAGE: the forward reads the batch's weights staged densely (k_lr_stage)
   DevMem d_frun, d_wstage;
   int hot = 1;  // SWPS_LR_HOT: the forward reads the batch's hot keys' weights from LDS (k_lr_forward_g)
+  // SWPS_LR_NHOT: how many (<= kLrHot).  Same-box A/B at the Criteo step, round 4 (forward µs):
+  // 256 13.84, 512 13.53, 768 14.0-14.3, 1024 15.6 — each block loads them all
+  uint32_t nhot = 512;
   DevMem d_hot_of_run, d_hgrun, d_hrow, d_fhot;
   std::vector<uint32_t> bnhot;
   uint64_t max_bruns = 0;
@@ -1687,7 +1711,7 @@ int lr_index(swps_lr *l) {
       ord.clear();
       for (uint64_t q = l->brun[b]; q < l->brun[b + 1]; q++)
         if (cnt[q] >= 8) ord.push_back((uint32_t)q);
-      const size_t h = std::min<size_t>(ord.size(), kLrHot);
+      const size_t h = std::min<size_t>(ord.size(), (size_t)l->nhot);
       std::partial_sort(ord.begin(), ord.begin() + h, ord.end(), [&](uint32_t x, uint32_t y) {
         return cnt[x] != cnt[y] ? cnt[x] > cnt[y] : x < y;
       });
@@ -2065,6 +2089,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   if (const char *e = getenv("SWPS_LR_FWD_C")) l->fwd_c = atoi(e);      // A/B, tests
   if (const char *e = getenv("SWPS_LR_STAGE")) l->stage = atoi(e);        // A/B, tests
   if (const char *e = getenv("SWPS_LR_HOT")) l->hot = atoi(e);            // A/B, tests
+  if (const char *e = getenv("SWPS_LR_NHOT")) l->nhot = (uint32_t)std::min(std::max(atoi(e), 1), kLrHot);
   if (const char *e = getenv("SWPS_LR_FWD_RECORDS")) l->fwd_records = atoi(e);  // A/B, tests
   if (const char *e = getenv("SWPS_LR_INLINE")) l->inline_records = atoi(e);     // A/B, tests       // timing experiments (wrong results)
   if (const char *e = getenv("SWPS_LR_FUSED")) l->fused_reduce = atoi(e) != 0;  // A/B timing, tests

@@ -463,6 +463,34 @@ def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits, chunk):
         assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max(), (np.abs(a - b).max(), np.abs(a).max())
 
 
+@pytest.mark.parametrize("fc", ["1", "0"])
+def test_lr_hot_key_count_bit_identical(lib, gpu, monkeypatch, fc):
+    """The forward's LDS copy of the batch's hottest keys' weights (SWPS_LR_NHOT = 1, 256, 512
+    the default, 1024 the most: four loads per thread) == no LDS copy, bit for bit, in
+    k_lr_forward_c and k_lr_forward_g: Criteo batches of 8,191 rows (over 1,024 keys with runs
+    of >= 8 records), fast and exact sums."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(24000, seed=13)
+    monkeypatch.setenv("SWPS_LR_FWD_C", fc)
+    res = []
+    for hot, nhot in (("0", "512"), ("1", "512"), ("1", "1"), ("1", "256"), ("1", "1024"), ("1", "700")):
+        monkeypatch.setenv("SWPS_LR_HOT", hot)
+        monkeypatch.setenv("SWPS_LR_NHOT", nhot)
+        out = []
+        for fast in (False, True):
+            t = lib.Table("lr", capacity=1 << 20, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+            m = lib.LR(t, minibatch=8190, init_ref=False, fast_sums=fast)
+            m.load_csr(y, off, f, v)
+            m.init()
+            out += [m.train(2), m.params()[1]]
+            m.close()
+            t.close()
+        res.append(out)
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("groups,stage,hot", [("2", "0", "1"), ("4", "0", "1"), ("2", "1", "0"), ("2", "0", "0")])
 def test_lr_forward_groups_bit_identical(lib, gpu, monkeypatch, groups, stage, hot):
     """k_lr_forward_g (2 / 4 groups of 3 rows per wave, every group's loads and gathers issued
