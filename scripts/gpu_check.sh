@@ -18,5 +18,5 @@ rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 [ -n "$NO_BENCH" ] && exit $rc
-step bench 600 python bench.py --steps 20 --warmup 5 || exit $?
+step bench 600 python bench.py || exit $?  # the driver's command
 exit $rc

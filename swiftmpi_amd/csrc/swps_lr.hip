@@ -869,7 +869,7 @@ __global__ __launch_bounds__(256) void k_lr_reduce_fused(LrReduce a, const uint3
 // random order within a key's run): 2.56M divergent 4-B reads per Criteo batch.  Cut the batch
 // into tiles of 2^tb rows: the static index orders each batch's records by (tile, key), so a
 // block loads its tile's slice of e into LDS once and reads every record's e from LDS.  A block
-// takes 1,024 consecutive records of one tile (4 per thread, coalesced) and sums each key's
+// takes kTileChunk (1,536) consecutive records of one tile (6 per thread, coalesced) and sums each key's
 // records with one block-wide segmented scan; a piece = a key's records inside one block.  A key
 // with a single piece is applied by k_lr_tiles itself; the others get one fp64 partial per piece,
 // added in (tile, record) order by k_lr_tiles_fin.  Same fp32 products e*x_i as the record path,
@@ -1446,7 +1446,7 @@ void lr_xcd_order(std::vector<T> &v, int E, uint64_t q0, uint64_t q1, const std:
   std::copy(out.begin(), out.end(), v.begin() + q0 * E);
 }
 
-// The tile index (k_lr_tiles): every batch's records in (tile, key) order; the blocks (1,024
+// The tile index (k_lr_tiles): every batch's records in (tile, key) order; the blocks (kTileChunk
 // consecutive records of one tile); the pieces (a key's records inside one block) with their
 // run, their partial's slot in (key, record) order, and per run its piece count and first slot;
 // per batch the runs with more than one piece.  ks / perm / rid / tmp are lr_index's scratch.
