@@ -943,12 +943,13 @@ def bench_s2v(args, ctx, corpus_batches=None):
 
 def _free_port_pair():
     """A port P on 127.0.0.1 with P and P + 1 both free (torch.distributed's
-    store at MASTER_PORT, the library's bootstrap at MASTER_PORT + 1)."""
+    store at MASTER_PORT, the library's bootstrap at MASTER_PORT + 1), below Linux's
+    ephemeral range (32768-60999) so no outgoing connection takes it meanwhile."""
     import random
     import socket
     rng = random.Random()
     while True:
-        p = rng.randrange(20000, 60000)
+        p = rng.randrange(15000, 32000)
         socks = []
         try:
             for q in (p, p + 1):

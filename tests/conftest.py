@@ -14,25 +14,43 @@ _USED_PORTS = set()
 
 
 def free_port():
-    """A free TCP port on 127.0.0.1 not handed out before in this session and
-    not adjacent to one (the library bootstraps RCCL at MASTER_PORT + 1; two
-    bind-to-0 probes in a row may return the same port)."""
+    """A free TCP port P on 127.0.0.1 (P + 1 free too: the library bootstraps RCCL at
+    MASTER_PORT + 1) not handed out before in this session nor adjacent to one, drawn
+    below Linux's ephemeral range (32768-60999), where the kernel's own outgoing
+    connections cannot take it between this probe and the bind that follows (a
+    bind-to-0 probe hands out exactly such a port: EADDRINUSE on a busy box)."""
     import random
     import socket
     rng = random.Random()
     while True:
-        p = rng.randrange(20000, 60000)
+        p = rng.randrange(15000, 32000)
         if p in _USED_PORTS or p + 1 in _USED_PORTS or p - 1 in _USED_PORTS:
             continue
-        s = socket.socket()
+        socks = []
         try:
-            s.bind(("127.0.0.1", p))
+            for q in (p, p + 1):
+                sk = socket.socket()
+                socks.append(sk)
+                sk.bind(("127.0.0.1", q))
         except OSError:
             continue
         finally:
-            s.close()
+            for sk in socks:
+                sk.close()
         _USED_PORTS.add(p)
         return p
+
+
+def init_gloo1():
+    """A world-1 gloo process group on a free port (a fresh port on the rare EADDRINUSE)."""
+    import torch.distributed as dist
+    for attempt in range(5):
+        try:
+            dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % free_port(), rank=0, world_size=1)
+            return
+        except dist.DistNetworkError:
+            if attempt == 4:
+                raise
 
 
 def pytest_configure(config):
@@ -106,16 +124,10 @@ def gpu(lib):
 def gloo1():
     """A world-1 gloo process group for the sharded paths (torn down after
     the test if this fixture created it)."""
-    import socket
-
     import torch.distributed as dist
     own = not dist.is_initialized()
     if own:
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
-        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+        init_gloo1()
     yield dist
     if own:
         dist.destroy_process_group()

@@ -206,12 +206,8 @@ def test_sharded_world1_equals_unsharded(lib, gpu, tmp_path, dtype, fp64i, overl
     kw = dict(window=3, negative=4, minibatch=13, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=fp64i)
     own = not dist.is_initialized()
     if own:
-        import socket
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
-        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+        from conftest import init_gloo1
+        init_gloo1()
     try:
         t = lib.Table("w2v", dim=D, capacity=1000, dtype=dtype, learning_rate=0.7, init="hash", seed=3)
         sh = ShardedWord2Vec(t, overlap=overlap, **kw)
