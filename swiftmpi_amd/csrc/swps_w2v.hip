@@ -2090,7 +2090,7 @@ struct swps_w2v {
   int push_t = 1;     // fast mode: k_push_t (SWPS_PUSH_T=0: k_push, for A/B timing)
   int gather_unr = 8;         // k_gather_t rows in flight per wave (SWPS_GATHER_UNR: 4, 8, 16; A/B timing)
   int push_wpe = 0;  // SWPS_PUSH_WPE: 0 = by batch size, 4 / 1 = k_push_b<1,1,0> at 4 waves per SIMD or not
-  int push_unr = 8;  // SWPS_PUSH_UNR=4: k_push_b<1,1,0> with 4 record rows in flight (A/B)
+  int push_unr = 4;  // k_push_b<1,1,0>'s record rows in flight: 4 (SWPS_PUSH_UNR8=1: 8, the previous default)
   uint32_t gather_grid = 65536;  // k_gather_t / k_combine grid cap in blocks (SWPS_GATHER_GRID; A/B: 2048..65536 -> 65536 best)
   bool cache_pad = true;  // worker-cache rows padded to 128 B (SWPS_CACHE_PAD=0: D-strided, for A/B timing)
   int cs = 0;              // worker-cache row stride in elements (set with the cache allocation)
@@ -3908,16 +3908,12 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
           // (same-box A/B: B = 100 2.87e8 -> 3.06e8 words/s, B = 5000 -0.1 %); SWPS_PUSH_WPE=1 / 4 forces
           const bool wpe4 = w->push_wpe == 4 || (w->push_wpe == 0 && U < 65536);
           hipEvent_t pb = tm.ext(), pe = tm.ext();  // profiled: the kernel's own start / end stamps
-          if (w->push_unr == 4 && w->bfp_rb == 0 && bfp_shape(D) == 11) {  // A/B: 4 record rows in flight
-            if (w->push_wpe == 5)
-              hipExtLaunchKernelGGL(k_push_b<1, 1, 0, 4, false, 5>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part,
-                                    (double *)nullptr);
-            else if (wpe4)
-              hipExtLaunchKernelGGL(k_push_b<1, 1, 0, 4, false, 4>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part,
-                                    (double *)nullptr);
-            else
-              hipExtLaunchKernelGGL(k_push_b<1, 1, 0, 4, false, 1>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part,
-                                    (double *)nullptr);
+          if (w->push_unr == 4 && w->bfp_rb == 0 && bfp_shape(D) == 11) {
+            // D = 257..320, bfp32: 4 record rows in flight, 114 VGPRs, 4 waves per SIMD without spills
+            // (same-box A/B, round 4: B = 100 3.01e8 -> 3.09e8 words/s, B = 5000 +0.1 %; 5 / 6 / 8 rows:
+            // 3.07 / 3.03 / 3.01e8 at B = 100; 5 waves per SIMD (13 spills) 2.85e8)
+            hipExtLaunchKernelGGL(k_push_b<1, 1, 0, 4, false, 4>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part,
+                                  (double *)nullptr);
           } else if (wpe4 && w->bfp_rb == 0 && bfp_shape(D) == 11) {
             hipExtLaunchKernelGGL(k_push_b<1, 1, 0, 8, false, 4>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part,
                                   (double *)nullptr);
@@ -4164,7 +4160,7 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
   if (const char *e = getenv("SWPS_REC_GENERIC")) w->rec_generic = atoi(e) != 0;
   if (const char *e = getenv("SWPS_GATHER_GRID")) w->gather_grid = std::max(64, atoi(e));
   if (const char *e = getenv("SWPS_PUSH_WPE")) w->push_wpe = atoi(e);  // A/B: push occupancy
-  if (const char *e = getenv("SWPS_PUSH_UNR")) w->push_unr = atoi(e);  // A/B: record rows in flight
+  if (const char *e = getenv("SWPS_PUSH_UNR8")) w->push_unr = atoi(e) ? 8 : 4;  // A/B, tests
   int rc = check_cfg(w);
   if (!rc && hipHostMalloc((void **)&w->h_small, 64) != hipSuccess) rc = fail(SWPS_E_OOM, "pinned alloc");
   if (!rc) rc = w->d_rows_touched.ensure(16);

@@ -210,16 +210,15 @@ def test_bench_kernels_single_batch(lib, oracle_mod, gpu, tmp_path, D, mode, lin
     assert rel.max() <= tol, float(rel.max())
 
 
-@pytest.mark.parametrize("env,fixed,fp64i", [("SWPS_SORT_WIDE", "", False), ("SWPS_FUSED_PUSH", "", False),
-                                             ("SWPS_MULTI_SORT", "", False),
-                                             ("SWPS_MULTI_SORT", "SWPS_FUSED_PUSH=0", False),
-                                             ("SWPS_MULTI_SORT", "", True), ("SWPS_SPLIT_PUSH", "", False),
-                                             ("SWPS_SORT_IOTA", "", False),
-                                             ("SWPS_SEG4", "", False), ("SWPS_TOK_LOCAL", "", False),
-                                             ("SWPS_TOK_LOCAL", "", "'bfp32'"), ("SWPS_ITEM_HEADS", "", False)])
-def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed, fp64i):
-    """Three 5000-line batches of the bench corpus train to the same bits with
-    either setting of:
+@pytest.mark.parametrize("env,fixed,fp64i,mb", [(e, f, x, 5000) for e, f, x in (
+    ("SWPS_SORT_WIDE", "", False), ("SWPS_FUSED_PUSH", "", False), ("SWPS_MULTI_SORT", "", False),
+    ("SWPS_MULTI_SORT", "SWPS_FUSED_PUSH=0", False), ("SWPS_MULTI_SORT", "", True), ("SWPS_SPLIT_PUSH", "", False),
+    ("SWPS_SORT_IOTA", "", False), ("SWPS_SEG4", "", False), ("SWPS_TOK_LOCAL", "", False),
+    ("SWPS_TOK_LOCAL", "", "'bfp32'"), ("SWPS_ITEM_HEADS", "", False), ("SWPS_PUSH_UNR8", "", "'bfp32'"))]
+    + [("SWPS_PUSH_UNR8", "", "'bfp32'", 100)])
+def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed, fp64i, mb):
+    """Three 5000-line batches (forty 100-line ones) of the bench corpus train to the same bits
+    with either setting of:
     * SWPS_SORT_WIDE — the minibatch key indices need 18 bits: they sort in two
       9-bit onesweep passes (swps_sort.h) instead of three 8-bit ones (same
       stable order);
@@ -242,7 +241,9 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed,
       lookups of k_tok_local vs random local / row lookups (fast mode and the
       headline's bfp32);
     * SWPS_ITEM_HEADS — k_item_desc's (key, kind) run of each item from a
-      max-scan of the runs' first items vs a binary search."""
+      max-scan of the runs' first items vs a binary search;
+    * SWPS_PUSH_UNR8 — k_push_b's single-chunk runs summed with 8 record rows
+      in flight vs 4 (the same record order), at 5000 and at 100 lines."""
     res = []
     for k_v in fixed.split():
         monkeypatch.setenv(*k_v.split("="))
@@ -254,11 +255,11 @@ def test_variant_bit_identical_at_bench_scale(lib, gpu, monkeypatch, env, fixed,
                 "from swiftmpi_amd.synth import zipf_tokens; ids, off = zipf_tokens(17005207, 253854, 1000, seed=8); "
                 "keys = np.array([sw.bkdr('w%%d' %% i) for i in range(253854)], dtype=np.uint64); "
                 "t = sw.Table('w2v', dim=300, capacity=260000, dtype='f32', init='hash', seed=1); "
-                "w = sw.Word2Vec(t, minibatch=5000, sample=1e-5, init='table', fp64_intermediates=%s); "
-                "w.load_tokens(ids, off, keys); w.init(); w.train_batches(3); p = w.get_params(); "
+                "w = sw.Word2Vec(t, minibatch=%d, sample=1e-5, init='table', fp64_intermediates=%s); "
+                "w.load_tokens(ids, off, keys); w.init(); w.train_batches(%d); p = w.get_params(); "
                 "import hashlib; print('H', hashlib.sha256(p.tobytes()).hexdigest(), w.stats()['pairs'])"
                 % (str(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))),
-                   fp64i))
+                   mb, fp64i, 3 if mb >= 5000 else 40))
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         res.append([l for l in r.stdout.splitlines() if l.startswith("H ")][-1])
