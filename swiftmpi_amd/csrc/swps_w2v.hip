@@ -3931,6 +3931,8 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
           }
           goto push_done;
         }
+        // (4 record rows in flight here: 94 VGPRs, 5 waves per SIMD, but the sharded world-1 push
+        // 2.487 -> 2.506 ms, same-box A/B, round 4: kept at 8)
 #define SWPS_F(a_, b_, r_) k_push_b<a_, b_, r_, 8, true><<<pgrid, 256, 0, s>>>(pa, part, g64)
         const int world = w->world;
         if (w->split_grads && world > 1 && world <= kMaxSplitOwners) {  // two owner-half passes (below)
