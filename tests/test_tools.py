@@ -41,6 +41,28 @@ def test_pmc_summary_read_requests_by_size(tmp_path):
     assert s["config"] == {"app": "w2v"}
 
 
+def test_pmc_summary_sq_wave_state_fractions(tmp_path):
+    """An SQ pass (scripts/gpu_sq.sh): WAIT_ANY / WAIT_INST_ANY / ACTIVE_INST_ANY as fractions
+    of WAVE_CYCLES (they partition it), cycles and instructions per wave; no byte fields."""
+    k = "void (anonymous namespace)::k_lr_tiles<6, 256>((anonymous namespace)::LrReduce, (anonymous namespace)::LrTiles)"
+    sq = str(tmp_path / "sq")
+    rows = []
+    for i in range(2):
+        rows += [(i, k, "SQ_WAVES", 100), (i, k, "SQ_WAVE_CYCLES", 10000), (i, k, "SQ_WAIT_ANY", 5000),
+                 (i, k, "SQ_WAIT_INST_ANY", 3000), (i, k, "SQ_ACTIVE_INST_ANY", 2000), (i, k, "SQ_INSTS_VALU", 600),
+                 (i, k, "SQ_INSTS_VMEM_RD", 30), (i, k, "SQ_BUSY_CYCLES", 9000)]
+    _csv(sq, rows)
+    out = str(tmp_path / "sq.json")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), out, sq, "--last", "2"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    e = json.load(open(out))["kernels"]["k_lr_tiles<6, 256>"]
+    assert (e["parked_frac"], e["issue_stall_frac"], e["active_frac"]) == (0.5, 0.3, 0.2)
+    assert e["quad_cycles_per_wave"] == 100.0 and e["valu_per_wave"] == 6.0 and e["vmem_rd_per_wave"] == 0.3
+    assert e["hbm_bytes"] is None
+    assert "parked 0.50" in r.stdout
+
+
 def test_bench_pmc_lookup_matches_config_and_kernel_base_names(tmp_path, monkeypatch):
     import importlib.util
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
