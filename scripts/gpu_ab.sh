@@ -3,6 +3,7 @@
 # then the default bench (B = 5000 + its B = 100 leg) once per variant, REPS
 # rounds interleaved.  Variants are ';'-separated env assignments:
 #   VARIANTS="SWPS_FUSED_PUSH=0;SWPS_FUSED_PUSH=1" REPS=2 bash scripts/gpu_ab.sh
+# (an unused name such as SWPS_NOP=1 stands for the defaults)
 # Stops at the first GPU fault / abort / timeout.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
