@@ -253,6 +253,350 @@ def cpu_baseline_s2v(toks, off, args, docs):
                       % (docs, n, len(words), dt)}
 
 
+MODE_DESC = {"parity": "fp64 neu1/neu1e + gradient partials (reference-parity mode)",
+             "bfp40": "block-fp neu1/neu1e, int32 + int8 mantissas per row exponent, fp64 sums (5 B/element)",
+             "bfp32": "block-fp neu1/neu1e, int32 mantissas per row exponent, fp64 sums (4 B/element)",
+             "fast": "fp32 neu1/neu1e + partials (fast mode: outside the 1e-5 single-batch bar)"}
+INTER = {"bfp40": "bfp40", "bfp32": "bfp32", "fast": False, "parity": True}
+
+# ---- per-rank deadline, phases and fault injection ---------------------------------------------
+# A rank that waits on a lost or stuck peer must not hang the job until the driver's own timeout:
+# the library's RCCL guard aborts a communicator whose exchange does not retire in
+# SWPS_COMM_TIMEOUT_S (include/swps.h), torch.distributed's barriers get the same timeout, and
+# every rank arms an overall deadline (SWPS_BENCH_DEADLINE_S) that ends the process with rc 124
+# naming the phase it was in.  SWPS_BENCH_FAULT=<rank>:<phase> makes that rank kill itself
+# (SIGKILL) when it enters the phase: the test of those paths (tests/test_bench_gpu.py).
+_PHASE = {"name": "start", "rank": 0}
+
+
+def set_phase(name):
+    _PHASE["name"] = name
+    f = os.environ.get("SWPS_BENCH_FAULT")
+    if f and f.split(":")[0] == str(_PHASE["rank"]) and f.split(":", 1)[1] == name:
+        import signal
+        print("bench.py: rank %d: SWPS_BENCH_FAULT: killed entering phase %s" % (_PHASE["rank"], name),
+              file=sys.stderr, flush=True)
+        os.kill(os.getpid(), signal.SIGKILL)
+
+
+def arm_deadline(rank):
+    import threading
+    _PHASE["rank"] = rank
+    limit = float(os.environ.get("SWPS_BENCH_DEADLINE_S", "1500"))
+
+    def expire():
+        print("bench.py: rank %d: deadline of %g s exceeded in phase %s; exiting" % (rank, limit, _PHASE["name"]),
+              file=sys.stderr, flush=True)
+        os._exit(124)
+    t = threading.Timer(limit, expire)
+    t.daemon = True
+    t.start()
+
+
+def comm_timeout_s():
+    return float(os.environ.get("SWPS_COMM_TIMEOUT_S", "120"))
+
+
+class Ctx:
+    """One process per GPU: rank / world / device, torch.distributed (for the bench's own
+    barrier and max-over-ranks timing) and the library's communicator, made once and shared by
+    every sharded leg (RCCL when each rank has its own GPU, the library's TCP transport when
+    ranks share one)."""
+
+    def __init__(self, sharded):
+        import torch
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        ngpu = torch.cuda.device_count()
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(ngpu, 1)
+        torch.cuda.set_device(self.local)
+        self.dist, self.backend, self._comm = None, None, []
+        self.sharded = self.world > 1 or sharded
+        if self.sharded:
+            import datetime
+            import torch.distributed as dist
+            self.dist = dist
+            if "MASTER_ADDR" not in os.environ:
+                os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
+            to = datetime.timedelta(seconds=comm_timeout_s())
+            if ngpu >= self.world:  # one GPU per rank: RCCL over xGMI
+                self.backend = "nccl"
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local), timeout=to)
+            else:                    # functional check with ranks sharing a GPU
+                self.backend = "gloo"
+                dist.init_process_group("gloo", timeout=to)
+
+    def tuple(self):
+        return (self.rank, self.world, self.local, self.dist, self.backend)
+
+    def barrier(self):
+        import torch
+        torch.cuda.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def comm(self):
+        """The library's communicator (None if it could not be made on every rank)."""
+        if not self._comm and self.dist is not None:
+            import torch
+            from swiftmpi_amd.comm import Comm
+            port = int(os.environ.get("MASTER_PORT", "29533")) + 1
+            addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+            set_phase("communicator")
+            try:
+                c = (Comm.rccl(self.rank, self.world, self.local, addr=addr, port=port)
+                     if self.backend == "nccl" else Comm.tcp(self.rank, self.world, self.local, addr=addr, port=port))
+                ok = 1
+            except Exception as e:  # noqa: BLE001 — reported, and every rank falls back together
+                print("native communicator failed on rank %d: %s" % (self.rank, e), file=sys.stderr, flush=True)
+                c, ok = None, 0
+            t = torch.tensor([ok], dtype=torch.int32, device="cuda")
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+            self._comm.append(c if int(t.item()) else None)
+        return self._comm[0] if self._comm else None
+
+    def transport(self):
+        c = self._comm[0] if self._comm else None
+        return c.transport() if c is not None else None
+
+    def max_sum(self, dt, units):
+        """(max over ranks of dt, sum over ranks of units)."""
+        if self.dist is None:
+            return dt, float(units)
+        import torch
+        tt = torch.tensor([dt, float(units)], dtype=torch.float64, device="cuda")
+        mx = tt.clone()
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(tt, op=self.dist.ReduceOp.SUM)
+        return float(mx[0]), float(tt[1])
+
+
+def exchange_block(xs, steps, step_s, world, note):
+    """xGMI accounting of a sharded leg: bytes this rank sent to other ranks per step, over the
+    exchanges' event time on their stream (profiled pass), against 7 links x 153 GB/s."""
+    if xs is None:
+        return None
+    xg = xs["bytes_remote"] / (xs["ms"] * 1e-3) / 1e9 if xs["ms"] > 0 else 0.0
+    return {"bytes_remote_per_step": xs["bytes_remote"] / steps, "bytes_total_per_step": xs["bytes_total"] / steps,
+            "a2a_per_step": xs["calls"] / steps, "ms_per_step": xs["ms"] / steps,
+            "share_of_step": xs["ms"] / (step_s * 1e3) if step_s > 0 else None,
+            "GBps": xg, "peak": XGMI_PEAK_GBS, "frac": xg / XGMI_PEAK_GBS, "world": world, "note": note}
+
+
+def w2v_leg(sw, ctx, args, ids, off, keys, prec, minibatch, dim, frag_num, steps, warmup, tokens, vocab,
+            profile=True, setup_s=None):
+    """Build a CBOW-NS context on this rank's corpus (key-sharded over ctx's communicator when
+    ctx.sharded, else one HBM shard), warm up, time `steps` minibatches (barrier + sync on both
+    sides, max over ranks), then a second, profiled pass for the per-kernel roofline.  Returns
+    the leg's raw measurements."""
+    kw = dict(window=args.window, negative=args.negative, minibatch=minibatch, sample=args.sample, alpha=args.alpha,
+              profile=False, fp64_intermediates=INTER[prec], sampler=args.sampler)
+    t = sw.Table("w2v", dim=dim, capacity=vocab, dtype=args.dtype, learning_rate=args.lr, device=ctx.local,
+                 init="hash", seed=1)
+    comm = ctx.comm() if ctx.sharded and args.driver == "native" else None
+    if comm is not None:  # the library's own exchange
+        from swiftmpi_amd.dist import NativeShardedWord2Vec
+        w = NativeShardedWord2Vec(t, comm, frag_num=frag_num, **kw)
+    elif ctx.sharded:     # key-sharded over the ranks (BasicHashFrag), all-to-all per minibatch
+        from swiftmpi_amd.dist import ShardedWord2Vec
+        w = ShardedWord2Vec(t, frag_num=frag_num, pipeline=ctx.sharded and args.pipeline, **kw)
+    else:
+        w = sw.Word2Vec(t, init="ref", **kw)
+    t0 = time.perf_counter()
+    w.load_tokens(ids, off, keys)
+    t1 = time.perf_counter()
+    w.init()
+    if setup_s is not None:
+        setup_s.update(ingest=t1 - t0, first_pull=time.perf_counter() - t1)
+    info = w.info()
+    w.train_batches(warmup)
+    w.sync()
+
+    def timed(n):
+        s0 = w.stats()
+        ctx.barrier()
+        a = time.perf_counter()
+        w.train_batches(n)
+        w.sync()
+        ctx.barrier()
+        dt = time.perf_counter() - a
+        s1 = w.stats()
+        return dt, {k: s1[k] - s0[k] for k in s1 if k not in ("lstate", "fstate")}
+
+    dt, d = timed(steps)                    # the measured region: no event timing inside
+    res = {"dt": dt, "d": d, "info": info, "steps": steps, "warmup": warmup}
+    if profile:
+        w.set_profile(True)                 # a second, profiled pass for the per-kernel roofline
+        w.kernel_times(reset=True)
+        gw = getattr(w, "w", w)             # the per-rank Word2Vec (sharded: its learner)
+        g0 = gw.sum_stats()
+        if ctx.sharded:
+            w.set_exchange_profile(True)
+        dpt, dp = timed(steps)
+        res.update(dpt=dpt, dp=dp, kt=w.kernel_times(), g0=g0, g1=gw.sum_stats(),
+                   xs=w.exchange_stats() if ctx.sharded else None)
+        w.set_profile(False)
+        if ctx.sharded:
+            w.set_exchange_profile(False)
+    del w
+    t.close()
+    return res
+
+
+def w2v_roofline(r, args, prec, minibatch, dim, tokens, vocab, world, sharded):
+    """Roofline of the dominant kernel group of a w2v leg (the segmented gradient sums + fused
+    push), its PMC traffic from the committed passes of the same workload, the
+    forward's PMC rate and the whole step's §8(d) bytes."""
+    D, es = dim, (8 if args.dtype == "f64" else 4)
+    parity_main = prec == "parity"
+    bfp_main = prec.startswith("bfp") and args.dtype == "f32"
+    rb = 1 if prec == "bfp40" else 0
+    ea = 8 if (parity_main or args.dtype == "f64") else 4   # neu1/neu1e element size
+    # BFP modes: a record reads its position's mantissas (4 B, + the int8 residual in bfp40) per
+    # element and the row scale (4 B); partials and the mean-gradient payload are fp64
+    rec_row = D * (4 + rb) + 4 if bfp_main else D * ea
+    pa = 8 if bfp_main else ea
+    d, dp, kt, g0, g1 = r["d"], r["dp"], r["kt"], r["g0"], r["g1"]
+    dt = r["dt"]
+    # SURVEY.md §8(d) algorithmic bytes of k_forward: every context/target row occurrence read
+    # (4·D per row in fp32) + neu1, neu1e written per position
+    fwd_ms, fwd_n = kt["forward"]
+    fwd_bytes = es * D * (dp["ctx_rows"] + dp["tgt_rows"]) + 2 * rec_row * dp["kept"]
+    fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+    # the dominant kernel by time: the segmented gradient sums + AdaGrad push.  Each gradient
+    # record reads its source row (neu1 or neu1e of its position) and its 4-B record index; each
+    # item (chunk of <= 128 records of one key) that goes through a partial writes it (+ a 16-B
+    # descriptor) and the push reads it back; each pushed key reads h,v,h2,v2 (4·D·es), writes
+    # them (4·D·es) and its pre-update h,v to the worker cache (2·D·es) + 8 B of bounds.
+    g_rec, g_items = g1["records"] - g0["records"], g1["items"] - g0["items"]
+    g_mitems = g1["multi_items"] - g0["multi_items"]
+    nbat = g1["batches"] - g0["batches"]
+    fused = nbat > 0 and g1["fused"] - g0["fused"] == nbat
+    fused_g = nbat > 0 and g1.get("fused_grads", 0) - g0.get("fused_grads", 0) == nbat
+    # small batches run the multi-chunk gather on a side stream beside the push: the push timer
+    # then spans the whole group
+    split = nbat > 0 and g1.get("split", 0) - g0.get("split", 0) == nbat
+    gat_ms, gat_n = kt["gather"]
+    push_ms, push_n = kt.get("push", (0.0, 0))
+    kn = ("k_gather_b", "k_combine_b", "k_push_b") if bfp_main else ("k_gather_t", "k_combine", "k_push_thp")
+    if fused_g:  # sharded learner: the fused push stops at the mean gradients (2·D·pa written per key)
+        sum_kernel = "%s + %s + %s<TO_GRADS> (segmented gradient sums + fused mean gradients of the push payload)" % kn
+        gat_bytes = g_rec * (rec_row + 4) + g_mitems * (2 * D * pa + 16) + dp["pushed"] * (2 * D * pa + 8)
+        sum_ms = push_ms if split else gat_ms + push_ms
+    elif fused:
+        sum_kernel = "%s + %s + %s (segmented gradient sums + fused AdaGrad push)" % kn
+        gat_bytes = g_rec * (rec_row + 4) + g_mitems * (2 * D * pa + 16) + dp["pushed"] * (10 * es * D + 8)
+        sum_ms = push_ms if split else gat_ms + push_ms
+    else:
+        sum_kernel = ("k_gather + k_combine" if (parity_main or args.dtype == "f64") else "k_gather_t + k_combine") + \
+            " (segmented gradient sums)"
+        gat_bytes = g_rec * (D * ea + 4) + g_items * (D * ea + 16)
+        sum_ms = gat_ms
+    gat_gbs = gat_bytes / (sum_ms * 1e-3) / 1e9 if sum_ms > 0 else 0.0
+    # whole step (§8(d) full formula): rows read + gradients written + pull 16D/key + push (40D+8)/key
+    step_bytes = (2 * es * D * (dp["ctx_rows"] + dp["tgt_rows"]) + d["pulled"] * 4 * es * D +
+                  d["pushed"] * (10 * es * D + 8))
+    step_gbs = step_bytes / dt / 1e9
+    # the metric's "sparse push/pull HBM GB/s".  Single GPU: the pull is no kernel of its own —
+    # the forward reads the batch's keys straight from the table rows (counted in
+    # roofline.forward) and the push leaves their pre-update h, v in the worker cache
+    pp = {}
+    for name, nbytes in (("pull", dp["pulled"] * 4 * es * D), ("push", dp["pushed"] * (12 * es * D + 8))):
+        ms, n = kt.get(name, (0.0, 0))
+        if ms > 0 and not sharded and not ((fused or fused_g) and name == "push"):
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            pp[name] = {"GBps": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": nbytes / max(n, 1),
+                        "avg_launch_ms": ms / max(n, 1)}
+    if not sharded and "pull" not in pp:
+        pp["pull"] = "fused: k_forward reads the pulled keys' table rows directly; k_push writes their cache rows"
+    # HBM traffic of the same kernels from the committed PMC passes of this exact workload
+    # (scripts/gpu_profile.sh -> scripts/pmc_summary.py); null otherwise
+    mine = dict(app="w2v", minibatch=minibatch, dim=dim, dtype=args.dtype, mode=prec, world=world, tokens=tokens,
+                vocab=vocab, line_len=args.line_len, sharded=bool(sharded), sampler=args.sampler)
+    if bfp_main:
+        grp = ("k_gather_b", "k_combine_b", "k_push_b")
+    elif parity_main or args.dtype == "f64":
+        grp = ("k_gather", "k_combine") + (("k_push_thp", "k_push_tg") if (fused or fused_g) else ())
+    else:
+        grp = ("k_gather_t", "k_combine") + (("k_push_thp", "k_push_tg") if (fused or fused_g) else ())
+    tr, traffic_src = pmc_traffic(mine, {"sum": grp, "forward": ("k_forward_t", "k_forward_b", "k_forward_b8",
+                                                                  "k_forward")})
+    fwd_traffic = tr["forward"]
+    return {"bound": "hbm", "kernel": sum_kernel, "achieved": gat_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gat_gbs / HBM_PEAK_GBS, "traffic": tr["sum"], "traffic_source": traffic_src,
+            "bytes_per_launch": gat_bytes / max(gat_n, 1), "avg_launch_ms": sum_ms / max(gat_n, 1),
+            "launches": gat_n, "records_per_launch": g_rec / max(gat_n, 1),
+            "items_per_launch": g_items / max(gat_n, 1),
+            "partial_items_per_launch": (g_mitems if fused else g_items) / max(gat_n, 1),
+            "gather_ms_per_launch": gat_ms / max(gat_n, 1), "push_ms_per_launch": push_ms / max(push_n, 1),
+            # k_forward: its row-occurrence bytes count every context/target row read, most of them
+            # L2 / Infinity-Cache hits (hot Zipf rows), so they are no roofline quantity
+            # (row_bytes_GBps); its roofline fraction is the PMC-measured memory-side traffic of the
+            # same launches over their time
+            "forward": {"kernel": "k_forward_b" if bfp_main else "k_forward_t",
+                        "row_bytes_GBps": fwd_gbs, "row_bytes_per_launch": fwd_bytes / max(fwd_n, 1),
+                        "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n, "traffic": fwd_traffic,
+                        "hbm_GBps": (fwd_traffic / (fwd_ms / max(fwd_n, 1) * 1e-3) / 1e9
+                                     if fwd_traffic and fwd_ms > 0 else None),
+                        "frac": (fwd_traffic / (fwd_ms / max(fwd_n, 1) * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                 if fwd_traffic and fwd_ms > 0 else None)},
+            "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS, "pull_push": pp or None}
+
+
+def parallelism(ctx, args, frag_num):
+    if not ctx.sharded:
+        return "1 GPU, one HBM shard"
+    tr = ctx.transport()
+    via = (("library-issued RCCL" if tr[0] == "rccl" else "library TCP transport") if tr is not None and
+           args.driver == "native" else ("RCCL" if ctx.backend == "nccl" else "gloo"))
+    return ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num %d), %s all-to-all-v, %s"
+            % (ctx.world, frag_num, via, "pipelined: pull(i+1)/push(i) overlap learn(i), staleness 1"
+               if args.pipeline else "lockstep pull/learn/push"))
+
+
+def with_transport(out, ctx):
+    tr = ctx.transport()
+    if tr is not None:  # the library's own communicator: what its transport reports
+        out["transport"] = tr[0]
+        out["rccl_ranks" if tr[0] == "rccl" else "transport_ranks"] = tr[1]
+    return out
+
+
+def config4_leg(sw, ctx, args):
+    """BASELINE config 4 as weak scaling: each rank trains its own 1e9/8-token share (125M
+    tokens, Zipf over V = 1M, 1000-token lines, seed 4 + rank), D = 300, W = N = 5, minibatch
+    5000 lines, keys hash-sharded over the ranks with frag_num 8000 — at N = 8 the job is
+    config 4's whole 1e9-token corpus; at N = 1 the same per-rank workload on one HBM shard."""
+    set_phase("config4")
+    tokens, vocab = args.config4_tokens, 1000000
+    ids, off = make_corpus(tokens, vocab, args.line_len, seed=4 + ctx.rank)
+    import swiftmpi_amd as sw_
+    keys = word_keys(sw_, vocab)
+    setup_s = {}
+    r = w2v_leg(sw, ctx, args, ids, off, keys, args.precision, args.minibatch, 300, 8000, args.config4_steps, 3,
+                tokens, vocab, setup_s=setup_s)
+    del ids, off
+    dt, total = ctx.max_sum(r["dt"], r["d"]["words"])
+    roof = w2v_roofline(r, args, args.precision, args.minibatch, 300, tokens, vocab, ctx.world, ctx.sharded)
+    out = {"metric": "SGNS trained words/sec (BASELINE config 4: Zipf V=1M, D=300, 1e9 tokens over 8 GPUs)",
+           "value": total / dt, "unit": "words/s", "n_gpus": ctx.world, "steps": r["steps"], "warmup": r["warmup"],
+           "ms_per_step": dt * 1e3 / r["steps"], "higher_is_better": True, "scaling": "weak",
+           "config": {"workload": "word2vec CBOW-NS, per rank %d tokens (1e9/8: config 4's per-GPU share) of Zipf(s=1) "
+                                  "over V=%d, dim 300, window %d, negative %d, sample %g, minibatch %d lines of %d "
+                                  "tokens; %d tokens over all ranks"
+                                  % (tokens, vocab, args.window, args.negative, args.sample, args.minibatch,
+                                     args.line_len, tokens * ctx.world),
+                      "parallelism": parallelism(ctx, args, 8000), "mode": args.precision,
+                      "vocab_per_rank": r["info"]["vocab"], "batches_per_epoch": r["info"]["batches"],
+                      "kept_positions_per_s": r["d"]["kept"] * ctx.world / dt,
+                      "pulled_keys_per_step": r["d"]["pulled"] / r["steps"], "setup_s": setup_s},
+           "roofline": roof,
+           "exchange": exchange_block(r.get("xs"), r["steps"], r.get("dpt", 0.0), ctx.world,
+                                      "remote bytes (keys 8 B, rows 2*D*4 B, grads 2*D*8 B per remote key) / "
+                                      "all-to-all time (events on the exchange stream, profiled pass)")}
+    return with_transport(out, ctx)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,6 +642,9 @@ def main():
                     help="minibatches of the BASELINE config-1 leg (D = 100, minibatch 100) on the GPU; 0 = skip")
     ap.add_argument("--config1-cpu-lines", type=int, default=600,
                     help="lines per rank of the config-1 CPU leg (2 ranks in lockstep, oracle W2VMulti)")
+    ap.add_argument("--config4-tokens", type=int, default=125000000,
+                    help="tokens per rank of the config-4 leg (1e9 / 8: config 4's per-GPU share); 0 = skip the leg")
+    ap.add_argument("--config4-steps", type=int, default=10, help="timed minibatches of the config-4 leg")
     ap.add_argument("--sampler", default="table", choices=["table", "alias"],
                     help="negative sampler: the reference's unigram table (bit-exact draws) or an alias table")
     ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
@@ -307,281 +654,70 @@ def main():
                     help="LR: the reference's sequential fp32 per-key sums (bit-exact) instead of fast fp64 sums")
     ap.add_argument("--s2v-docs", type=int, default=8192, help="sent2vec documents per minibatch")
     ap.add_argument("--no-app-legs", action="store_true",
-                    help="skip the LR (config 3) and sent2vec (config 5) legs of the default line")
+                    help="skip the config-4, LR (config 3) and sent2vec (config 5) legs of the default line")
     ap.add_argument("--app-steps", type=int, default=20, help="timed LR minibatches of the default line's lr leg")
     args = ap.parse_args()
+    if args.parity:
+        args.precision = "parity"
+    arm_deadline(int(os.environ.get("RANK", "0")))
     if args.app != "w2v":
         return bench_other(args)
 
-    import torch
     import swiftmpi_amd as sw
+    set_phase("init")
+    ctx = Ctx(args.sharded)
+    rank, world = ctx.rank, ctx.world
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    ngpu = torch.cuda.device_count()
-    sharded = world > 1 or args.sharded
-    backend = None
-    if sharded:
-        import torch.distributed as dist
-        local = local % max(ngpu, 1)
-        torch.cuda.set_device(local)
-        if "MASTER_ADDR" not in os.environ:
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
-        if ngpu >= world:  # one GPU per rank: RCCL over xGMI
-            backend = "nccl"
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:               # functional check with ranks sharing a GPU
-            backend = "gloo"
-            dist.init_process_group("gloo")
-    else:
-        torch.cuda.set_device(local)
-
+    set_phase("headline")
     ids, off = make_corpus(args.tokens, args.vocab, args.line_len, seed=8 + rank)
     print("corpus: %d tokens" % len(ids), file=sys.stderr, flush=True)
     keys = word_keys(sw, args.vocab)
-
-    def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    setup_s = {}
-    _comm = []
-
-    def native_comm():  # one communicator per process, reused by every leg
-        if not _comm:
-            from swiftmpi_amd.comm import Comm
-            port = int(os.environ.get("MASTER_PORT", "29533")) + 1
-            addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-            try:
-                c = (Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
-                     else Comm.tcp(rank, world, local, addr=addr, port=port))
-                ok = 1
-            except Exception as e:  # noqa: BLE001 — reported, and every rank falls back together
-                print("native communicator failed on rank %d: %s" % (rank, e), file=sys.stderr, flush=True)
-                c, ok = None, 0
-            t = torch.tensor([ok], dtype=torch.int32, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            _comm.append(c if int(t.item()) else None)
-        return _comm[0]
-
-    def build(fp64_intermediates, minibatch=None, dim=None):
-        kw = dict(window=args.window, negative=args.negative, minibatch=minibatch or args.minibatch, sample=args.sample,
-                  alpha=args.alpha, profile=False, fp64_intermediates=fp64_intermediates, sampler=args.sampler)
-        t = sw.Table("w2v", dim=dim or args.dim, capacity=args.vocab, dtype=args.dtype, learning_rate=args.lr,
-                     device=local, init="hash", seed=1)
-        if sharded and args.driver == "native" and native_comm() is not None:  # the library's own exchange
-            from swiftmpi_amd.dist import NativeShardedWord2Vec
-            w = NativeShardedWord2Vec(t, native_comm(), frag_num=args.frag_num, **kw)
-        elif sharded:  # key-sharded over the ranks (BasicHashFrag), RCCL all-to-all per minibatch
-            from swiftmpi_amd.dist import ShardedWord2Vec
-            w = ShardedWord2Vec(t, frag_num=args.frag_num, pipeline=pipelined, **kw)
-        else:
-            w = sw.Word2Vec(t, init="ref", **kw)
-        t0 = time.perf_counter()
-        w.load_tokens(ids, off, keys)
-        t1 = time.perf_counter()
-        w.init()
-        setup_s.update(ingest=t1 - t0, first_pull=time.perf_counter() - t1)
-        return t, w
-
-    def timed(w, steps):
-        s0 = w.stats()
-        barrier()
-        t0 = time.perf_counter()
-        w.train_batches(steps)
-        w.sync()
-        barrier()
-        dt = time.perf_counter() - t0
-        s1 = w.stats()
-        return dt, {k: s1[k] - s0[k] for k in s1 if k not in ("lstate", "fstate")}
-
-    if args.parity:
-        args.precision = "parity"
     prec = args.precision
-    parity_main = prec == "parity"
-    bfp_main = prec.startswith("bfp") and args.dtype == "f32"
-    rb = 1 if prec == "bfp40" else 0  # BFP residual bytes per element
-    INTER = {"bfp40": "bfp40", "bfp32": "bfp32", "fast": False, "parity": True}
-    pipelined = sharded and args.pipeline
-    t, w = build(fp64_intermediates=INTER[prec])
-    info = w.info()
-    w.train_batches(args.warmup)
-    w.sync()
-    dt, d = timed(w, args.steps)           # the measured region: no event timing inside
-    words = d["words"]
-    w.set_profile(True)                     # a second, profiled pass for the per-kernel roofline
-    w.kernel_times(reset=True)
-    gw = getattr(w, "w", w)                 # the per-rank Word2Vec (sharded: its learner)
-    g0 = gw.sum_stats()
-    if sharded:
-        w.set_exchange_profile(True)
-    dpt, dp = timed(w, args.steps)
-    kt = w.kernel_times()
-    g1 = gw.sum_stats()
-    xs = w.exchange_stats() if sharded else None
-    w.set_profile(False)
-    if sharded:
-        w.set_exchange_profile(False)
-    del w, t
-    if dist is not None:
-        tt = torch.tensor([dt, float(words)], dtype=torch.float64, device="cuda")
-        mx = tt.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-        dt, total_words = float(mx[0]), float(tt[1])
-    else:
-        total_words = float(words)
-
-    D, es = args.dim, (8 if args.dtype == "f64" else 4)
-    ea = 8 if (parity_main or args.dtype == "f64") else 4   # neu1/neu1e element size
-    # BFP modes: a record reads its position's mantissas (4 B, + the int8 residual in bfp40) per
-    # element and the row scale (4 B); partials and the mean-gradient payload are fp64
-    rec_row = D * (4 + rb) + 4 if bfp_main else D * ea
-    pa = 8 if bfp_main else ea
-    kept = d["kept"]
-    # SURVEY.md §8(d) algorithmic bytes of k_forward: every context/target row
-    # occurrence read (4·D per row in fp32) + neu1, neu1e written (2·D·ea per position)
-    ctx_rows, tgt_rows = dp["ctx_rows"], dp["tgt_rows"]
-    fwd_ms, fwd_n = kt["forward"]
-    fwd_bytes = es * D * (ctx_rows + tgt_rows) + 2 * rec_row * dp["kept"]
-    fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
-    # the dominant kernel by time: the segmented gradient sums + AdaGrad push.
-    # Algorithmic bytes: each gradient record reads its source row (neu1 or neu1e of its
-    # position, D·ea) and its 4-B record index; each item (chunk of <= 128 records of one
-    # key) that goes through a partial writes it (D·ea + a 16-B descriptor read) and the
-    # push reads it back (D·ea); each pushed key reads h,v,h2,v2 (4·D·es), writes them
-    # (4·D·es) and its pre-update h,v to the worker cache (2·D·es) + 8 B of bounds.
-    # Fused push (k_push_thp, the fast-mode default): k_gather_t + k_combine sum only the
-    # multi-chunk runs, k_push_thp sums the single-chunk runs itself -> the group is
-    # k_gather_t + k_combine + k_push_thp, timed by the gather and push timers.
-    # Otherwise the group is k_gather_t + k_combine alone (the push is reported below).
-    g_rec, g_items = g1["records"] - g0["records"], g1["items"] - g0["items"]
-    g_mrec, g_mitems = g1["multi_records"] - g0["multi_records"], g1["multi_items"] - g0["multi_items"]
-    nbat = g1["batches"] - g0["batches"]
-    fused = nbat > 0 and g1["fused"] - g0["fused"] == nbat
-    fused_g = nbat > 0 and g1.get("fused_grads", 0) - g0.get("fused_grads", 0) == nbat
-    # small batches run the multi-chunk gather on a side stream beside the push: the push timer
-    # (push start .. the multi-chunk halves' push end) then spans the whole group
-    split = nbat > 0 and g1.get("split", 0) - g0.get("split", 0) == nbat
-    gat_ms, gat_n = kt["gather"]
-    push_ms, push_n = kt.get("push", (0.0, 0))
-    kn = ("k_gather_b", "k_combine_b", "k_push_b") if bfp_main else ("k_gather_t", "k_combine", "k_push_thp")
-    if fused_g:  # sharded learner: the fused push stops at the mean gradients (2·D·pa written per key)
-        sum_kernel = ("%s + %s + %s<TO_GRADS> (segmented gradient sums + fused mean "
-                      "gradients of the push payload)" % kn)
-        gat_bytes = g_rec * (rec_row + 4) + g_mitems * (2 * D * pa + 16) + dp["pushed"] * (2 * D * pa + 8)
-        sum_ms = push_ms if split else gat_ms + push_ms
-    elif fused:
-        sum_kernel = "%s + %s + %s (segmented gradient sums + fused AdaGrad push)" % kn
-        gat_bytes = (g_rec * (rec_row + 4) + g_mitems * (2 * D * pa + 16) +
-                     dp["pushed"] * (10 * es * D + 8))
-        sum_ms = push_ms if split else gat_ms + push_ms
-    else:
-        sum_kernel = ("k_gather + k_combine" if (parity_main or args.dtype == "f64") else "k_gather_t + k_combine") + \
-            " (segmented gradient sums)"
-        gat_bytes = g_rec * (D * ea + 4) + g_items * (D * ea + 16)
-        sum_ms = gat_ms
-    gat_gbs = gat_bytes / (sum_ms * 1e-3) / 1e9 if sum_ms > 0 else 0.0
-    # whole step (§8(d) full formula): rows read + gradients written + pull 16D/key + push (40D+8)/key
-    step_bytes = (2 * es * D * (dp["ctx_rows"] + dp["tgt_rows"]) + d["pulled"] * 4 * es * D +
-                  d["pushed"] * (10 * es * D + 8))
-    step_gbs = step_bytes / dt / 1e9
-    # the metric's "sparse push/pull HBM GB/s".  Single GPU: the pull is no
-    # kernel of its own — the forward reads the batch's keys straight from the
-    # table rows (counted in roofline.forward) and the push leaves their
-    # pre-update h, v in the worker cache.  Push (§8(d) + that cache write):
-    # mean grads 2·D, read h,v,h2,v2 4·D, write 4·D, cache h,v 2·D elements
-    # + the count per key, over the push kernel's event time in the profiled
-    # pass (sharded mode: the owner-side install / serve kernels are not in
-    # these timers, so the fields are omitted)
-    pp = {}
-    for name, nbytes in (("pull", dp["pulled"] * 4 * es * D), ("push", dp["pushed"] * (12 * es * D + 8))):
-        ms, n = kt.get(name, (0.0, 0))
-        if ms > 0 and not sharded and not ((fused or fused_g) and name == "push"):
-            gbs = nbytes / (ms * 1e-3) / 1e9
-            pp[name] = {"GBps": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": nbytes / max(n, 1),
-                        "avg_launch_ms": ms / max(n, 1)}
-    if not sharded and "pull" not in pp:
-        pp["pull"] = "fused: k_forward reads the pulled keys' table rows directly; k_push writes their cache rows"
-    # xGMI: bytes this rank's all-to-alls sent to other ranks per step, over the
-    # exchanges' event time on their stream, against 7 links x 153 GB/s
-    exchange = None
-    if xs is not None:
-        xg = xs["bytes_remote"] / (xs["ms"] * 1e-3) / 1e9 if xs["ms"] > 0 else 0.0
-        exchange = {"bytes_remote_per_step": xs["bytes_remote"] / args.steps,
-                    "bytes_total_per_step": xs["bytes_total"] / args.steps,
-                    "a2a_per_step": xs["calls"] / args.steps, "ms_per_step": xs["ms"] / args.steps,
-                    "share_of_step": xs["ms"] / (dpt * 1e3) if dpt > 0 else None,
-                    "GBps": xg, "peak": XGMI_PEAK_GBS, "frac": xg / XGMI_PEAK_GBS,
-                    "note": "remote bytes (keys 8 B, rows and grads %d B per remote key) / all-to-all time "
-                            "(events on the exchange stream, profiled pass); world %d" % (2 * D * es, world)}
-    # HBM traffic of the same kernel from the committed PMC passes of this exact
-    # command (scripts/gpu_profile.sh -> scripts/pmc_summary.py); null otherwise
-    # (per-launch bytes do not depend on --steps / --warmup: only the workload
-    # keys must match)
-    mine = dict(app="w2v", minibatch=args.minibatch, dim=args.dim, dtype=args.dtype, mode=prec, world=world,
-                tokens=args.tokens, vocab=args.vocab, line_len=args.line_len, sharded=bool(sharded),
-                sampler=args.sampler)
-    if bfp_main:
-        grp = ("k_gather_b", "k_combine_b", "k_push_b")
-    elif parity_main or args.dtype == "f64":
-        grp = ("k_gather", "k_combine") + (("k_push_thp", "k_push_tg") if (fused or fused_g) else ())
-    else:
-        grp = ("k_gather_t", "k_combine") + (("k_push_thp", "k_push_tg") if (fused or fused_g) else ())
-    tr, traffic_src = pmc_traffic(mine, {"sum": grp, "forward": ("k_forward_t", "k_forward_b", "k_forward_b8",
-                                                                  "k_forward")})
-    traffic, fwd_traffic = tr["sum"], tr["forward"]
+    setup_s = {}
+    r = w2v_leg(sw, ctx, args, ids, off, keys, prec, args.minibatch, args.dim, args.frag_num, args.steps,
+                args.warmup, args.tokens, args.vocab, setup_s=setup_s)
+    dt, total_words = ctx.max_sum(r["dt"], r["d"]["words"])
+    roof = w2v_roofline(r, args, prec, args.minibatch, args.dim, args.tokens, args.vocab, world, ctx.sharded)
+    d, info = r["d"], r["info"]
+    one = rank == 0 and world == 1 and not ctx.sharded
 
     # the other precision modes on the same workload, timed the same way
-    MODE_DESC = {"parity": "fp64 neu1/neu1e + gradient partials (reference-parity mode)",
-                 "bfp40": "block-fp neu1/neu1e, int32 + int8 mantissas per row exponent, fp64 sums (5 B/element)",
-                 "bfp32": "block-fp neu1/neu1e, int32 mantissas per row exponent, fp64 sums (4 B/element)",
-                 "fast": "fp32 neu1/neu1e + partials (fast mode: outside the 1e-5 single-batch bar)"}
     other_modes = {}
-    if rank == 0 and world == 1 and not args.no_parity_leg and args.dtype == "f32":
+    if one and not args.no_parity_leg and args.dtype == "f32":
+        set_phase("other_modes")
         for m in ("parity", "bfp40", "bfp32", "fast"):
-            if m == prec:
-                continue
-            t2, w2 = build(fp64_intermediates=INTER[m])
-            w2.train_batches(args.warmup)
-            w2.sync()
-            pdt, pd = timed(w2, args.steps)
-            other_modes[m] = {"value": pd["words"] / pdt, "ms_per_step": pdt * 1e3 / args.steps,
-                              "mode": MODE_DESC[m]}
-            del w2, t2
-    # SURVEY.md §8(d) config 1's minibatch (B = 100 lines of the same
-    # 1000-token lines), same mode as the headline, timed the same way over
-    # --b100-steps minibatches (the driver-visible small-batch number)
+            if m != prec:
+                q = w2v_leg(sw, ctx, args, ids, off, keys, m, args.minibatch, args.dim, args.frag_num, args.steps,
+                            args.warmup, args.tokens, args.vocab, profile=False)
+                other_modes[m] = {"value": q["d"]["words"] / q["dt"], "ms_per_step": q["dt"] * 1e3 / args.steps,
+                                  "mode": MODE_DESC[m]}
+    # SURVEY.md §8(d) config 1's minibatch (B = 100 lines of the same 1000-token lines), same mode as
+    # the headline, timed the same way over --b100-steps minibatches (the small-batch number)
     b100_leg = None
-    if rank == 0 and world == 1 and not sharded and args.b100_steps > 0 and args.minibatch != 100:
-        t3, w3 = build(fp64_intermediates=INTER[prec], minibatch=100)
-        w3.train_batches(10)
-        w3.sync()
-        bdt, bd = timed(w3, args.b100_steps)
-        b100_leg = {"value": bd["words"] / bdt, "unit": "words/s", "minibatch": 100, "steps": args.b100_steps,
-                    "warmup": 10, "ms_per_step": bdt * 1e3 / args.b100_steps,
-                    "kept_positions_per_s": bd["kept"] / bdt, "pulled_keys_per_step": bd["pulled"] / args.b100_steps}
-        del w3, t3
-
-    # BASELINE config 1 (D = 100, minibatch 100 lines) on this GPU, same mode, beside its CPU
-    # run (2 ranks in lockstep, cpu_baseline_config1)
+    if one and args.b100_steps > 0 and args.minibatch != 100:
+        set_phase("minibatch_100")
+        q = w2v_leg(sw, ctx, args, ids, off, keys, prec, 100, args.dim, args.frag_num, args.b100_steps, 10,
+                    args.tokens, args.vocab, profile=False)
+        b100_leg = {"value": q["d"]["words"] / q["dt"], "unit": "words/s", "minibatch": 100,
+                    "steps": args.b100_steps, "warmup": 10, "ms_per_step": q["dt"] * 1e3 / args.b100_steps,
+                    "kept_positions_per_s": q["d"]["kept"] / q["dt"],
+                    "pulled_keys_per_step": q["d"]["pulled"] / args.b100_steps}
+    # BASELINE config 1 (D = 100, minibatch 100 lines) on this GPU, same mode, beside its CPU run
+    # (2 ranks in lockstep, cpu_baseline_config1)
     config1 = None
-    if rank == 0 and world == 1 and not sharded and args.config1_steps > 0:
-        t4, w4 = build(fp64_intermediates=INTER[prec], minibatch=100, dim=100)
-        w4.train_batches(10)
-        w4.sync()
-        cdt, cd = timed(w4, args.config1_steps)
-        config1 = {"gpu": {"value": cd["words"] / cdt, "unit": "words/s", "n_gpus": 1, "dim": 100, "minibatch": 100,
-                           "steps": args.config1_steps, "ms_per_step": cdt * 1e3 / args.config1_steps},
+    if one and args.config1_steps > 0:
+        set_phase("config1")
+        q = w2v_leg(sw, ctx, args, ids, off, keys, prec, 100, 100, args.frag_num, args.config1_steps, 10,
+                    args.tokens, args.vocab, profile=False)
+        config1 = {"gpu": {"value": q["d"]["words"] / q["dt"], "unit": "words/s", "n_gpus": 1, "dim": 100,
+                           "minibatch": 100, "steps": args.config1_steps,
+                           "ms_per_step": q["dt"] * 1e3 / args.config1_steps},
                    "note": "BASELINE config 1 (D=100, window 5, negative 5, minibatch 100): the GPU on one rank's "
                            "corpus; the reference's 2-rank CPU plumbing as cpu_2rank"}
-        del w4, t4
         if not args.no_cpu_baseline:
             config1["cpu_2rank"] = cpu_baseline_config1(ids, off, args, args.config1_cpu_lines)
 
+    D = args.dim
     out = {
         "metric": "SGNS trained words/sec at 1/8 GPUs; sparse push/pull HBM GB/s vs peak",
         "value": total_words / dt,
@@ -607,133 +743,63 @@ def main():
                            (", alias sampler" if args.sampler == "alias" else ""),
                    "workload": "word2vec CBOW-NS (the reference's 'SGNS' app) text8-shaped corpus %d tokens, "
                                "vocab %d, dim %d, window %d, negative %d, sample %g, minibatch %d lines of %d "
-                               "tokens, table in one HBM shard" % (args.tokens, info["vocab"], D, args.window,
-                                                                  args.negative, args.sample, args.minibatch,
-                                                                  args.line_len),
+                               "tokens, %s" % (args.tokens, info["vocab"], D, args.window, args.negative, args.sample,
+                                               args.minibatch, args.line_len,
+                                               "table in one HBM shard" if not ctx.sharded else
+                                               "per rank (weak scaling: each rank its own corpus)"),
                    "global_batch": args.minibatch * world,
-                   "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num %d), %s all-to-all-v, %s"
-                                   % (world, args.frag_num,
-                                      ("library-issued RCCL" if backend == "nccl" else "library TCP transport")
-                                      if args.driver == "native" and _comm and _comm[0] is not None
-                                      else ("RCCL" if backend == "nccl" else "gloo"),
-                                      "pipelined: pull(i+1)/push(i) overlap learn(i), staleness 1" if pipelined
-                                      else "lockstep pull/learn/push"))
-                   if sharded else "1 GPU, one HBM shard",
-                   "kept_positions_per_s": kept * world / dt, "batches_per_epoch": info["batches"],
+                   "parallelism": parallelism(ctx, args, args.frag_num),
+                   "kept_positions_per_s": d["kept"] * world / dt, "batches_per_epoch": info["batches"],
                    "pulled_keys_per_step": d["pulled"] / args.steps,
                    "setup_s": dict(setup_s)},
-        "roofline": {"bound": "hbm", "kernel": sum_kernel,
-                     "achieved": gat_gbs, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": gat_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "bytes_per_launch": gat_bytes / max(gat_n, 1), "avg_launch_ms": sum_ms / max(gat_n, 1),
-                     "launches": gat_n, "records_per_launch": g_rec / max(gat_n, 1),
-                     "items_per_launch": g_items / max(gat_n, 1),
-                     "partial_items_per_launch": (g_mitems if fused else g_items) / max(gat_n, 1),
-                     "gather_ms_per_launch": gat_ms / max(gat_n, 1),
-                     "push_ms_per_launch": push_ms / max(push_n, 1),
-                     # k_forward: its row-occurrence bytes count every context/target row read,
-                     # most of them L2 / Infinity-Cache hits (hot Zipf rows), so they are no
-                     # roofline quantity (row_bytes_GBps); its roofline fraction is the
-                     # PMC-measured memory-side traffic of the same launches over their time
-                     "forward": {"kernel": "k_forward_b" if bfp_main else "k_forward_t",
-                                 "row_bytes_GBps": fwd_gbs, "row_bytes_per_launch": fwd_bytes / max(fwd_n, 1),
-                                 "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n,
-                                 "traffic": fwd_traffic,
-                                 "hbm_GBps": (fwd_traffic / (fwd_ms / max(fwd_n, 1) * 1e-3) / 1e9
-                                              if fwd_traffic and fwd_ms > 0 else None),
-                                 "frac": (fwd_traffic / (fwd_ms / max(fwd_n, 1) * 1e-3) / 1e9 / HBM_PEAK_GBS
-                                          if fwd_traffic and fwd_ms > 0 else None)},
-                     "step_GBps": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
-                     "pull_push": pp or None},
-        "kernel_ms": {k: v[0] for k, v in kt.items()},
+        "roofline": roof,
+        "kernel_ms": {k: v[0] for k, v in r["kt"].items()},
         "other_modes": other_modes or None,
         "minibatch_100": b100_leg,
         "config1": config1,
-        "exchange": exchange,
+        "exchange": exchange_block(r.get("xs"), args.steps, r.get("dpt", 0.0), world,
+                                   "remote bytes (keys 8 B, rows and grads %d B per remote key) / all-to-all time "
+                                   "(events on the exchange stream, profiled pass); world %d"
+                                   % (2 * D * (8 if args.dtype == "f64" else 4), world)),
     }
-    if _comm and _comm[0] is not None:  # the library's own communicator: what its transport reports
-        kind, nranks = _comm[0].transport()
-        out["transport"] = kind
-        out["rccl_ranks" if kind == "rccl" else "transport_ranks"] = nranks
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    with_transport(out, ctx)
+    if one and not args.no_cpu_baseline:
+        set_phase("cpu_baseline")
         out["cpu_baseline"] = cpu_baseline(ids, off, keys, args, args.cpu_lines)
-    # BASELINE configs 3 and 5 at their per-GPU shapes beside the headline (each with its own
-    # roofline and CPU baseline): the driver's default line carries every app of the hot path
-    if rank == 0 and world == 1 and not sharded and not args.no_app_legs:
-        del ids, off
-        one = (0, 1, local, None, None)
+    del ids, off
+    # BASELINE configs 4, 3 and 5 at their per-GPU shapes beside the headline, at every N (each
+    # rank its own share: weak scaling; the same legs at N = 1 give each curve its base point),
+    # each with its own roofline, exchange block and (N = 1) CPU baseline
+    if not args.no_app_legs:
+        if args.config4_tokens > 0:
+            out["config4"] = config4_leg(sw, ctx, args)
         la = argparse.Namespace(**vars(args))
         la.steps, la.warmup = args.app_steps, 3
-        out["lr"] = bench_lr(la, one, corpus_batches=10, cpu_rows=10 * (args.lr_batch + 1))
+        set_phase("lr")
+        out["lr"] = bench_lr(la, ctx, corpus_batches=10, cpu_rows=10 * (args.lr_batch + 1))
         sa = argparse.Namespace(**vars(args))
         sa.steps, sa.warmup = 31, 31  # one launch of 31 minibatches (swps_s2v group_docs) per pass
-        out["s2v"] = bench_s2v(sa, one, corpus_batches=31)
+        set_phase("s2v")
+        out["s2v"] = bench_s2v(sa, ctx, corpus_batches=31)
+    set_phase("report")
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
-
-
-def _dist_init(args):
-    import torch
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
-    dist, backend = None, None
-    if world > 1 or args.sharded:
-        import torch.distributed as dist
-        if "MASTER_ADDR" not in os.environ:
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
-        if torch.cuda.device_count() >= world:
-            backend = "nccl"
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            backend = "gloo"
-            dist.init_process_group("gloo")
-    return rank, world, local, dist, backend
+    if ctx.dist is not None:
+        ctx.dist.destroy_process_group()
 
 
 def bench_other(args):
     """Config 3 (sparse LR, Criteo shape, key-sharded over the GPUs) and
     config 5 (sent2vec, doc-sharded, word table replicated) — one JSON line
     each, same timing contract as the headline."""
-    ctx = _dist_init(args)
-    rank, dist = ctx[0], ctx[3]
+    set_phase("init")
+    ctx = Ctx(args.sharded)
+    set_phase(args.app)
     out = bench_lr(args, ctx) if args.app == "lr" else bench_s2v(args, ctx)
-    if rank == 0:
+    if ctx.rank == 0:
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
-
-
-def _other_helpers(ctx):
-    import torch
-    dist = ctx[3]
-
-    def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    def finish(dt, units):
-        if dist is not None:
-            tt = torch.tensor([dt, float(units)], dtype=torch.float64, device="cuda")
-            mx = tt.clone()
-            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-            return float(mx[0]), float(tt[1])
-        return dt, float(units)
-
-    def run_timed(run, sync, n):
-        barrier()
-        t0 = time.perf_counter()
-        run(n)
-        sync()
-        barrier()
-        return time.perf_counter() - t0
-    return finish, run_timed
+    if ctx.dist is not None:
+        ctx.dist.destroy_process_group()
 
 
 def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
@@ -743,60 +809,70 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
     fewer wrap around, like further epochs)."""
     import swiftmpi_amd as sw
     from swiftmpi_amd.synth import criteo
-    rank, world, local, dist, backend = ctx
-    finish, run_timed = _other_helpers(ctx)
+    rank, world, local, dist = ctx.rank, ctx.world, ctx.local, ctx.dist
     steps, warm = args.steps, args.warmup
     B1 = args.lr_batch + 1
     nb = corpus_batches or (2 * steps + warm)
     y, off, f, v = criteo(B1 * nb, seed=3 + rank)
     lr_rate = args.lr if args.lr != 0.7 else 0.05
     t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=lr_rate, init="hash", seed=1, device=local)
-    comm = None
-    if dist is not None and args.driver == "native":  # the library issues the exchange
-        from swiftmpi_amd.comm import Comm
-        import torch
-        port = int(os.environ.get("MASTER_PORT", "29533")) + 1
-        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-        try:
-            comm = (Comm.rccl(rank, world, local, addr=addr, port=port) if backend == "nccl"
-                    else Comm.tcp(rank, world, local, addr=addr, port=port))
-        except Exception as e:  # noqa: BLE001 — every rank falls back to the Python driver together
-            print("native communicator failed on rank %d: %s" % (rank, e), file=sys.stderr, flush=True)
-        ok = torch.tensor([int(comm is not None)], dtype=torch.int32, device="cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if not int(ok.item()):
-            comm = None
+    comm = ctx.comm() if dist is not None and args.driver == "native" else None  # the library issues the exchange
+    # end to end: load (the CSR rows to the GPU, the per-batch key-sorted index, the first full
+    # pull) and the first epoch over the nb minibatches, to its last push (lr.cpp:157-238 rebuilds
+    # that index per minibatch; here it is built once at load)
+    ctx.barrier()
+    t0 = time.perf_counter()
     if comm is not None:
         m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
         m.load_csr(y, off, f, v)
         m.shard_comm(comm, frag_num=2000)
+        t1 = time.perf_counter()
         m.init()
         run = m.train_batches
     elif dist is not None:
         from swiftmpi_amd.dist import ShardedLR
         m = ShardedLR(t, frag_num=2000, minibatch=args.lr_batch, profile=False, fast_sums=not args.lr_exact)
         m.load_csr(y, off, f, v)
+        t1 = time.perf_counter()
         m.init()
         run = m.train_steps
     else:
         m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
         m.load_csr(y, off, f, v)
+        t1 = time.perf_counter()
         m.init()
         run = m.train_batches
+    m.sync()
+    t2 = time.perf_counter()
+    run(nb)                                # the first epoch
+    m.sync()
+    ctx.barrier()
+    e2e = time.perf_counter() - t0
+    setup_s = {"load": t1 - t0, "first_pull": t2 - t1, "first_epoch": time.perf_counter() - t2}
     run(warm)
     m.sync()
-    dt = run_timed(run, m.sync, steps)     # the measured region: no event timing inside
+
+    def run_timed(n):
+        ctx.barrier()
+        a = time.perf_counter()
+        run(n)
+        m.sync()
+        ctx.barrier()
+        return time.perf_counter() - a
+
+    dt = run_timed(steps)                  # the measured region: no event timing inside
     m.set_profile(True)                    # a second, profiled pass for the per-kernel roofline
     m.kernel_times(reset=True)
-    run_timed(run, m.sync, steps)
+    if comm is not None:
+        m.exchange_stats(on=1)
+    dpt = run_timed(steps)
     kt = m.kernel_times()
+    xs = m.exchange_stats(on=0) if comm is not None else None
     m.set_profile(False)
-    xport = comm.transport() if comm is not None else None
     m.close()
     t.close()
-    if comm is not None:
-        comm.close()
-    dt, total = finish(dt, steps * B1)
+    e2e, e2e_rows = ctx.max_sum(e2e, nb * B1)
+    dt, total = ctx.max_sum(dt, steps * B1)
     # SURVEY.md §8(d) LR bytes, over the profiled pass's batches (warm + steps + k) mod nb:
     # k_lr_forward: per feature its shard row index, x_i and weight (4 B each); per example 20 B
     # (row offset, label, e, e^2).  Push (k_lr_records + k_lr_reduce_*, the push timer): per
@@ -851,20 +927,26 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
            "config": {"workload": "sparse logistic regression (BASELINE config 3 shape), 39 features/row, "
                                   "2^24 hashed feature space, %d rows per GPU per minibatch, AdaGrad lr %g, "
                                   "%d minibatches of data" % (B1, lr_rate, nb),
-                      "parallelism": ("key-sharded PS over %d GPU(s), %s all-to-all-v%s"
-                                      % (world, backend, ", library-issued" if comm is not None else ""))
+                      "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num 2000), %s all-to-all-v%s"
+                                      % (world, ctx.backend, ", library-issued" if comm is not None else ""))
                       if dist is not None else "1 GPU, one HBM shard",
                       "mode": "exact (sequential fp32 per-key sums, bit-exact with the reference)" if args.lr_exact
                       else "fast (fp64 per-key sums%s; within 1e-5 of the oracle)"
                       % (" through row tiles" if tiles else ", wave tree-reduced"),
                       "features_per_s": total * nnz / max(steps * B1, 1) / dt,
-                      "unique_keys_per_step": uniq / steps},
+                      "unique_keys_per_step": uniq / steps, "setup_s": setup_s,
+                      "end_to_end": {"value": e2e_rows / e2e, "unit": "examples/s", "s": e2e, "minibatches": nb,
+                                     "note": "load (CSR to the GPU, the per-batch key-sorted index built once for "
+                                             "the corpus, the first full pull) + the first epoch to its last push, "
+                                             "max over ranks; `value` is the steady state of later epochs"}},
            "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
                             step_GBps=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS, other=other),
-           "kernel_ms": {k: v[0] for k, v in kt.items() if v[1]}}
-    if xport is not None:
-        out["rccl_ranks" if xport[0] == "rccl" else "transport_ranks"] = xport[1]
-        out["transport"] = xport[0]
+           "kernel_ms": {k: v[0] for k, v in kt.items() if v[1]},
+           "exchange": exchange_block(xs, steps, dpt, world, "remote bytes (keys 8 B, weights 4 B, mean gradients 4 B "
+                                                             "per remote key) / all-to-all time (events on the "
+                                                             "exchange stream, profiled pass)")}
+    if comm is not None:
+        with_transport(out, ctx)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_lr(y, off, f, v, args.lr_batch, lr_rate,
                                               cpu_rows if cpu_rows is not None else args.cpu_rows)
@@ -878,8 +960,7 @@ def bench_s2v(args, ctx, corpus_batches=None):
     import torch
     import swiftmpi_amd as sw
     from swiftmpi_amd.synth import zipf_tokens
-    rank, world, local, dist, backend = ctx
-    finish, run_timed = _other_helpers(ctx)
+    rank, world, local = ctx.rank, ctx.world, ctx.local
     steps, warm = args.steps, args.warmup
     V, D = 1000000, args.dim
     # a minibatch is the next B + 1 documents (sent2vec.cpp on word2vec.h's MiniBatch); the
@@ -897,21 +978,41 @@ def bench_s2v(args, ctx, corpus_batches=None):
     del keys
     s2 = sw.Sent2Vec(t, window=args.window, negative=args.negative, minibatch=args.s2v_docs, niters=1,
                      alpha=args.alpha)
+    # end to end: sent2vec is one pass over its documents (sent2vec.cpp:95-103), so the load (docs
+    # to the GPU, per-minibatch vocabularies, unigram run starts and rand() streams fixed at load)
+    # is timed with the first pass over the corpus
+    ctx.barrier()
+    t0 = time.perf_counter()
     s2.load_tokens(toks, off, sent)  # each rank generated its own docs: doc-sharded by construction
+    s2.sync()
+    t1 = time.perf_counter()
     s2.train_batches(warm)
     s2.sync()
+    ctx.barrier()
+    e2e = time.perf_counter() - t0
     st0 = s2.stats()
-    dt = run_timed(s2.train_batches, s2.sync, steps)
+    setup_s = {"load": t1 - t0, "first_pass": e2e - (t1 - t0)}
+
+    def run_timed(n):
+        ctx.barrier()
+        a = time.perf_counter()
+        s2.train_batches(n)
+        s2.sync()
+        ctx.barrier()
+        return time.perf_counter() - a
+
+    dt = run_timed(steps)
     st1 = s2.stats()
     s2.set_profile(True)
     s2.kernel_times(reset=True)
-    run_timed(s2.train_batches, s2.sync, steps)
+    run_timed(steps)
     st2 = s2.stats()
     kt = s2.kernel_times()
     s2.set_profile(False)
     s2.close()
     t.close()
-    dt, total = finish(dt, st1["positions"] - st0["positions"])
+    e2e, e2e_words = ctx.max_sum(e2e, st0["positions"])
+    dt, total = ctx.max_sum(dt, st1["positions"] - st0["positions"])
     # SURVEY.md §8(d) sent2vec bytes of the docs kernel: 4*D per word row read (contexts + targets)
     # + 8*D per document (its row read and written)
     rows_read = (st2["ctx_rows"] - st1["ctx_rows"]) + (st2["tgt_rows"] - st1["tgt_rows"])
@@ -927,7 +1028,12 @@ def bench_s2v(args, ctx, corpus_batches=None):
            "config": {"workload": "sent2vec (BASELINE config 5 shape), D=%d, window %d, negative %d, %d docs "
                                   "per minibatch, word table 1M x %d, %d documents"
                                   % (D, args.window, args.negative, args.s2v_docs, D, nd),
-                      "parallelism": "doc-sharded over %d GPU(s), no exchange (replicas only)" % world},
+                      "parallelism": "doc-sharded over %d GPU(s), no exchange (replicas only)" % world,
+                      "setup_s": setup_s,
+                      "end_to_end": {"value": e2e_words / e2e, "unit": "words/s", "s": e2e,
+                                     "note": "load + the single pass over this leg's %d documents per rank (the "
+                                             "reference's sent2vec is one pass), max over ranks; `value` re-trains "
+                                             "the same documents (steady state)" % nd}},
            "roofline": {"bound": "hbm", "kernel": "k_s2v_docs", "achieved": doc_gbs, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": doc_gbs / HBM_PEAK_GBS, "traffic": tr["docs"],
                         "traffic_source": tsrc,
@@ -969,26 +1075,42 @@ def launch_ranks(n, argv):
     start N rank processes of this script — one per GPU, RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as torch.distributed.run would —
     and wait for them.  This process never touches the GPU (child processes,
-    no exec).  Rank 0 prints the JSON line; if any rank fails the others are
-    stopped and the first failing exit code is returned."""
+    no exec).  Rank 0 prints the JSON line.  If any rank fails, the others are
+    stopped (SIGTERM, then SIGKILL after 10 s) and the first failing exit code is
+    returned; past the overall deadline (SWPS_BENCH_DEADLINE_S + 60 s) every rank
+    is killed and 124 returned."""
     import subprocess
     port = _free_port_pair()
+    deadline = time.time() + float(os.environ.get("SWPS_BENCH_DEADLINE_S", "1500")) + 60
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
-    rc = 0
-    while procs:
-        for p in list(procs):
+    rc, stop_at = 0, None
+    live = list(procs)
+    while live:
+        for p in list(live):
             c = p.poll()
             if c is None:
                 continue
-            procs.remove(p)
+            live.remove(p)
             if c != 0 and rc == 0:
-                rc = c
-                for q in procs:  # the others would wait forever in a collective
+                rc = c if c > 0 else 128 - c  # a signal: 128 + its number, as a shell reports it
+                print("bench.py: rank %d exited with %d; stopping the other ranks" % (procs.index(p), c),
+                      file=sys.stderr, flush=True)
+                for q in live:  # the others would wait in a collective until their own deadlines
                     q.terminate()
+                stop_at = time.time() + 10
+        if live and ((stop_at and time.time() > stop_at) or time.time() > deadline):
+            if not stop_at:
+                print("bench.py: overall deadline exceeded; killing every rank", file=sys.stderr, flush=True)
+                rc = rc or 124
+            for q in live:
+                q.kill()
+            for q in live:
+                q.wait()
+            live = []
         time.sleep(0.2)
     return rc
 
@@ -1012,4 +1134,12 @@ if __name__ == "__main__":
     _rc = _launcher()
     if _rc is not None:
         sys.exit(_rc)
-    main()
+    try:
+        main()
+    except BaseException as _e:  # noqa: BLE001 — name the rank and phase, and do not hang in teardown
+        import traceback
+        traceback.print_exc()
+        print("bench.py: rank %s failed in phase %s: %s" % (os.environ.get("RANK", "0"), _PHASE["name"], _e),
+              file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(1)

@@ -200,6 +200,17 @@ int swps_comm_info(swps_comm *c, int32_t *rank, int32_t *world);
 #define SWPS_COMM_TCP 2
 #define SWPS_COMM_HOST 3
 int swps_comm_transport(swps_comm *c, int32_t *kind, int32_t *ranks);
+/* RCCL deadline (no reference counterpart: its ZeroMQ requests block forever, transfer.h:86-241).
+ * An RCCL communicator is non-blocking and guarded: its initialisation and every exchange must
+ * retire within `seconds` (default 120, env SWPS_COMM_TIMEOUT_S); otherwise — or on an RCCL
+ * asynchronous error — the library aborts the communicator (ncclCommAbort: a rank waiting on a
+ * lost peer stops waiting), prints "swps: rank R of N: <exchange> ..." to stderr, and every later
+ * call on it (and on tables / app contexts routed over it) fails with SWPS_E_RCCL and that
+ * message.  swps_comm_check reports that state; swps_comm_abort aborts on the caller's behalf (a
+ * launcher that saw a sibling rank die).  The TCP transport's deadline is its timeout_ms. */
+int swps_comm_set_timeout(swps_comm *c, double seconds);
+int swps_comm_check(swps_comm *c);
+int swps_comm_abort(swps_comm *c, const char *why);
 
 /* ---- key-sharded table (the GPU-to-shard map, src/cluster) --------------
  * swps_table_route binds a local shard to a communicator: this table then
@@ -510,6 +521,8 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
  * swps_lr_train / train_batches and swps_lr_predict (a full pull first)
  * become collective; swps_lr_train's errors are this rank's rows'. */
 int swps_lr_shard_comm(swps_lr *l, swps_comm *comm, int32_t frag_num);
+/* as swps_w2v_exchange_stats, for the library-driven sharded LR */
+int swps_lr_exchange_stats(swps_lr *l, int32_t on, double *out4);
 
 #ifdef __cplusplus
 }

@@ -93,6 +93,8 @@ def lib():
         L.orc_lr_num_keys.argtypes = [_p]
         L.orc_lr_params.argtypes = [_p, _p, _p, _p]
         L.orc_lr_predict.argtypes = [_p, _p, _p]
+        L.orc_lr_load.argtypes = [_p, _p, _p, ctypes.c_uint64]
+        L.orc_lr_predict_mode.argtypes = [_p, _p]
         L.orc_lr_pull_order.restype = _u64
         L.orc_lr_pull_order.argtypes = [_p, _p, _u64]
         L.orc_s2v_create.restype = _p
@@ -303,6 +305,18 @@ class LR:
         t = np.zeros(n, dtype=np.float32)
         lib().orc_lr_predict(self.h, _ptr(p), _ptr(t))
         return p, t
+
+    def load(self, keys, vals):
+        """ClusterServer::load of an LR dump: assign, draw nothing (server.h:49-62)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        vals = np.ascontiguousarray(vals, dtype=np.float32)
+        lib().orc_lr_load(self.h, _ptr(keys), _ptr(vals), len(keys))
+
+    def predict_mode(self):
+        """lr.cpp:240-295: per-minibatch pulls (misses drawn in key-set order), then predictions."""
+        p = np.zeros(int(lib().orc_lr_num_instances(self.h)), dtype=np.float32)
+        lib().orc_lr_predict_mode(self.h, _ptr(p))
+        return p
 
     def pull_order(self):
         cap = 1 << 26

@@ -1137,6 +1137,46 @@ void orc_lr_predict(void *h, float *pred, float *target) {
   }
 }
 
+// ClusterServer::load (server.h:49-62) of an LR dump (LRParam operator>>, lr.cpp:28-31): the
+// dumped keys get their values, grad2sum 0, and nothing is drawn (init_param is not called)
+void orc_lr_load(void *h, const uint32_t *keys, const float *vals, uint64_t n) {
+  LR *m = (LR *)h;
+  for (uint64_t i = 0; i < n; i++) {
+    LRParam p;
+    p.val = vals[i];
+    m->server[keys[i]] = p;
+  }
+}
+
+// lr.cpp:240-295 predict mode (after load_param, no training): per minibatch the keys of the next
+// B+1 valid lines (gather_keys(file, minibatch), lr.cpp:308-351) are pulled — a key the server
+// lacks gets init_param's gen_float() draw, in the key set's iteration order (lr.cpp:45-50) — and
+// those lines are predicted from the pulled values (predict_instance, lr.cpp:376-385)
+void orc_lr_predict_mode(void *h, float *pred) {
+  LR *m = (LR *)h;
+  size_t li = 0;
+  while (li < m->ins.size()) {
+    std::unordered_set<uint32_t> K;
+    size_t end = std::min(m->ins.size(), li + (size_t)m->minibatch + 1);
+    for (size_t j = li; j < end; j++)
+      for (auto &f : m->ins[j].feas) K.insert(f.first);
+    m->cache.clear();
+    m->grads.clear();
+    for (auto k : K) m->cache[k] = 0;
+    m->pull(K);
+    for (size_t j = li; j < end; j++) {
+      float sum = 0;
+      for (auto &f : m->ins[j].feas) {
+        float w = m->cache[f.first];
+        float prod = w * f.second;
+        sum += prod;
+      }
+      pred[j] = 1. / (1. + std::exp(-sum));
+    }
+    li = end;
+  }
+}
+
 // order in which the first full pull visits keys (unordered_set iteration)
 uint64_t orc_lr_pull_order(void *h, uint32_t *out, uint64_t cap) {
   LR *m = (LR *)h;

@@ -122,11 +122,16 @@ class Table:
 
     def __init__(self, layout="w2v", dim=100, capacity=1 << 20, dtype="f32", learning_rate=0.7, fudge=1e-6,
                  init="hash", seed=0, device=0, push_rule="adagrad"):
-        cfg = capi.TableCfg(device, capi.LAYOUT_W2V if layout == "w2v" else capi.LAYOUT_LR,
-                            capi.F64 if dtype == "f64" else capi.F32, dim, capacity, learning_rate, fudge,
-                            {"hash": capi.INIT_HASH, "zero": capi.INIT_ZERO, "flcg": capi.INIT_FLCG}.get(init, capi.INIT_ZERO),
-                            seed,
-                            {"adagrad": capi.PUSH_ADAGRAD, "sgd": capi.PUSH_SGD}[push_rule])
+        inits = {"hash": capi.INIT_HASH, "zero": capi.INIT_ZERO, "flcg": capi.INIT_FLCG}
+        rules = {"adagrad": capi.PUSH_ADAGRAD, "sgd": capi.PUSH_SGD}
+        layouts = {"w2v": capi.LAYOUT_W2V, "lr": capi.LAYOUT_LR}
+        dtypes = {"f32": capi.F32, "f64": capi.F64}
+        for name, val, known in (("init", init, inits), ("push_rule", push_rule, rules), ("layout", layout, layouts),
+                                 ("dtype", dtype, dtypes)):
+            if val not in known:
+                raise ValueError("unknown %s %r (one of %s)" % (name, val, ", ".join(sorted(known))))
+        cfg = capi.TableCfg(device, layouts[layout], dtypes[dtype], dim, capacity, learning_rate, fudge,
+                            inits[init], seed, rules[push_rule])
         h = ctypes.c_void_p()
         check(capi.lib().swps_table_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -583,6 +588,12 @@ class LR:
         train_batches / predict become collective over `comm`."""
         check(capi.lib().swps_lr_shard_comm(self.h, comm.h, frag_num))
         self._comm = comm
+
+    def exchange_stats(self, on=-1):
+        """As Word2Vec.exchange_stats (swps_lr_exchange_stats)."""
+        out = np.zeros(4)
+        check(capi.lib().swps_lr_exchange_stats(self.h, on, ptr(out)))
+        return dict(zip(["bytes_remote", "bytes_total", "calls", "ms"], out.tolist()))
 
     def close(self):
         if getattr(self, "h", None):

@@ -89,6 +89,9 @@ PROTOS = {
     "swps_comm_destroy": (ctypes.c_int, [_p]),
     "swps_comm_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "swps_comm_transport": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "swps_comm_set_timeout": (ctypes.c_int, [_p, ctypes.c_double]),
+    "swps_comm_check": (ctypes.c_int, [_p]),
+    "swps_comm_abort": (ctypes.c_int, [_p, ctypes.c_char_p]),
     "swps_table_route": (ctypes.c_int, [_p, _p, _i32]),
     "swps_finish": (ctypes.c_int, [_p]),
     "swps_barrier": (ctypes.c_int, [_p]),
@@ -142,6 +145,7 @@ PROTOS = {
     "swps_w2v_shard_comm": (ctypes.c_int, [_p, _p, _i32]),
     "swps_w2v_exchange_stats": (ctypes.c_int, [_p, _i32, _p]),
     "swps_lr_shard_comm": (ctypes.c_int, [_p, _p, _i32]),
+    "swps_lr_exchange_stats": (ctypes.c_int, [_p, _i32, _p]),
     "swps_unigram_starts": (ctypes.c_int, [_p, _p, _u64, _u64, _p]),
     "swps_glibc_rand": (ctypes.c_int, [ctypes.c_uint32, _u64, _u64, _p]),
     "swps_s2v_create": (ctypes.c_int, [_p, ctypes.POINTER(S2VCfg), ctypes.POINTER(_p)]),

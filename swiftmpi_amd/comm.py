@@ -83,6 +83,17 @@ class Comm:
         check(capi.lib().swps_comm_transport(self.h, ctypes.byref(k), ctypes.byref(n)))
         return {1: "rccl", 2: "tcp", 3: "host"}[k.value], n.value
 
+    def set_timeout(self, seconds):
+        """Deadline for the communicator's initialisation and each exchange (RCCL guard)."""
+        check(capi.lib().swps_comm_set_timeout(self.h, float(seconds)))
+
+    def check(self):
+        """Raise SwpsError if the RCCL guard aborted this communicator."""
+        check(capi.lib().swps_comm_check(self.h))
+
+    def abort(self, why="aborted by the caller"):
+        check(capi.lib().swps_comm_abort(self.h, why.encode()))
+
     def close(self):
         if getattr(self, "h", None):
             capi.lib().swps_comm_destroy(self.h)

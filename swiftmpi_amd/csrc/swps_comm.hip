@@ -26,8 +26,12 @@
 
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <thread>
 
 #include "swps_internal.h"
@@ -36,6 +40,32 @@
 using namespace swps;
 
 struct TcpStar;
+// RCCL deadline guard.  A peer that dies or stops inside a collective leaves this rank's RCCL
+// kernels spinning and its host blocked in a stream wait until some outer timeout kills the job.
+// The guard bounds that: every collective is followed by an event on its stream, and a watchdog
+// thread polls the oldest pending event and ncclCommGetAsyncError; when an exchange has not
+// retired within the deadline (SWPS_COMM_TIMEOUT_S, default 120 s, or swps_comm_set_timeout), or
+// RCCL reports an asynchronous error, it aborts the communicator (ncclCommAbort: the spinning
+// kernels exit, so the blocked stream waits return) and latches a message naming the rank and the
+// exchange; every later call on the communicator fails with SWPS_E_RCCL and that message.  The
+// communicator is non-blocking (ncclConfig_t.blocking = 0), so its initialisation is polled
+// against the same deadline instead of blocking in ncclCommInitRank.
+struct CommGuard {
+  struct Pending {
+    hipEvent_t ev;
+    const char *phase;
+    std::chrono::steady_clock::time_point t0;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Pending> pending;
+  std::vector<hipEvent_t> spare;
+  std::thread th;
+  bool stop = false;
+  std::atomic<bool> aborted{false};
+  std::string msg;  // set once, before `aborted`
+};
+
 struct swps_comm {
   int32_t rank = 0, world = 1, device = 0;
   bool rccl = false;
@@ -43,17 +73,128 @@ struct swps_comm {
   swps_transport tr{};
   TcpStar *tcp = nullptr;  // swps_comm_create_tcp's transport state (owned)
   DevMem d_hdr;  // RCCL header all-gather buffers
+  double timeout_s = 120.0;  // RCCL deadline per exchange (CommGuard)
+  std::unique_ptr<CommGuard> guard;  // RCCL, world > 1
 };
 
 namespace {
 
 enum { kOpPull = 0, kOpPush = 1, kOpFinish = 2 };
 
+// a non-blocking communicator may answer ncclInProgress: the call is queued (comm_settle waits)
 #define SWPS_NCCL(call)                                                                                   \
   do {                                                                                                    \
     ncclResult_t r_ = (call);                                                                             \
-    if (r_ != ncclSuccess) return ::swps::fail(SWPS_E_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    if (r_ != ncclSuccess && r_ != ncclInProgress)                                                        \
+      return ::swps::fail(SWPS_E_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_));              \
   } while (0)
+
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// abort the communicator once (watchdog or a host-side deadline) and latch the message
+void comm_abort(swps_comm *c, const std::string &why) {
+  CommGuard *g = c->guard.get();
+  if (!g) return;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->aborted.load()) return;
+    g->msg = "rank " + std::to_string(c->rank) + " of " + std::to_string(c->world) + ": " + why;
+    g->aborted.store(true);
+  }
+  fprintf(stderr, "swps: %s; aborting the RCCL communicator\n", g->msg.c_str());
+  fflush(stderr);
+  (void)ncclCommAbort(c->nc);  // frees the communicator: never destroyed again
+}
+
+int comm_aborted(swps_comm *c) {
+  if (c->guard && c->guard->aborted.load()) return fail(SWPS_E_RCCL, c->guard->msg);
+  return SWPS_OK;
+}
+
+// a non-blocking communicator's queued call: poll ncclCommGetAsyncError until it leaves
+// ncclInProgress, against the deadline
+int comm_settle(swps_comm *c, const char *phase) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    SWPS_TRY(comm_aborted(c));
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t r = ncclCommGetAsyncError(c->nc, &st);
+    if (r != ncclSuccess) return fail(SWPS_E_RCCL, std::string("ncclCommGetAsyncError: ") + ncclGetErrorString(r));
+    if (st == ncclSuccess) return SWPS_OK;
+    if (st != ncclInProgress) {
+      comm_abort(c, std::string(phase) + ": " + ncclGetErrorString(st));
+      return comm_aborted(c);
+    }
+    if (seconds_since(t0) > c->timeout_s) {
+      comm_abort(c, std::string(phase) + " still in progress after " + std::to_string((int)c->timeout_s) + " s");
+      return comm_aborted(c);
+    }
+    std::this_thread::yield();
+  }
+}
+
+// after a collective is queued on s: settle it, then hand its completion event to the watchdog
+int comm_track(swps_comm *c, hipStream_t s, const char *phase) {
+  SWPS_TRY(comm_settle(c, phase));
+  CommGuard *g = c->guard.get();
+  if (!g) return SWPS_OK;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->spare.empty()) {
+      ev = g->spare.back();
+      g->spare.pop_back();
+    }
+  }
+  if (!ev) SWPS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  SWPS_HIP(hipEventRecord(ev, s));
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->pending.push_back({ev, phase, std::chrono::steady_clock::now()});
+  }
+  g->cv.notify_one();
+  return SWPS_OK;
+}
+
+void watchdog(swps_comm *c) {
+  CommGuard *g = c->guard.get();
+  (void)hipSetDevice(c->device);
+  std::unique_lock<std::mutex> lk(g->mu);
+  while (!g->stop) {
+    g->cv.wait_for(lk, std::chrono::milliseconds(20));
+    if (g->stop || g->aborted.load()) continue;
+    std::string why;
+    while (!g->pending.empty()) {
+      CommGuard::Pending &p = g->pending.front();
+      const hipError_t q = hipEventQuery(p.ev);
+      if (q == hipSuccess) {
+        g->spare.push_back(p.ev);
+        g->pending.pop_front();
+        continue;
+      }
+      if (q != hipErrorNotReady) {
+        (void)hipGetLastError();
+        why = std::string(p.phase) + ": " + hipGetErrorString(q);
+      } else if (seconds_since(p.t0) > c->timeout_s) {
+        why = std::string(p.phase) + " did not complete within " + std::to_string((int)c->timeout_s) +
+              " s (a peer rank lost or stuck)";
+      }
+      break;
+    }
+    if (why.empty() && !g->pending.empty()) {
+      ncclResult_t st = ncclSuccess;
+      if (ncclCommGetAsyncError(c->nc, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+        why = std::string(g->pending.front().phase) + ": RCCL asynchronous error: " + ncclGetErrorString(st);
+    }
+    if (!why.empty()) {
+      lk.unlock();
+      comm_abort(c, why);
+      lk.lock();
+    }
+  }
+}
 
 inline unsigned nblocks(uint64_t threads, unsigned bs = 256) {
   return (unsigned)std::max<uint64_t>(1, (threads + bs - 1) / bs);
@@ -192,7 +333,8 @@ int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void 
     for (int r = 0; r < world; r++) b[r] = k[r] * w;
     return b;
   };
-  SWPS_TRY(comm_alltoallv(t->comm, keys_s, scaled(send_k, 8), t->r_rkeys.p, scaled(recv_k, 8), s, t->stage));
+  SWPS_TRY(comm_alltoallv(t->comm, keys_s, scaled(send_k, 8), t->r_rkeys.p, scaled(recv_k, 8), s, t->stage,
+                          "routed keys"));
   const size_t vb = agreed == kOpPull ? pb : gb;
   SWPS_TRY(t->r_rows.ensure(std::max<uint64_t>(nrecv, 1) * 4));
   SWPS_TRY(t->r_rbuf.ensure(std::max<uint64_t>(nrecv, 1) * vb));
@@ -204,7 +346,8 @@ int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void 
   if (agreed == kOpPush) {
     if (n) k_gather_rows<<<nblocks(n * 64), 256, 0, s>>>(perm, n, (const char *)d_io, t->r_buf.as<char>(), gb);
     SWPS_HIP(hipGetLastError());
-    SWPS_TRY(comm_alltoallv(t->comm, t->r_buf.p, scaled(send_k, gb), t->r_rbuf.p, scaled(recv_k, gb), s, t->stage));
+    SWPS_TRY(comm_alltoallv(t->comm, t->r_buf.p, scaled(send_k, gb), t->r_rbuf.p, scaled(recv_k, gb), s, t->stage,
+                            "routed push gradients"));
     t->rstats[3] += n * (8 + gb);
     t->rstats[4] += remote * (8 + gb);
     // ---- 4. owner: the push rule, one step per source in rank order ----
@@ -222,7 +365,8 @@ int route_round(swps_table *t, int op, const uint64_t *d_keys, uint64_t n, void 
     SWPS_TRY(table_copy_pull(t, t->r_rows.as<uint32_t>(), nrecv, t->r_rbuf.p, s));
   }
   // ---- 5. values back to the requesters, then to the caller's key order ----
-  SWPS_TRY(comm_alltoallv(t->comm, t->r_rbuf.p, scaled(recv_k, pb), t->r_buf.p, scaled(send_k, pb), s, t->stage));
+  SWPS_TRY(comm_alltoallv(t->comm, t->r_rbuf.p, scaled(recv_k, pb), t->r_buf.p, scaled(send_k, pb), s, t->stage,
+                          "routed pull values"));
   t->rstats[3] += n * 8 + nrecv * pb;
   t->rstats[4] += remote * 8;
   for (int r = 0; r < world; r++)
@@ -347,13 +491,15 @@ int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipS
     if (c->tr.allgather(c->tr.ctx, in, out, bytes) != 0) return fail(SWPS_E_RCCL, "host transport all-gather failed");
     return SWPS_OK;
   }
+  SWPS_TRY(comm_aborted(c));
   SWPS_TRY(c->d_hdr.ensure(bytes * (c->world + 1)));
   char *d = c->d_hdr.as<char>();
   SWPS_HIP(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, s));
   SWPS_NCCL(ncclAllGather(d, d + bytes, bytes, ncclChar, c->nc, s));
+  SWPS_TRY(comm_track(c, s, "header all-gather"));
   SWPS_HIP(hipMemcpyAsync(out, d + bytes, bytes * c->world, hipMemcpyDeviceToHost, s));
-  SWPS_HIP(hipStreamSynchronize(s));
-  return SWPS_OK;
+  SWPS_HIP(hipStreamSynchronize(s));  // returns once the guard aborts a stuck exchange
+  return comm_aborted(c);
 }
 
 template <typename V>
@@ -384,7 +530,7 @@ int scatter_rows(const void *src, const uint32_t *pos, uint64_t n, uint64_t row_
 // order), ordered on stream s: RCCL send/recv groups, or host staging
 // through `st` and the transport's callback (synchronous)
 int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
-                   const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg) {
+                   const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg, const char *phase) {
   uint64_t st = 0, rt = 0;
   for (int r = 0; r < c->world; r++) {
     st += sb[r];
@@ -395,6 +541,7 @@ int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t>
     return SWPS_OK;
   }
   if (c->rccl) {
+    SWPS_TRY(comm_aborted(c));
     SWPS_NCCL(ncclGroupStart());
     uint64_t so = 0, ro = 0;
     for (int r = 0; r < c->world; r++) {
@@ -404,7 +551,7 @@ int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t>
       ro += rb[r];
     }
     SWPS_NCCL(ncclGroupEnd());
-    return SWPS_OK;
+    return comm_track(c, s, phase);
   }
   stg.send.resize(std::max<uint64_t>(st, 1));
   stg.recv.resize(std::max<uint64_t>(rt, 1));
@@ -422,7 +569,7 @@ int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t>
 // peer's segment)
 int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb,
                         const std::vector<uint64_t> &so, void *d_recv, const std::vector<uint64_t> &rb,
-                        const std::vector<uint64_t> &ro, hipStream_t s, HostStage &stg) {
+                        const std::vector<uint64_t> &ro, hipStream_t s, HostStage &stg, const char *phase) {
   uint64_t st = 0, rt = 0;
   for (int r = 0; r < c->world; r++) {
     st += sb[r];
@@ -434,13 +581,14 @@ int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint
     return SWPS_OK;
   }
   if (c->rccl) {
+    SWPS_TRY(comm_aborted(c));
     SWPS_NCCL(ncclGroupStart());
     for (int r = 0; r < c->world; r++) {
       if (sb[r]) SWPS_NCCL(ncclSend((const char *)d_send + so[r], sb[r], ncclChar, r, c->nc, s));
       if (rb[r]) SWPS_NCCL(ncclRecv((char *)d_recv + ro[r], rb[r], ncclChar, r, c->nc, s));
     }
     SWPS_NCCL(ncclGroupEnd());
-    return SWPS_OK;
+    return comm_track(c, s, phase);
   }
   stg.send.resize(std::max<uint64_t>(st, 1));
   stg.recv.resize(std::max<uint64_t>(rt, 1));
@@ -463,6 +611,7 @@ int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint
   return SWPS_OK;
 }
 
+int comm_status(swps_comm *c) { return c ? comm_aborted(c) : SWPS_OK; }
 int comm_rank(const swps_comm *c) { return c->rank; }
 int comm_world(const swps_comm *c) { return c->world; }
 int comm_device(const swps_comm *c) { return c->device; }
@@ -560,15 +709,30 @@ int swps_comm_create_rccl(const uint8_t *id, int32_t rank, int32_t world, int32_
   SWPS_HIP(hipSetDevice(device));
   ncclUniqueId u;
   memcpy(u.internal, id, SWPS_COMM_ID_BYTES);
-  ncclComm_t nc;
-  SWPS_NCCL(ncclCommInitRank(&nc, world, u, rank));
-  swps_comm *c = new swps_comm();
+  std::unique_ptr<swps_comm> c(new swps_comm());
   c->rank = rank;
   c->world = world;
   c->device = device;
   c->rccl = true;
+  if (const char *e = getenv("SWPS_COMM_TIMEOUT_S")) c->timeout_s = std::max(1.0, atof(e));
+  // non-blocking: the initialisation is polled against the deadline (comm_settle), and so is every
+  // queued call after it (SWPS_RCCL_BLOCKING=1: a blocking communicator, no deadline on init)
+  const char *bl = getenv("SWPS_RCCL_BLOCKING");
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = (bl && atoi(bl)) ? 1 : 0;
+  ncclComm_t nc = nullptr;
+  const ncclResult_t r = ncclCommInitRankConfig(&nc, world, u, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (nc) (void)ncclCommAbort(nc);
+    return fail(SWPS_E_RCCL, std::string("rank ") + std::to_string(rank) + ": ncclCommInitRankConfig: " +
+                                 ncclGetErrorString(r));
+  }
   c->nc = nc;
-  *out = c;
+  c->guard.reset(new CommGuard());  // world 1 too: the init deadline and the same code path
+  const int rc = comm_settle(c.get(), "RCCL initialisation");
+  if (rc != SWPS_OK) return rc;  // aborted (and freed) by comm_abort
+  c->guard->th = std::thread(watchdog, c.get());
+  *out = c.release();
   return SWPS_OK;
 }
 
@@ -663,9 +827,44 @@ int swps_comm_create_tcp(const char *addr, int32_t port, int32_t rank, int32_t w
 int swps_comm_destroy(swps_comm *c) {
   if (!c) return SWPS_OK;
   (void)hipSetDevice(c->device);
-  if (c->nc) (void)ncclCommDestroy(c->nc);
+  if (CommGuard *g = c->guard.get()) {
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      g->stop = true;
+    }
+    g->cv.notify_all();
+    if (g->th.joinable()) g->th.join();
+  }
+  if (c->nc && !(c->guard && c->guard->aborted.load())) {
+    // non-blocking: finalize (flushes the queued exchanges), wait for quiescence, then free
+    const ncclResult_t r = ncclCommFinalize(c->nc);
+    if (r == ncclSuccess || r == ncclInProgress) (void)comm_settle(c, "RCCL finalize");
+    if (!c->guard->aborted.load()) (void)ncclCommDestroy(c->nc);
+  }
+  if (c->guard) {
+    for (auto &p : c->guard->pending) (void)hipEventDestroy(p.ev);
+    for (auto ev : c->guard->spare) (void)hipEventDestroy(ev);
+  }
   delete c->tcp;
   delete c;
+  return SWPS_OK;
+}
+
+int swps_comm_set_timeout(swps_comm *c, double seconds) {
+  if (!c || !(seconds > 0)) return fail(SWPS_E_CFG, "null communicator or non-positive timeout");
+  c->timeout_s = seconds;
+  return SWPS_OK;
+}
+
+int swps_comm_check(swps_comm *c) {
+  if (!c) return fail(SWPS_E_CFG, "null communicator");
+  return comm_aborted(c);
+}
+
+int swps_comm_abort(swps_comm *c, const char *why) {
+  if (!c) return fail(SWPS_E_CFG, "null communicator");
+  if (!c->guard) return SWPS_OK;
+  comm_abort(c, why ? why : "aborted by the caller");
   return SWPS_OK;
 }
 
@@ -679,6 +878,7 @@ int swps_comm_info(swps_comm *c, int32_t *rank, int32_t *world) {
 int swps_comm_transport(swps_comm *c, int32_t *kind, int32_t *ranks) {
   if (!c) return fail(SWPS_E_CFG, "null communicator");
   int32_t n = c->world;
+  SWPS_TRY(comm_aborted(c));
   if (c->nc) SWPS_NCCL(ncclCommCount(c->nc, &n));  // what RCCL itself reports for the communicator
   if (kind) *kind = c->rccl ? SWPS_COMM_RCCL : c->tcp ? SWPS_COMM_TCP : SWPS_COMM_HOST;
   if (ranks) *ranks = n;

@@ -142,7 +142,7 @@ int ShardDriver::split_prepare(uint64_t st) {
   SWPS_TRY(flags.ensure(std::max<uint64_t>(n, 1)));
   SWPS_TRY(myflags.ensure(std::max<uint64_t>(m, 1)));
   SWPS_TRY(ops.late_mask(ops.h, (int64_t)(3 * st), (int64_t)(3 * prev), flags.as<uint8_t>(), n));
-  SWPS_TRY(exchange(flags.p, rk, myflags.p, sk, 1, S));  // the owners' flags to their requesters
+  SWPS_TRY(exchange(flags.p, rk, myflags.p, sk, 1, S, "early/late pull flags"));  // the owners' flags to their requesters
   std::vector<uint8_t> hf(n), hm(m);
   std::vector<uint64_t> keys(n);
   if (n) SWPS_HIP(hipMemcpyAsync(hf.data(), flags.p, n, hipMemcpyDeviceToHost, S));
@@ -199,7 +199,7 @@ int ShardDriver::serve_early(uint64_t st) {
   const uint64_t vb = ops.width * ops.val_bytes;
   SWPS_TRY(ops.set_slot(ops.h, (int64_t)(3 * st + 1)));
   SWPS_TRY(ops.serve_pull(ops.h, e.ek.as<uint64_t>(), e.es.data(), 0, vals.p));
-  SWPS_TRY(exchange(vals.p, e.es.data(), evals[ebuf].p, e.ed.data(), vb, S));
+  SWPS_TRY(exchange(vals.p, e.es.data(), evals[ebuf].p, e.ed.data(), vb, S, "early pull values"));
   early_buf = ebuf;
   ebuf ^= 1;
   return SWPS_OK;
@@ -212,7 +212,7 @@ static std::vector<uint64_t> scaled(const uint64_t *k, int world, uint64_t w) {
 }
 
 int ShardDriver::exchange(const void *d_send, const uint64_t *sk, void *d_recv, const uint64_t *rk, uint64_t w,
-                          hipStream_t s) {
+                          hipStream_t s, const char *phase) {
   if (world == 1 && d_send == d_recv) {  // an aliased world-1 exchange: nothing moves
     if (xprof) {
       bytes_total += sk[0] * w;
@@ -228,10 +228,11 @@ int ShardDriver::exchange(const void *d_send, const uint64_t *sk, void *d_recv, 
     }
     calls++;
   }
-  SWPS_TRY(comm_alltoallv(c, d_send, scaled(sk, world, w), d_recv, scaled(rk, world, w), s, stage));
+  SWPS_TRY(comm_alltoallv(c, d_send, scaled(sk, world, w), d_recv, scaled(rk, world, w), s, stage, phase));
   if (xprof) {
     SWPS_HIP(hipEventRecord(ev_x1, s));
     SWPS_HIP(hipEventSynchronize(ev_x1));  // profiled runs only
+    SWPS_TRY(comm_status(c));
     float ms = 0;
     SWPS_HIP(hipEventElapsedTime(&ms, ev_x0, ev_x1));
     xms += ms;
@@ -241,7 +242,7 @@ int ShardDriver::exchange(const void *d_send, const uint64_t *sk, void *d_recv, 
 
 int ShardDriver::exchange_disp(const void *d_send, const std::vector<uint64_t> &sb, const std::vector<uint64_t> &so,
                                void *d_recv, const std::vector<uint64_t> &rb, const std::vector<uint64_t> &ro,
-                               hipStream_t s) {
+                               hipStream_t s, const char *phase) {
   if (xprof) {
     SWPS_HIP(hipEventRecord(ev_x0, s));
     for (int r = 0; r < world; r++) {
@@ -250,10 +251,11 @@ int ShardDriver::exchange_disp(const void *d_send, const std::vector<uint64_t> &
     }
     calls++;
   }
-  SWPS_TRY(comm_alltoallv_disp(c, d_send, sb, so, d_recv, rb, ro, s, stage));
+  SWPS_TRY(comm_alltoallv_disp(c, d_send, sb, so, d_recv, rb, ro, s, stage, phase));
   if (xprof) {
     SWPS_HIP(hipEventRecord(ev_x1, s));
     SWPS_HIP(hipEventSynchronize(ev_x1));  // profiled runs only
+    SWPS_TRY(comm_status(c));
     float ms = 0;
     SWPS_HIP(hipEventElapsedTime(&ms, ev_x0, ev_x1));
     xms += ms;
@@ -279,11 +281,12 @@ int ShardDriver::full_pull() {
   SWPS_TRY(frk.ensure(std::max<uint64_t>(nr, 1) * 8));
   SWPS_TRY(fv.ensure(std::max<uint64_t>(nr, 1) * ops.width * ops.val_bytes));
   SWPS_TRY(fmv.ensure(std::max<uint64_t>(n, 1) * ops.width * ops.val_bytes));
-  SWPS_TRY(exchange(fk.p, cnt.data(), frk.p, rc.data(), 8, ops.cs));
+  SWPS_TRY(exchange(fk.p, cnt.data(), frk.p, rc.data(), 8, ops.cs, "full-pull keys"));
   SWPS_TRY(ops.serve_pull(ops.h, frk.as<uint64_t>(), rc.data(), 1, fv.p));
-  SWPS_TRY(exchange(fv.p, rc.data(), fmv.p, cnt.data(), ops.width * ops.val_bytes, ops.cs));
+  SWPS_TRY(exchange(fv.p, rc.data(), fmv.p, cnt.data(), ops.width * ops.val_bytes, ops.cs, "full-pull values"));
   SWPS_TRY(ops.install(ops.h, fmv.p));
   SWPS_HIP(hipStreamSynchronize(ops.cs));
+  SWPS_TRY(comm_status(c));
   fk.release();
   frk.release();
   fv.release();
@@ -321,7 +324,7 @@ int ShardDriver::steps(uint64_t count) {
         uint64_t n = 0;
         SWPS_TRY(ops.request(ops.h, 0, cnt.data(), keys.as<uint64_t>(), &n));
       }
-      SWPS_TRY(exchange(keys.p, sk, rkp, rk, 8, S));
+      SWPS_TRY(exchange(keys.p, sk, rkp, rk, 8, S, "pull keys"));
       if (key_cache) rk_valid[st] = 1;
     }
     // slot ids of the app's per-slot caches: 3*st the whole key set (pull and push), 3*st + 1 its
@@ -340,7 +343,7 @@ int ShardDriver::steps(uint64_t count) {
       early_pending = false;
       SWPS_TRY(ops.set_slot(ops.h, (int64_t)(3 * st + 2)));
       SWPS_TRY(ops.serve_pull(ops.h, e.lk.as<uint64_t>(), e.ls.data(), 0, vals.p));
-      SWPS_TRY(exchange(vals.p, e.ls.data(), lvals.p, e.ld.data(), vb, S));
+      SWPS_TRY(exchange(vals.p, e.ls.data(), lvals.p, e.ld.data(), vb, S, "late pull values"));
       const void *ev = evals[early_buf].p;
       if (ops.install_parts) {  // the step installs both parts itself (no assembly pass)
         if (mine && ns)
@@ -356,7 +359,7 @@ int ShardDriver::steps(uint64_t count) {
         SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, nullptr));
       } else {
         SWPS_TRY(ops.serve_pull(ops.h, rkp, rk, 0, vals.p));
-        SWPS_TRY(exchange(vals.p, rk, mv, sk, vb, S));
+        SWPS_TRY(exchange(vals.p, rk, mv, sk, vb, S, "pull values"));
       }
     }
     SWPS_HIP(hipEventRecord(ev_pull, S));
@@ -391,7 +394,7 @@ int ShardDriver::steps(uint64_t count) {
       }
       if (eh) SWPS_HIP(hipStreamWaitEvent(S, eh, 0));
       else SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
-      SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S));
+      SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S, "push gradients"));
       for (int r = 0; r < world; r++) {
         so[r] += sb[r];
         ro[r] += rb[r];
@@ -399,10 +402,10 @@ int ShardDriver::steps(uint64_t count) {
         rb[r] = (rk[r] - rk[r] / 2) * gb;
       }
       SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
-      SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S));
+      SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S, "push gradients"));
     } else {
       SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
-      SWPS_TRY(exchange(grads.p, sk, rg, rk, gb, S));
+      SWPS_TRY(exchange(grads.p, sk, rg, rk, gb, S, "push gradients"));
     }
     SWPS_TRY(ops.serve_push(ops.h, rkp, rg, rk));
     if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, -1));
@@ -414,9 +417,9 @@ int ShardDriver::steps(uint64_t count) {
 }
 
 int ShardDriver::sync() {
-  SWPS_HIP(hipStreamSynchronize(S));
+  SWPS_HIP(hipStreamSynchronize(S));  // returns once the RCCL guard aborts a stuck exchange
   SWPS_HIP(hipStreamSynchronize(ops.cs));
-  return SWPS_OK;
+  return comm_status(c);
 }
 
 }  // namespace swps

@@ -193,7 +193,10 @@ namespace swps {
 constexpr uint64_t kEmptyKey = ~0ULL;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 // table internals used by the app contexts (same library)
-int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s);
+// init = false: no init_param for the new keys (their rows are about to be assigned whole; an
+// SWPS_INIT_FLCG table draws nothing)
+int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s,
+                         bool init = true);
 int table_find_or_insert_placed(swps_table *t, const uint64_t *d_keys, uint64_t n, const uint32_t *place,
                                 uint32_t *d_rows_out, hipStream_t s);
 int table_lookup(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s);
@@ -223,11 +226,16 @@ int check_app_table(swps_table *t);
 int comm_allgather(swps_comm *c, const void *in, void *out, uint64_t bytes, hipStream_t s);
 // dst rows pos[i] = src rows i (row_bytes each, a multiple of 4), ordered on s
 int scatter_rows(const void *src, const uint32_t *pos, uint64_t n, uint64_t row_bytes, void *dst, hipStream_t s);
+// phase: what the exchange carries, named by the RCCL deadline guard when it does not retire
 int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb, void *d_recv,
-                   const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg);
+                   const std::vector<uint64_t> &rb, hipStream_t s, HostStage &stg,
+                   const char *phase = "all-to-all-v");
 int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint64_t> &sb,
                         const std::vector<uint64_t> &so, void *d_recv, const std::vector<uint64_t> &rb,
-                        const std::vector<uint64_t> &ro, hipStream_t s, HostStage &stg);
+                        const std::vector<uint64_t> &ro, hipStream_t s, HostStage &stg,
+                        const char *phase = "all-to-all-v");
+// SWPS_OK, or SWPS_E_RCCL with the guard's message once the communicator was aborted
+int comm_status(swps_comm *c);
 int comm_rank(const swps_comm *c);
 int comm_world(const swps_comm *c);
 int comm_device(const swps_comm *c);
@@ -318,8 +326,10 @@ struct ShardDriver {
   int full_pull();
   int steps(uint64_t count);
   int sync();
-  int exchange(const void *d_send, const uint64_t *sk, void *d_recv, const uint64_t *rk, uint64_t w, hipStream_t s);
+  int exchange(const void *d_send, const uint64_t *sk, void *d_recv, const uint64_t *rk, uint64_t w, hipStream_t s,
+               const char *phase = "all-to-all-v");
   int exchange_disp(const void *d_send, const std::vector<uint64_t> &sb, const std::vector<uint64_t> &so,
-                    void *d_recv, const std::vector<uint64_t> &rb, const std::vector<uint64_t> &ro, hipStream_t s);
+                    void *d_recv, const std::vector<uint64_t> &rb, const std::vector<uint64_t> &ro, hipStream_t s,
+                    const char *phase = "all-to-all-v");
 };
 }  // namespace swps

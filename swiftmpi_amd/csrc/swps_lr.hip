@@ -2516,6 +2516,23 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
   return table_push_sources(l->t, l->d_serve_rows.as<uint32_t>(), n, d_grads, l->s, false, nsrc <= 1);
 }
 
+int swps_lr_exchange_stats(swps_lr *l, int32_t on, double *out4) {
+  if (!l->drv) return fail(SWPS_E_STATE, "not driven by swps_lr_shard_comm");
+  SWPS_TRY(l->drv->sync());
+  if (out4) {
+    out4[0] = (double)l->drv->bytes_remote;
+    out4[1] = (double)l->drv->bytes_total;
+    out4[2] = (double)l->drv->calls;
+    out4[3] = l->drv->xms;
+  }
+  if (on >= 0) {
+    l->drv->xprof = on != 0;
+    l->drv->bytes_remote = l->drv->bytes_total = l->drv->calls = 0;
+    l->drv->xms = 0;
+  }
+  return SWPS_OK;
+}
+
 int swps_lr_shard_comm(swps_lr *l, swps_comm *c, int32_t frag_num) {
   if (!c) return fail(SWPS_E_CFG, "null communicator");
   if (comm_device(c) != l->t->cfg.device) return fail(SWPS_E_CFG, "communicator and table are on different devices");

@@ -571,7 +571,7 @@ static int init_new_rows(swps_table *t, const uint64_t *d_keys, uint64_t n, cons
 // find-or-insert + init_param of the new keys, stream-ordered (errors latched
 // in counters[1]); `isnew` is the table's own scratch
 static int find_or_insert_async(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out,
-                                hipStream_t s) {
+                                hipStream_t s, bool init = true) {
   if (n == 0) return SWPS_OK;
   SWPS_TRY(t->isnew.ensure(n));
   uint8_t *isnew = t->isnew.as<uint8_t>();
@@ -579,12 +579,13 @@ static int find_or_insert_async(swps_table *t, const uint64_t *d_keys, uint64_t 
                                                   t->row_key.as<uint64_t>(), t->counters.as<uint32_t>(), t->mask,
                                                   t->cfg.capacity, d_rows_out, isnew);
   SWPS_HIP(hipGetLastError());
-  return init_new_rows(t, d_keys, n, d_rows_out, isnew, s);
+  return init ? init_new_rows(t, d_keys, n, d_rows_out, isnew, s) : SWPS_OK;
 }
 
-int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s) {
+int table_find_or_insert(swps_table *t, const uint64_t *d_keys, uint64_t n, uint32_t *d_rows_out, hipStream_t s,
+                         bool init) {
   if (n == 0) return SWPS_OK;
-  SWPS_TRY(find_or_insert_async(t, d_keys, n, d_rows_out, s));
+  SWPS_TRY(find_or_insert_async(t, d_keys, n, d_rows_out, s, init));
   return table_check_error(t, s);
 }
 
@@ -596,6 +597,13 @@ int table_find_or_insert_placed(swps_table *t, const uint64_t *d_keys, uint64_t 
                                 uint32_t *d_rows_out, hipStream_t s) {
   if (n == 0) return SWPS_OK;
   if (t->mask >= 0xFFFFFFFFull) return table_find_or_insert(t, d_keys, n, d_rows_out, s);
+  // the placement must be a permutation: checked before any slot is claimed, so a bad one leaves
+  // the table untouched
+  std::vector<uint32_t> order(n, 0xFFFFFFFFu), newrow(n, 0);
+  for (uint64_t i = 0; i < n; i++) {
+    if (place[i] >= n || order[place[i]] != 0xFFFFFFFFu) return fail(SWPS_E_CFG, "placement is not a permutation");
+    order[place[i]] = (uint32_t)i;
+  }
   SWPS_TRY(t->isnew.ensure(n));
   uint8_t *isnew = t->isnew.as<uint8_t>();
   k_claim_slots<<<blocks_for(n), 256, 0, s>>>(d_keys, n, t->keys.as<uint64_t>(), t->slot_row.as<uint32_t>(),
@@ -606,11 +614,6 @@ int table_find_or_insert_placed(swps_table *t, const uint64_t *d_keys, uint64_t 
   SWPS_HIP(hipMemcpyAsync(nw.data(), isnew, n, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipMemcpyAsync(&base, t->counters.p, 4, hipMemcpyDeviceToHost, s));
   SWPS_HIP(hipStreamSynchronize(s));
-  std::vector<uint32_t> order(n, 0xFFFFFFFFu), newrow(n, 0);
-  for (uint64_t i = 0; i < n; i++) {
-    if (place[i] >= n || order[place[i]] != 0xFFFFFFFFu) return fail(SWPS_E_CFG, "placement is not a permutation");
-    order[place[i]] = (uint32_t)i;
-  }
   uint64_t next = base;
   for (uint64_t j = 0; j < n; j++)
     if (nw[order[j]]) newrow[order[j]] = (uint32_t)std::min<uint64_t>(next++, 0xFFFFFFFFull);
@@ -972,7 +975,9 @@ int swps_assign(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d
   SWPS_HIP(hipSetDevice(t->cfg.device));
   SWPS_TRY(t->scratch.ensure(n * 4));
   uint32_t *rows = t->scratch.as<uint32_t>();
-  SWPS_TRY(table_find_or_insert(t, d_keys, n, rows, t->stream));
+  // ClusterServer::load / an assignment never runs init_param (server.h:49-62): the new rows are
+  // written whole below, and an SWPS_INIT_FLCG table's float-LCG stream does not move
+  SWPS_TRY(table_find_or_insert(t, d_keys, n, rows, t->stream, false));
   SWPS_TRY(table_set_rows(t, rows, n, d_rows, t->stream));
   SWPS_HIP(hipStreamSynchronize(t->stream));
   return SWPS_OK;

@@ -3908,11 +3908,11 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
           // (same-box A/B: B = 100 2.87e8 -> 3.06e8 words/s, B = 5000 -0.1 %); SWPS_PUSH_WPE=1 / 4 forces
           const bool wpe4 = w->push_wpe == 4 || (w->push_wpe == 0 && U < 65536);
           hipEvent_t pb = tm.ext(), pe = tm.ext();  // profiled: the kernel's own start / end stamps
-          if (w->push_unr == 4 && U < 65536 && w->bfp_rb == 0 && bfp_shape(D) == 11) {
+          if (wpe4 && w->push_unr == 4 && U < 65536 && w->bfp_rb == 0 && bfp_shape(D) == 11) {
             // D = 257..320, bfp32, small batches: 4 record rows in flight, 114 VGPRs, 4 waves per SIMD
             // without spills (same-box A/B, round 4: B = 100 3.01e8 -> 3.09e8 words/s; 5 / 6 / 8 rows:
             // 3.07 / 3.03 / 3.01e8; 5 waves per SIMD (13 spills) 2.85e8).  Not above 64k keys: B = 5000
-            // +0.1 %, the config-4 shape's push 4.78 -> 5.00 ms
+            // +0.1 %, the config-4 shape's push 4.78 -> 5.00 ms.  SWPS_PUSH_WPE=1 turns it off too
             hipExtLaunchKernelGGL(k_push_b<1, 1, 0, 4, false, 4>, dim3(pgrid), dim3(256), 0, s, pb, pe, 0, pa, part,
                                   (double *)nullptr);
           } else if (wpe4 && w->bfp_rb == 0 && bfp_shape(D) == 11) {

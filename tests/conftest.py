@@ -42,15 +42,14 @@ def free_port():
 
 
 def init_gloo1():
-    """A world-1 gloo process group on a free port (a fresh port on the rare EADDRINUSE)."""
+    """A world-1 gloo process group rendezvousing through a fresh file (file://
+    init): no port is probed or bound, so there is no probe-then-bind race."""
+    import tempfile
     import torch.distributed as dist
-    for attempt in range(5):
-        try:
-            dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % free_port(), rank=0, world_size=1)
-            return
-        except dist.DistNetworkError:
-            if attempt == 4:
-                raise
+    fd, path = tempfile.mkstemp(prefix="swps_gloo1_")
+    os.close(fd)
+    os.unlink(path)  # FileStore creates it; a stale file from an earlier group would be reused
+    dist.init_process_group("gloo", init_method="file://" + path, rank=0, world_size=1)
 
 
 def pytest_configure(config):

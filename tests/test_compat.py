@@ -391,3 +391,76 @@ def test_reference_lr_main_unchanged_matches_oracle(lib, oracle_mod, gpu, tmp_pa
     m.init()
     p, _ = m.predict()
     assert len(p_ref) == len(p) > 0 and np.allclose(p_ref, p, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_reference_lr_predict_partial_dump(lib, oracle_mod, gpu, tmp_path):
+    """lr.cpp predict mode over a dump that lacks two thirds of the data's keys
+    (ADVICE r04): ClusterServer::load assigns the dumped rows without drawing
+    (server.h:49-62 never calls init_param), and each minibatch's pull gives the
+    keys the server lacks LRPullAccessMethod::init_param's gen_float() draws in
+    the key set's iteration order (lr.cpp:45-50, 240-295) — the predictions
+    equal the oracle's restatement of that predict mode."""
+    ref = _ref_bin("lr")
+    data = os.path.join(GOLDEN, "lr_data.txt")
+    t0 = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+    m0 = lib.LR(t0, minibatch=200)
+    m0.load_text(data)
+    m0.init()
+    k0, _, _ = m0.params()
+    keys = k0[::3]
+    vals = np.array(["%g" % (0.25 + 1e-3 * i) for i in range(len(keys))], dtype=np.float32)
+    dump = str(tmp_path / "partial.txt")
+    with open(dump, "w") as f:
+        for k, x in zip(keys, vals):
+            f.write("%d\t%g\n" % (k, x))
+    prefix = str(tmp_path / "lr_param")
+    conf = tmp_path / "lr.conf"
+    conf.write_text(LR_REF_CONF % prefix)
+    pred = str(tmp_path / "pred.txt")
+    r = subprocess.run([ref, "-mode", "predict", "-config", str(conf), "-dataset", data, "-param_path", dump,
+                        "-out_prefix", pred, "-niters", "1"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    p_ref = np.loadtxt(pred)
+    orc = oracle_mod.LR(data, 200, 0.05)
+    orc.load(keys, vals)
+    p_orc = orc.predict_mode()
+    assert len(p_ref) == len(p_orc) > 0
+    assert np.allclose(p_ref, p_orc, rtol=2e-6, atol=1e-6), np.abs(p_ref - p_orc).max()
+
+
+@pytest.mark.gpu
+def test_flcg_table_load_draws_nothing(lib, gpu, tmp_path):
+    """An SWPS_INIT_FLCG table (lr.cpp's gen_float init_param): load / assign
+    insert the dumped keys without moving the float-LCG stream, so the first
+    pulled miss gets the stream's first draw."""
+    import torch
+    seq = _flcg_seq(64)
+    dump = str(tmp_path / "d.txt")
+    with open(dump, "w") as f:
+        for k in range(1, 41):
+            f.write("%d\t%g\n" % (k, 0.5))
+    t = lib.Table("lr", capacity=1024, dtype="f32", learning_rate=0.05, init="flcg")
+    t.load(dump)
+    keys = torch.arange(100, 110, dtype=torch.int64, device="cuda")
+    got = t.pull(keys)[:, 0].cpu().numpy()
+    assert np.array_equal(got, seq[:10]), (got, seq[:10])
+    old = t.pull(torch.arange(1, 5, dtype=torch.int64, device="cuda"))[:, 0].cpu().numpy()
+    assert (old == np.float32(0.5)).all()
+
+
+def _flcg_seq(n):
+    """gen_float() of swift_snails::Random (utils/random.h:33-36): y = y * 4903917 + 11 from
+    ULONG_MAX / 2, value (float)y / 2^64 with (float)y rounded to nearest even."""
+    out, y = np.zeros(n, dtype=np.float32), (2 ** 64 - 1) // 2
+    for i in range(n):
+        y = (y * 4903917 + 11) % 2 ** 64
+        b, q = y.bit_length(), y
+        if b > 24:
+            sh = b - 24
+            q, r = y >> sh, y & ((1 << sh) - 1)
+            if r > 1 << (sh - 1) or (r == 1 << (sh - 1) and q & 1):
+                q += 1
+            q <<= sh
+        out[i] = np.float32(q / 2.0 ** 64)
+    return out

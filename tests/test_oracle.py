@@ -90,3 +90,22 @@ def test_w2v_oracle_determinism(oracle_mod, tmp_path):
     assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
     st = outs[0][1]
     assert st["pushes"] > 0 and st["kept"] > 0
+
+
+def test_oracle_lr_predict_mode(oracle_mod):
+    """The oracle's lr.cpp predict mode (per-minibatch pulls) over a full dump of trained weights
+    predicts exactly what orc_lr_predict does with those weights; over an empty dump every weight
+    is a gen_float() draw, the first in the first minibatch's key-set order."""
+    import os
+    from conftest import GOLDEN
+    data = os.path.join(GOLDEN, "lr_data.txt")
+    a = oracle_mod.LR(data, 200, 0.05)
+    a.train(2)
+    k, w, _ = a.params()
+    p_a, _ = a.predict()
+    b = oracle_mod.LR(data, 200, 0.05)
+    b.load(k, w)
+    assert np.array_equal(b.predict_mode(), p_a)
+    c = oracle_mod.LR(data, 200, 0.05)
+    p = c.predict_mode()
+    assert np.isfinite(p).all() and len(p) == len(p_a)
