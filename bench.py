@@ -650,6 +650,9 @@ def main():
     ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
                     help="w2v: the headline (config 2); lr: config 3 shape; s2v: config 5 shape")
     ap.add_argument("--lr-batch", type=int, default=65536, help="LR rows per GPU per minibatch (config 3)")
+    ap.add_argument("--lr-plan", default="step", choices=["step", "load"],
+                    help="LR: each minibatch's index built inside its step (beside the previous one; the "
+                         "reference gathers per minibatch, lr.cpp:215-227) or once at load for every minibatch")
     ap.add_argument("--lr-exact", action="store_true",
                     help="LR: the reference's sequential fp32 per-key sums (bit-exact) instead of fast fp64 sums")
     ap.add_argument("--s2v-docs", type=int, default=8192, help="sent2vec documents per minibatch")
@@ -823,7 +826,8 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
     ctx.barrier()
     t0 = time.perf_counter()
     if comm is not None:
-        m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
+        m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact,
+                  plan=args.lr_plan)
         m.load_csr(y, off, f, v)
         m.shard_comm(comm, frag_num=2000)
         t1 = time.perf_counter()
@@ -837,7 +841,8 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
         m.init()
         run = m.train_steps
     else:
-        m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact)
+        m = sw.LR(t, minibatch=args.lr_batch, init_ref=False, profile=False, fast_sums=not args.lr_exact,
+                  plan=args.lr_plan)
         m.load_csr(y, off, f, v)
         t1 = time.perf_counter()
         m.init()

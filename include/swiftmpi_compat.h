@@ -874,6 +874,7 @@ class LRApp {
     c.init_ref = comm ? 0 : 1;
     c.profile = 0;
     c.fast_sums = 0;
+    c.plan = SWPS_LR_PLAN_STEP;
     swps_check(swps_lr_create(_t, &c, &_l));
     swps_check(swps_lr_load_text(_l, path.c_str()));
     if (comm) swps_check(swps_lr_shard_comm(_l, comm, global_frag_num()));

@@ -478,7 +478,14 @@ typedef struct {
   int32_t fast_sums;  /* 0: each key's gradient sum is the reference's sequential fp32 chain in record
                        * order (bit-exact); 1: fp64 sums, long runs tree-reduced across a wave (fast
                        * mode: deterministic, not bit-exact — within 1e-5 of the oracle) */
+  int32_t plan;       /* SWPS_LR_PLAN_STEP (0): each minibatch's key-sorted index is built inside its
+                       * training step, on a second stream beside the previous step (lr.cpp:215-227
+                       * gathers each minibatch inside the loop) — single GPU, fast sums; otherwise,
+                       * and with SWPS_LR_PLAN_LOAD (1), every minibatch's index is built once at load
+                       * and reused every epoch.  Same results either way. */
 } swps_lr_cfg;
+#define SWPS_LR_PLAN_STEP 0
+#define SWPS_LR_PLAN_LOAD 1
 
 int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out);
 int swps_lr_destroy(swps_lr *l);

@@ -574,9 +574,15 @@ class Sent2Vec:
 class LR:
     """Sparse logistic regression with server-side AdaGrad (lr.cpp:133-411)."""
 
-    def __init__(self, table, minibatch=200, init_ref=True, profile=False, fast_sums=False):
+    def __init__(self, table, minibatch=200, init_ref=True, profile=False, fast_sums=False, plan="step"):
+        """plan: "step" builds each minibatch's index inside its step (beside the previous step,
+        lr.cpp:215-227's per-minibatch gather; single GPU with fast_sums), "load" every
+        minibatch's index once at load (reused each epoch).  Same results."""
         assert table.layout == "lr"
-        cfg = capi.LRCfg(minibatch, int(init_ref), int(profile), int(fast_sums))
+        plans = {"step": capi.LR_PLAN_STEP, "load": capi.LR_PLAN_LOAD}
+        if plan not in plans:
+            raise ValueError("unknown plan %r (step or load)" % (plan,))
+        cfg = capi.LRCfg(minibatch, int(init_ref), int(profile), int(fast_sums), plans[plan])
         h = ctypes.c_void_p()
         check(capi.lib().swps_lr_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h

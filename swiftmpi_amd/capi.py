@@ -20,6 +20,7 @@ INIT_ZERO, INIT_HASH, INIT_FLCG = 0, 1, 2
 KEY_BKDR, KEY_ATOI = 0, 1
 W2V_INIT_REF, W2V_INIT_TABLE = 0, 1
 PUSH_ADAGRAD, PUSH_SGD = 0, 1
+LR_PLAN_STEP, LR_PLAN_LOAD = 0, 1
 COMM_ID_BYTES = 128
 
 # swps_transport callbacks (host all-gather / all-to-all-v)
@@ -57,7 +58,7 @@ class W2VCfg(ctypes.Structure):
 
 
 class LRCfg(ctypes.Structure):
-    _fields_ = [("minibatch", _i32), ("init_ref", _i32), ("profile", _i32), ("fast_sums", _i32)]
+    _fields_ = [("minibatch", _i32), ("init_ref", _i32), ("profile", _i32), ("fast_sums", _i32), ("plan", _i32)]
 
 
 class S2VCfg(ctypes.Structure):

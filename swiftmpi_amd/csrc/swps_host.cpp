@@ -56,6 +56,50 @@ int32_t GlibcRand::next() {
   return (int32_t)((uint32_t)v >> 1);
 }
 
+namespace {
+// a (mod x^31 - x^28 - 1) polynomial over Z / 2^32: c[j] is the coefficient of x^j
+void poly31_mulmod(const uint32_t *a, const uint32_t *b, uint32_t *out) {
+  uint32_t t[61] = {0};
+  for (int i = 0; i < 31; i++)
+    for (int j = 0; j < 31; j++) t[i + j] += a[i] * b[j];
+  for (int d = 60; d >= 31; d--) {  // x^d = x^(d-3) + x^(d-31)
+    t[d - 3] += t[d];
+    t[d - 31] += t[d];
+  }
+  for (int i = 0; i < 31; i++) out[i] = t[i];
+}
+}  // namespace
+
+void GlibcRand::discard(uint64_t k) {
+  if (k < 4096) {
+    for (uint64_t i = 0; i < k; i++) (void)next();
+    return;
+  }
+  // the ring holds o[i-34 .. i-1] (r[idx] the oldest) and the next output is o[i]; with
+  // b_j = o[i-31+j], o[i-31+e] = sum_j a_j b_j where sum_j a_j x^j = x^e mod P (o[n] = o[n-3] +
+  // o[n-31]: x^31 = x^28 + 1).  After k outputs the ring holds o[i+k-34+t], t = 0..33: e = k-3+t
+  uint32_t b[31];
+  for (int j = 0; j < 31; j++) b[j] = (uint32_t)r[(idx + 3 + j) % 34];
+  uint32_t a[31] = {0}, x[31] = {0};
+  a[0] = 1;
+  x[1] = 1;
+  for (uint64_t e = k - 3; e; e >>= 1) {
+    if (e & 1) poly31_mulmod(a, x, a);
+    poly31_mulmod(x, x, x);
+  }
+  for (int t = 0; t < 34; t++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 31; j++) v += a[j] * b[j];
+    r[t] = (int32_t)v;
+    const uint32_t top = a[30];  // a <- x * a mod P
+    for (int j = 30; j > 0; j--) a[j] = a[j - 1];
+    a[0] = top;
+    a[28] += top;
+  }
+  idx = 0;
+  produced += k;
+}
+
 int Config::parse(const std::string &path) {
   std::ifstream f(path);
   if (!f) return fail(SWPS_E_IO, "conf can not open: " + path);

@@ -147,6 +147,79 @@ struct GlibcRand {
   uint64_t produced = 0;
   explicit GlibcRand(uint32_t seed);
   int32_t next();
+  // k calls of next() whose outputs nobody reads: a jump of the linear recurrence (x^k mod
+  // x^31 - x^28 - 1 by square-and-multiply) for long skips, stepping for short ones
+  void discard(uint64_t k);
+};
+// Host open-addressed u64 -> int32 map (linear probing on fmix64, power-of-two capacity, a
+// generation stamp per slot so clear() is O(1)): the host schedules' per-token counting, where
+// std::unordered_map's node allocations dominated.  Iteration order is not exposed; callers that
+// need the reference's std::unordered_set order keep one of those beside it.
+struct FlatMap64 {
+  std::vector<uint64_t> k;
+  std::vector<int32_t> v;
+  std::vector<uint32_t> st;
+  uint32_t gen = 1;
+  uint64_t mask = 0;
+  size_t n = 0;
+  explicit FlatMap64(size_t cap = 16) { reset(cap); }
+  void reset(size_t cap) {
+    size_t c = 16;
+    while (c < 2 * cap) c <<= 1;
+    k.assign(c, 0);
+    v.assign(c, 0);
+    st.assign(c, 0);
+    mask = c - 1;
+    n = 0;
+    gen = 1;
+  }
+  void clear() {
+    if (++gen == 0) {
+      std::fill(st.begin(), st.end(), 0u);
+      gen = 1;
+    }
+    n = 0;
+  }
+  size_t size() const { return n; }
+  // the value slot of key (0 when inserted); *fresh = inserted by this call
+  int32_t &at(uint64_t key, bool *fresh = nullptr) {
+    if (2 * (n + 1) > mask + 1) grow();
+    uint64_t i = fmix64(key) & mask;
+    while (st[i] == gen) {
+      if (k[i] == key) {
+        if (fresh) *fresh = false;
+        return v[i];
+      }
+      i = (i + 1) & mask;
+    }
+    st[i] = gen;
+    k[i] = key;
+    v[i] = 0;
+    n++;
+    if (fresh) *fresh = true;
+    return v[i];
+  }
+  bool contains(uint64_t key) const {
+    uint64_t i = fmix64(key) & mask;
+    while (st[i] == gen) {
+      if (k[i] == key) return true;
+      i = (i + 1) & mask;
+    }
+    return false;
+  }
+  void grow() {
+    std::vector<uint64_t> ok;
+    std::vector<int32_t> ov;
+    ok.reserve(n);
+    ov.reserve(n);
+    for (size_t i = 0; i <= mask; i++)
+      if (st[i] == gen) {
+        ok.push_back(k[i]);
+        ov.push_back(v[i]);
+      }
+    reset(2 * (mask + 1));
+    for (size_t i = 0; i < ok.size(); i++) at(ok[i]) = ov[i];
+  }
 };
 // reference config file format (utils/ConfigParser.h:84-115)
 struct Config {

@@ -1111,12 +1111,17 @@ __device__ __forceinline__ void fin_apply(const LrReduce &a, uint4 rc, uint32_t 
   r[1] = g2;
   r[0] = w + step / sqrtf(g2 + a.fudge);
 }
+// cnt != nullptr (the per-step plan): ns = cnt[0], nl = cnt[1] from the device, the grid an upper bound
 __global__ __launch_bounds__(256) void k_lr_tiles_fin(LrReduce a, const uint4 *__restrict__ ms,
                                                       const uint32_t *__restrict__ msrow, uint32_t ns,
                                                       const uint4 *__restrict__ ml, const uint32_t *__restrict__ mlrow,
                                                       uint32_t nl, uint32_t LB, const double *__restrict__ part,
-                                                      uint64_t q0) {
+                                                      uint64_t q0, const uint32_t *__restrict__ cnt = nullptr) {
   const int lane = threadIdx.x & 63;
+  if (cnt) {
+    ns = cnt[0];
+    nl = cnt[1];
+  }
   if (blockIdx.x < LB) {
     for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nl; q += LB * 4) {
       const uint4 rc = ml[q];
@@ -1138,19 +1143,19 @@ __global__ __launch_bounds__(256) void k_lr_tiles_fin(LrReduce a, const uint4 *_
     }
     return;
   }
-  const uint32_t q = (blockIdx.x - LB) * blockDim.x + threadIdx.x;
-  if (q >= ns) return;
-  const uint4 rc = ms[q];
-  const uint32_t row = a.grads ? 0u : msrow[q];
-  double v[kTileFinShort];
+  for (uint32_t q = (blockIdx.x - LB) * blockDim.x + threadIdx.x; q < ns; q += (gridDim.x - LB) * blockDim.x) {
+    const uint4 rc = ms[q];
+    const uint32_t row = a.grads ? 0u : msrow[q];
+    double v[kTileFinShort];
 #pragma unroll
-  for (int j = 0; j < (int)kTileFinShort; j++) v[j] = (uint32_t)j < rc.y ? part[rc.x + j] : 0.0;
-  const float w = a.grads ? 0.f : a.rows[(uint64_t)row * 2], g = a.grads ? 0.f : a.rows[(uint64_t)row * 2 + 1];
-  double s = 0;
+    for (int j = 0; j < (int)kTileFinShort; j++) v[j] = (uint32_t)j < rc.y ? part[rc.x + j] : 0.0;
+    const float w = a.grads ? 0.f : a.rows[(uint64_t)row * 2], g = a.grads ? 0.f : a.rows[(uint64_t)row * 2 + 1];
+    double s = 0;
 #pragma unroll
-  for (int j = 0; j < (int)kTileFinShort; j++)
-    if ((uint32_t)j < rc.y) s += v[j];
-  fin_apply(a, rc, row, w, g, s, q0);
+    for (int j = 0; j < (int)kTileFinShort; j++)
+      if ((uint32_t)j < rc.y) s += v[j];
+    fin_apply(a, rc, row, w, g, s, q0);
+  }
 }
 
 // ---- the tile index (built at load with the record index; fast sums) ----
@@ -1240,6 +1245,195 @@ __global__ void k_lr_tile_dst(const uint32_t *__restrict__ tinfo, const uint32_t
                               uint32_t *__restrict__ tdst) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p < S2) tdst[p] = (tinfo[p] >> 31) ? urow[tgrun[p]] : tslot[p];
+}
+
+// ---- the per-step plan (swps_lr_cfg.plan = SWPS_LR_PLAN_STEP, the default) -------------------
+// What the static index (lr_index + lr_tile_index) builds for every batch at load, built for one
+// batch on a plan stream while the previous batch trains: lr.cpp:215-227 gathers, dedups and pulls
+// each minibatch's keys inside its training loop, and so does this path — on the GPU, with no host
+// round trip.  Two orders of the batch's records:
+//   K order — stable by vid: one run per pushed key, a key's records in row order;
+//   T order — K order stable by row tile: the (tile, key) order the row tiles (k_lr_tiles) walk.
+// A piece (a key's records inside one kTileChunk block of a tile) starts at a (tile, key) head or
+// at a block cut in T order.  In K order a key's pieces appear in T order, so one scan of the
+// piece heads in K order numbers the partial slots in (key, piece) order: the static index's
+// slots.  Same records, pieces, partial slots and sums as the static index: bit-identical.
+__global__ void k_plan_keys(const uint64_t *__restrict__ row_off, uint64_t r0, uint64_t nrb, uint64_t z0,
+                            const int32_t *__restrict__ fvid, uint32_t *__restrict__ key, uint32_t *__restrict__ rid) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nrb) return;
+  for (uint64_t c = row_off[r0 + j]; c < row_off[r0 + j + 1]; c++) {
+    key[c - z0] = (uint32_t)fvid[c];
+    rid[c - z0] = (uint32_t)j;
+  }
+}
+__global__ void k_plan_tile(const uint32_t *__restrict__ permK, const uint32_t *__restrict__ rid, uint64_t n, int tb,
+                            uint32_t *__restrict__ tkey) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) tkey[j] = rid[permK[j]] >> tb;
+}
+// T order: the records' (row in tile | run head, x_i), piece heads (run head or block cut), and
+// every K position's T position
+__global__ void k_plan_torder(const uint32_t *__restrict__ permT, const uint32_t *__restrict__ permK,
+                              const uint32_t *__restrict__ ks1, const uint32_t *__restrict__ rid,
+                              const float *__restrict__ fval, const uint64_t *__restrict__ row_off, uint64_t r0,
+                              uint64_t z0, uint64_t n, int tb, uint32_t chunk, uint16_t *__restrict__ trow,
+                              float *__restrict__ tval, uint32_t *__restrict__ ph, uint32_t *__restrict__ invT) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t j = permT[t], c = permK[j];
+  const uint32_t r = rid[c], tile = r >> tb, vid = ks1[j];
+  bool head = t == 0;
+  if (!head) {
+    const uint32_t jp = permT[t - 1];
+    head = ks1[jp] != vid || (rid[permK[jp]] >> tb) != tile;
+  }
+  trow[t] = (uint16_t)((r & ((1u << tb) - 1)) | (head ? kTileHead : 0));
+  tval[t] = fval[z0 + c];
+  const uint64_t ts = row_off[r0 + ((uint64_t)tile << tb)] - z0;  // the tile's first record (T = CSR at tiles)
+  ph[t] = (head || (t - ts) % chunk == 0) ? 1u : 0u;
+  invT[j] = (uint32_t)t;
+}
+// K order: (piece head << 32 | key head), scanned together
+__global__ void k_plan_kflags(const uint32_t *__restrict__ ks1, const uint32_t *__restrict__ invT,
+                              const uint32_t *__restrict__ ph, uint64_t n, uint64_t *__restrict__ packed) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  packed[j] = ((uint64_t)ph[invT[j]] << 32) | ((j == 0 || ks1[j] != ks1[j - 1]) ? 1u : 0u);
+}
+__global__ void k_plan_kstart(const uint64_t *__restrict__ pk, uint64_t n, uint32_t *__restrict__ kstart) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t k = (uint32_t)pk[j];
+  if (j == 0 || (uint32_t)pk[j - 1] != k) kstart[k - 1] = (uint32_t)j;
+}
+constexpr uint32_t kPlanHotBins = 4096;
+// per key (grid-stride over the batch's U keys, U on the device): its partial slots, records and
+// shard row; the keys with several pieces into the finisher's lists (any order: each key's
+// partials are summed in slot order whatever its list position); the hot-key histogram
+__global__ void k_plan_kinfo(const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ pk, uint64_t n,
+                             const uint32_t *__restrict__ ks1, const uint32_t *__restrict__ vid_row,
+                             uint32_t *__restrict__ kwhole, uint32_t *__restrict__ krow, uint4 *__restrict__ ms,
+                             uint32_t *__restrict__ msrow, uint4 *__restrict__ ml, uint32_t *__restrict__ mlrow,
+                             uint32_t *__restrict__ cnt, uint32_t *__restrict__ hist) {
+  const uint32_t U = (uint32_t)pk[n - 1];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < U; k += gridDim.x * blockDim.x) {
+    const uint32_t s = kstart[k], e = k + 1 < U ? kstart[k + 1] : (uint32_t)n;
+    const uint32_t slot0 = (uint32_t)(pk[s] >> 32) - 1, np = (uint32_t)(pk[e - 1] >> 32) - slot0;
+    const uint32_t recs = e - s, row = vid_row[ks1[s]];
+    kwhole[k] = np == 1 ? 1u : 0u;
+    krow[k] = row;
+    if (np > 1) {
+      const bool lng = np > kTileFinShort;
+      const uint32_t q = atomicAdd(&cnt[lng ? 1 : 0], 1u);
+      (lng ? ml : ms)[q] = make_uint4(slot0, np, recs, k);
+      (lng ? mlrow : msrow)[q] = row;
+    }
+    if (hist && recs >= 8) atomicAdd(&hist[min(recs, kPlanHotBins - 1)], 1u);
+  }
+}
+// the hot keys: every key with more records than the threshold bin, then keys of that bin while
+// slots remain (which of those tie keys get in changes nothing but the LDS they are read from)
+__global__ void k_plan_hot_thresh(uint32_t *__restrict__ hist, uint32_t nhot, uint32_t *__restrict__ thr) {
+  __shared__ uint32_t part[256];
+  const int tid = threadIdx.x;
+  constexpr int PER = kPlanHotBins / 256;
+  uint32_t s = 0;  // this thread's bins [tid*PER, (tid+1)*PER)
+  for (int i = 0; i < PER; i++) s += hist[tid * PER + i];
+  part[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t above = 0;  // keys in bins above the current one
+    int T = 8;
+    bool found = false;
+    for (int q = 255; q >= 0 && !found; q--) {
+      if (above + part[q] < nhot) {
+        above += part[q];
+        continue;
+      }
+      for (int b = q * PER + PER - 1; b >= q * PER; b--) {
+        if (above + hist[b] >= nhot) {
+          T = b;
+          found = true;
+          break;
+        }
+        above += hist[b];
+      }
+    }
+    if (!found) {  // fewer candidates than slots: every key of >= 8 records
+      T = 8;
+      above = 0;
+      for (int b = kPlanHotBins - 1; b > 8; b--) above += hist[b];
+    }
+    thr[0] = (uint32_t)T;
+    thr[1] = 0;      // next slot for keys above T
+    thr[2] = above;  // next slot for keys of bin T
+  }
+}
+__global__ void k_plan_hot_assign(const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ pk, uint64_t n,
+                                  const uint32_t *__restrict__ krow, uint32_t nhot, uint32_t *__restrict__ thr,
+                                  int32_t *__restrict__ khot, uint32_t *__restrict__ hrow) {
+  const uint32_t U = (uint32_t)pk[n - 1];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < U; k += gridDim.x * blockDim.x) {
+    const uint32_t e = k + 1 < U ? kstart[k + 1] : (uint32_t)n;
+    const uint32_t recs = e - kstart[k], bin = min(recs, kPlanHotBins - 1);
+    int32_t h = -1;
+    if (recs >= 8 && bin > thr[0]) {
+      h = (int32_t)atomicAdd(&thr[1], 1u);
+    } else if (recs >= 8 && bin == thr[0]) {
+      const uint32_t q = atomicAdd(&thr[2], 1u);
+      if (q < nhot) h = (int32_t)q;
+    }
+    khot[k] = h;
+    if (h >= 0) hrow[h] = krow[k];
+  }
+}
+// every record (K order): its forward code (hot rank or shard row) at its CSR position; every
+// piece head: its destination (a whole run's shard row, else its partial slot) and whole-run flag
+__global__ void k_plan_records(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ permK,
+                               const uint32_t *__restrict__ invT, const uint32_t *__restrict__ pidT, uint64_t n,
+                               const uint32_t *__restrict__ kwhole, const uint32_t *__restrict__ krow,
+                               const int32_t *__restrict__ khot, uint32_t *__restrict__ fcode,
+                               uint32_t *__restrict__ tinfo, uint32_t *__restrict__ tdst) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t v = pk[j];
+  const uint32_t k = (uint32_t)v - 1, row = krow[k];
+  const int32_t h = khot ? khot[k] : -1;
+  fcode[permK[j]] = h >= 0 ? (kLrHotBit | (uint32_t)h) : row;
+  if (j == 0 || (pk[j - 1] >> 32) != (v >> 32)) {
+    const uint32_t q = pidT[invT[j]] - 1, whole = kwhole[k];
+    tinfo[q] = whole ? 0x80000000u : 0u;
+    tdst[q] = whole ? row : (uint32_t)(v >> 32) - 1;
+  }
+}
+// the tiles' blocks: per tile its kTileChunk-record blocks {tile, first / end record, first / end
+// piece}; tfirst = each tile's first block (exclusive scan of the per-tile block counts)
+__global__ void k_plan_tile_nch(const uint64_t *__restrict__ row_off, uint64_t r0, uint64_t nrb, int tb,
+                                uint32_t chunk, uint64_t ntile, uint32_t *__restrict__ tn) {
+  const uint64_t tl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tl >= ntile) return;
+  const uint64_t rs = r0 + (tl << tb), re = r0 + min(nrb, (tl + 1) << tb);
+  tn[tl] = (uint32_t)((row_off[re] - row_off[rs] + chunk - 1) / chunk);
+}
+__global__ void k_plan_chunks(const uint64_t *__restrict__ row_off, uint64_t r0, uint64_t nrb, uint64_t z0, int tb,
+                              uint32_t chunk, uint64_t ntile, const uint32_t *__restrict__ tfirst,
+                              const uint32_t *__restrict__ pidT, uint64_t n, uint64_t nch, uint32_t *__restrict__ out) {
+  const uint64_t tl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tl >= ntile) return;
+  const uint64_t rs = r0 + (tl << tb), re = r0 + min(nrb, (tl + 1) << tb);
+  const uint64_t a = row_off[rs] - z0, b = row_off[re] - z0;
+  uint64_t q = tfirst[tl];
+  const uint32_t S2 = n ? pidT[n - 1] : 0u;
+  for (uint64_t c0 = a; c0 < b; c0 += chunk, q++) {
+    const uint64_t c1 = min(b, c0 + chunk);
+    uint32_t *e = out + q * 5;
+    e[0] = (uint32_t)tl;
+    e[1] = (uint32_t)c0;
+    e[2] = (uint32_t)c1;
+    e[3] = pidT[c0] - 1;
+    e[4] = q + 1 < nch ? (c1 < n ? pidT[c1] - 1 : S2) : S2;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_lr_predict(const uint64_t *__restrict__ row_off, const int32_t *__restrict__ fvid,
@@ -1401,6 +1595,26 @@ struct swps_lr {
   DevMem d_K, d_vkeys, d_init_order, d_wcache, d_local, d_serve_rows;
   swps::ShardDriver *drv = nullptr;  // swps_lr_shard_comm: the library drives the exchange
   uint64_t serve_n = 0;
+  // the static per-batch index (lr_index) exists; the per-step plan builds none at load
+  bool index_built = false;
+  // per-step plan (cfg.plan == SWPS_LR_PLAN_STEP; single GPU, fast sums through row tiles): the
+  // plan stream, its scratch, and two slots of what a step reads (plan(i+1) fills one while step i
+  // reads the other)
+  bool plan_step = false, plan_ready = false;
+  hipStream_t ps = nullptr;
+  struct PlanSlot {
+    swps::DevMem fcode, hrow, trow, tval, chunk, tinfo, tdst, ms, msrow, ml, mlrow, cnt;
+    uint64_t nch = 0;
+    hipEvent_t ready = nullptr, used = nullptr;
+    bool pending_use = false;
+  };
+  PlanSlot pslot[2];
+  swps::DevMem p_key, p_ks1, p_permK, p_rid, p_tkey, p_tks, p_permT, p_ph, p_pidT, p_invT, p_packed, p_pk, p_kstart,
+      p_kwhole, p_krow, p_khot, p_hist, p_thr, p_tn, p_tfirst, p_tmp;
+  uint64_t plan_next = 0;  // the first step whose plan is not enqueued yet
+  int plan_vbits = 1;
+  bool plan_sync = true;  // the next plan waits for the compute stream (shard rows just (re)initialised)
+  hipEvent_t ev_rows = nullptr;
   int B1() const { return cfg.minibatch + 1; }
 };
 
@@ -1619,12 +1833,9 @@ int lr_index(swps_lr *l) {
   const uint64_t n = l->row_off[nr];
   if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 features per rank");
   std::vector<uint64_t> bnz0(nb + 1);
-  l->max_bnnz = 0;
   for (uint64_t b = 0; b <= nb; b++) bnz0[b] = l->row_off[std::min<uint64_t>(nr, b * B1)];
-  l->bmaxf.assign(nb, 0);
-  for (uint64_t r = 0; r < nr; r++)
-    l->bmaxf[r / B1] = std::max<uint32_t>(l->bmaxf[r / B1], (uint32_t)(l->row_off[r + 1] - l->row_off[r]));
-  for (uint64_t b = 0; b < nb; b++) l->max_bnnz = std::max<uint64_t>(l->max_bnnz, bnz0[b + 1] - bnz0[b]);
+  l->index_built = true;
+  l->rows_mapped = false;
   DevMem d_bnz0, key, idx, ks, perm, head, rid1, rkey, tmp;
   SWPS_TRY(upload(d_bnz0, bnz0, s));
   SWPS_TRY(l->d_srow.ensure(std::max<uint64_t>(n, 1) * 4));
@@ -1771,14 +1982,288 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   SWPS_TRY(l->d_vid_row.ensure(std::max<size_t>(1, l->vocab_keys.size()) * 4));
   SWPS_TRY(l->d_err.ensure((std::max<uint64_t>(1, nr) + 4) * 4));  // + slack: k_lr_tiles' 16-B loads
   SWPS_TRY(l->d_err2.ensure(std::max<uint64_t>(1, nr) * 4));
-  SWPS_TRY(lr_index(l));
+  // per batch: its longest row and record count
+  {
+    const uint64_t B1 = l->B1();
+    l->max_bnnz = 0;
+    l->bmaxf.assign(l->nbatches, 0);
+    for (uint64_t r = 0; r < nr; r++)
+      l->bmaxf[r / B1] = std::max<uint32_t>(l->bmaxf[r / B1], (uint32_t)(l->row_off[r + 1] - l->row_off[r]));
+    for (uint64_t b = 0; b < l->nbatches; b++)
+      l->max_bnnz = std::max<uint64_t>(l->max_bnnz,
+                                       l->row_off[std::min<uint64_t>(nr, (b + 1) * B1)] - l->row_off[b * B1]);
+  }
+  // the per-step plan builds each batch's index while the previous batch trains; otherwise (exact
+  // sums, the record path, SWPS_LR_PLAN_LOAD) every batch's index is built here, once
+  l->index_built = false;
+  l->plan_ready = false;
+  l->plan_next = 0;
+  if (!(l->cfg.plan == SWPS_LR_PLAN_STEP && l->cfg.fast_sums && l->tiles)) SWPS_TRY(lr_index(l));
   l->rows_mapped = false;
   SWPS_HIP(hipStreamSynchronize(s));
   l->loaded = true;
   return SWPS_OK;
 }
 
+// the forward's chunks of whole rows of every batch (k_lr_forward_c), once: from the row lengths
+// only (rows never span chunks; a row longer than a chunk's capacity turns the form off)
+int lr_fwd_chunks(swps_lr *l) {
+  if (!(l->fwd_c && l->rows_per_wave == 1 && !l->fwd_diag && !l->stage && l->bfchunk.empty())) return SWPS_OK;
+  const uint64_t nr = l->label.size();
+  hipStream_t s = l->s;
+  std::vector<uint2> ch;
+  l->fwd_rpt = l->fwd_c == 4 || l->fwd_c == 16 ? l->fwd_c : kLrFwdRpt;  // records per thread (A/B: 4, 8, 16)
+  const uint64_t cap = (uint64_t)l->fwd_rpt * 256;
+  l->bfchunk.assign(1, 0);
+  for (uint64_t b = 0; b < l->nbatches && l->fwd_c; b++) {
+    const uint64_t a0 = b * l->B1(), a1 = std::min<uint64_t>(nr, a0 + l->B1());
+    uint64_t first = a0;
+    for (uint64_t r = a0; r < a1; r++) {
+      if (l->row_off[r + 1] - l->row_off[r] > cap) {
+        l->fwd_c = 0;
+        break;
+      }
+      if (l->row_off[r + 1] - l->row_off[first] > cap) {
+        ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(r - first)));
+        first = r;
+      }
+    }
+    if (a1 > first) ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(a1 - first)));
+    l->bfchunk.push_back(ch.size());
+  }
+  if (l->fwd_c) {
+    SWPS_TRY(upload(l->d_fchunk, ch, s));
+    SWPS_HIP(hipStreamSynchronize(s));  // `ch` is a local
+  }
+  return SWPS_OK;
+}
+
+// ---- the per-step plan: setup, one batch's plan on the plan stream, the planned step ----------
+bool lr_plan_usable(const swps_lr *l) {
+  return l->cfg.plan == SWPS_LR_PLAN_STEP && !l->sharded && l->cfg.fast_sums && l->tiles && l->fwd_c &&
+         l->rows_per_wave == 1 && !l->fwd_diag && !l->stage && !l->fwd_records && !l->inline_records &&
+         l->tile_threads == 256 && l->nbatches > 0;
+}
+
+int lr_plan_setup(swps_lr *l) {
+  const uint64_t n = std::max<uint64_t>(l->max_bnnz, 1), V = std::max<uint64_t>(l->vocab_keys.size(), 1);
+  const uint64_t B1 = l->B1(), ntile = (B1 + (1ULL << l->tile_bits) - 1) >> l->tile_bits;
+  int vb = 1;
+  while ((1ULL << vb) < V) vb++;
+  l->plan_vbits = vb;
+  int tbits = 1;
+  while ((1ULL << tbits) < ntile) tbits++;
+  if (!l->ps) SWPS_HIP(hipStreamCreateWithFlags(&l->ps, hipStreamNonBlocking));
+  for (auto &p : l->pslot) {
+    if (!p.ready) SWPS_HIP(hipEventCreateWithFlags(&p.ready, hipEventDisableTiming));
+    if (!p.used) SWPS_HIP(hipEventCreateWithFlags(&p.used, hipEventDisableTiming));
+    SWPS_TRY(p.fcode.ensure(n * 4));
+    SWPS_TRY(p.hrow.ensure(kLrHot * 4));
+    SWPS_TRY(p.trow.ensure(n * 2 + 16));
+    SWPS_TRY(p.tval.ensure(n * 4 + 16));
+    SWPS_TRY(p.tinfo.ensure(n * 4));
+    SWPS_TRY(p.tdst.ensure(n * 4));
+    SWPS_TRY(p.ms.ensure(n * 16));
+    SWPS_TRY(p.msrow.ensure(n * 4));
+    SWPS_TRY(p.ml.ensure(n * 16));
+    SWPS_TRY(p.mlrow.ensure(n * 4));
+    SWPS_TRY(p.cnt.ensure(16));
+    // blocks per batch: at most ntile + records / chunk
+    SWPS_TRY(p.chunk.ensure((ntile + n / l->tile_chunk + 1) * 5 * 4));
+  }
+  for (DevMem *m : {&l->p_key, &l->p_ks1, &l->p_permK, &l->p_rid, &l->p_tkey, &l->p_tks, &l->p_permT, &l->p_ph,
+                    &l->p_pidT, &l->p_invT, &l->p_kstart, &l->p_kwhole, &l->p_krow, &l->p_khot})
+    SWPS_TRY(m->ensure(n * 4));
+  SWPS_TRY(l->p_packed.ensure(n * 8));
+  SWPS_TRY(l->p_pk.ensure(n * 8));
+  SWPS_TRY(l->p_hist.ensure(kPlanHotBins * 4));
+  SWPS_TRY(l->p_thr.ensure(16));
+  SWPS_TRY(l->p_tn.ensure(ntile * 4 + 4));
+  SWPS_TRY(l->p_tfirst.ensure(ntile * 4 + 4));
+  // temporary storage for the largest of the plan's sorts and scans (sized once: a grow inside a
+  // step would free memory the other stream may still use)
+  size_t b = 0, mx = 0;
+  SWPS_HIP(sort_pairs_iota(nullptr, b, l->p_key.as<uint32_t>(), l->p_ks1.as<uint32_t>(), l->p_permK.as<uint32_t>(),
+                           n, vb, l->ps));
+  mx = std::max(mx, b);
+  b = 0;
+  SWPS_HIP(sort_pairs_iota(nullptr, b, l->p_tkey.as<uint32_t>(), l->p_tks.as<uint32_t>(), l->p_permT.as<uint32_t>(),
+                           n, tbits, l->ps));
+  mx = std::max(mx, b);
+  b = 0;
+  SWPS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b, l->p_ph.as<uint32_t>(), l->p_pidT.as<uint32_t>(), (int)n,
+                                            l->ps));
+  mx = std::max(mx, b);
+  b = 0;
+  SWPS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b, l->p_packed.as<uint64_t>(), l->p_pk.as<uint64_t>(), (int)n,
+                                            l->ps));
+  mx = std::max(mx, b);
+  b = 0;
+  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b, l->p_tn.as<uint32_t>(), l->p_tfirst.as<uint32_t>(),
+                                            (int)ntile, l->ps));
+  mx = std::max(mx, b);
+  SWPS_TRY(l->p_tmp.ensure(mx));
+  SWPS_TRY(l->d_tpart.ensure(n * 8));
+  SWPS_HIP(hipDeviceSynchronize());  // the allocations above precede every plan
+  l->plan_ready = true;
+  return SWPS_OK;
+}
+
+// the plan of training step `step` (batch step % nbatches) into slot step & 1, on the plan stream
+int lr_plan(swps_lr *l, uint64_t step) {
+  swps_lr::PlanSlot &p = l->pslot[step & 1];
+  const uint64_t nr = l->label.size(), bi = step % l->nbatches, B1 = l->B1();
+  const uint64_t r0 = bi * B1, r1 = std::min<uint64_t>(nr, r0 + B1), nrb = r1 - r0;
+  const uint64_t z0 = l->row_off[r0], n = l->row_off[r1] - z0;
+  const int tb = l->tile_bits;
+  const uint32_t chunk = l->tile_chunk;
+  const uint64_t ntile = (nrb + (1ULL << tb) - 1) >> tb;
+  hipStream_t P = l->ps;
+  if (p.pending_use) SWPS_HIP(hipStreamWaitEvent(P, p.used, 0));  // its reader, step - 2, is done
+  if (l->plan_sync) {  // the plan reads the shard rows of the vids (swps_lr_init, compute stream)
+    if (!l->ev_rows) SWPS_HIP(hipEventCreateWithFlags(&l->ev_rows, hipEventDisableTiming));
+    SWPS_HIP(hipEventRecord(l->ev_rows, l->s));
+    SWPS_HIP(hipStreamWaitEvent(P, l->ev_rows, 0));
+    l->plan_sync = false;
+  }
+  p.pending_use = false;
+  p.nch = 0;
+  for (uint64_t tl = 0; tl < ntile; tl++) {  // the tiles launch's grid (host: the batch's CSR offsets)
+    const uint64_t rs = r0 + (tl << tb), re = r0 + std::min<uint64_t>(nrb, (tl + 1) << tb);
+    p.nch += (l->row_off[re] - l->row_off[rs] + chunk - 1) / chunk;
+  }
+  hipEvent_t e0 = l->timer.begin(P);
+  if (n) {
+    int tbits = 1;
+    while ((1ULL << tbits) < ntile) tbits++;
+    uint32_t *key = l->p_key.as<uint32_t>(), *ks1 = l->p_ks1.as<uint32_t>(), *permK = l->p_permK.as<uint32_t>();
+    uint32_t *rid = l->p_rid.as<uint32_t>(), *tkey = l->p_tkey.as<uint32_t>(), *permT = l->p_permT.as<uint32_t>();
+    uint32_t *ph = l->p_ph.as<uint32_t>(), *pidT = l->p_pidT.as<uint32_t>(), *invT = l->p_invT.as<uint32_t>();
+    uint64_t *packed = l->p_packed.as<uint64_t>(), *pk = l->p_pk.as<uint64_t>();
+    k_plan_keys<<<nblk(nrb), 256, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, z0, l->d_fvid.as<int32_t>(), key,
+                                           rid);
+    SWPS_HIP(hipGetLastError());
+    size_t b = l->p_tmp.bytes;
+    SWPS_HIP(sort_pairs_iota(l->p_tmp.p, b, key, ks1, permK, n, l->plan_vbits, P));  // K order
+    k_plan_tile<<<nblk(n), 256, 0, P>>>(permK, rid, n, tb, tkey);
+    b = l->p_tmp.bytes;
+    SWPS_HIP(sort_pairs_iota(l->p_tmp.p, b, tkey, l->p_tks.as<uint32_t>(), permT, n, tbits, P));  // T order
+    k_plan_torder<<<nblk(n), 256, 0, P>>>(permT, permK, ks1, rid, l->d_fval.as<float>(), l->d_row_off.as<uint64_t>(),
+                                           r0, z0, n, tb, chunk, p.trow.as<uint16_t>(), p.tval.as<float>(), ph, invT);
+    SWPS_HIP(hipGetLastError());
+    b = l->p_tmp.bytes;
+    SWPS_HIP(hipcub::DeviceScan::InclusiveSum(l->p_tmp.p, b, ph, pidT, (int)n, P));
+    k_plan_kflags<<<nblk(n), 256, 0, P>>>(ks1, invT, ph, n, packed);
+    b = l->p_tmp.bytes;
+    SWPS_HIP(hipcub::DeviceScan::InclusiveSum(l->p_tmp.p, b, packed, pk, (int)n, P));
+    k_plan_kstart<<<nblk(n), 256, 0, P>>>(pk, n, l->p_kstart.as<uint32_t>());
+    SWPS_HIP(hipMemsetAsync(p.cnt.p, 0, 16, P));
+    const bool hot = l->hot != 0;
+    if (hot) {
+      SWPS_HIP(hipMemsetAsync(l->p_hist.p, 0, kPlanHotBins * 4, P));
+      SWPS_HIP(hipMemsetAsync(p.hrow.p, 0, kLrHot * 4, P));  // unused slots read row 0 (never referenced)
+    }
+    const unsigned kg = std::min<unsigned>(nblk(n), 2048);
+    k_plan_kinfo<<<kg, 256, 0, P>>>(l->p_kstart.as<uint32_t>(), pk, n, ks1, l->d_vid_row.as<uint32_t>(),
+                                     l->p_kwhole.as<uint32_t>(), l->p_krow.as<uint32_t>(), (uint4 *)p.ms.p,
+                                     p.msrow.as<uint32_t>(), (uint4 *)p.ml.p, p.mlrow.as<uint32_t>(),
+                                     p.cnt.as<uint32_t>(), hot ? l->p_hist.as<uint32_t>() : nullptr);
+    if (hot) {
+      k_plan_hot_thresh<<<1, 256, 0, P>>>(l->p_hist.as<uint32_t>(), l->nhot, l->p_thr.as<uint32_t>());
+      k_plan_hot_assign<<<kg, 256, 0, P>>>(l->p_kstart.as<uint32_t>(), pk, n, l->p_krow.as<uint32_t>(), l->nhot,
+                                            l->p_thr.as<uint32_t>(), l->p_khot.as<int32_t>(), p.hrow.as<uint32_t>());
+    }
+    k_plan_records<<<nblk(n), 256, 0, P>>>(pk, permK, invT, pidT, n, l->p_kwhole.as<uint32_t>(),
+                                            l->p_krow.as<uint32_t>(), hot ? l->p_khot.as<int32_t>() : nullptr,
+                                            p.fcode.as<uint32_t>(), p.tinfo.as<uint32_t>(), p.tdst.as<uint32_t>());
+    k_plan_tile_nch<<<nblk(ntile), 256, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, tb, chunk, ntile,
+                                                 l->p_tn.as<uint32_t>());
+    b = l->p_tmp.bytes;
+    SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(l->p_tmp.p, b, l->p_tn.as<uint32_t>(), l->p_tfirst.as<uint32_t>(),
+                                              (int)ntile, P));
+    k_plan_chunks<<<nblk(ntile), 256, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, z0, tb, chunk, ntile,
+                                               l->p_tfirst.as<uint32_t>(), pidT, n, p.nch, p.chunk.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+  }
+  l->timer.end(1, e0, P);
+  SWPS_HIP(hipEventRecord(p.ready, P));
+  return SWPS_OK;
+}
+
+// one training step from its plan (the static index's kernels, fed by the plan's slot), then the
+// next step's plan on the plan stream while this one trains
+int lr_batch_planned(swps_lr *l) {
+  if (!l->plan_ready) SWPS_TRY(lr_plan_setup(l));
+  const uint64_t step = l->cursor, nr = l->label.size(), bi = step % l->nbatches;
+  const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1()), nrb = r1 - r0;
+  const uint64_t z0 = l->row_off[r0], nnz = l->row_off[r1] - z0;
+  hipStream_t s = l->s;
+  if (l->plan_next <= step) {
+    SWPS_TRY(lr_plan(l, step));
+    l->plan_next = step + 1;
+  }
+  swps_lr::PlanSlot &p = l->pslot[step & 1];
+  l->cursor++;
+  SWPS_HIP(hipStreamWaitEvent(s, p.ready, 0));
+  if (nnz) {
+    const uint64_t nfc = l->bfchunk[bi + 1] - l->bfchunk[bi];
+    hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
+    const bool hot = l->hot != 0;
+    auto kc = l->fwd_rpt == 4 ? k_lr_forward_c<4> : l->fwd_rpt == 16 ? k_lr_forward_c<16> : k_lr_forward_c<kLrFwdRpt>;
+    hipExtLaunchKernelGGL(kc, dim3((unsigned)nfc), dim3(256), 0, s, fb, fe, 0,
+                          (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi],
+                          (const uint64_t *)l->d_row_off.as<uint64_t>(),
+                          (const uint32_t *)(p.fcode.as<uint32_t>() - z0), (const float *)l->d_fval.as<float>(),
+                          (const float *)l->d_label.as<float>(), r0, (const float *)l->t->rows.as<float>(), 2,
+                          l->d_err.as<float>(), l->d_err2.as<float>(),
+                          hot ? (const uint32_t *)p.hrow.as<uint32_t>() : (const uint32_t *)nullptr,
+                          hot ? l->nhot : 0u);
+    l->timer.ext_end(0, fb, fe);
+    LrReduce ra{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, l->t->rows.as<float>(),
+                l->t->cfg.learning_rate, l->t->cfg.fudge, nullptr, nullptr, nullptr, nullptr, 1,
+                nullptr, nullptr, l->d_err.as<float>()};
+    LrTiles tt{p.trow.as<uint16_t>(), p.tval.as<float>(), p.chunk.as<uint32_t>(), p.tinfo.as<uint32_t>(),
+               p.tdst.as<uint32_t>(), l->d_tpart.as<double>(), l->d_err.as<float>(), r0, nrb, l->tile_bits, 0};
+    hipEvent_t tb0 = l->timer.ext(), te0 = l->timer.ext(), tb1 = l->timer.ext(), te1 = l->timer.ext();
+    auto kt = l->tile_chunk == 512    ? k_lr_tiles<2>
+              : l->tile_chunk == 1024 ? k_lr_tiles<4>
+              : l->tile_chunk == 1280 ? k_lr_tiles<5>
+              : l->tile_chunk == 1536 ? k_lr_tiles<6>
+              : l->tile_chunk == 1792 ? k_lr_tiles<7>
+              : l->tile_chunk == 4096 ? k_lr_tiles<16>
+                                      : k_lr_tiles<8>;
+    if (p.nch) hipExtLaunchKernelGGL(kt, dim3((unsigned)p.nch), dim3(256), 0, s, tb0, te0, 0, ra, tt);
+    // the finisher's counts live on the device: LB blocks stride over the long keys, the rest
+    // over the short ones
+    const uint32_t LB = 256, SB = 512;
+    hipExtLaunchKernelGGL(k_lr_tiles_fin, dim3(LB + SB), dim3(256), 0, s, p.nch ? tb1 : tb0, p.nch ? te1 : te0, 0, ra,
+                          (const uint4 *)p.ms.p, (const uint32_t *)p.msrow.as<uint32_t>(), 0u, (const uint4 *)p.ml.p,
+                          (const uint32_t *)p.mlrow.as<uint32_t>(), 0u, LB, (const double *)l->d_tpart.as<double>(),
+                          (uint64_t)0, (const uint32_t *)p.cnt.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+    l->timer.ext_end(3, tb0, te0);
+    if (p.nch) {
+      l->timer.ext_more(3, tb1, te1);
+    } else if (tb1) {
+      (void)hipEventDestroy(tb1);
+      (void)hipEventDestroy(te1);
+    }
+  }
+  SWPS_HIP(hipEventRecord(p.used, s));
+  p.pending_use = true;
+  if (l->plan_next == step + 1) {  // the next step's plan, beside this step
+    SWPS_TRY(lr_plan(l, step + 1));
+    l->plan_next = step + 2;
+  }
+  return SWPS_OK;
+}
+
 int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr) {
+  if (!l->sharded) {
+    SWPS_TRY(lr_fwd_chunks(l));
+    if (lr_plan_usable(l)) return lr_batch_planned(l);
+  }
+  if (!l->index_built) SWPS_TRY(lr_index(l));  // the static per-batch index, built once
   const uint64_t nr = l->label.size();
   const uint64_t bi = l->cursor % l->nbatches;
   const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1());
@@ -1838,34 +2323,7 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
   const uint32_t mf = l->bmaxf[bi];  // the batch's longest row
   SWPS_TRY(l->d_val_s.ensure((l->max_bnnz + 4) * 4));
   const bool scat = l->fwd_records && l->rows_per_wave == 1 && mf <= 64;  // the forward writes the records
-  if (l->fwd_c && !scat && l->rows_per_wave == 1 && !l->fwd_diag && !l->stage && l->bfchunk.empty()) {
-    // the static chunks of whole rows of every batch, once (rows never span chunks; a row longer
-    // than a chunk's capacity turns the form off)
-    std::vector<uint2> ch;
-    l->fwd_rpt = l->fwd_c == 4 || l->fwd_c == 16 ? l->fwd_c : kLrFwdRpt;  // records per thread (A/B: 4, 8, 16)
-    const uint64_t cap = (uint64_t)l->fwd_rpt * 256;
-    l->bfchunk.assign(1, 0);
-    for (uint64_t b = 0; b < l->nbatches && l->fwd_c; b++) {
-      const uint64_t a0 = b * l->B1(), a1 = std::min<uint64_t>(nr, a0 + l->B1());
-      uint64_t first = a0;
-      for (uint64_t r = a0; r < a1; r++) {
-        if (l->row_off[r + 1] - l->row_off[r] > cap) {
-          l->fwd_c = 0;
-          break;
-        }
-        if (l->row_off[r + 1] - l->row_off[first] > cap) {
-          ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(r - first)));
-          first = r;
-        }
-      }
-      if (a1 > first) ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(a1 - first)));
-      l->bfchunk.push_back(ch.size());
-    }
-    if (l->fwd_c) {
-      SWPS_TRY(upload(l->d_fchunk, ch, s));
-      SWPS_HIP(hipStreamSynchronize(s));  // `ch` is a local
-    }
-  }
+  if (!scat) SWPS_TRY(lr_fwd_chunks(l));
   const uint64_t nfc = l->fwd_c && l->bfchunk.size() > bi + 1 ? l->bfchunk[bi + 1] - l->bfchunk[bi] : 0;
   if (nfc && !scat && l->rows_per_wave == 1 && !l->fwd_diag && !l->stage) {  // record-contiguous chunks of rows
     hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
@@ -2008,7 +2466,7 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
                             nch ? tb1 : tb0, nch ? te1 : te0, 0, ra,
                             (const uint4 *)l->d_tmulti.p + l->bmulti[bi], (const uint32_t *)l->d_tmsrow.as<uint32_t>() + l->bmulti[bi], nm,
                             (const uint4 *)l->d_tmlong.p + l->bmlong[bi], (const uint32_t *)l->d_tmlrow.as<uint32_t>() + l->bmlong[bi], nl,
-                            LB, (const double *)l->d_tpart.as<double>(), (uint64_t)q0);
+                            LB, (const double *)l->d_tpart.as<double>(), (uint64_t)q0, (const uint32_t *)nullptr);
     }
     SWPS_HIP(hipGetLastError());
     if (nch || fin) {
@@ -2121,6 +2579,15 @@ int swps_lr_destroy(swps_lr *l) {
   if (!l) return SWPS_OK;
   (void)hipSetDevice(l->t->cfg.device);
   (void)hipStreamSynchronize(l->s);
+  if (l->ps) {
+    (void)hipStreamSynchronize(l->ps);
+    (void)hipStreamDestroy(l->ps);
+  }
+  for (auto &p : l->pslot) {
+    if (p.ready) (void)hipEventDestroy(p.ready);
+    if (p.used) (void)hipEventDestroy(p.used);
+  }
+  if (l->ev_rows) (void)hipEventDestroy(l->ev_rows);
   l->timer.resolve();
   if (l->h_small) (void)hipHostFree(l->h_small);
   delete l->drv;
@@ -2209,6 +2676,11 @@ int swps_lr_init(swps_lr *l) {
   else
     SWPS_TRY(table_find_or_insert(l->t, dk.as<uint64_t>(), V, l->d_vid_row.as<uint32_t>(), l->s));
   l->rows_mapped = false;  // vid_row changed: k_lr_map_rows again at the next batch
+  if (l->ps) {  // a prefetched plan holds the old shard rows: plan again
+    SWPS_HIP(hipStreamSynchronize(l->ps));
+    l->plan_next = l->cursor;
+  }
+  l->plan_sync = true;
   if (l->cfg.init_ref) {
     // LRPullAccessMethod::init_param (lr.cpp:48-50): w = gen_float() per miss, in first-pull order
     std::vector<uint32_t> vid_row(V), rid;
@@ -2286,6 +2758,7 @@ int swps_lr_train(swps_lr *l, int32_t niters, double *err_out) {
 int swps_lr_sync(swps_lr *l) {
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
   if (l->drv) SWPS_TRY(l->drv->sync());
+  if (l->ps) SWPS_HIP(hipStreamSynchronize(l->ps));  // the prefetched next plan included
   SWPS_HIP(hipStreamSynchronize(l->s));
   l->timer.resolve();
   return SWPS_OK;
@@ -2378,6 +2851,8 @@ int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
   if (l->cfg.init_ref)
     return fail(SWPS_E_UNSUPPORTED, "sharded mode initialises on the owners (init_ref = 0, SWPS_INIT_HASH): the "
                                     "reference's float-LCG order depends on message arrival");
+  SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  if (!l->index_built) SWPS_TRY(lr_index(l));  // the sharded step reads the static index
   std::vector<uint32_t> map(frag_num);
   SWPS_TRY(swps_hashfrag_table(frag_num, world, map.data()));
   const uint64_t V = l->vocab_keys.size(), nb = l->nbatches, nr = l->label.size();

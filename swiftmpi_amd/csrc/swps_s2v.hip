@@ -483,10 +483,22 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   SWPS_TRY(swps_table_size(m->t, &have));
   std::vector<uint64_t> tk(std::max<uint64_t>(have, 1));
   SWPS_TRY(swps_table_keys(m->t, tk.data(), tk.size(), &got));
-  std::unordered_set<uint64_t> present(tk.begin(), tk.begin() + got);
+  FlatMap64 present(got + 1024);
+  for (uint64_t i = 0; i < got; i++) present.at(tk[i]) = 1;
+  // the rand() stream: the draws nobody reads (the WParam a pull constructs for a key the server
+  // already holds, server.h:143-150) are counted and skipped in one jump before the next read
   GlibcRand rnd(m->cfg.rand_seed);
-  for (uint64_t i = 0; i < m->cfg.rand_offset; i++) (void)rnd.next();
+  rnd.discard(m->cfg.rand_offset);
+  uint64_t skip = 0;
+  auto draw = [&]() {
+    if (skip) {
+      rnd.discard(skip);
+      skip = 0;
+    }
+    return rnd.next();
+  };
   auto rand_val = [&](int32_t r) { return ((double)(r / (float)2147483647) - 0.5) / (double)(size_t)D; };
+  std::vector<uint64_t> first_seen;  // the minibatch vocab in first-occurrence order (freq's keys)
   std::vector<uint64_t> miss_keys;
   std::vector<double> miss_rows;     // [h | v | h2 = 0 | v2 = 0] per miss
   std::unordered_set<uint64_t> lk;   // MiniBatch::_local_keys: one object, cleared per minibatch
@@ -503,46 +515,48 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   m->misses = m->max_recs = m->max_docs = 0;
   uint64_t lstate = 2008ULL;  // utils/random.h:44-47
   uint64_t li = 0;
-  std::unordered_map<uint64_t, int32_t> freq;
+  FlatMap64 freq(1 << 16);
   while (true) {
     // gather_keys(file, line_id, B) (word2vec.h:323-377)
     lk.clear();
     freq.clear();
+    first_seen.clear();
     int cnt = 0;
     for (uint64_t j = li; j < nl;) {
       const uint64_t l = j++;
       if (!valid[l]) continue;
       for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) {
-        auto it = freq.find(tok_keys[i]);
-        if (it != freq.end())
-          it->second++;
-        else {
-          freq.emplace(tok_keys[i], 1);
+        bool fresh = false;
+        freq.at(tok_keys[i], &fresh)++;
+        if (fresh) {
+          first_seen.push_back(tok_keys[i]);
           lk.insert(tok_keys[i]);
         }
       }
       if (++cnt > B) break;
     }
     if (lk.size() < 5) break;  // sent2vec.cpp:97
-    if (freq.count(0))
+    if (freq.contains(0))
       return fail(SWPS_E_UNSUPPORTED, "a minibatch vocab holds key 0 (atoi of a non-numeric word): the reference "
                                       "redraws negatives that hit it, a data-dependent draw count");
     // MiniBatch::pull: one WParam (2·D rand()) per pulled key in `_local_keys`
     // order; a miss is inserted with it (server.h:143-150, accessmethod.h:63-70)
     for (uint64_t k : lk) {
-      if (present.count(k)) {
-        for (int i = 0; i < 2 * D; i++) (void)rnd.next();
+      if (present.contains(k)) {
+        skip += 2 * (uint64_t)D;
         continue;
       }
       const size_t o = miss_rows.size();
       miss_rows.resize(o + 4 * (size_t)D, 0.0);
-      for (int i = 0; i < 2 * D; i++) miss_rows[o + i] = rand_val(rnd.next());
-      for (uint64_t i = 0; i < m->cfg.rand_insert_extra; i++) (void)rnd.next();
+      for (int i = 0; i < 2 * D; i++) miss_rows[o + i] = rand_val(draw());
+      skip += m->cfg.rand_insert_extra;
       miss_keys.push_back(k);
-      present.insert(k);
+      present.at(k) = 1;
       m->misses++;
     }
-    std::vector<std::pair<uint64_t, int32_t>> vc(freq.begin(), freq.end());
+    std::vector<std::pair<uint64_t, int32_t>> vc;
+    vc.reserve(first_seen.size());
+    for (uint64_t k : first_seen) vc.emplace_back(k, freq.at(k));
     std::sort(vc.begin(), vc.end());
     std::vector<uint64_t> st;
     s2v_unigram_starts(vc, T, st);
@@ -560,7 +574,7 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
       for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) doc_tok_keys.push_back(tok_keys[i]);
       m->doc_tok.push_back(doc_tok_keys.size());
       m->doc_rec.push_back(m->doc_rec.back() + L * (uint64_t)m->cfg.niters);
-      for (int i = 0; i < D; i++) init.push_back(rnd.next());
+      for (int i = 0; i < D; i++) init.push_back(draw());
       m->doc_lcg.push_back(lstate);
       lstate = lcg_jump(lstate, (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1)), kLcgA, kLcgC);
     }
@@ -572,6 +586,7 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     m->batches.push_back(b);
   }
   m->lstate_end = lstate;
+  rnd.discard(skip);
   m->rand_calls = rnd.produced;  // includes the rand_offset skipped above
   m->nlines = nl;
   m->ntok = doc_tok_keys.size();

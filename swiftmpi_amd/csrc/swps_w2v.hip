@@ -4545,7 +4545,7 @@ int swps_unigram_starts(const uint64_t *keys, const int32_t *counts, uint64_t V,
 
 int swps_glibc_rand(uint32_t seed, uint64_t skip, uint64_t n, int32_t *out) {
   GlibcRand r(seed);
-  for (uint64_t i = 0; i < skip; i++) (void)r.next();
+  r.discard(skip);
   for (uint64_t i = 0; i < n; i++) out[i] = r.next();
   return SWPS_OK;
 }

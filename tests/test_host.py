@@ -53,7 +53,8 @@ def test_hash_functions_match_oracle(lib, oracle_mod):
 
 
 def test_glibc_rand_emulation(lib, oracle_mod):
-    for seed, skip in [(1, 0), (1, 2), (7, 1000), (0, 5)]:
+    # skips of 4096+ take the polynomial jump (GlibcRand::discard), shorter ones step
+    for seed, skip in [(1, 0), (1, 2), (7, 1000), (0, 5), (1, 4096), (3, 4097), (1, 1234567), (9, 30000001)]:
         assert np.array_equal(lib.glibc_rand(3000, seed, skip), oracle_mod.libc_rand(3000, seed, skip))
 
 

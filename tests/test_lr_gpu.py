@@ -527,3 +527,63 @@ def test_lr_forward_groups_bit_identical(lib, gpu, monkeypatch, groups, stage, h
         res.append(out)
     for a, b in zip(res[0], res[1]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("env", [{}, {"SWPS_LR_TILE_BITS": "6"}, {"SWPS_LR_TILE_BITS": "4"},
+                                 {"SWPS_LR_TILE_CHUNK": "512"}, {"SWPS_LR_TILE_CHUNK": "4096"},
+                                 {"SWPS_LR_HOT": "0"}, {"SWPS_LR_NHOT": "1"}])
+def test_lr_plan_step_equals_plan_load(lib, gpu, monkeypatch, env):
+    """The per-step plan (each minibatch's key-sorted index, (tile, key) order, pieces, partial
+    slots and hot keys built on the plan stream beside the previous step; lr.cpp:215-227) trains
+    bit for bit like the index built once at load: errors, weights and AdaGrad sums after 2
+    epochs, on Criteo-shaped rows (hot keys split across blocks) and ragged rows of 1-60
+    features, with default, shrunken (64 / 16 rows) tiles, other block sizes and the hot-key LDS
+    copy off or down to one key."""
+    from swiftmpi_amd.synth import criteo
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    y, off, f, v = criteo(20000, seed=7)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(1, 61, 4000)
+    roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    feat = rng.integers(0, 3000, int(roff[-1])).astype(np.uint32)
+    vals = rng.random(int(roff[-1])).astype(np.float32)
+    yl = (rng.random(4000) < 0.5).astype(np.float32)
+    res = []
+    for plan in ("load", "step", "step"):
+        out = []
+        for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
+            t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+            m = lib.LR(t, minibatch=B, init_ref=False, fast_sums=True, plan=plan)
+            m.load_csr(*data)
+            m.init()
+            out += [m.train(2), m.params()[1], m.params()[2]]
+            m.close()
+            t.close()
+        res.append(out)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+    for a, b in zip(res[1], res[2]):
+        assert np.array_equal(a, b)
+
+
+def test_lr_plan_step_config3_batch(lib, gpu):
+    """At BASELINE config 3's per-GPU batch (65,537 Criteo-shaped rows over 2^24 keys, 3 batches,
+    train_batches in uneven calls so plans are prefetched across calls): the per-step plan =
+    the load-time index, bit for bit."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(3 * 65537, seed=3)
+    res = []
+    for plan in ("load", "step"):
+        t = lib.Table("lr", capacity=1 << 22, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+        m = lib.LR(t, minibatch=65536, init_ref=False, fast_sums=True, plan=plan)
+        m.load_csr(y, off, f, v)
+        m.init()
+        for n in (1, 3, 2):
+            m.train_batches(n)
+        m.sync()
+        res.append(m.params())
+        m.close()
+        t.close()
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
