@@ -650,7 +650,7 @@ def main():
     ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
                     help="w2v: the headline (config 2); lr: config 3 shape; s2v: config 5 shape")
     ap.add_argument("--lr-batch", type=int, default=65536, help="LR rows per GPU per minibatch (config 3)")
-    ap.add_argument("--lr-plan", default="step", choices=["step", "load"],
+    ap.add_argument("--lr-plan", default="step", choices=["step", "load", "none"],
                     help="LR: each minibatch's index built inside its step (beside the previous one; the "
                          "reference gathers per minibatch, lr.cpp:215-227) or once at load for every minibatch")
     ap.add_argument("--lr-exact", action="store_true",

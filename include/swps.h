@@ -486,6 +486,10 @@ typedef struct {
 } swps_lr_cfg;
 #define SWPS_LR_PLAN_STEP 0
 #define SWPS_LR_PLAN_LOAD 1
+/* no index at all (single GPU, fast sums): each record's term e*x_i is added to its key's sum as
+ * a 64-bit fixed-point integer (scale 2^s fixed at load so no sum reaches 2^62) by atomics — exact
+ * integer sums, so deterministic in any order; each key's mean within ~2^-s of the fp64 sum's */
+#define SWPS_LR_PLAN_NONE 2
 
 int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out);
 int swps_lr_destroy(swps_lr *l);

@@ -579,7 +579,7 @@ class LR:
         lr.cpp:215-227's per-minibatch gather; single GPU with fast_sums), "load" every
         minibatch's index once at load (reused each epoch).  Same results."""
         assert table.layout == "lr"
-        plans = {"step": capi.LR_PLAN_STEP, "load": capi.LR_PLAN_LOAD}
+        plans = {"step": capi.LR_PLAN_STEP, "load": capi.LR_PLAN_LOAD, "none": capi.LR_PLAN_NONE}
         if plan not in plans:
             raise ValueError("unknown plan %r (step or load)" % (plan,))
         cfg = capi.LRCfg(minibatch, int(init_ref), int(profile), int(fast_sums), plans[plan])

@@ -20,7 +20,7 @@ INIT_ZERO, INIT_HASH, INIT_FLCG = 0, 1, 2
 KEY_BKDR, KEY_ATOI = 0, 1
 W2V_INIT_REF, W2V_INIT_TABLE = 0, 1
 PUSH_ADAGRAD, PUSH_SGD = 0, 1
-LR_PLAN_STEP, LR_PLAN_LOAD = 0, 1
+LR_PLAN_STEP, LR_PLAN_LOAD, LR_PLAN_NONE = 0, 1, 2
 COMM_ID_BYTES = 128
 
 # swps_transport callbacks (host all-gather / all-to-all-v)

@@ -1258,38 +1258,71 @@ __global__ void k_lr_tile_dst(const uint32_t *__restrict__ tinfo, const uint32_t
 // at a block cut in T order.  In K order a key's pieces appear in T order, so one scan of the
 // piece heads in K order numbers the partial slots in (key, piece) order: the static index's
 // slots.  Same records, pieces, partial slots and sums as the static index: bit-identical.
-__global__ void k_plan_keys(const uint64_t *__restrict__ row_off, uint64_t r0, uint64_t nrb, uint64_t z0,
-                            const int32_t *__restrict__ fvid, uint32_t *__restrict__ key, uint32_t *__restrict__ rid) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nrb) return;
-  for (uint64_t c = row_off[r0 + j]; c < row_off[r0 + j + 1]; c++) {
-    key[c - z0] = (uint32_t)fvid[c];
-    rid[c - z0] = (uint32_t)j;
+constexpr uint32_t kPlanHotBins = 80;  // record counts >= 8 in quarter-octave bins
+__device__ __forceinline__ uint32_t plan_hot_bin(uint32_t recs) {
+  const uint32_t lg = 31u - (uint32_t)__clz(recs);  // recs >= 8: lg >= 3
+  return min(4u * lg + ((recs >> (lg - 2)) & 3u), kPlanHotBins - 1);
+}
+// one block: zero the plan's counters, the hot histogram and hot rows; each tile's first block
+// (the exclusive scan of its kTileChunk-record block counts, from the CSR)
+__global__ __launch_bounds__(1024) void k_plan_reset(const uint64_t *__restrict__ row_off, uint64_t r0, uint64_t nrb,
+                                                     int tb, uint32_t chunk, uint64_t ntile,
+                                                     uint32_t *__restrict__ tfirst, uint32_t *__restrict__ cnt,
+                                                     uint32_t *__restrict__ hist, uint32_t *__restrict__ hrow,
+                                                     uint32_t nhrow) {
+  __shared__ uint32_t part[1024];
+  const uint32_t tid = threadIdx.x;
+  if (tid < 4) cnt[tid] = 0;
+  if (tid < kPlanHotBins) hist[tid] = 0;
+  for (uint32_t q = tid; q < nhrow; q += 1024) hrow[q] = 0;  // unused slots read row 0 (never referenced)
+  const uint64_t per = (ntile + 1023) / 1024, t0 = tid * per, t1 = min(ntile, t0 + per);
+  auto nchunks = [&](uint64_t tl) {
+    const uint64_t rs = r0 + (tl << tb), re = r0 + min(nrb, (tl + 1) << tb);
+    return (uint32_t)((row_off[re] - row_off[rs] + chunk - 1) / chunk);
+  };
+  uint32_t s = 0;
+  for (uint64_t tl = t0; tl < t1; tl++) s += nchunks(tl);
+  part[tid] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan over the threads' sums
+    const uint32_t v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - s;
+  for (uint64_t tl = t0; tl < t1; tl++) {
+    tfirst[tl] = run;
+    run += nchunks(tl);
   }
 }
-__global__ void k_plan_tile(const uint32_t *__restrict__ permK, const uint32_t *__restrict__ rid, uint64_t n, int tb,
-                            uint32_t *__restrict__ tkey) {
+// K order: each record's row (batch-relative) and tile, and whether it starts its key's records in
+// its tile — a (tile, key) run head in T order — carried into the tile sort's values
+__global__ void k_plan_tile(const uint32_t *__restrict__ permK, const uint32_t *__restrict__ ks1,
+                            const uint32_t *__restrict__ rid, uint64_t z0, uint64_t r0, uint64_t n, int tb,
+                            uint32_t *__restrict__ tkey, uint32_t *__restrict__ val2, uint32_t *__restrict__ rowK) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < n) tkey[j] = rid[permK[j]] >> tb;
+  if (j >= n) return;
+  const uint32_t r = rid[z0 + permK[j]] - (uint32_t)r0, tile = r >> tb;
+  bool head = j == 0;
+  if (!head) head = ks1[j] != ks1[j - 1] || ((rid[z0 + permK[j - 1]] - (uint32_t)r0) >> tb) != tile;
+  tkey[j] = tile;
+  rowK[j] = r;
+  val2[j] = (uint32_t)j | (head ? 0x80000000u : 0u);
 }
 // T order: the records' (row in tile | run head, x_i), piece heads (run head or block cut), and
 // every K position's T position
-__global__ void k_plan_torder(const uint32_t *__restrict__ permT, const uint32_t *__restrict__ permK,
-                              const uint32_t *__restrict__ ks1, const uint32_t *__restrict__ rid,
+__global__ void k_plan_torder(const uint32_t *__restrict__ v2s, const uint32_t *__restrict__ tks,
+                              const uint32_t *__restrict__ rowK, const uint32_t *__restrict__ permK,
                               const float *__restrict__ fval, const uint64_t *__restrict__ row_off, uint64_t r0,
                               uint64_t z0, uint64_t n, int tb, uint32_t chunk, uint16_t *__restrict__ trow,
                               float *__restrict__ tval, uint32_t *__restrict__ ph, uint32_t *__restrict__ invT) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  const uint32_t j = permT[t], c = permK[j];
-  const uint32_t r = rid[c], tile = r >> tb, vid = ks1[j];
-  bool head = t == 0;
-  if (!head) {
-    const uint32_t jp = permT[t - 1];
-    head = ks1[jp] != vid || (rid[permK[jp]] >> tb) != tile;
-  }
-  trow[t] = (uint16_t)((r & ((1u << tb) - 1)) | (head ? kTileHead : 0));
-  tval[t] = fval[z0 + c];
+  const uint32_t v = v2s[t], j = v & 0x7FFFFFFFu, tile = tks[t];
+  const bool head = (v >> 31) != 0;
+  trow[t] = (uint16_t)((rowK[j] & ((1u << tb) - 1)) | (head ? kTileHead : 0));
+  tval[t] = fval[z0 + permK[j]];
   const uint64_t ts = row_off[r0 + ((uint64_t)tile << tb)] - z0;  // the tile's first record (T = CSR at tiles)
   ph[t] = (head || (t - ts) % chunk == 0) ? 1u : 0u;
   invT[j] = (uint32_t)t;
@@ -1307,82 +1340,100 @@ __global__ void k_plan_kstart(const uint64_t *__restrict__ pk, uint64_t n, uint3
   const uint32_t k = (uint32_t)pk[j];
   if (j == 0 || (uint32_t)pk[j - 1] != k) kstart[k - 1] = (uint32_t)j;
 }
-constexpr uint32_t kPlanHotBins = 4096;
+// a wave's lanes with `take` get consecutive slots of *ctr (one atomic per wave)
+__device__ __forceinline__ uint32_t wave_claim(bool take, uint32_t *ctr) {
+  const uint64_t m = __ballot(take);
+  if (!m) return 0;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+}
 // per key (grid-stride over the batch's U keys, U on the device): its partial slots, records and
 // shard row; the keys with several pieces into the finisher's lists (any order: each key's
-// partials are summed in slot order whatever its list position); the hot-key histogram
-__global__ void k_plan_kinfo(const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ pk, uint64_t n,
-                             const uint32_t *__restrict__ ks1, const uint32_t *__restrict__ vid_row,
-                             uint32_t *__restrict__ kwhole, uint32_t *__restrict__ krow, uint4 *__restrict__ ms,
-                             uint32_t *__restrict__ msrow, uint4 *__restrict__ ml, uint32_t *__restrict__ mlrow,
-                             uint32_t *__restrict__ cnt, uint32_t *__restrict__ hist) {
-  const uint32_t U = (uint32_t)pk[n - 1];
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < U; k += gridDim.x * blockDim.x) {
-    const uint32_t s = kstart[k], e = k + 1 < U ? kstart[k + 1] : (uint32_t)n;
-    const uint32_t slot0 = (uint32_t)(pk[s] >> 32) - 1, np = (uint32_t)(pk[e - 1] >> 32) - slot0;
-    const uint32_t recs = e - s, row = vid_row[ks1[s]];
-    kwhole[k] = np == 1 ? 1u : 0u;
-    krow[k] = row;
-    if (np > 1) {
-      const bool lng = np > kTileFinShort;
-      const uint32_t q = atomicAdd(&cnt[lng ? 1 : 0], 1u);
-      (lng ? ml : ms)[q] = make_uint4(slot0, np, recs, k);
-      (lng ? mlrow : msrow)[q] = row;
-    }
-    if (hist && recs >= 8) atomicAdd(&hist[min(recs, kPlanHotBins - 1)], 1u);
-  }
-}
-// the hot keys: every key with more records than the threshold bin, then keys of that bin while
-// slots remain (which of those tie keys get in changes nothing but the LDS they are read from)
-__global__ void k_plan_hot_thresh(uint32_t *__restrict__ hist, uint32_t nhot, uint32_t *__restrict__ thr) {
-  __shared__ uint32_t part[256];
-  const int tid = threadIdx.x;
-  constexpr int PER = kPlanHotBins / 256;
-  uint32_t s = 0;  // this thread's bins [tid*PER, (tid+1)*PER)
-  for (int i = 0; i < PER; i++) s += hist[tid * PER + i];
-  part[tid] = s;
+// partials are summed in slot order whatever its list position); the hot-key histogram (per block
+// in LDS, then one atomic per bin)
+__global__ __launch_bounds__(256) void k_plan_kinfo(const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ pk,
+                                                    uint64_t n, const uint32_t *__restrict__ ks1,
+                                                    const uint32_t *__restrict__ vid_row, uint32_t *__restrict__ kwhole,
+                                                    uint32_t *__restrict__ krow, uint4 *__restrict__ ms,
+                                                    uint32_t *__restrict__ msrow, uint4 *__restrict__ ml,
+                                                    uint32_t *__restrict__ mlrow, uint32_t *__restrict__ cnt,
+                                                    uint32_t *__restrict__ hist) {
+  __shared__ uint32_t lh[kPlanHotBins];
+  for (uint32_t b = threadIdx.x; b < kPlanHotBins; b += blockDim.x) lh[b] = 0;
   __syncthreads();
-  if (tid == 0) {
-    uint32_t above = 0;  // keys in bins above the current one
-    int T = 8;
-    bool found = false;
-    for (int q = 255; q >= 0 && !found; q--) {
-      if (above + part[q] < nhot) {
-        above += part[q];
-        continue;
-      }
-      for (int b = q * PER + PER - 1; b >= q * PER; b--) {
-        if (above + hist[b] >= nhot) {
-          T = b;
-          found = true;
-          break;
-        }
-        above += hist[b];
-      }
+  const uint32_t U = (uint32_t)pk[n - 1];
+  const uint32_t stride = gridDim.x * blockDim.x;
+  // every lane runs the same number of iterations (the wave-wide claims need whole waves)
+  for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < U; k0 += stride) {
+    const uint32_t k = k0 + threadIdx.x;
+    const bool on = k < U;
+    uint32_t slot0 = 0, np = 0, recs = 0, row = 0;
+    if (on) {
+      const uint32_t s = kstart[k], e = k + 1 < U ? kstart[k + 1] : (uint32_t)n;
+      slot0 = (uint32_t)(pk[s] >> 32) - 1;
+      np = (uint32_t)(pk[e - 1] >> 32) - slot0;
+      recs = e - s;
+      row = vid_row[ks1[s]];
+      kwhole[k] = np == 1 ? 1u : 0u;
+      krow[k] = row;
     }
-    if (!found) {  // fewer candidates than slots: every key of >= 8 records
-      T = 8;
-      above = 0;
-      for (int b = kPlanHotBins - 1; b > 8; b--) above += hist[b];
+    const bool shrt = on && np > 1 && np <= kTileFinShort, lng = on && np > kTileFinShort;
+    const uint32_t qs = wave_claim(shrt, &cnt[0]), ql = wave_claim(lng, &cnt[1]);
+    if (shrt) {
+      ms[qs] = make_uint4(slot0, np, recs, k);
+      msrow[qs] = row;
     }
-    thr[0] = (uint32_t)T;
-    thr[1] = 0;      // next slot for keys above T
-    thr[2] = above;  // next slot for keys of bin T
+    if (lng) {
+      ml[ql] = make_uint4(slot0, np, recs, k);
+      mlrow[ql] = row;
+    }
+    if (hist && on && recs >= 8) atomicAdd(&lh[plan_hot_bin(recs)], 1u);
   }
+  if (!hist) return;
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kPlanHotBins; b += blockDim.x)
+    if (lh[b]) atomicAdd(&hist[b], lh[b]);
+}
+// the hot keys: every key in a bin above the threshold bin, then keys of that bin while slots
+// remain (which of those get in changes nothing but the LDS they are read from)
+__global__ void k_plan_hot_thresh(const uint32_t *__restrict__ hist, uint32_t nhot, uint32_t *__restrict__ thr) {
+  if (threadIdx.x != 0) return;
+  uint32_t above = 0;
+  int T = -1;
+  for (int b = (int)kPlanHotBins - 1; b >= 0; b--) {
+    if (above + hist[b] >= nhot) {
+      T = b;
+      break;
+    }
+    above += hist[b];
+  }
+  thr[0] = T < 0 ? 0u : (uint32_t)T;  // fewer candidates than slots: all of them (above = their count)
+  thr[1] = 0;                         // next slot for keys above the threshold bin
+  thr[2] = T < 0 ? nhot : above;      // next slot for keys of the threshold bin
+  thr[3] = T < 0 ? 1u : 0u;
 }
 __global__ void k_plan_hot_assign(const uint32_t *__restrict__ kstart, const uint64_t *__restrict__ pk, uint64_t n,
                                   const uint32_t *__restrict__ krow, uint32_t nhot, uint32_t *__restrict__ thr,
                                   int32_t *__restrict__ khot, uint32_t *__restrict__ hrow) {
   const uint32_t U = (uint32_t)pk[n - 1];
+  const uint32_t T = thr[0];
+  const bool all = thr[3] != 0;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < U; k += gridDim.x * blockDim.x) {
     const uint32_t e = k + 1 < U ? kstart[k + 1] : (uint32_t)n;
-    const uint32_t recs = e - kstart[k], bin = min(recs, kPlanHotBins - 1);
+    const uint32_t recs = e - kstart[k];
     int32_t h = -1;
-    if (recs >= 8 && bin > thr[0]) {
-      h = (int32_t)atomicAdd(&thr[1], 1u);
-    } else if (recs >= 8 && bin == thr[0]) {
-      const uint32_t q = atomicAdd(&thr[2], 1u);
-      if (q < nhot) h = (int32_t)q;
+    if (recs >= 8) {
+      const uint32_t b = plan_hot_bin(recs);
+      if (all || b > T) {
+        h = (int32_t)atomicAdd(&thr[1], 1u);
+      } else if (b == T) {
+        const uint32_t q = atomicAdd(&thr[2], 1u);
+        if (q < nhot) h = (int32_t)q;
+      }
     }
     khot[k] = h;
     if (h >= 0) hrow[h] = krow[k];
@@ -1407,32 +1458,224 @@ __global__ void k_plan_records(const uint64_t *__restrict__ pk, const uint32_t *
     tdst[q] = whole ? row : (uint32_t)(v >> 32) - 1;
   }
 }
-// the tiles' blocks: per tile its kTileChunk-record blocks {tile, first / end record, first / end
-// piece}; tfirst = each tile's first block (exclusive scan of the per-tile block counts)
-__global__ void k_plan_tile_nch(const uint64_t *__restrict__ row_off, uint64_t r0, uint64_t nrb, int tb,
-                                uint32_t chunk, uint64_t ntile, uint32_t *__restrict__ tn) {
-  const uint64_t tl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tl >= ntile) return;
-  const uint64_t rs = r0 + (tl << tb), re = r0 + min(nrb, (tl + 1) << tb);
-  tn[tl] = (uint32_t)((row_off[re] - row_off[rs] + chunk - 1) / chunk);
-}
+// the tiles' blocks, a thread per block: {tile, first / end record, first / end piece}
 __global__ void k_plan_chunks(const uint64_t *__restrict__ row_off, uint64_t r0, uint64_t nrb, uint64_t z0, int tb,
                               uint32_t chunk, uint64_t ntile, const uint32_t *__restrict__ tfirst,
                               const uint32_t *__restrict__ pidT, uint64_t n, uint64_t nch, uint32_t *__restrict__ out) {
-  const uint64_t tl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tl >= ntile) return;
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nch) return;
+  uint64_t lo = 0, hi = ntile;  // the last tile whose first block <= q (empty tiles own no block)
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (tfirst[mid] <= q)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  uint64_t tl = lo;
+  while (tl + 1 < ntile && tfirst[tl + 1] <= q) tl++;
   const uint64_t rs = r0 + (tl << tb), re = r0 + min(nrb, (tl + 1) << tb);
-  const uint64_t a = row_off[rs] - z0, b = row_off[re] - z0;
-  uint64_t q = tfirst[tl];
-  const uint32_t S2 = n ? pidT[n - 1] : 0u;
-  for (uint64_t c0 = a; c0 < b; c0 += chunk, q++) {
-    const uint64_t c1 = min(b, c0 + chunk);
-    uint32_t *e = out + q * 5;
-    e[0] = (uint32_t)tl;
-    e[1] = (uint32_t)c0;
-    e[2] = (uint32_t)c1;
-    e[3] = pidT[c0] - 1;
-    e[4] = q + 1 < nch ? (c1 < n ? pidT[c1] - 1 : S2) : S2;
+  const uint64_t b = row_off[re] - z0;
+  const uint64_t c0 = row_off[rs] - z0 + (q - tfirst[tl]) * chunk, c1 = min(b, c0 + chunk);
+  uint32_t *e = out + q * 5;
+  e[0] = (uint32_t)tl;
+  e[1] = (uint32_t)c0;
+  e[2] = (uint32_t)c1;
+  e[3] = pidT[c0] - 1;
+  e[4] = c1 < n ? pidT[c1] - 1 : pidT[n - 1];
+}
+
+// ---- the fixed-point step (swps_lr_cfg.plan = SWPS_LR_PLAN_NONE): no index at all ------------
+// lr.cpp's minibatch as the reference runs it — gather the batch's keys, pull, learn, push the
+// per-key mean — with the per-key gradient sums made order-free instead of sorted: every record's
+// e*x_i (the reference's fp32 `grad`, lr.cpp:368) is added as a 64-bit fixed-point integer
+// (scale 2^s chosen at load so that no sum can overflow: |sum| < 2^62), so the sums are exact
+// integers whatever order the atomics land in — deterministic run to run, and each key's mean
+// float(sum / count) is within a few 2^-s of the fp64 sum's (fast mode's definition).  A block
+// takes a chunk of whole rows (k_lr_forward_c's forward: same products, same ordered fp32 row
+// sums, the same e), then adds its records' terms: the hot keys' (the corpus's most frequent,
+// fixed at load) into LDS, flushed with one global atomic per key per block; the rest straight to
+// the key's accumulator.  The first add to a key (its count was 0) appends its shard row to the
+// batch's pushed-key list; k_lr_fx_apply then applies the mean and AdaGrad to every listed row
+// (lr.cpp:68-75) and clears its accumulator.  Keys are found per record from a per-key code
+// (shard row, or hot rank | kLrHotBit) — the pull's lookup — with no per-batch index.
+template <int RPT>
+__global__ __launch_bounds__(256) void k_lr_fx_step(const uint2 *__restrict__ chunks,
+                                                    const uint64_t *__restrict__ row_off,
+                                                    const int32_t *__restrict__ fvid,
+                                                    const uint32_t *__restrict__ vcode,
+                                                    const float *__restrict__ fval, const float *__restrict__ label,
+                                                    uint64_t r0, const float *__restrict__ rows,
+                                                    const uint32_t *__restrict__ hrow, uint32_t nhot,
+                                                    float *__restrict__ err, float *__restrict__ err2,
+                                                    unsigned long long *__restrict__ acc_sum,
+                                                    uint32_t *__restrict__ acc_cnt, uint32_t *__restrict__ list,
+                                                    uint32_t *__restrict__ list_n, double scale) {
+  constexpr int CAP = RPT * 256;
+  __shared__ float prod[CAP];
+  __shared__ uint16_t rl[CAP];   // each record's row within the chunk
+  __shared__ float es[CAP];      // each row's error
+  __shared__ float wh[kLrHot];
+  __shared__ unsigned long long hs[kLrHot];
+  __shared__ uint32_t hc[kLrHot];
+  const int tid = threadIdx.x;
+  HotW hw;
+  hw.ld(rows, hrow, nhot, tid);
+  for (uint32_t q = (uint32_t)tid; q < nhot; q += 256u) {
+    hs[q] = 0ull;
+    hc[q] = 0u;
+  }
+  const uint2 ch = chunks[blockIdx.x];  // first row (batch-relative), rows
+  const uint64_t rf = r0 + ch.x;
+  const uint64_t c0 = row_off[rf], c1 = row_off[rf + ch.y];
+  const uint32_t n = (uint32_t)(c1 - c0);
+  int32_t f[RPT];
+  float x[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; k++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+    f[k] = i < n ? fvid[c0 + i] : 0;
+    x[k] = i < n ? fval[c0 + i] : 0.f;
+  }
+  uint32_t code[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; k++) code[k] = ((uint32_t)tid + (uint32_t)k * 256u) < n ? vcode[f[k]] : 0u;
+  uint64_t ra = 0, rb = 0;
+  float y = 0.f;
+  if ((uint32_t)tid < ch.y) {
+    ra = row_off[rf + tid];
+    rb = row_off[rf + tid + 1];
+    y = label[rf + tid];
+  }
+  if (hrow) hw.st(wh, nhot, tid);
+  __syncthreads();
+  float w[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; k++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+    w[k] = i >= n ? 0.f : (code[k] & kLrHotBit) ? wh[code[k] & (kLrHotBit - 1)] : rows[(uint64_t)code[k] * 2];
+  }
+#pragma unroll
+  for (int k = 0; k < RPT; k++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+    if (i < n) prod[i] = w[k] * x[k];
+  }
+  for (uint32_t r = (uint32_t)tid; r < ch.y; r += 256u) {  // each record's row
+    const uint64_t a = r < 256u ? ra : row_off[rf + r], b = r < 256u ? rb : row_off[rf + r + 1];
+    for (uint64_t c = a; c < b; c++) rl[c - c0] = (uint16_t)r;
+  }
+  __syncthreads();
+  for (uint32_t r = (uint32_t)tid; r < ch.y; r += 256u) {  // lr.cpp:358-367, in feature order
+    if (r >= 256u) {
+      ra = row_off[rf + r];
+      rb = row_off[rf + r + 1];
+      y = label[rf + r];
+    }
+    float sum = 0.f;
+    for (uint32_t c = (uint32_t)(ra - c0); c < (uint32_t)(rb - c0); c++) sum += prod[c];
+    const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
+    const float error = y - predict;
+    err[rf + r] = error;
+    err2[rf + r] = error * error;
+    es[r] = error;
+  }
+  __syncthreads();
+  // every record's term grad = error * x_i (lr.cpp:368) in fixed point
+#pragma unroll
+  for (int k = 0; k < RPT; k++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+    bool first = false;
+    uint32_t row = 0;
+    if (i < n) {
+      const float g = es[rl[i]] * x[k];
+      const unsigned long long q = (unsigned long long)__double2ll_rn((double)g * scale);
+      if (code[k] & kLrHotBit) {
+        const uint32_t h = code[k] & (kLrHotBit - 1);
+        atomicAdd(&hs[h], q);
+        atomicAdd(&hc[h], 1u);
+      } else {
+        row = code[k];
+        atomicAdd(&acc_sum[row], q);
+        first = atomicAdd(&acc_cnt[row], 1u) == 0u;
+      }
+    }
+    const uint32_t slot = wave_claim(first, list_n);
+    if (first) list[slot] = row;
+  }
+  if (!hrow) return;
+  __syncthreads();
+  for (uint32_t q0 = 0; q0 < nhot; q0 += 256u) {  // the hot keys: one global add per key per block
+    const uint32_t q = q0 + (uint32_t)tid;
+    const uint32_t c = q < nhot ? hc[q] : 0u;
+    bool first = false;
+    uint32_t row = 0;
+    if (c) {
+      row = hrow[q];
+      atomicAdd(&acc_sum[row], hs[q]);
+      first = atomicAdd(&acc_cnt[row], c) == 0u;
+    }
+    const uint32_t slot = wave_claim(first, list_n);
+    if (first) list[slot] = row;
+  }
+}
+
+// the batch's pushed keys: mean = float(sum / count) and AdaGrad on the shard row (lr.cpp:32-38,
+// 68-75), the accumulator cleared for the next batch; zeroes the next batch's list counter
+__global__ __launch_bounds__(256) void k_lr_fx_apply(const uint32_t *__restrict__ list,
+                                                     const uint32_t *__restrict__ list_n,
+                                                     uint32_t *__restrict__ next_n,
+                                                     unsigned long long *__restrict__ acc_sum,
+                                                     uint32_t *__restrict__ acc_cnt, float *__restrict__ rows, float lr,
+                                                     float fudge, double inv_scale) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *next_n = 0u;
+  const uint32_t n = *list_n;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const uint32_t row = list[q];
+    const long long s = (long long)acc_sum[row];
+    const uint32_t c = acc_cnt[row];
+    float *r = rows + (uint64_t)row * 2;
+    const float w = r[0], g2 = r[1];
+    acc_sum[row] = 0ull;
+    acc_cnt[row] = 0u;
+    const float m = (float)(((double)s * inv_scale) / (double)c);
+    const float ng2 = g2 + m * m;
+    const float step = lr * m;
+    r[1] = ng2;
+    r[0] = w + step / sqrtf(ng2 + fudge);
+  }
+}
+// the per-key codes of the fixed-point step: hot rank | kLrHotBit, else the key's shard row
+__global__ void k_lr_fx_codes(const uint32_t *__restrict__ vid_row, uint64_t V, const int32_t *__restrict__ hot_of_vid,
+                              uint32_t *__restrict__ vcode) {
+  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= V) return;
+  const int32_t h = hot_of_vid ? hot_of_vid[v] : -1;
+  vcode[v] = h >= 0 ? (kLrHotBit | (uint32_t)h) : vid_row[v];
+}
+__global__ void k_lr_fx_hrow(const uint32_t *__restrict__ hot_vid, uint32_t nhot, const uint32_t *__restrict__ vid_row,
+                             uint32_t *__restrict__ hrow) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nhot) hrow[q] = vid_row[hot_vid[q]];
+}
+
+// ---- the corpus vocabulary on the GPU (lr_ingest): vid = rank of the key among the distinct keys
+__global__ void k_lr_voc_heads(const uint32_t *__restrict__ ks, uint64_t n, uint32_t *__restrict__ head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1u : 0u;
+}
+// every record's vid; per distinct key its key, its first record (the stable sort keeps CSR order)
+// and its first position in key order (the next key's minus its own = its record count)
+__global__ void k_lr_voc_ids(const uint32_t *__restrict__ ks, const uint32_t *__restrict__ perm,
+                             const uint32_t *__restrict__ rank, uint64_t n, int32_t *__restrict__ fvid,
+                             uint32_t *__restrict__ ukey, uint32_t *__restrict__ ufirst, uint32_t *__restrict__ ustart) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = rank[i] - 1;
+  fvid[perm[i]] = (int32_t)r;
+  if (i == 0 || ks[i] != ks[i - 1]) {
+    ukey[r] = ks[i];
+    ufirst[r] = perm[i];
+    ustart[r] = (uint32_t)i;
   }
 }
 
@@ -1528,7 +1771,9 @@ struct swps_lr {
   std::vector<uint64_t> row_off;
   std::vector<int32_t> fvid;
   std::vector<float> fval;
-  std::vector<uint64_t> vocab_keys;  // vid order = first-pull order
+  std::vector<uint64_t> vocab_keys;  // vid order = key order (lr_vocab)
+  std::vector<uint32_t> vocab_cnt;   // records per key in the corpus
+  std::vector<uint32_t> pull_order;  // init_ref: the vids in the first pull's order (lr.cpp:161-166)
   // the table layout of the single-GPU init: vid -> rank of its new row (SWPS_LR_PLACE=1: by
   // (batch, row tile, key) of first appearance, 2: by (batch, key); 0, the default: the insert's own
   // order).  Same-box A/B at the Criteo step, round 4: the forward's L2-miss reads fell 47.3 ->
@@ -1609,8 +1854,15 @@ struct swps_lr {
     bool pending_use = false;
   };
   PlanSlot pslot[2];
-  swps::DevMem p_key, p_ks1, p_permK, p_rid, p_tkey, p_tks, p_permT, p_ph, p_pidT, p_invT, p_packed, p_pk, p_kstart,
-      p_kwhole, p_krow, p_khot, p_hist, p_thr, p_tn, p_tfirst, p_tmp;
+  swps::DevMem p_ks1, p_permK, p_tkey, p_tks, p_val2, p_v2s, p_rowK, p_ph, p_pidT, p_invT, p_packed, p_pk, p_kstart,
+      p_kwhole, p_krow, p_khot, p_hist, p_thr, p_tfirst, p_tmp;
+  swps::DevMem d_rid;  // the row of every record (per-step plan)
+  // the fixed-point step (cfg.plan == SWPS_LR_PLAN_NONE): per-key codes, hot keys, accumulators
+  bool fx_ready = false;
+  int fx_bits = 40;                      // fixed-point scale 2^fx_bits (load: no sum can reach 2^62)
+  std::vector<uint32_t> fx_hot_vids;     // the corpus's most frequent keys (load)
+  swps::DevMem d_vcode, d_fx_hot, d_fx_hrow, d_acc_sum, d_acc_cnt, d_fx_list, d_fx_n;
+  int plan_sort = 1;   // SWPS_LR_PLAN_SORT: tile shape of the plan's radix sorts (sort_pairs_tiled)
   uint64_t plan_next = 0;  // the first step whose plan is not enqueued yet
   int plan_vbits = 1;
   bool plan_sync = true;  // the next plan waits for the compute stream (shard rows just (re)initialised)
@@ -1941,15 +2193,92 @@ int lr_index(swps_lr *l) {
   return SWPS_OK;
 }
 
+// every record's vid on the host (the sharded schedule, the row placement experiment), once
+int lr_fvid_host(swps_lr *l) {
+  const uint64_t n = l->row_off.empty() ? 0 : l->row_off.back();
+  if (l->fvid.size() == n) return SWPS_OK;
+  l->fvid.resize(n);
+  if (n) SWPS_HIP(hipMemcpyAsync(l->fvid.data(), l->d_fvid.p, n * 4, hipMemcpyDeviceToHost, l->s));
+  SWPS_HIP(hipStreamSynchronize(l->s));
+  return SWPS_OK;
+}
+
+// The corpus vocabulary on the GPU: a stable radix sort of every record's key gives the distinct
+// keys in key order — vid = rank — each key's first record and record count.  The reference's
+// first pull visits lr.cpp:161-166's `_local_keys` (std::unordered_set<unsigned>) in iteration
+// order, which depends only on the order the keys were first inserted: with init_ref, the V
+// distinct keys (not the records) are inserted in first-occurrence order on the host and the
+// iteration order kept as the init's pull order.
+int lr_vocab(swps_lr *l, const std::vector<uint32_t> &feat) {
+  hipStream_t s = l->s;
+  const uint64_t n = feat.size();
+  if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 features per rank");
+  SWPS_TRY(l->d_fvid.ensure(std::max<uint64_t>(n, 1) * 4));
+  l->vocab_keys.clear();
+  l->pull_order.clear();
+  l->vocab_cnt.clear();
+  l->fvid.clear();
+  if (!n) return SWPS_OK;
+  DevMem dfeat, ks, perm, head, rank, ukey, ufirst, ustart, tmp;
+  SWPS_TRY(upload(dfeat, feat, s));
+  SWPS_TRY(ks.ensure(n * 4));
+  SWPS_TRY(perm.ensure(n * 4));
+  size_t b = 0;
+  SWPS_HIP(sort_pairs_iota(nullptr, b, dfeat.as<uint32_t>(), ks.as<uint32_t>(), perm.as<uint32_t>(), n, 32, s));
+  SWPS_TRY(tmp.ensure(b));
+  b = tmp.bytes;
+  SWPS_HIP(sort_pairs_iota(tmp.p, b, dfeat.as<uint32_t>(), ks.as<uint32_t>(), perm.as<uint32_t>(), n, 32, s));
+  dfeat.release();
+  SWPS_TRY(head.ensure(n * 4));
+  SWPS_TRY(rank.ensure(n * 4));
+  k_lr_voc_heads<<<nblk(n), 256, 0, s>>>(ks.as<uint32_t>(), n, head.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  SWPS_TRY(lr_scan_incl(head.as<uint32_t>(), rank.as<uint32_t>(), n, tmp, s));
+  uint32_t V = 0;
+  SWPS_HIP(hipMemcpyAsync(&V, rank.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipStreamSynchronize(s));
+  SWPS_TRY(ukey.ensure((uint64_t)V * 4));
+  SWPS_TRY(ufirst.ensure((uint64_t)V * 4));
+  SWPS_TRY(ustart.ensure((uint64_t)V * 4));
+  k_lr_voc_ids<<<nblk(n), 256, 0, s>>>(ks.as<uint32_t>(), perm.as<uint32_t>(), rank.as<uint32_t>(), n,
+                                       l->d_fvid.as<int32_t>(), ukey.as<uint32_t>(), ufirst.as<uint32_t>(),
+                                       ustart.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
+  std::vector<uint32_t> uk(V), us(V);
+  SWPS_HIP(hipMemcpyAsync(uk.data(), ukey.p, (uint64_t)V * 4, hipMemcpyDeviceToHost, s));
+  SWPS_HIP(hipMemcpyAsync(us.data(), ustart.p, (uint64_t)V * 4, hipMemcpyDeviceToHost, s));
+  std::vector<uint32_t> order;
+  if (l->cfg.init_ref) {  // the distinct keys by first occurrence
+    DevMem fs, ord;
+    SWPS_TRY(fs.ensure((uint64_t)V * 4));
+    SWPS_TRY(ord.ensure((uint64_t)V * 4));
+    int fb = 1;
+    while ((1ULL << fb) < n) fb++;
+    b = 0;
+    SWPS_HIP(sort_pairs_iota(nullptr, b, ufirst.as<uint32_t>(), fs.as<uint32_t>(), ord.as<uint32_t>(), V, fb, s));
+    SWPS_TRY(tmp.ensure(b));
+    b = tmp.bytes;
+    SWPS_HIP(sort_pairs_iota(tmp.p, b, ufirst.as<uint32_t>(), fs.as<uint32_t>(), ord.as<uint32_t>(), V, fb, s));
+    order.resize(V);
+    SWPS_HIP(hipMemcpyAsync(order.data(), ord.p, (uint64_t)V * 4, hipMemcpyDeviceToHost, s));
+  }
+  SWPS_HIP(hipStreamSynchronize(s));
+  l->vocab_keys.assign(uk.begin(), uk.end());
+  l->vocab_cnt.resize(V);
+  for (uint32_t r = 0; r < V; r++) l->vocab_cnt[r] = (r + 1 < V ? us[r + 1] : (uint32_t)n) - us[r];
+  if (l->cfg.init_ref) {
+    std::unordered_set<uint32_t> K0;  // default-constructed, grown by inserts: the reference's buckets
+    for (uint32_t r : order) K0.insert(uk[r]);
+    l->pull_order.reserve(V);
+    for (uint32_t k : K0) l->pull_order.push_back((uint32_t)(std::lower_bound(uk.begin(), uk.end(), k) - uk.begin()));
+  }
+  return SWPS_OK;
+}
+
 int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
-  std::unordered_set<uint32_t> K0;
-  for (auto f : feat) K0.insert(f);
-  l->vocab_keys.assign(K0.begin(), K0.end());
-  std::unordered_map<uint32_t, int32_t> vid;
-  vid.reserve(K0.size() * 2);
-  for (size_t i = 0; i < l->vocab_keys.size(); i++) vid[(uint32_t)l->vocab_keys[i]] = (int32_t)i;
-  l->fvid.resize(feat.size());
-  for (size_t i = 0; i < feat.size(); i++) l->fvid[i] = vid[feat[i]];
+  SWPS_TRY(lr_vocab(l, feat));
+  feat.clear();
+  feat.shrink_to_fit();
   const uint64_t nr = l->label.size();
   l->nbatches = nr ? (nr + l->B1() - 1) / l->B1() : 0;
   // the rows the single-GPU init gives the keys (swps_lr_init): in the order the keys first appear,
@@ -1960,6 +2289,7 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   // touching one line per key in a table of millions of rows
   l->vid_place.clear();
   if (l->place) {
+    SWPS_TRY(lr_fvid_host(l));
     const uint64_t B1 = l->B1(), V = l->vocab_keys.size();
     const uint64_t ntile = (B1 + (1ULL << l->tile_bits) - 1) >> l->tile_bits;
     std::vector<uint64_t> grp(V, ~0ull);
@@ -1977,7 +2307,6 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   hipStream_t s = l->s;
   SWPS_TRY(upload(l->d_label, l->label, s));
   SWPS_TRY(upload(l->d_row_off, l->row_off, s));
-  SWPS_TRY(upload(l->d_fvid, l->fvid, s));
   SWPS_TRY(upload(l->d_fval, l->fval, s));
   SWPS_TRY(l->d_vid_row.ensure(std::max<size_t>(1, l->vocab_keys.size()) * 4));
   SWPS_TRY(l->d_err.ensure((std::max<uint64_t>(1, nr) + 4) * 4));  // + slack: k_lr_tiles' 16-B loads
@@ -1998,7 +2327,26 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   l->index_built = false;
   l->plan_ready = false;
   l->plan_next = 0;
-  if (!(l->cfg.plan == SWPS_LR_PLAN_STEP && l->cfg.fast_sums && l->tiles)) SWPS_TRY(lr_index(l));
+  l->fx_ready = false;
+  if (l->cfg.plan == SWPS_LR_PLAN_NONE && l->cfg.fast_sums) {
+    // the fixed-point step: its scale (every sum below 2^62: |e| <= max|y| + 1, at most the batch's
+    // records per key) and the corpus's most frequent keys (their sums go through LDS)
+    float mx = 0.f, my = 0.f;
+    for (float v : l->fval) mx = std::max(mx, std::fabs(v));
+    for (float v : l->label) my = std::max(my, std::fabs(v));
+    const double bound = std::max(1e-30, ((double)my + 1.0) * (double)mx * (double)std::max<uint64_t>(l->max_bnnz, 1));
+    l->fx_bits = (int)std::min(40.0, std::floor(62.0 - std::log2(bound)));
+    const std::vector<uint32_t> &cnt = l->vocab_cnt;
+    std::vector<uint32_t> ord;
+    for (uint32_t v = 0; v < cnt.size(); v++)
+      if (cnt[v] >= 8) ord.push_back(v);
+    const size_t h = std::min<size_t>(ord.size(), (size_t)l->nhot);
+    std::partial_sort(ord.begin(), ord.begin() + h, ord.end(),
+                      [&](uint32_t a, uint32_t b) { return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b; });
+    l->fx_hot_vids.assign(ord.begin(), ord.begin() + h);
+  }
+  if (!((l->cfg.plan == SWPS_LR_PLAN_STEP || l->cfg.plan == SWPS_LR_PLAN_NONE) && l->cfg.fast_sums && l->tiles))
+    SWPS_TRY(lr_index(l));
   l->rows_mapped = false;
   SWPS_HIP(hipStreamSynchronize(s));
   l->loaded = true;
@@ -2045,6 +2393,75 @@ bool lr_plan_usable(const swps_lr *l) {
          l->tile_threads == 256 && l->nbatches > 0;
 }
 
+bool lr_fx_usable(const swps_lr *l) {
+  return l->cfg.plan == SWPS_LR_PLAN_NONE && !l->sharded && l->cfg.fast_sums && l->fwd_c && l->rows_per_wave == 1 &&
+         !l->fwd_diag && !l->stage && l->nbatches > 0 && l->fwd_rpt == kLrFwdRpt;
+}
+
+// one batch of the fixed-point step: k_lr_fx_step over the batch's chunks of whole rows, then
+// k_lr_fx_apply over its pushed keys
+int lr_batch_fx(swps_lr *l) {
+  hipStream_t s = l->s;
+  const uint64_t V = std::max<uint64_t>(l->vocab_keys.size(), 1), cap = l->t->cfg.capacity;
+  if (!l->fx_ready) {  // the per-key codes (shard rows are fixed from swps_lr_init on) and buffers
+    const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
+    const uint32_t nh = hot ? (uint32_t)l->fx_hot_vids.size() : 0u;
+    SWPS_TRY(l->d_vcode.ensure(V * 4));
+    SWPS_TRY(l->d_fx_hrow.ensure(kLrHot * 4));
+    std::vector<int32_t> hov;
+    if (hot) {
+      hov.assign(V, -1);
+      for (uint32_t q = 0; q < nh; q++) hov[l->fx_hot_vids[q]] = (int32_t)q;
+    }
+    DevMem dhov;
+    if (hot) {
+      SWPS_TRY(upload(dhov, hov, s));
+      SWPS_TRY(upload(l->d_fx_hot, l->fx_hot_vids, s));
+      k_lr_fx_hrow<<<nblk(nh), 256, 0, s>>>(l->d_fx_hot.as<uint32_t>(), nh, l->d_vid_row.as<uint32_t>(),
+                                            l->d_fx_hrow.as<uint32_t>());
+    }
+    k_lr_fx_codes<<<nblk(V), 256, 0, s>>>(l->d_vid_row.as<uint32_t>(), l->vocab_keys.size(),
+                                          hot ? dhov.as<int32_t>() : nullptr, l->d_vcode.as<uint32_t>());
+    SWPS_HIP(hipGetLastError());
+    if (!l->d_acc_sum.p) {
+      SWPS_TRY(l->d_acc_sum.ensure(cap * 8));
+      SWPS_TRY(l->d_acc_cnt.ensure(cap * 4));
+      SWPS_HIP(hipMemsetAsync(l->d_acc_sum.p, 0, cap * 8, s));
+      SWPS_HIP(hipMemsetAsync(l->d_acc_cnt.p, 0, cap * 4, s));
+    }
+    SWPS_TRY(l->d_fx_list.ensure(std::max<uint64_t>(l->max_bnnz, 1) * 4));
+    SWPS_TRY(l->d_fx_n.ensure(16));
+    SWPS_HIP(hipMemsetAsync(l->d_fx_n.p, 0, 16, s));
+    SWPS_HIP(hipStreamSynchronize(s));  // dhov
+    l->fx_ready = true;
+  }
+  const uint64_t step = l->cursor, nr = l->label.size(), bi = step % l->nbatches;
+  const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1());
+  l->cursor++;
+  if (l->row_off[r1] == l->row_off[r0]) return SWPS_OK;
+  const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
+  const uint64_t nfc = l->bfchunk[bi + 1] - l->bfchunk[bi];
+  uint32_t *cur = l->d_fx_n.as<uint32_t>() + (step & 1), *next = l->d_fx_n.as<uint32_t>() + ((step + 1) & 1);
+  hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
+  hipExtLaunchKernelGGL(k_lr_fx_step<kLrFwdRpt>, dim3((unsigned)nfc), dim3(256), 0, s, fb, fe, 0,
+                        (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi],
+                        (const uint64_t *)l->d_row_off.as<uint64_t>(), (const int32_t *)l->d_fvid.as<int32_t>(),
+                        (const uint32_t *)l->d_vcode.as<uint32_t>(), (const float *)l->d_fval.as<float>(),
+                        (const float *)l->d_label.as<float>(), r0, (const float *)l->t->rows.as<float>(),
+                        hot ? (const uint32_t *)l->d_fx_hrow.as<uint32_t>() : (const uint32_t *)nullptr,
+                        hot ? (uint32_t)l->fx_hot_vids.size() : 0u, l->d_err.as<float>(), l->d_err2.as<float>(),
+                        l->d_acc_sum.as<unsigned long long>(), l->d_acc_cnt.as<uint32_t>(),
+                        l->d_fx_list.as<uint32_t>(), cur, std::ldexp(1.0, l->fx_bits));
+  l->timer.ext_end(0, fb, fe);
+  hipEvent_t ab = l->timer.ext(), ae = l->timer.ext();
+  hipExtLaunchKernelGGL(k_lr_fx_apply, dim3(512), dim3(256), 0, s, ab, ae, 0, (const uint32_t *)l->d_fx_list.as<uint32_t>(),
+                        (const uint32_t *)cur, next, l->d_acc_sum.as<unsigned long long>(), l->d_acc_cnt.as<uint32_t>(),
+                        l->t->rows.as<float>(), l->t->cfg.learning_rate, l->t->cfg.fudge, std::ldexp(1.0, -l->fx_bits));
+  SWPS_HIP(hipGetLastError());
+  l->timer.ext_end(3, ab, ae);
+  return SWPS_OK;
+}
+
 int lr_plan_setup(swps_lr *l) {
   const uint64_t n = std::max<uint64_t>(l->max_bnnz, 1), V = std::max<uint64_t>(l->vocab_keys.size(), 1);
   const uint64_t B1 = l->B1(), ntile = (B1 + (1ULL << l->tile_bits) - 1) >> l->tile_bits;
@@ -2053,6 +2470,7 @@ int lr_plan_setup(swps_lr *l) {
   l->plan_vbits = vb;
   int tbits = 1;
   while ((1ULL << tbits) < ntile) tbits++;
+  if (const char *e = getenv("SWPS_LR_PLAN_SORT")) l->plan_sort = atoi(e);  // tile shape of the plan's sorts (A/B)
   if (!l->ps) SWPS_HIP(hipStreamCreateWithFlags(&l->ps, hipStreamNonBlocking));
   for (auto &p : l->pslot) {
     if (!p.ready) SWPS_HIP(hipEventCreateWithFlags(&p.ready, hipEventDisableTiming));
@@ -2068,27 +2486,31 @@ int lr_plan_setup(swps_lr *l) {
     SWPS_TRY(p.ml.ensure(n * 16));
     SWPS_TRY(p.mlrow.ensure(n * 4));
     SWPS_TRY(p.cnt.ensure(16));
-    // blocks per batch: at most ntile + records / chunk
-    SWPS_TRY(p.chunk.ensure((ntile + n / l->tile_chunk + 1) * 5 * 4));
+    SWPS_TRY(p.chunk.ensure((ntile + n / l->tile_chunk + 1) * 5 * 4));  // blocks: <= tiles + records / chunk
   }
-  for (DevMem *m : {&l->p_key, &l->p_ks1, &l->p_permK, &l->p_rid, &l->p_tkey, &l->p_tks, &l->p_permT, &l->p_ph,
+  for (DevMem *m : {&l->p_ks1, &l->p_permK, &l->p_tkey, &l->p_tks, &l->p_val2, &l->p_v2s, &l->p_rowK, &l->p_ph,
                     &l->p_pidT, &l->p_invT, &l->p_kstart, &l->p_kwhole, &l->p_krow, &l->p_khot})
     SWPS_TRY(m->ensure(n * 4));
   SWPS_TRY(l->p_packed.ensure(n * 8));
   SWPS_TRY(l->p_pk.ensure(n * 8));
   SWPS_TRY(l->p_hist.ensure(kPlanHotBins * 4));
   SWPS_TRY(l->p_thr.ensure(16));
-  SWPS_TRY(l->p_tn.ensure(ntile * 4 + 4));
   SWPS_TRY(l->p_tfirst.ensure(ntile * 4 + 4));
+  // the row of every record (the CSR expanded once, like row_off itself)
+  const uint64_t nr = l->label.size(), N = l->row_off[nr];
+  SWPS_TRY(l->d_rid.ensure(std::max<uint64_t>(N, 1) * 4));
+  k_lr_rowid<<<nblk(nr), 256, 0, l->s>>>(l->d_row_off.as<uint64_t>(), nr, l->d_rid.as<uint32_t>());
+  SWPS_HIP(hipGetLastError());
   // temporary storage for the largest of the plan's sorts and scans (sized once: a grow inside a
   // step would free memory the other stream may still use)
   size_t b = 0, mx = 0;
-  SWPS_HIP(sort_pairs_iota(nullptr, b, l->p_key.as<uint32_t>(), l->p_ks1.as<uint32_t>(), l->p_permK.as<uint32_t>(),
-                           n, vb, l->ps));
+  const rocprim::counting_iterator<uint32_t> iota(0u);
+  SWPS_HIP(sort_pairs_tiled(l->plan_sort, nullptr, b, l->p_ks1.as<uint32_t>(), l->p_ks1.as<uint32_t>(), iota,
+                            l->p_permK.as<uint32_t>(), n, vb, l->ps));
   mx = std::max(mx, b);
   b = 0;
-  SWPS_HIP(sort_pairs_iota(nullptr, b, l->p_tkey.as<uint32_t>(), l->p_tks.as<uint32_t>(), l->p_permT.as<uint32_t>(),
-                           n, tbits, l->ps));
+  SWPS_HIP(sort_pairs_tiled(l->plan_sort, nullptr, b, l->p_tkey.as<uint32_t>(), l->p_tks.as<uint32_t>(),
+                            (const uint32_t *)l->p_val2.as<uint32_t>(), l->p_v2s.as<uint32_t>(), n, tbits, l->ps));
   mx = std::max(mx, b);
   b = 0;
   SWPS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b, l->p_ph.as<uint32_t>(), l->p_pidT.as<uint32_t>(), (int)n,
@@ -2097,10 +2519,6 @@ int lr_plan_setup(swps_lr *l) {
   b = 0;
   SWPS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, b, l->p_packed.as<uint64_t>(), l->p_pk.as<uint64_t>(), (int)n,
                                             l->ps));
-  mx = std::max(mx, b);
-  b = 0;
-  SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b, l->p_tn.as<uint32_t>(), l->p_tfirst.as<uint32_t>(),
-                                            (int)ntile, l->ps));
   mx = std::max(mx, b);
   SWPS_TRY(l->p_tmp.ensure(mx));
   SWPS_TRY(l->d_tpart.ensure(n * 8));
@@ -2120,13 +2538,13 @@ int lr_plan(swps_lr *l, uint64_t step) {
   const uint64_t ntile = (nrb + (1ULL << tb) - 1) >> tb;
   hipStream_t P = l->ps;
   if (p.pending_use) SWPS_HIP(hipStreamWaitEvent(P, p.used, 0));  // its reader, step - 2, is done
+  p.pending_use = false;
   if (l->plan_sync) {  // the plan reads the shard rows of the vids (swps_lr_init, compute stream)
     if (!l->ev_rows) SWPS_HIP(hipEventCreateWithFlags(&l->ev_rows, hipEventDisableTiming));
     SWPS_HIP(hipEventRecord(l->ev_rows, l->s));
     SWPS_HIP(hipStreamWaitEvent(P, l->ev_rows, 0));
     l->plan_sync = false;
   }
-  p.pending_use = false;
   p.nch = 0;
   for (uint64_t tl = 0; tl < ntile; tl++) {  // the tiles launch's grid (host: the batch's CSR offsets)
     const uint64_t rs = r0 + (tl << tb), re = r0 + std::min<uint64_t>(nrb, (tl + 1) << tb);
@@ -2136,20 +2554,27 @@ int lr_plan(swps_lr *l, uint64_t step) {
   if (n) {
     int tbits = 1;
     while ((1ULL << tbits) < ntile) tbits++;
-    uint32_t *key = l->p_key.as<uint32_t>(), *ks1 = l->p_ks1.as<uint32_t>(), *permK = l->p_permK.as<uint32_t>();
-    uint32_t *rid = l->p_rid.as<uint32_t>(), *tkey = l->p_tkey.as<uint32_t>(), *permT = l->p_permT.as<uint32_t>();
+    uint32_t *ks1 = l->p_ks1.as<uint32_t>(), *permK = l->p_permK.as<uint32_t>();
+    uint32_t *tkey = l->p_tkey.as<uint32_t>(), *val2 = l->p_val2.as<uint32_t>(), *v2s = l->p_v2s.as<uint32_t>();
     uint32_t *ph = l->p_ph.as<uint32_t>(), *pidT = l->p_pidT.as<uint32_t>(), *invT = l->p_invT.as<uint32_t>();
     uint64_t *packed = l->p_packed.as<uint64_t>(), *pk = l->p_pk.as<uint64_t>();
-    k_plan_keys<<<nblk(nrb), 256, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, z0, l->d_fvid.as<int32_t>(), key,
-                                           rid);
+    const bool hot = l->hot != 0;
+    k_plan_reset<<<1, 1024, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, tb, chunk, ntile,
+                                    l->p_tfirst.as<uint32_t>(), p.cnt.as<uint32_t>(), l->p_hist.as<uint32_t>(),
+                                    p.hrow.as<uint32_t>(), hot ? (uint32_t)kLrHot : 0u);
     SWPS_HIP(hipGetLastError());
-    size_t b = l->p_tmp.bytes;
-    SWPS_HIP(sort_pairs_iota(l->p_tmp.p, b, key, ks1, permK, n, l->plan_vbits, P));  // K order
-    k_plan_tile<<<nblk(n), 256, 0, P>>>(permK, rid, n, tb, tkey);
-    b = l->p_tmp.bytes;
-    SWPS_HIP(sort_pairs_iota(l->p_tmp.p, b, tkey, l->p_tks.as<uint32_t>(), permT, n, tbits, P));  // T order
-    k_plan_torder<<<nblk(n), 256, 0, P>>>(permT, permK, ks1, rid, l->d_fval.as<float>(), l->d_row_off.as<uint64_t>(),
-                                           r0, z0, n, tb, chunk, p.trow.as<uint16_t>(), p.tval.as<float>(), ph, invT);
+    const rocprim::counting_iterator<uint32_t> iota(0u);
+    size_t b = l->p_tmp.bytes;  // K order: the batch's records stable by vid, straight from the CSR
+    SWPS_HIP(sort_pairs_tiled(l->plan_sort, l->p_tmp.p, b, (const uint32_t *)(l->d_fvid.as<int32_t>() + z0), ks1,
+                              iota, permK, n, l->plan_vbits, P));
+    k_plan_tile<<<nblk(n), 256, 0, P>>>(permK, ks1, l->d_rid.as<uint32_t>(), z0, r0, n, tb, tkey, val2,
+                                         l->p_rowK.as<uint32_t>());
+    b = l->p_tmp.bytes;  // T order: K order stable by tile
+    SWPS_HIP(sort_pairs_tiled(l->plan_sort, l->p_tmp.p, b, (const uint32_t *)tkey, l->p_tks.as<uint32_t>(),
+                              (const uint32_t *)val2, v2s, n, tbits, P));
+    k_plan_torder<<<nblk(n), 256, 0, P>>>(v2s, l->p_tks.as<uint32_t>(), l->p_rowK.as<uint32_t>(), permK,
+                                           l->d_fval.as<float>(), l->d_row_off.as<uint64_t>(), r0, z0, n, tb, chunk,
+                                           p.trow.as<uint16_t>(), p.tval.as<float>(), ph, invT);
     SWPS_HIP(hipGetLastError());
     b = l->p_tmp.bytes;
     SWPS_HIP(hipcub::DeviceScan::InclusiveSum(l->p_tmp.p, b, ph, pidT, (int)n, P));
@@ -2157,31 +2582,20 @@ int lr_plan(swps_lr *l, uint64_t step) {
     b = l->p_tmp.bytes;
     SWPS_HIP(hipcub::DeviceScan::InclusiveSum(l->p_tmp.p, b, packed, pk, (int)n, P));
     k_plan_kstart<<<nblk(n), 256, 0, P>>>(pk, n, l->p_kstart.as<uint32_t>());
-    SWPS_HIP(hipMemsetAsync(p.cnt.p, 0, 16, P));
-    const bool hot = l->hot != 0;
-    if (hot) {
-      SWPS_HIP(hipMemsetAsync(l->p_hist.p, 0, kPlanHotBins * 4, P));
-      SWPS_HIP(hipMemsetAsync(p.hrow.p, 0, kLrHot * 4, P));  // unused slots read row 0 (never referenced)
-    }
-    const unsigned kg = std::min<unsigned>(nblk(n), 2048);
+    const unsigned kg = std::min<unsigned>(nblk(n), 512);
     k_plan_kinfo<<<kg, 256, 0, P>>>(l->p_kstart.as<uint32_t>(), pk, n, ks1, l->d_vid_row.as<uint32_t>(),
                                      l->p_kwhole.as<uint32_t>(), l->p_krow.as<uint32_t>(), (uint4 *)p.ms.p,
                                      p.msrow.as<uint32_t>(), (uint4 *)p.ml.p, p.mlrow.as<uint32_t>(),
                                      p.cnt.as<uint32_t>(), hot ? l->p_hist.as<uint32_t>() : nullptr);
     if (hot) {
-      k_plan_hot_thresh<<<1, 256, 0, P>>>(l->p_hist.as<uint32_t>(), l->nhot, l->p_thr.as<uint32_t>());
+      k_plan_hot_thresh<<<1, 64, 0, P>>>(l->p_hist.as<uint32_t>(), l->nhot, l->p_thr.as<uint32_t>());
       k_plan_hot_assign<<<kg, 256, 0, P>>>(l->p_kstart.as<uint32_t>(), pk, n, l->p_krow.as<uint32_t>(), l->nhot,
                                             l->p_thr.as<uint32_t>(), l->p_khot.as<int32_t>(), p.hrow.as<uint32_t>());
     }
     k_plan_records<<<nblk(n), 256, 0, P>>>(pk, permK, invT, pidT, n, l->p_kwhole.as<uint32_t>(),
                                             l->p_krow.as<uint32_t>(), hot ? l->p_khot.as<int32_t>() : nullptr,
                                             p.fcode.as<uint32_t>(), p.tinfo.as<uint32_t>(), p.tdst.as<uint32_t>());
-    k_plan_tile_nch<<<nblk(ntile), 256, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, tb, chunk, ntile,
-                                                 l->p_tn.as<uint32_t>());
-    b = l->p_tmp.bytes;
-    SWPS_HIP(hipcub::DeviceScan::ExclusiveSum(l->p_tmp.p, b, l->p_tn.as<uint32_t>(), l->p_tfirst.as<uint32_t>(),
-                                              (int)ntile, P));
-    k_plan_chunks<<<nblk(ntile), 256, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, z0, tb, chunk, ntile,
+    k_plan_chunks<<<nblk(p.nch), 256, 0, P>>>(l->d_row_off.as<uint64_t>(), r0, nrb, z0, tb, chunk, ntile,
                                                l->p_tfirst.as<uint32_t>(), pidT, n, p.nch, p.chunk.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
   }
@@ -2261,6 +2675,7 @@ int lr_batch_planned(swps_lr *l) {
 int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr) {
   if (!l->sharded) {
     SWPS_TRY(lr_fwd_chunks(l));
+    if (lr_fx_usable(l)) return lr_batch_fx(l);
     if (lr_plan_usable(l)) return lr_batch_planned(l);
   }
   if (!l->index_built) SWPS_TRY(lr_index(l));  // the static per-batch index, built once
@@ -2681,6 +3096,7 @@ int swps_lr_init(swps_lr *l) {
     l->plan_next = l->cursor;
   }
   l->plan_sync = true;
+  l->fx_ready = false;  // the fixed-point step's per-key codes hold shard rows
   if (l->cfg.init_ref) {
     // LRPullAccessMethod::init_param (lr.cpp:48-50): w = gen_float() per miss, in first-pull order
     std::vector<uint32_t> vid_row(V), rid;
@@ -2690,7 +3106,8 @@ int swps_lr_init(swps_lr *l) {
     rows.reserve(V * 2);
     rid.reserve(V);
     uint64_t y = std::numeric_limits<unsigned long>::max() / 2;
-    for (uint64_t i = 0; i < V; i++) {
+    for (uint64_t j = 0; j < V; j++) {
+      const uint64_t i = l->pull_order.size() == V ? l->pull_order[j] : j;  // first-pull order
       if (!pre.empty() && pre[i] != kNoRow) continue;
       y = y * kFlcgA + kLcgC;
       rows.push_back(flcg_value(y));
@@ -2858,6 +3275,7 @@ int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
   const uint64_t V = l->vocab_keys.size(), nb = l->nbatches, nr = l->label.size();
   std::vector<int32_t> owner(V);
   for (uint64_t i = 0; i < V; i++) owner[i] = (int32_t)map[fmix64(l->vocab_keys[i]) % (uint64_t)frag_num] - 1;
+  SWPS_TRY(lr_fvid_host(l));
   // per batch: unique vids in owner order, then vid order (counting sort by owner)
   std::vector<uint64_t> stamp(V, ~0ULL);
   std::vector<int32_t> uniq;

@@ -111,6 +111,34 @@ inline hipError_t sort_pairs_iota(void *tmp, size_t &bytes, const K *kin, K *kou
   return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);
 }
 
+// Explicit tile shapes for mid-size sorts (the LR per-step plan: ~2.5M records per minibatch):
+// rocPRIM's default 1024 x 16-item tiles leave ~150 workgroups per onesweep pass for 256 CUs.
+// mode 1: 256 x 8 items, 2: 512 x 8, 3: 256 x 16, else rocPRIM's default (8-bit digits throughout)
+template <unsigned BS, unsigned IPT>
+using OnesweepTile = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<BS, IPT>, rocprim::kernel_config<BS, IPT>, 8,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+template <typename K, typename VI, typename V>
+inline hipError_t sort_pairs_tiled(int mode, void *tmp, size_t &bytes, const K *kin, K *kout, VI vin, V *vout,
+                                   uint64_t n, int bits, hipStream_t s) {
+  switch (mode) {
+    case 1:
+      return rocprim::radix_sort_pairs<OnesweepTile<256, 8>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                             (unsigned)bits, s);
+    case 2:
+      return rocprim::radix_sort_pairs<OnesweepTile<512, 8>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                             (unsigned)bits, s);
+    case 3:
+      return rocprim::radix_sort_pairs<OnesweepTile<256, 16>>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                              (unsigned)bits, s);
+    default:
+      return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits,
+                                                    s);
+  }
+}
+
 // keys-only form (same onesweep configuration)
 template <typename K>
 inline hipError_t sort_keys(void *tmp, size_t &bytes, const K *kin, K *kout, uint64_t n, int bits, hipStream_t s) {

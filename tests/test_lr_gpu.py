@@ -159,8 +159,9 @@ def test_lr_criteo_shape_properties(lib, gpu):
     assert np.isfinite(ws[0]).all() and errs[0][2] < errs[0][0]
 
 
+@pytest.mark.parametrize("plan", ["step", "none"])
 @pytest.mark.parametrize("B", [200, 1604])
-def test_lr_fast_sums_within_1e5_of_oracle(lib, oracle_mod, gpu, B):
+def test_lr_fast_sums_within_1e5_of_oracle(lib, oracle_mod, gpu, B, plan):
     """Fast mode (fp64 per-key sums, long runs tree-reduced over a wave
     instead of the reference's sequential fp32 chain): weights and AdaGrad
     sums within 1e-5 relative of the oracle after 5 epochs, epoch errors
@@ -172,7 +173,7 @@ def test_lr_fast_sums_within_1e5_of_oracle(lib, oracle_mod, gpu, B):
     runs = []
     for _ in range(2):
         t = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
-        m = lib.LR(t, minibatch=B, fast_sums=True)
+        m = lib.LR(t, minibatch=B, fast_sums=True, plan=plan)
         m.load_text(DATA)
         m.init()
         e = m.train(5)
@@ -342,7 +343,7 @@ def criteo_text(tmp_path_factory):
     return path
 
 
-@pytest.mark.parametrize("fast", [False, True])
+@pytest.mark.parametrize("fast", [False, True, "none"])
 def test_lr_config3_batches_match_oracle(lib, oracle_mod, gpu, criteo_text, fast):
     """BASELINE config 3's per-GPU batch (65,537 rows, 39 features, keys
     < 2^24, AdaGrad lr 0.05) for 3 batches x 2 epochs against the oracle
@@ -362,7 +363,7 @@ def test_lr_config3_batches_match_oracle(lib, oracle_mod, gpu, criteo_text, fast
     e_o = orc.train(2)
     ko, wo, go = orc.params()
     t = lib.Table("lr", capacity=1 << 22, dtype="f32", learning_rate=0.05)
-    m = lib.LR(t, minibatch=65536, fast_sums=fast)
+    m = lib.LR(t, minibatch=65536, fast_sums=bool(fast), plan="none" if fast == "none" else "step")
     m.load_text(criteo_text)
     m.init()
     assert m.info()["batches"] >= 3
@@ -587,3 +588,39 @@ def test_lr_plan_step_config3_batch(lib, gpu):
         t.close()
     for a, b in zip(res[0], res[1]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("hot", ["1", "0"])
+def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
+    """The fixed-point step (plan="none": no index; each key's sum of e*x_i as a 64-bit integer
+    at scale 2^s by atomics) is run-to-run bit-identical whatever order its atomics land in, and
+    within 1e-6 of the sorted fp64 sums (plan="load") after 2 epochs, relative to the weights'
+    scale, on Criteo-shaped rows (hot keys: LDS sums, one global add per block) and ragged rows of
+    1-60 features; its per-batch errors equal the sorted path's for the first batch (same forward)."""
+    from swiftmpi_amd.synth import criteo
+    monkeypatch.setenv("SWPS_LR_HOT", hot)
+    y, off, f, v = criteo(20000, seed=7)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(1, 61, 4000)
+    roff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    feat = rng.integers(0, 3000, int(roff[-1])).astype(np.uint32)
+    vals = rng.random(int(roff[-1])).astype(np.float32)
+    yl = (rng.random(4000) < 0.5).astype(np.float32)
+    res = []
+    for plan in ("load", "none", "none"):
+        out = []
+        for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
+            t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+            m = lib.LR(t, minibatch=B, init_ref=False, fast_sums=True, plan=plan)
+            m.load_csr(*data)
+            m.init()
+            out += [m.train(2), m.params()[1], m.params()[2]]
+            m.close()
+            t.close()
+        res.append(out)
+    for a, b in zip(res[1], res[2]):
+        assert np.array_equal(a, b)
+    for a, b in zip(res[0], res[1]):
+        a = np.asarray(a, dtype=np.float64)
+        b = np.asarray(b, dtype=np.float64)
+        assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max(), (np.abs(a - b).max(), np.abs(a).max())
