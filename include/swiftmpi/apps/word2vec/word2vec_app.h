@@ -37,22 +37,23 @@ inline int len_vec() {
 /* the server-side row [h | v | h2sum | v2sum] lives in the HBM shard */
 struct WParam {};
 
-/* PS-level values, as the reference's GlobalPullAccess / GlobalPushAccess carry them */
+/* PS-level values, as the reference's GlobalPullAccess / GlobalPushAccess carry them
+ * (word2vec.h:50-100: zero-initialised Vecs) */
 struct WLocalParam {
-  std::vector<double> h, v;
-  WLocalParam() : h(len_vec(), 0.0), v(len_vec(), 0.0) {}
+  Vec h, v;
+  WLocalParam() : h(len_vec()), v(len_vec()) {}
 };
 struct WLocalGrad {
-  std::vector<double> h_grad, v_grad;
+  Vec h_grad, v_grad;
   int h_count = 0, v_count = 0;
-  WLocalGrad() : h_grad(len_vec(), 0.0), v_grad(len_vec(), 0.0) {}
-  void accu_h(const std::vector<double> &g) {
+  WLocalGrad() : h_grad(len_vec()), v_grad(len_vec()) {}
+  void accu_h(const Vec &g) {
     h_count++;
-    for (size_t i = 0; i < h_grad.size(); i++) h_grad[i] += g[i];
+    h_grad += g;
   }
-  void accu_v(const std::vector<double> &g) {
+  void accu_v(const Vec &g) {
     v_count++;
-    for (size_t i = 0; i < v_grad.size(); i++) v_grad[i] += g[i];
+    v_grad += g;
   }
   void reset() { *this = WLocalGrad(); }
 };
@@ -63,8 +64,12 @@ template <> struct PullCodec<WLocalParam> {
   static int elems() { return 2 * len_vec(); }
   static void decode(const double *w, WLocalParam &p) {
     const int D = len_vec();
-    p.h.assign(w, w + D);
-    p.v.assign(w + D, w + 2 * D);
+    p.h.init(D);
+    p.v.init(D);
+    for (int i = 0; i < D; i++) {
+      p.h[i] = w[i];
+      p.v[i] = w[D + i];
+    }
   }
 };
 template <> struct PushCodec<WLocalGrad> {  // the mean gradient, word2vec_global.h:122-134
@@ -90,9 +95,6 @@ class WPushAccessMethod : public PushAccessMethod<w2v_key_t, WParam, WLocalGrad>
 typedef ClusterServer<w2v_key_t, WParam, WLocalParam, WLocalGrad, WPullAccessMethod, WPushAccessMethod> server_t;
 typedef GlobalPullAccess<w2v_key_t, WLocalParam, WLocalGrad> pull_access_t;
 typedef GlobalPushAccess<w2v_key_t, WLocalParam, WLocalGrad> push_access_t;
-
-/* the reference's minibatch worker (gather / pull / learn / push): the library's device loop */
-class MiniBatch {};
 
 namespace swift_snails {
 inline int w2v_intermediates() {

@@ -16,7 +16,9 @@
  *   GlobalMPI / global_mpi()       utils/mpi.h:7-55 (rank / size from the launcher's environment)
  *   fms::CMDLine                   utils/CMDLine.h:17-183
  *   format_string                  utils/string.h:69-89
+ *   split / BKDRHash               utils/string.h:34-48, 130-137
  *   LineFileReader                 utils/string.h:91-121
+ *   Vec                            utils/vec1.h:6-258
  *   AsynExec / async_exec          utils/AsynExec.h:17-123
  *   SpinLock                       utils/SpinLock.h
  *   LOG / DLOG / CHECK_* / RAW_LOG_*   glog, as utils/common.h pulls it in
@@ -25,6 +27,7 @@
 #ifndef SWIFTMPI_SWIFTMPI_H_
 #define SWIFTMPI_SWIFTMPI_H_
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
@@ -173,6 +176,109 @@ class LineFileReader {
   char *_buffer = NULL;
   size_t _cap = 0, _length = 0;
   FILE *_file = nullptr;
+};
+
+/* split on any of `delim`'s characters, empty fields dropped (utils/string.h:34-48) */
+inline std::vector<std::string> split(const std::string &s, const std::string &delim) {
+  std::vector<std::string> cols;
+  size_t at = s.find_first_not_of(delim);
+  while (at != std::string::npos) {
+    const size_t end = s.find_first_of(delim, at);
+    cols.push_back(s.substr(at, end == std::string::npos ? std::string::npos : end - at));
+    at = end == std::string::npos ? end : s.find_first_not_of(delim, end);
+  }
+  return cols;
+}
+/* h = h * seed + (char)c over the bytes, char signed as on x86 (utils/string.h:130-137) */
+template <typename T = unsigned int> T BKDRHash(const char *str, T seed = 13131) {
+  T h = 0;
+  for (; *str; str++) h = h * seed + (T)(*str);
+  return h;
+}
+
+/* ---- utils/vec1.h Vec: the apps' host fp64 vector ----------------------------
+ * What an unchanged app computes with on the host (sent2vec.cpp's learn_instance); the
+ * library's kernels never use it.  random() is Vec::randInit (vec1.h:229-232): (rand() /
+ * (float)RAND_MAX - 0.5) / size from the process's libc rand(), element by element. */
+class Vec {
+ public:
+  typedef double value_type;
+  Vec() {}
+  explicit Vec(size_t n) : _d(n, 0.0) {}
+  void init(size_t n, bool random_init = false) {
+    _d.assign(n, 0.0);
+    if (random_init) random();
+  }
+  void clear() { std::fill(_d.begin(), _d.end(), 0.0); }
+  void random() {
+    for (size_t i = 0; i < _d.size(); i++) _d[i] = (std::rand() / (float)RAND_MAX - 0.5) / _d.size();
+  }
+  size_t size() const { return _d.size(); }
+  value_type *data() { return _d.data(); }
+  const value_type *data() const { return _d.data(); }
+  value_type &operator[](size_t i) { return _d[i]; }
+  const value_type &operator[](size_t i) const { return _d[i]; }
+  value_type dot(const Vec &o) const {  // sequential fp64 sum (vec1.h:103-110)
+    CHECK_EQ(size(), o.size());
+    value_type r = 0.0;
+    for (size_t i = 0; i < size(); i++) r += _d[i] * o._d[i];
+    return r;
+  }
+  std::string to_str() const {
+    std::ostringstream os;
+    os << *this;
+    return os.str();
+  }
+  friend std::ostream &operator<<(std::ostream &os, const Vec &v) {  // "Vec:\t" then "x " per element
+    os << "Vec:\t";
+    for (size_t i = 0; i < v.size(); i++) os << v._d[i] << " ";
+    return os;
+  }
+  template <class F> friend Vec zip(const Vec &a, const Vec &b, F f) {
+    CHECK_EQ(a.size(), b.size());
+    Vec r(a.size());
+    for (size_t i = 0; i < a.size(); i++) r._d[i] = f(a._d[i], b._d[i]);
+    return r;
+  }
+  template <class F> friend Vec map1(const Vec &a, F f) {
+    Vec r(a.size());
+    for (size_t i = 0; i < a.size(); i++) r._d[i] = f(a._d[i]);
+    return r;
+  }
+  friend Vec operator*(const Vec &a, value_type b) { return map1(a, [b](value_type x) { return x * b; }); }
+  friend Vec operator*(value_type b, const Vec &a) { return a * b; }
+  friend Vec operator*(const Vec &a, const Vec &b) { return zip(a, b, [](value_type x, value_type y) { return x * y; }); }
+  friend Vec operator/(const Vec &a, value_type b) { return map1(a, [b](value_type x) { return x / b; }); }
+  friend Vec operator/(value_type b, const Vec &a) { return map1(a, [b](value_type x) { return b / x; }); }
+  friend Vec operator/(const Vec &a, const Vec &b) { return zip(a, b, [](value_type x, value_type y) { return x / y; }); }
+  friend Vec operator+(const Vec &a, value_type b) { return map1(a, [b](value_type x) { return x + b; }); }
+  friend Vec operator+(value_type b, const Vec &a) { return a + b; }
+  friend Vec operator+(const Vec &a, const Vec &b) { return zip(a, b, [](value_type x, value_type y) { return x + y; }); }
+  friend Vec operator-(const Vec &a, value_type b) { return map1(a, [b](value_type x) { return x - b; }); }
+  friend Vec operator-(value_type b, const Vec &a) { return map1(a, [b](value_type x) { return b - x; }); }
+  friend Vec operator-(const Vec &a, const Vec &b) { return zip(a, b, [](value_type x, value_type y) { return x - y; }); }
+  friend Vec &operator+=(Vec &a, const Vec &b) {
+    CHECK_EQ(a.size(), b.size());
+    for (size_t i = 0; i < a.size(); i++) a._d[i] += b._d[i];
+    return a;
+  }
+  friend Vec &operator+=(Vec &a, value_type b) {
+    for (auto &x : a._d) x += b;
+    return a;
+  }
+  friend Vec &operator-=(Vec &a, const Vec &b) {
+    CHECK_EQ(a.size(), b.size());
+    for (size_t i = 0; i < a.size(); i++) a._d[i] -= b._d[i];
+    return a;
+  }
+  friend Vec &operator-=(Vec &a, value_type b) {
+    for (auto &x : a._d) x -= b;
+    return a;
+  }
+  friend Vec sqrt(const Vec &a) { return map1(a, [](value_type x) { return std::sqrt(x); }); }
+
+ private:
+  std::vector<value_type> _d;
 };
 
 /* ---- utils/SpinLock.h ------------------------------------------------------- */

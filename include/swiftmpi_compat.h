@@ -733,6 +733,14 @@ template <typename Key, typename Param, typename PullVal, typename Grad, typenam
 void ClusterServer<Key, Param, PullVal, Grad, PullM, PushM>::load(const std::string &path) {
   swps_table *t = global_swps_table();
   if (!t) throw SwpsError(SWPS_E_STATE, "no shard: create a Cluster first");
+  // server.h:49-62 constructs one `param_t param;` before reading the dump: word2vec's WParam
+  // draws h then v from libc rand() (word2vec.h:36-44, Vec::randInit) — the process's rand()
+  // stream moves by 2·D as the reference's did (LRParam draws nothing)
+  if (layout() == SWPS_LAYOUT_W2V) {
+    int32_t row = 0;
+    swps_check(swps_table_row_elems(t, &row, nullptr, nullptr));
+    for (int32_t i = 0; i < row / 2; i++) (void)std::rand();
+  }
   swps_check(swps_load(t, path.c_str(), global_frag_num(), global_node().second, global_node().first));
 }
 template <class ServerT> ServerT &global_server() {

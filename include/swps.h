@@ -121,6 +121,11 @@ int swps_push(swps_table *t, const uint64_t *d_keys, uint64_t n, const void *d_g
  * (include/swiftmpi_compat.h: GlobalPullAccess / GlobalPushAccess). */
 int swps_pull_h(swps_table *t, const uint64_t *keys, uint64_t n, void *vals);
 int swps_push_h(swps_table *t, const uint64_t *keys, uint64_t n, const void *grads);
+/* Host forms of a key probe and a whole-row assignment on a local (unrouted) table:
+ * SparseTableShard::find / ::assign (sparsetable.h:28-48).  present[i] = 1 when the shard holds
+ * keys[i]; rows[n][row elems] in fp64, converted to the table dtype (no init_param draws). */
+int swps_table_find_h(swps_table *t, const uint64_t *keys, uint64_t n, uint8_t *present);
+int swps_assign_h(swps_table *t, const uint64_t *keys, uint64_t n, const double *rows);
 /* Stream-ordered forms of swps_pull / swps_push on a local (unrouted) table:
  * issued on `stream` (a hipStream_t of the table's device; NULL = the
  * table's own stream) with no host sync.  Table-full / unknown-key errors are

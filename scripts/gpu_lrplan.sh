@@ -13,6 +13,8 @@ run() {  # tag plan [VAR=value ...]
 }
 run none none SWPS_X=1
 run none_nohot none SWPS_LR_HOT=0
+run none_h1024 none SWPS_LR_NHOT=1024
+run none_h256 none SWPS_LR_NHOT=256
 run step0 step SWPS_LR_PLAN_SORT=0
 run load load SWPS_X=1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lrplan_prof -o run -- python3 bench.py --app lr --lr-plan none --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/lrplan_prof.log 2>&1 || exit 1

@@ -98,6 +98,8 @@ PROTOS = {
     "swps_barrier": (ctypes.c_int, [_p]),
     "swps_route_stats": (ctypes.c_int, [_p, _p]),
     "swps_push_h": (ctypes.c_int, [_p, _p, _u64, _p]),
+    "swps_table_find_h": (ctypes.c_int, [_p, _p, _u64, _p]),
+    "swps_assign_h": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_assign": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_export": (ctypes.c_int, [_p, _p, _u64, _p]),
     "swps_table_keys": (ctypes.c_int, [_p, _p, _u64, ctypes.POINTER(_u64)]),

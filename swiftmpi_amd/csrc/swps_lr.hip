@@ -1510,7 +1510,8 @@ __global__ __launch_bounds__(256) void k_lr_fx_step(const uint2 *__restrict__ ch
                                                     float *__restrict__ err, float *__restrict__ err2,
                                                     unsigned long long *__restrict__ acc_sum,
                                                     uint32_t *__restrict__ acc_cnt, uint32_t *__restrict__ list,
-                                                    uint32_t *__restrict__ list_n, double scale) {
+                                                    uint32_t *__restrict__ list_n, double scale,
+                                                    uint32_t *__restrict__ stamp, uint32_t tag) {
   constexpr int CAP = RPT * 256;
   __shared__ float prod[CAP];
   __shared__ uint16_t rl[CAP];   // each record's row within the chunk
@@ -1518,6 +1519,7 @@ __global__ __launch_bounds__(256) void k_lr_fx_step(const uint2 *__restrict__ ch
   __shared__ float wh[kLrHot];
   __shared__ unsigned long long hs[kLrHot];
   __shared__ uint32_t hc[kLrHot];
+  __shared__ uint32_t bn, bbase;  // the block's first-touched rows (listed in prod's LDS once the sums are done)
   const int tid = threadIdx.x;
   HotW hw;
   hw.ld(rows, hrow, nhot, tid);
@@ -1525,6 +1527,7 @@ __global__ __launch_bounds__(256) void k_lr_fx_step(const uint2 *__restrict__ ch
     hs[q] = 0ull;
     hc[q] = 0u;
   }
+  if (tid == 0) bn = 0u;
   const uint2 ch = chunks[blockIdx.x];  // first row (batch-relative), rows
   const uint64_t rf = r0 + ch.x;
   const uint64_t c0 = row_off[rf], c1 = row_off[rf + ch.y];
@@ -1580,12 +1583,11 @@ __global__ __launch_bounds__(256) void k_lr_fx_step(const uint2 *__restrict__ ch
     es[r] = error;
   }
   __syncthreads();
+  uint32_t *blist = reinterpret_cast<uint32_t *>(prod);  // free now: CAP >= the block's records + hot keys
   // every record's term grad = error * x_i (lr.cpp:368) in fixed point
 #pragma unroll
   for (int k = 0; k < RPT; k++) {
     const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
-    bool first = false;
-    uint32_t row = 0;
     if (i < n) {
       const float g = es[rl[i]] * x[k];
       const unsigned long long q = (unsigned long long)__double2ll_rn((double)g * scale);
@@ -1594,29 +1596,31 @@ __global__ __launch_bounds__(256) void k_lr_fx_step(const uint2 *__restrict__ ch
         atomicAdd(&hs[h], q);
         atomicAdd(&hc[h], 1u);
       } else {
-        row = code[k];
-        atomicAdd(&acc_sum[row], q);
-        first = atomicAdd(&acc_cnt[row], 1u) == 0u;
+        const uint32_t row = code[k];
+        atomicAdd(&acc_sum[row], q);  // no return value wanted: fire and forget
+        atomicAdd(&acc_cnt[row], 1u);
+        // the batch's first touch of the key lists it: a plain read filters the repeats (the tag is
+        // written only by the exchange, so reading it means the key is listed already)
+        if (stamp[row] != tag && atomicExch(&stamp[row], tag) != tag) blist[atomicAdd(&bn, 1u)] = row;
       }
     }
-    const uint32_t slot = wave_claim(first, list_n);
-    if (first) list[slot] = row;
   }
-  if (!hrow) return;
-  __syncthreads();
-  for (uint32_t q0 = 0; q0 < nhot; q0 += 256u) {  // the hot keys: one global add per key per block
-    const uint32_t q = q0 + (uint32_t)tid;
-    const uint32_t c = q < nhot ? hc[q] : 0u;
-    bool first = false;
-    uint32_t row = 0;
-    if (c) {
-      row = hrow[q];
-      atomicAdd(&acc_sum[row], hs[q]);
-      first = atomicAdd(&acc_cnt[row], c) == 0u;
+  if (hrow) {
+    __syncthreads();
+    for (uint32_t q = (uint32_t)tid; q < nhot; q += 256u) {  // the hot keys: one global add per key per block
+      const uint32_t c = hc[q];
+      if (c) {
+        const uint32_t row = hrow[q];
+        atomicAdd(&acc_sum[row], hs[q]);
+        atomicAdd(&acc_cnt[row], c);
+        if (stamp[row] != tag && atomicExch(&stamp[row], tag) != tag) blist[atomicAdd(&bn, 1u)] = row;
+      }
     }
-    const uint32_t slot = wave_claim(first, list_n);
-    if (first) list[slot] = row;
   }
+  __syncthreads();
+  if (tid == 0) bbase = bn ? atomicAdd(list_n, bn) : 0u;  // one reservation per block
+  __syncthreads();
+  for (uint32_t q = (uint32_t)tid; q < bn; q += 256u) list[bbase + q] = blist[q];
 }
 
 // the batch's pushed keys: mean = float(sum / count) and AdaGrad on the shard row (lr.cpp:32-38,
@@ -1861,7 +1865,8 @@ struct swps_lr {
   bool fx_ready = false;
   int fx_bits = 40;                      // fixed-point scale 2^fx_bits (load: no sum can reach 2^62)
   std::vector<uint32_t> fx_hot_vids;     // the corpus's most frequent keys (load)
-  swps::DevMem d_vcode, d_fx_hot, d_fx_hrow, d_acc_sum, d_acc_cnt, d_fx_list, d_fx_n;
+  swps::DevMem d_vcode, d_fx_hot, d_fx_hrow, d_acc_sum, d_acc_cnt, d_fx_list, d_fx_n, d_fx_stamp;
+  uint32_t fx_tag = 0;  // the step's tag in d_fx_stamp (never 0: the stamps start at 0)
   int plan_sort = 1;   // SWPS_LR_PLAN_SORT: tile shape of the plan's radix sorts (sort_pairs_tiled)
   uint64_t plan_next = 0;  // the first step whose plan is not enqueued yet
   int plan_vbits = 1;
@@ -2426,8 +2431,11 @@ int lr_batch_fx(swps_lr *l) {
     if (!l->d_acc_sum.p) {
       SWPS_TRY(l->d_acc_sum.ensure(cap * 8));
       SWPS_TRY(l->d_acc_cnt.ensure(cap * 4));
+      SWPS_TRY(l->d_fx_stamp.ensure(cap * 4));
       SWPS_HIP(hipMemsetAsync(l->d_acc_sum.p, 0, cap * 8, s));
       SWPS_HIP(hipMemsetAsync(l->d_acc_cnt.p, 0, cap * 4, s));
+      SWPS_HIP(hipMemsetAsync(l->d_fx_stamp.p, 0, cap * 4, s));
+      l->fx_tag = 0;
     }
     SWPS_TRY(l->d_fx_list.ensure(std::max<uint64_t>(l->max_bnnz, 1) * 4));
     SWPS_TRY(l->d_fx_n.ensure(16));
@@ -2451,7 +2459,8 @@ int lr_batch_fx(swps_lr *l) {
                         hot ? (const uint32_t *)l->d_fx_hrow.as<uint32_t>() : (const uint32_t *)nullptr,
                         hot ? (uint32_t)l->fx_hot_vids.size() : 0u, l->d_err.as<float>(), l->d_err2.as<float>(),
                         l->d_acc_sum.as<unsigned long long>(), l->d_acc_cnt.as<uint32_t>(),
-                        l->d_fx_list.as<uint32_t>(), cur, std::ldexp(1.0, l->fx_bits));
+                        l->d_fx_list.as<uint32_t>(), cur, std::ldexp(1.0, l->fx_bits),
+                        l->d_fx_stamp.as<uint32_t>(), ++l->fx_tag ? l->fx_tag : ++l->fx_tag);
   l->timer.ext_end(0, fb, fe);
   hipEvent_t ab = l->timer.ext(), ae = l->timer.ext();
   hipExtLaunchKernelGGL(k_lr_fx_apply, dim3(512), dim3(256), 0, s, ab, ae, 0, (const uint32_t *)l->d_fx_list.as<uint32_t>(),

@@ -35,6 +35,7 @@
 #include <unordered_set>
 
 #include "swps_internal.h"
+#include "swps_rand.h"
 #include "swps_wave.h"
 
 using namespace swps;
@@ -354,6 +355,26 @@ enum { ST_REC = 0, ST_DOC, ST_N };
 
 }  // namespace
 
+// the sentences' Vec::random draws (utils/vec1.h:229-232: D rand() outputs per sentence, one
+// contiguous run of the stream per minibatch) on the device: a thread per chunk {first output's
+// destination, its stream index, count <= kRandRun} jumps there (swps_rand.h) and steps
+__global__ __launch_bounds__(64) void k_s2v_rand(const uint32_t *__restrict__ base, const uint64_t *__restrict__ ch,
+                                                 uint64_t nch, int32_t *__restrict__ out) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nch) return;
+  const uint64_t dst = ch[3 * q], o = ch[3 * q + 1], cnt = ch[3 * q + 2];
+  uint32_t ring[31];
+  glibc_ring_at(base, o - 31, ring);  // o[o-31 .. o-1]
+  int h = 0;  // ring[h] = o[i-31], ring[(h+28)%31] = o[i-3]
+  for (uint64_t k = 0; k < cnt; k++) {
+    const int h28 = h + 28 >= 31 ? h + 28 - 31 : h + 28;
+    const uint32_t v = ring[h] + ring[h28];
+    ring[h] = v;
+    h = h + 1 == 31 ? 0 : h + 1;
+    out[dst + k] = (int32_t)(v >> 1);
+  }
+}
+
 struct swps_s2v {
   swps_table *t = nullptr;
   swps_s2v_cfg cfg{};
@@ -502,9 +523,10 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   std::vector<uint64_t> miss_keys;
   std::vector<double> miss_rows;     // [h | v | h2 = 0 | v2 = 0] per miss
   std::unordered_set<uint64_t> lk;   // MiniBatch::_local_keys: one object, cleared per minibatch
+  uint64_t lk_max = 0;               // the largest key set inserted into it so far
   std::vector<uint64_t> vocab_keys;  // concatenated minibatch vocabs (std::map order)
   std::vector<uint64_t> starts_all;
-  std::vector<int32_t> init;  // [docs][D] rand() outputs
+  std::vector<uint64_t> rand_chunks;  // the sentences' rand() outputs: {destination, stream index, count}
   std::vector<uint64_t> doc_tok_keys;
   std::vector<uint32_t> doc_batch;  // sentence -> minibatch
   m->batches.clear();
@@ -528,20 +550,35 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
       for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) {
         bool fresh = false;
         freq.at(tok_keys[i], &fresh)++;
-        if (fresh) {
-          first_seen.push_back(tok_keys[i]);
-          lk.insert(tok_keys[i]);
-        }
+        if (fresh) first_seen.push_back(tok_keys[i]);
       }
       if (++cnt > B) break;
     }
-    if (lk.size() < 5) break;  // sent2vec.cpp:97
+    if (first_seen.size() < 5) break;  // sent2vec.cpp:97
     if (freq.contains(0))
       return fail(SWPS_E_UNSUPPORTED, "a minibatch vocab holds key 0 (atoi of a non-numeric word): the reference "
                                       "redraws negatives that hit it, a data-dependent draw count");
     // MiniBatch::pull: one WParam (2·D rand()) per pulled key in `_local_keys`
-    // order; a miss is inserted with it (server.h:143-150, accessmethod.h:63-70)
+    // order; a miss is inserted with it (server.h:143-150, accessmethod.h:63-70).  Only the misses'
+    // draws are read, so a minibatch without misses skips 2·D per key in one jump.  `_local_keys`
+    // is one std::unordered_set cleared per minibatch: its iteration order depends on its bucket
+    // count, which depends only on the largest key set inserted so far (clear() keeps the buckets;
+    // libstdc++ grows them only when a count passes that maximum) — so the set is filled, in the
+    // reference's insertion order, only for a minibatch with misses or a new largest key set
+    bool miss = false;
+    for (uint64_t k : first_seen)
+      if (!present.contains(k)) {
+        miss = true;
+        break;
+      }
+    if (miss || first_seen.size() > lk_max) {
+      lk.clear();
+      for (uint64_t k : first_seen) lk.insert(k);
+      lk_max = std::max<uint64_t>(lk_max, first_seen.size());
+    }
+    if (!miss) skip += 2 * (uint64_t)D * first_seen.size();
     for (uint64_t k : lk) {
+      if (!miss) break;
       if (present.contains(k)) {
         skip += 2 * (uint64_t)D;
         continue;
@@ -563,7 +600,9 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     swps_s2v::Batch b{m->doc_id.size(), 0, vocab_keys.size(), starts_all.size(), (uint32_t)vc.size(), 0};
     for (auto &kc : vc) vocab_keys.push_back(kc.first);
     starts_all.insert(starts_all.end(), st.begin(), st.end());
-    // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not
+    // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not; the sentences' Vec::random
+    // draws are this minibatch's next run of the stream (drawn on the device below)
+    const uint64_t run_o = 344 + rnd.produced + skip, run_d0 = m->doc_id.size();
     int lc = 0;
     while (lc <= B && li < nl) {
       const uint64_t l = li++;
@@ -574,11 +613,13 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
       for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) doc_tok_keys.push_back(tok_keys[i]);
       m->doc_tok.push_back(doc_tok_keys.size());
       m->doc_rec.push_back(m->doc_rec.back() + L * (uint64_t)m->cfg.niters);
-      for (int i = 0; i < D; i++) init.push_back(draw());
+      skip += (uint64_t)D;
       m->doc_lcg.push_back(lstate);
       lstate = lcg_jump(lstate, (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1)), kLcgA, kLcgC);
     }
     b.d1 = m->doc_id.size();
+    for (uint64_t k = 0, tot = (b.d1 - run_d0) * (uint64_t)D; k < tot; k += kRandRun)
+      rand_chunks.insert(rand_chunks.end(), {run_d0 * (uint64_t)D + k, run_o + k, std::min<uint64_t>(kRandRun, tot - k)});
     b.recs = m->doc_rec[b.d1] - m->doc_rec[b.d0];
     doc_batch.resize(b.d1, (uint32_t)m->batches.size());
     m->max_recs = std::max(m->max_recs, b.recs);
@@ -639,7 +680,19 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   SWPS_TRY(upload(m->d_doc_tok, m->doc_tok, s));
   SWPS_TRY(upload(m->d_doc_rec, m->doc_rec, s));
   SWPS_TRY(upload(m->d_doc_lcg, m->doc_lcg, s));
-  SWPS_TRY(upload(m->d_init, init, s));
+  {
+    const uint64_t nd = m->doc_id.size(), nch = rand_chunks.size() / 3;
+    SWPS_TRY(m->d_init.ensure(std::max<uint64_t>(nd, 1) * D * 4));
+    if (nch) {
+      DevMem dbase, dch;
+      SWPS_TRY(upload(dbase, glibc_base(m->cfg.rand_seed), s));
+      SWPS_TRY(upload(dch, rand_chunks, s));
+      k_s2v_rand<<<(unsigned)((nch + 63) / 64), 64, 0, s>>>(dbase.as<uint32_t>(), dch.as<uint64_t>(), nch,
+                                                            m->d_init.as<int32_t>());
+      SWPS_HIP(hipGetLastError());
+      SWPS_HIP(hipStreamSynchronize(s));
+    }
+  }
   std::vector<float> ex(1000);
   for (int i = 0; i < 1000; i++) {  // ExpTable (word2vec.h:241-253)
     float x = (i / (float)1000 * 2 - 1) * 6;

@@ -1022,6 +1022,48 @@ int swps_pull_h(swps_table *t, const uint64_t *keys, uint64_t n, void *vals) {
   return SWPS_OK;
 }
 
+// SparseTableShard::find (sparsetable.h:28-37) for a batch of host keys: present[i] = 1 when the
+// local shard holds keys[i].  Local tables only (a routed table's keys live on their owners).
+int swps_table_find_h(swps_table *t, const uint64_t *keys, uint64_t n, uint8_t *present) {
+  if (!t || (n && (!keys || !present))) return fail(SWPS_E_CFG, "null argument");
+  if (t->comm) return fail(SWPS_E_UNSUPPORTED, "swps_table_find_h on a routed table");
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  DevMem dk, dr;
+  SWPS_TRY(dk.ensure(n * 8));
+  SWPS_TRY(dr.ensure(n * 4));
+  SWPS_HIP(hipMemcpyAsync(dk.p, keys, n * 8, hipMemcpyHostToDevice, t->stream));
+  SWPS_TRY(table_probe(t, dk.as<uint64_t>(), n, dr.as<uint32_t>(), t->stream));
+  std::vector<uint32_t> rows(n);
+  SWPS_HIP(hipMemcpyAsync(rows.data(), dr.p, n * 4, hipMemcpyDeviceToHost, t->stream));
+  SWPS_HIP(hipStreamSynchronize(t->stream));
+  for (uint64_t i = 0; i < n; i++) present[i] = rows[i] != kNoRow ? 1 : 0;
+  return SWPS_OK;
+}
+
+// swps_assign with host rows in the reference's value type (fp64, [n][row elems]), converted to
+// the table dtype: SparseTableShard::assign (sparsetable.h:38-48) of whole rows, nothing drawn
+int swps_assign_h(swps_table *t, const uint64_t *keys, uint64_t n, const double *rows) {
+  if (!t || (n && (!keys || !rows))) return fail(SWPS_E_CFG, "null argument");
+  if (t->comm) return fail(SWPS_E_UNSUPPORTED, "swps_assign_h on a routed table");
+  if (n == 0) return SWPS_OK;
+  SWPS_HIP(hipSetDevice(t->cfg.device));
+  const uint64_t m = n * (uint64_t)t->row_elems;
+  DevMem dk, dv;
+  SWPS_TRY(dk.ensure(n * 8));
+  SWPS_TRY(dv.ensure(m * t->esize));
+  SWPS_HIP(hipMemcpyAsync(dk.p, keys, n * 8, hipMemcpyHostToDevice, t->stream));
+  if (t->esize == 8) {
+    SWPS_HIP(hipMemcpyAsync(dv.p, rows, m * 8, hipMemcpyHostToDevice, t->stream));
+    SWPS_HIP(hipStreamSynchronize(t->stream));
+  } else {
+    std::vector<float> f(rows, rows + m);
+    SWPS_HIP(hipMemcpyAsync(dv.p, f.data(), m * 4, hipMemcpyHostToDevice, t->stream));
+    SWPS_HIP(hipStreamSynchronize(t->stream));
+  }
+  return swps_assign(t, dk.as<uint64_t>(), n, dv.p);  // syncs before dk / dv go out of scope
+}
+
 int swps_push_h(swps_table *t, const uint64_t *keys, uint64_t n, const void *grads) {
   if (n == 0 && !t->comm) return SWPS_OK;
   SWPS_HIP(hipSetDevice(t->cfg.device));

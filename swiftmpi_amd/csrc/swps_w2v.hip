@@ -41,6 +41,7 @@
 #include <hip/hip_ext.h>
 
 #include "swps_internal.h"
+#include "swps_rand.h"
 #include "swps_sort.h"
 #include "swps_wave.h"
 
@@ -3099,49 +3100,14 @@ template <typename T> int pull_all(swps_w2v *w) {
 // 31-coefficient polynomials) and then steps the recurrence.  Output k
 // (after `skip` earlier calls) is element k % 2D of key k / 2D's [h | v],
 // (rand()/(float)RAND_MAX - 0.5) / D, written straight into the table row.
-struct Poly31 {
-  uint32_t c[31];
-};
-__device__ void poly_mulmod(const Poly31 &a, const Poly31 &b, Poly31 &out) {
-  uint32_t t[61];
-  for (int i = 0; i < 61; i++) t[i] = 0;
-  for (int i = 0; i < 31; i++)
-    for (int j = 0; j < 31; j++) t[i + j] += a.c[i] * b.c[j];
-  for (int d = 60; d >= 31; d--) {  // x^d = x^(d-3) + x^(d-31)
-    t[d - 3] += t[d];
-    t[d - 31] += t[d];
-  }
-  for (int i = 0; i < 31; i++) out.c[i] = t[i];
-}
-
-constexpr uint64_t kRandRun = 8192;  // outputs per thread
-
 template <typename T>
 __global__ __launch_bounds__(64) void k_rand_init(const uint32_t *__restrict__ base, uint64_t first, uint64_t total,
                                                    int D, const uint32_t *__restrict__ vid_row, T *__restrict__ rows) {
   const uint64_t k0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRandRun;
   if (k0 >= total) return;
   // o[m] for the 31 values before output k0: m = first + k0 - 31 + d, d = 0..30
-  const uint64_t m0 = first + k0 - 31;
-  Poly31 r, x;  // r = x^(m0-3) mod P
-  for (int i = 0; i < 31; i++) {
-    r.c[i] = i == 0 ? 1u : 0u;
-    x.c[i] = i == 1 ? 1u : 0u;
-  }
-  for (uint64_t e = m0 - 3; e; e >>= 1) {
-    if (e & 1) poly_mulmod(r, x, r);
-    poly_mulmod(x, x, x);
-  }
   uint32_t ring[31];
-  for (int d = 0; d < 31; d++) {
-    uint32_t v = 0;
-    for (int j = 0; j < 31; j++) v += r.c[j] * base[j];
-    ring[d] = v;
-    const uint32_t top = r.c[30];  // r <- x * r mod P
-    for (int j = 30; j > 0; j--) r.c[j] = r.c[j - 1];
-    r.c[0] = top;
-    r.c[28] += top;
-  }
+  glibc_ring_at(base, first + k0 - 31, ring);
   const uint64_t k1 = min(total, k0 + kRandRun);
   int h = 0;  // ring[h] = o[i-31], ring[(h+28)%31] = o[i-3]
   for (uint64_t k = k0; k < k1; k++) {
@@ -3167,20 +3133,7 @@ template <typename T> int rand_init_gpu(swps_w2v *w) {
   const uint64_t V = w->vocab_keys.size();
   const int D = w->D;
   // o[3..33] after srand(seed) (GlibcRand's seeding, swps_host.cpp)
-  std::vector<uint32_t> base(31);
-  {
-    int32_t s0[34];
-    uint32_t seed = w->cfg.rand_seed ? w->cfg.rand_seed : 1;
-    s0[0] = (int32_t)seed;
-    for (int i = 1; i < 31; i++) {
-      int64_t hi = s0[i - 1] / 127773, lo = s0[i - 1] % 127773;
-      int64_t v = 16807 * lo - 2836 * hi;
-      if (v < 0) v += 2147483647;
-      s0[i] = (int32_t)v;
-    }
-    for (int i = 31; i < 34; i++) s0[i] = s0[i - 31];
-    for (int j = 0; j < 31; j++) base[j] = (uint32_t)s0[3 + j];
-  }
+  const std::vector<uint32_t> base = glibc_base(w->cfg.rand_seed);
   const uint64_t total = V * 2 * (uint64_t)D;
   const uint64_t first = 344 + w->cfg.rand_offset;  // o index of the first output used
   DevMem d_base;

@@ -16,7 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference/src/apps"
 OUT = os.path.join(HERE, "_ref_apps")
-APPS = {"w2v": "word2vec/w2v.cpp", "w2v_local": "word2vec/w2v_local.cpp", "lr": "logistic/lr.cpp"}
+APPS = {"w2v": "word2vec/w2v.cpp", "w2v_local": "word2vec/w2v_local.cpp", "lr": "logistic/lr.cpp",
+        "sent2vec": "sent2vec/sent2vec.cpp"}
 
 
 def command(name):

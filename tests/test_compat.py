@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, ROOT, int_corpus, zipf_corpus
+from conftest import GOLDEN, ROOT, int_corpus, word_dump, zipf_corpus
 
 W2V_CONF = """[ worker ]
 minibatch: 20
@@ -290,7 +290,7 @@ def test_host_body_rules_are_recognised(lib, tmp_path):
 
 
 def test_reference_mains_compile_unchanged(lib):
-    """apps/word2vec/w2v.cpp, w2v_local.cpp and apps/logistic/lr.cpp, read
+    """apps/word2vec/w2v.cpp, w2v_local.cpp, apps/logistic/lr.cpp and apps/sent2vec/sent2vec.cpp, read
     where they lie under /root/reference, compile with g++ -std=c++11 against
     include/swiftmpi/ (the reference's include names) and link libswps.so;
     the binaries run (usage path, no GPU work)."""
@@ -298,11 +298,13 @@ def test_reference_mains_compile_unchanged(lib):
     if not os.path.isdir(b.REF):
         pytest.skip("no reference tree here (the GPU box uses the binaries built in the build container)")
     bins = b.build()
-    assert set(bins) == {"w2v", "w2v_local", "lr"}
+    assert set(bins) == {"w2v", "w2v_local", "lr", "sent2vec"}
     r = subprocess.run([bins["lr"], "-mode"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "missing parameter" in r.stderr and "Train Mode" in r.stdout
     r = subprocess.run([bins["w2v"]], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "Word2Vec application" in r.stdout
+    r = subprocess.run([bins["sent2vec"]], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "Doc2Vec" in r.stdout
 
 
 def _ref_bin(name):
@@ -464,3 +466,35 @@ def _flcg_seq(n):
             q <<= sh
         out[i] = np.float32(q / 2.0 ** 64)
     return out
+
+
+@pytest.mark.gpu
+def test_reference_sent2vec_main_unchanged_matches_oracle(oracle_mod, lib, gpu, tmp_path):
+    """sent2vec.cpp itself: WordMiniBatch over word2vec.h's host MiniBatch (gather_keys / pull /
+    table / param / clear over the PS API on the HBM shard) and its own fp64 learn_instance on the
+    host.  The dump covers 120 of the corpus's 150 keys, so pulls insert the rest with the server's
+    rand() rows (the in-process server's WParam per pulled key, accessmethod.h:63-70).  Its output
+    file (sentence id, "Vec:", D values at 6 digits) = the oracle's S2V (fp32 storage like the
+    shard, no rand() before the load) within 1e-5."""
+    ref = _ref_bin("sent2vec")
+    conf = tmp_path / "demo.conf"
+    conf.write_text(W2V_CONF)
+    corpus = int_corpus(str(tmp_path / "s.txt"), 90, 150, seed=44)
+    dump = word_dump(str(tmp_path / "w.txt"), 120, 16, seed=45)
+    out = str(tmp_path / "sent.txt")
+    _run(ref, "-config", str(conf), "-data", corpus, "-wordvec", dump, "-niters", "2", "-output", out)
+    orc = oracle_mod.S2V(corpus, 16, window=3, negative=4, minibatch=20, niters=2, table_size=10 ** 8,
+                         storage_f32=True, rand_offset=0)
+    orc.load_words(dump)
+    orc.train()
+    io, vo, _ = orc.docs()
+    ids, vecs = [], []
+    for line in open(out):
+        sid, body = line.rstrip("\n").split("\t", 1)
+        assert body.startswith("Vec:\t")
+        ids.append(int(sid))
+        vecs.append([float(x) for x in body[5:].split()])
+    assert len(ids) == len(io) > 50 and np.array_equal(np.array(ids, dtype=np.uint64), io)
+    vecs = np.array(vecs)
+    assert vecs.shape == vo.shape
+    assert np.allclose(vecs, vo, rtol=1e-5, atol=1e-7), np.abs(vecs - vo).max()
