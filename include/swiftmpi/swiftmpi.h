@@ -199,7 +199,8 @@ template <typename T = unsigned int> T BKDRHash(const char *str, T seed = 13131)
 /* ---- utils/vec1.h Vec: the apps' host fp64 vector ----------------------------
  * What an unchanged app computes with on the host (sent2vec.cpp's learn_instance); the
  * library's kernels never use it.  random() is Vec::randInit (vec1.h:229-232): (rand() /
- * (float)RAND_MAX - 0.5) / size from the process's libc rand(), element by element. */
+ * (float)RAND_MAX - 0.5) / size from the process's rand() stream (process_rand, swiftmpi_compat.h),
+ * element by element. */
 class Vec {
  public:
   typedef double value_type;
@@ -211,7 +212,7 @@ class Vec {
   }
   void clear() { std::fill(_d.begin(), _d.end(), 0.0); }
   void random() {
-    for (size_t i = 0; i < _d.size(); i++) _d[i] = (std::rand() / (float)RAND_MAX - 0.5) / _d.size();
+    for (size_t i = 0; i < _d.size(); i++) _d[i] = (process_rand()() / (float)RAND_MAX - 0.5) / _d.size();
   }
   size_t size() const { return _d.size(); }
   value_type *data() { return _d.data(); }

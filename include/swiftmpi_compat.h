@@ -206,6 +206,47 @@ inline Random &global_random() {
   return r;
 }
 
+/* ---- the reference process's libc rand() stream -------------------------------
+ * Vec::randInit and the server's WParam draw glibc rand() after the default srand(1)
+ * (vec1.h:229-232, word2vec.h:38-44).  In this process the ROCm runtime calls srand() and rand()
+ * itself (libhsa-runtime64 imports both, at HIP initialisation and later), which would reseed and
+ * advance that stream under the app at run-dependent points.  The apps' draws therefore come from
+ * this copy of it: glibc's TYPE_3 additive generator — r[i] = r[i-31] + r[i-3] (mod 2^32) seeded
+ * by the 16807 LCG, r[31..33] = r[0..2], 310 outputs discarded, each output r >> 1 — which returns
+ * what rand() returns in a process that calls nothing else (tests/test_compat.py checks it against
+ * libc).  One stream per process, like rand(); not thread-safe, like the reference's nthreads = 1. */
+class ProcessRand {
+ public:
+  explicit ProcessRand(uint32_t seed = 1) {
+    int32_t w = seed ? (int32_t)seed : 1;
+    _r[0] = (uint32_t)w;
+    for (int i = 1; i < 31; i++) {
+      const int32_t hi = w / 127773, lo = w % 127773;
+      w = 16807 * lo - 2836 * hi;
+      if (w < 0) w += 2147483647;
+      _r[i] = (uint32_t)w;
+    }
+    for (int i = 31; i < 34; i++) _r[i] = _r[i - 31];
+    _i = 34;
+    for (int k = 0; k < 310; k++) next_raw();
+  }
+  int operator()() { return (int)(next_raw() >> 1); }
+
+ private:
+  uint32_t next_raw() {
+    const uint32_t v = _r[(_i - 31) % 34] + _r[(_i - 3) % 34];
+    _r[_i % 34] = v;
+    _i++;
+    return v;
+  }
+  uint32_t _r[34];
+  uint64_t _i;
+};
+inline ProcessRand &process_rand() {
+  static ProcessRand r(1);
+  return r;
+}
+
 /* ---- wire codecs ----------------------------------------------------------
  * Typed form (a specialisation states the wire directly):
  *   PullCodec<Val>:  typedef wire_t (double for word2vec, float for LR);
@@ -704,7 +745,13 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
     swps_table_destroy(_t);
     swps_comm_destroy(_comm);
   }
-  void initialize() {}
+  /* the reference's initialize binds its transfer's listeners to random ports: one rand() per
+   * bind, two binds (common.h:92-96 via Listener.h:83) — the process's rand() stream moves by 2
+   * before an app draws, as SWPS_W2V_INIT_REF's rand_offset = 2 assumes */
+  void initialize() {
+    (void)process_rand()();
+    (void)process_rand()();
+  }
   /* The worker is done: keep serving the other ranks until all are
    * (swps_finish), then SparseTable::output (sparsetable.h:127-132) of this
    * rank's shard to exactly `path` (cluster.h:41-50; the reference's mains
@@ -739,7 +786,7 @@ void ClusterServer<Key, Param, PullVal, Grad, PullM, PushM>::load(const std::str
   if (layout() == SWPS_LAYOUT_W2V) {
     int32_t row = 0;
     swps_check(swps_table_row_elems(t, &row, nullptr, nullptr));
-    for (int32_t i = 0; i < row / 2; i++) (void)std::rand();
+    for (int32_t i = 0; i < row / 2; i++) (void)process_rand()();
   }
   swps_check(swps_load(t, path.c_str(), global_frag_num(), global_node().second, global_node().first));
 }

@@ -289,6 +289,25 @@ def test_host_body_rules_are_recognised(lib, tmp_path):
                      "half_adagrad error -7", "flcg_momentum error -7"], lines
 
 
+def test_process_rand_is_libc_rand(tmp_path):
+    """swift_snails::process_rand() (the apps' Vec::randInit / WParam stream, kept apart from the
+    ROCm runtime's own srand()/rand() calls) returns what glibc's rand() does after srand(1) — the
+    default — call for call, over 10^6 calls; and after srand(7) for ProcessRand(7)."""
+    src = tmp_path / "pr.cpp"
+    src.write_text('#include <cstdio>\n#include <cstdlib>\n#include "swiftmpi_compat.h"\n'
+                   "int main() {\n"
+                   "  for (int i = 0; i < 1000000; i++) if (swift_snails::process_rand()() != rand()) return 1;\n"
+                   "  srand(7); swift_snails::ProcessRand r(7);\n"
+                   "  for (int i = 0; i < 100000; i++) if (r() != rand()) return 2;\n"
+                   "  std::puts(\"ok\"); return 0;\n}\n")
+    out = str(tmp_path / "pr")
+    r = subprocess.run(["g++", "-std=c++11", "-O2", "-I" + os.path.join(ROOT, "include"), str(src), "-o", out],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([out], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", (r.returncode, r.stdout)
+
+
 def test_reference_mains_compile_unchanged(lib):
     """apps/word2vec/w2v.cpp, w2v_local.cpp, apps/logistic/lr.cpp and apps/sent2vec/sent2vec.cpp, read
     where they lie under /root/reference, compile with g++ -std=c++11 against
@@ -475,7 +494,7 @@ def test_reference_sent2vec_main_unchanged_matches_oracle(oracle_mod, lib, gpu, 
     host.  The dump covers 120 of the corpus's 150 keys, so pulls insert the rest with the server's
     rand() rows (the in-process server's WParam per pulled key, accessmethod.h:63-70).  Its output
     file (sentence id, "Vec:", D values at 6 digits) = the oracle's S2V (fp32 storage like the
-    shard, no rand() before the load) within 1e-5."""
+    shard; rand() moved by Cluster::initialize's two port binds before the load) within 1e-5."""
     ref = _ref_bin("sent2vec")
     conf = tmp_path / "demo.conf"
     conf.write_text(W2V_CONF)
@@ -484,7 +503,7 @@ def test_reference_sent2vec_main_unchanged_matches_oracle(oracle_mod, lib, gpu, 
     out = str(tmp_path / "sent.txt")
     _run(ref, "-config", str(conf), "-data", corpus, "-wordvec", dump, "-niters", "2", "-output", out)
     orc = oracle_mod.S2V(corpus, 16, window=3, negative=4, minibatch=20, niters=2, table_size=10 ** 8,
-                         storage_f32=True, rand_offset=0)
+                         storage_f32=True, rand_offset=2)
     orc.load_words(dump)
     orc.train()
     io, vo, _ = orc.docs()
