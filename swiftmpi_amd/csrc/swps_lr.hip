@@ -1648,6 +1648,273 @@ __global__ __launch_bounds__(256) void k_lr_fx_apply(const uint32_t *__restrict_
     r[0] = w + step / sqrtf(ng2 + fudge);
   }
 }
+// ---- the fixed-point step, bucketed (the default form of SWPS_LR_PLAN_NONE) ------------------
+// The same integer sums as k_lr_fx_step, with no global atomic per record.  The vocabulary is cut
+// into buckets of 2^kLrFxVB consecutive vids (a bucket's accumulators fit one block's LDS).
+// k_lr_fxb_step: a block walks chunks of whole rows (forward as k_lr_fx_step); per chunk it sorts
+//   its non-hot records by bucket in LDS (a counting sort: the order within a bucket is whatever
+//   the LDS atomics give — the sums below do not depend on it) and writes them, (vid, e*x_i as
+//   fp32), into the chunk's own span of `rec` with the chunk's bucket offsets (boff, u16); hot
+//   keys' terms stay in the block's LDS over all its chunks and go out once, as one row of the
+//   [block][hot] partial matrix (no atomics: every entry written).
+// k_lr_fxb_push: block b < nbk owns bucket b: it adds every chunk's records of the bucket into LDS
+//   (the fixed point of each term computed exactly as k_lr_fx_step does), then applies the mean
+//   and AdaGrad to each touched key's shard row; the blocks after them each reduce 64 hot keys'
+//   column of the partial matrix and apply theirs.  Integer sums: the result is the atomic form's,
+//   bit for bit, whatever the order.
+constexpr int kLrFxVB = 12;
+constexpr uint32_t kLrFxMaxBk = 4096;  // buckets (V <= 2^24); beyond it the atomic form runs
+template <int RPT, bool AFF>
+__global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ chunks, uint32_t nchunks,
+                                                     const uint64_t *__restrict__ row_off,
+                                                     const int32_t *__restrict__ fvid,
+                                                     const uint32_t *__restrict__ vcode,
+                                                     const float *__restrict__ fval, const float *__restrict__ label,
+                                                     uint64_t r0, const float *__restrict__ rows,
+                                                     const uint32_t *__restrict__ hrow, uint32_t nhot,
+                                                     float *__restrict__ err, float *__restrict__ err2, double scale,
+                                                     uint32_t nbk, uint2 *__restrict__ rec, uint16_t *__restrict__ boff,
+                                                     unsigned long long *__restrict__ hsum,
+                                                     uint32_t *__restrict__ hcnt, uint32_t row_base, uint32_t diag) {
+  constexpr int CAP = RPT * 256;
+  __shared__ float prod[CAP];
+  __shared__ uint16_t rl[CAP];
+  __shared__ float es[CAP];
+  __shared__ float wh[kLrHot];
+  __shared__ unsigned long long hs[kLrHot];
+  __shared__ uint32_t hc[kLrHot];
+  extern __shared__ uint32_t bc[];  // [nbk]: dynamic
+  const int tid = threadIdx.x;
+  HotW hw;
+  hw.ld(rows, hrow, nhot, tid);
+  for (uint32_t q = (uint32_t)tid; q < nhot; q += 256u) {
+    hs[q] = 0ull;
+    hc[q] = 0u;
+  }
+  if (hrow) hw.st(wh, nhot, tid);
+  const uint64_t z0 = row_off[r0];
+  for (uint32_t cix = blockIdx.x; cix < nchunks; cix += gridDim.x) {
+    const uint2 ch = chunks[cix];
+    const uint64_t rf = r0 + ch.x;
+    const uint64_t c0 = row_off[rf], c1 = row_off[rf + ch.y];
+    const uint32_t n = (uint32_t)(c1 - c0);
+    int32_t f[RPT];
+    float x[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      f[k] = i < n ? fvid[c0 + i] : 0;
+      x[k] = i < n ? fval[c0 + i] : 0.f;
+    }
+    uint32_t code[RPT];  // AFF: f is the key's fid (hot keys first) and its shard row row_base + fid
+#pragma unroll
+    for (int k = 0; k < RPT; k++)
+      code[k] = ((uint32_t)tid + (uint32_t)k * 256u) >= n ? 0u
+                : AFF ? ((uint32_t)f[k] < nhot ? (kLrHotBit | (uint32_t)f[k]) : row_base + (uint32_t)f[k])
+                      : vcode[f[k]];
+    uint64_t ra = 0, rb = 0;
+    float y = 0.f;
+    if ((uint32_t)tid < ch.y) {
+      ra = row_off[rf + tid];
+      rb = row_off[rf + tid + 1];
+      y = label[rf + tid];
+    }
+    for (uint32_t q = (uint32_t)tid; q < nbk; q += 256u) bc[q] = 0u;
+    __syncthreads();  // wh stored (first chunk); the previous chunk's LDS reads done
+    float w[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      w[k] = i >= n ? 0.f : (code[k] & kLrHotBit) ? wh[code[k] & (kLrHotBit - 1)] : rows[(uint64_t)code[k] * 2];
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      if (i < n) prod[i] = w[k] * x[k];
+    }
+    for (uint32_t r = (uint32_t)tid; r < ch.y; r += 256u) {
+      const uint64_t a = r < 256u ? ra : row_off[rf + r], b = r < 256u ? rb : row_off[rf + r + 1];
+      for (uint64_t c = a; c < b; c++) rl[c - c0] = (uint16_t)r;
+    }
+    __syncthreads();
+    for (uint32_t r = (uint32_t)tid; r < ch.y; r += 256u) {  // lr.cpp:358-367, in feature order
+      if (r >= 256u) {
+        ra = row_off[rf + r];
+        rb = row_off[rf + r + 1];
+        y = label[rf + r];
+      }
+      float sum = 0.f;
+      for (uint32_t c = (uint32_t)(ra - c0); c < (uint32_t)(rb - c0); c++) sum += prod[c];
+      const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
+      const float error = y - predict;
+      err[rf + r] = error;
+      err2[rf + r] = error * error;
+      es[r] = error;
+    }
+    __syncthreads();
+    float g[RPT];
+    uint32_t rk[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      g[k] = 0.f;
+      rk[k] = 0u;
+      if (i < n) {
+        g[k] = es[rl[i]] * x[k];  // lr.cpp:368
+        if (code[k] & kLrHotBit) {
+          const uint32_t h = code[k] & (kLrHotBit - 1);
+          atomicAdd(&hs[h], (unsigned long long)__double2ll_rn((double)g[k] * scale));
+          atomicAdd(&hc[h], 1u);
+        } else {
+          rk[k] = atomicAdd(&bc[(uint32_t)f[k] >> kLrFxVB], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {  // one wave: exclusive scan of the bucket counts, the chunk's offsets row
+      const uint32_t per = (nbk + 63u) / 64u, b0 = (uint32_t)tid * per, b1 = min(nbk, b0 + per);
+      uint32_t s = 0;
+      for (uint32_t q = b0; q < b1; q++) s += bc[q];
+      uint32_t inc = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (tid >= d) inc += o;
+      }
+      uint32_t run = inc - s;
+      uint16_t *orow = boff + (uint64_t)cix * (nbk + 1);
+      for (uint32_t q = b0; q < b1; q++) {
+        const uint32_t c = bc[q];
+        bc[q] = run;
+        orow[q] = (uint16_t)run;
+        run += c;
+      }
+      if (tid == 63) orow[nbk] = (uint16_t)inc;
+    }
+    __syncthreads();
+    const uint64_t base = c0 - z0;
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      if (i < n && !(code[k] & kLrHotBit) && !(diag & 4u))
+        rec[base + bc[(uint32_t)f[k] >> kLrFxVB] + rk[k]] = make_uint2((uint32_t)f[k], __float_as_uint(g[k]));
+    }
+    __syncthreads();  // bc / es / rl are the next chunk's
+  }
+  if (nhot && !(diag & 8u)) {
+    __syncthreads();
+    unsigned long long *hsr = hsum + (uint64_t)blockIdx.x * nhot;
+    uint32_t *hcr = hcnt + (uint64_t)blockIdx.x * nhot;
+    for (uint32_t q = (uint32_t)tid; q < nhot; q += 256u) {
+      hsr[q] = hs[q];
+      hcr[q] = hc[q];
+    }
+  }
+}
+
+__device__ __forceinline__ void lr_fx_adagrad(float *__restrict__ r, long long s, uint32_t c, float lr, float fudge,
+                                              double inv_scale) {  // lr.cpp:32-38, 68-75 (k_lr_fx_apply's rule)
+  const float w = r[0], g2 = r[1];
+  const float m = (float)(((double)s * inv_scale) / (double)c);
+  const float ng2 = g2 + m * m;
+  const float step = lr * m;
+  r[1] = ng2;
+  r[0] = w + step / sqrtf(ng2 + fudge);
+}
+
+constexpr uint32_t kLrFxbPushT = 1024;  // k_lr_fxb_push's threads: one block per bucket, 16 waves
+__global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__restrict__ rec,
+                                                             const uint16_t *__restrict__ boff,
+                                                             const uint32_t *__restrict__ chunk_c0, uint32_t nchunks,
+                                                             uint32_t nbk, const uint32_t *__restrict__ vid_row,
+                                                             const unsigned long long *__restrict__ hsum,
+                                                             const uint32_t *__restrict__ hcnt, uint32_t hblocks,
+                                                             const uint32_t *__restrict__ hrow, uint32_t nhot,
+                                                             float *__restrict__ rows, float lr, float fudge,
+                                                             double scale, double inv_scale, uint32_t aff,
+                                                             uint32_t row_base, uint32_t first_block) {
+  constexpr uint32_t T = 1u << kLrFxVB, NT = kLrFxbPushT, PER = T / NT;
+  __shared__ unsigned long long as[T];
+  __shared__ uint32_t ac[T];
+  const uint32_t tid = threadIdx.x, bid = blockIdx.x + first_block;
+  if (bid < nbk) {
+    const uint32_t b = bid;
+    for (uint32_t v = tid; v < T; v += NT) {
+      as[v] = 0ull;
+      ac[v] = 0u;
+    }
+    __syncthreads();
+    for (uint32_t s = tid; s < nchunks; s += NT) {  // the chunks' segments of this bucket
+      const uint16_t *orow = boff + (uint64_t)s * (nbk + 1);
+      const uint32_t lo = orow[b], hi = orow[b + 1];
+      const uint2 *src = rec + chunk_c0[s];
+      uint2 r[4];  // the first four records' loads in flight together
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (lo + k < hi) r[k] = src[lo + k];
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (lo + k < hi) {
+          atomicAdd(&as[r[k].x & (T - 1)], (unsigned long long)__double2ll_rn((double)__uint_as_float(r[k].y) * scale));
+          atomicAdd(&ac[r[k].x & (T - 1)], 1u);
+        }
+      for (uint32_t j = lo + 4; j < hi; j++) {
+        const uint2 q = src[j];
+        atomicAdd(&as[q.x & (T - 1)], (unsigned long long)__double2ll_rn((double)__uint_as_float(q.y) * scale));
+        atomicAdd(&ac[q.x & (T - 1)], 1u);
+      }
+    }
+    __syncthreads();
+    uint32_t c[PER], row[PER];  // the thread's PER vids: row loads, then [w | g2] loads, all in flight
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+      c[k] = ac[tid + k * NT];
+      if (c[k]) row[k] = aff ? row_base + (b << kLrFxVB) + tid + k * NT : vid_row[(b << kLrFxVB) + tid + k * NT];
+    }
+    float2 wg[PER];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++)
+      if (c[k]) wg[k] = *reinterpret_cast<const float2 *>(rows + (uint64_t)row[k] * 2);
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++)
+      if (c[k]) {  // lr.cpp:32-38, 68-75 (k_lr_fx_apply's rule)
+        const float m = (float)(((double)(long long)as[tid + k * NT] * inv_scale) / (double)c[k]);
+        const float ng2 = wg[k].y + m * m;
+        const float step = lr * m;
+        *reinterpret_cast<float2 *>(rows + (uint64_t)row[k] * 2) = make_float2(wg[k].x + step / sqrtf(ng2 + fudge), ng2);
+      }
+    return;
+  }
+  // 64 hot keys per block: 16 row groups sum each key's column of the step's block partials
+  const uint32_t h0 = (bid - nbk) * 64u, kk = tid & 63u, rg = tid >> 6;
+  const uint32_t h = h0 + kk;
+  unsigned long long s = 0ull;
+  uint32_t c = 0u;
+  if (h < nhot) {
+#pragma unroll 4
+    for (uint32_t blk = rg; blk < hblocks; blk += 16u) {
+      s += hsum[(uint64_t)blk * nhot + h];
+      c += hcnt[(uint64_t)blk * nhot + h];
+    }
+  }
+  as[tid] = s;
+  ac[tid] = c;
+  __syncthreads();
+  if (rg == 0 && h < nhot) {
+    for (uint32_t g = 1; g < 16u; g++) {
+      s += as[g * 64u + kk];
+      c += ac[g * 64u + kk];
+    }
+    if (c) lr_fx_adagrad(rows + (uint64_t)hrow[h] * 2, (long long)s, c, lr, fudge, inv_scale);
+  }
+}
+
+// every record's fid (the fixed-point step's key numbering)
+__global__ void k_lr_fx_fid(const int32_t *__restrict__ fvid, uint64_t n, const uint32_t *__restrict__ fid,
+                            int32_t *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int32_t)fid[fvid[i]];
+}
 // the per-key codes of the fixed-point step: hot rank | kLrHotBit, else the key's shard row
 __global__ void k_lr_fx_codes(const uint32_t *__restrict__ vid_row, uint64_t V, const int32_t *__restrict__ hot_of_vid,
                               uint32_t *__restrict__ vcode) {
@@ -1866,6 +2133,19 @@ struct swps_lr {
   int fx_bits = 40;                      // fixed-point scale 2^fx_bits (load: no sum can reach 2^62)
   std::vector<uint32_t> fx_hot_vids;     // the corpus's most frequent keys (load)
   swps::DevMem d_vcode, d_fx_hot, d_fx_hrow, d_acc_sum, d_acc_cnt, d_fx_list, d_fx_n, d_fx_stamp;
+  // the bucketed form (k_lr_fxb_step / k_lr_fxb_push; SWPS_LR_FX_ATOMIC=1 runs the atomic one)
+  swps::DevMem d_fchunk_c0;              // each chunk's first record, relative to its batch's first
+  swps::DevMem d_fxb_rec, d_fxb_boff, d_fxb_hsum, d_fxb_hcnt;
+  int fx_atomic = 0;
+  uint32_t fxb_grid = 768, fxb_nbk = 0, fxb_diag = 0;
+  // fid: the fixed-point step's key numbering — hot keys first (rank), then the rest in row-placement
+  // order; swps_lr_init places the rows in fid order, so a key's shard row is fx_row_base + fid
+  // (fx_affine, checked after the init) and the step needs no per-key code gather
+  std::vector<uint32_t> fx_fid;
+  swps::DevMem d_ffid;  // every record's fid
+  bool fx_affine = false;
+  uint32_t fx_row_base = 0;
+  uint64_t max_bchunks = 0;
   uint32_t fx_tag = 0;  // the step's tag in d_fx_stamp (never 0: the stamps start at 0)
   int plan_sort = 1;   // SWPS_LR_PLAN_SORT: tile shape of the plan's radix sorts (sort_pairs_tiled)
   uint64_t plan_next = 0;  // the first step whose plan is not enqueued yet
@@ -2349,6 +2629,20 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
     std::partial_sort(ord.begin(), ord.begin() + h, ord.end(),
                       [&](uint32_t a, uint32_t b) { return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b; });
     l->fx_hot_vids.assign(ord.begin(), ord.begin() + h);
+    // fids: the hot keys by rank, then the others in the placement order above (or by vid); the
+    // rows are placed in that order
+    const uint64_t V = l->vocab_keys.size();
+    std::vector<uint32_t> by(V);
+    if (l->vid_place.size() == V)
+      for (uint64_t v = 0; v < V; v++) by[l->vid_place[v]] = (uint32_t)v;
+    else
+      for (uint64_t v = 0; v < V; v++) by[v] = (uint32_t)v;
+    l->fx_fid.assign(V, ~0u);
+    for (size_t q = 0; q < h; q++) l->fx_fid[l->fx_hot_vids[q]] = (uint32_t)q;
+    uint32_t next = (uint32_t)h;
+    for (uint64_t j = 0; j < V; j++)
+      if (l->fx_fid[by[j]] == ~0u) l->fx_fid[by[j]] = next++;
+    l->vid_place = l->fx_fid;
   }
   if (!((l->cfg.plan == SWPS_LR_PLAN_STEP || l->cfg.plan == SWPS_LR_PLAN_NONE) && l->cfg.fast_sums && l->tiles))
     SWPS_TRY(lr_index(l));
@@ -2365,6 +2659,7 @@ int lr_fwd_chunks(swps_lr *l) {
   const uint64_t nr = l->label.size();
   hipStream_t s = l->s;
   std::vector<uint2> ch;
+  std::vector<uint32_t> c0;
   l->fwd_rpt = l->fwd_c == 4 || l->fwd_c == 16 ? l->fwd_c : kLrFwdRpt;  // records per thread (A/B: 4, 8, 16)
   const uint64_t cap = (uint64_t)l->fwd_rpt * 256;
   l->bfchunk.assign(1, 0);
@@ -2378,14 +2673,20 @@ int lr_fwd_chunks(swps_lr *l) {
       }
       if (l->row_off[r + 1] - l->row_off[first] > cap) {
         ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(r - first)));
+        c0.push_back((uint32_t)(l->row_off[first] - l->row_off[a0]));
         first = r;
       }
     }
-    if (a1 > first) ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(a1 - first)));
+    if (a1 > first) {
+      ch.push_back(make_uint2((uint32_t)(first - a0), (uint32_t)(a1 - first)));
+      c0.push_back((uint32_t)(l->row_off[first] - l->row_off[a0]));
+    }
     l->bfchunk.push_back(ch.size());
+    l->max_bchunks = std::max<uint64_t>(l->max_bchunks, l->bfchunk[b + 1] - l->bfchunk[b]);
   }
   if (l->fwd_c) {
     SWPS_TRY(upload(l->d_fchunk, ch, s));
+    SWPS_TRY(upload(l->d_fchunk_c0, c0, s));
     SWPS_HIP(hipStreamSynchronize(s));  // `ch` is a local
   }
   return SWPS_OK;
@@ -2403,8 +2704,8 @@ bool lr_fx_usable(const swps_lr *l) {
          !l->fwd_diag && !l->stage && l->nbatches > 0 && l->fwd_rpt == kLrFwdRpt;
 }
 
-// one batch of the fixed-point step: k_lr_fx_step over the batch's chunks of whole rows, then
-// k_lr_fx_apply over its pushed keys
+// one batch of the fixed-point step: k_lr_fxb_step over the batch's chunks of whole rows, then
+// k_lr_fxb_push over its buckets and hot keys (the atomic form: k_lr_fx_step, k_lr_fx_apply)
 int lr_batch_fx(swps_lr *l) {
   hipStream_t s = l->s;
   const uint64_t V = std::max<uint64_t>(l->vocab_keys.size(), 1), cap = l->t->cfg.capacity;
@@ -2428,7 +2729,40 @@ int lr_batch_fx(swps_lr *l) {
     k_lr_fx_codes<<<nblk(V), 256, 0, s>>>(l->d_vid_row.as<uint32_t>(), l->vocab_keys.size(),
                                           hot ? dhov.as<int32_t>() : nullptr, l->d_vcode.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
-    if (!l->d_acc_sum.p) {
+    const char *ea = getenv("SWPS_LR_FX_ATOMIC");  // A/B and tests: the per-record atomic form
+    l->fx_atomic = ea && atoi(ea) != 0;
+    if (const char *eg = getenv("SWPS_LR_FXB_GRID")) l->fxb_grid = (uint32_t)std::max(1, atoi(eg));
+    if (const char *ed = getenv("SWPS_LR_FXB_DIAG")) l->fxb_diag = (uint32_t)atoi(ed);
+    l->fxb_nbk = (uint32_t)((V + (1u << kLrFxVB) - 1) >> kLrFxVB);
+    if (l->fxb_nbk > kLrFxMaxBk) l->fx_atomic = 1;
+    l->fx_affine = false;
+    if (!l->fx_atomic && l->fx_fid.size() == V && l->vocab_keys.size() == V &&
+        !(getenv("SWPS_LR_FX_AFFINE") && atoi(getenv("SWPS_LR_FX_AFFINE")) == 0)) {
+      // rows placed in fid order by swps_lr_init (a table that held some keys before breaks it)
+      std::vector<uint32_t> vr(V);
+      SWPS_HIP(hipMemcpyAsync(vr.data(), l->d_vid_row.p, V * 4, hipMemcpyDeviceToHost, s));
+      SWPS_HIP(hipStreamSynchronize(s));
+      const uint32_t base = vr[0] - l->fx_fid[0];
+      bool aff = (uint64_t)base + V <= l->t->cfg.capacity;
+      for (uint64_t v = 0; v < V && aff; v++) aff = vr[v] == base + l->fx_fid[v];
+      if (aff) {
+        DevMem dfid;
+        SWPS_TRY(upload(dfid, l->fx_fid, s));
+        const uint64_t nnz = l->row_off.back();
+        SWPS_TRY(l->d_ffid.ensure(std::max<uint64_t>(nnz, 1) * 4));
+        k_lr_fx_fid<<<nblk(nnz), 256, 0, s>>>(l->d_fvid.as<int32_t>(), nnz, dfid.as<uint32_t>(), l->d_ffid.as<int32_t>());
+        SWPS_HIP(hipGetLastError());
+        SWPS_HIP(hipStreamSynchronize(s));
+        l->fx_affine = true;
+        l->fx_row_base = base;
+      }
+    }
+    if (!l->fx_atomic) {
+      SWPS_TRY(l->d_fxb_rec.ensure(std::max<uint64_t>(l->max_bnnz, 1) * 8));
+      SWPS_TRY(l->d_fxb_boff.ensure(std::max<uint64_t>(l->max_bchunks, 1) * (l->fxb_nbk + 1) * 2));
+      SWPS_TRY(l->d_fxb_hsum.ensure((uint64_t)l->fxb_grid * kLrHot * 8));
+      SWPS_TRY(l->d_fxb_hcnt.ensure((uint64_t)l->fxb_grid * kLrHot * 4));
+    } else if (!l->d_acc_sum.p) {
       SWPS_TRY(l->d_acc_sum.ensure(cap * 8));
       SWPS_TRY(l->d_acc_cnt.ensure(cap * 4));
       SWPS_TRY(l->d_fx_stamp.ensure(cap * 4));
@@ -2449,6 +2783,41 @@ int lr_batch_fx(swps_lr *l) {
   if (l->row_off[r1] == l->row_off[r0]) return SWPS_OK;
   const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
   const uint64_t nfc = l->bfchunk[bi + 1] - l->bfchunk[bi];
+  if (!l->fx_atomic) {
+    const uint32_t nh = hot ? (uint32_t)l->fx_hot_vids.size() : 0u, grid = (uint32_t)std::min<uint64_t>(nfc, l->fxb_grid);
+    const double scale = std::ldexp(1.0, l->fx_bits);
+    hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
+    const size_t dyn = (size_t)l->fxb_nbk * 4;
+    hipExtLaunchKernelGGL(l->fx_affine ? k_lr_fxb_step<kLrFwdRpt, true> : k_lr_fxb_step<kLrFwdRpt, false>, dim3(grid),
+                          dim3(256), dyn, s, fb, fe, 0,
+                          (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
+                          (const uint64_t *)l->d_row_off.as<uint64_t>(),
+                          (const int32_t *)(l->fx_affine ? l->d_ffid.as<int32_t>() : l->d_fvid.as<int32_t>()),
+                          (const uint32_t *)l->d_vcode.as<uint32_t>(), (const float *)l->d_fval.as<float>(),
+                          (const float *)l->d_label.as<float>(), r0, (const float *)l->t->rows.as<float>(),
+                          hot ? (const uint32_t *)l->d_fx_hrow.as<uint32_t>() : (const uint32_t *)nullptr, nh,
+                          l->d_err.as<float>(), l->d_err2.as<float>(), scale, l->fxb_nbk, l->d_fxb_rec.as<uint2>(),
+                          l->d_fxb_boff.as<uint16_t>(), l->d_fxb_hsum.as<unsigned long long>(),
+                          l->d_fxb_hcnt.as<uint32_t>(), l->fx_row_base, l->fxb_diag);
+    l->timer.ext_end(0, fb, fe);
+    hipEvent_t ab = l->timer.ext(), ae = l->timer.ext();
+    // SWPS_LR_FXB_DIAG (timing experiments only; results wrong): 1 buckets only, 2 hot keys only,
+    // 4 no record scatter, 8 no hot partials
+    const uint32_t pb0 = (l->fxb_diag & 2u) ? l->fxb_nbk : 0u,
+                   pb1 = (l->fxb_diag & 1u) ? l->fxb_nbk : l->fxb_nbk + (nh + 63u) / 64u;
+    hipExtLaunchKernelGGL(k_lr_fxb_push, dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), 0, s, ab, ae, 0,
+                          (const uint2 *)l->d_fxb_rec.as<uint2>(), (const uint16_t *)l->d_fxb_boff.as<uint16_t>(),
+                          (const uint32_t *)l->d_fchunk_c0.as<uint32_t>() + l->bfchunk[bi], (uint32_t)nfc, l->fxb_nbk,
+                          (const uint32_t *)l->d_vid_row.as<uint32_t>(),
+                          (const unsigned long long *)l->d_fxb_hsum.as<unsigned long long>(),
+                          (const uint32_t *)l->d_fxb_hcnt.as<uint32_t>(), grid,
+                          (const uint32_t *)l->d_fx_hrow.as<uint32_t>(), nh, l->t->rows.as<float>(),
+                          l->t->cfg.learning_rate, l->t->cfg.fudge, scale, std::ldexp(1.0, -l->fx_bits),
+                          (uint32_t)l->fx_affine, l->fx_row_base, pb0);
+    SWPS_HIP(hipGetLastError());
+    l->timer.ext_end(3, ab, ae);
+    return SWPS_OK;
+  }
   uint32_t *cur = l->d_fx_n.as<uint32_t>() + (step & 1), *next = l->d_fx_n.as<uint32_t>() + ((step + 1) & 1);
   hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
   hipExtLaunchKernelGGL(k_lr_fx_step<kLrFwdRpt>, dim3((unsigned)nfc), dim3(256), 0, s, fb, fe, 0,

@@ -456,8 +456,10 @@ def test_lr_tiles_match_record_path(lib, gpu, monkeypatch, bits, chunk):
             m.init()
             out += [m.train(2), m.params()[1], m.params()[2]]
         res.append(out)
-    for a, b in zip(res[1], res[2]):
+    for a, b, c, d in zip(res[1], res[2], res[3], res[4]):  # run to run; bucketed = atomic = gathered codes
         assert np.array_equal(a, b)
+        assert np.array_equal(a, c)
+        assert np.array_equal(a, d)
     for a, b in zip(res[0], res[1]):
         a = np.asarray(a, dtype=np.float64)
         b = np.asarray(b, dtype=np.float64)
@@ -593,7 +595,10 @@ def test_lr_plan_step_config3_batch(lib, gpu):
 @pytest.mark.parametrize("hot", ["1", "0"])
 def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
     """The fixed-point step (plan="none": no index; each key's sum of e*x_i as a 64-bit integer
-    at scale 2^s by atomics) is run-to-run bit-identical whatever order its atomics land in, and
+    at scale 2^s) is run-to-run bit-identical whatever order its adds land in, its bucketed form
+    (k_lr_fxb_*: LDS sums per key bucket, hot keys' per-block partials) equals its per-record
+    atomic form (SWPS_LR_FX_ATOMIC=1) and its form with gathered key codes instead of rows placed
+    by fid (SWPS_LR_FX_AFFINE=0) bit for bit, and it is
     within 1e-6 of the sorted fp64 sums (plan="load") after 2 epochs, relative to the weights'
     scale, on Criteo-shaped rows (hot keys: LDS sums, one global add per block) and ragged rows of
     1-60 features; its per-batch errors equal the sorted path's for the first batch (same forward)."""
@@ -607,7 +612,10 @@ def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
     vals = rng.random(int(roff[-1])).astype(np.float32)
     yl = (rng.random(4000) < 0.5).astype(np.float32)
     res = []
-    for plan in ("load", "none", "none"):
+    for plan, atomic, affine in (("load", "0", "1"), ("none", "0", "1"), ("none", "0", "1"), ("none", "1", "1"),
+                                 ("none", "0", "0")):
+        monkeypatch.setenv("SWPS_LR_FX_ATOMIC", atomic)
+        monkeypatch.setenv("SWPS_LR_FX_AFFINE", affine)
         out = []
         for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
             t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
@@ -618,8 +626,10 @@ def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
             m.close()
             t.close()
         res.append(out)
-    for a, b in zip(res[1], res[2]):
+    for a, b, c, d in zip(res[1], res[2], res[3], res[4]):  # run to run; bucketed = atomic = gathered codes
         assert np.array_equal(a, b)
+        assert np.array_equal(a, c)
+        assert np.array_equal(a, d)
     for a, b in zip(res[0], res[1]):
         a = np.asarray(a, dtype=np.float64)
         b = np.asarray(b, dtype=np.float64)
