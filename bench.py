@@ -650,9 +650,11 @@ def main():
     ap.add_argument("--app", default="w2v", choices=["w2v", "lr", "s2v"],
                     help="w2v: the headline (config 2); lr: config 3 shape; s2v: config 5 shape")
     ap.add_argument("--lr-batch", type=int, default=65536, help="LR rows per GPU per minibatch (config 3)")
-    ap.add_argument("--lr-plan", default="step", choices=["step", "load", "none"],
-                    help="LR: each minibatch's index built inside its step (beside the previous one; the "
-                         "reference gathers per minibatch, lr.cpp:215-227) or once at load for every minibatch")
+    ap.add_argument("--lr-plan", default="none", choices=["step", "load", "none"],
+                    help="LR: none = the fixed-point step (no per-minibatch index: each step groups its "
+                         "minibatch's keys itself, as the reference gathers per minibatch, lr.cpp:215-227); "
+                         "step = a sorted index per minibatch built beside the previous step; load = every "
+                         "minibatch's sorted index built once at load")
     ap.add_argument("--lr-exact", action="store_true",
                     help="LR: the reference's sequential fp32 per-key sums (bit-exact) instead of fast fp64 sums")
     ap.add_argument("--s2v-docs", type=int, default=8192, help="sent2vec documents per minibatch")
@@ -874,6 +876,9 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
     kt = m.kernel_times()
     xs = m.exchange_stats(on=0) if comm is not None else None
     m.set_profile(False)
+    pbat = [(warm + steps + k) % nb for k in range(steps)]  # the profiled pass's batches
+    fxb = [m.fx_bytes(b) for b in pbat] if args.lr_plan == "none" and comm is None and dist is None else []
+    fx = bool(fxb) and all(d["form"] == 1 for d in fxb)
     m.close()
     t.close()
     e2e, e2e_rows = ctx.max_sum(e2e, nb * B1)
@@ -884,15 +889,18 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
     # feature the sorted (row, x_i), the gathered e and the record written then read back (20 B);
     # per unique key its run (key, count, offset, shard row: 16 B) + the [w | g2] row read and
     # written (16 B).
-    pbat = [(warm + steps + k) % nb for k in range(steps)]
     nnz = sum(int(off[(b + 1) * B1] - off[b * B1]) for b in pbat)
     uniq = sum(len(np.unique(f[off[b * B1]:off[(b + 1) * B1]])) for b in pbat)
     fwd_ms, fwd_n = kt["forward"]
     fwd_bytes = 12 * nnz + 20 * steps * B1
-    tiles = not args.lr_exact and os.environ.get("SWPS_LR_TILES", "1") != "0"
+    tiles = not args.lr_exact and os.environ.get("SWPS_LR_TILES", "1") != "0" and not fx
+    if fx:  # the fixed-point step's own model (swps_lr_fx_bytes)
+        fwd_bytes = sum(d["step"] for d in fxb)
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
     push_ms, push_n = kt.get("push", (0.0, 0))
-    if tiles:  # row tiles: per feature its (row, x_i) (6 B); per piece its run and slot (8 B), per
+    if fx:
+        push_bytes = sum(d["push"] for d in fxb)
+    elif tiles:  # row tiles: per feature its (row, x_i) (6 B); per piece its run and slot (8 B), per
         # partial its fp64 write + read (16 B); per unique key its run (16 B) + the row RMW (16 B)
         pieces = partials = 0
         for b in pbat:
@@ -904,20 +912,24 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
         push_bytes = 20 * nnz + 32 * uniq
     push_gbs = push_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
     step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
-    kf = {"kernel": "k_lr_forward_c" if os.environ.get("SWPS_LR_FWD_C", "1") != "0" else "k_lr_forward_g",
+    kf = {"kernel": "k_lr_fxb_step (forward + per-chunk bucket sort + hot-key partials)" if fx
+          else "k_lr_forward_c" if os.environ.get("SWPS_LR_FWD_C", "1") != "0" else "k_lr_forward_g",
           "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
           "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
     kp = {"kernel": ("k_lr_records + k_lr_reduce_short + k_lr_reduce_long" if args.lr_exact
+                     else "k_lr_fxb_push (bucket LDS sums, hot-key column sums)" if fx
                      else "k_lr_tiles + k_lr_tiles_fin" if tiles
                      else "k_lr_records + k_lr_reduce_fused") + " (per-key mean + AdaGrad push)",
           "achieved": push_gbs, "frac": push_gbs / HBM_PEAK_GBS,
           "bytes_per_launch": push_bytes / max(push_n, 1), "avg_launch_ms": push_ms / max(push_n, 1),
           "launches": push_n}
     tr, tsrc = pmc_traffic(dict(app="lr", lr_batch=args.lr_batch, exact=bool(args.lr_exact), world=world,
-                                sharded=dist is not None),
-                           {"forward": ("k_lr_forward_c", "k_lr_forward_r", "k_lr_forward", "k_lr_forward_g"),
+                                sharded=dist is not None, plan=args.lr_plan),
+                           {"forward": ("k_lr_forward_c", "k_lr_forward_r", "k_lr_forward", "k_lr_forward_g",
+                                        "k_lr_fxb_step", "k_lr_fx_step"),
                             "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
-                                     "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin")})
+                                     "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin", "k_lr_fxb_push",
+                                     "k_lr_fx_apply")})
     for kd, name in ((kf, "forward"), (kp, "push")):
         kd["traffic"] = tr[name]
         kd["traffic_source"] = tsrc
@@ -936,14 +948,21 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
                                       % (world, ctx.backend, ", library-issued" if comm is not None else ""))
                       if dist is not None else "1 GPU, one HBM shard",
                       "mode": "exact (sequential fp32 per-key sums, bit-exact with the reference)" if args.lr_exact
-                      else "fast (fp64 per-key sums%s; within 1e-5 of the oracle)"
-                      % (" through row tiles" if tiles else ", wave tree-reduced"),
+                      else ("fixed point (each key's sum of e*x_i as an exact 64-bit integer at scale 2^s "
+                            "fixed at load: order-free, deterministic; no per-batch index, every minibatch's "
+                            "key grouping done inside its step; within 1e-6 of the fp64 sums)"
+                            if fx else "fast (fp64 per-key sums%s; within 1e-5 of the oracle)"
+                            % (" through row tiles" if tiles else ", wave tree-reduced")),
+                      "plan": args.lr_plan,
                       "features_per_s": total * nnz / max(steps * B1, 1) / dt,
                       "unique_keys_per_step": uniq / steps, "setup_s": setup_s,
                       "end_to_end": {"value": e2e_rows / e2e, "unit": "examples/s", "s": e2e, "minibatches": nb,
-                                     "note": "load (CSR to the GPU, the per-batch key-sorted index built once for "
-                                             "the corpus, the first full pull) + the first epoch to its last push, "
-                                             "max over ranks; `value` is the steady state of later epochs"}},
+                                     "note": ("load (CSR to the GPU, the vocabulary, the first full pull) + the "
+                                              "first epoch to its last push, max over ranks; no per-batch index "
+                                              "exists (plan none)" if fx else
+                                              "load (CSR to the GPU, the per-batch key-sorted index built once for "
+                                              "the corpus, the first full pull) + the first epoch to its last push, "
+                                              "max over ranks") + "; `value` is the steady state of later epochs"}},
            "roofline": dict(dom, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
                             step_GBps=step_gbs, step_frac=step_gbs / HBM_PEAK_GBS, other=other),
            "kernel_ms": {k: v[0] for k, v in kt.items() if v[1]},

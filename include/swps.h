@@ -539,6 +539,10 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
 int swps_lr_shard_comm(swps_lr *l, swps_comm *comm, int32_t frag_num);
 /* as swps_w2v_exchange_stats, for the library-driven sharded LR */
 int swps_lr_exchange_stats(swps_lr *l, int32_t on, double *out4);
+/* the fixed-point step (SWPS_LR_PLAN_NONE) on one batch, for roofline accounting: out8 = {step
+ * kernel bytes, push kernel bytes, form (1 bucketed, 2 atomic, 0 not running), hot keys, buckets,
+ * step blocks, non-hot records, distinct non-hot keys}; zeros before the first step */
+int swps_lr_fx_bytes(swps_lr *l, uint64_t batch, uint64_t *out8);
 
 #ifdef __cplusplus
 }

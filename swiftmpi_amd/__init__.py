@@ -601,6 +601,15 @@ class LR:
         check(capi.lib().swps_lr_exchange_stats(self.h, on, ptr(out)))
         return dict(zip(["bytes_remote", "bytes_total", "calls", "ms"], out.tolist()))
 
+    def fx_bytes(self, batch):
+        """The fixed-point step's algorithmic bytes on `batch` (swps_lr_fx_bytes): a dict with
+        step / push bytes, form (1 bucketed, 2 atomic, 0 other plan), hot, buckets, blocks,
+        nonhot records, distinct nonhot keys."""
+        out = np.zeros(8, dtype=np.uint64)
+        check(capi.lib().swps_lr_fx_bytes(self.h, batch, ptr(out)))
+        return dict(zip(["step", "push", "form", "hot", "buckets", "blocks", "nonhot", "uniq"],
+                        [int(x) for x in out]))
+
     def close(self):
         if getattr(self, "h", None):
             capi.lib().swps_lr_destroy(self.h)

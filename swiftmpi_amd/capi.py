@@ -149,6 +149,7 @@ PROTOS = {
     "swps_w2v_exchange_stats": (ctypes.c_int, [_p, _i32, _p]),
     "swps_lr_shard_comm": (ctypes.c_int, [_p, _p, _i32]),
     "swps_lr_exchange_stats": (ctypes.c_int, [_p, _i32, _p]),
+    "swps_lr_fx_bytes": (ctypes.c_int, [_p, _u64, _p]),
     "swps_unigram_starts": (ctypes.c_int, [_p, _p, _u64, _u64, _p]),
     "swps_glibc_rand": (ctypes.c_int, [ctypes.c_uint32, _u64, _u64, _p]),
     "swps_s2v_create": (ctypes.c_int, [_p, ctypes.POINTER(S2VCfg), ctypes.POINTER(_p)]),

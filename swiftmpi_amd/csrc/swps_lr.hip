@@ -1653,18 +1653,19 @@ __global__ __launch_bounds__(256) void k_lr_fx_apply(const uint32_t *__restrict_
 // into buckets of 2^kLrFxVB consecutive vids (a bucket's accumulators fit one block's LDS).
 // k_lr_fxb_step: a block walks chunks of whole rows (forward as k_lr_fx_step); per chunk it sorts
 //   its non-hot records by bucket in LDS (a counting sort: the order within a bucket is whatever
-//   the LDS atomics give — the sums below do not depend on it) and writes them, (vid, e*x_i as
-//   fp32), into the chunk's own span of `rec` with the chunk's bucket offsets (boff, u16); hot
+//   the LDS atomics give — the sums below do not depend on it) and writes them, (key, e*x_i as
+//   fp32), into the chunk's own span of `rec` with the chunk's bucket offsets (boff[bucket]
+//   [chunk], u16: one bucket's offsets contiguous for its reader); hot
 //   keys' terms stay in the block's LDS over all its chunks and go out once, as one row of the
 //   [block][hot] partial matrix (no atomics: every entry written).
 // k_lr_fxb_push: block b < nbk owns bucket b: it adds every chunk's records of the bucket into LDS
 //   (the fixed point of each term computed exactly as k_lr_fx_step does), then applies the mean
-//   and AdaGrad to each touched key's shard row; the blocks after them each reduce 64 hot keys'
-//   column of the partial matrix and apply theirs.  Integer sums: the result is the atomic form's,
+//   and AdaGrad to each touched key's shard row; the blocks after them each reduce 16 hot keys'
+//   columns of the partial matrix and apply theirs.  Integer sums: the result is the atomic form's,
 //   bit for bit, whatever the order.
 constexpr int kLrFxVB = 12;
 constexpr uint32_t kLrFxMaxBk = 4096;  // buckets (V <= 2^24); beyond it the atomic form runs
-template <int RPT, bool AFF>
+template <int RPT, bool AFF, int HC>
 __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ chunks, uint32_t nchunks,
                                                      const uint64_t *__restrict__ row_off,
                                                      const int32_t *__restrict__ fvid,
@@ -1674,15 +1675,16 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
                                                      const uint32_t *__restrict__ hrow, uint32_t nhot,
                                                      float *__restrict__ err, float *__restrict__ err2, double scale,
                                                      uint32_t nbk, uint2 *__restrict__ rec, uint16_t *__restrict__ boff,
+                                                     uint32_t bstride,
                                                      unsigned long long *__restrict__ hsum,
                                                      uint32_t *__restrict__ hcnt, uint32_t row_base, uint32_t diag) {
   constexpr int CAP = RPT * 256;
   __shared__ float prod[CAP];
   __shared__ uint16_t rl[CAP];
   __shared__ float es[CAP];
-  __shared__ float wh[kLrHot];
-  __shared__ unsigned long long hs[kLrHot];
-  __shared__ uint32_t hc[kLrHot];
+  __shared__ float wh[HC];
+  __shared__ unsigned long long hs[HC];
+  __shared__ uint32_t hc[HC];
   extern __shared__ uint32_t bc[];  // [nbk]: dynamic
   const int tid = threadIdx.x;
   HotW hw;
@@ -1782,14 +1784,13 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
         if (tid >= d) inc += o;
       }
       uint32_t run = inc - s;
-      uint16_t *orow = boff + (uint64_t)cix * (nbk + 1);
-      for (uint32_t q = b0; q < b1; q++) {
+      for (uint32_t q = b0; q < b1; q++) {  // boff[bucket][chunk]: a bucket's offsets contiguous
         const uint32_t c = bc[q];
         bc[q] = run;
-        orow[q] = (uint16_t)run;
+        boff[(uint64_t)q * bstride + cix] = (uint16_t)run;
         run += c;
       }
-      if (tid == 63) orow[nbk] = (uint16_t)inc;
+      if (tid == 63) boff[(uint64_t)nbk * bstride + cix] = (uint16_t)inc;
     }
     __syncthreads();
     const uint64_t base = c0 - z0;
@@ -1823,19 +1824,23 @@ __device__ __forceinline__ void lr_fx_adagrad(float *__restrict__ r, long long s
 }
 
 constexpr uint32_t kLrFxbPushT = 1024;  // k_lr_fxb_push's threads: one block per bucket, 16 waves
+constexpr uint32_t kLrFxbHotK = 16;     // hot keys per k_lr_fxb_push block (64 row groups each)
 __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__restrict__ rec,
                                                              const uint16_t *__restrict__ boff,
                                                              const uint32_t *__restrict__ chunk_c0, uint32_t nchunks,
-                                                             uint32_t nbk, const uint32_t *__restrict__ vid_row,
+                                                             uint32_t nbk, uint32_t bstride,
+                                                             const uint32_t *__restrict__ vid_row,
                                                              const unsigned long long *__restrict__ hsum,
                                                              const uint32_t *__restrict__ hcnt, uint32_t hblocks,
                                                              const uint32_t *__restrict__ hrow, uint32_t nhot,
                                                              float *__restrict__ rows, float lr, float fudge,
                                                              double scale, double inv_scale, uint32_t aff,
-                                                             uint32_t row_base, uint32_t first_block) {
+                                                             uint32_t row_base, uint32_t first_block,
+                                                             uint32_t diag) {
   constexpr uint32_t T = 1u << kLrFxVB, NT = kLrFxbPushT, PER = T / NT;
   __shared__ unsigned long long as[T];
   __shared__ uint32_t ac[T];
+  extern __shared__ uint32_t dyn_lds[];  // bucket blocks: 2 * nchunks + 1 words
   const uint32_t tid = threadIdx.x, bid = blockIdx.x + first_block;
   if (bid < nbk) {
     const uint32_t b = bid;
@@ -1844,27 +1849,65 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
       ac[v] = 0u;
     }
     __syncthreads();
-    for (uint32_t s = tid; s < nchunks; s += NT) {  // the chunks' segments of this bucket
-      const uint16_t *orow = boff + (uint64_t)s * (nbk + 1);
-      const uint32_t lo = orow[b], hi = orow[b + 1];
-      const uint2 *src = rec + chunk_c0[s];
-      uint2 r[4];  // the first four records' loads in flight together
+    // the bucket's records as one list over the chunks' segments (prefix in LDS): a lane takes the
+    // j-th record of the list, so one wave's lanes read neighbouring records of a few chunks —
+    // different keys, few LDS conflicts — and every lane has about the same number
+    uint32_t *segoff = dyn_lds;                 // [nchunks + 1]
+    uint32_t *segbase = dyn_lds + nchunks + 1;  // [nchunks]: the segment's first record in rec
+    __shared__ uint32_t wsum[NT / 64];
+    const uint32_t per = (nchunks + NT - 1) / NT, s0 = tid * per, s1 = min(nchunks, s0 + per);
+    uint32_t tot = 0;
+    for (uint32_t sq = s0; sq < s1; sq++) {
+      const uint32_t lo = boff[(uint64_t)b * bstride + sq], hi = boff[(uint64_t)(b + 1) * bstride + sq];
+      segbase[sq] = chunk_c0[sq] + lo;
+      segoff[sq] = hi - lo;  // length for now
+      tot += hi - lo;
+    }
+    uint32_t inc = tot;  // block-wide exclusive scan of the threads' totals
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d, 64);
+      if ((tid & 63u) >= (uint32_t)d) inc += o;
+    }
+    if ((tid & 63u) == 63u) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t w = 0; w < (tid >> 6); w++) wbase += wsum[w];
+    uint32_t run = wbase + inc - tot;
+    for (uint32_t sq = s0; sq < s1; sq++) {
+      const uint32_t len = segoff[sq];
+      segoff[sq] = run;
+      run += len;
+    }
+    if (tid == NT - 1) segoff[nchunks] = run;
+    __syncthreads();
+    const uint32_t R = (diag & 32u) ? 0u : segoff[nchunks];
+    for (uint32_t j0 = tid; j0 < R; j0 += 4 * NT) {
+      uint2 r[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t j = j0 + (uint32_t)k * NT;
+        if (j < R) {
+          uint32_t lo = 0, hi = nchunks;  // the last segment starting at or before j
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (segoff[mid] <= j)
+              lo = mid;
+            else
+              hi = mid;
+          }
+          r[k] = rec[segbase[lo] + (j - segoff[lo])];
+        }
+      }
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        if (lo + k < hi) r[k] = src[lo + k];
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (lo + k < hi) {
+        if (j0 + (uint32_t)k * NT < R) {
           atomicAdd(&as[r[k].x & (T - 1)], (unsigned long long)__double2ll_rn((double)__uint_as_float(r[k].y) * scale));
           atomicAdd(&ac[r[k].x & (T - 1)], 1u);
         }
-      for (uint32_t j = lo + 4; j < hi; j++) {
-        const uint2 q = src[j];
-        atomicAdd(&as[q.x & (T - 1)], (unsigned long long)__double2ll_rn((double)__uint_as_float(q.y) * scale));
-        atomicAdd(&ac[q.x & (T - 1)], 1u);
-      }
     }
     __syncthreads();
+    if (diag & 16u) return;
     uint32_t c[PER], row[PER];  // the thread's PER vids: row loads, then [w | g2] loads, all in flight
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
@@ -1885,14 +1928,16 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
       }
     return;
   }
-  // 64 hot keys per block: 16 row groups sum each key's column of the step's block partials
-  const uint32_t h0 = (bid - nbk) * 64u, kk = tid & 63u, rg = tid >> 6;
+  // kLrFxbHotK hot keys per block: the other threads' row groups sum each key's column of the step's
+  // block partials, then the groups' sums are added in LDS
+  constexpr uint32_t KPB = kLrFxbHotK, RG = NT / KPB;
+  const uint32_t h0 = (bid - nbk) * KPB, kk = tid % KPB, rg = tid / KPB;
   const uint32_t h = h0 + kk;
   unsigned long long s = 0ull;
   uint32_t c = 0u;
   if (h < nhot) {
 #pragma unroll 4
-    for (uint32_t blk = rg; blk < hblocks; blk += 16u) {
+    for (uint32_t blk = rg; blk < hblocks; blk += RG) {
       s += hsum[(uint64_t)blk * nhot + h];
       c += hcnt[(uint64_t)blk * nhot + h];
     }
@@ -1900,13 +1945,15 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
   as[tid] = s;
   ac[tid] = c;
   __syncthreads();
-  if (rg == 0 && h < nhot) {
-    for (uint32_t g = 1; g < 16u; g++) {
-      s += as[g * 64u + kk];
-      c += ac[g * 64u + kk];
+  for (uint32_t w = RG / 2; w >= 1; w >>= 1) {  // tree over the row groups
+    if (rg < w) {
+      as[tid] += as[tid + w * KPB];
+      ac[tid] += ac[tid + w * KPB];
     }
-    if (c) lr_fx_adagrad(rows + (uint64_t)hrow[h] * 2, (long long)s, c, lr, fudge, inv_scale);
+    __syncthreads();
   }
+  if (rg == 0 && h < nhot && ac[tid])
+    lr_fx_adagrad(rows + (uint64_t)hrow[h] * 2, (long long)as[tid], ac[tid], lr, fudge, inv_scale);
 }
 
 // every record's fid (the fixed-point step's key numbering)
@@ -2661,6 +2708,12 @@ int lr_fwd_chunks(swps_lr *l) {
   std::vector<uint2> ch;
   std::vector<uint32_t> c0;
   l->fwd_rpt = l->fwd_c == 4 || l->fwd_c == 16 ? l->fwd_c : kLrFwdRpt;  // records per thread (A/B: 4, 8, 16)
+  if (l->cfg.plan == SWPS_LR_PLAN_NONE && l->cfg.fast_sums && l->fwd_c == 1) {
+    // the fixed-point step: chunks of 4,096 records (its push reads each (chunk, bucket) segment:
+    // fewer, longer segments); SWPS_LR_FX_RPT = 8 for 2,048
+    const char *e = getenv("SWPS_LR_FX_RPT");
+    l->fwd_rpt = e && atoi(e) == 8 ? 8 : 16;
+  }
   const uint64_t cap = (uint64_t)l->fwd_rpt * 256;
   l->bfchunk.assign(1, 0);
   for (uint64_t b = 0; b < l->nbatches && l->fwd_c; b++) {
@@ -2701,7 +2754,7 @@ bool lr_plan_usable(const swps_lr *l) {
 
 bool lr_fx_usable(const swps_lr *l) {
   return l->cfg.plan == SWPS_LR_PLAN_NONE && !l->sharded && l->cfg.fast_sums && l->fwd_c && l->rows_per_wave == 1 &&
-         !l->fwd_diag && !l->stage && l->nbatches > 0 && l->fwd_rpt == kLrFwdRpt;
+         !l->fwd_diag && !l->stage && l->nbatches > 0 && (l->fwd_rpt == 8 || l->fwd_rpt == 16);
 }
 
 // one batch of the fixed-point step: k_lr_fxb_step over the batch's chunks of whole rows, then
@@ -2734,7 +2787,7 @@ int lr_batch_fx(swps_lr *l) {
     if (const char *eg = getenv("SWPS_LR_FXB_GRID")) l->fxb_grid = (uint32_t)std::max(1, atoi(eg));
     if (const char *ed = getenv("SWPS_LR_FXB_DIAG")) l->fxb_diag = (uint32_t)atoi(ed);
     l->fxb_nbk = (uint32_t)((V + (1u << kLrFxVB) - 1) >> kLrFxVB);
-    if (l->fxb_nbk > kLrFxMaxBk) l->fx_atomic = 1;
+    if (l->fxb_nbk > kLrFxMaxBk || (2 * l->max_bchunks + 1) * 4 > 96 * 1024) l->fx_atomic = 1;  // LDS bounds
     l->fx_affine = false;
     if (!l->fx_atomic && l->fx_fid.size() == V && l->vocab_keys.size() == V &&
         !(getenv("SWPS_LR_FX_AFFINE") && atoi(getenv("SWPS_LR_FX_AFFINE")) == 0)) {
@@ -2788,8 +2841,12 @@ int lr_batch_fx(swps_lr *l) {
     const double scale = std::ldexp(1.0, l->fx_bits);
     hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
     const size_t dyn = (size_t)l->fxb_nbk * 4;
-    hipExtLaunchKernelGGL(l->fx_affine ? k_lr_fxb_step<kLrFwdRpt, true> : k_lr_fxb_step<kLrFwdRpt, false>, dim3(grid),
-                          dim3(256), dyn, s, fb, fe, 0,
+    auto *kern = l->fwd_rpt == 16
+                     ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<16, true, 512> : k_lr_fxb_step<16, false, 512>)
+                                  : (l->fx_affine ? k_lr_fxb_step<16, true, kLrHot> : k_lr_fxb_step<16, false, kLrHot>))
+                     : (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, true, 512> : k_lr_fxb_step<8, false, 512>)
+                                  : (l->fx_affine ? k_lr_fxb_step<8, true, kLrHot> : k_lr_fxb_step<8, false, kLrHot>));
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), dyn, s, fb, fe, 0,
                           (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
                           (const uint64_t *)l->d_row_off.as<uint64_t>(),
                           (const int32_t *)(l->fx_affine ? l->d_ffid.as<int32_t>() : l->d_fvid.as<int32_t>()),
@@ -2797,30 +2854,34 @@ int lr_batch_fx(swps_lr *l) {
                           (const float *)l->d_label.as<float>(), r0, (const float *)l->t->rows.as<float>(),
                           hot ? (const uint32_t *)l->d_fx_hrow.as<uint32_t>() : (const uint32_t *)nullptr, nh,
                           l->d_err.as<float>(), l->d_err2.as<float>(), scale, l->fxb_nbk, l->d_fxb_rec.as<uint2>(),
-                          l->d_fxb_boff.as<uint16_t>(), l->d_fxb_hsum.as<unsigned long long>(),
+                          l->d_fxb_boff.as<uint16_t>(), (uint32_t)l->max_bchunks, l->d_fxb_hsum.as<unsigned long long>(),
                           l->d_fxb_hcnt.as<uint32_t>(), l->fx_row_base, l->fxb_diag);
     l->timer.ext_end(0, fb, fe);
     hipEvent_t ab = l->timer.ext(), ae = l->timer.ext();
     // SWPS_LR_FXB_DIAG (timing experiments only; results wrong): 1 buckets only, 2 hot keys only,
-    // 4 no record scatter, 8 no hot partials
+    // 4 no record scatter, 8 no hot partials, 16 buckets without the row updates, 32 buckets
+    // without their records
     const uint32_t pb0 = (l->fxb_diag & 2u) ? l->fxb_nbk : 0u,
-                   pb1 = (l->fxb_diag & 1u) ? l->fxb_nbk : l->fxb_nbk + (nh + 63u) / 64u;
-    hipExtLaunchKernelGGL(k_lr_fxb_push, dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), 0, s, ab, ae, 0,
+                   pb1 = (l->fxb_diag & 1u) ? l->fxb_nbk : l->fxb_nbk + (nh + kLrFxbHotK - 1) / kLrFxbHotK;
+    hipExtLaunchKernelGGL(k_lr_fxb_push, dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), (2 * nfc + 1) * 4, s, ab,
+                          ae, 0,
                           (const uint2 *)l->d_fxb_rec.as<uint2>(), (const uint16_t *)l->d_fxb_boff.as<uint16_t>(),
                           (const uint32_t *)l->d_fchunk_c0.as<uint32_t>() + l->bfchunk[bi], (uint32_t)nfc, l->fxb_nbk,
+                          (uint32_t)l->max_bchunks,
                           (const uint32_t *)l->d_vid_row.as<uint32_t>(),
                           (const unsigned long long *)l->d_fxb_hsum.as<unsigned long long>(),
                           (const uint32_t *)l->d_fxb_hcnt.as<uint32_t>(), grid,
                           (const uint32_t *)l->d_fx_hrow.as<uint32_t>(), nh, l->t->rows.as<float>(),
                           l->t->cfg.learning_rate, l->t->cfg.fudge, scale, std::ldexp(1.0, -l->fx_bits),
-                          (uint32_t)l->fx_affine, l->fx_row_base, pb0);
+                          (uint32_t)l->fx_affine, l->fx_row_base, pb0, l->fxb_diag);
     SWPS_HIP(hipGetLastError());
     l->timer.ext_end(3, ab, ae);
     return SWPS_OK;
   }
   uint32_t *cur = l->d_fx_n.as<uint32_t>() + (step & 1), *next = l->d_fx_n.as<uint32_t>() + ((step + 1) & 1);
   hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
-  hipExtLaunchKernelGGL(k_lr_fx_step<kLrFwdRpt>, dim3((unsigned)nfc), dim3(256), 0, s, fb, fe, 0,
+  hipExtLaunchKernelGGL(l->fwd_rpt == 16 ? k_lr_fx_step<16> : k_lr_fx_step<8>, dim3((unsigned)nfc), dim3(256), 0, s, fb,
+                        fe, 0,
                         (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi],
                         (const uint64_t *)l->d_row_off.as<uint64_t>(), (const int32_t *)l->d_fvid.as<int32_t>(),
                         (const uint32_t *)l->d_vcode.as<uint32_t>(), (const float *)l->d_fval.as<float>(),
@@ -3785,6 +3846,51 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
   for (int r = 0; r < l->world; r++) nsrc += src_counts[r] > 0;
   // one AdaGrad step per source, in rank order, all sources in one pass
   return table_push_sources(l->t, l->d_serve_rows.as<uint32_t>(), n, d_grads, l->s, false, nsrc <= 1);
+}
+
+// the fixed-point step's algorithmic bytes for batch `batch` (what the bucketed
+// form must move at least once): out[0] k_lr_fxb_step, out[1] k_lr_fxb_push, out[2] 1 when the
+// bucketed form runs (2: the atomic form, 0: another plan), out[3] hot keys, out[4] buckets,
+// out[5] the step's blocks, out[6] non-hot records, out[7] distinct non-hot keys
+int swps_lr_fx_bytes(swps_lr *l, uint64_t batch, uint64_t *out8) {
+  if (!l->loaded || batch >= l->nbatches) return fail(SWPS_E_CFG, "no such batch");
+  for (int i = 0; i < 8; i++) out8[i] = 0;
+  if (!lr_fx_usable(l) || !l->fx_ready) return SWPS_OK;
+  SWPS_TRY(lr_fvid_host(l));
+  const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
+  const uint64_t nh = hot ? l->fx_hot_vids.size() : 0;
+  std::vector<uint8_t> ishot(l->vocab_keys.size(), 0);
+  for (uint64_t q = 0; q < nh; q++) ishot[l->fx_hot_vids[q]] = 1;
+  const uint64_t r0 = batch * l->B1(), r1 = std::min<uint64_t>(l->label.size(), r0 + l->B1());
+  const uint64_t nnz = l->row_off[r1] - l->row_off[r0], nrows = r1 - r0;
+  uint64_t nonhot = 0, uniq = 0;
+  std::unordered_set<int32_t> u;
+  for (uint64_t c = l->row_off[r0]; c < l->row_off[r1]; c++) {
+    const int32_t v = l->fvid[c];
+    if (ishot[v]) continue;
+    nonhot++;
+    u.insert(v);
+  }
+  uniq = u.size();
+  const uint64_t nch = l->bfchunk[batch + 1] - l->bfchunk[batch];
+  const uint64_t grid = std::min<uint64_t>(nch, l->fxb_grid), nbk = l->fxb_nbk;
+  if (l->fx_atomic) {
+    out8[2] = 2;
+    return SWPS_OK;
+  }
+  // step: per record its fid, x_i and weight (12 B), per row its offset, label, e, e^2 (20 B), per
+  // non-hot record its (fid, e*x_i) written (8 B), the chunks' bucket offsets, the hot partials
+  out8[0] = 12 * nnz + 20 * nrows + 8 * nonhot + 2 * (nbk + 1) * nch + 12 * nh * grid;
+  // push: the records and offsets read back, each distinct non-hot key's [w | g2] read and written,
+  // the hot partials read, the hot keys' rows read and written
+  out8[1] = 8 * nonhot + 2 * (nbk + 1) * nch + 16 * uniq + 12 * nh * grid + 16 * nh;
+  out8[2] = 1;
+  out8[3] = nh;
+  out8[4] = nbk;
+  out8[5] = grid;
+  out8[6] = nonhot;
+  out8[7] = uniq;
+  return SWPS_OK;
 }
 
 int swps_lr_exchange_stats(swps_lr *l, int32_t on, double *out4) {
