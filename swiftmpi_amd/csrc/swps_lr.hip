@@ -1665,8 +1665,8 @@ __global__ __launch_bounds__(256) void k_lr_fx_apply(const uint32_t *__restrict_
 //   bit for bit, whatever the order.
 constexpr int kLrFxVB = 12;
 constexpr uint32_t kLrFxMaxBk = 4096;  // buckets (V <= 2^24); beyond it the atomic form runs
-template <int RPT, bool AFF, int HC>
-__global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ chunks, uint32_t nchunks,
+template <int RPT, int NT, bool AFF, int HC>
+__global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ chunks, uint32_t nchunks,
                                                      const uint64_t *__restrict__ row_off,
                                                      const int32_t *__restrict__ fvid,
                                                      const uint32_t *__restrict__ vcode,
@@ -1678,7 +1678,7 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
                                                      uint32_t bstride,
                                                      unsigned long long *__restrict__ hsum,
                                                      uint32_t *__restrict__ hcnt, uint32_t row_base, uint32_t diag) {
-  constexpr int CAP = RPT * 256;
+  constexpr int CAP = RPT * NT;
   __shared__ float prod[CAP];
   __shared__ uint16_t rl[CAP];
   __shared__ float es[CAP];
@@ -1687,13 +1687,22 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
   __shared__ uint32_t hc[HC];
   extern __shared__ uint32_t bc[];  // [nbk]: dynamic
   const int tid = threadIdx.x;
-  HotW hw;
-  hw.ld(rows, hrow, nhot, tid);
-  for (uint32_t q = (uint32_t)tid; q < nhot; q += 256u) {
+  constexpr int HPT = (HC + NT - 1) / NT;  // the block's hot weights: loads first, LDS stores later
+  float hv[HPT];
+#pragma unroll
+  for (int j = 0; j < HPT; j++) {
+    const uint32_t q = (uint32_t)tid + (uint32_t)(NT * j);
+    hv[j] = hrow && q < nhot ? rows[(uint64_t)(AFF ? row_base + q : hrow[q]) * 2] : 0.f;
+  }
+  for (uint32_t q = (uint32_t)tid; q < nhot; q += (uint32_t)NT) {
     hs[q] = 0ull;
     hc[q] = 0u;
   }
-  if (hrow) hw.st(wh, nhot, tid);
+#pragma unroll
+  for (int j = 0; j < HPT; j++) {
+    const uint32_t q = (uint32_t)tid + (uint32_t)(NT * j);
+    if (hrow && q < nhot) wh[q] = hv[j];
+  }
   const uint64_t z0 = row_off[r0];
   for (uint32_t cix = blockIdx.x; cix < nchunks; cix += gridDim.x) {
     const uint2 ch = chunks[cix];
@@ -1704,14 +1713,14 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
     float x[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
-      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
       f[k] = i < n ? fvid[c0 + i] : 0;
       x[k] = i < n ? fval[c0 + i] : 0.f;
     }
     uint32_t code[RPT];  // AFF: f is the key's fid (hot keys first) and its shard row row_base + fid
 #pragma unroll
     for (int k = 0; k < RPT; k++)
-      code[k] = ((uint32_t)tid + (uint32_t)k * 256u) >= n ? 0u
+      code[k] = ((uint32_t)tid + (uint32_t)k * (uint32_t)NT) >= n ? 0u
                 : AFF ? ((uint32_t)f[k] < nhot ? (kLrHotBit | (uint32_t)f[k]) : row_base + (uint32_t)f[k])
                       : vcode[f[k]];
     uint64_t ra = 0, rb = 0;
@@ -1721,26 +1730,26 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
       rb = row_off[rf + tid + 1];
       y = label[rf + tid];
     }
-    for (uint32_t q = (uint32_t)tid; q < nbk; q += 256u) bc[q] = 0u;
+    for (uint32_t q = (uint32_t)tid; q < nbk; q += (uint32_t)NT) bc[q] = 0u;
     __syncthreads();  // wh stored (first chunk); the previous chunk's LDS reads done
     float w[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
-      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
       w[k] = i >= n ? 0.f : (code[k] & kLrHotBit) ? wh[code[k] & (kLrHotBit - 1)] : rows[(uint64_t)code[k] * 2];
     }
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
-      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
       if (i < n) prod[i] = w[k] * x[k];
     }
-    for (uint32_t r = (uint32_t)tid; r < ch.y; r += 256u) {
-      const uint64_t a = r < 256u ? ra : row_off[rf + r], b = r < 256u ? rb : row_off[rf + r + 1];
+    for (uint32_t r = (uint32_t)tid; r < ch.y; r += (uint32_t)NT) {
+      const uint64_t a = r < (uint32_t)NT ? ra : row_off[rf + r], b = r < (uint32_t)NT ? rb : row_off[rf + r + 1];
       for (uint64_t c = a; c < b; c++) rl[c - c0] = (uint16_t)r;
     }
     __syncthreads();
-    for (uint32_t r = (uint32_t)tid; r < ch.y; r += 256u) {  // lr.cpp:358-367, in feature order
-      if (r >= 256u) {
+    for (uint32_t r = (uint32_t)tid; r < ch.y; r += (uint32_t)NT) {  // lr.cpp:358-367, in feature order
+      if (r >= (uint32_t)NT) {
         ra = row_off[rf + r];
         rb = row_off[rf + r + 1];
         y = label[rf + r];
@@ -1758,22 +1767,24 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
     uint32_t rk[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
-      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
       g[k] = 0.f;
       rk[k] = 0u;
       if (i < n) {
         g[k] = es[rl[i]] * x[k];  // lr.cpp:368
         if (code[k] & kLrHotBit) {
           const uint32_t h = code[k] & (kLrHotBit - 1);
-          atomicAdd(&hs[h], (unsigned long long)__double2ll_rn((double)g[k] * scale));
-          atomicAdd(&hc[h], 1u);
-        } else {
+          if (!(diag & 64u)) {
+            atomicAdd(&hs[h], (unsigned long long)__double2ll_rn((double)g[k] * scale));
+            atomicAdd(&hc[h], 1u);
+          }
+        } else if (!(diag & 128u)) {
           rk[k] = atomicAdd(&bc[(uint32_t)f[k] >> kLrFxVB], 1u);
         }
       }
     }
     __syncthreads();
-    if (tid < 64) {  // one wave: exclusive scan of the bucket counts, the chunk's offsets row
+    if (tid < 64 && !(diag & 128u)) {  // one wave: exclusive scan of the bucket counts, the chunk's offsets
       const uint32_t per = (nbk + 63u) / 64u, b0 = (uint32_t)tid * per, b1 = min(nbk, b0 + per);
       uint32_t s = 0;
       for (uint32_t q = b0; q < b1; q++) s += bc[q];
@@ -1796,7 +1807,7 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
     const uint64_t base = c0 - z0;
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
-      const uint32_t i = (uint32_t)tid + (uint32_t)k * 256u;
+      const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
       if (i < n && !(code[k] & kLrHotBit) && !(diag & 4u))
         rec[base + bc[(uint32_t)f[k] >> kLrFxVB] + rk[k]] = make_uint2((uint32_t)f[k], __float_as_uint(g[k]));
     }
@@ -1806,7 +1817,7 @@ __global__ __launch_bounds__(256) void k_lr_fxb_step(const uint2 *__restrict__ c
     __syncthreads();
     unsigned long long *hsr = hsum + (uint64_t)blockIdx.x * nhot;
     uint32_t *hcr = hcnt + (uint64_t)blockIdx.x * nhot;
-    for (uint32_t q = (uint32_t)tid; q < nhot; q += 256u) {
+    for (uint32_t q = (uint32_t)tid; q < nhot; q += (uint32_t)NT) {
       hsr[q] = hs[q];
       hcr[q] = hc[q];
     }
@@ -2185,6 +2196,7 @@ struct swps_lr {
   swps::DevMem d_fxb_rec, d_fxb_boff, d_fxb_hsum, d_fxb_hcnt;
   int fx_atomic = 0;
   uint32_t fxb_grid = 768, fxb_nbk = 0, fxb_diag = 0;
+  int fx_nt = 256;  // the fixed-point step's threads per block at 4,096-record chunks (SWPS_LR_FX_NT)
   // fid: the fixed-point step's key numbering — hot keys first (rank), then the rest in row-placement
   // order; swps_lr_init places the rows in fid order, so a key's shard row is fx_row_base + fid
   // (fx_affine, checked after the init) and the step needs no per-key code gather
@@ -2786,6 +2798,7 @@ int lr_batch_fx(swps_lr *l) {
     l->fx_atomic = ea && atoi(ea) != 0;
     if (const char *eg = getenv("SWPS_LR_FXB_GRID")) l->fxb_grid = (uint32_t)std::max(1, atoi(eg));
     if (const char *ed = getenv("SWPS_LR_FXB_DIAG")) l->fxb_diag = (uint32_t)atoi(ed);
+    if (const char *en = getenv("SWPS_LR_FX_NT")) l->fx_nt = atoi(en) == 512 ? 512 : 256;
     l->fxb_nbk = (uint32_t)((V + (1u << kLrFxVB) - 1) >> kLrFxVB);
     if (l->fxb_nbk > kLrFxMaxBk || (2 * l->max_bchunks + 1) * 4 > 96 * 1024) l->fx_atomic = 1;  // LDS bounds
     l->fx_affine = false;
@@ -2841,12 +2854,18 @@ int lr_batch_fx(swps_lr *l) {
     const double scale = std::ldexp(1.0, l->fx_bits);
     hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
     const size_t dyn = (size_t)l->fxb_nbk * 4;
-    auto *kern = l->fwd_rpt == 16
-                     ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<16, true, 512> : k_lr_fxb_step<16, false, 512>)
-                                  : (l->fx_affine ? k_lr_fxb_step<16, true, kLrHot> : k_lr_fxb_step<16, false, kLrHot>))
-                     : (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, true, 512> : k_lr_fxb_step<8, false, 512>)
-                                  : (l->fx_affine ? k_lr_fxb_step<8, true, kLrHot> : k_lr_fxb_step<8, false, kLrHot>));
-    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), dyn, s, fb, fe, 0,
+    // chunks of 4,096 records: 512 threads x 8 (default) or 256 x 16; of 2,048: 256 x 8
+    const int nt = l->fwd_rpt == 16 && l->fx_nt == 512 ? 512 : 256, rpt = nt == 512 ? 8 : l->fwd_rpt;
+    auto *kern = nt == 512 ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, 512, true, 512> : k_lr_fxb_step<8, 512, false, 512>)
+                                        : (l->fx_affine ? k_lr_fxb_step<8, 512, true, kLrHot>
+                                                        : k_lr_fxb_step<8, 512, false, kLrHot>))
+                 : rpt == 16 ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<16, 256, true, 512>
+                                                          : k_lr_fxb_step<16, 256, false, 512>)
+                                          : (l->fx_affine ? k_lr_fxb_step<16, 256, true, kLrHot>
+                                                          : k_lr_fxb_step<16, 256, false, kLrHot>))
+                 : (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, 256, true, 512> : k_lr_fxb_step<8, 256, false, 512>)
+                              : (l->fx_affine ? k_lr_fxb_step<8, 256, true, kLrHot> : k_lr_fxb_step<8, 256, false, kLrHot>));
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(nt), dyn, s, fb, fe, 0,
                           (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
                           (const uint64_t *)l->d_row_off.as<uint64_t>(),
                           (const int32_t *)(l->fx_affine ? l->d_ffid.as<int32_t>() : l->d_fvid.as<int32_t>()),
@@ -2860,7 +2879,7 @@ int lr_batch_fx(swps_lr *l) {
     hipEvent_t ab = l->timer.ext(), ae = l->timer.ext();
     // SWPS_LR_FXB_DIAG (timing experiments only; results wrong): 1 buckets only, 2 hot keys only,
     // 4 no record scatter, 8 no hot partials, 16 buckets without the row updates, 32 buckets
-    // without their records
+    // without their records, 64 no hot-key LDS sums, 128 no bucket sort
     const uint32_t pb0 = (l->fxb_diag & 2u) ? l->fxb_nbk : 0u,
                    pb1 = (l->fxb_diag & 1u) ? l->fxb_nbk : l->fxb_nbk + (nh + kLrFxbHotK - 1) / kLrFxbHotK;
     hipExtLaunchKernelGGL(k_lr_fxb_push, dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), (2 * nfc + 1) * 4, s, ab,
