@@ -235,13 +235,14 @@ static inline double diag_r(double x, int bit) {
 static inline void diag_row(const std::vector<double> &x, std::vector<double> &out, int bit) {
   out = x;
   if (!((orc_diag_round >> bit) & 1)) return;
-  if (orc_diag_round & (256 | 512)) {  // bits 8 / 9: block floating point, int32 / int40 mantissas, one exponent
+  if (orc_diag_round & (256 | 512 | 1024)) {  // bits 8 / 9 / 10: block floating point, int32 / int40 / int24
+                                                // mantissas, one exponent
     double mx = 0;
     for (double v : x) mx = std::max(mx, std::fabs(v));
     if (mx == 0) return;
     int e;
     std::frexp(mx, &e);
-    const int mb = (orc_diag_round & 256) ? 31 : 39;
+    const int mb = (orc_diag_round & 256) ? 31 : (orc_diag_round & 1024) ? 23 : 39;
     const double u = std::ldexp(1.0, e - mb);
     for (size_t i = 0; i < x.size(); i++) out[i] = std::nearbyint(x[i] / u) * u;
     return;

@@ -11,7 +11,7 @@ bits: 1 neu1 -> fp32, 2 neu1e -> fp32, 4 128-record chunk partials -> fp32,
 8 mean -> fp32 (3 | 4 | 8 = fast mode's roundings, 15); 16: bits 1/2 keep a
 bf16 residual; 32: an int16 residual per element; 64: int16 residual with one
 scale per row (+128: int8); 256 / 512: block floating point rows with int32 /
-int40 mantissas (BFP32 / BFP40)."""
+int40 mantissas (BFP32 / BFP40); 1024: int24 mantissas (BFP24)."""
 import os
 import sys
 
@@ -23,7 +23,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle  # noqa: E402
 from test_bench_shape_gpu import CFG, corpus, rel_err  # noqa: E402
 
-MODES = [("fast (fp32)", 15), ("BFP32", 259), ("fp32 + int16/row", 67 | 2 | 1), ("BFP40", 515)]
+MODES = [("fast (fp32)", 15), ("BFP32", 259), ("fp32 + int16/row", 67 | 2 | 1), ("BFP40", 515), ("BFP24", 1027)]
+if os.environ.get("DIAG_MODES"):
+    MODES = [m for m in MODES if m[0] in os.environ["DIAG_MODES"].split(",")]
 
 
 def run(path, D, bits, minibatch, epochs):

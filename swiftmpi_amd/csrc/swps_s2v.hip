@@ -32,6 +32,9 @@
 #include <cstdio>
 #include <limits>
 #include <unordered_map>
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <unordered_set>
 
 #include "swps_internal.h"
@@ -495,6 +498,15 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   const int D = m->D, B = m->cfg.minibatch, N = m->N, S = 2 * m->W + m->N + 1;
   const uint64_t T = m->cfg.unigram_size;
   hipStream_t s = m->s;
+  const bool tm = getenv("SWPS_S2V_LOAD_TIMES") != nullptr;  // phase times on stderr
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double tph = now();
+  auto phase = [&](const char *what) {
+    if (!tm) return;
+    const double t = now();
+    fprintf(stderr, "[s2v load] %-28s %8.3f s\n", what, t - tph);
+    tph = t;
+  };
   SWPS_HIP(hipSetDevice(m->t->cfg.device));
   std::vector<uint8_t> valid(nl);
   for (uint64_t l = 0; l < nl; l++)
@@ -506,6 +518,7 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   SWPS_TRY(swps_table_keys(m->t, tk.data(), tk.size(), &got));
   FlatMap64 present(got + 1024);
   for (uint64_t i = 0; i < got; i++) present.at(tk[i]) = 1;
+  phase("table keys + present map");
   // the rand() stream: the draws nobody reads (the WParam a pull constructs for a key the server
   // already holds, server.h:143-150) are counted and skipped in one jump before the next read
   GlibcRand rnd(m->cfg.rand_seed);
@@ -519,7 +532,6 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     return rnd.next();
   };
   auto rand_val = [&](int32_t r) { return ((double)(r / (float)2147483647) - 0.5) / (double)(size_t)D; };
-  std::vector<uint64_t> first_seen;  // the minibatch vocab in first-occurrence order (freq's keys)
   std::vector<uint64_t> miss_keys;
   std::vector<double> miss_rows;     // [h | v | h2 = 0 | v2 = 0] per miss
   std::unordered_set<uint64_t> lk;   // MiniBatch::_local_keys: one object, cleared per minibatch
@@ -536,26 +548,74 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   m->doc_lcg.clear();
   m->misses = m->max_recs = m->max_docs = 0;
   uint64_t lstate = 2008ULL;  // utils/random.h:44-47
-  uint64_t li = 0;
-  FlatMap64 freq(1 << 16);
-  while (true) {
-    // gather_keys(file, line_id, B) (word2vec.h:323-377)
-    lk.clear();
-    freq.clear();
-    first_seen.clear();
-    int cnt = 0;
-    for (uint64_t j = li; j < nl;) {
-      const uint64_t l = j++;
-      if (!valid[l]) continue;
-      for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) {
-        bool fresh = false;
-        freq.at(tok_keys[i], &fresh)++;
-        if (fresh) first_seen.push_back(tok_keys[i]);
+  // Per minibatch k, everything that depends on its own lines only — gather_keys' window (the next
+  // B + 1 valid lines from line k (B + 1), word2vec.h:323-377), its vocab in first-occurrence and in
+  // std::map order, the unigram run starts, the keys the table did not hold at load — is built by
+  // worker threads; the pass after them carries what runs through the minibatches in order (the
+  // rand() stream, the table's inserts, `_local_keys`' bucket count, the LCG, the documents).
+  struct Plan {
+    std::vector<uint64_t> first;  // the gather's vocab, first-occurrence order
+    std::vector<uint64_t> vkeys;  // std::map order
+    std::vector<uint64_t> st;     // unigram run starts
+    std::vector<uint64_t> cand;   // first-occurrence keys absent from the table at load
+    bool zero = false;
+  };
+  const uint64_t K = nl ? (nl + (uint64_t)B) / (uint64_t)(B + 1) : 0;  // handler windows of B + 1 lines
+  std::vector<Plan> plan(K);
+  {
+    int nth = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char *e = getenv("SWPS_S2V_THREADS")) nth = std::max(1, atoi(e));
+    nth = (int)std::min<uint64_t>((uint64_t)nth, std::max<uint64_t>(K, 1));
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+      FlatMap64 fq(1 << 16);
+      std::vector<std::pair<uint64_t, int32_t>> vc;
+      for (uint64_t k; (k = next.fetch_add(1)) < K;) {
+        Plan &pl = plan[k];
+        fq.clear();
+        int cnt = 0;
+        for (uint64_t j = k * (uint64_t)(B + 1); j < nl;) {
+          const uint64_t l = j++;
+          if (!valid[l]) continue;
+          for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) {
+            bool fresh = false;
+            fq.at(tok_keys[i], &fresh)++;
+            if (fresh) pl.first.push_back(tok_keys[i]);
+          }
+          if (++cnt > B) break;
+        }
+        if (pl.first.size() < 5) continue;  // the loop ends here (sent2vec.cpp:97)
+        pl.zero = fq.contains(0);
+        vc.clear();
+        for (uint64_t key : pl.first) {
+          vc.emplace_back(key, fq.at(key));
+          if (!present.contains(key)) pl.cand.push_back(key);
+        }
+        std::sort(vc.begin(), vc.end());
+        s2v_unigram_starts(vc, T, pl.st);
+        pl.vkeys.resize(vc.size());
+        for (size_t q = 0; q < vc.size(); q++) pl.vkeys[q] = vc[q].first;
       }
-      if (++cnt > B) break;
-    }
+    };
+    std::vector<std::thread> th;
+    for (int q = 1; q < nth; q++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+  }
+  phase("minibatch vocabs (threads)");
+  FlatMap64 inserted(1024);  // keys the minibatches so far inserted (the server's inserts persist)
+  doc_tok_keys.reserve(tok_keys.size());
+  m->doc_id.reserve(nl);
+  m->doc_tok.reserve(nl + 1);
+  m->doc_rec.reserve(nl + 1);
+  m->doc_lcg.reserve(nl);
+  doc_batch.reserve(nl);
+  for (uint64_t k = 0; k < K; k++) {
+    Plan &pl = plan[k];
+    const std::vector<uint64_t> &first_seen = pl.first;
+    const uint64_t li = k * (uint64_t)(B + 1);
     if (first_seen.size() < 5) break;  // sent2vec.cpp:97
-    if (freq.contains(0))
+    if (pl.zero)
       return fail(SWPS_E_UNSUPPORTED, "a minibatch vocab holds key 0 (atoi of a non-numeric word): the reference "
                                       "redraws negatives that hit it, a data-dependent draw count");
     // MiniBatch::pull: one WParam (2·D rand()) per pulled key in `_local_keys`
@@ -566,20 +626,20 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     // libstdc++ grows them only when a count passes that maximum) — so the set is filled, in the
     // reference's insertion order, only for a minibatch with misses or a new largest key set
     bool miss = false;
-    for (uint64_t k : first_seen)
-      if (!present.contains(k)) {
+    for (uint64_t key : pl.cand)
+      if (!inserted.contains(key)) {
         miss = true;
         break;
       }
     if (miss || first_seen.size() > lk_max) {
       lk.clear();
-      for (uint64_t k : first_seen) lk.insert(k);
+      for (uint64_t key : first_seen) lk.insert(key);
       lk_max = std::max<uint64_t>(lk_max, first_seen.size());
     }
     if (!miss) skip += 2 * (uint64_t)D * first_seen.size();
-    for (uint64_t k : lk) {
+    for (uint64_t key : lk) {
       if (!miss) break;
-      if (present.contains(k)) {
+      if (present.contains(key) || inserted.contains(key)) {
         skip += 2 * (uint64_t)D;
         continue;
       }
@@ -587,30 +647,24 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
       miss_rows.resize(o + 4 * (size_t)D, 0.0);
       for (int i = 0; i < 2 * D; i++) miss_rows[o + i] = rand_val(draw());
       skip += m->cfg.rand_insert_extra;
-      miss_keys.push_back(k);
-      present.at(k) = 1;
+      miss_keys.push_back(key);
+      inserted.at(key) = 1;
       m->misses++;
     }
-    std::vector<std::pair<uint64_t, int32_t>> vc;
-    vc.reserve(first_seen.size());
-    for (uint64_t k : first_seen) vc.emplace_back(k, freq.at(k));
-    std::sort(vc.begin(), vc.end());
-    std::vector<uint64_t> st;
-    s2v_unigram_starts(vc, T, st);
-    swps_s2v::Batch b{m->doc_id.size(), 0, vocab_keys.size(), starts_all.size(), (uint32_t)vc.size(), 0};
-    for (auto &kc : vc) vocab_keys.push_back(kc.first);
-    starts_all.insert(starts_all.end(), st.begin(), st.end());
+    swps_s2v::Batch b{m->doc_id.size(), 0, vocab_keys.size(), starts_all.size(), (uint32_t)pl.vkeys.size(), 0};
+    vocab_keys.insert(vocab_keys.end(), pl.vkeys.begin(), pl.vkeys.end());
+    starts_all.insert(starts_all.end(), pl.st.begin(), pl.st.end());
+    std::vector<uint64_t>().swap(pl.first);
+    std::vector<uint64_t>().swap(pl.vkeys);
+    std::vector<uint64_t>().swap(pl.st);
     // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not; the sentences' Vec::random
     // draws are this minibatch's next run of the stream (drawn on the device below)
     const uint64_t run_o = 344 + rnd.produced + skip, run_d0 = m->doc_id.size();
-    int lc = 0;
-    while (lc <= B && li < nl) {
-      const uint64_t l = li++;
-      lc++;
+    for (uint64_t l = li; l < std::min<uint64_t>(nl, li + (uint64_t)(B + 1)); l++) {
       if (!valid[l]) continue;
       const uint64_t L = line_off[l + 1] - line_off[l];
       m->doc_id.push_back(sent_ids[l]);
-      for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) doc_tok_keys.push_back(tok_keys[i]);
+      doc_tok_keys.insert(doc_tok_keys.end(), tok_keys.begin() + line_off[l], tok_keys.begin() + line_off[l + 1]);
       m->doc_tok.push_back(doc_tok_keys.size());
       m->doc_rec.push_back(m->doc_rec.back() + L * (uint64_t)m->cfg.niters);
       skip += (uint64_t)D;
@@ -618,14 +672,15 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
       lstate = lcg_jump(lstate, (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1)), kLcgA, kLcgC);
     }
     b.d1 = m->doc_id.size();
-    for (uint64_t k = 0, tot = (b.d1 - run_d0) * (uint64_t)D; k < tot; k += kRandRun)
-      rand_chunks.insert(rand_chunks.end(), {run_d0 * (uint64_t)D + k, run_o + k, std::min<uint64_t>(kRandRun, tot - k)});
+    for (uint64_t q = 0, tot = (b.d1 - run_d0) * (uint64_t)D; q < tot; q += kRandRun)
+      rand_chunks.insert(rand_chunks.end(), {run_d0 * (uint64_t)D + q, run_o + q, std::min<uint64_t>(kRandRun, tot - q)});
     b.recs = m->doc_rec[b.d1] - m->doc_rec[b.d0];
     doc_batch.resize(b.d1, (uint32_t)m->batches.size());
     m->max_recs = std::max(m->max_recs, b.recs);
     m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
     m->batches.push_back(b);
   }
+  phase("minibatch schedule (host)");
   m->lstate_end = lstate;
   rnd.discard(skip);
   m->rand_calls = rnd.produced;  // includes the rand_offset skipped above
@@ -657,6 +712,7 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     SWPS_TRY(table_lookup(m->t, dt.as<uint64_t>(), doc_tok_keys.size(), m->d_tok_row.as<uint32_t>(), s));
     SWPS_TRY(table_check_error(m->t, s));  // syncs; every key is present by now
   }
+  phase("misses + row lookups");
   SWPS_TRY(upload(m->d_starts, starts_all, s));
   {
     std::vector<uint64_t> bv0, bs0;
@@ -705,6 +761,7 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   SWPS_TRY(m->d_err.ensure(std::max<uint64_t>(nd, 1) * 4));
   SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(m->max_recs, 1) * (uint64_t)S * 4));
   SWPS_HIP(hipStreamSynchronize(s));  // host vectors above go out of scope
+  phase("uploads + sentence rand()");
   m->loaded = true;
   m->cursor = 0;
   return SWPS_OK;
