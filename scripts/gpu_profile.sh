@@ -61,7 +61,7 @@ for L in $LEGS; do
                 bench.py --gpus 1 --steps 200 --warmup 10 --minibatch 100 --no-cpu-baseline --no-parity-leg --config1-steps 0 --no-app-legs ;;
     w2v_parity) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"parity\", \"sharded\": false}" $W2V --parity ;;
     w2v_fast) leg $L 20 "{$W2VCFG, $TEXT8, \"minibatch\": 5000, \"mode\": \"fast\", \"sharded\": false}" $W2V --precision fast ;;
-    lr) leg $L 20 '{"app": "lr", "lr_batch": 65536, "exact": false, "world": 1, "sharded": false}' \
+    lr) leg $L 20 '{"app": "lr", "lr_batch": 65536, "exact": false, "world": 1, "sharded": false, "plan": "none"}' \
           bench.py --app lr --steps 20 --warmup 3 --no-cpu-baseline ;;
     # 124 + 31 minibatches of 8193 docs: every docs launch (one per 31 minibatches: 262,144 docs at
     # most) the same size, so rocprof's per-launch average and the profiled pass's agree
