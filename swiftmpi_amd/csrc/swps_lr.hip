@@ -25,6 +25,7 @@
 #include <limits>
 #include <string>
 #include <unordered_map>
+#include <chrono>
 #include <unordered_set>
 
 #include "swps_internal.h"
@@ -2619,8 +2620,25 @@ int lr_vocab(swps_lr *l, const std::vector<uint32_t> &feat) {
   return SWPS_OK;
 }
 
+// SWPS_LR_LOAD_TIMES: the load's phases on stderr
+struct LoadTimer {
+  bool on = getenv("SWPS_LR_LOAD_TIMES") != nullptr;
+  double t = now();
+  static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void operator()(const char *what) {
+    if (!on) return;
+    const double u = now();
+    fprintf(stderr, "[lr load] %-30s %8.4f s\n", what, u - t);
+    t = u;
+  }
+};
+
 int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
+  LoadTimer phase;
   SWPS_TRY(lr_vocab(l, feat));
+  phase("vocabulary (GPU sort)");
   feat.clear();
   feat.shrink_to_fit();
   const uint64_t nr = l->label.size();
@@ -2648,6 +2666,7 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
     l->vid_place.resize(V);
     for (uint64_t j = 0; j < V; j++) l->vid_place[ord[j].second] = (uint32_t)j;
   }
+  phase("row placement (host)");
   hipStream_t s = l->s;
   SWPS_TRY(upload(l->d_label, l->label, s));
   SWPS_TRY(upload(l->d_row_off, l->row_off, s));
@@ -2672,6 +2691,7 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
   l->plan_ready = false;
   l->plan_next = 0;
   l->fx_ready = false;
+  phase("uploads + batch extents");
   if (l->cfg.plan == SWPS_LR_PLAN_NONE && l->cfg.fast_sums) {
     // the fixed-point step: its scale (every sum below 2^62: |e| <= max|y| + 1, at most the batch's
     // records per key) and the corpus's most frequent keys (their sums go through LDS)
@@ -2702,6 +2722,7 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
     for (uint64_t j = 0; j < V; j++)
       if (l->fx_fid[by[j]] == ~0u) l->fx_fid[by[j]] = next++;
     l->vid_place = l->fx_fid;
+    phase("fixed-point scale, hot keys, fids");
   }
   if (!((l->cfg.plan == SWPS_LR_PLAN_STEP || l->cfg.plan == SWPS_LR_PLAN_NONE) && l->cfg.fast_sums && l->tiles))
     SWPS_TRY(lr_index(l));
