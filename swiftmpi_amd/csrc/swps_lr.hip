@@ -26,6 +26,7 @@
 #include <string>
 #include <unordered_map>
 #include <chrono>
+#include <thread>
 #include <unordered_set>
 
 #include "swps_internal.h"
@@ -2554,9 +2555,8 @@ int lr_fvid_host(swps_lr *l) {
 // order, which depends only on the order the keys were first inserted: with init_ref, the V
 // distinct keys (not the records) are inserted in first-occurrence order on the host and the
 // iteration order kept as the init's pull order.
-int lr_vocab(swps_lr *l, const std::vector<uint32_t> &feat) {
+int lr_vocab(swps_lr *l, const uint32_t *feat, uint64_t n) {
   hipStream_t s = l->s;
-  const uint64_t n = feat.size();
   if (n >= (1ULL << 32)) return fail(SWPS_E_UNSUPPORTED, "more than 2^32 features per rank");
   SWPS_TRY(l->d_fvid.ensure(std::max<uint64_t>(n, 1) * 4));
   l->vocab_keys.clear();
@@ -2565,7 +2565,8 @@ int lr_vocab(swps_lr *l, const std::vector<uint32_t> &feat) {
   l->fvid.clear();
   if (!n) return SWPS_OK;
   DevMem dfeat, ks, perm, head, rank, ukey, ufirst, ustart, tmp;
-  SWPS_TRY(upload(dfeat, feat, s));
+  SWPS_TRY(dfeat.ensure(n * 4));
+  SWPS_HIP(hipMemcpyAsync(dfeat.p, feat, n * 4, hipMemcpyHostToDevice, s));
   SWPS_TRY(ks.ensure(n * 4));
   SWPS_TRY(perm.ensure(n * 4));
   size_t b = 0;
@@ -2635,12 +2636,11 @@ struct LoadTimer {
   }
 };
 
-int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
+// feat: the caller's array of every record's key (read during this call only)
+int lr_ingest(swps_lr *l, const uint32_t *feat, uint64_t nfeat) {
   LoadTimer phase;
-  SWPS_TRY(lr_vocab(l, feat));
+  SWPS_TRY(lr_vocab(l, feat, nfeat));
   phase("vocabulary (GPU sort)");
-  feat.clear();
-  feat.shrink_to_fit();
   const uint64_t nr = l->label.size();
   l->nbatches = nr ? (nr + l->B1() - 1) / l->B1() : 0;
   // the rows the single-GPU init gives the keys (swps_lr_init): in the order the keys first appear,
@@ -2696,7 +2696,20 @@ int lr_ingest(swps_lr *l, std::vector<uint32_t> &&feat) {
     // the fixed-point step: its scale (every sum below 2^62: |e| <= max|y| + 1, at most the batch's
     // records per key) and the corpus's most frequent keys (their sums go through LDS)
     float mx = 0.f, my = 0.f;
-    for (float v : l->fval) mx = std::max(mx, std::fabs(v));
+    {  // max |x_i| over the corpus: threads over slices
+      const uint64_t nf = l->fval.size();
+      const int nth = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, nf >> 22));
+      std::vector<float> part(nth, 0.f);
+      std::vector<std::thread> th;
+      for (int q = 0; q < nth; q++)
+        th.emplace_back([&, q] {
+          float m = 0.f;
+          for (uint64_t i = nf * q / nth; i < nf * (q + 1) / nth; i++) m = std::max(m, std::fabs(l->fval[i]));
+          part[q] = m;
+        });
+      for (auto &t : th) t.join();
+      for (float m : part) mx = std::max(mx, m);
+    }
     for (float v : l->label) my = std::max(my, std::fabs(v));
     const double bound = std::max(1e-30, ((double)my + 1.0) * (double)mx * (double)std::max<uint64_t>(l->max_bnnz, 1));
     l->fx_bits = (int)std::min(40.0, std::floor(62.0 - std::log2(bound)));
@@ -3526,7 +3539,7 @@ int swps_lr_load_text(swps_lr *l, const char *path) {
   free(buf);
   fclose(f);
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
-  return lr_ingest(l, std::move(feat));
+  return lr_ingest(l, feat.data(), feat.size());
 }
 
 int swps_lr_load_csr(swps_lr *l, const float *labels, uint64_t nrows, const uint64_t *row_off, const uint32_t *feat,
@@ -3537,7 +3550,7 @@ int swps_lr_load_csr(swps_lr *l, const float *labels, uint64_t nrows, const uint
   const uint64_t nnz = row_off[nrows];
   l->fval.assign(vals, vals + nnz);
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
-  return lr_ingest(l, std::vector<uint32_t>(feat, feat + nnz));
+  return lr_ingest(l, feat, nnz);
 }
 
 int swps_lr_init(swps_lr *l) {
