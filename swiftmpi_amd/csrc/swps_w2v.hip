@@ -144,26 +144,39 @@ __global__ __launch_bounds__(256) void k_pull(const int32_t *__restrict__ K, uin
 }
 
 // float-LCG keep flags for the epoch (to_sample, word2vec_global.h:725-731):
-// token t consumes the (t+1)-th draw after the epoch's start state.  Each
-// thread jumps once to the start of its run of kKeepRun tokens, then steps.
+// token t consumes the (t+1)-th draw after the epoch's start state.  k_keep_mb:
+// each thread jumps once to the start of its run of kKeepRun tokens, then steps.
 constexpr int kKeepRun = 16;
-__global__ void k_keep(const int32_t *__restrict__ tok, uint64_t nt, const float *__restrict__ ran, uint64_t fstate,
-                       int sample_on, int32_t *__restrict__ kflag) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = r * kKeepRun;
-  if (i0 > nt) return;
-  uint64_t y = sample_on ? lcg_jump(fstate, i0, kFlcgA, kLcgC) : 0;
-  for (uint64_t i = i0; i < i0 + kKeepRun && i <= nt; i++) {
-    if (i == nt) {
-      kflag[i] = 0;
-      break;
-    }
-    int32_t keep = 1;
-    if (sample_on) {
-      y = y * kFlcgA + kLcgC;
-      keep = flcg_value(y) > ran[tok[i]];
+// float-LCG (subsampling) jumps by 2^i draws, x -> c_f2A[i] x + c_f2C[i] (set at create)
+__constant__ uint64_t c_f2A[64];
+__constant__ uint64_t c_f2C[64];
+__device__ __forceinline__ uint64_t flcg_jump_p2(uint64_t x, uint64_t k) {
+  for (int i = 0; k; i++, k >>= 1)
+    if (k & 1) x = c_f2A[i] * x + c_f2C[i];
+  return x;
+}
+// A wave takes 64 * kKeepIt consecutive tokens, lane l the tokens base + l + 64 j (coalesced loads and
+// stores); the lane's float-LCG state jumps once to its first token, then 64 draws per step.
+constexpr int kKeepIt = 16;
+__global__ __launch_bounds__(256) void k_keep(const int32_t *__restrict__ tok, uint64_t nt,
+                                              const float *__restrict__ ran, uint64_t fstate, int sample_on,
+                                              int32_t *__restrict__ kflag) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t lane = g & 63, base = (g >> 6) * (64ULL * kKeepIt);
+  if (base > nt) return;
+  uint64_t y = sample_on ? flcg_jump_p2(fstate, base + lane) : 0;  // the state after token base+lane-1's draw
+  const uint64_t A64 = c_f2A[6], C64 = c_f2C[6];
+#pragma unroll 4
+  for (int j = 0; j < kKeepIt; j++) {
+    const uint64_t i = base + lane + 64ULL * (uint64_t)j;
+    if (i > nt) break;
+    int32_t keep = 0;  // kflag[nt] = 0: the scan's end
+    if (i < nt) {
+      keep = 1;
+      if (sample_on) keep = flcg_value(y * kFlcgA + kLcgC) > ran[tok[i]];  // word2vec_global.h:725-731
     }
     kflag[i] = keep;
+    y = A64 * y + C64;
   }
 }
 
@@ -3281,8 +3294,8 @@ int plan_epoch(swps_w2v *w) {
                                                               (uint32_t)nb, w->d_tw.as<int32_t>(), w->cfg.sample,
                                                               w->fstate, sample_on, w->d_kflag.as<int32_t>());
   } else {
-    k_keep<<<nblk((T + kKeepRun) / kKeepRun), 256, 0, s>>>(w->d_tok.as<int32_t>(), T, w->d_ran.as<float>(), w->fstate,
-                                                           sample_on, w->d_kflag.as<int32_t>());
+    k_keep<<<nblk((T + 64 * kKeepIt) / (64 * kKeepIt) * 64), 256, 0, s>>>(w->d_tok.as<int32_t>(), T, w->d_ran.as<float>(),
+                                                                          w->fstate, sample_on, w->d_kflag.as<int32_t>());
   }
   SWPS_HIP(hipGetLastError());
   size_t tb1 = 0, tb2 = 0;
@@ -4134,10 +4147,18 @@ int swps_w2v_create(swps_table *t, const swps_w2v_cfg *cfg, swps_w2v **out) {
       PA[i] = lcg_jump(1, 1ULL << i, kLcgA, kLcgC) - lcg_jump(0, 1ULL << i, kLcgA, kLcgC);
       PC[i] = lcg_jump(0, 1ULL << i, kLcgA, kLcgC);
     }
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_jumpA), A, sizeof(A)) != hipSuccess ||
+    uint64_t FA[64], FC[64];  // the subsampling float LCG's jumps by 2^i draws
+    for (int i = 0; i < 64; i++) {
+      FA[i] = lcg_jump(1, 1ULL << i, kFlcgA, kLcgC) - lcg_jump(0, 1ULL << i, kFlcgA, kLcgC);
+      FC[i] = lcg_jump(0, 1ULL << i, kFlcgA, kLcgC);
+    }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_f2A), FA, sizeof(FA)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_f2C), FC, sizeof(FC)) != hipSuccess)
+      rc = fail(SWPS_E_HIP, "constant upload");
+    if (!rc && (hipMemcpyToSymbol(HIP_SYMBOL(c_jumpA), A, sizeof(A)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_jumpC), C, sizeof(C)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_p2A), PA, sizeof(PA)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_p2C), PC, sizeof(PC)) != hipSuccess)
+        hipMemcpyToSymbol(HIP_SYMBOL(c_p2C), PC, sizeof(PC)) != hipSuccess))
       rc = fail(SWPS_E_HIP, "constant upload");
   }
   if (rc) {
