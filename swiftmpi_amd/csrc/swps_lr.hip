@@ -1765,23 +1765,24 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
       es[r] = error;
     }
     __syncthreads();
-    float g[RPT];
-    uint32_t rk[RPT];
+    // every record's term g = e * x_i (lr.cpp:368): a hot key's into its LDS sum, the others into
+    // prod (free since the row sums) with their rank inside their bucket in rl (free after g) —
+    // nothing but f (and, without AFF, the codes) stays in registers across the scan below
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
       const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
-      g[k] = 0.f;
-      rk[k] = 0u;
       if (i < n) {
-        g[k] = es[rl[i]] * x[k];  // lr.cpp:368
-        if (code[k] & kLrHotBit) {
-          const uint32_t h = code[k] & (kLrHotBit - 1);
+        const float g = es[rl[i]] * x[k];
+        const bool hot = AFF ? (uint32_t)f[k] < nhot : (code[k] & kLrHotBit) != 0;
+        if (hot) {
+          const uint32_t h = AFF ? (uint32_t)f[k] : code[k] & (kLrHotBit - 1);
           if (!(diag & 64u)) {
-            atomicAdd(&hs[h], (unsigned long long)__double2ll_rn((double)g[k] * scale));
+            atomicAdd(&hs[h], (unsigned long long)__double2ll_rn((double)g * scale));
             atomicAdd(&hc[h], 1u);
           }
-        } else if (!(diag & 128u)) {
-          rk[k] = atomicAdd(&bc[(uint32_t)f[k] >> kLrFxVB], 1u);
+        } else {
+          prod[i] = g;
+          rl[i] = (diag & 128u) ? (uint16_t)0 : (uint16_t)atomicAdd(&bc[(uint32_t)f[k] >> kLrFxVB], 1u);
         }
       }
     }
@@ -1810,8 +1811,9 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
       const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
-      if (i < n && !(code[k] & kLrHotBit) && !(diag & 4u))
-        rec[base + bc[(uint32_t)f[k] >> kLrFxVB] + rk[k]] = make_uint2((uint32_t)f[k], __float_as_uint(g[k]));
+      const bool hot = AFF ? (uint32_t)f[k] < nhot : (code[k] & kLrHotBit) != 0;
+      if (i < n && !hot && !(diag & 4u))
+        rec[base + bc[(uint32_t)f[k] >> kLrFxVB] + rl[i]] = make_uint2((uint32_t)f[k], __float_as_uint(prod[i]));
     }
     __syncthreads();  // bc / es / rl are the next chunk's
   }
