@@ -2237,6 +2237,7 @@ struct swps_w2v {
   int overlap = -1;
   hipStream_t s_prep = nullptr;
   hipEvent_t ev_learn = nullptr, ev_prep = nullptr;
+  hipEvent_t fwd_event = nullptr;  // learn_batch records it after the forward when set (overlap mode 2)
   DevMem *prep_set[kPrepBufs] = {&d_pos_tok, &d_rec,  &d_pkeys, &d_pvals, &d_pkeys_s, &d_pvals_s, &d_tmp,
                                  &d_seg,     &d_icnt, &d_ioff,  &d_desc,  &d_lead,    &d_multi, &d_krow, &d_local};
   // stats
@@ -3761,6 +3762,7 @@ template <typename T, typename A> int learn_batch(swps_w2v *w, const void *d_val
     SWPS_HIP(hipGetLastError());
     tm.end(KT_FWD, ef, s);
   }
+  if (w->fwd_event) SWPS_HIP(hipEventRecord(w->fwd_event, s));
   // fast mode, single GPU: the push sums the single-chunk runs itself (k_push_tg)
   const bool fast_tail = std::is_same<T, float>::value && std::is_same<A, float>::value && w->tail &&
                          w->fused_push && D < 512 && pb.sorted && !w->bfp;
@@ -4056,6 +4058,33 @@ template <typename T, typename A> int train_overlapped(swps_w2v *w, uint64_t cou
   }
   const hipStream_t s = w->s;
   bool prep_pending = false;  // batch i's prep ran on s_prep (ev_prep)
+  if (w->overlap == 2) {
+    // prep(i+1) issued after learn(i), waiting for forward(i): it runs beside the gather and the
+    // push (latency-bound) instead of beside the forward (bandwidth-bound).  It writes the other
+    // buffer set, whose last user learn(i-1) finished before forward(i) did.
+    for (uint64_t i = 0; i < count; i++) {
+      if (!w->pb.valid) SWPS_TRY(prep_batch(w));  // inline on s (first batch of the call)
+      if (prep_pending) SWPS_HIP(hipStreamWaitEvent(s, w->ev_prep, 0));
+      w->fwd_event = i + 1 < count ? w->ev_learn : nullptr;
+      const int lrc = learn_batch<T, A>(w);  // cursor -> i + 1
+      w->fwd_event = nullptr;
+      SWPS_TRY(lrc);
+      prep_pending = false;
+      if (i + 1 < count) {
+        SWPS_HIP(hipStreamWaitEvent(w->s_prep, w->ev_learn, 0));
+        swap_prep_set(w);  // the other set becomes the current one: prep(i+1) fills it, learn(i+1) reads it
+        w->s = w->s_prep;
+        w->pb = swps_w2v::Prepped();
+        const int rc = prep_batch(w);
+        w->s = s;
+        SWPS_TRY(rc);
+        SWPS_HIP(hipEventRecord(w->ev_prep, w->s_prep));
+        prep_pending = true;
+      }
+    }
+    if (prep_pending) SWPS_HIP(hipStreamWaitEvent(s, w->ev_prep, 0));
+    return SWPS_OK;
+  }
   for (uint64_t i = 0; i < count; i++) {
     if (!w->pb.valid) SWPS_TRY(prep_batch(w));  // inline on s (first batch of the call)
     const swps_w2v::Prepped cur = w->pb;

@@ -429,7 +429,8 @@ def test_fast_kernel_variants_bit_identical(lib, gpu, monkeypatch, combine):
 @pytest.mark.parametrize("dtype,fp64i", [("f32", False), ("f32", True), ("f64", True), ("f32", "bfp40")])
 def test_overlapped_driver_bit_identical(lib, gpu, monkeypatch, dtype, fp64i):
     """prep(i+1) on a second stream into a second buffer set while learn(i)
-    runs (SWPS_OVERLAP=1, opt-in) == the sequential loop, bit for bit,
+    runs (SWPS_OVERLAP=1; =2: issued after learn(i), beside its gather and push) == the
+    sequential loop, bit for bit,
     across epoch boundaries and uneven train_batches chunks; RNG states and
     counters equal too."""
     rng = np.random.default_rng(5)
@@ -440,7 +441,7 @@ def test_overlapped_driver_bit_identical(lib, gpu, monkeypatch, dtype, fp64i):
     off = np.arange(0, lines * L + 1, L, dtype=np.uint64)
     keys = np.array([lib.bkdr("w%d" % i) for i in range(V)], dtype=np.uint64)
     res = []
-    for ov in ("0", "1"):
+    for ov in ("0", "1", "2"):  # 2: prep(i+1) issued after learn(i), waiting for its forward
         monkeypatch.setenv("SWPS_OVERLAP", ov)
         t = lib.Table("w2v", dim=64 if dtype == "f64" else 300, capacity=V, dtype=dtype, learning_rate=0.7)
         w = lib.Word2Vec(t, window=5, negative=5, minibatch=20, sample=1e-3, unigram_size=10 ** 6,
@@ -454,8 +455,9 @@ def test_overlapped_driver_bit_identical(lib, gpu, monkeypatch, dtype, fp64i):
         st = w.stats()
         res.append((w.get_params(), {k: st[k] for k in ("batches", "kept", "words", "lstate", "fstate",
                                                         "pulled", "pushed")}))
-    assert res[0][1] == res[1][1]
-    assert np.array_equal(res[0][0], res[1][0])
+    for r in res[1:]:
+        assert res[0][1] == r[1]
+        assert np.array_equal(res[0][0], r[0])
 
 
 def test_specialised_records_kernel_bit_identical(lib, gpu, tmp_path, monkeypatch):
