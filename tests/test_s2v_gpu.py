@@ -248,3 +248,39 @@ def test_s2v_config5_shape(lib, oracle_mod, gpu, tmp_path):
                           rows[:, :2 * D])  # the word rows the slice trained on are the 1M table's
     rel = np.abs(vg - vo) / np.maximum(np.abs(vo), 1e-3)
     assert rel.max() < 1e-5, rel.max()
+
+
+def test_s2v_config5_full_rank_share(lib, gpu):
+    """BASELINE config 5 at its full per-GPU share (1e7 docs / 8 GPUs = 1.25M docs of 50-200
+    Zipf(1M) tokens, 156M words, minibatches of 8192 against a 1M x 300 hash-initialised word
+    table): loaded and trained twice, the sentence vectors are bit-identical run to run and
+    finite, every document and position is counted, and the load (the per-minibatch vocabularies
+    on worker threads) finishes in seconds."""
+    import time
+    import torch
+    from swiftmpi_amd.synth import zipf_tokens
+    V, nd, D = 1_000_000, 1_250_000, 300
+    rng = np.random.default_rng(7)
+    lens = rng.integers(50, 201, nd)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    ids, _ = zipf_tokens(int(off[-1]), V, 100, seed=7)
+    toks = ids.astype(np.uint64) + 1
+    del ids
+    sent = (np.arange(nd, dtype=np.uint64) + np.uint64(1)) * np.uint64(2654435761)
+    t = lib.Table("w2v", dim=D, capacity=V + 1024, dtype="f32", init="hash", seed=3)
+    t.pull(torch.arange(1, V + 1, dtype=torch.int64, device="cuda"))
+    outs, loads = [], []
+    for _ in range(2):
+        s = lib.Sent2Vec(t, window=5, negative=5, minibatch=8192, niters=1)
+        t0 = time.perf_counter()
+        s.load_tokens(toks, off, sent)
+        loads.append(time.perf_counter() - t0)
+        s.train()
+        outs.append((s.docs()[1], s.stats()))
+        del s
+    print("load s", loads)
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.isfinite(outs[0][0]).all()
+    st = outs[0][1]
+    assert st["docs"] == nd and st["positions"] == int(off[-1])
+    assert min(loads) < 30.0
