@@ -12,9 +12,10 @@ run() {  # tag plan [VAR=value ...]
   grep '^{' gpurun_out/lrplan_bench_$tag.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', '%.4g' % d['value'], '%.4f' % d['ms_per_step'], {k: round(v, 3) for k, v in d['kernel_ms'].items()}, d['config']['setup_s'], d['config']['end_to_end']['value'])"
 }
 run none none SWPS_X=1
-run nt512 none SWPS_LR_FX_NT=512
-run none2 none SWPS_X=2
-run nt512b none SWPS_LR_FX_NT=512
+run place1 none SWPS_LR_PLACE=1
+run place2 none SWPS_LR_PLACE=2
+run none_b none SWPS_X=2
+run place1b none SWPS_LR_PLACE=1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lrplan_prof -o run -- python3 bench.py --app lr --lr-plan none --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/lrplan_prof.log 2>&1 || exit 1
 f=$(find gpurun_out/lrplan_prof -name "*kernel_stats.csv" | head -1)
 cp "$f" gpurun_out/lrplan_kernel_stats.csv

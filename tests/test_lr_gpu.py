@@ -632,3 +632,30 @@ def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
         a = np.asarray(a, dtype=np.float64)
         b = np.asarray(b, dtype=np.float64)
         assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max(), (np.abs(a - b).max(), np.abs(a).max())
+
+
+def test_lr_config3_full_rank_share(lib, gpu):
+    """BASELINE config 3 at its full per-GPU share (45,840,617 Criteo-shaped rows / 8 GPUs =
+    5.73M rows, 223M records, minibatches of 65,536 over a 2^24 hashed feature space): the
+    fixed-point step (plan none) trains one epoch twice, bit-identical run to run, finite, every
+    batch's examples counted."""
+    from swiftmpi_amd.synth import criteo
+    rows = 45_840_617 // 8
+    y, off, f, v = criteo(rows, seed=3)
+    outs = []
+    for _ in range(2):
+        t = lib.Table("lr", capacity=1 << 24, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+        m = lib.LR(t, minibatch=65536, init_ref=False, fast_sums=True, plan="none")
+        m.load_csr(y, off, f, v)
+        m.init()
+        err = m.train(1)
+        k, w, g2 = m.params()
+        assert m.fx_bytes(0)["form"] == 1  # the bucketed fixed-point step ran
+        assert m.info()["rows"] == rows and m.info()["batches"] == (rows + 65536) // 65537
+        outs.append((err, w, g2, len(k)))
+        m.close()
+        t.close()
+    assert outs[0][3] == outs[1][3] > 1_000_000
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        assert np.array_equal(a, b)
+    assert np.isfinite(outs[0][1]).all() and np.isfinite(outs[0][0]).all()
