@@ -216,6 +216,25 @@ int swps_comm_transport(swps_comm *c, int32_t *kind, int32_t *ranks);
 int swps_comm_set_timeout(swps_comm *c, double seconds);
 int swps_comm_check(swps_comm *c);
 int swps_comm_abort(swps_comm *c, const char *why);
+/* Device-initiated all-to-all-v over IPC-mapped peer memory (opt-in, collective; the ranks of one
+ * node, world <= 8; replaces the payload path of every later exchange on this communicator — the
+ * reference's ZeroMQ request / response payloads, transfer.h:86-241, as the pull / push traffic of
+ * global_pull_access.h:28-107 and server.h:156-176).  Each rank allocates an inbox of
+ * world x 2 x slot_bytes (0: SWPS_COMM_IPC_SLOT_MB, default 4 MiB) and control words in uncached
+ * device memory and maps every peer's through hipIpcGetMemHandle / hipIpcOpenMemHandle; one
+ * exchange is then one kernel on the caller's stream, with no host synchronisation and no RCCL or
+ * host-transport call (headers and counts still use the communicator's transport).  Segments
+ * larger than a slot stream through it in rounds.  Waits are bounded by the communicator's
+ * deadline (swps_comm_set_timeout): a lost peer makes the next call fail with SWPS_E_RCCL. */
+int swps_comm_enable_ipc(swps_comm *c, uint64_t slot_bytes);
+/* out4 = {enabled, slot bytes, exchanges issued, bytes sent to other ranks} */
+int swps_comm_ipc_info(swps_comm *c, uint64_t *out4);
+/* Collective all-to-all-v of device buffers on `stream` (a hipStream_t; NULL: the null stream):
+ * send holds the segments for ranks 0..world-1 back to back (send_bytes[r] each), recv receives
+ * rank r's segment at the sum of recv_bytes[0..r-1].  Over RCCL and IPC it is stream-ordered and
+ * returns at once; over a host transport it returns once the exchange is done. */
+int swps_comm_alltoallv(swps_comm *c, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                        const uint64_t *recv_bytes, void *stream);
 
 /* ---- key-sharded table (the GPU-to-shard map, src/cluster) --------------
  * swps_table_route binds a local shard to a communicator: this table then

@@ -93,6 +93,9 @@ PROTOS = {
     "swps_comm_set_timeout": (ctypes.c_int, [_p, ctypes.c_double]),
     "swps_comm_check": (ctypes.c_int, [_p]),
     "swps_comm_abort": (ctypes.c_int, [_p, ctypes.c_char_p]),
+    "swps_comm_enable_ipc": (ctypes.c_int, [_p, ctypes.c_uint64]),
+    "swps_comm_ipc_info": (ctypes.c_int, [_p, _p]),
+    "swps_comm_alltoallv": (ctypes.c_int, [_p, _p, _p, _p, _p, _p]),
     "swps_table_route": (ctypes.c_int, [_p, _p, _i32]),
     "swps_finish": (ctypes.c_int, [_p]),
     "swps_barrier": (ctypes.c_int, [_p]),

@@ -83,6 +83,29 @@ class Comm:
         check(capi.lib().swps_comm_transport(self.h, ctypes.byref(k), ctypes.byref(n)))
         return {1: "rccl", 2: "tcp", 3: "host"}[k.value], n.value
 
+    def enable_ipc(self, slot_bytes=0):
+        """Collective: later exchanges move device to device through IPC-mapped peer inboxes
+        (swps_comm_enable_ipc; the ranks of one node)."""
+        check(capi.lib().swps_comm_enable_ipc(self.h, int(slot_bytes)))
+        return self
+
+    def ipc_info(self):
+        """{"enabled", "slot_bytes", "exchanges", "bytes_remote"} of the IPC exchange."""
+        out = (ctypes.c_uint64 * 4)()
+        check(capi.lib().swps_comm_ipc_info(self.h, out))
+        return dict(zip(("enabled", "slot_bytes", "exchanges", "bytes_remote"), (int(v) for v in out)))
+
+    def alltoallv(self, send, send_counts, recv, recv_counts, stream=None):
+        """Collective all-to-all-v of two device tensors (counts in elements, per rank) on
+        `stream` (torch's current stream by default)."""
+        import torch
+        es = send.element_size()
+        sb = (ctypes.c_uint64 * self.world)(*(int(n) * es for n in send_counts))
+        rb = (ctypes.c_uint64 * self.world)(*(int(n) * es for n in recv_counts))
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        check(capi.lib().swps_comm_alltoallv(self.h, ctypes.c_void_p(send.data_ptr()), sb,
+                                             ctypes.c_void_p(recv.data_ptr()), rb, ctypes.c_void_p(s)))
+
     def set_timeout(self, seconds):
         """Deadline for the communicator's initialisation and each exchange (RCCL guard)."""
         check(capi.lib().swps_comm_set_timeout(self.h, float(seconds)))

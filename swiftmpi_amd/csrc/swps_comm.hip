@@ -66,6 +66,38 @@ struct CommGuard {
   std::string msg;  // set once, before `aborted`
 };
 
+// Device-initiated all-to-all-v (swps_comm_enable_ipc, opt-in; the ranks of one node).  Every rank
+// owns an inbox (world sources x 2 parities x slot bytes) and a block of control words, both in
+// uncached device memory, and maps every peer's pair through hipIpcOpenMemHandle.  One exchange is
+// one kernel on the caller's stream (k_ipc_a2a): per (peer, channel) a send workgroup copies its
+// part of the segment into the peer's inbox and bumps the peer's ready word; a receive workgroup
+// waits for its ready word, copies the inbox out to the receive buffer and bumps the sender's ack
+// word, which frees that parity for the sender's round after next.  Ready / ack words are
+// monotonic round counts kept in step on both sides by the host (each side knows every segment's
+// length: the collective's counts), so nothing is reset between exchanges and no handshake runs
+// on the host.  Spins are bounded by the communicator's deadline: a rank whose peer never comes
+// sets a local dead word (the rest of its workgroups stop) and a host-mapped error word, and the
+// next call on the communicator fails with SWPS_E_RCCL.  Headers and counts still go through the
+// communicator's own transport.
+constexpr int kIpcMaxWorld = 8;   // one node
+constexpr int kIpcCh = 8;         // channels (workgroups) per peer and direction
+constexpr uint64_t kIpcMinPart = 4096;  // a segment is split over channels in parts of >= 4 KiB
+constexpr int kIpcAck = kIpcMaxWorld * kIpcCh;  // control words: ready[src][ch], ack[dst][ch], dead
+constexpr int kIpcDead = 2 * kIpcMaxWorld * kIpcCh;
+constexpr uint64_t kIpcCtrlBytes = 4096;
+
+struct IpcState {
+  uint64_t slot = 0, sub = 0;  // per (source, parity) inbox slot; per channel sub-slot
+  void *inbox = nullptr, *ctrl = nullptr;  // this rank's (uncached device memory)
+  std::vector<void *> peer_inbox, peer_ctrl;  // every rank's, as mapped here (own: local)
+  uint64_t *err_host = nullptr, *err_dev = nullptr;  // host-mapped error word
+  std::vector<uint64_t> sc, rc;  // rounds sent to / received from [peer][channel] so far
+  hipEvent_t last = nullptr;  // the previous exchange's kernel: exchanges run in issue order
+  bool issued = false;
+  uint64_t ticks_per_s = 0;
+  uint64_t calls = 0, bytes_remote = 0;
+};
+
 struct swps_comm {
   int32_t rank = 0, world = 1, device = 0;
   bool rccl = false;
@@ -75,6 +107,8 @@ struct swps_comm {
   DevMem d_hdr;  // RCCL header all-gather buffers
   double timeout_s = 120.0;  // RCCL deadline per exchange (CommGuard)
   std::unique_ptr<CommGuard> guard;  // RCCL, world > 1
+  std::unique_ptr<IpcState> ipc;  // swps_comm_enable_ipc
+  HostStage stage;  // swps_comm_alltoallv over a host transport
 };
 
 namespace {
@@ -108,8 +142,21 @@ void comm_abort(swps_comm *c, const std::string &why) {
   (void)ncclCommAbort(c->nc);  // frees the communicator: never destroyed again
 }
 
+// the IPC exchange's error word: 0, or 1 << 63 | receive << 8 | peer of the first wait that timed out
+std::string ipc_error(const swps_comm *c) {
+  const IpcState *p = c->ipc.get();
+  if (!p || !p->err_host) return "";
+  const uint64_t e = __atomic_load_n(p->err_host, __ATOMIC_ACQUIRE);
+  if (!e) return "";
+  return "rank " + std::to_string(c->rank) + " of " + std::to_string(c->world) + ": IPC exchange: no " +
+         ((e >> 8) & 1 ? "data from" : "acknowledgement from") + " rank " + std::to_string(e & 0xff) +
+         " within " + std::to_string((int)c->timeout_s) + " s (a peer rank lost or stuck)";
+}
+
 int comm_aborted(swps_comm *c) {
   if (c->guard && c->guard->aborted.load()) return fail(SWPS_E_RCCL, c->guard->msg);
+  const std::string e = ipc_error(c);
+  if (!e.empty()) return fail(SWPS_E_RCCL, e);
   return SWPS_OK;
 }
 
@@ -526,6 +573,177 @@ int scatter_rows(const void *src, const uint32_t *pos, uint64_t n, uint64_t row_
   return SWPS_OK;
 }
 
+// ---- the IPC exchange (IpcState) ----
+struct IpcArgs {
+  char *inbox[kIpcMaxWorld];
+  uint64_t *ctrl[kIpcMaxWorld];
+  const char *send;
+  char *recv;
+  uint64_t sb[kIpcMaxWorld], so[kIpcMaxWorld], rb[kIpcMaxWorld], ro[kIpcMaxWorld];
+  uint64_t sc[kIpcMaxWorld][kIpcCh], rc[kIpcMaxWorld][kIpcCh];  // rounds before this exchange
+  uint64_t slot, sub, deadline;  // deadline in wall-clock ticks
+  uint64_t *err;
+  int32_t rank, world;
+};
+
+// channel ch's part of an L-byte segment: parts of ceil(L / kIpcCh) bytes rounded up to 16, at
+// least kIpcMinPart (a small segment uses the first channels only); the same on both sides
+__host__ __device__ inline void ipc_span(uint64_t L, int ch, uint64_t *off, uint64_t *len) {
+  uint64_t part = ((L + kIpcCh - 1) / kIpcCh + 15) & ~15ull;
+  if (part < kIpcMinPart) part = kIpcMinPart;
+  const uint64_t o = part * (uint64_t)ch;
+  *off = o < L ? o : L;
+  *len = o < L ? (L - o < part ? L - o : part) : 0;
+}
+
+// block-wide copy (256 threads): 16-B words when both ends and the length allow it
+__device__ inline void ipc_copy(char *dst, const char *src, uint64_t n) {
+  const uint64_t t = threadIdx.x;
+  const uint64_t al = (uint64_t)(uintptr_t)dst | (uint64_t)(uintptr_t)src | n;
+  if ((al & 15) == 0) {
+    const uint4 *s = (const uint4 *)src;
+    uint4 *d = (uint4 *)dst;
+    const uint64_t m = n >> 4;
+    uint64_t i = t;
+    for (; i + 768 < m; i += 1024) {  // four loads in flight per lane
+      const uint4 a = s[i], b = s[i + 256], c = s[i + 512], e = s[i + 768];
+      d[i] = a;
+      d[i + 256] = b;
+      d[i + 512] = c;
+      d[i + 768] = e;
+    }
+    for (; i < m; i += 256) d[i] = s[i];
+  } else if ((al & 3) == 0) {
+    const uint32_t *s = (const uint32_t *)src;
+    uint32_t *d = (uint32_t *)dst;
+    for (uint64_t i = t; i < (n >> 2); i += 256) d[i] = s[i];
+  } else {
+    for (uint64_t i = t; i < n; i += 256) dst[i] = src[i];
+  }
+}
+
+// lane 0 polls w (relaxed, system scope) until it reaches v; false (and the error words set) once
+// the deadline passes or another workgroup of this rank gave up; uniform over the block
+__device__ bool ipc_wait(uint64_t *w, uint64_t v, const IpcArgs &a, uint64_t code) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    int r = 1;
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+      uint64_t *dead = a.ctrl[a.rank] + kIpcDead;
+      const uint64_t t0 = wall_clock64();
+      for (unsigned it = 1;; it++) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= v) break;
+        if ((it & 63) == 0 && (__hip_atomic_load(dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                               wall_clock64() - t0 > a.deadline)) {
+          __hip_atomic_store(dead, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          r = 0;
+          break;
+        }
+      }
+    }
+    ok = r;
+  }
+  __syncthreads();
+  return ok != 0;
+}
+
+// grid: world x kIpcCh send workgroups, then as many receive workgroups
+__global__ __launch_bounds__(256) void k_ipc_a2a(IpcArgs a) {
+  const int ch = blockIdx.x % kIpcCh;
+  const int peer = (blockIdx.x / kIpcCh) % a.world;
+  const bool rx = blockIdx.x >= (unsigned)(a.world * kIpcCh);
+  const int me = a.rank;
+  uint64_t off, len;
+  if (!rx) {
+    ipc_span(a.sb[peer], ch, &off, &len);
+    if (!len) return;
+    const char *src = a.send + a.so[peer] + off;
+    if (peer == me) {  // the own segment: straight into the receive buffer
+      ipc_copy(a.recv + a.ro[me] + off, src, len);
+      return;
+    }
+    uint64_t *ready = a.ctrl[peer] + me * kIpcCh + ch;          // the peer's word for (me, ch)
+    uint64_t *ack = a.ctrl[me] + kIpcAck + peer * kIpcCh + ch;  // mine, bumped by the peer
+    char *box = a.inbox[peer] + (uint64_t)me * 2 * a.slot + (uint64_t)ch * a.sub;
+    const uint64_t code = (1ull << 63) | (uint64_t)peer;
+    uint64_t g = a.sc[peer][ch];
+    for (uint64_t d = 0; d < len; d += a.sub, g++) {
+      if (g >= 2 && !ipc_wait(ack, g - 1, a, code)) return;  // round g-2 (same parity) consumed
+      ipc_copy(box + (g & 1) * a.slot, src + d, len - d < a.sub ? len - d : a.sub);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(ready, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  } else {
+    ipc_span(a.rb[peer], ch, &off, &len);
+    if (!len || peer == me) return;
+    uint64_t *ready = a.ctrl[me] + peer * kIpcCh + ch;
+    uint64_t *ack = a.ctrl[peer] + kIpcAck + me * kIpcCh + ch;
+    const char *box = a.inbox[me] + (uint64_t)peer * 2 * a.slot + (uint64_t)ch * a.sub;
+    char *dst = a.recv + a.ro[peer] + off;
+    const uint64_t code = (1ull << 63) | (1ull << 8) | (uint64_t)peer;
+    uint64_t g = a.rc[peer][ch];
+    for (uint64_t d = 0; d < len; d += a.sub, g++) {
+      if (!ipc_wait(ready, g + 1, a, code)) return;
+      if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      ipc_copy(dst + d, box + (g & 1) * a.slot, len - d < a.sub ? len - d : a.sub);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the inbox reads are done before the ack
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(ack, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+int ipc_alltoallv(swps_comm *c, const void *d_send, const uint64_t *sb, const uint64_t *so, void *d_recv,
+                  const uint64_t *rb, const uint64_t *ro, hipStream_t s) {
+  IpcState &p = *c->ipc;
+  SWPS_TRY(comm_aborted(c));
+  IpcArgs a{};
+  const int W = c->world;
+  for (int r = 0; r < W; r++) {
+    a.inbox[r] = (char *)p.peer_inbox[r];
+    a.ctrl[r] = (uint64_t *)p.peer_ctrl[r];
+    a.sb[r] = sb[r];
+    a.so[r] = so[r];
+    a.rb[r] = rb[r];
+    a.ro[r] = ro[r];
+    for (int ch = 0; ch < kIpcCh; ch++) {
+      a.sc[r][ch] = p.sc[r * kIpcCh + ch];
+      a.rc[r][ch] = p.rc[r * kIpcCh + ch];
+      uint64_t off, len;
+      ipc_span(sb[r], ch, &off, &len);
+      if (r != c->rank) p.sc[r * kIpcCh + ch] += (len + p.sub - 1) / p.sub;
+      ipc_span(rb[r], ch, &off, &len);
+      if (r != c->rank) p.rc[r * kIpcCh + ch] += (len + p.sub - 1) / p.sub;
+    }
+    if (r != c->rank) p.bytes_remote += sb[r];
+  }
+  if (sb[c->rank] != rb[c->rank]) return fail(SWPS_E_STATE, "IPC exchange: own segment sizes differ");
+  a.send = (const char *)d_send;
+  a.recv = (char *)d_recv;
+  a.slot = p.slot;
+  a.sub = p.sub;
+  a.deadline = (uint64_t)(c->timeout_s * (double)p.ticks_per_s);
+  a.err = p.err_dev;
+  a.rank = c->rank;
+  a.world = W;
+  if (p.issued) SWPS_HIP(hipStreamWaitEvent(s, p.last, 0));
+  k_ipc_a2a<<<2 * W * kIpcCh, 256, 0, s>>>(a);
+  SWPS_HIP(hipGetLastError());
+  SWPS_HIP(hipEventRecord(p.last, s));
+  p.issued = true;
+  p.calls++;
+  return SWPS_OK;
+}
+
 // all-to-all-v of device buffers (byte counts per peer, blocks in rank
 // order), ordered on stream s: RCCL send/recv groups, or host staging
 // through `st` and the transport's callback (synchronous)
@@ -539,6 +757,14 @@ int comm_alltoallv(swps_comm *c, const void *d_send, const std::vector<uint64_t>
   if (c->world == 1) {
     if (st) SWPS_HIP(hipMemcpyAsync(d_recv, d_send, st, hipMemcpyDeviceToDevice, s));
     return SWPS_OK;
+  }
+  if (c->ipc) {
+    std::vector<uint64_t> so(c->world), ro(c->world);
+    for (int r = 1; r < c->world; r++) {
+      so[r] = so[r - 1] + sb[r - 1];
+      ro[r] = ro[r - 1] + rb[r - 1];
+    }
+    return ipc_alltoallv(c, d_send, sb.data(), so.data(), d_recv, rb.data(), ro.data(), s);
   }
   if (c->rccl) {
     SWPS_TRY(comm_aborted(c));
@@ -580,6 +806,7 @@ int comm_alltoallv_disp(swps_comm *c, const void *d_send, const std::vector<uint
                                        hipMemcpyDeviceToDevice, s));
     return SWPS_OK;
   }
+  if (c->ipc) return ipc_alltoallv(c, d_send, sb.data(), so.data(), d_recv, rb.data(), ro.data(), s);
   if (c->rccl) {
     SWPS_TRY(comm_aborted(c));
     SWPS_NCCL(ncclGroupStart());
@@ -827,6 +1054,26 @@ int swps_comm_create_tcp(const char *addr, int32_t port, int32_t rank, int32_t w
 int swps_comm_destroy(swps_comm *c) {
   if (!c) return SWPS_OK;
   (void)hipSetDevice(c->device);
+  if (IpcState *p = c->ipc.get(); p && c->world > 1) {
+    // peers store into this rank's inbox / ctrl words until their last exchange has retired: wait
+    // for every rank's device (an all-gather behind a device sync) unless the communicator is dead
+    const bool ok = hipDeviceSynchronize() == hipSuccess && comm_aborted(c) == SWPS_OK;
+    if (ok) {
+      std::vector<int64_t> all(c->world);
+      const int64_t one = 1;
+      (void)comm_allgather(c, &one, all.data(), 8, nullptr);
+    }
+    for (int r = 0; r < c->world; r++)
+      if (r != c->rank) {
+        if (p->peer_inbox[r]) (void)hipIpcCloseMemHandle(p->peer_inbox[r]);
+        if (p->peer_ctrl[r]) (void)hipIpcCloseMemHandle(p->peer_ctrl[r]);
+      }
+    (void)hipFree(p->inbox);
+    (void)hipFree(p->ctrl);
+    (void)hipHostFree(p->err_host);
+    if (p->last) (void)hipEventDestroy(p->last);
+    c->ipc.reset();
+  }
   if (CommGuard *g = c->guard.get()) {
     {
       std::lock_guard<std::mutex> lk(g->mu);
@@ -882,6 +1129,93 @@ int swps_comm_transport(swps_comm *c, int32_t *kind, int32_t *ranks) {
   if (c->nc) SWPS_NCCL(ncclCommCount(c->nc, &n));  // what RCCL itself reports for the communicator
   if (kind) *kind = c->rccl ? SWPS_COMM_RCCL : c->tcp ? SWPS_COMM_TCP : SWPS_COMM_HOST;
   if (ranks) *ranks = n;
+  return SWPS_OK;
+}
+
+int swps_comm_enable_ipc(swps_comm *c, uint64_t slot_bytes) {
+  if (!c) return fail(SWPS_E_CFG, "null communicator");
+  if (c->ipc) return fail(SWPS_E_STATE, "IPC exchange already enabled");
+  if (c->world > kIpcMaxWorld)
+    return fail(SWPS_E_CFG, "IPC exchange: world " + std::to_string(c->world) + " > " +
+                                std::to_string(kIpcMaxWorld) + " (one node)");
+  SWPS_TRY(comm_aborted(c));
+  if (!slot_bytes) {
+    const char *e = getenv("SWPS_COMM_IPC_SLOT_MB");
+    slot_bytes = (uint64_t)((e ? std::max(1.0, atof(e)) : 4.0) * (1 << 20));
+  }
+  const uint64_t q = (uint64_t)kIpcCh * 4096;  // sub-slots of whole pages
+  slot_bytes = (slot_bytes + q - 1) / q * q;
+  SWPS_HIP(hipSetDevice(c->device));
+  std::unique_ptr<IpcState> p(new IpcState());
+  p->slot = slot_bytes;
+  p->sub = slot_bytes / kIpcCh;
+  const int W = c->world;
+  p->sc.assign((size_t)W * kIpcCh, 0);
+  p->rc.assign((size_t)W * kIpcCh, 0);
+  p->peer_inbox.assign(W, nullptr);
+  p->peer_ctrl.assign(W, nullptr);
+  if (W > 1) {
+    int khz = 0;
+    SWPS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    p->ticks_per_s = (uint64_t)std::max(khz, 1) * 1000;
+    auto undo = [&](const std::string &why) {
+      for (int r = 0; r < W; r++)
+        if (r != c->rank) {
+          if (p->peer_inbox[r]) (void)hipIpcCloseMemHandle(p->peer_inbox[r]);
+          if (p->peer_ctrl[r]) (void)hipIpcCloseMemHandle(p->peer_ctrl[r]);
+        }
+      if (p->inbox) (void)hipFree(p->inbox);
+      if (p->ctrl) (void)hipFree(p->ctrl);
+      if (p->err_host) (void)hipHostFree(p->err_host);
+      (void)hipGetLastError();
+      return fail(SWPS_E_RCCL, "IPC exchange: " + why);
+    };
+    if (hipExtMallocWithFlags(&p->inbox, (size_t)W * 2 * p->slot, hipDeviceMallocUncached) != hipSuccess ||
+        hipExtMallocWithFlags(&p->ctrl, kIpcCtrlBytes, hipDeviceMallocUncached) != hipSuccess)
+      return undo("uncached allocation failed");
+    if (hipMemset(p->ctrl, 0, kIpcCtrlBytes) != hipSuccess ||
+        hipHostMalloc((void **)&p->err_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return undo("control words");
+    *p->err_host = 0;
+    if (hipHostGetDevicePointer((void **)&p->err_dev, p->err_host, 0) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      return undo("error word");
+    hipIpcMemHandle_t mine[2], all[2 * kIpcMaxWorld];
+    if (hipIpcGetMemHandle(&mine[0], p->inbox) != hipSuccess || hipIpcGetMemHandle(&mine[1], p->ctrl) != hipSuccess)
+      return undo("hipIpcGetMemHandle failed");
+    // every rank's ctrl words are zero before its handles leave it, so a peer's first store lands after
+    if (comm_allgather(c, mine, all, sizeof(mine), nullptr) != SWPS_OK) return undo("handle all-gather failed");
+    for (int r = 0; r < W; r++) {
+      if (r == c->rank) {
+        p->peer_inbox[r] = p->inbox;
+        p->peer_ctrl[r] = p->ctrl;
+        continue;
+      }
+      if (hipIpcOpenMemHandle(&p->peer_inbox[r], all[2 * r], hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+          hipIpcOpenMemHandle(&p->peer_ctrl[r], all[2 * r + 1], hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+        return undo("hipIpcOpenMemHandle of rank " + std::to_string(r) + "'s buffers failed");
+    }
+    SWPS_HIP(hipEventCreateWithFlags(&p->last, hipEventDisableTiming));
+  }
+  c->ipc = std::move(p);
+  return SWPS_OK;
+}
+
+int swps_comm_alltoallv(swps_comm *c, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                        const uint64_t *recv_bytes, void *stream) {
+  if (!c || !send_bytes || !recv_bytes) return fail(SWPS_E_CFG, "null argument");
+  SWPS_HIP(hipSetDevice(c->device));
+  const std::vector<uint64_t> sb(send_bytes, send_bytes + c->world), rb(recv_bytes, recv_bytes + c->world);
+  return comm_alltoallv(c, d_send, sb, d_recv, rb, (hipStream_t)stream, c->stage, "all-to-all-v");
+}
+
+int swps_comm_ipc_info(swps_comm *c, uint64_t *out4) {
+  if (!c || !out4) return fail(SWPS_E_CFG, "null argument");
+  const IpcState *p = c->ipc.get();
+  out4[0] = p ? 1 : 0;
+  out4[1] = p ? p->slot : 0;
+  out4[2] = p ? p->calls : 0;
+  out4[3] = p ? p->bytes_remote : 0;
   return SWPS_OK;
 }
 

@@ -1,0 +1,163 @@
+"""The device-initiated IPC exchange (swps_comm_enable_ipc) against the library's TCP transport,
+two ranks on one GPU (same-device IPC):
+
+  1. swps_comm_alltoallv on seeded segments — empty, odd-sized (byte / 4-byte / 16-byte paths),
+     several times a slot (segments stream through the two parities in rounds), from two streams
+     in turn — must deliver exactly what the TCP transport delivers;
+  2. the library-driven LR and CBOW loops (swps_lr_shard_comm / swps_w2v_shard_comm) over an
+     IPC communicator must leave every rank's shard bit-identical to the same loops over TCP;
+  3. the per-exchange latency of a small exchange (the LR step's size class) over both, printed
+     as one JSON line ("IPC_LAT {...}").
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
+        --master-port 29571 tests/dist_ipc_check.py --tcp-port 29581
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from dist_native_check import corpus, lr_data  # noqa: E402
+
+
+def segments(call, world, rank, slot):
+    """Byte counts [src][dst] for one call: every pattern from empty to 2.5 slots."""
+    rng = np.random.default_rng(1000 + call)
+    sizes = [0, 1, 7, 16, 4096, 4100, 65536, slot - 16, slot + 3, int(2.5 * slot), 12, 40000]
+    m = np.array([[sizes[int(rng.integers(0, len(sizes)))] for _ in range(world)] for _ in range(world)])
+    return m
+
+
+def payload(call, src, dst, n):
+    g = np.random.default_rng((call * 7919 + src * 131 + dst) & 0xFFFFFFFF)
+    return g.integers(0, 256, n, dtype=np.uint8)
+
+
+def raw_exchange(comm, rank, world, slot, calls, streams):
+    out = []
+    for call in range(calls):
+        m = segments(call, world, rank, slot)
+        send = np.concatenate([payload(call, rank, d, int(m[rank, d])) for d in range(world)] + [np.zeros(0, np.uint8)])
+        st = streams[call % len(streams)]
+        with torch.cuda.stream(st):
+            ds = torch.as_tensor(send, device="cuda") if send.size else torch.zeros(1, dtype=torch.uint8, device="cuda")
+            dr = torch.full((max(int(m[:, rank].sum()), 1),), 0xAB, dtype=torch.uint8, device="cuda")
+            comm.alltoallv(ds, m[rank, :], dr, m[:, rank], stream=st)
+            got = dr[:int(m[:, rank].sum())].cpu().numpy()
+        want = np.concatenate([payload(call, s, rank, int(m[s, rank])) for s in range(world)] + [np.zeros(0, np.uint8)])
+        assert np.array_equal(got, want), ("raw exchange differs", call, rank, m.tolist())
+        out.append(got)
+    return out
+
+
+def latency(comm, world, nbytes, reps=200):
+    send = torch.arange(nbytes * world, dtype=torch.int64, device="cuda").to(torch.uint8)
+    recv = torch.empty_like(send)
+    cnt = [nbytes] * world
+    for _ in range(10):
+        comm.alltoallv(send, cnt, recv, cnt)
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(reps):
+        comm.alltoallv(send, cnt, recv, cnt)
+    e1.record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps * 1e6
+    return {"device_us": e0.elapsed_time(e1) / reps * 1e3, "wall_us": wall}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tcp-port", type=int, default=29581)
+    a = ap.parse_args()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    import swiftmpi_amd as sw
+    from swiftmpi_amd.comm import Comm
+    torch.cuda.set_device(0)
+    slot = 64 << 10  # small: 2.5-slot segments take several rounds per channel
+    tcp = Comm.tcp(rank, world, 0, port=a.tcp_port)
+    ipc = Comm.tcp(rank, world, 0, port=a.tcp_port + 1).enable_ipc(slot)
+    ipc.set_timeout(60)
+    info = ipc.ipc_info()
+    assert info["enabled"] == 1 and info["slot_bytes"] == slot, info
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    # 1. raw exchanges
+    rt = raw_exchange(tcp, rank, world, slot, 24, streams)
+    ri = raw_exchange(ipc, rank, world, slot, 24, streams)
+    assert all(np.array_equal(x, y) for x, y in zip(rt, ri))
+    ipc.check()
+    print("rank %d raw ok: %d exchanges" % (rank, len(ri)), flush=True)
+    # 2. the library-driven loops, TCP vs IPC
+    tmp = tempfile.mkdtemp()
+    lpath = lr_data(os.path.join(tmp, "l%d.txt" % rank), rank)
+    res = {}
+    for name, comm in (("tcp", tcp), ("ipc", ipc)):
+        t = sw.Table("lr", capacity=8192, dtype="f32", learning_rate=0.05, init="hash", seed=5, device=0)
+        m = sw.LR(t, minibatch=50, init_ref=False)
+        m.load_text(lpath)
+        m.shard_comm(comm, frag_num=2000)
+        m.init()
+        err = m.train(3)
+        pred = m.predict()
+        k = np.sort(t.keys())
+        res[name] = (err, pred[0], k, t.export(torch.as_tensor(k.astype(np.int64), device="cuda")).cpu())
+        m.close()
+        t.close()
+    a_, b_ = res["tcp"], res["ipc"]
+    assert np.array_equal(a_[0], b_[0]) and np.array_equal(a_[1], b_[1]) and np.array_equal(a_[2], b_[2])
+    assert torch.equal(a_[3], b_[3])
+    print("rank %d lr ok: %d keys" % (rank, len(a_[2])), flush=True)
+    path = corpus(os.path.join(tmp, "c%d.txt" % rank), rank)
+    kw = dict(window=4, negative=4, minibatch=19, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=False)
+    res = {}
+    for name, comm in (("tcp", tcp), ("ipc", ipc)):
+        t = sw.Table("w2v", dim=300, capacity=4096, dtype="f32", learning_rate=0.7, init="hash", seed=3, device=0)
+        w = sw.Word2Vec(t, init="table", **kw)
+        w.load_text(path)
+        w.shard_comm(comm, frag_num=1000)
+        w.init()
+        w.train_batches(2 * 9 + 1)
+        w.sync()
+        k = np.sort(t.keys())
+        res[name] = (k, t.export(torch.as_tensor(k.astype(np.int64), device="cuda")).cpu(), w.stats())
+        w.close()
+        t.close()
+    a_, b_ = res["tcp"], res["ipc"]
+    assert np.array_equal(a_[0], b_[0]) and torch.equal(a_[1], b_[1])
+    assert a_[2]["lstate"] == b_[2]["lstate"], (a_[2], b_[2])
+    print("rank %d w2v ok: %d keys" % (rank, len(a_[0])), flush=True)
+    # 3. latency of one exchange (8 KiB / 64 KiB per peer)
+    lat = {}
+    for nb in (8 << 10, 64 << 10):
+        lat["tcp_%dKiB" % (nb >> 10)] = latency(tcp, world, nb, reps=100)
+        lat["ipc_%dKiB" % (nb >> 10)] = latency(ipc, world, nb, reps=400)
+    ipc.check()
+    info = ipc.ipc_info()
+    if rank == 0:
+        print("IPC_LAT " + json.dumps({"world": world, "same_gpu": True, "slot_bytes": slot, "latency": lat,
+                                       "ipc_exchanges": info["exchanges"], "ipc_bytes_remote": info["bytes_remote"]}),
+              flush=True)
+    ipc.close()
+    tcp.close()
+    dist.barrier()
+    if rank == 0:
+        print("IPC OK")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

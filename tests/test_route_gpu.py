@@ -149,6 +149,21 @@ def test_native_sharded_driver_equals_python_driver(lib, gpu):
     assert r.returncode == 0 and "NATIVE OK" in r.stdout
 
 
+def test_ipc_exchange_equals_tcp(lib, gpu):
+    """The device-initiated IPC exchange (swps_comm_enable_ipc) == the TCP transport, bit for bit:
+    raw all-to-all-v calls (empty / odd / multi-slot segments, two streams) and the library-driven
+    LR and CBOW loops, two ranks on one GPU (tests/dist_ipc_check.py); prints the per-exchange
+    latency of both."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist_ipc_check.py"), "--tcp-port", str(_port())]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    print(r.stdout[-6000:])
+    print("\n".join(ln for ln in r.stderr.splitlines() if "rank0" in ln or "Error" in ln)[-6000:])
+    assert r.returncode == 0 and "IPC OK" in r.stdout
+
+
 @pytest.mark.parametrize("split", ["0", "1"])
 def test_native_sharded_driver_rccl_world1(lib, gpu, tmp_path, monkeypatch, split):
     """The library-driven loop over RCCL at world 1 == the unsharded context
