@@ -310,7 +310,8 @@ class Ctx:
         ngpu = torch.cuda.device_count()
         self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(ngpu, 1)
         torch.cuda.set_device(self.local)
-        self.dist, self.backend, self._comm = None, None, []
+        self.dist, self.backend, self._comm, self._ipc = None, None, [], None
+        self.exchange = os.environ.get("SWPS_BENCH_EXCHANGE", "auto")  # main() sets --exchange
         self.sharded = self.world > 1 or sharded
         if self.sharded:
             import datetime
@@ -359,6 +360,47 @@ class Ctx:
         c = self._comm[0] if self._comm else None
         return c.transport() if c is not None else None
 
+    def close(self):
+        """Every rank at the same point: the IPC communicator's teardown is collective (peers store
+        into this rank's inboxes until their last exchange retires)."""
+        if self._ipc and self._ipc[0] is not None:
+            self._ipc[0].close()
+        self._ipc = [None]
+
+    def ipc_comm(self):
+        """A second library communicator whose exchanges run device to device through IPC-mapped
+        peer inboxes (swps_comm_enable_ipc), for the latency-bound LR leg.  A canary exchange
+        (segments of 1 KiB to 2.5 inbox slots, every byte checked on the device) must come out
+        exact on every rank, within a 30-s deadline; otherwise every rank falls back to comm()
+        together.  None at world 1 or when --exchange base."""
+        if self._ipc is None:
+            self._ipc = [None]
+            if self.dist is not None and 1 < self.world <= 8 and self.exchange != "base":
+                import torch
+                from swiftmpi_amd.comm import Comm
+                port = int(os.environ.get("MASTER_PORT", "29533")) + 3
+                addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+                set_phase("ipc communicator")
+                c, ok = None, 0
+                try:
+                    c = (Comm.rccl(self.rank, self.world, self.local, addr=addr, port=port)
+                         if self.backend == "nccl" else Comm.tcp(self.rank, self.world, self.local, addr=addr, port=port))
+                    c.set_timeout(min(30.0, comm_timeout_s()))
+                    c.enable_ipc()
+                    ok = int(ipc_canary(c, self.rank, self.world))
+                    c.set_timeout(comm_timeout_s())
+                except Exception as e:  # noqa: BLE001 — reported; every rank falls back together
+                    print("IPC exchange unavailable on rank %d: %s" % (self.rank, e), file=sys.stderr, flush=True)
+                    ok = 0
+                t = torch.tensor([ok], dtype=torch.int32, device="cuda")
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+                if int(t.item()):
+                    self._ipc = [c]
+                else:
+                    print("rank %d: IPC canary failed somewhere; LR exchanges stay on the base transport"
+                          % self.rank, file=sys.stderr, flush=True)
+        return self._ipc[0]
+
     def max_sum(self, dt, units):
         """(max over ranks of dt, sum over ranks of units)."""
         if self.dist is None:
@@ -369,6 +411,26 @@ class Ctx:
         self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
         self.dist.all_reduce(tt, op=self.dist.ReduceOp.SUM)
         return float(mx[0]), float(tt[1])
+
+
+def ipc_canary(c, rank, world):
+    """One exchange through the IPC path with every segment size class (1 KiB .. 2.5 slots: the
+    multi-round path) and a per-(src, dst) byte pattern, checked on the device."""
+    import torch
+    slot = c.ipc_info()["slot_bytes"]
+    sizes = [1024, 5 * slot // 2 + 7, 4099, slot, 64 << 10, 3 * slot // 2, 17, 1 << 20]
+
+    def seg(src, dst):
+        n = sizes[(src * 3 + dst) % len(sizes)]
+        return (torch.arange(n, dtype=torch.int64, device="cuda") * (2 * src + 3) + 7 * dst).to(torch.uint8)
+    send = torch.cat([seg(rank, d) for d in range(world)])
+    want = torch.cat([seg(s_, rank) for s_ in range(world)])
+    recv = torch.zeros_like(want)
+    c.alltoallv(send, [sizes[(rank * 3 + d) % len(sizes)] for d in range(world)], recv,
+                [sizes[(s_ * 3 + rank) % len(sizes)] for s_ in range(world)])
+    torch.cuda.synchronize()
+    c.check()
+    return bool(torch.equal(recv, want))
 
 
 def exchange_block(xs, steps, step_s, world, note):
@@ -621,6 +683,9 @@ def main():
     ap.add_argument("--driver", default="native", choices=["python", "native"],
                     help="sharded exchange: swiftmpi_amd/dist.py over torch.distributed, or the library's own "
                          "(swps_w2v_shard_comm over RCCL / its TCP transport)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "base"],
+                    help="N > 1 LR leg: auto = the device-initiated IPC exchange (swps_comm_enable_ipc) when its "
+                         "canary passes on every rank, else the base transport; base = RCCL / TCP only")
     ap.add_argument("--pipeline", action="store_true",
                     help="sharded path: the bounded-staleness driver (pull(i+1)/push(i) overlap learn(i)) instead "
                          "of the default lockstep pull/learn/push order (exact reference semantics)")
@@ -662,6 +727,7 @@ def main():
                     help="skip the config-4, LR (config 3) and sent2vec (config 5) legs of the default line")
     ap.add_argument("--app-steps", type=int, default=20, help="timed LR minibatches of the default line's lr leg")
     args = ap.parse_args()
+    os.environ["SWPS_BENCH_EXCHANGE"] = args.exchange  # read by Ctx (the LR leg's IPC communicator)
     if args.parity:
         args.precision = "parity"
     arm_deadline(int(os.environ.get("RANK", "0")))
@@ -789,6 +855,7 @@ def main():
     set_phase("report")
     if rank == 0:
         print(json.dumps(out), flush=True)
+    ctx.close()
     if ctx.dist is not None:
         ctx.dist.destroy_process_group()
 
@@ -803,6 +870,7 @@ def bench_other(args):
     out = bench_lr(args, ctx) if args.app == "lr" else bench_s2v(args, ctx)
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
+    ctx.close()
     if ctx.dist is not None:
         ctx.dist.destroy_process_group()
 
@@ -822,6 +890,9 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
     lr_rate = args.lr if args.lr != 0.7 else 0.05
     t = sw.Table("lr", capacity=1 << 23, dtype="f32", learning_rate=lr_rate, init="hash", seed=1, device=local)
     comm = ctx.comm() if dist is not None and args.driver == "native" else None  # the library issues the exchange
+    ipc = ctx.ipc_comm() if comm is not None else None
+    if ipc is not None:  # the latency-bound exchange: device to device through IPC-mapped inboxes
+        comm = ipc
     # end to end: load (the CSR rows to the GPU, the per-batch key-sorted index, the first full
     # pull) and the first epoch over the nb minibatches, to its last push (lr.cpp:157-238 rebuilds
     # that index per minibatch; here it is built once at load)
@@ -945,7 +1016,8 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
                                   "2^24 hashed feature space, %d rows per GPU per minibatch, AdaGrad lr %g, "
                                   "%d minibatches of data" % (B1, lr_rate, nb),
                       "parallelism": ("key-sharded PS over %d GPU(s) (BasicHashFrag frag_num 2000), %s all-to-all-v%s"
-                                      % (world, ctx.backend, ", library-issued" if comm is not None else ""))
+                                      % (world, "device-initiated IPC" if ipc is not None else ctx.backend,
+                                         ", library-issued" if comm is not None else ""))
                       if dist is not None else "1 GPU, one HBM shard",
                       "mode": "exact (sequential fp32 per-key sums, bit-exact with the reference)" if args.lr_exact
                       else ("fixed point (each key's sum of e*x_i as an exact 64-bit integer at scale 2^s "
@@ -971,6 +1043,9 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
                                                              "exchange stream, profiled pass)")}
     if comm is not None:
         with_transport(out, ctx)
+        if ipc is not None:
+            out["transport"] += "+ipc"
+            out["ipc"] = ipc.ipc_info()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_lr(y, off, f, v, args.lr_batch, lr_rate,
                                               cpu_rows if cpu_rows is not None else args.cpu_rows)
