@@ -142,12 +142,16 @@ void comm_abort(swps_comm *c, const std::string &why) {
   (void)ncclCommAbort(c->nc);  // frees the communicator: never destroyed again
 }
 
-// the IPC exchange's error word: 0, or 1 << 63 | receive << 8 | peer of the first wait that timed out
+// the IPC exchange's error word: 0, or 1 << 63 | receive << 8 | peer of a wait that timed out, or
+// 1 << 63 | 1 << 9: an exchange found the dead word set
 std::string ipc_error(const swps_comm *c) {
   const IpcState *p = c->ipc.get();
   if (!p || !p->err_host) return "";
   const uint64_t e = __atomic_load_n(p->err_host, __ATOMIC_ACQUIRE);
   if (!e) return "";
+  if ((e >> 9) & 1)
+    return "rank " + std::to_string(c->rank) + " of " + std::to_string(c->world) +
+           ": IPC exchange: a rank gave up on an earlier exchange (a peer rank lost or stuck)";
   return "rank " + std::to_string(c->rank) + " of " + std::to_string(c->world) + ": IPC exchange: no " +
          ((e >> 8) & 1 ? "data from" : "acknowledgement from") + " rank " + std::to_string(e & 0xff) +
          " within " + std::to_string((int)c->timeout_s) + " s (a peer rank lost or stuck)";
@@ -623,7 +627,7 @@ __device__ inline void ipc_copy(char *dst, const char *src, uint64_t n) {
 }
 
 // lane 0 polls w (relaxed, system scope) until it reaches v; false (and the error words set) once
-// the deadline passes or another workgroup of this rank gave up; uniform over the block
+// the deadline passes or a workgroup of this rank or of a peer gave up; uniform over the block
 __device__ bool ipc_wait(uint64_t *w, uint64_t v, const IpcArgs &a, uint64_t code) {
   __shared__ int ok;
   if (threadIdx.x == 0) {
@@ -636,7 +640,10 @@ __device__ bool ipc_wait(uint64_t *w, uint64_t v, const IpcArgs &a, uint64_t cod
         if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= v) break;
         if ((it & 63) == 0 && (__hip_atomic_load(dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
                                wall_clock64() - t0 > a.deadline)) {
-          __hip_atomic_store(dead, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          // this rank's other workgroups and every peer's stop at their next check (a peer's
+          // next exchange then fails instead of waiting out its own deadline)
+          for (int r = 0; r < a.world; r++)
+            __hip_atomic_store(a.ctrl[r] + kIpcDead, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(a.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           r = 0;
           break;
@@ -650,7 +657,7 @@ __device__ bool ipc_wait(uint64_t *w, uint64_t v, const IpcArgs &a, uint64_t cod
 }
 
 // grid: world x kIpcCh send workgroups, then as many receive workgroups
-__global__ __launch_bounds__(256) void k_ipc_a2a(IpcArgs a) {
+__device__ __forceinline__ void ipc_body(const IpcArgs &a) {
   const int ch = blockIdx.x % kIpcCh;
   const int peer = (blockIdx.x / kIpcCh) % a.world;
   const bool rx = blockIdx.x >= (unsigned)(a.world * kIpcCh);
@@ -700,6 +707,17 @@ __global__ __launch_bounds__(256) void k_ipc_a2a(IpcArgs a) {
       if (threadIdx.x == 0) __hip_atomic_store(ack, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_ipc_a2a(IpcArgs a) {
+  // a rank (this one or a peer) that gave up on an earlier exchange marked every rank dead: an
+  // exchange whose waits all happen to be met (stale rounds) must still fail.  The load is in
+  // flight during the copies.
+  uint64_t d0 = 0;
+  if (threadIdx.x == 0) d0 = __hip_atomic_load(a.ctrl[a.rank] + kIpcDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  ipc_body(a);
+  if (threadIdx.x == 0 && d0)
+    __hip_atomic_store(a.err, (1ull << 63) | (1ull << 9), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 int ipc_alltoallv(swps_comm *c, const void *d_send, const uint64_t *sb, const uint64_t *so, void *d_recv,
@@ -1057,7 +1075,10 @@ int swps_comm_destroy(swps_comm *c) {
   if (IpcState *p = c->ipc.get(); p && c->world > 1) {
     // peers store into this rank's inbox / ctrl words until their last exchange has retired: wait
     // for every rank's device (an all-gather behind a device sync) unless the communicator is dead
-    const bool ok = hipDeviceSynchronize() == hipSuccess && comm_aborted(c) == SWPS_OK;
+    uint64_t dead = 1;  // set by a rank that gave up on an exchange: its peers skip the barrier
+    const bool ok = hipDeviceSynchronize() == hipSuccess && comm_aborted(c) == SWPS_OK &&
+                    hipMemcpy(&dead, (uint64_t *)p->ctrl + kIpcDead, 8, hipMemcpyDeviceToHost) == hipSuccess &&
+                    dead == 0;
     if (ok) {
       std::vector<int64_t> all(c->world);
       const int64_t one = 1;

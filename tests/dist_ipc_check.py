@@ -7,7 +7,9 @@ two ranks on one GPU (same-device IPC):
   2. the library-driven LR and CBOW loops (swps_lr_shard_comm / swps_w2v_shard_comm) over an
      IPC communicator must leave every rank's shard bit-identical to the same loops over TCP;
   3. the per-exchange latency of a small exchange (the LR step's size class) over both, printed
-     as one JSON line ("IPC_LAT {...}").
+     as one JSON line ("IPC_LAT {...}");
+  4. a lost peer: a lone exchange fails within its deadline, naming the peer, and the peer's next
+     exchange fails at once.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
         --master-port 29571 tests/dist_ipc_check.py --tcp-port 29581
@@ -151,7 +153,39 @@ def main():
         print("IPC_LAT " + json.dumps({"world": world, "same_gpu": True, "slot_bytes": slot, "latency": lat,
                                        "ipc_exchanges": info["exchanges"], "ipc_bytes_remote": info["bytes_remote"]}),
               flush=True)
-    ipc.close()
+    # 4. a lost peer: rank 0 exchanges alone (rank 1 never joins) and must fail within its 2-s
+    # deadline; its give-up marks every rank dead, so rank 1's next exchange fails at once
+    from swiftmpi_amd.capi import SwpsError
+    dist.barrier()
+    one = torch.ones(1024 * world, dtype=torch.uint8, device="cuda")
+    got = torch.empty_like(one)
+    if rank == 0:
+        ipc.set_timeout(2)
+        t0 = time.perf_counter()
+        ipc.alltoallv(one, [1024] * world, got, [1024] * world)
+        torch.cuda.synchronize()
+        waited = time.perf_counter() - t0
+        try:
+            ipc.check()
+            raise AssertionError("a lone exchange did not time out")
+        except SwpsError as e:
+            assert "IPC exchange" in str(e) and "rank 1" in str(e), str(e)
+        assert waited < 30, waited
+        print("rank 0 lost peer detected after %.1f s: ok" % waited, flush=True)
+    dist.barrier()
+    if rank == 1:
+        t0 = time.perf_counter()
+        ipc.alltoallv(one, [1024] * world, got, [1024] * world)
+        torch.cuda.synchronize()
+        try:
+            ipc.check()
+            raise AssertionError("an exchange with a dead peer did not fail")
+        except SwpsError as e:
+            assert "IPC exchange" in str(e), str(e)
+        assert time.perf_counter() - t0 < 10
+        print("rank 1 dead peer detected: ok", flush=True)
+    dist.barrier()
+    ipc.close()  # neither rank waits for the other here (both saw the dead word)
     tcp.close()
     dist.barrier()
     if rank == 0:
