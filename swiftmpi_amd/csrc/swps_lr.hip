@@ -2173,6 +2173,15 @@ struct swps_lr {
   DevMem d_K, d_vkeys, d_init_order, d_wcache, d_local, d_serve_rows;
   swps::ShardDriver *drv = nullptr;  // swps_lr_shard_comm: the library drives the exchange
   uint64_t serve_n = 0;
+  // the library driver's step slot (AppOps::set_slot): the keys an owner serves at a slot are the
+  // same every epoch, so their row lookups and the push's grouping sort are kept per slot
+  int64_t slot = -1;
+  struct SlotRows {
+    DevMem rows, sorted;
+    uint64_t n = 0;
+    bool sorted_valid = false;
+  };
+  std::vector<std::unique_ptr<SlotRows>> slot_rows;
   // the static per-batch index (lr_index) exists; the per-step plan builds none at load
   bool index_built = false;
   // per-step plan (cfg.plan == SWPS_LR_PLAN_STEP; single GPU, fast sums through row tiles): the
@@ -3853,6 +3862,18 @@ int swps_lr_serve_pull(swps_lr *l, const uint64_t *d_keys, const uint64_t *src_c
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
   uint64_t n = 0;
   for (int r = 0; r < l->world; r++) n += src_counts[r];
+  if (!insert && l->slot >= 0) {  // a driver step slot: the same keys every epoch
+    while ((uint64_t)l->slot >= l->slot_rows.size()) l->slot_rows.emplace_back(new swps_lr::SlotRows());
+    auto &e = *l->slot_rows[l->slot];
+    if (e.n != n || !e.rows.p) {
+      SWPS_TRY(e.rows.ensure(std::max<uint64_t>(n, 1) * 4));
+      SWPS_TRY(table_lookup(l->t, d_keys, n, e.rows.as<uint32_t>(), l->s));
+      e.n = n;
+      e.sorted_valid = false;
+    }
+    l->serve_n = n;
+    return table_copy_pull(l->t, e.rows.as<uint32_t>(), n, d_vals, l->s);
+  }
   SWPS_TRY(l->d_serve_rows.ensure(std::max<uint64_t>(n, 1) * 4));
   uint32_t *rows = l->d_serve_rows.as<uint32_t>();
   if (insert) {  // keys are distinct within a source, not across sources
@@ -3896,9 +3917,16 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
   uint64_t n = 0;
   for (int r = 0; r < l->world; r++) n += src_counts[r];
   if (n != l->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
-  SWPS_TRY(table_lookup(l->t, d_keys, n, l->d_serve_rows.as<uint32_t>(), l->s));
   int nsrc = 0;
   for (int r = 0; r < l->world; r++) nsrc += src_counts[r] > 0;
+  if (l->slot >= 0 && (uint64_t)l->slot < l->slot_rows.size() && l->slot_rows[l->slot]->n == n &&
+      l->slot_rows[l->slot]->rows.p) {  // this slot's pull looked the same keys up
+    auto &e = *l->slot_rows[l->slot];
+    return table_push_sources(l->t, e.rows.as<uint32_t>(), n, d_grads, l->s, false, nsrc <= 1, &e.sorted,
+                              &e.sorted_valid);
+  }
+  SWPS_TRY(l->d_serve_rows.ensure(std::max<uint64_t>(n, 1) * 4));
+  SWPS_TRY(table_lookup(l->t, d_keys, n, l->d_serve_rows.as<uint32_t>(), l->s));
   // one AdaGrad step per source, in rank order, all sources in one pass
   return table_push_sources(l->t, l->d_serve_rows.as<uint32_t>(), n, d_grads, l->s, false, nsrc <= 1);
 }
@@ -3993,6 +4021,13 @@ int swps_lr_shard_comm(swps_lr *l, swps_comm *c, int32_t frag_num) {
   o.serve_push = [](void *h, const uint64_t *k, const void *g, const uint64_t *sc) {
     return swps_lr_serve_push((swps_lr *)h, k, (const float *)g, sc);
   };
+  // per-slot row lookups and push grouping (SWPS_LR_SLOT_ROWS=0: look the rows up every call)
+  const char *sr = getenv("SWPS_LR_SLOT_ROWS");
+  if (!(sr && atoi(sr) == 0))
+    o.set_slot = [](void *h, int64_t slot) {
+      ((swps_lr *)h)->slot = slot;
+      return (int)SWPS_OK;
+    };
   const int rc = d->setup();
   if (rc) {
     delete d;

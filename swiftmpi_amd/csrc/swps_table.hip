@@ -252,6 +252,16 @@ __global__ void k_copy_rows_out(const uint32_t *__restrict__ rows_idx, uint64_t 
   for (int e = lane; e < ncopy; e += 64) out[w * ncopy + e] = r == kNoRow ? (T)0 : rows[(uint64_t)r * R + e];
 }
 
+// narrow rows (LR: one fp32 weight per key): one thread per row, ncopy <= 4 elements
+template <typename T>
+__global__ void k_copy_rows_out_t(const uint32_t *__restrict__ rows_idx, uint64_t n, const T *__restrict__ rows, int R,
+                                  int ncopy, T *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = rows_idx[i];
+  for (int e = 0; e < ncopy; e++) out[i * ncopy + e] = r == kNoRow ? (T)0 : rows[(uint64_t)r * R + e];
+}
+
 // the same with 16-B lanes (row stride and copy width multiples of 16 B)
 __global__ void k_copy_rows_out16(const uint32_t *__restrict__ rows_idx, uint64_t n, const uint4 *__restrict__ rows,
                                   int R16, int ncopy16, uint4 *__restrict__ out) {
@@ -682,7 +692,14 @@ int table_get_rows(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_va
 int table_copy_pull(swps_table *t, const uint32_t *d_rows, uint64_t n, void *d_vals, hipStream_t s) {
   if (n == 0) return SWPS_OK;
   const size_t rb = (size_t)t->row_elems * t->esize, cb = (size_t)t->pull_elems * t->esize;
-  if (rb % 16 == 0 && cb % 16 == 0)
+  if (t->pull_elems <= 4 && cb < 16) {  // a wave per row would leave 63 lanes idle
+    if (t->cfg.dtype == SWPS_F64)
+      k_copy_rows_out_t<double><<<blocks_for(n), 256, 0, s>>>(d_rows, n, t->rows.as<double>(), t->row_elems,
+                                                              t->pull_elems, (double *)d_vals);
+    else
+      k_copy_rows_out_t<float><<<blocks_for(n), 256, 0, s>>>(d_rows, n, t->rows.as<float>(), t->row_elems,
+                                                             t->pull_elems, (float *)d_vals);
+  } else if (rb % 16 == 0 && cb % 16 == 0)
     k_copy_rows_out16<<<blocks_for(n * 64), 256, 0, s>>>(d_rows, n, t->rows.as<uint4>(), (int)(rb / 16),
                                                         (int)(cb / 16), (uint4 *)d_vals);
   else if (t->cfg.dtype == SWPS_F64)
