@@ -123,13 +123,17 @@ def main():
     dev = 0
     torch.cuda.set_device(dev)
     comm = Comm.host(device=dev)
+    if "--ipc" in sys.argv:  # payloads device to device through IPC-mapped inboxes (small slots: rounds)
+        comm.enable_ipc(64 << 10)
+        comm.set_timeout(60)
     for i, (layout, dtype, rule) in enumerate([("w2v", "f32", "adagrad"), ("w2v", "f64", "adagrad"),
                                                ("lr", "f32", "adagrad"), ("w2v", "f32", "sgd")]):
         run_case(sw, comm, rank, world, dev, layout, dtype, rule, seed=5 + i)
+    info = comm.ipc_info()
     comm.close()
     dist.barrier()
     if rank == 0:
-        print("ROUTE OK")
+        print("ROUTE OK", "(ipc: %d exchanges)" % info["exchanges"] if "--ipc" in sys.argv else "")
     dist.destroy_process_group()
 
 

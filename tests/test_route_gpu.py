@@ -57,11 +57,15 @@ def test_rccl_world1_routed_equals_local(lib, gpu, layout, dtype):
     comm.close()
 
 
-def test_routed_two_ranks_host_transport(lib, gpu):
+@pytest.mark.parametrize("ipc", [False, True])
+def test_routed_two_ranks_host_transport(lib, gpu, ipc):
+    """ipc: the same rounds with the payloads through the device-initiated IPC exchange
+    (swps_comm_enable_ipc; headers still over the host transport), incl. the rounds the last
+    rank runs while the others serve from swps_finish."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(ROOT, "tests", "dist_route_check.py")]
+           os.path.join(ROOT, "tests", "dist_route_check.py")] + (["--ipc"] if ipc else [])
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     print(r.stdout[-6000:])
     print("\n".join(ln for ln in r.stderr.splitlines() if "rank0" in ln or "Error" in ln)[-6000:])
