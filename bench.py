@@ -363,9 +363,10 @@ class Ctx:
     def close(self):
         """Every rank at the same point: the IPC communicator's teardown is collective (peers store
         into this rank's inboxes until their last exchange retires)."""
-        if self._ipc and self._ipc[0] is not None:
-            self._ipc[0].close()
-        self._ipc = [None]
+        c = getattr(self, "_ipc_made", None)
+        if c is not None:
+            c.close()
+        self._ipc, self._ipc_made = [None], None
 
     def ipc_comm(self):
         """A second library communicator whose exchanges run device to device through IPC-mapped
@@ -394,6 +395,7 @@ class Ctx:
                     ok = 0
                 t = torch.tensor([ok], dtype=torch.int32, device="cuda")
                 self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+                self._ipc_made = c  # closed by close() on every rank at once (its teardown is collective)
                 if int(t.item()):
                     self._ipc = [c]
                 else:
