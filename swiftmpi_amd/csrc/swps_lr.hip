@@ -1840,6 +1840,10 @@ __device__ __forceinline__ void lr_fx_adagrad(float *__restrict__ r, long long s
 
 constexpr uint32_t kLrFxbPushT = 1024;  // k_lr_fxb_push's threads: one block per bucket, 16 waves
 constexpr uint32_t kLrFxbHotK = 16;     // hot keys per k_lr_fxb_push block (64 row groups each)
+// TO_GRADS (the sharded learner, swps_lr_step): no AdaGrad here — each present key's mean goes to
+// the push payload, rows[vid_row[vid]] (vid_row = the batch's key positions, rows = the payload;
+// hrow = the hot keys' vids); the owners apply it (swps_lr_serve_push)
+template <bool TO_GRADS>
 __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__restrict__ rec,
                                                              const uint16_t *__restrict__ boff,
                                                              const uint32_t *__restrict__ chunk_c0, uint32_t nchunks,
@@ -1923,6 +1927,14 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
     }
     __syncthreads();
     if (diag & 16u) return;
+    if (TO_GRADS) {  // vid = the bucket's key (records carry vids: no affine placement)
+#pragma unroll
+      for (uint32_t k = 0; k < PER; k++) {
+        const uint32_t v = tid + k * NT, c = ac[v];
+        if (c) rows[vid_row[(b << kLrFxVB) + v]] = (float)(((double)(long long)as[v] * inv_scale) / (double)c);
+      }
+      return;
+    }
     uint32_t c[PER], row[PER];  // the thread's PER vids: row loads, then [w | g2] loads, all in flight
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
@@ -1967,8 +1979,12 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
     }
     __syncthreads();
   }
-  if (rg == 0 && h < nhot && ac[tid])
-    lr_fx_adagrad(rows + (uint64_t)hrow[h] * 2, (long long)as[tid], ac[tid], lr, fudge, inv_scale);
+  if (rg == 0 && h < nhot && ac[tid]) {
+    if (TO_GRADS)
+      rows[vid_row[hrow[h]]] = (float)(((double)(long long)as[tid] * inv_scale) / (double)ac[tid]);
+    else
+      lr_fx_adagrad(rows + (uint64_t)hrow[h] * 2, (long long)as[tid], ac[tid], lr, fudge, inv_scale);
+  }
 }
 
 // every record's fid (the fixed-point step's key numbering)
@@ -1983,12 +1999,12 @@ __global__ void k_lr_fx_codes(const uint32_t *__restrict__ vid_row, uint64_t V, 
   const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= V) return;
   const int32_t h = hot_of_vid ? hot_of_vid[v] : -1;
-  vcode[v] = h >= 0 ? (kLrHotBit | (uint32_t)h) : vid_row[v];
+  vcode[v] = h >= 0 ? (kLrHotBit | (uint32_t)h) : vid_row ? vid_row[v] : (uint32_t)v;  // null: the vid
 }
 __global__ void k_lr_fx_hrow(const uint32_t *__restrict__ hot_vid, uint32_t nhot, const uint32_t *__restrict__ vid_row,
                              uint32_t *__restrict__ hrow) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < nhot) hrow[q] = vid_row[hot_vid[q]];
+  if (q < nhot) hrow[q] = vid_row ? vid_row[hot_vid[q]] : hot_vid[q];
 }
 
 // ---- the corpus vocabulary on the GPU (lr_ingest): vid = rank of the key among the distinct keys
@@ -2031,10 +2047,10 @@ __global__ __launch_bounds__(256) void k_lr_predict(const uint64_t *__restrict__
 
 // pulled weights [U] (request order K) into the worker cache; local[vid] = u
 __global__ void k_lr_install(const int32_t *__restrict__ K, uint64_t U, const float *__restrict__ vals,
-                             float *__restrict__ wcache, int32_t *__restrict__ local) {
+                             float *__restrict__ wcache, int32_t *__restrict__ local, int stride) {
   uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= U) return;
-  wcache[K[u]] = vals[u];
+  wcache[(uint64_t)K[u] * stride] = vals[u];
   if (local) local[K[u]] = (int32_t)u;
 }
 
@@ -2171,6 +2187,10 @@ struct swps_lr {
   std::vector<int32_t> allK, init_order;  // vids
   std::vector<uint64_t> kofs, bU, bcounts, icounts;
   DevMem d_K, d_vkeys, d_init_order, d_wcache, d_local, d_serve_rows;
+  // the sharded learner runs the fixed-point step (plan none, fast sums): the pulled weights at
+  // stride 2 (wcache2[2 * vid], the step's row layout) and the mean gradients from its push
+  bool fx_sharded = false;
+  DevMem d_wcache2;
   swps::ShardDriver *drv = nullptr;  // swps_lr_shard_comm: the library drives the exchange
   uint64_t serve_n = 0;
   // the library driver's step slot (AppOps::set_slot): the keys an owner serves at a slot are the
@@ -2814,10 +2834,21 @@ bool lr_fx_usable(const swps_lr *l) {
          !l->fwd_diag && !l->stage && l->nbatches > 0 && (l->fwd_rpt == 8 || l->fwd_rpt == 16);
 }
 
+// the sharded learner's fixed-point step: the bucketed form only (its LDS bounds), vids as keys
+bool lr_fx_sharded_usable(const swps_lr *l) {
+  const uint64_t V = l->vocab_keys.size();
+  const char *e = getenv("SWPS_LR_FX_SHARDED");
+  return l->cfg.plan == SWPS_LR_PLAN_NONE && l->cfg.fast_sums && l->fwd_c && l->rows_per_wave == 1 &&
+         !l->fwd_diag && !l->stage && l->nbatches > 0 && (l->fwd_rpt == 8 || l->fwd_rpt == 16) && V > 0 &&
+         ((V + (1u << kLrFxVB) - 1) >> kLrFxVB) <= kLrFxMaxBk && (2 * l->max_bchunks + 1) * 4 <= 96 * 1024 &&
+         !(getenv("SWPS_LR_FX_ATOMIC") && atoi(getenv("SWPS_LR_FX_ATOMIC")) != 0) && !(e && atoi(e) == 0);
+}
+
 // one batch of the fixed-point step: k_lr_fxb_step over the batch's chunks of whole rows, then
 // k_lr_fxb_push over its buckets and hot keys (the atomic form: k_lr_fx_step, k_lr_fx_apply)
-int lr_batch_fx(swps_lr *l) {
+int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr) {
   hipStream_t s = l->s;
+  const bool shd = l->fx_sharded;
   const uint64_t V = std::max<uint64_t>(l->vocab_keys.size(), 1), cap = l->t->cfg.capacity;
   if (!l->fx_ready) {  // the per-key codes (shard rows are fixed from swps_lr_init on) and buffers
     const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
@@ -2830,13 +2861,14 @@ int lr_batch_fx(swps_lr *l) {
       for (uint32_t q = 0; q < nh; q++) hov[l->fx_hot_vids[q]] = (int32_t)q;
     }
     DevMem dhov;
+    // sharded: a key's "row" is its vid (wcache2[2 * vid]); single GPU: its shard row
+    const uint32_t *vr = shd ? nullptr : l->d_vid_row.as<uint32_t>();
     if (hot) {
       SWPS_TRY(upload(dhov, hov, s));
       SWPS_TRY(upload(l->d_fx_hot, l->fx_hot_vids, s));
-      k_lr_fx_hrow<<<nblk(nh), 256, 0, s>>>(l->d_fx_hot.as<uint32_t>(), nh, l->d_vid_row.as<uint32_t>(),
-                                            l->d_fx_hrow.as<uint32_t>());
+      k_lr_fx_hrow<<<nblk(nh), 256, 0, s>>>(l->d_fx_hot.as<uint32_t>(), nh, vr, l->d_fx_hrow.as<uint32_t>());
     }
-    k_lr_fx_codes<<<nblk(V), 256, 0, s>>>(l->d_vid_row.as<uint32_t>(), l->vocab_keys.size(),
+    k_lr_fx_codes<<<nblk(V), 256, 0, s>>>(vr, l->vocab_keys.size(),
                                           hot ? dhov.as<int32_t>() : nullptr, l->d_vcode.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
     const char *ea = getenv("SWPS_LR_FX_ATOMIC");  // A/B and tests: the per-record atomic form
@@ -2846,8 +2878,9 @@ int lr_batch_fx(swps_lr *l) {
     if (const char *en = getenv("SWPS_LR_FX_NT")) l->fx_nt = atoi(en) == 512 ? 512 : 256;
     l->fxb_nbk = (uint32_t)((V + (1u << kLrFxVB) - 1) >> kLrFxVB);
     if (l->fxb_nbk > kLrFxMaxBk || (2 * l->max_bchunks + 1) * 4 > 96 * 1024) l->fx_atomic = 1;  // LDS bounds
+    if (shd && l->fx_atomic) return fail(SWPS_E_STATE, "sharded fixed-point step needs the bucketed form");
     l->fx_affine = false;
-    if (!l->fx_atomic && l->fx_fid.size() == V && l->vocab_keys.size() == V &&
+    if (!shd && !l->fx_atomic && l->fx_fid.size() == V && l->vocab_keys.size() == V &&
         !(getenv("SWPS_LR_FX_AFFINE") && atoi(getenv("SWPS_LR_FX_AFFINE")) == 0)) {
       // rows placed in fid order by swps_lr_init (a table that held some keys before breaks it)
       std::vector<uint32_t> vr(V);
@@ -2894,6 +2927,13 @@ int lr_batch_fx(swps_lr *l) {
   if (l->row_off[r1] == l->row_off[r0]) return SWPS_OK;
   const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
   const uint64_t nfc = l->bfchunk[bi + 1] - l->bfchunk[bi];
+  if (shd) {  // the owners' pull values at the step's row layout; each key's position for the payload
+    const uint64_t U = l->bU[bi];
+    if (U)
+      k_lr_install<<<nblk(U), 256, 0, s>>>(l->d_K.as<int32_t>() + l->kofs[bi], U, d_vals, l->d_wcache2.as<float>(),
+                                           l->d_local.as<int32_t>(), 2);
+    SWPS_HIP(hipGetLastError());
+  }
   if (!l->fx_atomic) {
     const uint32_t nh = hot ? (uint32_t)l->fx_hot_vids.size() : 0u, grid = (uint32_t)std::min<uint64_t>(nfc, l->fxb_grid);
     const double scale = std::ldexp(1.0, l->fx_bits);
@@ -2915,7 +2955,8 @@ int lr_batch_fx(swps_lr *l) {
                           (const uint64_t *)l->d_row_off.as<uint64_t>(),
                           (const int32_t *)(l->fx_affine ? l->d_ffid.as<int32_t>() : l->d_fvid.as<int32_t>()),
                           (const uint32_t *)l->d_vcode.as<uint32_t>(), (const float *)l->d_fval.as<float>(),
-                          (const float *)l->d_label.as<float>(), r0, (const float *)l->t->rows.as<float>(),
+                          (const float *)l->d_label.as<float>(), r0,
+                          (const float *)(shd ? l->d_wcache2.as<float>() : l->t->rows.as<float>()),
                           hot ? (const uint32_t *)l->d_fx_hrow.as<uint32_t>() : (const uint32_t *)nullptr, nh,
                           l->d_err.as<float>(), l->d_err2.as<float>(), scale, l->fxb_nbk, l->d_fxb_rec.as<uint2>(),
                           l->d_fxb_boff.as<uint16_t>(), (uint32_t)l->max_bchunks, l->d_fxb_hsum.as<unsigned long long>(),
@@ -2927,15 +2968,16 @@ int lr_batch_fx(swps_lr *l) {
     // without their records, 64 no hot-key LDS sums, 128 no bucket sort
     const uint32_t pb0 = (l->fxb_diag & 2u) ? l->fxb_nbk : 0u,
                    pb1 = (l->fxb_diag & 1u) ? l->fxb_nbk : l->fxb_nbk + (nh + kLrFxbHotK - 1) / kLrFxbHotK;
-    hipExtLaunchKernelGGL(k_lr_fxb_push, dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), (2 * nfc + 1) * 4, s, ab,
+    hipExtLaunchKernelGGL(shd ? k_lr_fxb_push<true> : k_lr_fxb_push<false>, dim3(std::max(1u, pb1 - pb0)),
+                          dim3(kLrFxbPushT), (2 * nfc + 1) * 4, s, ab,
                           ae, 0,
                           (const uint2 *)l->d_fxb_rec.as<uint2>(), (const uint16_t *)l->d_fxb_boff.as<uint16_t>(),
                           (const uint32_t *)l->d_fchunk_c0.as<uint32_t>() + l->bfchunk[bi], (uint32_t)nfc, l->fxb_nbk,
                           (uint32_t)l->max_bchunks,
-                          (const uint32_t *)l->d_vid_row.as<uint32_t>(),
+                          (const uint32_t *)(shd ? (const uint32_t *)l->d_local.as<int32_t>() : l->d_vid_row.as<uint32_t>()),
                           (const unsigned long long *)l->d_fxb_hsum.as<unsigned long long>(),
                           (const uint32_t *)l->d_fxb_hcnt.as<uint32_t>(), grid,
-                          (const uint32_t *)l->d_fx_hrow.as<uint32_t>(), nh, l->t->rows.as<float>(),
+                          (const uint32_t *)l->d_fx_hrow.as<uint32_t>(), nh, shd ? d_grads : l->t->rows.as<float>(),
                           l->t->cfg.learning_rate, l->t->cfg.fudge, scale, std::ldexp(1.0, -l->fx_bits),
                           (uint32_t)l->fx_affine, l->fx_row_base, pb0, l->fxb_diag);
     SWPS_HIP(hipGetLastError());
@@ -3180,6 +3222,8 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     SWPS_TRY(lr_fwd_chunks(l));
     if (lr_fx_usable(l)) return lr_batch_fx(l);
     if (lr_plan_usable(l)) return lr_batch_planned(l);
+  } else if (l->fx_sharded) {
+    return lr_batch_fx(l, d_vals, d_grads);
   }
   if (!l->index_built) SWPS_TRY(lr_index(l));  // the static per-batch index, built once
   const uint64_t nr = l->label.size();
@@ -3195,7 +3239,7 @@ int lr_batch(swps_lr *l, const float *d_vals = nullptr, float *d_grads = nullptr
     const uint64_t U = l->bU[bi];
     if (U)
       k_lr_install<<<nblk(U), 256, 0, s>>>(l->d_K.as<int32_t>() + l->kofs[bi], U, d_vals, l->d_wcache.as<float>(),
-                                           l->d_local.as<int32_t>());
+                                           l->d_local.as<int32_t>(), 1);
     SWPS_HIP(hipGetLastError());
     rows = l->d_wcache.as<float>();
     fidx = (const uint32_t *)l->d_fvid.as<int32_t>();
@@ -3772,7 +3816,11 @@ int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
     return fail(SWPS_E_UNSUPPORTED, "sharded mode initialises on the owners (init_ref = 0, SWPS_INIT_HASH): the "
                                     "reference's float-LCG order depends on message arrival");
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
-  if (!l->index_built) SWPS_TRY(lr_index(l));  // the sharded step reads the static index
+  // plan none with fast sums: the learner runs the fixed-point step (no index); otherwise the
+  // sharded step reads the static index
+  SWPS_TRY(lr_fwd_chunks(l));
+  l->fx_sharded = lr_fx_sharded_usable(l);
+  if (!l->fx_sharded && !l->index_built) SWPS_TRY(lr_index(l));
   std::vector<uint32_t> map(frag_num);
   SWPS_TRY(swps_hashfrag_table(frag_num, world, map.data()));
   const uint64_t V = l->vocab_keys.size(), nb = l->nbatches, nr = l->label.size();
@@ -3821,6 +3869,10 @@ int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
   SWPS_TRY(l->d_wcache.ensure(std::max<uint64_t>(V, 1) * 4));
   SWPS_TRY(l->d_local.ensure(std::max<uint64_t>(V, 1) * 4));
   SWPS_HIP(hipMemsetAsync(l->d_wcache.p, 0, std::max<uint64_t>(V, 1) * 4, l->s));
+  if (l->fx_sharded) {
+    SWPS_TRY(l->d_wcache2.ensure(std::max<uint64_t>(V, 1) * 8));
+    SWPS_HIP(hipMemsetAsync(l->d_wcache2.p, 0, std::max<uint64_t>(V, 1) * 8, l->s));
+  }
   SWPS_HIP(hipStreamSynchronize(l->s));
   l->rank = rank;
   l->world = world;
@@ -3895,8 +3947,9 @@ int swps_lr_install(swps_lr *l, const float *d_vals) {
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
   const uint64_t V = l->vocab_keys.size();
   if (V)
-    k_lr_install<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals, l->d_wcache.as<float>(),
-                                            nullptr);
+    k_lr_install<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals,
+                                            l->fx_sharded ? l->d_wcache2.as<float>() : l->d_wcache.as<float>(),
+                                            nullptr, l->fx_sharded ? 2 : 1);
   SWPS_HIP(hipGetLastError());
   l->inited = true;
   return SWPS_OK;

@@ -5,7 +5,9 @@ two ranks on one GPU (same-device IPC):
      several times a slot (segments stream through the two parities in rounds), from two streams
      in turn — must deliver exactly what the TCP transport delivers;
   2. the library-driven LR and CBOW loops (swps_lr_shard_comm / swps_w2v_shard_comm) over an
-     IPC communicator must leave every rank's shard bit-identical to the same loops over TCP;
+     IPC communicator must leave every rank's shard bit-identical to the same loops over TCP, and
+     the sharded fixed-point LR step (plan none) on disjoint per-rank keys must equal each rank's
+     single-GPU fixed-point training;
   3. the per-exchange latency of a small exchange (the LR step's size class) over both, printed
      as one JSON line ("IPC_LAT {...}");
   4. a lost peer: a lone exchange fails within its deadline, naming the peer, and the peer's next
@@ -123,6 +125,43 @@ def main():
     assert np.array_equal(a_[0], b_[0]) and np.array_equal(a_[1], b_[1]) and np.array_equal(a_[2], b_[2])
     assert torch.equal(a_[3], b_[3])
     print("rank %d lr ok: %d keys" % (rank, len(a_[2])), flush=True)
+    # 2b. the sharded fixed-point step (plan none, fast sums) at world 2: each rank's keys are
+    # disjoint from the other's (offset rank << 20), so the union of the shards must equal each
+    # rank's own single-GPU fixed-point training, key for key and bit for bit — over TCP and IPC
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(3000 + 700 * rank, seed=50 + rank, bits=14)
+    f = f + np.uint32(rank << 20)
+    lk = dict(capacity=1 << 16, dtype="f32", learning_rate=0.05, init="hash", seed=4, device=0)
+    res = {}
+    for name, comm in (("tcp", tcp), ("ipc", ipc), ("single", None)):
+        t = sw.Table("lr", **lk)
+        m = sw.LR(t, minibatch=255, init_ref=False, fast_sums=True, plan="none")
+        m.load_csr(y, off, f, v)
+        if comm is not None:
+            m.shard_comm(comm, frag_num=2000)
+        m.init()
+        m.train(2)
+        k = np.sort(t.keys())
+        res[name] = (k, t.export(torch.as_tensor(k.astype(np.int64), device="cuda")).cpu().numpy())
+        m.close()
+        t.close()
+    assert np.array_equal(res["tcp"][0], res["ipc"][0]) and np.array_equal(res["tcp"][1], res["ipc"][1])
+    objs = [None] * world
+    dist.all_gather_object(objs, (res["ipc"][0].tolist(), res["ipc"][1].tolist(), res["single"][0].tolist(),
+                                  res["single"][1].tolist()))
+    if rank == 0:
+        owned = {}
+        for k, r, _, _ in objs:
+            for a, b in zip(k, r):
+                assert a not in owned, "key owned twice"
+                owned[a] = tuple(b)
+        n = 0
+        for _, _, k, r in objs:
+            for a, b in zip(k, r):
+                assert owned[a] == tuple(b), ("fixed-point shard differs", a, owned[a], b)
+                n += 1
+        assert n == len(owned), (n, len(owned))
+        print("lr fixed point sharded ok: %d keys" % n, flush=True)
     path = corpus(os.path.join(tmp, "c%d.txt" % rank), rank)
     kw = dict(window=4, negative=4, minibatch=19, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=False)
     res = {}

@@ -659,3 +659,37 @@ def test_lr_config3_full_rank_share(lib, gpu):
     for a, b in zip(outs[0][:3], outs[1][:3]):
         assert np.array_equal(a, b)
     assert np.isfinite(outs[0][1]).all() and np.isfinite(outs[0][0]).all()
+
+
+@pytest.mark.parametrize("B", [4095, 200])
+def test_sharded_fixed_point_world1_equals_unsharded(lib, gpu, B):
+    """The sharded learner's fixed-point step (plan none, fast sums: swps_lr_step writes each
+    key's mean of its integer sums as the push payload and the owner applies AdaGrad,
+    k_lr_fxb_push<TO_GRADS>) through the library driver at world 1 (RCCL) == the single-GPU
+    fixed-point step, bit for bit: weights, AdaGrad sums and epoch errors over 3 epochs."""
+    import torch
+    from conftest import free_port
+    from swiftmpi_amd.comm import Comm
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(12 * B + 7, seed=21, bits=16)
+    res = []
+    for sharded in (False, True):
+        t = lib.Table("lr", capacity=1 << 17, dtype="f32", learning_rate=0.05, init="hash", seed=4)
+        m = lib.LR(t, minibatch=B, init_ref=False, fast_sums=True, plan="none")
+        m.load_csr(y, off, f, v)
+        comm = None
+        if sharded:
+            comm = Comm.rccl(0, 1, port=free_port())
+            m.shard_comm(comm, frag_num=2000)
+        m.init()
+        e = m.train(3)
+        k = np.sort(t.keys())
+        rows = t.export(torch.as_tensor(k.astype(np.int64), device="cuda")).cpu().numpy()
+        res.append((e, k, rows))
+        m.close()
+        t.close()
+        if comm is not None:
+            comm.close()
+    assert np.array_equal(res[0][1], res[1][1])
+    assert np.array_equal(res[0][2], res[1][2]), float(np.abs(res[0][2] - res[1][2]).max())
+    assert np.array_equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
