@@ -1841,8 +1841,8 @@ __device__ __forceinline__ void lr_fx_adagrad(float *__restrict__ r, long long s
 constexpr uint32_t kLrFxbPushT = 1024;  // k_lr_fxb_push's threads: one block per bucket, 16 waves
 constexpr uint32_t kLrFxbHotK = 16;     // hot keys per k_lr_fxb_push block (64 row groups each)
 // TO_GRADS (the sharded learner, swps_lr_step): no AdaGrad here — each present key's mean goes to
-// the push payload, rows[vid_row[vid]] (vid_row = the batch's key positions, rows = the payload;
-// hrow = the hot keys' vids); the owners apply it (swps_lr_serve_push)
+// the push payload, rows[vid_row[fid]] (vid_row = the batch's key positions by fid, rows = the
+// payload; hrow[q] = q); the owners apply it (swps_lr_serve_push)
 template <bool TO_GRADS>
 __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__restrict__ rec,
                                                              const uint16_t *__restrict__ boff,
@@ -1927,7 +1927,7 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
     }
     __syncthreads();
     if (diag & 16u) return;
-    if (TO_GRADS) {  // vid = the bucket's key (records carry vids: no affine placement)
+    if (TO_GRADS) {  // the bucket's key (records carry fids: the affine form with row base 0)
 #pragma unroll
       for (uint32_t k = 0; k < PER; k++) {
         const uint32_t v = tid + k * NT, c = ac[v];
@@ -2052,6 +2052,18 @@ __global__ void k_lr_install(const int32_t *__restrict__ K, uint64_t U, const fl
   if (u >= U) return;
   wcache[(uint64_t)K[u] * stride] = vals[u];
   if (local) local[K[u]] = (int32_t)u;
+}
+
+// the sharded fixed-point step's install: the value of key K[u] at its fid's row of the step's layout
+// (wcache2[2 * fid]: the affine form with row base 0, hot keys first), and its position u by fid
+__global__ void k_lr_install_fx(const int32_t *__restrict__ K, uint64_t U, const float *__restrict__ vals,
+                                const uint32_t *__restrict__ fid, float *__restrict__ wcache2,
+                                uint32_t *__restrict__ localf) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  const uint32_t q = fid[K[u]];
+  wcache2[(uint64_t)q * 2] = vals[u];
+  if (localf) localf[q] = (uint32_t)u;
 }
 
 __global__ void k_lr_keys(const int32_t *__restrict__ K, uint64_t n, const uint64_t *__restrict__ vkeys,
@@ -2190,7 +2202,7 @@ struct swps_lr {
   // the sharded learner runs the fixed-point step (plan none, fast sums): the pulled weights at
   // stride 2 (wcache2[2 * vid], the step's row layout) and the mean gradients from its push
   bool fx_sharded = false;
-  DevMem d_wcache2;
+  DevMem d_wcache2, d_fx_fidv, d_localf;  // [2V] weights by fid; fid by vid; batch position by fid
   swps::ShardDriver *drv = nullptr;  // swps_lr_shard_comm: the library drives the exchange
   uint64_t serve_n = 0;
   // the library driver's step slot (AppOps::set_slot): the keys an owner serves at a slot are the
@@ -2841,7 +2853,8 @@ bool lr_fx_sharded_usable(const swps_lr *l) {
   return l->cfg.plan == SWPS_LR_PLAN_NONE && l->cfg.fast_sums && l->fwd_c && l->rows_per_wave == 1 &&
          !l->fwd_diag && !l->stage && l->nbatches > 0 && (l->fwd_rpt == 8 || l->fwd_rpt == 16) && V > 0 &&
          ((V + (1u << kLrFxVB) - 1) >> kLrFxVB) <= kLrFxMaxBk && (2 * l->max_bchunks + 1) * 4 <= 96 * 1024 &&
-         !(getenv("SWPS_LR_FX_ATOMIC") && atoi(getenv("SWPS_LR_FX_ATOMIC")) != 0) && !(e && atoi(e) == 0);
+         !(getenv("SWPS_LR_FX_ATOMIC") && atoi(getenv("SWPS_LR_FX_ATOMIC")) != 0) && !(e && atoi(e) == 0) &&
+         l->fx_fid.size() == V;
 }
 
 // one batch of the fixed-point step: k_lr_fxb_step over the batch's chunks of whole rows, then
@@ -2880,6 +2893,19 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
     if (l->fxb_nbk > kLrFxMaxBk || (2 * l->max_bchunks + 1) * 4 > 96 * 1024) l->fx_atomic = 1;  // LDS bounds
     if (shd && l->fx_atomic) return fail(SWPS_E_STATE, "sharded fixed-point step needs the bucketed form");
     l->fx_affine = false;
+    if (shd) {  // the affine form over wcache2 (row base 0): records carry fids, hot key q = fid q
+      const uint64_t nnz = l->row_off.back();
+      SWPS_TRY(l->d_ffid.ensure(std::max<uint64_t>(nnz, 1) * 4));
+      k_lr_fx_fid<<<nblk(nnz), 256, 0, s>>>(l->d_fvid.as<int32_t>(), nnz, l->d_fx_fidv.as<uint32_t>(),
+                                            l->d_ffid.as<int32_t>());
+      std::vector<uint32_t> iota(std::max<uint32_t>(nh, 1));
+      for (uint32_t q = 0; q < iota.size(); q++) iota[q] = q;
+      SWPS_TRY(upload(l->d_fx_hrow, iota, s));
+      SWPS_HIP(hipGetLastError());
+      SWPS_HIP(hipStreamSynchronize(s));
+      l->fx_affine = true;
+      l->fx_row_base = 0;
+    }
     if (!shd && !l->fx_atomic && l->fx_fid.size() == V && l->vocab_keys.size() == V &&
         !(getenv("SWPS_LR_FX_AFFINE") && atoi(getenv("SWPS_LR_FX_AFFINE")) == 0)) {
       // rows placed in fid order by swps_lr_init (a table that held some keys before breaks it)
@@ -2930,8 +2956,9 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
   if (shd) {  // the owners' pull values at the step's row layout; each key's position for the payload
     const uint64_t U = l->bU[bi];
     if (U)
-      k_lr_install<<<nblk(U), 256, 0, s>>>(l->d_K.as<int32_t>() + l->kofs[bi], U, d_vals, l->d_wcache2.as<float>(),
-                                           l->d_local.as<int32_t>(), 2);
+      k_lr_install_fx<<<nblk(U), 256, 0, s>>>(l->d_K.as<int32_t>() + l->kofs[bi], U, d_vals,
+                                              l->d_fx_fidv.as<uint32_t>(), l->d_wcache2.as<float>(),
+                                              l->d_localf.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
   }
   if (!l->fx_atomic) {
@@ -2974,7 +3001,7 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
                           (const uint2 *)l->d_fxb_rec.as<uint2>(), (const uint16_t *)l->d_fxb_boff.as<uint16_t>(),
                           (const uint32_t *)l->d_fchunk_c0.as<uint32_t>() + l->bfchunk[bi], (uint32_t)nfc, l->fxb_nbk,
                           (uint32_t)l->max_bchunks,
-                          (const uint32_t *)(shd ? (const uint32_t *)l->d_local.as<int32_t>() : l->d_vid_row.as<uint32_t>()),
+                          (const uint32_t *)(shd ? l->d_localf.as<uint32_t>() : l->d_vid_row.as<uint32_t>()),
                           (const unsigned long long *)l->d_fxb_hsum.as<unsigned long long>(),
                           (const uint32_t *)l->d_fxb_hcnt.as<uint32_t>(), grid,
                           (const uint32_t *)l->d_fx_hrow.as<uint32_t>(), nh, shd ? d_grads : l->t->rows.as<float>(),
@@ -3872,6 +3899,8 @@ int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
   if (l->fx_sharded) {
     SWPS_TRY(l->d_wcache2.ensure(std::max<uint64_t>(V, 1) * 8));
     SWPS_HIP(hipMemsetAsync(l->d_wcache2.p, 0, std::max<uint64_t>(V, 1) * 8, l->s));
+    SWPS_TRY(upload(l->d_fx_fidv, l->fx_fid, l->s));
+    SWPS_TRY(l->d_localf.ensure(std::max<uint64_t>(V, 1) * 4));
   }
   SWPS_HIP(hipStreamSynchronize(l->s));
   l->rank = rank;
@@ -3946,10 +3975,12 @@ int swps_lr_install(swps_lr *l, const float *d_vals) {
   if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
   const uint64_t V = l->vocab_keys.size();
-  if (V)
-    k_lr_install<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals,
-                                            l->fx_sharded ? l->d_wcache2.as<float>() : l->d_wcache.as<float>(),
-                                            nullptr, l->fx_sharded ? 2 : 1);
+  if (V && l->fx_sharded)
+    k_lr_install_fx<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals, l->d_fx_fidv.as<uint32_t>(),
+                                               l->d_wcache2.as<float>(), nullptr);
+  else if (V)
+    k_lr_install<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals, l->d_wcache.as<float>(),
+                                            nullptr, 1);
   SWPS_HIP(hipGetLastError());
   l->inited = true;
   return SWPS_OK;
