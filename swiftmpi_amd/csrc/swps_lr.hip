@@ -20,6 +20,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <limits>
@@ -3854,34 +3855,54 @@ int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
   std::vector<int32_t> owner(V);
   for (uint64_t i = 0; i < V; i++) owner[i] = (int32_t)map[fmix64(l->vocab_keys[i]) % (uint64_t)frag_num] - 1;
   SWPS_TRY(lr_fvid_host(l));
-  // per batch: unique vids in owner order, then vid order (counting sort by owner)
-  std::vector<uint64_t> stamp(V, ~0ULL);
-  std::vector<int32_t> uniq;
-  std::vector<uint64_t> start(world + 1);
-  l->allK.clear();
+  // per batch: unique vids in owner order, then vid order (counting sort by owner) — batches are
+  // independent: worker threads build them (each its own stamp array), then one concatenation
   l->kofs.assign(nb, 0);
   l->bU.assign(nb, 0);
   l->bcounts.assign(nb * world, 0);
-  for (uint64_t bi = 0; bi < nb; bi++) {
-    const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1());
-    uniq.clear();
-    for (uint64_t i = l->row_off[r0]; i < l->row_off[r1]; i++) {
-      const int32_t v = l->fvid[i];
-      if (stamp[v] != bi) {
-        stamp[v] = bi;
-        uniq.push_back(v);
+  std::vector<std::vector<int32_t>> kb(nb);
+  {
+    const unsigned nth = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({nb, 16, std::max(1u, std::thread::hardware_concurrency())}));
+    std::atomic<uint64_t> next_b{0};
+    auto work = [&]() {
+      std::vector<uint32_t> stamp(V, 0u);
+      std::vector<int32_t> uniq;
+      std::vector<uint64_t> start(world + 1);
+      for (uint64_t bi; (bi = next_b.fetch_add(1)) < nb;) {
+        const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1());
+        const uint32_t tag = (uint32_t)bi + 1u;
+        uniq.clear();
+        for (uint64_t i = l->row_off[r0]; i < l->row_off[r1]; i++) {
+          const int32_t v = l->fvid[i];
+          if (stamp[v] != tag) {
+            stamp[v] = tag;
+            uniq.push_back(v);
+          }
+        }
+        std::sort(uniq.begin(), uniq.end());
+        uint64_t *cnt = &l->bcounts[bi * world];
+        for (int32_t v : uniq) cnt[owner[v]]++;
+        start[0] = 0;
+        for (int r = 0; r < world; r++) start[r + 1] = start[r] + cnt[r];
+        std::vector<int32_t> &dst = kb[bi];
+        dst.resize(uniq.size());
+        for (int32_t v : uniq) dst[start[owner[v]]++] = v;
       }
-    }
-    std::sort(uniq.begin(), uniq.end());
-    uint64_t *cnt = &l->bcounts[bi * world];
-    for (int32_t v : uniq) cnt[owner[v]]++;
-    start[0] = 0;
-    for (int r = 0; r < world; r++) start[r + 1] = start[r] + cnt[r];
+    };
+    std::vector<std::thread> th;
+    for (unsigned q = 1; q < nth; q++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+  }
+  l->allK.clear();
+  uint64_t tot = 0;
+  for (uint64_t bi = 0; bi < nb; bi++) tot += kb[bi].size();
+  l->allK.reserve(tot);
+  for (uint64_t bi = 0; bi < nb; bi++) {
     l->kofs[bi] = l->allK.size();
-    l->bU[bi] = uniq.size();
-    l->allK.resize(l->allK.size() + uniq.size());
-    int32_t *dst = l->allK.data() + l->kofs[bi];
-    for (int32_t v : uniq) dst[start[owner[v]]++] = v;
+    l->bU[bi] = kb[bi].size();
+    l->allK.insert(l->allK.end(), kb[bi].begin(), kb[bi].end());
+    std::vector<int32_t>().swap(kb[bi]);
   }
   l->init_order.resize(V);
   for (uint64_t i = 0; i < V; i++) l->init_order[i] = (int32_t)i;
