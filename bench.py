@@ -950,7 +950,8 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
     xs = m.exchange_stats(on=0) if comm is not None else None
     m.set_profile(False)
     pbat = [(warm + steps + k) % nb for k in range(steps)]  # the profiled pass's batches
-    fxb = [m.fx_bytes(b) for b in pbat] if args.lr_plan == "none" and comm is None and dist is None else []
+    # the fixed-point step runs unsharded and on the library driver's sharded learner (plan none)
+    fxb = [m.fx_bytes(b) for b in pbat] if args.lr_plan == "none" and (comm is not None or dist is None) else []
     fx = bool(fxb) and all(d["form"] == 1 for d in fxb)
     m.close()
     t.close()

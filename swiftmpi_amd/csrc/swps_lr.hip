@@ -4043,7 +4043,7 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
 int swps_lr_fx_bytes(swps_lr *l, uint64_t batch, uint64_t *out8) {
   if (!l->loaded || batch >= l->nbatches) return fail(SWPS_E_CFG, "no such batch");
   for (int i = 0; i < 8; i++) out8[i] = 0;
-  if (!lr_fx_usable(l) || !l->fx_ready) return SWPS_OK;
+  if (!(lr_fx_usable(l) || l->fx_sharded) || !l->fx_ready) return SWPS_OK;  // sharded: the same model
   SWPS_TRY(lr_fvid_host(l));
   const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
   const uint64_t nh = hot ? l->fx_hot_vids.size() : 0;
