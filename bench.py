@@ -458,6 +458,8 @@ def w2v_leg(sw, ctx, args, ids, off, keys, prec, minibatch, dim, frag_num, steps
     t = sw.Table("w2v", dim=dim, capacity=vocab, dtype=args.dtype, learning_rate=args.lr, device=ctx.local,
                  init="hash", seed=1)
     comm = ctx.comm() if ctx.sharded and args.driver == "native" else None
+    if comm is not None and cbow_ipc(ctx, args):
+        comm = ctx.ipc_comm()  # opt-in: the CBOW legs' exchanges through the IPC path too
     if comm is not None:  # the library's own exchange
         from swiftmpi_amd.dist import NativeShardedWord2Vec
         w = NativeShardedWord2Vec(t, comm, frag_num=frag_num, **kw)
@@ -618,12 +620,18 @@ def parallelism(ctx, args, frag_num):
                if args.pipeline else "lockstep pull/learn/push"))
 
 
-def with_transport(out, ctx):
+def with_transport(out, ctx, ipc=False):
     tr = ctx.transport()
     if tr is not None:  # the library's own communicator: what its transport reports
-        out["transport"] = tr[0]
+        out["transport"] = tr[0] + ("+ipc" if ipc else "")
         out["rccl_ranks" if tr[0] == "rccl" else "transport_ranks"] = tr[1]
     return out
+
+
+def cbow_ipc(ctx, args):
+    """--exchange ipc-all: the CBOW legs' exchanges go through the IPC communicator."""
+    return (ctx.sharded and args.driver == "native" and args.exchange == "ipc-all" and ctx.dist is not None
+            and ctx.ipc_comm() is not None)
 
 
 def config4_leg(sw, ctx, args):
@@ -658,7 +666,7 @@ def config4_leg(sw, ctx, args):
            "exchange": exchange_block(r.get("xs"), r["steps"], r.get("dpt", 0.0), ctx.world,
                                       "remote bytes (keys 8 B, rows 2*D*4 B, grads 2*D*8 B per remote key) / "
                                       "all-to-all time (events on the exchange stream, profiled pass)")}
-    return with_transport(out, ctx)
+    return with_transport(out, ctx, cbow_ipc(ctx, args))
 
 
 def main():
@@ -685,9 +693,10 @@ def main():
     ap.add_argument("--driver", default="native", choices=["python", "native"],
                     help="sharded exchange: swiftmpi_amd/dist.py over torch.distributed, or the library's own "
                          "(swps_w2v_shard_comm over RCCL / its TCP transport)")
-    ap.add_argument("--exchange", default="auto", choices=["auto", "base"],
+    ap.add_argument("--exchange", default="auto", choices=["auto", "base", "ipc-all"],
                     help="N > 1 LR leg: auto = the device-initiated IPC exchange (swps_comm_enable_ipc) when its "
-                         "canary passes on every rank, else the base transport; base = RCCL / TCP only")
+                         "canary passes on every rank, else the base transport; base = RCCL / TCP only; ipc-all = "
+                         "the CBOW legs (headline, config 4) through it too (opt-in: unmeasured against RCCL at N = 8)")
     ap.add_argument("--pipeline", action="store_true",
                     help="sharded path: the bounded-staleness driver (pull(i+1)/push(i) overlap learn(i)) instead "
                          "of the default lockstep pull/learn/push order (exact reference semantics)")
@@ -835,7 +844,7 @@ def main():
                                    "(events on the exchange stream, profiled pass); world %d"
                                    % (2 * D * (8 if args.dtype == "f64" else 4), world)),
     }
-    with_transport(out, ctx)
+    with_transport(out, ctx, cbow_ipc(ctx, args))
     if one and not args.no_cpu_baseline:
         set_phase("cpu_baseline")
         out["cpu_baseline"] = cpu_baseline(ids, off, keys, args, args.cpu_lines)
