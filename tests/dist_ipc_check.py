@@ -208,11 +208,11 @@ def main():
             ipc.check()
             raise AssertionError("a lone exchange did not time out")
         except SwpsError as e:
-            assert "IPC exchange" in str(e) and "rank 1" in str(e), str(e)
+            assert "IPC exchange" in str(e) and ("rank 1" in str(e) or world > 2), str(e)
         assert waited < 30, waited
         print("rank 0 lost peer detected after %.1f s: ok" % waited, flush=True)
     dist.barrier()
-    if rank == 1:
+    if rank != 0:
         t0 = time.perf_counter()
         ipc.alltoallv(one, [1024] * world, got, [1024] * world)
         torch.cuda.synchronize()
@@ -222,7 +222,7 @@ def main():
         except SwpsError as e:
             assert "IPC exchange" in str(e), str(e)
         assert time.perf_counter() - t0 < 10
-        print("rank 1 dead peer detected: ok", flush=True)
+        print("rank %d dead peer detected: ok" % rank, flush=True)
     dist.barrier()
     ipc.close()  # neither rank waits for the other here (both saw the dead word)
     tcp.close()

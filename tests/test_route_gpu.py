@@ -153,13 +153,14 @@ def test_native_sharded_driver_equals_python_driver(lib, gpu):
     assert r.returncode == 0 and "NATIVE OK" in r.stdout
 
 
-def test_ipc_exchange_equals_tcp(lib, gpu):
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_ipc_exchange_equals_tcp(lib, gpu, ranks):
     """The device-initiated IPC exchange (swps_comm_enable_ipc) == the TCP transport, bit for bit:
     raw all-to-all-v calls (empty / odd / multi-slot segments, two streams) and the library-driven
-    LR and CBOW loops, two ranks on one GPU (tests/dist_ipc_check.py); prints the per-exchange
-    latency of both."""
+    LR and CBOW loops, 2 and 4 ranks on one GPU (tests/dist_ipc_check.py); prints the per-exchange
+    latency of both, and a lost peer fails every rank's next exchange."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "dist_ipc_check.py"), "--tcp-port", str(_port())]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
