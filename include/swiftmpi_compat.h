@@ -735,6 +735,9 @@ template <class WorkerT, class ServerT, class KeyT> class Cluster {
         swps_check(swps_comm_bootstrap_tcp(addr ? addr : "127.0.0.1", port, _rank, _world, timeout, id.data()));
         swps_check(swps_comm_create_rccl(id.data(), _rank, _world, dev, &_comm));
       }
+      // SWPS_COMM_IPC=1: the exchanges' payloads device to device through IPC-mapped peer
+      // inboxes (swps_comm_enable_ipc; the ranks of one node)
+      if (_world > 1 && env_int("SWPS_COMM_IPC", nullptr, 0)) swps_check(swps_comm_enable_ipc(_comm, 0));
       swps_check(swps_table_route(_t, _comm, global_frag_num()));
       global_swps_comm() = _comm;
     }

@@ -109,11 +109,13 @@ def test_compat_ps_client_two_ranks(compat_bin, gpu, tmp_path):
 
 
 @pytest.mark.gpu
-def test_compat_w2v_main_two_ranks_matches_python_driver(compat_bin, lib, gpu, tmp_path):
+@pytest.mark.parametrize("ipc", ["0", "1"])
+def test_compat_w2v_main_two_ranks_matches_python_driver(compat_bin, lib, gpu, tmp_path, ipc):
     """apps/word2vec/w2v.cpp's main on two C++ ranks (one GPU, TCP transport):
     each rank trains its own corpus, the library runs the key-sharded
     exchange (swps_w2v_shard_comm) — every rank's dumped shard equals the one
-    the Python driver over gloo produces (tests/dist_w2v_dump.py)."""
+    the Python driver over gloo produces (tests/dist_w2v_dump.py).  ipc = 1:
+    the Cluster's exchanges through the IPC path (SWPS_COMM_IPC=1)."""
     import sys
     conf = tmp_path / "demo.conf"
     conf.write_text(W2V_CONF)
@@ -123,7 +125,7 @@ def test_compat_w2v_main_two_ranks_matches_python_driver(compat_bin, lib, gpu, t
     procs = []
     for rank in range(2):
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   SWPS_BOOTSTRAP_PORT=port, SWPS_TRANSPORT="tcp", HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   SWPS_BOOTSTRAP_PORT=port, SWPS_TRANSPORT="tcp", HSA_ENABLE_IPC_MODE_LEGACY="0", SWPS_COMM_IPC=ipc)
         procs.append(subprocess.Popen([compat_bin, "w2v", "-config", str(conf), "-data", data[rank], "-niters", "2",
                                        "-output", cpp_out], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                       text=True, env=env))
