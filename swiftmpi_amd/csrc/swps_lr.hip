@@ -3996,10 +3996,9 @@ int swps_lr_install(swps_lr *l, const float *d_vals) {
   if (!l->sharded) return fail(SWPS_E_STATE, "not sharded");
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
   const uint64_t V = l->vocab_keys.size();
-  if (V && l->fx_sharded)
-    k_lr_install_fx<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals, l->d_fx_fidv.as<uint32_t>(),
-                                               l->d_wcache2.as<float>(), nullptr);
-  else if (V)
+  // the full pull's values by vid (swps_lr_predict reads them; the fixed-point step installs each
+  // batch's own at its layout)
+  if (V)
     k_lr_install<<<nblk(V), 256, 0, l->s>>>(l->d_init_order.as<int32_t>(), V, d_vals, l->d_wcache.as<float>(),
                                             nullptr, 1);
   SWPS_HIP(hipGetLastError());

@@ -666,7 +666,8 @@ def test_sharded_fixed_point_world1_equals_unsharded(lib, gpu, B):
     """The sharded learner's fixed-point step (plan none, fast sums: swps_lr_step writes each
     key's mean of its integer sums as the push payload and the owner applies AdaGrad,
     k_lr_fxb_push<TO_GRADS>) through the library driver at world 1 (RCCL) == the single-GPU
-    fixed-point step, bit for bit: weights, AdaGrad sums and epoch errors over 3 epochs."""
+    fixed-point step, bit for bit: weights, AdaGrad sums and epoch errors over 3 epochs, and the
+    predictions after them."""
     import torch
     from conftest import free_port
     from swiftmpi_amd.comm import Comm
@@ -683,9 +684,10 @@ def test_sharded_fixed_point_world1_equals_unsharded(lib, gpu, B):
             m.shard_comm(comm, frag_num=2000)
         m.init()
         e = m.train(3)
+        p = m.predict()[0]  # sharded: a full pull refreshes the worker cache first
         k = np.sort(t.keys())
         rows = t.export(torch.as_tensor(k.astype(np.int64), device="cuda")).cpu().numpy()
-        res.append((e, k, rows))
+        res.append((e, k, rows, p))
         m.close()
         t.close()
         if comm is not None:
@@ -693,3 +695,4 @@ def test_sharded_fixed_point_world1_equals_unsharded(lib, gpu, B):
     assert np.array_equal(res[0][1], res[1][1])
     assert np.array_equal(res[0][2], res[1][2]), float(np.abs(res[0][2] - res[1][2]).max())
     assert np.array_equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
+    assert np.array_equal(res[0][3], res[1][3])
