@@ -1079,10 +1079,12 @@ int swps_comm_destroy(swps_comm *c) {
     const bool ok = hipDeviceSynchronize() == hipSuccess && comm_aborted(c) == SWPS_OK &&
                     hipMemcpy(&dead, (uint64_t *)p->ctrl + kIpcDead, 8, hipMemcpyDeviceToHost) == hipSuccess &&
                     dead == 0;
-    if (ok) {
+    hipStream_t hs = nullptr;
+    if (ok && hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) == hipSuccess) {
       std::vector<int64_t> all(c->world);
       const int64_t one = 1;
-      (void)comm_allgather(c, &one, all.data(), 8, nullptr);
+      (void)comm_allgather(c, &one, all.data(), 8, hs);
+      (void)hipStreamDestroy(hs);
     }
     for (int r = 0; r < c->world; r++)
       if (r != c->rank) {
@@ -1205,7 +1207,11 @@ int swps_comm_enable_ipc(swps_comm *c, uint64_t slot_bytes) {
     if (hipIpcGetMemHandle(&mine[0], p->inbox) != hipSuccess || hipIpcGetMemHandle(&mine[1], p->ctrl) != hipSuccess)
       return undo("hipIpcGetMemHandle failed");
     // every rank's ctrl words are zero before its handles leave it, so a peer's first store lands after
-    if (comm_allgather(c, mine, all, sizeof(mine), nullptr) != SWPS_OK) return undo("handle all-gather failed");
+    hipStream_t hs = nullptr;
+    if (hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) != hipSuccess) return undo("stream");
+    const int ag = comm_allgather(c, mine, all, sizeof(mine), hs);
+    (void)hipStreamDestroy(hs);
+    if (ag != SWPS_OK) return undo("handle all-gather failed");
     for (int r = 0; r < W; r++) {
       if (r == c->rank) {
         p->peer_inbox[r] = p->inbox;
