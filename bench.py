@@ -388,7 +388,10 @@ class Ctx:
                          if self.backend == "nccl" else Comm.tcp(self.rank, self.world, self.local, addr=addr, port=port))
                     c.set_timeout(min(30.0, comm_timeout_s()))
                     c.enable_ipc()
-                    ok = int(ipc_canary(c, self.rank, self.world))
+                    ok, report = c.canary()
+                    ok = int(ok)
+                    for rec in report:  # where the first wrong byte of each peer's segment came in
+                        print("IPC canary mismatch: %s" % json.dumps(rec), file=sys.stderr, flush=True)
                     c.set_timeout(comm_timeout_s())
                 except Exception as e:  # noqa: BLE001 — reported; every rank falls back together
                     print("IPC exchange unavailable on rank %d: %s" % (self.rank, e), file=sys.stderr, flush=True)
@@ -413,26 +416,6 @@ class Ctx:
         self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
         self.dist.all_reduce(tt, op=self.dist.ReduceOp.SUM)
         return float(mx[0]), float(tt[1])
-
-
-def ipc_canary(c, rank, world):
-    """One exchange through the IPC path with every segment size class (1 KiB .. 2.5 slots: the
-    multi-round path) and a per-(src, dst) byte pattern, checked on the device."""
-    import torch
-    slot = c.ipc_info()["slot_bytes"]
-    sizes = [1024, 5 * slot // 2 + 7, 4099, slot, 64 << 10, 3 * slot // 2, 17, 1 << 20]
-
-    def seg(src, dst):
-        n = sizes[(src * 3 + dst) % len(sizes)]
-        return (torch.arange(n, dtype=torch.int64, device="cuda") * (2 * src + 3) + 7 * dst).to(torch.uint8)
-    send = torch.cat([seg(rank, d) for d in range(world)])
-    want = torch.cat([seg(s_, rank) for s_ in range(world)])
-    recv = torch.zeros_like(want)
-    c.alltoallv(send, [sizes[(rank * 3 + d) % len(sizes)] for d in range(world)], recv,
-                [sizes[(s_ * 3 + rank) % len(sizes)] for s_ in range(world)])
-    torch.cuda.synchronize()
-    c.check()
-    return bool(torch.equal(recv, want))
 
 
 def exchange_block(xs, steps, step_s, world, note):

@@ -528,6 +528,12 @@ int swps_lr_train_batches(swps_lr *l, uint64_t count);
 int swps_lr_predict(swps_lr *l, float *pred_out, float *target_out, uint64_t cap);
 int swps_lr_params(swps_lr *l, uint32_t *keys, float *w, float *g2, uint64_t cap, uint64_t *n);
 int swps_lr_info(swps_lr *l, uint64_t *out4); /* nrows, nkeys, nbatches, nnz */
+/* the plan the step runs (after load): out5 = {plan running, plan asked for, fixed-point scale bits s,
+ * the floor s must reach, 1 when the fixed point (SWPS_LR_PLAN_NONE) was asked for and its scale
+ * fell below the floor — heavy-tailed x_i: the load then switched to SWPS_LR_PLAN_STEP (fp64 sums)}.
+ * Loads refuse non-finite labels or feature values with SWPS_E_CFG (lr.cpp:103-131 would train on
+ * them). */
+int swps_lr_plan_info(swps_lr *l, int32_t *out5);
 int swps_lr_sync(swps_lr *l);
 int swps_lr_set_profile(swps_lr *l, int32_t on); /* per-kernel HIP-event timing on/off (swps_lr_cfg.profile at create) */
 int swps_lr_kernel_times(swps_lr *l, double *out8, int32_t reset);

@@ -581,7 +581,7 @@ class LR:
         assert table.layout == "lr"
         plans = {"step": capi.LR_PLAN_STEP, "load": capi.LR_PLAN_LOAD, "none": capi.LR_PLAN_NONE}
         if plan not in plans:
-            raise ValueError("unknown plan %r (step or load)" % (plan,))
+            raise ValueError("unknown plan %r (step, load or none)" % (plan,))
         cfg = capi.LRCfg(minibatch, int(init_ref), int(profile), int(fast_sums), plans[plan])
         h = ctypes.c_void_p()
         check(capi.lib().swps_lr_create(table.h, ctypes.byref(cfg), ctypes.byref(h)))
@@ -600,6 +600,16 @@ class LR:
         out = np.zeros(4)
         check(capi.lib().swps_lr_exchange_stats(self.h, on, ptr(out)))
         return dict(zip(["bytes_remote", "bytes_total", "calls", "ms"], out.tolist()))
+
+    def plan_info(self):
+        """swps_lr_plan_info: the plan the step runs and the fixed point's scale against its floor
+        (fallback True: plan "none" was asked for, heavy-tailed x_i put the scale below the floor,
+        and the load switched to plan "step", fp64 sums)."""
+        o = np.zeros(5, dtype=np.int32)
+        check(capi.lib().swps_lr_plan_info(self.h, ptr(o)))
+        names = {0: "step", 1: "load", 2: "none"}
+        return {"plan": names.get(int(o[0]), int(o[0])), "plan_asked": names.get(int(o[1]), int(o[1])),
+                "fx_bits": int(o[2]), "fx_floor": int(o[3]), "fallback": bool(o[4])}
 
     def fx_bytes(self, batch):
         """The fixed-point step's algorithmic bytes on `batch` (swps_lr_fx_bytes): a dict with

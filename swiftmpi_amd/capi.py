@@ -180,6 +180,7 @@ PROTOS = {
     "swps_lr_predict": (ctypes.c_int, [_p, _p, _p, _u64]),
     "swps_lr_params": (ctypes.c_int, [_p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
     "swps_lr_info": (ctypes.c_int, [_p, _p]),
+    "swps_lr_plan_info": (ctypes.c_int, [_p, _p]),
     "swps_lr_sync": (ctypes.c_int, [_p]),
     "swps_lr_kernel_times": (ctypes.c_int, [_p, _p, _i32]),
     "swps_lr_set_profile": (ctypes.c_int, [_p, _i32]),

@@ -6,12 +6,16 @@ group (gloo: several ranks sharing one GPU in tests — RCCL refuses that).
 The library issues the exchanges itself (include/swps.h "communicator");
 this module only builds the handle."""
 import ctypes
+import os
 import traceback
 
 import numpy as np
 
 from . import capi
 from .capi import check
+
+IPC_CHANNELS = 8     # swps_comm.hip kIpcCh: workgroups per peer and direction
+IPC_MIN_PART = 4096  # swps_comm.hip kIpcMinPart: a segment's least per-channel part
 
 
 class Comm:
@@ -105,6 +109,62 @@ class Comm:
         s = (stream or torch.cuda.current_stream()).cuda_stream
         check(capi.lib().swps_comm_alltoallv(self.h, ctypes.c_void_p(send.data_ptr()), sb,
                                              ctypes.c_void_p(recv.data_ptr()), rb, ctypes.c_void_p(s)))
+
+    def canary(self):
+        """One IPC exchange with every segment size class (17 B .. 2.5 inbox slots: the multi-round
+        path) and a per-(source, destination) byte pattern, checked on the device.  Returns
+        (ok, report): report lists, per source rank whose segment arrived wrong, where — the peer,
+        the channel and round of the exchange that carried the first wrong byte, its byte offset in
+        that peer's segment and in the receive buffer, the 8-byte words expected and received there,
+        and the count of wrong bytes — so a cross-device ordering fault can be located from one
+        record.  SWPS_IPC_DIAG_CORRUPT=<rank>:<offset> flips the received byte at <offset> on rank
+        <rank> before the check (a test of this report)."""
+        import torch
+        slot = self.ipc_info()["slot_bytes"]
+        sizes = [1024, 5 * slot // 2 + 7, 4099, slot, 64 << 10, 3 * slot // 2, 17, 1 << 20]
+        rank, world = self.rank, self.world
+
+        def size(src, dst):
+            return sizes[(src * 3 + dst) % len(sizes)]
+
+        def seg(src, dst):
+            n = size(src, dst)
+            return (torch.arange(n, dtype=torch.int64, device="cuda") * (2 * src + 3) + 7 * dst).to(torch.uint8)
+        send = torch.cat([seg(rank, d) for d in range(world)])
+        want = torch.cat([seg(s_, rank) for s_ in range(world)])
+        recv = torch.zeros_like(want)
+        self.alltoallv(send, [size(rank, d) for d in range(world)], recv, [size(s_, rank) for s_ in range(world)])
+        torch.cuda.synchronize()
+        self.check()
+        inj = os.environ.get("SWPS_IPC_DIAG_CORRUPT")
+        if inj:
+            r_, o_ = (int(x) for x in inj.split(":"))
+            if r_ == rank:
+                recv[o_] ^= 0xFF
+        bad = recv != want
+        if not bool(bad.any()):
+            return True, []
+        report = []
+        sub = slot // IPC_CHANNELS
+        base = 0
+        for src in range(world):
+            n = size(src, rank)
+            b = bad[base:base + n]
+            if bool(b.any()):
+                off = int(torch.nonzero(b)[0])
+                # the channel / round that carried it: swps_comm.hip ipc_span's split of an n-byte
+                # segment into IPC_CHANNELS parts (16-B multiples, at least IPC_MIN_PART bytes),
+                # each part streamed through sub-slots of slot / IPC_CHANNELS bytes
+                part = max(IPC_MIN_PART, ((n + IPC_CHANNELS - 1) // IPC_CHANNELS + 15) & ~15)
+                ch = off // part
+                w0 = (base + off) & ~7
+                report.append({"rank": rank, "peer": src, "channel": ch, "round": (off - ch * part) // sub,
+                               "offset": off, "recv_offset": base + off, "segment_bytes": n,
+                               "bad_bytes": int(b.sum()),
+                               "expected": want[w0:w0 + 8].cpu().numpy().tobytes()[::-1].hex(),
+                               "got": recv[w0:w0 + 8].cpu().numpy().tobytes()[::-1].hex()})
+            base += n
+        return False, report
 
     def set_timeout(self, seconds):
         """Deadline for the communicator's initialisation and each exchange (RCCL guard)."""

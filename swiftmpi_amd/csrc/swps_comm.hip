@@ -109,6 +109,11 @@ struct swps_comm {
   std::unique_ptr<CommGuard> guard;  // RCCL, world > 1
   std::unique_ptr<IpcState> ipc;  // swps_comm_enable_ipc
   HostStage stage;  // swps_comm_alltoallv over a host transport
+  // swps_comm_alltoallv called with the null stream on an RCCL communicator: the exchange runs on
+  // this non-blocking stream instead, ordered after and before the null stream by two events (an
+  // RCCL communicator never sees the null stream)
+  hipStream_t nstream = nullptr;
+  hipEvent_t nev_in = nullptr, nev_out = nullptr;
 };
 
 namespace {
@@ -470,6 +475,17 @@ struct TcpStar {
 };
 
 namespace {
+// the TCP transport's receive deadline: set it to ms (< 0: leave it); the previous value (-1 when the
+// communicator has no TCP transport)
+int tcp_timeout(swps_comm *c, int ms) {
+  if (!c->tcp) return -1;
+  const int old = c->tcp->timeout_ms;
+  if (ms >= 0) c->tcp->timeout_ms = ms;
+  return old;
+}
+}  // namespace
+
+namespace {
 
 int star_allgather(void *ctx, const void *in, void *out, uint64_t bytes) {
   TcpStar *t = (TcpStar *)ctx;
@@ -724,6 +740,8 @@ int ipc_alltoallv(swps_comm *c, const void *d_send, const uint64_t *sb, const ui
                   const uint64_t *rb, const uint64_t *ro, hipStream_t s) {
   IpcState &p = *c->ipc;
   SWPS_TRY(comm_aborted(c));
+  // argument errors first: the round counters below must advance on every rank or on none
+  if (sb[c->rank] != rb[c->rank]) return fail(SWPS_E_STATE, "IPC exchange: own segment sizes differ");
   IpcArgs a{};
   const int W = c->world;
   for (int r = 0; r < W; r++) {
@@ -744,7 +762,6 @@ int ipc_alltoallv(swps_comm *c, const void *d_send, const uint64_t *sb, const ui
     }
     if (r != c->rank) p.bytes_remote += sb[r];
   }
-  if (sb[c->rank] != rb[c->rank]) return fail(SWPS_E_STATE, "IPC exchange: own segment sizes differ");
   a.send = (const char *)d_send;
   a.recv = (char *)d_recv;
   a.slot = p.slot;
@@ -1073,18 +1090,28 @@ int swps_comm_destroy(swps_comm *c) {
   if (!c) return SWPS_OK;
   (void)hipSetDevice(c->device);
   if (IpcState *p = c->ipc.get(); p && c->world > 1) {
-    // peers store into this rank's inbox / ctrl words until their last exchange has retired: wait
-    // for every rank's device (an all-gather behind a device sync) unless the communicator is dead
-    uint64_t dead = 1;  // set by a rank that gave up on an exchange: its peers skip the barrier
-    const bool ok = hipDeviceSynchronize() == hipSuccess && comm_aborted(c) == SWPS_OK &&
-                    hipMemcpy(&dead, (uint64_t *)p->ctrl + kIpcDead, 8, hipMemcpyDeviceToHost) == hipSuccess &&
-                    dead == 0;
+    // peers store into this rank's inbox / ctrl words until their last exchange has retired: every
+    // rank syncs its device and then joins one all-gather of its status (the dead word) — also a
+    // rank that gave up on an exchange, so a peer whose exchanges all completed never waits alone.
+    // The all-gather is bounded by a short deadline (a peer whose process is gone costs that, not
+    // the communicator's full timeout); a communicator already aborted cannot join it.
+    uint64_t dead = 1;
+    if (hipDeviceSynchronize() == hipSuccess)
+      (void)hipMemcpy(&dead, (uint64_t *)p->ctrl + kIpcDead, 8, hipMemcpyDeviceToHost);
+    (void)hipGetLastError();
     hipStream_t hs = nullptr;
-    if (ok && hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) == hipSuccess) {
+    if (comm_aborted(c) == SWPS_OK && hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) == hipSuccess) {
+      const double t_keep = c->timeout_s;
+      const int tcp_keep = tcp_timeout(c, -1);
+      const double t_short = std::min(t_keep, 10.0);
+      c->timeout_s = t_short;
+      (void)tcp_timeout(c, (int)(t_short * 1000));
       std::vector<int64_t> all(c->world);
-      const int64_t one = 1;
-      (void)comm_allgather(c, &one, all.data(), 8, hs);
+      const int64_t st = (int64_t)dead;
+      (void)comm_allgather(c, &st, all.data(), 8, hs);
       (void)hipStreamDestroy(hs);
+      c->timeout_s = t_keep;
+      (void)tcp_timeout(c, tcp_keep);
     }
     for (int r = 0; r < c->world; r++)
       if (r != c->rank) {
@@ -1097,6 +1124,9 @@ int swps_comm_destroy(swps_comm *c) {
     if (p->last) (void)hipEventDestroy(p->last);
     c->ipc.reset();
   }
+  if (c->nstream) (void)hipStreamDestroy(c->nstream);
+  if (c->nev_in) (void)hipEventDestroy(c->nev_in);
+  if (c->nev_out) (void)hipEventDestroy(c->nev_out);
   if (CommGuard *g = c->guard.get()) {
     {
       std::lock_guard<std::mutex> lk(g->mu);
@@ -1193,36 +1223,62 @@ int swps_comm_enable_ipc(swps_comm *c, uint64_t slot_bytes) {
       (void)hipGetLastError();
       return fail(SWPS_E_RCCL, "IPC exchange: " + why);
     };
+    // collective from here on: a rank whose own setup fails still joins the handle all-gather (with
+    // ok = 0), and the handles' opens are confirmed by a second all-gather, so every rank enables
+    // the exchange or every rank undoes it — none waits alone in a collective the others left
+    std::string why;
+    hipIpcMemHandle_t mh[2];
     if (hipExtMallocWithFlags(&p->inbox, (size_t)W * 2 * p->slot, hipDeviceMallocUncached) != hipSuccess ||
         hipExtMallocWithFlags(&p->ctrl, kIpcCtrlBytes, hipDeviceMallocUncached) != hipSuccess)
-      return undo("uncached allocation failed");
-    if (hipMemset(p->ctrl, 0, kIpcCtrlBytes) != hipSuccess ||
-        hipHostMalloc((void **)&p->err_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-      return undo("control words");
-    *p->err_host = 0;
-    if (hipHostGetDevicePointer((void **)&p->err_dev, p->err_host, 0) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess)
-      return undo("error word");
-    hipIpcMemHandle_t mine[2], all[2 * kIpcMaxWorld];
-    if (hipIpcGetMemHandle(&mine[0], p->inbox) != hipSuccess || hipIpcGetMemHandle(&mine[1], p->ctrl) != hipSuccess)
-      return undo("hipIpcGetMemHandle failed");
+      why = "uncached allocation failed";
+    else if (hipMemset(p->ctrl, 0, kIpcCtrlBytes) != hipSuccess ||
+             hipHostMalloc((void **)&p->err_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      why = "control words";
+    else if ((*p->err_host = 0, hipHostGetDevicePointer((void **)&p->err_dev, p->err_host, 0) != hipSuccess) ||
+             hipDeviceSynchronize() != hipSuccess)
+      why = "error word";
+    else if (hipIpcGetMemHandle(&mh[0], p->inbox) != hipSuccess || hipIpcGetMemHandle(&mh[1], p->ctrl) != hipSuccess)
+      why = "hipIpcGetMemHandle failed";
+    (void)hipGetLastError();
+    struct Hdr {
+      int64_t ok;
+      hipIpcMemHandle_t h[2];
+    } mine{}, all[kIpcMaxWorld];
+    mine.ok = why.empty() ? 1 : 0;
+    if (mine.ok) {
+      mine.h[0] = mh[0];
+      mine.h[1] = mh[1];
+    }
     // every rank's ctrl words are zero before its handles leave it, so a peer's first store lands after
     hipStream_t hs = nullptr;
     if (hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) != hipSuccess) return undo("stream");
-    const int ag = comm_allgather(c, mine, all, sizeof(mine), hs);
-    (void)hipStreamDestroy(hs);
-    if (ag != SWPS_OK) return undo("handle all-gather failed");
-    for (int r = 0; r < W; r++) {
+    if (comm_allgather(c, &mine, all, sizeof(Hdr), hs) != SWPS_OK) {
+      (void)hipStreamDestroy(hs);
+      return undo("handle all-gather failed");
+    }
+    for (int r = 0; r < W; r++)
+      if (!all[r].ok) {
+        (void)hipStreamDestroy(hs);
+        return undo(r == c->rank ? why : "rank " + std::to_string(r) + " could not set up its buffers");
+      }
+    for (int r = 0; r < W && why.empty(); r++) {
       if (r == c->rank) {
         p->peer_inbox[r] = p->inbox;
         p->peer_ctrl[r] = p->ctrl;
         continue;
       }
-      if (hipIpcOpenMemHandle(&p->peer_inbox[r], all[2 * r], hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
-          hipIpcOpenMemHandle(&p->peer_ctrl[r], all[2 * r + 1], hipIpcMemLazyEnablePeerAccess) != hipSuccess)
-        return undo("hipIpcOpenMemHandle of rank " + std::to_string(r) + "'s buffers failed");
+      if (hipIpcOpenMemHandle(&p->peer_inbox[r], all[r].h[0], hipIpcMemLazyEnablePeerAccess) != hipSuccess ||
+          hipIpcOpenMemHandle(&p->peer_ctrl[r], all[r].h[1], hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+        why = "hipIpcOpenMemHandle of rank " + std::to_string(r) + "'s buffers failed";
     }
-    SWPS_HIP(hipEventCreateWithFlags(&p->last, hipEventDisableTiming));
+    (void)hipGetLastError();
+    int64_t opened = why.empty() ? 1 : 0, okv[kIpcMaxWorld];
+    const int ag2 = comm_allgather(c, &opened, okv, 8, hs);
+    (void)hipStreamDestroy(hs);
+    if (ag2 != SWPS_OK) return undo("open confirmation all-gather failed");
+    for (int r = 0; r < W; r++)
+      if (!okv[r]) return undo(r == c->rank ? why : "rank " + std::to_string(r) + " could not map its peers' buffers");
+    if (hipEventCreateWithFlags(&p->last, hipEventDisableTiming) != hipSuccess) return undo("event");
   }
   c->ipc = std::move(p);
   return SWPS_OK;
@@ -1233,7 +1289,21 @@ int swps_comm_alltoallv(swps_comm *c, const void *d_send, const uint64_t *send_b
   if (!c || !send_bytes || !recv_bytes) return fail(SWPS_E_CFG, "null argument");
   SWPS_HIP(hipSetDevice(c->device));
   const std::vector<uint64_t> sb(send_bytes, send_bytes + c->world), rb(recv_bytes, recv_bytes + c->world);
-  return comm_alltoallv(c, d_send, sb, d_recv, rb, (hipStream_t)stream, c->stage, "all-to-all-v");
+  hipStream_t s = (hipStream_t)stream;
+  if (!s && c->rccl && c->world > 1) {  // an RCCL communicator never sees the null stream
+    if (!c->nstream) {
+      SWPS_HIP(hipStreamCreateWithFlags(&c->nstream, hipStreamNonBlocking));
+      SWPS_HIP(hipEventCreateWithFlags(&c->nev_in, hipEventDisableTiming));
+      SWPS_HIP(hipEventCreateWithFlags(&c->nev_out, hipEventDisableTiming));
+    }
+    SWPS_HIP(hipEventRecord(c->nev_in, nullptr));
+    SWPS_HIP(hipStreamWaitEvent(c->nstream, c->nev_in, 0));
+    SWPS_TRY(comm_alltoallv(c, d_send, sb, d_recv, rb, c->nstream, c->stage, "all-to-all-v"));
+    SWPS_HIP(hipEventRecord(c->nev_out, c->nstream));
+    SWPS_HIP(hipStreamWaitEvent(nullptr, c->nev_out, 0));
+    return SWPS_OK;
+  }
+  return comm_alltoallv(c, d_send, sb, d_recv, rb, s, c->stage, "all-to-all-v");
 }
 
 int swps_comm_ipc_info(swps_comm *c, uint64_t *out4) {

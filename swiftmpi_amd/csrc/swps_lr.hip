@@ -1667,8 +1667,12 @@ __global__ __launch_bounds__(256) void k_lr_fx_apply(const uint32_t *__restrict_
 //   columns of the partial matrix and apply theirs.  Integer sums: the result is the atomic form's,
 //   bit for bit, whatever the order.
 constexpr int kLrFxVB = 12;
+// the fill counters are packed [group][bucket]: one wave's reservations (consecutive buckets) are
+// 64 consecutive words — a few 128-B requests at the memory side, not 64 (scattered returning
+// atomics run ~17x slower per byte: MI355X_MICROARCH.md, Global float atomics)
+constexpr uint32_t kLrFxMaxGBits = 3;      // at most 8 chunk groups per bucket region
 constexpr uint32_t kLrFxMaxBk = 4096;  // buckets (V <= 2^24); beyond it the atomic form runs
-template <int RPT, int NT, bool AFF, int HC>
+template <int RPT, int NT, bool AFF, int HC, bool RES>
 __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ chunks, uint32_t nchunks,
                                                      const uint64_t *__restrict__ row_off,
                                                      const int32_t *__restrict__ fvid,
@@ -1680,8 +1684,18 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
                                                      uint32_t nbk, uint2 *__restrict__ rec, uint16_t *__restrict__ boff,
                                                      uint32_t bstride,
                                                      unsigned long long *__restrict__ hsum,
-                                                     uint32_t *__restrict__ hcnt, uint32_t row_base, uint32_t diag) {
+                                                     uint32_t *__restrict__ hcnt, uint32_t row_base,
+                                                     uint32_t *__restrict__ fill, const uint32_t *__restrict__ rbase,
+                                                     uint32_t gbits, uint32_t diag) {
   constexpr int CAP = RPT * NT;
+  // RES (the bucket regions): bucket q's records of the whole batch go to 2^gbits sub-regions of
+  // rec, one per chunk group g = chunk % 2^gbits: [rbase[q << gbits | g], rbase[(q << gbits | g) + 1])
+  // (sized at load for any batch), each chunk reserving its span there with one returning atomic on
+  // fill[g * nbk + q] — issued as soon as the chunk's bucket counts are known,
+  // waited for only at the record writes (the forward hides it), and spread over the groups' words
+  // (a word takes about 88 returning atomics per us).  The records of a bucket land in an order that
+  // varies run to run; their sums are exact integers, so the results do not (k_lr_fxb_push reads
+  // the sub-regions as contiguous runs).
   __shared__ float prod[CAP];
   __shared__ uint16_t rl[CAP];
   __shared__ float es[CAP];
@@ -1741,6 +1755,15 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
       const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
       w[k] = i >= n ? 0.f : (code[k] & kLrHotBit) ? wh[code[k] & (kLrHotBit - 1)] : rows[(uint64_t)code[k] * 2];
     }
+    uint32_t rk[RES ? RPT : 1];  // RES: each non-hot record's rank inside its bucket in this chunk
+    if constexpr (RES) {
+#pragma unroll
+      for (int k = 0; k < RPT; k++) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
+        const bool hot = AFF ? (uint32_t)f[k] < nhot : (code[k] & kLrHotBit) != 0;
+        rk[k] = (i < n && !hot) ? atomicAdd(&bc[(uint32_t)f[k] >> kLrFxVB], 1u) : 0u;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
       const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
@@ -1751,14 +1774,41 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
       for (uint64_t c = a; c < b; c++) rl[c - c0] = (uint16_t)r;
     }
     __syncthreads();
+    constexpr int RQ = RES ? 2 : 1;  // RES: the chunk's span in each bucket's region (the atomics'
+    uint32_t res[RQ], rbq[RQ];       // results wait in registers until the record writes)
+    if constexpr (RES) {
+      const uint32_t g = cix & ((1u << gbits) - 1u);
+#pragma unroll
+      for (int j = 0; j < RQ; j++) {
+        const uint32_t q = (uint32_t)tid + (uint32_t)(j * NT), qg = (q << gbits) | g;
+        const uint32_t c = q < nbk ? bc[q] : 0u;
+        rbq[j] = q < nbk ? rbase[qg] : 0u;
+        res[j] = c && !(diag & 256u) ? atomicAdd(&fill[(uint64_t)g * nbk + q], c) : 0u;
+      }
+      for (uint32_t q = (uint32_t)tid + (uint32_t)(RQ * NT); q < nbk; q += (uint32_t)NT) {  // beyond 2 per thread
+        const uint32_t c = bc[q], qg = (q << gbits) | g;
+        bc[q] = rbase[qg] + (c ? atomicAdd(&fill[(uint64_t)g * nbk + q], c) : 0u);
+      }
+    }
     for (uint32_t r = (uint32_t)tid; r < ch.y; r += (uint32_t)NT) {  // lr.cpp:358-367, in feature order
       if (r >= (uint32_t)NT) {
         ra = row_off[rf + r];
         rb = row_off[rf + r + 1];
         y = label[rf + r];
       }
+      // the products added one by one in feature order (the reference's fp32 `sum += w*x`); their LDS
+      // loads go out 8 at a time so the chain waits on the adds, not on one load per feature
       float sum = 0.f;
-      for (uint32_t c = (uint32_t)(ra - c0); c < (uint32_t)(rb - c0); c++) sum += prod[c];
+      uint32_t c = (uint32_t)(ra - c0);
+      const uint32_t ce = (uint32_t)(rb - c0);
+      for (; c + 8 <= ce; c += 8) {
+        float pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) pv[u] = prod[c + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) sum += pv[u];
+      }
+      for (; c < ce; c++) sum += prod[c];
       const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
       const float error = y - predict;
       err[rf + r] = error;
@@ -1783,12 +1833,20 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
           }
         } else {
           prod[i] = g;
-          rl[i] = (diag & 128u) ? (uint16_t)0 : (uint16_t)atomicAdd(&bc[(uint32_t)f[k] >> kLrFxVB], 1u);
+          if constexpr (!RES)
+            rl[i] = (diag & 128u) ? (uint16_t)0 : (uint16_t)atomicAdd(&bc[(uint32_t)f[k] >> kLrFxVB], 1u);
         }
       }
     }
+    if constexpr (RES) {  // each bucket's first slot of this chunk's span
+#pragma unroll
+      for (int j = 0; j < RQ; j++) {
+        const uint32_t q = (uint32_t)tid + (uint32_t)(j * NT);
+        if (q < nbk) bc[q] = rbq[j] + res[j];
+      }
+    }
     __syncthreads();
-    if (tid < 64 && !(diag & 128u)) {  // one wave: exclusive scan of the bucket counts, the chunk's offsets
+    if (!RES && tid < 64 && !(diag & 128u)) {  // one wave: exclusive scan of the bucket counts, the chunk's offsets
       const uint32_t per = (nbk + 63u) / 64u, b0 = (uint32_t)tid * per, b1 = min(nbk, b0 + per);
       uint32_t s = 0;
       for (uint32_t q = b0; q < b1; q++) s += bc[q];
@@ -1807,14 +1865,15 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
       }
       if (tid == 63) boff[(uint64_t)nbk * bstride + cix] = (uint16_t)inc;
     }
-    __syncthreads();
-    const uint64_t base = c0 - z0;
+    if constexpr (!RES) __syncthreads();
+    const uint64_t base = RES ? 0 : c0 - z0;
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
       const uint32_t i = (uint32_t)tid + (uint32_t)k * (uint32_t)NT;
       const bool hot = AFF ? (uint32_t)f[k] < nhot : (code[k] & kLrHotBit) != 0;
       if (i < n && !hot && !(diag & 4u))
-        rec[base + bc[(uint32_t)f[k] >> kLrFxVB] + rl[i]] = make_uint2((uint32_t)f[k], __float_as_uint(prod[i]));
+        rec[base + bc[(uint32_t)f[k] >> kLrFxVB] + (RES ? rk[k] : (uint32_t)rl[i])] =
+            make_uint2((uint32_t)f[k], __float_as_uint(prod[i]));
     }
     __syncthreads();  // bc / es / rl are the next chunk's
   }
@@ -1823,6 +1882,178 @@ __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ ch
     unsigned long long *hsr = hsum + (uint64_t)blockIdx.x * nhot;
     uint32_t *hcr = hcnt + (uint64_t)blockIdx.x * nhot;
     for (uint32_t q = (uint32_t)tid; q < nhot; q += (uint32_t)NT) {
+      hsr[q] = hs[q];
+      hcr[q] = hc[q];
+    }
+  }
+}
+
+// k_lr_fxr_step: k_lr_fxb_step's work for the bench's form (rows placed by fid, bucket regions),
+// written without per-record branches so every per-record LDS / memory step of a thread goes out
+// as one batch.  A record past the chunk's end, and for the bucket count a hot record, is a dummy:
+// its LDS updates land in one of 32 spare slots (lane-spread, never read) and its record is not
+// written.  Same products, same ordered row sums, same integer terms: bit-identical to
+// k_lr_fxb_step (test_lr_fixed_point_step).
+constexpr uint32_t kLrFxDummy = 32;
+template <int RPT, int NT, int HC>
+__global__ __launch_bounds__(NT) void k_lr_fxr_step(const uint2 *__restrict__ chunks, uint32_t nchunks,
+                                                     const uint64_t *__restrict__ row_off,
+                                                     const int32_t *__restrict__ ffid, const float *__restrict__ fval,
+                                                     const float *__restrict__ label, uint64_t r0,
+                                                     const float *__restrict__ rows, uint32_t nhot,
+                                                     float *__restrict__ err, float *__restrict__ err2, double scale,
+                                                     uint32_t nbk, uint2 *__restrict__ rec,
+                                                     unsigned long long *__restrict__ hsum,
+                                                     uint32_t *__restrict__ hcnt, uint32_t row_base,
+                                                     uint32_t *__restrict__ fill, const uint32_t *__restrict__ rbase,
+                                                     uint32_t gbits, uint32_t diag) {
+  constexpr int CAP = RPT * NT;
+  __shared__ float prod[CAP];
+  __shared__ uint16_t rl[CAP];
+  __shared__ float es[CAP];
+  __shared__ float wh[HC];
+  __shared__ unsigned long long hs[HC + kLrFxDummy];
+  __shared__ uint32_t hc[HC + kLrFxDummy];
+  extern __shared__ uint32_t bc[];  // [nbk + kLrFxDummy]: dynamic
+  const uint32_t tid = threadIdx.x, dum = tid & (kLrFxDummy - 1u);
+  constexpr int HPT = (HC + NT - 1) / NT;
+  float hv[HPT];
+#pragma unroll
+  for (int j = 0; j < HPT; j++) {
+    const uint32_t q = tid + (uint32_t)(NT * j);
+    hv[j] = q < nhot ? rows[(uint64_t)(row_base + q) * 2] : 0.f;
+  }
+  for (uint32_t q = tid; q < (uint32_t)HC + kLrFxDummy; q += (uint32_t)NT) {
+    hs[q] = 0ull;
+    hc[q] = 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < HPT; j++) {
+    const uint32_t q = tid + (uint32_t)(NT * j);
+    if (q < (uint32_t)HC) wh[q] = hv[j];
+  }
+  const uint32_t gmask = (1u << gbits) - 1u;
+  for (uint32_t cix = blockIdx.x; cix < nchunks; cix += gridDim.x) {
+    const uint2 ch = chunks[cix];
+    const uint64_t rf = r0 + ch.x;
+    const uint64_t c0 = row_off[rf], c1 = row_off[rf + ch.y];
+    const uint32_t n = (uint32_t)(c1 - c0);
+    int32_t f[RPT];
+    float x[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {  // past the end: the chunk's last record, x = 0
+      const uint32_t i = tid + (uint32_t)k * (uint32_t)NT;
+      const uint64_t c = c0 + min(i, n - 1u);
+      f[k] = ffid[c];
+      x[k] = fval[c];
+    }
+    uint64_t ra = 0, rb = 0;
+    float y = 0.f;
+    if (tid < ch.y) {
+      ra = row_off[rf + tid];
+      rb = row_off[rf + tid + 1];
+      y = label[rf + tid];
+    }
+    for (uint32_t q = tid; q < nbk + kLrFxDummy; q += (uint32_t)NT) bc[q] = 0u;
+    __syncthreads();  // bc zeroed, wh stored (first chunk), the previous chunk's LDS reads done
+    // the non-hot records' ranks in their buckets (hot records and the dummies: spare slots) and
+    // the weights: hot from LDS, the others gathered (a hot / dummy record loads row row_base)
+    uint32_t rk[RPT];
+    float w[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = tid + (uint32_t)k * (uint32_t)NT;
+      const bool cold = i < n && (uint32_t)f[k] >= nhot;
+      const uint32_t fk = (uint32_t)f[k];
+      rk[k] = atomicAdd(&bc[cold ? (fk >> kLrFxVB) : nbk + dum], 1u);
+      const float g = rows[(uint64_t)(row_base + (cold ? fk : 0u)) * 2];
+      const float h = wh[fk < nhot ? fk : 0u];
+      w[k] = fk < nhot ? h : g;
+    }
+    __syncthreads();  // the chunk's bucket counts
+    // its span in each bucket's region: a returning atomic per bucket, waited for at the record
+    // writes (the forward runs meanwhile)
+    constexpr int RQ = 2;
+    uint32_t res[RQ], rbq[RQ];
+    const uint32_t grp = cix & gmask;
+#pragma unroll
+    for (int j = 0; j < RQ; j++) {
+      const uint32_t q = tid + (uint32_t)(j * NT), qg = (q << gbits) | grp;
+      const uint32_t c = q < nbk ? bc[q] : 0u;
+      rbq[j] = q < nbk ? rbase[qg] : 0u;
+      res[j] = c && !(diag & 256u) ? atomicAdd(&fill[(uint64_t)grp * nbk + q], c) : 0u;
+    }
+    for (uint32_t q = tid + (uint32_t)(RQ * NT); q < nbk; q += (uint32_t)NT) {  // beyond 2 per thread
+      const uint32_t c = bc[q], qg = (q << gbits) | grp;
+      bc[q] = rbase[qg] + (c ? atomicAdd(&fill[(uint64_t)grp * nbk + q], c) : 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; k++) prod[tid + (uint32_t)k * (uint32_t)NT] = w[k] * x[k];
+    for (uint32_t r = tid; r < ch.y; r += (uint32_t)NT) {
+      const uint64_t a = r < (uint32_t)NT ? ra : row_off[rf + r], b = r < (uint32_t)NT ? rb : row_off[rf + r + 1];
+      for (uint64_t c = a; c < b; c++) rl[c - c0] = (uint16_t)r;
+    }
+    __syncthreads();
+    for (uint32_t r = tid; r < ch.y; r += (uint32_t)NT) {  // lr.cpp:358-367, in feature order
+      if (r >= (uint32_t)NT) {
+        ra = row_off[rf + r];
+        rb = row_off[rf + r + 1];
+        y = label[rf + r];
+      }
+      float sum = 0.f;
+      uint32_t c = (uint32_t)(ra - c0);
+      const uint32_t ce = (uint32_t)(rb - c0);
+      for (; c + 8 <= ce; c += 8) {
+        float pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) pv[u] = prod[c + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) sum += pv[u];
+      }
+      for (; c < ce; c++) sum += prod[c];
+      const float predict = (float)(1. / (1. + (double)(float)exp((double)(-sum))));
+      const float error = y - predict;
+      err[rf + r] = error;
+      err2[rf + r] = error * error;
+      es[r] = error;
+    }
+    __syncthreads();
+    // every record's term g = e * x_i (lr.cpp:368): a hot key's into its LDS sum, the others into
+    // prod (their record); the dummies' (x = 0) and the non-hot records' LDS adds go to spare slots
+    uint16_t rr[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) rr[k] = rl[tid + (uint32_t)k * (uint32_t)NT];
+    float ev[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) ev[k] = es[rr[k] & (CAP - 1)];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = tid + (uint32_t)k * (uint32_t)NT;
+      const float g = ev[k] * x[k];
+      const bool hot = i < n && (uint32_t)f[k] < nhot;
+      const uint32_t h = hot ? (uint32_t)f[k] : (uint32_t)HC + dum;
+      atomicAdd(&hs[h], (unsigned long long)__double2ll_rn((double)g * scale));
+      atomicAdd(&hc[h], 1u);
+      prod[i] = g;
+    }
+#pragma unroll
+    for (int j = 0; j < RQ; j++) {  // the spans' first slots
+      const uint32_t q = tid + (uint32_t)(j * NT);
+      if (q < nbk) bc[q] = rbq[j] + res[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+      const uint32_t i = tid + (uint32_t)k * (uint32_t)NT;
+      if (i < n && (uint32_t)f[k] >= nhot && !(diag & 4u))
+        rec[bc[(uint32_t)f[k] >> kLrFxVB] + rk[k]] = make_uint2((uint32_t)f[k], __float_as_uint(prod[i]));
+    }
+    __syncthreads();  // bc / es / rl are the next chunk's
+  }
+  if (nhot && !(diag & 8u)) {
+    unsigned long long *hsr = hsum + (uint64_t)blockIdx.x * nhot;
+    uint32_t *hcr = hcnt + (uint64_t)blockIdx.x * nhot;
+    for (uint32_t q = tid; q < nhot; q += (uint32_t)NT) {
       hsr[q] = hs[q];
       hcr[q] = hc[q];
     }
@@ -1844,7 +2075,7 @@ constexpr uint32_t kLrFxbHotK = 16;     // hot keys per k_lr_fxb_push block (64 
 // TO_GRADS (the sharded learner, swps_lr_step): no AdaGrad here — each present key's mean goes to
 // the push payload, rows[vid_row[fid]] (vid_row = the batch's key positions by fid, rows = the
 // payload; hrow[q] = q); the owners apply it (swps_lr_serve_push)
-template <bool TO_GRADS>
+template <bool TO_GRADS, bool RES>
 __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__restrict__ rec,
                                                              const uint16_t *__restrict__ boff,
                                                              const uint32_t *__restrict__ chunk_c0, uint32_t nchunks,
@@ -1856,14 +2087,109 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
                                                              float *__restrict__ rows, float lr, float fudge,
                                                              double scale, double inv_scale, uint32_t aff,
                                                              uint32_t row_base, uint32_t first_block,
-                                                             uint32_t diag) {
+                                                             uint32_t bper, uint32_t *__restrict__ fill,
+                                                             const uint32_t *__restrict__ rbase, uint32_t nkeys,
+                                                             uint32_t gbits, uint32_t diag) {
   constexpr uint32_t T = 1u << kLrFxVB, NT = kLrFxbPushT, PER = T / NT;
   __shared__ unsigned long long as[T];
   __shared__ uint32_t ac[T];
   extern __shared__ uint32_t dyn_lds[];  // bucket blocks: 2 * nchunks + 1 words
   const uint32_t tid = threadIdx.x, bid = blockIdx.x + first_block;
-  if (bid < nbk) {
-    const uint32_t b = bid;
+  // bper > 0: the bucket blocks dealt XCD-contiguous — blocks are dealt round-robin over the 8 XCDs,
+  // so block i (on XCD i % 8) takes bucket (i % 8) * bper + i / 8 and each XCD owns a run of
+  // neighbouring buckets: the 128-B lines a chunk's neighbouring bucket segments share are read
+  // through one L2 (speed only; any placement gives the same sums)
+  const uint32_t nbb = bper ? 8u * bper : nbk;
+  if (bid < nbb) {
+    const uint32_t b = bper ? (bid & 7u) * bper + (bid >> 3) : bid;
+    if (b >= nbk) return;
+    if constexpr (RES) {
+      // the bucket's records are one contiguous run of rec; its rows one contiguous run of the
+      // table (affine form): their loads go out first, beside the count, so the row updates need no
+      // further round trip
+      constexpr uint32_t GM = 1u << kLrFxMaxGBits;
+      __shared__ uint32_t sR[GM], sB[GM];
+      const uint32_t G = 1u << gbits;
+      if (tid < G) {  // the groups' counts, and the counters' reset for the next step (in order per thread)
+        const uint64_t qg = ((uint64_t)b << gbits) | tid;
+        const uint32_t r0 = fill[(uint64_t)tid * nbk + b];
+        sR[tid] = (diag & 32u) ? 0u : r0;
+        sB[tid] = rbase[qg];
+        fill[(uint64_t)tid * nbk + b] = 0u;
+      }
+      const bool pre = !TO_GRADS && aff;
+      float2 wg[PER];
+#pragma unroll
+      for (uint32_t k = 0; k < PER; k++) {
+        const uint32_t v = (b << kLrFxVB) + tid + k * NT;
+        wg[k] = pre && v < nkeys ? *reinterpret_cast<const float2 *>(rows + (uint64_t)(row_base + v) * 2)
+                                 : make_float2(0.f, 0.f);
+      }
+      for (uint32_t v = tid; v < T; v += NT) {
+        as[v] = 0ull;
+        ac[v] = 0u;
+      }
+      __syncthreads();
+      uint32_t gp[GM + 1], gb[GM];  // the groups' runs as one list: prefix of their counts
+      gp[0] = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < GM; g++) {
+        gp[g + 1] = gp[g] + (g < G ? sR[g] : 0u);
+        gb[g] = g < G ? sB[g] : 0u;
+      }
+      const uint32_t R = gp[GM];
+      for (uint32_t j0 = tid; j0 < R; j0 += 4 * NT) {
+        uint2 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t j = j0 + (uint32_t)k * NT;
+          if (j < R) {
+            uint32_t a = gb[0] + j;
+#pragma unroll
+            for (uint32_t g = 1; g < GM; g++)
+              if (j >= gp[g]) a = gb[g] + (j - gp[g]);
+            r[k] = rec[a];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (j0 + (uint32_t)k * NT < R) {
+            atomicAdd(&as[r[k].x & (T - 1)], (unsigned long long)__double2ll_rn((double)__uint_as_float(r[k].y) * scale));
+            atomicAdd(&ac[r[k].x & (T - 1)], 1u);
+          }
+      }
+      __syncthreads();
+      if (diag & 16u) return;
+      if (TO_GRADS) {
+#pragma unroll
+        for (uint32_t k = 0; k < PER; k++) {
+          const uint32_t v = tid + k * NT, c = ac[v];
+          if (c) rows[vid_row[(b << kLrFxVB) + v]] = (float)(((double)(long long)as[v] * inv_scale) / (double)c);
+        }
+        return;
+      }
+      uint32_t c[PER], row[PER];
+#pragma unroll
+      for (uint32_t k = 0; k < PER; k++) {
+        c[k] = ac[tid + k * NT];
+        if (c[k] && !pre) row[k] = vid_row[(b << kLrFxVB) + tid + k * NT];
+      }
+      if (!pre) {
+#pragma unroll
+        for (uint32_t k = 0; k < PER; k++)
+          if (c[k]) wg[k] = *reinterpret_cast<const float2 *>(rows + (uint64_t)row[k] * 2);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < PER; k++)
+        if (c[k]) {  // lr.cpp:32-38, 68-75 (k_lr_fx_apply's rule)
+          const float m = (float)(((double)(long long)as[tid + k * NT] * inv_scale) / (double)c[k]);
+          const float ng2 = wg[k].y + m * m;
+          const float step = lr * m;
+          const uint64_t rr = pre ? (uint64_t)row_base + (b << kLrFxVB) + tid + k * NT : row[k];
+          *reinterpret_cast<float2 *>(rows + rr * 2) = make_float2(wg[k].x + step / sqrtf(ng2 + fudge), ng2);
+        }
+      return;
+    }
     for (uint32_t v = tid; v < T; v += NT) {
       as[v] = 0ull;
       ac[v] = 0u;
@@ -1959,7 +2285,7 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
   // kLrFxbHotK hot keys per block: the other threads' row groups sum each key's column of the step's
   // block partials, then the groups' sums are added in LDS
   constexpr uint32_t KPB = kLrFxbHotK, RG = NT / KPB;
-  const uint32_t h0 = (bid - nbk) * KPB, kk = tid % KPB, rg = tid / KPB;
+  const uint32_t h0 = (bid - nbb) * KPB, kk = tid % KPB, rg = tid / KPB;
   const uint32_t h = h0 + kk;
   unsigned long long s = 0ull;
   uint32_t c = 0u;
@@ -2235,13 +2561,22 @@ struct swps_lr {
   // the fixed-point step (cfg.plan == SWPS_LR_PLAN_NONE): per-key codes, hot keys, accumulators
   bool fx_ready = false;
   int fx_bits = 40;                      // fixed-point scale 2^fx_bits (load: no sum can reach 2^62)
+  int fx_floor = 0;                      // the least fx_bits the fixed point runs at (lr_ingest)
+  bool fx_fallback = false;              // the fixed point was asked for, fx_bits fell below the floor
+  int32_t plan_req = 0;                  // the caller's plan (cfg.plan is the one running)
   std::vector<uint32_t> fx_hot_vids;     // the corpus's most frequent keys (load)
   swps::DevMem d_vcode, d_fx_hot, d_fx_hrow, d_acc_sum, d_acc_cnt, d_fx_list, d_fx_n, d_fx_stamp;
   // the bucketed form (k_lr_fxb_step / k_lr_fxb_push; SWPS_LR_FX_ATOMIC=1 runs the atomic one)
   swps::DevMem d_fchunk_c0;              // each chunk's first record, relative to its batch's first
   swps::DevMem d_fxb_rec, d_fxb_boff, d_fxb_hsum, d_fxb_hcnt;
+  swps::DevMem d_fxb_fill, d_fxb_rbase;  // the bucket regions (fxb_res): fill counters, region starts
+  bool fxb_res = true;                   // SWPS_LR_FXB_RES=0: the per-chunk bucket segments (round 5)
+  bool fxr = true;                       // k_lr_fxr_step (SWPS_LR_FXR=0: k_lr_fxb_step<..., RES>)
+  uint32_t fxb_gbits = 0;                // chunk groups per bucket region: 2^fxb_gbits
+  uint64_t fxb_region_recs = 0;          // the regions' total capacity (records)
   int fx_atomic = 0;
   uint32_t fxb_grid = 768, fxb_nbk = 0, fxb_diag = 0;
+  bool fxb_xcd = true;  // k_lr_fxb_push's bucket blocks XCD-contiguous (SWPS_LR_FXB_XCD=0: in order)
   int fx_nt = 256;  // the fixed-point step's threads per block at 4,096-record chunks (SWPS_LR_FX_NT)
   // fid: the fixed-point step's key numbering — hot keys first (rank), then the rest in row-placement
   // order; swps_lr_init places the rows in fid order, so a key's shard row is fx_row_base + fid
@@ -2680,9 +3015,53 @@ struct LoadTimer {
   }
 };
 
+// every label and feature value finite (lr.cpp:103-131 parses "nan" / "inf" with %f and trains on
+// them silently; here they are refused at load: they would make every sum they reach — and the
+// fixed-point scale, from max |x_i| — undefined).  Threads over slices of the values.
+int lr_check_finite(const swps_lr *l) {
+  for (uint64_t r = 0; r < l->label.size(); r++)
+    if (!std::isfinite(l->label[r])) return fail(SWPS_E_CFG, "non-finite label at row " + std::to_string(r));
+  const uint64_t nf = l->fval.size();
+  const int nth = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, nf >> 22));
+  std::vector<uint64_t> bad(nth, ~0ull);
+  std::vector<std::thread> th;
+  for (int q = 0; q < nth; q++)
+    th.emplace_back([&, q] {
+      for (uint64_t i = nf * q / nth; i < nf * (q + 1) / nth; i++)
+        if (!std::isfinite(l->fval[i])) {
+          bad[q] = i;
+          return;
+        }
+    });
+  for (auto &t : th) t.join();
+  for (uint64_t b : bad)
+    if (b != ~0ull) {
+      const uint64_t row = (uint64_t)(std::upper_bound(l->row_off.begin(), l->row_off.end(), b) - l->row_off.begin()) - 1;
+      return fail(SWPS_E_CFG, "non-finite feature value at record " + std::to_string(b) + " (row " +
+                                  std::to_string(row) + ")");
+    }
+  return SWPS_OK;
+}
+
+// the 1st percentile of |x_i| over the nonzero values (a deterministic sample of at most 2^20 of them)
+double lr_small_abs_x(const swps_lr *l) {
+  const uint64_t nf = l->fval.size(), step = std::max<uint64_t>(1, nf >> 20);
+  std::vector<float> a;
+  a.reserve(nf / step + 1);
+  for (uint64_t i = 0; i < nf; i += step)
+    if (l->fval[i] != 0.f) a.push_back(std::fabs(l->fval[i]));
+  if (a.empty()) return 0.0;
+  std::nth_element(a.begin(), a.begin() + a.size() / 100, a.end());
+  return a[a.size() / 100];
+}
+
 // feat: the caller's array of every record's key (read during this call only)
 int lr_ingest(swps_lr *l, const uint32_t *feat, uint64_t nfeat) {
   LoadTimer phase;
+  SWPS_TRY(lr_check_finite(l));
+  l->cfg.plan = l->plan_req;  // a reload decides the fixed point's floor again
+  l->fx_fallback = false;
+  l->fx_floor = 0;
   SWPS_TRY(lr_vocab(l, feat, nfeat));
   phase("vocabulary (GPU sort)");
   const uint64_t nr = l->label.size();
@@ -2757,6 +3136,20 @@ int lr_ingest(swps_lr *l, const uint32_t *feat, uint64_t nfeat) {
     for (float v : l->label) my = std::max(my, std::fabs(v));
     const double bound = std::max(1e-30, ((double)my + 1.0) * (double)mx * (double)std::max<uint64_t>(l->max_bnnz, 1));
     l->fx_bits = (int)std::min(40.0, std::floor(62.0 - std::log2(bound)));
+    // the floor: a term e * x_i is rounded to a multiple of 2^-s, so the quantum must stay below
+    // 1e-7 of a small term — |e| = 0.5 times the 1st percentile of |x_i| — as fp32's own rounding
+    // of such a term (2^-24 relative) would.  Heavy-tailed values (|x_i| from 1e-4 to 1e6) push s
+    // down past it (s = 26 against a floor of 38 there; Criteo's shape: 39 against 30); then the
+    // step runs the fp64-sum path (plan step) instead, and swps_lr_plan_info says so.
+    const double small = lr_small_abs_x(l);
+    l->fx_floor = small > 0 ? (int)std::ceil(std::log2(1.0 / (1e-7 * 0.5 * small))) : 0;
+    if (getenv("SWPS_LR_FX_FLOOR")) l->fx_floor = atoi(getenv("SWPS_LR_FX_FLOOR"));  // tests: force it
+    if (l->fx_bits < l->fx_floor) {
+      l->fx_fallback = true;
+      l->cfg.plan = SWPS_LR_PLAN_STEP;
+    }
+  }
+  if (l->cfg.plan == SWPS_LR_PLAN_NONE && l->cfg.fast_sums) {
     const std::vector<uint32_t> &cnt = l->vocab_cnt;
     std::vector<uint32_t> ord;
     for (uint32_t v = 0; v < cnt.size(); v++)
@@ -2889,6 +3282,7 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
     l->fx_atomic = ea && atoi(ea) != 0;
     if (const char *eg = getenv("SWPS_LR_FXB_GRID")) l->fxb_grid = (uint32_t)std::max(1, atoi(eg));
     if (const char *ed = getenv("SWPS_LR_FXB_DIAG")) l->fxb_diag = (uint32_t)atoi(ed);
+    if (const char *ex = getenv("SWPS_LR_FXB_XCD")) l->fxb_xcd = atoi(ex) != 0;
     if (const char *en = getenv("SWPS_LR_FX_NT")) l->fx_nt = atoi(en) == 512 ? 512 : 256;
     l->fxb_nbk = (uint32_t)((V + (1u << kLrFxVB) - 1) >> kLrFxVB);
     if (l->fxb_nbk > kLrFxMaxBk || (2 * l->max_bchunks + 1) * 4 > 96 * 1024) l->fx_atomic = 1;  // LDS bounds
@@ -2927,6 +3321,55 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
         l->fx_affine = true;
         l->fx_row_base = base;
       }
+    }
+    if (const char *er = getenv("SWPS_LR_FXB_RES")) l->fxb_res = atoi(er) != 0;
+    if (const char *er = getenv("SWPS_LR_FXR")) l->fxr = atoi(er) != 0;
+    if (!l->fx_atomic && l->fxb_res) {
+      // the bucket regions: bucket q's region holds any batch's records of its keys — at most the
+      // batch's records, and at most the corpus count of its non-hot keys
+      const std::vector<uint32_t> &cnt = l->vocab_cnt;
+      std::vector<uint8_t> ishot(V, 0);
+      if (hot)
+        for (uint32_t q = 0; q < nh; q++) ishot[l->fx_hot_vids[q]] = 1;
+      std::vector<uint64_t> bsum(l->fxb_nbk, 0);
+      for (uint64_t v = 0; v < l->vocab_keys.size(); v++)
+        if (!ishot[v]) {
+          const uint64_t key = l->fx_affine ? l->fx_fid[v] : v;
+          bsum[key >> kLrFxVB] += cnt[v];
+        }
+      // 2^gbits chunk groups per bucket (chunk % 2^gbits), each its own sub-region and counter: a
+      // group's sub-region also holds at most its chunks' records.  The most groups whose regions
+      // stay within 2^31 records and 4 GB (SWPS_LR_FXB_GBITS caps it)
+      const uint64_t chunk_rec = (uint64_t)l->fwd_rpt * 256;
+      int gmax = (int)kLrFxMaxGBits;
+      if (const char *eg = getenv("SWPS_LR_FXB_GBITS")) gmax = std::min(std::max(atoi(eg), 0), gmax);
+      std::vector<uint32_t> rb;
+      uint64_t tot = ~0ull;
+      for (int gb = gmax; gb >= 0; gb--) {
+        const uint64_t G = 1ull << gb, grp = ((l->max_bchunks + G - 1) / G) * chunk_rec;
+        rb.assign(((uint64_t)l->fxb_nbk << gb) + 1, 0);
+        tot = 0;
+        for (uint64_t qg = 0; qg < ((uint64_t)l->fxb_nbk << gb) && tot < (1ull << 31); qg++) {
+          rb[qg] = (uint32_t)tot;
+          tot += std::min<uint64_t>(std::min<uint64_t>(bsum[qg >> gb], l->max_bnnz), grp);
+        }
+        l->fxb_gbits = (uint32_t)gb;
+        if (tot < (1ull << 31) && (tot * 8 <= (4ull << 30) || gb == 0)) break;
+      }
+      if (tot < (1ull << 31)) {
+        const uint64_t nqg = (uint64_t)l->fxb_nbk << l->fxb_gbits;
+        rb[nqg] = (uint32_t)tot;
+        SWPS_TRY(upload(l->d_fxb_rbase, rb, s));
+        SWPS_TRY(l->d_fxb_fill.ensure(nqg * 4));
+        SWPS_HIP(hipMemsetAsync(l->d_fxb_fill.p, 0, nqg * 4, s));
+        SWPS_TRY(l->d_fxb_rec.ensure(std::max<uint64_t>(tot, 1) * 8));
+        l->fxb_region_recs = tot;
+        SWPS_HIP(hipStreamSynchronize(s));  // rb
+      } else {
+        l->fxb_res = false;
+      }
+    } else {
+      l->fxb_res = false;
     }
     if (!l->fx_atomic) {
       SWPS_TRY(l->d_fxb_rec.ensure(std::max<uint64_t>(l->max_bnnz, 1) * 8));
@@ -2968,16 +3411,41 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
     hipEvent_t fb = l->timer.ext(), fe = l->timer.ext();
     const size_t dyn = (size_t)l->fxb_nbk * 4;
     // chunks of 4,096 records: 512 threads x 8 (default) or 256 x 16; of 2,048: 256 x 8
-    const int nt = l->fwd_rpt == 16 && l->fx_nt == 512 ? 512 : 256, rpt = nt == 512 ? 8 : l->fwd_rpt;
-    auto *kern = nt == 512 ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, 512, true, 512> : k_lr_fxb_step<8, 512, false, 512>)
-                                        : (l->fx_affine ? k_lr_fxb_step<8, 512, true, kLrHot>
-                                                        : k_lr_fxb_step<8, 512, false, kLrHot>))
-                 : rpt == 16 ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<16, 256, true, 512>
-                                                          : k_lr_fxb_step<16, 256, false, 512>)
-                                          : (l->fx_affine ? k_lr_fxb_step<16, 256, true, kLrHot>
-                                                          : k_lr_fxb_step<16, 256, false, kLrHot>))
-                 : (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, 256, true, 512> : k_lr_fxb_step<8, 256, false, 512>)
-                              : (l->fx_affine ? k_lr_fxb_step<8, 256, true, kLrHot> : k_lr_fxb_step<8, 256, false, kLrHot>));
+    const bool res = l->fxb_res;
+    const int nt = l->fwd_rpt == 16 && l->fx_nt == 512 && !res ? 512 : 256, rpt = nt == 512 ? 8 : l->fwd_rpt;
+    auto *kern = res ? (rpt == 16 ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<16, 256, true, 512, true>
+                                                               : k_lr_fxb_step<16, 256, false, 512, true>)
+                                               : (l->fx_affine ? k_lr_fxb_step<16, 256, true, kLrHot, true>
+                                                               : k_lr_fxb_step<16, 256, false, kLrHot, true>))
+                                  : (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, 256, true, 512, true>
+                                                               : k_lr_fxb_step<8, 256, false, 512, true>)
+                                               : (l->fx_affine ? k_lr_fxb_step<8, 256, true, kLrHot, true>
+                                                               : k_lr_fxb_step<8, 256, false, kLrHot, true>)))
+                 : nt == 512 ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, 512, true, 512, false>
+                                                          : k_lr_fxb_step<8, 512, false, 512, false>)
+                                          : (l->fx_affine ? k_lr_fxb_step<8, 512, true, kLrHot, false>
+                                                          : k_lr_fxb_step<8, 512, false, kLrHot, false>))
+                 : rpt == 16 ? (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<16, 256, true, 512, false>
+                                                          : k_lr_fxb_step<16, 256, false, 512, false>)
+                                          : (l->fx_affine ? k_lr_fxb_step<16, 256, true, kLrHot, false>
+                                                          : k_lr_fxb_step<16, 256, false, kLrHot, false>))
+                 : (nh <= 512 ? (l->fx_affine ? k_lr_fxb_step<8, 256, true, 512, false>
+                                              : k_lr_fxb_step<8, 256, false, 512, false>)
+                              : (l->fx_affine ? k_lr_fxb_step<8, 256, true, kLrHot, false>
+                                              : k_lr_fxb_step<8, 256, false, kLrHot, false>));
+    if (res && l->fx_affine && l->fxr) {  // the branch-free form (bit-identical)
+      auto *kr = rpt == 16 ? (nh <= 512 ? k_lr_fxr_step<16, 256, 512> : k_lr_fxr_step<16, 256, kLrHot>)
+                           : (nh <= 512 ? k_lr_fxr_step<8, 256, 512> : k_lr_fxr_step<8, 256, kLrHot>);
+      hipExtLaunchKernelGGL(kr, dim3(grid), dim3(256), (size_t)(l->fxb_nbk + kLrFxDummy) * 4, s, fb, fe, 0,
+                            (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
+                            (const uint64_t *)l->d_row_off.as<uint64_t>(), (const int32_t *)l->d_ffid.as<int32_t>(),
+                            (const float *)l->d_fval.as<float>(), (const float *)l->d_label.as<float>(), r0,
+                            (const float *)(shd ? l->d_wcache2.as<float>() : l->t->rows.as<float>()),
+                            hot ? nh : 0u, l->d_err.as<float>(), l->d_err2.as<float>(), scale, l->fxb_nbk,
+                            l->d_fxb_rec.as<uint2>(), l->d_fxb_hsum.as<unsigned long long>(),
+                            l->d_fxb_hcnt.as<uint32_t>(), l->fx_row_base, l->d_fxb_fill.as<uint32_t>(),
+                            (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), l->fxb_gbits, l->fxb_diag);
+    } else
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(nt), dyn, s, fb, fe, 0,
                           (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
                           (const uint64_t *)l->d_row_off.as<uint64_t>(),
@@ -2988,16 +3456,19 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
                           hot ? (const uint32_t *)l->d_fx_hrow.as<uint32_t>() : (const uint32_t *)nullptr, nh,
                           l->d_err.as<float>(), l->d_err2.as<float>(), scale, l->fxb_nbk, l->d_fxb_rec.as<uint2>(),
                           l->d_fxb_boff.as<uint16_t>(), (uint32_t)l->max_bchunks, l->d_fxb_hsum.as<unsigned long long>(),
-                          l->d_fxb_hcnt.as<uint32_t>(), l->fx_row_base, l->fxb_diag);
+                          l->d_fxb_hcnt.as<uint32_t>(), l->fx_row_base, l->d_fxb_fill.as<uint32_t>(),
+                          (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), l->fxb_gbits, l->fxb_diag);
     l->timer.ext_end(0, fb, fe);
     hipEvent_t ab = l->timer.ext(), ae = l->timer.ext();
     // SWPS_LR_FXB_DIAG (timing experiments only; results wrong): 1 buckets only, 2 hot keys only,
     // 4 no record scatter, 8 no hot partials, 16 buckets without the row updates, 32 buckets
-    // without their records, 64 no hot-key LDS sums, 128 no bucket sort
-    const uint32_t pb0 = (l->fxb_diag & 2u) ? l->fxb_nbk : 0u,
-                   pb1 = (l->fxb_diag & 1u) ? l->fxb_nbk : l->fxb_nbk + (nh + kLrFxbHotK - 1) / kLrFxbHotK;
-    hipExtLaunchKernelGGL(shd ? k_lr_fxb_push<true> : k_lr_fxb_push<false>, dim3(std::max(1u, pb1 - pb0)),
-                          dim3(kLrFxbPushT), (2 * nfc + 1) * 4, s, ab,
+    // without their records, 64 no hot-key LDS sums, 128 no bucket sort, 256 no region reservation
+    const uint32_t bper = l->fxb_xcd ? (l->fxb_nbk + 7u) / 8u : 0u, nbb = bper ? 8u * bper : l->fxb_nbk;
+    const uint32_t pb0 = (l->fxb_diag & 2u) ? nbb : 0u,
+                   pb1 = (l->fxb_diag & 1u) ? nbb : nbb + (nh + kLrFxbHotK - 1) / kLrFxbHotK;
+    hipExtLaunchKernelGGL(shd ? (res ? k_lr_fxb_push<true, true> : k_lr_fxb_push<true, false>)
+                              : (res ? k_lr_fxb_push<false, true> : k_lr_fxb_push<false, false>),
+                          dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), res ? 0 : (2 * nfc + 1) * 4, s, ab,
                           ae, 0,
                           (const uint2 *)l->d_fxb_rec.as<uint2>(), (const uint16_t *)l->d_fxb_boff.as<uint16_t>(),
                           (const uint32_t *)l->d_fchunk_c0.as<uint32_t>() + l->bfchunk[bi], (uint32_t)nfc, l->fxb_nbk,
@@ -3007,7 +3478,9 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
                           (const uint32_t *)l->d_fxb_hcnt.as<uint32_t>(), grid,
                           (const uint32_t *)l->d_fx_hrow.as<uint32_t>(), nh, shd ? d_grads : l->t->rows.as<float>(),
                           l->t->cfg.learning_rate, l->t->cfg.fudge, scale, std::ldexp(1.0, -l->fx_bits),
-                          (uint32_t)l->fx_affine, l->fx_row_base, pb0, l->fxb_diag);
+                          (uint32_t)l->fx_affine, l->fx_row_base, pb0, bper, l->d_fxb_fill.as<uint32_t>(),
+                          (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), (uint32_t)l->vocab_keys.size(),
+                          l->fxb_gbits, l->fxb_diag);
     SWPS_HIP(hipGetLastError());
     l->timer.ext_end(3, ab, ae);
     return SWPS_OK;
@@ -3529,6 +4002,7 @@ int swps_lr_create(swps_table *t, const swps_lr_cfg *cfg, swps_lr **out) {
   swps_lr *l = new swps_lr();
   l->t = t;
   l->cfg = *cfg;
+  l->plan_req = cfg->plan;
   l->s = t->stream;
   l->timer.on = cfg->profile != 0;
   if (const char *e = getenv("SWPS_LR_PACK")) l->rows_per_wave = atoi(e);  // A/B timing, tests
@@ -3800,6 +4274,15 @@ int swps_lr_params(swps_lr *l, uint32_t *keys, float *w, float *g2, uint64_t cap
   return SWPS_OK;
 }
 
+int swps_lr_plan_info(swps_lr *l, int32_t *o) {
+  o[0] = l->cfg.plan;
+  o[1] = l->plan_req;
+  o[2] = l->fx_bits;
+  o[3] = l->fx_floor;
+  o[4] = l->fx_fallback ? 1 : 0;
+  return SWPS_OK;
+}
+
 int swps_lr_info(swps_lr *l, uint64_t *o) {
   o[0] = l->label.size();
   o[1] = l->vocab_keys.size();
@@ -4067,10 +4550,12 @@ int swps_lr_fx_bytes(swps_lr *l, uint64_t batch, uint64_t *out8) {
   }
   // step: per record its fid, x_i and weight (12 B), per row its offset, label, e, e^2 (20 B), per
   // non-hot record its (fid, e*x_i) written (8 B), the chunks' bucket offsets, the hot partials
-  out8[0] = 12 * nnz + 20 * nrows + 8 * nonhot + 2 * (nbk + 1) * nch + 12 * nh * grid;
+  // (the bucket regions, fxb_res: no offsets — each chunk's span comes from an atomic per bucket)
+  const uint64_t offs = l->fxb_res ? 0 : 2 * (nbk + 1) * nch;
+  out8[0] = 12 * nnz + 20 * nrows + 8 * nonhot + offs + 12 * nh * grid;
   // push: the records and offsets read back, each distinct non-hot key's [w | g2] read and written,
   // the hot partials read, the hot keys' rows read and written
-  out8[1] = 8 * nonhot + 2 * (nbk + 1) * nch + 16 * uniq + 12 * nh * grid + 16 * nh;
+  out8[1] = 8 * nonhot + offs + 16 * uniq + 12 * nh * grid + 16 * nh;
   out8[2] = 1;
   out8[3] = nh;
   out8[4] = nbk;

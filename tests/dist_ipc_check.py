@@ -11,7 +11,9 @@ two ranks on one GPU (same-device IPC):
   3. the per-exchange latency of a small exchange (the LR step's size class) over both, printed
      as one JSON line ("IPC_LAT {...}");
   4. a lost peer: a lone exchange fails within its deadline, naming the peer, and the peer's next
-     exchange fails at once.
+     exchange fails at once; closing the communicator afterwards takes seconds on every rank.
+  (2c: two ranks pushing the same keys to one owner in a step, fixed point vs fp64 sums; 3b: the
+  bench's canary and its mismatch report, on an injected wrong byte.)
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
         --master-port 29571 tests/dist_ipc_check.py --tcp-port 29581
@@ -162,6 +164,31 @@ def main():
                 n += 1
         assert n == len(owned), (n, len(owned))
         print("lr fixed point sharded ok: %d keys" % n, flush=True)
+    # 2c. shared keys: both ranks' rows draw from one key space, so in one step two
+    # learners push the same key to its owner (the N > 1 LR leg's case).  The sharded fixed-point
+    # step (plan none) must equal itself over TCP and IPC bit for bit, and the sharded fp64-sum step
+    # (plan load, fast sums) within 1e-6 relative — the single-GPU bar between the two sum forms
+    y, off, f, v = criteo(3000 + 500 * rank, seed=70 + rank, bits=13)
+    res = {}
+    for name, comm, plan in (("tcp", tcp, "none"), ("ipc", ipc, "none"), ("load", ipc, "load")):
+        t = sw.Table("lr", **lk)
+        m = sw.LR(t, minibatch=255, init_ref=False, fast_sums=True, plan=plan)
+        m.load_csr(y, off, f, v)
+        m.shard_comm(comm, frag_num=2000)
+        m.init()
+        m.train(2)
+        k = np.sort(t.keys())
+        res[name] = (k, t.export(torch.as_tensor(k.astype(np.int64), device="cuda")).cpu().numpy())
+        m.close()
+        t.close()
+    assert np.array_equal(res["tcp"][0], res["ipc"][0]) and np.array_equal(res["tcp"][1], res["ipc"][1])
+    assert np.array_equal(res["ipc"][0], res["load"][0])
+    a_, b_ = res["ipc"][1].astype(np.float64), res["load"][1].astype(np.float64)
+    assert np.abs(a_ - b_).max() <= 1e-6 * np.abs(b_).max(), (np.abs(a_ - b_).max(), np.abs(b_).max())
+    shared = [None] * world
+    dist.all_gather_object(shared, set(np.unique(f).tolist()))
+    print("rank %d lr shared keys ok: %d keys owned, %d keys in both ranks' data" %
+          (rank, len(res["ipc"][0]), len(shared[0] & shared[1 % world])), flush=True)
     path = corpus(os.path.join(tmp, "c%d.txt" % rank), rank)
     kw = dict(window=4, negative=4, minibatch=19, sample=1e-3, unigram_size=10 ** 6, fp64_intermediates=False)
     res = {}
@@ -192,6 +219,23 @@ def main():
         print("IPC_LAT " + json.dumps({"world": world, "same_gpu": True, "slot_bytes": slot, "latency": lat,
                                        "ipc_exchanges": info["exchanges"], "ipc_bytes_remote": info["bytes_remote"]}),
               flush=True)
+    # 3b. the canary (bench.py's gate for the IPC path) passes, and a wrong byte injected on rank
+    # world - 1 at offset 5000 of the receive buffer (inside rank 0's segment, whose first part is
+    # 1 KiB .. 2.5 slots) is reported with the peer, the channel / round and the offset
+    ok, rep = ipc.canary()
+    assert ok and not rep, rep
+    os.environ["SWPS_IPC_DIAG_CORRUPT"] = "%d:%d" % (world - 1, 5000)
+    ok, rep = ipc.canary()
+    del os.environ["SWPS_IPC_DIAG_CORRUPT"]
+    if rank == world - 1:
+        assert not ok and len(rep) == 1, rep
+        r0 = rep[0]
+        assert r0["peer"] == 0 and r0["recv_offset"] == 5000 and r0["offset"] == 5000 and r0["bad_bytes"] == 1, r0
+        assert r0["expected"] != r0["got"] and r0["channel"] >= 0 and r0["round"] >= 0, r0
+        print("rank %d canary report ok: %s" % (rank, json.dumps(r0)), flush=True)
+    else:
+        assert ok and not rep, rep
+    ipc.check()
     # 4. a lost peer: rank 0 exchanges alone (rank 1 never joins) and must fail within its 2-s
     # deadline; its give-up marks every rank dead, so rank 1's next exchange fails at once
     from swiftmpi_amd.capi import SwpsError
@@ -224,7 +268,10 @@ def main():
         assert time.perf_counter() - t0 < 10
         print("rank %d dead peer detected: ok" % rank, flush=True)
     dist.barrier()
-    ipc.close()  # neither rank waits for the other here (both saw the dead word)
+    t0 = time.perf_counter()
+    ipc.close()  # collective: every rank joins one bounded all-gather, also after a dead exchange
+    assert time.perf_counter() - t0 < 15, time.perf_counter() - t0
+    print("rank %d close after a dead exchange: %.2f s" % (rank, time.perf_counter() - t0), flush=True)
     tcp.close()
     dist.barrier()
     if rank == 0:

@@ -610,10 +610,20 @@ def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
     vals = rng.random(int(roff[-1])).astype(np.float32)
     yl = (rng.random(4000) < 0.5).astype(np.float32)
     res = []
-    for plan, atomic, affine in (("load", "0", "1"), ("none", "0", "1"), ("none", "0", "1"), ("none", "1", "1"),
-                                 ("none", "0", "0")):
+    # (plan, atomic form, rows placed by fid, bucket regions: SWPS_LR_FXB_RES=0 is round 5's per-chunk
+    # bucket segments)
+    # bucket regions, chunk groups per region: SWPS_LR_FXB_GBITS; the branch-free step kernel
+    # k_lr_fxr_step, SWPS_LR_FXR=0: k_lr_fxb_step)
+    for plan, atomic, affine, bres, gbits, fxr in (
+            ("load", "0", "1", "1", "3", "1"), ("none", "0", "1", "1", "3", "1"), ("none", "0", "1", "1", "3", "1"),
+            ("none", "1", "1", "1", "3", "1"), ("none", "0", "0", "1", "3", "1"), ("none", "0", "1", "0", "3", "1"),
+            ("none", "0", "0", "0", "3", "1"), ("none", "0", "1", "1", "0", "1"), ("none", "0", "0", "1", "1", "1"),
+            ("none", "0", "1", "1", "3", "0")):
         monkeypatch.setenv("SWPS_LR_FX_ATOMIC", atomic)
         monkeypatch.setenv("SWPS_LR_FX_AFFINE", affine)
+        monkeypatch.setenv("SWPS_LR_FXB_RES", bres)
+        monkeypatch.setenv("SWPS_LR_FXB_GBITS", gbits)
+        monkeypatch.setenv("SWPS_LR_FXR", fxr)
         out = []
         for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
             t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
@@ -624,14 +634,102 @@ def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
             m.close()
             t.close()
         res.append(out)
-    for a, b, c, d in zip(res[1], res[2], res[3], res[4]):  # run to run; bucketed = atomic = gathered codes
-        assert np.array_equal(a, b)
-        assert np.array_equal(a, c)
-        assert np.array_equal(a, d)
+    for a, *others in zip(*res[1:]):  # run to run; bucketed = atomic = gathered codes = segments
+        for b in others:
+            assert np.array_equal(a, b)
     for a, b in zip(res[0], res[1]):
         a = np.asarray(a, dtype=np.float64)
         b = np.asarray(b, dtype=np.float64)
         assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max(), (np.abs(a - b).max(), np.abs(a).max())
+
+
+def _libsvm_heavy_tailed(path, rows=4000, keys=3000, seed=12):
+    """libsvm-style rows (lr.cpp:103-131's text format): 5-30 Zipf-drawn keys per row, values
+    log-uniform over 1e-4 .. 1e6 (ten decades, as unscaled counts and amounts sit in real
+    libsvm data), random labels."""
+    rng = np.random.default_rng(seed)
+    p = 1.0 / np.arange(1, keys + 1)
+    p /= p.sum()
+    with open(path, "w") as fh:
+        for _ in range(rows):
+            n = int(rng.integers(5, 31))
+            fs = rng.choice(keys, n, p=p)
+            vs = (10.0 ** rng.uniform(-4, 6, n)).astype(np.float32)
+            fh.write("%d %s\n" % (int(rng.random() < 0.5), " ".join("%d:%.9g" % (a, b) for a, b in zip(fs, vs))))
+    return path
+
+
+def test_lr_heavy_tailed_values_fall_back_to_fp64_sums(lib, oracle_mod, gpu, tmp_path):
+    """Verdict r05 item 4: the fixed-point step (plan none) sizes its scale 2^s so no sum can
+    overflow (s = 62 - log2((max|y| + 1) * max|x_i| * batch records)); heavy-tailed x_i push s so
+    low that small terms e * x_i would round away.  The load then switches to the fp64-sum path
+    (plan step) and says so (swps_lr_plan_info), and training stays within 1e-5 of the oracle's
+    fp64-sum variant after 2 epochs (weights, AdaGrad sums, epoch errors) — where forcing the fixed
+    point on the same data (floor 0) does not."""
+    path = _libsvm_heavy_tailed(str(tmp_path / "heavy.txt"))
+    o64 = oracle_mod.LR(path, 999, 0.05, sum_f64=True)
+    e_64 = o64.train(2)
+    k64, w64, g64 = o64.params()
+    t = lib.Table("lr", capacity=1 << 14, dtype="f32", learning_rate=0.05)
+    m = lib.LR(t, minibatch=999, fast_sums=True, plan="none")
+    m.load_text(path)
+    pi = m.plan_info()
+    assert pi["fallback"] and pi["plan"] == "step" and pi["plan_asked"] == "none", pi
+    assert pi["fx_bits"] < pi["fx_floor"], pi
+    m.init()
+    e_g = m.train(2)
+    kg, wg, gg = m.params()
+    m.close()
+    t.close()
+    assert np.array_equal(k64, kg)
+    assert np.allclose(wg, w64, rtol=1e-5, atol=1e-6), np.abs(wg - w64).max()
+    assert np.allclose(gg, g64, rtol=1e-5, atol=1e-7), np.abs(gg - g64).max()
+    assert np.allclose(e_g, e_64, rtol=1e-5)
+
+
+def test_lr_criteo_keeps_the_fixed_point(lib, gpu):
+    """The floor does not trip on the bench's Criteo shape (values in (0, 1]): plan none runs."""
+    from swiftmpi_amd.synth import criteo
+    y, off, f, v = criteo(20000, seed=7)
+    t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
+    m = lib.LR(t, minibatch=4095, init_ref=False, fast_sums=True, plan="none")
+    m.load_csr(y, off, f, v)
+    pi = m.plan_info()
+    m.close()
+    t.close()
+    assert not pi["fallback"] and pi["plan"] == "none" and pi["fx_bits"] >= pi["fx_floor"], pi
+
+
+@pytest.mark.parametrize("where", ["value_text", "value_csr", "label_csr"])
+def test_lr_nonfinite_input_fails_loudly(lib, gpu, tmp_path, where):
+    """A NaN / inf feature value or label is refused at load with SWPS_E_CFG naming where it is
+    (the reference's parse_instance2 reads "nan" with %f and trains on it silently)."""
+    t = lib.Table("lr", capacity=4096, dtype="f32", learning_rate=0.05)
+    m = lib.LR(t, minibatch=10, fast_sums=True, plan="none")
+    try:
+        if where == "value_text":
+            path = str(tmp_path / "nan.txt")
+            with open(path, "w") as fh:
+                fh.write("1 3:0.5 7:1\n0 3:nan 9:1\n1 2:1\n")
+            with pytest.raises(lib.SwpsError) as ei:
+                m.load_text(path)
+            assert "record 2" in str(ei.value) and "row 1" in str(ei.value), str(ei.value)
+        else:
+            y = np.array([1, 0, 1], dtype=np.float32)
+            off = np.array([0, 2, 4, 5], dtype=np.uint64)
+            f = np.array([3, 7, 3, 9, 2], dtype=np.uint32)
+            v = np.array([0.5, 1, 1, 1, 1], dtype=np.float32)
+            if where == "value_csr":
+                v[4] = np.inf
+            else:
+                y[2] = np.nan
+            with pytest.raises(lib.SwpsError) as ei:
+                m.load_csr(y, off, f, v)
+            assert ei.value.code == -5, ei.value.code  # SWPS_E_CFG
+            assert ("record 4" if where == "value_csr" else "label at row 2") in str(ei.value), str(ei.value)
+    finally:
+        m.close()
+        t.close()
 
 
 def test_lr_config3_full_rank_share(lib, gpu):
