@@ -474,6 +474,13 @@ int swps_s2v_load_text(swps_s2v *s, const char *path);
 int swps_s2v_shard(swps_s2v *s, int32_t rank, int32_t world, int32_t frag_num);
 int swps_s2v_load_tokens(swps_s2v *s, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,
                          uint64_t nlines, const uint64_t *sent_ids);
+/* Sent2Vec::train (sent2vec.cpp:95-103) as the reference runs it: ONE pass that loads and trains —
+ * each minibatch's vocabulary, unigram run starts, pull and rand() bookkeeping are built on host
+ * threads while the GPU trains the minibatches before it (groups of 2, 4, then 8).  Returns after
+ * the pass (synced); the same results as swps_s2v_load_tokens + swps_s2v_train, bit for bit.  The
+ * arrays are read during the call only; no table call may run concurrently. */
+int swps_s2v_run_tokens(swps_s2v *s, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,
+                        uint64_t nlines, const uint64_t *sent_ids);
 /* nlines, sentences, minibatches, tokens, inserted keys, max sentences per
  * minibatch, max records per minibatch, rand() calls, LCG state at the end */
 int swps_s2v_info(swps_s2v *s, uint64_t *out9);

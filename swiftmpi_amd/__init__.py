@@ -513,6 +513,18 @@ class Sent2Vec:
         check(capi.lib().swps_s2v_load_tokens(self.h, ptr(tok_keys), len(tok_keys), ptr(line_off),
                                                len(line_off) - 1, ptr(sent_ids)))
 
+    def run_tokens(self, tok_keys, line_off, sent_ids):
+        """The reference's single pass (Sent2Vec::train, sent2vec.cpp:95-103): load and train every
+        minibatch once, the host's per-minibatch work overlapped with the GPU's training
+        (swps_s2v_run_tokens; = load_tokens + train bit for bit)."""
+        self._create()
+        tok_keys = np.ascontiguousarray(tok_keys, dtype=np.uint64)
+        line_off = np.ascontiguousarray(line_off, dtype=np.uint64)
+        sent_ids = np.ascontiguousarray(sent_ids, dtype=np.uint64)
+        assert len(sent_ids) == len(line_off) - 1
+        check(capi.lib().swps_s2v_run_tokens(self.h, ptr(tok_keys), len(tok_keys), ptr(line_off),
+                                              len(line_off) - 1, ptr(sent_ids)))
+
     def shard(self, rank, world, frag_num=1000):
         """Keep only the documents BasicHashFrag assigns to `rank` (call before
         loading; config 5's doc-sharded layout, no exchange)."""

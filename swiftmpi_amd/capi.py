@@ -160,6 +160,7 @@ PROTOS = {
     "swps_s2v_load_text": (ctypes.c_int, [_p, ctypes.c_char_p]),
     "swps_s2v_shard": (ctypes.c_int, [_p, _i32, _i32, _i32]),
     "swps_s2v_load_tokens": (ctypes.c_int, [_p, _p, _u64, _p, _u64, _p]),
+    "swps_s2v_run_tokens": (ctypes.c_int, [_p, _p, _u64, _p, _u64, _p]),
     "swps_s2v_info": (ctypes.c_int, [_p, _p]),
     "swps_s2v_train_batches": (ctypes.c_int, [_p, _u64]),
     "swps_s2v_train": (ctypes.c_int, [_p]),

@@ -1670,7 +1670,7 @@ constexpr int kLrFxVB = 12;
 // the fill counters are packed [group][bucket]: one wave's reservations (consecutive buckets) are
 // 64 consecutive words — a few 128-B requests at the memory side, not 64 (scattered returning
 // atomics run ~17x slower per byte: MI355X_MICROARCH.md, Global float atomics)
-constexpr uint32_t kLrFxMaxGBits = 3;      // at most 8 chunk groups per bucket region
+constexpr uint32_t kLrFxMaxGBits = 4;      // at most 16 chunk groups per bucket region
 constexpr uint32_t kLrFxMaxBk = 4096;  // buckets (V <= 2^24); beyond it the atomic form runs
 template <int RPT, int NT, bool AFF, int HC, bool RES>
 __global__ __launch_bounds__(NT) void k_lr_fxb_step(const uint2 *__restrict__ chunks, uint32_t nchunks,
@@ -3341,8 +3341,8 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
       // group's sub-region also holds at most its chunks' records.  The most groups whose regions
       // stay within 2^31 records and 4 GB (SWPS_LR_FXB_GBITS caps it)
       const uint64_t chunk_rec = (uint64_t)l->fwd_rpt * 256;
-      int gmax = (int)kLrFxMaxGBits;
-      if (const char *eg = getenv("SWPS_LR_FXB_GBITS")) gmax = std::min(std::max(atoi(eg), 0), gmax);
+      int gmax = 3;  // 8 groups (SWPS_LR_FXB_GBITS: 0 .. kLrFxMaxGBits)
+      if (const char *eg = getenv("SWPS_LR_FXB_GBITS")) gmax = std::min(std::max(atoi(eg), 0), (int)kLrFxMaxGBits);
       std::vector<uint32_t> rb;
       uint64_t tot = ~0ull;
       for (int gb = gmax; gb >= 0; gb--) {

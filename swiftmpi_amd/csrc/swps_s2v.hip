@@ -467,34 +467,53 @@ void s2v_unigram_starts(const std::vector<std::pair<uint64_t, int32_t>> &vc, uin
   }
 }
 
-// The host schedule: Sent2Vec::train's loop (sent2vec.cpp:95-103) replayed
-// over the parsed corpus.  tok_keys/line_off describe every line, sent_ids
-// the BKDR hash of each line (sent2vec.cpp:75).
-int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std::vector<uint64_t> &line_off,
-                   const std::vector<uint64_t> &sent_ids);
+// The corpus as the caller holds it (read in place during the load, never copied on the host):
+// tok_keys[line_off[l] .. line_off[l + 1]) are line l's word keys, sent_ids[l] the BKDR hash of
+// the line (sent2vec.cpp:75)
+struct S2VCorpus {
+  const uint64_t *tok_keys, *line_off, *sent_ids;
+  uint64_t nl;
+  bool train;  // the single pass (swps_s2v_run_tokens): each group trains as soon as it is loaded
+};
+
+// The host schedule: Sent2Vec::train's loop (sent2vec.cpp:95-103) replayed over the parsed corpus.
+int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c);
+template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1);
 
 // Documents are independent and the word table is read-only:
 // a rank trains exactly the lines whose sentence id BasicHashFrag assigns to
 // it (hashfrag.h:33-56), with no exchange.
-int s2v_ingest(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std::vector<uint64_t> &line_off,
-               const std::vector<uint64_t> &sent_ids) {
-  if (m->shard_world <= 1) return s2v_ingest_all(m, tok_keys, line_off, sent_ids);
+int s2v_ingest(swps_s2v *m, const S2VCorpus &c) {
+  if (m->shard_world <= 1) return s2v_ingest_all(m, c);
   std::vector<uint32_t> map(m->shard_frag);
   SWPS_TRY(swps_hashfrag_table(m->shard_frag, m->shard_world, map.data()));
   std::vector<uint64_t> k2, off2{0}, id2;
-  const uint64_t nl = line_off.size() - 1;
-  for (uint64_t l = 0; l < nl; l++) {
-    if ((int32_t)map[fmix64(sent_ids[l]) % (uint64_t)m->shard_frag] - 1 != m->shard_rank) continue;
-    k2.insert(k2.end(), tok_keys.begin() + line_off[l], tok_keys.begin() + line_off[l + 1]);
+  for (uint64_t l = 0; l < c.nl; l++) {
+    if ((int32_t)map[fmix64(c.sent_ids[l]) % (uint64_t)m->shard_frag] - 1 != m->shard_rank) continue;
+    k2.insert(k2.end(), c.tok_keys + c.line_off[l], c.tok_keys + c.line_off[l + 1]);
     off2.push_back(k2.size());
-    id2.push_back(sent_ids[l]);
+    id2.push_back(c.sent_ids[l]);
   }
-  return s2v_ingest_all(m, k2, off2, id2);
+  return s2v_ingest_all(m, S2VCorpus{k2.data(), off2.data(), id2.data(), id2.size(), c.train});
 }
 
-int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std::vector<uint64_t> &line_off,
-                   const std::vector<uint64_t> &sent_ids) {
-  const uint64_t nl = line_off.size() - 1;
+// every document's token rows from the rows of every corpus token (a wave per document): the
+// documents are the valid lines of the minibatches trained, in order
+__global__ __launch_bounds__(256) void k_s2v_doc_rows(const uint32_t *__restrict__ all_row,
+                                                      const uint64_t *__restrict__ line_off,
+                                                      const uint32_t *__restrict__ doc_line,
+                                                      const uint64_t *__restrict__ doc_tok, uint64_t nd,
+                                                      uint32_t *__restrict__ tok_row) {
+  const uint64_t d = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (d >= nd) return;
+  const uint64_t a = line_off[doc_line[d]], n = doc_tok[d + 1] - doc_tok[d], o = doc_tok[d];
+  for (uint64_t i = lane; i < n; i += 64) tok_row[o + i] = all_row[a + i];
+}
+
+int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
+  const uint64_t *tok_keys = c.tok_keys, *line_off = c.line_off, *sent_ids = c.sent_ids;
+  const uint64_t nl = c.nl;
   const int D = m->D, B = m->cfg.minibatch, N = m->N, S = 2 * m->W + m->N + 1;
   const uint64_t T = m->cfg.unigram_size;
   hipStream_t s = m->s;
@@ -539,7 +558,8 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   std::vector<uint64_t> vocab_keys;  // concatenated minibatch vocabs (std::map order)
   std::vector<uint64_t> starts_all;
   std::vector<uint64_t> rand_chunks;  // the sentences' rand() outputs: {destination, stream index, count}
-  std::vector<uint64_t> doc_tok_keys;
+  std::vector<uint32_t> doc_line;   // sentence -> its line
+  uint64_t doc_ntok = 0;
   std::vector<uint32_t> doc_batch;  // sentence -> minibatch
   m->batches.clear();
   m->doc_id.clear();
@@ -562,15 +582,21 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
   };
   const uint64_t K = nl ? (nl + (uint64_t)B) / (uint64_t)(B + 1) : 0;  // handler windows of B + 1 lines
   std::vector<Plan> plan(K);
+  // the workers take the minibatches in order and flag each plan when it is done; the pass below
+  // (this thread) follows them minibatch by minibatch instead of waiting for all of them
+  std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[std::max<uint64_t>(K, 1)]);
+  for (uint64_t k = 0; k < K; k++) ready[k].store(0, std::memory_order_relaxed);
+  std::atomic<uint64_t> next{0};
+  std::atomic<bool> quit{false};
+  std::vector<std::thread> workers;
   {
     int nth = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
     if (const char *e = getenv("SWPS_S2V_THREADS")) nth = std::max(1, atoi(e));
     nth = (int)std::min<uint64_t>((uint64_t)nth, std::max<uint64_t>(K, 1));
-    std::atomic<uint64_t> next{0};
     auto work = [&]() {
       FlatMap64 fq(1 << 16);
       std::vector<std::pair<uint64_t, int32_t>> vc;
-      for (uint64_t k; (k = next.fetch_add(1)) < K;) {
+      for (uint64_t k; !quit.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < K;) {
         Plan &pl = plan[k];
         fq.clear();
         int cnt = 0;
@@ -584,7 +610,10 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
           }
           if (++cnt > B) break;
         }
-        if (pl.first.size() < 5) continue;  // the loop ends here (sent2vec.cpp:97)
+        if (pl.first.size() < 5) {  // the loop ends here (sent2vec.cpp:97)
+          ready[k].store(1, std::memory_order_release);
+          continue;
+        }
         pl.zero = fq.contains(0);
         vc.clear();
         for (uint64_t key : pl.first) {
@@ -595,22 +624,218 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
         s2v_unigram_starts(vc, T, pl.st);
         pl.vkeys.resize(vc.size());
         for (size_t q = 0; q < vc.size(); q++) pl.vkeys[q] = vc[q].first;
+        ready[k].store(1, std::memory_order_release);
       }
     };
-    std::vector<std::thread> th;
-    for (int q = 1; q < nth; q++) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
+    for (int q = 0; q < nth; q++) workers.emplace_back(work);
   }
-  phase("minibatch vocabs (threads)");
+  struct Join {  // the workers end with this scope, on every return path
+    std::vector<std::thread> &w;
+    std::atomic<bool> &q;
+    ~Join() {
+      q.store(true);
+      for (auto &t : w)
+        if (t.joinable()) t.join();
+    }
+  } join{workers, quit};
+  auto wait_plan = [&](uint64_t k) {
+    for (unsigned it = 0; !ready[k].load(std::memory_order_acquire); it++)
+      if (it < 64)
+        std::this_thread::yield();
+      else
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+  };
   FlatMap64 inserted(1024);  // keys the minibatches so far inserted (the server's inserts persist)
-  doc_tok_keys.reserve(tok_keys.size());
-  m->doc_id.reserve(nl);
-  m->doc_tok.reserve(nl + 1);
-  m->doc_rec.reserve(nl + 1);
-  m->doc_lcg.reserve(nl);
-  doc_batch.reserve(nl);
+  // Bounds for the device arrays, from the line lengths alone, so everything the pass below makes
+  // can go to the device group by group (never reallocated while a group trains): the gather
+  // windows' tokens bound the minibatch vocabularies, the valid lines the documents, each
+  // pipeline group's records the record buffer
+  uint64_t wtok = 0, ndmax = 0;
+  std::vector<uint64_t> krec(K, 0), kdoc(K, 0);
   for (uint64_t k = 0; k < K; k++) {
+    int cnt = 0;
+    for (uint64_t l = k * (uint64_t)(B + 1); l < nl;) {
+      const uint64_t q = l++;
+      if (!valid[q]) continue;
+      wtok += line_off[q + 1] - line_off[q];
+      if (++cnt > B) break;
+    }
+    for (uint64_t l = k * (uint64_t)(B + 1); l < std::min<uint64_t>(nl, (k + 1) * (uint64_t)(B + 1)); l++)
+      if (valid[l]) {
+        kdoc[k]++;
+        krec[k] += (line_off[l + 1] - line_off[l]) * (uint64_t)m->cfg.niters;
+      }
+    ndmax += kdoc[k];
+  }
+  // pipeline groups: 2, 4, then 8 minibatches (at most group_docs documents), so the first group
+  // trains early while the later ones are planned
+  std::vector<uint64_t> gend;
+  uint64_t grec_max = 0;
+  for (uint64_t k0 = 0, gsz = 2; k0 < K; gsz = std::min<uint64_t>(8, 2 * gsz)) {
+    uint64_t k1 = k0 + 1, docs = kdoc[k0], recs = krec[k0];
+    while (k1 < K && k1 - k0 < gsz && docs + kdoc[k1] <= m->group_docs) {
+      docs += kdoc[k1];
+      recs += krec[k1];
+      k1++;
+    }
+    gend.push_back(k1);
+    grec_max = std::max(grec_max, recs);
+    k0 = k1;
+  }
+  const uint64_t ntok_all = line_off[nl], nchunk_max = ndmax * (uint64_t)D / kRandRun + K + 1;
+  std::vector<uint64_t> vocab_keys_r, starts_r, rand_r;
+  vocab_keys.reserve(wtok);
+  starts_all.reserve(wtok + K);
+  rand_chunks.reserve(3 * nchunk_max);
+  doc_line.reserve(ndmax);
+  m->doc_id.reserve(ndmax);
+  m->doc_tok.reserve(ndmax + 1);
+  m->doc_rec.reserve(ndmax + 1);
+  m->doc_lcg.reserve(ndmax);
+  doc_batch.reserve(ndmax);
+  std::vector<uint64_t> bv0(K), bs0(K);
+  std::vector<uint32_t> bU(K);
+  DevMem d_vkeys, d_keys_all, d_all_row, d_line_off, d_doc_line, d_chunks, d_base;
+  SWPS_TRY(d_vkeys.ensure(std::max<uint64_t>(wtok, 1) * 8));
+  SWPS_TRY(m->d_vocab_row.ensure(std::max<uint64_t>(wtok, 1) * 4));
+  SWPS_TRY(m->d_starts.ensure((wtok + K + 1) * 8));
+  SWPS_TRY(m->d_doc_tok.ensure((ndmax + 1) * 8));
+  SWPS_TRY(m->d_doc_rec.ensure((ndmax + 1) * 8));
+  SWPS_TRY(m->d_doc_lcg.ensure(std::max<uint64_t>(ndmax, 1) * 8));
+  SWPS_TRY(m->d_doc_batch.ensure(std::max<uint64_t>(ndmax, 1) * 4));
+  SWPS_TRY(d_doc_line.ensure(std::max<uint64_t>(ndmax, 1) * 4));
+  SWPS_TRY(m->d_bv0.ensure(std::max<uint64_t>(K, 1) * 8));
+  SWPS_TRY(m->d_bs0.ensure(std::max<uint64_t>(K, 1) * 8));
+  SWPS_TRY(m->d_bU.ensure(std::max<uint64_t>(K, 1) * 4));
+  SWPS_TRY(m->d_init.ensure(std::max<uint64_t>(ndmax, 1) * D * 4));
+  SWPS_TRY(m->d_out.ensure(std::max<uint64_t>(ndmax, 1) * D * (m->f64 ? 8 : 4)));
+  SWPS_TRY(m->d_err.ensure(std::max<uint64_t>(ndmax, 1) * 4));
+  SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(grec_max, 1) * (uint64_t)S * 4));
+  SWPS_TRY(m->d_tok_row.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
+  SWPS_TRY(d_keys_all.ensure(std::max<uint64_t>(ntok_all, 1) * 8));
+  SWPS_TRY(d_all_row.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
+  SWPS_TRY(d_line_off.ensure((nl + 1) * 8));
+  SWPS_TRY(d_chunks.ensure(3 * nchunk_max * 8));
+  {
+    std::vector<float> ex(1000);
+    for (int i = 0; i < 1000; i++) {  // ExpTable (word2vec.h:241-253)
+      float x = (i / (float)1000 * 2 - 1) * 6;
+      float e = (float)std::exp((double)x);
+      ex[i] = e / (e + 1);
+    }
+    SWPS_TRY(upload(m->d_exptab, ex, s));
+    SWPS_TRY(upload(d_base, glibc_base(m->cfg.rand_seed), s));
+    SWPS_HIP(hipStreamSynchronize(s));  // ex, the base vector: locals
+  }
+  // the load stream: each group's uploads, lookups and rand() rows; the training of a group waits
+  // for its event on the table's stream
+  struct LoadStream {
+    hipStream_t s = nullptr;
+    std::vector<hipEvent_t> ev;
+    ~LoadStream() {
+      if (s) (void)hipStreamSynchronize(s);
+      for (auto e : ev) (void)hipEventDestroy(e);
+      if (s) (void)hipStreamDestroy(s);
+    }
+  } ls;
+  SWPS_HIP(hipStreamCreateWithFlags(&ls.s, hipStreamNonBlocking));
+  if (nl) SWPS_HIP(hipMemcpyAsync(d_line_off.p, line_off, (nl + 1) * 8, hipMemcpyHostToDevice, ls.s));
+  const uint64_t zero = 0;
+  SWPS_HIP(hipMemcpyAsync(m->d_doc_tok.p, &zero, 8, hipMemcpyHostToDevice, ls.s));
+  SWPS_HIP(hipMemcpyAsync(m->d_doc_rec.p, &zero, 8, hipMemcpyHostToDevice, ls.s));
+  SWPS_HIP(hipStreamSynchronize(ls.s));  // `zero` is a local
+  m->cursor = 0;
+  m->loaded = false;
+  size_t mk_done = 0;  // misses already in the table
+  uint64_t kf = 0, rc_done = 0;  // minibatches / rand chunks already on the device
+  // one group's device part: its misses into the table, its vocabularies' rows and run starts, its
+  // documents' arrays, token rows and rand() rows; then (train) its records + docs launch
+  auto flush = [&](uint64_t k1) -> int {
+    if (k1 == kf) return SWPS_OK;
+    if (miss_keys.size() > mk_done) {  // rows = [h | v | h2 = 0 | v2 = 0]; the table's own stream (syncs)
+      const std::vector<uint64_t> mk(miss_keys.begin() + mk_done, miss_keys.end());
+      DevMem dk, dv;
+      SWPS_TRY(upload(dk, mk, s));
+      if (m->f64) {
+        const std::vector<double> fr(miss_rows.begin() + mk_done * 4 * D, miss_rows.end());
+        SWPS_TRY(upload(dv, fr, s));
+        SWPS_HIP(hipStreamSynchronize(s));
+      } else {
+        const std::vector<float> fr(miss_rows.begin() + mk_done * 4 * D, miss_rows.end());
+        SWPS_TRY(upload(dv, fr, s));
+        SWPS_HIP(hipStreamSynchronize(s));
+      }
+      SWPS_TRY(swps_assign(m->t, dk.as<uint64_t>(), mk.size(), dv.p));
+      mk_done = miss_keys.size();
+    }
+    hipStream_t q = ls.s;
+    const swps_s2v::Batch &b0 = m->batches[kf], &b1 = m->batches[k1 - 1];
+    const uint64_t v0 = b0.v0, v1 = b1.v0 + b1.U, s0 = b0.s0, s1 = starts_all.size(), d0 = b0.d0, d1 = b1.d1;
+    for (uint64_t k = kf; k < k1; k++) {
+      bv0[k] = m->batches[k].v0;
+      bs0[k] = m->batches[k].s0;
+      bU[k] = m->batches[k].U;
+    }
+    if (v1 > v0) {
+      SWPS_HIP(hipMemcpyAsync(d_vkeys.as<uint64_t>() + v0, vocab_keys.data() + v0, (v1 - v0) * 8,
+                              hipMemcpyHostToDevice, q));
+      SWPS_TRY(table_lookup(m->t, d_vkeys.as<uint64_t>() + v0, v1 - v0, m->d_vocab_row.as<uint32_t>() + v0, q));
+    }
+    if (s1 > s0)
+      SWPS_HIP(hipMemcpyAsync(m->d_starts.as<uint64_t>() + s0, starts_all.data() + s0, (s1 - s0) * 8,
+                              hipMemcpyHostToDevice, q));
+    SWPS_HIP(hipMemcpyAsync(m->d_bv0.as<uint64_t>() + kf, bv0.data() + kf, (k1 - kf) * 8, hipMemcpyHostToDevice, q));
+    SWPS_HIP(hipMemcpyAsync(m->d_bs0.as<uint64_t>() + kf, bs0.data() + kf, (k1 - kf) * 8, hipMemcpyHostToDevice, q));
+    SWPS_HIP(hipMemcpyAsync(m->d_bU.as<uint32_t>() + kf, bU.data() + kf, (k1 - kf) * 4, hipMemcpyHostToDevice, q));
+    if (d1 > d0) {
+      SWPS_HIP(hipMemcpyAsync(m->d_doc_tok.as<uint64_t>() + d0 + 1, m->doc_tok.data() + d0 + 1, (d1 - d0) * 8,
+                              hipMemcpyHostToDevice, q));
+      SWPS_HIP(hipMemcpyAsync(m->d_doc_rec.as<uint64_t>() + d0 + 1, m->doc_rec.data() + d0 + 1, (d1 - d0) * 8,
+                              hipMemcpyHostToDevice, q));
+      SWPS_HIP(hipMemcpyAsync(m->d_doc_lcg.as<uint64_t>() + d0, m->doc_lcg.data() + d0, (d1 - d0) * 8,
+                              hipMemcpyHostToDevice, q));
+      SWPS_HIP(hipMemcpyAsync(m->d_doc_batch.as<uint32_t>() + d0, doc_batch.data() + d0, (d1 - d0) * 4,
+                              hipMemcpyHostToDevice, q));
+      SWPS_HIP(hipMemcpyAsync(d_doc_line.as<uint32_t>() + d0, doc_line.data() + d0, (d1 - d0) * 4,
+                              hipMemcpyHostToDevice, q));
+      // the group's lines' token keys (read in place from the caller's array) -> rows -> documents
+      const uint64_t la = kf * (uint64_t)(B + 1), lb = std::min<uint64_t>(nl, k1 * (uint64_t)(B + 1));
+      const uint64_t t0 = line_off[la], t1 = line_off[lb];
+      if (t1 > t0) {
+        SWPS_HIP(hipMemcpyAsync(d_keys_all.as<uint64_t>() + t0, tok_keys + t0, (t1 - t0) * 8, hipMemcpyHostToDevice, q));
+        // probed, not looked up: a short line's keys (read, never gathered) may be absent; the
+        // documents' keys are all in their minibatches' vocabularies, whose lookup above latches
+        SWPS_TRY(table_probe(m->t, d_keys_all.as<uint64_t>() + t0, t1 - t0, d_all_row.as<uint32_t>() + t0, q));
+      }
+      k_s2v_doc_rows<<<(unsigned)(((d1 - d0) * 64 + 255) / 256), 256, 0, q>>>(
+          d_all_row.as<uint32_t>(), d_line_off.as<uint64_t>(), d_doc_line.as<uint32_t>() + d0,
+          m->d_doc_tok.as<uint64_t>() + d0, d1 - d0, m->d_tok_row.as<uint32_t>());
+      SWPS_HIP(hipGetLastError());
+    }
+    const uint64_t nch = rand_chunks.size() / 3;
+    if (nch > rc_done) {
+      SWPS_HIP(hipMemcpyAsync(d_chunks.as<uint64_t>() + 3 * rc_done, rand_chunks.data() + 3 * rc_done,
+                              (nch - rc_done) * 24, hipMemcpyHostToDevice, q));
+      k_s2v_rand<<<(unsigned)((nch - rc_done + 63) / 64), 64, 0, q>>>(
+          d_base.as<uint32_t>(), d_chunks.as<uint64_t>() + 3 * rc_done, nch - rc_done, m->d_init.as<int32_t>());
+      SWPS_HIP(hipGetLastError());
+      rc_done = nch;
+    }
+    hipEvent_t ev;
+    SWPS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ls.ev.push_back(ev);
+    SWPS_HIP(hipEventRecord(ev, q));
+    if (c.train) {  // the group trains on the table's stream as soon as its data is there
+      SWPS_HIP(hipStreamWaitEvent(s, ev, 0));
+      SWPS_TRY(m->f64 ? s2v_group<double>(m, kf, k1) : s2v_group<float>(m, kf, k1));
+      m->cursor = k1;
+    }
+    kf = k1;
+    return SWPS_OK;
+  };
+  size_t gi = 0;
+  for (uint64_t k = 0; k < K; k++) {
+    wait_plan(k);
     Plan &pl = plan[k];
     const std::vector<uint64_t> &first_seen = pl.first;
     const uint64_t li = k * (uint64_t)(B + 1);
@@ -658,14 +883,15 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     std::vector<uint64_t>().swap(pl.vkeys);
     std::vector<uint64_t>().swap(pl.st);
     // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not; the sentences' Vec::random
-    // draws are this minibatch's next run of the stream (drawn on the device below)
+    // draws are this minibatch's next run of the stream (drawn on the device, k_s2v_rand)
     const uint64_t run_o = 344 + rnd.produced + skip, run_d0 = m->doc_id.size();
     for (uint64_t l = li; l < std::min<uint64_t>(nl, li + (uint64_t)(B + 1)); l++) {
       if (!valid[l]) continue;
       const uint64_t L = line_off[l + 1] - line_off[l];
       m->doc_id.push_back(sent_ids[l]);
-      doc_tok_keys.insert(doc_tok_keys.end(), tok_keys.begin() + line_off[l], tok_keys.begin() + line_off[l + 1]);
-      m->doc_tok.push_back(doc_tok_keys.size());
+      doc_line.push_back((uint32_t)l);
+      doc_ntok += L;
+      m->doc_tok.push_back(doc_ntok);
       m->doc_rec.push_back(m->doc_rec.back() + L * (uint64_t)m->cfg.niters);
       skip += (uint64_t)D;
       m->doc_lcg.push_back(lstate);
@@ -679,91 +905,24 @@ int s2v_ingest_all(swps_s2v *m, const std::vector<uint64_t> &tok_keys, const std
     m->max_recs = std::max(m->max_recs, b.recs);
     m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
     m->batches.push_back(b);
+    if (gi < gend.size() && k + 1 == gend[gi]) {
+      SWPS_TRY(flush(k + 1));
+      gi++;
+    }
   }
-  phase("minibatch schedule (host)");
+  quit.store(true);  // plans past the corpus end (sent2vec.cpp:97) are not needed
+  SWPS_TRY(flush(m->batches.size()));
+  phase("minibatch vocabs + schedule + groups (host)");
   m->lstate_end = lstate;
   rnd.discard(skip);
   m->rand_calls = rnd.produced;  // includes the rand_offset skipped above
   m->nlines = nl;
-  m->ntok = doc_tok_keys.size();
-  // misses into the table (they persist for later minibatches, like the
-  // server's inserts); rows = [h | v | h2 = 0 | v2 = 0]
-  if (!miss_keys.empty()) {
-    DevMem dk, dv;
-    SWPS_TRY(upload(dk, miss_keys, s));
-    if (m->f64) {
-      SWPS_TRY(upload(dv, miss_rows, s));
-      SWPS_HIP(hipStreamSynchronize(s));
-    } else {
-      std::vector<float> fr(miss_rows.begin(), miss_rows.end());
-      SWPS_TRY(upload(dv, fr, s));
-      SWPS_HIP(hipStreamSynchronize(s));
-    }
-    SWPS_TRY(swps_assign(m->t, dk.as<uint64_t>(), miss_keys.size(), dv.p));
-  }
-  // key -> word-table row for the minibatch vocabs and every sentence token
-  {
-    DevMem dk, dt;
-    SWPS_TRY(upload(dk, vocab_keys, s));
-    SWPS_TRY(m->d_vocab_row.ensure(std::max<size_t>(vocab_keys.size(), 1) * 4));
-    SWPS_TRY(table_lookup(m->t, dk.as<uint64_t>(), vocab_keys.size(), m->d_vocab_row.as<uint32_t>(), s));
-    SWPS_TRY(upload(dt, doc_tok_keys, s));
-    SWPS_TRY(m->d_tok_row.ensure(std::max<size_t>(doc_tok_keys.size(), 1) * 4));
-    SWPS_TRY(table_lookup(m->t, dt.as<uint64_t>(), doc_tok_keys.size(), m->d_tok_row.as<uint32_t>(), s));
-    SWPS_TRY(table_check_error(m->t, s));  // syncs; every key is present by now
-  }
-  phase("misses + row lookups");
-  SWPS_TRY(upload(m->d_starts, starts_all, s));
-  {
-    std::vector<uint64_t> bv0, bs0;
-    std::vector<uint32_t> bU;
-    for (auto &b : m->batches) {
-      bv0.push_back(b.v0);
-      bs0.push_back(b.s0);
-      bU.push_back(b.U);
-    }
-    if (doc_batch.empty()) doc_batch.push_back(0);
-    if (bv0.empty()) {
-      bv0.push_back(0);
-      bs0.push_back(0);
-      bU.push_back(0);
-    }
-    SWPS_TRY(upload(m->d_doc_batch, doc_batch, s));
-    SWPS_TRY(upload(m->d_bv0, bv0, s));
-    SWPS_TRY(upload(m->d_bs0, bs0, s));
-    SWPS_TRY(upload(m->d_bU, bU, s));
-  }
-  SWPS_TRY(upload(m->d_doc_tok, m->doc_tok, s));
-  SWPS_TRY(upload(m->d_doc_rec, m->doc_rec, s));
-  SWPS_TRY(upload(m->d_doc_lcg, m->doc_lcg, s));
-  {
-    const uint64_t nd = m->doc_id.size(), nch = rand_chunks.size() / 3;
-    SWPS_TRY(m->d_init.ensure(std::max<uint64_t>(nd, 1) * D * 4));
-    if (nch) {
-      DevMem dbase, dch;
-      SWPS_TRY(upload(dbase, glibc_base(m->cfg.rand_seed), s));
-      SWPS_TRY(upload(dch, rand_chunks, s));
-      k_s2v_rand<<<(unsigned)((nch + 63) / 64), 64, 0, s>>>(dbase.as<uint32_t>(), dch.as<uint64_t>(), nch,
-                                                            m->d_init.as<int32_t>());
-      SWPS_HIP(hipGetLastError());
-      SWPS_HIP(hipStreamSynchronize(s));
-    }
-  }
-  std::vector<float> ex(1000);
-  for (int i = 0; i < 1000; i++) {  // ExpTable (word2vec.h:241-253)
-    float x = (i / (float)1000 * 2 - 1) * 6;
-    float e = (float)std::exp((double)x);
-    ex[i] = e / (e + 1);
-  }
-  SWPS_TRY(upload(m->d_exptab, ex, s));
-  const uint64_t nd = m->doc_id.size();
-  SWPS_TRY(m->d_out.ensure(std::max<uint64_t>(nd, 1) * D * (m->f64 ? 8 : 4)));
-  SWPS_TRY(m->d_err.ensure(std::max<uint64_t>(nd, 1) * 4));
-  SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(m->max_recs, 1) * (uint64_t)S * 4));
-  SWPS_HIP(hipStreamSynchronize(s));  // host vectors above go out of scope
-  phase("uploads + sentence rand()");
+  m->ntok = doc_ntok;
+  SWPS_HIP(hipStreamSynchronize(ls.s));
+  SWPS_TRY(table_check_error(m->t, s));  // syncs (a training pass too); every key was present
+  phase("last uploads + lookups");
   m->loaded = true;
-  m->cursor = 0;
+  if (!c.train) m->cursor = 0;
   return SWPS_OK;
 }
 
@@ -920,7 +1079,7 @@ int swps_s2v_load_text(swps_s2v *m, const char *path) {
   }
   free(buf);
   fclose(f);
-  return s2v_ingest(m, keys, off, ids);
+  return s2v_ingest(m, S2VCorpus{keys.data(), off.data(), ids.data(), ids.size(), false});
 }
 
 int swps_s2v_shard(swps_s2v *m, int32_t rank, int32_t world, int32_t frag_num) {
@@ -935,9 +1094,19 @@ int swps_s2v_shard(swps_s2v *m, int32_t rank, int32_t world, int32_t frag_num) {
 int swps_s2v_load_tokens(swps_s2v *m, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,
                          uint64_t nlines, const uint64_t *sent_ids) {
   if (line_off[0] != 0 || line_off[nlines] != ntok) return fail(SWPS_E_CFG, "line_off must span [0, ntok]");
-  return s2v_ingest(m, std::vector<uint64_t>(tok_keys, tok_keys + ntok),
-                    std::vector<uint64_t>(line_off, line_off + nlines + 1),
-                    std::vector<uint64_t>(sent_ids, sent_ids + nlines));
+  for (uint64_t l = 0; l < nlines; l++)
+    if (line_off[l + 1] < line_off[l]) return fail(SWPS_E_CFG, "line_off must not decrease");
+  // the caller's arrays are read in place (valid during this call)
+  return s2v_ingest(m, S2VCorpus{tok_keys, line_off, sent_ids, nlines, false});
+}
+
+int swps_s2v_run_tokens(swps_s2v *m, const uint64_t *tok_keys, uint64_t ntok, const uint64_t *line_off,
+                        uint64_t nlines, const uint64_t *sent_ids) {
+  if (line_off[0] != 0 || line_off[nlines] != ntok) return fail(SWPS_E_CFG, "line_off must span [0, ntok]");
+  for (uint64_t l = 0; l < nlines; l++)
+    if (line_off[l + 1] < line_off[l]) return fail(SWPS_E_CFG, "line_off must not decrease");
+  SWPS_TRY(s2v_ingest(m, S2VCorpus{tok_keys, line_off, sent_ids, nlines, true}));
+  return swps_s2v_sync(m);
 }
 
 int swps_s2v_info(swps_s2v *m, uint64_t *o) {

@@ -182,6 +182,62 @@ def test_s2v_bench_dim_matches_oracle(lib, oracle_mod, gpu, tmp_path, dtype, D):
         assert rel.max() < 1e-5, rel.max()
 
 
+def _tokens_of(lib, path):
+    """(tok_keys, line_off, sent_ids) of a text corpus as the loaders parse it: split(" "), atoi
+    keys (word2vec.h:206,212-224), sentence id = BKDR of the line (sent2vec.cpp:75)."""
+    toks, off, ids = [], [0], []
+    with open(path) as f:
+        for line in f:
+            line = line.rstrip("\n")
+            ids.append(lib.bkdr(line))
+            toks += [int(w) for w in line.split(" ") if w]
+            off.append(len(toks))
+    return (np.array(toks, dtype=np.uint64), np.array(off, dtype=np.uint64), np.array(ids, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("B,min_len,lo,hi,extra,nlines", [(20, 1, 5, 25, 0, 130), (9, 8, 1, 20, 32, 90),
+                                                          (7, 1, 5, 25, 0, 300), (1, 1, 5, 25, 0, 40)])
+def test_s2v_single_pass_equals_load_then_train(lib, oracle_mod, gpu, tmp_path, B, min_len, lo, hi, extra, nlines):
+    """The reference's single pass (swps_s2v_run_tokens: each minibatch group planned on host threads
+    while the GPU trains the groups before it) = load_tokens + train, bit for bit: sentence ids and
+    vectors, errors, the rows the pulls inserted, the rand() call count and the LCG end state — with
+    misses (keys the loaded word dump lacks), short lines and the tail stop; and = the oracle."""
+    import torch
+    D = 16
+    corpus = int_corpus(str(tmp_path / "c.txt"), nlines, 150, seed=5, lo=lo, hi=hi)
+    dump = word_dump(str(tmp_path / "w.txt"), 120, D, seed=6)
+    toks, off, ids = _tokens_of(lib, corpus)
+    res = []
+    for single in (False, True):
+        t = lib.Table("w2v", dim=D, capacity=214, dtype="f64")
+        s = lib.Sent2Vec(t, window=3, negative=4, minibatch=B, niters=2, min_sentence_length=min_len,
+                         unigram_size=10 ** 6, rand_offset=2, rand_insert_extra=extra)
+        s.load_word_vector(dump)
+        if single:
+            s.run_tokens(toks, off, ids)
+        else:
+            s.load_tokens(toks, off, ids)
+            s.train()
+        keys = np.sort(t.keys())
+        res.append((s.docs(), s.info(), s.stats(), keys,
+                    t.export(torch.as_tensor(keys.astype(np.int64), device="cuda")).cpu().numpy()))
+        del s
+        t.close()
+    (da, ia, sa, ka, ra), (db, ib, sb, kb, rb) = res
+    for x, y in zip(da, db):
+        assert np.array_equal(x, y)
+    assert ia == ib and sa == sb, (ia, ib, sa, sb)
+    assert np.array_equal(ka, kb) and np.array_equal(ra, rb)
+    orc = oracle_mod.S2V(corpus, D, window=3, negative=4, minibatch=B, niters=2, min_sentence_length=min_len,
+                         table_size=10 ** 6, rand_offset=2, rand_insert_extra=extra)
+    orc.load_words(dump)
+    orc.train()
+    io, vo, _ = orc.docs()
+    assert len(io) > 0 and np.array_equal(io, db[0])
+    assert ib["lstate"] == orc.stats()["rng"] and ib["rand_calls"] == orc.stats()["rand_calls"]
+    assert np.allclose(db[1], vo, rtol=1e-9, atol=1e-12), np.abs(db[1] - vo).max()
+
+
 def _zipf_docs(rng, V, nd, lo=50, hi=200):
     p = 1.0 / np.arange(1, V + 1)
     cdf = np.cumsum(p / p.sum())
@@ -253,9 +309,9 @@ def test_s2v_config5_shape(lib, oracle_mod, gpu, tmp_path):
 def test_s2v_config5_full_rank_share(lib, gpu):
     """BASELINE config 5 at its full per-GPU share (1e7 docs / 8 GPUs = 1.25M docs of 50-200
     Zipf(1M) tokens, 156M words, minibatches of 8192 against a 1M x 300 hash-initialised word
-    table): loaded and trained twice, the sentence vectors are bit-identical run to run and
-    finite, every document and position is counted, and the load (the per-minibatch vocabularies
-    on worker threads) finishes in seconds."""
+    table): loaded and trained, then run as the single pass (swps_s2v_run_tokens), the sentence
+    vectors are bit-identical between the two and finite, every document and position is counted,
+    and the load (the per-minibatch vocabularies on worker threads) finishes in seconds."""
     import time
     import torch
     from swiftmpi_amd.synth import zipf_tokens
@@ -270,15 +326,19 @@ def test_s2v_config5_full_rank_share(lib, gpu):
     t = lib.Table("w2v", dim=D, capacity=V + 1024, dtype="f32", init="hash", seed=3)
     t.pull(torch.arange(1, V + 1, dtype=torch.int64, device="cuda"))
     outs, loads = [], []
-    for _ in range(2):
+    for single in (False, True):  # load + train, then the single pass (swps_s2v_run_tokens)
         s = lib.Sent2Vec(t, window=5, negative=5, minibatch=8192, niters=1)
         t0 = time.perf_counter()
-        s.load_tokens(toks, off, sent)
+        if single:
+            s.run_tokens(toks, off, sent)
+        else:
+            s.load_tokens(toks, off, sent)
         loads.append(time.perf_counter() - t0)
-        s.train()
+        if not single:
+            s.train()
         outs.append((s.docs()[1], s.stats()))
         del s
-    print("load s", loads)
+    print("load s, single pass s", loads)
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.isfinite(outs[0][0]).all()
     st = outs[0][1]
