@@ -717,6 +717,8 @@ def main():
     ap.add_argument("--lr-exact", action="store_true",
                     help="LR: the reference's sequential fp32 per-key sums (bit-exact) instead of fast fp64 sums")
     ap.add_argument("--s2v-docs", type=int, default=8192, help="sent2vec documents per minibatch")
+    ap.add_argument("--no-lr-sharded-base", action="store_true",
+                    help="skip the lr leg's world-1 sharded base point (lr.sharded_world1) at N = 1")
     ap.add_argument("--no-app-legs", action="store_true",
                     help="skip the config-4, LR (config 3) and sent2vec (config 5) legs of the default line")
     ap.add_argument("--app-steps", type=int, default=20, help="timed LR minibatches of the default line's lr leg")
@@ -846,6 +848,23 @@ def main():
         sa.steps, sa.warmup = 31, 31  # one launch of 31 minibatches (swps_s2v group_docs) per pass
         set_phase("s2v")
         out["s2v"] = bench_s2v(sa, ctx, corpus_batches=31)
+        if world == 1 and not ctx.sharded and not args.no_lr_sharded_base:
+            # the N > 1 LR leg runs the key-sharded protocol (owner pull, exchange, install, the step,
+            # the mean-gradient push, owner AdaGrad); its world-1 run is the like-for-like base point
+            # of the scaling curve (lr.value above is the unsharded single-GPU step)
+            set_phase("lr_sharded_world1")
+            sctx = Ctx(True)
+            lb = argparse.Namespace(**vars(la))
+            lb.no_cpu_baseline = True
+            q = bench_lr(lb, sctx, corpus_batches=10)
+            out["lr"]["sharded_world1"] = {
+                "value": q["value"], "unit": q["unit"], "ms_per_step": q["ms_per_step"], "kernel_ms": q["kernel_ms"],
+                "parallelism": q["config"]["parallelism"],
+                "note": "the same workload through the key-sharded protocol at world 1 (no remote bytes): the base "
+                        "point for the N > 1 lr legs, which run this protocol"}
+            sctx.close()
+            if sctx.dist is not None:
+                sctx.dist.destroy_process_group()
     set_phase("report")
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -978,7 +997,7 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
         push_bytes = 20 * nnz + 32 * uniq
     push_gbs = push_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
     step_gbs = (fwd_bytes + push_bytes) * world / dt / 1e9
-    kf = {"kernel": "k_lr_fxb_step (forward + per-chunk bucket sort + hot-key partials)" if fx
+    kf = {"kernel": "k_lr_fxr_step (forward + per-chunk bucket sort into the bucket regions + hot-key partials)" if fx
           else "k_lr_forward_c" if os.environ.get("SWPS_LR_FWD_C", "1") != "0" else "k_lr_forward_g",
           "achieved": fwd_gbs, "frac": fwd_gbs / HBM_PEAK_GBS,
           "bytes_per_launch": fwd_bytes / max(fwd_n, 1), "avg_launch_ms": fwd_ms / max(fwd_n, 1), "launches": fwd_n}
@@ -992,7 +1011,7 @@ def bench_lr(args, ctx, corpus_batches=None, cpu_rows=None):
     tr, tsrc = pmc_traffic(dict(app="lr", lr_batch=args.lr_batch, exact=bool(args.lr_exact), world=world,
                                 sharded=dist is not None, plan=args.lr_plan),
                            {"forward": ("k_lr_forward_c", "k_lr_forward_r", "k_lr_forward", "k_lr_forward_g",
-                                        "k_lr_fxb_step", "k_lr_fx_step"),
+                                        "k_lr_fxb_step", "k_lr_fxr_step", "k_lr_fx_step"),
                             "push": ("k_lr_records", "k_lr_reduce_fused", "k_lr_reduce_short", "k_lr_reduce_long",
                                      "k_lr_reduce_long_fast", "k_lr_tiles", "k_lr_tiles_fin", "k_lr_fxb_push",
                                      "k_lr_fx_apply")})

@@ -1906,7 +1906,12 @@ __global__ __launch_bounds__(NT) void k_lr_fxr_step(const uint2 *__restrict__ ch
                                                      unsigned long long *__restrict__ hsum,
                                                      uint32_t *__restrict__ hcnt, uint32_t row_base,
                                                      uint32_t *__restrict__ fill, const uint32_t *__restrict__ rbase,
-                                                     uint32_t gbits, uint32_t diag) {
+                                                     uint32_t gbits, const float *__restrict__ wmir, uint32_t diag) {
+  // wmir (single GPU): the weights as a dense array by fid, kept by k_lr_fxb_push beside the [w | g2]
+  // rows — a 128-B line holds 32 of them instead of 16, so the gathers of the non-hot weights touch
+  // half the lines (in every XCD's L2 that reads them); null: the rows themselves
+  const float *wsrc = wmir ? wmir : rows;
+  const uint64_t wst = wmir ? 1 : 2, wb = wmir ? 0 : row_base;
   constexpr int CAP = RPT * NT;
   __shared__ float prod[CAP];
   __shared__ uint16_t rl[CAP];
@@ -1921,7 +1926,7 @@ __global__ __launch_bounds__(NT) void k_lr_fxr_step(const uint2 *__restrict__ ch
 #pragma unroll
   for (int j = 0; j < HPT; j++) {
     const uint32_t q = tid + (uint32_t)(NT * j);
-    hv[j] = q < nhot ? rows[(uint64_t)(row_base + q) * 2] : 0.f;
+    hv[j] = q < nhot ? wsrc[(wb + q) * wst] : 0.f;
   }
   for (uint32_t q = tid; q < (uint32_t)HC + kLrFxDummy; q += (uint32_t)NT) {
     hs[q] = 0ull;
@@ -1966,7 +1971,7 @@ __global__ __launch_bounds__(NT) void k_lr_fxr_step(const uint2 *__restrict__ ch
       const bool cold = i < n && (uint32_t)f[k] >= nhot;
       const uint32_t fk = (uint32_t)f[k];
       rk[k] = atomicAdd(&bc[cold ? (fk >> kLrFxVB) : nbk + dum], 1u);
-      const float g = rows[(uint64_t)(row_base + (cold ? fk : 0u)) * 2];
+      const float g = wsrc[(wb + (cold ? fk : 0u)) * wst];
       const float h = wh[fk < nhot ? fk : 0u];
       w[k] = fk < nhot ? h : g;
     }
@@ -2089,7 +2094,8 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
                                                              uint32_t row_base, uint32_t first_block,
                                                              uint32_t bper, uint32_t *__restrict__ fill,
                                                              const uint32_t *__restrict__ rbase, uint32_t nkeys,
-                                                             uint32_t gbits, uint32_t diag) {
+                                                             uint32_t gbits, float *__restrict__ wmir,
+                                                             const uint8_t *__restrict__ pfb, uint32_t diag) {
   constexpr uint32_t T = 1u << kLrFxVB, NT = kLrFxbPushT, PER = T / NT;
   __shared__ unsigned long long as[T];
   __shared__ uint32_t ac[T];
@@ -2117,7 +2123,10 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
         sB[tid] = rbase[qg];
         fill[(uint64_t)tid * nbk + b] = 0u;
       }
-      const bool pre = !TO_GRADS && aff;
+      // the rows' loads beside the count only for the buckets whose keys most batches touch (pfb,
+      // from the corpus counts at load): elsewhere the untouched rows' bytes would outweigh the
+      // round trip they save
+      const bool aff_rows = !TO_GRADS && aff, pre = aff_rows && (!pfb || pfb[b]);
       float2 wg[PER];
 #pragma unroll
       for (uint32_t k = 0; k < PER; k++) {
@@ -2172,7 +2181,7 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
 #pragma unroll
       for (uint32_t k = 0; k < PER; k++) {
         c[k] = ac[tid + k * NT];
-        if (c[k] && !pre) row[k] = vid_row[(b << kLrFxVB) + tid + k * NT];
+        if (c[k] && !pre) row[k] = aff_rows ? row_base + (b << kLrFxVB) + tid + k * NT : vid_row[(b << kLrFxVB) + tid + k * NT];
       }
       if (!pre) {
 #pragma unroll
@@ -2186,7 +2195,9 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
           const float ng2 = wg[k].y + m * m;
           const float step = lr * m;
           const uint64_t rr = pre ? (uint64_t)row_base + (b << kLrFxVB) + tid + k * NT : row[k];
-          *reinterpret_cast<float2 *>(rows + rr * 2) = make_float2(wg[k].x + step / sqrtf(ng2 + fudge), ng2);
+          const float nw = wg[k].x + step / sqrtf(ng2 + fudge);
+          *reinterpret_cast<float2 *>(rows + rr * 2) = make_float2(nw, ng2);
+          if (wmir) wmir[(b << kLrFxVB) + tid + k * NT] = nw;  // the step's dense copy (fid order)
         }
       return;
     }
@@ -2289,11 +2300,21 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
   const uint32_t h = h0 + kk;
   unsigned long long s = 0ull;
   uint32_t c = 0u;
-  if (h < nhot) {
-#pragma unroll 4
-    for (uint32_t blk = rg; blk < hblocks; blk += RG) {
-      s += hsum[(uint64_t)blk * nhot + h];
-      c += hcnt[(uint64_t)blk * nhot + h];
+  if (h < nhot) {  // up to 16 partial rows per thread in flight at once (768 step blocks / 64 groups = 12)
+    for (uint32_t b0 = rg; b0 < hblocks; b0 += 16 * RG) {
+      unsigned long long ps[16];
+      uint32_t pc[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const uint32_t blk = b0 + (uint32_t)u * RG;
+        ps[u] = blk < hblocks ? hsum[(uint64_t)blk * nhot + h] : 0ull;
+        pc[u] = blk < hblocks ? hcnt[(uint64_t)blk * nhot + h] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        s += ps[u];
+        c += pc[u];
+      }
     }
   }
   as[tid] = s;
@@ -2309,9 +2330,17 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
   if (rg == 0 && h < nhot && ac[tid]) {
     if (TO_GRADS)
       rows[vid_row[hrow[h]]] = (float)(((double)(long long)as[tid] * inv_scale) / (double)ac[tid]);
-    else
+    else {
       lr_fx_adagrad(rows + (uint64_t)hrow[h] * 2, (long long)as[tid], ac[tid], lr, fudge, inv_scale);
+      if (wmir) wmir[h] = rows[(uint64_t)hrow[h] * 2];  // hot key q = fid q (affine form)
+    }
   }
+}
+
+// the step's dense weight copy: wmir[fid] = the w of shard row row_base + fid
+__global__ void k_lr_mirror(const float *__restrict__ rows, uint32_t row_base, uint64_t V, float *__restrict__ wmir) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < V) wmir[q] = rows[((uint64_t)row_base + q) * 2];
 }
 
 // every record's fid (the fixed-point step's key numbering)
@@ -2572,6 +2601,12 @@ struct swps_lr {
   swps::DevMem d_fxb_fill, d_fxb_rbase;  // the bucket regions (fxb_res): fill counters, region starts
   bool fxb_res = true;                   // SWPS_LR_FXB_RES=0: the per-chunk bucket segments (round 5)
   bool fxr = true;                       // k_lr_fxr_step (SWPS_LR_FXR=0: k_lr_fxb_step<..., RES>)
+  // the step's dense weight copy by fid (single GPU, k_lr_fxr_step + RES): refreshed from the rows at
+  // the start of every swps_lr_train_batches call (anything else that writes the table — pulls, pushes,
+  // loads — runs between calls), then kept by the push
+  swps::DevMem d_wmir, d_pfb;             // weights by fid; per bucket: prefetch its rows in the push
+  bool fx_mirror = true, mirror_stale = true;
+  int fx_pf = 1;                          // SWPS_LR_FX_PF: 0 no bucket prefetches, 1 dense buckets, 2 all
   uint32_t fxb_gbits = 0;                // chunk groups per bucket region: 2^fxb_gbits
   uint64_t fxb_region_recs = 0;          // the regions' total capacity (records)
   int fx_atomic = 0;
@@ -3324,6 +3359,7 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
     }
     if (const char *er = getenv("SWPS_LR_FXB_RES")) l->fxb_res = atoi(er) != 0;
     if (const char *er = getenv("SWPS_LR_FXR")) l->fxr = atoi(er) != 0;
+    if (const char *em = getenv("SWPS_LR_FX_MIRROR")) l->fx_mirror = atoi(em) != 0;
     if (!l->fx_atomic && l->fxb_res) {
       // the bucket regions: bucket q's region holds any batch's records of its keys — at most the
       // batch's records, and at most the corpus count of its non-hot keys
@@ -3355,6 +3391,15 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
         }
         l->fxb_gbits = (uint32_t)gb;
         if (tot < (1ull << 31) && (tot * 8 <= (4ull << 30) || gb == 0)) break;
+      }
+      if (const char *ep = getenv("SWPS_LR_FX_PF")) l->fx_pf = atoi(ep);
+      {  // prefetch a bucket's rows in the push where a batch touches many of its keys: on average
+         // at least 1,024 non-hot records per batch (of 4,096 keys)
+        std::vector<uint8_t> pf(l->fxb_nbk);
+        for (uint32_t q = 0; q < l->fxb_nbk; q++)
+          pf[q] = l->fx_pf == 2 || (l->fx_pf == 1 && bsum[q] >= 1024ull * std::max<uint64_t>(l->nbatches, 1));
+        SWPS_TRY(upload(l->d_pfb, pf, s));
+        SWPS_HIP(hipStreamSynchronize(s));
       }
       if (tot < (1ull << 31)) {
         const uint64_t nqg = (uint64_t)l->fxb_nbk << l->fxb_gbits;
@@ -3433,6 +3478,13 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
                                               : k_lr_fxb_step<8, 256, false, 512, false>)
                               : (l->fx_affine ? k_lr_fxb_step<8, 256, true, kLrHot, false>
                                               : k_lr_fxb_step<8, 256, false, kLrHot, false>));
+    const bool mir = res && l->fx_affine && l->fxr && l->fx_mirror && !shd;
+    if (mir && l->mirror_stale) {  // the dense weight copy from the rows (swps_lr_train_batches' start)
+      SWPS_TRY(l->d_wmir.ensure(V * 4));
+      k_lr_mirror<<<nblk(V), 256, 0, s>>>(l->t->rows.as<float>(), l->fx_row_base, V, l->d_wmir.as<float>());
+      SWPS_HIP(hipGetLastError());
+      l->mirror_stale = false;
+    }
     if (res && l->fx_affine && l->fxr) {  // the branch-free form (bit-identical)
       auto *kr = rpt == 16 ? (nh <= 512 ? k_lr_fxr_step<16, 256, 512> : k_lr_fxr_step<16, 256, kLrHot>)
                            : (nh <= 512 ? k_lr_fxr_step<8, 256, 512> : k_lr_fxr_step<8, 256, kLrHot>);
@@ -3444,7 +3496,8 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
                             hot ? nh : 0u, l->d_err.as<float>(), l->d_err2.as<float>(), scale, l->fxb_nbk,
                             l->d_fxb_rec.as<uint2>(), l->d_fxb_hsum.as<unsigned long long>(),
                             l->d_fxb_hcnt.as<uint32_t>(), l->fx_row_base, l->d_fxb_fill.as<uint32_t>(),
-                            (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), l->fxb_gbits, l->fxb_diag);
+                            (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), l->fxb_gbits,
+                            mir ? (const float *)l->d_wmir.as<float>() : (const float *)nullptr, l->fxb_diag);
     } else
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(nt), dyn, s, fb, fe, 0,
                           (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
@@ -3480,7 +3533,9 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
                           l->t->cfg.learning_rate, l->t->cfg.fudge, scale, std::ldexp(1.0, -l->fx_bits),
                           (uint32_t)l->fx_affine, l->fx_row_base, pb0, bper, l->d_fxb_fill.as<uint32_t>(),
                           (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), (uint32_t)l->vocab_keys.size(),
-                          l->fxb_gbits, l->fxb_diag);
+                          l->fxb_gbits, mir ? l->d_wmir.as<float>() : (float *)nullptr,
+                          res && l->fx_pf != 2 ? (const uint8_t *)l->d_pfb.as<uint8_t>() : (const uint8_t *)nullptr,
+                          l->fxb_diag);
     SWPS_HIP(hipGetLastError());
     l->timer.ext_end(3, ab, ae);
     return SWPS_OK;
@@ -4184,6 +4239,7 @@ int swps_lr_train_batches(swps_lr *l, uint64_t count) {
   if (!l->inited) return fail(SWPS_E_STATE, "call swps_lr_init first");
   if (l->nbatches == 0) return SWPS_OK;
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
+  l->mirror_stale = true;  // the table may have been written since the last call
   for (uint64_t i = 0; i < count; i++) SWPS_TRY(lr_batch(l));
   return SWPS_OK;
 }

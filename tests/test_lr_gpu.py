@@ -610,20 +610,23 @@ def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
     vals = rng.random(int(roff[-1])).astype(np.float32)
     yl = (rng.random(4000) < 0.5).astype(np.float32)
     res = []
-    # (plan, atomic form, rows placed by fid, bucket regions: SWPS_LR_FXB_RES=0 is round 5's per-chunk
-    # bucket segments)
-    # bucket regions, chunk groups per region: SWPS_LR_FXB_GBITS; the branch-free step kernel
-    # k_lr_fxr_step, SWPS_LR_FXR=0: k_lr_fxb_step)
-    for plan, atomic, affine, bres, gbits, fxr in (
-            ("load", "0", "1", "1", "3", "1"), ("none", "0", "1", "1", "3", "1"), ("none", "0", "1", "1", "3", "1"),
-            ("none", "1", "1", "1", "3", "1"), ("none", "0", "0", "1", "3", "1"), ("none", "0", "1", "0", "3", "1"),
-            ("none", "0", "0", "0", "3", "1"), ("none", "0", "1", "1", "0", "1"), ("none", "0", "0", "1", "1", "1"),
-            ("none", "0", "1", "1", "3", "0")):
-        monkeypatch.setenv("SWPS_LR_FX_ATOMIC", atomic)
-        monkeypatch.setenv("SWPS_LR_FX_AFFINE", affine)
-        monkeypatch.setenv("SWPS_LR_FXB_RES", bres)
-        monkeypatch.setenv("SWPS_LR_FXB_GBITS", gbits)
-        monkeypatch.setenv("SWPS_LR_FXR", fxr)
+    # variants (env over the default, the bucketed fixed-point step): the sorted fp64 sums (plan load);
+    # run to run; the per-record atomic form; rows not placed by fid (gathered key codes); round 5's
+    # per-chunk bucket segments (SWPS_LR_FXB_RES=0) with and without placement; one / two chunk
+    # groups per bucket region; k_lr_fxb_step instead of the branch-free k_lr_fxr_step; the step's
+    # weights from the rows instead of the dense copy by fid; the push prefetching no / every
+    # bucket's rows
+    base = dict(SWPS_LR_FX_ATOMIC="0", SWPS_LR_FX_AFFINE="1", SWPS_LR_FXB_RES="1", SWPS_LR_FXB_GBITS="3",
+                SWPS_LR_FXR="1", SWPS_LR_FX_MIRROR="1", SWPS_LR_FX_PF="1")
+    variants = [("load", {}), ("none", {}), ("none", {}), ("none", dict(SWPS_LR_FX_ATOMIC="1")),
+                ("none", dict(SWPS_LR_FX_AFFINE="0")), ("none", dict(SWPS_LR_FXB_RES="0")),
+                ("none", dict(SWPS_LR_FXB_RES="0", SWPS_LR_FX_AFFINE="0")), ("none", dict(SWPS_LR_FXB_GBITS="0")),
+                ("none", dict(SWPS_LR_FXB_GBITS="1", SWPS_LR_FX_AFFINE="0")), ("none", dict(SWPS_LR_FXR="0")),
+                ("none", dict(SWPS_LR_FX_MIRROR="0")), ("none", dict(SWPS_LR_FX_PF="0")),
+                ("none", dict(SWPS_LR_FX_PF="2"))]
+    for plan, env in variants:
+        for k, val in dict(base, **env).items():
+            monkeypatch.setenv(k, val)
         out = []
         for data, B in (((y, off, f, v), 4095), ((yl, roff, feat, vals), 700)):
             t = lib.Table("lr", capacity=1 << 18, dtype="f32", learning_rate=0.05, init="hash", seed=1)
