@@ -447,13 +447,47 @@ void ev_resolve(swps_s2v *m) {
 // run-length unigram^0.75 table of word2vec.h:398-425 over a vocab in std::map
 // (ascending key) order: word i owns slots [st[i], st[i+1]).  The literal walk
 // moves to word i+1 after the first slot a with a/T > d1_i.
+// pow(c, 0.75) of the small counts most words have, computed once (the same std::pow call: the same bits)
+struct Pow75 {
+  double t[4096];
+  Pow75() {
+    for (int c = 0; c < 4096; c++) t[c] = std::pow(c, 0.75);
+  }
+  double operator()(int32_t c) const { return c >= 0 && c < 4096 ? t[c] : std::pow(c, 0.75); }
+};
+const Pow75 &pow75() {
+  static const Pow75 p;
+  return p;
+}
+
+// (key, count) by key, ascending — std::sort's order for distinct keys — as an LSD radix sort of
+// 8-bit digits that skips the digits every key shares
+void s2v_sort_by_key(std::vector<std::pair<uint64_t, int32_t>> &a, std::vector<std::pair<uint64_t, int32_t>> &tmp) {
+  const size_t n = a.size();
+  tmp.resize(n);
+  for (int sh = 0; sh < 64; sh += 8) {
+    size_t h[256] = {0};
+    for (auto &x : a) h[(x.first >> sh) & 255]++;
+    if (h[(a.empty() ? 0 : a[0].first >> sh) & 255] == n) continue;
+    size_t o = 0;
+    for (int b = 0; b < 256; b++) {
+      const size_t c = h[b];
+      h[b] = o;
+      o += c;
+    }
+    for (auto &x : a) tmp[h[(x.first >> sh) & 255]++] = x;
+    a.swap(tmp);
+  }
+}
+
 void s2v_unigram_starts(const std::vector<std::pair<uint64_t, int32_t>> &vc, uint64_t T, std::vector<uint64_t> &st) {
   const size_t V = vc.size();
+  const Pow75 &P = pow75();
   double pw = 0;
-  for (auto &kc : vc) pw += std::pow(kc.second, 0.75);
+  for (auto &kc : vc) pw += P(kc.second);
   st.assign(V + 1, T);
   st[0] = 0;
-  double d1 = std::pow(vc[0].second, 0.75) / (double)pw;
+  double d1 = P(vc[0].second) / (double)pw;
   for (size_t i = 0; i + 1 < V; i++) {
     const uint64_t lo = st[i];
     auto pred = [&](uint64_t a) { return (int64_t)a / (double)T > d1; };
@@ -463,7 +497,7 @@ void s2v_unigram_starts(const std::vector<std::pair<uint64_t, int32_t>> &vc, uin
     while (a < T && !pred(a)) a++;
     if (a >= T) break;  // word i runs to the end; later words get no slots
     st[i + 1] = a + 1;
-    d1 += std::pow(vc[i + 1].second, 0.75) / (double)pw;
+    d1 += P(vc[i + 1].second) / (double)pw;
   }
 }
 
@@ -530,14 +564,28 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   std::vector<uint8_t> valid(nl);
   for (uint64_t l = 0; l < nl; l++)
     valid[l] = (int64_t)(line_off[l + 1] - line_off[l]) >= (int64_t)m->cfg.min_sentence_length;
-  // keys the server already holds (the loaded word vectors)
+  // keys the server already holds (the loaded word vectors): the map is filled by a thread beside
+  // the plan workers (they need it only for their last step, the keys the table lacks)
   uint64_t have = 0, got = 0;
   SWPS_TRY(swps_table_size(m->t, &have));
   std::vector<uint64_t> tk(std::max<uint64_t>(have, 1));
   SWPS_TRY(swps_table_keys(m->t, tk.data(), tk.size(), &got));
+  phase("table keys");
   FlatMap64 present(got + 1024);
-  for (uint64_t i = 0; i < got; i++) present.at(tk[i]) = 1;
-  phase("table keys + present map");
+  std::atomic<int> present_ready{0};
+  std::thread present_th([&] {
+    for (uint64_t i = 0; i < got; i++) present.at(tk[i]) = 1;
+    present_ready.store(1, std::memory_order_release);
+  });
+  struct JoinOne {
+    std::thread &t;
+    ~JoinOne() {
+      if (t.joinable()) t.join();
+    }
+  } join_present{present_th};
+  auto wait_present = [&] {
+    while (!present_ready.load(std::memory_order_acquire)) std::this_thread::yield();
+  };
   // the rand() stream: the draws nobody reads (the WParam a pull constructs for a key the server
   // already holds, server.h:143-150) are counted and skipped in one jump before the next read
   GlibcRand rnd(m->cfg.rand_seed);
@@ -554,7 +602,6 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   std::vector<uint64_t> miss_keys;
   std::vector<double> miss_rows;     // [h | v | h2 = 0 | v2 = 0] per miss
   std::unordered_set<uint64_t> lk;   // MiniBatch::_local_keys: one object, cleared per minibatch
-  uint64_t lk_max = 0;               // the largest key set inserted into it so far
   std::vector<uint64_t> vocab_keys;  // concatenated minibatch vocabs (std::map order)
   std::vector<uint64_t> starts_all;
   std::vector<uint64_t> rand_chunks;  // the sentences' rand() outputs: {destination, stream index, count}
@@ -590,12 +637,14 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   std::atomic<bool> quit{false};
   std::vector<std::thread> workers;
   {
-    int nth = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    // 12 plan workers (16 on the GPU boxes' CPU share measured 1.8e8 words/s single-pass, 12 2.0e8,
+    // 8 1.9e8: the pass below, the group uploads and the runtime's threads need cores too)
+    int nth = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
     if (const char *e = getenv("SWPS_S2V_THREADS")) nth = std::max(1, atoi(e));
     nth = (int)std::min<uint64_t>((uint64_t)nth, std::max<uint64_t>(K, 1));
     auto work = [&]() {
       FlatMap64 fq(1 << 16);
-      std::vector<std::pair<uint64_t, int32_t>> vc;
+      std::vector<std::pair<uint64_t, int32_t>> vc, vtmp;
       for (uint64_t k; !quit.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < K;) {
         Plan &pl = plan[k];
         fq.clear();
@@ -616,11 +665,11 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
         }
         pl.zero = fq.contains(0);
         vc.clear();
-        for (uint64_t key : pl.first) {
-          vc.emplace_back(key, fq.at(key));
+        for (uint64_t key : pl.first) vc.emplace_back(key, fq.at(key));
+        s2v_sort_by_key(vc, vtmp);
+        wait_present();
+        for (uint64_t key : pl.first)
           if (!present.contains(key)) pl.cand.push_back(key);
-        }
-        std::sort(vc.begin(), vc.end());
         s2v_unigram_starts(vc, T, pl.st);
         pl.vkeys.resize(vc.size());
         for (size_t q = 0; q < vc.size(); q++) pl.vkeys[q] = vc[q].first;
@@ -667,13 +716,15 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       }
     ndmax += kdoc[k];
   }
-  // pipeline groups: 2, 4, then 8 minibatches (at most group_docs documents), so the first group
-  // trains early while the later ones are planned
+  // pipeline groups: 2, 4, then 8 minibatches (at most group_docs documents), the last ones 4 and
+  // 2 again, so the first group trains early while the later ones are planned and little is left
+  // to train after the last plan
   std::vector<uint64_t> gend;
   uint64_t grec_max = 0;
   for (uint64_t k0 = 0, gsz = 2; k0 < K; gsz = std::min<uint64_t>(8, 2 * gsz)) {
+    const uint64_t lim = K - k0 <= 6 ? std::min<uint64_t>(gsz, K - k0 <= 2 ? 2 : 4) : gsz;
     uint64_t k1 = k0 + 1, docs = kdoc[k0], recs = krec[k0];
-    while (k1 < K && k1 - k0 < gsz && docs + kdoc[k1] <= m->group_docs) {
+    while (k1 < K && k1 - k0 < lim && docs + kdoc[k1] <= m->group_docs) {
       docs += kdoc[k1];
       recs += krec[k1];
       k1++;
@@ -834,8 +885,14 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     return SWPS_OK;
   };
   size_t gi = 0;
+  wait_present();
+  double t_wait = 0, t_flush = 0;  // SWPS_S2V_LOAD_TIMES: the pass's time waiting for plans, in flushes
   for (uint64_t k = 0; k < K; k++) {
-    wait_plan(k);
+    {
+      const double a = tm ? now() : 0;
+      wait_plan(k);
+      if (tm) t_wait += now() - a;
+    }
     Plan &pl = plan[k];
     const std::vector<uint64_t> &first_seen = pl.first;
     const uint64_t li = k * (uint64_t)(B + 1);
@@ -847,19 +904,20 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     // order; a miss is inserted with it (server.h:143-150, accessmethod.h:63-70).  Only the misses'
     // draws are read, so a minibatch without misses skips 2·D per key in one jump.  `_local_keys`
     // is one std::unordered_set cleared per minibatch: its iteration order depends on its bucket
-    // count, which depends only on the largest key set inserted so far (clear() keeps the buckets;
-    // libstdc++ grows them only when a count passes that maximum) — so the set is filled, in the
-    // reference's insertion order, only for a minibatch with misses or a new largest key set
+    // count, which depends only on the key counts inserted so far (clear() keeps the buckets;
+    // libstdc++'s prime rehash policy grows them only when an insert takes the element count past
+    // the bucket count, at max_load_factor 1) — so the set is filled, in the reference's insertion
+    // order, only for a minibatch with misses (its iteration is read) or one whose key count would
+    // grow the buckets
     bool miss = false;
     for (uint64_t key : pl.cand)
       if (!inserted.contains(key)) {
         miss = true;
         break;
       }
-    if (miss || first_seen.size() > lk_max) {
+    if (miss || lk.bucket_count() <= 1 || first_seen.size() > lk.bucket_count()) {  // (a new set grows at once)
       lk.clear();
       for (uint64_t key : first_seen) lk.insert(key);
-      lk_max = std::max<uint64_t>(lk_max, first_seen.size());
     }
     if (!miss) skip += 2 * (uint64_t)D * first_seen.size();
     for (uint64_t key : lk) {
@@ -906,12 +964,15 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
     m->batches.push_back(b);
     if (gi < gend.size() && k + 1 == gend[gi]) {
+      const double a = tm ? now() : 0;
       SWPS_TRY(flush(k + 1));
+      if (tm) t_flush += now() - a;
       gi++;
     }
   }
   quit.store(true);  // plans past the corpus end (sent2vec.cpp:97) are not needed
   SWPS_TRY(flush(m->batches.size()));
+  if (tm) fprintf(stderr, "[s2v load]   of which waiting for plans %.3f s, group uploads + launches %.3f s\n", t_wait, t_flush);
   phase("minibatch vocabs + schedule + groups (host)");
   m->lstate_end = lstate;
   rnd.discard(skip);
