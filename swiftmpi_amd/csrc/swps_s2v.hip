@@ -572,9 +572,20 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   SWPS_TRY(swps_table_keys(m->t, tk.data(), tk.size(), &got));
   phase("table keys");
   FlatMap64 present(got + 1024);
+  // and the keys' order: rank_of_row[row] = the rank of row's key among the table's keys (tk lists
+  // the keys by row), row_of_rank its inverse — a plan orders a minibatch's vocabulary by marking
+  // ranks in a bitmap instead of sorting keys
+  std::vector<uint32_t> rank_of_row(got), row_of_rank(got);
   std::atomic<int> present_ready{0};
   std::thread present_th([&] {
     for (uint64_t i = 0; i < got; i++) present.at(tk[i]) = 1;
+    std::vector<std::pair<uint64_t, int32_t>> kr(got), tmp;
+    for (uint64_t i = 0; i < got; i++) kr[i] = {tk[i], (int32_t)i};
+    s2v_sort_by_key(kr, tmp);
+    for (uint64_t q = 0; q < got; q++) {
+      row_of_rank[q] = (uint32_t)kr[q].second;
+      rank_of_row[kr[q].second] = (uint32_t)q;
+    }
     present_ready.store(1, std::memory_order_release);
   });
   struct JoinOne {
@@ -602,8 +613,7 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   std::vector<uint64_t> miss_keys;
   std::vector<double> miss_rows;     // [h | v | h2 = 0 | v2 = 0] per miss
   std::unordered_set<uint64_t> lk;   // MiniBatch::_local_keys: one object, cleared per minibatch
-  std::vector<uint64_t> vocab_keys;  // concatenated minibatch vocabs (std::map order)
-  std::vector<uint64_t> starts_all;
+  uint64_t nvocab = 0, nstarts = 0;  // the minibatch vocabs (std::map order) and run starts so far (on the device)
   std::vector<uint64_t> rand_chunks;  // the sentences' rand() outputs: {destination, stream index, count}
   std::vector<uint32_t> doc_line;   // sentence -> its line
   uint64_t doc_ntok = 0;
@@ -636,6 +646,58 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   std::atomic<uint64_t> next{0};
   std::atomic<bool> quit{false};
   std::vector<std::thread> workers;
+  // every token's table row at load (kNoRow: a key the table lacks), fetched by a thread in chunks
+  // of whole lines — the caller's keys to the device (they stay there for the documents' rows), a
+  // probe, the rows back — so the plans count by row in dense arrays and wait only for their lines
+  const uint64_t ntok_all = line_off[nl];
+  DevMem d_keys_all, d_all_row;
+  SWPS_TRY(d_keys_all.ensure(std::max<uint64_t>(ntok_all, 1) * 8));
+  SWPS_TRY(d_all_row.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
+  std::vector<uint32_t> rows_h(ntok_all);
+  std::atomic<uint64_t> rows_upto{0};
+  std::atomic<int> fetch_rc{SWPS_OK};
+  std::atomic<bool> fetch_stop{false};  // set only on the way out (the groups need every line's rows)
+  std::thread fetch_th([&] {
+    hipStream_t fs = nullptr;
+    int rc = hipSetDevice(m->t->cfg.device) == hipSuccess && hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) == hipSuccess
+                 ? SWPS_OK : SWPS_E_HIP;
+    uint64_t l0 = 0, chunk = 1 << 20;  // the first chunks small: the first plans start early
+    while (rc == SWPS_OK && l0 < nl && !fetch_stop.load(std::memory_order_relaxed)) {
+      uint64_t l1 = l0 + 1;
+      while (l1 < nl && line_off[l1] - line_off[l0] < chunk) l1++;
+      const uint64_t t0 = line_off[l0], t1 = line_off[l1];
+      if (t1 > t0 && (hipMemcpyAsync(d_keys_all.as<uint64_t>() + t0, tok_keys + t0, (t1 - t0) * 8,
+                                     hipMemcpyHostToDevice, fs) != hipSuccess ||
+                      table_probe(m->t, d_keys_all.as<uint64_t>() + t0, t1 - t0, d_all_row.as<uint32_t>() + t0, fs) ||
+                      hipMemcpyAsync(rows_h.data() + t0, d_all_row.as<uint32_t>() + t0, (t1 - t0) * 4,
+                                     hipMemcpyDeviceToHost, fs) != hipSuccess ||
+                      hipStreamSynchronize(fs) != hipSuccess))
+        rc = SWPS_E_HIP;
+      rows_upto.store(t1, std::memory_order_release);
+      l0 = l1;
+      chunk = std::min<uint64_t>(chunk * 2, 8u << 20);
+    }
+    if (fs) (void)hipStreamDestroy(fs);
+    if (rc != SWPS_OK) {
+      fetch_rc.store(rc);
+      rows_upto.store(~0ull, std::memory_order_release);  // nobody waits forever
+    }
+  });
+  struct JoinFetch {
+    std::thread &t;
+    std::atomic<bool> &q;
+    ~JoinFetch() {
+      q.store(true);
+      if (t.joinable()) t.join();
+    }
+  } join_fetch{fetch_th, fetch_stop};
+  auto wait_rows = [&](uint64_t t) {
+    for (unsigned it = 0; rows_upto.load(std::memory_order_acquire) < t; it++)
+      if (it < 64)
+        std::this_thread::yield();
+      else
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+  };
   {
     // 12 plan workers (16 on the GPU boxes' CPU share measured 1.8e8 words/s single-pass, 12 2.0e8,
     // 8 1.9e8: the pass below, the group uploads and the runtime's threads need cores too)
@@ -643,19 +705,49 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     if (const char *e = getenv("SWPS_S2V_THREADS")) nth = std::max(1, atoi(e));
     nth = (int)std::min<uint64_t>((uint64_t)nth, std::max<uint64_t>(K, 1));
     auto work = [&]() {
-      FlatMap64 fq(1 << 16);
-      std::vector<std::pair<uint64_t, int32_t>> vc, vtmp;
+      // counts by row in dense arrays (a generation stamp per row instead of clearing); keys the
+      // table lacks (row kNoRow: the minibatch's pull inserts them) in a hash map
+      FlatMap64 fq(1 << 10);
+      std::vector<uint32_t> stamp(std::max<uint64_t>(got, 1), 0), bits((got + 31) / 32 + 1, 0);
+      std::vector<int32_t> cntr(std::max<uint64_t>(got, 1), 0);
+      std::vector<std::pair<uint64_t, int32_t>> vc, va, vtmp;
+      std::vector<uint32_t> prow;  // the minibatch's present rows, first-seen order
+      uint32_t gen = 0;
       for (uint64_t k; !quit.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < K;) {
         Plan &pl = plan[k];
         fq.clear();
+        if (++gen == 0) {
+          std::fill(stamp.begin(), stamp.end(), 0u);
+          gen = 1;
+        }
+        bool zero = false;
         int cnt = 0;
+        prow.clear();
         for (uint64_t j = k * (uint64_t)(B + 1); j < nl;) {
           const uint64_t l = j++;
           if (!valid[l]) continue;
+          wait_rows(line_off[l + 1]);
           for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) {
-            bool fresh = false;
-            fq.at(tok_keys[i], &fresh)++;
-            if (fresh) pl.first.push_back(tok_keys[i]);
+            const uint32_t r = rows_h[i];
+            const uint64_t key = tok_keys[i];
+            zero |= key == 0;
+            if (r != kNoRow && r < got) {
+              if (stamp[r] != gen) {
+                stamp[r] = gen;
+                cntr[r] = 1;
+                pl.first.push_back(key);
+                prow.push_back(r);
+              } else {
+                cntr[r]++;
+              }
+            } else {
+              bool fresh = false;
+              fq.at(key, &fresh)++;
+              if (fresh) {
+                pl.first.push_back(key);
+                pl.cand.push_back(key);  // absent from the table at load, first-occurrence order
+              }
+            }
           }
           if (++cnt > B) break;
         }
@@ -663,13 +755,39 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
           ready[k].store(1, std::memory_order_release);
           continue;
         }
-        pl.zero = fq.contains(0);
-        vc.clear();
-        for (uint64_t key : pl.first) vc.emplace_back(key, fq.at(key));
-        s2v_sort_by_key(vc, vtmp);
+        pl.zero = zero;
+        // std::map order: the present keys by rank (a bitmap of ranks), merged with the absent
+        // ones (few; sorted) — the same (key, count) sequence as sorting every pair by key
         wait_present();
-        for (uint64_t key : pl.first)
-          if (!present.contains(key)) pl.cand.push_back(key);
+        vc.clear();
+        va.clear();
+        for (uint64_t key : pl.cand) va.emplace_back(key, fq.at(key));
+        s2v_sort_by_key(va, vtmp);
+        uint64_t lo = ~0ull, hi = 0;
+        const size_t npres = prow.size();
+        vc.reserve(pl.first.size());
+        {
+          for (uint32_t r : prow) {  // the present rows' ranks
+            const uint32_t q = rank_of_row[r];
+            bits[q >> 5] |= 1u << (q & 31);
+            lo = std::min<uint64_t>(lo, q >> 5);
+            hi = std::max<uint64_t>(hi, q >> 5);
+          }
+          size_t ia = 0;
+          for (uint64_t w = lo; npres && w <= hi; w++) {
+            uint32_t b = bits[w];
+            bits[w] = 0;
+            while (b) {
+              const uint32_t q = (uint32_t)(w << 5) + (uint32_t)__builtin_ctz(b);
+              b &= b - 1;
+              const uint32_t r = row_of_rank[q];
+              const uint64_t key = tk[r];
+              while (ia < va.size() && va[ia].first < key) vc.push_back(va[ia++]);
+              vc.emplace_back(key, cntr[r]);
+            }
+          }
+          while (ia < va.size()) vc.push_back(va[ia++]);
+        }
         s2v_unigram_starts(vc, T, pl.st);
         pl.vkeys.resize(vc.size());
         for (size_t q = 0; q < vc.size(); q++) pl.vkeys[q] = vc[q].first;
@@ -733,10 +851,8 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     grec_max = std::max(grec_max, recs);
     k0 = k1;
   }
-  const uint64_t ntok_all = line_off[nl], nchunk_max = ndmax * (uint64_t)D / kRandRun + K + 1;
-  std::vector<uint64_t> vocab_keys_r, starts_r, rand_r;
-  vocab_keys.reserve(wtok);
-  starts_all.reserve(wtok + K);
+  const uint64_t nchunk_max = ndmax * (uint64_t)D / kRandRun + K + 1;
+
   rand_chunks.reserve(3 * nchunk_max);
   doc_line.reserve(ndmax);
   m->doc_id.reserve(ndmax);
@@ -746,7 +862,7 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   doc_batch.reserve(ndmax);
   std::vector<uint64_t> bv0(K), bs0(K);
   std::vector<uint32_t> bU(K);
-  DevMem d_vkeys, d_keys_all, d_all_row, d_line_off, d_doc_line, d_chunks, d_base;
+  DevMem d_vkeys, d_line_off, d_doc_line, d_chunks, d_base;
   SWPS_TRY(d_vkeys.ensure(std::max<uint64_t>(wtok, 1) * 8));
   SWPS_TRY(m->d_vocab_row.ensure(std::max<uint64_t>(wtok, 1) * 4));
   SWPS_TRY(m->d_starts.ensure((wtok + K + 1) * 8));
@@ -763,8 +879,6 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   SWPS_TRY(m->d_err.ensure(std::max<uint64_t>(ndmax, 1) * 4));
   SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(grec_max, 1) * (uint64_t)S * 4));
   SWPS_TRY(m->d_tok_row.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
-  SWPS_TRY(d_keys_all.ensure(std::max<uint64_t>(ntok_all, 1) * 8));
-  SWPS_TRY(d_all_row.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
   SWPS_TRY(d_line_off.ensure((nl + 1) * 8));
   SWPS_TRY(d_chunks.ensure(3 * nchunk_max * 8));
   {
@@ -821,20 +935,26 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     }
     hipStream_t q = ls.s;
     const swps_s2v::Batch &b0 = m->batches[kf], &b1 = m->batches[k1 - 1];
-    const uint64_t v0 = b0.v0, v1 = b1.v0 + b1.U, s0 = b0.s0, s1 = starts_all.size(), d0 = b0.d0, d1 = b1.d1;
+    const uint64_t v0 = b0.v0, v1 = b1.v0 + b1.U, d0 = b0.d0, d1 = b1.d1;
     for (uint64_t k = kf; k < k1; k++) {
       bv0[k] = m->batches[k].v0;
       bs0[k] = m->batches[k].s0;
       bU[k] = m->batches[k].U;
+      // each minibatch's vocabulary and run starts straight from its plan (a pageable copy is staged
+      // before the call returns: the plan's vectors can go)
+      Plan &pk = plan[k];
+      if (!pk.vkeys.empty())
+        SWPS_HIP(hipMemcpyAsync(d_vkeys.as<uint64_t>() + bv0[k], pk.vkeys.data(), pk.vkeys.size() * 8,
+                                hipMemcpyHostToDevice, q));
+      if (!pk.st.empty())
+        SWPS_HIP(hipMemcpyAsync(m->d_starts.as<uint64_t>() + bs0[k], pk.st.data(), pk.st.size() * 8,
+                                hipMemcpyHostToDevice, q));
+      SWPS_HIP(hipStreamSynchronize(q));  // (staged already; to be safe before the vectors go)
+      std::vector<uint64_t>().swap(pk.vkeys);
+      std::vector<uint64_t>().swap(pk.st);
     }
-    if (v1 > v0) {
-      SWPS_HIP(hipMemcpyAsync(d_vkeys.as<uint64_t>() + v0, vocab_keys.data() + v0, (v1 - v0) * 8,
-                              hipMemcpyHostToDevice, q));
+    if (v1 > v0)
       SWPS_TRY(table_lookup(m->t, d_vkeys.as<uint64_t>() + v0, v1 - v0, m->d_vocab_row.as<uint32_t>() + v0, q));
-    }
-    if (s1 > s0)
-      SWPS_HIP(hipMemcpyAsync(m->d_starts.as<uint64_t>() + s0, starts_all.data() + s0, (s1 - s0) * 8,
-                              hipMemcpyHostToDevice, q));
     SWPS_HIP(hipMemcpyAsync(m->d_bv0.as<uint64_t>() + kf, bv0.data() + kf, (k1 - kf) * 8, hipMemcpyHostToDevice, q));
     SWPS_HIP(hipMemcpyAsync(m->d_bs0.as<uint64_t>() + kf, bs0.data() + kf, (k1 - kf) * 8, hipMemcpyHostToDevice, q));
     SWPS_HIP(hipMemcpyAsync(m->d_bU.as<uint32_t>() + kf, bU.data() + kf, (k1 - kf) * 4, hipMemcpyHostToDevice, q));
@@ -849,15 +969,15 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
                               hipMemcpyHostToDevice, q));
       SWPS_HIP(hipMemcpyAsync(d_doc_line.as<uint32_t>() + d0, doc_line.data() + d0, (d1 - d0) * 4,
                               hipMemcpyHostToDevice, q));
-      // the group's lines' token keys (read in place from the caller's array) -> rows -> documents
+      // the group's lines' token rows: probed by the fetch thread at load; again once the pulls
+      // inserted keys (their rows exist only now).  Probed, not looked up: a short line's keys
+      // (read, never gathered) may be absent; the documents' keys are all in their minibatches'
+      // vocabularies, whose lookup above latches
       const uint64_t la = kf * (uint64_t)(B + 1), lb = std::min<uint64_t>(nl, k1 * (uint64_t)(B + 1));
       const uint64_t t0 = line_off[la], t1 = line_off[lb];
-      if (t1 > t0) {
-        SWPS_HIP(hipMemcpyAsync(d_keys_all.as<uint64_t>() + t0, tok_keys + t0, (t1 - t0) * 8, hipMemcpyHostToDevice, q));
-        // probed, not looked up: a short line's keys (read, never gathered) may be absent; the
-        // documents' keys are all in their minibatches' vocabularies, whose lookup above latches
+      wait_rows(t1);  // (the plans of these minibatches waited for them already)
+      if (t1 > t0 && !miss_keys.empty())
         SWPS_TRY(table_probe(m->t, d_keys_all.as<uint64_t>() + t0, t1 - t0, d_all_row.as<uint32_t>() + t0, q));
-      }
       k_s2v_doc_rows<<<(unsigned)(((d1 - d0) * 64 + 255) / 256), 256, 0, q>>>(
           d_all_row.as<uint32_t>(), d_line_off.as<uint64_t>(), d_doc_line.as<uint32_t>() + d0,
           m->d_doc_tok.as<uint64_t>() + d0, d1 - d0, m->d_tok_row.as<uint32_t>());
@@ -886,7 +1006,9 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   };
   size_t gi = 0;
   wait_present();
+  std::vector<std::pair<uint64_t, uint64_t>> jmp;  // per document length: (A^k, c (A^k - 1) / (A - 1))
   double t_wait = 0, t_flush = 0;  // SWPS_S2V_LOAD_TIMES: the pass's time waiting for plans, in flushes
+  double t_lk = 0, t_vocab = 0, t_docs = 0;  // ... refilling _local_keys, appending vocabularies, documents
   for (uint64_t k = 0; k < K; k++) {
     {
       const double a = tm ? now() : 0;
@@ -915,10 +1037,12 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
         miss = true;
         break;
       }
+    const double tb0 = tm ? now() : 0;
     if (miss || lk.bucket_count() <= 1 || first_seen.size() > lk.bucket_count()) {  // (a new set grows at once)
       lk.clear();
       for (uint64_t key : first_seen) lk.insert(key);
     }
+    if (tm) t_lk += now() - tb0;
     if (!miss) skip += 2 * (uint64_t)D * first_seen.size();
     for (uint64_t key : lk) {
       if (!miss) break;
@@ -934,12 +1058,13 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       inserted.at(key) = 1;
       m->misses++;
     }
-    swps_s2v::Batch b{m->doc_id.size(), 0, vocab_keys.size(), starts_all.size(), (uint32_t)pl.vkeys.size(), 0};
-    vocab_keys.insert(vocab_keys.end(), pl.vkeys.begin(), pl.vkeys.end());
-    starts_all.insert(starts_all.end(), pl.st.begin(), pl.st.end());
+    const double tb1 = tm ? now() : 0;
+    swps_s2v::Batch b{m->doc_id.size(), 0, nvocab, nstarts, (uint32_t)pl.vkeys.size(), 0};
+    nvocab += pl.vkeys.size();
+    nstarts += pl.st.size();
     std::vector<uint64_t>().swap(pl.first);
-    std::vector<uint64_t>().swap(pl.vkeys);
-    std::vector<uint64_t>().swap(pl.st);
+    if (tm) t_vocab += now() - tb1;
+    const double tb2 = tm ? now() : 0;
     // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not; the sentences' Vec::random
     // draws are this minibatch's next run of the stream (drawn on the device, k_s2v_rand)
     const uint64_t run_o = 344 + rnd.produced + skip, run_d0 = m->doc_id.size();
@@ -953,7 +1078,14 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       m->doc_rec.push_back(m->doc_rec.back() + L * (uint64_t)m->cfg.niters);
       skip += (uint64_t)D;
       m->doc_lcg.push_back(lstate);
-      lstate = lcg_jump(lstate, (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1)), kLcgA, kLcgC);
+      // the LCG's jump over a document: the same multiplier and increment for every length L
+      // (lcg_jump(x, k) = A^k x + c(A^k - 1)/(A - 1)), cached per L
+      if (L >= jmp.size()) jmp.resize(L + 1, {0, 0});
+      if (!jmp[L].first) {
+        const uint64_t kk = (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1));
+        jmp[L] = {lcg_jump(1, kk, kLcgA, kLcgC) - lcg_jump(0, kk, kLcgA, kLcgC), lcg_jump(0, kk, kLcgA, kLcgC)};
+      }
+      lstate = jmp[L].first * lstate + jmp[L].second;
     }
     b.d1 = m->doc_id.size();
     for (uint64_t q = 0, tot = (b.d1 - run_d0) * (uint64_t)D; q < tot; q += kRandRun)
@@ -963,6 +1095,7 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     m->max_recs = std::max(m->max_recs, b.recs);
     m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
     m->batches.push_back(b);
+    if (tm) t_docs += now() - tb2;
     if (gi < gend.size() && k + 1 == gend[gi]) {
       const double a = tm ? now() : 0;
       SWPS_TRY(flush(k + 1));
@@ -971,8 +1104,11 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     }
   }
   quit.store(true);  // plans past the corpus end (sent2vec.cpp:97) are not needed
+  if (fetch_rc.load() != SWPS_OK) return fail(fetch_rc.load(), "sent2vec load: token rows (HIP)");
   SWPS_TRY(flush(m->batches.size()));
-  if (tm) fprintf(stderr, "[s2v load]   of which waiting for plans %.3f s, group uploads + launches %.3f s\n", t_wait, t_flush);
+  if (tm)
+    fprintf(stderr, "[s2v load]   of which waiting for plans %.3f s, group uploads + launches %.3f s, _local_keys %.3f s, "
+                    "vocabularies %.3f s, documents %.3f s\n", t_wait, t_flush, t_lk, t_vocab, t_docs);
   phase("minibatch vocabs + schedule + groups (host)");
   m->lstate_end = lstate;
   rnd.discard(skip);
