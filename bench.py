@@ -844,33 +844,42 @@ def main():
         la.steps, la.warmup = args.app_steps, 3
         set_phase("lr")
         out["lr"] = bench_lr(la, ctx, corpus_batches=10, cpu_rows=10 * (args.lr_batch + 1))
+        if os.environ.get("BENCH_ORDER") != "s2v_first":
+            lr_sharded_base(out, ctx, args, la)
         sa = argparse.Namespace(**vars(args))
         sa.steps, sa.warmup = 31, 31  # one launch of 31 minibatches (swps_s2v group_docs) per pass
         set_phase("s2v")
         out["s2v"] = bench_s2v(sa, ctx, corpus_batches=31)
-        if world == 1 and not ctx.sharded and not args.no_lr_sharded_base:
-            # the N > 1 LR leg runs the key-sharded protocol (owner pull, exchange, install, the step,
-            # the mean-gradient push, owner AdaGrad); its world-1 run is the like-for-like base point
-            # of the scaling curve (lr.value above is the unsharded single-GPU step)
-            set_phase("lr_sharded_world1")
-            sctx = Ctx(True)
-            lb = argparse.Namespace(**vars(la))
-            lb.no_cpu_baseline = True
-            q = bench_lr(lb, sctx, corpus_batches=10)
-            out["lr"]["sharded_world1"] = {
-                "value": q["value"], "unit": q["unit"], "ms_per_step": q["ms_per_step"], "kernel_ms": q["kernel_ms"],
-                "parallelism": q["config"]["parallelism"],
-                "note": "the same workload through the key-sharded protocol at world 1 (no remote bytes): the base "
-                        "point for the N > 1 lr legs, which run this protocol"}
-            sctx.close()
-            if sctx.dist is not None:
-                sctx.dist.destroy_process_group()
+        if os.environ.get("BENCH_ORDER") == "s2v_first":
+            lr_sharded_base(out, ctx, args, la)
     set_phase("report")
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
     if ctx.dist is not None:
         ctx.dist.destroy_process_group()
+
+
+def lr_sharded_base(out, ctx, args, la):
+    """lr.sharded_world1 (N = 1 only): the lr leg's workload through the key-sharded protocol."""
+    if ctx.world != 1 or ctx.sharded or args.no_lr_sharded_base:
+        return
+    # the N > 1 LR leg runs the key-sharded protocol (owner pull, exchange, install, the step,
+    # the mean-gradient push, owner AdaGrad); its world-1 run is the like-for-like base point
+    # of the scaling curve (lr.value above is the unsharded single-GPU step)
+    set_phase("lr_sharded_world1")
+    sctx = Ctx(True)
+    lb = argparse.Namespace(**vars(la))
+    lb.no_cpu_baseline = True
+    q = bench_lr(lb, sctx, corpus_batches=10)
+    out["lr"]["sharded_world1"] = {
+        "value": q["value"], "unit": q["unit"], "ms_per_step": q["ms_per_step"], "kernel_ms": q["kernel_ms"],
+        "parallelism": q["config"]["parallelism"],
+        "note": "the same workload through the key-sharded protocol at world 1 (no remote bytes): the base "
+                "point for the N > 1 lr legs, which run this protocol"}
+    sctx.close()
+    if sctx.dist is not None:
+        sctx.dist.destroy_process_group()
 
 
 def bench_other(args):

@@ -3486,9 +3486,12 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
       l->mirror_stale = false;
     }
     if (res && l->fx_affine && l->fxr) {  // the branch-free form (bit-identical)
-      auto *kr = rpt == 16 ? (nh <= 512 ? k_lr_fxr_step<16, 256, 512> : k_lr_fxr_step<16, 256, kLrHot>)
-                           : (nh <= 512 ? k_lr_fxr_step<8, 256, 512> : k_lr_fxr_step<8, 256, kLrHot>);
-      hipExtLaunchKernelGGL(kr, dim3(grid), dim3(256), (size_t)(l->fxb_nbk + kLrFxDummy) * 4, s, fb, fe, 0,
+      // SWPS_LR_FX_NT=512 with 4,096-record chunks: 512 threads x 8 records (A/B)
+      const bool w512 = l->fx_nt == 512 && l->fwd_rpt == 16;
+      auto *kr = w512 ? (nh <= 512 ? k_lr_fxr_step<8, 512, 512> : k_lr_fxr_step<8, 512, kLrHot>)
+                 : rpt == 16 ? (nh <= 512 ? k_lr_fxr_step<16, 256, 512> : k_lr_fxr_step<16, 256, kLrHot>)
+                             : (nh <= 512 ? k_lr_fxr_step<8, 256, 512> : k_lr_fxr_step<8, 256, kLrHot>);
+      hipExtLaunchKernelGGL(kr, dim3(grid), dim3(w512 ? 512 : 256), (size_t)(l->fxb_nbk + kLrFxDummy) * 4, s, fb, fe, 0,
                             (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
                             (const uint64_t *)l->d_row_off.as<uint64_t>(), (const int32_t *)l->d_ffid.as<int32_t>(),
                             (const float *)l->d_fval.as<float>(), (const float *)l->d_label.as<float>(), r0,

@@ -615,15 +615,15 @@ def test_lr_fixed_point_step(lib, gpu, monkeypatch, hot):
     # per-chunk bucket segments (SWPS_LR_FXB_RES=0) with and without placement; one / two chunk
     # groups per bucket region; k_lr_fxb_step instead of the branch-free k_lr_fxr_step; the step's
     # weights from the rows instead of the dense copy by fid; the push prefetching no / every
-    # bucket's rows
+    # bucket's rows; k_lr_fxr_step with 512 threads x 8 records
     base = dict(SWPS_LR_FX_ATOMIC="0", SWPS_LR_FX_AFFINE="1", SWPS_LR_FXB_RES="1", SWPS_LR_FXB_GBITS="3",
-                SWPS_LR_FXR="1", SWPS_LR_FX_MIRROR="1", SWPS_LR_FX_PF="1")
+                SWPS_LR_FXR="1", SWPS_LR_FX_MIRROR="1", SWPS_LR_FX_PF="1", SWPS_LR_FX_NT="256")
     variants = [("load", {}), ("none", {}), ("none", {}), ("none", dict(SWPS_LR_FX_ATOMIC="1")),
                 ("none", dict(SWPS_LR_FX_AFFINE="0")), ("none", dict(SWPS_LR_FXB_RES="0")),
                 ("none", dict(SWPS_LR_FXB_RES="0", SWPS_LR_FX_AFFINE="0")), ("none", dict(SWPS_LR_FXB_GBITS="0")),
                 ("none", dict(SWPS_LR_FXB_GBITS="1", SWPS_LR_FX_AFFINE="0")), ("none", dict(SWPS_LR_FXR="0")),
                 ("none", dict(SWPS_LR_FX_MIRROR="0")), ("none", dict(SWPS_LR_FX_PF="0")),
-                ("none", dict(SWPS_LR_FX_PF="2"))]
+                ("none", dict(SWPS_LR_FX_PF="2")), ("none", dict(SWPS_LR_FX_NT="512"))]
     for plan, env in variants:
         for k, val in dict(base, **env).items():
             monkeypatch.setenv(k, val)
