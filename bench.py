@@ -871,12 +871,30 @@ def lr_sharded_base(out, ctx, args, la):
     sctx = Ctx(True)
     lb = argparse.Namespace(**vars(la))
     lb.no_cpu_baseline = True
-    q = bench_lr(lb, sctx, corpus_batches=10)
+    # two forms: the full protocol (SWPS_PULL_IN_PLACE=0: owner copy, install, step, payload, owner
+    # AdaGrad — what every rank runs at N > 1, less the remote bytes) and world 1's own in-place form
+    # (the install reads the shard rows, the push applies AdaGrad to them)
+    q = {}
+    prev = os.environ.get("SWPS_PULL_IN_PLACE")
+    try:
+        for form, env in (("protocol", "0"), ("in_place", "1")):
+            os.environ["SWPS_PULL_IN_PLACE"] = env
+            q[form] = bench_lr(lb, sctx, corpus_batches=10)
+    finally:
+        if prev is None:
+            os.environ.pop("SWPS_PULL_IN_PLACE", None)
+        else:
+            os.environ["SWPS_PULL_IN_PLACE"] = prev
+    p, i = q["protocol"], q["in_place"]
     out["lr"]["sharded_world1"] = {
-        "value": q["value"], "unit": q["unit"], "ms_per_step": q["ms_per_step"], "kernel_ms": q["kernel_ms"],
-        "parallelism": q["config"]["parallelism"],
-        "note": "the same workload through the key-sharded protocol at world 1 (no remote bytes): the base "
-                "point for the N > 1 lr legs, which run this protocol"}
+        "value": p["value"], "unit": p["unit"], "ms_per_step": p["ms_per_step"], "kernel_ms": p["kernel_ms"],
+        "parallelism": p["config"]["parallelism"],
+        "note": "the same workload through the key-sharded protocol at world 1 (no remote bytes, SWPS_PULL_IN_PLACE=0):"
+                " the like-for-like base point for the N > 1 lr legs, which run this protocol",
+        "in_place": {"value": i["value"], "ms_per_step": i["ms_per_step"], "kernel_ms": i["kernel_ms"],
+                     "note": "the library driver's default at world 1: the step's install reads the shard rows the "
+                             "owner looked up and its push applies AdaGrad to them (no owner copy, payload or owner "
+                             "apply)"}}
     sctx.close()
     if sctx.dist is not None:
         sctx.dist.destroy_process_group()

@@ -298,6 +298,9 @@ int ShardDriver::full_pull() {
 
 int ShardDriver::steps(uint64_t count) {
   const uint64_t vb = ops.width * ops.val_bytes, gb = ops.width * ops.grad_bytes;
+  // one stream (apps without a serve stream: LR): its own order is the events' order, so the
+  // cross-stream records and waits are skipped (each costs host time and a packet in the queue)
+  const bool one = S == ops.cs;
   for (uint64_t k = 0; k < count; k++) {
     const uint64_t st = cursor % spe;
     const uint64_t *sk = &send[st * world], *rk = &recv[st * world];
@@ -314,7 +317,7 @@ int ShardDriver::steps(uint64_t count) {
     const bool alias = world == 1 && !split_pull;
     void *mv = alias ? vals.p : myvals.p, *rg = alias ? grads.p : rgrads.p;
     // ---- S: pull(i) (C's earlier work on these buffers is ordered by events) ----
-    SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+    if (!one) SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
     // every rank runs the same steps, so every rank takes the same branch (the exchange is collective)
     const bool kc = key_cache && rk_valid[st];
     uint64_t *rkp = key_cache ? rk_cache.as<uint64_t>() + rk_off[st] : rkeys.as<uint64_t>();
@@ -362,11 +365,11 @@ int ShardDriver::steps(uint64_t count) {
         SWPS_TRY(exchange(vals.p, rk, mv, sk, vb, S, "pull values"));
       }
     }
-    SWPS_HIP(hipEventRecord(ev_pull, S));
+    if (!one) SWPS_HIP(hipEventRecord(ev_pull, S));
     // ---- C: learn(i), then prep(i+1) ----
-    SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_pull, 0));
+    if (!one) SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_pull, 0));
     if (mine) SWPS_TRY(ops.step(ops.h, ns ? mv : nullptr, ns ? grads.p : nullptr));
-    SWPS_HIP(hipEventRecord(ev_learn, ops.cs));
+    if (!one) SWPS_HIP(hipEventRecord(ev_learn, ops.cs));
     const uint64_t nxt = (cursor + 1) % spe;
     if (ops.prep && k + 1 < count && nxt < nb) SWPS_TRY(ops.prep(ops.h));
     // ---- S: the next step's early pull, while this one learns (its rows cannot change at push(i)) ----
@@ -393,7 +396,7 @@ int ShardDriver::steps(uint64_t count) {
         b += rk[r];
       }
       if (eh) SWPS_HIP(hipStreamWaitEvent(S, eh, 0));
-      else SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+      else if (!one) SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
       SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S, "push gradients"));
       for (int r = 0; r < world; r++) {
         so[r] += sb[r];
@@ -401,18 +404,20 @@ int ShardDriver::steps(uint64_t count) {
         sb[r] = (sk[r] - sk[r] / 2) * gb;
         rb[r] = (rk[r] - rk[r] / 2) * gb;
       }
-      SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+      if (!one) SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
       SWPS_TRY(exchange_disp(grads.p, sb, so, rgrads.p, rb, ro, S, "push gradients"));
     } else {
-      SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
+      if (!one) SWPS_HIP(hipStreamWaitEvent(S, ev_learn, 0));
       SWPS_TRY(exchange(grads.p, sk, rg, rk, gb, S, "push gradients"));
     }
     SWPS_TRY(ops.serve_push(ops.h, rkp, rg, rk));
     if (ops.set_slot) SWPS_TRY(ops.set_slot(ops.h, -1));
     cursor++;
   }
-  SWPS_HIP(hipEventRecord(ev_learn, S));  // the next call's C work waits for this push
-  SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_learn, 0));
+  if (S != ops.cs) {
+    SWPS_HIP(hipEventRecord(ev_learn, S));  // the next call's C work waits for this push
+    SWPS_HIP(hipStreamWaitEvent(ops.cs, ev_learn, 0));
+  }
   return SWPS_OK;
 }
 

@@ -2181,7 +2181,10 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
 #pragma unroll
       for (uint32_t k = 0; k < PER; k++) {
         c[k] = ac[tid + k * NT];
-        if (c[k] && !pre) row[k] = aff_rows ? row_base + (b << kLrFxVB) + tid + k * NT : vid_row[(b << kLrFxVB) + tid + k * NT];
+        if (c[k] && !pre) {
+          row[k] = aff_rows ? row_base + (b << kLrFxVB) + tid + k * NT : vid_row[(b << kLrFxVB) + tid + k * NT];
+          if (row[k] == kNoRow) c[k] = 0u;  // world 1 in place: a key the shard lacks
+        }
       }
       if (!pre) {
 #pragma unroll
@@ -2277,7 +2280,10 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
       c[k] = ac[tid + k * NT];
-      if (c[k]) row[k] = aff ? row_base + (b << kLrFxVB) + tid + k * NT : vid_row[(b << kLrFxVB) + tid + k * NT];
+      if (c[k]) {
+        row[k] = aff ? row_base + (b << kLrFxVB) + tid + k * NT : vid_row[(b << kLrFxVB) + tid + k * NT];
+        if (row[k] == kNoRow) c[k] = 0u;  // world 1 in place: a key the shard lacks
+      }
     }
     float2 wg[PER];
 #pragma unroll
@@ -2330,7 +2336,7 @@ __global__ __launch_bounds__(kLrFxbPushT) void k_lr_fxb_push(const uint2 *__rest
   if (rg == 0 && h < nhot && ac[tid]) {
     if (TO_GRADS)
       rows[vid_row[hrow[h]]] = (float)(((double)(long long)as[tid] * inv_scale) / (double)ac[tid]);
-    else {
+    else if (hrow[h] != kNoRow) {
       lr_fx_adagrad(rows + (uint64_t)hrow[h] * 2, (long long)as[tid], ac[tid], lr, fudge, inv_scale);
       if (wmir) wmir[h] = rows[(uint64_t)hrow[h] * 2];  // hot key q = fid q (affine form)
     }
@@ -2412,14 +2418,26 @@ __global__ void k_lr_install(const int32_t *__restrict__ K, uint64_t U, const fl
 
 // the sharded fixed-point step's install: the value of key K[u] at its fid's row of the step's layout
 // (wcache2[2 * fid]: the affine form with row base 0, hot keys first), and its position u by fid
+// (stride 1: the dense copy the branch-free step gathers from)
 __global__ void k_lr_install_fx(const int32_t *__restrict__ K, uint64_t U, const float *__restrict__ vals,
-                                const uint32_t *__restrict__ fid, float *__restrict__ wcache2,
+                                const uint32_t *__restrict__ fid, float *__restrict__ wcache2, uint32_t stride,
                                 uint32_t *__restrict__ localf) {
   const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= U) return;
   const uint32_t q = fid[K[u]];
-  wcache2[(uint64_t)q * 2] = vals[u];
+  wcache2[(uint64_t)q * stride] = vals[u];
   if (localf) localf[q] = (uint32_t)u;
+}
+// world 1 in place: the weight of key K[u] read from its shard row prow[u] (the slot's lookup), and
+// that row by fid — the push applies AdaGrad there (an absent key: weight 0, row kNoRow, skipped)
+__global__ void k_lr_install_fx_rows(const int32_t *__restrict__ K, uint64_t U, const uint32_t *__restrict__ prow,
+                                     const float *__restrict__ rows, const uint32_t *__restrict__ fid,
+                                     float *__restrict__ wcache2, uint32_t stride, uint32_t *__restrict__ localf) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  const uint32_t q = fid[K[u]], r = prow[u];
+  wcache2[(uint64_t)q * stride] = r == kNoRow ? 0.f : rows[(uint64_t)r * 2];
+  localf[q] = r;
 }
 
 __global__ void k_lr_keys(const int32_t *__restrict__ K, uint64_t n, const uint64_t *__restrict__ vkeys,
@@ -2559,8 +2577,19 @@ struct swps_lr {
   // stride 2 (wcache2[2 * vid], the step's row layout) and the mean gradients from its push
   bool fx_sharded = false;
   DevMem d_wcache2, d_fx_fidv, d_localf;  // [2V] weights by fid; fid by vid; batch position by fid
+  DevMem d_wdense;  // [V] the same weights dense by fid (the branch-free step's gathers: 32 per line)
   swps::ShardDriver *drv = nullptr;  // swps_lr_shard_comm: the library drives the exchange
   uint64_t serve_n = 0;
+  // world 1 in place (AppOps::pull_in_place): serve_pull only looks the slot's rows up, the step's
+  // install reads the weights from those shard rows and its push applies AdaGrad to them — the
+  // owner's copy, the payload and the owner's apply are gone; serve_push then has nothing to do
+  const uint32_t *pull_rows = nullptr;
+  bool pushed_in_place = false;
+  // world 1, rows placed by fid (the full pull inserts them in fid order): shard row = w1_base + fid,
+  // so the in-place step is the single-GPU affine step (dense weight copy kept by the push, no
+  // install); -1: not affine (the install reads the rows the slot's lookup names)
+  int64_t w1_base = -1;
+  DevMem d_w1_hrow;  // the hot keys' shard rows (w1_base + q)
   // the library driver's step slot (AppOps::set_slot): the keys an owner serves at a slot are the
   // same every epoch, so their row lookups and the push's grouping sort are kept per slot
   int64_t slot = -1;
@@ -3439,16 +3468,42 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
   const uint64_t step = l->cursor, nr = l->label.size(), bi = step % l->nbatches;
   const uint64_t r0 = bi * l->B1(), r1 = std::min<uint64_t>(nr, r0 + l->B1());
   l->cursor++;
-  if (l->row_off[r1] == l->row_off[r0]) return SWPS_OK;
+  if (l->row_off[r1] == l->row_off[r0]) {
+    l->pull_rows = nullptr;
+    l->pushed_in_place = false;
+    return SWPS_OK;
+  }
   const bool hot = l->hot != 0 && !l->fx_hot_vids.empty();
   const uint64_t nfc = l->bfchunk[bi + 1] - l->bfchunk[bi];
-  if (shd) {  // the owners' pull values at the step's row layout; each key's position for the payload
+  // sharded, branch-free step: the pulled weights dense by fid (its gathers read 32 per line)
+  const bool shd_dense = shd && !l->fx_atomic && l->fxb_res && l->fx_affine && l->fxr;
+  // world 1 in place (serve_pull looked the slot's rows up and copied nothing): the install reads the
+  // shard rows, localf holds each key's row, and the push applies AdaGrad there (no payload)
+  const uint32_t *prow = shd ? l->pull_rows : nullptr;
+  l->pull_rows = nullptr;
+  const bool w1aff = prow && shd_dense && l->w1_base >= 0;
+  if (w1aff) {  // the single-GPU affine form: the dense copy from the rows once per train call
+    SWPS_TRY(l->d_wdense.ensure(V * 4));
+    if (l->mirror_stale) {
+      k_lr_mirror<<<nblk(V), 256, 0, s>>>(l->t->rows.as<float>(), (uint32_t)l->w1_base, V, l->d_wdense.as<float>());
+      SWPS_HIP(hipGetLastError());
+      l->mirror_stale = false;
+    }
+    l->pushed_in_place = true;
+  } else if (shd) {  // the owners' pull values at the step's row layout; each key's position for the payload
     const uint64_t U = l->bU[bi];
-    if (U)
+    if (shd_dense) SWPS_TRY(l->d_wdense.ensure(V * 4));
+    float *wc = shd_dense ? l->d_wdense.as<float>() : l->d_wcache2.as<float>();
+    const uint32_t ws = shd_dense ? 1u : 2u;
+    if (U && prow)
+      k_lr_install_fx_rows<<<nblk(U), 256, 0, s>>>(l->d_K.as<int32_t>() + l->kofs[bi], U, prow,
+                                                   l->t->rows.as<float>(), l->d_fx_fidv.as<uint32_t>(), wc, ws,
+                                                   l->d_localf.as<uint32_t>());
+    else if (U)
       k_lr_install_fx<<<nblk(U), 256, 0, s>>>(l->d_K.as<int32_t>() + l->kofs[bi], U, d_vals,
-                                              l->d_fx_fidv.as<uint32_t>(), l->d_wcache2.as<float>(),
-                                              l->d_localf.as<uint32_t>());
+                                              l->d_fx_fidv.as<uint32_t>(), wc, ws, l->d_localf.as<uint32_t>());
     SWPS_HIP(hipGetLastError());
+    l->pushed_in_place = prow != nullptr;
   }
   if (!l->fx_atomic) {
     const uint32_t nh = hot ? (uint32_t)l->fx_hot_vids.size() : 0u, grid = (uint32_t)std::min<uint64_t>(nfc, l->fxb_grid);
@@ -3500,7 +3555,10 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
                             l->d_fxb_rec.as<uint2>(), l->d_fxb_hsum.as<unsigned long long>(),
                             l->d_fxb_hcnt.as<uint32_t>(), l->fx_row_base, l->d_fxb_fill.as<uint32_t>(),
                             (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), l->fxb_gbits,
-                            mir ? (const float *)l->d_wmir.as<float>() : (const float *)nullptr, l->fxb_diag);
+                            shd_dense ? (const float *)l->d_wdense.as<float>()
+                            : mir     ? (const float *)l->d_wmir.as<float>()
+                                      : (const float *)nullptr,
+                            l->fxb_diag);
     } else
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(nt), dyn, s, fb, fe, 0,
                           (const uint2 *)l->d_fchunk.as<uint2>() + l->bfchunk[bi], (uint32_t)nfc,
@@ -3522,6 +3580,44 @@ int lr_batch_fx(swps_lr *l, const float *d_vals = nullptr, float *d_grads = null
     const uint32_t bper = l->fxb_xcd ? (l->fxb_nbk + 7u) / 8u : 0u, nbb = bper ? 8u * bper : l->fxb_nbk;
     const uint32_t pb0 = (l->fxb_diag & 2u) ? nbb : 0u,
                    pb1 = (l->fxb_diag & 1u) ? nbb : nbb + (nh + kLrFxbHotK - 1) / kLrFxbHotK;
+    if (w1aff) {  // world 1, rows by fid: the single-GPU push (affine rows, prefetch, dense copy kept)
+      hipExtLaunchKernelGGL(res ? k_lr_fxb_push<false, true> : k_lr_fxb_push<false, false>,
+                            dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), res ? 0 : (2 * nfc + 1) * 4, s, ab,
+                            ae, 0,
+                            (const uint2 *)l->d_fxb_rec.as<uint2>(), (const uint16_t *)l->d_fxb_boff.as<uint16_t>(),
+                            (const uint32_t *)l->d_fchunk_c0.as<uint32_t>() + l->bfchunk[bi], (uint32_t)nfc,
+                            l->fxb_nbk, (uint32_t)l->max_bchunks, (const uint32_t *)l->d_localf.as<uint32_t>(),
+                            (const unsigned long long *)l->d_fxb_hsum.as<unsigned long long>(),
+                            (const uint32_t *)l->d_fxb_hcnt.as<uint32_t>(), grid,
+                            (const uint32_t *)l->d_w1_hrow.as<uint32_t>(), nh, l->t->rows.as<float>(),
+                            l->t->cfg.learning_rate, l->t->cfg.fudge, scale, std::ldexp(1.0, -l->fx_bits), 1u,
+                            (uint32_t)l->w1_base, pb0, bper, l->d_fxb_fill.as<uint32_t>(),
+                            (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(), (uint32_t)l->vocab_keys.size(),
+                            l->fxb_gbits, l->d_wdense.as<float>(),
+                            res && l->fx_pf != 2 ? (const uint8_t *)l->d_pfb.as<uint8_t>() : (const uint8_t *)nullptr,
+                            l->fxb_diag);
+      SWPS_HIP(hipGetLastError());
+      l->timer.ext_end(3, ab, ae);
+      return SWPS_OK;
+    }
+    if (prow) {  // world 1 in place: AdaGrad on the shard rows localf names (hot key q = fid q)
+      hipExtLaunchKernelGGL(res ? k_lr_fxb_push<false, true> : k_lr_fxb_push<false, false>,
+                            dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), res ? 0 : (2 * nfc + 1) * 4, s, ab,
+                            ae, 0,
+                            (const uint2 *)l->d_fxb_rec.as<uint2>(), (const uint16_t *)l->d_fxb_boff.as<uint16_t>(),
+                            (const uint32_t *)l->d_fchunk_c0.as<uint32_t>() + l->bfchunk[bi], (uint32_t)nfc,
+                            l->fxb_nbk, (uint32_t)l->max_bchunks, (const uint32_t *)l->d_localf.as<uint32_t>(),
+                            (const unsigned long long *)l->d_fxb_hsum.as<unsigned long long>(),
+                            (const uint32_t *)l->d_fxb_hcnt.as<uint32_t>(), grid,
+                            (const uint32_t *)l->d_localf.as<uint32_t>(), nh, l->t->rows.as<float>(),
+                            l->t->cfg.learning_rate, l->t->cfg.fudge, scale, std::ldexp(1.0, -l->fx_bits), 0u, 0u,
+                            pb0, bper, l->d_fxb_fill.as<uint32_t>(), (const uint32_t *)l->d_fxb_rbase.as<uint32_t>(),
+                            (uint32_t)l->vocab_keys.size(), l->fxb_gbits, (float *)nullptr, (const uint8_t *)nullptr,
+                            l->fxb_diag);
+      SWPS_HIP(hipGetLastError());
+      l->timer.ext_end(3, ab, ae);
+      return SWPS_OK;
+    }
     hipExtLaunchKernelGGL(shd ? (res ? k_lr_fxb_push<true, true> : k_lr_fxb_push<true, false>)
                               : (res ? k_lr_fxb_push<false, true> : k_lr_fxb_push<false, false>),
                           dim3(std::max(1u, pb1 - pb0)), dim3(kLrFxbPushT), res ? 0 : (2 * nfc + 1) * 4, s, ab,
@@ -4236,6 +4332,7 @@ int swps_lr_init(swps_lr *l) {
 int swps_lr_train_batches(swps_lr *l, uint64_t count) {
   if (l->drv) {
     SWPS_HIP(hipSetDevice(l->t->cfg.device));
+    l->mirror_stale = true;  // world 1 in place, rows by fid: the table may have been written since
     return l->drv->steps(count);  // collective
   }
   if (l->sharded) return fail(SWPS_E_STATE, "sharded: drive swps_lr_request/serve_pull/step/serve_push");
@@ -4448,8 +4545,16 @@ int swps_lr_shard(swps_lr *l, int32_t rank, int32_t world, int32_t frag_num) {
   }
   l->init_order.resize(V);
   for (uint64_t i = 0; i < V; i++) l->init_order[i] = (int32_t)i;
-  std::stable_sort(l->init_order.begin(), l->init_order.end(),
-                   [&](int32_t a, int32_t b) { return owner[a] < owner[b]; });
+  // the full pull's keys by owner, and within an owner in fid order when the fixed-point step runs:
+  // the owner inserts them in that order, so its rows follow the step's buckets (at world 1 the rows
+  // are base + fid, and the in-place push updates each bucket's rows as one contiguous run)
+  if (l->fx_sharded && l->fx_fid.size() == V)
+    std::sort(l->init_order.begin(), l->init_order.end(), [&](int32_t a, int32_t b) {
+      return owner[a] != owner[b] ? owner[a] < owner[b] : l->fx_fid[a] < l->fx_fid[b];
+    });
+  else
+    std::stable_sort(l->init_order.begin(), l->init_order.end(),
+                     [&](int32_t a, int32_t b) { return owner[a] < owner[b]; });
   l->icounts.assign(world, 0);
   for (uint64_t i = 0; i < V; i++) l->icounts[owner[i]]++;
   SWPS_HIP(hipSetDevice(l->t->cfg.device));
@@ -4516,15 +4621,50 @@ int swps_lr_serve_pull(swps_lr *l, const uint64_t *d_keys, const uint64_t *src_c
       e.sorted_valid = false;
     }
     l->serve_n = n;
+    if (!d_vals && n) {  // the driver's in-place pull (AppOps::pull_in_place): the step reads these rows
+      if (l->world != 1 || !l->fx_sharded) return fail(SWPS_E_STATE, "an in-place pull needs world 1 and the fixed-point step");
+      l->pull_rows = e.rows.as<uint32_t>();
+      return SWPS_OK;
+    }
     return table_copy_pull(l->t, e.rows.as<uint32_t>(), n, d_vals, l->s);
   }
+  if (!d_vals && n) return fail(SWPS_E_STATE, "serve_pull without a value buffer needs a world-1 driver step slot");
   SWPS_TRY(l->d_serve_rows.ensure(std::max<uint64_t>(n, 1) * 4));
   uint32_t *rows = l->d_serve_rows.as<uint32_t>();
   if (insert) {  // keys are distinct within a source, not across sources
     uint64_t off = 0;
+    std::vector<uint32_t> iota;
     for (int r = 0; r < l->world; r++) {
-      SWPS_TRY(table_find_or_insert(l->t, d_keys + off, src_counts[r], rows + off, l->s));
+      if (l->fx_sharded) {  // new rows in request order (by fid: swps_lr_shard's init_order)
+        iota.resize(src_counts[r]);
+        for (uint64_t q = 0; q < src_counts[r]; q++) iota[q] = (uint32_t)q;
+        SWPS_TRY(table_find_or_insert_placed(l->t, d_keys + off, src_counts[r], iota.data(), rows + off, l->s));
+      } else {
+        SWPS_TRY(table_find_or_insert(l->t, d_keys + off, src_counts[r], rows + off, l->s));
+      }
       off += src_counts[r];
+    }
+    // world 1: the full pull's keys in fid order (swps_lr_shard's init_order) — when their rows came
+    // out as base + fid, the in-place step runs the single-GPU affine form
+    const uint64_t V = l->vocab_keys.size();
+    l->w1_base = -1;
+    const char *wa = getenv("SWPS_LR_W1_AFFINE");  // 0: the install / row-indexed push (A/B, tests)
+    if (l->world == 1 && l->fx_sharded && n == V && V && l->fx_fid.size() == V && !(wa && atoi(wa) == 0)) {
+      std::vector<uint32_t> hr(n);
+      SWPS_HIP(hipMemcpyAsync(hr.data(), rows, n * 4, hipMemcpyDeviceToHost, l->s));
+      SWPS_HIP(hipStreamSynchronize(l->s));
+      bool aff = (uint64_t)hr[0] + V <= l->t->cfg.capacity;
+      for (uint64_t j = 0; j < n && aff; j++)
+        aff = hr[j] == hr[0] + (uint32_t)j && l->fx_fid[l->init_order[j]] == (uint32_t)j;
+      const uint32_t nh = (uint32_t)l->fx_hot_vids.size();
+      if (aff) {
+        std::vector<uint32_t> hrow(std::max<uint32_t>(nh, 1));
+        for (uint32_t q = 0; q < hrow.size(); q++) hrow[q] = hr[0] + q;
+        SWPS_TRY(upload(l->d_w1_hrow, hrow, l->s));
+        SWPS_HIP(hipStreamSynchronize(l->s));
+        l->w1_base = hr[0];
+        l->mirror_stale = true;
+      }
     }
   } else {
     SWPS_TRY(table_lookup(l->t, d_keys, n, rows, l->s));
@@ -4563,6 +4703,10 @@ int swps_lr_serve_push(swps_lr *l, const uint64_t *d_keys, const float *d_grads,
   uint64_t n = 0;
   for (int r = 0; r < l->world; r++) n += src_counts[r];
   if (n != l->serve_n) return fail(SWPS_E_STATE, "push does not match the served pull");
+  if (l->pushed_in_place) {  // world 1 in place: the step's push already applied AdaGrad to these rows
+    l->pushed_in_place = false;
+    return SWPS_OK;
+  }
   int nsrc = 0;
   for (int r = 0; r < l->world; r++) nsrc += src_counts[r] > 0;
   if (l->slot >= 0 && (uint64_t)l->slot < l->slot_rows.size() && l->slot_rows[l->slot]->n == n &&
@@ -4676,6 +4820,10 @@ int swps_lr_shard_comm(swps_lr *l, swps_comm *c, int32_t frag_num) {
       ((swps_lr *)h)->slot = slot;
       return (int)SWPS_OK;
     };
+  // world 1 with the fixed-point step: pull and push in place on the shard rows (the driver passes
+  // no value buffer; SWPS_PULL_IN_PLACE=0 keeps the copy, the payload and the owner's apply)
+  const char *pip = getenv("SWPS_PULL_IN_PLACE");
+  o.pull_in_place = l->fx_sharded && !(pip && atoi(pip) == 0);
   const int rc = d->setup();
   if (rc) {
     delete d;

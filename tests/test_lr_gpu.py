@@ -762,14 +762,20 @@ def test_lr_config3_full_rank_share(lib, gpu):
     assert np.isfinite(outs[0][1]).all() and np.isfinite(outs[0][0]).all()
 
 
+@pytest.mark.parametrize("inplace", [1, 2, 0])
 @pytest.mark.parametrize("B", [4095, 200])
-def test_sharded_fixed_point_world1_equals_unsharded(lib, gpu, B):
+def test_sharded_fixed_point_world1_equals_unsharded(lib, gpu, B, inplace, monkeypatch):
     """The sharded learner's fixed-point step (plan none, fast sums: swps_lr_step writes each
     key's mean of its integer sums as the push payload and the owner applies AdaGrad,
     k_lr_fxb_push<TO_GRADS>) through the library driver at world 1 (RCCL) == the single-GPU
     fixed-point step, bit for bit: weights, AdaGrad sums and epoch errors over 3 epochs, and the
-    predictions after them."""
+    predictions after them.  inplace=1 (the default at world 1): the pull reads the shard rows and
+    the push applies AdaGrad to them (no copy, payload or owner apply) — with the rows placed by
+    fid, the single-GPU affine step itself; 2: in place through the install and a row-indexed push
+    (SWPS_LR_W1_AFFINE=0); 0: the full protocol."""
     import torch
+    monkeypatch.setenv("SWPS_PULL_IN_PLACE", str(min(inplace, 1)))
+    monkeypatch.setenv("SWPS_LR_W1_AFFINE", "0" if inplace == 2 else "1")
     from conftest import free_port
     from swiftmpi_amd.comm import Comm
     from swiftmpi_amd.synth import criteo
