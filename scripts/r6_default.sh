@@ -11,7 +11,8 @@ d = json.load(open("gpurun_out/r06_bench_default.json"))
 print("headline %.4g words/s  %.3f ms  frac %.3f" % (d["value"], d["ms_per_step"], d["roofline"]["frac"]))
 print("b100 %.4g  config4 %.4g  config1 gpu %.4g" % (d["minibatch_100"]["value"], d["config4"]["value"], d["config1"]["gpu"]["value"]))
 lr = d["lr"]; s = d["s2v"]
-print("lr %.4g ex/s %.4f ms  sharded_w1 %s" % (lr["value"], lr["ms_per_step"], {k: lr["sharded_world1"][k] for k in ("value", "ms_per_step")}))
+q = lr["sharded_world1"]
+print("lr %.4g ex/s %.4f ms  sharded_w1 protocol %.4g %.4f ms  in place %.4g %.4f ms" % (lr["value"], lr["ms_per_step"], q["value"], q["ms_per_step"], q["in_place"]["value"], q["in_place"]["ms_per_step"]))
 print("s2v single pass %.4g words/s, steady %.4g" % (s["value"], s["config"]["steady_state"]["value"]))
 print("cpu", d["cpu_baseline"]["value"], {k: v["value"] for k, v in (d.get("other_modes") or {}).items()})
 PY
