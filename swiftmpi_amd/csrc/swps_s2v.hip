@@ -37,6 +37,10 @@
 #include <thread>
 #include <unordered_set>
 
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "swps_internal.h"
 #include "swps_rand.h"
 #include "swps_wave.h"
@@ -704,7 +708,15 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     int nth = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
     if (const char *e = getenv("SWPS_S2V_THREADS")) nth = std::max(1, atoi(e));
     nth = (int)std::min<uint64_t>((uint64_t)nth, std::max<uint64_t>(K, 1));
+    // the workers below the pass's priority (SWPS_S2V_NICE, default 10; 0: same): the pass, the
+    // fetch thread and the group uploads are the pipeline's sequential part and must not wait for a
+    // core behind the plan workers
+    static const int nice_w = [] {
+      const char *e = getenv("SWPS_S2V_NICE");
+      return e ? atoi(e) : 10;
+    }();
     auto work = [&]() {
+      if (nice_w > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_w);
       // counts by row in dense arrays (a generation stamp per row instead of clearing); keys the
       // table lacks (row kNoRow: the minibatch's pull inserts them) in a hash map
       FlatMap64 fq(1 << 10);
@@ -854,13 +866,69 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   const uint64_t nchunk_max = ndmax * (uint64_t)D / kRandRun + K + 1;
 
   rand_chunks.reserve(3 * nchunk_max);
-  doc_line.reserve(ndmax);
-  m->doc_id.reserve(ndmax);
-  m->doc_tok.reserve(ndmax + 1);
-  m->doc_rec.reserve(ndmax + 1);
-  m->doc_lcg.reserve(ndmax);
-  doc_batch.reserve(ndmax);
-  std::vector<uint64_t> bv0(K), bs0(K);
+  // The documents (the training handler's sentences, sent2vec.cpp:48-93) depend only on the lines:
+  // minibatch k's are the valid lines of its B + 1, at dbase[k] .. dbase[k + 1).  A thread fills
+  // every array for all minibatches in order (the LCG state runs through them) and flags each
+  // minibatch; the pass reads them once flagged.  Arrays past the last minibatch trained are cut
+  // after the pass.
+  std::vector<uint64_t> dbase(K + 1, 0), lst_end(K, 0);
+  for (uint64_t k = 0; k < K; k++) dbase[k + 1] = dbase[k] + kdoc[k];
+  std::unique_ptr<std::atomic<int>[]> dready(new std::atomic<int>[std::max<uint64_t>(K, 1)]);
+  for (uint64_t k = 0; k < K; k++) dready[k].store(0, std::memory_order_relaxed);
+  std::atomic<bool> docs_quit{false};
+  std::thread docs_th([&] {
+    m->doc_id.resize(ndmax);
+    m->doc_tok.resize(ndmax + 1);
+    m->doc_rec.resize(ndmax + 1);
+    m->doc_lcg.resize(ndmax);
+    doc_line.resize(ndmax);
+    doc_batch.resize(ndmax);
+    m->doc_tok[0] = m->doc_rec[0] = 0;
+    uint64_t ls_ = lstate, ntok = 0, nrec = 0, d = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> jmp;  // per document length: (A^k, c (A^k - 1) / (A - 1))
+    for (uint64_t k = 0; k < K && !docs_quit.load(std::memory_order_relaxed); k++) {
+      const uint64_t li = k * (uint64_t)(B + 1);
+      for (uint64_t l = li; l < std::min<uint64_t>(nl, li + (uint64_t)(B + 1)); l++) {
+        if (!valid[l]) continue;
+        const uint64_t L = line_off[l + 1] - line_off[l];
+        m->doc_id[d] = sent_ids[l];
+        doc_line[d] = (uint32_t)l;
+        doc_batch[d] = (uint32_t)k;
+        ntok += L;
+        nrec += L * (uint64_t)m->cfg.niters;
+        m->doc_tok[d + 1] = ntok;
+        m->doc_rec[d + 1] = nrec;
+        m->doc_lcg[d] = ls_;
+        // the LCG's jump over a document: the same multiplier and increment for every length L
+        // (lcg_jump(x, k) = A^k x + c(A^k - 1)/(A - 1)), cached per L
+        if (L >= jmp.size()) jmp.resize(L + 1, {0, 0});
+        if (!jmp[L].first) {
+          const uint64_t kk = (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1));
+          jmp[L] = {lcg_jump(1, kk, kLcgA, kLcgC) - lcg_jump(0, kk, kLcgA, kLcgC), lcg_jump(0, kk, kLcgA, kLcgC)};
+        }
+        ls_ = jmp[L].first * ls_ + jmp[L].second;
+        d++;
+      }
+      lst_end[k] = ls_;
+      dready[k].store(1, std::memory_order_release);
+    }
+  });
+  struct JoinDocs {
+    std::thread &t;
+    std::atomic<bool> &q;
+    ~JoinDocs() {
+      q.store(true);
+      if (t.joinable()) t.join();
+    }
+  } join_docs{docs_th, docs_quit};
+  auto wait_docs = [&](uint64_t k) {
+    for (unsigned it = 0; !dready[k].load(std::memory_order_acquire); it++)
+      if (it < 64)
+        std::this_thread::yield();
+      else
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+  };
+  std::vector<uint64_t> bv0(K), bs0(K), plan_st_n(K, 0);
   std::vector<uint32_t> bU(K);
   DevMem d_vkeys, d_line_off, d_doc_line, d_chunks, d_base;
   SWPS_TRY(d_vkeys.ensure(std::max<uint64_t>(wtok, 1) * 8));
@@ -892,6 +960,33 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     SWPS_TRY(upload(d_base, glibc_base(m->cfg.rand_seed), s));
     SWPS_HIP(hipStreamSynchronize(s));  // ex, the base vector: locals
   }
+  // the groups' vocabularies and run starts go up from two pinned staging buffers in turn (one copy
+  // each per group; a pageable copy per minibatch ran at ~2 GB/s and synchronised the load stream):
+  // a buffer is refilled once the copy that last read it is done
+  struct Pinned {
+    void *p = nullptr;
+    uint64_t bytes = 0;
+    hipEvent_t done = nullptr;
+    ~Pinned() {
+      if (done) {
+        (void)hipEventSynchronize(done);
+        (void)hipEventDestroy(done);
+      }
+      if (p) (void)hipHostFree(p);
+    }
+    int ensure(uint64_t n) {
+      if (done) SWPS_HIP(hipEventSynchronize(done));
+      if (n <= bytes) return SWPS_OK;
+      if (p) SWPS_HIP(hipHostFree(p));
+      p = nullptr;
+      bytes = 0;
+      const uint64_t want = std::max<uint64_t>(n + n / 4, 4u << 20);
+      if (hipHostMalloc(&p, want) != hipSuccess) return fail(SWPS_E_OOM, "pinned staging buffer");
+      bytes = want;
+      return SWPS_OK;
+    }
+  } pin[2];
+  int pin_next = 0;
   // the load stream: each group's uploads, lookups and rand() rows; the training of a group waits
   // for its event on the table's stream
   struct LoadStream {
@@ -915,8 +1010,10 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   uint64_t kf = 0, rc_done = 0;  // minibatches / rand chunks already on the device
   // one group's device part: its misses into the table, its vocabularies' rows and run starts, its
   // documents' arrays, token rows and rand() rows; then (train) its records + docs launch
+  double t_fv = 0, t_fm = 0;  // SWPS_S2V_LOAD_TIMES: the flushes' vocabulary copies, miss inserts
   auto flush = [&](uint64_t k1) -> int {
     if (k1 == kf) return SWPS_OK;
+    const double fa = tm ? now() : 0;
     if (miss_keys.size() > mk_done) {  // rows = [h | v | h2 = 0 | v2 = 0]; the table's own stream (syncs)
       const std::vector<uint64_t> mk(miss_keys.begin() + mk_done, miss_keys.end());
       DevMem dk, dv;
@@ -933,26 +1030,35 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       SWPS_TRY(swps_assign(m->t, dk.as<uint64_t>(), mk.size(), dv.p));
       mk_done = miss_keys.size();
     }
+    const double fb = tm ? now() : 0;
+    if (tm) t_fm += fb - fa;
     hipStream_t q = ls.s;
     const swps_s2v::Batch &b0 = m->batches[kf], &b1 = m->batches[k1 - 1];
     const uint64_t v0 = b0.v0, v1 = b1.v0 + b1.U, d0 = b0.d0, d1 = b1.d1;
+    // the group's vocabularies are consecutive in d_vkeys (v0 .. v1) and so are its run starts: one
+    // pinned buffer holds both, one copy each
+    const uint64_t sv0 = b0.s0, sv1 = b1.s0 + plan_st_n[k1 - 1];
+    Pinned &pb = pin[pin_next];
+    pin_next ^= 1;
+    SWPS_TRY(pb.ensure(((v1 - v0) + (sv1 - sv0)) * 8));
+    uint64_t *hv = (uint64_t *)pb.p, *hs = hv + (v1 - v0);
     for (uint64_t k = kf; k < k1; k++) {
       bv0[k] = m->batches[k].v0;
       bs0[k] = m->batches[k].s0;
       bU[k] = m->batches[k].U;
-      // each minibatch's vocabulary and run starts straight from its plan (a pageable copy is staged
-      // before the call returns: the plan's vectors can go)
       Plan &pk = plan[k];
-      if (!pk.vkeys.empty())
-        SWPS_HIP(hipMemcpyAsync(d_vkeys.as<uint64_t>() + bv0[k], pk.vkeys.data(), pk.vkeys.size() * 8,
-                                hipMemcpyHostToDevice, q));
-      if (!pk.st.empty())
-        SWPS_HIP(hipMemcpyAsync(m->d_starts.as<uint64_t>() + bs0[k], pk.st.data(), pk.st.size() * 8,
-                                hipMemcpyHostToDevice, q));
-      SWPS_HIP(hipStreamSynchronize(q));  // (staged already; to be safe before the vectors go)
+      std::copy(pk.vkeys.begin(), pk.vkeys.end(), hv + (bv0[k] - v0));
+      std::copy(pk.st.begin(), pk.st.end(), hs + (bs0[k] - sv0));
       std::vector<uint64_t>().swap(pk.vkeys);
       std::vector<uint64_t>().swap(pk.st);
     }
+    if (v1 > v0)
+      SWPS_HIP(hipMemcpyAsync(d_vkeys.as<uint64_t>() + v0, hv, (v1 - v0) * 8, hipMemcpyHostToDevice, q));
+    if (sv1 > sv0)
+      SWPS_HIP(hipMemcpyAsync(m->d_starts.as<uint64_t>() + sv0, hs, (sv1 - sv0) * 8, hipMemcpyHostToDevice, q));
+    if (!pb.done) SWPS_HIP(hipEventCreateWithFlags(&pb.done, hipEventDisableTiming));
+    SWPS_HIP(hipEventRecord(pb.done, q));
+    if (tm) t_fv += now() - fb;
     if (v1 > v0)
       SWPS_TRY(table_lookup(m->t, d_vkeys.as<uint64_t>() + v0, v1 - v0, m->d_vocab_row.as<uint32_t>() + v0, q));
     SWPS_HIP(hipMemcpyAsync(m->d_bv0.as<uint64_t>() + kf, bv0.data() + kf, (k1 - kf) * 8, hipMemcpyHostToDevice, q));
@@ -1006,7 +1112,6 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   };
   size_t gi = 0;
   wait_present();
-  std::vector<std::pair<uint64_t, uint64_t>> jmp;  // per document length: (A^k, c (A^k - 1) / (A - 1))
   double t_wait = 0, t_flush = 0;  // SWPS_S2V_LOAD_TIMES: the pass's time waiting for plans, in flushes
   double t_lk = 0, t_vocab = 0, t_docs = 0;  // ... refilling _local_keys, appending vocabularies, documents
   for (uint64_t k = 0; k < K; k++) {
@@ -1059,39 +1164,22 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       m->misses++;
     }
     const double tb1 = tm ? now() : 0;
-    swps_s2v::Batch b{m->doc_id.size(), 0, nvocab, nstarts, (uint32_t)pl.vkeys.size(), 0};
+    swps_s2v::Batch b{dbase[k], 0, nvocab, nstarts, (uint32_t)pl.vkeys.size(), 0};
     nvocab += pl.vkeys.size();
     nstarts += pl.st.size();
+    plan_st_n[k] = pl.st.size();
     std::vector<uint64_t>().swap(pl.first);
     if (tm) t_vocab += now() - tb1;
     const double tb2 = tm ? now() : 0;
     // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not; the sentences' Vec::random
     // draws are this minibatch's next run of the stream (drawn on the device, k_s2v_rand)
-    const uint64_t run_o = 344 + rnd.produced + skip, run_d0 = m->doc_id.size();
-    for (uint64_t l = li; l < std::min<uint64_t>(nl, li + (uint64_t)(B + 1)); l++) {
-      if (!valid[l]) continue;
-      const uint64_t L = line_off[l + 1] - line_off[l];
-      m->doc_id.push_back(sent_ids[l]);
-      doc_line.push_back((uint32_t)l);
-      doc_ntok += L;
-      m->doc_tok.push_back(doc_ntok);
-      m->doc_rec.push_back(m->doc_rec.back() + L * (uint64_t)m->cfg.niters);
-      skip += (uint64_t)D;
-      m->doc_lcg.push_back(lstate);
-      // the LCG's jump over a document: the same multiplier and increment for every length L
-      // (lcg_jump(x, k) = A^k x + c(A^k - 1)/(A - 1)), cached per L
-      if (L >= jmp.size()) jmp.resize(L + 1, {0, 0});
-      if (!jmp[L].first) {
-        const uint64_t kk = (uint64_t)m->cfg.niters * (1 + L * (uint64_t)(N + 1));
-        jmp[L] = {lcg_jump(1, kk, kLcgA, kLcgC) - lcg_jump(0, kk, kLcgA, kLcgC), lcg_jump(0, kk, kLcgA, kLcgC)};
-      }
-      lstate = jmp[L].first * lstate + jmp[L].second;
-    }
-    b.d1 = m->doc_id.size();
+    wait_docs(k);  // the documents' arrays (the docs thread)
+    const uint64_t run_o = 344 + rnd.produced + skip, run_d0 = dbase[k];
+    skip += (uint64_t)D * kdoc[k];  // each sentence's Vec::random: D draws
+    b.d1 = dbase[k + 1];
     for (uint64_t q = 0, tot = (b.d1 - run_d0) * (uint64_t)D; q < tot; q += kRandRun)
       rand_chunks.insert(rand_chunks.end(), {run_d0 * (uint64_t)D + q, run_o + q, std::min<uint64_t>(kRandRun, tot - q)});
     b.recs = m->doc_rec[b.d1] - m->doc_rec[b.d0];
-    doc_batch.resize(b.d1, (uint32_t)m->batches.size());
     m->max_recs = std::max(m->max_recs, b.recs);
     m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
     m->batches.push_back(b);
@@ -1107,9 +1195,21 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   if (fetch_rc.load() != SWPS_OK) return fail(fetch_rc.load(), "sent2vec load: token rows (HIP)");
   SWPS_TRY(flush(m->batches.size()));
   if (tm)
-    fprintf(stderr, "[s2v load]   of which waiting for plans %.3f s, group uploads + launches %.3f s, _local_keys %.3f s, "
-                    "vocabularies %.3f s, documents %.3f s\n", t_wait, t_flush, t_lk, t_vocab, t_docs);
+    fprintf(stderr, "[s2v load]   of which waiting for plans %.3f s, group uploads + launches %.3f s (vocabulary copies %.3f, "
+                    "miss inserts %.3f), _local_keys %.3f s, vocabularies %.3f s, documents %.3f s\n", t_wait, t_flush,
+            t_fv, t_fm, t_lk, t_vocab, t_docs);
   phase("minibatch vocabs + schedule + groups (host)");
+  {  // the documents of the minibatches trained (the pass may stop early: sent2vec.cpp:97)
+    docs_quit.store(true);
+    if (docs_th.joinable()) docs_th.join();
+    const uint64_t nb = m->batches.size(), ndt = nb ? m->batches.back().d1 : 0;
+    m->doc_id.resize(ndt);
+    m->doc_tok.resize(ndt + 1);
+    m->doc_rec.resize(ndt + 1);
+    m->doc_lcg.resize(ndt);
+    doc_ntok = m->doc_tok[ndt];
+    if (nb) lstate = lst_end[nb - 1];
+  }
   m->lstate_end = lstate;
   rnd.discard(skip);
   m->rand_calls = rnd.produced;  // includes the rand_offset skipped above
