@@ -43,6 +43,7 @@
 
 #include "swps_internal.h"
 #include "swps_rand.h"
+#include "swps_sort.h"
 #include "swps_wave.h"
 
 using namespace swps;
@@ -407,6 +408,9 @@ struct swps_s2v {
   // device
   DevMem d_tok_row, d_doc_tok, d_doc_rec, d_doc_lcg, d_vocab_row, d_starts, d_init, d_exptab, d_rec, d_out, d_err,
       d_rows_read;
+  DevMem d_rec2;                // the single pass: the second records buffer (groups alternate)
+  hipEvent_t ev_rec = nullptr;  // the single pass: a group's records built on the load stream
+  hipEvent_t ev_docs[2] = {nullptr, nullptr};  // ... and the last documents launch that read each buffer
   DevMem d_doc_batch, d_bv0, d_bs0, d_bU;  // sentence -> minibatch; per minibatch vocab / run-start offsets, size
   // consecutive minibatches per launch, up to this many sentences (SWPS_S2V_GROUP; 0 = one minibatch):
   // the word table is read-only while training and every miss was inserted at load, so the
@@ -422,18 +426,18 @@ struct swps_s2v {
 
 namespace {
 
-hipEvent_t ev_begin(swps_s2v *m) {
+hipEvent_t ev_begin(swps_s2v *m, hipStream_t st = nullptr) {
   if (!m->timing) return nullptr;
   hipEvent_t e;
   (void)hipEventCreate(&e);
-  (void)hipEventRecord(e, m->s);
+  (void)hipEventRecord(e, st ? st : m->s);
   return e;
 }
-void ev_end(swps_s2v *m, int k, hipEvent_t b) {
+void ev_end(swps_s2v *m, int k, hipEvent_t b, hipStream_t st = nullptr) {
   if (!b) return;
   hipEvent_t e;
   (void)hipEventCreate(&e);
-  (void)hipEventRecord(e, m->s);
+  (void)hipEventRecord(e, st ? st : m->s);
   m->pending.push_back({k, {b, e}});
 }
 void ev_resolve(swps_s2v *m) {
@@ -516,7 +520,8 @@ struct S2VCorpus {
 
 // The host schedule: Sent2Vec::train's loop (sent2vec.cpp:95-103) replayed over the parsed corpus.
 int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c);
-template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1);
+template <typename T>
+int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1, hipStream_t rs = nullptr, DevMem *rec = nullptr);
 
 // Documents are independent and the word table is read-only:
 // a rank trains exactly the lines whose sentence id BasicHashFrag assigns to
@@ -533,6 +538,20 @@ int s2v_ingest(swps_s2v *m, const S2VCorpus &c) {
     id2.push_back(c.sent_ids[l]);
   }
   return s2v_ingest_all(m, S2VCorpus{k2.data(), off2.data(), id2.data(), id2.size(), c.train});
+}
+
+// the table's rows by key rank: rank_of_row[srow[q]] = q (srow: the rows sorted by key)
+__global__ void k_s2v_rank_scatter(const uint32_t *__restrict__ srow, uint64_t n, uint32_t *__restrict__ rank_of_row) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) rank_of_row[srow[q]] = (uint32_t)q;
+}
+// every token's key rank among the table's keys at load (kNoRow: a key the table lacks)
+__global__ void k_s2v_rank_map(const uint32_t *__restrict__ row, uint64_t n, const uint32_t *__restrict__ rank_of_row,
+                               uint64_t got, uint32_t *__restrict__ rank) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = row[i];
+  rank[i] = r != kNoRow && r < got ? rank_of_row[r] : kNoRow;
 }
 
 // every document's token rows from the rows of every corpus token (a wave per document): the
@@ -575,31 +594,13 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   std::vector<uint64_t> tk(std::max<uint64_t>(have, 1));
   SWPS_TRY(swps_table_keys(m->t, tk.data(), tk.size(), &got));
   phase("table keys");
-  FlatMap64 present(got + 1024);
-  // and the keys' order: rank_of_row[row] = the rank of row's key among the table's keys (tk lists
-  // the keys by row), row_of_rank its inverse — a plan orders a minibatch's vocabulary by marking
-  // ranks in a bitmap instead of sorting keys
-  std::vector<uint32_t> rank_of_row(got), row_of_rank(got);
-  std::atomic<int> present_ready{0};
-  std::thread present_th([&] {
-    for (uint64_t i = 0; i < got; i++) present.at(tk[i]) = 1;
-    std::vector<std::pair<uint64_t, int32_t>> kr(got), tmp;
-    for (uint64_t i = 0; i < got; i++) kr[i] = {tk[i], (int32_t)i};
-    s2v_sort_by_key(kr, tmp);
-    for (uint64_t q = 0; q < got; q++) {
-      row_of_rank[q] = (uint32_t)kr[q].second;
-      rank_of_row[kr[q].second] = (uint32_t)q;
-    }
-    present_ready.store(1, std::memory_order_release);
-  });
-  struct JoinOne {
-    std::thread &t;
-    ~JoinOne() {
-      if (t.joinable()) t.join();
-    }
-  } join_present{present_th};
+  std::unique_ptr<FlatMap64> present;
+  // built on the first minibatch with misses only (a corpus whose words the table holds never
+  // needs it, and its 1M inserts would take a core from the plan workers at the start)
   auto wait_present = [&] {
-    while (!present_ready.load(std::memory_order_acquire)) std::this_thread::yield();
+    if (present) return;
+    present.reset(new FlatMap64(got + 1024));
+    for (uint64_t i = 0; i < got; i++) present->at(tk[i]) = 1;
   };
   // the rand() stream: the draws nobody reads (the WParam a pull constructs for a key the server
   // already holds, server.h:143-150) are counted and skipped in one jump before the next read
@@ -653,11 +654,19 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   // every token's table row at load (kNoRow: a key the table lacks), fetched by a thread in chunks
   // of whole lines — the caller's keys to the device (they stay there for the documents' rows), a
   // probe, the rows back — so the plans count by row in dense arrays and wait only for their lines
+  // — and, first, the table's keys sorted on the device: every token's key rank (its position in
+  // std::map order among the table's keys) comes back instead of its row, and a plan counts by rank
+  // and reads its vocabulary off a bitmap of ranks in key order (tks_h: the keys by rank)
   const uint64_t ntok_all = line_off[nl];
-  DevMem d_keys_all, d_all_row;
+  DevMem d_keys_all, d_all_row, d_all_rank, d_rank_of_row;
   SWPS_TRY(d_keys_all.ensure(std::max<uint64_t>(ntok_all, 1) * 8));
   SWPS_TRY(d_all_row.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
-  std::vector<uint32_t> rows_h(ntok_all);
+  SWPS_TRY(d_all_rank.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
+  SWPS_TRY(d_rank_of_row.ensure(std::max<uint64_t>(got, 1) * 4));
+  // the tokens' key ranks (not zero-filled: a plan reads a line's only after the fetch stored them)
+  std::unique_ptr<uint32_t[]> rows_h(new uint32_t[std::max<uint64_t>(ntok_all, 1)]);
+  std::vector<uint64_t> tks_h(std::max<uint64_t>(got, 1));
+  std::atomic<int> tks_ready{0};
   std::atomic<uint64_t> rows_upto{0};
   std::atomic<int> fetch_rc{SWPS_OK};
   std::atomic<bool> fetch_stop{false};  // set only on the way out (the groups need every line's rows)
@@ -665,6 +674,26 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     hipStream_t fs = nullptr;
     int rc = hipSetDevice(m->t->cfg.device) == hipSuccess && hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) == hipSuccess
                  ? SWPS_OK : SWPS_E_HIP;
+    if (rc == SWPS_OK && got) {  // the table's keys by rank (rows sorted by key, rocPRIM onesweep)
+      DevMem skeys, srows, tmp;
+      size_t sb = 0;
+      if (skeys.ensure(got * 8) || srows.ensure(got * 4) ||
+          sort_pairs_iota(nullptr, sb, m->t->row_key.as<uint64_t>(), skeys.as<uint64_t>(), srows.as<uint32_t>(), got,
+                          64, fs) != hipSuccess ||
+          tmp.ensure(std::max<size_t>(sb, 1)))
+        rc = SWPS_E_HIP;
+      sb = tmp.bytes;
+      if (rc == SWPS_OK &&
+          (sort_pairs_iota(tmp.p, sb, m->t->row_key.as<uint64_t>(), skeys.as<uint64_t>(), srows.as<uint32_t>(), got, 64,
+                           fs) != hipSuccess ||
+           (k_s2v_rank_scatter<<<(unsigned)((got + 255) / 256), 256, 0, fs>>>(srows.as<uint32_t>(), got,
+                                                                              d_rank_of_row.as<uint32_t>()),
+            hipGetLastError() != hipSuccess) ||
+           hipMemcpyAsync(tks_h.data(), skeys.p, got * 8, hipMemcpyDeviceToHost, fs) != hipSuccess ||
+           hipStreamSynchronize(fs) != hipSuccess))
+        rc = SWPS_E_HIP;
+    }
+    tks_ready.store(1, std::memory_order_release);
     uint64_t l0 = 0, chunk = 1 << 20;  // the first chunks small: the first plans start early
     while (rc == SWPS_OK && l0 < nl && !fetch_stop.load(std::memory_order_relaxed)) {
       uint64_t l1 = l0 + 1;
@@ -673,7 +702,11 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       if (t1 > t0 && (hipMemcpyAsync(d_keys_all.as<uint64_t>() + t0, tok_keys + t0, (t1 - t0) * 8,
                                      hipMemcpyHostToDevice, fs) != hipSuccess ||
                       table_probe(m->t, d_keys_all.as<uint64_t>() + t0, t1 - t0, d_all_row.as<uint32_t>() + t0, fs) ||
-                      hipMemcpyAsync(rows_h.data() + t0, d_all_row.as<uint32_t>() + t0, (t1 - t0) * 4,
+                      (k_s2v_rank_map<<<(unsigned)((t1 - t0 + 255) / 256), 256, 0, fs>>>(
+                           d_all_row.as<uint32_t>() + t0, t1 - t0, d_rank_of_row.as<uint32_t>(), got,
+                           d_all_rank.as<uint32_t>() + t0),
+                       hipGetLastError() != hipSuccess) ||
+                      hipMemcpyAsync(rows_h.get() + t0, d_all_rank.as<uint32_t>() + t0, (t1 - t0) * 4,
                                      hipMemcpyDeviceToHost, fs) != hipSuccess ||
                       hipStreamSynchronize(fs) != hipSuccess))
         rc = SWPS_E_HIP;
@@ -717,40 +750,52 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     }();
     auto work = [&]() {
       if (nice_w > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_w);
-      // counts by row in dense arrays (a generation stamp per row instead of clearing); keys the
-      // table lacks (row kNoRow: the minibatch's pull inserts them) in a hash map
+      // counts by key rank in one dense array ({generation stamp, count} per rank: one line per
+      // token), the ranks seen marked in a bitmap as they come; keys the table lacks (rank kNoRow:
+      // the minibatch's pull inserts them) in a hash map
+      struct RankCount {
+        uint32_t gen;
+        int32_t cnt;
+      };
       FlatMap64 fq(1 << 10);
-      std::vector<uint32_t> stamp(std::max<uint64_t>(got, 1), 0), bits((got + 31) / 32 + 1, 0);
-      std::vector<int32_t> cntr(std::max<uint64_t>(got, 1), 0);
+      std::vector<RankCount> rc(std::max<uint64_t>(got, 1), RankCount{0u, 0});
+      std::vector<uint32_t> bits((got + 31) / 32 + 1, 0);
       std::vector<std::pair<uint64_t, int32_t>> vc, va, vtmp;
-      std::vector<uint32_t> prow;  // the minibatch's present rows, first-seen order
       uint32_t gen = 0;
+      const uint32_t rmax = got ? (uint32_t)(got - 1) : 0u;
       for (uint64_t k; !quit.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < K;) {
         Plan &pl = plan[k];
         fq.clear();
         if (++gen == 0) {
-          std::fill(stamp.begin(), stamp.end(), 0u);
+          for (auto &e : rc) e.gen = 0u;
           gen = 1;
         }
         bool zero = false;
         int cnt = 0;
-        prow.clear();
+        uint64_t npres = 0, lo = ~0ull, hi = 0;
         for (uint64_t j = k * (uint64_t)(B + 1); j < nl;) {
           const uint64_t l = j++;
           if (!valid[l]) continue;
           wait_rows(line_off[l + 1]);
-          for (uint64_t i = line_off[l]; i < line_off[l + 1]; i++) {
-            const uint32_t r = rows_h[i];
+          const uint64_t e1 = line_off[l + 1];
+          for (uint64_t i = line_off[l]; i < e1; i++) {
+            // the rank 24 tokens ahead (this line's, or a stale value: a prefetch only)
+            if (i + 24 < e1) __builtin_prefetch(&rc[std::min(rows_h[i + 24], rmax)], 1);
+            const uint32_t q = rows_h[i];
             const uint64_t key = tok_keys[i];
             zero |= key == 0;
-            if (r != kNoRow && r < got) {
-              if (stamp[r] != gen) {
-                stamp[r] = gen;
-                cntr[r] = 1;
+            if (q < got) {  // (kNoRow: absent; after a failed fetch, anything: the load fails anyway)
+              RankCount &e = rc[q];
+              if (e.gen != gen) {
+                e.gen = gen;
+                e.cnt = 1;
                 pl.first.push_back(key);
-                prow.push_back(r);
+                bits[q >> 5] |= 1u << (q & 31);
+                lo = std::min<uint64_t>(lo, q >> 5);
+                hi = std::max<uint64_t>(hi, q >> 5);
+                npres++;
               } else {
-                cntr[r]++;
+                e.cnt++;
               }
             } else {
               bool fresh = false;
@@ -764,27 +809,20 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
           if (++cnt > B) break;
         }
         if (pl.first.size() < 5) {  // the loop ends here (sent2vec.cpp:97)
+          for (uint64_t w = lo; npres && w <= hi; w++) bits[w] = 0;
           ready[k].store(1, std::memory_order_release);
           continue;
         }
         pl.zero = zero;
-        // std::map order: the present keys by rank (a bitmap of ranks), merged with the absent
-        // ones (few; sorted) — the same (key, count) sequence as sorting every pair by key
-        wait_present();
+        // std::map order: the present keys by rank (the bitmap), merged with the absent ones (few;
+        // sorted) — the same (key, count) sequence as sorting every pair by key
+        while (!tks_ready.load(std::memory_order_acquire)) std::this_thread::yield();
         vc.clear();
         va.clear();
         for (uint64_t key : pl.cand) va.emplace_back(key, fq.at(key));
         s2v_sort_by_key(va, vtmp);
-        uint64_t lo = ~0ull, hi = 0;
-        const size_t npres = prow.size();
         vc.reserve(pl.first.size());
         {
-          for (uint32_t r : prow) {  // the present rows' ranks
-            const uint32_t q = rank_of_row[r];
-            bits[q >> 5] |= 1u << (q & 31);
-            lo = std::min<uint64_t>(lo, q >> 5);
-            hi = std::max<uint64_t>(hi, q >> 5);
-          }
           size_t ia = 0;
           for (uint64_t w = lo; npres && w <= hi; w++) {
             uint32_t b = bits[w];
@@ -792,10 +830,9 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
             while (b) {
               const uint32_t q = (uint32_t)(w << 5) + (uint32_t)__builtin_ctz(b);
               b &= b - 1;
-              const uint32_t r = row_of_rank[q];
-              const uint64_t key = tk[r];
+              const uint64_t key = tks_h[q];
               while (ia < va.size() && va[ia].first < key) vc.push_back(va[ia++]);
-              vc.emplace_back(key, cntr[r]);
+              vc.emplace_back(key, rc[q].cnt);
             }
           }
           while (ia < va.size()) vc.push_back(va[ia++]);
@@ -946,6 +983,7 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   SWPS_TRY(m->d_out.ensure(std::max<uint64_t>(ndmax, 1) * D * (m->f64 ? 8 : 4)));
   SWPS_TRY(m->d_err.ensure(std::max<uint64_t>(ndmax, 1) * 4));
   SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(grec_max, 1) * (uint64_t)S * 4));
+  if (c.train) SWPS_TRY(m->d_rec2.ensure(std::max<uint64_t>(grec_max, 1) * (uint64_t)S * 4));
   SWPS_TRY(m->d_tok_row.ensure(std::max<uint64_t>(ntok_all, 1) * 4));
   SWPS_TRY(d_line_off.ensure((nl + 1) * 8));
   SWPS_TRY(d_chunks.ensure(3 * nchunk_max * 8));
@@ -998,7 +1036,12 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       if (s) (void)hipStreamDestroy(s);
     }
   } ls;
-  SWPS_HIP(hipStreamCreateWithFlags(&ls.s, hipStreamNonBlocking));
+  {  // at the highest priority: its small kernels (doc rows, rand() rows, records) get CUs as the
+     // training kernel's waves retire instead of after the whole kernel
+    int lo = 0, hi = 0;
+    SWPS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    SWPS_HIP(hipStreamCreateWithPriority(&ls.s, hipStreamNonBlocking, hi));
+  }
   if (nl) SWPS_HIP(hipMemcpyAsync(d_line_off.p, line_off, (nl + 1) * 8, hipMemcpyHostToDevice, ls.s));
   const uint64_t zero = 0;
   SWPS_HIP(hipMemcpyAsync(m->d_doc_tok.p, &zero, 8, hipMemcpyHostToDevice, ls.s));
@@ -1011,6 +1054,7 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   // one group's device part: its misses into the table, its vocabularies' rows and run starts, its
   // documents' arrays, token rows and rand() rows; then (train) its records + docs launch
   double t_fv = 0, t_fm = 0;  // SWPS_S2V_LOAD_TIMES: the flushes' vocabulary copies, miss inserts
+  uint64_t nflush = 0;        // groups trained so far (their records buffers alternate)
   auto flush = [&](uint64_t k1) -> int {
     if (k1 == kf) return SWPS_OK;
     const double fa = tm ? now() : 0;
@@ -1035,13 +1079,21 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     hipStream_t q = ls.s;
     const swps_s2v::Batch &b0 = m->batches[kf], &b1 = m->batches[k1 - 1];
     const uint64_t v0 = b0.v0, v1 = b1.v0 + b1.U, d0 = b0.d0, d1 = b1.d1;
-    // the group's vocabularies are consecutive in d_vkeys (v0 .. v1) and so are its run starts: one
-    // pinned buffer holds both, one copy each
-    const uint64_t sv0 = b0.s0, sv1 = b1.s0 + plan_st_n[k1 - 1];
+    // Everything the group sends up goes through one pinned staging buffer (two in turn): its
+    // vocabularies and run starts (consecutive in d_vkeys / d_starts), the per-minibatch offsets, the
+    // documents' arrays and the rand() chunks.  A pageable copy waits for the load stream's earlier
+    // work, which queues behind the training kernels: the pass would wait for the GPU at every copy.
+    const uint64_t sv0 = b0.s0, sv1 = b1.s0 + plan_st_n[k1 - 1], nk = k1 - kf, nd = d1 - d0;
+    const uint64_t nch = rand_chunks.size() / 3, nc = nch - rc_done;
+    auto al = [](uint64_t b) { return (b + 15) & ~15ull; };
+    const uint64_t o_st = al((v1 - v0) * 8), o_bv = o_st + al((sv1 - sv0) * 8), o_bs = o_bv + al(nk * 8),
+                   o_bu = o_bs + al(nk * 8), o_dt = o_bu + al(nk * 4), o_dr = o_dt + al(nd * 8), o_dl = o_dr + al(nd * 8),
+                   o_db = o_dl + al(nd * 8), o_dn = o_db + al(nd * 4), o_rc = o_dn + al(nd * 4), o_end = o_rc + al(nc * 24);
     Pinned &pb = pin[pin_next];
     pin_next ^= 1;
-    SWPS_TRY(pb.ensure(((v1 - v0) + (sv1 - sv0)) * 8));
-    uint64_t *hv = (uint64_t *)pb.p, *hs = hv + (v1 - v0);
+    SWPS_TRY(pb.ensure(o_end));  // waits for the copies that last read this buffer
+    char *h = (char *)pb.p;
+    uint64_t *hv = (uint64_t *)h, *hs = (uint64_t *)(h + o_st);
     for (uint64_t k = kf; k < k1; k++) {
       bv0[k] = m->batches[k].v0;
       bs0[k] = m->batches[k].s0;
@@ -1052,29 +1104,38 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       std::vector<uint64_t>().swap(pk.vkeys);
       std::vector<uint64_t>().swap(pk.st);
     }
-    if (v1 > v0)
-      SWPS_HIP(hipMemcpyAsync(d_vkeys.as<uint64_t>() + v0, hv, (v1 - v0) * 8, hipMemcpyHostToDevice, q));
-    if (sv1 > sv0)
-      SWPS_HIP(hipMemcpyAsync(m->d_starts.as<uint64_t>() + sv0, hs, (sv1 - sv0) * 8, hipMemcpyHostToDevice, q));
+    std::copy(bv0.begin() + kf, bv0.begin() + k1, (uint64_t *)(h + o_bv));
+    std::copy(bs0.begin() + kf, bs0.begin() + k1, (uint64_t *)(h + o_bs));
+    std::copy(bU.begin() + kf, bU.begin() + k1, (uint32_t *)(h + o_bu));
+    if (nd) {
+      std::copy(m->doc_tok.begin() + d0 + 1, m->doc_tok.begin() + d1 + 1, (uint64_t *)(h + o_dt));
+      std::copy(m->doc_rec.begin() + d0 + 1, m->doc_rec.begin() + d1 + 1, (uint64_t *)(h + o_dr));
+      std::copy(m->doc_lcg.begin() + d0, m->doc_lcg.begin() + d1, (uint64_t *)(h + o_dl));
+      std::copy(doc_batch.begin() + d0, doc_batch.begin() + d1, (uint32_t *)(h + o_db));
+      std::copy(doc_line.begin() + d0, doc_line.begin() + d1, (uint32_t *)(h + o_dn));
+    }
+    if (nc) std::copy(rand_chunks.begin() + 3 * rc_done, rand_chunks.begin() + 3 * nch, (uint64_t *)(h + o_rc));
+    auto up = [&](void *dst, uint64_t off, uint64_t bytes) -> int {
+      if (bytes) SWPS_HIP(hipMemcpyAsync(dst, h + off, bytes, hipMemcpyHostToDevice, q));
+      return SWPS_OK;
+    };
+    SWPS_TRY(up(d_vkeys.as<uint64_t>() + v0, 0, (v1 - v0) * 8));
+    SWPS_TRY(up(m->d_starts.as<uint64_t>() + sv0, o_st, (sv1 - sv0) * 8));
+    SWPS_TRY(up(m->d_bv0.as<uint64_t>() + kf, o_bv, nk * 8));
+    SWPS_TRY(up(m->d_bs0.as<uint64_t>() + kf, o_bs, nk * 8));
+    SWPS_TRY(up(m->d_bU.as<uint32_t>() + kf, o_bu, nk * 4));
+    SWPS_TRY(up(m->d_doc_tok.as<uint64_t>() + d0 + 1, o_dt, nd * 8));
+    SWPS_TRY(up(m->d_doc_rec.as<uint64_t>() + d0 + 1, o_dr, nd * 8));
+    SWPS_TRY(up(m->d_doc_lcg.as<uint64_t>() + d0, o_dl, nd * 8));
+    SWPS_TRY(up(m->d_doc_batch.as<uint32_t>() + d0, o_db, nd * 4));
+    SWPS_TRY(up(d_doc_line.as<uint32_t>() + d0, o_dn, nd * 4));
+    SWPS_TRY(up(d_chunks.as<uint64_t>() + 3 * rc_done, o_rc, nc * 24));
     if (!pb.done) SWPS_HIP(hipEventCreateWithFlags(&pb.done, hipEventDisableTiming));
     SWPS_HIP(hipEventRecord(pb.done, q));
     if (tm) t_fv += now() - fb;
     if (v1 > v0)
       SWPS_TRY(table_lookup(m->t, d_vkeys.as<uint64_t>() + v0, v1 - v0, m->d_vocab_row.as<uint32_t>() + v0, q));
-    SWPS_HIP(hipMemcpyAsync(m->d_bv0.as<uint64_t>() + kf, bv0.data() + kf, (k1 - kf) * 8, hipMemcpyHostToDevice, q));
-    SWPS_HIP(hipMemcpyAsync(m->d_bs0.as<uint64_t>() + kf, bs0.data() + kf, (k1 - kf) * 8, hipMemcpyHostToDevice, q));
-    SWPS_HIP(hipMemcpyAsync(m->d_bU.as<uint32_t>() + kf, bU.data() + kf, (k1 - kf) * 4, hipMemcpyHostToDevice, q));
-    if (d1 > d0) {
-      SWPS_HIP(hipMemcpyAsync(m->d_doc_tok.as<uint64_t>() + d0 + 1, m->doc_tok.data() + d0 + 1, (d1 - d0) * 8,
-                              hipMemcpyHostToDevice, q));
-      SWPS_HIP(hipMemcpyAsync(m->d_doc_rec.as<uint64_t>() + d0 + 1, m->doc_rec.data() + d0 + 1, (d1 - d0) * 8,
-                              hipMemcpyHostToDevice, q));
-      SWPS_HIP(hipMemcpyAsync(m->d_doc_lcg.as<uint64_t>() + d0, m->doc_lcg.data() + d0, (d1 - d0) * 8,
-                              hipMemcpyHostToDevice, q));
-      SWPS_HIP(hipMemcpyAsync(m->d_doc_batch.as<uint32_t>() + d0, doc_batch.data() + d0, (d1 - d0) * 4,
-                              hipMemcpyHostToDevice, q));
-      SWPS_HIP(hipMemcpyAsync(d_doc_line.as<uint32_t>() + d0, doc_line.data() + d0, (d1 - d0) * 4,
-                              hipMemcpyHostToDevice, q));
+    if (nd) {
       // the group's lines' token rows: probed by the fetch thread at load; again once the pulls
       // inserted keys (their rows exist only now).  Probed, not looked up: a short line's keys
       // (read, never gathered) may be absent; the documents' keys are all in their minibatches'
@@ -1084,17 +1145,14 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       wait_rows(t1);  // (the plans of these minibatches waited for them already)
       if (t1 > t0 && !miss_keys.empty())
         SWPS_TRY(table_probe(m->t, d_keys_all.as<uint64_t>() + t0, t1 - t0, d_all_row.as<uint32_t>() + t0, q));
-      k_s2v_doc_rows<<<(unsigned)(((d1 - d0) * 64 + 255) / 256), 256, 0, q>>>(
+      k_s2v_doc_rows<<<(unsigned)((nd * 64 + 255) / 256), 256, 0, q>>>(
           d_all_row.as<uint32_t>(), d_line_off.as<uint64_t>(), d_doc_line.as<uint32_t>() + d0,
-          m->d_doc_tok.as<uint64_t>() + d0, d1 - d0, m->d_tok_row.as<uint32_t>());
+          m->d_doc_tok.as<uint64_t>() + d0, nd, m->d_tok_row.as<uint32_t>());
       SWPS_HIP(hipGetLastError());
     }
-    const uint64_t nch = rand_chunks.size() / 3;
-    if (nch > rc_done) {
-      SWPS_HIP(hipMemcpyAsync(d_chunks.as<uint64_t>() + 3 * rc_done, rand_chunks.data() + 3 * rc_done,
-                              (nch - rc_done) * 24, hipMemcpyHostToDevice, q));
-      k_s2v_rand<<<(unsigned)((nch - rc_done + 63) / 64), 64, 0, q>>>(
-          d_base.as<uint32_t>(), d_chunks.as<uint64_t>() + 3 * rc_done, nch - rc_done, m->d_init.as<int32_t>());
+    if (nc) {
+      k_s2v_rand<<<(unsigned)((nc + 63) / 64), 64, 0, q>>>(d_base.as<uint32_t>(), d_chunks.as<uint64_t>() + 3 * rc_done, nc,
+                                                          m->d_init.as<int32_t>());
       SWPS_HIP(hipGetLastError());
       rc_done = nch;
     }
@@ -1103,15 +1161,16 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     ls.ev.push_back(ev);
     SWPS_HIP(hipEventRecord(ev, q));
     if (c.train) {  // the group trains on the table's stream as soon as its data is there
-      SWPS_HIP(hipStreamWaitEvent(s, ev, 0));
-      SWPS_TRY(m->f64 ? s2v_group<double>(m, kf, k1) : s2v_group<float>(m, kf, k1));
+      // its records on the load stream (after its uploads) into the buffer the group before last
+      // used: the documents of the previous group may still be reading the other one
+      DevMem *rb = (nflush++ & 1) ? &m->d_rec2 : &m->d_rec;
+      SWPS_TRY(m->f64 ? s2v_group<double>(m, kf, k1, q, rb) : s2v_group<float>(m, kf, k1, q, rb));
       m->cursor = k1;
     }
     kf = k1;
     return SWPS_OK;
   };
   size_t gi = 0;
-  wait_present();
   double t_wait = 0, t_flush = 0;  // SWPS_S2V_LOAD_TIMES: the pass's time waiting for plans, in flushes
   double t_lk = 0, t_vocab = 0, t_docs = 0;  // ... refilling _local_keys, appending vocabularies, documents
   for (uint64_t k = 0; k < K; k++) {
@@ -1122,7 +1181,6 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     }
     Plan &pl = plan[k];
     const std::vector<uint64_t> &first_seen = pl.first;
-    const uint64_t li = k * (uint64_t)(B + 1);
     if (first_seen.size() < 5) break;  // sent2vec.cpp:97
     if (pl.zero)
       return fail(SWPS_E_UNSUPPORTED, "a minibatch vocab holds key 0 (atoi of a non-numeric word): the reference "
@@ -1149,9 +1207,10 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     }
     if (tm) t_lk += now() - tb0;
     if (!miss) skip += 2 * (uint64_t)D * first_seen.size();
+    if (miss) wait_present();  // the table's keys at load (the map thread), read only for misses
     for (uint64_t key : lk) {
       if (!miss) break;
-      if (present.contains(key) || inserted.contains(key)) {
+      if (present->contains(key) || inserted.contains(key)) {
         skip += 2 * (uint64_t)D;
         continue;
       }
@@ -1234,15 +1293,19 @@ template <typename T, int NCH, bool TAIL> void launch_docs(const S2VDocArgs<T> &
 }
 
 // minibatches [c0, c1) (consecutive, no wrap) in one records + docs launch
-template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1) {
+// rs / rec (the single pass): the group's records are built on the load stream rs into rec (one of
+// two buffers in turn) while the previous group trains; the documents wait for them
+template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1, hipStream_t rs, DevMem *rec) {
   hipStream_t s = m->s;
+  DevMem &drec = rec ? *rec : m->d_rec;
+  hipStream_t qs = rs ? rs : s;
   const uint64_t d0 = m->batches[c0].d0, d1 = m->batches[c1 - 1].d1, nd = d1 - d0;
   uint64_t recs = 0;
   for (uint64_t c = c0; c < c1; c++) recs += m->batches[c].recs;
   m->st_batches += c1 - c0;
   if (nd == 0) return SWPS_OK;
   const int S = 2 * m->W + m->N + 1;
-  SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(recs, 1) * (uint64_t)S * 4));
+  if (!rec) SWPS_TRY(m->d_rec.ensure(std::max<uint64_t>(recs, 1) * (uint64_t)S * 4));
   S2VRecArgs ra{m->d_tok_row.as<uint32_t>(),
                 m->d_doc_tok.as<uint64_t>(),
                 m->d_doc_rec.as<uint64_t>(),
@@ -1261,12 +1324,19 @@ template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1) {
                 m->N,
                 m->cfg.niters,
                 ~0ULL / (uint64_t)m->W,
-                m->d_rec.as<int32_t>()};
-  hipEvent_t e0 = ev_begin(m);
-  k_s2v_records<<<nblk(nd * 64), 256, 0, s>>>(ra);
+                drec.as<int32_t>()};
+  const int rb = rec == &m->d_rec2 ? 1 : 0;
+  if (rs && m->ev_docs[rb]) SWPS_HIP(hipStreamWaitEvent(rs, m->ev_docs[rb], 0));  // its last reader is done
+  hipEvent_t e0 = ev_begin(m, qs);
+  k_s2v_records<<<nblk(nd * 64), 256, 0, qs>>>(ra);
   SWPS_HIP(hipGetLastError());
-  ev_end(m, ST_REC, e0);
-  S2VDocArgs<T> da{m->d_rec.as<int32_t>(), m->d_doc_tok.as<uint64_t>(), m->d_doc_rec.as<uint64_t>(), d0, nd,
+  ev_end(m, ST_REC, e0, qs);
+  if (rs) {  // the documents wait for the records (and everything earlier on the load stream)
+    if (!m->ev_rec) SWPS_HIP(hipEventCreateWithFlags(&m->ev_rec, hipEventDisableTiming));
+    SWPS_HIP(hipEventRecord(m->ev_rec, rs));
+    SWPS_HIP(hipStreamWaitEvent(s, m->ev_rec, 0));
+  }
+  S2VDocArgs<T> da{drec.as<int32_t>(), m->d_doc_tok.as<uint64_t>(), m->d_doc_rec.as<uint64_t>(), d0, nd,
                    m->d_init.as<int32_t>(), m->t->rows.as<T>(), m->d_exptab.as<float>(), m->D, m->W, m->N,
                    m->cfg.niters, m->cfg.alpha, m->d_out.as<T>(), m->d_err.as<float>(),
                    m->d_rows_read.as<unsigned long long>()};
@@ -1285,6 +1355,10 @@ template <typename T> int s2v_group(swps_s2v *m, uint64_t c0, uint64_t c1) {
     default: launch_docs<T, 4, false>(da, s, wpe); break;
   }
   SWPS_HIP(hipGetLastError());
+  if (rs) {
+    if (!m->ev_docs[rb]) SWPS_HIP(hipEventCreateWithFlags(&m->ev_docs[rb], hipEventDisableTiming));
+    SWPS_HIP(hipEventRecord(m->ev_docs[rb], s));
+  }
   ev_end(m, ST_DOC, e1);
   m->st_docs += nd;
   m->st_pos += recs;
@@ -1343,6 +1417,9 @@ int swps_s2v_destroy(swps_s2v *m) {
   (void)hipSetDevice(m->t->cfg.device);
   (void)hipStreamSynchronize(m->s);
   ev_resolve(m);
+  if (m->ev_rec) (void)hipEventDestroy(m->ev_rec);
+  for (auto e : m->ev_docs)
+    if (e) (void)hipEventDestroy(e);
   delete m;
   (void)hipGetLastError();  // leave no sticky error from the calls above
   return SWPS_OK;
