@@ -854,13 +854,6 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
         if (t.joinable()) t.join();
     }
   } join{workers, quit};
-  auto wait_plan = [&](uint64_t k) {
-    for (unsigned it = 0; !ready[k].load(std::memory_order_acquire); it++)
-      if (it < 64)
-        std::this_thread::yield();
-      else
-        std::this_thread::sleep_for(std::chrono::microseconds(50));
-  };
   FlatMap64 inserted(1024);  // keys the minibatches so far inserted (the server's inserts persist)
   // Bounds for the device arrays, from the line lengths alone, so everything the pass below makes
   // can go to the device group by group (never reallocated while a group trains): the gather
@@ -883,22 +876,20 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       }
     ndmax += kdoc[k];
   }
-  // pipeline groups: 2, 4, then 8 minibatches (at most group_docs documents), the last ones 4 and
-  // 2 again, so the first group trains early while the later ones are planned and little is left
-  // to train after the last plan
-  std::vector<uint64_t> gend;
+  // pipeline groups: consecutive minibatches, at most kGroupMax and group_docs documents; the pass
+  // sends a group up when it is full or when the GPU has nothing left to train (the first groups
+  // are small, so training starts after the first plan, and the GPU never waits for a full group
+  // while plans are late).  The records buffers hold the largest group any such rule can make.
+  constexpr uint64_t kGroupMax = 8;
   uint64_t grec_max = 0;
-  for (uint64_t k0 = 0, gsz = 2; k0 < K; gsz = std::min<uint64_t>(8, 2 * gsz)) {
-    const uint64_t lim = K - k0 <= 6 ? std::min<uint64_t>(gsz, K - k0 <= 2 ? 2 : 4) : gsz;
+  for (uint64_t k0 = 0; k0 < K; k0++) {
     uint64_t k1 = k0 + 1, docs = kdoc[k0], recs = krec[k0];
-    while (k1 < K && k1 - k0 < lim && docs + kdoc[k1] <= m->group_docs) {
+    while (k1 < K && k1 - k0 < kGroupMax && docs + kdoc[k1] <= m->group_docs) {
       docs += kdoc[k1];
       recs += krec[k1];
       k1++;
     }
-    gend.push_back(k1);
     grec_max = std::max(grec_max, recs);
-    k0 = k1;
   }
   const uint64_t nchunk_max = ndmax * (uint64_t)D / kRandRun + K + 1;
 
@@ -1025,6 +1016,20 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     }
   } pin[2];
   int pin_next = 0;
+  // both buffers allocated by a thread at the start, sized for a full group at a guessed vocabulary
+  // of a third of its window's tokens (a larger group grows them in ensure): pinning tens of MB in
+  // the first flushes delayed the first full groups by ~10 ms each
+  std::thread prepin([&] {
+    if (!c.train || !K || hipSetDevice(m->t->cfg.device) != hipSuccess) return;
+    const uint64_t est = std::min<uint64_t>(kGroupMax * (wtok / K + 1) * 16 / 3 + (4u << 20), 256u << 20);
+    for (auto &b : pin) (void)b.ensure(est);
+  });
+  struct JoinPin {
+    std::thread &t;
+    ~JoinPin() {
+      if (t.joinable()) t.join();
+    }
+  } join_pin{prepin};
   // the load stream: each group's uploads, lookups and rand() rows; the training of a group waits
   // for its event on the table's stream
   struct LoadStream {
@@ -1054,6 +1059,14 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   // one group's device part: its misses into the table, its vocabularies' rows and run starts, its
   // documents' arrays, token rows and rand() rows; then (train) its records + docs launch
   double t_fv = 0, t_fm = 0;  // SWPS_S2V_LOAD_TIMES: the flushes' vocabulary copies, miss inserts
+  struct OwnedEvent {
+    hipEvent_t e = nullptr;
+    ~OwnedEvent() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev_gpu;
+  // nothing left to train: no group sent yet, or the last one done
+  auto gpu_idle = [&]() { return !ev_gpu.e || hipEventQuery(ev_gpu.e) == hipSuccess; };
   uint64_t nflush = 0;        // groups trained so far (their records buffers alternate)
   auto flush = [&](uint64_t k1) -> int {
     if (k1 == kf) return SWPS_OK;
@@ -1089,20 +1102,30 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     const uint64_t o_st = al((v1 - v0) * 8), o_bv = o_st + al((sv1 - sv0) * 8), o_bs = o_bv + al(nk * 8),
                    o_bu = o_bs + al(nk * 8), o_dt = o_bu + al(nk * 4), o_dr = o_dt + al(nd * 8), o_dl = o_dr + al(nd * 8),
                    o_db = o_dl + al(nd * 8), o_dn = o_db + al(nd * 4), o_rc = o_dn + al(nd * 4), o_end = o_rc + al(nc * 24);
+    if (prepin.joinable()) prepin.join();
     Pinned &pb = pin[pin_next];
     pin_next ^= 1;
     SWPS_TRY(pb.ensure(o_end));  // waits for the copies that last read this buffer
     char *h = (char *)pb.p;
     uint64_t *hv = (uint64_t *)h, *hs = (uint64_t *)(h + o_st);
+    // each minibatch's plan into the staging buffer on a thread of its own (~3.5 MB each)
+    auto stage = [&](uint64_t k) {
+      Plan &pk = plan[k];
+      std::copy(pk.vkeys.begin(), pk.vkeys.end(), hv + (m->batches[k].v0 - v0));
+      std::copy(pk.st.begin(), pk.st.end(), hs + (m->batches[k].s0 - sv0));
+      std::vector<uint64_t>().swap(pk.vkeys);
+      std::vector<uint64_t>().swap(pk.st);
+    };
+    {
+      std::vector<std::thread> cp;
+      for (uint64_t k = kf + 1; k < k1; k++) cp.emplace_back(stage, k);
+      stage(kf);
+      for (auto &t : cp) t.join();
+    }
     for (uint64_t k = kf; k < k1; k++) {
       bv0[k] = m->batches[k].v0;
       bs0[k] = m->batches[k].s0;
       bU[k] = m->batches[k].U;
-      Plan &pk = plan[k];
-      std::copy(pk.vkeys.begin(), pk.vkeys.end(), hv + (bv0[k] - v0));
-      std::copy(pk.st.begin(), pk.st.end(), hs + (bs0[k] - sv0));
-      std::vector<uint64_t>().swap(pk.vkeys);
-      std::vector<uint64_t>().swap(pk.st);
     }
     std::copy(bv0.begin() + kf, bv0.begin() + k1, (uint64_t *)(h + o_bv));
     std::copy(bs0.begin() + kf, bs0.begin() + k1, (uint64_t *)(h + o_bs));
@@ -1166,17 +1189,28 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       DevMem *rb = (nflush++ & 1) ? &m->d_rec2 : &m->d_rec;
       SWPS_TRY(m->f64 ? s2v_group<double>(m, kf, k1, q, rb) : s2v_group<float>(m, kf, k1, q, rb));
       m->cursor = k1;
+      if (!ev_gpu.e) SWPS_HIP(hipEventCreateWithFlags(&ev_gpu.e, hipEventDisableTiming));
+      SWPS_HIP(hipEventRecord(ev_gpu.e, s));  // the GPU's queue of training ends here
     }
     kf = k1;
     return SWPS_OK;
   };
-  size_t gi = 0;
   double t_wait = 0, t_flush = 0;  // SWPS_S2V_LOAD_TIMES: the pass's time waiting for plans, in flushes
   double t_lk = 0, t_vocab = 0, t_docs = 0;  // ... refilling _local_keys, appending vocabularies, documents
   for (uint64_t k = 0; k < K; k++) {
     {
       const double a = tm ? now() : 0;
-      wait_plan(k);
+      // waiting for plan k: the minibatches already passed go up as soon as the GPU runs dry
+      for (unsigned it = 0; !ready[k].load(std::memory_order_acquire); it++) {
+        if (c.train && m->batches.size() > kf && gpu_idle()) {
+          SWPS_TRY(flush(m->batches.size()));
+          continue;
+        }
+        if (it < 64)
+          std::this_thread::yield();
+        else
+          std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
       if (tm) t_wait += now() - a;
     }
     Plan &pl = plan[k];
@@ -1243,11 +1277,14 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     m->max_docs = std::max(m->max_docs, b.d1 - b.d0);
     m->batches.push_back(b);
     if (tm) t_docs += now() - tb2;
-    if (gi < gend.size() && k + 1 == gend[gi]) {
-      const double a = tm ? now() : 0;
-      SWPS_TRY(flush(k + 1));
-      if (tm) t_flush += now() - a;
-      gi++;
+    {  // the group goes up when full (the next minibatch would not fit) or the GPU has run dry
+      const uint64_t pend = k + 1 - kf, docs = dbase[k + 1] - dbase[kf];
+      const bool full = pend >= kGroupMax || (k + 1 < K && docs + kdoc[k + 1] > m->group_docs);
+      if (full || (c.train && gpu_idle())) {
+        const double a = tm ? now() : 0;
+        SWPS_TRY(flush(k + 1));
+        if (tm) t_flush += now() - a;
+      }
     }
   }
   quit.store(true);  // plans past the corpus end (sent2vec.cpp:97) are not needed
