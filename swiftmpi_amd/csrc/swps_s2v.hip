@@ -1019,10 +1019,14 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   // both buffers allocated by a thread at the start, sized for a full group at a guessed vocabulary
   // of a third of its window's tokens (a larger group grows them in ensure): pinning tens of MB in
   // the first flushes delayed the first full groups by ~10 ms each
+  phase("plans started, bounds, device arrays");
+  double t_pin = 0, t_first_flush = 0, t_pass0 = now();  // SWPS_S2V_LOAD_TIMES
   std::thread prepin([&] {
     if (!c.train || !K || hipSetDevice(m->t->cfg.device) != hipSuccess) return;
+    const double a = now();
     const uint64_t est = std::min<uint64_t>(kGroupMax * (wtok / K + 1) * 16 / 3 + (4u << 20), 256u << 20);
     for (auto &b : pin) (void)b.ensure(est);
+    t_pin = now() - a;
   });
   struct JoinPin {
     std::thread &t;
@@ -1103,6 +1107,7 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
                    o_bu = o_bs + al(nk * 8), o_dt = o_bu + al(nk * 4), o_dr = o_dt + al(nd * 8), o_dl = o_dr + al(nd * 8),
                    o_db = o_dl + al(nd * 8), o_dn = o_db + al(nd * 4), o_rc = o_dn + al(nd * 4), o_end = o_rc + al(nc * 24);
     if (prepin.joinable()) prepin.join();
+    if (tm && !t_first_flush) t_first_flush = now() - t_pass0;
     Pinned &pb = pin[pin_next];
     pin_next ^= 1;
     SWPS_TRY(pb.ensure(o_end));  // waits for the copies that last read this buffer
@@ -1292,8 +1297,9 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
   SWPS_TRY(flush(m->batches.size()));
   if (tm)
     fprintf(stderr, "[s2v load]   of which waiting for plans %.3f s, group uploads + launches %.3f s (vocabulary copies %.3f, "
-                    "miss inserts %.3f), _local_keys %.3f s, vocabularies %.3f s, documents %.3f s\n", t_wait, t_flush,
-            t_fv, t_fm, t_lk, t_vocab, t_docs);
+                    "miss inserts %.3f), _local_keys %.3f s, vocabularies %.3f s, documents %.3f s; first flush %.3f s "
+                    "after the schedule, pinned staging %.3f s\n", t_wait, t_flush,
+            t_fv, t_fm, t_lk, t_vocab, t_docs, t_first_flush, t_pin);
   phase("minibatch vocabs + schedule + groups (host)");
   {  // the documents of the minibatches trained (the pass may stop early: sent2vec.cpp:97)
     docs_quit.store(true);
