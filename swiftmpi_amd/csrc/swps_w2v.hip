@@ -1779,6 +1779,9 @@ __global__ __launch_bounds__(256) void k_push_thp(PushArgs<float, float> a) {
     const int half = (int)(uh & 1);
     const bool multi = h.i1 - h.i0 > 1;
     bool other = (MODE == 1 && multi) || (MODE == 2 && !multi);
+    // the key's local slot is freed by its half-0 item in pass 1 even when pass 2 pushes that half
+    // (pass 2 never frees one): every key of the batch leaves the map, as in MODE 0
+    if (MODE == 1 && multi && lane == 0 && half == 0) a.local[h.vid] = -1;
     if (TO_GRADS && a.gpass) {  // the key's owner range: its first ohalf keys go in pass 1
       const uint32_t u = (uint32_t)(uh >> 1);
       uint32_t r = 0;
