@@ -674,8 +674,8 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     hipStream_t fs = nullptr;
     int rc = hipSetDevice(m->t->cfg.device) == hipSuccess && hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) == hipSuccess
                  ? SWPS_OK : SWPS_E_HIP;
+    DevMem skeys, srows, tmp;
     if (rc == SWPS_OK && got) {  // the table's keys by rank (rows sorted by key, rocPRIM onesweep)
-      DevMem skeys, srows, tmp;
       size_t sb = 0;
       if (skeys.ensure(got * 8) || srows.ensure(got * 4) ||
           sort_pairs_iota(nullptr, sb, m->t->row_key.as<uint64_t>(), skeys.as<uint64_t>(), srows.as<uint32_t>(), got,
@@ -688,12 +688,21 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
                            fs) != hipSuccess ||
            (k_s2v_rank_scatter<<<(unsigned)((got + 255) / 256), 256, 0, fs>>>(srows.as<uint32_t>(), got,
                                                                               d_rank_of_row.as<uint32_t>()),
-            hipGetLastError() != hipSuccess) ||
-           hipMemcpyAsync(tks_h.data(), skeys.p, got * 8, hipMemcpyDeviceToHost, fs) != hipSuccess ||
-           hipStreamSynchronize(fs) != hipSuccess))
+            hipGetLastError() != hipSuccess)))
         rc = SWPS_E_HIP;
     }
-    tks_ready.store(1, std::memory_order_release);
+    // the keys by rank come back after the first chunk's ranks (the plans need them only to order
+    // their vocabularies, after counting)
+    bool tks_done = false;
+    auto fetch_tks = [&] {
+      if (tks_done) return;
+      if (rc == SWPS_OK && got &&
+          (hipMemcpyAsync(tks_h.data(), skeys.p, got * 8, hipMemcpyDeviceToHost, fs) != hipSuccess ||
+           hipStreamSynchronize(fs) != hipSuccess))
+        rc = SWPS_E_HIP;
+      tks_done = true;
+      tks_ready.store(1, std::memory_order_release);
+    };
     uint64_t l0 = 0, chunk = 1 << 20;  // the first chunks small: the first plans start early
     while (rc == SWPS_OK && l0 < nl && !fetch_stop.load(std::memory_order_relaxed)) {
       uint64_t l1 = l0 + 1;
@@ -711,9 +720,11 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
                       hipStreamSynchronize(fs) != hipSuccess))
         rc = SWPS_E_HIP;
       rows_upto.store(t1, std::memory_order_release);
+      fetch_tks();
       l0 = l1;
       chunk = std::min<uint64_t>(chunk * 2, 8u << 20);
     }
+    fetch_tks();  // (no lines, or a failed fetch: the plans must not wait for it)
     if (fs) (void)hipStreamDestroy(fs);
     if (rc != SWPS_OK) {
       fetch_rc.store(rc);
@@ -1239,12 +1250,16 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
         miss = true;
         break;
       }
-    const double tb0 = tm ? now() : 0;
-    if (miss || lk.bucket_count() <= 1 || first_seen.size() > lk.bucket_count()) {  // (a new set grows at once)
+    // without misses the set is only kept for its bucket count: refilled after this minibatch's
+    // group decision (the first minibatch's 200k inserts are not on the way to the first launch)
+    const bool lk_refill = miss || lk.bucket_count() <= 1 || first_seen.size() > lk.bucket_count();  // (a new set grows at once)
+    auto refill_lk = [&] {
+      const double tb0 = tm ? now() : 0;
       lk.clear();
       for (uint64_t key : first_seen) lk.insert(key);
-    }
-    if (tm) t_lk += now() - tb0;
+      if (tm) t_lk += now() - tb0;
+    };
+    if (lk_refill && miss) refill_lk();
     if (!miss) skip += 2 * (uint64_t)D * first_seen.size();
     if (miss) wait_present();  // the table's keys at load (the map thread), read only for misses
     for (uint64_t key : lk) {
@@ -1266,7 +1281,6 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
     nvocab += pl.vkeys.size();
     nstarts += pl.st.size();
     plan_st_n[k] = pl.st.size();
-    std::vector<uint64_t>().swap(pl.first);
     if (tm) t_vocab += now() - tb1;
     const double tb2 = tm ? now() : 0;
     // the training handler (sent2vec.cpp:48-93): B+1 lines, valid or not; the sentences' Vec::random
@@ -1291,6 +1305,8 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
         if (tm) t_flush += now() - a;
       }
     }
+    if (lk_refill && !miss) refill_lk();
+    std::vector<uint64_t>().swap(pl.first);
   }
   quit.store(true);  // plans past the corpus end (sent2vec.cpp:97) are not needed
   if (fetch_rc.load() != SWPS_OK) return fail(fetch_rc.load(), "sent2vec load: token rows (HIP)");
