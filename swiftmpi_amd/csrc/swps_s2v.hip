@@ -746,6 +746,9 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
       else
         std::this_thread::sleep_for(std::chrono::microseconds(20));
   };
+  // SWPS_S2V_LOAD_TIMES: when the first plans were ready, from the workers' start
+  const double t_sched0 = now();
+  double t_plan[16] = {0};
   {
     // 12 plan workers (16 on the GPU boxes' CPU share measured 1.8e8 words/s single-pass, 12 2.0e8,
     // 8 1.9e8: the pass below, the group uploads and the runtime's threads need cores too)
@@ -849,6 +852,7 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
           while (ia < va.size()) vc.push_back(va[ia++]);
         }
         s2v_unigram_starts(vc, T, pl.st);
+        if (tm && k < 16) t_plan[k] = now() - t_sched0;
         pl.vkeys.resize(vc.size());
         for (size_t q = 0; q < vc.size(); q++) pl.vkeys[q] = vc[q].first;
         ready[k].store(1, std::memory_order_release);
@@ -1316,6 +1320,11 @@ int s2v_ingest_all(swps_s2v *m, const S2VCorpus &c) {
                     "miss inserts %.3f), _local_keys %.3f s, vocabularies %.3f s, documents %.3f s; first flush %.3f s "
                     "after the schedule, pinned staging %.3f s\n", t_wait, t_flush,
             t_fv, t_fm, t_lk, t_vocab, t_docs, t_first_flush, t_pin);
+  if (tm) {
+    fprintf(stderr, "[s2v load]   plans 0..15 ready at (ms from the workers' start):");
+    for (int q = 0; q < 16; q++) fprintf(stderr, " %.1f", t_plan[q] * 1e3);
+    fprintf(stderr, "; first flush at %.1f\n", (t_first_flush + t_pass0 - t_sched0) * 1e3);
+  }
   phase("minibatch vocabs + schedule + groups (host)");
   {  // the documents of the minibatches trained (the pass may stop early: sent2vec.cpp:97)
     docs_quit.store(true);
