@@ -83,3 +83,20 @@ def test_bench_rank_killed_fails_fast(lib, gpu):
     assert "rank 1 exited" in r.stderr and "SWPS_BENCH_FAULT" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert dt < 260
+
+
+def test_bench_gpus1_lr_sharded_base_forms(lib, gpu):
+    """At N = 1 the LR leg carries its world-1 sharded base point in both forms: the full protocol
+    (`lr.sharded_world1`, SWPS_PULL_IN_PLACE=0 — what every rank runs at N > 1) and the library
+    driver's in-place default (`.in_place`); the s2v leg's value is the load-inclusive single pass,
+    its re-train the `steady_state` sub-field."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"] + SMALL + LEGS
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    out = _line(r)
+    lr, s2 = out["lr"], out["s2v"]
+    q = lr["sharded_world1"]
+    print(lr["ms_per_step"], q["ms_per_step"], q["in_place"]["ms_per_step"], s2["value"])
+    assert q["value"] > 0 and q["in_place"]["value"] > 0 and "SWPS_PULL_IN_PLACE=0" in q["note"]
+    assert "key-sharded PS over 1 GPU(s)" in q["parallelism"]
+    assert s2["value"] == s2["config"]["end_to_end"]["value"] and s2["config"]["steady_state"]["value"] > 0
