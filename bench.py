@@ -838,7 +838,7 @@ def main():
     # rank its own share: weak scaling; the same legs at N = 1 give each curve its base point),
     # each with its own roofline, exchange block and (N = 1) CPU baseline
     if not args.no_app_legs:
-        if args.config4_tokens > 0:
+        if args.config4_tokens > 0 and args.config4_steps > 0:
             out["config4"] = config4_leg(sw, ctx, args)
         la = argparse.Namespace(**vars(args))
         la.steps, la.warmup = args.app_steps, 3
