@@ -2635,7 +2635,9 @@ struct swps_lr {
   // loads — runs between calls), then kept by the push
   swps::DevMem d_wmir, d_pfb;             // weights by fid; per bucket: prefetch its rows in the push
   bool fx_mirror = true, mirror_stale = true;
-  int fx_pf = 1;                          // SWPS_LR_FX_PF: 0 no bucket prefetches, 1 dense buckets, 2 all
+  // SWPS_LR_FX_PF: 0 no bucket prefetches, 1 dense buckets, 2 all (default: the same PMC traffic, and
+  // same box, 2 reps: --app lr 35.5 -> 35.2 us, the line's 10-batch leg 30.8 -> 30.7 us)
+  int fx_pf = 2;
   uint32_t fxb_gbits = 0;                // chunk groups per bucket region: 2^fxb_gbits
   uint64_t fxb_region_recs = 0;          // the regions' total capacity (records)
   int fx_atomic = 0;
